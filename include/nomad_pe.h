@@ -1,0 +1,269 @@
+/*
+ * nomad_pe.h — C ABI of the MI355X placement engine for Nomad's scheduler hot path.
+ *
+ * The engine replaces the placement stack behind `scheduler.Stack`
+ * (reference: scheduler/stack.go:23-32 — SetNodes / SetJob / Select) for the
+ * GenericStack (stack.go:41-179, 336-431) and SystemStack (stack.go:181-333).
+ * The Go callers (GenericScheduler.computePlacements, generic_sched.go:472-652;
+ * SystemScheduler.computePlacements, scheduler_system.go:283-425) stay
+ * unchanged; a cgo shim flattens structs.Node / structs.Job
+ * into the POD tables below and calls these entry points.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; every pointer is borrowed for the duration
+ *    of the call (cgo pointer rules) and copied by the engine.
+ *  - Strings are interned by the caller: one table per state snapshot
+ *    (pe_strtab), every string field is a uint32 id into it; equal strings must
+ *    share one id. PE_NONE marks "absent" where a field is optional.
+ *  - Every function returns 0 on success or a negative PE_E* code; the message
+ *    is available from pe_last_error(handle). "No feasible node" is NOT an
+ *    error: Select writes row = -1, exactly like a nil *RankedNode.
+ *  - A handle is used by one thread at a time (one Stack per eval worker,
+ *    nomad/worker.go:244-274). Handles are independent.
+ */
+#ifndef NOMAD_PE_H
+#define NOMAD_PE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PE_ABI_VERSION 1u
+#define PE_NONE 0xFFFFFFFFu
+#define PE_MAX_SCORES 8
+
+/* ---- status codes ------------------------------------------------------ */
+#define PE_OK 0
+#define PE_EINVAL (-1)       /* malformed input */
+#define PE_ESTATE (-2)       /* call order violated (e.g. Select before SetJob) */
+#define PE_EHIP (-3)         /* HIP runtime failure */
+#define PE_EUNSUPPORTED (-4) /* feature not on the device path (CSI, cores, ...):
+                                the shim falls back to the Go chain for this Select */
+#define PE_ENOMEM (-5)
+
+/* ---- interned strings -------------------------------------------------- */
+typedef struct pe_strtab {
+    const char* bytes;        /* concatenated bytes */
+    const uint32_t* offsets;  /* count+1 entries; string i = bytes[offsets[i], offsets[i+1]) */
+    uint32_t count;
+} pe_strtab;
+
+/* ---- typed device attribute (plugins/shared/structs/attribute.go:39-61) -- */
+#define PE_ATTR_INT 1
+#define PE_ATTR_FLOAT 2
+#define PE_ATTR_STRING 3
+#define PE_ATTR_BOOL 4
+typedef struct pe_attr {
+    uint32_t kind;    /* PE_ATTR_* */
+    uint32_t unit;    /* str id of the unit ("" if none) */
+    int64_t i;        /* int / bool value */
+    double f;         /* float value */
+    uint32_t s;       /* str id for string values */
+    uint32_t _pad;
+} pe_attr;
+
+/* ---- node table: the structs.Node fields the hot path reads -------------
+ * (nomad/structs/structs.go:1812-1914). One row per node of the State
+ * snapshot. CSR lists use off[n+1].                                         */
+typedef struct pe_node_table {
+    uint32_t n;
+    const uint32_t* id;              /* Node.ID                     */
+    const uint32_t* name;            /* Node.Name                   */
+    const uint32_t* datacenter;      /* Node.Datacenter             */
+    const uint32_t* node_class;      /* Node.NodeClass              */
+    const uint32_t* computed_class;  /* Node.ComputedClass (node_class.go:31) */
+    const int64_t* cpu_shares;       /* NodeResources.Cpu.CpuShares */
+    const int64_t* memory_mb;        /* NodeResources.Memory.MemoryMB */
+    const int64_t* disk_mb;          /* NodeResources.Disk.DiskMB   */
+    const int64_t* reserved_cpu;     /* ReservedResources.Cpu.CpuShares */
+    const int64_t* reserved_memory_mb;
+    const int64_t* reserved_disk_mb;
+    /* Attributes / Meta maps */
+    const uint32_t* attr_off; const uint32_t* attr_key; const uint32_t* attr_val;
+    const uint32_t* meta_off; const uint32_t* meta_key; const uint32_t* meta_val;
+    /* Drivers map: flags bit0 Detected, bit1 Healthy, bit2 DriverInfo==nil */
+    const uint32_t* drv_off; const uint32_t* drv_name; const uint8_t* drv_flags;
+    /* NodeResources.Networks: mode ("" = host), device, MBits */
+    const uint32_t* net_off; const uint32_t* net_mode; const uint32_t* net_device;
+    const int32_t* net_mbits;
+    /* NodeResources.NodeNetworks[*].Addresses[*].Alias (host networks) */
+    const uint32_t* alias_off; const uint32_t* alias_name;
+    /* node-reserved host ports that fall in the dynamic range [20000,32000) */
+    const int32_t* reserved_dyn_ports;
+    /* HostVolumes map */
+    const uint32_t* hv_off; const uint32_t* hv_name; const uint8_t* hv_read_only;
+    /* NodeResources.Devices (device groups) */
+    const uint32_t* dev_off;
+    const uint32_t* dev_vendor; const uint32_t* dev_type; const uint32_t* dev_name;
+    const uint32_t* dev_healthy;     /* healthy instance count */
+    const uint32_t* dev_attr_off;    /* CSR over device groups */
+    const uint32_t* dev_attr_key; const pe_attr* dev_attr_val;
+} pe_node_table;
+
+/* ---- existing allocations of the snapshot (state AllocsByNode) ---------- */
+typedef struct pe_alloc_table {
+    uint32_t count;
+    const uint32_t* node_row;        /* row in pe_node_table          */
+    const uint32_t* ns;              /* Allocation.Namespace          */
+    const uint32_t* job_id;          /* Allocation.JobID              */
+    const uint32_t* task_group;      /* Allocation.TaskGroup          */
+    const uint8_t* terminal;         /* Allocation.TerminalStatus()   */
+    const int32_t* priority;         /* Allocation.Job.Priority       */
+    const int64_t* cpu_shares;       /* ComparableResources().Flattened.Cpu.CpuShares */
+    const int64_t* memory_mb;        /* ...Flattened.Memory.MemoryMB  */
+    const int64_t* disk_mb;          /* ...Shared.DiskMB              */
+    const int32_t* net_mbits;        /* bandwidth held on the node's host device */
+    const int32_t* dyn_ports;        /* ports held in [20000,32000)  */
+    /* device instances held: CSR over allocs, (device group index on its node, count) */
+    const uint32_t* dev_off; const uint32_t* dev_group; const uint32_t* dev_count;
+} pe_alloc_table;
+
+/* ---- job specification (structs.Job / TaskGroup / Task) ----------------- */
+typedef struct pe_constraint { uint32_t ltarget, rtarget, operand; } pe_constraint;
+typedef struct pe_affinity { uint32_t ltarget, rtarget, operand; int32_t weight; } pe_affinity;
+typedef struct pe_spread_target { uint32_t value; int32_t percent; } pe_spread_target;
+typedef struct pe_spread {
+    uint32_t attribute; int32_t weight;       /* weight is an int8 in structs.Spread */
+    uint32_t target_off, target_count;        /* into pe_job.spread_targets */
+} pe_spread;
+typedef struct pe_device_request {           /* structs.RequestedDevice */
+    uint32_t name; uint32_t _pad; uint64_t count;
+    uint32_t constraint_off, constraint_count; /* into pe_job.device_constraints */
+    uint32_t affinity_off, affinity_count;     /* into pe_job.device_affinities  */
+} pe_device_request;
+#define PE_LC_MAIN 0
+#define PE_LC_PRESTART 1
+#define PE_LC_PRESTART_SIDECAR 2
+#define PE_LC_POSTSTOP 3
+#define PE_LC_POSTSTART 4   /* not counted by AllocatedResources.Comparable() */
+typedef struct pe_task {
+    uint32_t name, driver;
+    int64_t cpu, memory_mb, memory_max_mb;
+    int32_t cores;                            /* reserved cores (not on device path) */
+    uint32_t lifecycle;                       /* PE_LC_* */
+    int32_t has_network, net_mbits, net_dyn_ports, net_reserved_ports;
+    uint32_t constraint_off, constraint_count;
+    uint32_t affinity_off, affinity_count;
+    uint32_t device_off, device_count;
+} pe_task;
+typedef struct pe_task_group {
+    uint32_t name; int32_t count;
+    int64_t ephemeral_disk_mb;
+    uint32_t constraint_off, constraint_count;
+    uint32_t affinity_off, affinity_count;
+    uint32_t spread_off, spread_count;
+    uint32_t task_off, task_count;
+    int32_t has_network; uint32_t net_mode;   /* tg Networks[0] */
+    int32_t net_dyn_ports, net_reserved_ports;
+    uint32_t net_host_network;                /* host network alias of the ports ("default") */
+    uint32_t volume_off, volume_count;        /* host volume requests */
+    int32_t has_csi_volumes;                  /* CSI: not on the device path */
+} pe_task_group;
+#define PE_JOB_SERVICE 0
+#define PE_JOB_BATCH 1
+#define PE_JOB_SYSTEM 2
+#define PE_JOB_SYSBATCH 3
+typedef struct pe_job {
+    uint32_t id, ns, type; int32_t priority;
+    uint64_t version;
+    uint32_t constraint_off, constraint_count;
+    uint32_t affinity_off, affinity_count;
+    uint32_t spread_off, spread_count;
+    uint32_t tg_count;
+    const pe_task_group* task_groups;
+    const pe_task* tasks;
+    const pe_constraint* constraints;        /* job, tg and task constraints */
+    const pe_affinity* affinities;
+    const pe_spread* spreads;
+    const pe_spread_target* spread_targets;
+    const pe_device_request* devices;
+    const pe_constraint* device_constraints;
+    const pe_affinity* device_affinities;
+    const uint32_t* volume_source;           /* host volume requests: source name */
+    const uint8_t* volume_read_only;
+} pe_job;
+
+/* ---- stack configuration (SchedulerConfiguration, operator.go:128-210) --- */
+#define PE_STACK_GENERIC 0
+#define PE_STACK_SYSTEM 1
+#define PE_ALGO_BINPACK 0
+#define PE_ALGO_SPREAD 1
+typedef struct pe_config {
+    uint32_t stack_kind;      /* PE_STACK_* */
+    uint32_t batch;           /* GenericStack batch flag (limit 2) */
+    uint32_t algorithm;       /* PE_ALGO_* */
+    uint32_t memory_oversubscription;
+    uint32_t preempt;         /* eviction enabled for system stacks (stack.go:267-278) */
+    int32_t device;           /* HIP device ordinal */
+} pe_config;
+
+typedef struct pe_select_options {              /* SelectOptions, stack.go:34-39 */
+    const uint32_t* penalty_rows; uint32_t penalty_count;
+    const uint32_t* preferred_rows; uint32_t preferred_count;
+    uint32_t preempt;
+} pe_select_options;
+
+typedef struct pe_ranked_node {                 /* RankedNode, rank.go:21-36 */
+    int32_t row;              /* chosen node row, -1 = nil */
+    uint32_t n_scores;
+    double final_score;
+    double scores[PE_MAX_SCORES];   /* rank order: binpack, device-aff, anti-aff,
+                                       penalty, node-aff, spread, preemption */
+    /* AllocMetric side outputs (structs.go:9826-10026) */
+    uint32_t nodes_evaluated, nodes_filtered, nodes_exhausted;
+    uint32_t new_offset;      /* StaticIterator cursor after the Select */
+} pe_ranked_node;
+
+/* ---- entry points -------------------------------------------------------- */
+typedef struct pe_stack pe_stack;
+
+uint32_t pe_abi_version(void);
+/* NewGenericStack (stack.go:336) / NewSystemStack (stack.go:207) */
+pe_stack* pe_stack_create(const pe_config* cfg);
+void pe_stack_destroy(pe_stack* s);
+const char* pe_last_error(const pe_stack* s);
+/* State snapshot: nodes + non-terminal allocs (scheduler.State, scheduler.go:66-110).
+ * Uploads the node SoA to HBM; stays resident across evals until replaced. */
+int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
+                 const pe_alloc_table* allocs);
+/* Start a new evaluation on the resident snapshot: drop the plan (proposed
+ * allocs), the EvalEligibility memo and the job (NewEvalContext, context.go:86).
+ * The node SoA stays in HBM; only the dynamic columns are restored. */
+int pe_reset_plan(pe_stack* s);
+/* Stack.SetJob (stack.go:93-115 / 290-299). `strs` extends the table given to
+ * pe_set_state (same ids for its first entries, job strings appended). */
+int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* job);
+/* Stack.SetNodes (stack.go:71-91 / 285-288). `rows` is the node list AFTER the
+ * caller's shuffleNodes (util.go:366-372): the engine draws no randomness.
+ * Writes the LimitIterator limit to *limit_out (may be NULL). */
+int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out);
+/* Stack.Select (stack.go:117-179 / 301-333) */
+int pe_select(pe_stack* s, uint32_t tg_index, const pe_select_options* opts,
+              pe_ranked_node* out);
+/* Plan.AppendAlloc (structs.go:10707-10714) of an allocation of task group
+ * `tg_index` on node `row`: the proposed state seen by later Selects. */
+int pe_commit(pe_stack* s, uint32_t tg_index, int32_t row);
+/* Fused count loop of GenericScheduler.computePlacements (generic_sched.go:493-649)
+ * for `count` fresh placements of one task group (no preferred / penalty nodes):
+ * Select -> AppendAlloc repeated on the device; stops at the first nil option
+ * (failedTGAllocs short-circuit, generic_sched.go:519-523).
+ * out[count] receives each placement; *placed the number placed. */
+int pe_place(pe_stack* s, uint32_t tg_index, uint32_t count, pe_ranked_node* out,
+             uint32_t* placed);
+/* SystemScheduler.computePlacements (scheduler_system.go:283-425) for one task
+ * group over every row of the SetNodes list: one single-node Select per row.
+ * out_row_score[n] = FinalScore or NaN when filtered/exhausted;
+ * out_status[n] = 0 placed, 1 filtered, 2 exhausted. Commits placed allocs. */
+int pe_system_place(pe_stack* s, uint32_t tg_index, double* out_score,
+                    uint8_t* out_status, uint32_t* placed);
+/* Milliseconds spent in device kernels by the last pe_place / pe_system_place
+ * (HIP events on the engine's stream). */
+double pe_last_kernel_ms(const pe_stack* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NOMAD_PE_H */

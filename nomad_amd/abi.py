@@ -1,0 +1,196 @@
+"""ctypes mirror of include/nomad_pe.h (the engine's C ABI).
+
+Kept field-for-field identical to the header; tests/test_abi.py checks the
+sizes against offsets the library reports, and that every declared symbol is
+exported by nomad_amd/libnomadpe.so.
+"""
+import ctypes as C
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+i32p = C.POINTER(C.c_int32)
+i64p = C.POINTER(C.c_int64)
+f64p = C.POINTER(C.c_double)
+
+PE_NONE = 0xFFFFFFFF
+PE_MAX_SCORES = 8
+PE_OK, PE_EINVAL, PE_ESTATE, PE_EHIP, PE_EUNSUPPORTED, PE_ENOMEM = 0, -1, -2, -3, -4, -5
+
+PE_ATTR_INT, PE_ATTR_FLOAT, PE_ATTR_STRING, PE_ATTR_BOOL = 1, 2, 3, 4
+PE_LC_MAIN, PE_LC_PRESTART, PE_LC_PRESTART_SIDECAR, PE_LC_POSTSTOP, PE_LC_POSTSTART = 0, 1, 2, 3, 4
+PE_JOB_SERVICE, PE_JOB_BATCH, PE_JOB_SYSTEM, PE_JOB_SYSBATCH = 0, 1, 2, 3
+PE_STACK_GENERIC, PE_STACK_SYSTEM = 0, 1
+PE_ALGO_BINPACK, PE_ALGO_SPREAD = 0, 1
+
+
+class pe_strtab(C.Structure):
+    _fields_ = [("bytes", C.c_char_p), ("offsets", u32p), ("count", C.c_uint32)]
+
+
+class pe_attr(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("unit", C.c_uint32), ("i", C.c_int64), ("f", C.c_double),
+                ("s", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+class pe_node_table(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32),
+        ("id", u32p), ("name", u32p), ("datacenter", u32p), ("node_class", u32p),
+        ("computed_class", u32p),
+        ("cpu_shares", i64p), ("memory_mb", i64p), ("disk_mb", i64p),
+        ("reserved_cpu", i64p), ("reserved_memory_mb", i64p), ("reserved_disk_mb", i64p),
+        ("attr_off", u32p), ("attr_key", u32p), ("attr_val", u32p),
+        ("meta_off", u32p), ("meta_key", u32p), ("meta_val", u32p),
+        ("drv_off", u32p), ("drv_name", u32p), ("drv_flags", u8p),
+        ("net_off", u32p), ("net_mode", u32p), ("net_device", u32p), ("net_mbits", i32p),
+        ("alias_off", u32p), ("alias_name", u32p),
+        ("reserved_dyn_ports", i32p),
+        ("hv_off", u32p), ("hv_name", u32p), ("hv_read_only", u8p),
+        ("dev_off", u32p), ("dev_vendor", u32p), ("dev_type", u32p), ("dev_name", u32p),
+        ("dev_healthy", u32p),
+        ("dev_attr_off", u32p), ("dev_attr_key", u32p), ("dev_attr_val", C.POINTER(pe_attr)),
+    ]
+
+
+class pe_alloc_table(C.Structure):
+    _fields_ = [
+        ("count", C.c_uint32),
+        ("node_row", u32p), ("ns", u32p), ("job_id", u32p), ("task_group", u32p),
+        ("terminal", u8p), ("priority", i32p),
+        ("cpu_shares", i64p), ("memory_mb", i64p), ("disk_mb", i64p),
+        ("net_mbits", i32p), ("dyn_ports", i32p),
+        ("dev_off", u32p), ("dev_group", u32p), ("dev_count", u32p),
+    ]
+
+
+class pe_constraint(C.Structure):
+    _fields_ = [("ltarget", C.c_uint32), ("rtarget", C.c_uint32), ("operand", C.c_uint32)]
+
+
+class pe_affinity(C.Structure):
+    _fields_ = [("ltarget", C.c_uint32), ("rtarget", C.c_uint32), ("operand", C.c_uint32),
+                ("weight", C.c_int32)]
+
+
+class pe_spread_target(C.Structure):
+    _fields_ = [("value", C.c_uint32), ("percent", C.c_int32)]
+
+
+class pe_spread(C.Structure):
+    _fields_ = [("attribute", C.c_uint32), ("weight", C.c_int32),
+                ("target_off", C.c_uint32), ("target_count", C.c_uint32)]
+
+
+class pe_device_request(C.Structure):
+    _fields_ = [("name", C.c_uint32), ("_pad", C.c_uint32), ("count", C.c_uint64),
+                ("constraint_off", C.c_uint32), ("constraint_count", C.c_uint32),
+                ("affinity_off", C.c_uint32), ("affinity_count", C.c_uint32)]
+
+
+class pe_task(C.Structure):
+    _fields_ = [
+        ("name", C.c_uint32), ("driver", C.c_uint32),
+        ("cpu", C.c_int64), ("memory_mb", C.c_int64), ("memory_max_mb", C.c_int64),
+        ("cores", C.c_int32), ("lifecycle", C.c_uint32),
+        ("has_network", C.c_int32), ("net_mbits", C.c_int32), ("net_dyn_ports", C.c_int32),
+        ("net_reserved_ports", C.c_int32),
+        ("constraint_off", C.c_uint32), ("constraint_count", C.c_uint32),
+        ("affinity_off", C.c_uint32), ("affinity_count", C.c_uint32),
+        ("device_off", C.c_uint32), ("device_count", C.c_uint32),
+    ]
+
+
+class pe_task_group(C.Structure):
+    _fields_ = [
+        ("name", C.c_uint32), ("count", C.c_int32),
+        ("ephemeral_disk_mb", C.c_int64),
+        ("constraint_off", C.c_uint32), ("constraint_count", C.c_uint32),
+        ("affinity_off", C.c_uint32), ("affinity_count", C.c_uint32),
+        ("spread_off", C.c_uint32), ("spread_count", C.c_uint32),
+        ("task_off", C.c_uint32), ("task_count", C.c_uint32),
+        ("has_network", C.c_int32), ("net_mode", C.c_uint32),
+        ("net_dyn_ports", C.c_int32), ("net_reserved_ports", C.c_int32),
+        ("net_host_network", C.c_uint32),
+        ("volume_off", C.c_uint32), ("volume_count", C.c_uint32),
+        ("has_csi_volumes", C.c_int32),
+    ]
+
+
+class pe_job(C.Structure):
+    _fields_ = [
+        ("id", C.c_uint32), ("ns", C.c_uint32), ("type", C.c_uint32), ("priority", C.c_int32),
+        ("version", C.c_uint64),
+        ("constraint_off", C.c_uint32), ("constraint_count", C.c_uint32),
+        ("affinity_off", C.c_uint32), ("affinity_count", C.c_uint32),
+        ("spread_off", C.c_uint32), ("spread_count", C.c_uint32),
+        ("tg_count", C.c_uint32),
+        ("task_groups", C.POINTER(pe_task_group)),
+        ("tasks", C.POINTER(pe_task)),
+        ("constraints", C.POINTER(pe_constraint)),
+        ("affinities", C.POINTER(pe_affinity)),
+        ("spreads", C.POINTER(pe_spread)),
+        ("spread_targets", C.POINTER(pe_spread_target)),
+        ("devices", C.POINTER(pe_device_request)),
+        ("device_constraints", C.POINTER(pe_constraint)),
+        ("device_affinities", C.POINTER(pe_affinity)),
+        ("volume_source", u32p),
+        ("volume_read_only", u8p),
+    ]
+
+
+class pe_config(C.Structure):
+    _fields_ = [("stack_kind", C.c_uint32), ("batch", C.c_uint32), ("algorithm", C.c_uint32),
+                ("memory_oversubscription", C.c_uint32), ("preempt", C.c_uint32),
+                ("device", C.c_int32)]
+
+
+class pe_select_options(C.Structure):
+    _fields_ = [("penalty_rows", u32p), ("penalty_count", C.c_uint32),
+                ("preferred_rows", u32p), ("preferred_count", C.c_uint32),
+                ("preempt", C.c_uint32)]
+
+
+class pe_ranked_node(C.Structure):
+    _fields_ = [("row", C.c_int32), ("n_scores", C.c_uint32), ("final_score", C.c_double),
+                ("scores", C.c_double * PE_MAX_SCORES),
+                ("nodes_evaluated", C.c_uint32), ("nodes_filtered", C.c_uint32),
+                ("nodes_exhausted", C.c_uint32), ("new_offset", C.c_uint32)]
+
+
+# Entry points declared in include/nomad_pe.h: (name, restype, argtypes)
+def _sigs(prefix, handle):
+    H = C.c_void_p
+    return [
+        (prefix + "set_state", C.c_int, [H, C.POINTER(pe_strtab), C.POINTER(pe_node_table),
+                                         C.POINTER(pe_alloc_table)]),
+        (prefix + "set_job", C.c_int, [H, C.POINTER(pe_strtab), C.POINTER(pe_job)]),
+        (prefix + "reset_plan", C.c_int, [H]),
+        (prefix + "set_nodes", C.c_int, [H, u32p, C.c_uint32, u32p]),
+        (prefix + "select", C.c_int, [H, C.c_uint32, C.POINTER(pe_select_options),
+                                      C.POINTER(pe_ranked_node)]),
+        (prefix + "commit", C.c_int, [H, C.c_uint32, C.c_int32]),
+        (prefix + "place", C.c_int, [H, C.c_uint32, C.c_uint32, C.POINTER(pe_ranked_node), u32p]),
+        (prefix + "system_place", C.c_int, [H, C.c_uint32, f64p, u8p, u32p]),
+    ]
+
+
+ENGINE_SYMBOLS = [
+    "pe_abi_version", "pe_stack_create", "pe_stack_destroy", "pe_last_error", "pe_set_state",
+    "pe_reset_plan", "pe_set_job", "pe_set_nodes", "pe_select", "pe_commit", "pe_place", "pe_system_place",
+    "pe_last_kernel_ms",
+]
+
+
+def bind(lib, prefix, create_name, destroy_name, error_name):
+    """Attach restype/argtypes for the stack API on a loaded CDLL."""
+    for name, res, args in _sigs(prefix, None):
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    getattr(lib, create_name).restype = C.c_void_p
+    getattr(lib, create_name).argtypes = [C.POINTER(pe_config)]
+    getattr(lib, destroy_name).restype = None
+    getattr(lib, destroy_name).argtypes = [C.c_void_p]
+    getattr(lib, error_name).restype = C.c_char_p
+    getattr(lib, error_name).argtypes = [C.c_void_p]
+    return lib

@@ -1,0 +1,308 @@
+// Host-side constraint semantics (see constraint_eval.h).
+#include "constraint_eval.h"
+
+#include <algorithm>
+#include <cctype>
+#include <climits>
+
+namespace pe {
+
+namespace {
+
+inline bool ident_char(char c) { return std::isalnum((unsigned char)c) || c == '-' || c == '~'; }
+inline bool alpha_lead(char c) { return std::isalpha((unsigned char)c) || c == '-' || c == '~'; }
+inline bool digit(char c) { return c >= '0' && c <= '9'; }
+
+// strconv.ParseInt(s, 10, 64)
+bool to_i64(const std::string& s, int64_t* out) {
+    if (s.empty()) return false;
+    size_t i = 0;
+    bool neg = false;
+    if (s[0] == '+' || s[0] == '-') {
+        neg = s[0] == '-';
+        if (s.size() == 1) return false;
+        i = 1;
+    }
+    unsigned long long acc = 0;
+    const unsigned long long lim = neg ? (unsigned long long)INT64_MAX + 1ull : (unsigned long long)INT64_MAX;
+    for (; i < s.size(); i++) {
+        if (!digit(s[i])) return false;
+        unsigned d = (unsigned)(s[i] - '0');
+        if (acc > (lim - d) / 10) return false;
+        acc = acc * 10 + d;
+    }
+    *out = neg ? (int64_t)(0 - acc) : (int64_t)acc;
+    return true;
+}
+
+// ident+ ('.' ident+)* starting at p (first char already validated by caller
+// as part of an ident run). Returns the end position.
+size_t scan_dotted(const std::string& s, size_t p) {
+    while (p < s.size() && ident_char(s[p])) p++;
+    while (p + 1 < s.size() && s[p] == '.' && ident_char(s[p + 1])) {
+        p++;
+        while (p < s.size() && ident_char(s[p])) p++;
+    }
+    return p;
+}
+
+std::vector<std::string> split_on(const std::string& s, char sep) {
+    std::vector<std::string> out;
+    size_t b = 0;
+    for (;;) {
+        size_t e = s.find(sep, b);
+        out.emplace_back(s, b, e == std::string::npos ? std::string::npos : e - b);
+        if (e == std::string::npos) return out;
+        b = e + 1;
+    }
+}
+
+std::string strip(const std::string& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && std::isspace((unsigned char)s[a])) a++;
+    while (b > a && std::isspace((unsigned char)s[b - 1])) b--;
+    return s.substr(a, b - a);
+}
+
+int cmp_pre_part(const std::string& a, const std::string& b) {
+    if (a == b) return 0;
+    int64_t ai = 0, bi = 0;
+    const bool an = to_i64(a, &ai), bn = to_i64(b, &bi);
+    if (a.empty()) return bn ? -1 : 1;
+    if (b.empty()) return an ? 1 : -1;
+    if (an != bn) return an ? -1 : 1;
+    if (!an) return a > b ? 1 : -1;
+    return ai > bi ? 1 : -1;
+}
+
+std::string canonical(const SemVer& v) {
+    std::string o;
+    for (size_t i = 0; i < v.seg.size(); i++) {
+        if (i) o.push_back('.');
+        o += std::to_string(v.seg[i]);
+    }
+    if (!v.pre.empty()) o += "-" + v.pre;
+    if (!v.meta.empty()) o += "+" + v.meta;
+    return o;
+}
+
+}  // namespace
+
+bool parse_version(const std::string& s, bool semver, SemVer* out) {
+    size_t p = 0;
+    if (p < s.size() && s[p] == 'v') p++;
+    // segments: [0-9]+ ('.' [0-9]+)*
+    size_t seg_begin = p;
+    if (p >= s.size() || !digit(s[p])) return false;
+    while (p < s.size() && digit(s[p])) p++;
+    while (p + 1 < s.size() && s[p] == '.' && digit(s[p + 1])) {
+        p++;
+        while (p < s.size() && digit(s[p])) p++;
+    }
+    const std::string segs = s.substr(seg_begin, p - seg_begin);
+    std::string pre;
+    if (p < s.size() && s[p] != '+') {
+        if (s[p] == '-' && p + 1 < s.size() && digit(s[p + 1])) {
+            // numeric-led prerelease (group 4)
+            size_t e = scan_dotted(s, p + 1);
+            pre = s.substr(p + 1, e - p - 1);
+            p = e;
+        } else if (s[p] == '-' && p + 1 < s.size() && alpha_lead(s[p + 1])) {
+            size_t e = scan_dotted(s, p + 1);
+            pre = s.substr(p + 1, e - p - 1);
+            p = e;
+        } else if (!semver && alpha_lead(s[p])) {
+            // '-?' matched empty: the run starts at p (may itself be '-')
+            size_t e = scan_dotted(s, p);
+            pre = s.substr(p, e - p);
+            p = e;
+        } else {
+            return false;
+        }
+    }
+    std::string meta;
+    if (p < s.size() && s[p] == '+') {
+        if (p + 1 >= s.size() || !ident_char(s[p + 1])) return false;
+        size_t e = scan_dotted(s, p + 1);
+        meta = s.substr(p + 1, e - p - 1);
+        p = e;
+    }
+    if (p != s.size()) return false;
+    SemVer v;
+    for (const std::string& part : split_on(segs, '.')) {
+        int64_t x;
+        if (!to_i64(part, &x)) return false;
+        v.seg.push_back(x);
+    }
+    v.specified = (int)v.seg.size();
+    while (v.seg.size() < 3) v.seg.push_back(0);
+    v.pre = pre;
+    v.meta = meta;
+    *out = v;
+    return true;
+}
+
+int compare_versions(const SemVer& a, const SemVer& b) {
+    if (canonical(a) == canonical(b)) return 0;
+    if (a.seg == b.seg) {
+        if (a.pre.empty() && b.pre.empty()) return 0;
+        if (a.pre.empty()) return 1;
+        if (b.pre.empty()) return -1;
+        if (a.pre == b.pre) return 0;
+        auto pa = split_on(a.pre, '.'), pb = split_on(b.pre, '.');
+        const size_t n = std::max(pa.size(), pb.size());
+        for (size_t i = 0; i < n; i++) {
+            int c = cmp_pre_part(i < pa.size() ? pa[i] : std::string(), i < pb.size() ? pb[i] : std::string());
+            if (c) return c;
+        }
+        return 0;
+    }
+    const size_t la = a.seg.size(), lb = b.seg.size(), hs = std::max(la, lb);
+    for (size_t i = 0; i < hs; i++) {
+        if (i >= la) {
+            for (size_t k = i; k < lb; k++) if (b.seg[k] != 0) return -1;
+            return 0;
+        }
+        if (i >= lb) {
+            for (size_t k = i; k < la; k++) if (a.seg[k] != 0) return 1;
+            return 0;
+        }
+        if (a.seg[i] != b.seg[i]) return a.seg[i] < b.seg[i] ? -1 : 1;
+    }
+    return 0;
+}
+
+bool parse_version_constraints(const std::string& s, bool semver, std::vector<VersionConstraint>* out) {
+    static const struct { const char* tok; int op; } kOps[] = {
+        {"~>", 6}, {">=", 4}, {"<=", 5}, {"!=", 1}, {">", 2}, {"<", 3}, {"=", 0}};
+    out->clear();
+    for (const std::string& raw : split_on(s, ',')) {
+        std::string t = strip(raw);
+        int op = 0;
+        size_t skip = 0;
+        for (const auto& o : kOps) {
+            const size_t L = std::char_traits<char>::length(o.tok);
+            if (t.compare(0, L, o.tok) == 0) {
+                if (o.op == 6 && semver) return false;   // semver has no pessimistic operator
+                op = o.op;
+                skip = L;
+                break;
+            }
+        }
+        VersionConstraint c;
+        c.op = op;
+        if (!parse_version(strip(t.substr(skip)), semver, &c.v)) return false;
+        out->push_back(c);
+    }
+    return true;
+}
+
+static bool prerelease_ok(const SemVer& v, const SemVer& c) {
+    const bool vp = !v.pre.empty(), cp = !c.pre.empty();
+    if (cp && vp) return c.seg == v.seg;
+    if (!cp && vp) return false;
+    return true;
+}
+
+bool check_version_constraints(const std::vector<VersionConstraint>& cs, const SemVer& v, bool semver) {
+    for (const auto& c : cs) {
+        bool ok;
+        switch (c.op) {
+            case 0: ok = compare_versions(v, c.v) == 0; break;
+            case 1: ok = compare_versions(v, c.v) != 0; break;
+            case 2: ok = (semver || prerelease_ok(v, c.v)) && compare_versions(v, c.v) == 1; break;
+            case 3: ok = (semver || prerelease_ok(v, c.v)) && compare_versions(v, c.v) == -1; break;
+            case 4: ok = (semver || prerelease_ok(v, c.v)) && compare_versions(v, c.v) >= 0; break;
+            case 5: ok = (semver || prerelease_ok(v, c.v)) && compare_versions(v, c.v) <= 0; break;
+            case 6: {
+                ok = prerelease_ok(v, c.v) && !(!c.v.pre.empty() && v.pre.empty());
+                if (ok && compare_versions(v, c.v) == -1) ok = false;
+                const size_t cs_len = c.v.seg.size();
+                if (ok && cs_len > v.seg.size()) ok = false;
+                for (int i = 0; ok && i < c.v.specified - 1; i++)
+                    if (v.seg[i] != c.v.seg[i]) ok = false;
+                if (ok && c.v.seg[cs_len - 1] > v.seg[cs_len - 1]) ok = false;
+                break;
+            }
+            default: ok = false;
+        }
+        if (!ok) return false;
+    }
+    return true;
+}
+
+bool ConstraintEvaluator::version_match(bool semver, const Target& l, const Target& r) {
+    if (l.nil || r.nil) return false;
+    SemVer v;
+    if (!parse_version(l.value, false, &v)) return false;
+    auto& cache = ver_cache_[semver ? 1 : 0];
+    auto it = cache.find(r.value);
+    if (it == cache.end()) {
+        auto cs = std::make_shared<std::vector<VersionConstraint>>();
+        if (!parse_version_constraints(r.value, semver, cs.get())) return false;
+        it = cache.emplace(r.value, cs).first;
+    }
+    return check_version_constraints(*it->second, v, semver);
+}
+
+bool ConstraintEvaluator::regexp_match(const Target& l, const Target& r) {
+    if (l.nil || r.nil) return false;
+    if (re_bad_.count(r.value)) return false;
+    auto it = re_cache_.find(r.value);
+    if (it == re_cache_.end()) {
+        try {
+            it = re_cache_.emplace(r.value, std::make_shared<std::regex>(r.value, std::regex::ECMAScript)).first;
+        } catch (const std::regex_error&) {
+            re_bad_[r.value] = true;
+            return false;
+        }
+    }
+    return std::regex_search(l.value, *it->second);
+}
+
+static bool set_contains(const Target& l, const Target& r, bool all) {
+    if (l.nil || r.nil) return false;
+    std::vector<std::string> have;
+    for (auto& x : split_on(l.value, ',')) have.push_back(strip(x));
+    std::sort(have.begin(), have.end());
+    for (auto& x : split_on(r.value, ',')) {
+        const bool in = std::binary_search(have.begin(), have.end(), strip(x));
+        if (all && !in) return false;
+        if (!all && in) return true;
+    }
+    return all;
+}
+
+static bool same(const Target& a, const Target& b) {   // reflect.DeepEqual on resolved values
+    if (a.nil || b.nil) return a.nil && b.nil;
+    return a.value == b.value;
+}
+
+bool ConstraintEvaluator::check(const std::string& op, const Target& l, const Target& r) {
+    if (op == "distinct_hosts" || op == "distinct_property") return true;
+    if (op == "=" || op == "==" || op == "is") return l.found && r.found && same(l, r);
+    if (op == "!=" || op == "not") return !same(l, r);
+    if (op == "<" || op == "<=" || op == ">" || op == ">=") {
+        if (!(l.found && r.found) || l.nil || r.nil) return false;
+        const int c = l.value.compare(r.value);
+        if (op == "<") return c < 0;
+        if (op == "<=") return c <= 0;
+        if (op == ">") return c > 0;
+        return c >= 0;
+    }
+    if (op == "is_set") return l.found;
+    if (op == "is_not_set") return !l.found;
+    if (op == "version") return l.found && r.found && version_match(false, l, r);
+    if (op == "semver") return l.found && r.found && version_match(true, l, r);
+    if (op == "regexp") return l.found && r.found && regexp_match(l, r);
+    if (op == "set_contains" || op == "set_contains_all") return l.found && r.found && set_contains(l, r, true);
+    if (op == "set_contains_any") return l.found && r.found && set_contains(l, r, false);
+    return false;
+}
+
+bool target_escapes(const std::string& t) {
+    return t.rfind("${node.unique.", 0) == 0 || t.rfind("${attr.unique.", 0) == 0 ||
+           t.rfind("${meta.unique.", 0) == 0;
+}
+
+}  // namespace pe

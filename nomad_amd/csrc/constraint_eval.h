@@ -1,0 +1,61 @@
+// Host-side constraint semantics for pre-resolution (product code).
+//
+// The engine evaluates constraints once per distinct (class | value) on the
+// host and ships the verdicts to HBM as class / value tables. This header
+// implements the operand semantics of scheduler/feasible.go:785-1024
+// (checkConstraint and friends), go-version constraint matching
+// (github.com/hashicorp/go-version @ 2046c9d0f0b0, go.mod:75) and the semver
+// operand (helper/constraints/semver/constraints.go). Version strings are
+// parsed by a hand-written scanner equivalent to go-version's
+// VersionRegexpRaw / SemverRegexpRaw.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+#include <unordered_map>
+#include <memory>
+#include <regex>
+
+namespace pe {
+
+// A resolved constraint target: Go's (interface{}, found). `nil` only for an
+// unknown ${...} interpolation; a missing attribute is ("", false).
+struct Target {
+    bool nil = true;
+    bool found = false;
+    std::string value;
+};
+
+struct SemVer {
+    std::vector<int64_t> seg;   // padded to >= 3
+    int specified = 0;
+    std::string pre, meta;
+};
+
+// go-version NewVersion (semver=false) / NewSemver (semver=true)
+bool parse_version(const std::string& s, bool semver, SemVer* out);
+int compare_versions(const SemVer& a, const SemVer& b);
+
+struct VersionConstraint {
+    int op;        // 0 = 1 != 2 > 3 < 4 >= 5 <= 6 ~>
+    SemVer v;
+};
+bool parse_version_constraints(const std::string& s, bool semver, std::vector<VersionConstraint>* out);
+bool check_version_constraints(const std::vector<VersionConstraint>& cs, const SemVer& v, bool semver);
+
+class ConstraintEvaluator {
+public:
+    // checkConstraint (feasible.go:785-820)
+    bool check(const std::string& op, const Target& l, const Target& r);
+
+private:
+    bool version_match(bool semver, const Target& l, const Target& r);
+    bool regexp_match(const Target& l, const Target& r);
+    std::unordered_map<std::string, std::shared_ptr<std::vector<VersionConstraint>>> ver_cache_[2];
+    std::unordered_map<std::string, std::shared_ptr<std::regex>> re_cache_;
+    std::unordered_map<std::string, bool> re_bad_;
+};
+
+bool target_escapes(const std::string& t);   // node_class.go:120-132
+
+}  // namespace pe

@@ -1,0 +1,1163 @@
+// Host side of the MI355X placement engine: the C ABI of include/nomad_pe.h.
+//
+// Responsibilities (everything that is string work or per-eval setup):
+//  - pe_set_state: intern the snapshot, build the node SoA (row order) and
+//    upload it to HBM; base proposed usage from the non-terminal allocs.
+//  - pe_set_job:   parse the job, compute the task groups' resource asks
+//    (AllocatedResources.Comparable, structs.go:3445-3487), collision counts
+//    and spread use counts from the snapshot's allocs.
+//  - per Select:   pre-resolve constraints / drivers / volumes / networks per
+//    ComputedClass with the EvalEligibility memo emulated exactly (first node
+//    of a class in visit order decides, context.go:293-345, feasible.go:1061),
+//    node affinity per class, spread property values per class; upload the
+//    tables and launch the fused kernel (kernels.hip).
+// Nothing here evaluates a node's ranking on the CPU: feasibility of resources,
+// scoring and selection all run on the device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/nomad_pe.h"
+#include "constraint_eval.h"
+#include "engine_types.h"
+#include "gomath_dev.h"
+
+extern "C" hipError_t pe_launch_place(const pe::SelectArgs* a, hipStream_t st);
+extern "C" hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
+extern "C" hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a,
+                                       uint32_t row, hipStream_t st);
+
+namespace {
+
+using pe::Target;
+
+static std::string g_error;   // errors without a handle (create failures)
+
+struct DevMem {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevMem() = default;
+    DevMem(const DevMem&) = delete;
+    DevMem& operator=(const DevMem&) = delete;
+    ~DevMem() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t ensure(size_t b) {
+        if (b <= bytes && p) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&p, b ? b : 16);
+        if (e == hipSuccess) bytes = b ? b : 16;
+        return e;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostNode {
+    uint32_t id, name, dc, node_class, cclass;
+    uint32_t cls;
+    std::vector<std::pair<uint32_t, uint32_t>> attrs, meta;   // sorted by key id
+    std::vector<std::pair<uint32_t, uint8_t>> drivers;        // sorted by name id
+    std::vector<uint32_t> net_modes;
+    int n_device_nets;
+    int32_t first_mbits;
+    std::vector<uint32_t> aliases;
+    std::vector<std::pair<uint32_t, uint8_t>> volumes;        // sorted by name id
+    int n_devices;
+};
+
+struct HostAlloc {
+    uint32_t row, ns, job, tg;
+    bool terminal;
+};
+
+enum TargetKind { T_LITERAL, T_ID, T_DC, T_NAME, T_CLASS, T_ATTR, T_META, T_NIL };
+struct ParsedTarget {
+    TargetKind kind;
+    uint32_t key;          // attr/meta key str id (PE_NONE: key never interned -> absent)
+    std::string literal;
+    bool escapes;
+};
+
+struct ParsedConstraint {
+    ParsedTarget l, r;
+    std::string op;
+    bool escapes;
+};
+
+struct ParsedAffinity {
+    ParsedConstraint c;
+    int32_t weight;
+};
+
+struct SpreadSpec {
+    uint32_t attribute;            // str id of the attribute target
+    int32_t weight;
+    std::vector<std::pair<uint32_t, int32_t>> targets;
+};
+
+struct PsetDev {
+    ParsedTarget target;
+    std::unordered_map<uint32_t, uint32_t> value_index;   // str id -> dense
+    std::vector<uint32_t> value_str;
+    DevMem val_class, val_node, counts, desired;
+    std::vector<uint32_t> h_counts;
+    std::vector<double> h_desired;
+    bool even = false;
+    double weight_frac = 0;
+    bool per_node = false;
+};
+
+struct TgPlan {
+    uint32_t name;
+    int32_t count;
+    pe::Ask ask;
+    std::vector<ParsedConstraint> constraints;   // tg + task constraints
+    std::set<uint32_t> drivers;
+    std::vector<std::pair<uint32_t, bool>> volumes;
+    bool has_network = false;
+    uint32_t net_mode = 0, net_host = 0;
+    int32_t net_ports = 0;
+    std::vector<ParsedAffinity> affinities;      // job + tg + task
+    std::vector<SpreadSpec> spreads;             // tg spreads (job spreads kept on the job)
+    bool escaped = false;
+    std::string unsupported;
+    // device tables
+    DevMem class_ok, node_ok, class_aff, node_aff, alias_ok, coll_tg;
+    bool tables_valid = false;
+    bool has_aff_table = false, node_aff_used = false, node_ok_used = false, alias_used = false;
+    std::vector<std::unique_ptr<PsetDev>> psets;
+    bool psets_built = false;
+};
+
+}  // namespace
+
+struct pe_stack {
+    pe_config cfg{};
+    std::string err;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0;
+
+    // strings
+    std::vector<std::string> strs;
+    std::unordered_map<std::string, uint32_t> sid;
+
+    // state
+    std::vector<HostNode> nodes;
+    std::vector<HostAlloc> allocs;
+    uint32_t ncls = 0;
+    std::vector<uint32_t> class_rep;   // first row of each class
+    std::vector<int64_t> h_cap_cpu, h_cap_mem, h_cap_disk;
+    std::vector<int64_t> h_base_cpu, h_base_mem, h_base_disk;
+    std::vector<int32_t> h_base_mbits, h_base_dyn;
+    DevMem d_cls, d_cap_cpu, d_cap_mem, d_cap_disk, d_avail_mbits;
+    DevMem d_used_cpu, d_used_mem, d_used_disk, d_used_mbits, d_used_dyn, d_coll_job;
+    bool have_state = false;
+
+    // job
+    bool have_job = false, have_job_version = false;
+    uint64_t job_version = 0;
+    uint32_t job_id = 0, job_ns = 0;
+    int32_t job_priority = 0;
+    std::vector<ParsedConstraint> job_constraints;
+    bool job_escaped = false;
+    std::vector<ParsedAffinity> job_affinities;
+    std::vector<SpreadSpec> job_spreads;
+    std::vector<std::unique_ptr<TgPlan>> tgs;
+    std::vector<std::pair<uint32_t, uint32_t>> plan;   // committed (tg name id, row)
+
+    // SpreadIterator bookkeeping (spread.go:99-102, 254)
+    std::set<uint32_t> spread_info_done;
+    int32_t sum_spread_weights = 0;
+
+    // EvalEligibility memo, per task-group name: class -> -1 undecided / 0 / 1
+    std::map<uint32_t, std::vector<int8_t>> tg_memo;
+    std::vector<int8_t> job_memo;
+
+    // visit order
+    std::vector<uint32_t> visit;
+    DevMem d_visit, d_pref, d_penalty, d_out, d_status;
+    uint32_t offset = 0;
+    uint32_t limit = 2;
+    double log10 = 0;
+
+    // ---- helpers --------------------------------------------------------
+    int fail(int code, const std::string& m) { err = m; return code; }
+    const std::string& S(uint32_t id) const {
+        static const std::string empty;
+        return id < strs.size() ? strs[id] : empty;
+    }
+    uint32_t lookup(const std::string& s) const {
+        auto it = sid.find(s);
+        return it == sid.end() ? PE_NONE : it->second;
+    }
+    void add_strings(const pe_strtab* t) {
+        for (uint32_t i = (uint32_t)strs.size(); t && i < t->count; i++) {
+            strs.emplace_back(t->bytes + t->offsets[i], t->offsets[i + 1] - t->offsets[i]);
+            sid.emplace(strs.back(), i);
+        }
+    }
+};
+
+namespace {
+
+#define HIP_TRY(s, expr)                                                                \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess) return (s)->fail(PE_EHIP, std::string(#expr ": ") +       \
+                                               hipGetErrorString(_e));                  \
+    } while (0)
+
+template <class T>
+hipError_t upload(DevMem& m, const std::vector<T>& h) {
+    hipError_t e = m.ensure(h.size() * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (h.empty()) return hipSuccess;
+    return hipMemcpy(m.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+ParsedTarget parse_target(const pe_stack* s, const std::string& t) {
+    ParsedTarget p;
+    p.key = PE_NONE;
+    p.escapes = pe::target_escapes(t);
+    if (t.rfind("${", 0) != 0) { p.kind = T_LITERAL; p.literal = t; return p; }
+    if (t == "${node.unique.id}") { p.kind = T_ID; return p; }
+    if (t == "${node.datacenter}") { p.kind = T_DC; return p; }
+    if (t == "${node.unique.name}") { p.kind = T_NAME; return p; }
+    if (t == "${node.class}") { p.kind = T_CLASS; return p; }
+    auto strip = [&](size_t pre) {
+        std::string k = t.substr(pre);
+        if (!k.empty() && k.back() == '}') k.pop_back();
+        return k;
+    };
+    if (t.rfind("${attr.", 0) == 0) { p.kind = T_ATTR; p.key = s->lookup(strip(7)); return p; }
+    if (t.rfind("${meta.", 0) == 0) { p.kind = T_META; p.key = s->lookup(strip(7)); return p; }
+    p.kind = T_NIL;
+    return p;
+}
+
+bool find_kv(const std::vector<std::pair<uint32_t, uint32_t>>& v, uint32_t key, uint32_t* val) {
+    auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(key, 0u));
+    if (it == v.end() || it->first != key) return false;
+    *val = it->second;
+    return true;
+}
+
+// resolveTarget (feasible.go:748-781) on a host node; returns the value str id
+// in *vid when the value comes from the node (PE_NONE for literals / absent).
+Target resolve(const pe_stack* s, const ParsedTarget& p, const HostNode& n, uint32_t* vid = nullptr) {
+    Target t;
+    t.nil = false;
+    uint32_t v = PE_NONE;
+    switch (p.kind) {
+        case T_LITERAL: t.found = true; t.value = p.literal; break;
+        case T_ID: v = n.id; break;
+        case T_DC: v = n.dc; break;
+        case T_NAME: v = n.name; break;
+        case T_CLASS: v = n.node_class; break;
+        case T_ATTR:
+        case T_META: {
+            uint32_t x;
+            if (p.key != PE_NONE && find_kv(p.kind == T_ATTR ? n.attrs : n.meta, p.key, &x)) v = x;
+            else { t.found = false; t.value.clear(); if (vid) *vid = PE_NONE; return t; }
+            break;
+        }
+        case T_NIL: t.nil = true; t.found = false; if (vid) *vid = PE_NONE; return t;
+    }
+    if (v != PE_NONE) { t.found = true; t.value = s->S(v); }
+    if (vid) *vid = v;
+    return t;
+}
+
+ParsedConstraint parse_constraint(const pe_stack* s, const pe_constraint& c) {
+    ParsedConstraint p;
+    p.l = parse_target(s, s->S(c.ltarget));
+    p.r = parse_target(s, s->S(c.rtarget));
+    p.op = s->S(c.operand);
+    p.escapes = p.l.escapes || p.r.escapes;
+    return p;
+}
+
+bool meets(const pe_stack* s, pe::ConstraintEvaluator& ev, const ParsedConstraint& c, const HostNode& n) {
+    Target l = resolve(s, c.l, n), r = resolve(s, c.r, n);
+    return ev.check(c.op, l, r);
+}
+
+// job checkers (ConstraintChecker over job constraints)
+bool job_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const HostNode& n) {
+    for (auto& c : s->job_constraints) if (!meets(s, ev, c, n)) return false;
+    return true;
+}
+
+// tg checkers in GenericStack/SystemStack order: drivers, constraints, host
+// volumes, devices, network (stack.go:241-247, 374-380)
+bool tg_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g, const HostNode& n) {
+    for (uint32_t d : g.drivers) {   // DriverChecker.hasDrivers (feasible.go:462-500)
+        auto it = std::lower_bound(n.drivers.begin(), n.drivers.end(), std::make_pair(d, (uint8_t)0));
+        if (it != n.drivers.end() && it->first == d) {
+            const uint8_t f = it->second;
+            if (f & 4) return false;
+            if ((f & 1) && (f & 2)) continue;
+            return false;
+        }
+        uint32_t key = s->lookup("driver." + s->S(d)), val;
+        if (key == PE_NONE || !find_kv(n.attrs, key, &val)) return false;
+        const std::string& v = s->S(val);
+        if (v == "1" || v == "t" || v == "T" || v == "true" || v == "TRUE" || v == "True") continue;
+        return false;   // "0"/false or ParseBool error
+    }
+    for (auto& c : g.constraints) if (!meets(s, ev, c, n)) return false;
+    if (!g.volumes.empty()) {   // HostVolumeChecker.hasVolumes (feasible.go:171-207)
+        std::map<uint32_t, std::vector<bool>> req;
+        for (auto& v : g.volumes) req[v.first].push_back(v.second);
+        if (req.size() > n.volumes.size()) return false;
+        for (auto& kv : req) {
+            auto it = std::lower_bound(n.volumes.begin(), n.volumes.end(), std::make_pair(kv.first, (uint8_t)0));
+            if (it == n.volumes.end() || it->first != kv.first) return false;
+            if (!it->second) continue;
+            for (bool ro : kv.second) if (!ro) return false;
+        }
+    }
+    {   // NetworkChecker (feasible.go:362-429): runs for every task group; without a
+        // tg network it keeps the mode of the last one set (default "host").
+        const std::string want = s->S(g.net_mode).empty() ? std::string("host") : s->S(g.net_mode);
+        bool has = false;
+        for (uint32_t m : n.net_modes) {
+            const std::string& mode = s->S(m).empty() ? std::string("host") : s->S(m);
+            if (mode == want) { has = true; break; }
+        }
+        if (!has) {
+            bool legacy = false;
+            if (want == "bridge") {
+                uint32_t key = s->lookup("nomad.version"), val;
+                pe::SemVer v, c;
+                if (key != PE_NONE && find_kv(n.attrs, key, &val) && pe::parse_version(s->S(val), true, &v) &&
+                    pe::parse_version("0.12", false, &c)) {
+                    const bool pre_ok = v.pre.empty();
+                    legacy = pre_ok && pe::compare_versions(v, c) == -1;
+                }
+            }
+            if (!legacy) return false;
+        } else if (g.net_ports > 0) {
+            // hasHostNetworks: every port's host network must be an alias on the node
+            ParsedTarget hn = parse_target(s, s->S(g.net_host));
+            Target t = resolve(s, hn, n);
+            if (!t.found) return false;
+            uint32_t want_id = s->lookup(t.value);
+            if (std::find(n.aliases.begin(), n.aliases.end(), want_id) == n.aliases.end()) return false;
+        }
+    }
+    return true;
+}
+
+// AllocatedResources.Comparable() with lifecycle rules (structs.go:3445-3487)
+void tg_ask(const pe_job* j, const pe_task_group& t, pe::Ask* a) {
+    int64_t sc_c = 0, sc_m = 0, eph_c = 0, eph_m = 0, main_c = 0, main_m = 0, ps_c = 0, ps_m = 0;
+    a->task_mbits = 0; a->task_dyn = 0; a->has_task_net = 0;
+    for (uint32_t k = 0; k < t.task_count; k++) {
+        const pe_task& x = j->tasks[t.task_off + k];
+        switch (x.lifecycle) {
+            case PE_LC_MAIN: main_c += x.cpu; main_m += x.memory_mb; break;
+            case PE_LC_PRESTART: eph_c += x.cpu; eph_m += x.memory_mb; break;
+            case PE_LC_PRESTART_SIDECAR: sc_c += x.cpu; sc_m += x.memory_mb; break;
+            case PE_LC_POSTSTOP: ps_c += x.cpu; ps_m += x.memory_mb; break;
+            default: break;
+        }
+        if (x.has_network) {
+            a->has_task_net = 1;
+            a->task_mbits += x.net_mbits;
+            a->task_dyn += x.net_dyn_ports;
+        }
+    }
+    eph_c = std::max(std::max(eph_c, main_c), ps_c);
+    eph_m = std::max(std::max(eph_m, main_m), ps_m);
+    a->cpu = sc_c + eph_c;
+    a->mem = sc_m + eph_m;
+    a->disk = t.ephemeral_disk_mb;
+    a->tg_dyn = t.has_network ? t.net_dyn_ports : 0;
+    // NetworkIndex.AddAllocs contribution of the placed alloc (network.go:144-193)
+    if (t.has_network && t.net_dyn_ports + t.net_reserved_ports > 0) {
+        a->commit_mbits = 0;
+        a->commit_dyn = t.net_dyn_ports;
+    } else {
+        a->commit_mbits = a->task_mbits;
+        a->commit_dyn = a->task_dyn;
+    }
+    a->desired_count = t.count;
+}
+
+int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) {
+    const uint32_t n = nt->n;
+    s->nodes.assign(n, HostNode());
+    std::unordered_map<uint32_t, uint32_t> cls_of;
+    s->class_rep.clear();
+    s->h_cap_cpu.resize(n); s->h_cap_mem.resize(n); s->h_cap_disk.resize(n);
+    s->h_base_cpu.assign(n, 0); s->h_base_mem.assign(n, 0); s->h_base_disk.assign(n, 0);
+    s->h_base_mbits.assign(n, 0); s->h_base_dyn.assign(n, 0);
+    std::vector<uint32_t> h_cls(n);
+    std::vector<int32_t> h_avail(n);
+    for (uint32_t i = 0; i < n; i++) {
+        HostNode& h = s->nodes[i];
+        h.id = nt->id[i]; h.name = nt->name[i]; h.dc = nt->datacenter[i];
+        h.node_class = nt->node_class[i]; h.cclass = nt->computed_class[i];
+        auto it = cls_of.find(h.cclass);
+        if (it == cls_of.end()) {
+            it = cls_of.emplace(h.cclass, (uint32_t)s->class_rep.size()).first;
+            s->class_rep.push_back(i);
+        }
+        h.cls = it->second;
+        h_cls[i] = h.cls;
+        for (uint32_t k = nt->attr_off[i]; k < nt->attr_off[i + 1]; k++) h.attrs.emplace_back(nt->attr_key[k], nt->attr_val[k]);
+        for (uint32_t k = nt->meta_off[i]; k < nt->meta_off[i + 1]; k++) h.meta.emplace_back(nt->meta_key[k], nt->meta_val[k]);
+        std::sort(h.attrs.begin(), h.attrs.end());
+        std::sort(h.meta.begin(), h.meta.end());
+        for (uint32_t k = nt->drv_off[i]; k < nt->drv_off[i + 1]; k++) h.drivers.emplace_back(nt->drv_name[k], nt->drv_flags[k]);
+        std::sort(h.drivers.begin(), h.drivers.end());
+        h.n_device_nets = 0;
+        h.first_mbits = -1;
+        for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++) {
+            h.net_modes.push_back(nt->net_mode[k]);
+            if (!s->S(nt->net_device[k]).empty()) {
+                if (h.n_device_nets == 0) h.first_mbits = nt->net_mbits[k];
+                h.n_device_nets++;
+            }
+        }
+        for (uint32_t k = nt->alias_off[i]; k < nt->alias_off[i + 1]; k++) h.aliases.push_back(nt->alias_name[k]);
+        if (nt->hv_off)
+            for (uint32_t k = nt->hv_off[i]; k < nt->hv_off[i + 1]; k++) h.volumes.emplace_back(nt->hv_name[k], nt->hv_read_only[k]);
+        std::sort(h.volumes.begin(), h.volumes.end());
+        h.n_devices = nt->dev_off ? (int)(nt->dev_off[i + 1] - nt->dev_off[i]) : 0;
+        s->h_cap_cpu[i] = nt->cpu_shares[i] - nt->reserved_cpu[i];
+        s->h_cap_mem[i] = nt->memory_mb[i] - nt->reserved_memory_mb[i];
+        s->h_cap_disk[i] = nt->disk_mb[i] - nt->reserved_disk_mb[i];
+        h_avail[i] = h.first_mbits;
+        s->h_base_dyn[i] = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
+    }
+    s->ncls = (uint32_t)s->class_rep.size();
+    s->allocs.clear();
+    for (uint32_t i = 0; at && i < at->count; i++) {
+        const uint32_t row = at->node_row[i];
+        if (row >= n) return s->fail(PE_EINVAL, "alloc node_row out of range");
+        HostAlloc a{row, at->ns[i], at->job_id[i], at->task_group[i], at->terminal[i] != 0};
+        s->allocs.push_back(a);
+        if (a.terminal) continue;
+        s->h_base_cpu[row] += at->cpu_shares[i];
+        s->h_base_mem[row] += at->memory_mb[i];
+        s->h_base_disk[row] += at->disk_mb[i];
+        s->h_base_mbits[row] += at->net_mbits[i];
+        s->h_base_dyn[row] += at->dyn_ports[i];
+    }
+    HIP_TRY(s, upload(s->d_cls, h_cls));
+    HIP_TRY(s, upload(s->d_cap_cpu, s->h_cap_cpu));
+    HIP_TRY(s, upload(s->d_cap_mem, s->h_cap_mem));
+    HIP_TRY(s, upload(s->d_cap_disk, s->h_cap_disk));
+    HIP_TRY(s, upload(s->d_avail_mbits, h_avail));
+    HIP_TRY(s, upload(s->d_used_cpu, s->h_base_cpu));
+    HIP_TRY(s, upload(s->d_used_mem, s->h_base_mem));
+    HIP_TRY(s, upload(s->d_used_disk, s->h_base_disk));
+    HIP_TRY(s, upload(s->d_used_mbits, s->h_base_mbits));
+    HIP_TRY(s, upload(s->d_used_dyn, s->h_base_dyn));
+    std::vector<uint32_t> zeros(n, 0);
+    HIP_TRY(s, upload(s->d_coll_job, zeros));
+    return PE_OK;
+}
+
+pe::NodeSoA soa_of(pe_stack* s) {
+    pe::NodeSoA a;
+    a.n = (uint32_t)s->nodes.size();
+    a.cls = s->d_cls.as<uint32_t>();
+    a.cap_cpu = s->d_cap_cpu.as<int64_t>();
+    a.cap_mem = s->d_cap_mem.as<int64_t>();
+    a.cap_disk = s->d_cap_disk.as<int64_t>();
+    a.avail_mbits = s->d_avail_mbits.as<int32_t>();
+    a.used_cpu = s->d_used_cpu.as<int64_t>();
+    a.used_mem = s->d_used_mem.as<int64_t>();
+    a.used_disk = s->d_used_disk.as<int64_t>();
+    a.used_mbits = s->d_used_mbits.as<int32_t>();
+    a.used_dyn = s->d_used_dyn.as<int32_t>();
+    a.coll_job = s->d_coll_job.as<uint32_t>();
+    return a;
+}
+
+// Job-dependent per-node collision counts from the snapshot + the plan.
+int build_collisions(pe_stack* s) {
+    const size_t n = s->nodes.size();
+    std::vector<uint32_t> job(n, 0);
+    std::vector<std::vector<uint32_t>> tg(s->tgs.size(), std::vector<uint32_t>(n, 0));
+    auto add = [&](uint32_t row, uint32_t tgname) {
+        job[row]++;
+        for (size_t g = 0; g < s->tgs.size(); g++) if (s->tgs[g]->name == tgname) tg[g][row]++;
+    };
+    for (auto& a : s->allocs) if (!a.terminal && a.job == s->job_id) add(a.row, a.tg);
+    for (auto& p : s->plan) add(p.second, p.first);
+    HIP_TRY(s, upload(s->d_coll_job, job));
+    for (size_t g = 0; g < s->tgs.size(); g++) HIP_TRY(s, upload(s->tgs[g]->coll_tg, tg[g]));
+    return PE_OK;
+}
+
+// Spread property sets for a task group (spread.go:76-104, propertyset.go).
+int build_psets(pe_stack* s, TgPlan& g) {
+    g.psets.clear();
+    std::vector<const SpreadSpec*> specs;
+    for (auto& sp : s->job_spreads) specs.push_back(&sp);
+    for (auto& sp : g.spreads) specs.push_back(&sp);
+    if (specs.size() > (size_t)pe::kMaxPsets) { g.unsupported = "more than 4 spread stanzas"; return PE_OK; }
+    // computeSpreadInfo once per task group name; weights accumulate (spread.go:254)
+    if (!s->spread_info_done.count(g.name)) {
+        s->spread_info_done.insert(g.name);
+        for (auto& sp : g.spreads) s->sum_spread_weights += (int32_t)(int8_t)sp.weight;
+        for (auto& sp : s->job_spreads) s->sum_spread_weights += (int32_t)(int8_t)sp.weight;
+    }
+    // combined list for desired counts: tg spreads then job spreads, keyed by attribute
+    std::map<uint32_t, const SpreadSpec*> info;
+    for (auto& sp : g.spreads) info[sp.attribute] = &sp;
+    for (auto& sp : s->job_spreads) info[sp.attribute] = &sp;
+    const size_t n = s->nodes.size();
+    for (const SpreadSpec* sp : specs) {
+        auto ps = std::make_unique<PsetDev>();
+        ps->target = parse_target(s, s->S(sp->attribute));
+        ps->per_node = ps->target.escapes || ps->target.kind == T_ID || ps->target.kind == T_NAME;
+        auto value_of = [&](const HostNode& nd) -> uint32_t {
+            uint32_t vid;
+            Target t = resolve(s, ps->target, nd, &vid);
+            if (!t.found || t.nil) return pe::kMissing;
+            if (vid == PE_NONE) vid = s->lookup(t.value);   // literal attribute target
+            auto it = ps->value_index.find(vid);
+            if (it == ps->value_index.end()) {
+                it = ps->value_index.emplace(vid, (uint32_t)ps->value_str.size()).first;
+                ps->value_str.push_back(vid);
+            }
+            return it->second;
+        };
+        std::vector<uint32_t> by_class(s->ncls, pe::kMissing), by_node;
+        if (ps->per_node) {
+            by_node.resize(n);
+            for (size_t i = 0; i < n; i++) by_node[i] = value_of(s->nodes[i]);
+        } else {
+            for (uint32_t c = 0; c < s->ncls; c++) by_class[c] = value_of(s->nodes[s->class_rep[c]]);
+        }
+        // existing allocs of this job and task group (populateExisting) + plan allocs
+        auto node_val = [&](uint32_t row) {
+            return ps->per_node ? by_node[row] : by_class[s->nodes[row].cls];
+        };
+        ps->h_counts.assign(ps->value_str.size(), 0);
+        for (auto& a : s->allocs)
+            if (!a.terminal && a.ns == s->job_ns && a.job == s->job_id && a.tg == g.name) {
+                uint32_t v = node_val(a.row);
+                if (v != pe::kMissing) ps->h_counts[v]++;
+            }
+        for (auto& p : s->plan)
+            if (p.first == g.name) {
+                uint32_t v = node_val(p.second);
+                if (v != pe::kMissing) ps->h_counts[v]++;
+            }
+        if (ps->value_str.size() > (size_t)pe::kMaxValues) { g.unsupported = "spread attribute with > 256 values"; return PE_OK; }
+        const SpreadSpec* si = info[sp->attribute];
+        const double total = (double)g.count;
+        std::map<uint32_t, double> desired;
+        double sum = 0.0;
+        for (auto& t : si->targets) {
+            double d = ((double)t.second / (double)100) * total;
+            desired[t.first] = d;
+            sum += d;
+        }
+        bool has_star = false;
+        double star = 0;
+        const uint32_t star_id = s->lookup("*");
+        if (star_id != PE_NONE && desired.count(star_id)) { has_star = true; star = desired[star_id]; }
+        if (sum > 0 && sum < total) { has_star = true; star = total - sum; }   // implicitTarget
+        ps->even = si->targets.empty();
+        ps->h_desired.assign(ps->value_str.size(), std::nan(""));
+        for (size_t v = 0; v < ps->value_str.size(); v++) {
+            auto it = desired.find(ps->value_str[v]);
+            if (it != desired.end()) ps->h_desired[v] = it->second;
+            else if (has_star) ps->h_desired[v] = star;
+        }
+        ps->weight_frac = (double)(int8_t)si->weight / (double)s->sum_spread_weights;
+        HIP_TRY(s, upload(ps->val_class, by_class));
+        if (ps->per_node) HIP_TRY(s, upload(ps->val_node, by_node));
+        std::vector<uint32_t> cnt = ps->h_counts;
+        if (cnt.empty()) cnt.push_back(0);
+        HIP_TRY(s, upload(ps->counts, cnt));
+        std::vector<double> des = ps->h_desired;
+        if (des.empty()) des.push_back(0);
+        HIP_TRY(s, upload(ps->desired, des));
+        g.psets.push_back(std::move(ps));
+    }
+    g.psets_built = true;
+    return PE_OK;
+}
+
+// FeasibilityWrapper + EvalEligibility memo emulation for one task group over a
+// scan order (the visit order from the cursor). See SURVEY.md Appendix A3.
+int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start) {
+    pe::ConstraintEvaluator ev;
+    const size_t n = s->nodes.size();
+    auto& memo = s->tg_memo[g.name];
+    if (memo.size() != s->ncls) memo.assign(s->ncls, -1);
+    if (s->job_memo.size() != s->ncls) s->job_memo.assign(s->ncls, -1);
+    std::vector<uint8_t> class_ok(s->ncls, 0), node_ok;
+    const bool tg_escaped = g.escaped;
+    if (tg_escaped) {
+        // no memo for the task group: every node runs every check
+        node_ok.assign(n, 0);
+        for (uint32_t row = 0; row < n; row++)
+            node_ok[row] = job_feasible(s, ev, s->nodes[row]) && tg_feasible(s, ev, g, s->nodes[row]);
+        std::fill(class_ok.begin(), class_ok.end(), 1);
+    } else {
+        std::vector<uint8_t> job_ok_node;
+        if (s->job_escaped) {
+            job_ok_node.assign(n, 0);
+            for (uint32_t row = 0; row < n; row++) job_ok_node[row] = job_feasible(s, ev, s->nodes[row]);
+        }
+        const size_t m = order.size();
+        for (size_t k = 0; k < m; k++) {
+            const uint32_t row = order[(start + k) % m];
+            const uint32_t c = s->nodes[row].cls;
+            if (memo[c] != -1) continue;
+            bool jr;
+            if (s->job_escaped) jr = job_ok_node[row] != 0;
+            else {
+                if (s->job_memo[c] == -1) s->job_memo[c] = job_feasible(s, ev, s->nodes[row]) ? 1 : 0;
+                jr = s->job_memo[c] == 1;
+            }
+            if (!jr) continue;
+            memo[c] = tg_feasible(s, ev, g, s->nodes[row]) ? 1 : 0;
+        }
+        for (uint32_t c = 0; c < s->ncls; c++) {
+            bool ok = memo[c] == 1;
+            if (!s->job_escaped) {
+                if (s->job_memo[c] == -1) s->job_memo[c] = job_feasible(s, ev, s->nodes[s->class_rep[c]]) ? 1 : 0;
+                ok = ok && s->job_memo[c] == 1;
+            }
+            class_ok[c] = ok;
+        }
+        if (s->job_escaped) node_ok = job_ok_node;
+    }
+    HIP_TRY(s, upload(g.class_ok, class_ok));
+    g.node_ok_used = !node_ok.empty();
+    if (g.node_ok_used) HIP_TRY(s, upload(g.node_ok, node_ok));
+
+    // NodeAffinityIterator score per class (rank.go:698-725)
+    g.has_aff_table = !g.affinities.empty();
+    g.node_aff_used = false;
+    if (g.has_aff_table) {
+        bool escapes = false;
+        for (auto& a : g.affinities)
+            escapes = escapes || a.c.escapes || a.c.l.kind == T_ID || a.c.l.kind == T_NAME ||
+                      a.c.r.kind == T_ID || a.c.r.kind == T_NAME;
+        auto score = [&](const HostNode& nd) {
+            double sum_w = 0.0;
+            for (auto& a : g.affinities) sum_w += std::fabs((double)a.weight);
+            double total = 0.0;
+            for (auto& a : g.affinities) if (meets(s, ev, a.c, nd)) total += (double)a.weight;
+            const double norm = total / sum_w;
+            return total != 0.0 ? norm : 0.0;
+        };
+        if (escapes) {
+            std::vector<double> na(n);
+            for (size_t i = 0; i < n; i++) na[i] = score(s->nodes[i]);
+            HIP_TRY(s, upload(g.node_aff, na));
+            g.node_aff_used = true;
+        } else {
+            std::vector<double> ca(s->ncls);
+            for (uint32_t c = 0; c < s->ncls; c++) ca[c] = score(s->nodes[s->class_rep[c]]);
+            HIP_TRY(s, upload(g.class_aff, ca));
+        }
+    }
+    // AssignPorts needs an address of the ports' host network on the node
+    g.alias_used = false;
+    if (g.ask.tg_dyn > 0) {
+        std::vector<uint8_t> al(n, 0);
+        const uint32_t want = g.net_host;
+        for (size_t i = 0; i < n; i++) {
+            const auto& a = s->nodes[i].aliases;
+            al[i] = std::find(a.begin(), a.end(), want) != a.end();
+        }
+        HIP_TRY(s, upload(g.alias_ok, al));
+        g.alias_used = true;
+    }
+    g.tables_valid = true;
+    return PE_OK;
+}
+
+pe::TgTables tables_of(TgPlan& g) {
+    pe::TgTables t;
+    std::memset(&t, 0, sizeof(t));
+    t.class_ok = g.class_ok.as<uint8_t>();
+    t.node_ok = g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr;
+    t.class_aff = (g.has_aff_table && !g.node_aff_used) ? g.class_aff.as<double>() : nullptr;
+    t.node_aff = g.node_aff_used ? g.node_aff.as<double>() : nullptr;
+    t.alias_ok = g.alias_used ? g.alias_ok.as<uint8_t>() : nullptr;
+    t.coll_tg = g.coll_tg.as<uint32_t>();
+    t.n_psets = (int)g.psets.size();
+    for (int p = 0; p < t.n_psets; p++) {
+        PsetDev& ps = *g.psets[p];
+        t.pset_val_class[p] = ps.val_class.as<uint32_t>();
+        t.pset_val_node[p] = ps.per_node ? ps.val_node.as<uint32_t>() : nullptr;
+        t.pset_counts[p] = ps.counts.as<uint32_t>();
+        t.pset_desired[p] = ps.desired.as<double>();
+        t.pset_nvals[p] = (int)ps.value_str.size();
+        t.pset_even[p] = ps.even ? 1 : 0;
+        t.pset_weight_frac[p] = ps.weight_frac;
+    }
+    return t;
+}
+
+int prepare_tg(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& order, uint32_t start) {
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    if (!s->have_job) return s->fail(PE_ESTATE, "pe_set_job not called");
+    if (tgi >= s->tgs.size()) return s->fail(PE_EINVAL, "task group index out of range");
+    TgPlan& g = *s->tgs[tgi];
+    if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
+    if (!g.psets_built) {
+        int rc = build_psets(s, g);
+        if (rc) return rc;
+        if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
+    }
+    if (!g.tables_valid) {
+        int rc = build_tables(s, g, order, start);
+        if (rc) return rc;
+    }
+    return PE_OK;
+}
+
+pe::Ask ask_for(pe_stack* s, TgPlan& g) {
+    pe::Ask a = g.ask;
+    const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
+    if (!generic) { a.distinct_job = 0; a.distinct_tg = 0; a.desired_count = 0; }
+    a.algo_spread = s->cfg.algorithm == PE_ALGO_SPREAD;
+    a.anti_aff = generic ? 1 : 0;
+    return a;
+}
+
+void invalidate_tables(pe_stack* s) {
+    for (auto& g : s->tgs) g->tables_valid = false;
+}
+
+int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::vector<uint32_t>& order,
+              uint32_t offset, const pe_select_options* opts, pe_ranked_node* out, uint32_t* placed,
+              uint32_t* new_offset) {
+    TgPlan& g = *s->tgs[tgi];
+    if (order.empty()) {
+        for (uint32_t i = 0; i < count && i < 1; i++) {
+            std::memset(&out[i], 0, sizeof(out[i]));
+            out[i].row = -1;
+        }
+        *placed = 0;
+        *new_offset = 0;
+        return PE_OK;
+    }
+    HIP_TRY(s, upload(s->d_visit, order));
+    HIP_TRY(s, s->d_out.ensure(sizeof(pe_ranked_node) * std::max<uint32_t>(count, 1)));
+    HIP_TRY(s, s->d_status.ensure(16));
+    pe::SelectArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.soa = soa_of(s);
+    A.tg = tables_of(g);
+    A.ask = ask_for(s, g);
+    // job anti-affinity is always part of the GenericStack
+    A.perm = s->d_visit.as<uint32_t>();
+    A.n_visit = (uint32_t)order.size();
+    A.offset = offset;
+    A.limit = s->limit;
+    A.penalty_bits = nullptr;
+    if (opts && opts->penalty_count > 0) {
+        std::vector<uint32_t> bits((s->nodes.size() + 31) / 32, 0);
+        for (uint32_t i = 0; i < opts->penalty_count; i++) {
+            uint32_t r = opts->penalty_rows[i];
+            if (r < s->nodes.size()) bits[r >> 5] |= 1u << (r & 31);
+        }
+        HIP_TRY(s, upload(s->d_penalty, bits));
+        A.penalty_bits = s->d_penalty.as<uint32_t>();
+    }
+    A.log10 = s->log10;
+    A.count = count;
+    A.commit = commit;
+    A.out = s->d_out.as<pe_ranked_node>();
+    A.status = s->d_status.as<uint32_t>();
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, pe_launch_place(&A, s->stream));
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    uint32_t st[2];
+    HIP_TRY(s, hipMemcpyAsync(st, A.status, sizeof(st), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    const uint32_t got = std::min(count, st[0] + 1);   // placed + the failing Select
+    HIP_TRY(s, hipMemcpy(out, A.out, sizeof(pe_ranked_node) * got, hipMemcpyDeviceToHost));
+    *placed = st[0];
+    *new_offset = st[1];
+    if (commit)
+        for (uint32_t i = 0; i < st[0]; i++) s->plan.emplace_back(g.name, (uint32_t)out[i].row);
+    return PE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t pe_abi_version(void) { return PE_ABI_VERSION; }
+
+pe_stack* pe_stack_create(const pe_config* cfg) {
+    if (!cfg) { g_error = "null config"; return nullptr; }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) {
+        g_error = "no HIP device available: the placement engine runs only on the GPU";
+        return nullptr;
+    }
+    if (cfg->device < 0 || cfg->device >= ndev) { g_error = "device ordinal out of range"; return nullptr; }
+    auto* s = new pe_stack();
+    s->cfg = *cfg;
+    s->device = cfg->device;
+    if (hipSetDevice(s->device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) {
+        g_error = "HIP stream/event creation failed";
+        delete s;
+        return nullptr;
+    }
+    s->log10 = pe::gm::log_go(10.0);
+    return s;
+}
+
+void pe_stack_destroy(pe_stack* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    s->tgs.clear();
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+const char* pe_last_error(const pe_stack* s) { return s ? s->err.c_str() : g_error.c_str(); }
+
+double pe_last_kernel_ms(const pe_stack* s) { return s ? s->last_ms : 0.0; }
+
+int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
+    if (!s || !strs || !nodes) return PE_EINVAL;
+    HIP_TRY(s, hipSetDevice(s->device));
+    s->strs.clear();
+    s->sid.clear();
+    s->add_strings(strs);
+    s->have_state = false;
+    s->plan.clear();
+    s->tg_memo.clear();
+    s->job_memo.clear();
+    s->spread_info_done.clear();
+    s->sum_spread_weights = 0;
+    int rc = build_state(s, nodes, allocs);
+    if (rc) return rc;
+    s->have_state = true;
+    s->have_job = false;
+    s->have_job_version = false;
+    s->tgs.clear();
+    s->visit.clear();
+    s->offset = 0;
+    return PE_OK;
+}
+
+int pe_reset_plan(pe_stack* s) {
+    if (!s) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    HIP_TRY(s, hipSetDevice(s->device));
+    const size_t n = s->nodes.size();
+    HIP_TRY(s, hipMemcpyAsync(s->d_used_cpu.p, s->h_base_cpu.data(), n * 8, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(s->d_used_mem.p, s->h_base_mem.data(), n * 8, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(s->d_used_disk.p, s->h_base_disk.data(), n * 8, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(s->d_used_mbits.p, s->h_base_mbits.data(), n * 4, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(s->d_used_dyn.p, s->h_base_dyn.data(), n * 4, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    s->plan.clear();
+    s->tg_memo.clear();
+    s->job_memo.clear();
+    s->spread_info_done.clear();
+    s->sum_spread_weights = 0;
+    s->have_job = false;
+    s->have_job_version = false;
+    s->tgs.clear();
+    s->offset = 0;
+    return PE_OK;
+}
+
+int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
+    if (!s || !j) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    HIP_TRY(s, hipSetDevice(s->device));
+    s->add_strings(strs);
+    const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
+    if (generic && s->have_job_version && s->job_version == j->version) return PE_OK;   // stack.go:94-96
+    s->have_job_version = true;
+    s->job_version = j->version;
+    s->job_id = j->id;
+    s->job_ns = j->ns;
+    s->job_priority = j->priority;
+    s->job_constraints.clear();
+    s->job_escaped = false;
+    for (uint32_t i = 0; i < j->constraint_count; i++) {
+        s->job_constraints.push_back(parse_constraint(s, j->constraints[j->constraint_off + i]));
+        s->job_escaped = s->job_escaped || s->job_constraints.back().escapes;
+    }
+    bool job_distinct_hosts = false;
+    for (auto& c : s->job_constraints) {
+        if (c.op == "distinct_hosts") job_distinct_hosts = true;
+    }
+    s->job_affinities.clear();
+    for (uint32_t i = 0; i < j->affinity_count; i++)
+        s->job_affinities.push_back(ParsedAffinity{parse_constraint(s, *reinterpret_cast<const pe_constraint*>(&j->affinities[j->affinity_off + i])),
+                                                   j->affinities[j->affinity_off + i].weight});
+    auto conv_spreads = [&](uint32_t off, uint32_t cnt) {
+        std::vector<SpreadSpec> out;
+        for (uint32_t i = 0; i < cnt; i++) {
+            const pe_spread& sp = j->spreads[off + i];
+            SpreadSpec ss{sp.attribute, sp.weight, {}};
+            for (uint32_t k = 0; k < sp.target_count; k++)
+                ss.targets.emplace_back(j->spread_targets[sp.target_off + k].value, j->spread_targets[sp.target_off + k].percent);
+            out.push_back(ss);
+        }
+        return out;
+    };
+    s->job_spreads = conv_spreads(j->spread_off, j->spread_count);
+    std::string job_unsupported;
+    for (auto& c : s->job_constraints)
+        if (c.op == "distinct_property") job_unsupported = "distinct_property constraints";
+    s->tgs.clear();
+    for (uint32_t gi = 0; gi < j->tg_count; gi++) {
+        const pe_task_group& t = j->task_groups[gi];
+        auto g = std::make_unique<TgPlan>();
+        g->name = t.name;
+        g->count = t.count;
+        g->unsupported = job_unsupported;
+        tg_ask(j, t, &g->ask);
+        g->ask.distinct_job = job_distinct_hosts ? 1 : 0;
+        g->ask.distinct_tg = 0;
+        for (uint32_t k = 0; k < t.constraint_count; k++) {
+            g->constraints.push_back(parse_constraint(s, j->constraints[t.constraint_off + k]));
+            if (g->constraints.back().op == "distinct_hosts") g->ask.distinct_tg = 1;
+            if (g->constraints.back().op == "distinct_property") g->unsupported = "distinct_property constraints";
+        }
+        for (uint32_t k = 0; k < t.task_count; k++) {
+            const pe_task& x = j->tasks[t.task_off + k];
+            g->drivers.insert(x.driver);
+            for (uint32_t c = 0; c < x.constraint_count; c++) g->constraints.push_back(parse_constraint(s, j->constraints[x.constraint_off + c]));
+            if (x.device_count > 0) g->unsupported = "device requests";
+            if (x.cores > 0) g->unsupported = "reserved cores";
+            if (x.has_network && x.net_reserved_ports > 0) g->unsupported = "static port asks";
+        }
+        for (auto& c : g->constraints) g->escaped = g->escaped || c.escapes;
+        for (uint32_t k = 0; k < t.volume_count; k++)
+            g->volumes.emplace_back(j->volume_source[t.volume_off + k], j->volume_read_only[t.volume_off + k] != 0);
+        if (t.has_csi_volumes) g->unsupported = "CSI volumes";
+        g->has_network = t.has_network != 0;
+        g->net_mode = t.has_network ? t.net_mode : s->lookup("host");
+        g->net_host = t.net_host_network;
+        g->net_ports = t.net_dyn_ports + t.net_reserved_ports;
+        if (t.has_network && t.net_reserved_ports > 0) g->unsupported = "static port asks";
+        // affinities: job, task group, tasks (rank.go:671-686)
+        g->affinities = s->job_affinities;
+        for (uint32_t k = 0; k < t.affinity_count; k++)
+            g->affinities.push_back(ParsedAffinity{parse_constraint(s, *reinterpret_cast<const pe_constraint*>(&j->affinities[t.affinity_off + k])),
+                                                   j->affinities[t.affinity_off + k].weight});
+        for (uint32_t k = 0; k < t.task_count; k++) {
+            const pe_task& x = j->tasks[t.task_off + k];
+            for (uint32_t a = 0; a < x.affinity_count; a++)
+                g->affinities.push_back(ParsedAffinity{parse_constraint(s, *reinterpret_cast<const pe_constraint*>(&j->affinities[x.affinity_off + a])),
+                                                       j->affinities[x.affinity_off + a].weight});
+        }
+        g->spreads = conv_spreads(t.spread_off, t.spread_count);
+        if (!generic && (!g->spreads.empty() || !s->job_spreads.empty())) g->spreads.clear();
+        if (!generic) g->affinities.clear();
+        s->tgs.push_back(std::move(g));
+    }
+    if (!generic) s->job_spreads.clear();
+    // task networks must resolve against a single host device network on every node
+    for (auto& g : s->tgs) {
+        if (g->ask.has_task_net)
+            for (auto& nd : s->nodes)
+                if (nd.n_device_nets > 1) { g->unsupported = "task network asks on multi-device nodes"; break; }
+    }
+    s->have_job = true;
+    int rc = build_collisions(s);
+    if (rc) return rc;
+    return PE_OK;
+}
+
+int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
+    if (!s) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    s->visit.assign(rows, rows + n);
+    for (uint32_t r : s->visit) if (r >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range");
+    s->offset = 0;
+    uint32_t lim = 2;
+    if (s->cfg.stack_kind == PE_STACK_GENERIC && !s->cfg.batch && n > 0) {
+        uint32_t log_limit = (uint32_t)std::ceil(std::log2((double)n));
+        if (log_limit > lim) lim = log_limit;
+    }
+    s->limit = lim;
+    if (limit_out) *limit_out = lim;
+    invalidate_tables(s);
+    return PE_OK;
+}
+
+static bool tg_full_scan(pe_stack* s, TgPlan& g) {
+    return !g.affinities.empty() || !g.spreads.empty() || !s->job_spreads.empty();
+}
+
+int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
+    if (!s || !out) return PE_EINVAL;
+    HIP_TRY(s, hipSetDevice(s->device));
+    if (s->cfg.stack_kind != PE_STACK_GENERIC) {
+        // SystemStack.Select: single pass over the (single-node) list, no limit
+        int rc = prepare_tg(s, tgi, s->visit, 0);
+        if (rc) return rc;
+        uint32_t placed, no;
+        const uint32_t saved = s->limit;
+        s->limit = 1;
+        rc = run_place(s, tgi, 1, 0, s->visit, 0, nullptr, out, &placed, &no);
+        s->limit = saved;
+        return rc;
+    }
+    if (opts && opts->preferred_count > 0) {
+        // stack.go:121-132: select from the preferred nodes first, then the full
+        // list; SetNodes resets the cursor to 0 either way.
+        std::vector<uint32_t> pref(opts->preferred_rows, opts->preferred_rows + opts->preferred_count);
+        std::vector<uint32_t> scan = pref;
+        scan.insert(scan.end(), s->visit.begin(), s->visit.end());
+        invalidate_tables(s);
+        int rc = prepare_tg(s, tgi, scan, 0);
+        if (rc) return rc;
+        TgPlan& g = *s->tgs[tgi];
+        if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;
+        pe_select_options o2 = *opts;
+        o2.preferred_count = 0;
+        uint32_t placed, no;
+        rc = run_place(s, tgi, 1, 0, pref, 0, &o2, out, &placed, &no);
+        if (rc) return rc;
+        s->offset = 0;
+        invalidate_tables(s);
+        if (out->row >= 0) return PE_OK;
+        return pe_select(s, tgi, &o2, out);
+    }
+    int rc = prepare_tg(s, tgi, s->visit, s->offset);
+    if (rc) return rc;
+    TgPlan& g = *s->tgs[tgi];
+    if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;   // never reset until SetNodes (stack.go:165-167)
+    uint32_t placed, no;
+    rc = run_place(s, tgi, 1, 0, s->visit, s->offset, opts, out, &placed, &no);
+    if (rc) return rc;
+    s->offset = no;
+    return PE_OK;
+}
+
+int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
+    if (!s) return PE_EINVAL;
+    if (!s->have_job || tgi >= s->tgs.size() || row < 0 || (size_t)row >= s->nodes.size())
+        return s->fail(PE_EINVAL, "bad commit");
+    HIP_TRY(s, hipSetDevice(s->device));
+    TgPlan& g = *s->tgs[tgi];
+    if (!g.psets_built) {
+        int rc = build_psets(s, g);
+        if (rc) return rc;
+    }
+    pe::NodeSoA soa = soa_of(s);
+    pe::TgTables t = tables_of(g);
+    pe::Ask a = ask_for(s, g);
+    HIP_TRY(s, pe_launch_commit(&soa, &t, &a, (uint32_t)row, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    s->plan.emplace_back(g.name, (uint32_t)row);
+    // the coll_tg of other task groups with the same name also see this alloc
+    for (size_t k = 0; k < s->tgs.size(); k++)
+        if (k != tgi && s->tgs[k]->name == g.name) {
+            int rc = build_collisions(s);
+            if (rc) return rc;
+            break;
+        }
+    return PE_OK;
+}
+
+int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+    if (!s || (!out && count)) return PE_EINVAL;
+    if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place needs a generic stack");
+    HIP_TRY(s, hipSetDevice(s->device));
+    int rc = prepare_tg(s, tgi, s->visit, s->offset);
+    if (rc) return rc;
+    TgPlan& g = *s->tgs[tgi];
+    if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;
+    uint32_t p = 0, no = s->offset;
+    if (count) {
+        rc = run_place(s, tgi, count, 1, s->visit, s->offset, nullptr, out, &p, &no);
+        if (rc) return rc;
+    }
+    s->offset = no;
+    if (placed) *placed = p;
+    // multi-tg jobs sharing a name see these allocs in their collision counts
+    for (size_t k = 0; k < s->tgs.size(); k++)
+        if (k != tgi && s->tgs[k]->name == g.name) { rc = build_collisions(s); if (rc) return rc; break; }
+    return PE_OK;
+}
+
+int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
+    if (!s || !out_score || !out_status) return PE_EINVAL;
+    if (s->cfg.stack_kind != PE_STACK_SYSTEM) return s->fail(PE_ESTATE, "pe_system_place needs a system stack");
+    HIP_TRY(s, hipSetDevice(s->device));
+    {
+        // every node appears once: the single-node Selects are independent
+        std::vector<uint8_t> seen(s->nodes.size(), 0);
+        for (uint32_t r : s->visit) {
+            if (seen[r]) return s->fail(PE_EUNSUPPORTED, "duplicate rows in the system placement list");
+            seen[r] = 1;
+        }
+    }
+    int rc = prepare_tg(s, tgi, s->visit, 0);
+    if (rc) return rc;
+    TgPlan& g = *s->tgs[tgi];
+    const uint32_t n = (uint32_t)s->visit.size();
+    HIP_TRY(s, upload(s->d_visit, s->visit));
+    DevMem d_score, d_st;
+    HIP_TRY(s, d_score.ensure(sizeof(double) * std::max<uint32_t>(n, 1)));
+    HIP_TRY(s, d_st.ensure(std::max<uint32_t>(n, 1)));
+    HIP_TRY(s, s->d_status.ensure(16));
+    HIP_TRY(s, hipMemsetAsync(s->d_status.p, 0, 16, s->stream));
+    pe::SystemArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.soa = soa_of(s);
+    A.tg = tables_of(g);
+    A.ask = ask_for(s, g);
+    A.list = s->d_visit.as<uint32_t>();
+    A.n_list = n;
+    A.log10 = s->log10;
+    A.out_score = d_score.as<double>();
+    A.out_status = d_st.as<uint8_t>();
+    A.placed = s->d_status.as<uint32_t>();
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, pe_launch_system(&A, s->stream));
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    uint32_t p = 0;
+    HIP_TRY(s, hipMemcpyAsync(&p, A.placed, sizeof(p), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(out_score, A.out_score, sizeof(double) * n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(out_status, A.out_status, n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) s->plan.emplace_back(g.name, s->visit[i]);
+    if (placed) *placed = p;
+    return PE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// Shared host/device layout of the placement engine's HBM state and the
+// per-launch parameter block.
+#pragma once
+#include <stdint.h>
+#include "../../include/nomad_pe.h"
+
+namespace pe {
+
+constexpr int kMaxPsets = 4;          // spread property sets handled on device
+constexpr int kMaxValues = 256;       // distinct values per spread property on device
+constexpr uint32_t kMissing = 0xFFFFFFFFu;   // node has no value for the property
+constexpr int32_t kDynPortCapacity = 32000 - 20000 + 1;   // IndexesInRange is inclusive
+constexpr int kMaxSkip = 3;           // stack.go:17 maxSkip
+constexpr int kPlaceBlock = 256;      // threads of the persistent count-loop workgroup
+
+// Node SoA in HBM, row order of the State snapshot. Static columns are written
+// at pe_set_state; dynamic columns are the proposed state (existing allocs +
+// plan placements) and are updated by every commit.
+struct NodeSoA {
+    uint32_t n;
+    const uint32_t* cls;         // dense ComputedClass index
+    const int64_t* cap_cpu;      // NodeResources - ReservedResources (AllocsFit "available")
+    const int64_t* cap_mem;
+    const int64_t* cap_disk;
+    const int32_t* avail_mbits;  // bandwidth of the first host device network (-1: none)
+    int64_t* used_cpu;           // Σ proposed non-terminal allocs
+    int64_t* used_mem;
+    int64_t* used_disk;
+    int32_t* used_mbits;
+    int32_t* used_dyn;           // ports held in the dynamic range (incl. node-reserved)
+    uint32_t* coll_job;          // proposed allocs of the job per node
+};
+
+// Per (job, task group) feasibility / affinity / spread tables for a Select.
+struct TgTables {
+    const uint8_t* class_ok;     // [ncls] memoised job+tg feasibility per class
+    const uint8_t* node_ok;      // [n] or null: per-node verdict (escaped constraints)
+    const double* class_aff;     // [ncls] or null: normalised node-affinity score (0 = not appended)
+    const double* node_aff;      // [n] or null
+    const uint8_t* alias_ok;     // [n] or null: node has an address for the tg's port network
+    uint32_t* coll_tg;           // [n] proposed allocs of (job, tg) per node
+    int n_psets;
+    const uint32_t* pset_val_class[kMaxPsets];   // [ncls] value index or kMissing
+    const uint32_t* pset_val_node[kMaxPsets];    // [n] or null (escaped property)
+    uint32_t* pset_counts[kMaxPsets];            // [nvals] combined use (existing + proposed)
+    const double* pset_desired[kMaxPsets];       // [nvals] desired count, NaN = no target -> -1
+    int pset_nvals[kMaxPsets];
+    int pset_even[kMaxPsets];                    // no targets: evenSpreadScoreBoost
+    double pset_weight_frac[kMaxPsets];          // float64(weight) / float64(sumSpreadWeights)
+};
+
+struct Ask {
+    int64_t cpu, mem, disk;       // AllocatedResources.Comparable() of the task group
+    int32_t tg_dyn;               // tg network dynamic ports (AssignPorts)
+    int32_t has_task_net;         // task-level network asks present
+    int32_t task_mbits, task_dyn; // Σ over task networks
+    int32_t commit_mbits, commit_dyn;   // NetworkIndex contribution of the placed alloc
+    int32_t desired_count;        // tg.Count for job anti-affinity
+    int32_t distinct_job, distinct_tg;
+    int32_t algo_spread;
+    int32_t anti_aff;             // JobAntiAffinityIterator present (GenericStack only)
+};
+
+struct SelectArgs {
+    NodeSoA soa;
+    TgTables tg;
+    Ask ask;
+    const uint32_t* perm;         // visit order (SetNodes list after shuffle)
+    uint32_t n_visit;             // length of the visit list
+    uint32_t offset;              // StaticIterator cursor at entry
+    uint32_t limit;               // LimitIterator limit
+    const uint32_t* penalty_bits; // bitmask over rows or null
+    double log10;                 // go_log(10), computed on host
+    uint32_t count;               // placements to attempt
+    int commit;                   // apply Plan.AppendAlloc on device
+    pe_ranked_node* out;          // [count]
+    uint32_t* status;             // [0] placed, [1] final offset
+};
+
+struct SystemArgs {
+    NodeSoA soa;
+    TgTables tg;
+    Ask ask;
+    const uint32_t* list;         // SetNodes list (diff.place order)
+    uint32_t n_list;
+    double log10;
+    double* out_score;            // [n_list]
+    uint8_t* out_status;          // [n_list] 0 placed 1 filtered 2 exhausted
+    uint32_t* placed;             // [1] atomic counter
+};
+
+}  // namespace pe

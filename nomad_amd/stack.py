@@ -1,0 +1,249 @@
+"""Host-side mirror of the reference `scheduler.Stack` interface over a C ABI.
+
+`GenericStack` / `SystemStack` keep the reference's method names and argument
+meaning (scheduler/stack.go:23-39): SetNodes, SetJob, Select. `Place` is the
+fused count loop of GenericScheduler.computePlacements (generic_sched.go:493-649)
+and `SystemPlace` the SystemScheduler one (scheduler_system.go:283-425).
+
+The product backend is nomad_amd/libnomadpe.so (HIP, gfx950). There is no CPU
+fallback: constructing an engine stack without the library or without a GPU
+raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from .encode import EncodedJob, EncodedState, Interner
+from .structs import Allocation, Job, Node, SchedulerConfig
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ENGINE_LIB = os.path.join(_HERE, "libnomadpe.so")
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (code %d)" % (msg, code))
+        self.code = code
+
+
+class Unsupported(EngineError):
+    pass
+
+
+_engine = None
+
+
+def load_engine():
+    """Load the HIP engine library (fails loudly when it is missing)."""
+    global _engine
+    if _engine is None:
+        if not os.path.exists(ENGINE_LIB):
+            raise EngineError(-1, "nomad_amd/libnomadpe.so is not built: run __graft_entry__.build()")
+        lib = C.CDLL(ENGINE_LIB)
+        abi.bind(lib, "pe_", "pe_stack_create", "pe_stack_destroy", "pe_last_error")
+        lib.pe_abi_version.restype = C.c_uint32
+        lib.pe_last_kernel_ms.restype = C.c_double
+        lib.pe_last_kernel_ms.argtypes = [C.c_void_p]
+        _engine = lib
+    return _engine
+
+
+@dataclass
+class SelectOptions:
+    """SelectOptions (stack.go:34-39); nodes are given as node IDs or rows."""
+    penalty_node_ids: Sequence[str] = ()
+    preferred_nodes: Sequence[str] = ()
+    preempt: bool = False
+    alloc_name: str = ""
+
+
+@dataclass
+class RankedNode:
+    """RankedNode (rank.go:21-36) plus the AllocMetric counters."""
+    row: int
+    node: Optional[Node]
+    final_score: float
+    scores: List[float] = field(default_factory=list)
+    nodes_evaluated: int = 0
+    nodes_filtered: int = 0
+    nodes_exhausted: int = 0
+    new_offset: int = 0
+
+    @classmethod
+    def from_c(cls, r: abi.pe_ranked_node, nodes):
+        return cls(row=r.row, node=nodes[r.row] if r.row >= 0 else None, final_score=r.final_score,
+                   scores=[r.scores[i] for i in range(r.n_scores)], nodes_evaluated=r.nodes_evaluated,
+                   nodes_filtered=r.nodes_filtered, nodes_exhausted=r.nodes_exhausted,
+                   new_offset=r.new_offset)
+
+
+class _Stack:
+    """Stack over a C ABI with a given symbol prefix (engine: 'pe_')."""
+
+    stack_kind = abi.PE_STACK_GENERIC
+
+    def __init__(self, lib, prefix: str, batch: bool = False, config: SchedulerConfig = None,
+                 device: int = 0):
+        self._lib = lib
+        self._p = prefix
+        config = config or SchedulerConfig()
+        cfg = abi.pe_config()
+        cfg.stack_kind = self.stack_kind
+        cfg.batch = int(batch)
+        cfg.algorithm = abi.PE_ALGO_SPREAD if config.algorithm == "spread" else abi.PE_ALGO_BINPACK
+        cfg.memory_oversubscription = int(config.memory_oversubscription)
+        cfg.preempt = int(config.preempt_system) if self.stack_kind == abi.PE_STACK_SYSTEM else 0
+        cfg.device = device
+        self._cfg = cfg
+        create = getattr(lib, prefix + ("stack_create" if prefix == "pe_" else "create"))
+        self._h = create(C.byref(cfg))
+        if not self._h:
+            err = getattr(lib, prefix + "last_error")(None)
+            raise EngineError(-1, (err or b"stack creation failed").decode())
+        self.state: Optional[EncodedState] = None
+        self.job: Optional[EncodedJob] = None
+        self.nodes: List[Node] = []
+        self.limit = None
+
+    def close(self):
+        if self._h:
+            destroy = getattr(self._lib, self._p + ("stack_destroy" if self._p == "pe_" else "destroy"))
+            destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != abi.PE_OK:
+            msg = getattr(self._lib, self._p + "last_error")(self._h).decode()
+            raise (Unsupported if rc == abi.PE_EUNSUPPORTED else EngineError)(rc, msg)
+
+    def _fn(self, name):
+        return getattr(self._lib, self._p + name)
+
+    # -- scheduler.State snapshot -------------------------------------------
+    def SetState(self, nodes: Sequence[Node], allocs: Sequence[Allocation] = ()):
+        self.nodes = list(nodes)
+        self.state = EncodedState(nodes, allocs, Interner())
+        t = self.state.strtab()
+        self._check(self._fn("set_state")(self._h, C.byref(t), C.byref(self.state.node_table),
+                                          C.byref(self.state.alloc_table)))
+        return self.state
+
+    def ResetPlan(self):
+        """New evaluation on the resident snapshot (fresh EvalContext)."""
+        self._check(self._fn("reset_plan")(self._h))
+
+    def row(self, node_or_id) -> int:
+        nid = node_or_id if isinstance(node_or_id, str) else node_or_id.id
+        return self.state.row_of[nid]
+
+    # -- Stack interface -------------------------------------------------------
+    def SetJob(self, job: Job):
+        self.job = EncodedJob(job, self.state.interner)
+        self._job = job
+        t = self.job.strtab()
+        self._check(self._fn("set_job")(self._h, C.byref(t), C.byref(self.job.job)))
+
+    def SetNodes(self, nodes_in_visit_order) -> int:
+        """`nodes_in_visit_order`: Node objects / IDs / rows, already shuffled."""
+        rows = np.asarray([x if isinstance(x, (int, np.integer)) else self.row(x)
+                           for x in nodes_in_visit_order], dtype=np.uint32)
+        self._visit = rows
+        lim = C.c_uint32(0)
+        self._check(self._fn("set_nodes")(self._h, rows.ctypes.data_as(abi.u32p), len(rows), C.byref(lim)))
+        self.limit = lim.value
+        return self.limit
+
+    def _tg_index(self, tg):
+        if isinstance(tg, int):
+            return tg
+        for i, g in enumerate(self._job.task_groups):
+            if g is tg or g.name == tg:
+                return i
+        raise KeyError(tg)
+
+    def Select(self, tg, options: SelectOptions = None) -> Optional[RankedNode]:
+        opts = abi.pe_select_options()
+        keep = []
+        if options is not None:
+            if options.penalty_node_ids:
+                pen = np.asarray([self.row(x) for x in options.penalty_node_ids], dtype=np.uint32)
+                keep.append(pen)
+                opts.penalty_rows, opts.penalty_count = pen.ctypes.data_as(abi.u32p), len(pen)
+            if options.preferred_nodes:
+                pref = np.asarray([self.row(x) for x in options.preferred_nodes], dtype=np.uint32)
+                keep.append(pref)
+                opts.preferred_rows, opts.preferred_count = pref.ctypes.data_as(abi.u32p), len(pref)
+            opts.preempt = int(options.preempt)
+        out = abi.pe_ranked_node()
+        self._check(self._fn("select")(self._h, self._tg_index(tg), C.byref(opts), C.byref(out)))
+        r = RankedNode.from_c(out, self.nodes)
+        return r if r.row >= 0 else None
+
+    def SelectRaw(self, tg, options: SelectOptions = None) -> RankedNode:
+        """Select, but also returns the metrics when no node was found."""
+        out = abi.pe_ranked_node()
+        opts = abi.pe_select_options()
+        self._check(self._fn("select")(self._h, self._tg_index(tg), C.byref(opts), C.byref(out)))
+        return RankedNode.from_c(out, self.nodes)
+
+    def Commit(self, tg, node_or_row):
+        row = node_or_row if isinstance(node_or_row, (int, np.integer)) else self.row(node_or_row)
+        self._check(self._fn("commit")(self._h, self._tg_index(tg), int(row)))
+
+    def Place(self, tg, count: int) -> List[RankedNode]:
+        out = (abi.pe_ranked_node * max(1, count))()
+        placed = C.c_uint32(0)
+        self._check(self._fn("place")(self._h, self._tg_index(tg), count, out, C.byref(placed)))
+        n = min(count, placed.value + 1)
+        return [RankedNode.from_c(out[i], self.nodes) for i in range(n)]
+
+    def PlaceArrays(self, tg, count: int):
+        """Fused count loop returning (rows, final_scores, placed) as numpy arrays."""
+        out = (abi.pe_ranked_node * max(1, count))()
+        placed = C.c_uint32(0)
+        self._check(self._fn("place")(self._h, self._tg_index(tg), count, out, C.byref(placed)))
+        arr = np.ctypeslib.as_array(out)
+        return arr["row"].copy(), arr["final_score"].copy(), placed.value, arr
+
+    def SystemPlace(self, tg):
+        n = len(self._visit)
+        score = np.zeros(max(1, n), dtype=np.float64)
+        status = np.zeros(max(1, n), dtype=np.uint8)
+        placed = C.c_uint32(0)
+        self._check(self._fn("system_place")(self._h, self._tg_index(tg), score.ctypes.data_as(abi.f64p),
+                                             status.ctypes.data_as(abi.u8p), C.byref(placed)))
+        return score[:n], status[:n], placed.value
+
+
+class GenericStack(_Stack):
+    """NewGenericStack (stack.go:336-431) on the MI355X engine."""
+    stack_kind = abi.PE_STACK_GENERIC
+
+    def __init__(self, batch: bool = False, config: SchedulerConfig = None, device: int = 0):
+        super().__init__(load_engine(), "pe_", batch, config, device)
+
+    def last_kernel_ms(self) -> float:
+        return self._lib.pe_last_kernel_ms(self._h)
+
+
+class SystemStack(_Stack):
+    """NewSystemStack (stack.go:207-283) on the MI355X engine."""
+    stack_kind = abi.PE_STACK_SYSTEM
+
+    def __init__(self, sysbatch: bool = False, config: SchedulerConfig = None, device: int = 0):
+        super().__init__(load_engine(), "pe_", False, config, device)
+
+    def last_kernel_ms(self) -> float:
+        return self._lib.pe_last_kernel_ms(self._h)

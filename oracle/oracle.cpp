@@ -1,0 +1,1398 @@
+// ORACLE — test infrastructure only. Never linked or loaded by the product.
+//
+// C++ restatement of the reference placement stack with the reference's lazy
+// pull semantics, object for object:
+//   scheduler/stack.go        GenericStack / SystemStack (Select, SetNodes, SetJob)
+//   scheduler/feasible.go     StaticIterator, FeasibilityWrapper, checkers,
+//                             DistinctHosts / DistinctProperty iterators
+//   scheduler/rank.go         FeasibleRank, BinPack, JobAntiAffinity,
+//                             NodeReschedulingPenalty, NodeAffinity, ScoreNormalization
+//   scheduler/spread.go       SpreadIterator (+ evenSpreadScoreBoost)
+//   scheduler/propertyset.go  propertySet
+//   scheduler/select.go       LimitIterator, MaxScoreIterator
+//   scheduler/context.go      EvalContext.ProposedAllocs, EvalEligibility
+//   nomad/structs/funcs.go    AllocsFit, ScoreFitBinPack, ScoreFitSpread
+//   nomad/structs/network.go  NetworkIndex feasibility (ports counted, bandwidth)
+// Randomness (shuffleNodes, random port values) is an input / not modelled:
+// the caller passes the already-shuffled node order.
+// Out of the oracle's scope (returns PE_EUNSUPPORTED): preemption (evict),
+// device requests, reserved cores, CSI volumes, static reserved port asks.
+#include "oracle.h"
+#include "gomath.h"
+#include "semantics.h"
+
+#include <string>
+#include <vector>
+#include <map>
+#include <unordered_map>
+#include <set>
+#include <memory>
+#include <cmath>
+#include <climits>
+#include <stdexcept>
+#include <new>
+
+namespace {
+
+using orasem::Val;
+
+struct Unsupported : std::runtime_error {
+    explicit Unsupported(const std::string& m) : std::runtime_error(m) {}
+};
+
+static const int32_t kDynPortCapacity = 32000 - 20000 + 1;   // IndexesInRange is inclusive
+
+struct DriverInfo { bool detected, healthy, nil; };
+struct NetRes { std::string mode, device; int32_t mbits; };
+
+struct ONode {
+    int row;
+    std::string id, name, dc, node_class, computed_class;
+    int64_t cpu, mem, disk, rcpu, rmem, rdisk;
+    std::map<std::string, std::string> attrs, meta;
+    std::map<std::string, DriverInfo> drivers;
+    std::vector<NetRes> nets;
+    std::vector<std::string> aliases;
+    int32_t reserved_dyn;
+    std::map<std::string, bool> host_volumes;   // name -> read only
+    int n_devices;
+};
+
+struct OAlloc {
+    uint64_t id;
+    int node_row;
+    std::string ns, job_id, tg;
+    bool terminal;
+    int32_t priority;
+    int64_t cpu, mem, disk;
+    int32_t mbits, dyn_ports;
+};
+
+struct OTask {
+    std::string name, driver;
+    int64_t cpu, mem, mem_max;
+    int32_t cores;
+    uint32_t lifecycle;
+    bool has_network; int32_t net_mbits, net_dyn, net_reserved;
+    std::vector<const pe_constraint*> constraints;
+    std::vector<const pe_affinity*> affinities;
+    int n_devices;
+};
+
+struct OConstraint { std::string l, r, op; };
+struct OAffinity { std::string l, r, op; int32_t weight; };
+struct OSpreadTarget { std::string value; int32_t percent; };
+struct OSpread { std::string attribute; int8_t weight; std::vector<OSpreadTarget> targets; };
+
+struct OTaskGroup {
+    std::string name;
+    int32_t count;
+    int64_t disk;
+    std::vector<OConstraint> constraints;
+    std::vector<OAffinity> affinities;
+    std::vector<OSpread> spreads;
+    std::vector<OTask> tasks;
+    std::vector<std::vector<OConstraint>> task_constraints;
+    std::vector<std::vector<OAffinity>> task_affinities;
+    bool has_network; std::string net_mode, net_host_network;
+    int32_t net_dyn, net_reserved;
+    std::vector<std::pair<std::string, bool>> volumes;   // host volume requests (source, read only)
+    bool csi;
+};
+
+struct OJob {
+    std::string id, ns;
+    uint32_t type;
+    int32_t priority;
+    uint64_t version;
+    std::vector<OConstraint> constraints;
+    std::vector<OAffinity> affinities;
+    std::vector<OSpread> spreads;
+    std::vector<OTaskGroup> tgs;
+};
+
+// ---------------------------------------------------------------------------
+// AllocMetric (structs.go:9826-10026) — counters only
+struct Metrics {
+    uint32_t evaluated = 0, filtered = 0, exhausted = 0;
+    std::map<std::string, int> constraint_filtered, dimension_exhausted;
+    void EvaluateNode() { evaluated++; }
+    void FilterNode(const ONode*, const std::string& c) { filtered++; if (!c.empty()) constraint_filtered[c]++; }
+    void ExhaustedNode(const ONode*, const std::string& d) { exhausted++; if (!d.empty()) dimension_exhausted[d]++; }
+};
+
+enum ClassFeas { kUnknown = 0, kIneligible = 1, kEligible = 2, kEscaped = 3 };
+
+// EvalEligibility (context.go:190-345)
+struct Eligibility {
+    std::map<std::string, int> job;
+    bool job_escaped = false;
+    std::map<std::string, std::map<std::string, int>> tgs;
+    std::map<std::string, bool> tg_escaped;
+
+    static bool target_escapes(const std::string& t) {
+        return t.rfind("${node.unique.", 0) == 0 || t.rfind("${attr.unique.", 0) == 0 ||
+               t.rfind("${meta.unique.", 0) == 0;
+    }
+    static bool any_escaped(const std::vector<OConstraint>& cs) {
+        for (auto& c : cs) if (target_escapes(c.l) || target_escapes(c.r)) return true;
+        return false;
+    }
+    void SetJob(const OJob& j) {
+        job_escaped = any_escaped(j.constraints);
+        for (auto& tg : j.tgs) {
+            std::vector<OConstraint> cs = tg.constraints;
+            for (auto& tc : tg.task_constraints) cs.insert(cs.end(), tc.begin(), tc.end());
+            tg_escaped[tg.name] = any_escaped(cs);
+        }
+    }
+    int JobStatus(const std::string& cls) {
+        if (job_escaped) return kEscaped;
+        auto it = job.find(cls);
+        return it == job.end() ? kUnknown : it->second;
+    }
+    void SetJobEligibility(bool e, const std::string& cls) { job[cls] = e ? kEligible : kIneligible; }
+    int TaskGroupStatus(const std::string& tg, const std::string& cls) {
+        auto e = tg_escaped.find(tg);
+        if (e != tg_escaped.end() && e->second) return kEscaped;
+        auto it = tgs.find(tg);
+        if (it != tgs.end()) {
+            auto jt = it->second.find(cls);
+            if (jt != it->second.end()) return jt->second;
+        }
+        return kUnknown;
+    }
+    void SetTaskGroupEligibility(bool e, const std::string& tg, const std::string& cls) {
+        tgs[tg][cls] = e ? kEligible : kIneligible;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// State + Plan + EvalContext
+struct State {
+    std::vector<std::string> strs;
+    std::vector<ONode> nodes;
+    std::vector<OAlloc> allocs;
+    std::vector<std::vector<int>> allocs_by_node;   // indices into allocs
+};
+
+struct Plan {
+    std::map<int, std::vector<OAlloc>> node_allocation;   // NodeAllocation
+    std::map<int, std::vector<OAlloc>> node_update;       // NodeUpdate (stops)
+};
+
+struct EvalContext {
+    const State* state = nullptr;
+    Plan plan;
+    Metrics metrics;
+    Eligibility elig;
+    orasem::Caches caches;
+    uint64_t next_alloc_id = 1ull << 40;
+
+    void Reset() { metrics = Metrics(); }
+
+    // EvalContext.ProposedAllocs (context.go:120-157): non-terminal state allocs
+    // of the node, minus planned stops, plus planned placements (by ID).
+    std::vector<const OAlloc*> ProposedAllocs(int row) const {
+        std::map<uint64_t, const OAlloc*> ids;
+        std::set<uint64_t> removed;
+        auto up = plan.node_update.find(row);
+        if (up != plan.node_update.end()) for (auto& a : up->second) removed.insert(a.id);
+        for (int ai : state->allocs_by_node[row]) {
+            const OAlloc& a = state->allocs[ai];
+            if (a.terminal) continue;              // AllocsByNodeTerminal(ws, node, false)
+            if (removed.count(a.id)) continue;
+            ids[a.id] = &a;
+        }
+        auto pa = plan.node_allocation.find(row);
+        if (pa != plan.node_allocation.end()) for (auto& a : pa->second) ids[a.id] = &a;
+        std::vector<const OAlloc*> out;
+        for (auto& kv : ids) out.push_back(kv.second);
+        return out;
+    }
+};
+
+// resolveTarget (feasible.go:748-781)
+static Val resolve_target(const std::string& target, const ONode& n, bool* found) {
+    Val v; v.is_nil = false;
+    if (target.rfind("${", 0) != 0) { *found = true; v.s = target; return v; }
+    if (target == "${node.unique.id}") { *found = true; v.s = n.id; return v; }
+    if (target == "${node.datacenter}") { *found = true; v.s = n.dc; return v; }
+    if (target == "${node.unique.name}") { *found = true; v.s = n.name; return v; }
+    if (target == "${node.class}") { *found = true; v.s = n.node_class; return v; }
+    auto strip = [&](const std::string& pre) {
+        std::string s = target.substr(pre.size());
+        if (!s.empty() && s.back() == '}') s.pop_back();
+        return s;
+    };
+    if (target.rfind("${attr.", 0) == 0) {
+        auto it = n.attrs.find(strip("${attr."));
+        *found = it != n.attrs.end();
+        v.s = *found ? it->second : "";
+        return v;
+    }
+    if (target.rfind("${meta.", 0) == 0) {
+        auto it = n.meta.find(strip("${meta."));
+        *found = it != n.meta.end();
+        v.s = *found ? it->second : "";
+        return v;
+    }
+    *found = false; v.is_nil = true;
+    return v;
+}
+
+static bool meets_constraint(EvalContext& ctx, const OConstraint& c, const ONode& n) {
+    bool lf, rf;
+    Val l = resolve_target(c.l, n, &lf), r = resolve_target(c.r, n, &rf);
+    return orasem::check_constraint(ctx.caches, c.op, l, r, lf, rf);
+}
+
+// getProperty (propertyset.go:339-355)
+static bool get_property(const ONode* n, const std::string& prop, std::string* out) {
+    if (!n || prop.empty()) return false;
+    bool ok;
+    Val v = resolve_target(prop, *n, &ok);
+    if (!ok || v.is_nil) return false;
+    *out = v.s;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Feasibility checkers
+struct Checker { virtual ~Checker() {} virtual bool Feasible(const ONode& n) = 0; };
+
+struct ConstraintChecker : Checker {
+    EvalContext* ctx; std::vector<OConstraint> cs;
+    bool Feasible(const ONode& n) override {
+        for (auto& c : cs) {
+            if (!meets_constraint(*ctx, c, n)) {
+                ctx->metrics.FilterNode(&n, c.l + " " + c.op + " " + c.r);
+                return false;
+            }
+        }
+        return true;
+    }
+};
+
+// DriverChecker (feasible.go:433-500); drivers visited in sorted order (the
+// Go map order is random but the result is order independent).
+struct DriverChecker : Checker {
+    EvalContext* ctx; std::set<std::string> drivers;
+    bool has(const ONode& n) {
+        for (auto& d : drivers) {
+            auto it = n.drivers.find(d);
+            if (it != n.drivers.end()) {
+                if (it->second.nil) return false;
+                if (it->second.detected && it->second.healthy) continue;
+                return false;
+            }
+            auto at = n.attrs.find("driver." + d);
+            if (at == n.attrs.end()) return false;
+            // strconv.ParseBool
+            const std::string& v = at->second;
+            bool enabled;
+            if (v == "1" || v == "t" || v == "T" || v == "true" || v == "TRUE" || v == "True") enabled = true;
+            else if (v == "0" || v == "f" || v == "F" || v == "false" || v == "FALSE" || v == "False") enabled = false;
+            else return false;
+            if (!enabled) return false;
+        }
+        return true;
+    }
+    bool Feasible(const ONode& n) override {
+        if (has(n)) return true;
+        ctx->metrics.FilterNode(&n, "missing drivers");
+        return false;
+    }
+};
+
+// HostVolumeChecker (feasible.go:130-207)
+struct HostVolumeChecker : Checker {
+    EvalContext* ctx; std::map<std::string, std::vector<bool>> volumes;   // source -> read only flags
+    bool has(const ONode& n) {
+        if (volumes.empty()) return true;
+        if (volumes.size() > n.host_volumes.size()) return false;
+        for (auto& kv : volumes) {
+            auto it = n.host_volumes.find(kv.first);
+            if (it == n.host_volumes.end()) return false;
+            if (!it->second) continue;
+            for (bool ro : kv.second) if (!ro) return false;
+        }
+        return true;
+    }
+    bool Feasible(const ONode& n) override {
+        if (has(n)) return true;
+        ctx->metrics.FilterNode(&n, "missing compatible host volumes");
+        return false;
+    }
+};
+
+// DeviceChecker (feasible.go:1171-1274): device requests are outside the oracle.
+struct DeviceChecker : Checker {
+    bool requires = false;
+    bool Feasible(const ONode&) override {
+        if (requires) throw Unsupported("device requests");
+        return true;
+    }
+};
+
+// NetworkChecker (feasible.go:339-429)
+struct NetworkChecker : Checker {
+    EvalContext* ctx; std::string mode = "host"; std::vector<std::string> port_networks; bool has_ports = false;
+    bool has_network(const ONode& n) {
+        for (auto& nw : n.nets) {
+            std::string m = nw.mode.empty() ? "host" : nw.mode;
+            if (m == mode) return true;
+        }
+        return false;
+    }
+    bool Feasible(const ONode& n) override {
+        if (!has_network(n)) {
+            if (mode == "bridge") {
+                auto it = n.attrs.find("nomad.version");
+                if (it != n.attrs.end()) {
+                    orasem::Version v;
+                    if (orasem::new_version(it->second, true, &v)) {
+                        orasem::Version c; orasem::new_version("0.12", false, &c);
+                        if (orasem::prerelease_check(v, c) && orasem::version_compare(v, c) == -1) return true;
+                    }
+                }
+            }
+            ctx->metrics.FilterNode(&n, "missing network");
+            return false;
+        }
+        if (has_ports) {
+            for (auto& hn : port_networks) {
+                if (hn.empty()) continue;
+                bool ok; Val v = resolve_target(hn, n, &ok);
+                if (!ok) { ctx->metrics.FilterNode(&n, "invalid host network"); return false; }
+                bool found = false;
+                for (auto& a : n.aliases) if (a == v.s) { found = true; break; }
+                if (!found) { ctx->metrics.FilterNode(&n, "missing host network"); return false; }
+            }
+        }
+        return true;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Feasible iterators
+struct FeasibleIterator { virtual ~FeasibleIterator() {} virtual const ONode* Next() = 0; virtual void Reset() = 0; };
+
+// StaticIterator (feasible.go:74-117)
+struct StaticIterator : FeasibleIterator {
+    EvalContext* ctx; std::vector<const ONode*> nodes; int offset = 0, seen = 0;
+    const ONode* Next() override {
+        int n = (int)nodes.size();
+        if (offset == n || seen == n) {
+            if (seen != n) offset = 0;
+            else return nullptr;
+        }
+        int o = offset;
+        offset++; seen++;
+        ctx->metrics.EvaluateNode();
+        return nodes[o];
+    }
+    void Reset() override { seen = 0; }
+    void SetNodes(const std::vector<const ONode*>& ns) { nodes = ns; offset = 0; seen = 0; }
+};
+
+// FeasibilityWrapper (feasible.go:1026-1169); no availability checkers (CSI excluded).
+struct FeasibilityWrapper : FeasibleIterator {
+    EvalContext* ctx; FeasibleIterator* source;
+    std::vector<Checker*> job_checkers, tg_checkers;
+    std::string tg;
+    const ONode* Next() override {
+        Eligibility& e = ctx->elig;
+        for (;;) {
+        outer:
+            const ONode* option = source->Next();
+            if (!option) return nullptr;
+            bool job_escaped = false, job_unknown = false;
+            switch (e.JobStatus(option->computed_class)) {
+                case kIneligible: ctx->metrics.FilterNode(option, "computed class ineligible"); continue;
+                case kEscaped: job_escaped = true; break;
+                case kUnknown: job_unknown = true; break;
+            }
+            for (Checker* c : job_checkers) {
+                if (!c->Feasible(*option)) {
+                    if (!job_escaped) e.SetJobEligibility(false, option->computed_class);
+                    goto outer;
+                }
+            }
+            if (!job_escaped && job_unknown) e.SetJobEligibility(true, option->computed_class);
+            bool tg_escaped = false, tg_unknown = false;
+            switch (e.TaskGroupStatus(tg, option->computed_class)) {
+                case kIneligible: ctx->metrics.FilterNode(option, "computed class ineligible"); continue;
+                case kEligible: return option;    // available() is always true without CSI
+                case kEscaped: tg_escaped = true; break;
+                case kUnknown: tg_unknown = true; break;
+            }
+            for (Checker* c : tg_checkers) {
+                if (!c->Feasible(*option)) {
+                    if (!tg_escaped) e.SetTaskGroupEligibility(false, tg, option->computed_class);
+                    goto outer;
+                }
+            }
+            if (!tg_escaped && tg_unknown) e.SetTaskGroupEligibility(true, tg, option->computed_class);
+            return option;
+        }
+    }
+    void Reset() override { source->Reset(); }
+};
+
+// DistinctHostsIterator (feasible.go:502-599)
+struct DistinctHostsIterator : FeasibleIterator {
+    EvalContext* ctx; FeasibleIterator* source;
+    const OJob* job = nullptr; const OTaskGroup* tg = nullptr;
+    bool tg_dh = false, job_dh = false;
+    static bool has_dh(const std::vector<OConstraint>& cs) {
+        for (auto& c : cs) if (c.op == "distinct_hosts") return true;
+        return false;
+    }
+    void SetJob(const OJob* j) { job = j; job_dh = has_dh(j->constraints); }
+    void SetTaskGroup(const OTaskGroup* t) { tg = t; tg_dh = has_dh(t->constraints); }
+    bool satisfies(const ONode& n) {
+        if (!(job_dh || tg_dh)) return true;
+        for (const OAlloc* a : ctx->ProposedAllocs(n.row)) {
+            bool jc = a->job_id == job->id, tc = a->tg == tg->name;
+            if ((job_dh && jc) || (jc && tc)) return false;
+        }
+        return true;
+    }
+    const ONode* Next() override {
+        for (;;) {
+            const ONode* o = source->Next();
+            if (!o || !(job_dh || tg_dh)) return o;
+            if (!satisfies(*o)) { ctx->metrics.FilterNode(o, "distinct_hosts"); continue; }
+            return o;
+        }
+    }
+    void Reset() override { source->Reset(); }
+};
+
+// propertySet (propertyset.go:14-355)
+struct PropertySet {
+    EvalContext* ctx;
+    std::string job_id, ns, task_group, target;
+    uint64_t allowed = 0;
+    bool error = false; std::string error_msg;
+    std::map<std::string, uint64_t> existing, proposed, cleared;
+
+    bool keep(const OAlloc& a, bool filter_terminal) const {
+        if (filter_terminal && a.terminal) return false;
+        if (!task_group.empty() && a.tg != task_group) return false;
+        return true;
+    }
+    void populate_existing() {
+        // AllocsByJob(ws, ns, jobID, false): the job's allocs in the state store
+        for (const OAlloc& a : ctx->state->allocs) {
+            if (a.ns != ns || a.job_id != job_id) continue;
+            if (!keep(a, true)) continue;
+            std::string v;
+            if (get_property(&ctx->state->nodes[a.node_row], target, &v)) existing[v]++;
+        }
+    }
+    void PopulateProposed() {
+        proposed.clear(); cleared.clear();
+        for (auto& kv : ctx->plan.node_update)
+            for (auto& a : kv.second) {
+                if (!keep(a, false)) continue;
+                std::string v;
+                if (get_property(&ctx->state->nodes[a.node_row], target, &v)) cleared[v]++;
+            }
+        for (auto& kv : ctx->plan.node_allocation)
+            for (auto& a : kv.second) {
+                if (!keep(a, true)) continue;
+                std::string v;
+                if (get_property(&ctx->state->nodes[a.node_row], target, &v)) proposed[v]++;
+            }
+        for (auto& kv : proposed) {
+            auto it = cleared.find(kv.first);
+            if (it == cleared.end()) continue;
+            if (it->second == 0) cleared.erase(it);
+            else if (it->second > 1) it->second--;
+        }
+    }
+    void set_target(const std::string& attr, uint64_t allowed_count, const std::string& tg) {
+        if (!tg.empty()) task_group = tg;
+        target = attr;
+        allowed = allowed_count;
+        populate_existing();
+        PopulateProposed();
+    }
+    void SetConstraint(const OConstraint& c, const std::string& tg) {
+        uint64_t allowed_count = 1;
+        if (!c.r.empty()) {
+            // strconv.ParseUint(v, 10, 64)
+            bool ok = !c.r.empty();
+            unsigned __int128 v = 0;
+            for (char ch : c.r) {
+                if (ch < '0' || ch > '9') { ok = false; break; }
+                v = v * 10 + (ch - '0');
+                if (v > UINT64_MAX) { ok = false; break; }
+            }
+            if (!ok) { error = true; error_msg = "failed to convert RTarget"; return; }
+            allowed_count = (uint64_t)v;
+        }
+        set_target(c.l, allowed_count, tg);
+    }
+    std::map<std::string, uint64_t> CombinedUse() const {
+        std::map<std::string, uint64_t> use;
+        for (auto& kv : existing) use[kv.first] += kv.second;
+        for (auto& kv : proposed) use[kv.first] += kv.second;
+        for (auto& kv : cleared) {
+            auto it = use.find(kv.first);
+            if (it == use.end()) continue;
+            it->second = it->second >= kv.second ? it->second - kv.second : 0;
+        }
+        return use;
+    }
+    // UsedCount: returns false with an error message when unresolvable
+    bool UsedCount(const ONode& n, std::string* value, uint64_t* used, std::string* err) const {
+        if (error) { *err = error_msg; return false; }
+        if (!get_property(&n, target, value)) { *err = "missing property"; return false; }
+        auto use = CombinedUse();
+        auto it = use.find(*value);
+        *used = it == use.end() ? 0 : it->second;
+        return true;
+    }
+    bool SatisfiesDistinctProperties(const ONode& n, std::string* reason) const {
+        std::string v, err; uint64_t used = 0;
+        if (!UsedCount(n, &v, &used, &err)) { *reason = err; return false; }
+        if (used < allowed) return true;
+        *reason = "distinct_property: " + target + "=" + v;
+        return false;
+    }
+};
+
+// DistinctPropertyIterator (feasible.go:601-704)
+struct DistinctPropertyIterator : FeasibleIterator {
+    EvalContext* ctx; FeasibleIterator* source;
+    const OJob* job = nullptr; const OTaskGroup* tg = nullptr;
+    bool has = false;
+    std::vector<std::unique_ptr<PropertySet>> job_sets;
+    std::map<std::string, std::vector<std::unique_ptr<PropertySet>>> group_sets;
+    void SetJob(const OJob* j) {
+        job = j;
+        for (auto& c : j->constraints) {
+            if (c.op != "distinct_property") continue;
+            auto p = std::make_unique<PropertySet>();
+            p->ctx = ctx; p->job_id = j->id; p->ns = j->ns;
+            p->SetConstraint(c, "");
+            job_sets.push_back(std::move(p));
+        }
+    }
+    void SetTaskGroup(const OTaskGroup* t) {
+        tg = t;
+        if (!group_sets.count(t->name)) {
+            auto& v = group_sets[t->name];
+            for (auto& c : t->constraints) {
+                if (c.op != "distinct_property") continue;
+                auto p = std::make_unique<PropertySet>();
+                p->ctx = ctx; p->job_id = job->id; p->ns = job->ns;
+                p->SetConstraint(c, t->name);
+                v.push_back(std::move(p));
+            }
+        }
+        has = !job_sets.empty() || !group_sets[t->name].empty();
+    }
+    bool satisfies(const ONode& n, std::vector<std::unique_ptr<PropertySet>>& sets) {
+        for (auto& ps : sets) {
+            std::string reason;
+            if (!ps->SatisfiesDistinctProperties(n, &reason)) { ctx->metrics.FilterNode(&n, reason); return false; }
+        }
+        return true;
+    }
+    const ONode* Next() override {
+        for (;;) {
+            const ONode* o = source->Next();
+            if (!o || !has) return o;
+            if (!satisfies(*o, job_sets) || !satisfies(*o, group_sets[tg->name])) continue;
+            return o;
+        }
+    }
+    void Reset() override {
+        source->Reset();
+        for (auto& p : job_sets) p->PopulateProposed();
+        for (auto& kv : group_sets) for (auto& p : kv.second) p->PopulateProposed();
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Rank iterators
+struct RankedNode {
+    const ONode* node;
+    double final_score = 0;
+    std::vector<double> scores;
+};
+
+struct RankIterator { virtual ~RankIterator() {} virtual RankedNode* Next() = 0; virtual void Reset() = 0; };
+
+// FeasibleRankIterator (rank.go:77-107)
+struct FeasibleRankIterator : RankIterator {
+    FeasibleIterator* source;
+    std::vector<std::unique_ptr<RankedNode>> pool;
+    RankedNode* Next() override {
+        const ONode* o = source->Next();
+        if (!o) return nullptr;
+        pool.push_back(std::make_unique<RankedNode>());
+        pool.back()->node = o;
+        return pool.back().get();
+    }
+    void Reset() override { source->Reset(); pool.clear(); }
+};
+
+// The task group's resource ask: AllocatedResources.Comparable() (structs.go:3445-3487)
+struct Ask { int64_t cpu, mem, disk; };
+static Ask tg_ask(const OTaskGroup& tg, bool oversub) {
+    (void)oversub;
+    int64_t sc_cpu = 0, sc_mem = 0, eph_cpu = 0, eph_mem = 0, main_cpu = 0, main_mem = 0, ps_cpu = 0, ps_mem = 0;
+    for (auto& t : tg.tasks) {
+        switch (t.lifecycle) {
+            case PE_LC_MAIN: main_cpu += t.cpu; main_mem += t.mem; break;
+            case PE_LC_PRESTART: eph_cpu += t.cpu; eph_mem += t.mem; break;
+            case PE_LC_PRESTART_SIDECAR: sc_cpu += t.cpu; sc_mem += t.mem; break;
+            case PE_LC_POSTSTOP: ps_cpu += t.cpu; ps_mem += t.mem; break;
+            default: break;   // poststart hooks are not counted by Comparable()
+        }
+    }
+    eph_cpu = std::max(eph_cpu, main_cpu); eph_mem = std::max(eph_mem, main_mem);
+    eph_cpu = std::max(eph_cpu, ps_cpu); eph_mem = std::max(eph_mem, ps_mem);
+    return Ask{sc_cpu + eph_cpu, sc_mem + eph_mem, tg.disk};
+}
+
+// NetworkIndex contribution of an alloc of this task group (network.go:144-193):
+// allocs with task-group ports only count their ports; otherwise task networks.
+static void tg_net_contrib(const OTaskGroup& tg, int32_t* mbits, int32_t* dyn) {
+    *mbits = 0; *dyn = 0;
+    if (tg.has_network && tg.net_dyn + tg.net_reserved > 0) { *dyn = tg.net_dyn; return; }
+    for (auto& t : tg.tasks) if (t.has_network) { *mbits += t.net_mbits; *dyn += t.net_dyn; }
+}
+
+// BinPackIterator (rank.go:149-531), evict = false path.
+struct BinPackIterator : RankIterator {
+    EvalContext* ctx; RankIterator* source;
+    bool evict = false; int32_t priority = 0; std::string job_id;
+    const OTaskGroup* tg = nullptr;
+    bool spread_algo = false, oversub = false;
+
+    static double score_fit(bool spread, const ONode& n, int64_t ucpu, int64_t umem) {
+        double node_cpu = (double)n.cpu, node_mem = (double)n.mem;
+        node_cpu -= (double)n.rcpu; node_mem -= (double)n.rmem;
+        double fc = 1 - ((double)ucpu / node_cpu);
+        double fm = 1 - ((double)umem / node_mem);
+        double total = gomath::pow(10, fc) + gomath::pow(10, fm);
+        double s = spread ? total - 2 : 20.0 - total;
+        if (s > 18.0) s = 18.0; else if (s < 0) s = 0;
+        return s;
+    }
+
+    RankedNode* Next() override {
+        for (;;) {
+            RankedNode* option = source->Next();
+            if (!option) return nullptr;
+            const ONode& n = *option->node;
+            auto proposed = ctx->ProposedAllocs(n.row);
+            // NetworkIndex: SetNode + AddAllocs
+            int32_t used_dyn = n.reserved_dyn, used_mbits = 0;
+            for (const OAlloc* a : proposed) { if (a->terminal) continue; used_dyn += a->dyn_ports; used_mbits += a->mbits; }
+            if (tg->has_network) {
+                if (tg->net_reserved > 0) throw Unsupported("static port asks");
+                // AssignPorts: each dynamic port needs an address of its host network
+                // and one free port in [MinDynamicPort, MaxDynamicPort].
+                if (tg->net_dyn > 0) {
+                    bool has_addr = false;
+                    for (auto& a : n.aliases) if (a == tg->net_host_network) { has_addr = true; break; }
+                    if (!has_addr || kDynPortCapacity - used_dyn < 1) {
+                        if (evict) throw Unsupported("preemption");   // PreemptForNetwork path
+                        ctx->metrics.ExhaustedNode(&n, !has_addr ? "network: no addresses available"
+                                                                 : "network: dynamic port selection failed");
+                        continue;
+                    }
+                    used_dyn += tg->net_dyn;   // AddReservedPorts(offer)
+                }
+            }
+            bool skip = false;
+            for (auto& t : tg->tasks) {
+                if (t.has_network) {
+                    // AssignNetwork over the node's AvailNetworks (device != "")
+                    bool ok = false; std::string err = "no networks available";
+                    for (auto& nw : n.nets) {
+                        if (nw.device.empty()) continue;
+                        if (used_mbits + t.net_mbits > nw.mbits) { err = "bandwidth exceeded"; continue; }
+                        if (t.net_reserved > 0) throw Unsupported("static port asks");
+                        if (kDynPortCapacity - used_dyn < t.net_dyn) { err = "dynamic port selection failed"; continue; }
+                        ok = true; break;
+                    }
+                    if (!ok) {
+                        if (evict) throw Unsupported("preemption");   // PreemptForNetwork path
+                        ctx->metrics.ExhaustedNode(&n, "network: " + err); skip = true; break;
+                    }
+                    used_mbits += t.net_mbits; used_dyn += t.net_dyn;   // AddReserved(offer)
+                }
+                if (t.n_devices > 0) throw Unsupported("device requests");
+                if (t.cores > 0) throw Unsupported("reserved cores");
+            }
+            if (skip) continue;
+            Ask ask = tg_ask(*tg, oversub);
+            // AllocsFit(node, proposed + ask): used over non-terminal allocs
+            int64_t ucpu = ask.cpu, umem = ask.mem, udisk = ask.disk;
+            for (const OAlloc* a : proposed) { if (a->terminal) continue; ucpu += a->cpu; umem += a->mem; udisk += a->disk; }
+            int64_t acpu = n.cpu - n.rcpu, amem = n.mem - n.rmem, adisk = n.disk - n.rdisk;
+            const char* dim = nullptr;
+            if (acpu < ucpu) dim = "cpu";
+            else if (amem < umem) dim = "memory";
+            else if (adisk < udisk) dim = "disk";
+            if (dim) {
+                if (evict) throw Unsupported("preemption");   // PreemptForTaskGroup path
+                ctx->metrics.ExhaustedNode(&n, dim);
+                continue;
+            }
+            double fitness = score_fit(spread_algo, n, ucpu, umem);
+            option->scores.push_back(fitness / 18.0);
+            return option;
+        }
+    }
+    void Reset() override { source->Reset(); }
+};
+
+// JobAntiAffinityIterator (rank.go:533-601)
+struct JobAntiAffinityIterator : RankIterator {
+    EvalContext* ctx; RankIterator* source;
+    std::string job_id, tg; int desired = 0;
+    RankedNode* Next() override {
+        RankedNode* o = source->Next();
+        if (!o) return nullptr;
+        int coll = 0;
+        for (const OAlloc* a : ctx->ProposedAllocs(o->node->row))
+            if (a->job_id == job_id && a->tg == tg) coll++;
+        if (coll > 0) o->scores.push_back(-1 * (double)(coll + 1) / (double)desired);
+        return o;
+    }
+    void Reset() override { source->Reset(); }
+};
+
+// NodeReschedulingPenaltyIterator (rank.go:603-646)
+struct NodeReschedulingPenaltyIterator : RankIterator {
+    RankIterator* source; std::set<int> penalty;
+    RankedNode* Next() override {
+        RankedNode* o = source->Next();
+        if (!o) return nullptr;
+        if (penalty.count(o->node->row)) o->scores.push_back(-1);
+        return o;
+    }
+    void Reset() override { penalty.clear(); source->Reset(); }
+};
+
+// NodeAffinityIterator (rank.go:648-735)
+struct NodeAffinityIterator : RankIterator {
+    EvalContext* ctx; RankIterator* source;
+    std::vector<OAffinity> job_affs, affs;
+    void SetJob(const OJob* j) { job_affs = j->affinities; }
+    void SetTaskGroup(const OTaskGroup* t) {
+        affs.insert(affs.end(), job_affs.begin(), job_affs.end());
+        affs.insert(affs.end(), t->affinities.begin(), t->affinities.end());
+        for (auto& ta : t->task_affinities) affs.insert(affs.end(), ta.begin(), ta.end());
+    }
+    bool has() const { return !affs.empty(); }
+    RankedNode* Next() override {
+        RankedNode* o = source->Next();
+        if (!o) return nullptr;
+        if (!has()) return o;
+        double sum_w = 0.0;
+        for (auto& a : affs) sum_w += std::fabs((double)a.weight);
+        double total = 0.0;
+        for (auto& a : affs) {
+            bool lf, rf;
+            Val l = resolve_target(a.l, *o->node, &lf), r = resolve_target(a.r, *o->node, &rf);
+            if (orasem::check_constraint(ctx->caches, a.op, l, r, lf, rf)) total += (double)a.weight;
+        }
+        double norm = total / sum_w;
+        if (total != 0.0) o->scores.push_back(norm);
+        return o;
+    }
+    void Reset() override { source->Reset(); affs.clear(); }
+};
+
+// SpreadIterator (spread.go:13-257)
+struct SpreadInfo { int8_t weight; std::map<std::string, double> desired; };
+struct SpreadIterator : RankIterator {
+    EvalContext* ctx; RankIterator* source;
+    const OJob* job = nullptr; const OTaskGroup* tg = nullptr;
+    std::vector<OSpread> job_spreads;
+    std::map<std::string, std::map<std::string, SpreadInfo>> tg_spread_info;
+    int32_t sum_spread_weights = 0;
+    bool has_spread = false;
+    std::map<std::string, std::vector<std::unique_ptr<PropertySet>>> group_sets;
+
+    void SetJob(const OJob* j) { job = j; if (!j->spreads.empty()) job_spreads = j->spreads; }
+    void compute_spread_info(const OTaskGroup* t) {
+        std::map<std::string, SpreadInfo> infos;
+        double total = (double)t->count;
+        std::vector<OSpread> combined = t->spreads;
+        combined.insert(combined.end(), job_spreads.begin(), job_spreads.end());
+        for (auto& sp : combined) {
+            SpreadInfo si; si.weight = sp.weight;
+            double sum = 0.0;
+            for (auto& st : sp.targets) {
+                double d = ((double)st.percent / (double)100) * total;
+                si.desired[st.value] = d;
+                sum += d;
+            }
+            if (sum > 0 && sum < total) si.desired["*"] = total - sum;
+            infos[sp.attribute] = si;
+            sum_spread_weights += (int32_t)sp.weight;
+        }
+        tg_spread_info[t->name] = infos;
+    }
+    void SetTaskGroup(const OTaskGroup* t) {
+        tg = t;
+        if (!group_sets.count(t->name)) {
+            auto& v = group_sets[t->name];
+            for (auto& sp : job_spreads) {
+                auto p = std::make_unique<PropertySet>();
+                p->ctx = ctx; p->job_id = job->id; p->ns = job->ns;
+                p->set_target(sp.attribute, 0, t->name);
+                v.push_back(std::move(p));
+            }
+            for (auto& sp : t->spreads) {
+                auto p = std::make_unique<PropertySet>();
+                p->ctx = ctx; p->job_id = job->id; p->ns = job->ns;
+                p->set_target(sp.attribute, 0, t->name);
+                v.push_back(std::move(p));
+            }
+        }
+        has_spread = !group_sets[t->name].empty();
+        if (!tg_spread_info.count(t->name)) compute_spread_info(t);
+    }
+    static double even_boost(const PropertySet& ps, const ONode& n) {
+        auto use = ps.CombinedUse();
+        if (use.empty()) return 0.0;
+        std::string v;
+        if (!get_property(&n, ps.target, &v)) return -1.0;
+        uint64_t cur = use.count(v) ? use[v] : 0;
+        uint64_t mn = 0, mx = 0;
+        for (auto& kv : use) {
+            if (mn == 0 || kv.second < mn) mn = kv.second;
+            if (mx == 0 || kv.second > mx) mx = kv.second;
+        }
+        double delta_boost;
+        if (mn == 0) delta_boost = -1.0;
+        else { int64_t d = (int64_t)(mn - cur); delta_boost = (double)d / (double)mn; }
+        if (cur != mn) return delta_boost;
+        if (mn == mx) return -1.0;
+        if (mn == 0) return 1.0;
+        int64_t d = (int64_t)(mx - mn);
+        return (double)d / (double)mn;
+    }
+    RankedNode* Next() override {
+        for (;;) {
+            RankedNode* o = source->Next();
+            if (!o || !has_spread) return o;
+            double total = 0.0;
+            auto& infos = tg_spread_info[tg->name];
+            for (auto& ps : group_sets[tg->name]) {
+                std::string v, err; uint64_t used = 0;
+                bool ok = ps->UsedCount(*o->node, &v, &used, &err);
+                used += 1;
+                if (!ok) { total -= 1.0; continue; }
+                auto it = infos.find(ps->target);
+                SpreadInfo empty{0, {}};
+                const SpreadInfo& sd = it == infos.end() ? empty : it->second;
+                if (sd.desired.empty()) { total += even_boost(*ps, *o->node); continue; }
+                auto dit = sd.desired.find(v);
+                double desired;
+                if (dit == sd.desired.end()) {
+                    auto star = sd.desired.find("*");
+                    if (star == sd.desired.end()) { total -= 1.0; continue; }
+                    desired = star->second;
+                } else desired = dit->second;
+                double w = (double)sd.weight / (double)sum_spread_weights;
+                double boost = ((desired - (double)used) / desired) * w;
+                total += boost;
+            }
+            if (total != 0.0) o->scores.push_back(total);
+            return o;
+        }
+    }
+    void Reset() override {
+        source->Reset();
+        for (auto& kv : group_sets) for (auto& p : kv.second) p->PopulateProposed();
+    }
+};
+
+// ScoreNormalizationIterator (rank.go:737-771)
+struct ScoreNormalizationIterator : RankIterator {
+    RankIterator* source;
+    RankedNode* Next() override {
+        RankedNode* o = source->Next();
+        if (!o || o->scores.empty()) return o;
+        double sum = 0.0;
+        for (double s : o->scores) sum += s;
+        o->final_score = sum / (double)o->scores.size();
+        return o;
+    }
+    void Reset() override { source->Reset(); }
+};
+
+// LimitIterator (select.go:5-74)
+struct LimitIterator : RankIterator {
+    RankIterator* source; int limit; int max_skip; double threshold;
+    int seen = 0; std::vector<RankedNode*> skipped; size_t skipped_index = 0;
+    RankedNode* next_option() {
+        RankedNode* s = source->Next();
+        if (!s && skipped_index < skipped.size()) return skipped[skipped_index++];
+        return s;
+    }
+    RankedNode* Next() override {
+        if (seen == limit) return nullptr;
+        RankedNode* o = next_option();
+        if (!o) return nullptr;
+        if ((int)skipped.size() < max_skip) {
+            while (o && o->final_score <= threshold && (int)skipped.size() < max_skip) {
+                skipped.push_back(o);
+                o = source->Next();
+            }
+        }
+        seen++;
+        if (!o) return next_option();
+        return o;
+    }
+    void Reset() override { source->Reset(); seen = 0; skipped.clear(); skipped_index = 0; }
+};
+
+// MaxScoreIterator (select.go:76-116)
+struct MaxScoreIterator : RankIterator {
+    RankIterator* source; RankedNode* max = nullptr;
+    RankedNode* Next() override {
+        if (max) return nullptr;
+        for (;;) {
+            RankedNode* o = source->Next();
+            if (!o) return max;
+            if (!max || o->final_score > max->final_score) max = o;
+        }
+    }
+    void Reset() override { source->Reset(); max = nullptr; }
+};
+
+// StaticRankIterator (rank.go:109-147), for the LimitIterator KAT helper
+struct StaticRankIterator : RankIterator {
+    std::vector<RankedNode*> nodes; int offset = 0, seen = 0, pulled = 0;
+    RankedNode* Next() override {
+        int n = (int)nodes.size();
+        if (offset == n || seen == n) {
+            if (seen != n) offset = 0;
+            else return nullptr;
+        }
+        int o = offset; offset++; seen++; pulled++;
+        return nodes[o];
+    }
+    void Reset() override { seen = 0; }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// The stack handle
+struct oracle_stack {
+    pe_config cfg;
+    std::string err;
+    State state;
+    EvalContext ctx;
+    OJob job; bool have_job = false;
+    std::vector<const ONode*> base_nodes;
+
+    // chain
+    StaticIterator source;
+    ConstraintChecker job_constraint, tg_constraint;
+    DriverChecker tg_drivers;
+    HostVolumeChecker tg_volumes;
+    DeviceChecker tg_devices;
+    NetworkChecker tg_network;
+    FeasibilityWrapper wrapped;
+    DistinctHostsIterator distinct_hosts;
+    DistinctPropertyIterator distinct_property;
+    FeasibleRankIterator rank_source;
+    BinPackIterator bin_pack;
+    JobAntiAffinityIterator job_anti_aff;
+    NodeReschedulingPenaltyIterator penalty;
+    NodeAffinityIterator node_affinity;
+    SpreadIterator spread;
+    ScoreNormalizationIterator score_norm;
+    LimitIterator limit;
+    MaxScoreIterator max_score;
+    bool have_job_version = false; uint64_t job_version = 0;
+
+    explicit oracle_stack(const pe_config& c) : cfg(c) {
+        ctx.state = &state;
+        source.ctx = &ctx;
+        job_constraint.ctx = &ctx; tg_constraint.ctx = &ctx;
+        tg_drivers.ctx = &ctx; tg_volumes.ctx = &ctx; tg_network.ctx = &ctx;
+        wrapped.ctx = &ctx; wrapped.source = &source;
+        wrapped.job_checkers = {&job_constraint};
+        wrapped.tg_checkers = {&tg_drivers, &tg_constraint, &tg_volumes, &tg_devices, &tg_network};
+        bool generic = c.stack_kind == PE_STACK_GENERIC;
+        distinct_hosts.ctx = &ctx; distinct_hosts.source = &wrapped;
+        distinct_property.ctx = &ctx;
+        distinct_property.source = generic ? (FeasibleIterator*)&distinct_hosts : (FeasibleIterator*)&wrapped;
+        rank_source.source = &distinct_property;   // quota iterator is a no-op in OSS
+        bin_pack.ctx = &ctx; bin_pack.source = &rank_source;
+        bin_pack.evict = !generic && c.preempt;
+        bin_pack.spread_algo = c.algorithm == PE_ALGO_SPREAD;
+        bin_pack.oversub = c.memory_oversubscription != 0;
+        job_anti_aff.ctx = &ctx; job_anti_aff.source = &bin_pack;
+        penalty.source = &job_anti_aff;
+        node_affinity.ctx = &ctx; node_affinity.source = &penalty;
+        spread.ctx = &ctx; spread.source = &node_affinity;
+        score_norm.source = generic ? (RankIterator*)&spread : (RankIterator*)&bin_pack;
+        limit.source = &score_norm; limit.limit = 2; limit.max_skip = 3; limit.threshold = 0.0;
+        max_score.source = &limit;
+    }
+    const OTaskGroup& tg(uint32_t i) const { return job.tgs.at(i); }
+};
+
+static std::string S(const State& st, uint32_t id) {
+    if (id == PE_NONE || id >= st.strs.size()) return std::string();
+    return st.strs[id];
+}
+
+extern "C" {
+
+oracle_stack* oracle_create(const pe_config* cfg) {
+    if (!cfg) return nullptr;
+    return new oracle_stack(*cfg);
+}
+void oracle_destroy(oracle_stack* s) { delete s; }
+const char* oracle_last_error(const oracle_stack* s) { return s ? s->err.c_str() : "null handle"; }
+
+int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table* nt,
+                     const pe_alloc_table* at) {
+    State& st = s->state;
+    st = State();
+    for (uint32_t i = 0; i < strs->count; i++)
+        st.strs.emplace_back(strs->bytes + strs->offsets[i], strs->offsets[i + 1] - strs->offsets[i]);
+    st.nodes.resize(nt->n);
+    for (uint32_t i = 0; i < nt->n; i++) {
+        ONode& n = st.nodes[i];
+        n.row = (int)i;
+        n.id = S(st, nt->id[i]); n.name = S(st, nt->name[i]); n.dc = S(st, nt->datacenter[i]);
+        n.node_class = S(st, nt->node_class[i]); n.computed_class = S(st, nt->computed_class[i]);
+        n.cpu = nt->cpu_shares[i]; n.mem = nt->memory_mb[i]; n.disk = nt->disk_mb[i];
+        n.rcpu = nt->reserved_cpu[i]; n.rmem = nt->reserved_memory_mb[i]; n.rdisk = nt->reserved_disk_mb[i];
+        for (uint32_t k = nt->attr_off[i]; k < nt->attr_off[i + 1]; k++) n.attrs[S(st, nt->attr_key[k])] = S(st, nt->attr_val[k]);
+        for (uint32_t k = nt->meta_off[i]; k < nt->meta_off[i + 1]; k++) n.meta[S(st, nt->meta_key[k])] = S(st, nt->meta_val[k]);
+        for (uint32_t k = nt->drv_off[i]; k < nt->drv_off[i + 1]; k++) {
+            uint8_t f = nt->drv_flags[k];
+            n.drivers[S(st, nt->drv_name[k])] = DriverInfo{(f & 1) != 0, (f & 2) != 0, (f & 4) != 0};
+        }
+        for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++)
+            n.nets.push_back(NetRes{S(st, nt->net_mode[k]), S(st, nt->net_device[k]), nt->net_mbits[k]});
+        for (uint32_t k = nt->alias_off[i]; k < nt->alias_off[i + 1]; k++) n.aliases.push_back(S(st, nt->alias_name[k]));
+        n.reserved_dyn = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
+        if (nt->hv_off)
+            for (uint32_t k = nt->hv_off[i]; k < nt->hv_off[i + 1]; k++) n.host_volumes[S(st, nt->hv_name[k])] = nt->hv_read_only[k] != 0;
+        n.n_devices = nt->dev_off ? (int)(nt->dev_off[i + 1] - nt->dev_off[i]) : 0;
+    }
+    st.allocs.resize(at ? at->count : 0);
+    st.allocs_by_node.assign(nt->n, {});
+    for (uint32_t i = 0; at && i < at->count; i++) {
+        OAlloc& a = st.allocs[i];
+        a.id = i + 1;
+        a.node_row = (int)at->node_row[i];
+        if (a.node_row < 0 || a.node_row >= (int)nt->n) { s->err = "alloc node_row out of range"; return PE_EINVAL; }
+        a.ns = S(st, at->ns[i]); a.job_id = S(st, at->job_id[i]); a.tg = S(st, at->task_group[i]);
+        a.terminal = at->terminal[i] != 0; a.priority = at->priority[i];
+        a.cpu = at->cpu_shares[i]; a.mem = at->memory_mb[i]; a.disk = at->disk_mb[i];
+        a.mbits = at->net_mbits[i]; a.dyn_ports = at->dyn_ports[i];
+        st.allocs_by_node[a.node_row].push_back((int)i);
+    }
+    s->ctx.plan = Plan();
+    return PE_OK;
+}
+
+}  // extern "C"
+
+// Fresh EvalContext on the same snapshot: the chain and the eligibility memo
+// are rebuilt, exactly as a new eval would construct them.
+extern "C" int oracle_reset_plan(oracle_stack* s) {
+    State saved = std::move(s->state);
+    pe_config cfg = s->cfg;
+    s->~oracle_stack();
+    new (s) oracle_stack(cfg);
+    s->state = std::move(saved);
+    s->ctx.state = &s->state;
+    return PE_OK;
+}
+
+extern "C" {
+
+static std::vector<OConstraint> conv_constraints(const State& st, const pe_constraint* base, uint32_t off, uint32_t cnt) {
+    std::vector<OConstraint> out;
+    for (uint32_t i = 0; i < cnt; i++) out.push_back(OConstraint{S(st, base[off + i].ltarget), S(st, base[off + i].rtarget), S(st, base[off + i].operand)});
+    return out;
+}
+static std::vector<OAffinity> conv_affinities(const State& st, const pe_affinity* base, uint32_t off, uint32_t cnt) {
+    std::vector<OAffinity> out;
+    for (uint32_t i = 0; i < cnt; i++) out.push_back(OAffinity{S(st, base[off + i].ltarget), S(st, base[off + i].rtarget), S(st, base[off + i].operand), base[off + i].weight});
+    return out;
+}
+static std::vector<OSpread> conv_spreads(const State& st, const pe_job* j, uint32_t off, uint32_t cnt) {
+    std::vector<OSpread> out;
+    for (uint32_t i = 0; i < cnt; i++) {
+        const pe_spread& sp = j->spreads[off + i];
+        OSpread o; o.attribute = S(st, sp.attribute); o.weight = (int8_t)sp.weight;
+        for (uint32_t k = 0; k < sp.target_count; k++) {
+            const pe_spread_target& t = j->spread_targets[sp.target_off + k];
+            o.targets.push_back(OSpreadTarget{S(st, t.value), t.percent});
+        }
+        out.push_back(o);
+    }
+    return out;
+}
+
+int oracle_set_job(oracle_stack* s, const pe_strtab* strs, const pe_job* j) {
+    State& st = s->state;
+    for (uint32_t i = (uint32_t)st.strs.size(); strs && i < strs->count; i++)
+        st.strs.emplace_back(strs->bytes + strs->offsets[i], strs->offsets[i + 1] - strs->offsets[i]);
+    OJob job;
+    job.id = S(st, j->id); job.ns = S(st, j->ns); job.type = j->type; job.priority = j->priority; job.version = j->version;
+    job.constraints = conv_constraints(st, j->constraints, j->constraint_off, j->constraint_count);
+    job.affinities = conv_affinities(st, j->affinities, j->affinity_off, j->affinity_count);
+    job.spreads = conv_spreads(st, j, j->spread_off, j->spread_count);
+    for (uint32_t g = 0; g < j->tg_count; g++) {
+        const pe_task_group& t = j->task_groups[g];
+        OTaskGroup tg;
+        tg.name = S(st, t.name); tg.count = t.count; tg.disk = t.ephemeral_disk_mb;
+        tg.constraints = conv_constraints(st, j->constraints, t.constraint_off, t.constraint_count);
+        tg.affinities = conv_affinities(st, j->affinities, t.affinity_off, t.affinity_count);
+        tg.spreads = conv_spreads(st, j, t.spread_off, t.spread_count);
+        tg.has_network = t.has_network != 0; tg.net_mode = S(st, t.net_mode);
+        tg.net_host_network = S(st, t.net_host_network);
+        if (tg.net_host_network.empty()) tg.net_host_network = "default";
+        tg.net_dyn = t.net_dyn_ports; tg.net_reserved = t.net_reserved_ports;
+        for (uint32_t k = 0; k < t.volume_count; k++)
+            tg.volumes.push_back({S(st, j->volume_source[t.volume_off + k]), j->volume_read_only[t.volume_off + k] != 0});
+        tg.csi = t.has_csi_volumes != 0;
+        for (uint32_t k = 0; k < t.task_count; k++) {
+            const pe_task& pt = j->tasks[t.task_off + k];
+            OTask ot;
+            ot.name = S(st, pt.name); ot.driver = S(st, pt.driver);
+            ot.cpu = pt.cpu; ot.mem = pt.memory_mb; ot.mem_max = pt.memory_max_mb; ot.cores = pt.cores;
+            ot.lifecycle = pt.lifecycle;
+            ot.has_network = pt.has_network != 0; ot.net_mbits = pt.net_mbits; ot.net_dyn = pt.net_dyn_ports; ot.net_reserved = pt.net_reserved_ports;
+            ot.n_devices = (int)pt.device_count;
+            tg.tasks.push_back(ot);
+            tg.task_constraints.push_back(conv_constraints(st, j->constraints, pt.constraint_off, pt.constraint_count));
+            tg.task_affinities.push_back(conv_affinities(st, j->affinities, pt.affinity_off, pt.affinity_count));
+        }
+        job.tgs.push_back(tg);
+    }
+    // GenericStack.SetJob skips when the job version is unchanged (stack.go:94-96)
+    if (s->cfg.stack_kind == PE_STACK_GENERIC && s->have_job_version && s->job_version == job.version) return PE_OK;
+    s->have_job_version = true; s->job_version = job.version;
+    s->job = job; s->have_job = true;
+    const OJob* jp = &s->job;
+    s->job_constraint.cs = jp->constraints;
+    if (s->cfg.stack_kind == PE_STACK_GENERIC) s->distinct_hosts.SetJob(jp);
+    s->distinct_property.SetJob(jp);
+    s->bin_pack.priority = jp->priority; s->bin_pack.job_id = jp->id;
+    s->job_anti_aff.job_id = jp->id;
+    s->node_affinity.SetJob(jp);
+    s->spread.SetJob(jp);
+    s->ctx.elig.SetJob(*jp);
+    return PE_OK;
+}
+
+int oracle_set_nodes(oracle_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
+    std::vector<const ONode*> ns;
+    for (uint32_t i = 0; i < n; i++) {
+        if (rows[i] >= s->state.nodes.size()) { s->err = "row out of range"; return PE_EINVAL; }
+        ns.push_back(&s->state.nodes[rows[i]]);
+    }
+    s->base_nodes = ns;
+    s->source.SetNodes(ns);
+    int lim = 2;
+    if (s->cfg.stack_kind == PE_STACK_GENERIC && !s->cfg.batch && n > 0) {
+        int log_limit = (int)std::ceil(std::log2((double)n));
+        if (log_limit > lim) lim = log_limit;
+    }
+    s->limit.limit = lim;
+    if (limit_out) *limit_out = (uint32_t)lim;
+    return PE_OK;
+}
+
+// taskGroupConstraints (util.go:843-858) + per-tg parameterisation (stack.go:139-163)
+static void set_task_group(oracle_stack* s, const OTaskGroup& tg, bool system) {
+    std::vector<OConstraint> cs = tg.constraints;
+    std::set<std::string> drivers;
+    for (size_t k = 0; k < tg.tasks.size(); k++) {
+        drivers.insert(tg.tasks[k].driver);
+        cs.insert(cs.end(), tg.task_constraints[k].begin(), tg.task_constraints[k].end());
+    }
+    if (tg.csi) throw Unsupported("CSI volumes");
+    s->tg_drivers.drivers = drivers;
+    s->tg_constraint.cs = cs;
+    int ndev = 0; for (auto& t : tg.tasks) ndev += t.n_devices;
+    s->tg_devices.requires = ndev > 0;
+    s->tg_volumes.volumes.clear();
+    for (auto& v : tg.volumes) s->tg_volumes.volumes[v.first].push_back(v.second);
+    if (tg.has_network) {
+        s->tg_network.mode = tg.net_mode.empty() ? "host" : tg.net_mode;
+        s->tg_network.has_ports = true;   // c.ports is a non-nil slice after SetNetwork
+        s->tg_network.port_networks.assign((size_t)(tg.net_dyn + tg.net_reserved), tg.net_host_network);
+    }
+    s->wrapped.tg = tg.name;
+    if (!system) {
+        s->distinct_hosts.SetTaskGroup(&tg);
+    }
+    s->distinct_property.SetTaskGroup(&tg);
+    s->bin_pack.tg = &tg;
+}
+
+static void fill_out(pe_ranked_node* out, RankedNode* o, const oracle_stack* s) {
+    std::memset(out, 0, sizeof(*out));
+    out->row = o ? o->node->row : -1;
+    if (o) {
+        out->final_score = o->final_score;
+        out->n_scores = (uint32_t)std::min<size_t>(o->scores.size(), PE_MAX_SCORES);
+        for (uint32_t i = 0; i < out->n_scores; i++) out->scores[i] = o->scores[i];
+    }
+    out->nodes_evaluated = s->ctx.metrics.evaluated;
+    out->nodes_filtered = s->ctx.metrics.filtered;
+    out->nodes_exhausted = s->ctx.metrics.exhausted;
+    out->new_offset = s->source.nodes.empty() ? 0 : (uint32_t)(s->source.offset % (int)s->source.nodes.size());
+}
+
+static RankedNode* generic_select(oracle_stack* s, uint32_t tgi, const pe_select_options* opts) {
+    if (opts && opts->preferred_count > 0) {
+        std::vector<const ONode*> original = s->source.nodes;
+        std::vector<const ONode*> pref;
+        for (uint32_t i = 0; i < opts->preferred_count; i++) pref.push_back(&s->state.nodes.at(opts->preferred_rows[i]));
+        s->source.SetNodes(pref);
+        pe_select_options o2 = *opts; o2.preferred_count = 0; o2.preferred_rows = nullptr;
+        RankedNode* r = generic_select(s, tgi, &o2);
+        if (r) { s->source.SetNodes(original); return r; }
+        s->source.SetNodes(original);
+        return generic_select(s, tgi, &o2);
+    }
+    s->max_score.Reset();
+    s->ctx.Reset();
+    const OTaskGroup& tg = s->tg(tgi);
+    set_task_group(s, tg, false);
+    if (opts) s->bin_pack.evict = opts->preempt != 0;
+    s->job_anti_aff.tg = tg.name; s->job_anti_aff.desired = tg.count;
+    if (opts) for (uint32_t i = 0; i < opts->penalty_count; i++) s->penalty.penalty.insert((int)opts->penalty_rows[i]);
+    s->node_affinity.SetTaskGroup(&tg);
+    s->spread.SetTaskGroup(&tg);
+    if (s->node_affinity.has() || s->spread.has_spread) s->limit.limit = INT32_MAX;
+    return s->max_score.Next();
+}
+
+static RankedNode* system_select(oracle_stack* s, uint32_t tgi) {
+    s->score_norm.Reset();
+    s->ctx.Reset();
+    const OTaskGroup& tg = s->tg(tgi);
+    set_task_group(s, tg, true);
+    return s->score_norm.Next();
+}
+
+int oracle_select(oracle_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
+    if (!s->have_job || tgi >= s->job.tgs.size()) { s->err = "select before set_job / bad tg"; return PE_ESTATE; }
+    try {
+        RankedNode* o = s->cfg.stack_kind == PE_STACK_GENERIC ? generic_select(s, tgi, opts) : system_select(s, tgi);
+        fill_out(out, o, s);
+    } catch (const Unsupported& e) {
+        s->err = std::string("unsupported: ") + e.what();
+        return PE_EUNSUPPORTED;
+    }
+    return PE_OK;
+}
+
+// Plan.AppendAlloc of a fresh alloc of the task group (structs.go:10707-10714)
+int oracle_commit(oracle_stack* s, uint32_t tgi, int32_t row) {
+    if (!s->have_job || tgi >= s->job.tgs.size() || row < 0 || row >= (int32_t)s->state.nodes.size()) {
+        s->err = "bad commit"; return PE_EINVAL;
+    }
+    const OTaskGroup& tg = s->tg(tgi);
+    Ask ask = tg_ask(tg, s->bin_pack.oversub);
+    OAlloc a;
+    a.id = s->ctx.next_alloc_id++;
+    a.node_row = row; a.ns = s->job.ns; a.job_id = s->job.id; a.tg = tg.name;
+    a.terminal = false; a.priority = s->job.priority;
+    a.cpu = ask.cpu; a.mem = ask.mem; a.disk = ask.disk;
+    tg_net_contrib(tg, &a.mbits, &a.dyn_ports);
+    s->ctx.plan.node_allocation[row].push_back(a);
+    return PE_OK;
+}
+
+int oracle_place(oracle_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+    uint32_t p = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        pe_select_options opts; std::memset(&opts, 0, sizeof(opts));
+        int rc = oracle_select(s, tgi, &opts, &out[i]);
+        if (rc != PE_OK) return rc;
+        if (out[i].row < 0) break;   // failedTGAllocs: the rest of the tg is coalesced
+        oracle_commit(s, tgi, out[i].row);
+        p++;
+    }
+    if (placed) *placed = p;
+    return PE_OK;
+}
+
+int oracle_system_place(oracle_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status,
+                        uint32_t* placed) {
+    std::vector<const ONode*> all = s->base_nodes;
+    uint32_t p = 0;
+    for (size_t i = 0; i < all.size(); i++) {
+        s->source.SetNodes(std::vector<const ONode*>{all[i]});
+        pe_ranked_node r;
+        int rc = oracle_select(s, tgi, nullptr, &r);
+        if (rc != PE_OK) return rc;
+        if (r.row < 0) {
+            out_score[i] = NAN;
+            out_status[i] = s->ctx.metrics.filtered > 0 ? 1 : 2;
+            continue;
+        }
+        out_score[i] = r.final_score; out_status[i] = 0;
+        oracle_commit(s, tgi, r.row);
+        p++;
+    }
+    s->source.SetNodes(all);
+    if (placed) *placed = p;
+    return PE_OK;
+}
+
+double oracle_go_pow(double x, double y) { return gomath::pow(x, y); }
+double oracle_go_exp(double x) { return gomath::exp(x); }
+double oracle_go_log(double x) { return gomath::log(x); }
+
+double oracle_score_fit(int algo, int64_t cpu, int64_t mem, int64_t rcpu, int64_t rmem, int64_t ucpu, int64_t umem) {
+    ONode n; n.cpu = cpu; n.mem = mem; n.rcpu = rcpu; n.rmem = rmem;
+    return BinPackIterator::score_fit(algo == PE_ALGO_SPREAD, n, ucpu, umem);
+}
+
+int oracle_check_constraint(const char* op, const char* l, int ls, const char* r, int rs) {
+    orasem::Caches c;
+    Val lv, rv;
+    lv.is_nil = ls == 0; if (ls) lv.s = l ? l : "";
+    rv.is_nil = rs == 0; if (rs) rv.s = r ? r : "";
+    return orasem::check_constraint(c, op, lv, rv, ls == 1, rs == 1) ? 1 : 0;
+}
+
+int oracle_limit_iter(const double* scores, int n, int limit, double threshold, int max_skip,
+                      int* out_order, int* winner, int* pulled) {
+    std::vector<RankedNode> nodes((size_t)n);
+    StaticRankIterator src;
+    for (int i = 0; i < n; i++) { nodes[i].node = nullptr; nodes[i].final_score = scores[i]; src.nodes.push_back(&nodes[i]); }
+    LimitIterator lim; lim.source = &src; lim.limit = limit; lim.threshold = threshold; lim.max_skip = max_skip;
+    int k = 0;
+    std::vector<RankedNode*> emitted;
+    for (RankedNode* o = lim.Next(); o; o = lim.Next()) { out_order[k++] = (int)(o - nodes.data()); emitted.push_back(o); }
+    RankedNode* mx = nullptr;
+    for (RankedNode* o : emitted) if (!mx || o->final_score > mx->final_score) mx = o;
+    *winner = mx ? (int)(mx - nodes.data()) : -1;
+    *pulled = src.pulled;
+    return k;
+}
+
+}  // extern "C"

@@ -1,0 +1,342 @@
+// ORACLE — test infrastructure only (never linked into the product).
+//
+// Restatement of the constraint semantics the placement stack evaluates per node:
+//   checkConstraint / checkLexicalOrder / checkVersionMatch / checkRegexpMatch /
+//   checkSetContainsAll / checkSetContainsAny   (scheduler/feasible.go:785-1024)
+//   github.com/hashicorp/go-version @ v1.2.1-0.20191009193637-2046c9d0f0b0
+//     (go.mod:75; not vendored in the reference): NewVersion/NewSemver, Compare,
+//     comparePrereleases, Constraint operators incl. prereleaseCheck and "~>".
+//   helper/constraints/semver/constraints.go (semver operand: Semver 2.0 ordering,
+//     no "~>" operator).
+// Regexp: Go's RE2 is restated with std::regex (ECMAScript). The two agree on
+// the pattern class used by the reference KATs (feasible_test.go:1194-1229) and
+// the configs (anchors, classes, alternation, repetition); RE2-only syntax
+// (e.g. (?P<name>..), \pL) is outside the pinned set ("parity unpinned").
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+#include <regex>
+#include <map>
+#include <memory>
+#include <cctype>
+#include <climits>
+
+namespace orasem {
+
+// A resolved target: Go's (interface{}, bool). `nil` only for unknown ${...}
+// interpolations (feasible.go:778-779); a missing attribute resolves to ("", false).
+struct Val {
+    bool is_nil = true;
+    std::string s;
+};
+
+static inline bool deep_equal(const Val& a, const Val& b) {
+    if (a.is_nil || b.is_nil) return a.is_nil && b.is_nil;
+    return a.s == b.s;
+}
+
+// ---------------- go-version ----------------
+struct Version {
+    std::vector<int64_t> segments;  // padded to >= 3
+    int si = 0;                     // number of specified segments
+    std::string pre, metadata, original;
+};
+
+static inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
+static inline bool is_ident(char c) {   // [0-9A-Za-z\-~]
+    return std::isalnum((unsigned char)c) || c == '-' || c == '~';
+}
+
+// parse int64 like strconv.ParseInt(s, 10, 64)
+static inline bool parse_i64(const std::string& s, int64_t* out) {
+    if (s.empty()) return false;
+    size_t i = 0; bool neg = false;
+    if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; if (s.size() == 1) return false; }
+    __int128 v = 0;
+    for (; i < s.size(); i++) {
+        if (!is_digit(s[i])) return false;
+        v = v * 10 + (s[i] - '0');
+        if (v > (__int128)INT64_MAX + 1) return false;
+    }
+    if (neg) v = -v;
+    if (v > INT64_MAX || v < INT64_MIN) return false;
+    *out = (int64_t)v;
+    return true;
+}
+
+// dotted identifier list: ident(.ident)*  where the first ident obeys `first`
+static inline size_t match_dotted(const std::string& s, size_t p) {
+    size_t q = p;
+    if (q >= s.size() || !is_ident(s[q])) return std::string::npos;
+    while (q < s.size() && is_ident(s[q])) q++;
+    while (q < s.size() && s[q] == '.') {
+        size_t r = q + 1;
+        if (r >= s.size() || !is_ident(s[r])) break;
+        while (r < s.size() && is_ident(s[r])) r++;
+        q = r;
+    }
+    return q;
+}
+
+static inline const std::regex& version_re(bool semver) {
+    // Both patterns share one group layout (go-version version.go): 1 segments,
+    // 4 numeric-led prerelease, 7 alpha-led prerelease, 10 metadata. Semver
+    // requires the '-' before an alpha-led prerelease ("1.0beta1" is invalid).
+    static const std::regex v(
+        "^v?([0-9]+(\\.[0-9]+)*?)"
+        "(-([0-9]+[0-9A-Za-z\\-~]*(\\.[0-9A-Za-z\\-~]+)*)|(-?([A-Za-z\\-~]+[0-9A-Za-z\\-~]*(\\.[0-9A-Za-z\\-~]+)*)))?"
+        "(\\+([0-9A-Za-z\\-~]+(\\.[0-9A-Za-z\\-~]+)*))?$");
+    static const std::regex sv(
+        "^v?([0-9]+(\\.[0-9]+)*?)"
+        "(-([0-9]+[0-9A-Za-z\\-~]*(\\.[0-9A-Za-z\\-~]+)*)|(-([A-Za-z\\-~]+[0-9A-Za-z\\-~]*(\\.[0-9A-Za-z\\-~]+)*)))?"
+        "(\\+([0-9A-Za-z\\-~]+(\\.[0-9A-Za-z\\-~]+)*))?$");
+    return semver ? sv : v;
+}
+
+static inline bool new_version(const std::string& s, bool semver, Version* out) {
+    std::smatch m;
+    if (!std::regex_match(s, m, version_re(semver))) return false;
+    std::string segs = m[1].str();
+    Version v;
+    size_t start = 0;
+    while (true) {
+        size_t dot = segs.find('.', start);
+        std::string part = segs.substr(start, dot == std::string::npos ? std::string::npos : dot - start);
+        int64_t x;
+        if (!parse_i64(part, &x)) return false;
+        v.segments.push_back(x);
+        if (dot == std::string::npos) break;
+        start = dot + 1;
+    }
+    v.si = (int)v.segments.size();
+    while (v.segments.size() < 3) v.segments.push_back(0);
+    v.pre = m[7].matched ? m[7].str() : "";
+    if (v.pre.empty() && m[4].matched) v.pre = m[4].str();
+    v.metadata = m[10].matched ? m[10].str() : "";
+    v.original = s;
+    *out = v;
+    return true;
+}
+
+static inline std::string version_string(const Version& v) {
+    std::string o;
+    for (size_t i = 0; i < v.segments.size(); i++) {
+        if (i) o += ".";
+        o += std::to_string(v.segments[i]);
+    }
+    if (!v.pre.empty()) o += "-" + v.pre;
+    if (!v.metadata.empty()) o += "+" + v.metadata;
+    return o;
+}
+
+static inline int compare_part(const std::string& a, const std::string& b) {
+    if (a == b) return 0;
+    int64_t ai = 0, bi = 0;
+    bool an = parse_i64(a, &ai), bn = parse_i64(b, &bi);
+    if (a.empty()) return bn ? -1 : 1;
+    if (b.empty()) return an ? 1 : -1;
+    if (an && !bn) return -1;
+    if (!an && bn) return 1;
+    if (!an && !bn && a > b) return 1;
+    if (ai > bi) return 1;
+    return -1;
+}
+
+static inline std::vector<std::string> split(const std::string& s, char sep) {
+    std::vector<std::string> out;
+    size_t start = 0;
+    while (true) {
+        size_t p = s.find(sep, start);
+        out.push_back(s.substr(start, p == std::string::npos ? std::string::npos : p - start));
+        if (p == std::string::npos) break;
+        start = p + 1;
+    }
+    return out;
+}
+
+static inline int compare_prereleases(const std::string& a, const std::string& b) {
+    if (a == b) return 0;
+    auto as = split(a, '.'), bs = split(b, '.');
+    size_t n = std::max(as.size(), bs.size());
+    for (size_t i = 0; i < n; i++) {
+        std::string pa = i < as.size() ? as[i] : "";
+        std::string pb = i < bs.size() ? bs[i] : "";
+        int c = compare_part(pa, pb);
+        if (c != 0) return c;
+    }
+    return 0;
+}
+
+static inline bool all_zero(const std::vector<int64_t>& s, size_t from) {
+    for (size_t i = from; i < s.size(); i++) if (s[i] != 0) return false;
+    return true;
+}
+
+static inline int version_compare(const Version& v, const Version& o) {
+    if (version_string(v) == version_string(o)) return 0;
+    if (v.segments == o.segments) {
+        if (v.pre.empty() && o.pre.empty()) return 0;
+        if (v.pre.empty()) return 1;
+        if (o.pre.empty()) return -1;
+        return compare_prereleases(v.pre, o.pre);
+    }
+    size_t ls = v.segments.size(), lo = o.segments.size();
+    size_t hs = std::max(ls, lo);
+    for (size_t i = 0; i < hs; i++) {
+        if (i > ls - 1) { if (!all_zero(o.segments, i)) return -1; break; }
+        if (i > lo - 1) { if (!all_zero(v.segments, i)) return 1; break; }
+        int64_t l = v.segments[i], r = o.segments[i];
+        if (l == r) continue;
+        return l < r ? -1 : 1;
+    }
+    return 0;
+}
+
+enum Op { OP_EQ, OP_NE, OP_GT, OP_LT, OP_GE, OP_LE, OP_PESS };
+struct VConstraint { Op op; Version check; };
+
+static inline bool prerelease_check(const Version& v, const Version& c) {
+    bool vp = !v.pre.empty(), cp = !c.pre.empty();
+    if (cp && vp) return c.segments == v.segments;
+    if (!cp && vp) return false;
+    return true;
+}
+
+static inline bool vconstraint_check(const VConstraint& c, const Version& v, bool semver) {
+    int cmp;
+    switch (c.op) {
+        case OP_EQ: return version_compare(v, c.check) == 0;
+        case OP_NE: return version_compare(v, c.check) != 0;
+        default: break;
+    }
+    if (!semver && !prerelease_check(v, c.check)) return false;
+    switch (c.op) {
+        case OP_GT: return version_compare(v, c.check) == 1;
+        case OP_LT: return version_compare(v, c.check) == -1;
+        case OP_GE: return version_compare(v, c.check) >= 0;
+        case OP_LE: return version_compare(v, c.check) <= 0;
+        case OP_PESS: {
+            if (!c.check.pre.empty() && v.pre.empty()) return false;
+            cmp = version_compare(v, c.check);
+            if (cmp == -1) return false;
+            size_t cs = c.check.segments.size();
+            if (cs > v.segments.size()) return false;
+            for (int i = 0; i < c.check.si - 1; i++)
+                if (v.segments[i] != c.check.segments[i]) return false;
+            if (c.check.segments[cs - 1] > v.segments[cs - 1]) return false;
+            return true;
+        }
+        default: return false;
+    }
+}
+
+static inline std::string trim(const std::string& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && std::isspace((unsigned char)s[a])) a++;
+    while (b > a && std::isspace((unsigned char)s[b - 1])) b--;
+    return s.substr(a, b - a);
+}
+
+// version.NewConstraint / semver.NewConstraint: `^\s*(op)\s*(version)\s*$`
+static inline bool parse_constraints(const std::string& str, bool semver, std::vector<VConstraint>* out) {
+    out->clear();
+    for (const std::string& raw : split(str, ',')) {
+        std::string s = trim(raw);
+        Op op = OP_EQ; size_t p = 0;
+        if (!semver && s.compare(0, 2, "~>") == 0) { op = OP_PESS; p = 2; }
+        else if (s.compare(0, 2, ">=") == 0) { op = OP_GE; p = 2; }
+        else if (s.compare(0, 2, "<=") == 0) { op = OP_LE; p = 2; }
+        else if (s.compare(0, 2, "!=") == 0) { op = OP_NE; p = 2; }
+        else if (s.compare(0, 1, ">") == 0) { op = OP_GT; p = 1; }
+        else if (s.compare(0, 1, "<") == 0) { op = OP_LT; p = 1; }
+        else if (s.compare(0, 1, "=") == 0) { op = OP_EQ; p = 1; }
+        std::string vs = trim(s.substr(p));
+        Version v;
+        if (!new_version(vs, semver, &v)) return false;
+        out->push_back(VConstraint{op, v});
+    }
+    return true;
+}
+
+struct Caches {
+    std::map<std::string, std::shared_ptr<std::regex>> re;
+    std::map<std::string, std::shared_ptr<std::vector<VConstraint>>> ver, semver;
+};
+
+// checkVersionMatch (feasible.go:860-892); lVal int case is unreachable for
+// node attributes (they are strings).
+static inline bool check_version_match(Caches& c, bool semver, const Val& l, const Val& r) {
+    if (l.is_nil) return false;
+    Version v;
+    if (!new_version(l.s, false, &v)) return false;
+    if (r.is_nil) return false;
+    auto& cache = semver ? c.semver : c.ver;
+    auto it = cache.find(r.s);
+    std::shared_ptr<std::vector<VConstraint>> cs;
+    if (it != cache.end()) cs = it->second;
+    else {
+        auto p = std::make_shared<std::vector<VConstraint>>();
+        if (!parse_constraints(r.s, semver, p.get())) return false;
+        cache[r.s] = p; cs = p;
+    }
+    for (auto& k : *cs) if (!vconstraint_check(k, v, semver)) return false;
+    return true;
+}
+
+static inline bool check_regexp_match(Caches& c, const Val& l, const Val& r) {
+    if (l.is_nil || r.is_nil) return false;
+    auto it = c.re.find(r.s);
+    std::shared_ptr<std::regex> re;
+    if (it != c.re.end()) re = it->second;
+    else {
+        try { re = std::make_shared<std::regex>(r.s, std::regex::ECMAScript); }
+        catch (...) { return false; }
+        c.re[r.s] = re;
+    }
+    return std::regex_search(l.s, *re);
+}
+
+static inline bool check_set_contains_all(const Val& l, const Val& r) {
+    if (l.is_nil || r.is_nil) return false;
+    std::map<std::string, int> lookup;
+    for (auto& in : split(l.s, ',')) lookup[trim(in)] = 1;
+    for (auto& x : split(r.s, ',')) if (!lookup.count(trim(x))) return false;
+    return true;
+}
+
+static inline bool check_set_contains_any(const Val& l, const Val& r) {
+    if (l.is_nil || r.is_nil) return false;
+    std::map<std::string, int> lookup;
+    for (auto& in : split(l.s, ',')) lookup[trim(in)] = 1;
+    for (auto& x : split(r.s, ',')) if (lookup.count(trim(x))) return true;
+    return false;
+}
+
+static inline bool check_lexical_order(const std::string& op, const Val& l, const Val& r) {
+    if (l.is_nil || r.is_nil) return false;
+    if (op == "<") return l.s < r.s;
+    if (op == "<=") return l.s <= r.s;
+    if (op == ">") return l.s > r.s;
+    if (op == ">=") return l.s >= r.s;
+    return false;
+}
+
+// checkConstraint (feasible.go:785-820)
+static inline bool check_constraint(Caches& c, const std::string& op, const Val& l, const Val& r,
+                                    bool lf, bool rf) {
+    if (op == "distinct_hosts" || op == "distinct_property") return true;
+    if (op == "=" || op == "==" || op == "is") return lf && rf && deep_equal(l, r);
+    if (op == "!=" || op == "not") return !deep_equal(l, r);
+    if (op == "<" || op == "<=" || op == ">" || op == ">=") return lf && rf && check_lexical_order(op, l, r);
+    if (op == "is_set") return lf;
+    if (op == "is_not_set") return !lf;
+    if (op == "version") return lf && rf && check_version_match(c, false, l, r);
+    if (op == "semver") return lf && rf && check_version_match(c, true, l, r);
+    if (op == "regexp") return lf && rf && check_regexp_match(c, l, r);
+    if (op == "set_contains" || op == "set_contains_all") return lf && rf && check_set_contains_all(l, r);
+    if (op == "set_contains_any") return lf && rf && check_set_contains_any(l, r);
+    return false;
+}
+
+}  // namespace orasem

@@ -1,0 +1,111 @@
+"""GPU parity: the HIP engine against the oracle on identical seeded inputs.
+
+Bar (BASELINE.json north_star): chosen node rows, cursor offsets and filter /
+exhaust counts bit-exact; float64 scores bit-exact (same portable Pow
+algorithm on both sides; the 1e-12 relative bound vs Go is the documented
+tolerance, see oracle/gomath.h).
+"""
+import numpy as np
+import pytest
+
+from nomad_amd import synth
+from nomad_amd.structs import Constraint, SchedulerConfig
+from oracle.oracle import OracleGenericStack, OracleSystemStack
+from tests.helpers import assert_same_placements, run_place
+
+pytestmark = pytest.mark.gpu
+
+
+def engine_generic(**kw):
+    from nomad_amd.stack import GenericStack
+    return GenericStack(**kw)
+
+
+def engine_system(**kw):
+    from nomad_amd.stack import SystemStack
+    return SystemStack(**kw)
+
+
+def test_c1_mock_nodes_count10():
+    nodes, allocs = synth.cluster_c1(100, seed=42)
+    job = synth.mock_job(count=10)
+    perm = synth.shuffle(len(nodes), 1)
+    _, lim_o, ro = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    _, lim_e, re = run_place(engine_generic, nodes, allocs, job, perm)
+    assert lim_o == lim_e == 7
+    assert len(ro) == 10
+    assert_same_placements(re, ro)
+
+
+@pytest.mark.parametrize("n,count,seed", [(1000, 300, 3), (10000, 1000, 1)])
+def test_c2_binpack_windowed(n, count, seed):
+    nodes, allocs = synth.cluster_c2(n, seed=42)
+    job = synth.job_c2(count)
+    perm = synth.shuffle(len(nodes), seed)
+    _, lo, ro = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    _, le, re = run_place(engine_generic, nodes, allocs, job, perm)
+    assert lo == le
+    assert_same_placements(re, ro)
+
+
+def test_c2_spread_algorithm():
+    nodes, allocs = synth.cluster_c2(2000, seed=5)
+    job = synth.job_c2(400)
+    perm = synth.shuffle(len(nodes), 9)
+    cfg = SchedulerConfig(algorithm="spread")
+    _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, perm, config=cfg)
+    _, _, re = run_place(engine_generic, nodes, allocs, job, perm, config=cfg)
+    assert_same_placements(re, ro)
+
+
+def test_c3_spread_affinity_semver_regexp():
+    nodes, allocs = synth.cluster_c3(3000, seed=7)
+    job = synth.job_c3(300)
+    perm = synth.shuffle(len(nodes), 2)
+    _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    _, _, re = run_place(engine_generic, nodes, allocs, job, perm)
+    assert_same_placements(re, ro)
+
+
+def test_exhaustion_until_full():
+    """Small cluster, large count: placements run until no node fits (nil option)."""
+    nodes, allocs = synth.cluster_c2(50, seed=8)
+    job = synth.job_c2(5000)
+    perm = synth.shuffle(len(nodes), 4)
+    _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    _, _, re = run_place(engine_generic, nodes, allocs, job, perm)
+    assert ro[-1].row == -1
+    assert_same_placements(re, ro)
+
+
+def test_select_commit_path_matches_place():
+    nodes, allocs = synth.cluster_c2(500, seed=3)
+    job = synth.job_c2(50)
+    perm = synth.shuffle(len(nodes), 6)
+    o = OracleGenericStack(); o.SetState(nodes, allocs); o.SetJob(job); o.SetNodes(list(perm))
+    e = engine_generic(); e.SetState(nodes, allocs); e.SetJob(job); e.SetNodes(list(perm))
+    for _ in range(50):
+        a, b = o.SelectRaw(0), e.SelectRaw(0)
+        assert_same_placements([b], [a])
+        if a.row < 0:
+            break
+        o.Commit(0, a.row)
+        e.Commit(0, b.row)
+
+
+def test_system_job_sweep():
+    nodes, allocs = synth.cluster_c4(3000, seed=11)
+    job = synth.mock_system_job()
+    perm = synth.shuffle(len(nodes), 5)
+    res = []
+    for cls in (OracleSystemStack, engine_system):
+        st = cls()
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(list(perm))
+        res.append(st.SystemPlace(0))
+    (so, to, po), (se, te, pe) = res
+    assert po == pe
+    assert np.array_equal(to, te)
+    placed = to == 0
+    assert np.array_equal(so[placed], se[placed])
