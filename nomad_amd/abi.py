@@ -157,6 +157,10 @@ class pe_ranked_node(C.Structure):
                 ("nodes_exhausted", C.c_uint32), ("new_offset", C.c_uint32)]
 
 
+class pe_placement(C.Structure):
+    _fields_ = [("row", C.c_int32), ("nodes_evaluated", C.c_uint32), ("final_score", C.c_double)]
+
+
 # Entry points declared in include/nomad_pe.h: (name, restype, argtypes)
 def _sigs(prefix, handle):
     H = C.c_void_p
@@ -177,7 +181,7 @@ def _sigs(prefix, handle):
 ENGINE_SYMBOLS = [
     "pe_abi_version", "pe_stack_create", "pe_stack_destroy", "pe_last_error", "pe_set_state",
     "pe_reset_plan", "pe_set_job", "pe_set_nodes", "pe_select", "pe_commit", "pe_place", "pe_system_place",
-    "pe_last_kernel_ms",
+    "pe_last_kernel_ms", "pe_stage_orders", "pe_place_batch",
 ]
 
 

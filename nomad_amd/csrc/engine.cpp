@@ -30,10 +30,11 @@
 #include "engine_types.h"
 #include "gomath_dev.h"
 
-extern "C" hipError_t pe_launch_place(const pe::SelectArgs* a, hipStream_t st);
-extern "C" hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
-extern "C" hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a,
-                                       uint32_t row, hipStream_t st);
+size_t pe_place_lds_bytes(bool full, int hash_bits, bool net);
+hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
+hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
+hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
+                            hipStream_t st);
 
 namespace {
 
@@ -66,6 +67,7 @@ struct DevMem {
 struct HostNode {
     uint32_t id, name, dc, node_class, cclass;
     uint32_t cls;
+    uint32_t sig;          // (class, drivers, networks, aliases, volumes, devices) signature
     std::vector<std::pair<uint32_t, uint32_t>> attrs, meta;   // sorted by key id
     std::vector<std::pair<uint32_t, uint8_t>> drivers;        // sorted by name id
     std::vector<uint32_t> net_modes;
@@ -138,6 +140,10 @@ struct TgPlan {
     bool has_aff_table = false, node_aff_used = false, node_ok_used = false, alias_used = false;
     std::vector<std::unique_ptr<PsetDev>> psets;
     bool psets_built = false;
+    // memo emulation inputs
+    std::vector<uint8_t> sig_tg, class_uniform, class_verdict, job_ok_node;
+    std::vector<uint32_t> nonuniform;
+    DevMem class_ok_batch;
 };
 
 }  // namespace
@@ -159,6 +165,15 @@ struct pe_stack {
     std::vector<HostAlloc> allocs;
     uint32_t ncls = 0;
     std::vector<uint32_t> class_rep;   // first row of each class
+    // Nodes with equal ComputedClass AND equal non-hashed checker inputs
+    // (drivers, networks, host-network aliases, host volumes, device count)
+    // share a signature: every FeasibilityChecker verdict is a function of it.
+    std::vector<uint32_t> sig_rep, sig_cls;
+    std::vector<std::vector<uint32_t>> class_sigs;
+    // staged visit orders for pe_place_batch
+    DevMem d_orders;
+    std::vector<uint32_t> h_orders;
+    uint32_t staged_evals = 0, staged_n = 0;
     std::vector<int64_t> h_cap_cpu, h_cap_mem, h_cap_disk;
     std::vector<int64_t> h_base_cpu, h_base_mem, h_base_disk;
     std::vector<int32_t> h_base_mbits, h_base_dyn;
@@ -446,6 +461,38 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
         s->h_base_dyn[i] = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
     }
     s->ncls = (uint32_t)s->class_rep.size();
+    // checker-input signatures
+    {
+        std::map<std::vector<uint32_t>, uint32_t> sig_of;
+        s->sig_rep.clear();
+        s->sig_cls.clear();
+        s->class_sigs.assign(s->ncls, {});
+        std::vector<uint32_t> key;
+        for (uint32_t i = 0; i < n; i++) {
+            HostNode& h = s->nodes[i];
+            key.clear();
+            key.push_back(h.cls);
+            key.push_back((uint32_t)h.drivers.size());
+            for (auto& d : h.drivers) { key.push_back(d.first); key.push_back(d.second); }
+            key.push_back((uint32_t)h.net_modes.size());
+            for (uint32_t m : h.net_modes) key.push_back(m);
+            std::vector<uint32_t> al = h.aliases;
+            std::sort(al.begin(), al.end());
+            key.push_back((uint32_t)al.size());
+            key.insert(key.end(), al.begin(), al.end());
+            key.push_back((uint32_t)h.volumes.size());
+            for (auto& v : h.volumes) { key.push_back(v.first); key.push_back(v.second); }
+            key.push_back((uint32_t)h.n_devices);
+            auto it = sig_of.find(key);
+            if (it == sig_of.end()) {
+                it = sig_of.emplace(key, (uint32_t)s->sig_rep.size()).first;
+                s->sig_rep.push_back(i);
+                s->sig_cls.push_back(h.cls);
+                s->class_sigs[h.cls].push_back(it->second);
+            }
+            h.sig = it->second;
+        }
+    }
     s->allocs.clear();
     for (uint32_t i = 0; at && i < at->count; i++) {
         const uint32_t row = at->node_row[i];
@@ -600,6 +647,59 @@ int build_psets(pe_stack* s, TgPlan& g) {
     return PE_OK;
 }
 
+// Task-group checker verdict per signature and, per class, whether every
+// signature of the class agrees ("uniform": the memo outcome does not depend
+// on which member is visited first).
+void classify_classes(pe_stack* s, TgPlan& g, pe::ConstraintEvaluator& ev) {
+    if (!g.sig_tg.empty()) return;
+    g.sig_tg.assign(s->sig_rep.size(), 0);
+    for (size_t sg = 0; sg < s->sig_rep.size(); sg++)
+        g.sig_tg[sg] = tg_feasible(s, ev, g, s->nodes[s->sig_rep[sg]]) ? 1 : 0;
+    g.class_uniform.assign(s->ncls, 1);
+    g.class_verdict.assign(s->ncls, 0);
+    if (s->job_memo.size() != s->ncls) s->job_memo.assign(s->ncls, -1);
+    for (uint32_t c = 0; c < s->ncls; c++) {
+        const auto& sigs = s->class_sigs[c];
+        g.class_verdict[c] = g.sig_tg[sigs[0]];
+        for (uint32_t sg : sigs) if (g.sig_tg[sg] != g.class_verdict[c]) g.class_uniform[c] = 0;
+        if (!s->job_escaped && s->job_memo[c] == -1)
+            s->job_memo[c] = job_feasible(s, ev, s->nodes[s->class_rep[c]]) ? 1 : 0;
+    }
+    g.nonuniform.clear();
+    for (uint32_t c = 0; c < s->ncls; c++) if (!g.class_uniform[c]) g.nonuniform.push_back(c);
+}
+
+// EvalEligibility memo emulation: the first node of a
+// class that passes the job checks, in visit order from the cursor, decides
+// the task group's verdict for the class. Uniform classes are decided by any
+// member; only non-uniform ones need the scan.
+void decide_classes(pe_stack* s, TgPlan& g, pe::ConstraintEvaluator& ev, std::vector<int8_t>& memo,
+                    const uint32_t* order, size_t m, uint32_t start) {
+    (void)ev;
+    size_t pending = 0;
+    for (uint32_t c = 0; c < s->ncls; c++) {
+        if (memo[c] != -1) continue;
+        if (g.class_uniform[c]) memo[c] = g.class_verdict[c];
+        else pending++;
+    }
+    for (size_t k = 0; k < m && pending; k++) {
+        const uint32_t row = order[(start + k) % m];
+        const HostNode& nd = s->nodes[row];
+        const uint32_t c = nd.cls;
+        if (memo[c] != -1) continue;
+        const bool jr = s->job_escaped ? g.job_ok_node[row] != 0 : s->job_memo[c] == 1;
+        if (!jr) continue;
+        memo[c] = g.sig_tg[nd.sig];
+        pending--;
+    }
+}
+
+std::vector<uint8_t> class_verdicts(pe_stack* s, TgPlan& g, const std::vector<int8_t>& memo) {
+    std::vector<uint8_t> ok(s->ncls, 0);
+    for (uint32_t c = 0; c < s->ncls; c++) ok[c] = memo[c] == 1 && (s->job_escaped || s->job_memo[c] == 1);
+    return ok;
+}
+
 // FeasibilityWrapper + EvalEligibility memo emulation for one task group over a
 // scan order (the visit order from the cursor). See SURVEY.md Appendix A3.
 int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start) {
@@ -617,34 +717,16 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
             node_ok[row] = job_feasible(s, ev, s->nodes[row]) && tg_feasible(s, ev, g, s->nodes[row]);
         std::fill(class_ok.begin(), class_ok.end(), 1);
     } else {
-        std::vector<uint8_t> job_ok_node;
         if (s->job_escaped) {
-            job_ok_node.assign(n, 0);
-            for (uint32_t row = 0; row < n; row++) job_ok_node[row] = job_feasible(s, ev, s->nodes[row]);
+            g.job_ok_node.assign(n, 0);
+            for (uint32_t row = 0; row < n; row++) g.job_ok_node[row] = job_feasible(s, ev, s->nodes[row]);
+        } else {
+            g.job_ok_node.clear();
         }
-        const size_t m = order.size();
-        for (size_t k = 0; k < m; k++) {
-            const uint32_t row = order[(start + k) % m];
-            const uint32_t c = s->nodes[row].cls;
-            if (memo[c] != -1) continue;
-            bool jr;
-            if (s->job_escaped) jr = job_ok_node[row] != 0;
-            else {
-                if (s->job_memo[c] == -1) s->job_memo[c] = job_feasible(s, ev, s->nodes[row]) ? 1 : 0;
-                jr = s->job_memo[c] == 1;
-            }
-            if (!jr) continue;
-            memo[c] = tg_feasible(s, ev, g, s->nodes[row]) ? 1 : 0;
-        }
-        for (uint32_t c = 0; c < s->ncls; c++) {
-            bool ok = memo[c] == 1;
-            if (!s->job_escaped) {
-                if (s->job_memo[c] == -1) s->job_memo[c] = job_feasible(s, ev, s->nodes[s->class_rep[c]]) ? 1 : 0;
-                ok = ok && s->job_memo[c] == 1;
-            }
-            class_ok[c] = ok;
-        }
-        if (s->job_escaped) node_ok = job_ok_node;
+        classify_classes(s, g, ev);
+        decide_classes(s, g, ev, memo, order.data(), order.size(), start);
+        class_ok = class_verdicts(s, g, memo);
+        if (s->job_escaped) node_ok = g.job_ok_node;
     }
     HIP_TRY(s, upload(g.class_ok, class_ok));
     g.node_ok_used = !node_ok.empty();
@@ -747,33 +829,55 @@ void invalidate_tables(pe_stack* s) {
     for (auto& g : s->tgs) g->tables_valid = false;
 }
 
-int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::vector<uint32_t>& order,
-              uint32_t offset, const pe_select_options* opts, pe_ranked_node* out, uint32_t* placed,
-              uint32_t* new_offset) {
-    TgPlan& g = *s->tgs[tgi];
-    if (order.empty()) {
-        for (uint32_t i = 0; i < count && i < 1; i++) {
-            std::memset(&out[i], 0, sizeof(out[i]));
-            out[i].row = -1;
-        }
-        *placed = 0;
-        *new_offset = 0;
-        return PE_OK;
-    }
-    HIP_TRY(s, upload(s->d_visit, order));
-    HIP_TRY(s, s->d_out.ensure(sizeof(pe_ranked_node) * std::max<uint32_t>(count, 1)));
-    HIP_TRY(s, s->d_status.ensure(16));
-    pe::SelectArgs A;
+// Largest overlay (log2 entries) that fits the LDS budget of one workgroup.
+int max_hash_bits(bool full, bool net) {
+    int bits = 12;
+    while (bits > 6 && pe_place_lds_bytes(full, bits, net) > 96 * 1024) bits--;
+    return bits;
+}
+
+int hash_bits_for(uint32_t count, bool full, bool net) {
+    int bits = 6;
+    while (bits < 30 && (1u << bits) < 2u * std::max<uint32_t>(count, 1)) bits++;
+    return std::min(bits, max_hash_bits(full, net));
+}
+
+pe::BatchArgs batch_args(pe_stack* s, TgPlan& g) {
+    pe::BatchArgs A;
     std::memset(&A, 0, sizeof(A));
     A.soa = soa_of(s);
     A.tg = tables_of(g);
     A.ask = ask_for(s, g);
-    // job anti-affinity is always part of the GenericStack
-    A.perm = s->d_visit.as<uint32_t>();
-    A.n_visit = (uint32_t)order.size();
-    A.offset = offset;
     A.limit = s->limit;
-    A.penalty_bits = nullptr;
+    A.log10 = s->log10;
+    A.net_overlay = (g.ask.tg_dyn > 0 || g.ask.has_task_net) ? 1 : 0;
+    return A;
+}
+
+bool full_scan_kernel(pe_stack* s, TgPlan& g, uint32_t n) {
+    return !g.psets.empty() || s->limit >= n;
+}
+
+// One evaluation on the stack's plan (pe_select / pe_place): the fused count
+// loop in launches of at most H/2 placements, each merging its overlay back
+// into the HBM SoA so the plan persists.
+int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::vector<uint32_t>& order,
+              uint32_t offset, const pe_select_options* opts, pe_ranked_node* out, uint32_t* placed,
+              uint32_t* new_offset) {
+    TgPlan& g = *s->tgs[tgi];
+    *placed = 0;
+    *new_offset = offset;
+    if (order.empty()) {
+        if (count) { std::memset(&out[0], 0, sizeof(out[0])); out[0].row = -1; }
+        *new_offset = 0;
+        return PE_OK;
+    }
+    const uint32_t n = (uint32_t)order.size();
+    const bool full = full_scan_kernel(s, g, n);
+    pe::BatchArgs A = batch_args(s, g);
+    HIP_TRY(s, upload(s->d_visit, order));
+    A.perms = s->d_visit.as<uint32_t>();
+    A.n_visit = n;
     if (opts && opts->penalty_count > 0) {
         std::vector<uint32_t> bits((s->nodes.size() + 31) / 32, 0);
         for (uint32_t i = 0; i < opts->penalty_count; i++) {
@@ -783,26 +887,39 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         HIP_TRY(s, upload(s->d_penalty, bits));
         A.penalty_bits = s->d_penalty.as<uint32_t>();
     }
-    A.log10 = s->log10;
-    A.count = count;
+    A.hash_bits = hash_bits_for(count, full, A.net_overlay != 0);
+    const uint32_t chunk = std::max<uint32_t>(1, (1u << A.hash_bits) / 2);
+    HIP_TRY(s, s->d_out.ensure(sizeof(pe_ranked_node) * std::min(count, chunk)));
+    HIP_TRY(s, s->d_status.ensure(16));
     A.commit = commit;
-    A.out = s->d_out.as<pe_ranked_node>();
-    A.status = s->d_status.as<uint32_t>();
-    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-    HIP_TRY(s, pe_launch_place(&A, s->stream));
-    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
-    uint32_t st[2];
-    HIP_TRY(s, hipMemcpyAsync(st, A.status, sizeof(st), hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(s, hipStreamSynchronize(s->stream));
-    float ms = 0;
-    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
-    s->last_ms = ms;
-    const uint32_t got = std::min(count, st[0] + 1);   // placed + the failing Select
-    HIP_TRY(s, hipMemcpy(out, A.out, sizeof(pe_ranked_node) * got, hipMemcpyDeviceToHost));
-    *placed = st[0];
-    *new_offset = st[1];
-    if (commit)
-        for (uint32_t i = 0; i < st[0]; i++) s->plan.emplace_back(g.name, (uint32_t)out[i].row);
+    A.writeback = commit;
+    A.full_out = s->d_out.as<pe_ranked_node>();
+    A.eval_status = s->d_status.as<uint32_t>();
+    double total_ms = 0;
+    uint32_t done = 0;
+    while (done < count) {
+        const uint32_t c = std::min(chunk, count - done);
+        A.count = c;
+        A.offset0 = *new_offset;
+        HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+        HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
+        HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+        uint32_t st[2];
+        HIP_TRY(s, hipMemcpyAsync(st, A.eval_status, sizeof(st), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        float ms = 0;
+        HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        total_ms += ms;
+        const uint32_t got = std::min(c, st[0] + 1);   // placed + the failing Select
+        HIP_TRY(s, hipMemcpy(out + done, A.full_out, sizeof(pe_ranked_node) * got, hipMemcpyDeviceToHost));
+        if (commit)
+            for (uint32_t i = 0; i < st[0]; i++) s->plan.emplace_back(g.name, (uint32_t)out[done + i].row);
+        *placed += st[0];
+        *new_offset = st[1];
+        done += c;
+        if (st[0] < c) break;
+    }
+    s->last_ms = total_ms;
     return PE_OK;
 }
 
@@ -848,6 +965,14 @@ void pe_stack_destroy(pe_stack* s) {
 const char* pe_last_error(const pe_stack* s) { return s ? s->err.c_str() : g_error.c_str(); }
 
 double pe_last_kernel_ms(const pe_stack* s) { return s ? s->last_ms : 0.0; }
+
+int pe_check_constraint(const char* op, const char* l, int ls, const char* r, int rs) {
+    pe::ConstraintEvaluator ev;
+    pe::Target lt, rt;
+    lt.nil = ls == 0; lt.found = ls == 1; lt.value = (ls == 1 && l) ? l : "";
+    rt.nil = rs == 0; rt.found = rs == 1; rt.value = (rs == 1 && r) ? r : "";
+    return ev.check(op ? op : "", lt, rt) ? 1 : 0;
+}
 
 int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
     if (!s || !strs || !nodes) return PE_EINVAL;
@@ -1108,6 +1233,103 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     // multi-tg jobs sharing a name see these allocs in their collision counts
     for (size_t k = 0; k < s->tgs.size(); k++)
         if (k != tgi && s->tgs[k]->name == g.name) { rc = build_collisions(s); if (rc) return rc; break; }
+    return PE_OK;
+}
+
+int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint32_t n) {
+    if (!s || (!orders && n_evals && n)) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    HIP_TRY(s, hipSetDevice(s->device));
+    const size_t total = (size_t)n_evals * n;
+    for (size_t i = 0; i < total; i++)
+        if (orders[i] >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range in staged order");
+    s->h_orders.assign(orders, orders + total);
+    HIP_TRY(s, upload(s->d_orders, s->h_orders));
+    s->staged_evals = n_evals;
+    s->staged_n = n;
+    return PE_OK;
+}
+
+int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out, uint32_t* placed) {
+    if (!s || (!out && count)) return PE_EINVAL;
+    if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place_batch needs a generic stack");
+    if (!s->plan.empty()) return s->fail(PE_ESTATE, "batch evaluations start from a fresh plan (pe_reset_plan)");
+    if (!s->have_job || tgi >= s->tgs.size()) return s->fail(PE_ESTATE, "pe_set_job not called / bad task group");
+    HIP_TRY(s, hipSetDevice(s->device));
+    const uint32_t E = s->staged_evals, n = s->staged_n;
+    if (E == 0 || n == 0) {
+        for (uint32_t e = 0; e < E; e++) {
+            if (placed) placed[e] = 0;
+            if (count) { out[(size_t)e * count].row = -1; out[(size_t)e * count].nodes_evaluated = 0; }
+        }
+        return PE_OK;
+    }
+    TgPlan& g = *s->tgs[tgi];
+    if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
+    if (!g.psets_built) {
+        int rc = build_psets(s, g);
+        if (rc) return rc;
+        if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
+    }
+    // Each eval is a fresh EvalContext: build the tables with an empty memo.
+    const std::vector<uint32_t> order0(s->h_orders.begin(), s->h_orders.begin() + n);
+    auto saved_memo = s->tg_memo;
+    s->tg_memo.erase(g.name);
+    g.tables_valid = false;
+    int rc = build_tables(s, g, order0, 0);
+    s->tg_memo = saved_memo;
+    g.tables_valid = false;
+    if (rc) return rc;
+    // limit as SetNodes(order) + Select would set it (stack.go:83-90, 165-167)
+    uint32_t lim = 2;
+    if (!s->cfg.batch) lim = std::max<uint32_t>(2, (uint32_t)std::ceil(std::log2((double)n)));
+    if (!g.affinities.empty() || !g.spreads.empty() || !s->job_spreads.empty()) lim = 0x7FFFFFFF;
+    const uint32_t saved_limit = s->limit;
+    s->limit = lim;
+    pe::BatchArgs A = batch_args(s, g);
+    s->limit = saved_limit;
+    const bool full = !g.psets.empty() || lim >= n;
+    A.hash_bits = hash_bits_for(count, full, A.net_overlay != 0);
+    if ((1u << A.hash_bits) < 2u * count)
+        return s->fail(PE_EUNSUPPORTED, "count too large for the per-eval LDS overlay in batch mode");
+    if (!g.nonuniform.empty() && !g.node_ok_used) {
+        // order-dependent memo outcomes: one class table per eval
+        std::vector<uint8_t> tabs((size_t)E * s->ncls);
+        pe::ConstraintEvaluator ev;
+        for (uint32_t e = 0; e < E; e++) {
+            std::vector<int8_t> memo(s->ncls, -1);
+            decide_classes(s, g, ev, memo, s->h_orders.data() + (size_t)e * n, n, 0);
+            auto ok = class_verdicts(s, g, memo);
+            std::copy(ok.begin(), ok.end(), tabs.begin() + (size_t)e * s->ncls);
+        }
+        HIP_TRY(s, upload(g.class_ok_batch, tabs));
+        A.tg.class_ok = g.class_ok_batch.as<uint8_t>();
+        A.class_ok_stride = s->ncls;
+    }
+    A.perms = s->d_orders.as<uint32_t>();
+    A.perm_stride = n;
+    A.n_visit = n;
+    A.count = count;
+    A.offset0 = 0;
+    A.commit = 1;
+    A.writeback = 0;
+    DevMem d_out, d_st;
+    HIP_TRY(s, d_out.ensure(sizeof(pe_placement) * (size_t)E * std::max<uint32_t>(count, 1)));
+    HIP_TRY(s, d_st.ensure(sizeof(uint32_t) * 2 * (size_t)E));
+    A.out = d_out.as<pe_placement>();
+    A.eval_status = d_st.as<uint32_t>();
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, pe_launch_place(&A, E, full, s->stream));
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    std::vector<uint32_t> st(2 * (size_t)E);
+    HIP_TRY(s, hipMemcpyAsync(st.data(), A.eval_status, st.size() * 4, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(out, A.out, sizeof(pe_placement) * (size_t)E * count, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    if (placed)
+        for (uint32_t e = 0; e < E; e++) placed[e] = st[2 * e];
     return PE_OK;
 }
 

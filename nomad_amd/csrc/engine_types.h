@@ -61,20 +61,29 @@ struct Ask {
     int32_t anti_aff;             // JobAntiAffinityIterator present (GenericStack only)
 };
 
-struct SelectArgs {
+// One launch = n_evals independent evaluations (one workgroup each) of the same
+// task group over the same snapshot; eval e visits perms + e*perm_stride.
+struct BatchArgs {
     NodeSoA soa;
     TgTables tg;
     Ask ask;
-    const uint32_t* perm;         // visit order (SetNodes list after shuffle)
-    uint32_t n_visit;             // length of the visit list
-    uint32_t offset;              // StaticIterator cursor at entry
+    const uint32_t* perms;        // visit orders (SetNodes lists after shuffle)
+    uint32_t perm_stride;         // 0: all evals share one order
+    uint32_t class_ok_stride;     // 0: shared class table, else per-eval tables
+    const uint32_t* offsets;      // per-eval StaticIterator cursor, or null -> offset0
+    uint32_t offset0;
+    uint32_t n_visit;             // length of each visit list
     uint32_t limit;               // LimitIterator limit
+    uint32_t count;               // placements to attempt per eval
     const uint32_t* penalty_bits; // bitmask over rows or null
     double log10;                 // go_log(10), computed on host
-    uint32_t count;               // placements to attempt
-    int commit;                   // apply Plan.AppendAlloc on device
-    pe_ranked_node* out;          // [count]
-    uint32_t* status;             // [0] placed, [1] final offset
+    int hash_bits;                // LDS overlay capacity = 1 << hash_bits (>= 2 * count)
+    int net_overlay;              // overlay tracks network deltas
+    int commit;                   // apply Plan.AppendAlloc after each placement
+    int writeback;                // merge the overlay into the HBM SoA at the end
+    pe_ranked_node* full_out;     // [n_evals][count] full records, or null
+    pe_placement* out;            // [n_evals][count] compact records, or null
+    uint32_t* eval_status;        // [n_evals][2]: placed, final cursor
 };
 
 struct SystemArgs {

@@ -1,19 +1,24 @@
 // HIP kernels of the MI355X placement engine (gfx950, wave64).
 //
-// k_place   — persistent single-workgroup count loop: for each placement it
-//             sweeps the visit order from the StaticIterator cursor in chunks
-//             of kPlaceBlock positions, evaluates the fused ranking pipeline per
-//             node (FeasibilityWrapper verdict from the class table, distinct
-//             hosts, BinPack fit + ScoreFit, job anti-affinity, rescheduling
-//             penalty, node affinity, spread, ScoreNormalization), reproduces
-//             LimitIterator + MaxScoreIterator with ballot prefix counts, and
-//             commits the winner (Plan.AppendAlloc) to the HBM SoA before the
-//             next placement. One launch runs the whole count loop.
-// k_system  — SystemStack sweep: one single-node Select per list entry, every
-//             node independent (scheduler_system.go:290-422); grid-stride.
-// k_sweep_scores — full-scan scoring sweep with per-block (max, first-3
-//             non-positive) reduction records: the bandwidth-bound kernel used
-//             for roofline measurement and multi-GPU shards.
+// k_place<BLOCK, FULL>  persistent count loop, one workgroup per evaluation.
+//   The node SoA in HBM is the snapshot's proposed state and is read-only
+//   during the loop; each evaluation keeps the allocs it places in a private
+//   LDS overlay (open-addressed hash keyed by node row: cpu/mem/disk/collision/
+//   network deltas), so any number of evaluations share one L2-resident table
+//   (NumSchedulers workers, nomad/config.go:468). Per placement the workgroup
+//   sweeps the visit order from the StaticIterator cursor in chunks of BLOCK
+//   positions, runs the fused ranking pipeline per node (FeasibilityWrapper
+//   verdict from the class table, distinct_hosts, BinPack fit + ScoreFit, job
+//   anti-affinity, rescheduling penalty, node affinity, spread, score
+//   normalisation), reproduces LimitIterator + MaxScoreIterator with ballot
+//   prefix counts and commits the winner to the overlay
+//   (Plan.AppendAlloc). FULL=false: one wave per eval for windowed binpack
+//   (limit = ceil(log2 n)); FULL=true: 256 threads per eval for full scans
+//   (affinities / spreads: limit = MaxInt32) with per-value spread tables in LDS.
+//   With `writeback` the overlay is merged into the HBM SoA at the end (single
+//   eval API: the plan persists in the stack).
+// k_system              SystemStack: independent single-node Selects, grid-stride.
+// k_commit              one Plan.AppendAlloc on the HBM SoA (pe_commit).
 #include <hip/hip_runtime.h>
 #include "engine_types.h"
 #include "gomath_dev.h"
@@ -21,6 +26,7 @@
 namespace pe {
 
 enum : int { kOption = 0, kFiltered = 1, kExhausted = 2 };
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
 struct NodeEval {
     int status;
@@ -29,42 +35,90 @@ struct NodeEval {
     double parts[PE_MAX_SCORES];
 };
 
+// Per-eval LDS overlay of placed allocs (empty => null arrays, no deltas).
+struct Overlay {
+    uint32_t* keys;
+    int32_t* d_cpu;
+    int32_t* d_mem;
+    int32_t* d_disk;
+    uint32_t* d_coll;
+    int32_t* d_mbits;    // null when the task group asks no network
+    int32_t* d_dyn;
+    uint32_t mask;
+    int bits;
+};
+
+__device__ __forceinline__ uint32_t ov_hash(const Overlay& o, uint32_t row) {
+    return (row * 2654435761u) >> (32 - o.bits);
+}
+
+__device__ __forceinline__ int ov_find(const Overlay& o, uint32_t row) {
+    if (!o.keys) return -1;
+    uint32_t h = ov_hash(o, row);
+    for (;;) {
+        const uint32_t k = o.keys[h];
+        if (k == row) return (int)h;
+        if (k == kEmpty) return -1;
+        h = (h + 1) & o.mask;
+    }
+}
+
+__device__ __forceinline__ int ov_claim(const Overlay& o, uint32_t row) {
+    uint32_t h = ov_hash(o, row);
+    for (;;) {
+        const uint32_t k = o.keys[h];
+        if (k == row) return (int)h;
+        if (k == kEmpty) {
+            o.keys[h] = row;
+            o.d_cpu[h] = 0; o.d_mem[h] = 0; o.d_disk[h] = 0; o.d_coll[h] = 0;
+            if (o.d_mbits) { o.d_mbits[h] = 0; o.d_dyn[h] = 0; }
+            return (int)h;
+        }
+        h = (h + 1) & o.mask;
+    }
+}
+
 __device__ __forceinline__ uint32_t pset_value(const TgTables& t, int p, uint32_t row, uint32_t cls) {
     return t.pset_val_node[p] ? t.pset_val_node[p][row] : t.pset_val_class[p][cls];
 }
 
-// Fused per-node pipeline. `spread_tab` holds the per-value spread contribution
-// of each property set for the current plan (kMissing value -> -1.0).
+// Fused per-node pipeline over base (HBM) + overlay (LDS) state.
 template <bool kKeepParts>
-__device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, const Ask& a,
-                                          const uint32_t* penalty_bits, double log10,
-                                          const double* spread_tab, uint32_t row, NodeEval* out) {
+__device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
+                                          const Ask& a, const Overlay& ov, const uint32_t* penalty_bits,
+                                          double log10, const double* spread_tab, uint32_t row,
+                                          NodeEval* out) {
     const uint32_t c = s.cls[row];
     // FeasibilityWrapper: memoised job + task-group checks (host-resolved per class)
-    bool ok = t.class_ok[c] != 0;
+    bool ok = class_ok[c] != 0;
     if (t.node_ok) ok = ok && t.node_ok[row] != 0;
+    const int slot = ov_find(ov, row);
+    const uint32_t d_coll = slot >= 0 ? ov.d_coll[slot] : 0u;
     // DistinctHostsIterator (feasible.go:569-595)
     if (ok && (a.distinct_job | a.distinct_tg)) {
-        if (a.distinct_job && s.coll_job[row] > 0) ok = false;
-        if (a.distinct_tg && t.coll_tg[row] > 0) ok = false;
+        if (a.distinct_job && s.coll_job[row] + d_coll > 0) ok = false;
+        if (a.distinct_tg && t.coll_tg[row] + d_coll > 0) ok = false;
     }
     if (!ok) { out->status = kFiltered; return; }
     // BinPackIterator (rank.go:193-527): network offers, then AllocsFit
-    int32_t dyn = 0;
-    if (a.tg_dyn > 0 || a.has_task_net) dyn = s.used_dyn[row];
-    if (a.tg_dyn > 0) {
-        if ((t.alias_ok && !t.alias_ok[row]) || kDynPortCapacity - dyn < 1) { out->status = kExhausted; return; }
-        dyn += a.tg_dyn;
-    }
-    if (a.has_task_net) {
-        const int32_t avail = s.avail_mbits[row];
-        if (avail < 0 || s.used_mbits[row] + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) {
-            out->status = kExhausted; return;
+    if (a.tg_dyn > 0 || a.has_task_net) {
+        int32_t dyn = s.used_dyn[row] + (slot >= 0 && ov.d_dyn ? ov.d_dyn[slot] : 0);
+        if (a.tg_dyn > 0) {
+            if ((t.alias_ok && !t.alias_ok[row]) || kDynPortCapacity - dyn < 1) { out->status = kExhausted; return; }
+            dyn += a.tg_dyn;
+        }
+        if (a.has_task_net) {
+            const int32_t avail = s.avail_mbits[row];
+            const int32_t mb = s.used_mbits[row] + (slot >= 0 && ov.d_mbits ? ov.d_mbits[slot] : 0);
+            if (avail < 0 || mb + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) {
+                out->status = kExhausted; return;
+            }
         }
     }
-    const int64_t ucpu = s.used_cpu[row] + a.cpu;
-    const int64_t umem = s.used_mem[row] + a.mem;
-    const int64_t udisk = s.used_disk[row] + a.disk;
+    int64_t ucpu = s.used_cpu[row] + a.cpu;
+    int64_t umem = s.used_mem[row] + a.mem;
+    int64_t udisk = s.used_disk[row] + a.disk;
+    if (slot >= 0) { ucpu += ov.d_cpu[slot]; umem += ov.d_mem[slot]; udisk += ov.d_disk[slot]; }
     const int64_t ccpu = s.cap_cpu[row], cmem = s.cap_mem[row];
     if (ccpu < ucpu || cmem < umem || s.cap_disk[row] < udisk) { out->status = kExhausted; return; }
     // Scores in append order, summed left to right.
@@ -72,7 +126,7 @@ __device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, c
     double sum = fit;
     uint32_t k = 1;
     if (kKeepParts) out->parts[0] = fit;
-    const uint32_t coll = t.coll_tg[row];
+    const uint32_t coll = t.coll_tg[row] + d_coll;
     if (a.anti_aff && coll > 0) {   // JobAntiAffinityIterator (rank.go:588-591)
         const double pen = -1 * (double)(coll + 1) / (double)a.desired_count;
         sum += pen;
@@ -110,14 +164,14 @@ __device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, c
 }
 
 // evenSpreadScoreBoost (spread.go:178-228) / target boost (spread.go:143-164)
-// for every value of every property set; one thread per value.
-__device__ void build_spread_table(const TgTables& t, double* tab, uint32_t* scratch) {
+// per value of each property set, from the eval's LDS use counts.
+template <int BLOCK>
+__device__ void build_spread_table(const TgTables& t, const uint32_t* counts, double* tab, uint32_t* scratch) {
     const int tid = threadIdx.x;
     for (int p = 0; p < t.n_psets; p++) {
         const int nv = t.pset_nvals[p];
-        const uint32_t* cnt = t.pset_counts[p];
+        const uint32_t* cnt = counts + p * kMaxValues;
         if (t.pset_even[p]) {
-            // min / max over values present in the combined use map (count > 0)
             if (tid == 0) {
                 uint32_t mn = 0, mx = 0, present = 0;
                 for (int v = 0; v < nv; v++) {
@@ -131,7 +185,7 @@ __device__ void build_spread_table(const TgTables& t, double* tab, uint32_t* scr
             }
             __syncthreads();
             const uint32_t mn = scratch[0], mx = scratch[1], present = scratch[2];
-            for (int v = tid; v < nv; v += blockDim.x) {
+            for (int v = tid; v < nv; v += BLOCK) {
                 const uint32_t cur = cnt[v];
                 double b;
                 if (present == 0) b = 0.0;
@@ -148,7 +202,7 @@ __device__ void build_spread_table(const TgTables& t, double* tab, uint32_t* scr
             }
             __syncthreads();
         } else {
-            for (int v = tid; v < nv; v += blockDim.x) {
+            for (int v = tid; v < nv; v += BLOCK) {
                 const double desired = t.pset_desired[p][v];
                 double b;
                 if (desired != desired) b = -1.0;   // no target and no implicit "*"
@@ -164,53 +218,56 @@ __device__ void build_spread_table(const TgTables& t, double* tab, uint32_t* scr
 }
 
 template <int BLOCK>
-struct PlaceShared {
-    double spread_tab[kMaxPsets * (kMaxValues + 1)];
+struct LoopShared {
     uint32_t scratch[4];
     uint32_t wave_a[BLOCK / 64];
     uint32_t wave_b[BLOCK / 64];
     double red_score[BLOCK / 64];
     int red_pos[BLOCK / 64];
-    // LimitIterator skip list: up to kMaxSkip set-aside options
-    double aside_score[kMaxSkip];
+    double aside_score[kMaxSkip];   // LimitIterator skip list
     int aside_pos[kMaxSkip];
-    int aside_row[kMaxSkip];
-    uint32_t aside_nscores[kMaxSkip];
-    // loop state
-    int stop_j;          // chunk index of the limit-th returned option, or -1
-    int done;
+    int stop_j;
 };
+
+template <int BLOCK>
+__device__ __forceinline__ void block_sync() {
+    if constexpr (BLOCK > 64) __syncthreads();
+}
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m, int lane) {
     return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-// Exclusive block prefix of a predicate; returns (prefix, total).
+// Exclusive block prefix of a predicate; *total = block count.
 template <int BLOCK>
 __device__ __forceinline__ uint32_t block_prefix(bool pred, uint32_t* wave_tot, uint32_t* total) {
-    constexpr int W = BLOCK / 64;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     const uint64_t m = __ballot(pred);
-    if (lane == 0) wave_tot[wid] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t before = 0, tot = 0;
+    if constexpr (BLOCK == 64) {
+        *total = (uint32_t)__popcll(m);
+        return lanes_below(m, lane);
+    } else {
+        constexpr int W = BLOCK / 64;
+        const int wid = threadIdx.x >> 6;
+        if (lane == 0) wave_tot[wid] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < W; w++) {
-        const uint32_t x = wave_tot[w];
-        before += (w < wid) ? x : 0u;
-        tot += x;
+        for (int w = 0; w < W; w++) {
+            const uint32_t x = wave_tot[w];
+            before += (w < wid) ? x : 0u;
+            tot += x;
+        }
+        __syncthreads();
+        *total = tot;
+        return before + lanes_below(m, lane);
     }
-    __syncthreads();
-    *total = tot;
-    return before + lanes_below(m, lane);
 }
 
-// argmax over (score desc, pos asc) for candidates; returns winner in lane 0 of wave 0 via LDS
+// first strict maximum: max score, ties -> smallest position
 template <int BLOCK>
 __device__ __forceinline__ void block_argmax(bool cand, double score, int pos, double* red_score, int* red_pos,
                                              double* best_score, int* best_pos) {
-    constexpr int W = BLOCK / 64;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double s = cand ? score : -__builtin_inf();
     int p = cand ? pos : 0x7FFFFFFF;
 #pragma unroll
@@ -219,22 +276,267 @@ __device__ __forceinline__ void block_argmax(bool cand, double score, int pos, d
         const int op = __shfl_xor(p, off);
         if (os > s || (os == s && op < p)) { s = os; p = op; }
     }
-    if (lane == 0) { red_score[wid] = s; red_pos[wid] = p; }
-    __syncthreads();
-    double bs = red_score[0];
-    int bp = red_pos[0];
+    if constexpr (BLOCK == 64) {
+        *best_score = s;
+        *best_pos = p;
+    } else {
+        constexpr int W = BLOCK / 64;
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        if (lane == 0) { red_score[wid] = s; red_pos[wid] = p; }
+        __syncthreads();
+        double bs = red_score[0];
+        int bp = red_pos[0];
 #pragma unroll
-    for (int w = 1; w < W; w++) {
-        const double os = red_score[w];
-        const int op = red_pos[w];
-        if (os > bs || (os == bs && op < bp)) { bs = os; bp = op; }
+        for (int w = 1; w < W; w++) {
+            const double os = red_score[w];
+            const int op = red_pos[w];
+            if (os > bs || (os == bs && op < bp)) { bs = os; bp = op; }
+        }
+        *best_score = bs;
+        *best_pos = bp;
+        __syncthreads();
     }
-    *best_score = bs;
-    *best_pos = bp;
-    __syncthreads();
 }
 
-__device__ __forceinline__ void commit_row(const NodeSoA& s, const TgTables& t, const Ask& a, uint32_t row) {
+// Plan.AppendAlloc into the overlay (one lane).
+__device__ __forceinline__ void commit_overlay(const NodeSoA& s, const TgTables& t, const Ask& a,
+                                               const Overlay& ov, uint32_t* counts, uint32_t row) {
+    const int h = ov_claim(ov, row);
+    ov.d_cpu[h] += (int32_t)a.cpu;
+    ov.d_mem[h] += (int32_t)a.mem;
+    ov.d_disk[h] += (int32_t)a.disk;
+    ov.d_coll[h] += 1;
+    if (ov.d_mbits) { ov.d_mbits[h] += a.commit_mbits; ov.d_dyn[h] += a.commit_dyn; }
+    if (t.n_psets > 0) {
+        const uint32_t c = s.cls[row];
+        for (int p = 0; p < t.n_psets; p++) {
+            const uint32_t v = pset_value(t, p, row, c);
+            if (v != kMissing) counts[p * kMaxValues + v] += 1;
+        }
+    }
+}
+
+template <int BLOCK, bool FULL>
+__global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
+    __shared__ LoopShared<BLOCK> sh;
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+    const int tid = threadIdx.x;
+    const uint32_t e = blockIdx.x;
+    const uint32_t n = A.n_visit;
+    const uint32_t* perm = A.perms + (size_t)e * A.perm_stride;
+    const uint8_t* class_ok = A.tg.class_ok + (size_t)e * A.class_ok_stride;
+
+    // carve the overlay (and spread tables) out of dynamic LDS
+    const uint32_t H = 1u << A.hash_bits;
+    unsigned char* p = dyn_smem;
+    double* spread_tab = nullptr;
+    uint32_t* counts = nullptr;
+    if constexpr (FULL) {
+        spread_tab = reinterpret_cast<double*>(p);
+        p += sizeof(double) * kMaxPsets * (kMaxValues + 1);
+        counts = reinterpret_cast<uint32_t*>(p);
+        p += sizeof(uint32_t) * kMaxPsets * kMaxValues;
+    }
+    Overlay ov;
+    ov.bits = A.hash_bits;
+    ov.mask = H - 1;
+    ov.keys = reinterpret_cast<uint32_t*>(p); p += 4 * H;
+    ov.d_cpu = reinterpret_cast<int32_t*>(p); p += 4 * H;
+    ov.d_mem = reinterpret_cast<int32_t*>(p); p += 4 * H;
+    ov.d_disk = reinterpret_cast<int32_t*>(p); p += 4 * H;
+    ov.d_coll = reinterpret_cast<uint32_t*>(p); p += 4 * H;
+    ov.d_mbits = nullptr;
+    ov.d_dyn = nullptr;
+    if (A.net_overlay) {
+        ov.d_mbits = reinterpret_cast<int32_t*>(p); p += 4 * H;
+        ov.d_dyn = reinterpret_cast<int32_t*>(p); p += 4 * H;
+    }
+    for (uint32_t i = tid; i < H; i += BLOCK) ov.keys[i] = kEmpty;
+    if constexpr (FULL) {
+        for (int q = 0; q < A.tg.n_psets; q++)
+            for (int v = tid; v < A.tg.pset_nvals[q]; v += BLOCK) counts[q * kMaxValues + v] = A.tg.pset_counts[q][v];
+    }
+    __syncthreads();
+
+    uint32_t offset = A.offsets ? A.offsets[e] : A.offset0;
+    if (n) offset %= n;
+    uint32_t placed = 0;
+
+    for (uint32_t it = 0; it < A.count; it++) {
+        if constexpr (FULL) {
+            if (A.tg.n_psets > 0) build_spread_table<BLOCK>(A.tg, counts, spread_tab, sh.scratch);
+        }
+        uint32_t r = 0, a = 0;            // returned / set-aside options so far
+        double best_score = -__builtin_inf();
+        int best_pos = -1;                // relative visit position of the winner
+        uint32_t n_filtered = 0, n_exhausted = 0;
+        uint32_t consumed = n;
+        bool stopped = false;
+
+        for (uint32_t base = 0; base < n; base += BLOCK) {
+            const uint32_t j = base + tid;
+            const bool valid = j < n;
+            NodeEval ev;
+            ev.status = kFiltered;
+            ev.score = 0.0;
+            if (valid) {
+                uint32_t pos = offset + j;
+                if (pos >= n) pos -= n;
+                const uint32_t row = perm[pos];
+                eval_node<false>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab, row, &ev);
+            }
+            const bool is_opt = valid && ev.status == kOption;
+            const bool is_np = is_opt && ev.score <= 0.0;
+            uint32_t np_tot;
+            const uint32_t np_before = a + block_prefix<BLOCK>(is_np, sh.wave_a, &np_tot);
+            const bool aside = is_np && np_before < (uint32_t)kMaxSkip;
+            const bool ret = is_opt && !aside;
+            uint32_t ret_tot;
+            const uint32_t ret_before = r + block_prefix<BLOCK>(ret, sh.wave_b, &ret_tot);
+            // the limit-th returned option ends the pull
+            const bool is_stop = ret && ret_before == A.limit - 1u;
+            const uint64_t sm = __ballot(is_stop);
+            int stop_j;
+            if constexpr (BLOCK == 64) {
+                stop_j = sm ? (int)__ffsll((long long)sm) - 1 : -1;
+            } else {
+                if (tid == 0) sh.stop_j = -1;
+                __syncthreads();
+                if (is_stop) sh.stop_j = tid;
+                __syncthreads();
+                stop_j = sh.stop_j;
+            }
+            const bool pulled = valid && (stop_j < 0 || tid <= stop_j);
+            if (aside && pulled) {
+                sh.aside_score[np_before] = ev.score;
+                sh.aside_pos[np_before] = (int)j;
+            }
+            const bool cand = ret && ret_before < A.limit;
+            double cs;
+            int cp;
+            block_argmax<BLOCK>(cand, ev.score, (int)j, sh.red_score, sh.red_pos, &cs, &cp);
+            if (cp != 0x7FFFFFFF && cs > best_score) { best_score = cs; best_pos = cp; }
+            uint32_t f_tot, e_tot, a_tot;
+            block_prefix<BLOCK>(pulled && ev.status == kFiltered, sh.wave_a, &f_tot);
+            block_prefix<BLOCK>(pulled && ev.status == kExhausted, sh.wave_b, &e_tot);
+            block_prefix<BLOCK>(aside && pulled, sh.wave_a, &a_tot);
+            n_filtered += f_tot;
+            n_exhausted += e_tot;
+            a += a_tot;
+            if (stop_j >= 0) {
+                consumed = base + (uint32_t)stop_j + 1u;
+                r = A.limit;
+                stopped = true;
+                break;
+            }
+            r += ret_tot;
+        }
+        block_sync<BLOCK>();
+        if (!stopped) {
+            // source exhausted: set-aside options are emitted in order until the limit
+            const uint32_t take = min(a, A.limit - r);
+            for (uint32_t i = 0; i < take; i++) {
+                if (sh.aside_score[i] > best_score) { best_score = sh.aside_score[i]; best_pos = sh.aside_pos[i]; }
+            }
+        }
+        int win_row = -1;
+        if (best_pos >= 0) {
+            uint32_t pos = offset + (uint32_t)best_pos;
+            if (pos >= n) pos -= n;
+            win_row = (int)perm[pos];
+        }
+        uint32_t no = n ? offset + (consumed % n) : 0u;
+        if (no >= n) no -= n;
+        if (tid == 0) {
+            if (A.full_out) {
+                pe_ranked_node& o = A.full_out[(size_t)e * A.count + it];
+                o.row = win_row;
+                o.nodes_evaluated = consumed;
+                o.nodes_filtered = n_filtered;
+                o.nodes_exhausted = n_exhausted;
+                o.new_offset = no;
+                o.final_score = 0.0;
+                o.n_scores = 0;
+                for (int k = 0; k < PE_MAX_SCORES; k++) o.scores[k] = 0.0;
+                if (win_row >= 0) {
+                    NodeEval ev;
+                    eval_node<true>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab,
+                                    (uint32_t)win_row, &ev);
+                    o.final_score = ev.score;
+                    o.n_scores = ev.nscores;
+                    for (int k = 0; k < (int)ev.nscores && k < PE_MAX_SCORES; k++) o.scores[k] = ev.parts[k];
+                }
+            }
+            if (A.out) {
+                pe_placement& o = A.out[(size_t)e * A.count + it];
+                o.row = win_row;
+                o.nodes_evaluated = consumed;
+                o.final_score = win_row >= 0 ? best_score : 0.0;
+            }
+            if (win_row >= 0 && A.commit) commit_overlay(A.soa, A.tg, A.ask, ov, counts, (uint32_t)win_row);
+        }
+        offset = no;
+        __syncthreads();
+        if (win_row < 0) break;   // nil option: failedTGAllocs short-circuit
+        placed++;
+    }
+    if (tid == 0) {
+        A.eval_status[2 * e] = placed;
+        A.eval_status[2 * e + 1] = offset;
+    }
+    if (A.writeback) {
+        // merge the overlay into the HBM SoA: the stack's plan persists
+        for (uint32_t h = tid; h < H; h += BLOCK) {
+            const uint32_t row = ov.keys[h];
+            if (row == kEmpty) continue;
+            A.soa.used_cpu[row] += ov.d_cpu[h];
+            A.soa.used_mem[row] += ov.d_mem[h];
+            A.soa.used_disk[row] += ov.d_disk[h];
+            A.soa.coll_job[row] += ov.d_coll[h];
+            A.tg.coll_tg[row] += ov.d_coll[h];
+            if (ov.d_mbits) { A.soa.used_mbits[row] += ov.d_mbits[h]; A.soa.used_dyn[row] += ov.d_dyn[h]; }
+        }
+        if constexpr (FULL) {
+            for (int q = 0; q < A.tg.n_psets; q++)
+                for (int v = tid; v < A.tg.pset_nvals[q]; v += BLOCK) A.tg.pset_counts[q][v] = counts[q * kMaxValues + v];
+        }
+    }
+}
+
+// SystemStack: every list entry is an independent single-node Select.
+__global__ void __launch_bounds__(256) k_system(SystemArgs A) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t local = 0;
+    Overlay none;
+    none.keys = nullptr;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n_list; i += stride) {
+        const uint32_t row = A.list[i];
+        NodeEval ev;
+        eval_node<false>(A.soa, A.tg, A.tg.class_ok, A.ask, none, nullptr, A.log10, nullptr, row, &ev);
+        if (ev.status == kOption) {
+            A.out_score[i] = ev.score;
+            A.out_status[i] = 0;
+            // Plan.AppendAlloc: rows are unique in the list, so no races
+            A.soa.used_cpu[row] += A.ask.cpu;
+            A.soa.used_mem[row] += A.ask.mem;
+            A.soa.used_disk[row] += A.ask.disk;
+            A.soa.used_mbits[row] += A.ask.commit_mbits;
+            A.soa.used_dyn[row] += A.ask.commit_dyn;
+            A.soa.coll_job[row] += 1;
+            A.tg.coll_tg[row] += 1;
+            local++;
+        } else {
+            A.out_score[i] = __builtin_nan("");
+            A.out_status[i] = (uint8_t)ev.status;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_xor(local, off);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(A.placed, local);
+}
+
+// Host-driven Plan.AppendAlloc on the HBM SoA (pe_commit).
+__global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
     s.used_cpu[row] += a.cpu;
     s.used_mem[row] += a.mem;
     s.used_disk[row] += a.disk;
@@ -249,164 +551,26 @@ __device__ __forceinline__ void commit_row(const NodeSoA& s, const TgTables& t, 
     }
 }
 
-// Persistent count loop. One workgroup; see file header.
-template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) k_place(SelectArgs A) {
-    __shared__ PlaceShared<BLOCK> sh;
-    const int tid = threadIdx.x;
-    const uint32_t n = A.n_visit;
-    uint32_t offset = A.offset % (n ? n : 1);
-    uint32_t placed = 0;
-
-    for (uint32_t it = 0; it < A.count; it++) {
-        if (A.tg.n_psets > 0) build_spread_table(A.tg, sh.spread_tab, sh.scratch);
-
-        uint32_t r = 0, a = 0;            // returned / set-aside options so far
-        double best_score = -__builtin_inf();
-        int best_pos = -1;                // relative visit position of the winner
-        uint32_t n_filtered = 0, n_exhausted = 0;
-        uint32_t consumed = n;
-        bool stopped = false;
-
-        for (uint32_t base = 0; base < n; base += BLOCK) {
-            const uint32_t j = base + tid;
-            const bool valid = j < n;
-            NodeEval ev;
-            ev.status = kFiltered;
-            ev.score = 0.0;
-            uint32_t row = 0;
-            if (valid) {
-                uint32_t pos = offset + j;
-                if (pos >= n) pos -= n;
-                row = A.perm[pos];
-                eval_node<false>(A.soa, A.tg, A.ask, A.penalty_bits, A.log10, sh.spread_tab, row, &ev);
-            }
-            const bool is_opt = valid && ev.status == kOption;
-            const bool is_np = is_opt && ev.score <= 0.0;
-            uint32_t np_tot;
-            const uint32_t np_before = a + block_prefix<BLOCK>(is_np, sh.wave_a, &np_tot);
-            const bool aside = is_np && np_before < (uint32_t)kMaxSkip;
-            const bool ret = is_opt && !aside;
-            uint32_t ret_tot;
-            const uint32_t ret_before = r + block_prefix<BLOCK>(ret, sh.wave_b, &ret_tot);
-            // the limit-th returned option ends the pull
-            if (tid == 0) sh.stop_j = -1;
-            __syncthreads();
-            if (ret && ret_before == A.limit - 1u) sh.stop_j = (int)tid;
-            __syncthreads();
-            const int stop_j = sh.stop_j;
-            const bool pulled = valid && (stop_j < 0 || (int)tid <= stop_j);
-            // set-aside options actually pulled
-            if (aside && pulled) {
-                sh.aside_score[np_before] = ev.score;
-                sh.aside_pos[np_before] = (int)j;
-                sh.aside_row[np_before] = (int)row;
-            }
-            const bool cand = ret && ret_before < A.limit;
-            double cs; int cp;
-            block_argmax<BLOCK>(cand, ev.score, (int)j, sh.red_score, sh.red_pos, &cs, &cp);
-            if (cp != 0x7FFFFFFF && cs > best_score) { best_score = cs; best_pos = cp; }
-            // metrics over pulled positions
-            uint32_t f_tot, e_tot;
-            block_prefix<BLOCK>(pulled && ev.status == kFiltered, sh.wave_a, &f_tot);
-            block_prefix<BLOCK>(pulled && ev.status == kExhausted, sh.wave_b, &e_tot);
-            n_filtered += f_tot;
-            n_exhausted += e_tot;
-            uint32_t aside_pulled;
-            block_prefix<BLOCK>(aside && pulled, sh.wave_a, &aside_pulled);
-            a += aside_pulled;
-            if (stop_j >= 0) {
-                consumed = base + (uint32_t)stop_j + 1u;
-                r = A.limit;
-                stopped = true;
-                break;
-            }
-            r += ret_tot;
-        }
-        if (!stopped) {
-            // source exhausted: skipped options are emitted in order until the limit
-            const uint32_t take = min(a, A.limit - r);
-            for (uint32_t i = 0; i < take; i++) {
-                if (sh.aside_score[i] > best_score) { best_score = sh.aside_score[i]; best_pos = sh.aside_pos[i]; }
-            }
-        }
-        // winner row and its score parts (recomputed by one lane for the record)
-        int win_row = -1;
-        if (best_pos >= 0) {
-            uint32_t pos = offset + (uint32_t)best_pos;
-            if (pos >= n) pos -= n;
-            win_row = (int)A.perm[pos];
-        }
-        if (tid == 0) {
-            pe_ranked_node& o = A.out[it];
-            o.row = win_row;
-            o.nodes_evaluated = consumed;
-            o.nodes_filtered = n_filtered;
-            o.nodes_exhausted = n_exhausted;
-            if (win_row >= 0) {
-                NodeEval ev;
-                eval_node<true>(A.soa, A.tg, A.ask, A.penalty_bits, A.log10, sh.spread_tab, (uint32_t)win_row, &ev);
-                o.final_score = ev.score;
-                o.n_scores = ev.nscores;
-                for (int k = 0; k < PE_MAX_SCORES; k++) o.scores[k] = k < (int)ev.nscores ? ev.parts[k] : 0.0;
-            } else {
-                o.final_score = 0.0;
-                o.n_scores = 0;
-                for (int k = 0; k < PE_MAX_SCORES; k++) o.scores[k] = 0.0;
-            }
-            uint32_t no = offset + (consumed % (n ? n : 1));
-            if (no >= n) no -= n;
-            o.new_offset = no;
-            if (win_row >= 0 && A.commit) commit_row(A.soa, A.tg, A.ask, (uint32_t)win_row);
-        }
-        if (n) offset = (offset + consumed % n) % n;
-        __syncthreads();
-        if (win_row < 0) break;   // nil option: failedTGAllocs short-circuit
-        placed++;
-    }
-    if (tid == 0) {
-        A.status[0] = placed;
-        A.status[1] = offset;
-    }
-}
-
-// SystemStack: every list entry is an independent single-node Select.
-__global__ void __launch_bounds__(256) k_system(SystemArgs A) {
-    const uint32_t stride = gridDim.x * blockDim.x;
-    uint32_t local = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n_list; i += stride) {
-        const uint32_t row = A.list[i];
-        NodeEval ev;
-        eval_node<false>(A.soa, A.tg, A.ask, nullptr, A.log10, nullptr, row, &ev);
-        if (ev.status == kOption) {
-            A.out_score[i] = ev.score;
-            A.out_status[i] = 0;
-            commit_row(A.soa, A.tg, A.ask, row);
-            local++;
-        } else {
-            A.out_score[i] = __builtin_nan("");
-            A.out_status[i] = (uint8_t)ev.status;
-        }
-    }
-    // one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) local += __shfl_xor(local, off);
-    if ((threadIdx.x & 63) == 0 && local) atomicAdd(A.placed, local);
-}
-
-// Host-side commit of a single placement (pe_commit).
-__global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) commit_row(s, t, a, row);
-}
-
 }  // namespace pe
 
 // ---- launch wrappers (host) ------------------------------------------------
-extern "C" hipError_t pe_launch_place(const pe::SelectArgs* a, hipStream_t st) {
-    hipLaunchKernelGGL(pe::k_place<pe::kPlaceBlock>, dim3(1), dim3(pe::kPlaceBlock), 0, st, *a);
+size_t pe_place_lds_bytes(bool full, int hash_bits, bool net) {
+    size_t b = (size_t)(net ? 7 : 5) * 4u * ((size_t)1 << hash_bits);
+    if (full) b += sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1) + 4u * pe::kMaxPsets * pe::kMaxValues;
+    return b;
+}
+
+hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st) {
+    const size_t lds = pe_place_lds_bytes(full, a->hash_bits, a->net_overlay != 0);
+    if (full) {
+        hipLaunchKernelGGL((pe::k_place<256, true>), dim3(n_evals), dim3(256), lds, st, *a);
+    } else {
+        hipLaunchKernelGGL((pe::k_place<64, false>), dim3(n_evals), dim3(64), lds, st, *a);
+    }
     return hipGetLastError();
 }
 
-extern "C" hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st) {
+hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st) {
     uint32_t blocks = (a->n_list + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
@@ -414,8 +578,8 @@ extern "C" hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st) 
     return hipGetLastError();
 }
 
-extern "C" hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a,
-                                       uint32_t row, hipStream_t st) {
+hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
+                            hipStream_t st) {
     hipLaunchKernelGGL(pe::k_commit, dim3(1), dim3(64), 0, st, *s, *t, *a, row);
     return hipGetLastError();
 }

@@ -50,6 +50,10 @@ def load_engine():
         lib.pe_abi_version.restype = C.c_uint32
         lib.pe_last_kernel_ms.restype = C.c_double
         lib.pe_last_kernel_ms.argtypes = [C.c_void_p]
+        lib.pe_stage_orders.restype = C.c_int
+        lib.pe_stage_orders.argtypes = [C.c_void_p, abi.u32p, C.c_uint32, C.c_uint32]
+        lib.pe_place_batch.restype = C.c_int
+        lib.pe_place_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(abi.pe_placement), abi.u32p]
         _engine = lib
     return _engine
 
@@ -233,6 +237,25 @@ class GenericStack(_Stack):
 
     def __init__(self, batch: bool = False, config: SchedulerConfig = None, device: int = 0):
         super().__init__(load_engine(), "pe_", batch, config, device)
+
+    def StageOrders(self, orders: np.ndarray):
+        """Stage E visit orders (E x n rows, each a shuffled SetNodes list) in HBM."""
+        o = np.ascontiguousarray(np.asarray(orders, dtype=np.uint32))
+        if o.ndim != 2:
+            raise ValueError("orders must be 2-D (evals x nodes)")
+        self._check(self._lib.pe_stage_orders(self._h, o.ctypes.data_as(abi.u32p), o.shape[0], o.shape[1]))
+        self._staged = o.shape[0]
+
+    def PlaceBatch(self, tg, count: int):
+        """Independent evaluations over the staged orders; returns (rows, scores, evaluated, placed)."""
+        E = self._staged
+        out = np.zeros(max(1, E * count), dtype=[("row", "<i4"), ("nodes_evaluated", "<u4"), ("final_score", "<f8")])
+        placed = np.zeros(max(1, E), dtype=np.uint32)
+        self._check(self._lib.pe_place_batch(self._h, self._tg_index(tg), count,
+                                             out.ctypes.data_as(C.POINTER(abi.pe_placement)),
+                                             placed.ctypes.data_as(abi.u32p)))
+        out = out[:E * count].reshape(E, count)
+        return out["row"], out["final_score"], out["nodes_evaluated"], placed[:E]
 
     def last_kernel_ms(self) -> float:
         return self._lib.pe_last_kernel_ms(self._h)

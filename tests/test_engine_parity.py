@@ -93,6 +93,33 @@ def test_select_commit_path_matches_place():
         e.Commit(0, b.row)
 
 
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_batch_evals_match_single_eval_oracle(cfg):
+    """pe_place_batch: every concurrent eval equals SetNodes(order) + Place on the oracle."""
+    if cfg == "c2":
+        nodes, allocs = synth.cluster_c2(2000, seed=21)
+        job = synth.job_c2(300)
+    else:
+        nodes, allocs = synth.cluster_c3(1500, seed=4)
+        job = synth.job_c3(120)
+    E = 6
+    orders = np.stack([synth.shuffle(len(nodes), 100 + e) for e in range(E)])
+    e = engine_generic()
+    e.SetState(nodes, allocs)
+    e.SetJob(job)
+    e.StageOrders(orders)
+    count = job.task_groups[0].count
+    rows, scores, evaluated, placed = e.PlaceBatch(0, count)
+    for k in range(E):
+        _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, orders[k])
+        assert placed[k] == sum(1 for r in ro if r.row >= 0)
+        for i, r in enumerate(ro):
+            assert rows[k, i] == r.row, (k, i)
+            assert evaluated[k, i] == r.nodes_evaluated, (k, i)
+            if r.row >= 0:
+                assert scores[k, i] == r.final_score, (k, i)
+
+
 def test_system_job_sweep():
     nodes, allocs = synth.cluster_c4(3000, seed=11)
     job = synth.mock_system_job()
