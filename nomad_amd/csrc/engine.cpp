@@ -35,6 +35,8 @@ hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, 
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
                             hipStream_t st);
+hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
+                               hipStream_t st);
 
 namespace {
 
@@ -143,7 +145,7 @@ struct TgPlan {
     // memo emulation inputs
     std::vector<uint8_t> sig_tg, class_uniform, class_verdict, job_ok_node;
     std::vector<uint32_t> nonuniform;
-    DevMem class_ok_batch;
+    DevMem class_ok_batch, node_feas;
 };
 
 }  // namespace
@@ -174,11 +176,8 @@ struct pe_stack {
     DevMem d_orders;
     std::vector<uint32_t> h_orders;
     uint32_t staged_evals = 0, staged_n = 0;
-    std::vector<int64_t> h_cap_cpu, h_cap_mem, h_cap_disk;
-    std::vector<int64_t> h_base_cpu, h_base_mem, h_base_disk;
-    std::vector<int32_t> h_base_mbits, h_base_dyn;
-    DevMem d_cls, d_cap_cpu, d_cap_mem, d_cap_disk, d_avail_mbits;
-    DevMem d_used_cpu, d_used_mem, d_used_disk, d_used_mbits, d_used_dyn, d_coll_job;
+    std::vector<pe::NodeRec> h_base_rec;     // snapshot proposed state (no plan)
+    DevMem d_rec, d_base_rec, d_coll_job;
     bool have_state = false;
 
     // job
@@ -418,11 +417,8 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     s->nodes.assign(n, HostNode());
     std::unordered_map<uint32_t, uint32_t> cls_of;
     s->class_rep.clear();
-    s->h_cap_cpu.resize(n); s->h_cap_mem.resize(n); s->h_cap_disk.resize(n);
-    s->h_base_cpu.assign(n, 0); s->h_base_mem.assign(n, 0); s->h_base_disk.assign(n, 0);
-    s->h_base_mbits.assign(n, 0); s->h_base_dyn.assign(n, 0);
-    std::vector<uint32_t> h_cls(n);
-    std::vector<int32_t> h_avail(n);
+    s->h_base_rec.assign(n, pe::NodeRec());
+    std::memset(s->h_base_rec.data(), 0, sizeof(pe::NodeRec) * n);
     for (uint32_t i = 0; i < n; i++) {
         HostNode& h = s->nodes[i];
         h.id = nt->id[i]; h.name = nt->name[i]; h.dc = nt->datacenter[i];
@@ -433,7 +429,7 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
             s->class_rep.push_back(i);
         }
         h.cls = it->second;
-        h_cls[i] = h.cls;
+        s->h_base_rec[i].cls = h.cls;
         for (uint32_t k = nt->attr_off[i]; k < nt->attr_off[i + 1]; k++) h.attrs.emplace_back(nt->attr_key[k], nt->attr_val[k]);
         for (uint32_t k = nt->meta_off[i]; k < nt->meta_off[i + 1]; k++) h.meta.emplace_back(nt->meta_key[k], nt->meta_val[k]);
         std::sort(h.attrs.begin(), h.attrs.end());
@@ -454,11 +450,12 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
             for (uint32_t k = nt->hv_off[i]; k < nt->hv_off[i + 1]; k++) h.volumes.emplace_back(nt->hv_name[k], nt->hv_read_only[k]);
         std::sort(h.volumes.begin(), h.volumes.end());
         h.n_devices = nt->dev_off ? (int)(nt->dev_off[i + 1] - nt->dev_off[i]) : 0;
-        s->h_cap_cpu[i] = nt->cpu_shares[i] - nt->reserved_cpu[i];
-        s->h_cap_mem[i] = nt->memory_mb[i] - nt->reserved_memory_mb[i];
-        s->h_cap_disk[i] = nt->disk_mb[i] - nt->reserved_disk_mb[i];
-        h_avail[i] = h.first_mbits;
-        s->h_base_dyn[i] = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
+        pe::NodeRec& r = s->h_base_rec[i];
+        r.cap_cpu = nt->cpu_shares[i] - nt->reserved_cpu[i];
+        r.cap_mem = nt->memory_mb[i] - nt->reserved_memory_mb[i];
+        r.cap_disk = nt->disk_mb[i] - nt->reserved_disk_mb[i];
+        r.avail_mbits = h.first_mbits;
+        r.used_dyn = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
     }
     s->ncls = (uint32_t)s->class_rep.size();
     // checker-input signatures
@@ -500,22 +497,15 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
         HostAlloc a{row, at->ns[i], at->job_id[i], at->task_group[i], at->terminal[i] != 0};
         s->allocs.push_back(a);
         if (a.terminal) continue;
-        s->h_base_cpu[row] += at->cpu_shares[i];
-        s->h_base_mem[row] += at->memory_mb[i];
-        s->h_base_disk[row] += at->disk_mb[i];
-        s->h_base_mbits[row] += at->net_mbits[i];
-        s->h_base_dyn[row] += at->dyn_ports[i];
+        pe::NodeRec& r = s->h_base_rec[row];
+        r.used_cpu += at->cpu_shares[i];
+        r.used_mem += at->memory_mb[i];
+        r.used_disk += at->disk_mb[i];
+        r.used_mbits += at->net_mbits[i];
+        r.used_dyn += at->dyn_ports[i];
     }
-    HIP_TRY(s, upload(s->d_cls, h_cls));
-    HIP_TRY(s, upload(s->d_cap_cpu, s->h_cap_cpu));
-    HIP_TRY(s, upload(s->d_cap_mem, s->h_cap_mem));
-    HIP_TRY(s, upload(s->d_cap_disk, s->h_cap_disk));
-    HIP_TRY(s, upload(s->d_avail_mbits, h_avail));
-    HIP_TRY(s, upload(s->d_used_cpu, s->h_base_cpu));
-    HIP_TRY(s, upload(s->d_used_mem, s->h_base_mem));
-    HIP_TRY(s, upload(s->d_used_disk, s->h_base_disk));
-    HIP_TRY(s, upload(s->d_used_mbits, s->h_base_mbits));
-    HIP_TRY(s, upload(s->d_used_dyn, s->h_base_dyn));
+    HIP_TRY(s, upload(s->d_base_rec, s->h_base_rec));
+    HIP_TRY(s, upload(s->d_rec, s->h_base_rec));
     std::vector<uint32_t> zeros(n, 0);
     HIP_TRY(s, upload(s->d_coll_job, zeros));
     return PE_OK;
@@ -524,16 +514,7 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
 pe::NodeSoA soa_of(pe_stack* s) {
     pe::NodeSoA a;
     a.n = (uint32_t)s->nodes.size();
-    a.cls = s->d_cls.as<uint32_t>();
-    a.cap_cpu = s->d_cap_cpu.as<int64_t>();
-    a.cap_mem = s->d_cap_mem.as<int64_t>();
-    a.cap_disk = s->d_cap_disk.as<int64_t>();
-    a.avail_mbits = s->d_avail_mbits.as<int32_t>();
-    a.used_cpu = s->d_used_cpu.as<int64_t>();
-    a.used_mem = s->d_used_mem.as<int64_t>();
-    a.used_disk = s->d_used_disk.as<int64_t>();
-    a.used_mbits = s->d_used_mbits.as<int32_t>();
-    a.used_dyn = s->d_used_dyn.as<int32_t>();
+    a.rec = s->d_rec.as<pe::NodeRec>();
     a.coll_job = s->d_coll_job.as<uint32_t>();
     return a;
 }
@@ -731,6 +712,15 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
     HIP_TRY(s, upload(g.class_ok, class_ok));
     g.node_ok_used = !node_ok.empty();
     if (g.node_ok_used) HIP_TRY(s, upload(g.node_ok, node_ok));
+    {
+        // fold the class verdict into one byte per node (single round trip per node)
+        pe::NodeSoA soa = soa_of(s);
+        HIP_TRY(s, g.node_feas.ensure(std::max<size_t>(n, 1)));
+        HIP_TRY(s, pe_launch_fold_feas(&soa, g.class_ok.as<uint8_t>(),
+                                       g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr,
+                                       g.node_feas.as<uint8_t>(), s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+    }
 
     // NodeAffinityIterator score per class (rank.go:698-725)
     g.has_aff_table = !g.affinities.empty();
@@ -780,6 +770,7 @@ pe::TgTables tables_of(TgPlan& g) {
     std::memset(&t, 0, sizeof(t));
     t.class_ok = g.class_ok.as<uint8_t>();
     t.node_ok = g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr;
+    t.node_feas = g.node_feas.as<uint8_t>();
     t.class_aff = (g.has_aff_table && !g.node_aff_used) ? g.class_aff.as<double>() : nullptr;
     t.node_aff = g.node_aff_used ? g.node_aff.as<double>() : nullptr;
     t.alias_ok = g.alias_used ? g.alias_ok.as<uint8_t>() : nullptr;
@@ -1002,11 +993,8 @@ int pe_reset_plan(pe_stack* s) {
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     HIP_TRY(s, hipSetDevice(s->device));
     const size_t n = s->nodes.size();
-    HIP_TRY(s, hipMemcpyAsync(s->d_used_cpu.p, s->h_base_cpu.data(), n * 8, hipMemcpyHostToDevice, s->stream));
-    HIP_TRY(s, hipMemcpyAsync(s->d_used_mem.p, s->h_base_mem.data(), n * 8, hipMemcpyHostToDevice, s->stream));
-    HIP_TRY(s, hipMemcpyAsync(s->d_used_disk.p, s->h_base_disk.data(), n * 8, hipMemcpyHostToDevice, s->stream));
-    HIP_TRY(s, hipMemcpyAsync(s->d_used_mbits.p, s->h_base_mbits.data(), n * 4, hipMemcpyHostToDevice, s->stream));
-    HIP_TRY(s, hipMemcpyAsync(s->d_used_dyn.p, s->h_base_dyn.data(), n * 4, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(s->d_rec.p, s->d_base_rec.p, n * sizeof(pe::NodeRec), hipMemcpyDeviceToDevice,
+                              s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     s->plan.clear();
     s->tg_memo.clear();
@@ -1304,6 +1292,7 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
         }
         HIP_TRY(s, upload(g.class_ok_batch, tabs));
         A.tg.class_ok = g.class_ok_batch.as<uint8_t>();
+        A.tg.node_feas = nullptr;
         A.class_ok_stride = s->ncls;
     }
     A.perms = s->d_orders.as<uint32_t>();

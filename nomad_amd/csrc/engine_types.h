@@ -13,28 +13,31 @@ constexpr int32_t kDynPortCapacity = 32000 - 20000 + 1;   // IndexesInRange is i
 constexpr int kMaxSkip = 3;           // stack.go:17 maxSkip
 constexpr int kPlaceBlock = 256;      // threads of the persistent count-loop workgroup
 
-// Node SoA in HBM, row order of the State snapshot. Static columns are written
-// at pe_set_state; dynamic columns are the proposed state (existing allocs +
-// plan placements) and are updated by every commit.
+// One node of the snapshot in HBM: a 64-byte record (one cache line, four
+// 16-byte loads per lane) holding everything BinPack needs. Capacities are
+// static (pe_set_state); the used_* fields and coll_job are the proposed state
+// (existing allocs + plan placements) and change with every commit.
+struct alignas(16) NodeRec {
+    int64_t cap_cpu, cap_mem, cap_disk;      // NodeResources - ReservedResources (AllocsFit "available")
+    int64_t used_cpu, used_mem, used_disk;   // Σ proposed non-terminal allocs
+    uint32_t cls;                            // dense ComputedClass index
+    int32_t avail_mbits;                     // bandwidth of the first host device network (-1: none)
+    int32_t used_mbits;                      // bandwidth held on the host device
+    int32_t used_dyn;                        // ports held in the dynamic range (incl. node-reserved)
+};
+static_assert(sizeof(NodeRec) == 64, "NodeRec must be one 64-byte line");
+
 struct NodeSoA {
     uint32_t n;
-    const uint32_t* cls;         // dense ComputedClass index
-    const int64_t* cap_cpu;      // NodeResources - ReservedResources (AllocsFit "available")
-    const int64_t* cap_mem;
-    const int64_t* cap_disk;
-    const int32_t* avail_mbits;  // bandwidth of the first host device network (-1: none)
-    int64_t* used_cpu;           // Σ proposed non-terminal allocs
-    int64_t* used_mem;
-    int64_t* used_disk;
-    int32_t* used_mbits;
-    int32_t* used_dyn;           // ports held in the dynamic range (incl. node-reserved)
-    uint32_t* coll_job;          // proposed allocs of the job per node
+    NodeRec* rec;                // [n], row order of the snapshot (job independent)
+    uint32_t* coll_job;          // [n] proposed allocs of the job (distinct_hosts only)
 };
 
 // Per (job, task group) feasibility / affinity / spread tables for a Select.
 struct TgTables {
     const uint8_t* class_ok;     // [ncls] memoised job+tg feasibility per class
     const uint8_t* node_ok;      // [n] or null: per-node verdict (escaped constraints)
+    const uint8_t* node_feas;    // [n] or null: class_ok[cls] & node_ok folded per node
     const double* class_aff;     // [ncls] or null: normalised node-affinity score (0 = not appended)
     const double* node_aff;      // [n] or null
     const uint8_t* alias_ok;     // [n] or null: node has an address for the tg's port network

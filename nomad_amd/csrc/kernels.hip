@@ -35,15 +35,11 @@ struct NodeEval {
     double parts[PE_MAX_SCORES];
 };
 
-// Per-eval LDS overlay of placed allocs (empty => null arrays, no deltas).
+// Per-eval LDS overlay of the allocs this eval placed: row -> k placements.
+// Every placement of the count loop has the same ask, so the deltas are k * ask.
 struct Overlay {
-    uint32_t* keys;
-    int32_t* d_cpu;
-    int32_t* d_mem;
-    int32_t* d_disk;
-    uint32_t* d_coll;
-    int32_t* d_mbits;    // null when the task group asks no network
-    int32_t* d_dyn;
+    uint32_t* keys;      // null: no overlay
+    uint32_t* k;
     uint32_t mask;
     int bits;
 };
@@ -52,28 +48,23 @@ __device__ __forceinline__ uint32_t ov_hash(const Overlay& o, uint32_t row) {
     return (row * 2654435761u) >> (32 - o.bits);
 }
 
-__device__ __forceinline__ int ov_find(const Overlay& o, uint32_t row) {
-    if (!o.keys) return -1;
+__device__ __forceinline__ uint32_t ov_count(const Overlay& o, uint32_t row) {
+    if (!o.keys) return 0;
     uint32_t h = ov_hash(o, row);
     for (;;) {
-        const uint32_t k = o.keys[h];
-        if (k == row) return (int)h;
-        if (k == kEmpty) return -1;
+        const uint32_t key = o.keys[h];
+        if (key == row) return o.k[h];
+        if (key == kEmpty) return 0;
         h = (h + 1) & o.mask;
     }
 }
 
-__device__ __forceinline__ int ov_claim(const Overlay& o, uint32_t row) {
+__device__ __forceinline__ void ov_add(const Overlay& o, uint32_t row) {
     uint32_t h = ov_hash(o, row);
     for (;;) {
-        const uint32_t k = o.keys[h];
-        if (k == row) return (int)h;
-        if (k == kEmpty) {
-            o.keys[h] = row;
-            o.d_cpu[h] = 0; o.d_mem[h] = 0; o.d_disk[h] = 0; o.d_coll[h] = 0;
-            if (o.d_mbits) { o.d_mbits[h] = 0; o.d_dyn[h] = 0; }
-            return (int)h;
-        }
+        const uint32_t key = o.keys[h];
+        if (key == row) { o.k[h] += 1; return; }
+        if (key == kEmpty) { o.keys[h] = row; o.k[h] = 1; return; }
         h = (h + 1) & o.mask;
     }
 }
@@ -88,45 +79,49 @@ __device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, c
                                           const Ask& a, const Overlay& ov, const uint32_t* penalty_bits,
                                           double log10, const double* spread_tab, uint32_t row,
                                           NodeEval* out) {
-    const uint32_t c = s.cls[row];
+    // one 64-byte record per node: issued together with the per-node verdict
+    const NodeRec r = s.rec[row];
+    const uint32_t c = r.cls;
     // FeasibilityWrapper: memoised job + task-group checks (host-resolved per class)
-    bool ok = class_ok[c] != 0;
-    if (t.node_ok) ok = ok && t.node_ok[row] != 0;
-    const int slot = ov_find(ov, row);
-    const uint32_t d_coll = slot >= 0 ? ov.d_coll[slot] : 0u;
+    bool ok;
+    if (t.node_feas) ok = t.node_feas[row] != 0;
+    else {
+        ok = class_ok[c] != 0;
+        if (t.node_ok) ok = ok && t.node_ok[row] != 0;
+    }
+    const uint32_t dk = ov_count(ov, row);   // placements of this eval on the node
+    const uint32_t coll = t.coll_tg[row] + dk;
     // DistinctHostsIterator (feasible.go:569-595)
     if (ok && (a.distinct_job | a.distinct_tg)) {
-        if (a.distinct_job && s.coll_job[row] + d_coll > 0) ok = false;
-        if (a.distinct_tg && t.coll_tg[row] + d_coll > 0) ok = false;
+        if (a.distinct_job && s.coll_job[row] + dk > 0) ok = false;
+        if (a.distinct_tg && coll > 0) ok = false;
     }
     if (!ok) { out->status = kFiltered; return; }
     // BinPackIterator (rank.go:193-527): network offers, then AllocsFit
     if (a.tg_dyn > 0 || a.has_task_net) {
-        int32_t dyn = s.used_dyn[row] + (slot >= 0 && ov.d_dyn ? ov.d_dyn[slot] : 0);
+        int32_t dyn = r.used_dyn + (int32_t)dk * a.commit_dyn;
         if (a.tg_dyn > 0) {
             if ((t.alias_ok && !t.alias_ok[row]) || kDynPortCapacity - dyn < 1) { out->status = kExhausted; return; }
             dyn += a.tg_dyn;
         }
         if (a.has_task_net) {
-            const int32_t avail = s.avail_mbits[row];
-            const int32_t mb = s.used_mbits[row] + (slot >= 0 && ov.d_mbits ? ov.d_mbits[slot] : 0);
+            const int32_t avail = r.avail_mbits;
+            const int32_t mb = r.used_mbits + (int32_t)dk * a.commit_mbits;
             if (avail < 0 || mb + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) {
                 out->status = kExhausted; return;
             }
         }
     }
-    int64_t ucpu = s.used_cpu[row] + a.cpu;
-    int64_t umem = s.used_mem[row] + a.mem;
-    int64_t udisk = s.used_disk[row] + a.disk;
-    if (slot >= 0) { ucpu += ov.d_cpu[slot]; umem += ov.d_mem[slot]; udisk += ov.d_disk[slot]; }
-    const int64_t ccpu = s.cap_cpu[row], cmem = s.cap_mem[row];
-    if (ccpu < ucpu || cmem < umem || s.cap_disk[row] < udisk) { out->status = kExhausted; return; }
+    const int64_t ucpu = r.used_cpu + (int64_t)(dk + 1) * a.cpu;
+    const int64_t umem = r.used_mem + (int64_t)(dk + 1) * a.mem;
+    const int64_t udisk = r.used_disk + (int64_t)(dk + 1) * a.disk;
+    const int64_t ccpu = r.cap_cpu, cmem = r.cap_mem;
+    if (ccpu < ucpu || cmem < umem || r.cap_disk < udisk) { out->status = kExhausted; return; }
     // Scores in append order, summed left to right.
     const double fit = gm::fit_score(ccpu, cmem, ucpu, umem, a.algo_spread, log10);
     double sum = fit;
     uint32_t k = 1;
     if (kKeepParts) out->parts[0] = fit;
-    const uint32_t coll = t.coll_tg[row] + d_coll;
     if (a.anti_aff && coll > 0) {   // JobAntiAffinityIterator (rank.go:588-591)
         const double pen = -1 * (double)(coll + 1) / (double)a.desired_count;
         sum += pen;
@@ -299,16 +294,11 @@ __device__ __forceinline__ void block_argmax(bool cand, double score, int pos, d
 }
 
 // Plan.AppendAlloc into the overlay (one lane).
-__device__ __forceinline__ void commit_overlay(const NodeSoA& s, const TgTables& t, const Ask& a,
-                                               const Overlay& ov, uint32_t* counts, uint32_t row) {
-    const int h = ov_claim(ov, row);
-    ov.d_cpu[h] += (int32_t)a.cpu;
-    ov.d_mem[h] += (int32_t)a.mem;
-    ov.d_disk[h] += (int32_t)a.disk;
-    ov.d_coll[h] += 1;
-    if (ov.d_mbits) { ov.d_mbits[h] += a.commit_mbits; ov.d_dyn[h] += a.commit_dyn; }
+__device__ __forceinline__ void commit_overlay(const NodeSoA& s, const TgTables& t, const Overlay& ov,
+                                               uint32_t* counts, uint32_t row) {
+    ov_add(ov, row);
     if (t.n_psets > 0) {
-        const uint32_t c = s.cls[row];
+        const uint32_t c = s.rec[row].cls;
         for (int p = 0; p < t.n_psets; p++) {
             const uint32_t v = pset_value(t, p, row, c);
             if (v != kMissing) counts[p * kMaxValues + v] += 1;
@@ -341,16 +331,7 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
     ov.bits = A.hash_bits;
     ov.mask = H - 1;
     ov.keys = reinterpret_cast<uint32_t*>(p); p += 4 * H;
-    ov.d_cpu = reinterpret_cast<int32_t*>(p); p += 4 * H;
-    ov.d_mem = reinterpret_cast<int32_t*>(p); p += 4 * H;
-    ov.d_disk = reinterpret_cast<int32_t*>(p); p += 4 * H;
-    ov.d_coll = reinterpret_cast<uint32_t*>(p); p += 4 * H;
-    ov.d_mbits = nullptr;
-    ov.d_dyn = nullptr;
-    if (A.net_overlay) {
-        ov.d_mbits = reinterpret_cast<int32_t*>(p); p += 4 * H;
-        ov.d_dyn = reinterpret_cast<int32_t*>(p); p += 4 * H;
-    }
+    ov.k = reinterpret_cast<uint32_t*>(p); p += 4 * H;
     for (uint32_t i = tid; i < H; i += BLOCK) ov.keys[i] = kEmpty;
     if constexpr (FULL) {
         for (int q = 0; q < A.tg.n_psets; q++)
@@ -473,7 +454,7 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
                 o.nodes_evaluated = consumed;
                 o.final_score = win_row >= 0 ? best_score : 0.0;
             }
-            if (win_row >= 0 && A.commit) commit_overlay(A.soa, A.tg, A.ask, ov, counts, (uint32_t)win_row);
+            if (win_row >= 0 && A.commit) commit_overlay(A.soa, A.tg, ov, counts, (uint32_t)win_row);
         }
         offset = no;
         __syncthreads();
@@ -489,12 +470,15 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
         for (uint32_t h = tid; h < H; h += BLOCK) {
             const uint32_t row = ov.keys[h];
             if (row == kEmpty) continue;
-            A.soa.used_cpu[row] += ov.d_cpu[h];
-            A.soa.used_mem[row] += ov.d_mem[h];
-            A.soa.used_disk[row] += ov.d_disk[h];
-            A.soa.coll_job[row] += ov.d_coll[h];
-            A.tg.coll_tg[row] += ov.d_coll[h];
-            if (ov.d_mbits) { A.soa.used_mbits[row] += ov.d_mbits[h]; A.soa.used_dyn[row] += ov.d_dyn[h]; }
+            const uint32_t k = ov.k[h];
+            NodeRec& r = A.soa.rec[row];
+            r.used_cpu += (int64_t)k * A.ask.cpu;
+            r.used_mem += (int64_t)k * A.ask.mem;
+            r.used_disk += (int64_t)k * A.ask.disk;
+            r.used_mbits += (int32_t)k * A.ask.commit_mbits;
+            r.used_dyn += (int32_t)k * A.ask.commit_dyn;
+            A.soa.coll_job[row] += k;
+            A.tg.coll_tg[row] += k;
         }
         if constexpr (FULL) {
             for (int q = 0; q < A.tg.n_psets; q++)
@@ -517,11 +501,12 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
             A.out_score[i] = ev.score;
             A.out_status[i] = 0;
             // Plan.AppendAlloc: rows are unique in the list, so no races
-            A.soa.used_cpu[row] += A.ask.cpu;
-            A.soa.used_mem[row] += A.ask.mem;
-            A.soa.used_disk[row] += A.ask.disk;
-            A.soa.used_mbits[row] += A.ask.commit_mbits;
-            A.soa.used_dyn[row] += A.ask.commit_dyn;
+            NodeRec& r = A.soa.rec[row];
+            r.used_cpu += A.ask.cpu;
+            r.used_mem += A.ask.mem;
+            r.used_disk += A.ask.disk;
+            r.used_mbits += A.ask.commit_mbits;
+            r.used_dyn += A.ask.commit_dyn;
             A.soa.coll_job[row] += 1;
             A.tg.coll_tg[row] += 1;
             local++;
@@ -537,17 +522,29 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
 // Host-driven Plan.AppendAlloc on the HBM SoA (pe_commit).
 __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    s.used_cpu[row] += a.cpu;
-    s.used_mem[row] += a.mem;
-    s.used_disk[row] += a.disk;
-    s.used_mbits[row] += a.commit_mbits;
-    s.used_dyn[row] += a.commit_dyn;
+    NodeRec& r = s.rec[row];
+    r.used_cpu += a.cpu;
+    r.used_mem += a.mem;
+    r.used_disk += a.disk;
+    r.used_mbits += a.commit_mbits;
+    r.used_dyn += a.commit_dyn;
     s.coll_job[row] += 1;
     t.coll_tg[row] += 1;
-    const uint32_t c = s.cls[row];
+    const uint32_t c = r.cls;
     for (int p = 0; p < t.n_psets; p++) {
         const uint32_t v = pset_value(t, p, row, c);
         if (v != kMissing) t.pset_counts[p][v] += 1;
+    }
+}
+
+// node_feas[row] = class_ok[cls] && node_ok[row]: one verdict byte per node so
+// the count loop issues a single dependent round trip per node.
+__global__ void __launch_bounds__(256) k_fold_feas(NodeSoA s, const uint8_t* class_ok, const uint8_t* node_ok,
+                                                   uint8_t* feas) {
+    for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < s.n; row += gridDim.x * blockDim.x) {
+        bool ok = class_ok[s.rec[row].cls] != 0;
+        if (node_ok) ok = ok && node_ok[row] != 0;
+        feas[row] = ok ? 1 : 0;
     }
 }
 
@@ -555,7 +552,8 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row) {
 
 // ---- launch wrappers (host) ------------------------------------------------
 size_t pe_place_lds_bytes(bool full, int hash_bits, bool net) {
-    size_t b = (size_t)(net ? 7 : 5) * 4u * ((size_t)1 << hash_bits);
+    (void)net;
+    size_t b = (size_t)2 * 4u * ((size_t)1 << hash_bits);
     if (full) b += sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1) + 4u * pe::kMaxPsets * pe::kMaxValues;
     return b;
 }
@@ -581,5 +579,14 @@ hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st) {
 hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
                             hipStream_t st) {
     hipLaunchKernelGGL(pe::k_commit, dim3(1), dim3(64), 0, st, *s, *t, *a, row);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
+                               hipStream_t st) {
+    uint32_t blocks = (s->n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_fold_feas, dim3(blocks), dim3(256), 0, st, *s, class_ok, node_ok, feas);
     return hipGetLastError();
 }

@@ -161,8 +161,11 @@ class _Stack:
 
     def SetNodes(self, nodes_in_visit_order) -> int:
         """`nodes_in_visit_order`: Node objects / IDs / rows, already shuffled."""
-        rows = np.asarray([x if isinstance(x, (int, np.integer)) else self.row(x)
-                           for x in nodes_in_visit_order], dtype=np.uint32)
+        if isinstance(nodes_in_visit_order, np.ndarray) and nodes_in_visit_order.dtype.kind in "iu":
+            rows = np.ascontiguousarray(nodes_in_visit_order, dtype=np.uint32)
+        else:
+            rows = np.asarray([x if isinstance(x, (int, np.integer)) else self.row(x)
+                               for x in nodes_in_visit_order], dtype=np.uint32)
         self._visit = rows
         lim = C.c_uint32(0)
         self._check(self._fn("set_nodes")(self._h, rows.ctypes.data_as(abi.u32p), len(rows), C.byref(lim)))
