@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--evals", type=int, default=1024, help="concurrent evaluations per step")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--sweep-nodes", type=int, default=1 << 24,
+                   help="nodes of the scoring-sweep roofline measurement (0 = skip)")
     return p.parse_args()
 
 
@@ -110,6 +112,43 @@ def cpu_baseline(nodes, allocs, job, seconds):
     multi = {"value": tot / wall, "unit": "placements/s", "cores": threads, "kind": "port",
              "sample": "%d threads x independent evals for %.1f s (box CPU share)" % (threads, wall)}
     return one, multi
+
+
+SWEEP_BYTES_PER_NODE = 73   # 64 B NodeRec + 1 B folded verdict + 4 B (job,tg) collisions + 4 B visit rank
+
+
+def sweep_roofline(n, device, selects=6):
+    """Scoring-sweep roofline: full-scan Selects (C3-like job: constraints,
+    affinity, spread => limit MaxInt32) over an n-node columnar cluster in HBM.
+    One Select = spread-table kernel + k_sweep over all rows + record merge."""
+    from nomad_amd import synth, synth_columnar
+    from nomad_amd.stack import GenericStack
+    t0 = time.perf_counter()
+    cs = synth_columnar.ColumnarState(n, seed=7, kind="c3")
+    st = GenericStack(device=device)
+    st.SetStateColumnar(cs)
+    st.SetJob(synth.job_c3(1000))
+    perm = np.random.Generator(np.random.PCG64(3)).permutation(n).astype(np.uint32)
+    st.SetNodes(perm)
+    setup_s = time.perf_counter() - t0
+    times = []
+    row = None
+    for i in range(selects):
+        t1 = time.perf_counter()
+        r = st.SelectRaw(0)
+        wall = time.perf_counter() - t1
+        if i >= 1:
+            times.append((st.last_kernel_ms(), wall))
+        row = r.row
+    kernel_ms = float(np.median([t[0] for t in times]))
+    wall_ms = float(np.median([t[1] for t in times])) * 1000.0
+    achieved = n * SWEEP_BYTES_PER_NODE / (kernel_ms / 1000.0) / 1e9
+    st.close()
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_sweep<256> + k_sweep_merge",
+            "nodes": n, "bytes_per_node_eval": SWEEP_BYTES_PER_NODE, "kernel_ms": kernel_ms,
+            "select_wall_ms": wall_ms, "nodes_scored_per_s": n / (kernel_ms / 1000.0),
+            "winner_row": row, "setup_s": setup_s}
 
 
 def main():
@@ -196,6 +235,8 @@ def main():
                          "node_evals_per_launch": evals_per_launch,
                          "bytes_per_node_eval": BYTES_PER_NODE_EVAL},
         }
+        if args.sweep_nodes > 0:
+            line["sweep_roofline"] = sweep_roofline(args.sweep_nodes, local)
         if not args.no_cpu:
             one, multi = cpu_baseline(nodes, allocs, job, args.cpu_seconds)
             line["cpu_baseline"] = one

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <set>
@@ -37,6 +38,10 @@ hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const p
                             hipStream_t st);
 hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
                                hipStream_t st);
+hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec* merged, hipStream_t st);
+hipError_t pe_launch_node_record(const pe::SweepArgs* a, uint32_t row, pe_ranked_node* out, hipStream_t st);
+hipError_t pe_launch_spread_table(const pe::TgTables* t, double* tab, hipStream_t st);
+uint32_t pe_rec_winner(const pe::SweepRec* r);
 
 namespace {
 
@@ -66,18 +71,36 @@ struct DevMem {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Fixed per-node fields; the variable-length maps live in stack-owned CSR
+// arrays (sorted per node) and are reached through NodeView.
 struct HostNode {
     uint32_t id, name, dc, node_class, cclass;
     uint32_t cls;
     uint32_t sig;          // (class, drivers, networks, aliases, volumes, devices) signature
-    std::vector<std::pair<uint32_t, uint32_t>> attrs, meta;   // sorted by key id
-    std::vector<std::pair<uint32_t, uint8_t>> drivers;        // sorted by name id
-    std::vector<uint32_t> net_modes;
-    int n_device_nets;
     int32_t first_mbits;
-    std::vector<uint32_t> aliases;
-    std::vector<std::pair<uint32_t, uint8_t>> volumes;        // sorted by name id
-    int n_devices;
+    uint16_t n_device_nets, n_devices;
+};
+
+template <class T>
+struct Span {
+    const T* p = nullptr;
+    uint32_t n = 0;
+    const T* begin() const { return p; }
+    const T* end() const { return p + n; }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+};
+
+using KV = std::pair<uint32_t, uint32_t>;
+using KF = std::pair<uint32_t, uint8_t>;
+
+struct NodeView {
+    const HostNode* h;
+    uint32_t row;
+    Span<KV> attrs, meta;          // sorted by key id
+    Span<KF> drivers, volumes;     // sorted by name id
+    Span<uint32_t> net_modes, aliases;
+    uint32_t id() const { return h->id; }
 };
 
 struct HostAlloc {
@@ -164,6 +187,10 @@ struct pe_stack {
 
     // state
     std::vector<HostNode> nodes;
+    std::vector<uint32_t> attr_off, meta_off, drv_off, net_off, alias_off, hv_off;
+    std::vector<KV> attr_kv, meta_kv;
+    std::vector<KF> drv_kf, hv_kf;
+    std::vector<uint32_t> net_mode_ids, alias_ids;
     std::vector<HostAlloc> allocs;
     uint32_t ncls = 0;
     std::vector<uint32_t> class_rep;   // first row of each class
@@ -173,7 +200,12 @@ struct pe_stack {
     std::vector<uint32_t> sig_rep, sig_cls;
     std::vector<std::vector<uint32_t>> class_sigs;
     // staged visit orders for pe_place_batch
-    DevMem d_orders;
+    DevMem d_orders, d_batch_out, d_batch_status, d_sys_score, d_sys_status;
+    // full-scan sweep path
+    DevMem d_rank_of, d_sweep_recs, d_sweep_merged, d_spread_tab, d_record;
+    uint32_t sweep_min = 1u << 15;     // visit lists at least this long use the multi-CU sweep
+    bool visit_unique = true;
+    double last_sweep_ms = 0;
     std::vector<uint32_t> h_orders;
     uint32_t staged_evals = 0, staged_n = 0;
     std::vector<pe::NodeRec> h_base_rec;     // snapshot proposed state (no plan)
@@ -212,6 +244,18 @@ struct pe_stack {
     const std::string& S(uint32_t id) const {
         static const std::string empty;
         return id < strs.size() ? strs[id] : empty;
+    }
+    NodeView view(uint32_t row) const {
+        NodeView v;
+        v.h = &nodes[row];
+        v.row = row;
+        v.attrs = {attr_kv.data() + attr_off[row], attr_off[row + 1] - attr_off[row]};
+        v.meta = {meta_kv.data() + meta_off[row], meta_off[row + 1] - meta_off[row]};
+        v.drivers = {drv_kf.data() + drv_off[row], drv_off[row + 1] - drv_off[row]};
+        v.volumes = {hv_kf.data() + hv_off[row], hv_off[row + 1] - hv_off[row]};
+        v.net_modes = {net_mode_ids.data() + net_off[row], net_off[row + 1] - net_off[row]};
+        v.aliases = {alias_ids.data() + alias_off[row], alias_off[row + 1] - alias_off[row]};
+        return v;
     }
     uint32_t lookup(const std::string& s) const {
         auto it = sid.find(s);
@@ -262,7 +306,7 @@ ParsedTarget parse_target(const pe_stack* s, const std::string& t) {
     return p;
 }
 
-bool find_kv(const std::vector<std::pair<uint32_t, uint32_t>>& v, uint32_t key, uint32_t* val) {
+bool find_kv(const Span<KV>& v, uint32_t key, uint32_t* val) {
     auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(key, 0u));
     if (it == v.end() || it->first != key) return false;
     *val = it->second;
@@ -271,16 +315,16 @@ bool find_kv(const std::vector<std::pair<uint32_t, uint32_t>>& v, uint32_t key, 
 
 // resolveTarget (feasible.go:748-781) on a host node; returns the value str id
 // in *vid when the value comes from the node (PE_NONE for literals / absent).
-Target resolve(const pe_stack* s, const ParsedTarget& p, const HostNode& n, uint32_t* vid = nullptr) {
+Target resolve(const pe_stack* s, const ParsedTarget& p, const NodeView& n, uint32_t* vid = nullptr) {
     Target t;
     t.nil = false;
     uint32_t v = PE_NONE;
     switch (p.kind) {
         case T_LITERAL: t.found = true; t.value = p.literal; break;
-        case T_ID: v = n.id; break;
-        case T_DC: v = n.dc; break;
-        case T_NAME: v = n.name; break;
-        case T_CLASS: v = n.node_class; break;
+        case T_ID: v = n.h->id; break;
+        case T_DC: v = n.h->dc; break;
+        case T_NAME: v = n.h->name; break;
+        case T_CLASS: v = n.h->node_class; break;
         case T_ATTR:
         case T_META: {
             uint32_t x;
@@ -304,20 +348,20 @@ ParsedConstraint parse_constraint(const pe_stack* s, const pe_constraint& c) {
     return p;
 }
 
-bool meets(const pe_stack* s, pe::ConstraintEvaluator& ev, const ParsedConstraint& c, const HostNode& n) {
+bool meets(const pe_stack* s, pe::ConstraintEvaluator& ev, const ParsedConstraint& c, const NodeView& n) {
     Target l = resolve(s, c.l, n), r = resolve(s, c.r, n);
     return ev.check(c.op, l, r);
 }
 
 // job checkers (ConstraintChecker over job constraints)
-bool job_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const HostNode& n) {
+bool job_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const NodeView& n) {
     for (auto& c : s->job_constraints) if (!meets(s, ev, c, n)) return false;
     return true;
 }
 
 // tg checkers in GenericStack/SystemStack order: drivers, constraints, host
 // volumes, devices, network (stack.go:241-247, 374-380)
-bool tg_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g, const HostNode& n) {
+bool tg_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g, const NodeView& n) {
     for (uint32_t d : g.drivers) {   // DriverChecker.hasDrivers (feasible.go:462-500)
         auto it = std::lower_bound(n.drivers.begin(), n.drivers.end(), std::make_pair(d, (uint8_t)0));
         if (it != n.drivers.end() && it->first == d) {
@@ -419,6 +463,38 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     s->class_rep.clear();
     s->h_base_rec.assign(n, pe::NodeRec());
     std::memset(s->h_base_rec.data(), 0, sizeof(pe::NodeRec) * n);
+    // variable-length node maps: copied once into CSR arrays, sorted per node
+    auto copy_off = [&](std::vector<uint32_t>& dst, const uint32_t* off) {
+        dst.assign(n + 1, 0);
+        if (off) for (uint32_t i = 0; i <= n; i++) dst[i] = off[i] - off[0];
+    };
+    copy_off(s->attr_off, nt->attr_off);
+    copy_off(s->meta_off, nt->meta_off);
+    copy_off(s->drv_off, nt->drv_off);
+    copy_off(s->net_off, nt->net_off);
+    copy_off(s->alias_off, nt->alias_off);
+    copy_off(s->hv_off, nt->hv_off);
+    s->attr_kv.resize(s->attr_off[n]);
+    s->meta_kv.resize(s->meta_off[n]);
+    s->drv_kf.resize(s->drv_off[n]);
+    s->net_mode_ids.resize(s->net_off[n]);
+    s->alias_ids.resize(s->alias_off[n]);
+    s->hv_kf.resize(s->hv_off[n]);
+    const uint32_t a0 = nt->attr_off[0], m0 = nt->meta_off[0], d0 = nt->drv_off[0];
+    const uint32_t w0 = nt->net_off[0], l0 = nt->alias_off[0], v0 = nt->hv_off ? nt->hv_off[0] : 0;
+    for (size_t k = 0; k < s->attr_kv.size(); k++) s->attr_kv[k] = KV(nt->attr_key[a0 + k], nt->attr_val[a0 + k]);
+    for (size_t k = 0; k < s->meta_kv.size(); k++) s->meta_kv[k] = KV(nt->meta_key[m0 + k], nt->meta_val[m0 + k]);
+    for (size_t k = 0; k < s->drv_kf.size(); k++) s->drv_kf[k] = KF(nt->drv_name[d0 + k], nt->drv_flags[d0 + k]);
+    for (size_t k = 0; k < s->net_mode_ids.size(); k++) s->net_mode_ids[k] = nt->net_mode[w0 + k];
+    for (size_t k = 0; k < s->alias_ids.size(); k++) s->alias_ids[k] = nt->alias_name[l0 + k];
+    for (size_t k = 0; k < s->hv_kf.size(); k++) s->hv_kf[k] = KF(nt->hv_name[v0 + k], nt->hv_read_only[v0 + k]);
+    for (uint32_t i = 0; i < n; i++) {
+        std::sort(s->attr_kv.begin() + s->attr_off[i], s->attr_kv.begin() + s->attr_off[i + 1]);
+        std::sort(s->meta_kv.begin() + s->meta_off[i], s->meta_kv.begin() + s->meta_off[i + 1]);
+        std::sort(s->drv_kf.begin() + s->drv_off[i], s->drv_kf.begin() + s->drv_off[i + 1]);
+        std::sort(s->alias_ids.begin() + s->alias_off[i], s->alias_ids.begin() + s->alias_off[i + 1]);
+        std::sort(s->hv_kf.begin() + s->hv_off[i], s->hv_kf.begin() + s->hv_off[i + 1]);
+    }
     for (uint32_t i = 0; i < n; i++) {
         HostNode& h = s->nodes[i];
         h.id = nt->id[i]; h.name = nt->name[i]; h.dc = nt->datacenter[i];
@@ -430,26 +506,15 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
         }
         h.cls = it->second;
         s->h_base_rec[i].cls = h.cls;
-        for (uint32_t k = nt->attr_off[i]; k < nt->attr_off[i + 1]; k++) h.attrs.emplace_back(nt->attr_key[k], nt->attr_val[k]);
-        for (uint32_t k = nt->meta_off[i]; k < nt->meta_off[i + 1]; k++) h.meta.emplace_back(nt->meta_key[k], nt->meta_val[k]);
-        std::sort(h.attrs.begin(), h.attrs.end());
-        std::sort(h.meta.begin(), h.meta.end());
-        for (uint32_t k = nt->drv_off[i]; k < nt->drv_off[i + 1]; k++) h.drivers.emplace_back(nt->drv_name[k], nt->drv_flags[k]);
-        std::sort(h.drivers.begin(), h.drivers.end());
         h.n_device_nets = 0;
         h.first_mbits = -1;
         for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++) {
-            h.net_modes.push_back(nt->net_mode[k]);
             if (!s->S(nt->net_device[k]).empty()) {
                 if (h.n_device_nets == 0) h.first_mbits = nt->net_mbits[k];
                 h.n_device_nets++;
             }
         }
-        for (uint32_t k = nt->alias_off[i]; k < nt->alias_off[i + 1]; k++) h.aliases.push_back(nt->alias_name[k]);
-        if (nt->hv_off)
-            for (uint32_t k = nt->hv_off[i]; k < nt->hv_off[i + 1]; k++) h.volumes.emplace_back(nt->hv_name[k], nt->hv_read_only[k]);
-        std::sort(h.volumes.begin(), h.volumes.end());
-        h.n_devices = nt->dev_off ? (int)(nt->dev_off[i + 1] - nt->dev_off[i]) : 0;
+        h.n_devices = nt->dev_off ? (uint16_t)(nt->dev_off[i + 1] - nt->dev_off[i]) : 0;
         pe::NodeRec& r = s->h_base_rec[i];
         r.cap_cpu = nt->cpu_shares[i] - nt->reserved_cpu[i];
         r.cap_mem = nt->memory_mb[i] - nt->reserved_memory_mb[i];
@@ -460,34 +525,45 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     s->ncls = (uint32_t)s->class_rep.size();
     // checker-input signatures
     {
-        std::map<std::vector<uint32_t>, uint32_t> sig_of;
+        // 64-bit hash of the checker inputs; equal hashes are verified exactly
+        // against the signature's representative before being merged.
+        std::unordered_map<uint64_t, std::vector<uint32_t>> sig_of;
         s->sig_rep.clear();
         s->sig_cls.clear();
         s->class_sigs.assign(s->ncls, {});
-        std::vector<uint32_t> key;
+        auto same_inputs = [&](uint32_t a_row, uint32_t b_row) {
+            const NodeView x = s->view(a_row), y = s->view(b_row);
+            auto eq = [](auto u, auto v) { return u.size() == v.size() && std::equal(u.begin(), u.end(), v.begin()); };
+            return x.h->cls == y.h->cls && x.h->n_devices == y.h->n_devices && eq(x.drivers, y.drivers) &&
+                   eq(x.net_modes, y.net_modes) && eq(x.aliases, y.aliases) && eq(x.volumes, y.volumes);
+        };
         for (uint32_t i = 0; i < n; i++) {
             HostNode& h = s->nodes[i];
-            key.clear();
-            key.push_back(h.cls);
-            key.push_back((uint32_t)h.drivers.size());
-            for (auto& d : h.drivers) { key.push_back(d.first); key.push_back(d.second); }
-            key.push_back((uint32_t)h.net_modes.size());
-            for (uint32_t m : h.net_modes) key.push_back(m);
-            std::vector<uint32_t> al = h.aliases;
-            std::sort(al.begin(), al.end());
-            key.push_back((uint32_t)al.size());
-            key.insert(key.end(), al.begin(), al.end());
-            key.push_back((uint32_t)h.volumes.size());
-            for (auto& v : h.volumes) { key.push_back(v.first); key.push_back(v.second); }
-            key.push_back((uint32_t)h.n_devices);
-            auto it = sig_of.find(key);
-            if (it == sig_of.end()) {
-                it = sig_of.emplace(key, (uint32_t)s->sig_rep.size()).first;
+            const NodeView v = s->view(i);
+            uint64_t x = 1469598103934665603ull;
+            auto mix = [&](uint64_t y) { x = (x ^ y) * 1099511628211ull; x ^= x >> 29; };
+            mix(h.cls);
+            mix(h.n_devices);
+            mix(v.drivers.size());
+            for (auto& d : v.drivers) { mix(d.first); mix(d.second); }
+            mix(v.net_modes.size());
+            for (uint32_t m : v.net_modes) mix(m);
+            mix(v.aliases.size());
+            for (uint32_t al : v.aliases) mix(al);
+            mix(v.volumes.size());
+            for (auto& vv : v.volumes) { mix(vv.first); mix(vv.second); }
+            auto& bucket = sig_of[x];
+            uint32_t found = PE_NONE;
+            for (uint32_t sg : bucket)
+                if (same_inputs(s->sig_rep[sg], i)) { found = sg; break; }
+            if (found == PE_NONE) {
+                found = (uint32_t)s->sig_rep.size();
+                bucket.push_back(found);
                 s->sig_rep.push_back(i);
                 s->sig_cls.push_back(h.cls);
-                s->class_sigs[h.cls].push_back(it->second);
+                s->class_sigs[h.cls].push_back(found);
             }
-            h.sig = it->second;
+            h.sig = found;
         }
     }
     s->allocs.clear();
@@ -557,7 +633,7 @@ int build_psets(pe_stack* s, TgPlan& g) {
         auto ps = std::make_unique<PsetDev>();
         ps->target = parse_target(s, s->S(sp->attribute));
         ps->per_node = ps->target.escapes || ps->target.kind == T_ID || ps->target.kind == T_NAME;
-        auto value_of = [&](const HostNode& nd) -> uint32_t {
+        auto value_of = [&](const NodeView& nd) -> uint32_t {
             uint32_t vid;
             Target t = resolve(s, ps->target, nd, &vid);
             if (!t.found || t.nil) return pe::kMissing;
@@ -572,9 +648,9 @@ int build_psets(pe_stack* s, TgPlan& g) {
         std::vector<uint32_t> by_class(s->ncls, pe::kMissing), by_node;
         if (ps->per_node) {
             by_node.resize(n);
-            for (size_t i = 0; i < n; i++) by_node[i] = value_of(s->nodes[i]);
+            for (size_t i = 0; i < n; i++) by_node[i] = value_of(s->view((uint32_t)i));
         } else {
-            for (uint32_t c = 0; c < s->ncls; c++) by_class[c] = value_of(s->nodes[s->class_rep[c]]);
+            for (uint32_t c = 0; c < s->ncls; c++) by_class[c] = value_of(s->view(s->class_rep[c]));
         }
         // existing allocs of this job and task group (populateExisting) + plan allocs
         auto node_val = [&](uint32_t row) {
@@ -635,7 +711,7 @@ void classify_classes(pe_stack* s, TgPlan& g, pe::ConstraintEvaluator& ev) {
     if (!g.sig_tg.empty()) return;
     g.sig_tg.assign(s->sig_rep.size(), 0);
     for (size_t sg = 0; sg < s->sig_rep.size(); sg++)
-        g.sig_tg[sg] = tg_feasible(s, ev, g, s->nodes[s->sig_rep[sg]]) ? 1 : 0;
+        g.sig_tg[sg] = tg_feasible(s, ev, g, s->view(s->sig_rep[sg])) ? 1 : 0;
     g.class_uniform.assign(s->ncls, 1);
     g.class_verdict.assign(s->ncls, 0);
     if (s->job_memo.size() != s->ncls) s->job_memo.assign(s->ncls, -1);
@@ -644,7 +720,7 @@ void classify_classes(pe_stack* s, TgPlan& g, pe::ConstraintEvaluator& ev) {
         g.class_verdict[c] = g.sig_tg[sigs[0]];
         for (uint32_t sg : sigs) if (g.sig_tg[sg] != g.class_verdict[c]) g.class_uniform[c] = 0;
         if (!s->job_escaped && s->job_memo[c] == -1)
-            s->job_memo[c] = job_feasible(s, ev, s->nodes[s->class_rep[c]]) ? 1 : 0;
+            s->job_memo[c] = job_feasible(s, ev, s->view(s->class_rep[c])) ? 1 : 0;
     }
     g.nonuniform.clear();
     for (uint32_t c = 0; c < s->ncls; c++) if (!g.class_uniform[c]) g.nonuniform.push_back(c);
@@ -695,12 +771,12 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         // no memo for the task group: every node runs every check
         node_ok.assign(n, 0);
         for (uint32_t row = 0; row < n; row++)
-            node_ok[row] = job_feasible(s, ev, s->nodes[row]) && tg_feasible(s, ev, g, s->nodes[row]);
+            node_ok[row] = job_feasible(s, ev, s->view(row)) && tg_feasible(s, ev, g, s->view(row));
         std::fill(class_ok.begin(), class_ok.end(), 1);
     } else {
         if (s->job_escaped) {
             g.job_ok_node.assign(n, 0);
-            for (uint32_t row = 0; row < n; row++) g.job_ok_node[row] = job_feasible(s, ev, s->nodes[row]);
+            for (uint32_t row = 0; row < n; row++) g.job_ok_node[row] = job_feasible(s, ev, s->view(row));
         } else {
             g.job_ok_node.clear();
         }
@@ -730,7 +806,7 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         for (auto& a : g.affinities)
             escapes = escapes || a.c.escapes || a.c.l.kind == T_ID || a.c.l.kind == T_NAME ||
                       a.c.r.kind == T_ID || a.c.r.kind == T_NAME;
-        auto score = [&](const HostNode& nd) {
+        auto score = [&](const NodeView& nd) {
             double sum_w = 0.0;
             for (auto& a : g.affinities) sum_w += std::fabs((double)a.weight);
             double total = 0.0;
@@ -740,12 +816,12 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         };
         if (escapes) {
             std::vector<double> na(n);
-            for (size_t i = 0; i < n; i++) na[i] = score(s->nodes[i]);
+            for (size_t i = 0; i < n; i++) na[i] = score(s->view((uint32_t)i));
             HIP_TRY(s, upload(g.node_aff, na));
             g.node_aff_used = true;
         } else {
             std::vector<double> ca(s->ncls);
-            for (uint32_t c = 0; c < s->ncls; c++) ca[c] = score(s->nodes[s->class_rep[c]]);
+            for (uint32_t c = 0; c < s->ncls; c++) ca[c] = score(s->view(s->class_rep[c]));
             HIP_TRY(s, upload(g.class_aff, ca));
         }
     }
@@ -755,7 +831,7 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         std::vector<uint8_t> al(n, 0);
         const uint32_t want = g.net_host;
         for (size_t i = 0; i < n; i++) {
-            const auto& a = s->nodes[i].aliases;
+            const auto a = s->view((uint32_t)i).aliases;
             al[i] = std::find(a.begin(), a.end(), want) != a.end();
         }
         HIP_TRY(s, upload(g.alias_ok, al));
@@ -849,6 +925,74 @@ bool full_scan_kernel(pe_stack* s, TgPlan& g, uint32_t n) {
     return !g.psets.empty() || s->limit >= n;
 }
 
+// Full-scan Select (limit >= n) as a multi-CU sweep: every workgroup reduces
+// its rows to a SweepRec, one merge yields the winner.
+int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_ranked_node* out) {
+    const uint32_t n = (uint32_t)s->visit.size();
+    pe::SweepArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.soa = soa_of(s);
+    A.tg = tables_of(g);
+    A.ask = ask_for(s, g);
+    A.rank_of = s->d_rank_of.as<uint32_t>();
+    A.n_visit = n;
+    A.offset = s->offset;
+    A.row_begin = 0;
+    A.row_end = (uint32_t)s->nodes.size();
+    A.log10 = s->log10;
+    if (opts && opts->penalty_count > 0) {
+        std::vector<uint32_t> bits((s->nodes.size() + 31) / 32, 0);
+        for (uint32_t i = 0; i < opts->penalty_count; i++) {
+            uint32_t r = opts->penalty_rows[i];
+            if (r < s->nodes.size()) bits[r >> 5] |= 1u << (r & 31);
+        }
+        HIP_TRY(s, upload(s->d_penalty, bits));
+        A.penalty_bits = s->d_penalty.as<uint32_t>();
+    }
+    if (!g.psets.empty()) {
+        HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
+        HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
+        A.spread_tab = s->d_spread_tab.as<double>();
+    }
+    uint32_t blocks = (A.row_end + 256 * 8 - 1) / (256 * 8);   // ~8 rows per thread
+    blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 8192));
+    HIP_TRY(s, s->d_sweep_recs.ensure(sizeof(pe::SweepRec) * blocks));
+    HIP_TRY(s, s->d_sweep_merged.ensure(sizeof(pe::SweepRec)));
+    HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
+    A.recs = s->d_sweep_recs.as<pe::SweepRec>();
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, pe_launch_sweep(&A, blocks, s->d_sweep_merged.as<pe::SweepRec>(), s->stream));
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    pe::SweepRec rec;
+    HIP_TRY(s, hipMemcpyAsync(&rec, s->d_sweep_merged.p, sizeof(rec), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    s->last_sweep_ms = ms;
+    std::memset(out, 0, sizeof(*out));
+    const uint32_t rank = pe_rec_winner(&rec);
+    out->row = -1;
+    out->nodes_evaluated = n;   // every node is pulled: the stream is exhausted
+    out->nodes_filtered = rec.filtered;
+    out->nodes_exhausted = rec.exhausted;
+    out->new_offset = s->offset;   // a full pass leaves the cursor unchanged
+    if (rank != PE_NONE) {
+        uint32_t pos = s->offset + rank;
+        if (pos >= n) pos -= n;
+        const uint32_t row = s->visit[pos];
+        HIP_TRY(s, pe_launch_node_record(&A, row, s->d_record.as<pe_ranked_node>(), s->stream));
+        pe_ranked_node rr;
+        HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        out->row = (int32_t)row;
+        out->final_score = rr.final_score;
+        out->n_scores = rr.n_scores;
+        std::memcpy(out->scores, rr.scores, sizeof(out->scores));
+    }
+    return PE_OK;
+}
+
 // One evaluation on the stack's plan (pe_select / pe_place): the fused count
 // loop in launches of at most H/2 placements, each merging its overlay back
 // into the HBM SoA so the plan persists.
@@ -939,6 +1083,7 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
         return nullptr;
     }
     s->log10 = pe::gm::log_go(10.0);
+    if (const char* e = std::getenv("PE_SWEEP_MIN")) s->sweep_min = (uint32_t)std::strtoul(e, nullptr, 10);
     return s;
 }
 
@@ -1124,6 +1269,14 @@ int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_
     s->limit = lim;
     if (limit_out) *limit_out = lim;
     invalidate_tables(s);
+    // visit position of every row (sweep path ranks rows without a gather)
+    std::vector<uint32_t> rank_of(s->nodes.size(), PE_NONE);
+    s->visit_unique = true;
+    for (uint32_t i = 0; i < n; i++) {
+        if (rank_of[s->visit[i]] != PE_NONE) s->visit_unique = false;
+        rank_of[s->visit[i]] = i;
+    }
+    HIP_TRY(s, upload(s->d_rank_of, rank_of));
     return PE_OK;
 }
 
@@ -1170,6 +1323,10 @@ int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranke
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;   // never reset until SetNodes (stack.go:165-167)
+    if (s->limit >= s->visit.size() && s->visit.size() >= s->sweep_min) {
+        // a whole pass over a large list: multi-CU sweep instead of one workgroup
+        if (s->visit_unique) return run_sweep_select(s, g, opts, out);
+    }
     uint32_t placed, no;
     rc = run_place(s, tgi, 1, 0, s->visit, s->offset, opts, out, &placed, &no);
     if (rc) return rc;
@@ -1302,11 +1459,10 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
     A.offset0 = 0;
     A.commit = 1;
     A.writeback = 0;
-    DevMem d_out, d_st;
-    HIP_TRY(s, d_out.ensure(sizeof(pe_placement) * (size_t)E * std::max<uint32_t>(count, 1)));
-    HIP_TRY(s, d_st.ensure(sizeof(uint32_t) * 2 * (size_t)E));
-    A.out = d_out.as<pe_placement>();
-    A.eval_status = d_st.as<uint32_t>();
+    HIP_TRY(s, s->d_batch_out.ensure(sizeof(pe_placement) * (size_t)E * std::max<uint32_t>(count, 1)));
+    HIP_TRY(s, s->d_batch_status.ensure(sizeof(uint32_t) * 2 * (size_t)E));
+    A.out = s->d_batch_out.as<pe_placement>();
+    A.eval_status = s->d_batch_status.as<uint32_t>();
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     HIP_TRY(s, pe_launch_place(&A, E, full, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
@@ -1339,7 +1495,8 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     TgPlan& g = *s->tgs[tgi];
     const uint32_t n = (uint32_t)s->visit.size();
     HIP_TRY(s, upload(s->d_visit, s->visit));
-    DevMem d_score, d_st;
+    DevMem& d_score = s->d_sys_score;
+    DevMem& d_st = s->d_sys_status;
     HIP_TRY(s, d_score.ensure(sizeof(double) * std::max<uint32_t>(n, 1)));
     HIP_TRY(s, d_st.ensure(std::max<uint32_t>(n, 1)));
     HIP_TRY(s, s->d_status.ensure(16));

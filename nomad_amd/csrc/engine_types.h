@@ -89,6 +89,33 @@ struct BatchArgs {
     uint32_t* eval_status;        // [n_evals][2]: placed, final cursor
 };
 
+// Full-scan Select reduction record (one per workgroup, and per GPU shard).
+// With limit >= options the LimitIterator returns every option, the first
+// kMaxSkip non-positive ones (in visit order) moved to the end; MaxScore then
+// takes the first strict maximum. The record keeps
+// exactly what that rule needs and merges associatively.
+struct SweepRec {
+    double max_score;            // -inf: no option
+    uint32_t max_rank[4];        // earliest visit ranks scoring max_score (sorted, ~0u = empty)
+    uint32_t np_rank[kMaxSkip];  // earliest non-positive options (sorted by rank)
+    uint32_t options, filtered, exhausted, _pad;
+    double np_score[kMaxSkip];
+};
+
+struct SweepArgs {
+    NodeSoA soa;
+    TgTables tg;
+    Ask ask;
+    const uint32_t* rank_of;      // [n rows] visit position of the row, ~0u = not in the list
+    uint32_t n_visit;
+    uint32_t offset;              // StaticIterator cursor: rank = (pos - offset) mod n_visit
+    uint32_t row_begin, row_end;  // rows this launch (shard) sweeps
+    const uint32_t* penalty_bits;
+    double log10;
+    const double* spread_tab;     // [kMaxPsets][kMaxValues+1] or null
+    SweepRec* recs;               // [gridDim.x]
+};
+
 struct SystemArgs {
     NodeSoA soa;
     TgTables tg;

@@ -537,6 +537,141 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row) {
     }
 }
 
+// ---- full-scan scoring sweep --------------------------------------------------
+__host__ __device__ __forceinline__ void rec_init(SweepRec& r) {
+    r.max_score = -__builtin_inff();
+    for (int i = 0; i < 4; i++) r.max_rank[i] = 0xFFFFFFFFu;
+    for (int i = 0; i < kMaxSkip; i++) { r.np_rank[i] = 0xFFFFFFFFu; r.np_score[i] = 0.0; }
+    r.options = r.filtered = r.exhausted = r._pad = 0;
+}
+
+// insert x into a sorted list of N ranks (keeps the N smallest); branch-free on indices
+template <int N>
+__host__ __device__ __forceinline__ void ins_rank(uint32_t (&l)[N], uint32_t x) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t lo = l[i] < x ? l[i] : x, hi = l[i] < x ? x : l[i];
+        l[i] = lo;
+        x = hi;
+    }
+}
+
+__host__ __device__ __forceinline__ void ins_np(uint32_t (&rk)[kMaxSkip], double (&sc)[kMaxSkip], uint32_t x, double s) {
+#pragma unroll
+    for (int i = 0; i < kMaxSkip; i++) {
+        if (x < rk[i]) {
+            const uint32_t tr = rk[i]; const double ts = sc[i];
+            rk[i] = x; sc[i] = s;
+            x = tr; s = ts;
+        }
+    }
+}
+
+__device__ __forceinline__ void rec_add(SweepRec& r, uint32_t rank, double score) {
+    r.options++;
+    if (score > r.max_score) {
+        r.max_score = score;
+        r.max_rank[0] = rank;
+        r.max_rank[1] = r.max_rank[2] = r.max_rank[3] = 0xFFFFFFFFu;
+    } else if (score == r.max_score) {
+        ins_rank<4>(r.max_rank, rank);
+    }
+    if (score <= 0.0) ins_np(r.np_rank, r.np_score, rank, score);
+}
+
+__host__ __device__ __forceinline__ void rec_merge(SweepRec& a, const SweepRec& b) {
+    if (b.max_score > a.max_score) {
+        a.max_score = b.max_score;
+        for (int i = 0; i < 4; i++) a.max_rank[i] = b.max_rank[i];
+    } else if (b.max_score == a.max_score) {
+        for (int i = 0; i < 4; i++) ins_rank<4>(a.max_rank, b.max_rank[i]);
+    }
+    for (int i = 0; i < kMaxSkip; i++) ins_np(a.np_rank, a.np_score, b.np_rank[i], b.np_score[i]);
+    a.options += b.options;
+    a.filtered += b.filtered;
+    a.exhausted += b.exhausted;
+}
+
+// Winner rank of a merged record, ~0u = no option.
+__device__ __host__ __forceinline__ uint32_t rec_winner(const SweepRec& r) {
+    if (r.options == 0) return 0xFFFFFFFFu;
+    if (r.max_score > 0.0) return r.max_rank[0];
+    for (int i = 0; i < 4; i++) {
+        const uint32_t x = r.max_rank[i];
+        if (x == 0xFFFFFFFFu) break;
+        bool demoted = false;
+        for (int k = 0; k < kMaxSkip; k++) demoted = demoted || r.np_rank[k] == x;
+        if (!demoted) return x;
+    }
+    return r.max_rank[0];
+}
+
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_sweep(SweepArgs A) {
+    __shared__ SweepRec red[BLOCK];
+    SweepRec r;
+    rec_init(r);
+    Overlay none;
+    none.keys = nullptr;
+    const uint32_t n = A.n_visit;
+    for (uint32_t row = A.row_begin + blockIdx.x * BLOCK + threadIdx.x; row < A.row_end;
+         row += gridDim.x * BLOCK) {
+        const uint32_t pos = A.rank_of[row];
+        if (pos == 0xFFFFFFFFu) continue;
+        NodeEval ev;
+        eval_node<false>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, A.spread_tab, row, &ev);
+        if (ev.status == kFiltered) { r.filtered++; continue; }
+        if (ev.status == kExhausted) { r.exhausted++; continue; }
+        const uint32_t rank = pos >= A.offset ? pos - A.offset : pos + n - A.offset;
+        rec_add(r, rank, ev.score);
+    }
+    red[threadIdx.x] = r;
+    __syncthreads();
+    for (int s = BLOCK / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) rec_merge(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) A.recs[blockIdx.x] = red[0];
+}
+
+// Merge the per-workgroup records (one workgroup).
+__global__ void __launch_bounds__(256) k_sweep_merge(const SweepRec* recs, uint32_t count, SweepRec* out) {
+    __shared__ SweepRec red[256];
+    SweepRec r;
+    rec_init(r);
+    for (uint32_t i = threadIdx.x; i < count; i += 256) rec_merge(r, recs[i]);
+    red[threadIdx.x] = r;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) rec_merge(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = red[0];
+}
+
+// Spread contribution table in HBM for the sweep path (same code as the
+// persistent loop's LDS table, so both paths are bit-identical).
+__global__ void __launch_bounds__(256) k_spread_table(TgTables t, double* tab) {
+    __shared__ uint32_t counts[kMaxPsets * kMaxValues];
+    __shared__ uint32_t scratch[4];
+    for (int p = 0; p < t.n_psets; p++)
+        for (int v = threadIdx.x; v < t.pset_nvals[p]; v += 256) counts[p * kMaxValues + v] = t.pset_counts[p][v];
+    __syncthreads();
+    build_spread_table<256>(t, counts, tab, scratch);
+}
+
+// Score parts of one node (the winner's RankedNode record).
+__global__ void k_node_record(SweepArgs A, uint32_t row, pe_ranked_node* out) {
+    if (threadIdx.x != 0) return;
+    Overlay none;
+    none.keys = nullptr;
+    NodeEval ev;
+    eval_node<true>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, A.spread_tab, row, &ev);
+    out->final_score = ev.score;
+    out->n_scores = ev.nscores;
+    for (int k = 0; k < PE_MAX_SCORES; k++) out->scores[k] = k < (int)ev.nscores ? ev.parts[k] : 0.0;
+}
+
 // node_feas[row] = class_ok[cls] && node_ok[row]: one verdict byte per node so
 // the count loop issues a single dependent round trip per node.
 __global__ void __launch_bounds__(256) k_fold_feas(NodeSoA s, const uint8_t* class_ok, const uint8_t* node_ok,
@@ -590,3 +725,24 @@ hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, co
     hipLaunchKernelGGL(pe::k_fold_feas, dim3(blocks), dim3(256), 0, st, *s, class_ok, node_ok, feas);
     return hipGetLastError();
 }
+
+hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec* merged, hipStream_t st) {
+    hipLaunchKernelGGL((pe::k_sweep<256>), dim3(blocks), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(pe::k_sweep_merge, dim3(1), dim3(256), 0, st, (const pe::SweepRec*)a->recs, blocks, merged);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_node_record(const pe::SweepArgs* a, uint32_t row, pe_ranked_node* out, hipStream_t st) {
+    hipLaunchKernelGGL(pe::k_node_record, dim3(1), dim3(64), 0, st, *a, row, out);
+    return hipGetLastError();
+}
+
+uint32_t pe_rec_winner(const pe::SweepRec* r) { return pe::rec_winner(*r); }
+
+hipError_t pe_launch_spread_table(const pe::TgTables* t, double* tab, hipStream_t st) {
+    hipLaunchKernelGGL(pe::k_spread_table, dim3(1), dim3(256), 0, st, *t, tab);
+    return hipGetLastError();
+}
+
+void pe_rec_merge_host(pe::SweepRec* a, const pe::SweepRec* b) { pe::rec_merge(*a, *b); }
+void pe_rec_init_host(pe::SweepRec* a) { pe::rec_init(*a); }

@@ -81,7 +81,8 @@ class RankedNode:
 
     @classmethod
     def from_c(cls, r: abi.pe_ranked_node, nodes):
-        return cls(row=r.row, node=nodes[r.row] if r.row >= 0 else None, final_score=r.final_score,
+        return cls(row=r.row, node=nodes[r.row] if (nodes is not None and r.row >= 0) else None,
+                   final_score=r.final_score,
                    scores=[r.scores[i] for i in range(r.n_scores)], nodes_evaluated=r.nodes_evaluated,
                    nodes_filtered=r.nodes_filtered, nodes_exhausted=r.nodes_exhausted,
                    new_offset=r.new_offset)
@@ -143,6 +144,14 @@ class _Stack:
         self._check(self._fn("set_state")(self._h, C.byref(t), C.byref(self.state.node_table),
                                           C.byref(self.state.alloc_table)))
         return self.state
+
+    def SetStateColumnar(self, cs):
+        """Snapshot from a synth_columnar.ColumnarState (no per-node Python objects)."""
+        self.nodes = None
+        self.state = cs
+        t = cs.strtab()
+        self._check(self._fn("set_state")(self._h, C.byref(t), C.byref(cs.node_table), C.byref(cs.alloc_table)))
+        return cs
 
     def ResetPlan(self):
         """New evaluation on the resident snapshot (fresh EvalContext)."""

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from nomad_amd import synth
-from nomad_amd.structs import Constraint, SchedulerConfig
+from nomad_amd.structs import Allocation, Constraint, SchedulerConfig
 from oracle.oracle import OracleGenericStack, OracleSystemStack
 from tests.helpers import assert_same_placements, run_place
 
@@ -93,6 +93,41 @@ def test_select_commit_path_matches_place():
         e.Commit(0, b.row)
 
 
+def test_sweep_select_path_matches_oracle(monkeypatch):
+    """Full-scan Selects through the multi-CU sweep + SweepRec reduction (forced
+    with PE_SWEEP_MIN=1) against the oracle, Select -> Commit for 80 placements."""
+    monkeypatch.setenv("PE_SWEEP_MIN", "1")
+    nodes, allocs = synth.cluster_c3(2500, seed=13)
+    job = synth.job_c3(80)
+    perm = synth.shuffle(len(nodes), 8)
+    o = OracleGenericStack(); o.SetState(nodes, allocs); o.SetJob(job); o.SetNodes(list(perm))
+    e = engine_generic(); e.SetState(nodes, allocs); e.SetJob(job); e.SetNodes(list(perm))
+    for _ in range(80):
+        a, b = o.SelectRaw(0), e.SelectRaw(0)
+        assert_same_placements([b], [a])
+        if a.row < 0:
+            break
+        o.Commit(0, a.row)
+        e.Commit(0, b.row)
+
+
+def test_sweep_select_nonpositive_demotion(monkeypatch):
+    """All options score <= 0 (anti-affinity dominates): the first three
+    non-positive options are demoted behind the rest (select.go:35-74)."""
+    monkeypatch.setenv("PE_SWEEP_MIN", "1")
+    nodes, _ = synth.cluster_c3(300, seed=2)
+    job = synth.job_c3(2)          # desired count 2: each collision costs -(c+1)/2
+    allocs = [Allocation(node_id=n.id, job_id=job.id, task_group="web") for n in nodes for _ in range(3)]
+    perm = synth.shuffle(len(nodes), 4)
+    for use_sweep in ("1", "1000000"):
+        monkeypatch.setenv("PE_SWEEP_MIN", use_sweep)
+        o = OracleGenericStack(); o.SetState(nodes, allocs); o.SetJob(job); o.SetNodes(list(perm))
+        e = engine_generic(); e.SetState(nodes, allocs); e.SetJob(job); e.SetNodes(list(perm))
+        a, b = o.SelectRaw(0), e.SelectRaw(0)
+        assert a.row >= 0 and a.final_score <= 0
+        assert_same_placements([b], [a])
+
+
 @pytest.mark.parametrize("cfg", ["c2", "c3"])
 def test_batch_evals_match_single_eval_oracle(cfg):
     """pe_place_batch: every concurrent eval equals SetNodes(order) + Place on the oracle."""
@@ -118,6 +153,23 @@ def test_batch_evals_match_single_eval_oracle(cfg):
             assert evaluated[k, i] == r.nodes_evaluated, (k, i)
             if r.row >= 0:
                 assert scores[k, i] == r.final_score, (k, i)
+
+
+@pytest.mark.parametrize("kind", ["c3", "c4"])
+def test_columnar_cluster_place(kind):
+    """Vectorised (columnar) snapshot path: full count loop vs the oracle on the same tables."""
+    from nomad_amd import synth_columnar
+    cs = synth_columnar.ColumnarState(20000, seed=5, kind=kind, prefill=0.05)
+    job = synth.job_c3(200) if kind == "c3" else synth.job_c2(200)
+    perm = np.random.Generator(np.random.PCG64(9)).permutation(20000).astype(np.uint32)
+    res = []
+    for cls in (OracleGenericStack, engine_generic):
+        st = cls()
+        st.SetStateColumnar(cs)
+        st.SetJob(job)
+        st.SetNodes(perm)
+        res.append(st.Place(0, 200))
+    assert_same_placements(res[1], res[0])
 
 
 def test_system_job_sweep():
