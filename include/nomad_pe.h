@@ -266,10 +266,21 @@ int pe_place(pe_stack* s, uint32_t tg_index, uint32_t count, pe_ranked_node* out
  * order, an independent evaluation of `count` placements of task group
  * `tg_index` from the stack's current plan (offset 0), exactly as
  * SetNodes(order) + pe_place would, without modifying the stack's plan.
- * out[n_evals * count] (row-major by eval), placed[n_evals]. */
+ * out[n_evals * count] (row-major by eval), placed[n_evals]; either may be NULL:
+ * the results always land in a stack-owned page-locked buffer first, readable
+ * in place through pe_batch_results until the next pe_place_batch. The host
+ * preparation (fresh-memo feasibility tables, limit) is reused across calls
+ * until a mutating call (set_state / set_job / stage_orders / select / ...). */
 int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint32_t n);
 int pe_place_batch(pe_stack* s, uint32_t tg_index, uint32_t count, pe_placement* out,
                    uint32_t* placed);
+/* Results of the last pe_place_batch: out[n_evals * count]; status[2 * e] =
+ * placements of eval e, status[2 * e + 1] = its final StaticIterator offset. */
+int pe_batch_results(const pe_stack* s, const pe_placement** out, const uint32_t** status,
+                     uint32_t* n_evals, uint32_t* count);
+/* Phases of the last pe_place_batch in ms: [0] host preparation, [1] kernel
+ * (HIP events), [2] device-to-host result copy (HIP events), [3] call total. */
+void pe_last_phase_ms(const pe_stack* s, double* out4);
 /* SystemScheduler.computePlacements (scheduler_system.go:283-425) for one task
  * group over every row of the SetNodes list: one single-node Select per row.
  * out_row_score[n] = FinalScore or NaN when filtered/exhausted;

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <cstdlib>
@@ -31,7 +32,7 @@
 #include "engine_types.h"
 #include "gomath_dev.h"
 
-size_t pe_place_lds_bytes(bool full, int hash_bits, bool net);
+size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
@@ -42,6 +43,7 @@ hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec
 hipError_t pe_launch_node_record(const pe::SweepArgs* a, uint32_t row, pe_ranked_node* out, hipStream_t st);
 hipError_t pe_launch_spread_table(const pe::TgTables* t, double* tab, hipStream_t st);
 uint32_t pe_rec_winner(const pe::SweepRec* r);
+int pe_sweep_blocks_per_cu();
 
 namespace {
 
@@ -69,6 +71,36 @@ struct DevMem {
         return e;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Page-locked host buffer: device-to-host result copies run at DMA rate and the
+// caller can view the results in place (pe_batch_results).
+struct PinnedMem {
+    void* p = nullptr;
+    size_t bytes = 0;
+    PinnedMem() = default;
+    PinnedMem(const PinnedMem&) = delete;
+    PinnedMem& operator=(const PinnedMem&) = delete;
+    ~PinnedMem() { release(); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t ensure(size_t b) {
+        if (b <= bytes && p) return hipSuccess;
+        release();
+        hipError_t e = hipHostMalloc(&p, b ? b : 16, hipHostMallocMapped);
+        if (e == hipSuccess) bytes = b ? b : 16;
+        return e;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+    // the same bytes as seen from the device (kernels store results directly)
+    template <class T> T* dev() const {
+        void* d = nullptr;
+        if (!p || hipHostGetDevicePointer(&d, p, 0) != hipSuccess) return nullptr;
+        return static_cast<T*>(d);
+    }
 };
 
 // Fixed per-node fields; the variable-length maps live in stack-owned CSR
@@ -178,8 +210,10 @@ struct pe_stack {
     std::string err;
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double last_ms = 0;
+    int n_cu = 256;
+    int sweep_per_cu = 4;
 
     // strings
     std::vector<std::string> strs;
@@ -208,6 +242,15 @@ struct pe_stack {
     double last_sweep_ms = 0;
     std::vector<uint32_t> h_orders;
     uint32_t staged_evals = 0, staged_n = 0;
+    // Every mutating entry point bumps `gen`; a batch launch prepared at the
+    // current gen (fresh-memo tables, limit, overlay size) is reused as is.
+    uint64_t gen = 1, batch_gen = 0;
+    uint32_t batch_tgi = 0, batch_count = 0;
+    bool batch_full = false, batch_direct = false;
+    bool results_via_copy = false;     // PE_RESULTS_VIA_COPY=1: device buffer + one D2H copy
+    pe::BatchArgs batch_A{};
+    PinnedMem h_batch_out, h_batch_status;
+    double phase_ms[4] = {0, 0, 0, 0};   // host prep, kernels, result copy, total (last batch)
     std::vector<pe::NodeRec> h_base_rec;     // snapshot proposed state (no plan)
     DevMem d_rec, d_base_rec, d_coll_job;
     bool have_state = false;
@@ -897,16 +940,28 @@ void invalidate_tables(pe_stack* s) {
 }
 
 // Largest overlay (log2 entries) that fits the LDS budget of one workgroup.
-int max_hash_bits(bool full, bool net) {
+int max_hash_bits(bool full) {
     int bits = 12;
-    while (bits > 6 && pe_place_lds_bytes(full, bits, net) > 96 * 1024) bits--;
+    while (bits > 6 && pe_place_lds_bytes(full, bits, false) > 96 * 1024) bits--;
     return bits;
 }
 
-int hash_bits_for(uint32_t count, bool full, bool net) {
+int hash_bits_for(uint32_t count, bool full) {
     int bits = 6;
     while (bits < 30 && (1u << bits) < 2u * std::max<uint32_t>(count, 1)) bits++;
-    return std::min(bits, max_hash_bits(full, net));
+    return std::min(bits, max_hash_bits(full));
+}
+
+// Count bits of a packed windowed-kernel overlay entry (row << kbits | k), or 0
+// when the rows or `max_k` placements per node do not fit in 32 bits. Rows stay
+// below 2^rowbits - 1 so no entry equals the empty marker.
+int packed_kbits(const pe_stack* s, uint32_t max_k, bool full) {
+    if (full) return 0;
+    int rowbits = 1;
+    while (rowbits < 32 && ((uint64_t)1 << rowbits) <= (uint64_t)s->nodes.size()) rowbits++;
+    const int kbits = 32 - rowbits;
+    if (kbits < 2 || (uint64_t)max_k > ((uint64_t)1 << kbits) - 1) return 0;
+    return kbits;
 }
 
 pe::BatchArgs batch_args(pe_stack* s, TgPlan& g) {
@@ -954,8 +1009,10 @@ int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_r
         HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
         A.spread_tab = s->d_spread_tab.as<double>();
     }
-    uint32_t blocks = (A.row_end + 256 * 8 - 1) / (256 * 8);   // ~8 rows per thread
-    blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 8192));
+    // exactly one round of resident workgroups: a grid-stride pass with no
+    // tail, and few records for the merge
+    uint32_t blocks = (A.row_end - A.row_begin + 256 * 8 - 1) / (256 * 8);
+    blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)(s->n_cu * s->sweep_per_cu)));
     HIP_TRY(s, s->d_sweep_recs.ensure(sizeof(pe::SweepRec) * blocks));
     HIP_TRY(s, s->d_sweep_merged.ensure(sizeof(pe::SweepRec)));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
@@ -1022,7 +1079,8 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         HIP_TRY(s, upload(s->d_penalty, bits));
         A.penalty_bits = s->d_penalty.as<uint32_t>();
     }
-    A.hash_bits = hash_bits_for(count, full, A.net_overlay != 0);
+    A.hash_bits = hash_bits_for(count, full);
+    A.packed_overlay = packed_kbits(s, 1u << A.hash_bits, full);
     const uint32_t chunk = std::max<uint32_t>(1, (1u << A.hash_bits) / 2);
     HIP_TRY(s, s->d_out.ensure(sizeof(pe_ranked_node) * std::min(count, chunk)));
     HIP_TRY(s, s->d_status.ensure(16));
@@ -1077,13 +1135,19 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     s->cfg = *cfg;
     s->device = cfg->device;
     if (hipSetDevice(s->device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) {
+        hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
+        hipEventCreate(&s->ev2) != hipSuccess) {
         g_error = "HIP stream/event creation failed";
         delete s;
         return nullptr;
     }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess && cus > 0)
+        s->n_cu = cus;
+    s->sweep_per_cu = pe_sweep_blocks_per_cu();
     s->log10 = pe::gm::log_go(10.0);
     if (const char* e = std::getenv("PE_SWEEP_MIN")) s->sweep_min = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("PE_RESULTS_VIA_COPY")) s->results_via_copy = std::atoi(e) != 0;
     return s;
 }
 
@@ -1094,6 +1158,7 @@ void pe_stack_destroy(pe_stack* s) {
     s->tgs.clear();
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->ev2) (void)hipEventDestroy(s->ev2);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
@@ -1112,6 +1177,7 @@ int pe_check_constraint(const char* op, const char* l, int ls, const char* r, in
 
 int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
     if (!s || !strs || !nodes) return PE_EINVAL;
+    s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     s->strs.clear();
     s->sid.clear();
@@ -1136,6 +1202,7 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
 int pe_reset_plan(pe_stack* s) {
     if (!s) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     const size_t n = s->nodes.size();
     HIP_TRY(s, hipMemcpyAsync(s->d_rec.p, s->d_base_rec.p, n * sizeof(pe::NodeRec), hipMemcpyDeviceToDevice,
@@ -1156,6 +1223,7 @@ int pe_reset_plan(pe_stack* s) {
 int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     if (!s || !j) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     s->add_strings(strs);
     const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
@@ -1258,6 +1326,7 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
 int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
     if (!s) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    s->gen++;
     s->visit.assign(rows, rows + n);
     for (uint32_t r : s->visit) if (r >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range");
     s->offset = 0;
@@ -1286,6 +1355,7 @@ static bool tg_full_scan(pe_stack* s, TgPlan& g) {
 
 int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
     if (!s || !out) return PE_EINVAL;
+    s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     if (s->cfg.stack_kind != PE_STACK_GENERIC) {
         // SystemStack.Select: single pass over the (single-node) list, no limit
@@ -1338,6 +1408,7 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
     if (!s) return PE_EINVAL;
     if (!s->have_job || tgi >= s->tgs.size() || row < 0 || (size_t)row >= s->nodes.size())
         return s->fail(PE_EINVAL, "bad commit");
+    s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     TgPlan& g = *s->tgs[tgi];
     if (!g.psets_built) {
@@ -1363,6 +1434,7 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
 int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
     if (!s || (!out && count)) return PE_EINVAL;
     if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place needs a generic stack");
+    s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     int rc = prepare_tg(s, tgi, s->visit, s->offset);
     if (rc) return rc;
@@ -1384,6 +1456,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
 int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint32_t n) {
     if (!s || (!orders && n_evals && n)) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     const size_t total = (size_t)n_evals * n;
     for (size_t i = 0; i < total; i++)
@@ -1395,20 +1468,12 @@ int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint3
     return PE_OK;
 }
 
-int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out, uint32_t* placed) {
-    if (!s || (!out && count)) return PE_EINVAL;
-    if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place_batch needs a generic stack");
-    if (!s->plan.empty()) return s->fail(PE_ESTATE, "batch evaluations start from a fresh plan (pe_reset_plan)");
-    if (!s->have_job || tgi >= s->tgs.size()) return s->fail(PE_ESTATE, "pe_set_job not called / bad task group");
-    HIP_TRY(s, hipSetDevice(s->device));
+namespace {
+
+// Host preparation of a batch launch: fresh-memo feasibility tables, limit and
+// overlay size, exactly as SetNodes(order) + Select would set them up.
+int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
     const uint32_t E = s->staged_evals, n = s->staged_n;
-    if (E == 0 || n == 0) {
-        for (uint32_t e = 0; e < E; e++) {
-            if (placed) placed[e] = 0;
-            if (count) { out[(size_t)e * count].row = -1; out[(size_t)e * count].nodes_evaluated = 0; }
-        }
-        return PE_OK;
-    }
     TgPlan& g = *s->tgs[tgi];
     if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
     if (!g.psets_built) {
@@ -1434,7 +1499,8 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
     pe::BatchArgs A = batch_args(s, g);
     s->limit = saved_limit;
     const bool full = !g.psets.empty() || lim >= n;
-    A.hash_bits = hash_bits_for(count, full, A.net_overlay != 0);
+    A.hash_bits = hash_bits_for(count, full);
+    A.packed_overlay = packed_kbits(s, count, full);
     if ((1u << A.hash_bits) < 2u * count)
         return s->fail(PE_EUNSUPPORTED, "count too large for the per-eval LDS overlay in batch mode");
     if (!g.nonuniform.empty() && !g.node_ok_used) {
@@ -1461,26 +1527,109 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
     A.writeback = 0;
     HIP_TRY(s, s->d_batch_out.ensure(sizeof(pe_placement) * (size_t)E * std::max<uint32_t>(count, 1)));
     HIP_TRY(s, s->d_batch_status.ensure(sizeof(uint32_t) * 2 * (size_t)E));
+    HIP_TRY(s, s->h_batch_out.ensure(sizeof(pe_placement) * (size_t)E * std::max<uint32_t>(count, 1)));
+    HIP_TRY(s, s->h_batch_status.ensure(sizeof(uint32_t) * 2 * (size_t)E));
     A.out = s->d_batch_out.as<pe_placement>();
     A.eval_status = s->d_batch_status.as<uint32_t>();
+    s->batch_direct = false;
+    if (!full && !s->results_via_copy) {
+        // the windowed kernel streams its records into the mapped host buffer
+        pe_placement* o = s->h_batch_out.dev<pe_placement>();
+        uint32_t* st = s->h_batch_status.dev<uint32_t>();
+        if (o && st) {
+            A.out = o;
+            A.eval_status = st;
+            s->batch_direct = true;
+        }
+    }
+    s->batch_A = A;
+    s->batch_full = full;
+    s->batch_tgi = tgi;
+    s->batch_count = count;
+    s->batch_gen = s->gen;
+    return PE_OK;
+}
+
+}  // namespace
+
+int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out, uint32_t* placed) {
+    if (!s) return PE_EINVAL;
+    if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place_batch needs a generic stack");
+    if (!s->plan.empty()) return s->fail(PE_ESTATE, "batch evaluations start from a fresh plan (pe_reset_plan)");
+    if (!s->have_job || tgi >= s->tgs.size()) return s->fail(PE_ESTATE, "pe_set_job not called / bad task group");
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(s, hipSetDevice(s->device));
+    const uint32_t E = s->staged_evals, n = s->staged_n;
+    if (E == 0 || n == 0 || count == 0) {
+        HIP_TRY(s, s->h_batch_out.ensure(sizeof(pe_placement) * std::max<size_t>((size_t)E * count, 1)));
+        HIP_TRY(s, s->h_batch_status.ensure(sizeof(uint32_t) * 2 * std::max<uint32_t>(E, 1)));
+        pe_placement* res = s->h_batch_out.as<pe_placement>();
+        for (uint32_t e = 0; e < E; e++) {
+            s->h_batch_status.as<uint32_t>()[2 * e] = 0;
+            if (placed) placed[e] = 0;
+            if (count) {
+                res[(size_t)e * count].row = -1;
+                res[(size_t)e * count].nodes_evaluated = 0;
+                res[(size_t)e * count].final_score = 0.0;
+            }
+        }
+        if (out && count) std::memcpy(out, res, sizeof(pe_placement) * (size_t)E * count);
+        s->batch_count = count;
+        s->batch_gen = 0;
+        return PE_OK;
+    }
+    if (s->batch_gen != s->gen || s->batch_tgi != tgi || s->batch_count != count) {
+        int rc = prepare_batch(s, tgi, count);
+        if (rc) return rc;
+    }
+    const pe::BatchArgs& A = s->batch_A;
+    const auto t1 = std::chrono::steady_clock::now();
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-    HIP_TRY(s, pe_launch_place(&A, E, full, s->stream));
+    HIP_TRY(s, pe_launch_place(&A, E, s->batch_full, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
-    std::vector<uint32_t> st(2 * (size_t)E);
-    HIP_TRY(s, hipMemcpyAsync(st.data(), A.eval_status, st.size() * 4, hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(s, hipMemcpyAsync(out, A.out, sizeof(pe_placement) * (size_t)E * count, hipMemcpyDeviceToHost, s->stream));
+    if (!s->batch_direct) {
+        HIP_TRY(s, hipMemcpyAsync(s->h_batch_status.p, A.eval_status, sizeof(uint32_t) * 2 * (size_t)E,
+                                  hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(s->h_batch_out.p, A.out, sizeof(pe_placement) * (size_t)E * count,
+                                  hipMemcpyDeviceToHost, s->stream));
+    }
+    HIP_TRY(s, hipEventRecord(s->ev2, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
-    float ms = 0;
+    float ms = 0, copy_ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    HIP_TRY(s, hipEventElapsedTime(&copy_ms, s->ev1, s->ev2));
     s->last_ms = ms;
+    const uint32_t* st = s->h_batch_status.as<uint32_t>();
     if (placed)
         for (uint32_t e = 0; e < E; e++) placed[e] = st[2 * e];
+    if (out) std::memcpy(out, s->h_batch_out.p, sizeof(pe_placement) * (size_t)E * count);
+    const auto t2 = std::chrono::steady_clock::now();
+    s->phase_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    s->phase_ms[1] = ms;
+    s->phase_ms[2] = copy_ms;
+    s->phase_ms[3] = std::chrono::duration<double, std::milli>(t2 - t0).count();
     return PE_OK;
+}
+
+int pe_batch_results(const pe_stack* s, const pe_placement** out, const uint32_t** status, uint32_t* n_evals,
+                     uint32_t* count) {
+    if (!s) return PE_EINVAL;
+    if (out) *out = s->h_batch_out.as<const pe_placement>();
+    if (status) *status = s->h_batch_status.as<const uint32_t>();
+    if (n_evals) *n_evals = s->staged_evals;
+    if (count) *count = s->batch_count;
+    return PE_OK;
+}
+
+void pe_last_phase_ms(const pe_stack* s, double* out4) {
+    if (!s || !out4) return;
+    for (int i = 0; i < 4; i++) out4[i] = s->phase_ms[i];
 }
 
 int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     if (!s || !out_score || !out_status) return PE_EINVAL;
     if (s->cfg.stack_kind != PE_STACK_SYSTEM) return s->fail(PE_ESTATE, "pe_system_place needs a system stack");
+    s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     {
         // every node appears once: the single-node Selects are independent

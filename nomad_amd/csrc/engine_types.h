@@ -82,7 +82,8 @@ struct BatchArgs {
     double log10;                 // go_log(10), computed on host
     int hash_bits;                // LDS overlay capacity = 1 << hash_bits (>= 2 * count)
     int net_overlay;              // overlay tracks network deltas
-    int commit;                   // apply Plan.AppendAlloc after each placement
+    int packed_overlay;           // one u32 per overlay entry: row << 8 | k (rows < 2^24, count <= 255)
+    int commit;                 // apply Plan.AppendAlloc after each placement
     int writeback;                // merge the overlay into the HBM SoA at the end
     pe_ranked_node* full_out;     // [n_evals][count] full records, or null
     pe_placement* out;            // [n_evals][count] compact records, or null

@@ -37,11 +37,15 @@ struct NodeEval {
 
 // Per-eval LDS overlay of the allocs this eval placed: row -> k placements.
 // Every placement of the count loop has the same ask, so the deltas are k * ask.
+// Packed form (k == null): one u32 per entry, row << kshift | k, which halves
+// the LDS per evaluation and so doubles the evaluations resident per CU.
 struct Overlay {
     uint32_t* keys;      // null: no overlay
-    uint32_t* k;
+    uint32_t* k;         // null: packed entries
     uint32_t mask;
     int bits;
+    int kshift;
+    uint32_t kmask;
 };
 
 __device__ __forceinline__ uint32_t ov_hash(const Overlay& o, uint32_t row) {
@@ -51,6 +55,14 @@ __device__ __forceinline__ uint32_t ov_hash(const Overlay& o, uint32_t row) {
 __device__ __forceinline__ uint32_t ov_count(const Overlay& o, uint32_t row) {
     if (!o.keys) return 0;
     uint32_t h = ov_hash(o, row);
+    if (!o.k) {
+        for (;;) {
+            const uint32_t e = o.keys[h];
+            if (e == kEmpty) return 0;
+            if ((e >> o.kshift) == row) return e & o.kmask;
+            h = (h + 1) & o.mask;
+        }
+    }
     for (;;) {
         const uint32_t key = o.keys[h];
         if (key == row) return o.k[h];
@@ -61,6 +73,14 @@ __device__ __forceinline__ uint32_t ov_count(const Overlay& o, uint32_t row) {
 
 __device__ __forceinline__ void ov_add(const Overlay& o, uint32_t row) {
     uint32_t h = ov_hash(o, row);
+    if (!o.k) {
+        for (;;) {
+            const uint32_t e = o.keys[h];
+            if (e == kEmpty) { o.keys[h] = (row << o.kshift) | 1u; return; }
+            if ((e >> o.kshift) == row) { o.keys[h] = e + 1u; return; }
+            h = (h + 1) & o.mask;
+        }
+    }
     for (;;) {
         const uint32_t key = o.keys[h];
         if (key == row) { o.k[h] += 1; return; }
@@ -73,24 +93,36 @@ __device__ __forceinline__ uint32_t pset_value(const TgTables& t, int p, uint32_
     return t.pset_val_node[p] ? t.pset_val_node[p][row] : t.pset_val_class[p][cls];
 }
 
-// Fused per-node pipeline over base (HBM) + overlay (LDS) state.
+// The per-node HBM reads of the pipeline, all independent of each other: the
+// 64-byte record, the (job, tg) collision count and the folded verdict byte.
+struct NodeIn {
+    NodeRec r;
+    uint32_t coll_tg;
+    uint32_t feas;
+};
+
+__device__ __forceinline__ void load_node(const NodeSoA& s, const TgTables& t, uint32_t row, NodeIn& in) {
+    in.r = s.rec[row];
+    in.coll_tg = t.coll_tg[row];
+    in.feas = t.node_feas ? t.node_feas[row] : 1u;
+}
+
+// Fused per-node pipeline over base (HBM) + overlay (dk placements of this eval).
 template <bool kKeepParts>
-__device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
-                                          const Ask& a, const Overlay& ov, const uint32_t* penalty_bits,
-                                          double log10, const double* spread_tab, uint32_t row,
-                                          NodeEval* out) {
-    // one 64-byte record per node: issued together with the per-node verdict
-    const NodeRec r = s.rec[row];
+__device__ __forceinline__ void eval_loaded(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
+                                            const Ask& a, uint32_t dk, const uint32_t* penalty_bits,
+                                            double log10, const double* spread_tab, uint32_t row,
+                                            const NodeIn& in, NodeEval* out) {
+    const NodeRec& r = in.r;
     const uint32_t c = r.cls;
     // FeasibilityWrapper: memoised job + task-group checks (host-resolved per class)
     bool ok;
-    if (t.node_feas) ok = t.node_feas[row] != 0;
+    if (t.node_feas) ok = in.feas != 0;
     else {
         ok = class_ok[c] != 0;
         if (t.node_ok) ok = ok && t.node_ok[row] != 0;
     }
-    const uint32_t dk = ov_count(ov, row);   // placements of this eval on the node
-    const uint32_t coll = t.coll_tg[row] + dk;
+    const uint32_t coll = in.coll_tg + dk;
     // DistinctHostsIterator (feasible.go:569-595)
     if (ok && (a.distinct_job | a.distinct_tg)) {
         if (a.distinct_job && s.coll_job[row] + dk > 0) ok = false;
@@ -156,6 +188,17 @@ __device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, c
     out->status = kOption;
     out->score = sum / (double)k;   // ScoreNormalizationIterator (rank.go:762-767)
     out->nscores = k;
+}
+
+template <bool kKeepParts>
+__device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
+                                          const Ask& a, const Overlay& ov, const uint32_t* penalty_bits,
+                                          double log10, const double* spread_tab, uint32_t row,
+                                          NodeEval* out) {
+    NodeIn in;
+    load_node(s, t, row, in);
+    eval_loaded<kKeepParts>(s, t, class_ok, a, ov_count(ov, row), penalty_bits, log10, spread_tab, row, in,
+                            out);
 }
 
 // evenSpreadScoreBoost (spread.go:178-228) / target boost (spread.go:143-164)
@@ -227,6 +270,16 @@ struct LoopShared {
 template <int BLOCK>
 __device__ __forceinline__ void block_sync() {
     if constexpr (BLOCK > 64) __syncthreads();
+}
+
+// Ordering point for a single-wave workgroup: one wave's LDS operations execute
+// in program order, so a wavefront-scope fence (a compiler barrier, no waits)
+// is all the cross-lane hand-off through LDS needs. Unlike __syncthreads it
+// does not drain outstanding global stores.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m, int lane) {
@@ -303,6 +356,62 @@ __device__ __forceinline__ void commit_overlay(const NodeSoA& s, const TgTables&
             const uint32_t v = pset_value(t, p, row, c);
             if (v != kMissing) counts[p * kMaxValues + v] += 1;
         }
+    }
+}
+
+// Result records of placement `it` of evaluation e (one lane).
+__device__ __forceinline__ void emit_placement(const BatchArgs& A, const uint8_t* class_ok, const Overlay& ov,
+                                            const double* spread_tab, uint32_t e, uint32_t it, int win_row,
+                                            double best_score, uint32_t consumed, uint32_t n_filtered,
+                                            uint32_t n_exhausted, uint32_t new_offset) {
+    if (A.full_out) {
+        pe_ranked_node& o = A.full_out[(size_t)e * A.count + it];
+        o.row = win_row;
+        o.nodes_evaluated = consumed;
+        o.nodes_filtered = n_filtered;
+        o.nodes_exhausted = n_exhausted;
+        o.new_offset = new_offset;
+        o.final_score = 0.0;
+        o.n_scores = 0;
+        for (int k = 0; k < PE_MAX_SCORES; k++) o.scores[k] = 0.0;
+        if (win_row >= 0) {
+            NodeEval ev;
+            eval_node<true>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab,
+                            (uint32_t)win_row, &ev);
+            o.final_score = ev.score;
+            o.n_scores = ev.nscores;
+            for (int k = 0; k < (int)ev.nscores && k < PE_MAX_SCORES; k++) o.scores[k] = ev.parts[k];
+        }
+    }
+    if (A.out) {
+        pe_placement& o = A.out[(size_t)e * A.count + it];
+        o.row = win_row;
+        o.nodes_evaluated = consumed;
+        o.final_score = win_row >= 0 ? best_score : 0.0;
+    }
+}
+
+// Merge an evaluation's overlay into the HBM SoA (the stack's plan persists).
+template <int BLOCK, bool FULL>
+__device__ void writeback_overlay(const BatchArgs& A, const Overlay& ov, uint32_t H, const uint32_t* counts) {
+    for (uint32_t h = threadIdx.x; h < H; h += BLOCK) {
+        const uint32_t e = ov.keys[h];
+        if (e == kEmpty) continue;
+        const uint32_t row = ov.k ? e : e >> ov.kshift;
+        const uint32_t k = ov.k ? ov.k[h] : e & ov.kmask;
+        NodeRec& r = A.soa.rec[row];
+        r.used_cpu += (int64_t)k * A.ask.cpu;
+        r.used_mem += (int64_t)k * A.ask.mem;
+        r.used_disk += (int64_t)k * A.ask.disk;
+        r.used_mbits += (int32_t)k * A.ask.commit_mbits;
+        r.used_dyn += (int32_t)k * A.ask.commit_dyn;
+        A.soa.coll_job[row] += k;
+        A.tg.coll_tg[row] += k;
+    }
+    if constexpr (FULL) {
+        for (int q = 0; q < A.tg.n_psets; q++)
+            for (int v = threadIdx.x; v < A.tg.pset_nvals[q]; v += BLOCK)
+                A.tg.pset_counts[q][v] = counts[q * kMaxValues + v];
     }
 }
 
@@ -429,31 +538,8 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
         uint32_t no = n ? offset + (consumed % n) : 0u;
         if (no >= n) no -= n;
         if (tid == 0) {
-            if (A.full_out) {
-                pe_ranked_node& o = A.full_out[(size_t)e * A.count + it];
-                o.row = win_row;
-                o.nodes_evaluated = consumed;
-                o.nodes_filtered = n_filtered;
-                o.nodes_exhausted = n_exhausted;
-                o.new_offset = no;
-                o.final_score = 0.0;
-                o.n_scores = 0;
-                for (int k = 0; k < PE_MAX_SCORES; k++) o.scores[k] = 0.0;
-                if (win_row >= 0) {
-                    NodeEval ev;
-                    eval_node<true>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab,
-                                    (uint32_t)win_row, &ev);
-                    o.final_score = ev.score;
-                    o.n_scores = ev.nscores;
-                    for (int k = 0; k < (int)ev.nscores && k < PE_MAX_SCORES; k++) o.scores[k] = ev.parts[k];
-                }
-            }
-            if (A.out) {
-                pe_placement& o = A.out[(size_t)e * A.count + it];
-                o.row = win_row;
-                o.nodes_evaluated = consumed;
-                o.final_score = win_row >= 0 ? best_score : 0.0;
-            }
+            emit_placement(A, class_ok, ov, spread_tab, e, it, win_row, best_score, consumed, n_filtered,
+                           n_exhausted, no);
             if (win_row >= 0 && A.commit) commit_overlay(A.soa, A.tg, ov, counts, (uint32_t)win_row);
         }
         offset = no;
@@ -465,26 +551,204 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
         A.eval_status[2 * e] = placed;
         A.eval_status[2 * e + 1] = offset;
     }
-    if (A.writeback) {
-        // merge the overlay into the HBM SoA: the stack's plan persists
-        for (uint32_t h = tid; h < H; h += BLOCK) {
-            const uint32_t row = ov.keys[h];
-            if (row == kEmpty) continue;
-            const uint32_t k = ov.k[h];
-            NodeRec& r = A.soa.rec[row];
-            r.used_cpu += (int64_t)k * A.ask.cpu;
-            r.used_mem += (int64_t)k * A.ask.mem;
-            r.used_disk += (int64_t)k * A.ask.disk;
-            r.used_mbits += (int32_t)k * A.ask.commit_mbits;
-            r.used_dyn += (int32_t)k * A.ask.commit_dyn;
-            A.soa.coll_job[row] += k;
-            A.tg.coll_tg[row] += k;
+    if (A.writeback) writeback_overlay<BLOCK, FULL>(A, ov, H, counts);
+}
+
+// Windowed count loop (limit < n: no affinities or spreads, so a node's result
+// depends only on the snapshot and its own overlay count). One wave per
+// evaluation. Each placement pulls ~limit + filtered positions but a wave
+// evaluates 64 at a time, so the wave keeps a 128-position ring of evaluated
+// visit positions in registers (slot s of lane l = ring index 64 s + l) and
+// evaluates a chunk only when the pull runs past the cache. Committing the
+// winner changes only that node's overlay count: the cache is cut at the first
+// cached position holding the winner's row (only reachable when the visit list
+// wraps inside the ring, n < 128). Chunks are aligned to the ring so every lane
+// reads its own registers; the LimitIterator / MaxScoreIterator closed form is
+// the same ballot logic as k_place.
+__global__ void __launch_bounds__(64) k_window(BatchArgs A) {
+    __shared__ double aside_score[kMaxSkip];
+    __shared__ int aside_pos[kMaxSkip];
+    __shared__ pe_placement stage[64];
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+    const int lane = threadIdx.x;
+    const uint32_t e = blockIdx.x;
+    const uint32_t n = A.n_visit;
+    const uint32_t* perm = A.perms + (size_t)e * A.perm_stride;
+    const uint8_t* class_ok = A.tg.class_ok + (size_t)e * A.class_ok_stride;
+    const uint32_t H = 1u << A.hash_bits;
+    Overlay ov;
+    ov.bits = A.hash_bits;
+    ov.mask = H - 1;
+    ov.keys = reinterpret_cast<uint32_t*>(dyn_smem);
+    ov.k = A.packed_overlay ? nullptr : ov.keys + H;
+    ov.kshift = A.packed_overlay;
+    ov.kmask = A.packed_overlay ? (1u << A.packed_overlay) - 1u : 0u;
+    for (uint32_t i = lane; i < H; i += 64) ov.keys[i] = kEmpty;
+    __syncthreads();
+
+    uint32_t offset = A.offsets ? A.offsets[e] : A.offset0;
+    if (n) offset %= n;
+    uint32_t placed = 0;
+    int st0 = kFiltered, st1 = kFiltered;
+    double sc0 = 0.0, sc1 = 0.0;
+    uint32_t rw0 = kEmpty, rw1 = kEmpty;
+    uint32_t rb = 0;     // ring index of the cursor
+    uint32_t have = 0;   // relative positions [0, have) are cached (have <= min(n, 128) at loop top)
+
+    for (uint32_t it = 0; it < A.count; it++) {
+        uint32_t r = 0, a = 0;
+        double best_score = -__builtin_inf();
+        int best_pos = -1;
+        uint32_t n_filtered = 0, n_exhausted = 0;
+        uint32_t consumed = n;
+        bool stopped = false;
+        double lbest_s = -__builtin_inf();
+        int lbest_p = -1;
+        const uint32_t skew = rb & 63u;
+        for (uint32_t k = 0; 64u * k < n + skew; k++) {
+            const int j = (int)(64u * k + (uint32_t)lane) - (int)skew;   // relative visit position
+            const bool valid = j >= 0 && (uint32_t)j < n;
+            const bool s1 = (((rb >> 6) + k) & 1u) != 0;
+            int st = s1 ? st1 : st0;
+            double sc = s1 ? sc1 : sc0;
+            const bool need = valid && (uint32_t)j >= have;
+            if (__ballot(need)) {
+                // The pull ran past the cache: evaluate this chunk and the next
+                // one (every position >= have is uncached), all loads in flight
+                // before any compute.
+                const uint32_t j2 = (uint32_t)(j + 64);
+                const bool need2 = j2 < n;
+                uint32_t p1 = need ? offset + (uint32_t)j : 0u;
+                uint32_t p2 = need2 ? offset + j2 : 0u;
+                if (p1 >= n) p1 -= n;
+                if (p2 >= n) p2 -= n;
+                const uint32_t row1 = perm[p1], row2 = perm[p2];
+                NodeIn in1, in2;
+                load_node(A.soa, A.tg, row1, in1);
+                load_node(A.soa, A.tg, row2, in2);
+                const uint32_t dk1 = ov_count(ov, row1), dk2 = ov_count(ov, row2);
+                NodeEval e1, e2;
+                e1.score = 0.0;
+                e2.score = 0.0;
+                eval_loaded<false>(A.soa, A.tg, class_ok, A.ask, dk1, A.penalty_bits, A.log10, nullptr, row1, in1,
+                                   &e1);
+                eval_loaded<false>(A.soa, A.tg, class_ok, A.ask, dk2, A.penalty_bits, A.log10, nullptr, row2, in2,
+                                   &e2);
+                if (need) {
+                    st = e1.status;
+                    sc = e1.score;
+                    if (s1) { st1 = st; sc1 = sc; rw1 = row1; } else { st0 = st; sc0 = sc; rw0 = row1; }
+                }
+                if (need2) {
+                    if (s1) { st0 = e2.status; sc0 = e2.score; rw0 = row2; }
+                    else { st1 = e2.status; sc1 = e2.score; rw1 = row2; }
+                }
+                have = min(64u * (k + 2) - skew, n);
+            }
+
+            const bool is_opt = valid && st == kOption;
+            const bool is_np = is_opt && sc <= 0.0;
+            uint32_t np_tot;
+            const uint32_t np_before = a + block_prefix<64>(is_np, nullptr, &np_tot);
+            const bool aside = is_np && np_before < (uint32_t)kMaxSkip;
+            const bool ret = is_opt && !aside;
+            uint32_t ret_tot;
+            const uint32_t ret_before = r + block_prefix<64>(ret, nullptr, &ret_tot);
+            const uint64_t sm = __ballot(ret && ret_before == A.limit - 1u);
+            const int stop_lane = sm ? (int)__ffsll((long long)sm) - 1 : 64;
+            const bool pulled = valid && lane <= stop_lane;
+            if (aside && pulled) {
+                aside_score[np_before] = sc;
+                aside_pos[np_before] = j;
+            }
+            // lane-local first strict maximum; positions grow with the chunk,
+            // so one wave reduction per placement suffices
+            if (ret && ret_before < A.limit && sc > lbest_s) { lbest_s = sc; lbest_p = j; }
+            if (A.full_out) {
+                n_filtered += (uint32_t)__popcll(__ballot(pulled && st == kFiltered));
+                n_exhausted += (uint32_t)__popcll(__ballot(pulled && st == kExhausted));
+            }
+            a += (uint32_t)__popcll(__ballot(aside && pulled));
+            if (sm) {
+                consumed = 64u * k + (uint32_t)stop_lane - skew + 1u;
+                r = A.limit;
+                stopped = true;
+                break;
+            }
+            r += ret_tot;
         }
-        if constexpr (FULL) {
-            for (int q = 0; q < A.tg.n_psets; q++)
-                for (int v = tid; v < A.tg.pset_nvals[q]; v += BLOCK) A.tg.pset_counts[q][v] = counts[q * kMaxValues + v];
+        {
+            double cs;
+            int cp;
+            block_argmax<64>(lbest_p >= 0, lbest_s, lbest_p, nullptr, nullptr, &cs, &cp);
+            if (cp != 0x7FFFFFFF) { best_score = cs; best_pos = cp; }
         }
+        if (!stopped) {
+            const uint32_t take = min(a, A.limit - r);
+            for (uint32_t i = 0; i < take; i++) {
+                if (aside_score[i] > best_score) { best_score = aside_score[i]; best_pos = aside_pos[i]; }
+            }
+        }
+        int win_row = -1;
+        if (best_pos >= 0) {
+            if (best_pos + 128 >= (int)have) {
+                // still in the ring: positions [have - 128, have) are intact
+                const uint32_t idx = (rb + (uint32_t)best_pos) & 127u;
+                win_row = __shfl((int)((idx & 64u) ? rw1 : rw0), (int)(idx & 63u));
+            } else {
+                uint32_t pos = offset + (uint32_t)best_pos;
+                if (pos >= n) pos -= n;
+                win_row = (int)perm[pos];
+            }
+        }
+        uint32_t no = n ? offset + (consumed % n) : 0u;
+        if (no >= n) no -= n;
+        if (lane == 0) {
+            if (A.full_out)
+                emit_placement(A, class_ok, ov, nullptr, e, it, win_row, best_score, consumed, n_filtered,
+                               n_exhausted, no);
+            pe_placement& o = stage[it & 63u];
+            o.row = win_row;
+            o.nodes_evaluated = consumed;
+            o.final_score = win_row >= 0 ? best_score : 0.0;
+            if (win_row >= 0 && A.commit) ov_add(ov, (uint32_t)win_row);
+        }
+        wave_sync();
+        // compact records leave in 1 KB wave stores (possibly straight into
+        // mapped host memory, so the transfer overlaps the count loop)
+        if (A.out && ((it & 63u) == 63u || win_row < 0 || it + 1 == A.count)) {
+            const uint32_t fill = (it & 63u) + 1u;
+            if ((uint32_t)lane < fill)
+                A.out[(size_t)e * A.count + (it + 1u - fill) + lane] = stage[lane];
+        }
+        offset = no;
+        // slide the cache: a full pass (no stop) leaves the cursor in place but
+        // the ring is keyed by unwrapped position, so it restarts empty
+        if (stopped) {
+            rb = (rb + consumed) & 127u;
+            have = have > consumed ? have - consumed : 0u;
+        } else {
+            have = 0;
+        }
+        if (win_row >= 0 && A.commit && have) {
+            const uint32_t j0 = ((uint32_t)lane - rb) & 127u, j1 = (64u + (uint32_t)lane - rb) & 127u;
+            const bool bad0 = j0 < have && rw0 == (uint32_t)win_row;
+            const bool bad1 = j1 < have && rw1 == (uint32_t)win_row;
+            if (__ballot(bad0 || bad1)) {
+                uint32_t cut = min(bad0 ? j0 : 128u, bad1 ? j1 : 128u);
+                for (int off = 32; off > 0; off >>= 1) cut = min(cut, (uint32_t)__shfl_xor((int)cut, off));
+                if (cut < have) have = cut;
+            }
+        }
+        wave_sync();
+        if (win_row < 0) break;
+        placed++;
     }
+    if (lane == 0) {
+        A.eval_status[2 * e] = placed;
+        A.eval_status[2 * e + 1] = offset;
+    }
+    if (A.writeback) writeback_overlay<64, false>(A, ov, H, nullptr);
 }
 
 // SystemStack: every list entry is an independent single-node Select.
@@ -606,47 +870,94 @@ __device__ __host__ __forceinline__ uint32_t rec_winner(const SweepRec& r) {
     return r.max_rank[0];
 }
 
+__device__ __forceinline__ SweepRec rec_shfl_xor(const SweepRec& r, int off) {
+    SweepRec o;
+    o.max_score = __shfl_xor(r.max_score, off);
+#pragma unroll
+    for (int i = 0; i < 4; i++) o.max_rank[i] = (uint32_t)__shfl_xor((int)r.max_rank[i], off);
+#pragma unroll
+    for (int i = 0; i < kMaxSkip; i++) {
+        o.np_rank[i] = (uint32_t)__shfl_xor((int)r.np_rank[i], off);
+        o.np_score[i] = __shfl_xor(r.np_score[i], off);
+    }
+    o.options = (uint32_t)__shfl_xor((int)r.options, off);
+    o.filtered = (uint32_t)__shfl_xor((int)r.filtered, off);
+    o.exhausted = (uint32_t)__shfl_xor((int)r.exhausted, off);
+    o._pad = 0;
+    return o;
+}
+
+// Block reduction of per-thread records; the merge is commutative and
+// associative over disjoint row sets, so an xor butterfly inside each wave is
+// exact. Thread 0 returns the block's record.
+template <int BLOCK>
+__device__ __forceinline__ void rec_block_reduce(SweepRec& r, SweepRec* red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const SweepRec o = rec_shfl_xor(r, off);
+        rec_merge(r, o);
+    }
+    constexpr int W = BLOCK / 64;
+    if constexpr (W > 1) {
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        if (lane == 0) red[wid] = r;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 1; w < W; w++) rec_merge(r, red[w]);
+    }
+}
+
+// One pass of the scoring sweep over rows [row_begin, row_end): per-thread
+// records over a grid-stride slice, reduced per workgroup. Software-pipelined:
+// the next row's visit rank, 64-byte record, collision count and verdict are in
+// flight while the current row's fp64 scoring runs, so HBM streaming and the
+// two software Pow evaluations overlap inside every wave. Rows outside the
+// visit list are evaluated and dropped.
 template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK) k_sweep(SweepArgs A) {
-    __shared__ SweepRec red[BLOCK];
+    __shared__ SweepRec red[BLOCK / 64];
     SweepRec r;
     rec_init(r);
-    Overlay none;
-    none.keys = nullptr;
     const uint32_t n = A.n_visit;
-    for (uint32_t row = A.row_begin + blockIdx.x * BLOCK + threadIdx.x; row < A.row_end;
-         row += gridDim.x * BLOCK) {
-        const uint32_t pos = A.rank_of[row];
-        if (pos == 0xFFFFFFFFu) continue;
+    const uint32_t stride = gridDim.x * BLOCK;
+    uint32_t row = A.row_begin + blockIdx.x * BLOCK + threadIdx.x;
+    NodeIn nxt;
+    uint32_t nxt_pos = 0xFFFFFFFFu;
+    if (row < A.row_end) {
+        nxt_pos = A.rank_of[row];
+        load_node(A.soa, A.tg, row, nxt);
+    }
+    for (; row < A.row_end; row += stride) {
+        const NodeIn cur = nxt;
+        const uint32_t pos = nxt_pos;
+        const uint32_t ahead = row + stride;
+        if (ahead < A.row_end && ahead > row) {
+            nxt_pos = A.rank_of[ahead];
+            load_node(A.soa, A.tg, ahead, nxt);
+        }
         NodeEval ev;
-        eval_node<false>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, A.spread_tab, row, &ev);
+        ev.score = 0.0;
+        eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, A.penalty_bits, A.log10, A.spread_tab, row, cur,
+                           &ev);
+        if (pos == 0xFFFFFFFFu) continue;
         if (ev.status == kFiltered) { r.filtered++; continue; }
         if (ev.status == kExhausted) { r.exhausted++; continue; }
         const uint32_t rank = pos >= A.offset ? pos - A.offset : pos + n - A.offset;
         rec_add(r, rank, ev.score);
     }
-    red[threadIdx.x] = r;
-    __syncthreads();
-    for (int s = BLOCK / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) rec_merge(red[threadIdx.x], red[threadIdx.x + s]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) A.recs[blockIdx.x] = red[0];
+    rec_block_reduce<BLOCK>(r, red);
+    if (threadIdx.x == 0) A.recs[blockIdx.x] = r;
 }
 
-// Merge the per-workgroup records (one workgroup).
-__global__ void __launch_bounds__(256) k_sweep_merge(const SweepRec* recs, uint32_t count, SweepRec* out) {
-    __shared__ SweepRec red[256];
+// Merge the per-workgroup records (one 512-thread workgroup: a few records per
+// thread, so the dependent load chain stays short).
+__global__ void __launch_bounds__(512) k_sweep_merge(const SweepRec* recs, uint32_t count, SweepRec* out) {
+    __shared__ SweepRec red[8];
     SweepRec r;
     rec_init(r);
-    for (uint32_t i = threadIdx.x; i < count; i += 256) rec_merge(r, recs[i]);
-    red[threadIdx.x] = r;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) rec_merge(red[threadIdx.x], red[threadIdx.x + s]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *out = red[0];
+    for (uint32_t i = threadIdx.x; i < count; i += 512) rec_merge(r, recs[i]);
+    rec_block_reduce<512>(r, red);
+    if (threadIdx.x == 0) *out = r;
 }
 
 // Spread contribution table in HBM for the sweep path (same code as the
@@ -686,19 +997,19 @@ __global__ void __launch_bounds__(256) k_fold_feas(NodeSoA s, const uint8_t* cla
 }  // namespace pe
 
 // ---- launch wrappers (host) ------------------------------------------------
-size_t pe_place_lds_bytes(bool full, int hash_bits, bool net) {
-    (void)net;
-    size_t b = (size_t)2 * 4u * ((size_t)1 << hash_bits);
+size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed) {
+    size_t b = (size_t)(packed ? 4u : 8u) * ((size_t)1 << hash_bits);
     if (full) b += sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1) + 4u * pe::kMaxPsets * pe::kMaxValues;
     return b;
 }
 
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st) {
-    const size_t lds = pe_place_lds_bytes(full, a->hash_bits, a->net_overlay != 0);
+    if (full && a->packed_overlay) return hipErrorInvalidValue;   // packed entries: windowed kernel only
+    const size_t lds = pe_place_lds_bytes(full, a->hash_bits, a->packed_overlay != 0);
     if (full) {
         hipLaunchKernelGGL((pe::k_place<256, true>), dim3(n_evals), dim3(256), lds, st, *a);
     } else {
-        hipLaunchKernelGGL((pe::k_place<64, false>), dim3(n_evals), dim3(64), lds, st, *a);
+        hipLaunchKernelGGL(pe::k_window, dim3(n_evals), dim3(64), lds, st, *a);
     }
     return hipGetLastError();
 }
@@ -728,8 +1039,15 @@ hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, co
 
 hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec* merged, hipStream_t st) {
     hipLaunchKernelGGL((pe::k_sweep<256>), dim3(blocks), dim3(256), 0, st, *a);
-    hipLaunchKernelGGL(pe::k_sweep_merge, dim3(1), dim3(256), 0, st, (const pe::SweepRec*)a->recs, blocks, merged);
+    hipLaunchKernelGGL(pe::k_sweep_merge, dim3(1), dim3(512), 0, st, (const pe::SweepRec*)a->recs, blocks, merged);
     return hipGetLastError();
+}
+
+// Resident k_sweep<256> workgroups per CU (grid = one full wave of residency).
+int pe_sweep_blocks_per_cu() {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pe::k_sweep<256>, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+    return nb;
 }
 
 hipError_t pe_launch_node_record(const pe::SweepArgs* a, uint32_t row, pe_ranked_node* out, hipStream_t st) {

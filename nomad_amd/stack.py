@@ -54,6 +54,11 @@ def load_engine():
         lib.pe_stage_orders.argtypes = [C.c_void_p, abi.u32p, C.c_uint32, C.c_uint32]
         lib.pe_place_batch.restype = C.c_int
         lib.pe_place_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(abi.pe_placement), abi.u32p]
+        lib.pe_batch_results.restype = C.c_int
+        lib.pe_batch_results.argtypes = [C.c_void_p, C.POINTER(C.POINTER(abi.pe_placement)),
+                                         C.POINTER(abi.u32p), abi.u32p, abi.u32p]
+        lib.pe_last_phase_ms.restype = None
+        lib.pe_last_phase_ms.argtypes = [C.c_void_p, abi.f64p]
         _engine = lib
     return _engine
 
@@ -258,16 +263,39 @@ class GenericStack(_Stack):
         self._check(self._lib.pe_stage_orders(self._h, o.ctypes.data_as(abi.u32p), o.shape[0], o.shape[1]))
         self._staged = o.shape[0]
 
-    def PlaceBatch(self, tg, count: int):
-        """Independent evaluations over the staged orders; returns (rows, scores, evaluated, placed)."""
-        E = self._staged
-        out = np.zeros(max(1, E * count), dtype=[("row", "<i4"), ("nodes_evaluated", "<u4"), ("final_score", "<f8")])
-        placed = np.zeros(max(1, E), dtype=np.uint32)
-        self._check(self._lib.pe_place_batch(self._h, self._tg_index(tg), count,
-                                             out.ctypes.data_as(C.POINTER(abi.pe_placement)),
-                                             placed.ctypes.data_as(abi.u32p)))
-        out = out[:E * count].reshape(E, count)
-        return out["row"], out["final_score"], out["nodes_evaluated"], placed[:E]
+    _PLACEMENT = np.dtype([("row", "<i4"), ("nodes_evaluated", "<u4"), ("final_score", "<f8")])
+
+    def PlaceBatch(self, tg, count: int, copy: bool = True):
+        """Independent evaluations over the staged orders; returns (rows, scores, evaluated, placed).
+
+        copy=False returns views of the engine's page-locked result buffer
+        (valid until the next PlaceBatch) instead of copies."""
+        self._check(self._lib.pe_place_batch(self._h, self._tg_index(tg), count, None, None))
+        res = C.POINTER(abi.pe_placement)()
+        status = abi.u32p()
+        n_evals, cnt = C.c_uint32(0), C.c_uint32(0)
+        self._check(self._lib.pe_batch_results(self._h, C.byref(res), C.byref(status), C.byref(n_evals),
+                                               C.byref(cnt)))
+        E = n_evals.value
+        total = E * count
+        if total:
+            raw = np.ctypeslib.as_array(C.cast(res, C.POINTER(C.c_uint8)), shape=(total * 16,))
+            out = raw.view(self._PLACEMENT).reshape(E, count)
+            st = np.ctypeslib.as_array(status, shape=(2 * E,))
+            placed = st[0::2]
+        else:
+            out = np.zeros((E, count), dtype=self._PLACEMENT)
+            placed = np.zeros(E, dtype=np.uint32)
+        if copy:
+            out = out.copy()
+            placed = placed.copy()
+        return out["row"], out["final_score"], out["nodes_evaluated"], placed
+
+    def last_phase_ms(self):
+        """[host prep, kernel, D2H copy, total] of the last PlaceBatch, ms."""
+        buf = (C.c_double * 4)()
+        self._lib.pe_last_phase_ms(self._h, C.cast(buf, abi.f64p))
+        return list(buf)
 
     def last_kernel_ms(self) -> float:
         return self._lib.pe_last_kernel_ms(self._h)

@@ -37,7 +37,8 @@ def test_c1_mock_nodes_count10():
     assert_same_placements(re, ro)
 
 
-@pytest.mark.parametrize("n,count,seed", [(1000, 300, 3), (10000, 1000, 1)])
+@pytest.mark.parametrize("n,count,seed", [(1000, 300, 3), (10000, 1000, 1), (64, 150, 5), (65, 150, 6),
+                                          (130, 300, 7), (200, 700, 8)])
 def test_c2_binpack_windowed(n, count, seed):
     nodes, allocs = synth.cluster_c2(n, seed=42)
     job = synth.job_c2(count)
@@ -151,6 +152,39 @@ def test_batch_evals_match_single_eval_oracle(cfg):
         for i, r in enumerate(ro):
             assert rows[k, i] == r.row, (k, i)
             assert evaluated[k, i] == r.nodes_evaluated, (k, i)
+            if r.row >= 0:
+                assert scores[k, i] == r.final_score, (k, i)
+
+
+def test_batch_result_paths_agree(monkeypatch):
+    """Windowed batch records streamed into mapped host memory (64-record LDS
+    flushes, ragged tail, early nil stop) equal the device-buffer + copy path
+    and the oracle."""
+    nodes, allocs = synth.cluster_c2(12, seed=12)
+    job = synth.job_c2(1000)          # exhausts the cluster mid-way: nil option ends each eval
+    E = 5
+    orders = np.stack([synth.shuffle(len(nodes), 300 + e) for e in range(E)])
+    res = []
+    for via_copy in ("0", "1"):
+        monkeypatch.setenv("PE_RESULTS_VIA_COPY", via_copy)
+        e = engine_generic()
+        e.SetState(nodes, allocs)
+        e.SetJob(job)
+        e.StageOrders(orders)
+        res.append(e.PlaceBatch(0, 1000))
+        e.close()
+    assert np.array_equal(res[0][3], res[1][3])
+    for k in range(E):   # records past the nil stop are undefined
+        m = min(int(res[0][3][k]) + 1, 1000)
+        for a, b in zip(res[0][:3], res[1][:3]):
+            assert np.array_equal(a[k, :m], b[k, :m])
+    rows, scores, evaluated, placed = res[0]
+    for k in range(E):
+        _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, orders[k])
+        got = int(placed[k])
+        assert got == sum(1 for r in ro if r.row >= 0) and 0 < got < 1000
+        for i, r in enumerate(ro):
+            assert rows[k, i] == r.row and evaluated[k, i] == r.nodes_evaluated, (k, i)
             if r.row >= 0:
                 assert scores[k, i] == r.final_score, (k, i)
 
