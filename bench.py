@@ -202,7 +202,7 @@ def main():
     for i in range(5):
         lat.ResetPlan()
         lat.SetJob(job)
-        lat.SetNodes(orders[i])
+        lat.SetNodes(orders[i % E])
         t1 = time.perf_counter()
         lat.PlaceArrays(0, args.count)
         lat_times.append(time.perf_counter() - t1)

@@ -44,6 +44,10 @@ hipError_t pe_launch_node_record(const pe::SweepArgs* a, uint32_t row, pe_ranked
 hipError_t pe_launch_spread_table(const pe::TgTables* t, double* tab, hipStream_t st);
 uint32_t pe_rec_winner(const pe::SweepRec* r);
 int pe_sweep_blocks_per_cu();
+uint32_t pe_chain_max_n();
+size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n);
+int pe_chain_blocks_per_cu(size_t lds);
+hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st);
 
 namespace {
 
@@ -253,6 +257,11 @@ struct pe_stack {
     double phase_ms[4] = {0, 0, 0, 0};   // host prep, kernels, result copy, total (last batch)
     std::vector<pe::NodeRec> h_base_rec;     // snapshot proposed state (no plan)
     DevMem d_rec, d_base_rec, d_coll_job;
+    DevMem d_base;                     // windowed loops: per-row base value table
+    bool orders_unique = true;         // every staged order lists each row at most once
+    bool use_base = true;              // PE_WINDOW_LAZY=1: lazy per-position evaluation (k_window)
+    bool batch_chain = false;          // the prepared batch runs k_base + k_chain
+    uint32_t chain_grid = 256;
     bool have_state = false;
 
     // job
@@ -1081,6 +1090,21 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     }
     A.hash_bits = hash_bits_for(count, full);
     A.packed_overlay = packed_kbits(s, 1u << A.hash_bits, full);
+    bool chain = false;
+    if (!full && s->use_base && count > 1 && n <= pe_chain_max_n()) {
+        // count loop over one rotation at a time (k_base + k_chain): needs a
+        // visit list without repeated rows
+        std::vector<uint8_t> seen(s->nodes.size(), 0);
+        chain = true;
+        for (uint32_t r : order) {
+            if (seen[r]) { chain = false; break; }
+            seen[r] = 1;
+        }
+        if (chain) {
+            HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));
+            A.base = s->d_base.as<double>();
+        }
+    }
     const uint32_t chunk = std::max<uint32_t>(1, (1u << A.hash_bits) / 2);
     HIP_TRY(s, s->d_out.ensure(sizeof(pe_ranked_node) * std::min(count, chunk)));
     HIP_TRY(s, s->d_status.ensure(16));
@@ -1095,7 +1119,8 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         A.count = c;
         A.offset0 = *new_offset;
         HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-        HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
+        if (chain) HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream));
+        else HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
         HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
         uint32_t st[2];
         HIP_TRY(s, hipMemcpyAsync(st, A.eval_status, sizeof(st), hipMemcpyDeviceToHost, s->stream));
@@ -1148,6 +1173,7 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     s->log10 = pe::gm::log_go(10.0);
     if (const char* e = std::getenv("PE_SWEEP_MIN")) s->sweep_min = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("PE_RESULTS_VIA_COPY")) s->results_via_copy = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PE_WINDOW_LAZY")) s->use_base = std::atoi(e) == 0;
     return s;
 }
 
@@ -1463,6 +1489,18 @@ int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint3
         if (orders[i] >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range in staged order");
     s->h_orders.assign(orders, orders + total);
     HIP_TRY(s, upload(s->d_orders, s->h_orders));
+    {
+        // generation-stamped duplicate check over every staged order
+        std::vector<uint32_t> stamp(s->nodes.size(), 0);
+        s->orders_unique = true;
+        for (uint32_t e = 0; e < n_evals && s->orders_unique; e++) {
+            const uint32_t* o = orders + (size_t)e * n;
+            for (uint32_t i = 0; i < n; i++) {
+                if (stamp[o[i]] == e + 1) { s->orders_unique = false; break; }
+                stamp[o[i]] = e + 1;
+            }
+        }
+    }
     s->staged_evals = n_evals;
     s->staged_n = n;
     return PE_OK;
@@ -1525,6 +1563,15 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
     A.offset0 = 0;
     A.commit = 1;
     A.writeback = 0;
+    s->batch_chain = false;
+    if (!full && s->use_base && A.class_ok_stride == 0 && s->orders_unique && n <= pe_chain_max_n()) {
+        // one base pass shared by every evaluation, then k_chain (persistent grid)
+        HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));
+        A.base = s->d_base.as<double>();
+        s->batch_chain = true;
+        const size_t lds = pe_chain_lds_bytes(A.hash_bits, A.packed_overlay != 0, n);
+        s->chain_grid = (uint32_t)(pe_chain_blocks_per_cu(lds) * s->n_cu);
+    }
     HIP_TRY(s, s->d_batch_out.ensure(sizeof(pe_placement) * (size_t)E * std::max<uint32_t>(count, 1)));
     HIP_TRY(s, s->d_batch_status.ensure(sizeof(uint32_t) * 2 * (size_t)E));
     HIP_TRY(s, s->h_batch_out.ensure(sizeof(pe_placement) * (size_t)E * std::max<uint32_t>(count, 1)));
@@ -1585,7 +1632,8 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
     const pe::BatchArgs& A = s->batch_A;
     const auto t1 = std::chrono::steady_clock::now();
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-    HIP_TRY(s, pe_launch_place(&A, E, s->batch_full, s->stream));
+    if (s->batch_chain) HIP_TRY(s, pe_launch_chain(&A, E, s->chain_grid, s->stream));
+    else HIP_TRY(s, pe_launch_place(&A, E, s->batch_full, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     if (!s->batch_direct) {
         HIP_TRY(s, hipMemcpyAsync(s->h_batch_status.p, A.eval_status, sizeof(uint32_t) * 2 * (size_t)E,

@@ -85,6 +85,11 @@ struct BatchArgs {
     int packed_overlay;           // one u32 per overlay entry: row << 8 | k (rows < 2^24, count <= 255)
     int commit;                 // apply Plan.AppendAlloc after each placement
     int writeback;                // merge the overlay into the HBM SoA at the end
+    // Phase-static windowed loop (k_chain): base[row] = the row's pipeline
+    // result with no placement of this launch on it (finite FinalScore, -inf
+    // filtered, +inf exhausted), computed once per launch by k_base for all
+    // evaluations. Null: the lazy per-position loop (k_window).
+    double* base;
     pe_ranked_node* full_out;     // [n_evals][count] full records, or null
     pe_placement* out;            // [n_evals][count] compact records, or null
     uint32_t* eval_status;        // [n_evals][2]: placed, final cursor

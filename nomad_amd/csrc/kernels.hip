@@ -751,6 +751,437 @@ __global__ void __launch_bounds__(64) k_window(BatchArgs A) {
     if (A.writeback) writeback_overlay<64, false>(A, ov, H, nullptr);
 }
 
+// ---- shared base table ----------------------------------------------------------
+__device__ __forceinline__ double encode_eval(const NodeEval& ev) {
+    return ev.status == kOption ? ev.score : (ev.status == kFiltered ? -__builtin_inf() : __builtin_inf());
+}
+
+// base[row]: the fused pipeline of every row of the snapshot with no placement
+// of this launch on it. It does not depend on the visit order, so one pass
+// serves every evaluation of a batch.
+__global__ void __launch_bounds__(256) k_base(BatchArgs A) {
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t row = blockIdx.x * 256 + threadIdx.x; row < A.soa.n; row += stride) {
+        NodeIn in;
+        load_node(A.soa, A.tg, row, in);
+        NodeEval ev;
+        ev.score = 0.0;
+        eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+        A.base[row] = encode_eval(ev);
+    }
+}
+
+// ---- windowed count loop: phase-static selection ------------------------------
+//
+// Windowed binpack (limit = ceil(log2 n) < n; no affinity or spread) of one
+// evaluation. The value of visit position T (FinalScore, or filtered /
+// exhausted) depends only on the row there and on how many of this
+// evaluation's placements that row holds. A visit list without repeated rows
+// shows a row again only n positions later, and every Select's winner lies
+// behind the next Select's start, so once the cursor is at c the values of all
+// positions [c, c + n) (one rotation) are fixed: no Select that stops inside
+// that window can change them. A *phase* therefore:
+//   1. evaluates the n positions in parallel: base[row] (shared, k_base) or the
+//      row re-evaluated with its placement count from the LDS overlay;
+//   2. scans option / non-positive-option (N) counts into option indices and
+//      nb[k] = N options before option k;
+//   3. resolves the Select boundaries serially but in O(1) per Select: a Select
+//      starting at option i returns every positive option and every N after its
+//      third, so it stops at option i + L - 1 + m for the smallest m in {0,1,2}
+//      with exactly m N's in [i, i + L - 1 + m], else at i + L + 2
+//      (LimitIterator, select.go:35-74);
+//   4. finds every Select's winner at once (first strict maximum over its
+//      returned options: LDS atomicMax on an order-preserving key, then
+//      atomicMin on the option index) and commits the winners to the overlay
+//      (distinct rows within a phase, so the inserts are independent).
+// The next phase starts after the last stop. A Select that cannot stop inside
+// the window ends the phase early; if it is the phase's first one it has seen
+// the whole list: the stream is exhausted, set-aside options are appended
+// (at most `limit` in total) and the cursor stays (feasible.go:90-107).
+constexpr int kChainBlock = 1024;
+constexpr int kChainItems = 16;
+constexpr uint32_t kChainMaxN = kChainBlock * kChainItems;   // positions per phase held in registers
+constexpr int kChainMaxSel = 1024;                            // Selects resolved per phase
+constexpr int kChainTiles = kChainMaxN / 64;
+constexpr uint32_t kChainMaxRedo = 2048;                      // rows re-evaluated per phase (<= placements per launch)
+
+enum : int { kPhaseMore = 0, kPhaseCount = 1, kPhaseExhausted = 2 };
+
+struct ChainShared {
+    uint32_t tile_o[kChainTiles], tile_n[kChainTiles];    // per 64-position tile counts, then exclusive offsets
+    uint32_t sel_b[kChainMaxSel];                          // option index of each Select's stop
+    uint32_t sel_end[kChainMaxSel];                        // its visit position (relative to the phase start)
+    unsigned long long sel_max[kChainMaxSel];              // order-preserving key of the max returned score,
+                                                           // then the winner's FinalScore bits
+    uint32_t sel_arg[kChainMaxSel];                        // option index of the first maximum
+    uint32_t sel_row[kChainMaxSel];                        // the winner's row
+    uint32_t sel_f[kChainMaxSel], sel_x[kChainMaxSel];     // filtered / exhausted positions (metrics)
+    uint2 redo[kChainMaxRedo];                             // (row, placements) to re-evaluate; then the value
+    double aside_v[kMaxSkip];
+    uint32_t aside_row[kMaxSkip];
+    uint32_t tot_o, tot_n, nsel, mode, n_redo;
+};
+
+__device__ __forceinline__ unsigned long long order_key(double x) {
+    const unsigned long long b = (unsigned long long)gm::f2u(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ uint32_t wrap_pos(uint32_t x, uint32_t n) {
+    if (x < n) return x;
+    x -= n;
+    return x < n ? x : x % n;
+}
+
+// Plan.AppendAlloc into the overlay from many threads at once; the rows are
+// distinct, so no two threads race on one key.
+__device__ __forceinline__ void ov_add_atomic(const Overlay& o, uint32_t row) {
+    uint32_t h = ov_hash(o, row);
+    if (!o.k) {
+        const uint32_t fresh = (row << o.kshift) | 1u;
+        for (;;) {
+            uint32_t e = o.keys[h];
+            if (e == kEmpty) {
+                e = atomicCAS(&o.keys[h], kEmpty, fresh);
+                if (e == kEmpty) return;
+            }
+            if ((e >> o.kshift) == row) { atomicAdd(&o.keys[h], 1u); return; }
+            h = (h + 1) & o.mask;
+        }
+    }
+    for (;;) {
+        uint32_t key = o.keys[h];
+        if (key == kEmpty) {
+            key = atomicCAS(&o.keys[h], kEmpty, row);
+            if (key == kEmpty) { atomicAdd(&o.k[h], 1u); return; }
+        }
+        if (key == row) { atomicAdd(&o.k[h], 1u); return; }
+        h = (h + 1) & o.mask;
+    }
+}
+
+// first index s in [0, cnt) with a[s] >= x (a ascending; cnt if none)
+__device__ __forceinline__ uint32_t lower_bound_lds(const uint32_t* a, uint32_t cnt, uint32_t x) {
+    uint32_t lo = 0, hi = cnt;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Register state per position q of a thread: option index (14 bits) and, until
+// the Select ids are known, the N-option prefix (14 bits); afterwards the
+// Select id (10 bits) in the high half.
+constexpr uint32_t kIdxBits = 14, kIdxMask = (1u << kIdxBits) - 1u;
+
+__global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_evals) {
+    static_assert(kChainMaxN <= (1u << kIdxBits), "option index packing");
+    static_assert(kChainMaxSel <= (1 << (32 - 2 * kIdxBits + kIdxBits)), "select id packing");
+    __shared__ ChainShared sh;
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t n = A.n_visit;
+    const uint32_t L = A.limit;
+    const uint32_t H = 1u << A.hash_bits;
+    Overlay ov;
+    ov.bits = A.hash_bits;
+    ov.mask = H - 1;
+    ov.keys = reinterpret_cast<uint32_t*>(dyn_smem);
+    ov.k = A.packed_overlay ? nullptr : ov.keys + H;
+    ov.kshift = A.packed_overlay;
+    ov.kmask = A.packed_overlay ? (1u << A.packed_overlay) - 1u : 0u;
+    uint16_t* nb = reinterpret_cast<uint16_t*>(ov.keys + (A.packed_overlay ? H : 2 * H));   // [n + 1]
+
+    for (uint32_t e = blockIdx.x; e < n_evals; e += gridDim.x) {
+        const uint32_t* __restrict__ perm = A.perms + (size_t)e * A.perm_stride;
+        for (uint32_t i = tid; i < H; i += kChainBlock) {
+            ov.keys[i] = kEmpty;
+            if (ov.k) ov.k[i] = 0;
+        }
+        uint32_t cur = wrap_pos(A.offsets ? A.offsets[e] : A.offset0, n);
+        uint32_t placed = 0;
+        bool done = n == 0 || A.count == 0;
+        if (n == 0 && A.count && tid == 0 && A.out) {
+            pe_placement& o = A.out[(size_t)e * A.count];
+            o.row = -1; o.nodes_evaluated = 0; o.final_score = 0.0;
+        }
+        __syncthreads();
+        while (!done) {
+            // 1. values of the window [cur, cur + n): base, or queued for re-evaluation
+            uint32_t row[kChainItems];
+            double v[kChainItems];
+            if (tid == 0) sh.n_redo = 0;
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                row[q] = j < n ? perm[wrap_pos(cur + j, n)] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                v[q] = j < n ? A.base[row[q]] : -__builtin_inf();
+            }
+            __syncthreads();
+            uint32_t redo_mask = 0;
+            if (placed) {
+#pragma unroll
+                for (int q = 0; q < kChainItems; q++) {
+                    const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                    const uint32_t dk = j < n ? ov_count(ov, row[q]) : 0u;
+                    if (dk) {
+                        const uint32_t slot = atomicAdd(&sh.n_redo, 1u);
+                        sh.redo[slot] = make_uint2(row[q], dk);
+                        v[q] = gm::u2f((unsigned long long)slot);   // slot index until the value is back
+                        redo_mask |= 1u << q;
+                    }
+                }
+                __syncthreads();
+                const uint32_t nr = sh.n_redo;
+                for (uint32_t w = tid; w < nr; w += kChainBlock) {
+                    const uint2 rd = sh.redo[w];
+                    NodeIn in;
+                    load_node(A.soa, A.tg, rd.x, in);
+                    NodeEval ev;
+                    ev.score = 0.0;
+                    eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, rd.y, A.penalty_bits, A.log10, nullptr,
+                                       rd.x, in, &ev);
+                    const unsigned long long bits = (unsigned long long)gm::f2u(encode_eval(ev));
+                    sh.redo[w] = make_uint2((uint32_t)bits, (uint32_t)(bits >> 32));
+                }
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < kChainItems; q++) {
+                    if ((redo_mask >> q) & 1u) {
+                        const uint2 r2 = sh.redo[(uint32_t)gm::f2u(v[q])];
+                        v[q] = gm::u2f(((unsigned long long)r2.y << 32) | r2.x);
+                    }
+                }
+            }
+            uint32_t optmask = 0, nmask = 0;   // bit q: position holds an option / a non-positive option
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                const bool is_o = j < n && v[q] > -__builtin_inf() && v[q] < __builtin_inf();
+                const bool is_n = is_o && v[q] <= 0.0;
+                optmask |= (uint32_t)is_o << q;
+                nmask |= (uint32_t)is_n << q;
+                const uint64_t bo = __ballot(is_o), bn = __ballot(is_n);
+                if (lane == 0 && q * kChainBlock < (int)n) {
+                    sh.tile_o[q * (kChainBlock / 64) + wave] = (uint32_t)__popcll(bo);
+                    sh.tile_n[q * (kChainBlock / 64) + wave] = (uint32_t)__popcll(bn);
+                }
+            }
+            for (uint32_t s = tid; s < kChainMaxSel; s += kChainBlock) {
+                sh.sel_max[s] = 0ull;
+                sh.sel_arg[s] = kEmpty;
+                sh.sel_f[s] = 0;
+                sh.sel_x[s] = 0;
+            }
+            __syncthreads();
+            // 2. exclusive scan of the tile counts (wave 0)
+            const uint32_t ntiles = (n + 63) / 64;
+            if (wave == 0) {
+                constexpr int PER = kChainTiles / 64;
+                uint32_t so = 0, sn = 0, lo[PER], ln[PER];
+#pragma unroll
+                for (int k = 0; k < PER; k++) {
+                    const uint32_t t = (uint32_t)(lane * PER + k);
+                    lo[k] = t < ntiles ? sh.tile_o[t] : 0u;
+                    ln[k] = t < ntiles ? sh.tile_n[t] : 0u;
+                    so += lo[k];
+                    sn += ln[k];
+                }
+                uint32_t io = so, in_ = sn;   // inclusive wave scan
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t xo = (uint32_t)__shfl_up((int)io, off), xn = (uint32_t)__shfl_up((int)in_, off);
+                    if (lane >= off) { io += xo; in_ += xn; }
+                }
+                uint32_t eo = io - so, en = in_ - sn;
+#pragma unroll
+                for (int k = 0; k < PER; k++) {
+                    const uint32_t t = (uint32_t)(lane * PER + k);
+                    if (t < ntiles) { sh.tile_o[t] = eo; sh.tile_n[t] = en; }
+                    eo += lo[k];
+                    en += ln[k];
+                }
+                if (lane == 63) { sh.tot_o = io; sh.tot_n = in_; }
+            }
+            __syncthreads();
+            // 3. option index and N prefix of every option; nb[k] = N options before option k
+            uint32_t pk[kChainItems];
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                const uint64_t bo = __ballot((optmask >> q) & 1u), bn = __ballot((nmask >> q) & 1u);
+                const uint32_t t = (uint32_t)(q * (kChainBlock / 64) + wave);
+                const bool live = (uint32_t)(q * kChainBlock) < n;
+                const uint32_t k = (live ? sh.tile_o[t] : 0u) + lanes_below(bo, lane);
+                const uint32_t nbk = (live ? sh.tile_n[t] : 0u) + lanes_below(bn, lane);
+                pk[q] = (k & kIdxMask) | ((nbk & kIdxMask) << kIdxBits);
+                if ((optmask >> q) & 1u) nb[k] = (uint16_t)nbk;
+            }
+            const uint32_t tot_o = sh.tot_o, tot_n = sh.tot_n;
+            if (tid == 0) nb[tot_o] = (uint16_t)tot_n;
+            __syncthreads();
+            // 4. Select boundaries (one lane; 4 independent LDS reads per Select)
+            if (tid == 0) {
+                const uint32_t want = min(A.count - placed, (uint32_t)kChainMaxSel);
+                uint32_t i = 0, ns = 0;
+                int mode = kPhaseMore;
+                while (ns < want) {
+                    if (i + L - 1 >= tot_o) break;
+                    const uint32_t a0 = nb[i];
+                    const uint32_t a1 = nb[min(i + L, tot_o)];
+                    const uint32_t a2 = nb[min(i + L + 1, tot_o)];
+                    const uint32_t a3 = nb[min(i + L + 2, tot_o)];
+                    uint32_t b;
+                    if (a1 - a0 == 0) b = i + L - 1;
+                    else if (i + L >= tot_o) break;
+                    else if (a2 - a0 == 1) b = i + L;
+                    else if (i + L + 1 >= tot_o) break;
+                    else if (a3 - a0 == 2) b = i + L + 1;
+                    else if (i + L + 2 >= tot_o) break;
+                    else b = i + L + 2;
+                    sh.sel_b[ns++] = b;
+                    i = b + 1;
+                }
+                if (ns == 0) {
+                    // the first Select saw the whole list without reaching the limit
+                    mode = kPhaseExhausted;
+                    ns = tot_o ? 1u : 0u;
+                    if (ns) sh.sel_b[0] = tot_o - 1;
+                } else if (ns == A.count - placed) {
+                    mode = kPhaseCount;
+                }
+                sh.nsel = ns;
+                sh.mode = (uint32_t)mode;
+            }
+            __syncthreads();
+            const uint32_t nsel = sh.nsel;
+            const int mode = (int)sh.mode;
+            const uint32_t last_b = nsel ? sh.sel_b[nsel - 1] : 0u;
+            // 5. per-Select maxima over the returned options (a Select sets its
+            //    first three N options aside)
+            uint32_t retmask = 0;
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                const uint32_t k = pk[q] & kIdxMask;
+                uint32_t s = 0;
+                if (((optmask >> q) & 1u) && nsel && k <= last_b) {
+                    s = lower_bound_lds(sh.sel_b, nsel, k);
+                    const uint32_t i0 = s ? sh.sel_b[s - 1] + 1u : 0u;
+                    const uint32_t nrank = (pk[q] >> kIdxBits) - nb[i0];
+                    const bool aside = ((nmask >> q) & 1u) && nrank < (uint32_t)kMaxSkip;
+                    if (!aside) {
+                        retmask |= 1u << q;
+                        atomicMax(&sh.sel_max[s], order_key(v[q]));
+                    } else if (mode == kPhaseExhausted) {
+                        sh.aside_v[nrank] = v[q];
+                        sh.aside_row[nrank] = row[q];
+                    }
+                    if (k == sh.sel_b[s]) sh.sel_end[s] = (uint32_t)(q * kChainBlock + tid);
+                }
+                pk[q] = k | (s << kIdxBits);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                if ((retmask >> q) & 1u) {
+                    const uint32_t s = pk[q] >> kIdxBits;
+                    if (order_key(v[q]) == sh.sel_max[s]) atomicMin(&sh.sel_arg[s], pk[q] & kIdxMask);
+                }
+            }
+            if (A.full_out && (nsel || mode == kPhaseExhausted)) {
+                // AllocMetric counters: filtered / exhausted positions pulled by each Select
+                const uint32_t end = mode == kPhaseExhausted ? n - 1 : sh.sel_end[nsel - 1];
+#pragma unroll
+                for (int q = 0; q < kChainItems; q++) {
+                    const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                    if (j <= end && j < n && !((optmask >> q) & 1u)) {
+                        const uint32_t s = mode == kPhaseExhausted ? 0u : lower_bound_lds(sh.sel_end, nsel, j);
+                        atomicAdd(v[q] == -__builtin_inf() ? &sh.sel_f[s] : &sh.sel_x[s], 1u);
+                    }
+                }
+            }
+            __syncthreads();
+            // the first maximum of each Select publishes its row and FinalScore
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                if ((retmask >> q) & 1u) {
+                    const uint32_t s = pk[q] >> kIdxBits;
+                    if (sh.sel_arg[s] == (pk[q] & kIdxMask)) {
+                        sh.sel_row[s] = row[q];
+                        sh.sel_max[s] = (unsigned long long)gm::f2u(v[q]);
+                    }
+                }
+            }
+            __syncthreads();
+            // 6. emit the winners and commit them (Plan.AppendAlloc), one Select per thread
+            if (mode != kPhaseExhausted) {
+                for (uint32_t s = tid; s < nsel; s += kChainBlock) {
+                    const uint32_t start = s ? sh.sel_end[s - 1] + 1u : 0u;
+                    const uint32_t consumed = sh.sel_end[s] - start + 1u;
+                    const int win_row = (int)sh.sel_row[s];
+                    const double score = gm::u2f(sh.sel_max[s]);
+                    const uint32_t it = placed + s;
+                    if (A.full_out)
+                        emit_placement(A, A.tg.class_ok, ov, nullptr, e, it, win_row, score, consumed, sh.sel_f[s],
+                                       sh.sel_x[s], wrap_pos(cur + sh.sel_end[s] + 1u, n));
+                    if (A.out) {
+                        pe_placement& o = A.out[(size_t)e * A.count + it];
+                        o.row = win_row;
+                        o.nodes_evaluated = consumed;
+                        o.final_score = score;
+                    }
+                }
+                __syncthreads();   // emit_placement reads the overlay before the commits
+                if (A.commit)
+                    for (uint32_t s = tid; s < nsel; s += kChainBlock) ov_add_atomic(ov, sh.sel_row[s]);
+                placed += nsel;
+                cur = wrap_pos(cur + sh.sel_end[nsel - 1] + 1u, n);
+                done = mode == kPhaseCount;
+            } else {
+                // exhausted stream: returned options in order, then set-aside ones
+                // until the limit (select.go:35-74); the cursor stays
+                if (tid == 0) {
+                    const uint32_t a = min(tot_n, (uint32_t)kMaxSkip);
+                    const uint32_t r = tot_o - a;
+                    double best = -__builtin_inf();
+                    int win_row = -1;
+                    if (nsel && r) { best = gm::u2f(sh.sel_max[0]); win_row = (int)sh.sel_row[0]; }
+                    const uint32_t take = min(a, L > r ? L - r : 0u);
+                    for (uint32_t k = 0; k < take; k++)
+                        if (sh.aside_v[k] > best) { best = sh.aside_v[k]; win_row = (int)sh.aside_row[k]; }
+                    if (A.full_out)
+                        emit_placement(A, A.tg.class_ok, ov, nullptr, e, placed, win_row, best, n, sh.sel_f[0],
+                                       sh.sel_x[0], cur);
+                    if (A.out) {
+                        pe_placement& o = A.out[(size_t)e * A.count + placed];
+                        o.row = win_row;
+                        o.nodes_evaluated = n;
+                        o.final_score = win_row >= 0 ? best : 0.0;
+                    }
+                    if (win_row >= 0 && A.commit) ov_add(ov, (uint32_t)win_row);
+                    sh.mode = win_row >= 0 ? 1u : 0u;
+                }
+                __syncthreads();
+                if (sh.mode) placed++;
+                else done = true;   // nil option: failedTGAllocs short-circuit
+                if (placed >= A.count) done = true;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            A.eval_status[2 * e] = placed;
+            A.eval_status[2 * e + 1] = cur;
+        }
+        if (A.writeback) writeback_overlay<kChainBlock, false>(A, ov, H, nullptr);
+        __syncthreads();
+    }
+}
+
 // SystemStack: every list entry is an independent single-node Select.
 __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -1011,6 +1442,34 @@ hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, 
     } else {
         hipLaunchKernelGGL(pe::k_window, dim3(n_evals), dim3(64), lds, st, *a);
     }
+    return hipGetLastError();
+}
+
+// Phase-static windowed loop: k_base over the snapshot, then k_chain with a
+// persistent grid of at most `max_blocks` workgroups (one evaluation each at a time).
+uint32_t pe_chain_max_n() { return pe::kChainMaxN; }
+
+size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n) {
+    return (size_t)(packed ? 4u : 8u) * ((size_t)1 << hash_bits) + 2u * ((size_t)n + 2u);
+}
+
+int pe_chain_blocks_per_cu(size_t lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pe::k_chain, pe::kChainBlock, lds) != hipSuccess || nb <= 0)
+        nb = 1;
+    return nb;
+}
+
+hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st) {
+    if (!a->base || a->n_visit > pe::kChainMaxN || a->class_ok_stride) return hipErrorInvalidValue;
+    uint32_t blocks = (a->soa.n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_base, dim3(blocks), dim3(256), 0, st, *a);
+    const size_t lds = pe_chain_lds_bytes(a->hash_bits, a->packed_overlay != 0, a->n_visit);
+    uint32_t grid = n_evals < max_blocks ? n_evals : max_blocks;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(pe::k_chain, dim3(grid), dim3(pe::kChainBlock), lds, st, *a, n_evals);
     return hipGetLastError();
 }
 

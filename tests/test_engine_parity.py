@@ -189,6 +189,47 @@ def test_batch_result_paths_agree(monkeypatch):
                 assert scores[k, i] == r.final_score, (k, i)
 
 
+@pytest.mark.parametrize("n,count", [(40, 400), (3000, 900), (10000, 1000)])
+def test_phase_loop_matches_lazy_loop(monkeypatch, n, count):
+    """The phase-static windowed loop (k_base + k_chain: one rotation of the
+    visit list resolved at a time) equals the lazy per-position loop (k_window)
+    and the oracle, batched and single-eval, including walks that wrap the
+    list many times and an exhausted stream; a visit list with repeated rows
+    takes the lazy loop."""
+    nodes, allocs = synth.cluster_c2(n, seed=31)
+    job = synth.job_c2(count)
+    rng = np.random.Generator(np.random.PCG64(77))
+    orders = np.stack([synth.shuffle(n, 500 + e) for e in range(3)])
+    dup = synth.shuffle(n, 600).copy()
+    dup[rng.integers(0, n, size=n // 4)] = dup[rng.integers(0, n, size=n // 4)]   # repeated rows
+    res = []
+    for lazy in ("1", "0"):
+        monkeypatch.setenv("PE_WINDOW_LAZY", lazy)
+        e = engine_generic()
+        e.SetState(nodes, allocs)
+        e.SetJob(job)
+        e.StageOrders(orders)
+        res.append(e.PlaceBatch(0, count))
+        single = []
+        for order in list(orders) + [dup]:
+            e.ResetPlan()
+            e.SetJob(job)
+            e.SetNodes(order)
+            single.append(e.Place(0, count))
+        res.append(single)
+        e.close()
+    (b_lazy, s_lazy, b_chain, s_chain) = res
+    assert np.array_equal(b_lazy[3], b_chain[3])
+    for k in range(len(orders)):
+        m = min(int(b_chain[3][k]) + 1, count)
+        for a, b in zip(b_lazy[:3], b_chain[:3]):
+            assert np.array_equal(a[k, :m], b[k, :m]), k
+    for k, order in enumerate(list(orders) + [dup]):
+        assert_same_placements(s_chain[k], s_lazy[k])
+        _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, order)
+        assert_same_placements(s_chain[k], ro)
+
+
 @pytest.mark.parametrize("kind", ["c3", "c4"])
 def test_columnar_cluster_place(kind):
     """Vectorised (columnar) snapshot path: full count loop vs the oracle on the same tables."""
