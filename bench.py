@@ -30,7 +30,10 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # per node-evaluation: cls 4 + cap cpu/mem/disk 24 + used cpu/mem/disk 24
-# + (job,tg) collisions 4 = 56 B read; perm entry 4 B; no per-node write
+# + (job,tg) collisions 4 = 56 B read; perm entry 4 B; no per-node write. Node
+# evaluations = the nodes the reference chain visits (Σ nodes_evaluated over the
+# placements); the device evaluates each row once per launch (k_base) and
+# gathers the result per visit position (k_chain), see DESIGN.md §3.
 BYTES_PER_NODE_EVAL = 60
 
 
@@ -238,7 +241,7 @@ def main():
                             "note": "one eval, pe_place fused count loop, host call included"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_window", "kernel_ms": avg_kernel_s * 1000.0,
+                         "kernel": "k_base + k_chain", "kernel_ms": avg_kernel_s * 1000.0,
                          "node_evals_per_launch": evals_per_launch,
                          "bytes_per_node_eval": BYTES_PER_NODE_EVAL},
         }

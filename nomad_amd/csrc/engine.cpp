@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <cstdlib>
 #include <map>
@@ -45,6 +46,7 @@ hipError_t pe_launch_spread_table(const pe::TgTables* t, double* tab, hipStream_
 uint32_t pe_rec_winner(const pe::SweepRec* r);
 int pe_sweep_blocks_per_cu();
 uint32_t pe_chain_max_n();
+uint32_t pe_chain_max_limit();
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n);
 int pe_chain_blocks_per_cu(size_t lds);
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st);
@@ -258,6 +260,7 @@ struct pe_stack {
     std::vector<pe::NodeRec> h_base_rec;     // snapshot proposed state (no plan)
     DevMem d_rec, d_base_rec, d_coll_job;
     DevMem d_base;                     // windowed loops: per-row base value table
+    DevMem d_prof;                     // k_chain step profile (PE_CHAIN_PROF)
     bool orders_unique = true;         // every staged order lists each row at most once
     bool use_base = true;              // PE_WINDOW_LAZY=1: lazy per-position evaluation (k_window)
     bool batch_chain = false;          // the prepared batch runs k_base + k_chain
@@ -1091,7 +1094,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     A.hash_bits = hash_bits_for(count, full);
     A.packed_overlay = packed_kbits(s, 1u << A.hash_bits, full);
     bool chain = false;
-    if (!full && s->use_base && count > 1 && n <= pe_chain_max_n()) {
+    if (!full && s->use_base && count > 1 && n <= pe_chain_max_n() && A.limit <= pe_chain_max_limit()) {
         // count loop over one rotation at a time (k_base + k_chain): needs a
         // visit list without repeated rows
         std::vector<uint8_t> seen(s->nodes.size(), 0);
@@ -1103,6 +1106,11 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         if (chain) {
             HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));
             A.base = s->d_base.as<double>();
+            if (std::getenv("PE_CHAIN_PROF")) {
+                HIP_TRY(s, s->d_prof.ensure(8 * sizeof(unsigned long long)));
+                HIP_TRY(s, hipMemset(s->d_prof.p, 0, 8 * sizeof(unsigned long long)));
+                A.prof = s->d_prof.as<unsigned long long>();
+            }
         }
     }
     const uint32_t chunk = std::max<uint32_t>(1, (1u << A.hash_bits) / 2);
@@ -1138,6 +1146,13 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         if (st[0] < c) break;
     }
     s->last_ms = total_ms;
+    if (A.prof) {
+        unsigned long long pr[8];
+        HIP_TRY(s, hipMemcpy(pr, A.prof, sizeof(pr), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "k_chain step clocks: setup %llu values %llu scan %llu index %llu select-bounds %llu "
+                             "argmax %llu emit+commit %llu (thread 0, summed over phases; kernels %.3f ms)\n",
+                     pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], total_ms);
+    }
     return PE_OK;
 }
 
@@ -1564,7 +1579,8 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
     A.commit = 1;
     A.writeback = 0;
     s->batch_chain = false;
-    if (!full && s->use_base && A.class_ok_stride == 0 && s->orders_unique && n <= pe_chain_max_n()) {
+    if (!full && s->use_base && A.class_ok_stride == 0 && s->orders_unique && n <= pe_chain_max_n() &&
+        A.limit <= pe_chain_max_limit()) {
         // one base pass shared by every evaluation, then k_chain (persistent grid)
         HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));
         A.base = s->d_base.as<double>();

@@ -90,6 +90,7 @@ struct BatchArgs {
     // filtered, +inf exhausted), computed once per launch by k_base for all
     // evaluations. Null: the lazy per-position loop (k_window).
     double* base;
+    unsigned long long* prof;     // k_chain step clocks (PE_CHAIN_PROF), or null
     pe_ranked_node* full_out;     // [n_evals][count] full records, or null
     pe_placement* out;            // [n_evals][count] compact records, or null
     uint32_t* eval_status;        // [n_evals][2]: placed, final cursor

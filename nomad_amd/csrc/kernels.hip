@@ -806,6 +806,12 @@ constexpr int kChainTiles = kChainMaxN / 64;
 constexpr uint32_t kChainMaxRedo = 2048;                      // rows re-evaluated per phase (<= placements per launch)
 
 enum : int { kPhaseMore = 0, kPhaseCount = 1, kPhaseExhausted = 2 };
+constexpr int kSegE = 17;                 // entry offsets into a segment: a Select spans <= limit + 3 options
+constexpr uint32_t kSegLen = 256;         // options per segment of the boundary walk
+constexpr int kChainSegs = kChainMaxN / kSegLen;
+constexpr uint32_t kMaxChainLimit = kSegE - 3;
+constexpr uint16_t kNxFail = 0xFFFF;      // the Select starting at this option cannot stop in the window
+constexpr uint32_t kExFail = 0xFF;
 
 struct ChainShared {
     uint32_t tile_o[kChainTiles], tile_n[kChainTiles];    // per 64-position tile counts, then exclusive offsets
@@ -817,9 +823,12 @@ struct ChainShared {
     uint32_t sel_row[kChainMaxSel];                        // the winner's row
     uint32_t sel_f[kChainMaxSel], sel_x[kChainMaxSel];     // filtered / exhausted positions (metrics)
     uint2 redo[kChainMaxRedo];                             // (row, placements) to re-evaluate; then the value
+    uint16_t seg_tab[kChainSegs][kSegE];                  // per segment and entry offset: count | exit << 16
+    uint16_t seg_exit[kChainSegs][kSegE];
+    uint16_t seg_entry[kChainSegs], seg_base[kChainSegs];
     double aside_v[kMaxSkip];
     uint32_t aside_row[kMaxSkip];
-    uint32_t tot_o, tot_n, nsel, mode, n_redo;
+    uint32_t tot_o, tot_n, nsel, mode, n_redo, n_seg;
 };
 
 __device__ __forceinline__ unsigned long long order_key(double x) {
@@ -876,6 +885,17 @@ __device__ __forceinline__ uint32_t lower_bound_lds(const uint32_t* a, uint32_t 
 // Select id (10 bits) in the high half.
 constexpr uint32_t kIdxBits = 14, kIdxMask = (1u << kIdxBits) - 1u;
 
+// Optional step profile (PE_CHAIN_PROF): thread 0 accumulates shader clocks
+// per step into A.prof[0..7]; marks follow the block barriers.
+#define PE_PROF_MARK(k)                                                   \
+    do {                                                                  \
+        if (A.prof && tid == 0) {                                         \
+            const uint64_t now_ = __builtin_readcyclecounter();           \
+            A.prof[(k)] += now_ - prof_t;                                 \
+            prof_t = now_;                                                \
+        }                                                                 \
+    } while (0)
+
 __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_evals) {
     static_assert(kChainMaxN <= (1u << kIdxBits), "option index packing");
     static_assert(kChainMaxSel <= (1 << (32 - 2 * kIdxBits + kIdxBits)), "select id packing");
@@ -892,8 +912,10 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     ov.k = A.packed_overlay ? nullptr : ov.keys + H;
     ov.kshift = A.packed_overlay;
     ov.kmask = A.packed_overlay ? (1u << A.packed_overlay) - 1u : 0u;
-    uint16_t* nb = reinterpret_cast<uint16_t*>(ov.keys + (A.packed_overlay ? H : 2 * H));   // [n + 1]
+    uint16_t* nb = reinterpret_cast<uint16_t*>(ov.keys + (A.packed_overlay ? H : 2 * H));   // [n + 2]
+    uint16_t* nx = nb + ((n + 2 + 1) & ~1u);   // [n + 2]: next Select start per option, then Select id per option
 
+    uint64_t prof_t = A.prof ? __builtin_readcyclecounter() : 0;
     for (uint32_t e = blockIdx.x; e < n_evals; e += gridDim.x) {
         const uint32_t* __restrict__ perm = A.perms + (size_t)e * A.perm_stride;
         for (uint32_t i = tid; i < H; i += kChainBlock) {
@@ -909,6 +931,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
         }
         __syncthreads();
         while (!done) {
+            PE_PROF_MARK(0);
             // 1. values of the window [cur, cur + n): base, or queued for re-evaluation
             uint32_t row[kChainItems];
             double v[kChainItems];
@@ -980,6 +1003,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 sh.sel_x[s] = 0;
             }
             __syncthreads();
+            PE_PROF_MARK(1);
             // 2. exclusive scan of the tile counts (wave 0)
             const uint32_t ntiles = (n + 63) / 64;
             if (wave == 0) {
@@ -1010,6 +1034,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 if (lane == 63) { sh.tot_o = io; sh.tot_n = in_; }
             }
             __syncthreads();
+            PE_PROF_MARK(2);
             // 3. option index and N prefix of every option; nb[k] = N options before option k
             uint32_t pk[kChainItems];
 #pragma unroll
@@ -1025,43 +1050,107 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             const uint32_t tot_o = sh.tot_o, tot_n = sh.tot_n;
             if (tid == 0) nb[tot_o] = (uint16_t)tot_n;
             __syncthreads();
-            // 4. Select boundaries (one lane; 4 independent LDS reads per Select)
+            PE_PROF_MARK(3);
+            // 4. Select boundaries. A Select starting at option i stops at option
+            //    i + L - 1 + m for the smallest m in {0, 1, 2} with exactly m N's
+            //    in [i, i + L - 1 + m], else at i + L + 2 (its third N is set aside
+            //    and every later option returned). 4a: the next start nx[i] of every
+            //    option in parallel; 4b: per 64-option segment and entry offset the
+            //    Selects inside and the exit offset; 4c: one lane walks the
+            //    segments; 4d: the Selects are written out in parallel.
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                if ((optmask >> q) & 1u) {
+                    const uint32_t i = pk[q] & kIdxMask;
+                    const uint32_t a0 = pk[q] >> kIdxBits;
+                    uint32_t nxt = kNxFail;
+                    if (i + L - 1 < tot_o) {
+                        if (nb[min(i + L, tot_o)] - a0 == 0) nxt = i + L;
+                        else if (i + L < tot_o) {
+                            if (nb[i + L + 1] - a0 == 1) nxt = i + L + 1;
+                            else if (i + L + 1 < tot_o) {
+                                if (nb[i + L + 2] - a0 == 2) nxt = i + L + 2;
+                                else if (i + L + 2 < tot_o) nxt = i + L + 3;
+                            }
+                        }
+                    }
+                    nx[i] = (uint16_t)nxt;
+                }
+            }
+            if (tid == 0) nx[tot_o] = kNxFail;
+            __syncthreads();
+            const uint32_t n_seg = (tot_o + kSegLen - 1) / kSegLen;
+            const uint32_t E = L + 3;
+            for (uint32_t t = tid; t < n_seg * E; t += kChainBlock) {
+                const uint32_t g = t / E, o = t - g * E;
+                const uint32_t end = kSegLen * (g + 1);
+                uint32_t i = kSegLen * g + o, cnt = 0, ex = kExFail;
+                for (;;) {
+                    if (i >= end) { ex = i - end; break; }
+                    if (i >= tot_o) break;
+                    const uint32_t x = nx[i];
+                    if (x == kNxFail) break;
+                    cnt++;
+                    i = x;
+                }
+                sh.seg_tab[g][o] = (uint16_t)cnt;
+                sh.seg_exit[g][o] = (uint16_t)ex;
+            }
+            __syncthreads();
             if (tid == 0) {
                 const uint32_t want = min(A.count - placed, (uint32_t)kChainMaxSel);
-                uint32_t i = 0, ns = 0;
-                int mode = kPhaseMore;
-                while (ns < want) {
-                    if (i + L - 1 >= tot_o) break;
-                    const uint32_t a0 = nb[i];
-                    const uint32_t a1 = nb[min(i + L, tot_o)];
-                    const uint32_t a2 = nb[min(i + L + 1, tot_o)];
-                    const uint32_t a3 = nb[min(i + L + 2, tot_o)];
-                    uint32_t b;
-                    if (a1 - a0 == 0) b = i + L - 1;
-                    else if (i + L >= tot_o) break;
-                    else if (a2 - a0 == 1) b = i + L;
-                    else if (i + L + 1 >= tot_o) break;
-                    else if (a3 - a0 == 2) b = i + L + 1;
-                    else if (i + L + 2 >= tot_o) break;
-                    else b = i + L + 2;
-                    sh.sel_b[ns++] = b;
-                    i = b + 1;
+                uint32_t total = 0, o = 0, used = 0;
+                for (uint32_t g = 0; g < n_seg; g++) {
+                    const uint32_t cnt = sh.seg_tab[g][o], ex = sh.seg_exit[g][o];
+                    sh.seg_entry[g] = (uint16_t)o;
+                    sh.seg_base[g] = (uint16_t)total;
+                    used = g + 1;
+                    if (total + cnt >= want) { total = want; break; }
+                    total += cnt;
+                    if (ex == kExFail) break;
+                    o = ex;
                 }
+                int mode = kPhaseMore;
+                uint32_t ns = total;
                 if (ns == 0) {
                     // the first Select saw the whole list without reaching the limit
                     mode = kPhaseExhausted;
                     ns = tot_o ? 1u : 0u;
                     if (ns) sh.sel_b[0] = tot_o - 1;
+                    used = 0;
                 } else if (ns == A.count - placed) {
                     mode = kPhaseCount;
                 }
                 sh.nsel = ns;
                 sh.mode = (uint32_t)mode;
+                sh.n_seg = used;
+            }
+            __syncthreads();
+            {
+                const uint32_t ns = sh.nsel, used = sh.n_seg;
+                for (uint32_t g = tid; g < used; g += kChainBlock) {
+                    uint32_t i = kSegLen * g + sh.seg_entry[g], sel = sh.seg_base[g];
+                    while (sel < ns && i < kSegLen * (g + 1)) {
+                        const uint32_t x = nx[i];
+                        sh.sel_b[sel++] = x - 1u;
+                        i = x;
+                    }
+                }
+            }
+            __syncthreads();
+            {
+                // Select id of every option of a resolved Select (nx is free now)
+                const uint32_t ns = sh.nsel;
+                for (uint32_t sel = tid; sel < ns; sel += kChainBlock) {
+                    const uint32_t i0 = sel ? sh.sel_b[sel - 1] + 1u : 0u;
+                    for (uint32_t k = i0; k <= sh.sel_b[sel]; k++) nx[k] = (uint16_t)sel;
+                }
             }
             __syncthreads();
             const uint32_t nsel = sh.nsel;
             const int mode = (int)sh.mode;
             const uint32_t last_b = nsel ? sh.sel_b[nsel - 1] : 0u;
+            PE_PROF_MARK(4);
             // 5. per-Select maxima over the returned options (a Select sets its
             //    first three N options aside)
             uint32_t retmask = 0;
@@ -1070,7 +1159,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 const uint32_t k = pk[q] & kIdxMask;
                 uint32_t s = 0;
                 if (((optmask >> q) & 1u) && nsel && k <= last_b) {
-                    s = lower_bound_lds(sh.sel_b, nsel, k);
+                    s = nx[k];
                     const uint32_t i0 = s ? sh.sel_b[s - 1] + 1u : 0u;
                     const uint32_t nrank = (pk[q] >> kIdxBits) - nb[i0];
                     const bool aside = ((nmask >> q) & 1u) && nrank < (uint32_t)kMaxSkip;
@@ -1100,7 +1189,8 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 for (int q = 0; q < kChainItems; q++) {
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                     if (j <= end && j < n && !((optmask >> q) & 1u)) {
-                        const uint32_t s = mode == kPhaseExhausted ? 0u : lower_bound_lds(sh.sel_end, nsel, j);
+                        // pulled by the Select of the next option after j
+                        const uint32_t s = mode == kPhaseExhausted ? 0u : (uint32_t)nx[pk[q] & kIdxMask];
                         atomicAdd(v[q] == -__builtin_inf() ? &sh.sel_f[s] : &sh.sel_x[s], 1u);
                     }
                 }
@@ -1118,6 +1208,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
             }
             __syncthreads();
+            PE_PROF_MARK(5);
             // 6. emit the winners and commit them (Plan.AppendAlloc), one Select per thread
             if (mode != kPhaseExhausted) {
                 for (uint32_t s = tid; s < nsel; s += kChainBlock) {
@@ -1177,6 +1268,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             A.eval_status[2 * e] = placed;
             A.eval_status[2 * e + 1] = cur;
         }
+        PE_PROF_MARK(6);
         if (A.writeback) writeback_overlay<kChainBlock, false>(A, ov, H, nullptr);
         __syncthreads();
     }
@@ -1448,9 +1540,10 @@ hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, 
 // Phase-static windowed loop: k_base over the snapshot, then k_chain with a
 // persistent grid of at most `max_blocks` workgroups (one evaluation each at a time).
 uint32_t pe_chain_max_n() { return pe::kChainMaxN; }
+uint32_t pe_chain_max_limit() { return pe::kMaxChainLimit; }
 
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n) {
-    return (size_t)(packed ? 4u : 8u) * ((size_t)1 << hash_bits) + 2u * ((size_t)n + 2u);
+    return (size_t)(packed ? 4u : 8u) * ((size_t)1 << hash_bits) + 4u * (((size_t)n + 3u) & ~(size_t)1);
 }
 
 int pe_chain_blocks_per_cu(size_t lds) {
@@ -1461,7 +1554,8 @@ int pe_chain_blocks_per_cu(size_t lds) {
 }
 
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st) {
-    if (!a->base || a->n_visit > pe::kChainMaxN || a->class_ok_stride) return hipErrorInvalidValue;
+    if (!a->base || a->n_visit > pe::kChainMaxN || a->class_ok_stride || a->limit > pe::kMaxChainLimit)
+        return hipErrorInvalidValue;
     uint32_t blocks = (a->soa.n + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
