@@ -290,6 +290,9 @@ int pe_system_place(pe_stack* s, uint32_t tg_index, double* out_score,
 /* Milliseconds spent in device kernels by the last pe_place / pe_system_place
  * (HIP events on the engine's stream). */
 double pe_last_kernel_ms(const pe_stack* s);
+/* Algorithmic HBM bytes per node of the last full-scan sweep Select (73 with
+ * the verdict byte, 76 with the folded per-node score word), 0 if none ran. */
+uint32_t pe_last_sweep_bytes(const pe_stack* s);
 /* Host-side constraint semantics used for pre-resolution (checkConstraint,
  * feasible.go:785-820), exposed for known-answer tests; needs no device.
  * l_state / r_state: 0 nil (unknown ${...} target), 1 found, 2 missing ("", false). */

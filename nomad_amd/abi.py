@@ -182,7 +182,7 @@ ENGINE_SYMBOLS = [
     "pe_abi_version", "pe_stack_create", "pe_stack_destroy", "pe_last_error", "pe_set_state",
     "pe_reset_plan", "pe_set_job", "pe_set_nodes", "pe_select", "pe_commit", "pe_place", "pe_system_place",
     "pe_last_kernel_ms", "pe_stage_orders", "pe_place_batch", "pe_batch_results", "pe_last_phase_ms",
-    "pe_check_constraint",
+    "pe_check_constraint", "pe_last_sweep_bytes",
 ]
 
 

@@ -44,7 +44,9 @@ hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec
 hipError_t pe_launch_node_record(const pe::SweepArgs* a, uint32_t row, pe_ranked_node* out, hipStream_t st);
 hipError_t pe_launch_spread_table(const pe::TgTables* t, double* tab, hipStream_t st);
 uint32_t pe_rec_winner(const pe::SweepRec* r);
-int pe_sweep_blocks_per_cu();
+int pe_sweep_blocks_per_cu(bool aux);
+hipError_t pe_launch_fold_aux(const pe::NodeSoA* s, const pe::TgTables* t, const uint8_t* aff_idx_class,
+                              const uint8_t* aff_idx_node, uint32_t* aux, hipStream_t st);
 uint32_t pe_chain_max_n();
 uint32_t pe_chain_max_limit();
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n);
@@ -207,6 +209,10 @@ struct TgPlan {
     std::vector<uint8_t> sig_tg, class_uniform, class_verdict, job_ok_node;
     std::vector<uint32_t> nonuniform;
     DevMem class_ok_batch, node_feas;
+    // folded sweep inputs (SweepArgs::node_aux), rebuilt with the tables
+    std::vector<double> h_aff_class, h_aff_node;
+    DevMem node_aux, aff_vals, aff_idx;
+    bool aux_valid = false, aux_ok = false;
 };
 
 }  // namespace
@@ -219,7 +225,8 @@ struct pe_stack {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double last_ms = 0;
     int n_cu = 256;
-    int sweep_per_cu = 4;
+    int sweep_per_cu = 4, sweep_per_cu_aux = 4;
+    uint32_t last_sweep_bytes = 0;   // algorithmic bytes per node of the last sweep
 
     // strings
     std::vector<std::string> strs;
@@ -874,12 +881,20 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
             for (size_t i = 0; i < n; i++) na[i] = score(s->view((uint32_t)i));
             HIP_TRY(s, upload(g.node_aff, na));
             g.node_aff_used = true;
+            g.h_aff_node = std::move(na);
+            g.h_aff_class.clear();
         } else {
             std::vector<double> ca(s->ncls);
             for (uint32_t c = 0; c < s->ncls; c++) ca[c] = score(s->view(s->class_rep[c]));
             HIP_TRY(s, upload(g.class_aff, ca));
+            g.h_aff_class = std::move(ca);
+            g.h_aff_node.clear();
         }
+    } else {
+        g.h_aff_class.clear();
+        g.h_aff_node.clear();
     }
+    g.aux_valid = false;
     // AssignPorts needs an address of the ports' host network on the node
     g.alias_used = false;
     if (g.ask.tg_dyn > 0) {
@@ -988,6 +1003,45 @@ pe::BatchArgs batch_args(pe_stack* s, TgPlan& g) {
     return A;
 }
 
+// Fold the sweep's per-node inputs into one u32 per node (SweepArgs::node_aux)
+// when they fit: at most kAuxPsets spread properties of at most 255 values and
+// at most kAuxValues distinct affinity scores. Otherwise the sweep resolves
+// them through the class tables.
+int build_aux(pe_stack* s, TgPlan& g, const pe::TgTables& t) {
+    g.aux_valid = true;
+    g.aux_ok = false;
+    if (t.n_psets > pe::kAuxPsets) return PE_OK;
+    for (int p = 0; p < t.n_psets; p++)
+        if (t.pset_nvals[p] > (int)pe::kAuxMissing) return PE_OK;
+    // intern the affinity scores: index 0 is 0.0 (no score appended)
+    std::vector<double> vals{0.0};
+    std::map<uint64_t, uint8_t> index{{0, 0}};
+    const std::vector<double>& src = g.h_aff_node.empty() ? g.h_aff_class : g.h_aff_node;
+    std::vector<uint8_t> idx(src.size(), 0);
+    for (size_t i = 0; i < src.size(); i++) {
+        uint64_t bits;
+        std::memcpy(&bits, &src[i], 8);
+        auto it = index.find(bits);
+        if (it == index.end()) {
+            if (vals.size() >= (size_t)pe::kAuxValues) return PE_OK;
+            it = index.emplace(bits, (uint8_t)vals.size()).first;
+            vals.push_back(src[i]);
+        }
+        idx[i] = it->second;
+    }
+    vals.resize(pe::kAuxValues, 0.0);
+    HIP_TRY(s, upload(g.aff_vals, vals));
+    if (!idx.empty()) HIP_TRY(s, upload(g.aff_idx, idx));
+    const size_t n = s->nodes.size();
+    HIP_TRY(s, g.node_aux.ensure(sizeof(uint32_t) * std::max<size_t>(n, 1)));
+    pe::NodeSoA soa = soa_of(s);
+    const uint8_t* per_class = (!idx.empty() && g.h_aff_node.empty()) ? g.aff_idx.as<uint8_t>() : nullptr;
+    const uint8_t* per_node = (!idx.empty() && !g.h_aff_node.empty()) ? g.aff_idx.as<uint8_t>() : nullptr;
+    HIP_TRY(s, pe_launch_fold_aux(&soa, &t, per_class, per_node, g.node_aux.as<uint32_t>(), s->stream));
+    g.aux_ok = true;
+    return PE_OK;
+}
+
 bool full_scan_kernel(pe_stack* s, TgPlan& g, uint32_t n) {
     return !g.psets.empty() || s->limit >= n;
 }
@@ -1021,10 +1075,23 @@ int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_r
         HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
         A.spread_tab = s->d_spread_tab.as<double>();
     }
+    if (!g.aux_valid) {
+        int rc = build_aux(s, g, A.tg);
+        if (rc) return rc;
+    }
+    bool use_aux = g.aux_ok;
+    if (const char* e = std::getenv("PE_SWEEP_AUX")) use_aux = use_aux && std::atoi(e) != 0;
+    if (use_aux) {
+        A.node_aux = g.node_aux.as<uint32_t>();
+        A.aff_vals = g.aff_vals.as<double>();
+    }
+    s->last_sweep_bytes = use_aux ? 76u : 73u;
     // exactly one round of resident workgroups: a grid-stride pass with no
     // tail, and few records for the merge
     uint32_t blocks = (A.row_end - A.row_begin + 256 * 8 - 1) / (256 * 8);
-    blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)(s->n_cu * s->sweep_per_cu)));
+    uint32_t per_cu = (uint32_t)(use_aux ? s->sweep_per_cu_aux : s->sweep_per_cu);
+    if (const char* e = std::getenv("PE_SWEEP_BPC")) per_cu = (uint32_t)std::max(1, std::atoi(e));
+    blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)s->n_cu * per_cu));
     HIP_TRY(s, s->d_sweep_recs.ensure(sizeof(pe::SweepRec) * blocks));
     HIP_TRY(s, s->d_sweep_merged.ensure(sizeof(pe::SweepRec)));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
@@ -1184,7 +1251,8 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess && cus > 0)
         s->n_cu = cus;
-    s->sweep_per_cu = pe_sweep_blocks_per_cu();
+    s->sweep_per_cu = pe_sweep_blocks_per_cu(false);
+    s->sweep_per_cu_aux = pe_sweep_blocks_per_cu(true);
     s->log10 = pe::gm::log_go(10.0);
     if (const char* e = std::getenv("PE_SWEEP_MIN")) s->sweep_min = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("PE_RESULTS_VIA_COPY")) s->results_via_copy = std::atoi(e) != 0;
@@ -1207,6 +1275,8 @@ void pe_stack_destroy(pe_stack* s) {
 const char* pe_last_error(const pe_stack* s) { return s ? s->err.c_str() : g_error.c_str(); }
 
 double pe_last_kernel_ms(const pe_stack* s) { return s ? s->last_ms : 0.0; }
+
+uint32_t pe_last_sweep_bytes(const pe_stack* s) { return s ? s->last_sweep_bytes : 0u; }
 
 int pe_check_constraint(const char* op, const char* l, int ls, const char* r, int rs) {
     pe::ConstraintEvaluator ev;

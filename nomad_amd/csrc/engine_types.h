@@ -120,8 +120,17 @@ struct SweepArgs {
     const uint32_t* penalty_bits;
     double log10;
     const double* spread_tab;     // [kMaxPsets][kMaxValues+1] or null
+    // Folded per-node score inputs (k_fold_aux), or null: bit 31 the
+    // FeasibilityWrapper verdict, bits 0-7 an index into aff_vals (the node's
+    // NodeAffinityIterator score), bits 8+8p the node's value of spread
+    // property p (kAuxMissing = no value), for at most kAuxPsets properties.
+    const uint32_t* node_aux;     // [n rows]
+    const double* aff_vals;       // [kAuxValues]
     SweepRec* recs;               // [gridDim.x]
 };
+constexpr int kAuxPsets = 2;
+constexpr int kAuxValues = 256;
+constexpr uint32_t kAuxMissing = 255;
 
 struct SystemArgs {
     NodeSoA soa;

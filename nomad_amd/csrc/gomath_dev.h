@@ -61,6 +61,18 @@ __host__ __device__ __forceinline__ double ldexp_go(double frac, int exp) {
     return m * u2f(x);
 }
 
+// ldexp_go for a normal frac whose result is normal: the exponent field add
+// (the m == 1.0 branch of ldexp_go, bit-identical); anything else takes the
+// full routine.
+__host__ __device__ __forceinline__ double ldexp_fast(double frac, int exp) {
+    const uint64_t x = f2u(frac);
+    const int be = (int)((x >> kShift) & kMask);
+    const int ne = be + exp;
+    if (be != 0 && be != (int)kMask && ne > 0 && ne < (int)kMask)
+        return u2f(x + ((uint64_t)(int64_t)exp << kShift));
+    return ldexp_go(frac, exp);
+}
+
 // math.Modf for f >= 0
 __host__ __device__ __forceinline__ void modf_go(double f, double* ip, double* fp) {
     if (f < 1.0) {
@@ -94,7 +106,7 @@ __host__ __device__ __forceinline__ double exp_go(double x) {
     double t = r * r;
     double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
     double y = 1 - ((lo - (r * c) / (2 - c)) - hi);
-    return ldexp_go(y, k);
+    return ldexp_fast(y, k);
 }
 
 __host__ __device__ __forceinline__ double log_go(double x) {
@@ -152,6 +164,40 @@ __host__ __device__ __forceinline__ double pow10_go(double y, double log10) {
     return ldexp_go(a1, ae);
 }
 
+// pow10_go on the free fractions ScoreFit sees (0 < y < 1, y != 0.5): Modf
+// gives yi = 0, and for yf > 0.5 the shifted fraction yf - 1 with yi = 1, whose
+// one loop step multiplies by Frexp(10) = 0.625 * 2^4. The same operations in
+// the same order as pow10_go, without the loop; other y take pow10_go.
+// exp_go restricted to |x| < 2: NaN / overflow / underflow cannot occur, the
+// reduction gives |k| <= 3 and y in (0.7, 1.5), so the closing ldexp_go is the
+// exponent-field add (its m == 1.0 branch).
+__host__ __device__ __forceinline__ double exp_small(double x) {
+    const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10,
+                 Log2e = 1.44269504088896338700e+00, NearZero = 1.0 / (1 << 28);
+    const double P1 = 1.66666666666666657415e-01, P2 = -2.77777777770155933842e-03,
+                 P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+                 P5 = 4.13813679705723846039e-08;
+    if (-NearZero < x && x < NearZero) return 1.0 + x;
+    const int k = (int)(x < 0 ? Log2e * x - 0.5 : Log2e * x + 0.5);
+    double hi = x - (double)k * Ln2Hi;
+    double lo = (double)k * Ln2Lo;
+    double r = hi - lo;
+    double t = r * r;
+    double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    double y = 1 - ((lo - (r * c) / (2 - c)) - hi);
+    return u2f(f2u(y) + ((uint64_t)(int64_t)k << kShift));
+}
+
+__host__ __device__ __forceinline__ double pow10_unit(double y, double log10) {
+    if (y > 0.0 && y < 1.0 && y != 0.5) {
+        // (y - 1) * log10 in (-1.16, 0): exp in (0.31, 1), times 0.625 stays
+        // normal, so ldexp_go(., 4) is the exponent add as well
+        if (y > 0.5) return u2f(f2u(exp_small((y - 1.0) * log10) * 0.625) + (4ull << kShift));
+        return exp_small(y * log10);
+    }
+    return pow10_go(y, log10);
+}
+
 // ScoreFitBinPack / ScoreFitSpread (funcs.go:237-279) divided by
 // binPackingMaxFitScore (rank.go:514).
 __host__ __device__ __forceinline__ double fit_score(int64_t cap_cpu, int64_t cap_mem, int64_t util_cpu,
@@ -159,7 +205,7 @@ __host__ __device__ __forceinline__ double fit_score(int64_t cap_cpu, int64_t ca
     const double node_cpu = (double)cap_cpu, node_mem = (double)cap_mem;
     const double fc = 1 - ((double)util_cpu / node_cpu);
     const double fm = 1 - ((double)util_mem / node_mem);
-    const double total = pow10_go(fc, log10) + pow10_go(fm, log10);
+    const double total = pow10_unit(fc, log10) + pow10_unit(fm, log10);
     double s = spread ? total - 2 : 20.0 - total;
     if (s > 18.0) s = 18.0;
     else if (s < 0) s = 0;

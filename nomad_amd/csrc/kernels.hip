@@ -20,6 +20,7 @@
 // k_system              SystemStack: independent single-node Selects, grid-stride.
 // k_commit              one Plan.AppendAlloc on the HBM SoA (pe_commit).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include "engine_types.h"
 #include "gomath_dev.h"
 
@@ -107,12 +108,25 @@ __device__ __forceinline__ void load_node(const NodeSoA& s, const TgTables& t, u
     in.feas = t.node_feas ? t.node_feas[row] : 1u;
 }
 
-// Fused per-node pipeline over base (HBM) + overlay (dk placements of this eval).
-template <bool kKeepParts>
-__device__ __forceinline__ void eval_loaded(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
-                                            const Ask& a, uint32_t dk, const uint32_t* penalty_bits,
-                                            double log10, const double* spread_tab, uint32_t row,
-                                            const NodeIn& in, NodeEval* out) {
+// Inputs of the scoring half of the pipeline (everything after AllocsFit).
+// The table lookups (affinity, spread, penalty) are resolved by
+// lookup_scores so that their loads issue with the node's own loads; the
+// scoring half is then pure arithmetic.
+struct ScoreIn {
+    int64_t ccpu, cmem, ucpu, umem;   // capacity and proposed use including the ask
+    double aff;                       // NodeAffinityIterator score (0 = not appended)
+    double spread;                    // SpreadIterator total (0 = not appended)
+    uint32_t coll;                    // proposed allocs of (job, tg) on the node
+    uint32_t penalty;                 // node in the rescheduling penalty set
+};
+
+// Feasibility half of the fused per-node pipeline over base (HBM) + overlay
+// (dk placements of this eval): FeasibilityWrapper verdict, distinct_hosts,
+// BinPack network offers and AllocsFit. Returns kOption with the scoring
+// inputs filled, else kFiltered / kExhausted.
+__device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
+                                             const Ask& a, uint32_t dk, uint32_t row, const NodeIn& in,
+                                             ScoreIn* si) {
     const NodeRec& r = in.r;
     const uint32_t c = r.cls;
     // FeasibilityWrapper: memoised job + task-group checks (host-resolved per class)
@@ -128,29 +142,52 @@ __device__ __forceinline__ void eval_loaded(const NodeSoA& s, const TgTables& t,
         if (a.distinct_job && s.coll_job[row] + dk > 0) ok = false;
         if (a.distinct_tg && coll > 0) ok = false;
     }
-    if (!ok) { out->status = kFiltered; return; }
+    if (!ok) return kFiltered;
     // BinPackIterator (rank.go:193-527): network offers, then AllocsFit
     if (a.tg_dyn > 0 || a.has_task_net) {
         int32_t dyn = r.used_dyn + (int32_t)dk * a.commit_dyn;
         if (a.tg_dyn > 0) {
-            if ((t.alias_ok && !t.alias_ok[row]) || kDynPortCapacity - dyn < 1) { out->status = kExhausted; return; }
+            if ((t.alias_ok && !t.alias_ok[row]) || kDynPortCapacity - dyn < 1) return kExhausted;
             dyn += a.tg_dyn;
         }
         if (a.has_task_net) {
             const int32_t avail = r.avail_mbits;
             const int32_t mb = r.used_mbits + (int32_t)dk * a.commit_mbits;
-            if (avail < 0 || mb + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) {
-                out->status = kExhausted; return;
-            }
+            if (avail < 0 || mb + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) return kExhausted;
         }
     }
     const int64_t ucpu = r.used_cpu + (int64_t)(dk + 1) * a.cpu;
     const int64_t umem = r.used_mem + (int64_t)(dk + 1) * a.mem;
     const int64_t udisk = r.used_disk + (int64_t)(dk + 1) * a.disk;
-    const int64_t ccpu = r.cap_cpu, cmem = r.cap_mem;
-    if (ccpu < ucpu || cmem < umem || r.cap_disk < udisk) { out->status = kExhausted; return; }
-    // Scores in append order, summed left to right.
-    const double fit = gm::fit_score(ccpu, cmem, ucpu, umem, a.algo_spread, log10);
+    if (r.cap_cpu < ucpu || r.cap_mem < umem || r.cap_disk < udisk) return kExhausted;
+    si->ccpu = r.cap_cpu;
+    si->cmem = r.cap_mem;
+    si->ucpu = ucpu;
+    si->umem = umem;
+    si->coll = coll;
+    return kOption;
+}
+
+// Table lookups of the scoring half for an option: penalty bit, node affinity,
+// spread total (per-property boosts summed in property order, spread.go:145-170).
+__device__ __forceinline__ void lookup_scores(const TgTables& t, const uint32_t* penalty_bits,
+                                              const double* spread_tab, uint32_t row, uint32_t c, ScoreIn* si) {
+    si->penalty = penalty_bits ? (penalty_bits[row >> 5] >> (row & 31)) & 1u : 0u;
+    si->aff = (t.class_aff || t.node_aff) ? (t.node_aff ? t.node_aff[row] : t.class_aff[c]) : 0.0;
+    double total = 0.0;
+    for (int p = 0; p < t.n_psets; p++) {
+        const uint32_t v = pset_value(t, p, row, c);
+        total += (v == kMissing) ? -1.0 : spread_tab[p * (kMaxValues + 1) + v];
+    }
+    si->spread = total;
+}
+
+// Scoring half: scores in append order, summed left to
+// right, then ScoreNormalizationIterator.
+template <bool kKeepParts>
+__device__ __forceinline__ void score_option(const Ask& a, double log10, const ScoreIn& si, NodeEval* out) {
+    const uint32_t coll = si.coll;
+    const double fit = gm::fit_score(si.ccpu, si.cmem, si.ucpu, si.umem, a.algo_spread, log10);
     double sum = fit;
     uint32_t k = 1;
     if (kKeepParts) out->parts[0] = fit;
@@ -160,34 +197,37 @@ __device__ __forceinline__ void eval_loaded(const NodeSoA& s, const TgTables& t,
         if (kKeepParts) out->parts[k] = pen;
         k++;
     }
-    if (penalty_bits && ((penalty_bits[row >> 5] >> (row & 31)) & 1u)) {   // rank.go:632-635
+    if (si.penalty) {   // NodeReschedulingPenaltyIterator (rank.go:632-635)
         sum += -1.0;
         if (kKeepParts) out->parts[k] = -1.0;
         k++;
     }
-    if (t.class_aff || t.node_aff) {   // NodeAffinityIterator (rank.go:698-725)
-        const double aff = t.node_aff ? t.node_aff[row] : t.class_aff[c];
-        if (aff != 0.0) {
-            sum += aff;
-            if (kKeepParts) out->parts[k] = aff;
-            k++;
-        }
+    if (si.aff != 0.0) {   // NodeAffinityIterator (rank.go:698-725)
+        sum += si.aff;
+        if (kKeepParts) out->parts[k] = si.aff;
+        k++;
     }
-    if (t.n_psets > 0) {   // SpreadIterator (spread.go:110-174)
-        double total = 0.0;
-        for (int p = 0; p < t.n_psets; p++) {
-            const uint32_t v = pset_value(t, p, row, c);
-            total += (v == kMissing) ? -1.0 : spread_tab[p * (kMaxValues + 1) + v];
-        }
-        if (total != 0.0) {
-            sum += total;
-            if (kKeepParts) out->parts[k] = total;
-            k++;
-        }
+    if (si.spread != 0.0) {   // SpreadIterator (spread.go:110-174)
+        sum += si.spread;
+        if (kKeepParts) out->parts[k] = si.spread;
+        k++;
     }
     out->status = kOption;
     out->score = sum / (double)k;   // ScoreNormalizationIterator (rank.go:762-767)
     out->nscores = k;
+}
+
+// The whole fused per-node pipeline.
+template <bool kKeepParts>
+__device__ __forceinline__ void eval_loaded(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
+                                            const Ask& a, uint32_t dk, const uint32_t* penalty_bits,
+                                            double log10, const double* spread_tab, uint32_t row,
+                                            const NodeIn& in, NodeEval* out) {
+    ScoreIn si;
+    const int st = status_loaded(s, t, class_ok, a, dk, row, in, &si);
+    if (st != kOption) { out->status = st; return; }
+    lookup_scores(t, penalty_bits, spread_tab, row, in.r.cls, &si);
+    score_option<kKeepParts>(a, log10, si, out);
 }
 
 template <bool kKeepParts>
@@ -1430,44 +1470,175 @@ __device__ __forceinline__ void rec_block_reduce(SweepRec& r, SweepRec* red) {
     }
 }
 
-// One pass of the scoring sweep over rows [row_begin, row_end): per-thread
-// records over a grid-stride slice, reduced per workgroup. Software-pipelined:
-// the next row's visit rank, 64-byte record, collision count and verdict are in
-// flight while the current row's fp64 scoring runs, so HBM streaming and the
-// two software Pow evaluations overlap inside every wave. Rows outside the
-// visit list are evaluated and dropped.
-template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) k_sweep(SweepArgs A) {
+// One pass of the scoring sweep over rows [row_begin, row_end), one tile of
+// BLOCK rows per workgroup iteration (grid-stride), 64 rows per wave. Every
+// lane streams its row (64-byte record, collision count, verdict, visit rank),
+// runs the feasibility half and resolves the score-table lookups of an option.
+// Options go to a wave-private LDS ring (kQueue entries); whenever it holds 64
+// the wave runs the fp64 scoring half (two software Pow) on a full wave, so
+// the scoring is dense and no workgroup barrier sits in the loop. PF: the next
+// tile's loads are issued before the current tile is evaluated, so HBM
+// streaming overlaps the scoring. Per-lane SweepRec records, reduced per
+// workgroup at the end. Rows outside the visit list are dropped.
+//
+// AUX: the node's verdict, affinity index and spread values come folded in one
+// u32 per node (k_fold_aux) and resolve against LDS copies of the affinity
+// values and the spread boosts, so an option costs no dependent table load.
+template <int BLOCK, bool PF, int PROBE = 0, bool AUX = false>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AUX ? 4 : 5))) k_sweep(SweepArgs A) {
+    constexpr int W = BLOCK / 64;
+    constexpr uint32_t kQueue = 128;
+    __shared__ SweepRec red[W];
+    __shared__ ScoreIn q[W][kQueue];
+    __shared__ uint32_t q_rank[W][kQueue];
+    __shared__ double aff_lds[AUX ? kAuxValues : 1];
+    __shared__ double sp_lds[AUX ? kAuxPsets : 1][AUX ? kAuxValues : 1];
+    SweepRec r;
+    rec_init(r);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (AUX) {
+        for (int i = tid; i < kAuxValues; i += BLOCK) aff_lds[i] = A.aff_vals[i];
+        for (int p = 0; p < A.tg.n_psets; p++)
+            for (int i = tid; i < kAuxValues; i += BLOCK)
+                sp_lds[p][i] = i < A.tg.pset_nvals[p] ? A.spread_tab[p * (kMaxValues + 1) + i] : 0.0;
+        __syncthreads();
+    }
+    const uint32_t n = A.n_visit;
+    const uint32_t stride = gridDim.x * BLOCK;
+    ScoreIn* wq = q[wid];
+    uint32_t* wr = q_rank[wid];
+    uint32_t head = 0, qn = 0;   // wave-uniform ring state
+    auto score_from = [&](uint32_t at) {
+        const uint32_t i = (at + (uint32_t)lane) & (kQueue - 1);
+        NodeEval ev;
+        if (PROBE == 2) ev.score = wq[i].aff + wq[i].spread;
+        else score_option<false>(A.ask, A.log10, wq[i], &ev);
+        rec_add(r, wr[i], ev.score);
+    };
+    NodeIn nx;
+    uint32_t npos = kEmpty, naux = 0;
+    auto fetch = [&](uint32_t t) {
+        const uint32_t row = t + (uint32_t)tid;
+        npos = kEmpty;
+        if (row < A.row_end && row >= t) {
+            npos = A.rank_of[row];
+            if (AUX) {
+                nx.r = A.soa.rec[row];
+                nx.coll_tg = A.tg.coll_tg[row];
+                naux = A.node_aux[row];
+                nx.feas = naux >> 31;
+            } else {
+                load_node(A.soa, A.tg, row, nx);
+            }
+        }
+    };
+    uint32_t tile = A.row_begin + blockIdx.x * BLOCK;
+    if (PF) fetch(tile);
+    for (; tile < A.row_end; tile += stride) {
+        NodeIn in;
+        uint32_t pos, aux;
+        if (PF) {
+            in = nx;
+            pos = npos;
+            aux = naux;
+            const uint32_t nt = tile + stride;
+            if (nt > tile && nt < A.row_end) fetch(nt);
+        } else {
+            fetch(tile);
+            in = nx;
+            pos = npos;
+            aux = naux;
+        }
+        const uint32_t row = tile + (uint32_t)tid;
+        bool opt = false;
+        uint32_t rank = 0;
+        ScoreIn si;
+        if (pos != kEmpty) {
+            const int st = status_loaded(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, row, in, &si);
+            if (st == kFiltered) r.filtered++;
+            else if (st == kExhausted) r.exhausted++;
+            else {
+                opt = true;
+                rank = pos >= A.offset ? pos - A.offset : pos + n - A.offset;
+                if (PROBE == 1) {
+                    si.aff = si.spread = 0.0;
+                    si.penalty = 0;
+                } else if (AUX) {
+                    si.penalty = A.penalty_bits ? (A.penalty_bits[row >> 5] >> (row & 31)) & 1u : 0u;
+                    si.aff = aff_lds[aux & 255u];
+                    double total = 0.0;
+                    for (int p = 0; p < A.tg.n_psets; p++) {
+                        const uint32_t v = (aux >> (8 + 8 * p)) & 255u;
+                        total += (v == kAuxMissing) ? -1.0 : sp_lds[p][v];
+                    }
+                    si.spread = total;
+                } else {
+                    lookup_scores(A.tg, A.penalty_bits, A.spread_tab, row, in.r.cls, &si);
+                }
+            }
+        }
+        const uint64_t m = __ballot(opt);
+        if (opt) {
+            const uint32_t i = (head + qn + lanes_below(m, lane)) & (kQueue - 1);
+            wq[i] = si;
+            wr[i] = rank;
+        }
+        qn += (uint32_t)__popcll(m);
+        if (qn >= 64) {   // LDS ops of one wave complete in order: the ring is visible
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            score_from(head);
+            head = (head + 64) & (kQueue - 1);
+            qn -= 64;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if ((uint32_t)lane < qn) score_from(head);
+    rec_block_reduce<BLOCK>(r, red);
+    if (threadIdx.x == 0) A.recs[blockIdx.x] = r;
+}
+
+// Bound probes for the sweep (PE_SWEEP_VARIANT 5 / 6): 5 streams exactly the
+// sweep's bytes with trivial arithmetic; 6 runs the scoring arithmetic on
+// register-synthesised inputs without touching memory.
+template <int BLOCK, int MODE>
+__global__ void __launch_bounds__(BLOCK) k_sweep_probe(SweepArgs A) {
     __shared__ SweepRec red[BLOCK / 64];
     SweepRec r;
     rec_init(r);
-    const uint32_t n = A.n_visit;
     const uint32_t stride = gridDim.x * BLOCK;
-    uint32_t row = A.row_begin + blockIdx.x * BLOCK + threadIdx.x;
-    NodeIn nxt;
-    uint32_t nxt_pos = 0xFFFFFFFFu;
-    if (row < A.row_end) {
-        nxt_pos = A.rank_of[row];
-        load_node(A.soa, A.tg, row, nxt);
-    }
-    for (; row < A.row_end; row += stride) {
-        const NodeIn cur = nxt;
-        const uint32_t pos = nxt_pos;
-        const uint32_t ahead = row + stride;
-        if (ahead < A.row_end && ahead > row) {
-            nxt_pos = A.rank_of[ahead];
-            load_node(A.soa, A.tg, ahead, nxt);
+    uint64_t acc = 0;
+    for (uint32_t row = A.row_begin + blockIdx.x * BLOCK + threadIdx.x; row < A.row_end; row += stride) {
+        if (MODE == 5) {
+            NodeIn in;
+            load_node(A.soa, A.tg, row, in);
+            acc += (uint64_t)in.r.cap_cpu + (uint64_t)in.r.used_mem + (uint64_t)in.r.cap_disk + in.r.cls + in.coll_tg +
+                   in.feas + A.rank_of[row] + (uint64_t)in.r.used_cpu + (uint64_t)in.r.cap_mem +
+                   (uint64_t)in.r.used_disk + (uint64_t)in.r.avail_mbits;
+        } else {
+            NodeIn in;
+            in.r.cap_cpu = 4000 + (row & 1023);
+            in.r.cap_mem = 8192 + (row & 2047);
+            in.r.cap_disk = 100000;
+            in.r.used_cpu = row & 511;
+            in.r.used_mem = row & 255;
+            in.r.used_disk = 0;
+            in.r.cls = row & 7;
+            in.r.avail_mbits = -1;
+            in.r.used_mbits = 0;
+            in.r.used_dyn = 0;
+            in.coll_tg = 0;
+            in.feas = (row & 3) == 0;
+            TgTables t = A.tg;
+            t.node_feas = &A.tg.class_ok[0];   // unused: in.feas drives the verdict
+            NodeEval ev;
+            ev.score = 0.0;
+            eval_loaded<false>(A.soa, t, A.tg.class_ok, A.ask, 0u, nullptr, A.log10, A.spread_tab, row, in, &ev);
+            if (ev.status == kOption) rec_add(r, row, ev.score);
         }
-        NodeEval ev;
-        ev.score = 0.0;
-        eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, A.penalty_bits, A.log10, A.spread_tab, row, cur,
-                           &ev);
-        if (pos == 0xFFFFFFFFu) continue;
-        if (ev.status == kFiltered) { r.filtered++; continue; }
-        if (ev.status == kExhausted) { r.exhausted++; continue; }
-        const uint32_t rank = pos >= A.offset ? pos - A.offset : pos + n - A.offset;
-        rec_add(r, rank, ev.score);
     }
+    r.filtered += (uint32_t)acc;
     rec_block_reduce<BLOCK>(r, red);
     if (threadIdx.x == 0) A.recs[blockIdx.x] = r;
 }
@@ -1514,6 +1685,25 @@ __global__ void __launch_bounds__(256) k_fold_feas(NodeSoA s, const uint8_t* cla
         bool ok = class_ok[s.rec[row].cls] != 0;
         if (node_ok) ok = ok && node_ok[row] != 0;
         feas[row] = ok ? 1 : 0;
+    }
+}
+
+// node_aux[row] (SweepArgs): verdict bit, affinity index (per class, or per
+// node when the affinities escape the class), spread values of the first
+// kAuxPsets properties. Built once per (job, task group) tables.
+__global__ void __launch_bounds__(256) k_fold_aux(NodeSoA s, TgTables t, const uint8_t* aff_idx_class,
+                                                  const uint8_t* aff_idx_node, uint32_t* aux) {
+    for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < s.n; row += gridDim.x * blockDim.x) {
+        const uint32_t c = s.rec[row].cls;
+        bool ok = t.class_ok[c] != 0;
+        if (t.node_ok) ok = ok && t.node_ok[row] != 0;
+        uint32_t x = ok ? 1u << 31 : 0u;
+        x |= aff_idx_node ? aff_idx_node[row] : (aff_idx_class ? aff_idx_class[c] : 0u);
+        for (int p = 0; p < t.n_psets && p < kAuxPsets; p++) {
+            const uint32_t v = pset_value(t, p, row, c);
+            x |= (v == kMissing ? kAuxMissing : v) << (8 + 8 * p);
+        }
+        aux[row] = x;
     }
 }
 
@@ -1590,16 +1780,46 @@ hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, co
     return hipGetLastError();
 }
 
+hipError_t pe_launch_fold_aux(const pe::NodeSoA* s, const pe::TgTables* t, const uint8_t* aff_idx_class,
+                              const uint8_t* aff_idx_node, uint32_t* aux, hipStream_t st) {
+    uint32_t blocks = (s->n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_fold_aux, dim3(blocks), dim3(256), 0, st, *s, *t, aff_idx_class, aff_idx_node, aux);
+    return hipGetLastError();
+}
+
+static int sweep_variant() {
+    const char* e = std::getenv("PE_SWEEP_VARIANT");
+    return e ? std::atoi(e) : 0;
+}
+
 hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec* merged, hipStream_t st) {
-    hipLaunchKernelGGL((pe::k_sweep<256>), dim3(blocks), dim3(256), 0, st, *a);
+    // PE_SWEEP_VARIANT selects measurement variants (tools/sweep_variants.py):
+    // 1 = next-tile prefetch, 5 = streaming-only bound probe, 6 = arithmetic-only probe.
+    if (a->node_aux) {
+        hipLaunchKernelGGL((pe::k_sweep<256, false, 0, true>), dim3(blocks), dim3(256), 0, st, *a);
+        hipLaunchKernelGGL(pe::k_sweep_merge, dim3(1), dim3(512), 0, st, (const pe::SweepRec*)a->recs, blocks, merged);
+        return hipGetLastError();
+    }
+    switch (sweep_variant()) {
+        case 1: hipLaunchKernelGGL((pe::k_sweep<256, true>), dim3(blocks), dim3(256), 0, st, *a); break;
+        case 7: hipLaunchKernelGGL((pe::k_sweep<256, false, 1>), dim3(blocks), dim3(256), 0, st, *a); break;
+        case 8: hipLaunchKernelGGL((pe::k_sweep<256, false, 2>), dim3(blocks), dim3(256), 0, st, *a); break;
+        case 5: hipLaunchKernelGGL((pe::k_sweep_probe<256, 5>), dim3(blocks), dim3(256), 0, st, *a); break;
+        case 6: hipLaunchKernelGGL((pe::k_sweep_probe<256, 6>), dim3(blocks), dim3(256), 0, st, *a); break;
+        default: hipLaunchKernelGGL((pe::k_sweep<256, false>), dim3(blocks), dim3(256), 0, st, *a); break;
+    }
     hipLaunchKernelGGL(pe::k_sweep_merge, dim3(1), dim3(512), 0, st, (const pe::SweepRec*)a->recs, blocks, merged);
     return hipGetLastError();
 }
 
 // Resident k_sweep<256> workgroups per CU (grid = one full wave of residency).
-int pe_sweep_blocks_per_cu() {
+int pe_sweep_blocks_per_cu(bool aux) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pe::k_sweep<256>, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+    const hipError_t e = aux ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pe::k_sweep<256, false, 0, true>, 256, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pe::k_sweep<256, false>, 256, 0);
+    if (e != hipSuccess || nb <= 0) nb = 4;
     return nb;
 }
 

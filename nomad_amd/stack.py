@@ -50,6 +50,8 @@ def load_engine():
         lib.pe_abi_version.restype = C.c_uint32
         lib.pe_last_kernel_ms.restype = C.c_double
         lib.pe_last_kernel_ms.argtypes = [C.c_void_p]
+        lib.pe_last_sweep_bytes.restype = C.c_uint32
+        lib.pe_last_sweep_bytes.argtypes = [C.c_void_p]
         lib.pe_stage_orders.restype = C.c_int
         lib.pe_stage_orders.argtypes = [C.c_void_p, abi.u32p, C.c_uint32, C.c_uint32]
         lib.pe_place_batch.restype = C.c_int
@@ -299,6 +301,10 @@ class GenericStack(_Stack):
 
     def last_kernel_ms(self) -> float:
         return self._lib.pe_last_kernel_ms(self._h)
+
+    def last_sweep_bytes(self) -> int:
+        """Algorithmic bytes per node of the last full-scan sweep Select."""
+        return self._lib.pe_last_sweep_bytes(self._h)
 
 
 class SystemStack(_Stack):
