@@ -117,7 +117,24 @@ def cpu_baseline(nodes, allocs, job, seconds):
     return one, multi
 
 
-SWEEP_BYTES_PER_NODE = 73   # 64 B NodeRec + 1 B folded verdict + 4 B (job,tg) collisions + 4 B visit rank
+# Scoring sweep bytes per node (pe_last_sweep_bytes): 64 B NodeRec + 4 B folded
+# score word (verdict, affinity index, spread values; 1 B verdict when the word
+# does not apply: 73 B) + 4 B (job,tg) collisions + 4 B visit rank = 76 B.
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "sweep_traffic.json")
+
+
+def sweep_traffic(n, bytes_per_node):
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md
+    gfx950 correction), if they were taken on this workload."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("nodes") != n or t.get("bytes_per_node") != bytes_per_node:
+        return None, None
+    return t["bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT)
 
 
 def sweep_roofline(n, device, selects=6):
@@ -145,11 +162,14 @@ def sweep_roofline(n, device, selects=6):
         row = r.row
     kernel_ms = float(np.median([t[0] for t in times]))
     wall_ms = float(np.median([t[1] for t in times])) * 1000.0
-    achieved = n * SWEEP_BYTES_PER_NODE / (kernel_ms / 1000.0) / 1e9
+    bpn = st.last_sweep_bytes()
+    achieved = n * bpn / (kernel_ms / 1000.0) / 1e9
     st.close()
+    traffic, source = sweep_traffic(n, bpn)
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_sweep<256> + k_sweep_merge",
-            "nodes": n, "bytes_per_node_eval": SWEEP_BYTES_PER_NODE, "kernel_ms": kernel_ms,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": source,
+            "kernel": "k_sweep<256,aux> + k_sweep_merge",
+            "nodes": n, "bytes_per_node_eval": bpn, "kernel_ms": kernel_ms,
             "select_wall_ms": wall_ms, "nodes_scored_per_s": n / (kernel_ms / 1000.0),
             "winner_row": row, "setup_s": setup_s}
 
