@@ -31,9 +31,11 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 1u
+#define PE_ABI_VERSION 2u
 #define PE_NONE 0xFFFFFFFFu
 #define PE_MAX_SCORES 8
+#define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried per RankedNode */
+#define PE_MAX_DEVICE_REQ 4 /* device requests of a task group on the device path */
 
 /* ---- status codes ------------------------------------------------------ */
 #define PE_OK 0
@@ -119,6 +121,9 @@ typedef struct pe_alloc_table {
     const int32_t* dyn_ports;        /* ports held in [20000,32000)  */
     /* device instances held: CSR over allocs, (device group index on its node, count) */
     const uint32_t* dev_off; const uint32_t* dev_group; const uint32_t* dev_count;
+    /* TaskGroup.Migrate.MaxParallel of the alloc's job, or NULL = 0 for every
+       alloc (Preemptor.SetCandidates, scheduler/preemption.go:141-154) */
+    const int32_t* max_parallel;
 } pe_alloc_table;
 
 /* ---- job specification (structs.Job / TaskGroup / Task) ----------------- */
@@ -196,7 +201,10 @@ typedef struct pe_config {
     uint32_t batch;           /* GenericStack batch flag (limit 2) */
     uint32_t algorithm;       /* PE_ALGO_* */
     uint32_t memory_oversubscription;
-    uint32_t preempt;         /* eviction enabled for system stacks (stack.go:267-278) */
+    uint32_t preempt;         /* SystemStack: BinPack eviction enabled (stack.go:267-278).
+                                 GenericStack: PreemptionConfig.{Service,Batch}SchedulerEnabled:
+                                 pe_place retries a nil Select with Preempt=true
+                                 (selectNextOption, generic_sched.go:773-792) */
     int32_t device;           /* HIP device ordinal */
 } pe_config;
 
@@ -215,6 +223,13 @@ typedef struct pe_ranked_node {                 /* RankedNode, rank.go:21-36 */
     /* AllocMetric side outputs (structs.go:9826-10026) */
     uint32_t nodes_evaluated, nodes_filtered, nodes_exhausted;
     uint32_t new_offset;      /* StaticIterator cursor after the Select */
+    /* PreemptedAllocs (rank.go:511-513): rows of the pe_alloc_table snapshot */
+    uint32_t n_preempted;
+    uint32_t preempted[PE_MAX_PREEMPT];
+    /* TaskResources device offers (rank.go:404-405): per device request of the
+       task group (tasks in order), the index of the chosen device group on the node */
+    uint32_t n_device_offers;
+    uint32_t device_offer_group[PE_MAX_DEVICE_REQ];
 } pe_ranked_node;
 
 typedef struct pe_placement {                   /* compact per-placement record (batches) */
@@ -252,6 +267,11 @@ int pe_select(pe_stack* s, uint32_t tg_index, const pe_select_options* opts,
 /* Plan.AppendAlloc (structs.go:10707-10714) of an allocation of task group
  * `tg_index` on node `row`: the proposed state seen by later Selects. */
 int pe_commit(pe_stack* s, uint32_t tg_index, int32_t row);
+/* Plan.AppendAlloc plus Plan.AppendPreemptedAlloc of each preempted alloc
+ * (handlePreemptions, generic_sched.go:794-816): `preempted` are alloc-table
+ * rows, as returned in pe_ranked_node.preempted by a Select with Preempt. */
+int pe_commit_preempt(pe_stack* s, uint32_t tg_index, int32_t row, const uint32_t* preempted,
+                      uint32_t n_preempted);
 /* Fused count loop of GenericScheduler.computePlacements (generic_sched.go:493-649)
  * for `count` fresh placements of one task group (no preferred / penalty nodes):
  * Select -> AppendAlloc repeated on the device; stops at the first nil option

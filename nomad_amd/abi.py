@@ -14,6 +14,8 @@ f64p = C.POINTER(C.c_double)
 
 PE_NONE = 0xFFFFFFFF
 PE_MAX_SCORES = 8
+PE_MAX_PREEMPT = 16
+PE_MAX_DEVICE_REQ = 4
 PE_OK, PE_EINVAL, PE_ESTATE, PE_EHIP, PE_EUNSUPPORTED, PE_ENOMEM = 0, -1, -2, -3, -4, -5
 
 PE_ATTR_INT, PE_ATTR_FLOAT, PE_ATTR_STRING, PE_ATTR_BOOL = 1, 2, 3, 4
@@ -60,6 +62,7 @@ class pe_alloc_table(C.Structure):
         ("cpu_shares", i64p), ("memory_mb", i64p), ("disk_mb", i64p),
         ("net_mbits", i32p), ("dyn_ports", i32p),
         ("dev_off", u32p), ("dev_group", u32p), ("dev_count", u32p),
+        ("max_parallel", i32p),
     ]
 
 
@@ -154,7 +157,9 @@ class pe_ranked_node(C.Structure):
     _fields_ = [("row", C.c_int32), ("n_scores", C.c_uint32), ("final_score", C.c_double),
                 ("scores", C.c_double * PE_MAX_SCORES),
                 ("nodes_evaluated", C.c_uint32), ("nodes_filtered", C.c_uint32),
-                ("nodes_exhausted", C.c_uint32), ("new_offset", C.c_uint32)]
+                ("nodes_exhausted", C.c_uint32), ("new_offset", C.c_uint32),
+                ("n_preempted", C.c_uint32), ("preempted", C.c_uint32 * PE_MAX_PREEMPT),
+                ("n_device_offers", C.c_uint32), ("device_offer_group", C.c_uint32 * PE_MAX_DEVICE_REQ)]
 
 
 class pe_placement(C.Structure):
@@ -173,6 +178,7 @@ def _sigs(prefix, handle):
         (prefix + "select", C.c_int, [H, C.c_uint32, C.POINTER(pe_select_options),
                                       C.POINTER(pe_ranked_node)]),
         (prefix + "commit", C.c_int, [H, C.c_uint32, C.c_int32]),
+        (prefix + "commit_preempt", C.c_int, [H, C.c_uint32, C.c_int32, u32p, C.c_uint32]),
         (prefix + "place", C.c_int, [H, C.c_uint32, C.c_uint32, C.POINTER(pe_ranked_node), u32p]),
         (prefix + "system_place", C.c_int, [H, C.c_uint32, f64p, u8p, u32p]),
     ]
@@ -180,7 +186,7 @@ def _sigs(prefix, handle):
 
 ENGINE_SYMBOLS = [
     "pe_abi_version", "pe_stack_create", "pe_stack_destroy", "pe_last_error", "pe_set_state",
-    "pe_reset_plan", "pe_set_job", "pe_set_nodes", "pe_select", "pe_commit", "pe_place", "pe_system_place",
+    "pe_reset_plan", "pe_set_job", "pe_set_nodes", "pe_select", "pe_commit", "pe_commit_preempt", "pe_place", "pe_system_place",
     "pe_last_kernel_ms", "pe_stage_orders", "pe_place_batch", "pe_batch_results", "pe_last_phase_ms",
     "pe_check_constraint", "pe_last_sweep_bytes",
 ]

@@ -1,5 +1,7 @@
 // Host-side constraint semantics (see constraint_eval.h).
 #include "constraint_eval.h"
+#include <cmath>
+#include <cstring>
 
 #include <algorithm>
 #include <cctype>
@@ -297,6 +299,193 @@ bool ConstraintEvaluator::check(const std::string& op, const Target& l, const Ta
     if (op == "regexp") return l.found && r.found && regexp_match(l, r);
     if (op == "set_contains" || op == "set_contains_all") return l.found && r.found && set_contains(l, r, true);
     if (op == "set_contains_any") return l.found && r.found && set_contains(l, r, false);
+    return false;
+}
+
+// ---- device attributes ------------------------------------------------------
+namespace {
+struct UnitInfo { const char* name; uint8_t base; int64_t mult; bool inverse; };
+// plugins/shared/structs/units.go: byte, byte-rate, hertz, watt families
+const UnitInfo kUnits[] = {
+    {"KiB", 1, 1ll << 10, false}, {"MiB", 1, 1ll << 20, false}, {"GiB", 1, 1ll << 30, false},
+    {"TiB", 1, 1ll << 40, false}, {"PiB", 1, 1ll << 50, false}, {"EiB", 1, 1ll << 60, false},
+    {"kB", 1, 1000ll, false}, {"KB", 1, 1000ll, false}, {"MB", 1, 1000000ll, false},
+    {"GB", 1, 1000000000ll, false}, {"TB", 1, 1000000000000ll, false},
+    {"PB", 1, 1000000000000000ll, false}, {"EB", 1, 1000000000000000000ll, false},
+    {"KiB/s", 2, 1ll << 10, false}, {"MiB/s", 2, 1ll << 20, false}, {"GiB/s", 2, 1ll << 30, false},
+    {"TiB/s", 2, 1ll << 40, false}, {"PiB/s", 2, 1ll << 50, false}, {"EiB/s", 2, 1ll << 60, false},
+    {"kB/s", 2, 1000ll, false}, {"KB/s", 2, 1000ll, false}, {"MB/s", 2, 1000000ll, false},
+    {"GB/s", 2, 1000000000ll, false}, {"TB/s", 2, 1000000000000ll, false},
+    {"PB/s", 2, 1000000000000000ll, false}, {"EB/s", 2, 1000000000000000000ll, false},
+    {"MHz", 3, 1000000ll, false}, {"GHz", 3, 1000000000ll, false},
+    {"mW", 4, 1000ll, true}, {"W", 4, 1ll, false}, {"kW", 4, 1000ll, false},
+    {"MW", 4, 1000000ll, false}, {"GW", 4, 1000000000ll, false},
+};
+
+const UnitInfo* unit_of(const std::string& u) {
+    if (u.empty()) return nullptr;
+    for (const auto& x : kUnits) if (u == x.name) return &x;
+    return nullptr;
+}
+
+bool go_parse_int(const std::string& s, int64_t* out) {   // strconv.ParseInt(s, 10, 64)
+    if (s.empty()) return false;
+    size_t i = (s[0] == '+' || s[0] == '-') ? 1 : 0;
+    if (i == s.size()) return false;
+    unsigned __int128 v = 0;
+    for (size_t k = i; k < s.size(); k++) {
+        if (s[k] < '0' || s[k] > '9') return false;
+        v = v * 10 + (unsigned)(s[k] - '0');
+        if (v > ((unsigned __int128)1 << 63)) return false;
+    }
+    const bool neg = s[0] == '-';
+    if (!neg && v > (unsigned __int128)INT64_MAX) return false;
+    *out = neg ? (int64_t)(0 - (uint64_t)v) : (int64_t)v;
+    return true;
+}
+
+bool go_parse_float(const std::string& s, double* out) {   // strconv.ParseFloat(s, 64), decimal forms
+    if (s.empty()) return false;
+    std::string low;
+    for (char c : s) low.push_back((char)std::tolower((unsigned char)c));
+    const size_t sign = (low[0] == '+' || low[0] == '-') ? 1 : 0;
+    const std::string body = low.substr(sign);
+    if (body == "inf" || body == "infinity") { *out = low[0] == '-' ? -HUGE_VAL : HUGE_VAL; return true; }
+    if (body == "nan" && sign == 0) { *out = std::nan(""); return true; }
+    size_t k = sign;
+    bool digit = false, dot = false;
+    for (; k < low.size(); k++) {
+        if (low[k] >= '0' && low[k] <= '9') digit = true;
+        else if (low[k] == '.' && !dot) dot = true;
+        else break;
+    }
+    if (!digit) return false;
+    if (k < low.size() && low[k] == 'e') {
+        k++;
+        if (k < low.size() && (low[k] == '+' || low[k] == '-')) k++;
+        const size_t e0 = k;
+        while (k < low.size() && low[k] >= '0' && low[k] <= '9') k++;
+        if (k == e0) return false;
+    }
+    if (k != low.size()) return false;
+    *out = std::strtod(s.c_str(), nullptr);
+    return true;
+}
+}  // namespace
+
+DevAttr parse_dev_attr(const std::string& in) {
+    DevAttr a;
+    a.kind = DevAttr::kString;
+    if (in.empty()) return a;
+    std::string unit, numeric = in;
+    if (std::isalpha((unsigned char)in.back())) {
+        size_t best = 0;   // lengthSortedUnits: the longest matching suffix wins
+        for (const auto& u : kUnits) {
+            const size_t n = std::strlen(u.name);
+            if (n > best && in.size() >= n && in.compare(in.size() - n, n, u.name) == 0) {
+                best = n;
+                unit = u.name;
+            }
+        }
+        if (!unit.empty()) numeric = strip(in.substr(0, in.size() - unit.size()));
+    }
+    if (go_parse_int(numeric, &a.i)) { a.kind = DevAttr::kInt; a.unit = unit; return a; }
+    if (go_parse_float(numeric, &a.f)) { a.kind = DevAttr::kFloat; a.unit = unit; return a; }
+    if (in == "1" || in == "t" || in == "T" || in == "TRUE" || in == "true" || in == "True") {
+        a.kind = DevAttr::kBool; a.b = true; return a;
+    }
+    if (in == "0" || in == "f" || in == "F" || in == "FALSE" || in == "false" || in == "False") {
+        a.kind = DevAttr::kBool; a.b = false; return a;
+    }
+    a.s = in;
+    return a;
+}
+
+int compare_dev_attr(const DevAttr& a, const DevAttr& b, bool* ok) {
+    *ok = false;
+    const UnitInfo* ua = unit_of(a.unit);
+    const UnitInfo* ub = unit_of(b.unit);
+    // Comparable (attribute.go:296-320)
+    if (ua || ub) {
+        if (!(ua && ub) || ua->base != ub->base) return 0;
+    } else if (a.kind == DevAttr::kString && b.kind != DevAttr::kString) {
+        return 0;
+    } else if (a.kind == DevAttr::kBool && b.kind != DevAttr::kBool) {
+        return 0;
+    }
+    switch (a.kind) {
+        case DevAttr::kBool: *ok = true; return a.b == b.b ? 0 : 1;
+        case DevAttr::kString: *ok = true; return a.s == b.s ? 0 : (a.s < b.s ? -1 : 1);
+        case DevAttr::kInt:
+        case DevAttr::kFloat: break;
+        default: return 0;   // nullComparator
+    }
+    if (a.kind == DevAttr::kInt && b.kind == DevAttr::kInt) {   // intComparator on getInt()
+        auto scaled = [](const DevAttr& x, const UnitInfo* u) -> int64_t {
+            if (!u) return x.i;
+            return u->inverse ? x.i / u->mult : (int64_t)((uint64_t)x.i * (uint64_t)u->mult);
+        };
+        const int64_t x = scaled(a, ua), y = scaled(b, ub);
+        *ok = true;
+        return x == y ? 0 : (x < y ? -1 : 1);
+    }
+    if (b.kind != DevAttr::kInt && b.kind != DevAttr::kFloat) return 0;
+    // getBigFloat: value x multiplier (1/multiplier for inverse units)
+    auto big = [](const DevAttr& x, const UnitInfo* u) -> long double {
+        const long double v = x.kind == DevAttr::kInt ? (long double)x.i : (long double)x.f;
+        if (!u) return v;
+        return u->inverse ? v * (1.0L / (long double)u->mult) : v * (long double)u->mult;
+    };
+    const long double x = big(a, ua), y = big(b, ub);
+    *ok = true;
+    return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+bool ConstraintEvaluator::check_attr(const std::string& op, const DevAttr& l, bool lf, const DevAttr& r, bool rf) {
+    if (op == "distinct_hosts" || op == "distinct_property") return true;
+    const bool eq_ops = op == "=" || op == "==" || op == "is";
+    const bool ord_ops = op == "<" || op == "<=" || op == ">" || op == ">=";
+    if (op == "!=" || op == "not") {
+        if (!lf && !rf) return false;
+        if (lf != rf) return true;
+        bool ok;
+        const int v = compare_dev_attr(l, r, &ok);
+        return ok && v != 0;
+    }
+    if (eq_ops || ord_ops) {
+        if (!(lf && rf)) return false;
+        bool ok;
+        const int v = compare_dev_attr(l, r, &ok);
+        if (!ok) return false;
+        if (eq_ops) return v == 0;
+        if (op == "<") return v == -1;
+        if (op == "<=") return v != 1;
+        if (op == ">") return v == 1;
+        return v != -1;
+    }
+    if (op == "is_set") return lf;
+    if (op == "is_not_set") return !lf;
+    if (!(lf && rf)) return false;
+    if (op == "version" || op == "semver") {   // checkAttributeVersionMatch (feasible.go:896-930)
+        Target tl, tr;
+        tl.nil = tr.nil = false;
+        tl.found = tr.found = true;
+        if (l.kind == DevAttr::kString) tl.value = l.s;
+        else if (l.kind == DevAttr::kInt) tl.value = std::to_string(l.i);
+        else return false;
+        if (r.kind != DevAttr::kString) return false;
+        tr.value = r.s;
+        return version_match(op == "semver", tl, tr);
+    }
+    if (l.kind != DevAttr::kString || r.kind != DevAttr::kString) return false;
+    Target tl, tr;
+    tl.nil = tr.nil = false;
+    tl.found = tr.found = true;
+    tl.value = l.s;
+    tr.value = r.s;
+    if (op == "regexp") return regexp_match(tl, tr);
+    if (op == "set_contains" || op == "set_contains_all") return set_contains(tl, tr, true);
+    if (op == "set_contains_any") return set_contains(tl, tr, false);
     return false;
 }
 

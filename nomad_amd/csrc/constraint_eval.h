@@ -43,10 +43,26 @@ struct VersionConstraint {
 bool parse_version_constraints(const std::string& s, bool semver, std::vector<VersionConstraint>* out);
 bool check_version_constraints(const std::vector<VersionConstraint>& cs, const SemVer& v, bool semver);
 
+// Typed device attribute (plugins/shared/structs/attribute.go:85-101).
+struct DevAttr {
+    enum Kind : uint8_t { kNone, kInt, kFloat, kString, kBool } kind = kNone;
+    int64_t i = 0;
+    double f = 0;
+    bool b = false;
+    std::string s;
+    std::string unit;
+};
+// psstructs.ParseAttribute (attribute.go:55-103)
+DevAttr parse_dev_attr(const std::string& in);
+// Attribute.Compare (attribute.go:322-385); *ok = comparable
+int compare_dev_attr(const DevAttr& a, const DevAttr& b, bool* ok);
+
 class ConstraintEvaluator {
 public:
     // checkConstraint (feasible.go:785-820)
     bool check(const std::string& op, const Target& l, const Target& r);
+    // checkAttributeConstraint (feasible.go:1334-1447), also checkAttributeAffinity
+    bool check_attr(const std::string& op, const DevAttr& l, bool lf, const DevAttr& r, bool rf);
 
 private:
     bool version_match(bool semver, const Target& l, const Target& r);

@@ -146,6 +146,29 @@ struct NodeView {
 struct HostAlloc {
     uint32_t row, ns, job, tg;
     bool terminal;
+    int32_t priority = 0, max_parallel = 0;
+    int64_t cpu = 0, mem = 0, disk = 0;
+    uint32_t dev_begin = 0, dev_end = 0;   // into pe_stack::alloc_dev
+};
+
+// One device group of a node (NodeResources.Devices[i], structs.go:2980-3010).
+struct HostDevGroup {
+    uint32_t vendor, type, name, healthy;
+    uint32_t attr_begin, attr_end;          // into pe_stack::dev_attr
+};
+
+// A device-request target parsed once (resolveDeviceTarget, feasible.go:1304-1330).
+struct DevTarget {
+    int kind;            // 0 literal, 1 model, 2 vendor, 3 type, 4 attr, 5 unknown interpolation
+    pe::DevAttr literal;
+    uint32_t key;        // attr key str id (PE_NONE: never interned -> absent)
+};
+struct DevCond { DevTarget l, r; std::string op; int32_t weight; };
+struct DevReqSpec {
+    std::string vendor, type, name;   // RequestedDevice.ID() (structs.go:2738-2761)
+    bool nil_id;
+    uint32_t count;
+    std::vector<DevCond> constraints, affinities;
 };
 
 enum TargetKind { T_LITERAL, T_ID, T_DC, T_NAME, T_CLASS, T_ATTR, T_META, T_NIL };
@@ -205,6 +228,11 @@ struct TgPlan {
     bool has_aff_table = false, node_aff_used = false, node_ok_used = false, alias_used = false;
     std::vector<std::unique_ptr<PsetDev>> psets;
     bool psets_built = false;
+    // device requests (tasks in order) and the per-class match table
+    std::vector<DevReqSpec> dev_reqs;
+    DevMem dev_cls;
+    bool dev_cls_valid = false;
+    uint32_t* dev_free = nullptr;      // stack's dynamic free-instance column when dev_reqs is non-empty
     // memo emulation inputs
     std::vector<uint8_t> sig_tg, class_uniform, class_verdict, job_ok_node;
     std::vector<uint32_t> nonuniform;
@@ -239,6 +267,15 @@ struct pe_stack {
     std::vector<KF> drv_kf, hv_kf;
     std::vector<uint32_t> net_mode_ids, alias_ids;
     std::vector<HostAlloc> allocs;
+    std::vector<std::pair<uint32_t, uint32_t>> alloc_dev;   // (device group on the node, instances held)
+    // device groups per node (CSR) and their attributes
+    std::vector<uint32_t> dev_off;
+    std::vector<HostDevGroup> dev_groups;
+    std::vector<std::pair<uint32_t, pe::DevAttr>> dev_attr;   // sorted by key per group
+    uint32_t max_dev_groups = 0;
+    bool dev_packable = true;          // every node fits the packed 4 x u8 free-count column
+    std::vector<uint32_t> h_dev_free;  // snapshot free healthy instances per group (no plan)
+    DevMem d_dev_free, d_dev_free_base;
     uint32_t ncls = 0;
     std::vector<uint32_t> class_rep;   // first row of each class
     // Nodes with equal ComputedClass AND equal non-hashed checker inputs
@@ -415,6 +452,154 @@ bool meets(const pe_stack* s, pe::ConstraintEvaluator& ev, const ParsedConstrain
     return ev.check(c.op, l, r);
 }
 
+// ---- devices (host side) ------------------------------------------------------
+DevTarget parse_dev_target(const pe_stack* s, const std::string& t) {
+    DevTarget d;
+    d.key = PE_NONE;
+    if (t.rfind("${", 0) != 0) { d.kind = 0; d.literal = pe::parse_dev_attr(t); return d; }
+    if (t == "${device.model}") { d.kind = 1; return d; }
+    if (t == "${device.vendor}") { d.kind = 2; return d; }
+    if (t == "${device.type}") { d.kind = 3; return d; }
+    if (t.rfind("${device.attr.", 0) == 0) {
+        std::string k = t.substr(14);
+        if (!k.empty() && k.back() == '}') k.pop_back();
+        d.kind = 4;
+        d.key = s->lookup(k);
+        return d;
+    }
+    d.kind = 5;
+    return d;
+}
+
+// resolveDeviceTarget (feasible.go:1304-1330); returns found
+bool dev_resolve(const pe_stack* s, const DevTarget& t, const HostDevGroup& g, pe::DevAttr* out) {
+    switch (t.kind) {
+        case 0: *out = t.literal; return true;
+        case 1: out->kind = pe::DevAttr::kString; out->s = s->S(g.name); return true;
+        case 2: out->kind = pe::DevAttr::kString; out->s = s->S(g.vendor); return true;
+        case 3: out->kind = pe::DevAttr::kString; out->s = s->S(g.type); return true;
+        case 4: {
+            if (t.key == PE_NONE) return false;
+            auto b = s->dev_attr.begin() + g.attr_begin, e = s->dev_attr.begin() + g.attr_end;
+            auto it = std::lower_bound(b, e, t.key, [](const auto& x, uint32_t k) { return x.first < k; });
+            if (it == e || it->first != t.key) return false;
+            *out = it->second;
+            return true;
+        }
+        default: return false;
+    }
+}
+
+bool dev_cond(const pe_stack* s, pe::ConstraintEvaluator& ev, const DevCond& c, const HostDevGroup& g) {
+    pe::DevAttr l, r;
+    const bool lf = dev_resolve(s, c.l, g, &l), rf = dev_resolve(s, c.r, g, &r);
+    return ev.check_attr(c.op, l, lf, r, rf);
+}
+
+// nodeDeviceMatches (feasible.go:1278-1300) with DeviceIdTuple.Matches (structs.go:3130-3148)
+bool dev_matches(const pe_stack* s, pe::ConstraintEvaluator& ev, const DevReqSpec& q, const HostDevGroup& g) {
+    if (q.nil_id) return false;
+    if (!q.name.empty() && q.name != s->S(g.name)) return false;
+    if (!q.vendor.empty() && q.vendor != s->S(g.vendor)) return false;
+    if (!q.type.empty() && q.type != s->S(g.type)) return false;
+    for (auto& c : q.constraints)
+        if (!dev_cond(s, ev, c, g)) return false;
+    return true;
+}
+
+// DeviceChecker.hasDevices (feasible.go:1206-1274): healthy instances, groups in node order.
+bool has_devices(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g, uint32_t row) {
+    if (g.dev_reqs.empty()) return true;
+    const uint32_t b = s->dev_off[row], e = s->dev_off[row + 1];
+    if (b == e) return false;
+    std::vector<int64_t> avail(e - b);
+    for (uint32_t k = b; k < e; k++) avail[k - b] = s->dev_groups[k].healthy;
+    for (const DevReqSpec& q : g.dev_reqs) {
+        bool ok = false;
+        for (uint32_t k = b; k < e; k++) {
+            if (s->dev_groups[k].healthy == 0) continue;
+            const int64_t unused = avail[k - b];
+            if (unused == 0 || unused < (int64_t)q.count) continue;
+            if (dev_matches(s, ev, q, s->dev_groups[k])) {
+                avail[k - b] -= q.count;
+                ok = true;
+                break;
+            }
+        }
+        if (!ok) return false;
+    }
+    return true;
+}
+
+DevReqSpec parse_dev_request(const pe_stack* s, const pe_job* j, const pe_device_request& r) {
+    DevReqSpec q;
+    const std::string nm = s->S(r.name);
+    q.nil_id = nm.empty();
+    std::vector<std::string> parts;   // strings.SplitN(name, "/", 3)
+    size_t start = 0;
+    while (parts.size() < 2) {
+        const size_t k = nm.find('/', start);
+        if (k == std::string::npos) break;
+        parts.push_back(nm.substr(start, k - start));
+        start = k + 1;
+    }
+    parts.push_back(nm.substr(start));
+    if (parts.size() == 1) q.type = parts[0];
+    else if (parts.size() == 2) { q.vendor = parts[0]; q.type = parts[1]; }
+    else { q.vendor = parts[0]; q.type = parts[1]; q.name = parts[2]; }
+    q.count = (uint32_t)std::min<uint64_t>(r.count, 0xFFFFFFFFull);
+    for (uint32_t k = 0; k < r.constraint_count; k++) {
+        const pe_constraint& c = j->device_constraints[r.constraint_off + k];
+        q.constraints.push_back(DevCond{parse_dev_target(s, s->S(c.ltarget)), parse_dev_target(s, s->S(c.rtarget)),
+                                        s->S(c.operand), 0});
+    }
+    for (uint32_t k = 0; k < r.affinity_count; k++) {
+        const pe_affinity& a = j->device_affinities[r.affinity_off + k];
+        q.affinities.push_back(DevCond{parse_dev_target(s, s->S(a.ltarget)), parse_dev_target(s, s->S(a.rtarget)),
+                                       s->S(a.operand), a.weight});
+    }
+    return q;
+}
+
+// Per-class device table: match bits and AssignDevice scores of each request
+// against each device group of the class (class representative's groups).
+int build_dev_classes(pe_stack* s, TgPlan& g) {
+    pe::ConstraintEvaluator ev;
+    std::vector<pe::DevClass> tab(std::max<uint32_t>(s->ncls, 1));
+    std::memset(tab.data(), 0, sizeof(pe::DevClass) * tab.size());
+    for (uint32_t c = 0; c < s->ncls; c++) {
+        const uint32_t row = s->class_rep[c];
+        const uint32_t b = s->dev_off[row], e = s->dev_off[row + 1];
+        pe::DevClass& d = tab[c];
+        d.n_groups = e - b;
+        for (size_t q = 0; q < g.dev_reqs.size(); q++) {
+            const DevReqSpec& r = g.dev_reqs[q];
+            for (uint32_t k = b; k < e; k++) {
+                const HostDevGroup& grp = s->dev_groups[k];
+                if (!dev_matches(s, ev, r, grp)) continue;
+                d.match[q] |= (uint8_t)(1u << (k - b));
+                double choice = 0, sum = 0;
+                if (!r.affinities.empty()) {   // device.go:72-93
+                    double total = 0;
+                    for (auto& a : r.affinities) {
+                        total += std::fabs((double)a.weight);
+                        if (!dev_cond(s, ev, a, grp)) continue;
+                        choice += (double)a.weight;
+                        sum += (double)a.weight;
+                    }
+                    choice /= total;
+                }
+                d.choice[q][k - b] = choice;
+                d.matched[q][k - b] = sum;
+            }
+        }
+    }
+    HIP_TRY(s, upload(g.dev_cls, tab));
+    g.dev_cls_valid = true;
+    g.dev_free = s->d_dev_free.as<uint32_t>();
+    return PE_OK;
+}
+
 // job checkers (ConstraintChecker over job constraints)
 bool job_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const NodeView& n) {
     for (auto& c : s->job_constraints) if (!meets(s, ev, c, n)) return false;
@@ -450,6 +635,7 @@ bool tg_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g
             for (bool ro : kv.second) if (!ro) return false;
         }
     }
+    if (!has_devices(s, ev, g, n.row)) return false;
     {   // NetworkChecker (feasible.go:362-429): runs for every task group; without a
         // tg network it keeps the mode of the last one set (default "host").
         const std::string want = s->S(g.net_mode).empty() ? std::string("host") : s->S(g.net_mode);
@@ -585,6 +771,39 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
         r.used_dyn = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
     }
     s->ncls = (uint32_t)s->class_rep.size();
+    // device groups (NodeResources.Devices) with typed attributes
+    s->dev_off.assign(n + 1, 0);
+    s->dev_groups.clear();
+    s->dev_attr.clear();
+    s->max_dev_groups = 0;
+    s->dev_packable = true;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t g0 = nt->dev_off ? nt->dev_off[i] : 0, g1 = nt->dev_off ? nt->dev_off[i + 1] : 0;
+        for (uint32_t g = g0; g < g1; g++) {
+            HostDevGroup d{nt->dev_vendor[g], nt->dev_type[g], nt->dev_name[g], nt->dev_healthy[g], 0, 0};
+            d.attr_begin = (uint32_t)s->dev_attr.size();
+            for (uint32_t q = nt->dev_attr_off ? nt->dev_attr_off[g] : 0;
+                 nt->dev_attr_off && q < nt->dev_attr_off[g + 1]; q++) {
+                const pe_attr& pa = nt->dev_attr_val[q];
+                pe::DevAttr a;
+                switch (pa.kind) {
+                    case PE_ATTR_INT: a.kind = pe::DevAttr::kInt; a.i = pa.i; a.unit = s->S(pa.unit); break;
+                    case PE_ATTR_FLOAT: a.kind = pe::DevAttr::kFloat; a.f = pa.f; a.unit = s->S(pa.unit); break;
+                    case PE_ATTR_BOOL: a.kind = pe::DevAttr::kBool; a.b = pa.i != 0; break;
+                    default: a.kind = pe::DevAttr::kString; a.s = s->S(pa.s); break;
+                }
+                s->dev_attr.emplace_back(nt->dev_attr_key[q], a);
+            }
+            d.attr_end = (uint32_t)s->dev_attr.size();
+            std::sort(s->dev_attr.begin() + d.attr_begin, s->dev_attr.begin() + d.attr_end,
+                      [](const auto& x, const auto& y) { return x.first < y.first; });
+            if (d.healthy > 255) s->dev_packable = false;
+            s->dev_groups.push_back(d);
+        }
+        s->dev_off[i + 1] = (uint32_t)s->dev_groups.size();
+        s->max_dev_groups = std::max(s->max_dev_groups, g1 - g0);
+    }
+    if (s->max_dev_groups > (uint32_t)pe::kMaxDevGroups) s->dev_packable = false;
     // checker-input signatures
     {
         // 64-bit hash of the checker inputs; equal hashes are verified exactly
@@ -596,7 +815,11 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
         auto same_inputs = [&](uint32_t a_row, uint32_t b_row) {
             const NodeView x = s->view(a_row), y = s->view(b_row);
             auto eq = [](auto u, auto v) { return u.size() == v.size() && std::equal(u.begin(), u.end(), v.begin()); };
-            return x.h->cls == y.h->cls && x.h->n_devices == y.h->n_devices && eq(x.drivers, y.drivers) &&
+            if (x.h->n_devices != y.h->n_devices) return false;
+            for (uint32_t k = 0; k < x.h->n_devices; k++)   // DeviceChecker reads healthy counts
+                if (s->dev_groups[s->dev_off[a_row] + k].healthy != s->dev_groups[s->dev_off[b_row] + k].healthy)
+                    return false;
+            return x.h->cls == y.h->cls && eq(x.drivers, y.drivers) &&
                    eq(x.net_modes, y.net_modes) && eq(x.aliases, y.aliases) && eq(x.volumes, y.volumes);
         };
         for (uint32_t i = 0; i < n; i++) {
@@ -606,6 +829,7 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
             auto mix = [&](uint64_t y) { x = (x ^ y) * 1099511628211ull; x ^= x >> 29; };
             mix(h.cls);
             mix(h.n_devices);
+            for (uint32_t k = s->dev_off[i]; k < s->dev_off[i + 1]; k++) mix(s->dev_groups[k].healthy);
             mix(v.drivers.size());
             for (auto& d : v.drivers) { mix(d.first); mix(d.second); }
             mix(v.net_modes.size());
@@ -629,10 +853,23 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
         }
     }
     s->allocs.clear();
+    s->alloc_dev.clear();
+    std::vector<int64_t> dev_used(s->dev_groups.size(), 0);
     for (uint32_t i = 0; at && i < at->count; i++) {
         const uint32_t row = at->node_row[i];
         if (row >= n) return s->fail(PE_EINVAL, "alloc node_row out of range");
         HostAlloc a{row, at->ns[i], at->job_id[i], at->task_group[i], at->terminal[i] != 0};
+        a.priority = at->priority ? at->priority[i] : 0;
+        a.max_parallel = at->max_parallel ? at->max_parallel[i] : 0;
+        a.cpu = at->cpu_shares[i]; a.mem = at->memory_mb[i]; a.disk = at->disk_mb[i];
+        a.dev_begin = (uint32_t)s->alloc_dev.size();
+        for (uint32_t k = at->dev_off ? at->dev_off[i] : 0; at->dev_off && k < at->dev_off[i + 1]; k++) {
+            s->alloc_dev.emplace_back(at->dev_group[k], at->dev_count[k]);
+            const uint32_t g = at->dev_group[k];
+            if (!a.terminal && g < s->dev_off[row + 1] - s->dev_off[row])
+                dev_used[s->dev_off[row] + g] += at->dev_count[k];
+        }
+        a.dev_end = (uint32_t)s->alloc_dev.size();
         s->allocs.push_back(a);
         if (a.terminal) continue;
         pe::NodeRec& r = s->h_base_rec[row];
@@ -644,6 +881,17 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     }
     HIP_TRY(s, upload(s->d_base_rec, s->h_base_rec));
     HIP_TRY(s, upload(s->d_rec, s->h_base_rec));
+    // DeviceAccounter free counts (devices.go:25-100) packed 4 x u8 per node
+    s->h_dev_free.assign(n, 0);
+    if (s->dev_packable)
+        for (uint32_t i = 0; i < n; i++)
+            for (uint32_t k = 0; k < s->dev_off[i + 1] - s->dev_off[i]; k++) {
+                const uint32_t g = s->dev_off[i] + k;
+                const int64_t f = std::max<int64_t>(0, (int64_t)s->dev_groups[g].healthy - dev_used[g]);
+                s->h_dev_free[i] |= (uint32_t)f << (8 * k);
+            }
+    HIP_TRY(s, upload(s->d_dev_free_base, s->h_dev_free));
+    HIP_TRY(s, upload(s->d_dev_free, s->h_dev_free));
     std::vector<uint32_t> zeros(n, 0);
     HIP_TRY(s, upload(s->d_coll_job, zeros));
     return PE_OK;
@@ -921,6 +1169,10 @@ pe::TgTables tables_of(TgPlan& g) {
     t.node_aff = g.node_aff_used ? g.node_aff.as<double>() : nullptr;
     t.alias_ok = g.alias_used ? g.alias_ok.as<uint8_t>() : nullptr;
     t.coll_tg = g.coll_tg.as<uint32_t>();
+    if (!g.dev_reqs.empty()) {
+        t.dev_free = g.dev_free;
+        t.dev_cls = g.dev_cls.as<pe::DevClass>();
+    }
     t.n_psets = (int)g.psets.size();
     for (int p = 0; p < t.n_psets; p++) {
         PsetDev& ps = *g.psets[p];
@@ -1125,6 +1377,8 @@ int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_r
         out->final_score = rr.final_score;
         out->n_scores = rr.n_scores;
         std::memcpy(out->scores, rr.scores, sizeof(out->scores));
+        out->n_device_offers = rr.n_device_offers;
+        std::memcpy(out->device_offer_group, rr.device_offer_group, sizeof(out->device_offer_group));
     }
     return PE_OK;
 }
@@ -1318,6 +1572,8 @@ int pe_reset_plan(pe_stack* s) {
     const size_t n = s->nodes.size();
     HIP_TRY(s, hipMemcpyAsync(s->d_rec.p, s->d_base_rec.p, n * sizeof(pe::NodeRec), hipMemcpyDeviceToDevice,
                               s->stream));
+    HIP_TRY(s, hipMemcpyAsync(s->d_dev_free.p, s->d_dev_free_base.p, n * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                              s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     s->plan.clear();
     s->tg_memo.clear();
@@ -1392,7 +1648,8 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
             const pe_task& x = j->tasks[t.task_off + k];
             g->drivers.insert(x.driver);
             for (uint32_t c = 0; c < x.constraint_count; c++) g->constraints.push_back(parse_constraint(s, j->constraints[x.constraint_off + c]));
-            if (x.device_count > 0) g->unsupported = "device requests";
+            for (uint32_t d = 0; d < x.device_count; d++)
+                g->dev_reqs.push_back(parse_dev_request(s, j, j->devices[x.device_off + d]));
             if (x.cores > 0) g->unsupported = "reserved cores";
             if (x.has_network && x.net_reserved_ports > 0) g->unsupported = "static port asks";
         }
@@ -1415,6 +1672,26 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
             for (uint32_t a = 0; a < x.affinity_count; a++)
                 g->affinities.push_back(ParsedAffinity{parse_constraint(s, *reinterpret_cast<const pe_constraint*>(&j->affinities[x.affinity_off + a])),
                                                        j->affinities[x.affinity_off + a].weight});
+        }
+        if (!g->dev_reqs.empty()) {
+            if (g->dev_reqs.size() > (size_t)pe::kMaxDevReq) g->unsupported = "more than 4 device requests";
+            else if (!s->dev_packable) g->unsupported = "nodes with more than 4 device groups or 255 instances";
+            g->ask.n_dev = (int32_t)g->dev_reqs.size();
+            g->ask.dev_aff = 0;
+            g->ask.dev_tw = 0.0;
+            for (size_t q = 0; q < g->dev_reqs.size() && q < (size_t)pe::kMaxDevReq; q++) {
+                const DevReqSpec& r = g->dev_reqs[q];
+                if (r.count > 255) g->unsupported = "device request count above 255";
+                g->ask.dev_cnt[q] = (int32_t)std::min<uint32_t>(r.count, 255);
+                if (!r.affinities.empty()) {
+                    g->ask.dev_aff |= 1u << q;
+                    for (auto& a : r.affinities) g->ask.dev_tw += std::fabs((double)a.weight);
+                }
+            }
+            if (g->unsupported.empty()) {
+                int rc = build_dev_classes(s, *g);
+                if (rc) return rc;
+            }
         }
         g->spreads = conv_spreads(t.spread_off, t.spread_count);
         if (!generic && (!g->spreads.empty() || !s->job_spreads.empty())) g->spreads.clear();
@@ -1540,6 +1817,12 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
             break;
         }
     return PE_OK;
+}
+
+int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
+    if (!s) return PE_EINVAL;
+    if (n_preempted == 0) return pe_commit(s, tgi, row);
+    return s->fail(PE_EUNSUPPORTED, "preemption");
 }
 
 int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {

@@ -12,6 +12,21 @@ constexpr uint32_t kMissing = 0xFFFFFFFFu;   // node has no value for the proper
 constexpr int32_t kDynPortCapacity = 32000 - 20000 + 1;   // IndexesInRange is inclusive
 constexpr int kMaxSkip = 3;           // stack.go:17 maxSkip
 constexpr int kPlaceBlock = 256;      // threads of the persistent count-loop workgroup
+constexpr int kMaxDevReq = 4;         // device requests per task group on device
+constexpr int kMaxDevGroups = 4;      // device groups per node on device (u8 free counts packed in a u32)
+
+// Static device-match table of one ComputedClass for the task group's device
+// requests (class-exact: Node.ComputeClass hashes device identity and
+// attributes, node_class.go:86-101). For request q and device group g of the
+// class: match bit (nodeDeviceMatches), the AssignDevice choice score
+// (Σ matched affinity weights / Σ |weights|, 0 without affinities) and the
+// matched weight sum.
+struct DevClass {
+    uint8_t match[kMaxDevReq];            // bit g: group g matches request q
+    uint32_t n_groups;
+    double choice[kMaxDevReq][kMaxDevGroups];
+    double matched[kMaxDevReq][kMaxDevGroups];
+};
 
 // One node of the snapshot in HBM: a 64-byte record (one cache line, four
 // 16-byte loads per lane) holding everything BinPack needs. Capacities are
@@ -50,6 +65,9 @@ struct TgTables {
     int pset_nvals[kMaxPsets];
     int pset_even[kMaxPsets];                    // no targets: evenSpreadScoreBoost
     double pset_weight_frac[kMaxPsets];          // float64(weight) / float64(sumSpreadWeights)
+    // devices (only when the task group requests devices, else null)
+    uint32_t* dev_free;                          // [n] free healthy instances per group, 4 x u8
+    const DevClass* dev_cls;                     // [ncls]
 };
 
 struct Ask {
@@ -62,6 +80,10 @@ struct Ask {
     int32_t distinct_job, distinct_tg;
     int32_t algo_spread;
     int32_t anti_aff;             // JobAntiAffinityIterator present (GenericStack only)
+    int32_t n_dev;                // device requests of the task group (tasks in order)
+    uint32_t dev_aff;             // bit q: request q has affinities
+    int32_t dev_cnt[kMaxDevReq];  // RequestedDevice.Count
+    double dev_tw;                // Σ |affinity weight| over requests with affinities (0: no score)
 };
 
 // One launch = n_evals independent evaluations (one workgroup each) of the same

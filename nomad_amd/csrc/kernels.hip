@@ -100,12 +100,58 @@ struct NodeIn {
     NodeRec r;
     uint32_t coll_tg;
     uint32_t feas;
+    uint32_t dev_free;   // free healthy instances per device group (4 x u8), device asks only
 };
 
 __device__ __forceinline__ void load_node(const NodeSoA& s, const TgTables& t, uint32_t row, NodeIn& in) {
     in.r = s.rec[row];
     in.coll_tg = t.coll_tg[row];
     in.feas = t.node_feas ? t.node_feas[row] : 1u;
+    in.dev_free = t.dev_free ? t.dev_free[row] : 0u;
+}
+
+// deviceAllocator.AssignDevice for the task group's requests in order
+// (scheduler/device.go:32-131, BinPack rank.go:366-414) on a node's packed
+// free counts: per request the best-scoring matching group with enough free
+// instances, equal scores -> the later group (the reference walks a map);
+// the offer's instances are consumed (AddReserved). Returns false when a
+// request cannot be met; *matched = Σ matched weights of requests with
+// affinities.
+__device__ __forceinline__ bool dev_assign(const Ask& a, const DevClass& dc, uint32_t& free, double* matched,
+                                           uint32_t* groups = nullptr) {
+    double sum = 0.0;
+    if (dc.n_groups == 0) return false;   // "no devices available"
+    for (int q = 0; q < kMaxDevReq; q++) {
+        if (q >= a.n_dev) break;
+        const uint32_t cnt = (uint32_t)a.dev_cnt[q];
+        if (cnt == 0) return false;       // "invalid request of zero devices"
+        int best = -1;
+        double best_score = 0.0;
+        for (int g = 0; g < kMaxDevGroups; g++) {
+            if (g >= (int)dc.n_groups) break;
+            const uint32_t f = (free >> (8 * g)) & 255u;
+            if (f < cnt || !((dc.match[q] >> g) & 1u)) continue;
+            const double sc = dc.choice[q][g];
+            if (best >= 0 && sc < best_score) continue;
+            best = g;
+            best_score = sc;
+        }
+        if (best < 0) return false;        // "no devices match request"
+        free -= cnt << (8 * best);
+        if (groups) groups[q] = (uint32_t)best;
+        if ((a.dev_aff >> q) & 1u) sum += dc.matched[q][best];
+    }
+    *matched = sum;
+    return true;
+}
+
+// Device state after k further placements of the task group on a node.
+__device__ __forceinline__ uint32_t dev_after(const Ask& a, const DevClass& dc, uint32_t free, uint32_t k) {
+    for (uint32_t j = 0; j < k; j++) {
+        double m;
+        dev_assign(a, dc, free, &m);
+    }
+    return free;
 }
 
 // Inputs of the scoring half of the pipeline (everything after AllocsFit).
@@ -114,6 +160,7 @@ __device__ __forceinline__ void load_node(const NodeSoA& s, const TgTables& t, u
 // scoring half is then pure arithmetic.
 struct ScoreIn {
     int64_t ccpu, cmem, ucpu, umem;   // capacity and proposed use including the ask
+    double dev_aff;                   // BinPack device-affinity score (appended when Ask::dev_tw != 0)
     double aff;                       // NodeAffinityIterator score (0 = not appended)
     double spread;                    // SpreadIterator total (0 = not appended)
     uint32_t coll;                    // proposed allocs of (job, tg) on the node
@@ -156,6 +203,14 @@ __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t
             if (avail < 0 || mb + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) return kExhausted;
         }
     }
+    si->dev_aff = 0.0;
+    if (a.n_dev > 0) {   // devices: this eval's dk earlier placements first consumed their offers
+        const DevClass& dc = t.dev_cls[c];
+        uint32_t fr = dev_after(a, dc, in.dev_free, dk);
+        double m;
+        if (!dev_assign(a, dc, fr, &m)) return kExhausted;
+        if (a.dev_tw != 0.0) si->dev_aff = m / a.dev_tw;
+    }
     const int64_t ucpu = r.used_cpu + (int64_t)(dk + 1) * a.cpu;
     const int64_t umem = r.used_mem + (int64_t)(dk + 1) * a.mem;
     const int64_t udisk = r.used_disk + (int64_t)(dk + 1) * a.disk;
@@ -191,6 +246,11 @@ __device__ __forceinline__ void score_option(const Ask& a, double log10, const S
     double sum = fit;
     uint32_t k = 1;
     if (kKeepParts) out->parts[0] = fit;
+    if (a.dev_tw != 0.0) {   // device affinity (rank.go:518-523)
+        sum += si.dev_aff;
+        if (kKeepParts) out->parts[k] = si.dev_aff;
+        k++;
+    }
     if (a.anti_aff && coll > 0) {   // JobAntiAffinityIterator (rank.go:588-591)
         const double pen = -1 * (double)(coll + 1) / (double)a.desired_count;
         sum += pen;
@@ -399,6 +459,22 @@ __device__ __forceinline__ void commit_overlay(const NodeSoA& s, const TgTables&
     }
 }
 
+// TaskResources device offers of the chosen node (one lane).
+__device__ __forceinline__ void record_offers(const NodeSoA& s, const Ask& a, const TgTables& t, uint32_t row,
+                                              uint32_t dk, pe_ranked_node* o) {
+    o->n_device_offers = 0;
+    o->n_preempted = 0;
+    if (a.n_dev <= 0) return;
+    const DevClass& dc = t.dev_cls[s.rec[row].cls];
+    uint32_t fr = dev_after(a, dc, t.dev_free[row], dk);
+    double m;
+    uint32_t groups[kMaxDevReq];
+    if (!dev_assign(a, dc, fr, &m, groups)) return;
+    o->n_device_offers = (uint32_t)a.n_dev;
+    for (int q = 0; q < kMaxDevReq; q++)
+        if (q < a.n_dev) o->device_offer_group[q] = groups[q];
+}
+
 // Result records of placement `it` of evaluation e (one lane).
 __device__ __forceinline__ void emit_placement(const BatchArgs& A, const uint8_t* class_ok, const Overlay& ov,
                                             const double* spread_tab, uint32_t e, uint32_t it, int win_row,
@@ -413,6 +489,8 @@ __device__ __forceinline__ void emit_placement(const BatchArgs& A, const uint8_t
         o.new_offset = new_offset;
         o.final_score = 0.0;
         o.n_scores = 0;
+        o.n_preempted = 0;
+        o.n_device_offers = 0;
         for (int k = 0; k < PE_MAX_SCORES; k++) o.scores[k] = 0.0;
         if (win_row >= 0) {
             NodeEval ev;
@@ -421,6 +499,7 @@ __device__ __forceinline__ void emit_placement(const BatchArgs& A, const uint8_t
             o.final_score = ev.score;
             o.n_scores = ev.nscores;
             for (int k = 0; k < (int)ev.nscores && k < PE_MAX_SCORES; k++) o.scores[k] = ev.parts[k];
+            record_offers(A.soa, A.ask, A.tg, (uint32_t)win_row, ov_count(ov, (uint32_t)win_row), &o);
         }
     }
     if (A.out) {
@@ -447,6 +526,7 @@ __device__ void writeback_overlay(const BatchArgs& A, const Overlay& ov, uint32_
         r.used_dyn += (int32_t)k * A.ask.commit_dyn;
         A.soa.coll_job[row] += k;
         A.tg.coll_tg[row] += k;
+        if (A.ask.n_dev > 0) A.tg.dev_free[row] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[row], k);
     }
     if constexpr (FULL) {
         for (int q = 0; q < A.tg.n_psets; q++)
@@ -1336,6 +1416,7 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
             r.used_dyn += A.ask.commit_dyn;
             A.soa.coll_job[row] += 1;
             A.tg.coll_tg[row] += 1;
+            if (A.ask.n_dev > 0) A.tg.dev_free[row] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[row], 1);
             local++;
         } else {
             A.out_score[i] = __builtin_nan("");
@@ -1358,6 +1439,7 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row) {
     s.coll_job[row] += 1;
     t.coll_tg[row] += 1;
     const uint32_t c = r.cls;
+    if (a.n_dev > 0) t.dev_free[row] = dev_after(a, t.dev_cls[c], t.dev_free[row], 1);
     for (int p = 0; p < t.n_psets; p++) {
         const uint32_t v = pset_value(t, p, row, c);
         if (v != kMissing) t.pset_counts[p][v] += 1;
@@ -1525,6 +1607,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AUX 
             if (AUX) {
                 nx.r = A.soa.rec[row];
                 nx.coll_tg = A.tg.coll_tg[row];
+                nx.dev_free = A.tg.dev_free ? A.tg.dev_free[row] : 0u;
                 naux = A.node_aux[row];
                 nx.feas = naux >> 31;
             } else {
@@ -1675,6 +1758,7 @@ __global__ void k_node_record(SweepArgs A, uint32_t row, pe_ranked_node* out) {
     out->final_score = ev.score;
     out->n_scores = ev.nscores;
     for (int k = 0; k < PE_MAX_SCORES; k++) out->scores[k] = k < (int)ev.nscores ? ev.parts[k] : 0.0;
+    record_offers(A.soa, A.ask, A.tg, row, 0u, out);
 }
 
 // node_feas[row] = class_ok[cls] && node_ok[row]: one verdict byte per node so

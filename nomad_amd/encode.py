@@ -167,12 +167,18 @@ class EncodedState:
         at.net_mbits = _ptr(acol(lambda a: a.net_mbits, _i32), abi.i32p)
         at.dyn_ports = _ptr(acol(lambda a: a.dyn_ports, _i32), abi.i32p)
         doff = np.zeros(len(live) + 1, dtype=np.uint32)
-        keep.append(doff)
+        dgrp, dcnt = [], []
+        for i, a in enumerate(live):
+            for g, c in a.devices:
+                dgrp.append(g)
+                dcnt.append(c)
+            doff[i + 1] = len(dgrp)
+        dgrp_a, dcnt_a = _u32(dgrp if dgrp else [0]), _u32(dcnt if dcnt else [0])
+        keep.extend([doff, dgrp_a, dcnt_a])
         at.dev_off = _ptr(doff, abi.u32p)
-        empty = _u32([0])
-        keep.append(empty)
-        at.dev_group = _ptr(empty, abi.u32p)
-        at.dev_count = _ptr(empty, abi.u32p)
+        at.dev_group = _ptr(dgrp_a, abi.u32p)
+        at.dev_count = _ptr(dcnt_a, abi.u32p)
+        at.max_parallel = _ptr(acol(lambda a: a.max_parallel, _i32), abi.i32p)
         self.alloc_table = at
 
     def strtab(self):
@@ -205,6 +211,7 @@ class EncodedJob:
     def __init__(self, job: Job, interner: Interner):
         I = interner.intern
         cons, affs, spreads, targets, tasks, tgs = [], [], [], [], [], []
+        devs, dcons, daffs = [], [], []
         vol_src, vol_ro = [], []
 
         def add_cons(cs):
@@ -250,6 +257,17 @@ class EncodedJob:
                     pt.net_dyn_ports, pt.net_reserved_ports = t.network.dynamic_ports, len(t.network.reserved_ports)
                 pt.constraint_off, pt.constraint_count = add_cons(t.constraints)
                 pt.affinity_off, pt.affinity_count = add_affs(t.affinities)
+                pt.device_off, pt.device_count = len(devs), len(t.devices)
+                for d in t.devices:
+                    r = abi.pe_device_request()
+                    r.name, r.count = I(d.name), d.count
+                    r.constraint_off, r.constraint_count = len(dcons), len(d.constraints)
+                    for c in d.constraints:
+                        dcons.append(abi.pe_constraint(I(c.ltarget), I(c.rtarget), I(c.operand)))
+                    r.affinity_off, r.affinity_count = len(daffs), len(d.affinities)
+                    for a in d.affinities:
+                        daffs.append(abi.pe_affinity(I(a.ltarget), I(a.rtarget), I(a.operand), a.weight))
+                    devs.append(r)
                 tasks.append(pt)
             g.task_count = len(tg.tasks)
             if tg.network is not None:
@@ -271,8 +289,8 @@ class EncodedJob:
             return (T * max(1, len(xs)))(*xs)
         self._arrays = [arr(abi.pe_task_group, tgs), arr(abi.pe_task, tasks), arr(abi.pe_constraint, cons),
                         arr(abi.pe_affinity, affs), arr(abi.pe_spread, spreads),
-                        arr(abi.pe_spread_target, targets), arr(abi.pe_device_request, []),
-                        arr(abi.pe_constraint, []), arr(abi.pe_affinity, [])]
+                        arr(abi.pe_spread_target, targets), arr(abi.pe_device_request, devs),
+                        arr(abi.pe_constraint, dcons), arr(abi.pe_affinity, daffs)]
         (pj.task_groups, pj.tasks, pj.constraints, pj.affinities, pj.spreads, pj.spread_targets,
          pj.devices, pj.device_constraints, pj.device_affinities) = (
             C.cast(a, C.POINTER(type(a._type_()))) for a in self._arrays)

@@ -85,6 +85,8 @@ class RankedNode:
     nodes_filtered: int = 0
     nodes_exhausted: int = 0
     new_offset: int = 0
+    preempted: List[int] = field(default_factory=list)   # PreemptedAllocs: alloc-table rows
+    device_offers: List[int] = field(default_factory=list)   # chosen device group per request
 
     @classmethod
     def from_c(cls, r: abi.pe_ranked_node, nodes):
@@ -92,7 +94,8 @@ class RankedNode:
                    final_score=r.final_score,
                    scores=[r.scores[i] for i in range(r.n_scores)], nodes_evaluated=r.nodes_evaluated,
                    nodes_filtered=r.nodes_filtered, nodes_exhausted=r.nodes_exhausted,
-                   new_offset=r.new_offset)
+                   new_offset=r.new_offset, preempted=[r.preempted[i] for i in range(r.n_preempted)],
+                   device_offers=[r.device_offer_group[i] for i in range(r.n_device_offers)])
 
 
 class _Stack:
@@ -110,7 +113,8 @@ class _Stack:
         cfg.batch = int(batch)
         cfg.algorithm = abi.PE_ALGO_SPREAD if config.algorithm == "spread" else abi.PE_ALGO_BINPACK
         cfg.memory_oversubscription = int(config.memory_oversubscription)
-        cfg.preempt = int(config.preempt_system) if self.stack_kind == abi.PE_STACK_SYSTEM else 0
+        cfg.preempt = int(config.preempt_system if self.stack_kind == abi.PE_STACK_SYSTEM
+                          else config.preempt_service)
         cfg.device = device
         self._cfg = cfg
         create = getattr(lib, prefix + ("stack_create" if prefix == "pe_" else "create"))
@@ -218,12 +222,20 @@ class _Stack:
         """Select, but also returns the metrics when no node was found."""
         out = abi.pe_ranked_node()
         opts = abi.pe_select_options()
+        if options is not None:
+            opts.preempt = int(options.preempt)
         self._check(self._fn("select")(self._h, self._tg_index(tg), C.byref(opts), C.byref(out)))
         return RankedNode.from_c(out, self.nodes)
 
-    def Commit(self, tg, node_or_row):
+    def Commit(self, tg, node_or_row, preempted: Sequence[int] = ()):
+        """Plan.AppendAlloc (+ AppendPreemptedAlloc of `preempted` alloc-table rows)."""
         row = node_or_row if isinstance(node_or_row, (int, np.integer)) else self.row(node_or_row)
-        self._check(self._fn("commit")(self._h, self._tg_index(tg), int(row)))
+        if len(preempted):
+            pre = np.asarray(preempted, dtype=np.uint32)
+            self._check(self._fn("commit_preempt")(self._h, self._tg_index(tg), int(row),
+                                                   pre.ctypes.data_as(abi.u32p), len(pre)))
+        else:
+            self._check(self._fn("commit")(self._h, self._tg_index(tg), int(row)))
 
     def Place(self, tg, count: int) -> List[RankedNode]:
         out = (abi.pe_ranked_node * max(1, count))()

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import hashlib
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 
 @dataclass
@@ -115,6 +115,10 @@ class Allocation:
     dyn_ports: int = 0
     priority: int = 50
     terminal: bool = False
+    # (device group index on the node, healthy instances held): AllocatedDeviceResource
+    # DeviceIDs counted per group (nomad/structs/devices.go:62-100)
+    devices: List[Tuple[int, int]] = field(default_factory=list)
+    max_parallel: int = 0         # TaskGroup.Migrate.MaxParallel of the alloc's job (preemption.go:146-150)
 
 
 @dataclass
@@ -149,6 +153,16 @@ class Spread:
 
 
 @dataclass
+class RequestedDevice:
+    """structs.RequestedDevice (structs.go:2700-2761): name is vendor/type/model,
+    vendor/type or type."""
+    name: str = "gpu"
+    count: int = 1
+    constraints: List[Constraint] = field(default_factory=list)
+    affinities: List[Affinity] = field(default_factory=list)
+
+
+@dataclass
 class Task:
     name: str = "web"
     driver: str = "exec"
@@ -160,6 +174,7 @@ class Task:
     network: Optional[NetworkResource] = None
     constraints: List[Constraint] = field(default_factory=list)
     affinities: List[Affinity] = field(default_factory=list)
+    devices: List[RequestedDevice] = field(default_factory=list)
 
 
 @dataclass

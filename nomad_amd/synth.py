@@ -4,6 +4,8 @@
   C2  10k heterogeneous nodes, count=1000 binpack service job  
   C3  10k nodes / 3 DCs, semver + regexp constraints, affinity, spread
   C4  system job (mock.SystemJob, mock.go:1141-1201) on a large cluster
+  C5  device asks (nvidia/gpu count 2, memory constraint) with preemption of
+      priority-20 background allocs (mock.NvidiaNode, mock.go:131-158)
 
 Node IDs are deterministic UUIDs from a seeded generator so the memdb order
 (ascending ID, nomad/state/schema.go:109-115) is fixed. `shuffle` stands in
@@ -17,8 +19,8 @@ from typing import List, Tuple
 
 import numpy as np
 
-from .structs import (Affinity, Allocation, Constraint, DriverInfo, Job, NetworkResource, Node, Spread,
-                      SpreadTarget, Task, TaskGroup)
+from .structs import (Affinity, Allocation, Constraint, DeviceGroup, DriverInfo, Job, NetworkResource, Node,
+                      RequestedDevice, Spread, SpreadTarget, Task, TaskGroup)
 
 
 def uuids(n: int, seed: int) -> List[str]:
@@ -185,3 +187,64 @@ def cluster_c4(n: int = 100000, seed: int = 11):
                                      cpu_shares=nd.cpu_shares - 100 - 100, memory_mb=1024,
                                      disk_mb=300, priority=50))
     return nodes, allocs
+
+
+GPU_MODELS = {   # name -> device attributes (mock.NvidiaNode attribute set)
+    "a100": {"memory": (80, "GiB"), "cuda_cores": 6912, "graphics_clock": (1410, "MHz"),
+             "memory_bandwidth": (2039, "GB/s")},
+    "h100": {"memory": (80, "GiB"), "cuda_cores": 16896, "graphics_clock": (1755, "MHz"),
+             "memory_bandwidth": (3350, "GB/s")},
+    "1080ti": {"memory": (11, "GiB"), "cuda_cores": 3584, "graphics_clock": (1480, "MHz"),
+               "memory_bandwidth": (11, "GB/s")},
+}
+
+
+def nvidia_node(node_id: str, model: str = "1080ti", healthy: int = 2) -> Node:
+    """mock.NvidiaNode() (mock.go:131-158) with a chosen model / instance count."""
+    nd = mock_node(node_id)
+    nd.devices = [DeviceGroup("nvidia", "gpu", model, healthy, dict(GPU_MODELS[model]))]
+    nd.compute_class()
+    return nd
+
+
+def cluster_c5(n: int = 50000, seed: int = 5):
+    """60 % of the nodes carry one nvidia/gpu group (a100 / h100 / 1080ti, 4 or 8
+    healthy instances); priority-20 background allocs hold 0..all instances."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    ids = sorted(uuids(n, seed))
+    models = ["a100", "h100", "1080ti"]
+    nodes, allocs = [], []
+    for k, nid in enumerate(ids):
+        nd = mock_node(nid)
+        nd.name = "node-%05d" % k
+        nd.cpu_shares = int(CPU_CHOICES[rng.integers(1, 4)])
+        nd.memory_mb = int(MEM_CHOICES[rng.integers(1, 4)])
+        if rng.random() < 0.6:
+            inst = 4 if rng.random() < 0.5 else 8
+            model = models[int(rng.integers(0, 3))]
+            nd.devices = [DeviceGroup("nvidia", "gpu", model, inst, dict(GPU_MODELS[model]))]
+            held = int(rng.integers(0, inst + 1))
+            j = 0
+            while held > 0:
+                take = min(held, int(rng.integers(1, 5)))
+                allocs.append(Allocation(node_id=nid, job_id="batch-%d" % (k % 31), task_group="train",
+                                         cpu_shares=500, memory_mb=1024, disk_mb=300, priority=20,
+                                         devices=[(0, take)], max_parallel=(k % 3)))
+                held -= take
+                j += 1
+        nd.compute_class()
+        nodes.append(nd)
+    return nodes, allocs
+
+
+def job_c5(count: int = 1000) -> Job:
+    """Priority-80 service job: two GPUs with >= 40 GiB each, affinity for h100."""
+    return Job(
+        id="svc-c5", priority=80, datacenters=["dc1"],
+        constraints=[Constraint("${attr.kernel.name}", "linux", "=")],
+        task_groups=[TaskGroup(name="infer", count=count, ephemeral_disk_mb=150, tasks=[
+            Task(name="infer", driver="exec", cpu=1000, memory_mb=2048,
+                 devices=[RequestedDevice("nvidia/gpu", 2,
+                                          constraints=[Constraint("${device.attr.memory}", "40 GiB", ">=")],
+                                          affinities=[Affinity("${device.model}", "h100", "=", 50)])])])],
+    )

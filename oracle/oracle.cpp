@@ -15,8 +15,15 @@
 //   nomad/structs/network.go  NetworkIndex feasibility (ports counted, bandwidth)
 // Randomness (shuffleNodes, random port values) is an input / not modelled:
 // the caller passes the already-shuffled node order.
-// Out of the oracle's scope (returns PE_EUNSUPPORTED): preemption (evict),
-// device requests, reserved cores, CSI volumes, static reserved port asks.
+//   scheduler/device.go       deviceAllocator.AssignDevice (+ DeviceAccounter, devices.go)
+//   scheduler/preemption.go   Preemptor (PreemptForTaskGroup, PreemptForDevice),
+//                             PreemptionScoringIterator (rank.go:775-844)
+// Go map iteration order (ProposedAllocs, device groups, preemption device
+// groups) is replaced by a fixed order: allocs by ascending id (state table
+// order, then plan order), device groups in node order.
+// sort.Slice is Go 1.16's quickSort_func (go.mod: go 1.16), restated below.
+// Out of the oracle's scope (returns PE_EUNSUPPORTED): network preemption
+// (PreemptForNetwork), reserved cores, CSI volumes, static reserved port asks.
 #include "oracle.h"
 #include "gomath.h"
 #include "semantics.h"
@@ -31,6 +38,8 @@
 #include <climits>
 #include <stdexcept>
 #include <new>
+#include <cfloat>
+#include <algorithm>
 
 namespace {
 
@@ -45,6 +54,12 @@ static const int32_t kDynPortCapacity = 32000 - 20000 + 1;   // IndexesInRange i
 struct DriverInfo { bool detected, healthy, nil; };
 struct NetRes { std::string mode, device; int32_t mbits; };
 
+struct ODev {
+    std::string vendor, type, name;
+    int healthy;
+    std::map<std::string, orasem::Attr> attrs;
+};
+
 struct ONode {
     int row;
     std::string id, name, dc, node_class, computed_class;
@@ -56,6 +71,7 @@ struct ONode {
     int32_t reserved_dyn;
     std::map<std::string, bool> host_volumes;   // name -> read only
     int n_devices;
+    std::vector<ODev> devs;
 };
 
 struct OAlloc {
@@ -66,6 +82,18 @@ struct OAlloc {
     int32_t priority;
     int64_t cpu, mem, disk;
     int32_t mbits, dyn_ports;
+    std::vector<std::pair<int, int>> devs;   // (device group on the node, instances held)
+    int32_t max_parallel = 0;
+    int state_index = -1;                    // row of the state alloc table (-1: plan alloc)
+};
+
+struct OConstraint { std::string l, r, op; };
+struct OAffinity { std::string l, r, op; int32_t weight; };
+struct ODevReq {   // structs.RequestedDevice
+    std::string name;
+    uint64_t count;
+    std::vector<OConstraint> constraints;
+    std::vector<OAffinity> affinities;
 };
 
 struct OTask {
@@ -77,10 +105,8 @@ struct OTask {
     std::vector<const pe_constraint*> constraints;
     std::vector<const pe_affinity*> affinities;
     int n_devices;
+    std::vector<ODevReq> devices;
 };
-
-struct OConstraint { std::string l, r, op; };
-struct OAffinity { std::string l, r, op; int32_t weight; };
 struct OSpreadTarget { std::string value; int32_t percent; };
 struct OSpread { std::string attribute; int8_t weight; std::vector<OSpreadTarget> targets; };
 
@@ -179,6 +205,7 @@ struct State {
 struct Plan {
     std::map<int, std::vector<OAlloc>> node_allocation;   // NodeAllocation
     std::map<int, std::vector<OAlloc>> node_update;       // NodeUpdate (stops)
+    std::map<int, std::vector<OAlloc>> node_preemptions;  // NodePreemptions
 };
 
 struct EvalContext {
@@ -198,6 +225,8 @@ struct EvalContext {
         std::set<uint64_t> removed;
         auto up = plan.node_update.find(row);
         if (up != plan.node_update.end()) for (auto& a : up->second) removed.insert(a.id);
+        auto pp = plan.node_preemptions.find(row);
+        if (pp != plan.node_preemptions.end()) for (auto& a : pp->second) removed.insert(a.id);
         for (int ai : state->allocs_by_node[row]) {
             const OAlloc& a = state->allocs[ai];
             if (a.terminal) continue;              // AllocsByNodeTerminal(ws, node, false)
@@ -326,11 +355,142 @@ struct HostVolumeChecker : Checker {
     }
 };
 
-// DeviceChecker (feasible.go:1171-1274): device requests are outside the oracle.
+// ---------------------------------------------------------------------------
+// Devices: RequestedDevice.ID + DeviceIdTuple.Matches (structs.go:2738-2761,
+// 3130-3148), resolveDeviceTarget / nodeDeviceMatches (feasible.go:1278-1330).
+static bool device_id_matches(const ODev& d, const std::string& req) {
+    if (req.empty()) return false;   // RequestedDevice.ID() == nil
+    std::vector<std::string> parts;
+    size_t start = 0;
+    while (parts.size() < 2) {
+        size_t k = req.find('/', start);
+        if (k == std::string::npos) break;
+        parts.push_back(req.substr(start, k - start));
+        start = k + 1;
+    }
+    parts.push_back(req.substr(start));
+    std::string vendor, type, name;
+    if (parts.size() == 1) type = parts[0];
+    else if (parts.size() == 2) { vendor = parts[0]; type = parts[1]; }
+    else { vendor = parts[0]; type = parts[1]; name = parts[2]; }
+    if (!name.empty() && name != d.name) return false;
+    if (!vendor.empty() && vendor != d.vendor) return false;
+    if (!type.empty() && type != d.type) return false;
+    return true;
+}
+
+static orasem::Attr resolve_device_target(const std::string& t, const ODev& d, bool* found) {
+    orasem::Attr a;
+    *found = true;
+    if (t.rfind("${", 0) != 0) return orasem::parse_attribute(t);
+    if (t == "${device.model}") { a.kind = orasem::Attr::Str; a.s = d.name; return a; }
+    if (t == "${device.vendor}") { a.kind = orasem::Attr::Str; a.s = d.vendor; return a; }
+    if (t == "${device.type}") { a.kind = orasem::Attr::Str; a.s = d.type; return a; }
+    if (t.rfind("${device.attr.", 0) == 0) {
+        std::string k = t.substr(14);
+        if (!k.empty() && k.back() == '}') k.pop_back();
+        auto it = d.attrs.find(k);
+        if (it == d.attrs.end()) { *found = false; return a; }
+        return it->second;
+    }
+    *found = false;
+    return a;
+}
+
+static bool dev_check(orasem::Caches& c, const std::string& op, const std::string& l, const std::string& r,
+                      const ODev& d) {
+    bool lf, rf;
+    orasem::Attr lv = resolve_device_target(l, d, &lf), rv = resolve_device_target(r, d, &rf);
+    return orasem::check_attribute_constraint(c, op, lv, rv, lf, rf);
+}
+
+static bool node_device_matches(orasem::Caches& c, const ODev& d, const ODevReq& req) {
+    if (!device_id_matches(d, req.name)) return false;
+    for (auto& k : req.constraints)
+        if (!dev_check(c, k.op, k.l, k.r, d)) return false;
+    return true;
+}
+
+// DeviceChecker (feasible.go:1171-1274). The reference walks a map of device
+// groups; groups are visited here in node order.
 struct DeviceChecker : Checker {
-    bool requires = false;
-    bool Feasible(const ONode&) override {
-        if (requires) throw Unsupported("device requests");
+    EvalContext* ctx = nullptr;
+    std::vector<const ODevReq*> required;
+    bool has(const ONode& n) {
+        if (required.empty()) return true;
+        if (n.devs.empty()) return false;
+        std::vector<int64_t> avail(n.devs.size(), 0);
+        for (size_t g = 0; g < n.devs.size(); g++) avail[g] = n.devs[g].healthy;
+        for (const ODevReq* req : required) {
+            bool ok = false;
+            for (size_t g = 0; g < n.devs.size(); g++) {
+                if (n.devs[g].healthy == 0) continue;   // not in the `available` map
+                if (avail[g] == 0) continue;
+                if ((uint64_t)avail[g] < req->count) continue;
+                if (node_device_matches(ctx->caches, n.devs[g], *req)) {
+                    avail[g] -= (int64_t)req->count;
+                    ok = true;
+                    break;
+                }
+            }
+            if (!ok) return false;
+        }
+        return true;
+    }
+    bool Feasible(const ONode& n) override {
+        if (has(n)) return true;
+        ctx->metrics.FilterNode(&n, "missing devices");
+        return false;
+    }
+};
+
+// deviceAllocator over a DeviceAccounter (device.go:13-131, devices.go:25-100),
+// counted per device group: instances in use by proposed allocs / reservations.
+struct DevAlloc {
+    const ONode* n = nullptr;
+    std::vector<int64_t> used;
+    explicit DevAlloc(const ONode* node) : n(node), used(node->devs.size(), 0) {}
+    int64_t free_count(size_t g) const { return std::max<int64_t>(0, (int64_t)n->devs[g].healthy - used[g]); }
+    void AddAllocs(const std::vector<const OAlloc*>& allocs) {
+        for (const OAlloc* a : allocs) {
+            if (a->terminal) continue;
+            for (auto& d : a->devs)
+                if (d.first >= 0 && (size_t)d.first < used.size()) used[(size_t)d.first] += d.second;
+        }
+    }
+    // AddReserved of an offer: marks `count` instances used; instances already
+    // in use (an offer made by a fresh allocator after preemption, rank.go:470)
+    // do not change the free count.
+    void AddReserved(int g, int64_t count) { used[(size_t)g] += std::min<int64_t>(count, free_count((size_t)g)); }
+    // AssignDevice: best-scoring matching group with enough free instances;
+    // equal scores -> the later group (map order in the reference).
+    bool Assign(orasem::Caches& c, const ODevReq& req, int* group, double* matched, std::string* err) const {
+        if (n->devs.empty()) { *err = "no devices available"; return false; }
+        if (req.count == 0) { *err = "invalid request of zero devices"; return false; }
+        int offer = -1;
+        double offer_score = 0, offer_matched = 0;
+        for (size_t g = 0; g < n->devs.size(); g++) {
+            if ((uint64_t)free_count(g) < req.count) continue;
+            if (!node_device_matches(c, n->devs[g], req)) continue;
+            double choice = 0, sum = 0;
+            if (!req.affinities.empty()) {
+                double total = 0;
+                for (auto& a : req.affinities) {
+                    total += std::fabs((double)a.weight);
+                    if (!dev_check(c, a.op, a.l, a.r, n->devs[g])) continue;
+                    choice += (double)a.weight;
+                    sum += (double)a.weight;
+                }
+                choice /= total;
+            }
+            if (offer >= 0 && choice < offer_score) continue;
+            offer = (int)g;
+            offer_score = choice;
+            offer_matched = sum;
+        }
+        if (offer < 0) { *err = "no devices match request"; return false; }
+        *group = offer;
+        *matched = offer_matched;
         return true;
     }
 };
@@ -624,6 +784,8 @@ struct RankedNode {
     const ONode* node;
     double final_score = 0;
     std::vector<double> scores;
+    std::vector<const OAlloc*> preempted;   // PreemptedAllocs
+    std::vector<std::pair<int, int>> offers; // device offers (group, instances) per request
 };
 
 struct RankIterator { virtual ~RankIterator() {} virtual RankedNode* Next() = 0; virtual void Reset() = 0; };
@@ -669,10 +831,296 @@ static void tg_net_contrib(const OTaskGroup& tg, int32_t* mbits, int32_t* dyn) {
     for (auto& t : tg.tasks) if (t.has_network) { *mbits += t.net_mbits; *dyn += t.net_dyn; }
 }
 
-// BinPackIterator (rank.go:149-531), evict = false path.
+// Go 1.16 sort.Slice (sort/zsortfunc.go: quickSort_func with doPivot_func,
+// medianOfThree_func, heapSort_func, insertionSort_func). Not stable: the
+// order of equal elements is part of the reference's behaviour.
+template <class T, class Less>
+struct GoSort {
+    std::vector<T>& d;
+    Less less;
+    bool L(int i, int j) { return less(d[(size_t)i], d[(size_t)j]); }
+    void S(int i, int j) { std::swap(d[(size_t)i], d[(size_t)j]); }
+    void insertion(int a, int b) {
+        for (int i = a + 1; i < b; i++)
+            for (int j = i; j > a && L(j, j - 1); j--) S(j, j - 1);
+    }
+    void sift(int lo, int hi, int first) {
+        int root = lo;
+        for (;;) {
+            int child = 2 * root + 1;
+            if (child >= hi) return;
+            if (child + 1 < hi && L(first + child, first + child + 1)) child++;
+            if (!L(first + root, first + child)) return;
+            S(first + root, first + child);
+            root = child;
+        }
+    }
+    void heap(int a, int b) {
+        int first = a, lo = 0, hi = b - a;
+        for (int i = (hi - 1) / 2; i >= 0; i--) sift(i, hi, first);
+        for (int i = hi - 1; i >= 0; i--) { S(first, first + i); sift(lo, i, first); }
+    }
+    void median3(int m1, int m0, int m2) {
+        if (L(m1, m0)) S(m1, m0);
+        if (L(m2, m1)) { S(m2, m1); if (L(m1, m0)) S(m1, m0); }
+    }
+    void pivot(int lo, int hi, int* midlo, int* midhi) {
+        int m = (int)((unsigned)(lo + hi) >> 1);
+        if (hi - lo > 40) {
+            int s = (hi - lo) / 8;
+            median3(lo, lo + s, lo + 2 * s);
+            median3(m, m - s, m + s);
+            median3(hi - 1, hi - 1 - s, hi - 1 - 2 * s);
+        }
+        median3(lo, m, hi - 1);
+        int pv = lo, a = lo + 1, c = hi - 1;
+        for (; a < c && L(a, pv); a++) {}
+        int b = a;
+        for (;;) {
+            for (; b < c && !L(pv, b); b++) {}
+            for (; b < c && L(pv, c - 1); c--) {}
+            if (b >= c) break;
+            S(b, c - 1);
+            b++; c--;
+        }
+        bool protect = hi - c < 5;
+        if (!protect && hi - c < (hi - lo) / 4) {
+            int dups = 0;
+            if (!L(pv, hi - 1)) { S(c, hi - 1); c++; dups++; }
+            if (!L(b - 1, pv)) { b--; dups++; }
+            if (!L(m, pv)) { S(m, b - 1); b--; dups++; }
+            protect = dups > 1;
+        }
+        if (protect) {
+            for (;;) {
+                for (; a < b && !L(b - 1, pv); b--) {}
+                for (; a < b && L(a, pv); a++) {}
+                if (a >= b) break;
+                S(a, b - 1);
+                a++; b--;
+            }
+        }
+        S(pv, b - 1);
+        *midlo = b - 1; *midhi = c;
+    }
+    void quick(int a, int b, int depth) {
+        while (b - a > 12) {
+            if (depth == 0) { heap(a, b); return; }
+            depth--;
+            int mlo, mhi;
+            pivot(a, b, &mlo, &mhi);
+            if (mlo - a < b - mhi) { quick(a, mlo, depth); a = mhi; }
+            else { quick(mhi, b, depth); b = mlo; }
+        }
+        if (b - a > 1) {
+            for (int i = a + 6; i < b; i++) if (L(i, i - 6)) S(i, i - 6);
+            insertion(a, b);
+        }
+    }
+};
+template <class T, class Less>
+static void go_sort_slice(std::vector<T>& v, Less less) {
+    int n = (int)v.size(), depth = 0;
+    for (int i = n; i > 0; i >>= 1) depth++;
+    GoSort<T, Less> g{v, less};
+    g.quick(0, n, depth * 2);
+}
+
+// structs.RemoveAllocs (funcs.go:47-64): swap-with-last removal (reorders).
+static std::vector<const OAlloc*> remove_allocs(std::vector<const OAlloc*> v, const std::vector<const OAlloc*>& rm) {
+    std::set<uint64_t> ids;
+    for (auto* a : rm) ids.insert(a->id);
+    int n = (int)v.size();
+    for (int i = 0; i < n; i++) {
+        if (ids.count(v[(size_t)i]->id)) {
+            v[(size_t)i] = v[(size_t)n - 1];
+            i--; n--;
+        }
+    }
+    v.resize((size_t)n);
+    return v;
+}
+
+// ComparableResources restricted to the dimensions Superset checks (cpu,
+// memory, disk; structs.go:3891-3906).
+struct CRes {
+    int64_t cpu = 0, mem = 0, disk = 0;
+    void add(const CRes& o) { cpu += o.cpu; mem += o.mem; disk += o.disk; }
+    void sub(const CRes& o) { cpu -= o.cpu; mem -= o.mem; disk -= o.disk; }
+    bool superset(const CRes& o) const { return cpu >= o.cpu && mem >= o.mem && disk >= o.disk; }
+};
+static CRes res_of(const OAlloc* a) { return CRes{a->cpu, a->mem, a->disk}; }
+
+// basicResourceDistance / scoreForTaskGroup (preemption.go:603-651)
+static double basic_distance(const CRes& ask, const CRes& used) {
+    double mc = 0, cc = 0, dc = 0;
+    if (ask.mem > 0) mc = ((double)ask.mem - (double)used.mem) / (double)ask.mem;
+    if (ask.cpu > 0) cc = ((double)ask.cpu - (double)used.cpu) / (double)ask.cpu;
+    if (ask.disk > 0) dc = ((double)ask.disk - (double)used.disk) / (double)ask.disk;
+    return std::sqrt(gomath::pow(mc, 2) + gomath::pow(cc, 2) + gomath::pow(dc, 2));
+}
+static double score_for_tg(const CRes& ask, const CRes& used, int max_parallel, int num_preempted) {
+    double pen = 0.0;
+    if (max_parallel > 0 && num_preempted >= max_parallel) pen = (double)((num_preempted + 1) - max_parallel) * 50.0;
+    return basic_distance(ask, used) + pen;
+}
+
+// filterAndGroupPreemptibleAllocs (preemption.go:661-697)
+static std::vector<std::pair<int, std::vector<const OAlloc*>>> group_preemptible(int job_priority,
+                                                                              const std::vector<const OAlloc*>& cur) {
+    std::map<int, std::vector<const OAlloc*>> by;
+    for (const OAlloc* a : cur) {
+        if (job_priority - a->priority < 10) continue;
+        by[a->priority].push_back(a);
+    }
+    std::vector<std::pair<int, std::vector<const OAlloc*>>> out(by.begin(), by.end());   // ascending priority
+    return out;
+}
+
+// Preemptor (preemption.go:96-557) for one node of a BinPack pass.
+struct Preemptor {
+    int job_priority = 0;
+    std::string job_id, job_ns;
+    CRes remaining;
+    std::vector<const OAlloc*> current;
+    std::map<std::pair<std::string, std::string>, std::map<std::string, int>> preemptions;
+
+    void SetNode(const ONode& n) { remaining = CRes{n.cpu - n.rcpu, n.mem - n.rmem, n.disk - n.rdisk}; }
+    void SetPreemptions(const Plan& plan) {
+        preemptions.clear();
+        for (auto& kv : plan.node_preemptions)
+            for (auto& a : kv.second) preemptions[{a.job_id, a.ns}][a.tg]++;
+    }
+    void SetCandidates(const std::vector<const OAlloc*>& allocs) {
+        current.clear();
+        for (const OAlloc* a : allocs) {
+            if (a->job_id == job_id && a->ns == job_ns) continue;
+            current.push_back(a);
+        }
+    }
+    int num_preemptions(const OAlloc* a) const {
+        auto it = preemptions.find({a->job_id, a->ns});
+        if (it == preemptions.end()) return 0;
+        auto jt = it->second.find(a->tg);
+        return jt == it->second.end() ? 0 : jt->second;
+    }
+
+    // PreemptForTaskGroup (preemption.go:194-264)
+    std::vector<const OAlloc*> ForTaskGroup(const CRes& ask) {
+        CRes needed = ask;
+        for (const OAlloc* a : current) remaining.sub(res_of(a));
+        auto groups = group_preemptible(job_priority, current);
+        std::vector<const OAlloc*> best;
+        bool met = false;
+        CRes available = remaining;
+        for (auto& grp : groups) {
+            auto& v = grp.second;
+            while (!v.empty() && !met) {
+                int idx = -1;
+                double bd = DBL_MAX;
+                for (size_t i = 0; i < v.size(); i++) {
+                    double d = score_for_tg(needed, res_of(v[i]), v[i]->max_parallel, num_preemptions(v[i]));
+                    if (d < bd) { bd = d; idx = (int)i; }
+                }
+                if (idx < 0) idx = 0;
+                const OAlloc* closest = v[(size_t)idx];
+                available.add(res_of(closest));
+                met = available.superset(ask);
+                best.push_back(closest);
+                v[(size_t)idx] = v.back();
+                v.pop_back();
+                needed.sub(res_of(closest));
+            }
+            if (met) break;
+        }
+        if (!met) return {};
+        // filterSuperset (preemption.go:699-731)
+        go_sort_slice(best, [&](const OAlloc* x, const OAlloc* y) {
+            return basic_distance(ask, res_of(x)) > basic_distance(ask, res_of(y));
+        });
+        CRes avail = remaining;
+        std::vector<const OAlloc*> out;
+        for (const OAlloc* a : best) {
+            out.push_back(a);
+            avail.add(res_of(a));
+            if (avail.superset(ask)) break;
+        }
+        return out;
+    }
+
+    // PreemptForDevice + selectBestAllocs (preemption.go:472-601); device groups
+    // in node order (a map in the reference).
+    std::vector<const OAlloc*> ForDevice(orasem::Caches& c, const ONode& n, const ODevReq& req, const DevAlloc& da) {
+        struct Grp { std::vector<const OAlloc*> allocs; std::map<uint64_t, int64_t> inst; bool used = false; };
+        std::vector<Grp> grps(n.devs.size());
+        for (const OAlloc* a : current) {
+            for (auto& d : a->devs) {
+                if (d.first < 0 || (size_t)d.first >= n.devs.size()) continue;
+                if (!node_device_matches(c, n.devs[(size_t)d.first], req)) continue;
+                Grp& g = grps[(size_t)d.first];
+                g.used = true;
+                g.allocs.push_back(a);
+                g.inst[a->id] += d.second;
+            }
+        }
+        const int64_t needed = (int64_t)req.count;
+        struct Opt { std::vector<const OAlloc*> allocs; const std::map<uint64_t, int64_t>* inst; };
+        std::vector<Opt> options;
+        for (size_t gi = 0; gi < grps.size(); gi++) {
+            if (!grps[gi].used) continue;
+            auto byp = group_preemptible(job_priority, grps[gi].allocs);
+            int64_t cnt = 0;
+            std::vector<const OAlloc*> pre;
+            bool done = false;
+            for (auto& grp : byp) {
+                for (const OAlloc* a : grp.second) {
+                    cnt += grps[gi].inst[a->id];
+                    pre.push_back(a);
+                    if (cnt + da.free_count(gi) >= needed) { options.push_back(Opt{pre, &grps[gi].inst}); done = true; break; }
+                }
+                if (done) break;
+            }
+        }
+        if (options.empty()) return {};
+        int best_prio = INT32_MAX;
+        std::vector<const OAlloc*> best;
+        for (auto& o : options) {
+            const auto& inst = *o.inst;
+            go_sort_slice(o.allocs, [&](const OAlloc* x, const OAlloc* y) {
+                return inst.at(x->id) > inst.at(y->id);
+            });
+            std::set<int> prios;
+            int net = 0;
+            int64_t got = 0;
+            std::vector<const OAlloc*> filtered;
+            for (const OAlloc* a : o.allocs) {
+                if (got >= needed) break;
+                got += inst.at(a->id);
+                filtered.push_back(a);
+                if (prios.insert(a->priority).second) net += a->priority;
+            }
+            if (net < best_prio) { best_prio = net; best = filtered; }
+        }
+        return best;
+    }
+};
+
+// netPriority / preemptionScore (rank.go:808-844)
+static double preemption_score(const std::vector<const OAlloc*>& allocs) {
+    int sum = 0;
+    double mx = 0.0;
+    for (const OAlloc* a : allocs) {
+        if ((double)a->priority > mx) mx = (double)a->priority;
+        sum += a->priority;
+    }
+    const double net = mx + ((double)sum / mx);
+    return 1.0 / (1 + gomath::exp(0.0048 * (net - 2048.0)));
+}
+
+// BinPackIterator (rank.go:149-531)
 struct BinPackIterator : RankIterator {
     EvalContext* ctx; RankIterator* source;
-    bool evict = false; int32_t priority = 0; std::string job_id;
+    bool evict = false; int32_t priority = 0; std::string job_id, job_ns;
     const OTaskGroup* tg = nullptr;
     bool spread_algo = false, oversub = false;
 
@@ -696,6 +1144,14 @@ struct BinPackIterator : RankIterator {
             // NetworkIndex: SetNode + AddAllocs
             int32_t used_dyn = n.reserved_dyn, used_mbits = 0;
             for (const OAlloc* a : proposed) { if (a->terminal) continue; used_dyn += a->dyn_ports; used_mbits += a->mbits; }
+            DevAlloc dev(&n);
+            dev.AddAllocs(proposed);
+            double total_dev_w = 0.0, sum_dev_match = 0.0;
+            std::vector<const OAlloc*> to_preempt;
+            Preemptor pre;
+            pre.job_priority = priority; pre.job_id = job_id; pre.job_ns = job_ns;
+            pre.SetNode(n);
+            pre.SetPreemptions(ctx->plan);
             if (tg->has_network) {
                 if (tg->net_reserved > 0) throw Unsupported("static port asks");
                 // AssignPorts: each dynamic port needs an address of its host network
@@ -704,7 +1160,7 @@ struct BinPackIterator : RankIterator {
                     bool has_addr = false;
                     for (auto& a : n.aliases) if (a == tg->net_host_network) { has_addr = true; break; }
                     if (!has_addr || kDynPortCapacity - used_dyn < 1) {
-                        if (evict) throw Unsupported("preemption");   // PreemptForNetwork path
+                        if (evict) throw Unsupported("network preemption");   // PreemptForNetwork path
                         ctx->metrics.ExhaustedNode(&n, !has_addr ? "network: no addresses available"
                                                                  : "network: dynamic port selection failed");
                         continue;
@@ -713,6 +1169,7 @@ struct BinPackIterator : RankIterator {
                 }
             }
             bool skip = false;
+            option->offers.clear();
             for (auto& t : tg->tasks) {
                 if (t.has_network) {
                     // AssignNetwork over the node's AvailNetworks (device != "")
@@ -725,12 +1182,34 @@ struct BinPackIterator : RankIterator {
                         ok = true; break;
                     }
                     if (!ok) {
-                        if (evict) throw Unsupported("preemption");   // PreemptForNetwork path
+                        if (evict) throw Unsupported("network preemption");   // PreemptForNetwork path
                         ctx->metrics.ExhaustedNode(&n, "network: " + err); skip = true; break;
                     }
                     used_mbits += t.net_mbits; used_dyn += t.net_dyn;   // AddReserved(offer)
                 }
-                if (t.n_devices > 0) throw Unsupported("device requests");
+                // devices (rank.go:366-414)
+                for (auto& req : t.devices) {
+                    int g = -1; double matched = 0; std::string err;
+                    if (!dev.Assign(ctx->caches, req, &g, &matched, &err)) {
+                        if (!evict) { ctx->metrics.ExhaustedNode(&n, "devices: " + err); skip = true; break; }
+                        pre.SetCandidates(proposed);
+                        auto dp = pre.ForDevice(ctx->caches, n, req, dev);
+                        if (dp.empty()) { skip = true; break; }
+                        to_preempt.insert(to_preempt.end(), dp.begin(), dp.end());
+                        proposed = remove_allocs(proposed, to_preempt);
+                        // a fresh allocator (shadowing the outer one, rank.go:400-402)
+                        DevAlloc inner(&n);
+                        inner.AddAllocs(proposed);
+                        if (!inner.Assign(ctx->caches, req, &g, &matched, &err)) { skip = true; break; }
+                    }
+                    dev.AddReserved(g, (int64_t)req.count);
+                    option->offers.push_back({g, (int)req.count});
+                    if (!req.affinities.empty()) {
+                        for (auto& a : req.affinities) total_dev_w += std::fabs((double)a.weight);
+                        sum_dev_match += matched;
+                    }
+                }
+                if (skip) break;
                 if (t.cores > 0) throw Unsupported("reserved cores");
             }
             if (skip) continue;
@@ -744,12 +1223,17 @@ struct BinPackIterator : RankIterator {
             else if (amem < umem) dim = "memory";
             else if (adisk < udisk) dim = "disk";
             if (dim) {
-                if (evict) throw Unsupported("preemption");   // PreemptForTaskGroup path
-                ctx->metrics.ExhaustedNode(&n, dim);
-                continue;
+                if (!evict) { ctx->metrics.ExhaustedNode(&n, dim); continue; }
+                pre.SetCandidates(proposed);
+                auto tp = pre.ForTaskGroup(CRes{ask.cpu, ask.mem, ask.disk});
+                to_preempt.insert(to_preempt.end(), tp.begin(), tp.end());
+                if (tp.empty()) { ctx->metrics.ExhaustedNode(&n, dim); continue; }
             }
+            option->preempted = to_preempt;
+            // the score uses the utilisation computed before any preemption (rank.go:505-516)
             double fitness = score_fit(spread_algo, n, ucpu, umem);
             option->scores.push_back(fitness / 18.0);
+            if (total_dev_w != 0) option->scores.push_back(sum_dev_match / total_dev_w);
             return option;
         }
     }
@@ -921,6 +1405,18 @@ struct SpreadIterator : RankIterator {
     }
 };
 
+// PreemptionScoringIterator (rank.go:773-806)
+struct PreemptionScoringIterator : RankIterator {
+    RankIterator* source;
+    RankedNode* Next() override {
+        RankedNode* o = source->Next();
+        if (!o || o->preempted.empty()) return o;
+        o->scores.push_back(preemption_score(o->preempted));
+        return o;
+    }
+    void Reset() override { source->Reset(); }
+};
+
 // ScoreNormalizationIterator (rank.go:737-771)
 struct ScoreNormalizationIterator : RankIterator {
     RankIterator* source;
@@ -1018,16 +1514,19 @@ struct oracle_stack {
     NodeReschedulingPenaltyIterator penalty;
     NodeAffinityIterator node_affinity;
     SpreadIterator spread;
+    PreemptionScoringIterator preempt_score;
     ScoreNormalizationIterator score_norm;
     LimitIterator limit;
     MaxScoreIterator max_score;
     bool have_job_version = false; uint64_t job_version = 0;
+    int offer_row = -1;                                // device offers of the last Select's pick
+    std::vector<std::pair<int, int>> offers;
 
     explicit oracle_stack(const pe_config& c) : cfg(c) {
         ctx.state = &state;
         source.ctx = &ctx;
         job_constraint.ctx = &ctx; tg_constraint.ctx = &ctx;
-        tg_drivers.ctx = &ctx; tg_volumes.ctx = &ctx; tg_network.ctx = &ctx;
+        tg_drivers.ctx = &ctx; tg_volumes.ctx = &ctx; tg_network.ctx = &ctx; tg_devices.ctx = &ctx;
         wrapped.ctx = &ctx; wrapped.source = &source;
         wrapped.job_checkers = {&job_constraint};
         wrapped.tg_checkers = {&tg_drivers, &tg_constraint, &tg_volumes, &tg_devices, &tg_network};
@@ -1044,7 +1543,8 @@ struct oracle_stack {
         penalty.source = &job_anti_aff;
         node_affinity.ctx = &ctx; node_affinity.source = &penalty;
         spread.ctx = &ctx; spread.source = &node_affinity;
-        score_norm.source = generic ? (RankIterator*)&spread : (RankIterator*)&bin_pack;
+        preempt_score.source = &spread;
+        score_norm.source = generic ? (RankIterator*)&preempt_score : (RankIterator*)&bin_pack;
         limit.source = &score_norm; limit.limit = 2; limit.max_skip = 3; limit.threshold = 0.0;
         max_score.source = &limit;
     }
@@ -1092,6 +1592,25 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
         if (nt->hv_off)
             for (uint32_t k = nt->hv_off[i]; k < nt->hv_off[i + 1]; k++) n.host_volumes[S(st, nt->hv_name[k])] = nt->hv_read_only[k] != 0;
         n.n_devices = nt->dev_off ? (int)(nt->dev_off[i + 1] - nt->dev_off[i]) : 0;
+        for (int k = 0; k < n.n_devices; k++) {
+            const uint32_t g = nt->dev_off[i] + (uint32_t)k;
+            ODev d;
+            d.vendor = S(st, nt->dev_vendor[g]); d.type = S(st, nt->dev_type[g]); d.name = S(st, nt->dev_name[g]);
+            d.healthy = (int)nt->dev_healthy[g];
+            for (uint32_t q = nt->dev_attr_off[g]; nt->dev_attr_off && q < nt->dev_attr_off[g + 1]; q++) {
+                const pe_attr& pa = nt->dev_attr_val[q];
+                orasem::Attr a;
+                a.unit = S(st, pa.unit);
+                switch (pa.kind) {
+                    case PE_ATTR_INT: a.kind = orasem::Attr::Int; a.i = pa.i; break;
+                    case PE_ATTR_FLOAT: a.kind = orasem::Attr::Float; a.f = pa.f; break;
+                    case PE_ATTR_BOOL: a.kind = orasem::Attr::Bool; a.b = pa.i != 0; a.unit.clear(); break;
+                    default: a.kind = orasem::Attr::Str; a.s = S(st, pa.s); a.unit.clear(); break;
+                }
+                d.attrs[S(st, nt->dev_attr_key[q])] = a;
+            }
+            n.devs.push_back(d);
+        }
     }
     st.allocs.resize(at ? at->count : 0);
     st.allocs_by_node.assign(nt->n, {});
@@ -1104,6 +1623,11 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
         a.terminal = at->terminal[i] != 0; a.priority = at->priority[i];
         a.cpu = at->cpu_shares[i]; a.mem = at->memory_mb[i]; a.disk = at->disk_mb[i];
         a.mbits = at->net_mbits[i]; a.dyn_ports = at->dyn_ports[i];
+        a.state_index = (int)i;
+        a.max_parallel = at->max_parallel ? at->max_parallel[i] : 0;
+        if (at->dev_off)
+            for (uint32_t k = at->dev_off[i]; k < at->dev_off[i + 1]; k++)
+                a.devs.push_back({(int)at->dev_group[k], (int)at->dev_count[k]});
         st.allocs_by_node[a.node_row].push_back((int)i);
     }
     s->ctx.plan = Plan();
@@ -1181,6 +1705,14 @@ int oracle_set_job(oracle_stack* s, const pe_strtab* strs, const pe_job* j) {
             ot.lifecycle = pt.lifecycle;
             ot.has_network = pt.has_network != 0; ot.net_mbits = pt.net_mbits; ot.net_dyn = pt.net_dyn_ports; ot.net_reserved = pt.net_reserved_ports;
             ot.n_devices = (int)pt.device_count;
+            for (uint32_t q = 0; q < pt.device_count; q++) {
+                const pe_device_request& r = j->devices[pt.device_off + q];
+                ODevReq dr;
+                dr.name = S(st, r.name); dr.count = r.count;
+                dr.constraints = conv_constraints(st, j->device_constraints, r.constraint_off, r.constraint_count);
+                dr.affinities = conv_affinities(st, j->device_affinities, r.affinity_off, r.affinity_count);
+                ot.devices.push_back(dr);
+            }
             tg.tasks.push_back(ot);
             tg.task_constraints.push_back(conv_constraints(st, j->constraints, pt.constraint_off, pt.constraint_count));
             tg.task_affinities.push_back(conv_affinities(st, j->affinities, pt.affinity_off, pt.affinity_count));
@@ -1195,7 +1727,7 @@ int oracle_set_job(oracle_stack* s, const pe_strtab* strs, const pe_job* j) {
     s->job_constraint.cs = jp->constraints;
     if (s->cfg.stack_kind == PE_STACK_GENERIC) s->distinct_hosts.SetJob(jp);
     s->distinct_property.SetJob(jp);
-    s->bin_pack.priority = jp->priority; s->bin_pack.job_id = jp->id;
+    s->bin_pack.priority = jp->priority; s->bin_pack.job_id = jp->id; s->bin_pack.job_ns = jp->ns;
     s->job_anti_aff.job_id = jp->id;
     s->node_affinity.SetJob(jp);
     s->spread.SetJob(jp);
@@ -1232,8 +1764,8 @@ static void set_task_group(oracle_stack* s, const OTaskGroup& tg, bool system) {
     if (tg.csi) throw Unsupported("CSI volumes");
     s->tg_drivers.drivers = drivers;
     s->tg_constraint.cs = cs;
-    int ndev = 0; for (auto& t : tg.tasks) ndev += t.n_devices;
-    s->tg_devices.requires = ndev > 0;
+    s->tg_devices.required.clear();
+    for (auto& t : tg.tasks) for (auto& r : t.devices) s->tg_devices.required.push_back(&r);
     s->tg_volumes.volumes.clear();
     for (auto& v : tg.volumes) s->tg_volumes.volumes[v.first].push_back(v.second);
     if (tg.has_network) {
@@ -1261,6 +1793,14 @@ static void fill_out(pe_ranked_node* out, RankedNode* o, const oracle_stack* s) 
     out->nodes_filtered = s->ctx.metrics.filtered;
     out->nodes_exhausted = s->ctx.metrics.exhausted;
     out->new_offset = s->source.nodes.empty() ? 0 : (uint32_t)(s->source.offset % (int)s->source.nodes.size());
+    if (o) {
+        if (o->preempted.size() > PE_MAX_PREEMPT) throw Unsupported("more than PE_MAX_PREEMPT preempted allocs");
+        out->n_preempted = (uint32_t)o->preempted.size();
+        for (size_t i = 0; i < o->preempted.size(); i++) out->preempted[i] = (uint32_t)o->preempted[i]->state_index;
+        if (o->offers.size() > PE_MAX_DEVICE_REQ) throw Unsupported("more than PE_MAX_DEVICE_REQ device requests");
+        out->n_device_offers = (uint32_t)o->offers.size();
+        for (size_t i = 0; i < o->offers.size(); i++) out->device_offer_group[i] = (uint32_t)o->offers[i].first;
+    }
 }
 
 static RankedNode* generic_select(oracle_stack* s, uint32_t tgi, const pe_select_options* opts) {
@@ -1301,6 +1841,8 @@ int oracle_select(oracle_stack* s, uint32_t tgi, const pe_select_options* opts, 
     try {
         RankedNode* o = s->cfg.stack_kind == PE_STACK_GENERIC ? generic_select(s, tgi, opts) : system_select(s, tgi);
         fill_out(out, o, s);
+        s->offer_row = o ? o->node->row : -1;
+        if (o) s->offers = o->offers;
     } catch (const Unsupported& e) {
         s->err = std::string("unsupported: ") + e.what();
         return PE_EUNSUPPORTED;
@@ -1321,8 +1863,33 @@ int oracle_commit(oracle_stack* s, uint32_t tgi, int32_t row) {
     a.terminal = false; a.priority = s->job.priority;
     a.cpu = ask.cpu; a.mem = ask.mem; a.disk = ask.disk;
     tg_net_contrib(tg, &a.mbits, &a.dyn_ports);
+    if (row == s->offer_row) {
+        a.devs = s->offers;
+    } else {   // commit without a Select of this node: assign on the proposed state
+        const ONode& n = s->state.nodes[(size_t)row];
+        DevAlloc dev(&n);
+        dev.AddAllocs(s->ctx.ProposedAllocs(row));
+        for (auto& t : tg.tasks)
+            for (auto& r : t.devices) {
+                int g; double m; std::string err;
+                if (!dev.Assign(s->ctx.caches, r, &g, &m, &err)) continue;
+                dev.AddReserved(g, (int64_t)r.count);
+                a.devs.push_back({g, (int)r.count});
+            }
+    }
+    s->offer_row = -1;
     s->ctx.plan.node_allocation[row].push_back(a);
     return PE_OK;
+}
+
+// Plan.AppendPreemptedAlloc for each preempted alloc (generic_sched.go:794-816)
+int oracle_commit_preempt(oracle_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        if (preempted[i] >= s->state.allocs.size()) { s->err = "bad preempted alloc"; return PE_EINVAL; }
+        const OAlloc& a = s->state.allocs[preempted[i]];
+        s->ctx.plan.node_preemptions[a.node_row].push_back(a);
+    }
+    return oracle_commit(s, tgi, row);
 }
 
 int oracle_place(oracle_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
@@ -1331,8 +1898,13 @@ int oracle_place(oracle_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* 
         pe_select_options opts; std::memset(&opts, 0, sizeof(opts));
         int rc = oracle_select(s, tgi, &opts, &out[i]);
         if (rc != PE_OK) return rc;
+        if (out[i].row < 0 && s->cfg.preempt && s->cfg.stack_kind == PE_STACK_GENERIC) {
+            opts.preempt = 1;   // selectNextOption (generic_sched.go:786-790)
+            rc = oracle_select(s, tgi, &opts, &out[i]);
+            if (rc != PE_OK) return rc;
+        }
         if (out[i].row < 0) break;   // failedTGAllocs: the rest of the tg is coalesced
-        oracle_commit(s, tgi, out[i].row);
+        oracle_commit_preempt(s, tgi, out[i].row, out[i].preempted, out[i].n_preempted);
         p++;
     }
     if (placed) *placed = p;

@@ -24,6 +24,8 @@ int oracle_set_nodes(oracle_stack* s, const uint32_t* rows, uint32_t n, uint32_t
 int oracle_select(oracle_stack* s, uint32_t tg_index, const pe_select_options* opts,
                   pe_ranked_node* out);
 int oracle_commit(oracle_stack* s, uint32_t tg_index, int32_t row);
+int oracle_commit_preempt(oracle_stack* s, uint32_t tg_index, int32_t row, const uint32_t* preempted,
+                          uint32_t n_preempted);
 int oracle_place(oracle_stack* s, uint32_t tg_index, uint32_t count, pe_ranked_node* out,
                  uint32_t* placed);
 int oracle_system_place(oracle_stack* s, uint32_t tg_index, double* out_score,

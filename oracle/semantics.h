@@ -17,6 +17,9 @@
 #include <string>
 #include <vector>
 #include <regex>
+#include <cstring>
+#include <cmath>
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <cctype>
@@ -336,6 +339,204 @@ static inline bool check_constraint(Caches& c, const std::string& op, const Val&
     if (op == "regexp") return lf && rf && check_regexp_match(c, l, r);
     if (op == "set_contains" || op == "set_contains_all") return lf && rf && check_set_contains_all(l, r);
     if (op == "set_contains_any") return lf && rf && check_set_contains_any(l, r);
+    return false;
+}
+
+// ---------------- device attributes ----------------
+// plugins/shared/structs/attribute.go (ParseAttribute 55-103, Comparable 296-320,
+// Compare 322-385) and units.go (unit table); checkAttributeConstraint and
+// checkAttributeVersionMatch (scheduler/feasible.go:1334-1447, 896-930).
+// Numbers are compared through long double where Go uses a 256-bit big.Float:
+// exact whenever value bits + multiplier bits <= 64 (every unit multiplier here
+// is <= 2^60 or 10^18; beyond that the comparison is parity unpinned).
+struct Attr {
+    enum Kind { None, Int, Float, Str, Bool } kind = None;
+    int64_t i = 0;
+    double f = 0;
+    std::string s;
+    bool b = false;
+    std::string unit;
+};
+
+struct UnitDef { const char* name; int base; int64_t mult; bool inverse; };
+static inline const std::vector<UnitDef>& unit_table() {
+    static const std::vector<UnitDef> t = {
+        {"KiB", 1, 1ll << 10, false}, {"MiB", 1, 1ll << 20, false}, {"GiB", 1, 1ll << 30, false},
+        {"TiB", 1, 1ll << 40, false}, {"PiB", 1, 1ll << 50, false}, {"EiB", 1, 1ll << 60, false},
+        {"kB", 1, 1000ll, false}, {"KB", 1, 1000ll, false}, {"MB", 1, 1000000ll, false},
+        {"GB", 1, 1000000000ll, false}, {"TB", 1, 1000000000000ll, false},
+        {"PB", 1, 1000000000000000ll, false}, {"EB", 1, 1000000000000000000ll, false},
+        {"KiB/s", 2, 1ll << 10, false}, {"MiB/s", 2, 1ll << 20, false}, {"GiB/s", 2, 1ll << 30, false},
+        {"TiB/s", 2, 1ll << 40, false}, {"PiB/s", 2, 1ll << 50, false}, {"EiB/s", 2, 1ll << 60, false},
+        {"kB/s", 2, 1000ll, false}, {"KB/s", 2, 1000ll, false}, {"MB/s", 2, 1000000ll, false},
+        {"GB/s", 2, 1000000000ll, false}, {"TB/s", 2, 1000000000000ll, false},
+        {"PB/s", 2, 1000000000000000ll, false}, {"EB/s", 2, 1000000000000000000ll, false},
+        {"MHz", 3, 1000000ll, false}, {"GHz", 3, 1000000000ll, false},
+        {"mW", 4, 1000ll, true}, {"W", 4, 1ll, false}, {"kW", 4, 1000ll, false},
+        {"MW", 4, 1000000ll, false}, {"GW", 4, 1000000000ll, false},
+    };
+    return t;
+}
+static inline const UnitDef* find_unit(const std::string& u) {
+    if (u.empty()) return nullptr;
+    for (auto& d : unit_table()) if (u == d.name) return &d;
+    return nullptr;
+}
+
+static inline std::string trim_space(const std::string& x) {
+    size_t a = 0, b = x.size();
+    while (a < b && std::isspace((unsigned char)x[a])) a++;
+    while (b > a && std::isspace((unsigned char)x[b - 1])) b--;
+    return x.substr(a, b - a);
+}
+
+// strconv.ParseFloat(s, 64) for the decimal forms (sign, digits, '.', exponent,
+// inf/infinity/nan)
+static inline bool parse_f64(const std::string& x, double* out) {
+    if (x.empty()) return false;
+    std::string l;
+    for (char c : x) l += (char)std::tolower((unsigned char)c);
+    size_t p = (l[0] == '+' || l[0] == '-') ? 1 : 0;
+    std::string body = l.substr(p);
+    if (body == "inf" || body == "infinity") { *out = l[0] == '-' ? -HUGE_VAL : HUGE_VAL; return true; }
+    if (body == "nan" && p == 0) { *out = NAN; return true; }
+    bool digits = false, dot = false;
+    size_t i = p;
+    for (; i < l.size(); i++) {
+        if (is_digit(l[i])) digits = true;
+        else if (l[i] == '.' && !dot) dot = true;
+        else break;
+    }
+    if (!digits) return false;
+    if (i < l.size() && l[i] == 'e') {
+        i++;
+        if (i < l.size() && (l[i] == '+' || l[i] == '-')) i++;
+        bool ed = false;
+        while (i < l.size() && is_digit(l[i])) { i++; ed = true; }
+        if (!ed) return false;
+    }
+    if (i != l.size()) return false;
+    *out = std::strtod(x.c_str(), nullptr);
+    return true;
+}
+
+// psstructs.ParseAttribute (attribute.go:55-103)
+static inline Attr parse_attribute(const std::string& in) {
+    Attr a;
+    if (in.empty()) { a.kind = Attr::Str; return a; }
+    std::string unit, numeric = in;
+    if (std::isalpha((unsigned char)in.back())) {
+        // lengthSortedUnits: longest unit first
+        std::vector<const UnitDef*> us;
+        for (auto& d : unit_table()) us.push_back(&d);
+        std::stable_sort(us.begin(), us.end(), [](const UnitDef* x, const UnitDef* y) {
+            return std::strlen(x->name) > std::strlen(y->name);
+        });
+        for (auto* d : us) {
+            const size_t n = std::strlen(d->name);
+            if (in.size() >= n && in.compare(in.size() - n, n, d->name) == 0) { unit = d->name; break; }
+        }
+        if (!unit.empty()) numeric = trim_space(in.substr(0, in.size() - unit.size()));
+    }
+    int64_t iv;
+    if (parse_i64(numeric, &iv)) { a.kind = Attr::Int; a.i = iv; a.unit = unit; return a; }
+    double fv;
+    if (parse_f64(numeric, &fv)) { a.kind = Attr::Float; a.f = fv; a.unit = unit; return a; }
+    static const char* tr[] = {"1", "t", "T", "TRUE", "true", "True"};
+    static const char* fa[] = {"0", "f", "F", "FALSE", "false", "False"};
+    for (auto* t : tr) if (in == t) { a.kind = Attr::Bool; a.b = true; return a; }
+    for (auto* t : fa) if (in == t) { a.kind = Attr::Bool; a.b = false; return a; }
+    a.kind = Attr::Str; a.s = in;
+    return a;
+}
+
+static inline bool attr_comparable(const Attr& a, const Attr& b) {
+    const UnitDef* ua = find_unit(a.unit);
+    const UnitDef* ub = find_unit(b.unit);
+    if (ua && ub) return ua->base == ub->base;
+    if (ua || ub) return false;
+    if (a.kind == Attr::Str) return b.kind == Attr::Str;
+    if (a.kind == Attr::Bool) return b.kind == Attr::Bool;
+    return true;
+}
+
+// Attribute.Compare (attribute.go:322-385)
+static inline int attr_compare(const Attr& a, const Attr& b, bool* ok) {
+    *ok = false;
+    if (!attr_comparable(a, b)) return 0;
+    if (a.kind == Attr::Bool) { *ok = true; return a.b == b.b ? 0 : 1; }
+    if (a.kind == Attr::Str) { *ok = true; return a.s < b.s ? -1 : (a.s == b.s ? 0 : 1); }
+    if (a.kind != Attr::Int && a.kind != Attr::Float) return 0;   // nullComparator
+    if (a.kind == Attr::Int && b.kind == Attr::Int) {
+        auto scaled = [](const Attr& x) -> int64_t {   // getInt: int64 arithmetic (wraps like Go)
+            const UnitDef* u = find_unit(x.unit);
+            if (!u) return x.i;
+            if (u->inverse) return x.i / u->mult;
+            return (int64_t)((uint64_t)x.i * (uint64_t)u->mult);
+        };
+        const int64_t ai = scaled(a), bi = scaled(b);
+        *ok = true;
+        return ai == bi ? 0 : (ai < bi ? -1 : 1);
+    }
+    if (b.kind != Attr::Int && b.kind != Attr::Float) return 0;
+    auto big = [](const Attr& x) -> long double {
+        long double v = x.kind == Attr::Int ? (long double)x.i : (long double)x.f;
+        const UnitDef* u = find_unit(x.unit);
+        if (!u) return v;
+        return u->inverse ? v * (1.0L / (long double)u->mult) : v * (long double)u->mult;
+    };
+    const long double af = big(a), bf = big(b);
+    *ok = true;
+    return af < bf ? -1 : (af > bf ? 1 : 0);
+}
+
+// checkAttributeVersionMatch (feasible.go:896-930)
+static inline bool check_attr_version(Caches& c, bool semver, const Attr& l, const Attr& r) {
+    std::string vs;
+    if (l.kind == Attr::Str) vs = l.s;
+    else if (l.kind == Attr::Int) vs = std::to_string(l.i);
+    else return false;
+    if (r.kind != Attr::Str) return false;
+    Val lv, rv;
+    lv.is_nil = false; lv.s = vs;
+    rv.is_nil = false; rv.s = r.s;
+    return check_version_match(c, semver, lv, rv);
+}
+
+// checkAttributeConstraint (feasible.go:1334-1447)
+static inline bool check_attribute_constraint(Caches& c, const std::string& op, const Attr& l, const Attr& r,
+                                              bool lf, bool rf) {
+    if (op == "distinct_hosts" || op == "distinct_property") return true;
+    if (op == "!=" || op == "not") {
+        if (!(lf || rf)) return false;
+        if (lf != rf) return true;
+        bool ok;
+        int v = attr_compare(l, r, &ok);
+        return ok && v != 0;
+    }
+    if (op == "<" || op == "<=" || op == ">" || op == ">=" || op == "=" || op == "==" || op == "is") {
+        if (!(lf && rf)) return false;
+        bool ok;
+        int v = attr_compare(l, r, &ok);
+        if (!ok) return false;
+        if (op == "is" || op == "==" || op == "=") return v == 0;
+        if (op == "<") return v == -1;
+        if (op == "<=") return v != 1;
+        if (op == ">") return v == 1;
+        return v != -1;
+    }
+    if (op == "version" || op == "semver") return lf && rf && check_attr_version(c, op == "semver", l, r);
+    if (op == "regexp" || op == "set_contains" || op == "set_contains_all" || op == "set_contains_any") {
+        if (!(lf && rf) || l.kind != Attr::Str || r.kind != Attr::Str) return false;
+        Val lv, rv;
+        lv.is_nil = false; lv.s = l.s;
+        rv.is_nil = false; rv.s = r.s;
+        if (op == "regexp") return check_regexp_match(c, lv, rv);
+        if (op == "set_contains_any") return check_set_contains_any(lv, rv);
+        return check_set_contains_all(lv, rv);
+    }
+    if (op == "is_set") return lf;
+    if (op == "is_not_set") return !lf;
     return false;
 }
 
