@@ -37,7 +37,12 @@ size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
-                            hipStream_t st);
+                            uint32_t offers, hipStream_t st);
+hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs* r, hipStream_t st);
+hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ranked_node* out, uint32_t* mask,
+                                  hipStream_t st);
+hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
+                                    uint32_t* pcount, uint32_t* dev_free, hipStream_t st);
 hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
                                hipStream_t st);
 hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec* merged, hipStream_t st);
@@ -276,6 +281,19 @@ struct pe_stack {
     bool dev_packable = true;          // every node fits the packed 4 x u8 free-count column
     std::vector<uint32_t> h_dev_free;  // snapshot free healthy instances per group (no plan)
     DevMem d_dev_free, d_dev_free_base;
+    // preemption: non-terminal state allocs per node (CSR, table order) as PreemptAlloc
+    std::vector<uint32_t> h_node_alloc_off, h_palloc_index;   // CSR; slot -> alloc-table row
+    std::vector<uint32_t> alloc_slot;          // alloc-table row -> slot (PE_NONE: terminal)
+    std::vector<uint8_t> h_preempted;          // host mirror of Plan.NodePreemptions membership
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> job_keys;   // (job, ns) -> key
+    uint32_t n_jtg_keys = 0;
+    std::string preempt_unsupported;           // snapshot outside the on-device limits
+    DevMem d_node_alloc_off, d_palloc, d_preempted, d_pcount, d_own_existing;
+    DevMem d_ev_status, d_ev_score, d_ev_flags, d_ev_out, d_ev_mask;
+    uint32_t job_key = PE_NONE;
+    // device offers of the last Select's pick (committed as chosen)
+    int32_t offer_row = -1;
+    uint32_t offers = 0xFFFFFFFFu;
     uint32_t ncls = 0;
     std::vector<uint32_t> class_rep;   // first row of each class
     // Nodes with equal ComputedClass AND equal non-hashed checker inputs
@@ -892,6 +910,57 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
             }
     HIP_TRY(s, upload(s->d_dev_free_base, s->h_dev_free));
     HIP_TRY(s, upload(s->d_dev_free, s->h_dev_free));
+    // Preemptor inputs (preemption.go:96-154): non-terminal allocs per node in table order
+    {
+        s->preempt_unsupported.clear();
+        for (size_t g = 0; g < dev_used.size(); g++)
+            if (dev_used[g] > (int64_t)s->dev_groups[g].healthy)
+                s->preempt_unsupported = "device instances held beyond the healthy count";
+        s->job_keys.clear();
+        std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> jtg;
+        std::vector<uint32_t> cnt(n + 1, 0);
+        for (auto& a : s->allocs) if (!a.terminal) cnt[a.row + 1]++;
+        s->h_node_alloc_off.assign(n + 1, 0);
+        for (uint32_t i = 0; i < n; i++) s->h_node_alloc_off[i + 1] = s->h_node_alloc_off[i] + cnt[i + 1];
+        const uint32_t m = s->h_node_alloc_off[n];
+        std::vector<pe::PreemptAlloc> pa(std::max<uint32_t>(m, 1));
+        std::memset(pa.data(), 0, sizeof(pe::PreemptAlloc) * pa.size());
+        s->h_palloc_index.assign(m, 0);
+        s->alloc_slot.assign(s->allocs.size(), PE_NONE);
+        std::vector<uint32_t> fill(s->h_node_alloc_off.begin(), s->h_node_alloc_off.end() - 1);
+        for (uint32_t i = 0; i < s->allocs.size(); i++) {
+            const HostAlloc& a = s->allocs[i];
+            if (a.terminal) continue;
+            if (cnt[a.row + 1] > (uint32_t)pe::kMaxNodeAllocs)
+                s->preempt_unsupported = "more than 32 allocs on a node";
+            const uint32_t slot = fill[a.row]++;
+            s->h_palloc_index[slot] = i;
+            s->alloc_slot[i] = slot;
+            pe::PreemptAlloc& x = pa[slot];
+            x.cpu = a.cpu; x.mem = a.mem; x.disk = a.disk;
+            x.priority = a.priority; x.max_parallel = a.max_parallel;
+            x.job_key = s->job_keys.emplace(std::make_pair(a.job, a.ns), (uint32_t)s->job_keys.size()).first->second;
+            x.jtg_key = jtg.emplace(std::make_tuple(a.job, a.ns, a.tg), (uint32_t)jtg.size()).first->second;
+            x.mbits = at->net_mbits[i];
+            x.dyn = at->dyn_ports[i];
+            x.state_index = i;
+            const uint32_t ng = s->dev_off[a.row + 1] - s->dev_off[a.row];
+            for (uint32_t k = a.dev_begin; k < a.dev_end; k++) {
+                const uint32_t g = s->alloc_dev[k].first, c = s->alloc_dev[k].second;
+                if (g >= ng) continue;   // the group is no longer fingerprinted (devices.go:88-99)
+                if (x.n_dev >= 4 || g >= 4 || c > 255) { s->preempt_unsupported = "alloc device entries beyond 4 x 255"; continue; }
+                x.dev_g |= g << (8 * x.n_dev);
+                x.dev_c |= c << (8 * x.n_dev);
+                x.n_dev++;
+            }
+        }
+        s->n_jtg_keys = (uint32_t)jtg.size();
+        s->h_preempted.assign(std::max<uint32_t>(m, 1), 0);
+        HIP_TRY(s, upload(s->d_node_alloc_off, s->h_node_alloc_off));
+        HIP_TRY(s, upload(s->d_palloc, pa));
+        HIP_TRY(s, upload(s->d_preempted, s->h_preempted));
+        HIP_TRY(s, upload(s->d_pcount, std::vector<uint32_t>(std::max<uint32_t>(s->n_jtg_keys, 1), 0)));
+    }
     std::vector<uint32_t> zeros(n, 0);
     HIP_TRY(s, upload(s->d_coll_job, zeros));
     return PE_OK;
@@ -1383,6 +1452,115 @@ int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_r
     return PE_OK;
 }
 
+// Preemptor inputs on the device for the current job / task group.
+pe::PreemptArgs preempt_args(pe_stack* s, TgPlan& g) {
+    pe::PreemptArgs P;
+    std::memset(&P, 0, sizeof(P));
+    P.soa = soa_of(s);
+    P.tg = tables_of(g);
+    P.ask = ask_for(s, g);
+    P.node_alloc_off = s->d_node_alloc_off.as<uint32_t>();
+    P.allocs = s->d_palloc.as<pe::PreemptAlloc>();
+    P.preempted = s->d_preempted.as<uint8_t>();
+    P.pcount = s->d_pcount.as<uint32_t>();
+    P.own_existing = s->d_own_existing.as<uint32_t>();
+    P.job_key = s->job_key;
+    P.job_priority = s->job_priority;
+    P.log10 = s->log10;
+    return P;
+}
+
+// Select with Preempt=true (BinPack evict, rank.go:193-527 + PreemptionScoringIterator)
+// over `order` from cursor `offset`: every position evaluated in parallel, then
+// the LimitIterator window resolved on the device.
+int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t offset,
+                     const pe_select_options* opts, pe_ranked_node* out, uint32_t* new_offset) {
+    std::memset(out, 0, sizeof(*out));
+    out->row = -1;
+    const uint32_t n = (uint32_t)order.size();
+    *new_offset = n ? offset % n : 0;
+    if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
+    if (n == 0) return PE_OK;
+    pe::PreemptArgs P = preempt_args(s, g);
+    HIP_TRY(s, upload(s->d_visit, order));
+    P.visit = s->d_visit.as<uint32_t>();
+    P.n_visit = n;
+    if (opts && opts->penalty_count > 0) {
+        std::vector<uint32_t> bits((s->nodes.size() + 31) / 32, 0);
+        for (uint32_t i = 0; i < opts->penalty_count; i++) {
+            uint32_t r = opts->penalty_rows[i];
+            if (r < s->nodes.size()) bits[r >> 5] |= 1u << (r & 31);
+        }
+        HIP_TRY(s, upload(s->d_penalty, bits));
+        P.penalty_bits = s->d_penalty.as<uint32_t>();
+    }
+    if (!g.psets.empty()) {
+        HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
+        HIP_TRY(s, pe_launch_spread_table(&P.tg, s->d_spread_tab.as<double>(), s->stream));
+        P.spread_tab = s->d_spread_tab.as<double>();
+    }
+    HIP_TRY(s, s->d_ev_status.ensure(n));
+    HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * n));
+    HIP_TRY(s, s->d_ev_flags.ensure(16));
+    HIP_TRY(s, s->d_ev_out.ensure(16));
+    HIP_TRY(s, s->d_ev_mask.ensure(16));
+    HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
+    HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
+    P.status = s->d_ev_status.as<uint8_t>();
+    P.score = s->d_ev_score.as<double>();
+    P.flags = s->d_ev_flags.as<uint32_t>();
+    pe::EvictResolveArgs R;
+    R.status = P.status;
+    R.score = P.score;
+    R.n = n;
+    R.offset = offset % n;
+    R.limit = s->limit;
+    R.out = s->d_ev_out.as<int32_t>();
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, pe_launch_evict(&P, &R, s->stream));
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    int32_t res[4];
+    uint32_t flags = 0;
+    HIP_TRY(s, hipMemcpyAsync(res, R.out, sizeof(res), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(&flags, P.flags, sizeof(flags), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    if (flags & 1u)
+        return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the on-device "
+                                        "alloc limits");
+    const uint32_t consumed = (uint32_t)res[1];
+    out->nodes_evaluated = consumed;
+    out->nodes_filtered = (uint32_t)res[2];
+    out->nodes_exhausted = (uint32_t)res[3];
+    *new_offset = (uint32_t)(((uint64_t)(offset % n) + consumed) % n);
+    out->new_offset = *new_offset;
+    if (res[0] >= 0) {
+        const uint32_t row = order[(uint32_t)(((uint64_t)(offset % n) + (uint32_t)res[0]) % n)];
+        HIP_TRY(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
+                                          s->stream));
+        pe_ranked_node rr;
+        uint32_t mask = 0;
+        HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(&mask, s->d_ev_mask.p, sizeof(mask), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        out->row = (int32_t)row;
+        out->final_score = rr.final_score;
+        out->n_scores = rr.n_scores;
+        std::memcpy(out->scores, rr.scores, sizeof(out->scores));
+        out->n_device_offers = rr.n_device_offers;
+        std::memcpy(out->device_offer_group, rr.device_offer_group, sizeof(out->device_offer_group));
+        const uint32_t b = s->h_node_alloc_off[row];
+        for (uint32_t i = 0; i < 32; i++)
+            if ((mask >> i) & 1u) {
+                if (out->n_preempted >= PE_MAX_PREEMPT) return s->fail(PE_EUNSUPPORTED, "more than PE_MAX_PREEMPT preempted allocs");
+                out->preempted[out->n_preempted++] = s->h_palloc_index[b + i];
+            }
+    }
+    return PE_OK;
+}
+
 // One evaluation on the stack's plan (pe_select / pe_place): the fused count
 // loop in launches of at most H/2 placements, each merging its overlay back
 // into the HBM SoA so the plan persists.
@@ -1574,6 +1752,10 @@ int pe_reset_plan(pe_stack* s) {
                               s->stream));
     HIP_TRY(s, hipMemcpyAsync(s->d_dev_free.p, s->d_dev_free_base.p, n * sizeof(uint32_t), hipMemcpyDeviceToDevice,
                               s->stream));
+    std::fill(s->h_preempted.begin(), s->h_preempted.end(), 0);
+    HIP_TRY(s, hipMemsetAsync(s->d_preempted.p, 0, s->h_preempted.size(), s->stream));
+    HIP_TRY(s, hipMemsetAsync(s->d_pcount.p, 0, sizeof(uint32_t) * std::max<uint32_t>(s->n_jtg_keys, 1), s->stream));
+    s->offer_row = -1;
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     s->plan.clear();
     s->tg_memo.clear();
@@ -1706,6 +1888,14 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
                 if (nd.n_device_nets > 1) { g->unsupported = "task network asks on multi-device nodes"; break; }
     }
     s->have_job = true;
+    {   // the job's own state allocs per node (ProposedAllocs minus plan placements)
+        std::vector<uint32_t> own(s->nodes.size(), 0);
+        for (auto& a : s->allocs) if (!a.terminal && a.job == s->job_id) own[a.row]++;
+        HIP_TRY(s, upload(s->d_own_existing, own));
+        auto it = s->job_keys.find(std::make_pair(s->job_id, s->job_ns));
+        s->job_key = it == s->job_keys.end() ? PE_NONE : it->second;
+    }
+    s->offer_row = -1;
     int rc = build_collisions(s);
     if (rc) return rc;
     return PE_OK;
@@ -1741,7 +1931,26 @@ static bool tg_full_scan(pe_stack* s, TgPlan& g) {
     return !g.affinities.empty() || !g.spreads.empty() || !s->job_spreads.empty();
 }
 
+// Device offers of a Select result, one byte per request (~0u: none).
+static uint32_t pack_offers(const pe_ranked_node* out) {
+    if (out->row < 0 || out->n_device_offers == 0) return 0xFFFFFFFFu;
+    uint32_t w = 0;
+    for (uint32_t q = 0; q < out->n_device_offers && q < 4; q++) w |= (out->device_offer_group[q] & 255u) << (8 * q);
+    return w;
+}
+
+static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out);
+
 int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
+    const int rc = select_impl(s, tgi, opts, out);
+    if (rc == PE_OK && s && out) {
+        s->offer_row = out->row;
+        s->offers = pack_offers(out);
+    }
+    return rc;
+}
+
+static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
     if (!s || !out) return PE_EINVAL;
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
@@ -1770,17 +1979,25 @@ int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranke
         pe_select_options o2 = *opts;
         o2.preferred_count = 0;
         uint32_t placed, no;
-        rc = run_place(s, tgi, 1, 0, pref, 0, &o2, out, &placed, &no);
+        if (opts->preempt) rc = run_evict_select(s, g, pref, 0, &o2, out, &no);
+        else rc = run_place(s, tgi, 1, 0, pref, 0, &o2, out, &placed, &no);
         if (rc) return rc;
         s->offset = 0;
         invalidate_tables(s);
         if (out->row >= 0) return PE_OK;
-        return pe_select(s, tgi, &o2, out);
+        return select_impl(s, tgi, &o2, out);
     }
     int rc = prepare_tg(s, tgi, s->visit, s->offset);
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;   // never reset until SetNodes (stack.go:165-167)
+    if (opts && opts->preempt) {
+        uint32_t no;
+        rc = run_evict_select(s, g, s->visit, s->offset, opts, out, &no);
+        if (rc) return rc;
+        s->offset = no;
+        return PE_OK;
+    }
     if (s->limit >= s->visit.size() && s->visit.size() >= s->sweep_min) {
         // a whole pass over a large list: multi-CU sweep instead of one workgroup
         if (s->visit_unique) return run_sweep_select(s, g, opts, out);
@@ -1806,7 +2023,10 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
     pe::NodeSoA soa = soa_of(s);
     pe::TgTables t = tables_of(g);
     pe::Ask a = ask_for(s, g);
-    HIP_TRY(s, pe_launch_commit(&soa, &t, &a, (uint32_t)row, s->stream));
+    // the Select's own device offers when it chose this node (rank.go:404-405)
+    const uint32_t offers = row == s->offer_row ? s->offers : 0xFFFFFFFFu;
+    s->offer_row = -1;
+    HIP_TRY(s, pe_launch_commit(&soa, &t, &a, (uint32_t)row, offers, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     s->plan.emplace_back(g.name, (uint32_t)row);
     // the coll_tg of other task groups with the same name also see this alloc
@@ -1822,7 +2042,25 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
 int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
     if (!s) return PE_EINVAL;
     if (n_preempted == 0) return pe_commit(s, tgi, row);
-    return s->fail(PE_EUNSUPPORTED, "preemption");
+    if (!preempted || !s->have_job || tgi >= s->tgs.size() || row < 0 || (size_t)row >= s->nodes.size())
+        return s->fail(PE_EINVAL, "bad commit");
+    if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
+    // Plan.AppendPreemptedAlloc (structs.go:10664-10680) of allocs on the chosen node
+    uint32_t mask = 0;
+    const uint32_t b = s->h_node_alloc_off[(uint32_t)row];
+    for (uint32_t i = 0; i < n_preempted; i++) {
+        const uint32_t a = preempted[i];
+        if (a >= s->allocs.size() || s->alloc_slot[a] == PE_NONE || s->allocs[a].row != (uint32_t)row)
+            return s->fail(PE_EINVAL, "preempted alloc is not a live alloc of the node");
+        mask |= 1u << (s->alloc_slot[a] - b);
+    }
+    HIP_TRY(s, hipSetDevice(s->device));
+    TgPlan& g = *s->tgs[tgi];
+    pe::PreemptArgs P = preempt_args(s, g);
+    HIP_TRY(s, pe_launch_commit_preempt(&P, (uint32_t)row, mask, s->d_preempted.as<uint8_t>(),
+                                        s->d_pcount.as<uint32_t>(), s->d_dev_free.as<uint32_t>(), s->stream));
+    for (uint32_t i = 0; i < n_preempted; i++) s->h_preempted[s->alloc_slot[preempted[i]]] = 1;
+    return pe_commit(s, tgi, row);
 }
 
 int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
@@ -1838,6 +2076,30 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     if (count) {
         rc = run_place(s, tgi, count, 1, s->visit, s->offset, nullptr, out, &p, &no);
         if (rc) return rc;
+        s->offset = no;
+        // selectNextOption (generic_sched.go:773-792): a nil Select is retried
+        // with Preempt=true; the placement then evicts (handlePreemptions)
+        while (s->cfg.preempt && p < count) {
+            pe_select_options o;
+            std::memset(&o, 0, sizeof(o));
+            o.preempt = 1;
+            rc = run_evict_select(s, g, s->visit, s->offset, &o, &out[p], &no);
+            if (rc) return rc;
+            s->offset = no;
+            if (out[p].row < 0) break;
+            s->offer_row = out[p].row;
+            s->offers = pack_offers(&out[p]);
+            rc = pe_commit_preempt(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
+            if (rc) return rc;
+            p++;
+            if (p == count) break;
+            uint32_t p2 = 0;
+            rc = run_place(s, tgi, count - p, 1, s->visit, s->offset, nullptr, out + p, &p2, &no);
+            if (rc) return rc;
+            s->offset = no;
+            p += p2;
+        }
+        no = s->offset;
     }
     s->offset = no;
     if (placed) *placed = p;

@@ -154,6 +154,54 @@ constexpr int kAuxPsets = 2;
 constexpr int kAuxValues = 256;
 constexpr uint32_t kAuxMissing = 255;
 
+// ---- preemption (BinPack with eviction, scheduler/preemption.go) -------------
+constexpr int kMaxNodeAllocs = 32;    // allocs of one node considered for eviction on device
+constexpr int kMaxProposed = 64;      // ProposedAllocs list length (state allocs + plan placements)
+
+// A non-terminal state alloc as the Preemptor sees it (Allocation.ComparableResources,
+// structs.go:9656-9688; Job.Priority; TaskGroup.Migrate.MaxParallel).
+struct PreemptAlloc {
+    int64_t cpu, mem, disk;
+    int32_t priority, max_parallel;
+    uint32_t job_key;        // dense (job id, namespace)
+    uint32_t jtg_key;        // dense (job id, namespace, task group): plan preemption counter
+    int32_t mbits, dyn;      // NetworkIndex contribution (released on eviction)
+    uint32_t dev_g, dev_c;   // device entries: group / instances, one byte each
+    uint32_t n_dev;          // device entries (<= 4)
+    uint32_t state_index;    // row of the pe_alloc_table snapshot
+};
+static_assert(sizeof(PreemptAlloc) == 64, "PreemptAlloc is one 64-byte line");
+
+struct PreemptArgs {
+    NodeSoA soa;
+    TgTables tg;
+    Ask ask;
+    const uint32_t* node_alloc_off;   // [n + 1] CSR over rows: non-terminal state allocs in table order
+    const PreemptAlloc* allocs;       // [m]
+    const uint8_t* preempted;         // [m] Plan.NodePreemptions membership
+    const uint32_t* pcount;           // [keys] plan preemptions per (job, namespace, task group)
+    const uint32_t* own_existing;     // [n] non-terminal state allocs of the job being placed
+    uint32_t job_key;                 // (job, namespace) of the job being placed
+    int32_t job_priority;
+    const uint32_t* visit;            // visit list (rows)
+    uint32_t n_visit;
+    const uint32_t* penalty_bits;
+    double log10;
+    const double* spread_tab;
+    // per visit position
+    uint8_t* status;                  // kOption / kFiltered / kExhausted / kSkipped
+    double* score;
+    uint32_t* flags;                  // [1] bit 0: a node exceeded the on-device limits
+};
+
+// LimitIterator + MaxScoreIterator over per-position results.
+struct EvictResolveArgs {
+    const uint8_t* status;
+    const double* score;
+    uint32_t n, offset, limit;
+    int32_t* out;                     // [0] winner position (relative) or -1, [1] consumed, [2] filtered, [3] exhausted
+};
+
 struct SystemArgs {
     NodeSoA soa;
     TgTables tg;

@@ -1427,8 +1427,10 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(A.placed, local);
 }
 
-// Host-driven Plan.AppendAlloc on the HBM SoA (pe_commit).
-__global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row) {
+// Host-driven Plan.AppendAlloc on the HBM SoA (pe_commit). `offers`: the
+// device offers of the Select that chose the node (one byte per request), or
+// ~0u to assign them on the current state.
+__global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t offers) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     NodeRec& r = s.rec[row];
     r.used_cpu += a.cpu;
@@ -1439,7 +1441,19 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row) {
     s.coll_job[row] += 1;
     t.coll_tg[row] += 1;
     const uint32_t c = r.cls;
-    if (a.n_dev > 0) t.dev_free[row] = dev_after(a, t.dev_cls[c], t.dev_free[row], 1);
+    if (a.n_dev > 0) {
+        if (offers == 0xFFFFFFFFu) {
+            t.dev_free[row] = dev_after(a, t.dev_cls[c], t.dev_free[row], 1);
+        } else {
+            uint32_t fr = t.dev_free[row];
+            for (int q = 0; q < kMaxDevReq && q < a.n_dev; q++) {
+                const uint32_t g = (offers >> (8 * q)) & 255u, f = (fr >> (8 * g)) & 255u;
+                const uint32_t cnt = (uint32_t)a.dev_cnt[q];
+                fr -= (cnt < f ? cnt : f) << (8 * g);
+            }
+            t.dev_free[row] = fr;
+        }
+    }
     for (int p = 0; p < t.n_psets; p++) {
         const uint32_t v = pset_value(t, p, row, c);
         if (v != kMissing) t.pset_counts[p][v] += 1;
@@ -1791,6 +1805,8 @@ __global__ void __launch_bounds__(256) k_fold_aux(NodeSoA s, TgTables t, const u
     }
 }
 
+#include "evict.inc"
+
 }  // namespace pe
 
 // ---- launch wrappers (host) ------------------------------------------------
@@ -1850,8 +1866,30 @@ hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st) {
 }
 
 hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
-                            hipStream_t st) {
-    hipLaunchKernelGGL(pe::k_commit, dim3(1), dim3(64), 0, st, *s, *t, *a, row);
+                            uint32_t offers, hipStream_t st) {
+    hipLaunchKernelGGL(pe::k_commit, dim3(1), dim3(64), 0, st, *s, *t, *a, row, offers);
+    return hipGetLastError();
+}
+
+// Select with Preempt: per-position evict evaluation, then the window resolve.
+hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs* r, hipStream_t st) {
+    uint32_t blocks = (a->n_visit + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_evict, dim3(blocks), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(pe::k_evict_resolve, dim3(1), dim3(256), 0, st, *r);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ranked_node* out, uint32_t* mask,
+                                  hipStream_t st) {
+    hipLaunchKernelGGL(pe::k_evict_record, dim3(1), dim3(64), 0, st, *a, row, out, mask);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
+                                    uint32_t* pcount, uint32_t* dev_free, hipStream_t st) {
+    hipLaunchKernelGGL(pe::k_commit_preempt, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount, dev_free);
     return hipGetLastError();
 }
 

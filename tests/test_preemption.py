@@ -1,0 +1,180 @@
+"""Preemption: BinPack with eviction (Preemptor.PreemptForTaskGroup /
+PreemptForDevice, scheduler/preemption.go:194-601) and the
+PreemptionScoringIterator score (rank.go:773-844).
+
+Known-answer tests are the reference's TestPreemption cases without network
+preemption (scheduler/preemption_test.go:983-1324), rebuilt at the Stack
+boundary: one node, Select with Preempt=true, the set of preempted allocs.
+createAlloc gives allocs cpu / memory (and task networks) but no shared disk,
+and the ask has an empty EphemeralDisk, so disk is 0 on both sides.
+"""
+import math
+
+import pytest
+
+from nomad_amd import synth
+from nomad_amd.stack import SelectOptions
+from nomad_amd.structs import (Allocation, DeviceGroup, Job, NetworkResource, RequestedDevice,
+                               SchedulerConfig, Task, TaskGroup)
+from oracle.oracle import OracleGenericStack
+from tests.helpers import assert_same_placements, run_place
+
+
+def _engine(**kw):
+    from nomad_amd.stack import GenericStack
+    return GenericStack(**kw)
+
+
+STACKS = [pytest.param(OracleGenericStack, id="oracle"),
+          pytest.param(_engine, id="engine", marks=pytest.mark.gpu)]
+
+LOW, LOW2, HIGH = 30, 40, 100
+
+
+def preemption_node():
+    """preemption_test.go:174-284: 4000 cpu / 8192 MB, reserved 100 / 256, eth0
+    1000 MBits, 1080ti x4, 2080ti x5, F100 fpga (1 of 2 healthy)."""
+    nd = synth.mock_node("node-0")
+    nd.cpu_shares, nd.memory_mb, nd.disk_mb = 4000, 8192, 100 * 1024
+    nd.reserved_cpu, nd.reserved_memory_mb, nd.reserved_disk_mb = 100, 256, 4 * 1024
+    nd.reserved_host_ports = []
+    attrs = {"memory": (11, "GiB"), "cuda_cores": 3584, "graphics_clock": (1480, "MHz"),
+             "memory_bandwidth": (11, "GB/s")}
+    nd.devices = [DeviceGroup("nvidia", "gpu", "1080ti", 4, dict(attrs)),
+                  DeviceGroup("nvidia", "gpu", "2080ti", 5, dict(attrs)),
+                  DeviceGroup("intel", "fpga", "F100", 1, {"memory": (4, "GiB")})]
+    nd.compute_class()
+    return nd
+
+
+def alloc(i, prio, cpu, mem, devices=(), mbits=0):
+    job = {LOW: "low", LOW2: "low2", HIGH: "high"}[prio]
+    return Allocation(node_id="node-0", job_id=job, task_group="web", cpu_shares=cpu, memory_mb=mem,
+                      disk_mb=0, priority=prio, devices=list(devices), net_mbits=mbits)
+
+
+def ask_job(cpu, mem, device=None, mbits=0):
+    net = NetworkResource(mbits=mbits) if mbits else None
+    return Job(id="preemptor", priority=100, task_groups=[TaskGroup(name="web", count=1, ephemeral_disk_mb=0, tasks=[
+        Task(name="web", driver="exec", cpu=cpu, memory_mb=mem, network=net,
+             devices=[device] if device else [])])])
+
+
+CASES = {
+    "one device instance per alloc": (
+        [alloc(0, LOW, 500, 512, [(0, 1)]), alloc(1, LOW, 200, 512, [(0, 1)])],
+        ask_job(1000, 512, RequestedDevice("nvidia/gpu/1080ti", 4)), {0, 1}),
+    "multiple devices used": (
+        [alloc(0, LOW, 500, 512, [(0, 4)]), alloc(1, LOW, 200, 512, [(2, 1)])],
+        ask_job(1000, 512, RequestedDevice("nvidia/gpu/1080ti", 4)), {0}),
+    "allocs across multiple devices that match": (
+        [alloc(0, LOW, 500, 512, [(0, 2)]), alloc(1, HIGH, 200, 100, [(0, 1)]),
+         alloc(2, LOW, 200, 256, [(1, 2)]), alloc(3, LOW, 100, 256, [(1, 2)]),
+         alloc(4, LOW, 200, 512, [(2, 1)])],
+        ask_job(1000, 512, RequestedDevice("gpu", 4)), {2, 3}),
+    "lower/higher priority combinations": (
+        [alloc(0, LOW, 500, 512, [(0, 2)]), alloc(1, LOW2, 200, 100, [(0, 2)]),
+         alloc(2, LOW, 200, 256, [(1, 2)]), alloc(3, LOW, 100, 256, [(1, 2)]),
+         alloc(4, LOW, 100, 256, [(1, 1)]), alloc(5, LOW, 200, 512, [(2, 1)])],
+        ask_job(1000, 512, RequestedDevice("gpu", 4)), {2, 3}),
+    "device preemption not possible": (
+        [alloc(0, LOW, 500, 512, [(0, 4)]), alloc(1, LOW, 200, 512, [(2, 1)])],
+        ask_job(1000, 512, RequestedDevice("gpu", 6)), None),
+    "filter out superset allocs": (
+        [alloc(0, HIGH, 1800, 2256, mbits=150), alloc(1, LOW, 1500, 256, mbits=100),
+         alloc(2, LOW, 600, 256, mbits=300)],
+        ask_job(1000, 256, mbits=50), {1}),
+}
+
+
+def net_priority(prios):
+    mx = float(max(prios))
+    return mx + float(sum(prios)) / mx
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+@pytest.mark.parametrize("case", list(CASES))
+def test_preemption_kat(stack_cls, case):
+    allocs, job, expected = CASES[case]
+    node = preemption_node()
+    st = stack_cls()
+    st.SetState([node], allocs)
+    st.SetJob(job)
+    st.SetNodes([node])
+    plain = st.SelectRaw(0)
+    assert plain.row == -1                      # no fit without eviction
+    r = st.SelectRaw(0, SelectOptions(preempt=True))
+    if expected is None:
+        assert r.row == -1
+        return
+    assert r.row == 0
+    assert set(r.preempted) == expected
+    # PreemptionScoringIterator: 1 / (1 + exp(0.0048 (netPriority - 2048))) appended last
+    prios = [allocs[i].priority for i in r.preempted]
+    want = 1.0 / (1.0 + math.exp(0.0048 * (net_priority(prios) - 2048.0)))
+    assert abs(r.scores[-1] - want) <= 1e-12 * want
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_preemption_commit_frees_resources(stack_cls):
+    """Plan.AppendPreemptedAlloc removes the victims from ProposedAllocs
+    (context.go:134-138): after the preempting placement commits, the freed
+    instances are gone to the new alloc and a second identical ask needs
+    another eviction round."""
+    allocs, job, _ = CASES["one device instance per alloc"]
+    node = preemption_node()
+    st = stack_cls()
+    st.SetState([node], allocs)
+    st.SetJob(job)
+    st.SetNodes([node])
+    r = st.SelectRaw(0, SelectOptions(preempt=True))
+    st.Commit(0, r.row, r.preempted)
+    again = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert again.row == -1                      # 1080ti fully held by our own alloc
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_max_parallel_penalty(stack_cls):
+    """scoreForTaskGroup adds 50 x (preempted + 1 - maxParallel) once a job's
+    preemptions in the plan reach its migrate max_parallel
+    (preemption.go:633-642): the penalised alloc is passed over."""
+    node = preemption_node()
+    allocs = [Allocation(node_id="node-0", job_id="a", task_group="web", cpu_shares=1900, memory_mb=256,
+                         priority=LOW, max_parallel=1),
+              Allocation(node_id="node-0", job_id="b", task_group="web", cpu_shares=1950, memory_mb=256,
+                         priority=LOW),
+              Allocation(node_id="node-0", job_id="a", task_group="web", cpu_shares=10, memory_mb=10,
+                         priority=LOW, max_parallel=1)]
+    other = synth.mock_node("node-1")
+    other.reserved_host_ports = []
+    job = ask_job(1900, 256)
+    job.task_groups[0].count = 2
+    st = stack_cls()
+    st.SetState([node, other], allocs + [Allocation(node_id="node-1", job_id="a", task_group="web",
+                                                    cpu_shares=3000, memory_mb=64, priority=LOW,
+                                                    max_parallel=1)])
+    st.SetJob(job)
+    st.SetNodes([other])
+    r1 = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert r1.row == 1 and r1.preempted == [3]          # job "a" now has one preemption in the plan
+    st.Commit(0, r1.row, r1.preempted)
+    st.SetNodes([node])
+    r2 = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert r2.row == 0 and r2.preempted == [1]          # alloc 0 (closer) carries the +50 penalty
+
+
+# ---- GPU parity: count loop with preemption fallback (C5) ---------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,count,seed", [(400, 300, 1), (2000, 1500, 2)])
+def test_c5_preemption_count_loop(n, count, seed):
+    nodes, allocs = synth.cluster_c5(n, seed=seed)
+    job = synth.job_c5(count)
+    perm = synth.shuffle(len(nodes), seed + 20)
+    cfg = SchedulerConfig(preempt_service=True)
+    _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, perm, config=cfg)
+    _, _, re = run_place(_engine, nodes, allocs, job, perm, config=cfg)
+    assert any(x.preempted for x in ro)                 # the workload exercises eviction
+    assert_same_placements(re, ro)
+    assert [sorted(x.preempted) for x in re] == [sorted(x.preempted) for x in ro]
+    assert [x.device_offers for x in re] == [x.device_offers for x in ro]
