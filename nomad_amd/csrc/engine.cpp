@@ -43,6 +43,9 @@ hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ran
                                   hipStream_t st);
 hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
                                     uint32_t* pcount, uint32_t* dev_free, hipStream_t st);
+hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st);
+hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
+                                    uint32_t* dev_free, uint32_t* placed, hipStream_t st);
 hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
                                hipStream_t st);
 hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec* merged, hipStream_t st);
@@ -289,7 +292,7 @@ struct pe_stack {
     uint32_t n_jtg_keys = 0;
     std::string preempt_unsupported;           // snapshot outside the on-device limits
     DevMem d_node_alloc_off, d_palloc, d_preempted, d_pcount, d_own_existing;
-    DevMem d_ev_status, d_ev_score, d_ev_flags, d_ev_out, d_ev_mask;
+    DevMem d_ev_status, d_ev_score, d_ev_flags, d_ev_out, d_ev_mask, d_ev_rows, d_ev_masks, d_ev_offers;
     uint32_t job_key = PE_NONE;
     // device offers of the last Select's pick (committed as chosen)
     int32_t offer_row = -1;
@@ -1467,6 +1470,7 @@ pe::PreemptArgs preempt_args(pe_stack* s, TgPlan& g) {
     P.job_key = s->job_key;
     P.job_priority = s->job_priority;
     P.log10 = s->log10;
+    P.score_preemption = s->cfg.stack_kind == PE_STACK_GENERIC ? 1 : 0;
     return P;
 }
 
@@ -1955,13 +1959,15 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     if (s->cfg.stack_kind != PE_STACK_GENERIC) {
-        // SystemStack.Select: single pass over the (single-node) list, no limit
+        // SystemStack.Select: single pass over the (single-node) list, no limit;
+        // BinPack evicts when the scheduler configuration enables preemption
         int rc = prepare_tg(s, tgi, s->visit, 0);
         if (rc) return rc;
         uint32_t placed, no;
         const uint32_t saved = s->limit;
         s->limit = 1;
-        rc = run_place(s, tgi, 1, 0, s->visit, 0, nullptr, out, &placed, &no);
+        if (s->cfg.preempt) rc = run_evict_select(s, *s->tgs[tgi], s->visit, 0, nullptr, out, &no);
+        else rc = run_place(s, tgi, 1, 0, s->visit, 0, nullptr, out, &placed, &no);
         s->limit = saved;
         return rc;
     }
@@ -2352,6 +2358,93 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
     for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) s->plan.emplace_back(g.name, s->visit[i]);
+    if (s->cfg.preempt) {
+        // BinPack with evict (stack.go:267-278) on the nodes the plain fit exhausted
+        std::vector<uint32_t> pos, rows;
+        for (uint32_t i = 0; i < n; i++)
+            if (out_status[i] == 2) { pos.push_back(i); rows.push_back(s->visit[i]); }
+        if (!rows.empty()) {
+            if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
+            // the max_parallel penalty reads the plan's preemption counts, which
+            // earlier nodes grow: then the nodes go one at a time in list order
+            bool serial = false;
+            for (uint32_t r : rows) {
+                for (uint32_t k = s->h_node_alloc_off[r]; k < s->h_node_alloc_off[r + 1] && !serial; k++)
+                    serial = s->allocs[s->h_palloc_index[k]].max_parallel > 0;
+                if (serial) break;
+            }
+            if (serial) {
+                const uint32_t saved = s->limit;
+                s->limit = 1;
+                for (size_t k = 0; k < rows.size(); k++) {
+                    pe_ranked_node r;
+                    uint32_t no;
+                    rc = run_evict_select(s, g, std::vector<uint32_t>{rows[k]}, 0, nullptr, &r, &no);
+                    if (rc) { s->limit = saved; return rc; }
+                    if (r.row < 0) continue;
+                    s->offer_row = r.row;
+                    s->offers = pack_offers(&r);
+                    rc = pe_commit_preempt(s, tgi, r.row, r.preempted, r.n_preempted);
+                    if (rc) { s->limit = saved; return rc; }
+                    out_status[pos[k]] = 0;
+                    out_score[pos[k]] = r.final_score;
+                    p++;
+                }
+                s->limit = saved;
+            } else {
+                const uint32_t E = (uint32_t)rows.size();
+                pe::PreemptArgs P = preempt_args(s, g);
+                HIP_TRY(s, upload(s->d_ev_rows, rows));
+                HIP_TRY(s, s->d_ev_status.ensure(E));
+                HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * E));
+                HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * E));
+                HIP_TRY(s, s->d_ev_offers.ensure(sizeof(uint32_t) * E));
+                HIP_TRY(s, s->d_ev_flags.ensure(16));
+                HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
+                HIP_TRY(s, hipMemsetAsync(s->d_status.p, 0, 16, s->stream));
+                P.visit = s->d_ev_rows.as<uint32_t>();
+                P.n_visit = E;
+                P.status = s->d_ev_status.as<uint8_t>();
+                P.score = s->d_ev_score.as<double>();
+                P.mask_out = s->d_ev_masks.as<uint32_t>();
+                P.offers_out = s->d_ev_offers.as<uint32_t>();
+                P.flags = s->d_ev_flags.as<uint32_t>();
+                HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+                HIP_TRY(s, pe_launch_evict_only(&P, s->stream));
+                uint32_t flags = 0;
+                HIP_TRY(s, hipMemcpyAsync(&flags, P.flags, sizeof(flags), hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(s, hipStreamSynchronize(s->stream));
+                if (flags & 1u)
+                    return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the "
+                                                    "on-device alloc limits");
+                HIP_TRY(s, pe_launch_commit_evicted(&P, s->d_preempted.as<uint8_t>(), s->d_pcount.as<uint32_t>(),
+                                                    s->d_dev_free.as<uint32_t>(), s->d_status.as<uint32_t>(),
+                                                    s->stream));
+                HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+                std::vector<uint8_t> st(E);
+                std::vector<double> sc(E);
+                std::vector<uint32_t> masks(E);
+                HIP_TRY(s, hipMemcpyAsync(st.data(), P.status, E, hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(s, hipMemcpyAsync(sc.data(), P.score, sizeof(double) * E, hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(s, hipMemcpyAsync(masks.data(), P.mask_out, sizeof(uint32_t) * E, hipMemcpyDeviceToHost,
+                                          s->stream));
+                HIP_TRY(s, hipStreamSynchronize(s->stream));
+                float ms2 = 0;
+                HIP_TRY(s, hipEventElapsedTime(&ms2, s->ev0, s->ev1));
+                s->last_ms += ms2;
+                for (uint32_t k = 0; k < E; k++) {
+                    if (st[k] != 0) continue;   // exhausted / skipped nodes stay exhausted
+                    out_status[pos[k]] = 0;
+                    out_score[pos[k]] = sc[k];
+                    s->plan.emplace_back(g.name, rows[k]);
+                    const uint32_t b = s->h_node_alloc_off[rows[k]];
+                    for (uint32_t i = 0; i < 32; i++)
+                        if ((masks[k] >> i) & 1u) s->h_preempted[b + i] = 1;
+                    p++;
+                }
+            }
+        }
+    }
     if (placed) *placed = p;
     return PE_OK;
 }

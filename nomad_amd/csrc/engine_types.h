@@ -188,9 +188,12 @@ struct PreemptArgs {
     const uint32_t* penalty_bits;
     double log10;
     const double* spread_tab;
+    int32_t score_preemption;         // PreemptionScoringIterator in the chain (GenericStack only)
     // per visit position
     uint8_t* status;                  // kOption / kFiltered / kExhausted / kSkipped
     double* score;
+    uint32_t* mask_out;               // or null: preempted allocs (bits over the node's allocs)
+    uint32_t* offers_out;             // or null: device offers, one byte per request
     uint32_t* flags;                  // [1] bit 0: a node exceeded the on-device limits
 };
 

@@ -1881,9 +1881,26 @@ hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs*
     return hipGetLastError();
 }
 
+hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st) {
+    uint32_t blocks = (a->n_visit + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_evict, dim3(blocks), dim3(256), 0, st, *a);
+    return hipGetLastError();
+}
+
 hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ranked_node* out, uint32_t* mask,
                                   hipStream_t st) {
     hipLaunchKernelGGL(pe::k_evict_record, dim3(1), dim3(64), 0, st, *a, row, out, mask);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
+                                    uint32_t* dev_free, uint32_t* placed, hipStream_t st) {
+    uint32_t blocks = (a->n_visit + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_commit_evicted, dim3(blocks), dim3(256), 0, st, *a, preempted, pcount, dev_free, placed);
     return hipGetLastError();
 }
 

@@ -1926,7 +1926,7 @@ int oracle_system_place(oracle_stack* s, uint32_t tgi, double* out_score, uint8_
             continue;
         }
         out_score[i] = r.final_score; out_status[i] = 0;
-        oracle_commit(s, tgi, r.row);
+        oracle_commit_preempt(s, tgi, r.row, r.preempted, r.n_preempted);
         p++;
     }
     s->source.SetNodes(all);

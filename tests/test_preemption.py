@@ -178,3 +178,46 @@ def test_c5_preemption_count_loop(n, count, seed):
     assert_same_placements(re, ro)
     assert [sorted(x.preempted) for x in re] == [sorted(x.preempted) for x in ro]
     assert [x.device_offers for x in re] == [x.device_offers for x in ro]
+
+
+def _system_place(cls, nodes, allocs, job, cfg):
+    st = cls(config=cfg)
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(list(range(len(nodes))))
+    return st.SystemPlace(0)
+
+
+@pytest.mark.parametrize("max_parallel", [False, True])
+def test_system_preemption_oracle_places_more(max_parallel):
+    """SystemStack BinPack evicts when preemption is enabled (stack.go:267-278):
+    with it, nodes full of priority-20 GPU work take the system job."""
+    from oracle.oracle import OracleSystemStack
+    nodes, allocs = synth.cluster_c5(300, seed=8)
+    if not max_parallel:
+        for a in allocs:
+            a.max_parallel = 0
+    job = synth.job_c5(1)
+    job.type = 2
+    _, s0, p0 = _system_place(OracleSystemStack, nodes, allocs, job, SchedulerConfig())
+    _, s1, p1 = _system_place(OracleSystemStack, nodes, allocs, job, SchedulerConfig(preempt_system=True))
+    assert p1 > p0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_parallel", [False, True])
+def test_system_preemption_parity(max_parallel):
+    from nomad_amd.stack import SystemStack
+    from oracle.oracle import OracleSystemStack
+    nodes, allocs = synth.cluster_c5(3000, seed=9)
+    if not max_parallel:
+        for a in allocs:
+            a.max_parallel = 0
+    job = synth.job_c5(1)
+    job.type = 2
+    cfg = SchedulerConfig(preempt_system=True)
+    so, to, po = _system_place(OracleSystemStack, nodes, allocs, job, cfg)
+    se, te, pe = _system_place(SystemStack, nodes, allocs, job, cfg)
+    assert po == pe and (to == te).all()
+    m = to == 0
+    assert (so[m] == se[m]).all()
