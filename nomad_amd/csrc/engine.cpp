@@ -214,6 +214,8 @@ struct PsetDev {
     bool even = false;
     double weight_frac = 0;
     bool per_node = false;
+    bool distinct = false;         // distinct_property set (filter) instead of a spread (score)
+    uint32_t allowed = 1;
 };
 
 struct TgPlan {
@@ -236,6 +238,8 @@ struct TgPlan {
     bool has_aff_table = false, node_aff_used = false, node_ok_used = false, alias_used = false;
     std::vector<std::unique_ptr<PsetDev>> psets;
     bool psets_built = false;
+    int n_spread = 0;                  // psets[0, n_spread) are spreads, the rest distinct_property
+    std::vector<ParsedConstraint> distinct_props;   // tg + task distinct_property constraints
     // device requests (tasks in order) and the per-class match table
     std::vector<DevReqSpec> dev_reqs;
     DevMem dev_cls;
@@ -1082,6 +1086,76 @@ int build_psets(pe_stack* s, TgPlan& g) {
         HIP_TRY(s, upload(ps->desired, des));
         g.psets.push_back(std::move(ps));
     }
+    g.n_spread = (int)g.psets.size();
+    // distinct_property sets (propertyset.go:14-355): job-level ones count every
+    // alloc of the job, task-group ones only the group's (filterAllocs)
+    std::vector<std::pair<const ParsedConstraint*, bool>> dps;
+    for (auto& c : s->job_constraints) if (c.op == "distinct_property") dps.emplace_back(&c, true);
+    for (auto& c : g.distinct_props) dps.emplace_back(&c, false);
+    if (g.psets.size() + dps.size() > (size_t)pe::kMaxPsets) {
+        g.unsupported = "more than 4 spread and distinct_property sets";
+        return PE_OK;
+    }
+    for (auto& dp : dps) {
+        const ParsedConstraint& c = *dp.first;
+        const bool job_level = dp.second;
+        auto ps = std::make_unique<PsetDev>();
+        ps->distinct = true;
+        ps->target = c.l;
+        ps->per_node = ps->target.escapes || ps->target.kind == T_ID || ps->target.kind == T_NAME;
+        // RTarget: strconv.ParseUint, default 1; unparsable -> every node filtered
+        ps->allowed = 1;
+        if (c.r.kind == T_LITERAL && !c.r.literal.empty()) {
+            unsigned long long v = 0;
+            bool okp = true;
+            for (char ch : c.r.literal) {
+                if (ch < '0' || ch > '9' || v > (UINT64_MAX - 9) / 10) { okp = false; break; }
+                v = v * 10 + (unsigned)(ch - '0');
+            }
+            ps->allowed = okp ? (uint32_t)std::min<unsigned long long>(v, 0xFFFFFFFFull) : 0u;
+        } else if (c.r.kind != T_LITERAL) {
+            ps->allowed = 0;   // an interpolated RTarget does not parse as a count
+        }
+        auto value_of = [&](const NodeView& nd) -> uint32_t {
+            uint32_t vid;
+            Target t = resolve(s, ps->target, nd, &vid);
+            if (!t.found || t.nil) return pe::kMissing;
+            if (vid == PE_NONE) vid = s->lookup(t.value);
+            auto it = ps->value_index.find(vid);
+            if (it == ps->value_index.end()) {
+                it = ps->value_index.emplace(vid, (uint32_t)ps->value_str.size()).first;
+                ps->value_str.push_back(vid);
+            }
+            return it->second;
+        };
+        std::vector<uint32_t> by_class(s->ncls, pe::kMissing), by_node;
+        if (ps->per_node) {
+            by_node.resize(n);
+            for (size_t i = 0; i < n; i++) by_node[i] = value_of(s->view((uint32_t)i));
+        } else {
+            for (uint32_t c2 = 0; c2 < s->ncls; c2++) by_class[c2] = value_of(s->view(s->class_rep[c2]));
+        }
+        if (ps->value_str.size() > (size_t)pe::kMaxValues) { g.unsupported = "distinct_property with > 256 values"; return PE_OK; }
+        auto node_val = [&](uint32_t row) { return ps->per_node ? by_node[row] : by_class[s->nodes[row].cls]; };
+        ps->h_counts.assign(ps->value_str.size(), 0);
+        for (auto& a : s->allocs)
+            if (!a.terminal && a.ns == s->job_ns && a.job == s->job_id && (job_level || a.tg == g.name)) {
+                const uint32_t v = node_val(a.row);
+                if (v != pe::kMissing) ps->h_counts[v]++;
+            }
+        for (auto& p : s->plan)
+            if (job_level || p.first == g.name) {
+                const uint32_t v = node_val(p.second);
+                if (v != pe::kMissing) ps->h_counts[v]++;
+            }
+        HIP_TRY(s, upload(ps->val_class, by_class));
+        if (ps->per_node) HIP_TRY(s, upload(ps->val_node, by_node));
+        std::vector<uint32_t> cnt = ps->h_counts;
+        if (cnt.empty()) cnt.push_back(0);
+        HIP_TRY(s, upload(ps->counts, cnt));
+        HIP_TRY(s, upload(ps->desired, std::vector<double>(1, 0.0)));
+        g.psets.push_back(std::move(ps));
+    }
     g.psets_built = true;
     return PE_OK;
 }
@@ -1246,8 +1320,10 @@ pe::TgTables tables_of(TgPlan& g) {
         t.dev_cls = g.dev_cls.as<pe::DevClass>();
     }
     t.n_psets = (int)g.psets.size();
+    t.n_spread = g.n_spread;
     for (int p = 0; p < t.n_psets; p++) {
         PsetDev& ps = *g.psets[p];
+        t.pset_allowed[p] = ps.allowed;
         t.pset_val_class[p] = ps.val_class.as<uint32_t>();
         t.pset_val_node[p] = ps.per_node ? ps.val_node.as<uint32_t>() : nullptr;
         t.pset_counts[p] = ps.counts.as<uint32_t>();
@@ -1284,6 +1360,16 @@ pe::Ask ask_for(pe_stack* s, TgPlan& g) {
     a.algo_spread = s->cfg.algorithm == PE_ALGO_SPREAD;
     a.anti_aff = generic ? 1 : 0;
     return a;
+}
+
+// Job-level distinct_property counts every task group's allocs: after a commit
+// of one group the other groups' value counts are rebuilt from the plan.
+void invalidate_job_distinct(pe_stack* s, uint32_t tgi) {
+    bool job_distinct = false;
+    for (auto& c : s->job_constraints) job_distinct = job_distinct || c.op == "distinct_property";
+    if (!job_distinct) return;
+    for (size_t k = 0; k < s->tgs.size(); k++)
+        if (k != tgi) s->tgs[k]->psets_built = false;
 }
 
 void invalidate_tables(pe_stack* s) {
@@ -1814,7 +1900,8 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     s->job_spreads = conv_spreads(j->spread_off, j->spread_count);
     std::string job_unsupported;
     for (auto& c : s->job_constraints)
-        if (c.op == "distinct_property") job_unsupported = "distinct_property constraints";
+        if (c.op == "distinct_property" && !generic)
+            job_unsupported = "distinct_property on a system stack (placements couple through the value counts)";
     s->tgs.clear();
     for (uint32_t gi = 0; gi < j->tg_count; gi++) {
         const pe_task_group& t = j->task_groups[gi];
@@ -1828,7 +1915,10 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
         for (uint32_t k = 0; k < t.constraint_count; k++) {
             g->constraints.push_back(parse_constraint(s, j->constraints[t.constraint_off + k]));
             if (g->constraints.back().op == "distinct_hosts") g->ask.distinct_tg = 1;
-            if (g->constraints.back().op == "distinct_property") g->unsupported = "distinct_property constraints";
+            if (g->constraints.back().op == "distinct_property") {
+                if (!generic) g->unsupported = "distinct_property on a system stack (placements couple through the value counts)";
+                g->distinct_props.push_back(g->constraints.back());
+            }
         }
         for (uint32_t k = 0; k < t.task_count; k++) {
             const pe_task& x = j->tasks[t.task_off + k];
@@ -2004,7 +2094,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         s->offset = no;
         return PE_OK;
     }
-    if (s->limit >= s->visit.size() && s->visit.size() >= s->sweep_min) {
+    if (s->limit >= s->visit.size() && s->visit.size() >= s->sweep_min && g.n_spread == (int)g.psets.size()) {
         // a whole pass over a large list: multi-CU sweep instead of one workgroup
         if (s->visit_unique) return run_sweep_select(s, g, opts, out);
     }
@@ -2035,6 +2125,7 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
     HIP_TRY(s, pe_launch_commit(&soa, &t, &a, (uint32_t)row, offers, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     s->plan.emplace_back(g.name, (uint32_t)row);
+    invalidate_job_distinct(s, tgi);
     // the coll_tg of other task groups with the same name also see this alloc
     for (size_t k = 0; k < s->tgs.size(); k++)
         if (k != tgi && s->tgs[k]->name == g.name) {
@@ -2109,6 +2200,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     }
     s->offset = no;
     if (placed) *placed = p;
+    if (p) invalidate_job_distinct(s, tgi);
     // multi-tg jobs sharing a name see these allocs in their collision counts
     for (size_t k = 0; k < s->tgs.size(); k++)
         if (k != tgi && s->tgs[k]->name == g.name) { rc = build_collisions(s); if (rc) return rc; break; }

@@ -57,7 +57,9 @@ struct TgTables {
     const double* node_aff;      // [n] or null
     const uint8_t* alias_ok;     // [n] or null: node has an address for the tg's port network
     uint32_t* coll_tg;           // [n] proposed allocs of (job, tg) per node
-    int n_psets;
+    int n_psets;                                 // spread property sets first, then distinct_property sets
+    int n_spread;                                // psets [0, n_spread) score, [n_spread, n_psets) filter
+    uint32_t pset_allowed[kMaxPsets];            // distinct_property: allowed use count per value
     const uint32_t* pset_val_class[kMaxPsets];   // [ncls] value index or kMissing
     const uint32_t* pset_val_node[kMaxPsets];    // [n] or null (escaped property)
     uint32_t* pset_counts[kMaxPsets];            // [nvals] combined use (existing + proposed)

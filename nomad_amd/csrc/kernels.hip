@@ -171,9 +171,22 @@ struct ScoreIn {
 // (dk placements of this eval): FeasibilityWrapper verdict, distinct_hosts,
 // BinPack network offers and AllocsFit. Returns kOption with the scoring
 // inputs filled, else kFiltered / kExhausted.
+// DistinctPropertyIterator (feasible.go:601-704): the node's value of each
+// distinct_property set must exist and be used fewer than `allowed` times.
+// `tab` (the eval's per-value table, 0.0 = open) or the HBM counts.
+__device__ __forceinline__ bool distinct_ok(const TgTables& t, const double* tab, uint32_t row, uint32_t c) {
+    for (int p = t.n_spread; p < t.n_psets; p++) {
+        const uint32_t v = pset_value(t, p, row, c);
+        if (v == kMissing) return false;
+        const bool blocked = tab ? tab[p * (kMaxValues + 1) + v] != 0.0 : t.pset_counts[p][v] >= t.pset_allowed[p];
+        if (blocked) return false;
+    }
+    return true;
+}
+
 __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
                                              const Ask& a, uint32_t dk, uint32_t row, const NodeIn& in,
-                                             ScoreIn* si) {
+                                             ScoreIn* si, const double* ptab = nullptr) {
     const NodeRec& r = in.r;
     const uint32_t c = r.cls;
     // FeasibilityWrapper: memoised job + task-group checks (host-resolved per class)
@@ -189,6 +202,7 @@ __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t
         if (a.distinct_job && s.coll_job[row] + dk > 0) ok = false;
         if (a.distinct_tg && coll > 0) ok = false;
     }
+    if (ok && t.n_psets > t.n_spread) ok = distinct_ok(t, ptab, row, c);
     if (!ok) return kFiltered;
     // BinPackIterator (rank.go:193-527): network offers, then AllocsFit
     if (a.tg_dyn > 0 || a.has_task_net) {
@@ -230,7 +244,7 @@ __device__ __forceinline__ void lookup_scores(const TgTables& t, const uint32_t*
     si->penalty = penalty_bits ? (penalty_bits[row >> 5] >> (row & 31)) & 1u : 0u;
     si->aff = (t.class_aff || t.node_aff) ? (t.node_aff ? t.node_aff[row] : t.class_aff[c]) : 0.0;
     double total = 0.0;
-    for (int p = 0; p < t.n_psets; p++) {
+    for (int p = 0; p < t.n_spread; p++) {
         const uint32_t v = pset_value(t, p, row, c);
         total += (v == kMissing) ? -1.0 : spread_tab[p * (kMaxValues + 1) + v];
     }
@@ -284,7 +298,7 @@ __device__ __forceinline__ void eval_loaded(const NodeSoA& s, const TgTables& t,
                                             double log10, const double* spread_tab, uint32_t row,
                                             const NodeIn& in, NodeEval* out) {
     ScoreIn si;
-    const int st = status_loaded(s, t, class_ok, a, dk, row, in, &si);
+    const int st = status_loaded(s, t, class_ok, a, dk, row, in, &si, spread_tab);
     if (st != kOption) { out->status = st; return; }
     lookup_scores(t, penalty_bits, spread_tab, row, in.r.cls, &si);
     score_option<kKeepParts>(a, log10, si, out);
@@ -309,6 +323,10 @@ __device__ void build_spread_table(const TgTables& t, const uint32_t* counts, do
     for (int p = 0; p < t.n_psets; p++) {
         const int nv = t.pset_nvals[p];
         const uint32_t* cnt = counts + p * kMaxValues;
+        if (p >= t.n_spread) {   // distinct_property: 1.0 marks a value at its allowed count
+            for (int v = tid; v < nv; v += BLOCK) tab[p * (kMaxValues + 1) + v] = cnt[v] >= t.pset_allowed[p] ? 1.0 : 0.0;
+            continue;
+        }
         if (t.pset_even[p]) {
             if (tid == 0) {
                 uint32_t mn = 0, mx = 0, present = 0;
