@@ -15,6 +15,19 @@ reported beside it.
 
 Multi-GPU: the windowed binpack path does not shard; each rank
 runs its own batches on its own GPU (replicas, weak scaling).
+
+Beside the headline line's C2 numbers, the JSON carries one object per other
+BASELINE.json config (sections, --sections to choose):
+  c3          spread + affinity + semver/regexp job, count=1000 on 10k nodes in 3
+              DCs: one evaluation's full-pass count loop on one GPU
+  c4          system job on a 100k-node cluster sharded over the ranks (contiguous
+              ranges of the SetNodes list, no data-path collective)
+  c5          device asks (nvidia/gpu x2, memory >= 40 GiB) with preemption on 50k
+              nodes whose GPUs are mostly held by priority-20 work
+  c3_sharded  full-pass Selects over a 100k-node C3 cluster split across the
+              ranks: one 80-byte record all-gather (RCCL) per placement
+Each section times the engine on the GPU and the oracle (C++ restatement) on a
+bounded sample of the same workload on one host core.
 """
 import argparse
 import concurrent.futures as cf
@@ -49,6 +62,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--sweep-nodes", type=int, default=1 << 24,
                    help="nodes of the scoring-sweep roofline measurement (0 = skip)")
+    p.add_argument("--sections", default="c3,c4,c5,c3_sharded",
+                   help="comma list of extra config sections (empty = none)")
     return p.parse_args()
 
 
@@ -58,8 +73,15 @@ def dist_init():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
     if world > 1:
+        import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # CPU tensors (timing reductions) over gloo, GPU tensors (the shard
+        # record all-gather) over RCCL / xGMI
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+            dist.init_process_group("cpu:gloo,cuda:nccl")
+        else:
+            dist.init_process_group("gloo")
         pg = dist
     return rank, world, local, pg
 
@@ -174,6 +196,214 @@ def sweep_roofline(n, device, selects=6):
             "winner_row": row, "setup_s": setup_s}
 
 
+# ---- other BASELINE.json configs -------------------------------------------------
+
+def _oracle_rate(make_stack, place, budget_s):
+    """Placements/s of the oracle on one core: `place(stack, k)` places k
+    allocations; k grows until the sample takes ~budget_s."""
+    k, placed, dt = 8, 0, 0.0
+    while True:
+        st = make_stack()
+        t0 = time.perf_counter()
+        placed = place(st, k)
+        dt = time.perf_counter() - t0
+        if dt >= budget_s / 4 or placed < k:
+            return placed / dt if dt > 0 else 0.0, placed, dt
+        k *= 4
+
+
+def section_c3(device, cpu_s):
+    """C3: spread (dc1 50 % / dc2 30 %) + node affinity + semver / regexp
+    constraints, count=1000 on 10k nodes: limit MaxInt32, so every placement is
+    a full pass (fused count loop, one workgroup, per-value spread tables in LDS)."""
+    from nomad_amd import synth
+    from nomad_amd.stack import GenericStack
+    nodes, allocs = synth.cluster_c3(10000, seed=7)
+    job = synth.job_c3(1000)
+    perm = synth.shuffle(len(nodes), 17)
+    st = GenericStack(device=device)
+    st.SetState(nodes, allocs)
+    times = []
+    for i in range(3):
+        st.ResetPlan()
+        st.SetJob(job)
+        st.SetNodes(perm)
+        t0 = time.perf_counter()
+        _, _, placed, _ = st.PlaceArrays(0, 1000)
+        times.append(time.perf_counter() - t0)
+    kernel_ms = st.last_kernel_ms()
+    st.close()
+    wall = float(np.median(times[1:]))
+    out = {"workload": "C3: job_c3 count=1000 (spread + affinity + semver/regexp) on 10000 nodes, 3 DCs, "
+                       "one evaluation", "placements": int(placed), "placements_per_s": placed / wall,
+           "node_evals_per_s": placed * len(nodes) / wall, "wall_ms": wall * 1e3, "kernel_ms": kernel_ms}
+    if cpu_s > 0:
+        from oracle.oracle import OracleGenericStack
+
+        def mk():
+            o = OracleGenericStack()
+            o.SetState(nodes, allocs)
+            o.SetJob(job)
+            o.SetNodes(perm)
+            return o
+        rate, k, dt = _oracle_rate(mk, lambda o, k: o.PlaceArrays(0, k)[2], cpu_s)
+        out["cpu_baseline"] = {"value": rate, "unit": "placements/s", "cores": 1, "kind": "port",
+                               "sample": "first %d placements of the same evaluation in %.2f s" % (k, dt)}
+    return out
+
+
+def section_c4(device, rank, world, pg, cpu_s):
+    """C4: system job (mock.SystemJob) on 100k nodes (~10 % windows filtered, ~5 %
+    pre-filled), the SetNodes list split into one contiguous range per rank."""
+    from nomad_amd import shard, synth, synth_columnar
+    from nomad_amd.stack import SystemStack
+    n = 100000
+    cs = synth_columnar.ColumnarState(n, seed=11, kind="c4", prefill=0.05)
+    job = synth.mock_system_job()
+    rows = np.random.Generator(np.random.PCG64(5)).permutation(n).astype(np.uint32)
+    st = SystemStack(device=device)
+    st.SetStateColumnar(cs)
+    times, kms, placed = [], [], 0
+    for i in range(4):
+        st.ResetPlan()
+        st.SetJob(job)
+        barrier(pg)
+        t0 = time.perf_counter()
+        _, _, _, _, placed = shard.system_place_sharded(st, rows, rank, world)
+        dt = time.perf_counter() - t0
+        barrier(pg)
+        times.append(reduce(pg, dt, lambda d: d.ReduceOp.MAX))
+        kms.append(st.last_kernel_ms())
+    st.close()
+    total = int(reduce(pg, placed, lambda d: d.ReduceOp.SUM))
+    wall = float(np.median(times[1:]))
+    out = {"workload": "C4: mock.SystemJob on %d nodes, %d contiguous shards (one per GPU)" % (n, world),
+           "scaling": "strong", "placed": total, "nodes_per_s": n / wall, "wall_ms": wall * 1e3,
+           "kernel_ms_rank0": float(np.median(kms[1:]))}
+    if cpu_s > 0 and rank == 0:
+        from oracle.oracle import OracleSystemStack
+        ns = 20000
+        small = synth_columnar.ColumnarState(ns, seed=11, kind="c4", prefill=0.05)
+        o = OracleSystemStack()
+        o.SetStateColumnar(small)
+        o.SetJob(job)
+        o.SetNodes(np.arange(ns, dtype=np.uint32))
+        t0 = time.perf_counter()
+        o.SystemPlace(0)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port",
+                               "sample": "system placements over a %d-node C4 cluster in %.2f s" % (ns, dt)}
+    return out
+
+
+def section_c5(device, cpu_s):
+    """C5: count=1000 service job asking 2 x nvidia/gpu with memory >= 40 GiB on
+    50k nodes, 99 % of the GPU nodes fully held by priority-20 allocs, service
+    preemption enabled: after the free GPUs are used, every placement retries
+    with Preempt=true (selectNextOption) and evicts."""
+    from nomad_amd import synth
+    from nomad_amd.stack import GenericStack
+    from nomad_amd.structs import SchedulerConfig
+    nodes, allocs = synth.cluster_c5(50000, seed=5, busy=0.99)
+    job = synth.job_c5(1000)
+    perm = synth.shuffle(len(nodes), 77)
+    cfg = SchedulerConfig(preempt_service=True)
+    st = GenericStack(device=device, config=cfg)
+    st.SetState(nodes, allocs)
+    times = []
+    res = None
+    for i in range(3):
+        st.ResetPlan()
+        st.SetJob(job)
+        st.SetNodes(perm)
+        t0 = time.perf_counter()
+        res = st.Place(0, 1000)
+        times.append(time.perf_counter() - t0)
+    st.close()
+    wall = float(np.median(times[1:]))
+    placed = sum(1 for r in res if r.row >= 0)
+    pre = sum(1 for r in res if r.preempted)
+    out = {"workload": "C5: 2 x nvidia/gpu (memory >= 40 GiB, h100 affinity) count=1000 on 50000 nodes, "
+                       "preemption enabled, 99 % of GPU nodes busy", "placements": placed,
+           "preempting_placements": pre, "placements_per_s": placed / wall, "wall_ms": wall * 1e3}
+    if cpu_s > 0:
+        from oracle.oracle import OracleGenericStack
+
+        def mk(ns, al):
+            o = OracleGenericStack(config=cfg)
+            o.SetState(ns, al)
+            o.SetJob(job)
+            o.SetNodes(perm)
+            return o
+        # free-GPU regime: the evaluation's first placements
+        o = mk(nodes, allocs)
+        t0 = time.perf_counter()
+        k_free = o.PlaceArrays(0, 128)[2]
+        dt_free = time.perf_counter() - t0
+        # eviction regime: every GPU node held, so each placement fails its plain
+        # Select and evicts (a bounded sample of 3 placements)
+        bnodes, ballocs = synth.cluster_c5(50000, seed=5, busy=1.0)
+        o = mk(bnodes, ballocs)
+        t0 = time.perf_counter()
+        k_pre = o.PlaceArrays(0, 3)[2]
+        dt_pre = time.perf_counter() - t0
+        est = (placed - pre) * dt_free / max(1, k_free) + pre * dt_pre / max(1, k_pre)
+        out["cpu_baseline"] = {"value": placed / est if est > 0 else 0.0, "unit": "placements/s", "cores": 1,
+                               "kind": "port",
+                               "sample": "%d free-GPU placements in %.2f s and %d evicting placements (all GPU "
+                                         "nodes busy) in %.2f s, weighted by this run's %d / %d split"
+                                         % (k_free, dt_free, k_pre, dt_pre, placed - pre, pre)}
+    return out
+
+
+def section_c3_sharded(device, rank, world, pg, placements=64):
+    """Full-pass Selects of a C3 job over a 100k-node cluster split across the
+    ranks: per placement each GPU sweeps its rows, the 80-byte records are
+    all-gathered (RCCL over xGMI), every rank resolves and commits the winner."""
+    from nomad_amd import shard, synth, synth_columnar
+    from nomad_amd.stack import GenericStack
+    n = 100000
+    cs = synth_columnar.ColumnarState(n, seed=7, kind="c3")
+    job = synth.job_c3(placements)
+    perm = np.random.Generator(np.random.PCG64(3)).permutation(n).astype(np.uint32)
+    st = GenericStack(device=device)
+    st.SetStateColumnar(cs)
+    gdev = None
+    if world > 1:
+        import torch
+        gdev = torch.device("cuda", device) if torch.cuda.is_available() else None
+    walls, xs = [], []
+    for i in range(2):
+        st.ResetPlan()
+        st.SetJob(job)
+        st.SetNodes(perm)
+        sf = shard.ShardedFullScan(st, n, pg if world > 1 else None, gdev)
+        barrier(pg)
+        t0 = time.perf_counter()
+        ex = 0.0
+        res = []
+        for _ in range(placements):
+            r = sf.Select(0)
+            ex += sf.last_exchange_us
+            res.append(r)
+            if r.row < 0:
+                break
+            st.Commit(0, r.row)
+        dt = time.perf_counter() - t0
+        barrier(pg)
+        walls.append(reduce(pg, dt, lambda d: d.ReduceOp.MAX))
+        xs.append(ex / max(1, len(res)))
+    st.close()
+    placed = sum(1 for r in res if r.row >= 0)
+    wall = walls[-1]
+    return {"workload": "C3 job on %d nodes, full-pass Selects sharded over %d GPUs, %d placements"
+                        % (n, world, placements), "scaling": "strong", "placements": placed,
+            "placements_per_s": placed / wall, "ms_per_placement": wall / max(1, placed) * 1e3,
+            "node_evals_per_s": placed * n / wall,
+            "exchange_us_per_placement": xs[-1] if world > 1 else 0.0,
+            "exchange": "torch.distributed all_gather of 80 B per rank (RCCL)" if world > 1 else "none"}
+
+
 def main():
     args = parse()
     rank, world, local, pg = dist_init()
@@ -271,6 +501,20 @@ def main():
             one, multi = cpu_baseline(nodes, allocs, job, args.cpu_seconds)
             line["cpu_baseline"] = one
             line["cpu_baseline_multicore"] = multi
+    sections = [x for x in args.sections.split(",") if x]
+    cpu_s = 0.0 if args.no_cpu else 8.0
+    extra = {}
+    for sec in sections:
+        if sec in ("c3", "c5"):
+            if rank == 0:
+                extra[sec] = section_c3(local, cpu_s) if sec == "c3" else section_c5(local, cpu_s)
+            barrier(pg)
+        elif sec == "c4":
+            extra[sec] = section_c4(local, rank, world, pg, cpu_s)
+        elif sec == "c3_sharded":
+            extra[sec] = section_c3_sharded(local, rank, world, pg)
+    if rank == 0:
+        line["configs"] = extra
         print(json.dumps(line))
     st.close()
     lat.close()

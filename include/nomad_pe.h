@@ -307,6 +307,20 @@ void pe_last_phase_ms(const pe_stack* s, double* out4);
  * out_status[n] = 0 placed, 1 filtered, 2 exhausted. Commits placed allocs. */
 int pe_system_place(pe_stack* s, uint32_t tg_index, double* out_score,
                     uint8_t* out_status, uint32_t* placed);
+/* Full-scan Select sharded over GPUs (one process per GPU, each holding the
+ * same snapshot, job, SetNodes list and plan). Each rank sweeps
+ * the snapshot rows [row_begin, row_end) it owns into a pe_shard_rec: the
+ * LimitIterator/MaxScoreIterator state of its rows (max score and its earliest
+ * visit ranks, the first three non-positive options, option / filter / exhaust
+ * counts), which merges associatively. After one all-gather of the records,
+ * every rank calls pe_select_merge with all of them and gets the same Select
+ * result (stack.go:117-179 with limit MaxInt32; a full pass leaves the cursor
+ * unchanged), then commits it with pe_commit. Needs a full pass (affinities or
+ * spreads), a visit list without repeated rows and no distinct_property. */
+typedef struct pe_shard_rec { uint8_t bytes[80]; } pe_shard_rec;
+int pe_select_shard(pe_stack* s, uint32_t tg_index, uint32_t row_begin, uint32_t row_end, pe_shard_rec* out);
+int pe_select_merge(pe_stack* s, uint32_t tg_index, const pe_shard_rec* recs, uint32_t n_recs,
+                    pe_ranked_node* out);
 /* Milliseconds spent in device kernels by the last pe_place / pe_system_place
  * (HIP events on the engine's stream). */
 double pe_last_kernel_ms(const pe_stack* s);

@@ -162,6 +162,10 @@ class pe_ranked_node(C.Structure):
                 ("n_device_offers", C.c_uint32), ("device_offer_group", C.c_uint32 * PE_MAX_DEVICE_REQ)]
 
 
+class pe_shard_rec(C.Structure):
+    _fields_ = [("bytes", C.c_uint8 * 80)]
+
+
 class pe_placement(C.Structure):
     _fields_ = [("row", C.c_int32), ("nodes_evaluated", C.c_uint32), ("final_score", C.c_double)]
 
@@ -188,7 +192,7 @@ ENGINE_SYMBOLS = [
     "pe_abi_version", "pe_stack_create", "pe_stack_destroy", "pe_last_error", "pe_set_state",
     "pe_reset_plan", "pe_set_job", "pe_set_nodes", "pe_select", "pe_commit", "pe_commit_preempt", "pe_place", "pe_system_place",
     "pe_last_kernel_ms", "pe_stage_orders", "pe_place_batch", "pe_batch_results", "pe_last_phase_ms",
-    "pe_check_constraint", "pe_last_sweep_bytes",
+    "pe_check_constraint", "pe_last_sweep_bytes", "pe_select_shard", "pe_select_merge",
 ]
 
 

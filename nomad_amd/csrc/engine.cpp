@@ -44,6 +44,7 @@ hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ran
 hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
                                     uint32_t* pcount, uint32_t* dev_free, hipStream_t st);
 hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st);
+hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, hipStream_t st);
 hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
                                     uint32_t* dev_free, uint32_t* placed, hipStream_t st);
 hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
@@ -52,6 +53,8 @@ hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec
 hipError_t pe_launch_node_record(const pe::SweepArgs* a, uint32_t row, pe_ranked_node* out, hipStream_t st);
 hipError_t pe_launch_spread_table(const pe::TgTables* t, double* tab, hipStream_t st);
 uint32_t pe_rec_winner(const pe::SweepRec* r);
+void pe_rec_init(pe::SweepRec* r);
+void pe_rec_merge(pe::SweepRec* a, const pe::SweepRec* b);
 int pe_sweep_blocks_per_cu(bool aux);
 hipError_t pe_launch_fold_aux(const pe::NodeSoA* s, const pe::TgTables* t, const uint8_t* aff_idx_class,
                               const uint8_t* aff_idx_node, uint32_t* aux, hipStream_t st);
@@ -1458,9 +1461,12 @@ bool full_scan_kernel(pe_stack* s, TgPlan& g, uint32_t n) {
 
 // Full-scan Select (limit >= n) as a multi-CU sweep: every workgroup reduces
 // its rows to a SweepRec, one merge yields the winner.
-int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_ranked_node* out) {
+// The sweep over snapshot rows [row_begin, row_end) (one GPU's shard, or all
+// rows): per-workgroup SweepRec records merged into *rec.
+int sweep_partial(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_t row_begin, uint32_t row_end,
+                  pe::SweepArgs* args, pe::SweepRec* rec) {
     const uint32_t n = (uint32_t)s->visit.size();
-    pe::SweepArgs A;
+    pe::SweepArgs& A = *args;
     std::memset(&A, 0, sizeof(A));
     A.soa = soa_of(s);
     A.tg = tables_of(g);
@@ -1468,8 +1474,8 @@ int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_r
     A.rank_of = s->d_rank_of.as<uint32_t>();
     A.n_visit = n;
     A.offset = s->offset;
-    A.row_begin = 0;
-    A.row_end = (uint32_t)s->nodes.size();
+    A.row_begin = row_begin;
+    A.row_end = row_end;
     A.log10 = s->log10;
     if (opts && opts->penalty_count > 0) {
         std::vector<uint32_t> bits((s->nodes.size() + 31) / 32, 0);
@@ -1506,16 +1512,27 @@ int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_r
     HIP_TRY(s, s->d_sweep_merged.ensure(sizeof(pe::SweepRec)));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
     A.recs = s->d_sweep_recs.as<pe::SweepRec>();
+    if (row_end <= row_begin) {   // an empty shard contributes the identity record
+        pe_rec_init(rec);
+        s->last_ms = s->last_sweep_ms = 0;
+        return PE_OK;
+    }
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     HIP_TRY(s, pe_launch_sweep(&A, blocks, s->d_sweep_merged.as<pe::SweepRec>(), s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
-    pe::SweepRec rec;
-    HIP_TRY(s, hipMemcpyAsync(&rec, s->d_sweep_merged.p, sizeof(rec), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(rec, s->d_sweep_merged.p, sizeof(*rec), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
     s->last_sweep_ms = ms;
+    return PE_OK;
+}
+
+// Resolve a merged record into the Select result (winner record from the
+// resident snapshot; a full pass leaves the cursor unchanged).
+int sweep_finish(pe_stack* s, pe::SweepArgs& A, const pe::SweepRec& rec, pe_ranked_node* out) {
+    const uint32_t n = (uint32_t)s->visit.size();
     std::memset(out, 0, sizeof(*out));
     const uint32_t rank = pe_rec_winner(&rec);
     out->row = -1;
@@ -1538,6 +1555,28 @@ int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_r
         out->n_device_offers = rr.n_device_offers;
         std::memcpy(out->device_offer_group, rr.device_offer_group, sizeof(out->device_offer_group));
     }
+    return PE_OK;
+}
+
+int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_ranked_node* out) {
+    pe::SweepArgs A;
+    pe::SweepRec rec;
+    int rc = sweep_partial(s, g, opts, 0, (uint32_t)s->nodes.size(), &A, &rec);
+    if (rc) return rc;
+    return sweep_finish(s, A, rec, out);
+}
+
+// Options / filtered / exhausted over the current visit list (k_census).
+int census(pe_stack* s, TgPlan& g, uint32_t* cnt) {
+    pe::BatchArgs A = batch_args(s, g);
+    HIP_TRY(s, upload(s->d_visit, s->visit));
+    A.perms = s->d_visit.as<uint32_t>();
+    A.n_visit = (uint32_t)s->visit.size();
+    HIP_TRY(s, s->d_ev_out.ensure(16));
+    HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
+    HIP_TRY(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->stream));
+    HIP_TRY(s, hipMemcpyAsync(cnt, s->d_ev_out.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
     return PE_OK;
 }
 
@@ -2136,6 +2175,63 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
     return PE_OK;
 }
 
+// Common checks of the sharded full-pass Select (pe_select_shard / pe_select_merge).
+static int shard_prepare(pe_stack* s, uint32_t tgi, TgPlan** gp) {
+    if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "sharded Select needs a generic stack");
+    int rc = prepare_tg(s, tgi, s->visit, s->offset);
+    if (rc) return rc;
+    TgPlan& g = *s->tgs[tgi];
+    if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;
+    if (s->limit < s->visit.size())
+        return s->fail(PE_EUNSUPPORTED, "sharded Select needs a full pass (affinities or spreads: limit MaxInt32)");
+    if (!s->visit_unique) return s->fail(PE_EUNSUPPORTED, "sharded Select needs a visit list without repeated rows");
+    if (g.n_spread != (int)g.psets.size()) return s->fail(PE_EUNSUPPORTED, "sharded Select with distinct_property");
+    *gp = &g;
+    return PE_OK;
+}
+
+int pe_select_shard(pe_stack* s, uint32_t tgi, uint32_t row_begin, uint32_t row_end, pe_shard_rec* out) {
+    if (!s || !out) return PE_EINVAL;
+    if (row_begin > row_end || row_end > s->nodes.size()) return s->fail(PE_EINVAL, "bad shard row range");
+    s->gen++;
+    HIP_TRY(s, hipSetDevice(s->device));
+    TgPlan* g = nullptr;
+    int rc = shard_prepare(s, tgi, &g);
+    if (rc) return rc;
+    pe::SweepArgs A;
+    pe::SweepRec rec;
+    rc = sweep_partial(s, *g, nullptr, row_begin, row_end, &A, &rec);
+    if (rc) return rc;
+    std::memset(out, 0, sizeof(*out));
+    std::memcpy(out->bytes, &rec, sizeof(rec));
+    return PE_OK;
+}
+
+int pe_select_merge(pe_stack* s, uint32_t tgi, const pe_shard_rec* recs, uint32_t n_recs, pe_ranked_node* out) {
+    if (!s || !out || (!recs && n_recs)) return PE_EINVAL;
+    s->gen++;
+    HIP_TRY(s, hipSetDevice(s->device));
+    TgPlan* g = nullptr;
+    int rc = shard_prepare(s, tgi, &g);
+    if (rc) return rc;
+    pe::SweepRec all;
+    pe_rec_init(&all);
+    for (uint32_t i = 0; i < n_recs; i++) {
+        pe::SweepRec r;
+        std::memcpy(&r, recs[i].bytes, sizeof(r));
+        pe_rec_merge(&all, &r);
+    }
+    pe::SweepArgs A;
+    pe::SweepRec none;
+    rc = sweep_partial(s, *g, nullptr, 0, 0, &A, &none);   // tables for the winner's record
+    if (rc) return rc;
+    rc = sweep_finish(s, A, all, out);
+    if (rc) return rc;
+    s->offer_row = out->row;
+    s->offers = pack_offers(out);
+    return PE_OK;
+}
+
 int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
     if (!s) return PE_EINVAL;
     if (n_preempted == 0) return pe_commit(s, tgi, row);
@@ -2190,6 +2286,16 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
             if (rc) return rc;
             p++;
             if (p == count) break;
+            // a saturated cluster stays saturated: when the census finds no
+            // option the plain Select is nil (every node pulled, cursor kept)
+            // and the next placement goes straight to the eviction pass
+            if (!g.psets.empty()) { /* spread / distinct counts: take the count loop */ }
+            else {
+                uint32_t cnt[3];
+                rc = census(s, g, cnt);
+                if (rc) return rc;
+                if (cnt[0] == 0) continue;
+            }
             uint32_t p2 = 0;
             rc = run_place(s, tgi, count - p, 1, s->visit, s->offset, nullptr, out + p, &p2, &no);
             if (rc) return rc;

@@ -133,6 +133,8 @@ struct SweepRec {
     double np_score[kMaxSkip];
 };
 
+static_assert(sizeof(SweepRec) == sizeof(pe_shard_rec), "pe_shard_rec carries one SweepRec");
+
 struct SweepArgs {
     NodeSoA soa;
     TgTables tg;

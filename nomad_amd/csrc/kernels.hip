@@ -1445,6 +1445,27 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(A.placed, local);
 }
 
+// Outcome census of one Select pass over the visit list on the HBM state
+// (no overlay): counts[0] options, [1] filtered, [2] exhausted. With no option
+// the Select is nil after pulling every node, which the count loop's
+// preemption retry uses instead of a windowed scan of the whole list.
+__global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t c[3] = {0, 0, 0};
+    Overlay none;
+    none.keys = nullptr;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < A.n_visit; j += stride) {
+        NodeEval ev;
+        eval_node<false>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, nullptr, A.perms[j], &ev);
+        c[ev.status]++;
+    }
+    for (int k = 0; k < 3; k++) {
+        uint32_t x = c[k];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&counts[k], x);
+    }
+}
+
 // Host-driven Plan.AppendAlloc on the HBM SoA (pe_commit). `offers`: the
 // device offers of the Select that chose the node (one byte per request), or
 // ~0u to assign them on the current state.
@@ -1899,6 +1920,14 @@ hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs*
     return hipGetLastError();
 }
 
+hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, hipStream_t st) {
+    uint32_t blocks = (a->n_visit + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_census, dim3(blocks), dim3(256), 0, st, *a, counts);
+    return hipGetLastError();
+}
+
 hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st) {
     uint32_t blocks = (a->n_visit + 255) / 256;
     if (blocks > 2048) blocks = 2048;
@@ -1986,6 +2015,8 @@ hipError_t pe_launch_node_record(const pe::SweepArgs* a, uint32_t row, pe_ranked
 }
 
 uint32_t pe_rec_winner(const pe::SweepRec* r) { return pe::rec_winner(*r); }
+void pe_rec_init(pe::SweepRec* r) { pe::rec_init(*r); }
+void pe_rec_merge(pe::SweepRec* a, const pe::SweepRec* b) { pe::rec_merge(*a, *b); }
 
 hipError_t pe_launch_spread_table(const pe::TgTables* t, double* tab, hipStream_t st) {
     hipLaunchKernelGGL(pe::k_spread_table, dim3(1), dim3(256), 0, st, *t, tab);

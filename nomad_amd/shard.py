@@ -1,0 +1,92 @@
+"""Multi-GPU sharding of the placement path, one process per GPU.
+
+Every rank holds the same snapshot, job, SetNodes list and plan (replicated
+state, ~64 B per node in HBM); what is split is the work:
+
+* SystemScheduler (scheduler_system.go:283-425): each node's single-node Select
+  is independent, so the SetNodes list is cut into contiguous ranges, one per
+  rank, with no data-path collective (`system_place_sharded`).
+* Full-pass Selects (affinities / spreads, limit MaxInt32): each rank sweeps the
+  snapshot rows it owns into an 80-byte record of the LimitIterator +
+  MaxScoreIterator state (pe_select_shard); one all-gather of the records per
+  placement, then every rank resolves the same winner (pe_select_merge) and
+  applies the same commit (`ShardedFullScan`). The all-gather is the one
+  exchange step of the path and is latency-bound; `last_exchange_us` reports it.
+* Windowed binpack (limit = ceil(log2 n)) does not shard: ranks run replicas.
+
+The collective is torch.distributed's all_gather: RCCL over xGMI on GPU tensors
+(backend "nccl"), gloo on CPU tensors for the multi-process CPU tests.
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+REC_BYTES = 80   # sizeof(pe_shard_rec)
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [begin, end) of n items owned by `rank`."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def all_gather_bytes(dist, payload: bytes, device=None) -> List[bytes]:
+    """All-gather one fixed-size byte record per rank (rank order)."""
+    import torch
+    t = torch.tensor(np.frombuffer(payload, dtype=np.uint8).copy())
+    if device is not None:
+        t = t.to(device)
+    outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, t)
+    return [bytes(o.cpu().numpy().tobytes()) for o in outs]
+
+
+class ShardedFullScan:
+    """Full-pass Selects of one evaluation split over the ranks of `dist`.
+
+    `stack` is a GenericStack (or any object with SelectShard / SelectMerge /
+    Commit) on which SetState, SetJob and SetNodes were called identically on
+    every rank. With dist None (or world 1) it degenerates to local Selects."""
+
+    def __init__(self, stack, n_rows: int, dist=None, device=None):
+        self.stack = stack
+        self.dist = dist
+        self.rank = dist.get_rank() if dist is not None else 0
+        self.world = dist.get_world_size() if dist is not None else 1
+        self.device = device
+        self.rows = shard_range(n_rows, self.rank, self.world)
+        self.last_exchange_us = 0.0
+
+    def Select(self, tg):
+        rec = self.stack.SelectShard(tg, *self.rows)
+        if self.world > 1:
+            t0 = time.perf_counter()
+            recs = all_gather_bytes(self.dist, rec, self.device)
+            self.last_exchange_us = (time.perf_counter() - t0) * 1e6
+        else:
+            recs = [rec]
+        return self.stack.SelectMerge(tg, recs)
+
+    def Place(self, tg, count: int):
+        """The count loop (generic_sched.go:493-649): Select, then the same
+        Plan.AppendAlloc on every rank; stops at the first nil Select."""
+        out = []
+        for _ in range(count):
+            r = self.Select(tg)
+            out.append(r)
+            if r.row < 0:
+                break
+            self.stack.Commit(tg, r.row)
+        return out
+
+
+def system_place_sharded(stack, rows: Sequence[int], rank: int, world: int, tg=0):
+    """SystemScheduler placements over this rank's range of the SetNodes list.
+    Returns (begin, end, scores, statuses, placed) for the range."""
+    rows = np.asarray(rows, dtype=np.uint32)
+    b, e = shard_range(len(rows), rank, world)
+    stack.SetNodes(rows[b:e])
+    score, status, placed = stack.SystemPlace(tg)
+    return b, e, score, status, placed

@@ -61,6 +61,12 @@ def load_engine():
                                          C.POINTER(abi.u32p), abi.u32p, abi.u32p]
         lib.pe_last_phase_ms.restype = None
         lib.pe_last_phase_ms.argtypes = [C.c_void_p, abi.f64p]
+        lib.pe_select_shard.restype = C.c_int
+        lib.pe_select_shard.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                        C.POINTER(abi.pe_shard_rec)]
+        lib.pe_select_merge.restype = C.c_int
+        lib.pe_select_merge.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(abi.pe_shard_rec), C.c_uint32,
+                                        C.POINTER(abi.pe_ranked_node)]
         _engine = lib
     return _engine
 
@@ -304,6 +310,22 @@ class GenericStack(_Stack):
             out = out.copy()
             placed = placed.copy()
         return out["row"], out["final_score"], out["nodes_evaluated"], placed
+
+    def SelectShard(self, tg, row_begin: int, row_end: int) -> bytes:
+        """This GPU's part of a full-pass Select: the 80-byte record of snapshot
+        rows [row_begin, row_end) (pe_select_shard)."""
+        rec = abi.pe_shard_rec()
+        self._check(self._lib.pe_select_shard(self._h, self._tg_index(tg), row_begin, row_end, C.byref(rec)))
+        return bytes(rec.bytes)
+
+    def SelectMerge(self, tg, recs) -> RankedNode:
+        """Resolve the Select from every shard's record (pe_select_merge)."""
+        arr = (abi.pe_shard_rec * max(1, len(recs)))()
+        for i, r in enumerate(recs):
+            C.memmove(arr[i].bytes, bytes(r), 80)
+        out = abi.pe_ranked_node()
+        self._check(self._lib.pe_select_merge(self._h, self._tg_index(tg), arr, len(recs), C.byref(out)))
+        return RankedNode.from_c(out, self.nodes)
 
     def last_phase_ms(self):
         """[host prep, kernel, D2H copy, total] of the last PlaceBatch, ms."""

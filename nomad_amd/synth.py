@@ -207,9 +207,11 @@ def nvidia_node(node_id: str, model: str = "1080ti", healthy: int = 2) -> Node:
     return nd
 
 
-def cluster_c5(n: int = 50000, seed: int = 5):
+def cluster_c5(n: int = 50000, seed: int = 5, busy: float = 0.0):
     """60 % of the nodes carry one nvidia/gpu group (a100 / h100 / 1080ti, 4 or 8
-    healthy instances); priority-20 background allocs hold 0..all instances."""
+    healthy instances); priority-20 background allocs hold 0..all instances
+    (all of them on a `busy` fraction of the GPU nodes, so that a count=1000
+    ask must preempt)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     ids = sorted(uuids(n, seed))
     models = ["a100", "h100", "1080ti"]
@@ -224,6 +226,8 @@ def cluster_c5(n: int = 50000, seed: int = 5):
             model = models[int(rng.integers(0, 3))]
             nd.devices = [DeviceGroup("nvidia", "gpu", model, inst, dict(GPU_MODELS[model]))]
             held = int(rng.integers(0, inst + 1))
+            if busy > 0.0 and rng.random() < busy:
+                held = inst
             j = 0
             while held > 0:
                 take = min(held, int(rng.integers(1, 5)))

@@ -139,12 +139,25 @@ struct OJob {
 
 // ---------------------------------------------------------------------------
 // AllocMetric (structs.go:9826-10026) — counters only
+// Per-row outcome trace of one Select (oracle_full_pass): 1 filtered,
+// 2 exhausted, 0 option with its FinalScore.
+static thread_local uint8_t* g_trace_status = nullptr;
+static thread_local double* g_trace_score = nullptr;
+
 struct Metrics {
     uint32_t evaluated = 0, filtered = 0, exhausted = 0;
     std::map<std::string, int> constraint_filtered, dimension_exhausted;
     void EvaluateNode() { evaluated++; }
-    void FilterNode(const ONode*, const std::string& c) { filtered++; if (!c.empty()) constraint_filtered[c]++; }
-    void ExhaustedNode(const ONode*, const std::string& d) { exhausted++; if (!d.empty()) dimension_exhausted[d]++; }
+    void FilterNode(const ONode* n, const std::string& c) {
+        filtered++;
+        if (!c.empty()) constraint_filtered[c]++;
+        if (g_trace_status && n) g_trace_status[n->row] = 1;
+    }
+    void ExhaustedNode(const ONode* n, const std::string& d) {
+        exhausted++;
+        if (!d.empty()) dimension_exhausted[d]++;
+        if (g_trace_status && n) g_trace_status[n->row] = 2;
+    }
 };
 
 enum ClassFeas { kUnknown = 0, kIneligible = 1, kEligible = 2, kEscaped = 3 };
@@ -1426,6 +1439,7 @@ struct ScoreNormalizationIterator : RankIterator {
         double sum = 0.0;
         for (double s : o->scores) sum += s;
         o->final_score = sum / (double)o->scores.size();
+        if (g_trace_status) { g_trace_status[o->node->row] = 0; g_trace_score[o->node->row] = o->final_score; }
         return o;
     }
     void Reset() override { source->Reset(); }
@@ -1932,6 +1946,23 @@ int oracle_system_place(oracle_stack* s, uint32_t tgi, double* out_score, uint8_
     s->source.SetNodes(all);
     if (placed) *placed = p;
     return PE_OK;
+}
+
+// One Select of task group `tgi` with every visited row's outcome traced:
+// status_by_row[row] = 0 option (score_by_row = FinalScore), 1 filtered,
+// 2 exhausted, 255 not visited. Test hook for the sharded full-pass protocol.
+int oracle_full_pass(oracle_stack* s, uint32_t tgi, uint8_t* status_by_row, double* score_by_row,
+                     pe_ranked_node* out) {
+    const size_t n = s->state.nodes.size();
+    for (size_t i = 0; i < n; i++) { status_by_row[i] = 255; score_by_row[i] = 0.0; }
+    g_trace_status = status_by_row;
+    g_trace_score = score_by_row;
+    pe_select_options opts;
+    std::memset(&opts, 0, sizeof(opts));
+    const int rc = oracle_select(s, tgi, &opts, out);
+    g_trace_status = nullptr;
+    g_trace_score = nullptr;
+    return rc;
 }
 
 double oracle_go_pow(double x, double y) { return gomath::pow(x, y); }

@@ -31,6 +31,12 @@ int oracle_place(oracle_stack* s, uint32_t tg_index, uint32_t count, pe_ranked_n
 int oracle_system_place(oracle_stack* s, uint32_t tg_index, double* out_score,
                         uint8_t* out_status, uint32_t* placed);
 
+/* One Select with each visited row's outcome traced (0 option + FinalScore,
+ * 1 filtered, 2 exhausted, 255 not visited): test hook of the sharded
+ * full-pass protocol. */
+int oracle_full_pass(oracle_stack* s, uint32_t tg_index, uint8_t* status_by_row, double* score_by_row,
+                     pe_ranked_node* out);
+
 /* Known-answer-test helpers (scalar restatements). */
 double oracle_go_pow(double x, double y);
 double oracle_go_exp(double x);

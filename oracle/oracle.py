@@ -37,6 +37,8 @@ def load():
             build()
         lib = C.CDLL(LIB)
         abi.bind(lib, "oracle_", "oracle_create", "oracle_destroy", "oracle_last_error")
+        lib.oracle_full_pass.restype = C.c_int
+        lib.oracle_full_pass.argtypes = [C.c_void_p, C.c_uint32, abi.u8p, abi.f64p, C.POINTER(abi.pe_ranked_node)]
         lib.oracle_go_pow.restype = C.c_double
         lib.oracle_go_pow.argtypes = [C.c_double, C.c_double]
         lib.oracle_go_exp.restype = C.c_double

@@ -1,0 +1,148 @@
+"""Multi-process sharding on CPU ranks over gloo, world size 2.
+
+The product path runs one process per GPU over RCCL; here the same driver code
+(nomad_amd/shard.py) runs on CPU processes with the oracle standing in for the
+per-shard device work (the oracle is test infrastructure): system placements
+over contiguous list ranges, and full-pass Selects whose 80-byte records are
+all-gathered and merged every placement. Both must equal one process running
+the whole evaluation. The GPU test checks the engine's own shard records.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from nomad_amd import shard, synth
+from nomad_amd.structs import SchedulerConfig
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _system_worker(rank, world, port, q):
+    from oracle.oracle import OracleSystemStack
+    _init(rank, world, port)
+    nodes, allocs = synth.cluster_c4(1200, seed=11)
+    job = synth.mock_system_job()
+    rows = synth.shuffle(len(nodes), 3)
+    st = OracleSystemStack()
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    b, e, score, status, placed = shard.system_place_sharded(st, rows, rank, world)
+    got = [None] * world
+    dist.all_gather_object(got, (b, e, score.tolist(), status.tolist(), placed))
+    if rank == 0:
+        q.put(got)
+    dist.destroy_process_group()
+
+
+def _fullscan_worker(rank, world, port, q):
+    from oracle.shard_rec import OracleShardStack
+    _init(rank, world, port)
+    nodes, allocs = synth.cluster_c3(900, seed=21)
+    job = synth.job_c3(60)
+    perm = synth.shuffle(len(nodes), 4)
+    st = OracleShardStack()
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(list(perm))
+    sf = shard.ShardedFullScan(st, len(nodes), dist)
+    res = sf.Place(0, 60)
+    if rank == 0:
+        q.put([(r.row, r.final_score, r.nodes_filtered, r.nodes_exhausted) for r in res])
+    dist.destroy_process_group()
+
+
+def _run(worker, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 100000):
+        for w in (1, 2, 3, 8):
+            spans = [shard.shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def test_system_sharded_gloo_matches_single_process():
+    from oracle.oracle import OracleSystemStack
+    got = _run(_system_worker)
+    nodes, allocs = synth.cluster_c4(1200, seed=11)
+    job = synth.mock_system_job()
+    rows = synth.shuffle(len(nodes), 3)
+    st = OracleSystemStack()
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(list(rows))
+    score, status, placed = st.SystemPlace(0)
+    cat_status = np.concatenate([np.asarray(g[3], dtype=np.uint8) for g in got])
+    cat_score = np.concatenate([np.asarray(g[2]) for g in got])
+    assert sum(g[4] for g in got) == placed
+    assert np.array_equal(cat_status, status)
+    m = status == 0
+    assert np.array_equal(cat_score[m], score[m])
+
+
+def test_full_scan_sharded_gloo_matches_single_process():
+    from oracle.oracle import OracleGenericStack
+    got = _run(_fullscan_worker)
+    nodes, allocs = synth.cluster_c3(900, seed=21)
+    job = synth.job_c3(60)
+    perm = synth.shuffle(len(nodes), 4)
+    st = OracleGenericStack()
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(list(perm))
+    ref = st.Place(0, 60)
+    assert [(r.row, r.final_score, r.nodes_filtered, r.nodes_exhausted) for r in ref] == [tuple(x) for x in got]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [1, 2, 3, 8])
+def test_engine_shard_records_match_select(shards):
+    """pe_select_shard over disjoint row ranges + pe_select_merge == pe_select,
+    placement after placement (single process, shards as row ranges)."""
+    from nomad_amd.stack import GenericStack
+    nodes, allocs = synth.cluster_c3(5000, seed=22)
+    job = synth.job_c3(40)
+    perm = synth.shuffle(len(nodes), 8)
+    a, b = GenericStack(), GenericStack()
+    for st in (a, b):
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(list(perm))
+    for _ in range(40):
+        recs = [a.SelectShard(0, *shard.shard_range(len(nodes), r, shards)) for r in range(shards)]
+        x = a.SelectMerge(0, recs)
+        y = b.SelectRaw(0)
+        assert (x.row, x.final_score, x.scores, x.nodes_filtered, x.nodes_exhausted, x.new_offset) == \
+               (y.row, y.final_score, y.scores, y.nodes_filtered, y.nodes_exhausted, y.new_offset)
+        if x.row < 0:
+            break
+        a.Commit(0, x.row)
+        b.Commit(0, y.row)
