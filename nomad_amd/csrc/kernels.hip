@@ -383,6 +383,7 @@ struct LoopShared {
     double aside_score[kMaxSkip];   // LimitIterator skip list
     int aside_pos[kMaxSkip];
     int stop_j;
+    SweepRec red_rec[BLOCK / 64];   // full-pass mode: per-wave records
 };
 
 template <int BLOCK>
@@ -528,6 +529,112 @@ __device__ __forceinline__ void emit_placement(const BatchArgs& A, const uint8_t
     }
 }
 
+// ---- full-pass reduction records (LimitIterator with limit >= options) -------
+__host__ __device__ __forceinline__ void rec_init(SweepRec& r) {
+    r.max_score = -__builtin_inff();
+    for (int i = 0; i < 4; i++) r.max_rank[i] = 0xFFFFFFFFu;
+    for (int i = 0; i < kMaxSkip; i++) { r.np_rank[i] = 0xFFFFFFFFu; r.np_score[i] = 0.0; }
+    r.options = r.filtered = r.exhausted = r._pad = 0;
+}
+
+// insert x into a sorted list of N ranks (keeps the N smallest); branch-free on indices
+template <int N>
+__host__ __device__ __forceinline__ void ins_rank(uint32_t (&l)[N], uint32_t x) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t lo = l[i] < x ? l[i] : x, hi = l[i] < x ? x : l[i];
+        l[i] = lo;
+        x = hi;
+    }
+}
+
+__host__ __device__ __forceinline__ void ins_np(uint32_t (&rk)[kMaxSkip], double (&sc)[kMaxSkip], uint32_t x, double s) {
+#pragma unroll
+    for (int i = 0; i < kMaxSkip; i++) {
+        if (x < rk[i]) {
+            const uint32_t tr = rk[i]; const double ts = sc[i];
+            rk[i] = x; sc[i] = s;
+            x = tr; s = ts;
+        }
+    }
+}
+
+__device__ __forceinline__ void rec_add(SweepRec& r, uint32_t rank, double score) {
+    r.options++;
+    if (score > r.max_score) {
+        r.max_score = score;
+        r.max_rank[0] = rank;
+        r.max_rank[1] = r.max_rank[2] = r.max_rank[3] = 0xFFFFFFFFu;
+    } else if (score == r.max_score) {
+        ins_rank<4>(r.max_rank, rank);
+    }
+    if (score <= 0.0) ins_np(r.np_rank, r.np_score, rank, score);
+}
+
+__host__ __device__ __forceinline__ void rec_merge(SweepRec& a, const SweepRec& b) {
+    if (b.max_score > a.max_score) {
+        a.max_score = b.max_score;
+        for (int i = 0; i < 4; i++) a.max_rank[i] = b.max_rank[i];
+    } else if (b.max_score == a.max_score) {
+        for (int i = 0; i < 4; i++) ins_rank<4>(a.max_rank, b.max_rank[i]);
+    }
+    for (int i = 0; i < kMaxSkip; i++) ins_np(a.np_rank, a.np_score, b.np_rank[i], b.np_score[i]);
+    a.options += b.options;
+    a.filtered += b.filtered;
+    a.exhausted += b.exhausted;
+}
+
+// Winner rank of a merged record (SURVEY.md Appendix A1), ~0u = no option.
+__device__ __host__ __forceinline__ uint32_t rec_winner(const SweepRec& r) {
+    if (r.options == 0) return 0xFFFFFFFFu;
+    if (r.max_score > 0.0) return r.max_rank[0];
+    for (int i = 0; i < 4; i++) {
+        const uint32_t x = r.max_rank[i];
+        if (x == 0xFFFFFFFFu) break;
+        bool demoted = false;
+        for (int k = 0; k < kMaxSkip; k++) demoted = demoted || r.np_rank[k] == x;
+        if (!demoted) return x;
+    }
+    return r.max_rank[0];
+}
+
+__device__ __forceinline__ SweepRec rec_shfl_xor(const SweepRec& r, int off) {
+    SweepRec o;
+    o.max_score = __shfl_xor(r.max_score, off);
+#pragma unroll
+    for (int i = 0; i < 4; i++) o.max_rank[i] = (uint32_t)__shfl_xor((int)r.max_rank[i], off);
+#pragma unroll
+    for (int i = 0; i < kMaxSkip; i++) {
+        o.np_rank[i] = (uint32_t)__shfl_xor((int)r.np_rank[i], off);
+        o.np_score[i] = __shfl_xor(r.np_score[i], off);
+    }
+    o.options = (uint32_t)__shfl_xor((int)r.options, off);
+    o.filtered = (uint32_t)__shfl_xor((int)r.filtered, off);
+    o.exhausted = (uint32_t)__shfl_xor((int)r.exhausted, off);
+    o._pad = 0;
+    return o;
+}
+
+// Block reduction of per-thread records; the merge is commutative and
+// associative over disjoint row sets, so an xor butterfly inside each wave is
+// exact. Thread 0 returns the block's record.
+template <int BLOCK>
+__device__ __forceinline__ void rec_block_reduce(SweepRec& r, SweepRec* red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const SweepRec o = rec_shfl_xor(r, off);
+        rec_merge(r, o);
+    }
+    constexpr int W = BLOCK / 64;
+    if constexpr (W > 1) {
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        if (lane == 0) red[wid] = r;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 1; w < W; w++) rec_merge(r, red[w]);
+    }
+}
+
 // Merge an evaluation's overlay into the HBM SoA (the stack's plan persists).
 template <int BLOCK, bool FULL>
 __device__ void writeback_overlay(const BatchArgs& A, const Overlay& ov, uint32_t H, const uint32_t* counts) {
@@ -601,7 +708,40 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
         uint32_t consumed = n;
         bool stopped = false;
 
-        for (uint32_t base = 0; base < n; base += BLOCK) {
+        if (FULL && A.limit >= n) {
+            // A full pass (limit >= every option): no prefix walk,
+            // each lane folds its positions into a SweepRec, one block reduction
+            // per placement gives the winner and the counters.
+            SweepRec rec;
+            rec_init(rec);
+            for (uint32_t j = tid; j < n; j += BLOCK) {
+                uint32_t pos = offset + j;
+                if (pos >= n) pos -= n;
+                NodeEval ev;
+                eval_node<false>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab, perm[pos], &ev);
+                if (ev.status == kFiltered) rec.filtered++;
+                else if (ev.status == kExhausted) rec.exhausted++;
+                else rec_add(rec, j, ev.score);
+            }
+            rec_block_reduce<BLOCK>(rec, sh.red_rec);
+            if (tid == 0) {
+                const uint32_t w = rec_winner(rec);
+                sh.stop_j = w == 0xFFFFFFFFu ? -1 : (int)w;
+                sh.scratch[0] = rec.filtered;
+                sh.scratch[1] = rec.exhausted;
+                sh.red_score[0] = rec.max_score;   // the winner always scores the maximum
+            }
+            __syncthreads();
+            best_pos = sh.stop_j;
+            best_score = sh.red_score[0];
+            n_filtered = sh.scratch[0];
+            n_exhausted = sh.scratch[1];
+            consumed = n;
+            stopped = true;   // nothing set aside to append
+            __syncthreads();
+        }
+
+        for (uint32_t base = 0; base < n && !(FULL && A.limit >= n); base += BLOCK) {
             const uint32_t j = base + tid;
             const bool valid = j < n;
             NodeEval ev;
@@ -1499,112 +1639,6 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t of
     }
 }
 
-// ---- full-scan scoring sweep --------------------------------------------------
-__host__ __device__ __forceinline__ void rec_init(SweepRec& r) {
-    r.max_score = -__builtin_inff();
-    for (int i = 0; i < 4; i++) r.max_rank[i] = 0xFFFFFFFFu;
-    for (int i = 0; i < kMaxSkip; i++) { r.np_rank[i] = 0xFFFFFFFFu; r.np_score[i] = 0.0; }
-    r.options = r.filtered = r.exhausted = r._pad = 0;
-}
-
-// insert x into a sorted list of N ranks (keeps the N smallest); branch-free on indices
-template <int N>
-__host__ __device__ __forceinline__ void ins_rank(uint32_t (&l)[N], uint32_t x) {
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-        const uint32_t lo = l[i] < x ? l[i] : x, hi = l[i] < x ? x : l[i];
-        l[i] = lo;
-        x = hi;
-    }
-}
-
-__host__ __device__ __forceinline__ void ins_np(uint32_t (&rk)[kMaxSkip], double (&sc)[kMaxSkip], uint32_t x, double s) {
-#pragma unroll
-    for (int i = 0; i < kMaxSkip; i++) {
-        if (x < rk[i]) {
-            const uint32_t tr = rk[i]; const double ts = sc[i];
-            rk[i] = x; sc[i] = s;
-            x = tr; s = ts;
-        }
-    }
-}
-
-__device__ __forceinline__ void rec_add(SweepRec& r, uint32_t rank, double score) {
-    r.options++;
-    if (score > r.max_score) {
-        r.max_score = score;
-        r.max_rank[0] = rank;
-        r.max_rank[1] = r.max_rank[2] = r.max_rank[3] = 0xFFFFFFFFu;
-    } else if (score == r.max_score) {
-        ins_rank<4>(r.max_rank, rank);
-    }
-    if (score <= 0.0) ins_np(r.np_rank, r.np_score, rank, score);
-}
-
-__host__ __device__ __forceinline__ void rec_merge(SweepRec& a, const SweepRec& b) {
-    if (b.max_score > a.max_score) {
-        a.max_score = b.max_score;
-        for (int i = 0; i < 4; i++) a.max_rank[i] = b.max_rank[i];
-    } else if (b.max_score == a.max_score) {
-        for (int i = 0; i < 4; i++) ins_rank<4>(a.max_rank, b.max_rank[i]);
-    }
-    for (int i = 0; i < kMaxSkip; i++) ins_np(a.np_rank, a.np_score, b.np_rank[i], b.np_score[i]);
-    a.options += b.options;
-    a.filtered += b.filtered;
-    a.exhausted += b.exhausted;
-}
-
-// Winner rank of a merged record (SURVEY.md Appendix A1), ~0u = no option.
-__device__ __host__ __forceinline__ uint32_t rec_winner(const SweepRec& r) {
-    if (r.options == 0) return 0xFFFFFFFFu;
-    if (r.max_score > 0.0) return r.max_rank[0];
-    for (int i = 0; i < 4; i++) {
-        const uint32_t x = r.max_rank[i];
-        if (x == 0xFFFFFFFFu) break;
-        bool demoted = false;
-        for (int k = 0; k < kMaxSkip; k++) demoted = demoted || r.np_rank[k] == x;
-        if (!demoted) return x;
-    }
-    return r.max_rank[0];
-}
-
-__device__ __forceinline__ SweepRec rec_shfl_xor(const SweepRec& r, int off) {
-    SweepRec o;
-    o.max_score = __shfl_xor(r.max_score, off);
-#pragma unroll
-    for (int i = 0; i < 4; i++) o.max_rank[i] = (uint32_t)__shfl_xor((int)r.max_rank[i], off);
-#pragma unroll
-    for (int i = 0; i < kMaxSkip; i++) {
-        o.np_rank[i] = (uint32_t)__shfl_xor((int)r.np_rank[i], off);
-        o.np_score[i] = __shfl_xor(r.np_score[i], off);
-    }
-    o.options = (uint32_t)__shfl_xor((int)r.options, off);
-    o.filtered = (uint32_t)__shfl_xor((int)r.filtered, off);
-    o.exhausted = (uint32_t)__shfl_xor((int)r.exhausted, off);
-    o._pad = 0;
-    return o;
-}
-
-// Block reduction of per-thread records; the merge is commutative and
-// associative over disjoint row sets, so an xor butterfly inside each wave is
-// exact. Thread 0 returns the block's record.
-template <int BLOCK>
-__device__ __forceinline__ void rec_block_reduce(SweepRec& r, SweepRec* red) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const SweepRec o = rec_shfl_xor(r, off);
-        rec_merge(r, o);
-    }
-    constexpr int W = BLOCK / 64;
-    if constexpr (W > 1) {
-        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        if (lane == 0) red[wid] = r;
-        __syncthreads();
-        if (threadIdx.x == 0)
-            for (int w = 1; w < W; w++) rec_merge(r, red[w]);
-    }
-}
-
 // One pass of the scoring sweep over rows [row_begin, row_end), one tile of
 // BLOCK rows per workgroup iteration (grid-stride), 64 rows per wave. Every
 // lane streams its row (64-byte record, collision count, verdict, visit rank),
@@ -1859,7 +1893,9 @@ hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, 
     if (full && a->packed_overlay) return hipErrorInvalidValue;   // packed entries: windowed kernel only
     const size_t lds = pe_place_lds_bytes(full, a->hash_bits, a->packed_overlay != 0);
     if (full) {
-        hipLaunchKernelGGL((pe::k_place<256, true>), dim3(n_evals), dim3(256), lds, st, *a);
+        // few evaluations: 1024-lane workgroups keep more rows in flight per pass
+        if (n_evals <= 64) hipLaunchKernelGGL((pe::k_place<1024, true>), dim3(n_evals), dim3(1024), lds, st, *a);
+        else hipLaunchKernelGGL((pe::k_place<256, true>), dim3(n_evals), dim3(256), lds, st, *a);
     } else {
         hipLaunchKernelGGL(pe::k_window, dim3(n_evals), dim3(64), lds, st, *a);
     }
