@@ -44,7 +44,9 @@ hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ran
 hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
                                     uint32_t* pcount, uint32_t* dev_free, hipStream_t st);
 hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st);
-hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, hipStream_t st);
+hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* status, double* score,
+                            hipStream_t st);
+hipError_t pe_launch_resolve(const pe::EvictResolveArgs* r, hipStream_t st);
 hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
                                     uint32_t* dev_free, uint32_t* placed, hipStream_t st);
 hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
@@ -362,6 +364,7 @@ struct pe_stack {
     // visit order
     std::vector<uint32_t> visit;
     DevMem d_visit, d_pref, d_penalty, d_out, d_status;
+    bool d_visit_is_visit = false;     // d_visit holds the SetNodes list (skips re-uploads)
     uint32_t offset = 0;
     uint32_t limit = 2;
     double log10 = 0;
@@ -411,6 +414,15 @@ hipError_t upload(DevMem& m, const std::vector<T>& h) {
     if (e != hipSuccess) return e;
     if (h.empty()) return hipSuccess;
     return hipMemcpy(m.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+// Visit order into d_visit; the SetNodes list itself is uploaded once per SetNodes.
+hipError_t upload_visit(pe_stack* s, const std::vector<uint32_t>& order) {
+    const bool is_visit = &order == &s->visit;
+    if (is_visit && s->d_visit_is_visit) return hipSuccess;
+    hipError_t e = upload(s->d_visit, order);
+    s->d_visit_is_visit = is_visit && e == hipSuccess;
+    return e;
 }
 
 ParsedTarget parse_target(const pe_stack* s, const std::string& t) {
@@ -1569,16 +1581,24 @@ int run_sweep_select(pe_stack* s, TgPlan& g, const pe_select_options* opts, pe_r
 // Options / filtered / exhausted over the current visit list (k_census).
 int census(pe_stack* s, TgPlan& g, uint32_t* cnt) {
     pe::BatchArgs A = batch_args(s, g);
-    HIP_TRY(s, upload(s->d_visit, s->visit));
+    HIP_TRY(s, upload_visit(s, s->visit));
     A.perms = s->d_visit.as<uint32_t>();
     A.n_visit = (uint32_t)s->visit.size();
     HIP_TRY(s, s->d_ev_out.ensure(16));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
-    HIP_TRY(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->stream));
+    HIP_TRY(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), nullptr, nullptr, s->stream));
     HIP_TRY(s, hipMemcpyAsync(cnt, s->d_ev_out.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     return PE_OK;
 }
+
+constexpr uint32_t kParallelMinNodes = 4096;   // lists shorter than this keep the fused loop
+constexpr uint64_t kParallelWalk = 4096;        // expected positions per windowed Select
+
+// A plain Select over the visit list from the cursor with every position
+// evaluated in parallel (k_census with outcomes) and LimitIterator +
+// MaxScoreIterator resolved on the device (k_evict_resolve).
+int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* new_offset);
 
 // Preemptor inputs on the device for the current job / task group.
 pe::PreemptArgs preempt_args(pe_stack* s, TgPlan& g) {
@@ -1599,6 +1619,65 @@ pe::PreemptArgs preempt_args(pe_stack* s, TgPlan& g) {
     return P;
 }
 
+int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* new_offset) {
+    std::memset(out, 0, sizeof(*out));
+    out->row = -1;
+    const uint32_t n = (uint32_t)s->visit.size();
+    *new_offset = n ? s->offset % n : 0;
+    if (n == 0) return PE_OK;
+    pe::BatchArgs A = batch_args(s, g);
+    HIP_TRY(s, upload_visit(s, s->visit));
+    A.perms = s->d_visit.as<uint32_t>();
+    A.n_visit = n;
+    HIP_TRY(s, s->d_ev_status.ensure(n));
+    HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * n));
+    HIP_TRY(s, s->d_ev_out.ensure(16));
+    HIP_TRY(s, s->d_ev_mask.ensure(16));
+    HIP_TRY(s, s->d_ev_flags.ensure(16));
+    HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
+    HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
+    HIP_TRY(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->d_ev_status.as<uint8_t>(),
+                                s->d_ev_score.as<double>(), s->stream));
+    pe::EvictResolveArgs R;
+    R.status = s->d_ev_status.as<uint8_t>();
+    R.score = s->d_ev_score.as<double>();
+    R.n = n;
+    R.offset = s->offset % n;
+    R.limit = s->limit;
+    R.out = s->d_ev_out.as<int32_t>();
+    HIP_TRY(s, pe_launch_resolve(&R, s->stream));
+    int32_t res[4];
+    HIP_TRY(s, hipMemcpyAsync(res, R.out, sizeof(res), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    const uint32_t consumed = (uint32_t)res[1];
+    out->nodes_evaluated = consumed;
+    out->nodes_filtered = (uint32_t)res[2];
+    out->nodes_exhausted = (uint32_t)res[3];
+    *new_offset = (uint32_t)(((uint64_t)(s->offset % n) + consumed) % n);
+    out->new_offset = *new_offset;
+    if (res[0] >= 0) {
+        // the option's record: BinPack with evict gives the plain result on a
+        // node that fits (no preemption, no preemption score)
+        const uint32_t row = s->visit[(uint32_t)(((uint64_t)(s->offset % n) + (uint32_t)res[0]) % n)];
+        pe::PreemptArgs P = preempt_args(s, g);
+        P.visit = s->d_visit.as<uint32_t>();
+        P.n_visit = n;
+        P.flags = s->d_ev_flags.as<uint32_t>();
+        HIP_TRY(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
+                                          s->stream));
+        pe_ranked_node rr;
+        HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        out->row = (int32_t)row;
+        out->final_score = rr.final_score;
+        out->n_scores = rr.n_scores;
+        std::memcpy(out->scores, rr.scores, sizeof(out->scores));
+        out->n_device_offers = rr.n_device_offers;
+        std::memcpy(out->device_offer_group, rr.device_offer_group, sizeof(out->device_offer_group));
+    }
+    return PE_OK;
+}
+
 // Select with Preempt=true (BinPack evict, rank.go:193-527 + PreemptionScoringIterator)
 // over `order` from cursor `offset`: every position evaluated in parallel, then
 // the LimitIterator window resolved on the device.
@@ -1611,7 +1690,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
     if (n == 0) return PE_OK;
     pe::PreemptArgs P = preempt_args(s, g);
-    HIP_TRY(s, upload(s->d_visit, order));
+    HIP_TRY(s, upload_visit(s, order));
     P.visit = s->d_visit.as<uint32_t>();
     P.n_visit = n;
     if (opts && opts->penalty_count > 0) {
@@ -1707,7 +1786,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     const uint32_t n = (uint32_t)order.size();
     const bool full = full_scan_kernel(s, g, n);
     pe::BatchArgs A = batch_args(s, g);
-    HIP_TRY(s, upload(s->d_visit, order));
+    HIP_TRY(s, upload_visit(s, order));
     A.perms = s->d_visit.as<uint32_t>();
     A.n_visit = n;
     if (opts && opts->penalty_count > 0) {
@@ -2039,6 +2118,7 @@ int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     s->gen++;
     s->visit.assign(rows, rows + n);
+    s->d_visit_is_visit = false;
     for (uint32_t r : s->visit) if (r >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range");
     s->offset = 0;
     uint32_t lim = 2;
@@ -2266,6 +2346,47 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     TgPlan& g = *s->tgs[tgi];
     if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;
     uint32_t p = 0, no = s->offset;
+    // Sparse options (a saturated cluster): a windowed Select would walk
+    // ~limit * n / options positions with one wave. Then every Select
+    // evaluates the list in parallel and resolves the window on the device.
+    bool parallel = false;
+    const uint32_t nv = (uint32_t)s->visit.size();
+    if (count && g.psets.empty() && nv >= kParallelMinNodes) {
+        uint32_t cnt[3];
+        rc = census(s, g, cnt);
+        if (rc) return rc;
+        parallel = cnt[0] == 0 || (uint64_t)std::min<uint32_t>(s->limit, nv) * nv / cnt[0] > kParallelWalk;
+    }
+    if (parallel) {
+        while (p < count) {
+            rc = run_parallel_select(s, g, &out[p], &no);
+            if (rc) return rc;
+            s->offset = no;
+            if (out[p].row >= 0) {
+                s->offer_row = out[p].row;
+                s->offers = pack_offers(&out[p]);
+                rc = pe_commit(s, tgi, out[p].row);
+                if (rc) return rc;
+                p++;
+                continue;
+            }
+            if (!s->cfg.preempt) break;
+            pe_select_options o;   // selectNextOption: retry with Preempt=true
+            std::memset(&o, 0, sizeof(o));
+            o.preempt = 1;
+            rc = run_evict_select(s, g, s->visit, s->offset, &o, &out[p], &no);
+            if (rc) return rc;
+            s->offset = no;
+            if (out[p].row < 0) break;
+            s->offer_row = out[p].row;
+            s->offers = pack_offers(&out[p]);
+            rc = pe_commit_preempt(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
+            if (rc) return rc;
+            p++;
+        }
+        count = 0;   // done: skip the fused loop below
+        no = s->offset;
+    }
     if (count) {
         rc = run_place(s, tgi, count, 1, s->visit, s->offset, nullptr, out, &p, &no);
         if (rc) return rc;
@@ -2286,21 +2407,28 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
             if (rc) return rc;
             p++;
             if (p == count) break;
-            // a saturated cluster stays saturated: when the census finds no
-            // option the plain Select is nil (every node pulled, cursor kept)
-            // and the next placement goes straight to the eviction pass
-            if (!g.psets.empty()) { /* spread / distinct counts: take the count loop */ }
-            else {
-                uint32_t cnt[3];
-                rc = census(s, g, cnt);
+            if (!g.psets.empty()) {   // spread / distinct counts: the fused count loop
+                uint32_t p2 = 0;
+                rc = run_place(s, tgi, count - p, 1, s->visit, s->offset, nullptr, out + p, &p2, &no);
                 if (rc) return rc;
-                if (cnt[0] == 0) continue;
+                s->offset = no;
+                p += p2;
+                continue;
             }
-            uint32_t p2 = 0;
-            rc = run_place(s, tgi, count - p, 1, s->visit, s->offset, nullptr, out + p, &p2, &no);
-            if (rc) return rc;
-            s->offset = no;
-            p += p2;
+            // Options are sparse once the cluster is saturated: plain Selects
+            // evaluate the whole list in parallel and resolve the window on the
+            // device instead of walking it with one wave, until one is nil.
+            while (p < count) {
+                rc = run_parallel_select(s, g, &out[p], &no);
+                if (rc) return rc;
+                s->offset = no;
+                if (out[p].row < 0) break;
+                s->offer_row = out[p].row;
+                s->offers = pack_offers(&out[p]);
+                rc = pe_commit(s, tgi, out[p].row);
+                if (rc) return rc;
+                p++;
+            }
         }
         no = s->offset;
     }
@@ -2526,7 +2654,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     const uint32_t n = (uint32_t)s->visit.size();
-    HIP_TRY(s, upload(s->d_visit, s->visit));
+    HIP_TRY(s, upload_visit(s, s->visit));
     DevMem& d_score = s->d_sys_score;
     DevMem& d_st = s->d_sys_status;
     HIP_TRY(s, d_score.ensure(sizeof(double) * std::max<uint32_t>(n, 1)));

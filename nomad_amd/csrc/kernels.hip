@@ -1589,7 +1589,7 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
 // (no overlay): counts[0] options, [1] filtered, [2] exhausted. With no option
 // the Select is nil after pulling every node, which the count loop's
 // preemption retry uses instead of a windowed scan of the whole list.
-__global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts) {
+__global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts, uint8_t* status, double* score) {
     const uint32_t stride = gridDim.x * blockDim.x;
     uint32_t c[3] = {0, 0, 0};
     Overlay none;
@@ -1598,6 +1598,10 @@ __global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts) {
         NodeEval ev;
         eval_node<false>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, nullptr, A.perms[j], &ev);
         c[ev.status]++;
+        if (status) {   // per-position outcomes for a parallel Select (k_evict_resolve)
+            status[j] = (uint8_t)ev.status;
+            score[j] = ev.status == kOption ? ev.score : 0.0;
+        }
     }
     for (int k = 0; k < 3; k++) {
         uint32_t x = c[k];
@@ -1947,20 +1951,26 @@ hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const p
 }
 
 // Select with Preempt: per-position evict evaluation, then the window resolve.
+hipError_t pe_launch_resolve(const pe::EvictResolveArgs* r, hipStream_t st) {
+    hipLaunchKernelGGL(pe::k_evict_resolve, dim3(1), dim3(pe::kResolveBlock), 0, st, *r);
+    return hipGetLastError();
+}
+
 hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs* r, hipStream_t st) {
     uint32_t blocks = (a->n_visit + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(pe::k_evict, dim3(blocks), dim3(256), 0, st, *a);
-    hipLaunchKernelGGL(pe::k_evict_resolve, dim3(1), dim3(256), 0, st, *r);
+    hipLaunchKernelGGL(pe::k_evict_resolve, dim3(1), dim3(pe::kResolveBlock), 0, st, *r);
     return hipGetLastError();
 }
 
-hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, hipStream_t st) {
+hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* status, double* score,
+                            hipStream_t st) {
     uint32_t blocks = (a->n_visit + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(pe::k_census, dim3(blocks), dim3(256), 0, st, *a, counts);
+    hipLaunchKernelGGL(pe::k_census, dim3(blocks), dim3(256), 0, st, *a, counts, status, score);
     return hipGetLastError();
 }
 

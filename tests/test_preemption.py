@@ -221,3 +221,18 @@ def test_system_preemption_parity(max_parallel):
     assert po == pe and (to == te).all()
     m = to == 0
     assert (so[m] == se[m]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preempt", [False, True])
+def test_c5_sparse_parallel_count_loop(preempt):
+    """A saturated cluster (options sparse): the engine's count loop evaluates
+    each Select in parallel and resolves the window on the device."""
+    nodes, allocs = synth.cluster_c5(5000, seed=3, busy=0.99)
+    job = synth.job_c5(120)
+    perm = synth.shuffle(len(nodes), 31)
+    cfg = SchedulerConfig(preempt_service=preempt)
+    _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, perm, config=cfg)
+    _, _, re = run_place(_engine, nodes, allocs, job, perm, config=cfg)
+    assert_same_placements(re, ro)
+    assert [sorted(x.preempted) for x in re] == [sorted(x.preempted) for x in ro]
