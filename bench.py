@@ -78,6 +78,7 @@ def dist_init():
         # CPU tensors (timing reductions) over gloo, GPU tensors (the shard
         # record all-gather) over RCCL / xGMI
         if torch.cuda.is_available():
+            local = local % max(1, torch.cuda.device_count())   # rehearsals with fewer GPUs than ranks
             torch.cuda.set_device(local)
             dist.init_process_group("cpu:gloo,cuda:nccl")
         else:
@@ -372,6 +373,8 @@ def section_c3_sharded(device, rank, world, pg, placements=64):
     if world > 1:
         import torch
         gdev = torch.device("cuda", device) if torch.cuda.is_available() else None
+        if os.environ.get("PE_GATHER_CPU"):   # gloo over host memory instead of RCCL
+            gdev = None
     walls, xs = [], []
     for i in range(2):
         st.ResetPlan()
@@ -401,11 +404,16 @@ def section_c3_sharded(device, rank, world, pg, placements=64):
             "placements_per_s": placed / wall, "ms_per_placement": wall / max(1, placed) * 1e3,
             "node_evals_per_s": placed * n / wall,
             "exchange_us_per_placement": xs[-1] if world > 1 else 0.0,
-            "exchange": "torch.distributed all_gather of 80 B per rank (RCCL)" if world > 1 else "none"}
+            "exchange": ("none" if world == 1 else "torch.distributed all_gather of 80 B per rank (%s)"
+                         % ("RCCL" if gdev is not None else "gloo, host memory"))}
 
 
 def main():
     args = parse()
+    # Native libraries (gloo, RCCL) print banners on stdout; the contract is one
+    # JSON line there, so everything else goes to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     rank, world, local, pg = dist_init()
     from nomad_amd import synth
     from nomad_amd.stack import GenericStack
@@ -505,17 +513,21 @@ def main():
     cpu_s = 0.0 if args.no_cpu else 8.0
     extra = {}
     for sec in sections:
-        if sec in ("c3", "c5"):
-            if rank == 0:
-                extra[sec] = section_c3(local, cpu_s) if sec == "c3" else section_c5(local, cpu_s)
-            barrier(pg)
-        elif sec == "c4":
-            extra[sec] = section_c4(local, rank, world, pg, cpu_s)
-        elif sec == "c3_sharded":
-            extra[sec] = section_c3_sharded(local, rank, world, pg)
+        try:
+            if sec in ("c3", "c5"):
+                if rank == 0:
+                    extra[sec] = section_c3(local, cpu_s) if sec == "c3" else section_c5(local, cpu_s)
+            elif sec == "c4":
+                extra[sec] = section_c4(local, rank, world, pg, cpu_s)
+            elif sec == "c3_sharded":
+                extra[sec] = section_c3_sharded(local, rank, world, pg)
+        except Exception as e:   # an extra section never takes the headline line down
+            extra[sec] = {"error": "%s: %s" % (type(e).__name__, e)}
+        barrier(pg)
     if rank == 0:
         line["configs"] = extra
-        print(json.dumps(line))
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
     st.close()
     lat.close()
     if pg is not None:

@@ -15,7 +15,7 @@ cat "$OUT/bench.json"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
-  python3 "$ROOT/bench.py" --no-cpu --steps 10 --warmup 2 > "$OUT/trace.log" 2>&1
+  python3 "$ROOT/bench.py" --no-cpu --steps 10 --warmup 2 --sections "" > "$OUT/trace.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o fetch -- \
   python3 "$ROOT/tools/sweep_variants.py" 16777216 0 0 > "$OUT/pmc_fetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o write -- \
