@@ -144,6 +144,20 @@ def cpu_baseline(nodes, allocs, job, seconds):
 # score word (verdict, affinity index, spread values; 1 B verdict when the word
 # does not apply: 73 B) + 4 B (job,tg) collisions + 4 B visit rank = 76 B.
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "sweep_traffic.json")
+CHAIN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "chain_traffic.json")
+
+
+def chain_traffic(evals_per_launch):
+    """HBM bytes per k_chain launch from the committed PMC passes over this
+    same headline workload (tools/profile_round.sh), or None."""
+    try:
+        with open(CHAIN_TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("nodes") != int(evals_per_launch) or t.get("bytes_per_node") != BYTES_PER_NODE_EVAL:
+        return None
+    return t["bytes_per_launch"]
 
 
 def sweep_traffic(n, bytes_per_node):
@@ -498,7 +512,10 @@ def main():
             "single_eval": {"placements_per_s": single, "kernel_ms": single_kernel_ms,
                             "note": "one eval, pe_place fused count loop, host call included"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": chain_traffic(evals_per_launch),
+                         "traffic_note": "FETCH_SIZE x 2 + WRITE_SIZE per k_chain launch (the 10k-node table "
+                                         "is L2/MALL resident, so HBM traffic sits far below the algorithmic "
+                                         "bytes the lanes read)",
                          "kernel": "k_base + k_chain", "kernel_ms": avg_kernel_s * 1000.0,
                          "node_evals_per_launch": evals_per_launch,
                          "bytes_per_node_eval": BYTES_PER_NODE_EVAL},

@@ -20,7 +20,15 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
   python3 "$ROOT/tools/sweep_variants.py" 16777216 0 0 > "$OUT/pmc_fetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o write -- \
   python3 "$ROOT/tools/sweep_variants.py" 16777216 0 0 > "$OUT/pmc_write.log" 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/chain_fetch" -o fetch -- \
+  python3 "$ROOT/bench.py" --no-cpu --steps 2 --warmup 0 --sweep-nodes 0 --sections "" > "$OUT/chain_fetch.log" 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/chain_write" -o write -- \
+  python3 "$ROOT/bench.py" --no-cpu --steps 2 --warmup 0 --sweep-nodes 0 --sections "" > "$OUT/chain_write.log" 2>&1
 cd "$ROOT"
+EV=$(python3 -c "import json;print(int(json.load(open('$OUT/bench.json'))['roofline']['node_evals_per_launch']))")
+CF=$(find "$OUT/chain_fetch" -name "*counter_collection.csv" -print -quit)
+CW=$(find "$OUT/chain_write" -name "*counter_collection.csv" -print -quit)
+python3 tools/pmc_traffic.py "$CF" "$CW" "k_chain" "$EV" 60 "$OUT/chain_traffic.json"
 F=$(find "$OUT/pmc_fetch" -name "*counter_collection.csv" -print -quit)
 W=$(find "$OUT/pmc_write" -name "*counter_collection.csv" -print -quit)
 python3 tools/pmc_traffic.py "$F" "$W" "k_sweep<" 16777216 76 "$OUT/sweep_traffic.json"
