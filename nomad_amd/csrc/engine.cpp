@@ -330,6 +330,7 @@ struct pe_stack {
     bool results_via_copy = false;     // PE_RESULTS_VIA_COPY=1: device buffer + one D2H copy
     pe::BatchArgs batch_A{};
     PinnedMem h_batch_out, h_batch_status;
+    PinnedMem h_place_out, h_place_status;   // single-evaluation count loop results (mapped)
     double phase_ms[4] = {0, 0, 0, 0};   // host prep, kernels, result copy, total (last batch)
     std::vector<pe::NodeRec> h_base_rec;     // snapshot proposed state (no plan)
     DevMem d_rec, d_base_rec, d_coll_job;
@@ -1266,7 +1267,6 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         HIP_TRY(s, pe_launch_fold_feas(&soa, g.class_ok.as<uint8_t>(),
                                        g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr,
                                        g.node_feas.as<uint8_t>(), s->stream));
-        HIP_TRY(s, hipStreamSynchronize(s->stream));
     }
 
     // NodeAffinityIterator score per class (rank.go:698-725)
@@ -1804,11 +1804,15 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     if (!full && s->use_base && count > 1 && n <= pe_chain_max_n() && A.limit <= pe_chain_max_limit()) {
         // count loop over one rotation at a time (k_base + k_chain): needs a
         // visit list without repeated rows
-        std::vector<uint8_t> seen(s->nodes.size(), 0);
         chain = true;
-        for (uint32_t r : order) {
-            if (seen[r]) { chain = false; break; }
-            seen[r] = 1;
+        if (&order == &s->visit) {
+            chain = s->visit_unique;   // checked once per SetNodes
+        } else {
+            std::vector<uint8_t> seen(s->nodes.size(), 0);
+            for (uint32_t r : order) {
+                if (seen[r]) { chain = false; break; }
+                seen[r] = 1;
+            }
         }
         if (chain) {
             HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));
@@ -1821,12 +1825,15 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         }
     }
     const uint32_t chunk = std::max<uint32_t>(1, (1u << A.hash_bits) / 2);
-    HIP_TRY(s, s->d_out.ensure(sizeof(pe_ranked_node) * std::min(count, chunk)));
-    HIP_TRY(s, s->d_status.ensure(16));
+    // records and status land in mapped page-locked memory: the kernel writes
+    // them over PCIe while it runs, one stream sync per launch
+    HIP_TRY(s, s->h_place_out.ensure(sizeof(pe_ranked_node) * std::min(count, chunk)));
+    HIP_TRY(s, s->h_place_status.ensure(16));
     A.commit = commit;
     A.writeback = commit;
-    A.full_out = s->d_out.as<pe_ranked_node>();
-    A.eval_status = s->d_status.as<uint32_t>();
+    A.full_out = s->h_place_out.dev<pe_ranked_node>();
+    A.eval_status = s->h_place_status.dev<uint32_t>();
+    if (!A.full_out || !A.eval_status) return s->fail(PE_EHIP, "mapped result buffers unavailable");
     double total_ms = 0;
     uint32_t done = 0;
     while (done < count) {
@@ -1837,14 +1844,14 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         if (chain) HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream));
         else HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
         HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
-        uint32_t st[2];
-        HIP_TRY(s, hipMemcpyAsync(st, A.eval_status, sizeof(st), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
+        uint32_t st[2];
+        std::memcpy(st, s->h_place_status.as<uint32_t>(), sizeof(st));
         float ms = 0;
         HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
         total_ms += ms;
         const uint32_t got = std::min(c, st[0] + 1);   // placed + the failing Select
-        HIP_TRY(s, hipMemcpy(out + done, A.full_out, sizeof(pe_ranked_node) * got, hipMemcpyDeviceToHost));
+        std::memcpy(out + done, s->h_place_out.as<pe_ranked_node>(), sizeof(pe_ranked_node) * got);
         if (commit)
             for (uint32_t i = 0; i < st[0]; i++) s->plan.emplace_back(g.name, (uint32_t)out[done + i].row);
         *placed += st[0];
@@ -2336,7 +2343,13 @@ int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* pr
     return pe_commit(s, tgi, row);
 }
 
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+    const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
+    const double t_enter = prof ? now_us() : 0.0;
     if (!s || (!out && count)) return PE_EINVAL;
     if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place needs a generic stack");
     s->gen++;
@@ -2351,7 +2364,9 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     // evaluates the list in parallel and resolves the window on the device.
     bool parallel = false;
     const uint32_t nv = (uint32_t)s->visit.size();
-    if (count && g.psets.empty() && nv >= kParallelMinNodes) {
+    const double t_prep = prof ? now_us() : 0.0;
+    const bool chain_ok = nv <= pe_chain_max_n() && s->limit <= pe_chain_max_limit();
+    if (count && g.psets.empty() && nv >= kParallelMinNodes && (s->cfg.preempt || !chain_ok)) {
         uint32_t cnt[3];
         rc = census(s, g, cnt);
         if (rc) return rc;
@@ -2434,6 +2449,9 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     }
     s->offset = no;
     if (placed) *placed = p;
+    if (prof)
+        std::fprintf(stderr, "pe_place: prepare %.1f us, loop %.1f us (kernels %.1f us)\n", t_prep - t_enter,
+                     now_us() - t_prep, s->last_ms * 1e3);
     if (p) invalidate_job_distinct(s, tgi);
     // multi-tg jobs sharing a name see these allocs in their collision counts
     for (size_t k = 0; k < s->tgs.size(); k++)

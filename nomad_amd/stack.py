@@ -251,11 +251,15 @@ class _Stack:
         return [RankedNode.from_c(out[i], self.nodes) for i in range(n)]
 
     def PlaceArrays(self, tg, count: int):
-        """Fused count loop returning (rows, final_scores, placed) as numpy arrays."""
-        out = (abi.pe_ranked_node * max(1, count))()
-        placed = C.c_uint32(0)
+        """Fused count loop returning (rows, final_scores, placed, records) as numpy
+        arrays. The record buffer is reused across calls with the same count."""
+        cache = getattr(self, "_place_buf", None)
+        if cache is None or cache[0] != count:
+            out = (abi.pe_ranked_node * max(1, count))()
+            cache = (count, out, np.ctypeslib.as_array(out), C.c_uint32(0))
+            self._place_buf = cache
+        _, out, arr, placed = cache
         self._check(self._fn("place")(self._h, self._tg_index(tg), count, out, C.byref(placed)))
-        arr = np.ctypeslib.as_array(out)
         return arr["row"].copy(), arr["final_score"].copy(), placed.value, arr
 
     def SystemPlace(self, tg):
