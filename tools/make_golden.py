@@ -19,6 +19,7 @@ CASES = {
     "c1_mock_count10": dict(gen="c1", n=100, seed=42, perm_seed=1, count=10),
     "c2_binpack_2k": dict(gen="c2", n=2000, seed=42, perm_seed=5, count=400),
     "c3_spread_affinity_1k": dict(gen="c3", n=1000, seed=7, perm_seed=3, count=150),
+    "c5_devices_preempt_600": dict(gen="c5", n=600, seed=4, perm_seed=9, count=200, busy=0.9, preempt=True),
 }
 
 
@@ -29,6 +30,9 @@ def build(case):
     elif case["gen"] == "c2":
         nodes, allocs = synth.cluster_c2(case["n"], seed=case["seed"])
         job = synth.job_c2(case["count"])
+    elif case["gen"] == "c5":
+        nodes, allocs = synth.cluster_c5(case["n"], seed=case["seed"], busy=case["busy"])
+        job = synth.job_c5(case["count"])
     else:
         nodes, allocs = synth.cluster_c3(case["n"], seed=case["seed"])
         job = synth.job_c3(case["count"])
@@ -36,9 +40,14 @@ def build(case):
     return nodes, allocs, job, perm
 
 
+def config(case):
+    from nomad_amd.structs import SchedulerConfig
+    return SchedulerConfig(preempt_service=bool(case.get("preempt")))
+
+
 def run(name, case):
     nodes, allocs, job, perm = build(case)
-    st = OracleGenericStack()
+    st = OracleGenericStack(config=config(case))
     st.SetState(nodes, allocs)
     st.SetJob(job)
     limit = st.SetNodes(list(perm))
@@ -47,7 +56,8 @@ def run(name, case):
             "placements": [{"node_id": r.node.id if r.node else None, "row": r.row,
                             "final_score": r.final_score.hex(), "scores": [s.hex() for s in r.scores],
                             "evaluated": r.nodes_evaluated, "filtered": r.nodes_filtered,
-                            "exhausted": r.nodes_exhausted, "offset": r.new_offset} for r in res]}
+                            "exhausted": r.nodes_exhausted, "offset": r.new_offset,
+                            "preempted": sorted(r.preempted), "device_offers": r.device_offers} for r in res]}
 
 
 if __name__ == "__main__":
