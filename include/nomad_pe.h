@@ -332,6 +332,117 @@ uint32_t pe_last_sweep_bytes(const pe_stack* s);
  * l_state / r_state: 0 nil (unknown ${...} target), 1 found, 2 missing ("", false). */
 int pe_check_constraint(const char* op, const char* l, int l_state, const char* r, int r_state);
 
+/* ======================================================================== *
+ * Plan applier fit check (leader side).
+ *
+ * Replaces evaluatePlanPlacements' per-node worker calls
+ * (nomad/plan_apply.go:439-582) to evaluateNodePlan (plan_apply.go:611-674) →
+ * structs.AllocsFit(node, proposed, nil, checkDevices=true)
+ * (nomad/structs/funcs.go:148-211), with NetworkIndex.SetNode/AddAllocs
+ * (nomad/structs/network.go:92-193, 196-296) and DeviceAccounter
+ * (nomad/structs/devices.go:22-101). The planner handle keeps the state
+ * snapshot (nodes and their non-terminal allocations) resident in HBM; one
+ * kernel evaluates every node of a plan (one wavefront per plan node) and
+ * pe_planner_commit folds an applied plan back into the resident snapshot
+ * (the optimistic snapshot.UpsertPlanResults of planApply, plan_apply.go:207).
+ * Strings: every call carries its own pe_strtab; the planner interns by
+ * content, so ids need not be stable across calls.
+ * ======================================================================== */
+
+/* evaluateNodePlan outcome per plan node; the reason strings are the
+ * reference's (plan_apply.go:627-633, funcs.go:184-208, structs.go:3891-3905). */
+#define PE_PLAN_FIT 0
+#define PE_PLAN_NODE_MISSING 1      /* "node does not exist" */
+#define PE_PLAN_NODE_NOT_READY 2    /* "node is not ready for placements" */
+#define PE_PLAN_NODE_INELIGIBLE 3   /* "node is not eligible" */
+#define PE_PLAN_CORES 4             /* "cores" (overlap between allocs, or not a subset of the node's) */
+#define PE_PLAN_CPU 5               /* "cpu" */
+#define PE_PLAN_MEMORY 6            /* "memory" */
+#define PE_PLAN_DISK 7              /* "disk" */
+#define PE_PLAN_PORTS 8             /* "reserved port collision" */
+#define PE_PLAN_BANDWIDTH 9         /* "bandwidth exceeded": never (Overcommitted is disabled, network.go:79-90) */
+#define PE_PLAN_DEVICES 10          /* "device oversubscribed" */
+
+/* Nodes of the snapshot, the fields evaluateNodePlan / AllocsFit read. */
+typedef struct pe_plan_node_table {
+    uint32_t n;
+    const uint8_t* ready;            /* Node.Status == "ready" */
+    const uint8_t* eligible;         /* Node.SchedulingEligibility != "ineligible" */
+    const int64_t* cpu_shares;       /* NodeResources.Cpu.CpuShares */
+    const int64_t* memory_mb;
+    const int64_t* disk_mb;
+    const int64_t* reserved_cpu;     /* ReservedResources (0 when nil) */
+    const int64_t* reserved_memory_mb;
+    const int64_t* reserved_disk_mb;
+    /* NodeResources.Cpu.ReservableCpuCores minus ReservedResources.Cpu.ReservedCpuCores */
+    const uint32_t* core_off; const uint32_t* core_id;
+    /* NodeResources.Networks entries with Device != "": their IP (str id) */
+    const uint32_t* net_off; const uint32_t* net_ip;
+    /* NodeResources.NodeNetworks[*].Addresses[*]: Address and ReservedPorts spec (str ids) */
+    const uint32_t* addr_off; const uint32_t* addr_ip; const uint32_t* addr_reserved_ports;
+    /* ReservedResources.Networks.ReservedHostPorts spec (str id; "" when unset) */
+    const uint32_t* reserved_host_ports;
+    /* NodeResources.Devices: groups (vendor, type, name) and their instances */
+    const uint32_t* dev_off; const uint32_t* dev_vendor; const uint32_t* dev_type; const uint32_t* dev_name;
+    const uint32_t* inst_off;        /* CSR over device groups */
+    const uint32_t* inst_id; const uint8_t* inst_healthy;
+} pe_plan_node_table;
+
+/* Allocations: the snapshot's (node_row set) or a plan's (node_row ignored).
+ * Resources are Allocation.ComparableResources() (structs.go:9656-9688). */
+typedef struct pe_plan_alloc_table {
+    uint32_t count;
+    const uint32_t* node_row;
+    const uint8_t* terminal;         /* Allocation.TerminalStatus() */
+    const int64_t* cpu_shares;
+    const int64_t* memory_mb;
+    const int64_t* disk_mb;
+    /* Flattened.Cpu.ReservedCores (a set per alloc) */
+    const uint32_t* core_off; const uint32_t* core_id;
+    /* the ports NetworkIndex.AddAllocs marks (network.go:144-193): the
+       AllocatedResources.Shared.Ports (HostIP, Value) when non-empty, else the
+       Reserved+Dynamic ports of Shared.Networks and of each task's first network (IP) */
+    const uint32_t* port_off; const uint32_t* port_ip; const int64_t* port_value;
+    /* one entry per AllocatedDeviceResource.DeviceIDs element of every task */
+    const uint32_t* dev_off;
+    const uint32_t* dev_vendor; const uint32_t* dev_type; const uint32_t* dev_name; const uint32_t* dev_instance;
+} pe_plan_alloc_table;
+
+/* One plan (structs.Plan) as evaluatePlanPlacements sees it, node by node. */
+typedef struct pe_plan {
+    uint32_t n_nodes;                /* nodeIDList: NodeUpdate keys then NodeAllocation keys */
+    const uint32_t* node_row;        /* snapshot row, or PE_NONE when the node does not exist */
+    /* snapshot allocs RemoveAllocs drops on that node: NodeUpdate ∪ NodePreemptions ∪
+       NodeAllocation IDs (plan_apply.go:650-665), as indices into the snapshot alloc table */
+    const uint32_t* remove_off; const uint32_t* remove_alloc;
+    /* NodeAllocation[node]: CSR into `allocs` */
+    const uint32_t* place_off;
+    pe_plan_alloc_table allocs;
+} pe_plan;
+
+typedef struct pe_planner pe_planner;
+pe_planner* pe_planner_create(int device);
+void pe_planner_destroy(pe_planner* p);
+const char* pe_planner_last_error(const pe_planner* p);
+/* Upload the state snapshot: nodes and allocations (terminal ones are kept
+ * as rows but never counted). Replaces any earlier snapshot. */
+int pe_planner_set_state(pe_planner* p, const pe_strtab* strs, const pe_plan_node_table* nodes,
+                         const pe_plan_alloc_table* allocs);
+/* evaluateNodePlan for every plan node on the device: reason[i] = PE_PLAN_*.
+ * *n_fit = nodes that fit. The AllAtOnce / partial-commit bookkeeping of
+ * evaluatePlanPlacements stays with the caller (it needs only reason[]). */
+int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* plan, uint8_t* reason,
+                        uint32_t* n_fit);
+/* Apply the nodes whose reason is PE_PLAN_FIT to the resident snapshot:
+ * removed allocs stop counting, placed allocs are appended (ApplyPlanResults).
+ * `keep[i]` != 0 selects plan node i (the caller passes the result it applied). */
+int pe_planner_commit(pe_planner* p, const pe_strtab* strs, const pe_plan* plan, const uint8_t* keep);
+/* Device time of the last evaluate (HIP events around the kernel) and its
+ * algorithmic bytes (records and keys read + reasons written). */
+double pe_planner_kernel_ms(const pe_planner* p);
+uint64_t pe_planner_last_bytes(const pe_planner* p);
+uint32_t pe_planner_snapshot_allocs(const pe_planner* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -209,3 +209,75 @@ def bind(lib, prefix, create_name, destroy_name, error_name):
     getattr(lib, error_name).restype = C.c_char_p
     getattr(lib, error_name).argtypes = [C.c_void_p]
     return lib
+
+
+# ---- plan applier (pe_planner_*) ----------------------------------------------
+PE_PLAN_FIT, PE_PLAN_NODE_MISSING, PE_PLAN_NODE_NOT_READY, PE_PLAN_NODE_INELIGIBLE = 0, 1, 2, 3
+PE_PLAN_CORES, PE_PLAN_CPU, PE_PLAN_MEMORY, PE_PLAN_DISK = 4, 5, 6, 7
+PE_PLAN_PORTS, PE_PLAN_BANDWIDTH, PE_PLAN_DEVICES = 8, 9, 10
+# reason strings of evaluateNodePlan / AllocsFit (plan_apply.go:627-633, funcs.go:184-208)
+PLAN_REASONS = ["", "node does not exist", "node is not ready for placements", "node is not eligible",
+                "cores", "cpu", "memory", "disk", "reserved port collision", "bandwidth exceeded",
+                "device oversubscribed"]
+
+
+class pe_plan_node_table(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32), ("ready", u8p), ("eligible", u8p),
+        ("cpu_shares", i64p), ("memory_mb", i64p), ("disk_mb", i64p),
+        ("reserved_cpu", i64p), ("reserved_memory_mb", i64p), ("reserved_disk_mb", i64p),
+        ("core_off", u32p), ("core_id", u32p),
+        ("net_off", u32p), ("net_ip", u32p),
+        ("addr_off", u32p), ("addr_ip", u32p), ("addr_reserved_ports", u32p),
+        ("reserved_host_ports", u32p),
+        ("dev_off", u32p), ("dev_vendor", u32p), ("dev_type", u32p), ("dev_name", u32p),
+        ("inst_off", u32p), ("inst_id", u32p), ("inst_healthy", u8p),
+    ]
+
+
+class pe_plan_alloc_table(C.Structure):
+    _fields_ = [
+        ("count", C.c_uint32), ("node_row", u32p), ("terminal", u8p),
+        ("cpu_shares", i64p), ("memory_mb", i64p), ("disk_mb", i64p),
+        ("core_off", u32p), ("core_id", u32p),
+        ("port_off", u32p), ("port_ip", u32p), ("port_value", i64p),
+        ("dev_off", u32p), ("dev_vendor", u32p), ("dev_type", u32p), ("dev_name", u32p),
+        ("dev_instance", u32p),
+    ]
+
+
+class pe_plan(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint32), ("node_row", u32p),
+        ("remove_off", u32p), ("remove_alloc", u32p),
+        ("place_off", u32p), ("allocs", pe_plan_alloc_table),
+    ]
+
+
+PLANNER_SYMBOLS = [
+    "pe_planner_create", "pe_planner_destroy", "pe_planner_last_error", "pe_planner_set_state",
+    "pe_planner_evaluate", "pe_planner_commit", "pe_planner_kernel_ms", "pe_planner_last_bytes",
+    "pe_planner_snapshot_allocs",
+]
+
+
+def bind_planner(lib):
+    """Attach restype/argtypes for the pe_planner_* API on a loaded CDLL."""
+    H = C.c_void_p
+    sigs = [
+        ("pe_planner_create", C.c_void_p, [C.c_int]),
+        ("pe_planner_destroy", None, [H]),
+        ("pe_planner_last_error", C.c_char_p, [H]),
+        ("pe_planner_set_state", C.c_int, [H, C.POINTER(pe_strtab), C.POINTER(pe_plan_node_table),
+                                           C.POINTER(pe_plan_alloc_table)]),
+        ("pe_planner_evaluate", C.c_int, [H, C.POINTER(pe_strtab), C.POINTER(pe_plan), u8p, u32p]),
+        ("pe_planner_commit", C.c_int, [H, C.POINTER(pe_strtab), C.POINTER(pe_plan), u8p]),
+        ("pe_planner_kernel_ms", C.c_double, [H]),
+        ("pe_planner_last_bytes", C.c_uint64, [H]),
+        ("pe_planner_snapshot_allocs", C.c_uint32, [H]),
+    ]
+    for name, res, args in sigs:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib

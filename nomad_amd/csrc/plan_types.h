@@ -1,0 +1,82 @@
+// Device records of the plan applier fit check (include/nomad_pe.h, pe_planner_*).
+//
+// evaluateNodePlan (nomad/plan_apply.go:611-674) → AllocsFit(checkDevices=true)
+// (nomad/structs/funcs.go:148-211) per plan node. Everything AllocsFit decides
+// besides the resource sums is a set question over small keyed multisets:
+//   cores:   a core held by two counted allocs (funcs.go:166-175) or a held core
+//            outside the node's available set when that set is non-empty
+//            (ComparableResources.Superset, structs.go:3896-3898);
+//   ports:   an (IP, port) marked twice in the NetworkIndex bitmaps
+//            (network.go:196-233), node-reserved ports included (SetNode);
+//   devices: a healthy node instance held twice (DeviceAccounter.AddAllocs,
+//            devices.go:62-100; unknown / unhealthy instances are ignored).
+// Each is order independent, so the kernel stages every key of a plan node in
+// one buffer (LDS, or global scratch for very large nodes) and answers all
+// three with one pairwise pass over it.
+#pragma once
+#include <stdint.h>
+
+namespace pa {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// key = kind << 60 | value
+enum : uint32_t {
+    K_CORE_USED = 0,   // value: core id
+    K_CORE_AVAIL = 1,  // node available core
+    K_PORT_USED = 2,   // value: ip id << 16 | port
+    K_PORT_NODE = 3,   // node-reserved (ip, port) after SetNode (deduplicated)
+    K_DEV_USED = 4,    // value: instance id << 24 | device tuple id
+    K_DEV_AVAIL = 5,   // healthy node instance
+};
+constexpr uint64_t kValMask = (1ull << 60) - 1;
+
+__host__ __device__ inline uint64_t make_key(uint32_t kind, uint64_t v) { return (uint64_t)kind << 60 | (v & kValMask); }
+
+struct alignas(16) NodeRec {      // 48 B, one per snapshot node
+    int64_t cpu, mem, disk;       // NodeResources − ReservedResources (funcs.go:180-181)
+    uint32_t key_off, n_keys;     // static keys: available cores, reserved ports, healthy instances
+    uint32_t alloc_off, alloc_cnt;// contiguous snapshot allocs of this node in the pool
+    uint32_t alloc_keys;          // Σ keys of those allocs (sizes the scratch fallback)
+    uint8_t ready, eligible, setnode_collide, has_cores;
+};
+static_assert(sizeof(NodeRec) == 48, "NodeRec is 48 bytes");
+
+struct alignas(16) AllocRec {     // 32 B, snapshot pool entry or plan alloc
+    int64_t cpu, mem, disk;
+    uint32_t key_off;
+    uint16_t n_keys;
+    uint8_t terminal;
+    uint8_t bad_port;             // a port outside [0, 65536): AddReserved* returns collide
+};
+static_assert(sizeof(AllocRec) == 32, "AllocRec is 32 bytes");
+
+struct alignas(16) PlanNodeRec {  // 32 B, one per plan node
+    uint32_t row;                 // snapshot row or kNone
+    uint32_t place_off, place_cnt;// plan allocs
+    uint32_t rm_off, rm_cnt;      // removed pool indices (sorted ascending)
+    uint32_t scratch_off;         // kNone: keys fit the wave's LDS buffer
+    uint32_t key_bound;           // upper bound of staged keys
+    uint32_t _pad;
+};
+static_assert(sizeof(PlanNodeRec) == 32, "PlanNodeRec is 32 bytes");
+
+constexpr uint32_t kLdsKeys = 512;   // per-wave LDS key buffer (4 KiB)
+constexpr int kWaves = 4;            // waves per workgroup
+
+struct PlanArgs {
+    const NodeRec* nodes;
+    const AllocRec* pool;            // snapshot allocs, grouped by node
+    const uint64_t* node_keys;
+    const uint64_t* pool_keys;
+    const PlanNodeRec* pn;
+    uint32_t n_plan;
+    const uint32_t* rm;              // removed pool indices
+    const AllocRec* pallocs;         // plan allocs
+    const uint64_t* pkeys;
+    uint64_t* scratch;
+    uint8_t* reason;
+    uint32_t* n_fit;
+};
+
+}  // namespace pa

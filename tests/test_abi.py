@@ -28,6 +28,7 @@ def test_every_declared_symbol_is_exported():
     for name in names:
         assert hasattr(lib, name), name
     assert set(abi.ENGINE_SYMBOLS) <= set(names)
+    assert set(abi.PLANNER_SYMBOLS) <= set(names)
 
 
 def test_abi_version():
@@ -38,7 +39,8 @@ def test_abi_version():
 
 STRUCTS = ["pe_strtab", "pe_attr", "pe_node_table", "pe_alloc_table", "pe_constraint", "pe_affinity",
            "pe_spread_target", "pe_spread", "pe_device_request", "pe_task", "pe_task_group", "pe_job",
-           "pe_config", "pe_select_options", "pe_ranked_node", "pe_placement"]
+           "pe_config", "pe_select_options", "pe_ranked_node", "pe_placement",
+           "pe_plan_node_table", "pe_plan_alloc_table", "pe_plan"]
 
 
 def test_struct_layouts_match_ctypes():
@@ -70,3 +72,12 @@ def test_engine_fails_loudly_without_gpu():
     h = lib.pe_stack_create(C.byref(cfg))
     assert not h
     assert b"no HIP device" in lib.pe_last_error(None)
+
+
+def test_planner_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from nomad_amd.plan import Planner, PlannerError
+    with pytest.raises(PlannerError):
+        Planner()
