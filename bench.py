@@ -26,6 +26,8 @@ BASELINE.json config (sections, --sections to choose):
               nodes whose GPUs are mostly held by priority-20 work
   c3_sharded  full-pass Selects over a 100k-node C3 cluster split across the
               ranks: one 80-byte record all-gather (RCCL) per placement
+  plan_apply  plan applier fit check (evaluatePlanPlacements) of a system-job plan
+              over a 100k-node snapshot, node ranges sharded over the ranks
 Each section times the engine on the GPU and the oracle (C++ restatement) on a
 bounded sample of the same workload on one host core.
 """
@@ -62,7 +64,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--sweep-nodes", type=int, default=1 << 24,
                    help="nodes of the scoring-sweep roofline measurement (0 = skip)")
-    p.add_argument("--sections", default="c3,c4,c5,c3_sharded",
+    p.add_argument("--sections", default="c3,c4,c5,c3_sharded,plan_apply",
                    help="comma list of extra config sections (empty = none)")
     return p.parse_args()
 
@@ -145,6 +147,17 @@ def cpu_baseline(nodes, allocs, job, seconds):
 # does not apply: 73 B) + 4 B (job,tg) collisions + 4 B visit rank = 76 B.
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "sweep_traffic.json")
 CHAIN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "chain_traffic.json")
+PLAN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "plan_traffic.json")
+
+
+def plan_traffic(bytes_per_launch):
+    """HBM bytes per k_plan_eval launch from the committed FETCH_SIZE / WRITE_SIZE
+    passes (tools/plan_prof.sh), when they were taken on this same workload."""
+    try:
+        d = json.load(open(PLAN_TRAFFIC_FILE))
+    except (OSError, ValueError):
+        return None
+    return d["bytes_per_launch"] if int(d["nodes"]) == int(bytes_per_launch) else None
 
 
 def chain_traffic(evals_per_launch):
@@ -422,6 +435,70 @@ def section_c3_sharded(device, rank, world, pg, placements=64):
                          % ("RCCL" if gdev is not None else "gloo, host memory"))}
 
 
+def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
+    """Plan applier fit check: a system-job plan placing one
+    alloc on every node of a 100k-node snapshot, evaluatePlanPlacements ->
+    evaluateNodePlan -> AllocsFit(checkDevices=true) per plan node. Plan nodes are
+    independent: each rank holds the contiguous node range it owns (state and
+    plan), no data-path collective."""
+    from nomad_amd import abi
+    from nomad_amd.plan import Plan, Planner
+    from nomad_amd.synth_plan import system_plan
+    nodes, allocs, plan = system_plan(n, seed=42)
+    lo, hi = rank * n // world, (rank + 1) * n // world
+    mine = {x.id for x in nodes[lo:hi]}
+    my_nodes = nodes[lo:hi]
+    my_allocs = [a for a in allocs if a.node_id in mine]
+    my_plan = Plan(node_allocation={k: v for k, v in plan.node_allocation.items() if k in mine})
+    pl = Planner(device)
+    t0 = time.perf_counter()
+    pl.set_state(my_nodes, my_allocs)
+    upload_s = time.perf_counter() - t0
+    ep = pl.encode(my_plan)
+    codes = pl.evaluate(ep)
+    walls, kms = [], []
+    for _ in range(reps):
+        barrier(pg)
+        t0 = time.perf_counter()
+        codes = pl.evaluate(ep)
+        dt = time.perf_counter() - t0
+        barrier(pg)
+        walls.append(reduce(pg, dt, lambda d: d.ReduceOp.MAX))
+        kms.append(reduce(pg, pl.kernel_ms(), lambda d: d.ReduceOp.MAX))
+    fit = int(reduce(pg, int((codes == abi.PE_PLAN_FIT).sum()), lambda d: d.ReduceOp.SUM))
+    wall = float(np.median(walls))
+    kms_med = float(np.median(kms))
+    bytes_launch = pl.last_bytes()
+    achieved = bytes_launch / (kms_med * 1e-3) / 1e9
+    out = {"workload": "system-job plan: 1 alloc on each of %d nodes (0-3 existing allocs, ports, 4-64 cores, "
+                       "40%% with GPUs), %d contiguous node shard(s)" % (n, world),
+           "scaling": "strong", "plan_nodes": n, "fit": fit,
+           "plan_nodes_per_s": n / (kms_med * 1e-3), "kernel_ms": kms_med,
+           "call_ms": wall * 1e3, "plan_nodes_per_s_call": n / wall,
+           "call_note": "call = host flattening of the plan's allocs + PCIe upload + kernel + reasons back",
+           "snapshot_upload_s": upload_s,
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": plan_traffic(bytes_launch) if world == 1 else None,
+                        "kernel": "k_plan_eval",
+                        "bytes_per_launch_rank0": bytes_launch,
+                        "bytes_note": "records and keys read + 1 reason byte per plan node (DESIGN.md §9)"}}
+    pl.close()
+    if cpu_s > 0 and rank == 0:
+        from oracle import plan_apply as O
+        snap = O.Snapshot(my_nodes, my_allocs)
+        ids = ep.node_ids
+        t0 = time.perf_counter()
+        k = 0
+        while k < len(ids) and time.perf_counter() - t0 < cpu_s:
+            O.evaluate_node_plan(snap, my_plan, ids[k])
+            k += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": k / dt, "unit": "plan nodes/s", "cores": 1, "kind": "port",
+                               "sample": "evaluateNodePlan on the first %d plan nodes in %.2f s (oracle/plan_apply.py, "
+                                         "Python restatement; Go toolchain unavailable)" % (k, dt)}
+    return out
+
+
 def main():
     args = parse()
     # Native libraries (gloo, RCCL) print banners on stdout; the contract is one
@@ -538,6 +615,8 @@ def main():
                 extra[sec] = section_c4(local, rank, world, pg, cpu_s)
             elif sec == "c3_sharded":
                 extra[sec] = section_c3_sharded(local, rank, world, pg)
+            elif sec == "plan_apply":
+                extra[sec] = section_plan_apply(local, rank, world, pg, cpu_s)
         except Exception as e:   # an extra section never takes the headline line down
             extra[sec] = {"error": "%s: %s" % (type(e).__name__, e)}
         barrier(pg)

@@ -138,7 +138,7 @@ struct pe_planner {
     std::vector<uint64_t> pool_keys;
 
     DBuf d_nodes, d_node_keys, d_pool, d_pool_keys;
-    DBuf d_pn, d_rm, d_pallocs, d_pkeys, d_scratch, d_reason;
+    DBuf d_pn, d_rm, d_pallocs, d_pkeys, d_big, d_scratch, d_reason;
 
     int fail(int code, const std::string& m) { err = m; return code; }
 
@@ -149,13 +149,26 @@ struct pe_planner {
         sid.emplace(s, id);
         return id;
     }
+    // Caller string id -> internal id. A caller that keeps one growing table
+    // (ids stable, strings appended) pays only for the new strings: the mapped
+    // prefix is recognised by comparing its offsets and bytes.
+    std::vector<uint32_t> xl_off;
+    std::string xl_bytes;
     int map_strings(const pe_strtab* t) {
-        xl.clear();
-        if (!t) return PE_OK;
+        if (!t) { xl.clear(); xl_off.clear(); xl_bytes.clear(); return PE_OK; }
         if (t->count && (!t->offsets || !t->bytes)) return fail(PE_EINVAL, "bad string table");
-        xl.resize(t->count);
-        for (uint32_t i = 0; i < t->count; i++)
-            xl[i] = intern(std::string(t->bytes + t->offsets[i], t->offsets[i + 1] - t->offsets[i]));
+        size_t keep = 0;
+        const size_t have = xl.size();
+        if (have && t->count >= have && memcmp(t->offsets, xl_off.data(), (have + 1) * 4) == 0 &&
+            memcmp(t->bytes, xl_bytes.data(), xl_bytes.size()) == 0)
+            keep = have;
+        xl.resize(keep);
+        xl.reserve(t->count);
+        for (uint32_t i = (uint32_t)keep; i < t->count; i++)
+            xl.push_back(intern(std::string(t->bytes + t->offsets[i], t->offsets[i + 1] - t->offsets[i])));
+        xl_off.assign(t->offsets, t->offsets + t->count + 1);
+        xl_bytes.assign(t->bytes, t->count ? t->offsets[t->count] : 0);
+        if (t->count == 0) xl_off.assign(1, 0);
         return PE_OK;
     }
     bool str(uint32_t caller, uint32_t* out) const {
@@ -186,9 +199,13 @@ struct pe_planner {
         h->disk = t->disk_mb ? t->disk_mb[i] : 0;
         h->bad_port = 0;
         h->keys.clear();
-        if (t->core_off) {   // Flattened.Cpu.ReservedCores is a set (cpuset union, structs.go:3711-3719)
-            std::set<uint32_t> cores(t->core_id + t->core_off[i], t->core_id + t->core_off[i + 1]);
-            for (uint32_t c : cores) h->keys.push_back(pa::make_key(pa::K_CORE_USED, c));
+        if (t->core_off && t->core_off[i + 1] > t->core_off[i]) {
+            // Flattened.Cpu.ReservedCores is a set (cpuset union, structs.go:3711-3719)
+            const size_t b = h->keys.size();
+            for (uint32_t j = t->core_off[i]; j < t->core_off[i + 1]; j++)
+                h->keys.push_back(pa::make_key(pa::K_CORE_USED, t->core_id[j]));
+            std::sort(h->keys.begin() + b, h->keys.end());
+            h->keys.erase(std::unique(h->keys.begin() + b, h->keys.end()), h->keys.end());
         }
         if (t->port_off) {
             for (uint32_t j = t->port_off[i]; j < t->port_off[i + 1]; j++) {
@@ -223,7 +240,10 @@ struct pe_planner {
         nd->key_off = (uint32_t)node_keys.size();
         if (t->core_off) {
             std::set<uint32_t> cores(t->core_id + t->core_off[r], t->core_id + t->core_off[r + 1]);
-            for (uint32_t c : cores) node_keys.push_back(pa::make_key(pa::K_CORE_AVAIL, c));
+            for (uint32_t c : cores) {
+                if (c < 64) nd->core_mask |= 1ull << c;
+                else node_keys.push_back(pa::make_key(pa::K_CORE_AVAIL, c));
+            }
             nd->has_cores = !cores.empty();
         }
         // SetNode: bitmaps per IP; `collide` is assigned (not or-ed) by the
@@ -408,7 +428,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     if (np && plan->place_off[np] > pt.count) return p->fail(PE_EINVAL, "place_off exceeds plan allocs");
 
     std::vector<pa::PlanNodeRec> pn(np);
-    std::vector<uint32_t> rm;
+    std::vector<uint32_t> rm, big;
     std::vector<pa::AllocRec> pa_recs(pt.count);
     std::vector<uint64_t> pkeys;
     HAlloc h;
@@ -459,6 +479,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
         }
         r.key_bound = (uint32_t)std::min<uint64_t>(bound, 0xFFFFFFFFull);
         if (bound > pa::kLdsKeys) {
+            big.push_back(i);
             r.scratch_off = (uint32_t)scratch;
             scratch += bound;
             if (scratch > 0xFFFFFFF0ull) return p->fail(PE_ENOMEM, "plan key scratch too large");
@@ -469,6 +490,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
         (e = p->upload(p->d_rm, rm.data(), rm.size() * 4)) != hipSuccess ||
         (e = p->upload(p->d_pallocs, pa_recs.data(), pa_recs.size() * sizeof(pa::AllocRec))) != hipSuccess ||
         (e = p->upload(p->d_pkeys, pkeys.data(), pkeys.size() * 8)) != hipSuccess ||
+        (e = p->upload(p->d_big, big.data(), big.size() * 4)) != hipSuccess ||
         (e = p->d_scratch.reserve(std::max<uint64_t>(scratch, 1) * 8)) != hipSuccess ||
         (e = p->d_reason.reserve(std::max<uint32_t>(np, 1))) != hipSuccess)
         return p->fail(PE_EHIP, std::string("planner plan upload: ") + hipGetErrorString(e));
@@ -483,6 +505,8 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     a.pallocs = (const pa::AllocRec*)p->d_pallocs.p;
     a.pkeys = (const uint64_t*)p->d_pkeys.p;
     a.scratch = (uint64_t*)p->d_scratch.p;
+    a.big = (const uint32_t*)p->d_big.p;
+    a.n_big = (uint32_t)big.size();
     a.reason = (uint8_t*)p->d_reason.p;
     if ((e = hipEventRecord(p->e0, p->stream)) != hipSuccess || (e = pe_launch_plan_eval(&a, p->stream)) != hipSuccess ||
         (e = hipEventRecord(p->e1, p->stream)) != hipSuccess ||

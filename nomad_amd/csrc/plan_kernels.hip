@@ -1,21 +1,28 @@
 // Plan applier fit check on gfx950: evaluateNodePlan (nomad/plan_apply.go:611-674)
 // → AllocsFit(node, proposed, nil, checkDevices=true) (nomad/structs/funcs.go:148-211)
-// for every node of a plan, one wavefront per plan node, four per workgroup.
+// for every node of a plan.
 //
-// Per plan node the wave
+// k_plan_eval      a group of 16 lanes per plan node, four nodes per wavefront,
+//                  keys staged in a 1 KiB per-node LDS buffer (ds_* only).
+// k_plan_eval_big  one wavefront per plan node whose key bound exceeds that
+//                  buffer (nodes with hundreds of cores / ports), keys staged in
+//                  global scratch. Rare; listed by the host.
+//
+// Per plan node a group
 //   1. applies the node checks in the reference's order (evict-only plan ⇒ fit,
 //      plan_apply.go:614-616; missing / not ready / ineligible, :627-633);
 //   2. walks the node's snapshot allocs (contiguous 32-byte records) minus the
 //      plan's removals (binary search in the node's sorted removal list;
 //      RemoveAllocs, funcs.go:47-64) plus the plan's allocs, skipping terminal
 //      ones, and sums cpu / memory / disk (ComparableResources.Add);
-//   3. stages the static node keys and the counted allocs' keys into a
-//      wave-private LDS buffer (global scratch when a node exceeds it) and runs
-//      one pairwise pass that answers core overlap, core subset, port collision
-//      and device oversubscription together (plan_types.h);
+//   3. folds held cores with id < 64 into an LDS mask with atomicOr (overlap =
+//      a bit already set, funcs.go:166-175; subset test against the node's
+//      available-core mask, structs.go:3896-3898), stages every other key and
+//      runs one pairwise pass that answers the remaining core, port-collision
+//      and device-oversubscription questions together (plan_types.h);
 //   4. writes the first failing dimension in AllocsFit order.
-// HBM-bound integer work: no MFMA. Bytes per plan node are the records and keys
-// read plus one reason byte (pe_planner_last_bytes).
+// HBM/latency-bound integer work: no MFMA. Bytes per plan node are the records
+// and keys read plus one reason byte (pe_planner_last_bytes).
 #include <hip/hip_runtime.h>
 #include "../../include/nomad_pe.h"
 #include "plan_types.h"
@@ -34,13 +41,21 @@ __device__ __forceinline__ void wave_sync_global() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
 }
 
-__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
-    for (int off = 32; off > 0; off >>= 1) {
+template <int G>
+__device__ __forceinline__ int64_t group_sum64(int64_t v) {
+    for (int off = G / 2; off > 0; off >>= 1) {
         const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, off);
         const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)v >> 32), off);
         v += (int64_t)((uint64_t)hi << 32 | lo);
     }
     return v;
+}
+
+template <int G>
+__device__ __forceinline__ bool group_any(bool x, uint32_t lane) {
+    const uint64_t m = __ballot(x);
+    if (G == 64) return m != 0;
+    return ((m >> (lane & ~(uint32_t)(G - 1))) & ((1ull << (G & 63)) - 1)) != 0;
 }
 
 __device__ __forceinline__ bool removed(const uint32_t* rm, uint32_t n, uint32_t q) {
@@ -54,76 +69,91 @@ __device__ __forceinline__ bool removed(const uint32_t* rm, uint32_t n, uint32_t
     return false;
 }
 
-// Stage one counted alloc: sums and keys.
-__device__ __forceinline__ void take(const AllocRec& ar, const uint64_t* keys, uint64_t* buf, uint32_t* fill,
-                                     int64_t& cpu, int64_t& mem, int64_t& disk, bool& bad) {
-    cpu += ar.cpu;
-    mem += ar.mem;
-    disk += ar.disk;
-    bad |= ar.bad_port != 0;
-    if (ar.n_keys) {
-        const uint32_t base = atomicAdd(fill, (uint32_t)ar.n_keys);
-        for (uint32_t k = 0; k < ar.n_keys; k++) buf[base + k] = keys[ar.key_off + k];
+struct Acc {
+    int64_t cpu = 0, mem = 0, disk = 0;
+    bool bad = false, core_dup = false, core_missing = false;
+};
+
+// Stage one counted alloc: sums, masked cores, keys.
+template <typename Buf>
+__device__ __forceinline__ void take(const AllocRec& ar, const uint64_t* keys, Buf buf, uint32_t* fill,
+                                     unsigned long long* cmask, uint64_t node_mask, Acc& acc) {
+    acc.cpu += ar.cpu;
+    acc.mem += ar.mem;
+    acc.disk += ar.disk;
+    acc.bad |= ar.bad_port != 0;
+    if (!ar.n_keys) return;
+    const uint32_t base = atomicAdd(fill, (uint32_t)ar.n_keys);
+    for (uint32_t k = 0; k < ar.n_keys; k++) {
+        uint64_t key = keys[ar.key_off + k];
+        const uint64_t v = key & kValMask;
+        if ((uint32_t)(key >> 60) == K_CORE_USED && v < 64) {
+            const unsigned long long bit = 1ull << v;
+            const unsigned long long old = atomicOr(cmask, bit);
+            acc.core_dup |= (old & bit) != 0;
+            acc.core_missing |= (node_mask & bit) == 0;
+            key = kHole;
+        }
+        buf[base + k] = key;
     }
 }
 
-__device__ uint8_t fit_node(const PlanArgs& a, const PlanNodeRec& pn, const NodeRec& nd, uint32_t lane,
-                            uint64_t* lds_buf, uint32_t* fill) {
-    const bool global = pn.scratch_off != kNone;
-    uint64_t* buf = global ? a.scratch + pn.scratch_off : lds_buf;
-    for (uint32_t i = lane; i < nd.n_keys; i += 64) buf[i] = a.node_keys[nd.key_off + i];
-    if (lane == 0) *fill = nd.n_keys;
+template <int G, bool GLOBAL, typename Buf>
+__device__ __forceinline__ uint8_t fit_node(const PlanArgs& a, const PlanNodeRec& pn, const NodeRec& nd,
+                                            uint32_t lane, Buf buf, uint32_t* fill, unsigned long long* cmask) {
+    const uint32_t gl = lane & (G - 1);
+    for (uint32_t i = gl; i < nd.n_keys; i += G) buf[i] = a.node_keys[nd.key_off + i];
+    if (gl == 0) { *fill = nd.n_keys; *cmask = 0; }
     wave_sync_lds();
 
-    int64_t cpu = 0, mem = 0, disk = 0;
-    bool bad = false;
+    Acc acc;
     const uint32_t* rm = a.rm + pn.rm_off;
-    for (uint32_t i = lane; i < nd.alloc_cnt; i += 64) {
+    for (uint32_t i = gl; i < nd.alloc_cnt; i += G) {
         const uint32_t q = nd.alloc_off + i;
         const AllocRec ar = a.pool[q];
         if (ar.terminal || (pn.rm_cnt && removed(rm, pn.rm_cnt, q))) continue;
-        take(ar, a.pool_keys, buf, fill, cpu, mem, disk, bad);
+        take(ar, a.pool_keys, buf, fill, cmask, nd.core_mask, acc);
     }
-    for (uint32_t i = lane; i < pn.place_cnt; i += 64) {
+    for (uint32_t i = gl; i < pn.place_cnt; i += G) {
         const AllocRec ar = a.pallocs[pn.place_off + i];
         if (ar.terminal) continue;
-        take(ar, a.pkeys, buf, fill, cpu, mem, disk, bad);
+        take(ar, a.pkeys, buf, fill, cmask, nd.core_mask, acc);
     }
-    if (global) wave_sync_global(); else wave_sync_lds();
+    if (GLOBAL) wave_sync_global(); else wave_sync_lds();
     const uint32_t k = *fill;
-    cpu = wave_sum64(cpu);
-    mem = wave_sum64(mem);
-    disk = wave_sum64(disk);
-    bad = __ballot(bad) != 0;
+    const int64_t cpu = group_sum64<G>(acc.cpu);
+    const int64_t mem = group_sum64<G>(acc.mem);
+    const int64_t disk = group_sum64<G>(acc.disk);
 
     // One pairwise pass: for each staged key, look for an earlier equal key of
     // the same kind (a second holder) and for its AVAIL / NODE twin (kind + 1).
-    bool core_dup = false, core_missing = false, port_hit = false, dev_dup = false;
-    const uint32_t trips = (k + 63) & ~63u;
-    for (uint32_t i = lane; i < trips; i += 64) {
+    bool port_hit = false, dev_dup = false;
+    const uint32_t trips = (k + G - 1) & ~(uint32_t)(G - 1);
+    for (uint32_t i = gl; i < trips; i += G) {
         const bool valid = i < k;
-        const uint64_t x = valid ? buf[i] : ~0ull;
+        const uint64_t x = valid ? buf[i] : kHole;
         const uint32_t kx = (uint32_t)(x >> 60);
         const uint64_t vx = x & kValMask;
-        bool dupe = false, twin = false;
-        if (valid && (kx & 1u) == 0) {
+        if ((kx & 1u) == 0) {
+            bool dupe = false, twin = false;
+#pragma unroll 4
             for (uint32_t j = 0; j < k; j++) {
                 const uint64_t y = buf[j];
-                if ((y & kValMask) == vx) {
-                    const uint32_t ky = (uint32_t)(y >> 60);
-                    dupe |= (ky == kx) & (j < i);
-                    twin |= ky == kx + 1;
-                }
+                const bool eq = (y & kValMask) == vx;
+                const uint32_t ky = (uint32_t)(y >> 60);
+                dupe |= eq & (ky == kx) & (j < i);
+                twin |= eq & (ky == kx + 1);
             }
-            if (kx == K_CORE_USED) { core_dup |= dupe; core_missing |= !twin; }
+            if (kx == K_CORE_USED) { acc.core_dup |= dupe; acc.core_missing |= !twin; }
             else if (kx == K_PORT_USED) port_hit |= dupe | twin;
             else if (kx == K_DEV_USED) dev_dup |= dupe & twin;
         }
     }
-    core_dup = __ballot(core_dup) != 0;
-    core_missing = __ballot(core_missing) != 0;
-    port_hit = __ballot(port_hit) != 0;
-    dev_dup = __ballot(dev_dup) != 0;
+    const bool core_dup = group_any<G>(acc.core_dup, lane);
+    const bool core_missing = group_any<G>(acc.core_missing, lane);
+    const bool bad = group_any<G>(acc.bad, lane);
+    port_hit = group_any<G>(port_hit, lane);
+    dev_dup = group_any<G>(dev_dup, lane);
 
     // AllocsFit order (funcs.go:173-208, Superset structs.go:3891-3905)
     if (core_dup) return PE_PLAN_CORES;
@@ -136,24 +166,45 @@ __device__ uint8_t fit_node(const PlanArgs& a, const PlanNodeRec& pn, const Node
     return PE_PLAN_FIT;
 }
 
+// Node checks ahead of AllocsFit; returns true when the fit check must run.
+__device__ __forceinline__ bool precheck(const PlanArgs& a, const PlanNodeRec& pn, NodeRec* nd, uint8_t* r) {
+    if (pn.place_cnt == 0) { *r = PE_PLAN_FIT; return false; }            // evict-only (plan_apply.go:614-616)
+    if (pn.row == kNone) { *r = PE_PLAN_NODE_MISSING; return false; }
+    *nd = a.nodes[pn.row];
+    if (!nd->ready) { *r = PE_PLAN_NODE_NOT_READY; return false; }
+    if (!nd->eligible) { *r = PE_PLAN_NODE_INELIGIBLE; return false; }
+    return true;
+}
+
 __global__ void __launch_bounds__(64 * kWaves) k_plan_eval(PlanArgs a) {
-    __shared__ uint64_t lds_keys[kWaves][kLdsKeys];
-    __shared__ uint32_t fill[kWaves];
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t p = blockIdx.x * kWaves + w;
-    if (p >= a.n_plan) return;   // whole wave exits; no workgroup barrier below
+    __shared__ uint64_t lds_keys[kNodesPerBlock][kLdsKeys];
+    __shared__ uint32_t fill[kNodesPerBlock];
+    __shared__ unsigned long long cmask[kNodesPerBlock];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t slot = threadIdx.x / kGroup;
+    const uint32_t first = blockIdx.x * kNodesPerBlock + (threadIdx.x >> 6) * (64 / kGroup);
+    if (first >= a.n_plan) return;   // whole wave idle; no workgroup barrier below
+    const uint32_t p = blockIdx.x * kNodesPerBlock + slot;
+    if (p >= a.n_plan) return;       // group-uniform: the group's lanes leave together
     const PlanNodeRec pn = a.pn[p];
+    if (pn.scratch_off != kNone) return;   // k_plan_eval_big
+    NodeRec nd;
     uint8_t r;
-    if (pn.place_cnt == 0) {
-        r = PE_PLAN_FIT;                       // evict-only (plan_apply.go:614-616)
-    } else if (pn.row == kNone) {
-        r = PE_PLAN_NODE_MISSING;
-    } else {
-        const NodeRec nd = a.nodes[pn.row];
-        if (!nd.ready) r = PE_PLAN_NODE_NOT_READY;
-        else if (!nd.eligible) r = PE_PLAN_NODE_INELIGIBLE;
-        else r = fit_node(a, pn, nd, lane, lds_keys[w], &fill[w]);
-    }
+    if (precheck(a, pn, &nd, &r))
+        r = fit_node<kGroup, false>(a, pn, nd, lane, lds_keys[slot], &fill[slot], &cmask[slot]);
+    if ((lane & (kGroup - 1)) == 0) a.reason[p] = r;
+}
+
+__global__ void __launch_bounds__(64) k_plan_eval_big(PlanArgs a) {
+    __shared__ uint32_t fill;
+    __shared__ unsigned long long cmask;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t p = a.big[blockIdx.x];
+    const PlanNodeRec pn = a.pn[p];
+    NodeRec nd;
+    uint8_t r;
+    if (precheck(a, pn, &nd, &r))
+        r = fit_node<64, true>(a, pn, nd, lane, a.scratch + pn.scratch_off, &fill, &cmask);
     if (lane == 0) a.reason[p] = r;
 }
 
@@ -161,7 +212,8 @@ __global__ void __launch_bounds__(64 * kWaves) k_plan_eval(PlanArgs a) {
 
 hipError_t pe_launch_plan_eval(const pa::PlanArgs* a, hipStream_t st) {
     if (a->n_plan == 0) return hipSuccess;
-    const uint32_t blocks = (a->n_plan + pa::kWaves - 1) / pa::kWaves;
+    const uint32_t blocks = (a->n_plan + pa::kNodesPerBlock - 1) / pa::kNodesPerBlock;
     hipLaunchKernelGGL(pa::k_plan_eval, dim3(blocks), dim3(64 * pa::kWaves), 0, st, *a);
+    if (a->n_big) hipLaunchKernelGGL(pa::k_plan_eval_big, dim3(a->n_big), dim3(64), 0, st, *a);
     return hipGetLastError();
 }

@@ -33,14 +33,16 @@ constexpr uint64_t kValMask = (1ull << 60) - 1;
 
 __host__ __device__ inline uint64_t make_key(uint32_t kind, uint64_t v) { return (uint64_t)kind << 60 | (v & kValMask); }
 
-struct alignas(16) NodeRec {      // 48 B, one per snapshot node
+struct alignas(16) NodeRec {      // 64 B, one per snapshot node
     int64_t cpu, mem, disk;       // NodeResources − ReservedResources (funcs.go:180-181)
-    uint32_t key_off, n_keys;     // static keys: available cores, reserved ports, healthy instances
+    uint64_t core_mask;           // available cores with id < 64 (ids >= 64 are K_CORE_AVAIL keys)
+    uint32_t key_off, n_keys;     // static keys: cores >= 64, reserved ports, healthy instances
     uint32_t alloc_off, alloc_cnt;// contiguous snapshot allocs of this node in the pool
     uint32_t alloc_keys;          // Σ keys of those allocs (sizes the scratch fallback)
     uint8_t ready, eligible, setnode_collide, has_cores;
+    uint32_t _pad[2];
 };
-static_assert(sizeof(NodeRec) == 48, "NodeRec is 48 bytes");
+static_assert(sizeof(NodeRec) == 64, "NodeRec is 64 bytes");
 
 struct alignas(16) AllocRec {     // 32 B, snapshot pool entry or plan alloc
     int64_t cpu, mem, disk;
@@ -61,8 +63,14 @@ struct alignas(16) PlanNodeRec {  // 32 B, one per plan node
 };
 static_assert(sizeof(PlanNodeRec) == 32, "PlanNodeRec is 32 bytes");
 
-constexpr uint32_t kLdsKeys = 512;   // per-wave LDS key buffer (4 KiB)
-constexpr int kWaves = 4;            // waves per workgroup
+// k_plan_eval: a group of kGroup lanes per plan node (4 nodes per wavefront),
+// keys staged in a per-node LDS buffer of kLdsKeys; plan nodes whose key bound
+// exceeds it go to k_plan_eval_big (one wavefront each, global scratch).
+constexpr int kGroup = 16;
+constexpr int kWaves = 4;                               // waves per workgroup
+constexpr int kNodesPerBlock = kWaves * (64 / kGroup);
+constexpr uint32_t kLdsKeys = 128;                      // 1 KiB per plan node
+constexpr uint64_t kHole = ~0ull;                       // staged slot of a masked core (kind 15)
 
 struct PlanArgs {
     const NodeRec* nodes;
@@ -75,8 +83,9 @@ struct PlanArgs {
     const AllocRec* pallocs;         // plan allocs
     const uint64_t* pkeys;
     uint64_t* scratch;
+    const uint32_t* big;             // plan nodes past the LDS budget
+    uint32_t n_big;
     uint8_t* reason;
-    uint32_t* n_fit;
 };
 
 }  // namespace pa

@@ -286,10 +286,11 @@ def encode_allocs(allocs: Sequence[PlanAlloc], it: Interner, rows: Optional[Sequ
 class EncodedPlan:
     """A Plan flattened against a snapshot (node rows, snapshot alloc indices)."""
 
-    def __init__(self, plan: Plan, row_of: Dict[str, int], alloc_index: Dict[str, int]):
+    def __init__(self, plan: Plan, row_of: Dict[str, int], alloc_index: Dict[str, int],
+                 interner: Optional[Interner] = None):
         self.plan = plan
         self.node_ids = plan.node_ids()
-        it = Interner()
+        it = interner if interner is not None else Interner()
         rows, rm_items, placed = [], [], []
         for nid in self.node_ids:
             rows.append(row_of.get(nid, abi.PE_NONE))
@@ -350,7 +351,9 @@ class Planner:
         self.row_of = {n.id: i for i, n in enumerate(self.nodes)}
         self.allocs = list(allocs)
         self.alloc_index = {a.id: i for i, a in enumerate(self.allocs)}
-        it = Interner()
+        # one growing string table for the snapshot and every later plan: the
+        # library then maps only the strings a call adds
+        self.interner = it = Interner()
         nt, nk = encode_nodes(self.nodes, it)
         at, ak = encode_allocs(self.allocs, it, [self.row_of[a.node_id] for a in self.allocs])
         st, sk = it.table()
@@ -361,7 +364,7 @@ class Planner:
         return None if j is None else self.allocs[j]
 
     def encode(self, plan: Plan) -> EncodedPlan:
-        return EncodedPlan(plan, self.row_of, self.alloc_index)
+        return EncodedPlan(plan, self.row_of, self.alloc_index, self.interner)
 
     def evaluate(self, ep: EncodedPlan) -> np.ndarray:
         """Per-node PE_PLAN_* codes in ep.node_ids order (one kernel launch)."""
