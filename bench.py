@@ -442,14 +442,11 @@ def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
     independent: each rank holds the contiguous node range it owns (state and
     plan), no data-path collective."""
     from nomad_amd import abi
-    from nomad_amd.plan import Plan, Planner
+    from nomad_amd.plan import Planner
     from nomad_amd.synth_plan import system_plan
+    from nomad_amd.shard import shard_plan
     nodes, allocs, plan = system_plan(n, seed=42)
-    lo, hi = rank * n // world, (rank + 1) * n // world
-    mine = {x.id for x in nodes[lo:hi]}
-    my_nodes = nodes[lo:hi]
-    my_allocs = [a for a in allocs if a.node_id in mine]
-    my_plan = Plan(node_allocation={k: v for k, v in plan.node_allocation.items() if k in mine})
+    my_nodes, my_allocs, my_plan = shard_plan(nodes, allocs, plan, rank, world)
     pl = Planner(device)
     t0 = time.perf_counter()
     pl.set_state(my_nodes, my_allocs)

@@ -90,3 +90,26 @@ def system_place_sharded(stack, rows: Sequence[int], rank: int, world: int, tg=0
     stack.SetNodes(rows[b:e])
     score, status, placed = stack.SystemPlace(tg)
     return b, e, score, status, placed
+
+
+def shard_plan(nodes, allocs, plan, rank: int, world: int):
+    """Plan applier (plan_apply.go:439-582) over GPUs: evaluateNodePlan is
+    independent per node, so each rank owns a contiguous range of the node
+    list, holds only those nodes and their allocs as its resident snapshot, and
+    evaluates the plan nodes that fall in it. Plan nodes outside every range
+    (nodes that do not exist) go to the last rank. No data-path collective:
+    the per-node outcomes are concatenated by whoever assembles the PlanResult.
+    Returns (nodes, allocs, plan) of this rank."""
+    from .plan import Plan
+    b, e = shard_range(len(nodes), rank, world)
+    mine = {n.id for n in nodes[b:e]}
+    known = {n.id for n in nodes}
+
+    def owns(nid):
+        return nid in mine or (rank == world - 1 and nid not in known)
+
+    sub = Plan(node_update={k: v for k, v in plan.node_update.items() if owns(k)},
+               node_allocation={k: v for k, v in plan.node_allocation.items() if owns(k)},
+               node_preemptions={k: v for k, v in plan.node_preemptions.items() if owns(k)},
+               all_at_once=plan.all_at_once)
+    return nodes[b:e], [a for a in allocs if a.node_id in mine], sub

@@ -146,3 +146,41 @@ def test_engine_shard_records_match_select(shards):
             break
         a.Commit(0, x.row)
         b.Commit(0, y.row)
+
+
+def _plan_worker(rank, world, port, q):
+    from nomad_amd.plan import assemble_result
+    from nomad_amd.synth_plan import random_case
+    from oracle import plan_apply as O
+    _init(rank, world, port)
+    nodes, allocs, plan = random_case(31, n_nodes=40)
+    my_nodes, my_allocs, my_plan = shard.shard_plan(nodes, allocs, plan, rank, world)
+    snap = O.Snapshot(my_nodes, my_allocs)
+    ids, fits, why = O.evaluate_plan_placements(snap, my_plan)
+    got = [None] * world
+    dist.all_gather_object(got, list(zip(ids, fits, why)))
+    if rank == 0:
+        q.put(got)
+    dist.destroy_process_group()
+
+
+def test_plan_apply_sharded_equals_single():
+    """Plan applier over 2 gloo ranks (contiguous node ranges, no collective on
+    the data path) gives the same per-node outcomes as one process."""
+    from oracle import plan_apply as O
+    from nomad_amd.synth_plan import random_case
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    merged = {nid: (fit, why) for part in got for nid, fit, why in part}
+    nodes, allocs, plan = random_case(31, n_nodes=40)
+    ids, fits, why = O.evaluate_plan_placements(O.Snapshot(nodes, allocs), plan)
+    assert merged == {nid: (f, w) for nid, f, w in zip(ids, fits, why)}
+    assert sum(len(part) for part in got) == len(ids)
