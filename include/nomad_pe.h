@@ -327,6 +327,17 @@ double pe_last_kernel_ms(const pe_stack* s);
 /* Algorithmic HBM bytes per node of the last full-scan sweep Select (73 with
  * the verdict byte, 76 with the folded per-node score word), 0 if none ran. */
 uint32_t pe_last_sweep_bytes(const pe_stack* s);
+/* AllocMetric maps (structs.go:9826-10026) of Selects: ClassFiltered,
+ * ConstraintFiltered, ClassExhausted, DimensionExhausted — what
+ * `ctx.Metrics()` holds after GenericStack.Select (FilterNode / ExhaustedNode,
+ * structs.go:9907-9937). Off by default; switch on before the first Select of
+ * an evaluation (the maps depend on the EvalEligibility memo history).
+ * Available for plain Selects (no preferred nodes, no Preempt). */
+int pe_set_metrics(pe_stack* s, int on);
+/* The last Select's maps as text lines "KIND\tKEY\tCOUNT\n", KIND one of
+ * CF / KF / CE / DE, keys sorted. Writes at most cap bytes (NUL-terminated) and
+ * returns the bytes needed, or PE_ESTATE when the last Select has none. */
+int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap);
 /* Host-side constraint semantics used for pre-resolution (checkConstraint,
  * feasible.go:785-820), exposed for known-answer tests; needs no device.
  * l_state / r_state: 0 nil (unknown ${...} target), 1 found, 2 missing ("", false). */

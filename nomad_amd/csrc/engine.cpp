@@ -65,6 +65,8 @@ uint32_t pe_chain_max_limit();
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n);
 int pe_chain_blocks_per_cu(size_t lds);
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st);
+hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
+                           uint32_t n, uint32_t* out, hipStream_t st);
 
 namespace {
 
@@ -196,6 +198,7 @@ struct ParsedConstraint {
     ParsedTarget l, r;
     std::string op;
     bool escapes;
+    std::string ltext, text;   // LTarget, Constraint.String() "l op r" (structs.go:8292)
 };
 
 struct ParsedAffinity {
@@ -221,6 +224,7 @@ struct PsetDev {
     bool per_node = false;
     bool distinct = false;         // distinct_property set (filter) instead of a spread (score)
     uint32_t allowed = 1;
+    std::string target_text;       // LTarget of the distinct_property constraint (metrics reasons)
 };
 
 struct TgPlan {
@@ -362,6 +366,15 @@ struct pe_stack {
     std::map<uint32_t, std::vector<int8_t>> tg_memo;
     std::vector<int8_t> job_memo;
 
+    // AllocMetric maps (pe_set_metrics): the memo as the reference chain has
+    // seen it so far (classes become known only when one of their nodes is
+    // visited), and the last Select's maps as text
+    bool metrics_on = false, metrics_valid = false;
+    std::map<uint32_t, std::vector<int8_t>> ref_tg_memo;
+    std::vector<int8_t> ref_job_memo;
+    std::string metrics_text;
+    DevMem d_trace_rows, d_trace_out;
+
     // visit order
     std::vector<uint32_t> visit;
     DevMem d_visit, d_pref, d_penalty, d_out, d_status;
@@ -485,6 +498,8 @@ ParsedConstraint parse_constraint(const pe_stack* s, const pe_constraint& c) {
     p.r = parse_target(s, s->S(c.rtarget));
     p.op = s->S(c.operand);
     p.escapes = p.l.escapes || p.r.escapes;
+    p.ltext = s->S(c.ltarget);
+    p.text = p.ltext + " " + p.op + " " + s->S(c.rtarget);
     return p;
 }
 
@@ -642,41 +657,54 @@ int build_dev_classes(pe_stack* s, TgPlan& g) {
 }
 
 // job checkers (ConstraintChecker over job constraints)
+// First failing job checker's FilterNode reason, or nullptr (feasible).
+const char* job_fail(const pe_stack* s, pe::ConstraintEvaluator& ev, const NodeView& n) {
+    for (auto& c : s->job_constraints) if (!meets(s, ev, c, n)) return c.text.c_str();
+    return nullptr;
+}
+
 bool job_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const NodeView& n) {
-    for (auto& c : s->job_constraints) if (!meets(s, ev, c, n)) return false;
-    return true;
+    return job_fail(s, ev, n) == nullptr;
 }
 
 // tg checkers in GenericStack/SystemStack order: drivers, constraints, host
 // volumes, devices, network (stack.go:241-247, 374-380)
-bool tg_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g, const NodeView& n) {
+// First failing task-group checker's FilterNode reason (feasible.go:353, 378,
+// 467, 539-556, ConstraintChecker: Constraint.String()), or nullptr.
+const char* tg_fail(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g, const NodeView& n) {
+    static const char* kDrivers = "missing drivers";
+    static const char* kVolumes = "missing compatible host volumes";
+    static const char* kDevices = "missing devices";
+    static const char* kNetwork = "missing network";
+    static const char* kHostNet = "missing host network";
+    static const char* kBadHostNet = "invalid host network";
     for (uint32_t d : g.drivers) {   // DriverChecker.hasDrivers (feasible.go:462-500)
         auto it = std::lower_bound(n.drivers.begin(), n.drivers.end(), std::make_pair(d, (uint8_t)0));
         if (it != n.drivers.end() && it->first == d) {
             const uint8_t f = it->second;
-            if (f & 4) return false;
+            if (f & 4) return kDrivers;
             if ((f & 1) && (f & 2)) continue;
-            return false;
+            return kDrivers;
         }
         uint32_t key = s->lookup("driver." + s->S(d)), val;
-        if (key == PE_NONE || !find_kv(n.attrs, key, &val)) return false;
+        if (key == PE_NONE || !find_kv(n.attrs, key, &val)) return kDrivers;
         const std::string& v = s->S(val);
         if (v == "1" || v == "t" || v == "T" || v == "true" || v == "TRUE" || v == "True") continue;
-        return false;   // "0"/false or ParseBool error
+        return kDrivers;   // "0"/false or ParseBool error
     }
-    for (auto& c : g.constraints) if (!meets(s, ev, c, n)) return false;
+    for (auto& c : g.constraints) if (!meets(s, ev, c, n)) return c.text.c_str();
     if (!g.volumes.empty()) {   // HostVolumeChecker.hasVolumes (feasible.go:171-207)
         std::map<uint32_t, std::vector<bool>> req;
         for (auto& v : g.volumes) req[v.first].push_back(v.second);
-        if (req.size() > n.volumes.size()) return false;
+        if (req.size() > n.volumes.size()) return kVolumes;
         for (auto& kv : req) {
             auto it = std::lower_bound(n.volumes.begin(), n.volumes.end(), std::make_pair(kv.first, (uint8_t)0));
-            if (it == n.volumes.end() || it->first != kv.first) return false;
+            if (it == n.volumes.end() || it->first != kv.first) return kVolumes;
             if (!it->second) continue;
-            for (bool ro : kv.second) if (!ro) return false;
+            for (bool ro : kv.second) if (!ro) return kVolumes;
         }
     }
-    if (!has_devices(s, ev, g, n.row)) return false;
+    if (!has_devices(s, ev, g, n.row)) return kDevices;
     {   // NetworkChecker (feasible.go:362-429): runs for every task group; without a
         // tg network it keeps the mode of the last one set (default "host").
         const std::string want = s->S(g.net_mode).empty() ? std::string("host") : s->S(g.net_mode);
@@ -696,17 +724,21 @@ bool tg_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g
                     legacy = pre_ok && pe::compare_versions(v, c) == -1;
                 }
             }
-            if (!legacy) return false;
+            if (!legacy) return kNetwork;
         } else if (g.net_ports > 0) {
             // hasHostNetworks: every port's host network must be an alias on the node
             ParsedTarget hn = parse_target(s, s->S(g.net_host));
             Target t = resolve(s, hn, n);
-            if (!t.found) return false;
+            if (!t.found) return kBadHostNet;
             uint32_t want_id = s->lookup(t.value);
-            if (std::find(n.aliases.begin(), n.aliases.end(), want_id) == n.aliases.end()) return false;
+            if (std::find(n.aliases.begin(), n.aliases.end(), want_id) == n.aliases.end()) return kHostNet;
         }
     }
-    return true;
+    return nullptr;
+}
+
+bool tg_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g, const NodeView& n) {
+    return tg_fail(s, ev, g, n) == nullptr;
 }
 
 // AllocatedResources.Comparable() with lifecycle rules (structs.go:3445-3487)
@@ -1118,6 +1150,7 @@ int build_psets(pe_stack* s, TgPlan& g) {
         auto ps = std::make_unique<PsetDev>();
         ps->distinct = true;
         ps->target = c.l;
+        ps->target_text = c.ltext;
         ps->per_node = ps->target.escapes || ps->target.kind == T_ID || ps->target.kind == T_NAME;
         // RTarget: strconv.ParseUint, default 1; unparsable -> every node filtered
         ps->allowed = 1;
@@ -1944,6 +1977,8 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
     s->plan.clear();
     s->tg_memo.clear();
     s->job_memo.clear();
+    s->ref_tg_memo.clear();
+    s->ref_job_memo.clear();
     s->spread_info_done.clear();
     s->sum_spread_weights = 0;
     int rc = build_state(s, nodes, allocs);
@@ -1975,6 +2010,8 @@ int pe_reset_plan(pe_stack* s) {
     s->plan.clear();
     s->tg_memo.clear();
     s->job_memo.clear();
+    s->ref_tg_memo.clear();
+    s->ref_job_memo.clear();
     s->spread_info_done.clear();
     s->sum_spread_weights = 0;
     s->have_job = false;
@@ -2161,6 +2198,124 @@ static uint32_t pack_offers(const pe_ranked_node* out) {
 
 static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out);
 
+// AllocMetric maps of one plain Select (structs.go:9903-9937): the rows the
+// chain pulled (visit order from the Select's cursor), FeasibilityWrapper
+// reasons from the host-side checkers with the reference's memo transitions
+// (feasible.go:1061-1153), every later reason from k_trace on the device.
+static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
+                           uint32_t evaluated) {
+    s->metrics_valid = false;
+    const size_t m = order.size();
+    std::map<std::string, int> cf, kf, ce, de;
+    auto filter = [&](uint32_t row, const std::string& why) {
+        const uint32_t nc = s->nodes[row].node_class;
+        if (nc != PE_NONE && !s->S(nc).empty()) cf[s->S(nc)]++;
+        if (!why.empty()) kf[why]++;
+    };
+    auto exhaust = [&](uint32_t row, const std::string& dim) {
+        const uint32_t nc = s->nodes[row].node_class;
+        if (nc != PE_NONE && !s->S(nc).empty()) ce[s->S(nc)]++;
+        if (!dim.empty()) de[dim]++;
+    };
+    if (s->ref_job_memo.size() != s->ncls) s->ref_job_memo.assign(s->ncls, -1);
+    auto& rt = s->ref_tg_memo[g.name];
+    if (rt.size() != s->ncls) rt.assign(s->ncls, -1);
+    pe::ConstraintEvaluator ev;
+    std::vector<uint32_t> rows;
+    static const char* kIneligible = "computed class ineligible";
+    for (uint32_t k = 0; k < evaluated && m; k++) {
+        const uint32_t row = order[(start + k) % m];
+        const NodeView v = s->view(row);
+        const uint32_t c = s->nodes[row].cls;
+        const char* why = nullptr;
+        if (s->job_escaped) {
+            why = job_fail(s, ev, v);
+        } else if (s->ref_job_memo[c] == 0) {
+            why = kIneligible;
+        } else {
+            why = job_fail(s, ev, v);
+            if (why) s->ref_job_memo[c] = 0;
+            else if (s->ref_job_memo[c] == -1) s->ref_job_memo[c] = 1;
+        }
+        if (!why) {
+            if (g.escaped) {
+                why = tg_fail(s, ev, g, v);
+            } else if (rt[c] == 0) {
+                why = kIneligible;
+            } else if (rt[c] == -1) {
+                why = tg_fail(s, ev, g, v);
+                rt[c] = why ? 0 : 1;
+            }
+        }
+        if (why) filter(row, why);
+        else rows.push_back(row);
+    }
+    if (!rows.empty()) {
+        HIP_TRY(s, upload(s->d_trace_rows, rows));
+        HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
+        pe::NodeSoA soa = soa_of(s);
+        pe::TgTables t = tables_of(g);
+        pe::Ask a = ask_for(s, g);
+        HIP_TRY(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
+                                   s->d_trace_out.as<uint32_t>(), s->stream));
+        std::vector<uint32_t> codes(rows.size());
+        HIP_TRY(s, hipMemcpyAsync(codes.data(), s->d_trace_out.p, codes.size() * 4, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        std::map<int, std::vector<uint32_t>> counts;   // distinct_property use counts, read on demand
+        for (size_t i = 0; i < rows.size(); i++) {
+            const uint32_t row = rows[i], code = codes[i];
+            switch (code & 255u) {
+                case pe::kTrOption: break;
+                case pe::kTrDistinctHosts: filter(row, "distinct_hosts"); break;
+                case pe::kTrDistinctProp: {   // propertyset.go:213-244
+                    const int p = (int)(code >> 8);
+                    PsetDev& ps = *g.psets[p];
+                    uint32_t vid;
+                    Target tv = resolve(s, ps.target, s->view(row), &vid);
+                    if (!tv.found || tv.nil) {
+                        filter(row, "missing property \"" + ps.target_text + "\"");
+                        break;
+                    }
+                    if (vid == PE_NONE) vid = s->lookup(tv.value);
+                    auto it = ps.value_index.find(vid);
+                    uint64_t used = 0;
+                    if (it != ps.value_index.end()) {
+                        auto& cnt = counts[p];
+                        if (cnt.empty()) {
+                            cnt.resize(std::max<size_t>(ps.value_str.size(), 1));
+                            HIP_TRY(s, hipMemcpy(cnt.data(), ps.counts.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+                        }
+                        used = cnt[it->second];
+                    }
+                    filter(row, "distinct_property: " + ps.target_text + "=" + tv.value + " used by " +
+                                    std::to_string(used) + " allocs");
+                    break;
+                }
+                case pe::kTrNoAddr: exhaust(row, "network: no addresses available"); break;
+                case pe::kTrDynPorts: exhaust(row, "network: dynamic port selection failed"); break;
+                case pe::kTrNoNetworks: exhaust(row, "network: no networks available"); break;
+                case pe::kTrBandwidth: exhaust(row, "network: bandwidth exceeded"); break;
+                case pe::kTrTaskDyn: exhaust(row, "network: dynamic port selection failed"); break;
+                case pe::kTrDevNone: exhaust(row, "devices: no devices available"); break;
+                case pe::kTrDevZero: exhaust(row, "devices: invalid request of zero devices"); break;
+                case pe::kTrDevNoMatch: exhaust(row, "devices: no devices match request"); break;
+                case pe::kTrCpu: exhaust(row, "cpu"); break;
+                case pe::kTrMemory: exhaust(row, "memory"); break;
+                case pe::kTrDisk: exhaust(row, "disk"); break;
+                default: return s->fail(PE_EHIP, "k_trace: unknown outcome code");
+            }
+        }
+    }
+    std::string out;
+    auto put = [&](const char* k, const std::map<std::string, int>& mm) {
+        for (auto& kv : mm) out += std::string(k) + "\t" + kv.first + "\t" + std::to_string(kv.second) + "\n";
+    };
+    put("CF", cf); put("KF", kf); put("CE", ce); put("DE", de);
+    s->metrics_text = out;
+    s->metrics_valid = true;
+    return PE_OK;
+}
+
 int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
     const int rc = select_impl(s, tgi, opts, out);
     if (rc == PE_OK && s && out) {
@@ -2173,6 +2328,7 @@ int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranke
 static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
     if (!s || !out) return PE_EINVAL;
     s->gen++;
+    s->metrics_valid = false;
     HIP_TRY(s, hipSetDevice(s->device));
     if (s->cfg.stack_kind != PE_STACK_GENERIC) {
         // SystemStack.Select: single pass over the (single-node) list, no limit;
@@ -2220,15 +2376,20 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         s->offset = no;
         return PE_OK;
     }
-    if (s->limit >= s->visit.size() && s->visit.size() >= s->sweep_min && g.n_spread == (int)g.psets.size()) {
+    const uint32_t start = s->offset;
+    if (s->limit >= s->visit.size() && s->visit.size() >= s->sweep_min && g.n_spread == (int)g.psets.size() &&
+        s->visit_unique) {
         // a whole pass over a large list: multi-CU sweep instead of one workgroup
-        if (s->visit_unique) return run_sweep_select(s, g, opts, out);
+        rc = run_sweep_select(s, g, opts, out);
+        if (rc == PE_OK && s->metrics_on) rc = compute_metrics(s, g, s->visit, start, out->nodes_evaluated);
+        return rc;
     }
     uint32_t placed, no;
     rc = run_place(s, tgi, 1, 0, s->visit, s->offset, opts, out, &placed, &no);
     if (rc) return rc;
     s->offset = no;
-    return PE_OK;
+    if (s->metrics_on) rc = compute_metrics(s, g, s->visit, start, out->nodes_evaluated);
+    return rc;
 }
 
 int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
@@ -2794,3 +2955,21 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
 }
 
 }  // extern "C"
+
+extern "C" int pe_set_metrics(pe_stack* s, int on) {
+    if (!s) return PE_EINVAL;
+    s->metrics_on = on != 0;
+    s->metrics_valid = false;
+    return PE_OK;
+}
+
+extern "C" int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap) {
+    if (!s) return PE_EINVAL;
+    if (!s->metrics_valid) return PE_ESTATE;
+    if (buf && cap) {
+        const size_t k = std::min(cap - 1, s->metrics_text.size());
+        std::memcpy(buf, s->metrics_text.data(), k);
+        buf[k] = 0;
+    }
+    return (int64_t)s->metrics_text.size() + 1;
+}

@@ -21,6 +21,14 @@ constexpr int kMaxDevGroups = 4;      // device groups per node on device (u8 fr
 // class: match bit (nodeDeviceMatches), the AssignDevice choice score
 // (Σ matched affinity weights / Σ |weights|, 0 without affinities) and the
 // matched weight sum.
+// k_trace outcome codes (AllocMetric reasons after the FeasibilityWrapper)
+enum : uint32_t {
+    kTrOption = 0, kTrDistinctHosts = 1, kTrDistinctProp = 2,
+    kTrNoAddr = 10, kTrDynPorts = 11, kTrNoNetworks = 12, kTrBandwidth = 13, kTrTaskDyn = 14,
+    kTrDevNone = 20, kTrDevZero = 21, kTrDevNoMatch = 22,
+    kTrCpu = 30, kTrMemory = 31, kTrDisk = 32,
+};
+
 struct DevClass {
     uint8_t match[kMaxDevReq];            // bit g: group g matches request q
     uint32_t n_groups;

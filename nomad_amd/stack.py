@@ -14,7 +14,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -152,6 +152,36 @@ class _Stack:
 
     def _fn(self, name):
         return getattr(self._lib, self._p + name)
+
+    # -- AllocMetric maps (structs.go:9826-10026) ------------------------------
+    def EnableMetrics(self, on: bool = True):
+        """Collect ClassFiltered / ConstraintFiltered / ClassExhausted /
+        DimensionExhausted per Select (before the eval's first Select)."""
+        if hasattr(self._lib, self._p + "set_metrics"):
+            fn = self._fn("set_metrics")
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_void_p, C.c_int]
+            self._check(fn(self._h, int(on)))
+
+    def LastMetrics(self) -> Dict[str, Dict[str, int]]:
+        """The last Select's maps: {"ClassFiltered": {...}, "ConstraintFiltered": {...},
+        "ClassExhausted": {...}, "DimensionExhausted": {...}}."""
+        fn = self._fn("last_metrics")
+        fn.restype = C.c_int64
+        fn.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        need = fn(self._h, None, 0)
+        if need < 0:
+            self._check(int(need))
+        buf = C.create_string_buffer(int(need) + 1)
+        fn(self._h, buf, len(buf))
+        names = {"CF": "ClassFiltered", "KF": "ConstraintFiltered", "CE": "ClassExhausted",
+                 "DE": "DimensionExhausted"}
+        out = {v: {} for v in names.values()}
+        for line in buf.value.decode().split("\n"):
+            if line:
+                kind, key, cnt = line.split("\t")
+                out[names[kind]][key] = int(cnt)
+        return out
 
     # -- scheduler.State snapshot -------------------------------------------
     def SetState(self, nodes: Sequence[Node], allocs: Sequence[Allocation] = ()):

@@ -146,17 +146,29 @@ static thread_local double* g_trace_score = nullptr;
 
 struct Metrics {
     uint32_t evaluated = 0, filtered = 0, exhausted = 0;
-    std::map<std::string, int> constraint_filtered, dimension_exhausted;
+    std::map<std::string, int> class_filtered, constraint_filtered, class_exhausted, dimension_exhausted;
     void EvaluateNode() { evaluated++; }
-    void FilterNode(const ONode* n, const std::string& c) {
+    void FilterNode(const ONode* n, const std::string& c) {   // structs.go:9907-9921
         filtered++;
+        if (n && !n->node_class.empty()) class_filtered[n->node_class]++;
         if (!c.empty()) constraint_filtered[c]++;
         if (g_trace_status && n) g_trace_status[n->row] = 1;
     }
-    void ExhaustedNode(const ONode* n, const std::string& d) {
+    void ExhaustedNode(const ONode* n, const std::string& d) {   // structs.go:9923-9937
         exhausted++;
+        if (n && !n->node_class.empty()) class_exhausted[n->node_class]++;
         if (!d.empty()) dimension_exhausted[d]++;
         if (g_trace_status && n) g_trace_status[n->row] = 2;
+    }
+    // "KIND\tKEY\tCOUNT\n" lines, KIND in CF/KF/CE/DE, maps in key order
+    std::string Text() const {
+        std::string out;
+        auto put = [&](const char* k, const std::map<std::string, int>& m) {
+            for (auto& kv : m) out += std::string(k) + "\t" + kv.first + "\t" + std::to_string(kv.second) + "\n";
+        };
+        put("CF", class_filtered); put("KF", constraint_filtered);
+        put("CE", class_exhausted); put("DE", dimension_exhausted);
+        return out;
     }
 };
 
@@ -723,7 +735,7 @@ struct PropertySet {
     // UsedCount: returns false with an error message when unresolvable
     bool UsedCount(const ONode& n, std::string* value, uint64_t* used, std::string* err) const {
         if (error) { *err = error_msg; return false; }
-        if (!get_property(&n, target, value)) { *err = "missing property"; return false; }
+        if (!get_property(&n, target, value)) { *err = "missing property \"" + target + "\""; return false; }
         auto use = CombinedUse();
         auto it = use.find(*value);
         *used = it == use.end() ? 0 : it->second;
@@ -733,7 +745,7 @@ struct PropertySet {
         std::string v, err; uint64_t used = 0;
         if (!UsedCount(n, &v, &used, &err)) { *reason = err; return false; }
         if (used < allowed) return true;
-        *reason = "distinct_property: " + target + "=" + v;
+        *reason = "distinct_property: " + target + "=" + v + " used by " + std::to_string(used) + " allocs";
         return false;
     }
 };
@@ -1999,3 +2011,15 @@ int oracle_limit_iter(const double* scores, int n, int limit, double threshold, 
 }
 
 }  // extern "C"
+
+/* AllocMetric maps of the last Select (ClassFiltered, ConstraintFiltered,
+ * ClassExhausted, DimensionExhausted) as text; returns the bytes needed. */
+extern "C" size_t oracle_last_metrics(const oracle_stack* s, char* buf, size_t cap) {
+    const std::string t = s->ctx.metrics.Text();
+    if (buf && cap) {
+        const size_t k = std::min(cap - 1, t.size());
+        std::memcpy(buf, t.data(), k);
+        buf[k] = 0;
+    }
+    return t.size() + 1;
+}
