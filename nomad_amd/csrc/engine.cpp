@@ -66,7 +66,8 @@ size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n);
 int pe_chain_blocks_per_cu(size_t lds);
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st);
 hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
-                           uint32_t n, uint32_t* out, hipStream_t st);
+                           uint32_t n, uint32_t* out, const uint32_t* penalty_bits, double log10,
+                           const double* spread_tab, double* scores, hipStream_t st);
 
 namespace {
 
@@ -373,7 +374,7 @@ struct pe_stack {
     std::map<uint32_t, std::vector<int8_t>> ref_tg_memo;
     std::vector<int8_t> ref_job_memo;
     std::string metrics_text;
-    DevMem d_trace_rows, d_trace_out;
+    DevMem d_trace_rows, d_trace_out, d_trace_scores;
 
     // visit order
     std::vector<uint32_t> visit;
@@ -2202,8 +2203,65 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
 // chain pulled (visit order from the Select's cursor), FeasibilityWrapper
 // reasons from the host-side checkers with the reference's memo transitions
 // (feasible.go:1061-1153), every later reason from k_trace on the device.
+// NodeScoreMeta (structs.go:10030-10035) and the top-K ScoreHeap
+// (lib/kheap/score_heap.go) with Go's container/heap up/down, so ties keep the
+// reference's order.
+struct ScoreMeta {
+    uint32_t row;
+    std::vector<std::pair<std::string, double>> scores;   // sorted by name on output
+    double norm;
+};
+
+struct ScoreHeap {
+    std::vector<ScoreMeta> items;
+    size_t cap = 5;   // MaxRetainedNodeScores (structs.go:178)
+    bool less(size_t i, size_t j) const { return items[i].norm < items[j].norm; }
+    void up(size_t j) {
+        while (j > 0) {
+            const size_t i = (j - 1) / 2;
+            if (!less(j, i)) break;
+            std::swap(items[i], items[j]);
+            j = i;
+        }
+    }
+    bool down(size_t i0, size_t n) {
+        size_t i = i0;
+        for (;;) {
+            const size_t j1 = 2 * i + 1;
+            if (j1 >= n) break;
+            size_t j = j1;
+            if (j1 + 1 < n && less(j1 + 1, j1)) j = j1 + 1;
+            if (!less(j, i)) break;
+            std::swap(items[i], items[j]);
+            i = j;
+        }
+        return i > i0;
+    }
+    void push(ScoreMeta m) {   // heap.Push → ScoreHeap.Push (+ heap.Fix) then up(len-1)
+        if (items.size() < cap) {
+            items.push_back(std::move(m));
+        } else if (m.norm > items[0].norm) {
+            items[0] = std::move(m);
+            if (!down(0, items.size())) up(0);
+        }
+        up(items.size() - 1);
+    }
+    std::vector<ScoreMeta> reverse_items() {   // GetItemsReverse: heap.Pop until empty
+        std::vector<ScoreMeta> out(items.size());
+        size_t i = items.size();
+        while (!items.empty()) {
+            const size_t n = items.size() - 1;
+            std::swap(items[0], items[n]);
+            down(0, n);
+            out[--i] = std::move(items.back());
+            items.pop_back();
+        }
+        return out;
+    }
+};
+
 static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
-                           uint32_t evaluated) {
+                           uint32_t evaluated, const pe_select_options* opts) {
     s->metrics_valid = false;
     const size_t m = order.size();
     std::map<std::string, int> cf, kf, ce, de;
@@ -2250,22 +2308,58 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         if (why) filter(row, why);
         else rows.push_back(row);
     }
+    ScoreHeap heap;
     if (!rows.empty()) {
         HIP_TRY(s, upload(s->d_trace_rows, rows));
         HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
+        HIP_TRY(s, s->d_trace_scores.ensure(rows.size() * 6 * sizeof(double)));
         pe::NodeSoA soa = soa_of(s);
         pe::TgTables t = tables_of(g);
         pe::Ask a = ask_for(s, g);
+        const uint32_t* pbits = nullptr;
+        if (opts && opts->penalty_count > 0) {
+            std::vector<uint32_t> bits((s->nodes.size() + 31) / 32, 0);
+            for (uint32_t i = 0; i < opts->penalty_count; i++) {
+                const uint32_t r = opts->penalty_rows[i];
+                if (r < s->nodes.size()) bits[r >> 5] |= 1u << (r & 31);
+            }
+            HIP_TRY(s, upload(s->d_penalty, bits));
+            pbits = s->d_penalty.as<uint32_t>();
+        }
+        const double* stab = nullptr;
+        if (t.n_spread > 0) {
+            HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
+            HIP_TRY(s, pe_launch_spread_table(&t, s->d_spread_tab.as<double>(), s->stream));
+            stab = s->d_spread_tab.as<double>();
+        }
         HIP_TRY(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
-                                   s->d_trace_out.as<uint32_t>(), s->stream));
+                                   s->d_trace_out.as<uint32_t>(), pbits, s->log10, stab,
+                                   s->d_trace_scores.as<double>(), s->stream));
         std::vector<uint32_t> codes(rows.size());
+        std::vector<double> sc(rows.size() * 6);
         HIP_TRY(s, hipMemcpyAsync(codes.data(), s->d_trace_out.p, codes.size() * 4, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(sc.data(), s->d_trace_scores.p, sc.size() * 8, hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
+        const bool has_aff = !g.affinities.empty();
         std::map<int, std::vector<uint32_t>> counts;   // distinct_property use counts, read on demand
         for (size_t i = 0; i < rows.size(); i++) {
             const uint32_t row = rows[i], code = codes[i];
             switch (code & 255u) {
-                case pe::kTrOption: break;
+                case pe::kTrOption: {   // ScoreNode calls in chain order, then the NormScore push
+                    const double* o = &sc[i * 6];
+                    ScoreMeta sm;
+                    sm.row = row;
+                    sm.scores.emplace_back("binpack", o[0]);
+                    if (a.dev_tw != 0.0) sm.scores.emplace_back("devices", o[1]);
+                    if (a.anti_aff) sm.scores.emplace_back("job-anti-affinity", o[2]);
+                    sm.scores.emplace_back("node-reschedule-penalty", (code & pe::kTrPenalty) ? -1.0 : 0.0);
+                    if (!has_aff) sm.scores.emplace_back("node-affinity", 0.0);
+                    else if (o[3] != 0.0) sm.scores.emplace_back("node-affinity", o[3]);
+                    if (o[4] != 0.0) sm.scores.emplace_back("allocation-spread", o[4]);
+                    sm.norm = o[5];
+                    heap.push(std::move(sm));
+                    break;
+                }
                 case pe::kTrDistinctHosts: filter(row, "distinct_hosts"); break;
                 case pe::kTrDistinctProp: {   // propertyset.go:213-244
                     const int p = (int)(code >> 8);
@@ -2302,6 +2396,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                 case pe::kTrCpu: exhaust(row, "cpu"); break;
                 case pe::kTrMemory: exhaust(row, "memory"); break;
                 case pe::kTrDisk: exhaust(row, "disk"); break;
+                case pe::kTrMismatch: return s->fail(PE_EHIP, "k_trace: device verdict differs from the host walk");
                 default: return s->fail(PE_EHIP, "k_trace: unknown outcome code");
             }
         }
@@ -2311,6 +2406,20 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         for (auto& kv : mm) out += std::string(k) + "\t" + kv.first + "\t" + std::to_string(kv.second) + "\n";
     };
     put("CF", cf); put("KF", kf); put("CE", ce); put("DE", de);
+    // ScoreMetaData (PopulateScoreMetaData): "SM\trank\tnode id\tnorm\tname=value,..." (%.17g)
+    auto items = heap.reverse_items();
+    char num[64];
+    for (size_t i = 0; i < items.size(); i++) {
+        auto& it = items[i];
+        std::sort(it.scores.begin(), it.scores.end());
+        snprintf(num, sizeof num, "%.17g", it.norm);
+        out += "SM\t" + std::to_string(i) + "\t" + s->S(s->nodes[it.row].id) + "\t" + num + "\t";
+        for (size_t k = 0; k < it.scores.size(); k++) {
+            snprintf(num, sizeof num, "%.17g", it.scores[k].second);
+            out += (k ? "," : "") + it.scores[k].first + "=" + num;
+        }
+        out += "\n";
+    }
     s->metrics_text = out;
     s->metrics_valid = true;
     return PE_OK;
@@ -2381,14 +2490,14 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         s->visit_unique) {
         // a whole pass over a large list: multi-CU sweep instead of one workgroup
         rc = run_sweep_select(s, g, opts, out);
-        if (rc == PE_OK && s->metrics_on) rc = compute_metrics(s, g, s->visit, start, out->nodes_evaluated);
+        if (rc == PE_OK && s->metrics_on) rc = compute_metrics(s, g, s->visit, start, out->nodes_evaluated, opts);
         return rc;
     }
     uint32_t placed, no;
     rc = run_place(s, tgi, 1, 0, s->visit, s->offset, opts, out, &placed, &no);
     if (rc) return rc;
     s->offset = no;
-    if (s->metrics_on) rc = compute_metrics(s, g, s->visit, start, out->nodes_evaluated);
+    if (s->metrics_on) rc = compute_metrics(s, g, s->visit, start, out->nodes_evaluated, opts);
     return rc;
 }
 

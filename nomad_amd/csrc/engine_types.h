@@ -27,6 +27,8 @@ enum : uint32_t {
     kTrNoAddr = 10, kTrDynPorts = 11, kTrNoNetworks = 12, kTrBandwidth = 13, kTrTaskDyn = 14,
     kTrDevNone = 20, kTrDevZero = 21, kTrDevNoMatch = 22,
     kTrCpu = 30, kTrMemory = 31, kTrDisk = 32,
+    kTrMismatch = 254,          // device verdict disagrees with the host walk (bug guard)
+    kTrPenalty = 1u << 16,      // option: node in the rescheduling penalty set
 };
 
 struct DevClass {

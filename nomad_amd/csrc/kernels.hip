@@ -237,71 +237,6 @@ __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t
     return kOption;
 }
 
-// AllocMetric trace (structs.go:9903-9937): for visited rows that passed the
-// FeasibilityWrapper, which iterator stopped them and why, with the same state
-// the Select saw (HBM SoA, no overlay). Codes: kTr* in engine_types.h; a
-// distinct_property failure carries its set index in bits 8-15.
-__global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint32_t n, uint32_t* out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t row = rows[i];
-    NodeIn in;
-    load_node(s, t, row, in);
-    const NodeRec& r = in.r;
-    const uint32_t c = r.cls;
-    uint32_t code = kTrOption;
-    if ((a.distinct_job && s.coll_job[row] > 0) || (a.distinct_tg && in.coll_tg > 0)) {
-        code = kTrDistinctHosts;                                   // feasible.go:569-595
-    } else {
-        for (int p = t.n_spread; p < t.n_psets && code == kTrOption; p++) {
-            const uint32_t v = pset_value(t, p, row, c);
-            if (v == kMissing || t.pset_counts[p][v] >= t.pset_allowed[p]) code = kTrDistinctProp | ((uint32_t)p << 8);
-        }
-    }
-    if (code == kTrOption && (a.tg_dyn > 0 || a.has_task_net)) {   // rank.go:231-295
-        int32_t dyn = r.used_dyn;
-        if (a.tg_dyn > 0) {
-            if (t.alias_ok && !t.alias_ok[row]) code = kTrNoAddr;
-            else if (kDynPortCapacity - dyn < 1) code = kTrDynPorts;
-            dyn += a.tg_dyn;
-        }
-        if (code == kTrOption && a.has_task_net) {
-            if (r.avail_mbits < 0) code = kTrNoNetworks;
-            else if (r.used_mbits + a.task_mbits > r.avail_mbits) code = kTrBandwidth;
-            else if (kDynPortCapacity - dyn < a.task_dyn) code = kTrTaskDyn;
-        }
-    }
-    if (code == kTrOption && a.n_dev > 0) {                         // AssignDevice errors (device.go:32-131)
-        const DevClass& dc = t.dev_cls[c];
-        uint32_t free = in.dev_free;
-        if (dc.n_groups == 0) code = kTrDevNone;
-        for (int q = 0; q < kMaxDevReq && code == kTrOption; q++) {
-            if (q >= a.n_dev) break;
-            const uint32_t cnt = (uint32_t)a.dev_cnt[q];
-            if (cnt == 0) { code = kTrDevZero; break; }
-            int best = -1;
-            double best_score = 0.0;
-            for (int g = 0; g < kMaxDevGroups; g++) {
-                if (g >= (int)dc.n_groups) break;
-                const uint32_t f = (free >> (8 * g)) & 255u;
-                if (f < cnt || !((dc.match[q] >> g) & 1u)) continue;
-                const double sc = dc.choice[q][g];
-                if (best >= 0 && sc < best_score) continue;
-                best = g;
-                best_score = sc;
-            }
-            if (best < 0) { code = kTrDevNoMatch; break; }
-            free -= cnt << (8 * best);
-        }
-    }
-    if (code == kTrOption) {                                        // AllocsFit → Superset order
-        if (r.cap_cpu < r.used_cpu + a.cpu) code = kTrCpu;
-        else if (r.cap_mem < r.used_mem + a.mem) code = kTrMemory;
-        else if (r.cap_disk < r.used_disk + a.disk) code = kTrDisk;
-    }
-    out[i] = code;
-}
-
 // Table lookups of the scoring half for an option: penalty bit, node affinity,
 // spread total (per-property boosts summed in property order, spread.go:145-170).
 __device__ __forceinline__ void lookup_scores(const TgTables& t, const uint32_t* penalty_bits,
@@ -378,6 +313,94 @@ __device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, c
     load_node(s, t, row, in);
     eval_loaded<kKeepParts>(s, t, class_ok, a, ov_count(ov, row), penalty_bits, log10, spread_tab, row, in,
                             out);
+}
+
+// AllocMetric trace (structs.go:9903-9937): for visited rows that passed the
+// FeasibilityWrapper, which iterator stopped them and why, with the same state
+// the Select saw (HBM SoA, no overlay). Codes: kTr* in engine_types.h; a
+// distinct_property failure carries its set index in bits 8-15.
+// Options also get their named scores (ScoreNode calls, rank.go:516-522, 591-593,
+// 635-637, 704-722, spread.go:170, rank.go:769) as 6 doubles: binpack, devices,
+// job-anti-affinity, node-affinity, allocation-spread, normalized-score.
+__global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint32_t n, uint32_t* out,
+                        const uint32_t* penalty_bits, double log10, const double* spread_tab, double* sc) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t row = rows[i];
+    NodeIn in;
+    load_node(s, t, row, in);
+    const NodeRec& r = in.r;
+    const uint32_t c = r.cls;
+    uint32_t code = kTrOption;
+    if ((a.distinct_job && s.coll_job[row] > 0) || (a.distinct_tg && in.coll_tg > 0)) {
+        code = kTrDistinctHosts;                                   // feasible.go:569-595
+    } else {
+        for (int p = t.n_spread; p < t.n_psets && code == kTrOption; p++) {
+            const uint32_t v = pset_value(t, p, row, c);
+            if (v == kMissing || t.pset_counts[p][v] >= t.pset_allowed[p]) code = kTrDistinctProp | ((uint32_t)p << 8);
+        }
+    }
+    if (code == kTrOption && (a.tg_dyn > 0 || a.has_task_net)) {   // rank.go:231-295
+        int32_t dyn = r.used_dyn;
+        if (a.tg_dyn > 0) {
+            if (t.alias_ok && !t.alias_ok[row]) code = kTrNoAddr;
+            else if (kDynPortCapacity - dyn < 1) code = kTrDynPorts;
+            dyn += a.tg_dyn;
+        }
+        if (code == kTrOption && a.has_task_net) {
+            if (r.avail_mbits < 0) code = kTrNoNetworks;
+            else if (r.used_mbits + a.task_mbits > r.avail_mbits) code = kTrBandwidth;
+            else if (kDynPortCapacity - dyn < a.task_dyn) code = kTrTaskDyn;
+        }
+    }
+    if (code == kTrOption && a.n_dev > 0) {                         // AssignDevice errors (device.go:32-131)
+        const DevClass& dc = t.dev_cls[c];
+        uint32_t free = in.dev_free;
+        if (dc.n_groups == 0) code = kTrDevNone;
+        for (int q = 0; q < kMaxDevReq && code == kTrOption; q++) {
+            if (q >= a.n_dev) break;
+            const uint32_t cnt = (uint32_t)a.dev_cnt[q];
+            if (cnt == 0) { code = kTrDevZero; break; }
+            int best = -1;
+            double best_score = 0.0;
+            for (int g = 0; g < kMaxDevGroups; g++) {
+                if (g >= (int)dc.n_groups) break;
+                const uint32_t f = (free >> (8 * g)) & 255u;
+                if (f < cnt || !((dc.match[q] >> g) & 1u)) continue;
+                const double sc = dc.choice[q][g];
+                if (best >= 0 && sc < best_score) continue;
+                best = g;
+                best_score = sc;
+            }
+            if (best < 0) { code = kTrDevNoMatch; break; }
+            free -= cnt << (8 * best);
+        }
+    }
+    if (code == kTrOption) {                                        // AllocsFit → Superset order
+        if (r.cap_cpu < r.used_cpu + a.cpu) code = kTrCpu;
+        else if (r.cap_mem < r.used_mem + a.mem) code = kTrMemory;
+        else if (r.cap_disk < r.used_disk + a.disk) code = kTrDisk;
+    }
+    if (code == kTrOption) {
+        ScoreIn si;
+        if (status_loaded(s, t, t.class_ok, a, 0, row, in, &si) != kOption) {
+            out[i] = kTrMismatch;
+            return;
+        }
+        lookup_scores(t, penalty_bits, spread_tab, row, c, &si);
+        NodeEval ev;
+        score_option<true>(a, log10, si, &ev);
+        double* o = sc + (size_t)i * 6;
+        uint32_t k = 1;
+        o[0] = ev.parts[0];
+        o[1] = a.dev_tw != 0.0 ? ev.parts[k++] : 0.0;
+        o[2] = (a.anti_aff && si.coll > 0) ? ev.parts[k++] : 0.0;
+        if (si.penalty) { code |= kTrPenalty; k++; }
+        o[3] = si.aff != 0.0 ? ev.parts[k++] : 0.0;
+        o[4] = si.spread != 0.0 ? ev.parts[k++] : 0.0;
+        o[5] = ev.score;
+    }
+    out[i] = code;
 }
 
 // evenSpreadScoreBoost (spread.go:178-228) / target boost (spread.go:143-164)
@@ -2138,8 +2161,10 @@ void pe_rec_merge_host(pe::SweepRec* a, const pe::SweepRec* b) { pe::rec_merge(*
 void pe_rec_init_host(pe::SweepRec* a) { pe::rec_init(*a); }
 
 hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
-                           uint32_t n, uint32_t* out, hipStream_t st) {
+                           uint32_t n, uint32_t* out, const uint32_t* penalty_bits, double log10,
+                           const double* spread_tab, double* scores, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(pe::k_trace, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, n, out);
+    hipLaunchKernelGGL(pe::k_trace, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, n, out,
+                       penalty_bits, log10, spread_tab, scores);
     return hipGetLastError();
 }

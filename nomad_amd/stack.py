@@ -165,7 +165,8 @@ class _Stack:
 
     def LastMetrics(self) -> Dict[str, Dict[str, int]]:
         """The last Select's maps: {"ClassFiltered": {...}, "ConstraintFiltered": {...},
-        "ClassExhausted": {...}, "DimensionExhausted": {...}}."""
+        "ClassExhausted": {...}, "DimensionExhausted": {...}, "ScoreMetaData":
+        [(node id, NormScore, {scorer: score}), ...]}."""
         fn = self._fn("last_metrics")
         fn.restype = C.c_int64
         fn.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
@@ -177,10 +178,17 @@ class _Stack:
         names = {"CF": "ClassFiltered", "KF": "ConstraintFiltered", "CE": "ClassExhausted",
                  "DE": "DimensionExhausted"}
         out = {v: {} for v in names.values()}
+        out["ScoreMetaData"] = []
         for line in buf.value.decode().split("\n"):
-            if line:
-                kind, key, cnt = line.split("\t")
-                out[names[kind]][key] = int(cnt)
+            if not line:
+                continue
+            if line.startswith("SM\t"):   # PopulateScoreMetaData: top 5 by NormScore, descending
+                _, _, node_id, norm, parts = line.split("\t")
+                scores = dict((k, float(v)) for k, v in (p.split("=") for p in parts.split(",") if p))
+                out["ScoreMetaData"].append((node_id, float(norm), scores))
+                continue
+            kind, key, cnt = line.split("\t")
+            out[names[kind]][key] = int(cnt)
         return out
 
     # -- scheduler.State snapshot -------------------------------------------

@@ -144,9 +144,86 @@ struct OJob {
 static thread_local uint8_t* g_trace_status = nullptr;
 static thread_local double* g_trace_score = nullptr;
 
+// NodeScoreMeta (structs.go:10030-10035) and kheap.ScoreHeap
+// (lib/kheap/score_heap.go) over Go's container/heap (up / down / Fix / Pop).
+struct NodeScoreMeta {
+    std::string node_id;
+    std::map<std::string, double> scores;
+    double norm = 0;
+};
+
+struct GoScoreHeap {
+    std::vector<NodeScoreMeta> items;
+    int capacity = 5;   // MaxRetainedNodeScores
+    bool Less(int i, int j) const { return items[i].norm < items[j].norm; }
+    void Swap(int i, int j) { std::swap(items[i], items[j]); }
+    int Len() const { return (int)items.size(); }
+    void up(int j) {
+        for (;;) {
+            int i = (j - 1) / 2;   // Go integer division truncates toward zero
+            if (i == j || !Less(j, i)) break;
+            Swap(i, j);
+            j = i;
+        }
+    }
+    bool down(int i0, int n) {
+        int i = i0;
+        for (;;) {
+            int j1 = 2 * i + 1;
+            if (j1 >= n || j1 < 0) break;
+            int j = j1;
+            int j2 = j1 + 1;
+            if (j2 < n && Less(j2, j1)) j = j2;
+            if (!Less(j, i)) break;
+            Swap(i, j);
+            i = j;
+        }
+        return i > i0;
+    }
+    void Fix(int i) { if (!down(i, Len())) up(i); }
+    void HeapPush(const NodeScoreMeta& x) {   // heap.Push(h, x)
+        if (Len() < capacity) {
+            items.push_back(x);
+        } else if (x.norm > items[0].norm) {
+            items[0] = x;
+            Fix(0);
+        }
+        up(Len() - 1);
+    }
+    NodeScoreMeta HeapPop() {                  // heap.Pop(h)
+        int n = Len() - 1;
+        Swap(0, n);
+        down(0, n);
+        NodeScoreMeta it = items.back();
+        items.pop_back();
+        return it;
+    }
+    std::vector<NodeScoreMeta> GetItemsReverse() {
+        std::vector<NodeScoreMeta> ret(Len());
+        int i = Len() - 1;
+        while (Len() > 0) ret[i--] = HeapPop();
+        return ret;
+    }
+};
+
 struct Metrics {
     uint32_t evaluated = 0, filtered = 0, exhausted = 0;
     std::map<std::string, int> class_filtered, constraint_filtered, class_exhausted, dimension_exhausted;
+    std::unique_ptr<NodeScoreMeta> meta;
+    GoScoreHeap top;
+    void ScoreNode(const ONode* n, const std::string& name, double score) {   // structs.go:9977-10001
+        if (!meta || meta->node_id != n->id) {
+            meta.reset(new NodeScoreMeta());
+            meta->node_id = n->id;
+        }
+        if (name == "normalized-score") {
+            meta->norm = score;
+            top.HeapPush(*meta);
+            meta.reset();
+        } else {
+            meta->scores[name] = score;
+        }
+    }
     void EvaluateNode() { evaluated++; }
     void FilterNode(const ONode* n, const std::string& c) {   // structs.go:9907-9921
         filtered++;
@@ -168,6 +245,20 @@ struct Metrics {
         };
         put("CF", class_filtered); put("KF", constraint_filtered);
         put("CE", class_exhausted); put("DE", dimension_exhausted);
+        GoScoreHeap h = top;   // PopulateScoreMetaData
+        auto items = h.GetItemsReverse();
+        char num[64];
+        for (size_t i = 0; i < items.size(); i++) {
+            snprintf(num, sizeof num, "%.17g", items[i].norm);
+            out += "SM\t" + std::to_string(i) + "\t" + items[i].node_id + "\t" + num + "\t";
+            bool first = true;
+            for (auto& kv : items[i].scores) {
+                snprintf(num, sizeof num, "%.17g", kv.second);
+                out += (first ? "" : ",") + kv.first + "=" + num;
+                first = false;
+            }
+            out += "\n";
+        }
         return out;
     }
 };
@@ -1258,7 +1349,11 @@ struct BinPackIterator : RankIterator {
             // the score uses the utilisation computed before any preemption (rank.go:505-516)
             double fitness = score_fit(spread_algo, n, ucpu, umem);
             option->scores.push_back(fitness / 18.0);
-            if (total_dev_w != 0) option->scores.push_back(sum_dev_match / total_dev_w);
+            ctx->metrics.ScoreNode(&n, "binpack", fitness / 18.0);
+            if (total_dev_w != 0) {
+                option->scores.push_back(sum_dev_match / total_dev_w);
+                ctx->metrics.ScoreNode(&n, "devices", sum_dev_match / total_dev_w);
+            }
             return option;
         }
     }
@@ -1275,7 +1370,12 @@ struct JobAntiAffinityIterator : RankIterator {
         int coll = 0;
         for (const OAlloc* a : ctx->ProposedAllocs(o->node->row))
             if (a->job_id == job_id && a->tg == tg) coll++;
-        if (coll > 0) o->scores.push_back(-1 * (double)(coll + 1) / (double)desired);
+        if (coll > 0) {
+            o->scores.push_back(-1 * (double)(coll + 1) / (double)desired);
+            ctx->metrics.ScoreNode(o->node, "job-anti-affinity", o->scores.back());
+        } else {
+            ctx->metrics.ScoreNode(o->node, "job-anti-affinity", 0);
+        }
         return o;
     }
     void Reset() override { source->Reset(); }
@@ -1283,11 +1383,16 @@ struct JobAntiAffinityIterator : RankIterator {
 
 // NodeReschedulingPenaltyIterator (rank.go:603-646)
 struct NodeReschedulingPenaltyIterator : RankIterator {
-    RankIterator* source; std::set<int> penalty;
+    EvalContext* ctx = nullptr; RankIterator* source; std::set<int> penalty;
     RankedNode* Next() override {
         RankedNode* o = source->Next();
         if (!o) return nullptr;
-        if (penalty.count(o->node->row)) o->scores.push_back(-1);
+        if (penalty.count(o->node->row)) {
+            o->scores.push_back(-1);
+            ctx->metrics.ScoreNode(o->node, "node-reschedule-penalty", -1);
+        } else {
+            ctx->metrics.ScoreNode(o->node, "node-reschedule-penalty", 0);
+        }
         return o;
     }
     void Reset() override { penalty.clear(); source->Reset(); }
@@ -1307,7 +1412,7 @@ struct NodeAffinityIterator : RankIterator {
     RankedNode* Next() override {
         RankedNode* o = source->Next();
         if (!o) return nullptr;
-        if (!has()) return o;
+        if (!has()) { ctx->metrics.ScoreNode(o->node, "node-affinity", 0); return o; }
         double sum_w = 0.0;
         for (auto& a : affs) sum_w += std::fabs((double)a.weight);
         double total = 0.0;
@@ -1317,7 +1422,10 @@ struct NodeAffinityIterator : RankIterator {
             if (orasem::check_constraint(ctx->caches, a.op, l, r, lf, rf)) total += (double)a.weight;
         }
         double norm = total / sum_w;
-        if (total != 0.0) o->scores.push_back(norm);
+        if (total != 0.0) {
+            o->scores.push_back(norm);
+            ctx->metrics.ScoreNode(o->node, "node-affinity", norm);
+        }
         return o;
     }
     void Reset() override { source->Reset(); affs.clear(); }
@@ -1420,7 +1528,10 @@ struct SpreadIterator : RankIterator {
                 double boost = ((desired - (double)used) / desired) * w;
                 total += boost;
             }
-            if (total != 0.0) o->scores.push_back(total);
+            if (total != 0.0) {
+                o->scores.push_back(total);
+                ctx->metrics.ScoreNode(o->node, "allocation-spread", total);
+            }
             return o;
         }
     }
@@ -1432,11 +1543,13 @@ struct SpreadIterator : RankIterator {
 
 // PreemptionScoringIterator (rank.go:773-806)
 struct PreemptionScoringIterator : RankIterator {
+    EvalContext* ctx = nullptr;
     RankIterator* source;
     RankedNode* Next() override {
         RankedNode* o = source->Next();
         if (!o || o->preempted.empty()) return o;
         o->scores.push_back(preemption_score(o->preempted));
+        if (ctx) ctx->metrics.ScoreNode(o->node, "preemption", o->scores.back());
         return o;
     }
     void Reset() override { source->Reset(); }
@@ -1444,6 +1557,7 @@ struct PreemptionScoringIterator : RankIterator {
 
 // ScoreNormalizationIterator (rank.go:737-771)
 struct ScoreNormalizationIterator : RankIterator {
+    EvalContext* ctx = nullptr;
     RankIterator* source;
     RankedNode* Next() override {
         RankedNode* o = source->Next();
@@ -1451,6 +1565,7 @@ struct ScoreNormalizationIterator : RankIterator {
         double sum = 0.0;
         for (double s : o->scores) sum += s;
         o->final_score = sum / (double)o->scores.size();
+        if (ctx) ctx->metrics.ScoreNode(o->node, "normalized-score", o->final_score);
         if (g_trace_status) { g_trace_status[o->node->row] = 0; g_trace_score[o->node->row] = o->final_score; }
         return o;
     }
@@ -1566,11 +1681,11 @@ struct oracle_stack {
         bin_pack.spread_algo = c.algorithm == PE_ALGO_SPREAD;
         bin_pack.oversub = c.memory_oversubscription != 0;
         job_anti_aff.ctx = &ctx; job_anti_aff.source = &bin_pack;
-        penalty.source = &job_anti_aff;
+        penalty.ctx = &ctx; penalty.source = &job_anti_aff;
         node_affinity.ctx = &ctx; node_affinity.source = &penalty;
         spread.ctx = &ctx; spread.source = &node_affinity;
-        preempt_score.source = &spread;
-        score_norm.source = generic ? (RankIterator*)&preempt_score : (RankIterator*)&bin_pack;
+        preempt_score.ctx = &ctx; preempt_score.source = &spread;
+        score_norm.ctx = &ctx; score_norm.source = generic ? (RankIterator*)&preempt_score : (RankIterator*)&bin_pack;
         limit.source = &score_norm; limit.limit = 2; limit.max_skip = 3; limit.threshold = 0.0;
         max_score.source = &limit;
     }

@@ -1,6 +1,8 @@
 """AllocMetric maps of Select: ClassFiltered,
 ConstraintFiltered, ClassExhausted, DimensionExhausted
-(nomad/structs/structs.go:9903-9937), as `ctx.Metrics()` holds them after
+(nomad/structs/structs.go:9903-9937) and ScoreMetaData (ScoreNode +
+PopulateScoreMetaData over the top-5 kheap, structs.go:9976-10018,
+lib/kheap/score_heap.go), as `ctx.Metrics()` holds them after
 GenericStack.Select.
 
 KATs follow the reference's own assertions (stack_test.go:310-348
@@ -64,6 +66,12 @@ def test_binpack_overflow_kat(stack_cls):
     m = st.LastMetrics()
     assert m["ClassExhausted"] == {"linux-medium-pci": 1}
     assert m["DimensionExhausted"] == {"cpu": 1}
+    # "Expect score metadata for one node" (PopulateScoreMetaData, top 5 by NormScore)
+    assert len(m["ScoreMetaData"]) == 1
+    node_id, norm, scores = m["ScoreMetaData"][0]
+    assert node_id == "a" and norm == r.final_score
+    assert set(scores) == {"binpack", "job-anti-affinity", "node-reschedule-penalty", "node-affinity"}
+    assert scores["binpack"] == r.scores[0] and scores["node-affinity"] == 0.0
 
 
 def _loop(nodes, allocs, job, perm, placements, tg=0):
