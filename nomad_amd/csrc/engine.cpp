@@ -2469,6 +2469,12 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         if (opts->preempt) rc = run_evict_select(s, g, pref, 0, &o2, out, &no);
         else rc = run_place(s, tgi, 1, 0, pref, 0, &o2, out, &placed, &no);
         if (rc) return rc;
+        // the inner Select over the preferred list has its own AllocMetric
+        // (ctx.Reset per Select); its walk also advances the memo shadow
+        if (!opts->preempt && s->metrics_on) {
+            rc = compute_metrics(s, g, pref, 0, out->nodes_evaluated, &o2);
+            if (rc) return rc;
+        }
         s->offset = 0;
         invalidate_tables(s);
         if (out->row >= 0) return PE_OK;

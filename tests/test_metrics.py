@@ -160,3 +160,38 @@ def test_metrics_network_and_devices():
     job2.task_groups[0].tasks[0].network = NetworkResource(mbits=400)
     seen2 = _loop(nodes2, allocs2, job2, synth.shuffle(len(nodes2), 4), 100)
     assert any(k.startswith("network: ") for k in seen2["DimensionExhausted"])
+
+
+@pytest.mark.gpu
+def test_metrics_preferred_and_penalty_nodes():
+    # SelectOptions: PreferredNodes (inner Select over them first, its own
+    # AllocMetric) and PenaltyNodeIDs (node-reschedule-penalty score of -1)
+    import random
+    from nomad_amd.stack import GenericStack, SelectOptions
+    nodes, allocs = synth.cluster_c2(300, seed=5)
+    job = synth.job_c2(90)
+    perm = synth.shuffle(len(nodes), 8)
+    rng = random.Random(3)
+    sts = []
+    for cls in (GenericStack, OracleGenericStack):
+        st = cls()
+        st.EnableMetrics()
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(perm)
+        sts.append(st)
+    eng, ora = sts
+    for k in range(90):
+        opt = None
+        if k % 3 == 0:
+            opt = SelectOptions(preferred_nodes=[n.id for n in rng.sample(nodes, 3)],
+                                penalty_node_ids=[n.id for n in rng.sample(nodes, 40)])
+        elif k % 3 == 1:
+            opt = SelectOptions(penalty_node_ids=[n.id for n in rng.sample(nodes, 40)])
+        re, ro = eng.Select(0, opt), ora.Select(0, opt)
+        assert (re.row if re else -1) == (ro.row if ro else -1), k
+        assert eng.LastMetrics() == ora.LastMetrics(), k
+        if ro is None:
+            break
+        eng.Commit(0, re.row)
+        ora.Commit(0, ro.row)

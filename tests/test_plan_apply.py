@@ -356,3 +356,42 @@ def test_planner_system_plan_properties():
     for i, nid in enumerate(ep.node_ids[:2000]):
         assert _codes_to_pairs([a[i]])[0] == O.evaluate_node_plan(snap, plan, nid), nid
     assert (a == abi.PE_PLAN_FIT).mean() > 0.8
+
+
+# ---- committed golden vectors (tools/make_plan_golden.py) ----------------------
+
+def _golden():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "plan_apply.json")
+    return json.load(open(path))
+
+
+def test_oracle_matches_golden():
+    g = _golden()
+    for seed, want in g["random_case"].items():
+        nodes, allocs, plan = random_case(int(seed))
+        ids, fits, why = O.evaluate_plan_placements(O.Snapshot(nodes, allocs), plan)
+        assert [list(x) for x in zip(ids, fits, why)] == want, seed
+    sp = g["system_plan"]
+    nodes, allocs, plan = system_plan(sp["n"], sp["seed"])
+    ids, fits, why = O.evaluate_plan_placements(O.Snapshot(nodes, allocs), plan)
+    assert [list(x) for x in zip(ids, fits, why)] == sp["outcomes"]
+
+
+@pytest.mark.gpu
+def test_planner_matches_golden():
+    g = _golden()
+    pl = _planner()
+    for seed, want in g["random_case"].items():
+        nodes, allocs, plan = random_case(int(seed))
+        pl.set_state(nodes, allocs)
+        ep = pl.encode(plan)
+        got = [[nid, f, w] for nid, (f, w) in zip(ep.node_ids, _codes_to_pairs(pl.evaluate(ep)))]
+        assert got == want, seed
+    sp = g["system_plan"]
+    nodes, allocs, plan = system_plan(sp["n"], sp["seed"])
+    pl.set_state(nodes, allocs)
+    ep = pl.encode(plan)
+    got = [[nid, f, w] for nid, (f, w) in zip(ep.node_ids, _codes_to_pairs(pl.evaluate(ep)))]
+    assert got == sp["outcomes"]
