@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
@@ -23,7 +24,7 @@
 #include "../../include/nomad_pe.h"
 #include "plan_types.h"
 
-hipError_t pe_launch_plan_eval(const pa::PlanArgs* a, hipStream_t st);
+hipError_t pe_launch_plan_eval(const pa::PlanArgs* a, int group, hipStream_t st);
 
 namespace {
 
@@ -125,6 +126,7 @@ struct pe_planner {
     double last_ms = 0;
     uint64_t last_bytes = 0;
     bool have_state = false;
+    int group = 4;    // lanes per plan node in k_plan_eval (PE_PLAN_GROUP: 4 / 8 / 16 / 64; 4 measured fastest)
 
     std::unordered_map<std::string, uint32_t> sid;
     std::map<std::array<uint32_t, 3>, uint32_t> tuple_id;
@@ -371,6 +373,10 @@ pe_planner* pe_planner_create(int device) {
     if (hipSetDevice(device) != hipSuccess) return nullptr;
     auto* p = new pe_planner();
     p->device = device;
+    if (const char* g = getenv("PE_PLAN_GROUP")) {
+        const int v = atoi(g);
+        if (v == 4 || v == 8 || v == 16 || v == 64) p->group = v;
+    }
     if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&p->e0) != hipSuccess || hipEventCreate(&p->e1) != hipSuccess) {
         delete p;
@@ -478,7 +484,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
             bytes += sizeof(pa::AllocRec) + (pa_recs[j].terminal ? 0 : 8ull * pa_recs[j].n_keys);
         }
         r.key_bound = (uint32_t)std::min<uint64_t>(bound, 0xFFFFFFFFull);
-        if (bound > pa::kLdsKeys) {
+        if (bound > pa::lds_keys(p->group)) {
             big.push_back(i);
             r.scratch_off = (uint32_t)scratch;
             scratch += bound;
@@ -508,7 +514,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     a.big = (const uint32_t*)p->d_big.p;
     a.n_big = (uint32_t)big.size();
     a.reason = (uint8_t*)p->d_reason.p;
-    if ((e = hipEventRecord(p->e0, p->stream)) != hipSuccess || (e = pe_launch_plan_eval(&a, p->stream)) != hipSuccess ||
+    if ((e = hipEventRecord(p->e0, p->stream)) != hipSuccess || (e = pe_launch_plan_eval(&a, p->group, p->stream)) != hipSuccess ||
         (e = hipEventRecord(p->e1, p->stream)) != hipSuccess ||
         (np && (e = hipMemcpyAsync(reason, a.reason, np, hipMemcpyDeviceToHost, p->stream)) != hipSuccess) ||
         (e = hipStreamSynchronize(p->stream)) != hipSuccess)

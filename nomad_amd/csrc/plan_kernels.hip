@@ -2,8 +2,8 @@
 // → AllocsFit(node, proposed, nil, checkDevices=true) (nomad/structs/funcs.go:148-211)
 // for every node of a plan.
 //
-// k_plan_eval      a group of 16 lanes per plan node, four nodes per wavefront,
-//                  keys staged in a 1 KiB per-node LDS buffer (ds_* only).
+// k_plan_eval<G>   a group of G lanes per plan node (default 4: sixteen nodes per
+//                  wavefront), keys staged in a per-node LDS buffer (ds_* only).
 // k_plan_eval_big  one wavefront per plan node whose key bound exceeds that
 //                  buffer (nodes with hundreds of cores / ports), keys staged in
 //                  global scratch. Rare; listed by the host.
@@ -176,23 +176,26 @@ __device__ __forceinline__ bool precheck(const PlanArgs& a, const PlanNodeRec& p
     return true;
 }
 
+template <int G>
 __global__ void __launch_bounds__(64 * kWaves) k_plan_eval(PlanArgs a) {
-    __shared__ uint64_t lds_keys[kNodesPerBlock][kLdsKeys];
-    __shared__ uint32_t fill[kNodesPerBlock];
-    __shared__ unsigned long long cmask[kNodesPerBlock];
+    constexpr int NB = nodes_per_block(G);
+    constexpr uint32_t NK = lds_keys(G);
+    __shared__ uint64_t keys[NB][NK];
+    __shared__ uint32_t fill[NB];
+    __shared__ unsigned long long cmask[NB];
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t slot = threadIdx.x / kGroup;
-    const uint32_t first = blockIdx.x * kNodesPerBlock + (threadIdx.x >> 6) * (64 / kGroup);
+    const uint32_t slot = threadIdx.x / G;
+    const uint32_t first = blockIdx.x * NB + (threadIdx.x >> 6) * (64 / G);
     if (first >= a.n_plan) return;   // whole wave idle; no workgroup barrier below
-    const uint32_t p = blockIdx.x * kNodesPerBlock + slot;
+    const uint32_t p = blockIdx.x * NB + slot;
     if (p >= a.n_plan) return;       // group-uniform: the group's lanes leave together
     const PlanNodeRec pn = a.pn[p];
     if (pn.scratch_off != kNone) return;   // k_plan_eval_big
     NodeRec nd;
     uint8_t r;
     if (precheck(a, pn, &nd, &r))
-        r = fit_node<kGroup, false>(a, pn, nd, lane, lds_keys[slot], &fill[slot], &cmask[slot]);
-    if ((lane & (kGroup - 1)) == 0) a.reason[p] = r;
+        r = fit_node<G, false>(a, pn, nd, lane, keys[slot], &fill[slot], &cmask[slot]);
+    if ((lane & (G - 1)) == 0) a.reason[p] = r;
 }
 
 __global__ void __launch_bounds__(64) k_plan_eval_big(PlanArgs a) {
@@ -210,10 +213,22 @@ __global__ void __launch_bounds__(64) k_plan_eval_big(PlanArgs a) {
 
 }  // namespace pa
 
-hipError_t pe_launch_plan_eval(const pa::PlanArgs* a, hipStream_t st) {
+template <int G>
+static void launch_group(const pa::PlanArgs* a, hipStream_t st) {
+    const uint32_t blocks = (a->n_plan + pa::nodes_per_block(G) - 1) / pa::nodes_per_block(G);
+    hipLaunchKernelGGL(pa::k_plan_eval<G>, dim3(blocks), dim3(64 * pa::kWaves), 0, st, *a);
+}
+
+// group: lanes per plan node (4, 8, 16 or 64); the host sized the LDS / scratch
+// split with pa::lds_keys(group).
+hipError_t pe_launch_plan_eval(const pa::PlanArgs* a, int group, hipStream_t st) {
     if (a->n_plan == 0) return hipSuccess;
-    const uint32_t blocks = (a->n_plan + pa::kNodesPerBlock - 1) / pa::kNodesPerBlock;
-    hipLaunchKernelGGL(pa::k_plan_eval, dim3(blocks), dim3(64 * pa::kWaves), 0, st, *a);
+    switch (group) {
+        case 4: launch_group<4>(a, st); break;
+        case 8: launch_group<8>(a, st); break;
+        case 64: launch_group<64>(a, st); break;
+        default: launch_group<16>(a, st); break;
+    }
     if (a->n_big) hipLaunchKernelGGL(pa::k_plan_eval_big, dim3(a->n_big), dim3(64), 0, st, *a);
     return hipGetLastError();
 }

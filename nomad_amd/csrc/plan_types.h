@@ -63,13 +63,13 @@ struct alignas(16) PlanNodeRec {  // 32 B, one per plan node
 };
 static_assert(sizeof(PlanNodeRec) == 32, "PlanNodeRec is 32 bytes");
 
-// k_plan_eval: a group of kGroup lanes per plan node (4 nodes per wavefront),
-// keys staged in a per-node LDS buffer of kLdsKeys; plan nodes whose key bound
-// exceeds it go to k_plan_eval_big (one wavefront each, global scratch).
-constexpr int kGroup = 16;
+// k_plan_eval<G>: a group of G lanes per plan node (64/G nodes per wavefront),
+// keys staged in a per-node LDS buffer of lds_keys(G) (16 KiB per workgroup);
+// plan nodes whose key bound exceeds it go to k_plan_eval_big (one wavefront
+// each, global scratch). The host picks G (pe_planner, PE_PLAN_GROUP).
 constexpr int kWaves = 4;                               // waves per workgroup
-constexpr int kNodesPerBlock = kWaves * (64 / kGroup);
-constexpr uint32_t kLdsKeys = 128;                      // 1 KiB per plan node
+__host__ __device__ constexpr int nodes_per_block(int g) { return kWaves * (64 / g); }
+__host__ __device__ constexpr uint32_t lds_keys(int g) { return 2048u / (uint32_t)(kWaves * (64 / g)); }
 constexpr uint64_t kHole = ~0ull;                       // staged slot of a masked core (kind 15)
 
 struct PlanArgs {
