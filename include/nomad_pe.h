@@ -253,6 +253,16 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
 /* Start a new evaluation on the resident snapshot: drop the plan (proposed
  * allocs), the EvalEligibility memo and the job (NewEvalContext, context.go:86).
  * The node SoA stays in HBM; only the dynamic columns are restored. */
+/* Apply an allocation delta of the state store to the resident snapshot
+ * without reloading the nodes (client-status changes that make allocs
+ * terminal, allocs placed by other workers' applied plans; nomad/state
+ * UpsertAllocs / UpsertPlanResults). Entry i overwrites snapshot alloc
+ * index[i], or is appended when index[i] == PE_NONE (or index == NULL); the
+ * appended ones take the next indices in order. `strs` extends the snapshot's
+ * string table (same ids for the strings it already had). Equivalent to
+ * pe_set_state with the updated table: the plan, the memo and the job are
+ * reset (a state change starts a new evaluation). */
+int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index);
 int pe_reset_plan(pe_stack* s);
 /* Stack.SetJob (stack.go:93-115 / 290-299). `strs` extends the table given to
  * pe_set_state (same ids for its first entries, job strings appended). */

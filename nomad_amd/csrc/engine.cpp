@@ -164,6 +164,7 @@ struct HostAlloc {
     bool terminal;
     int32_t priority = 0, max_parallel = 0;
     int64_t cpu = 0, mem = 0, disk = 0;
+    int32_t mbits = 0, dyn = 0;            // network use on the node's host device
     uint32_t dev_begin = 0, dev_end = 0;   // into pe_stack::alloc_dev
 };
 
@@ -338,6 +339,7 @@ struct pe_stack {
     PinnedMem h_place_out, h_place_status;   // single-evaluation count loop results (mapped)
     double phase_ms[4] = {0, 0, 0, 0};   // host prep, kernels, result copy, total (last batch)
     std::vector<pe::NodeRec> h_base_rec;     // snapshot proposed state (no plan)
+    std::vector<pe::NodeRec> h_node_rec;     // node-only part (capacities, class, reserved ports)
     DevMem d_rec, d_base_rec, d_coll_job;
     DevMem d_base;                     // windowed loops: per-row base value table
     DevMem d_prof;                     // k_chain step profile (PE_CHAIN_PROF)
@@ -778,6 +780,9 @@ void tg_ask(const pe_job* j, const pe_task_group& t, pe::Ask* a) {
     a->desired_count = t.count;
 }
 
+int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index);
+int build_alloc_state(pe_stack* s);
+
 int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) {
     const uint32_t n = nt->n;
     s->nodes.assign(n, HostNode());
@@ -926,9 +931,19 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
             h.sig = found;
         }
     }
+    s->h_node_rec = s->h_base_rec;
     s->allocs.clear();
     s->alloc_dev.clear();
-    std::vector<int64_t> dev_used(s->dev_groups.size(), 0);
+    int rc = append_allocs(s, at, nullptr);
+    if (rc) return rc;
+    return build_alloc_state(s);
+}
+
+// Allocations of a pe_alloc_table into the host mirror: appended, or, with
+// `index`, written over existing entries (index[i] < allocs.size()) or
+// appended (index[i] == PE_NONE).
+int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index) {
+    const uint32_t n = (uint32_t)s->nodes.size();
     for (uint32_t i = 0; at && i < at->count; i++) {
         const uint32_t row = at->node_row[i];
         if (row >= n) return s->fail(PE_EINVAL, "alloc node_row out of range");
@@ -936,22 +951,41 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
         a.priority = at->priority ? at->priority[i] : 0;
         a.max_parallel = at->max_parallel ? at->max_parallel[i] : 0;
         a.cpu = at->cpu_shares[i]; a.mem = at->memory_mb[i]; a.disk = at->disk_mb[i];
+        a.mbits = at->net_mbits[i];
+        a.dyn = at->dyn_ports[i];
         a.dev_begin = (uint32_t)s->alloc_dev.size();
-        for (uint32_t k = at->dev_off ? at->dev_off[i] : 0; at->dev_off && k < at->dev_off[i + 1]; k++) {
+        for (uint32_t k = at->dev_off ? at->dev_off[i] : 0; at->dev_off && k < at->dev_off[i + 1]; k++)
             s->alloc_dev.emplace_back(at->dev_group[k], at->dev_count[k]);
-            const uint32_t g = at->dev_group[k];
-            if (!a.terminal && g < s->dev_off[row + 1] - s->dev_off[row])
-                dev_used[s->dev_off[row] + g] += at->dev_count[k];
-        }
         a.dev_end = (uint32_t)s->alloc_dev.size();
-        s->allocs.push_back(a);
+        const uint32_t at_index = index ? index[i] : PE_NONE;
+        if (at_index == PE_NONE) {
+            s->allocs.push_back(a);
+        } else {
+            if (at_index >= s->allocs.size()) return s->fail(PE_EINVAL, "alloc update index out of range");
+            s->allocs[at_index] = a;
+        }
+    }
+    return PE_OK;
+}
+
+// Everything derived from the snapshot's allocations: base proposed usage,
+// device free counts, the Preemptor's per-node candidate lists.
+int build_alloc_state(pe_stack* s) {
+    const uint32_t n = (uint32_t)s->nodes.size();
+    s->h_base_rec = s->h_node_rec;
+    std::vector<int64_t> dev_used(s->dev_groups.size(), 0);
+    for (const HostAlloc& a : s->allocs) {
         if (a.terminal) continue;
-        pe::NodeRec& r = s->h_base_rec[row];
-        r.used_cpu += at->cpu_shares[i];
-        r.used_mem += at->memory_mb[i];
-        r.used_disk += at->disk_mb[i];
-        r.used_mbits += at->net_mbits[i];
-        r.used_dyn += at->dyn_ports[i];
+        for (uint32_t k = a.dev_begin; k < a.dev_end; k++) {
+            const uint32_t g = s->alloc_dev[k].first;
+            if (g < s->dev_off[a.row + 1] - s->dev_off[a.row]) dev_used[s->dev_off[a.row] + g] += s->alloc_dev[k].second;
+        }
+        pe::NodeRec& r = s->h_base_rec[a.row];
+        r.used_cpu += a.cpu;
+        r.used_mem += a.mem;
+        r.used_disk += a.disk;
+        r.used_mbits += a.mbits;
+        r.used_dyn += a.dyn;
     }
     HIP_TRY(s, upload(s->d_base_rec, s->h_base_rec));
     HIP_TRY(s, upload(s->d_rec, s->h_base_rec));
@@ -997,8 +1031,8 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
             x.priority = a.priority; x.max_parallel = a.max_parallel;
             x.job_key = s->job_keys.emplace(std::make_pair(a.job, a.ns), (uint32_t)s->job_keys.size()).first->second;
             x.jtg_key = jtg.emplace(std::make_tuple(a.job, a.ns, a.tg), (uint32_t)jtg.size()).first->second;
-            x.mbits = at->net_mbits[i];
-            x.dyn = at->dyn_ports[i];
+            x.mbits = a.mbits;
+            x.dyn = a.dyn;
             x.state_index = i;
             const uint32_t ng = s->dev_off[a.row + 1] - s->dev_off[a.row];
             for (uint32_t k = a.dev_begin; k < a.dev_end; k++) {
@@ -1990,6 +2024,40 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
     s->tgs.clear();
     s->visit.clear();
     s->offset = 0;
+    return PE_OK;
+}
+
+int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index) {
+    if (!s || !allocs) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    s->gen++;
+    HIP_TRY(s, hipSetDevice(s->device));
+    s->add_strings(strs);
+    const size_t before = s->allocs.size();
+    int rc = append_allocs(s, allocs, index);
+    if (rc) {
+        s->allocs.resize(before);
+        s->have_state = false;   // partially applied: the caller must reload
+        return rc;
+    }
+    rc = build_alloc_state(s);
+    if (rc) { s->have_state = false; return rc; }
+    // a new evaluation context, as after pe_set_state
+    std::fill(s->h_preempted.begin(), s->h_preempted.end(), 0);
+    s->offer_row = -1;
+    s->plan.clear();
+    s->tg_memo.clear();
+    s->job_memo.clear();
+    s->ref_tg_memo.clear();
+    s->ref_job_memo.clear();
+    s->spread_info_done.clear();
+    s->sum_spread_weights = 0;
+    s->have_job = false;
+    s->have_job_version = false;
+    s->tgs.clear();
+    s->visit.clear();
+    s->offset = 0;
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
     return PE_OK;
 }
 

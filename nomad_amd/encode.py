@@ -147,6 +147,13 @@ class EncodedState:
         nt.dev_attr_val = C.cast(avals_a, C.POINTER(abi.pe_attr))
         self.node_table = nt
 
+        self.alloc_table = self.encode_alloc_table(allocs)
+
+    def encode_alloc_table(self, allocs: Sequence[Allocation]) -> abi.pe_alloc_table:
+        """pe_alloc_table over this state's interner and node rows (the arrays
+        stay alive with this object)."""
+        I = self.interner.intern
+        keep = self.keep
         at = abi.pe_alloc_table()
         live = [a for a in allocs]
         at.count = len(live)
@@ -179,7 +186,7 @@ class EncodedState:
         at.dev_group = _ptr(dgrp_a, abi.u32p)
         at.dev_count = _ptr(dcnt_a, abi.u32p)
         at.max_parallel = _ptr(acol(lambda a: a.max_parallel, _i32), abi.i32p)
-        self.alloc_table = at
+        return at
 
     def strtab(self):
         t, k = self.interner.table()

@@ -208,6 +208,19 @@ class _Stack:
         self._check(self._fn("set_state")(self._h, C.byref(t), C.byref(cs.node_table), C.byref(cs.alloc_table)))
         return cs
 
+    def UpdateAllocs(self, allocs: Sequence[Allocation], index: Optional[Sequence[int]] = None):
+        """State delta without a node reload (pe_update_allocs): allocs[i]
+        replaces snapshot alloc index[i] (None / -1: appended)."""
+        fn = self._fn("update_allocs")
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.POINTER(abi.pe_strtab), C.POINTER(abi.pe_alloc_table), abi.u32p]
+        at = self.state.encode_alloc_table(allocs)
+        idx = np.asarray([abi.PE_NONE if (index is None or index[i] is None or index[i] < 0) else index[i]
+                          for i in range(len(allocs))] or [0], dtype=np.uint32)
+        t = self.state.strtab()
+        self._check(fn(self._h, C.byref(t), C.byref(at), idx.ctypes.data_as(abi.u32p)))
+        self._job = None
+
     def ResetPlan(self):
         """New evaluation on the resident snapshot (fresh EvalContext)."""
         self._check(self._fn("reset_plan")(self._h))
