@@ -28,6 +28,8 @@ BASELINE.json config (sections, --sections to choose):
               ranks: one 80-byte record all-gather (RCCL) per placement
   plan_apply  plan applier fit check (evaluatePlanPlacements) of a system-job plan
               over a 100k-node snapshot, node ranges sharded over the ranks
+  ingest      full snapshot upload (pe_set_state) vs an alloc delta
+              (pe_update_allocs) on a 100k-node cluster
 Each section times the engine on the GPU and the oracle (C++ restatement) on a
 bounded sample of the same workload on one host core.
 """
@@ -64,7 +66,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--sweep-nodes", type=int, default=1 << 24,
                    help="nodes of the scoring-sweep roofline measurement (0 = skip)")
-    p.add_argument("--sections", default="c3,c4,c5,c3_sharded,plan_apply",
+    p.add_argument("--sections", default="c3,c4,c5,c3_sharded,plan_apply,ingest",
                    help="comma list of extra config sections (empty = none)")
     return p.parse_args()
 
@@ -435,6 +437,59 @@ def section_c3_sharded(device, rank, world, pg, placements=64):
                          % ("RCCL" if gdev is not None else "gloo, host memory"))}
 
 
+def section_ingest(device, n=100000, reps=5):
+    """Snapshot ingest: a full pe_set_state of an n-node
+    cluster against pe_update_allocs of a state-store delta (10 % of the allocs
+    turn terminal, n/20 new allocs from other workers' plans). C calls only; the
+    Python flattening (the cgo shim's work) is done before timing."""
+    import ctypes as C
+    import copy
+    import random
+    from nomad_amd import abi, synth
+    from nomad_amd.encode import EncodedState, Interner
+    from nomad_amd.stack import GenericStack
+    from nomad_amd.structs import Allocation
+    nodes, allocs = synth.cluster_c2(n, seed=42)
+    rng = random.Random(3)
+    changed, index = [], []
+    for i, a in enumerate(allocs):
+        if rng.random() < 0.1:
+            b = copy.copy(a)
+            b.terminal = True
+            changed.append(b)
+            index.append(i)
+    for k in range(n // 20):
+        nd = nodes[rng.randrange(n)]
+        changed.append(Allocation(node_id=nd.id, job_id="other-%d" % (k % 11), task_group="web",
+                                  cpu_shares=250, memory_mb=128, disk_mb=150))
+        index.append(abi.PE_NONE)
+    st = GenericStack(device=device)
+    lib, h = st._lib, st._h
+    lib.pe_update_allocs.restype = C.c_int
+    lib.pe_update_allocs.argtypes = [C.c_void_p, C.POINTER(abi.pe_strtab), C.POINTER(abi.pe_alloc_table), abi.u32p]
+    es = EncodedState(nodes, allocs, Interner())
+    t_full, t_upd = [], []
+    idx = np.asarray(index, dtype=np.uint32)
+    for _ in range(reps):
+        tab = es.strtab()
+        t0 = time.perf_counter()
+        rc = lib.pe_set_state(h, C.byref(tab), C.byref(es.node_table), C.byref(es.alloc_table))
+        t_full.append(time.perf_counter() - t0)
+        assert rc == 0
+        at = es.encode_alloc_table(changed)
+        tab = es.strtab()
+        t0 = time.perf_counter()
+        rc = lib.pe_update_allocs(h, C.byref(tab), C.byref(at), idx.ctypes.data_as(abi.u32p))
+        t_upd.append(time.perf_counter() - t0)
+        assert rc == 0
+    st.close()
+    full, upd = float(np.median(t_full)), float(np.median(t_upd))
+    return {"workload": "C2-shaped cluster of %d nodes, %d allocs; delta: %d allocs terminal + %d new"
+                        % (n, len(allocs), sum(1 for i in index if i != abi.PE_NONE),
+                           sum(1 for i in index if i == abi.PE_NONE)),
+            "set_state_ms": full * 1e3, "update_allocs_ms": upd * 1e3, "speedup": full / upd}
+
+
 def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
     """Plan applier fit check: a system-job plan placing one
     alloc on every node of a 100k-node snapshot, evaluatePlanPlacements ->
@@ -614,6 +669,9 @@ def main():
                 extra[sec] = section_c3_sharded(local, rank, world, pg)
             elif sec == "plan_apply":
                 extra[sec] = section_plan_apply(local, rank, world, pg, cpu_s)
+            elif sec == "ingest":
+                if rank == 0:
+                    extra[sec] = section_ingest(local)
         except Exception as e:   # an extra section never takes the headline line down
             extra[sec] = {"error": "%s: %s" % (type(e).__name__, e)}
         barrier(pg)
