@@ -2409,6 +2409,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         HIP_TRY(s, hipMemcpyAsync(sc.data(), s->d_trace_scores.p, sc.size() * 8, hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
         const bool has_aff = !g.affinities.empty();
+        const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
         std::map<int, std::vector<uint32_t>> counts;   // distinct_property use counts, read on demand
         for (size_t i = 0; i < rows.size(); i++) {
             const uint32_t row = rows[i], code = codes[i];
@@ -2419,11 +2420,13 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                     sm.row = row;
                     sm.scores.emplace_back("binpack", o[0]);
                     if (a.dev_tw != 0.0) sm.scores.emplace_back("devices", o[1]);
-                    if (a.anti_aff) sm.scores.emplace_back("job-anti-affinity", o[2]);
-                    sm.scores.emplace_back("node-reschedule-penalty", (code & pe::kTrPenalty) ? -1.0 : 0.0);
-                    if (!has_aff) sm.scores.emplace_back("node-affinity", 0.0);
-                    else if (o[3] != 0.0) sm.scores.emplace_back("node-affinity", o[3]);
-                    if (o[4] != 0.0) sm.scores.emplace_back("allocation-spread", o[4]);
+                    if (generic) {   // the SystemStack ranks with BinPack alone (stack.go:277-281)
+                        if (a.anti_aff) sm.scores.emplace_back("job-anti-affinity", o[2]);
+                        sm.scores.emplace_back("node-reschedule-penalty", (code & pe::kTrPenalty) ? -1.0 : 0.0);
+                        if (!has_aff) sm.scores.emplace_back("node-affinity", 0.0);
+                        else if (o[3] != 0.0) sm.scores.emplace_back("node-affinity", o[3]);
+                        if (o[4] != 0.0) sm.scores.emplace_back("allocation-spread", o[4]);
+                    }
                     sm.norm = o[5];
                     heap.push(std::move(sm));
                     break;
@@ -2518,6 +2521,8 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         if (s->cfg.preempt) rc = run_evict_select(s, *s->tgs[tgi], s->visit, 0, nullptr, out, &no);
         else rc = run_place(s, tgi, 1, 0, s->visit, 0, nullptr, out, &placed, &no);
         s->limit = saved;
+        if (rc == PE_OK && !s->cfg.preempt && s->metrics_on)
+            rc = compute_metrics(s, *s->tgs[tgi], s->visit, 0, out->nodes_evaluated, nullptr);
         return rc;
     }
     if (opts && opts->preferred_count > 0) {

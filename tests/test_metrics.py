@@ -195,3 +195,36 @@ def test_metrics_preferred_and_penalty_nodes():
             break
         eng.Commit(0, re.row)
         ora.Commit(0, ro.row)
+
+
+@pytest.mark.gpu
+def test_metrics_system_stack():
+    # SystemScheduler: one single-node Select per node (SetNodes([node])); the
+    # SystemStack ranks with BinPack alone, so ScoreMetaData holds binpack and
+    # normalized-score only (stack.go:277-281)
+    from nomad_amd.stack import SystemStack
+    from oracle.oracle import OracleSystemStack
+    nodes, allocs = synth.cluster_c4(300, seed=13)
+    job = synth.mock_system_job()
+    sts = []
+    for cls in (SystemStack, OracleSystemStack):
+        st = cls()
+        st.EnableMetrics()
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        sts.append(st)
+    eng, ora = sts
+    seen = set()
+    for nd in nodes:
+        eng.SetNodes([nd])
+        ora.SetNodes([nd])
+        re, ro = eng.SelectRaw(0), ora.SelectRaw(0)
+        assert (re.row, re.nodes_filtered, re.nodes_exhausted) == (ro.row, ro.nodes_filtered, ro.nodes_exhausted)
+        me, mo = eng.LastMetrics(), ora.LastMetrics()
+        assert me == mo, (nd.id, me, mo)
+        seen |= set(mo["ConstraintFiltered"]) | set(mo["DimensionExhausted"])
+        if ro.row >= 0:
+            assert set(mo["ScoreMetaData"][0][2]) <= {"binpack", "devices"}
+            eng.Commit(0, re.row)
+            ora.Commit(0, ro.row)
+    assert seen
