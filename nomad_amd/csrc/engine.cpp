@@ -2751,6 +2751,27 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
         count = 0;   // done: skip the fused loop below
         no = s->offset;
     }
+    if (count && !parallel && !s->cfg.preempt && s->limit >= nv && nv >= s->sweep_min && s->visit_unique &&
+        g.n_spread == (int)g.psets.size()) {
+        // A whole pass per placement over a long list: k_place would sweep it
+        // with one workgroup; the multi-CU sweep per Select is several times
+        // faster from sweep_min nodes on (C3 shape, 100k nodes: 669 -> ~180 us
+        // per placement). A full pass leaves the cursor where it is.
+        while (p < count) {
+            rc = prepare_tg(s, tgi, s->visit, s->offset);
+            if (rc) return rc;
+            rc = run_sweep_select(s, g, nullptr, &out[p]);
+            if (rc) return rc;
+            if (out[p].row < 0) break;
+            s->offer_row = out[p].row;
+            s->offers = pack_offers(&out[p]);
+            rc = pe_commit(s, tgi, out[p].row);
+            if (rc) return rc;
+            p++;
+        }
+        count = 0;
+        no = s->offset;
+    }
     if (count) {
         rc = run_place(s, tgi, count, 1, s->visit, s->offset, nullptr, out, &p, &no);
         if (rc) return rc;
