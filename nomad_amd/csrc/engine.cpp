@@ -65,6 +65,8 @@ uint32_t pe_chain_max_limit();
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n);
 int pe_chain_blocks_per_cu(size_t lds);
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st);
+hipError_t pe_launch_sweep_step(const pe::SweepArgs* a, uint32_t blocks, const uint32_t* visit, uint32_t n,
+                                uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
                            uint32_t n, uint32_t* out, const uint32_t* penalty_bits, double log10,
                            const double* spread_tab, double* scores, hipStream_t st);
@@ -324,6 +326,7 @@ struct pe_stack {
     // full-scan sweep path
     DevMem d_rank_of, d_sweep_recs, d_sweep_merged, d_spread_tab, d_record;
     uint32_t sweep_min = 1u << 15;     // visit lists at least this long use the multi-CU sweep
+    uint32_t loop_sweep_min = 8192;    // full-pass count loops this long run device-resident sweeps
     bool visit_unique = true;
     double last_sweep_ms = 0;
     std::vector<uint32_t> h_orders;
@@ -377,6 +380,7 @@ struct pe_stack {
     std::vector<int8_t> ref_job_memo;
     std::string metrics_text;
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
+    DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
 
     // visit order
     std::vector<uint32_t> visit;
@@ -1543,8 +1547,10 @@ bool full_scan_kernel(pe_stack* s, TgPlan& g, uint32_t n) {
 // its rows to a SweepRec, one merge yields the winner.
 // The sweep over snapshot rows [row_begin, row_end) (one GPU's shard, or all
 // rows): per-workgroup SweepRec records merged into *rec.
-int sweep_partial(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_t row_begin, uint32_t row_end,
-                  pe::SweepArgs* args, pe::SweepRec* rec) {
+// SweepArgs and grid of one full-pass Select over rows [row_begin, row_end)
+// (tables, aux fold, penalty bits); no launch.
+int sweep_setup(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_t row_begin, uint32_t row_end,
+                pe::SweepArgs* args, uint32_t* blocks_out) {
     const uint32_t n = (uint32_t)s->visit.size();
     pe::SweepArgs& A = *args;
     std::memset(&A, 0, sizeof(A));
@@ -1568,7 +1574,6 @@ int sweep_partial(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_
     }
     if (!g.psets.empty()) {
         HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
-        HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
         A.spread_tab = s->d_spread_tab.as<double>();
     }
     if (!g.aux_valid) {
@@ -1592,6 +1597,17 @@ int sweep_partial(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_
     HIP_TRY(s, s->d_sweep_merged.ensure(sizeof(pe::SweepRec)));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
     A.recs = s->d_sweep_recs.as<pe::SweepRec>();
+    *blocks_out = blocks;
+    return PE_OK;
+}
+
+int sweep_partial(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_t row_begin, uint32_t row_end,
+                  pe::SweepArgs* args, pe::SweepRec* rec) {
+    pe::SweepArgs& A = *args;
+    uint32_t blocks = 0;
+    int rc = sweep_setup(s, g, opts, row_begin, row_end, args, &blocks);
+    if (rc) return rc;
+    if (A.spread_tab) HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
     if (row_end <= row_begin) {   // an empty shard contributes the identity record
         pe_rec_init(rec);
         s->last_ms = s->last_sweep_ms = 0;
@@ -1970,6 +1986,7 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     s->sweep_per_cu_aux = pe_sweep_blocks_per_cu(true);
     s->log10 = pe::gm::log_go(10.0);
     if (const char* e = std::getenv("PE_SWEEP_MIN")) s->sweep_min = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("PE_LOOP_SWEEP_MIN")) s->loop_sweep_min = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("PE_RESULTS_VIA_COPY")) s->results_via_copy = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_WINDOW_LAZY")) s->use_base = std::atoi(e) == 0;
     return s;
@@ -2696,6 +2713,54 @@ static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Device-resident full-pass count loop (see pe_place). Same results as
+// `count` x (run_sweep_select + pe_commit).
+static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count, pe_ranked_node* out,
+                            uint32_t* placed) {
+    const uint32_t n = (uint32_t)s->visit.size();
+    pe::SweepArgs A;
+    uint32_t blocks = 0;
+    int rc = sweep_setup(s, g, nullptr, 0, (uint32_t)s->nodes.size(), &A, &blocks);
+    if (rc) return rc;
+    // one placement is latency-bound: spread the rows over more workgroups
+    // (256 rows each) than a single bandwidth-bound sweep would use
+    blocks = std::max<uint32_t>(blocks, std::min<uint32_t>(((uint32_t)s->nodes.size() + 255) / 256,
+                                                           (uint32_t)s->n_cu * (uint32_t)s->sweep_per_cu_aux));
+    if (const char* e = std::getenv("PE_LOOP_BLOCKS")) blocks = (uint32_t)std::max(1, std::atoi(e));
+    HIP_TRY(s, s->d_sweep_recs.ensure(sizeof(pe::SweepRec) * blocks));
+    A.recs = s->d_sweep_recs.as<pe::SweepRec>();
+    HIP_TRY(s, upload_visit(s, s->visit));
+    HIP_TRY(s, s->d_loop_out.ensure(sizeof(pe_ranked_node) * (size_t)(count + 1)));
+    HIP_TRY(s, s->d_loop_state.ensure(2 * sizeof(uint32_t)));
+    HIP_TRY(s, hipMemsetAsync(s->d_loop_state.p, 0, 2 * sizeof(uint32_t), s->stream));
+    uint32_t* state = s->d_loop_state.as<uint32_t>();
+    uint32_t h_state[2] = {0, 0};
+    const uint32_t chunk = 64;
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    // the first placement's spread table; each step rebuilds it for the next
+    if (A.spread_tab) HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
+    for (uint32_t k = 0; k < count && !h_state[0]; k += chunk) {
+        const uint32_t m = std::min(chunk, count - k);
+        for (uint32_t j = 0; j < m; j++)
+            HIP_TRY(s, pe_launch_sweep_step(&A, blocks, s->d_visit.as<uint32_t>(), n, s->offset,
+                                            s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+    }
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    const uint32_t p = h_state[1];
+    const uint32_t nrec = std::min(count, p + (h_state[0] ? 1u : 0u));
+    HIP_TRY(s, hipMemcpyAsync(out, s->d_loop_out.p, sizeof(pe_ranked_node) * nrec, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    for (uint32_t i = 0; i < p; i++) s->plan.emplace_back(g.name, (uint32_t)out[i].row);   // Plan.AppendAlloc
+    s->offer_row = -1;
+    *placed = p;
+    return PE_OK;
+}
+
 int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
     const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
     const double t_enter = prof ? now_us() : 0.0;
@@ -2751,24 +2816,17 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
         count = 0;   // done: skip the fused loop below
         no = s->offset;
     }
-    if (count && !parallel && !s->cfg.preempt && s->limit >= nv && nv >= s->sweep_min && s->visit_unique &&
-        g.n_spread == (int)g.psets.size()) {
+    bool same_name = false;   // pe_commit would rebuild other task groups' collision counts
+    for (size_t k = 0; k < s->tgs.size(); k++) same_name = same_name || (k != tgi && s->tgs[k]->name == g.name);
+    if (count && !parallel && !s->cfg.preempt && s->limit >= nv && nv >= s->loop_sweep_min && s->visit_unique &&
+        g.n_spread == (int)g.psets.size() && !same_name) {
         // A whole pass per placement over a long list: k_place would sweep it
-        // with one workgroup; the multi-CU sweep per Select is several times
-        // faster from sweep_min nodes on (C3 shape, 100k nodes: 669 -> ~180 us
-        // per placement). A full pass leaves the cursor where it is.
-        while (p < count) {
-            rc = prepare_tg(s, tgi, s->visit, s->offset);
-            if (rc) return rc;
-            rc = run_sweep_select(s, g, nullptr, &out[p]);
-            if (rc) return rc;
-            if (out[p].row < 0) break;
-            s->offer_row = out[p].row;
-            s->offers = pack_offers(&out[p]);
-            rc = pe_commit(s, tgi, out[p].row);
-            if (rc) return rc;
-            p++;
-        }
+        // with one workgroup. Here every placement is a multi-CU sweep +
+        // merge followed by k_sweep_step (winner record + commit on the
+        // device), queued back to back with no host round trip; the host only
+        // checks the stop flag between chunks. A full pass leaves the cursor.
+        rc = sweep_count_loop(s, g, tgi, count, out, &p);
+        if (rc) return rc;
         count = 0;
         no = s->offset;
     }

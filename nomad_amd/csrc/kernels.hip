@@ -1701,8 +1701,8 @@ __global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts, u
 // Host-driven Plan.AppendAlloc on the HBM SoA (pe_commit). `offers`: the
 // device offers of the Select that chose the node (one byte per request), or
 // ~0u to assign them on the current state.
-__global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t offers) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ __forceinline__ void commit_row(const NodeSoA& s, const TgTables& t, const Ask& a, uint32_t row,
+                                           uint32_t offers) {
     NodeRec& r = s.rec[row];
     r.used_cpu += a.cpu;
     r.used_mem += a.mem;
@@ -1729,6 +1729,11 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t of
         const uint32_t v = pset_value(t, p, row, c);
         if (v != kMissing) t.pset_counts[p][v] += 1;
     }
+}
+
+__global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t offers) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    commit_row(s, t, a, row, offers);
 }
 
 // One pass of the scoring sweep over rows [row_begin, row_end), one tile of
@@ -1938,6 +1943,73 @@ __global__ void k_node_record(SweepArgs A, uint32_t row, pe_ranked_node* out) {
     out->n_scores = ev.nscores;
     for (int k = 0; k < PE_MAX_SCORES; k++) out->scores[k] = k < (int)ev.nscores ? ev.parts[k] : 0.0;
     record_offers(A.soa, A.ask, A.tg, row, 0u, out);
+}
+
+// One placement of the device-resident full-pass count loop (pe_place on long
+// lists), after this placement's k_sweep: thread 0 merges the per-block
+// SweepRecs (k_sweep_merge), resolves the Select result (sweep_finish +
+// k_node_record) and commits the winner (k_commit with the record's device
+// offers); then the workgroup rebuilds the spread table for the next
+// placement from the updated counts (k_spread_table). state[0]: a nil Select
+// ended the loop (later steps do nothing); state[1]: placements so far.
+__global__ void __launch_bounds__(256) k_sweep_step(SweepArgs A, uint32_t nrecs, const uint32_t* visit, uint32_t n,
+                                                    uint32_t offset, pe_ranked_node* out, uint32_t* state) {
+    __shared__ uint32_t counts[kMaxPsets * kMaxValues];
+    __shared__ uint32_t scratch[4];
+    __shared__ SweepRec red[4];
+    __shared__ uint32_t go;
+    if (state[0]) return;   // every thread reads the flag before thread 0 may set it
+    SweepRec rec;
+    rec_init(rec);
+    for (uint32_t i = threadIdx.x; i < nrecs; i += 256) rec_merge(rec, A.recs[i]);
+    rec_block_reduce<256>(rec, red);
+    if (threadIdx.x == 0) {
+        go = 0;
+        {
+            pe_ranked_node* o = out + state[1];
+            pe_ranked_node z = {};
+            *o = z;
+            o->row = -1;
+            o->nodes_evaluated = n;            // a full pass pulls every node
+            o->nodes_filtered = rec.filtered;
+            o->nodes_exhausted = rec.exhausted;
+            o->new_offset = offset;            // and leaves the cursor where it is
+            const uint32_t rank = rec_winner(rec);
+            if (rank == kEmpty) {
+                state[0] = 1;
+            } else {
+                uint32_t pos = offset + rank;
+                if (pos >= n) pos -= n;
+                const uint32_t row = visit[pos];
+                Overlay none;
+                none.keys = nullptr;
+                NodeEval ev;
+                eval_node<true>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, A.spread_tab, row,
+                                &ev);
+                o->row = (int32_t)row;
+                o->final_score = ev.score;
+                o->n_scores = ev.nscores;
+                for (int k = 0; k < PE_MAX_SCORES; k++) o->scores[k] = k < (int)ev.nscores ? ev.parts[k] : 0.0;
+                record_offers(A.soa, A.ask, A.tg, row, 0u, o);
+                uint32_t offers = 0xFFFFFFFFu;
+                if (o->n_device_offers) {
+                    offers = 0;
+                    for (uint32_t q = 0; q < o->n_device_offers && q < 4; q++)
+                        offers |= (o->device_offer_group[q] & 255u) << (8 * q);
+                }
+                commit_row(A.soa, A.tg, A.ask, row, offers);
+                state[1] += 1;
+                go = A.spread_tab != nullptr;
+            }
+        }
+    }
+    __syncthreads();
+    if (!go) return;   // workgroup-uniform
+    const TgTables& t = A.tg;
+    for (int p = 0; p < t.n_psets; p++)
+        for (int v = threadIdx.x; v < t.pset_nvals[p]; v += 256) counts[p * kMaxValues + v] = t.pset_counts[p][v];
+    __syncthreads();
+    build_spread_table<256>(t, counts, const_cast<double*>(A.spread_tab), scratch);
 }
 
 // node_feas[row] = class_ok[cls] && node_ok[row]: one verdict byte per node so
@@ -2166,5 +2238,15 @@ hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(pe::k_trace, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, n, out,
                        penalty_bits, log10, spread_tab, scores);
+    return hipGetLastError();
+}
+
+// One placement of the device-resident count loop: k_sweep (no merge) over
+// `blocks` workgroups, then k_sweep_step.
+hipError_t pe_launch_sweep_step(const pe::SweepArgs* a, uint32_t blocks, const uint32_t* visit, uint32_t n,
+                                uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st) {
+    if (a->node_aux) hipLaunchKernelGGL((pe::k_sweep<256, false, 0, true>), dim3(blocks), dim3(256), 0, st, *a);
+    else hipLaunchKernelGGL((pe::k_sweep<256, false>), dim3(blocks), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(pe::k_sweep_step, dim3(1), dim3(256), 0, st, *a, blocks, visit, n, offset, out, state);
     return hipGetLastError();
 }

@@ -1,6 +1,6 @@
 """Full-pass count loops routed through the multi-CU sweep (pe_place when the
 list is at least sweep_min long): identical placements to the oracle. The
-threshold is lowered with PE_SWEEP_MIN so the path runs at test sizes."""
+threshold is lowered with PE_LOOP_SWEEP_MIN so the path runs at test sizes."""
 import os
 
 import pytest
@@ -12,15 +12,15 @@ from tests.helpers import assert_same_placements, run_place
 
 def _engine_low_threshold():
     from nomad_amd.stack import GenericStack
-    old = os.environ.get("PE_SWEEP_MIN")
-    os.environ["PE_SWEEP_MIN"] = "1000"
+    old = os.environ.get("PE_LOOP_SWEEP_MIN")
+    os.environ["PE_LOOP_SWEEP_MIN"] = "1000"
     try:
         return GenericStack()
     finally:
         if old is None:
-            del os.environ["PE_SWEEP_MIN"]
+            del os.environ["PE_LOOP_SWEEP_MIN"]
         else:
-            os.environ["PE_SWEEP_MIN"] = old
+            os.environ["PE_LOOP_SWEEP_MIN"] = old
 
 
 @pytest.mark.gpu
@@ -45,3 +45,18 @@ def test_sweep_count_loop_until_full():
     _, _, want = run_place(OracleGenericStack, nodes, allocs, job, perm)
     assert got[-1].row == -1
     assert_same_placements(got, want)
+
+
+@pytest.mark.gpu
+def test_sweep_count_loop_devices():
+    # device asks on the device-resident loop: the step kernel commits the
+    # record's device offers (AssignDevice choice) like pe_commit does
+    from nomad_amd.structs import Affinity
+    nodes, allocs = synth.cluster_c5(1500, seed=6, busy=0.3)
+    job = synth.job_c5(150)
+    job.affinities.append(Affinity("${node.datacenter}", "dc1", "=", 40))   # full pass (limit MaxInt32)
+    perm = synth.shuffle(1500, 2)
+    _, _, got = run_place(_engine_low_threshold, nodes, allocs, job, perm)
+    _, _, want = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    assert_same_placements(got, want)
+    assert [g.device_offers for g in got] == [w.device_offers for w in want]
