@@ -25,6 +25,8 @@
 #include "plan_types.h"
 
 hipError_t pe_launch_plan_eval(const pa::PlanArgs* a, int group, hipStream_t st);
+hipError_t pe_launch_plan_patch(pa::NodeRec* nodes, pa::AllocRec* pool, const uint32_t* dead, uint32_t n_dead,
+                                const uint32_t* rows, const pa::NodeRec* recs, uint32_t n_rows, hipStream_t st);
 
 namespace {
 
@@ -138,8 +140,9 @@ struct pe_planner {
     std::vector<uint32_t> pool_of;     // caller index -> pool index (kNone: terminal, not in the pool)
     std::vector<pa::AllocRec> pool;
     std::vector<uint64_t> pool_keys;
+    std::vector<pa::Chunk> chunks;     // allocs appended by commits since the last compaction
 
-    DBuf d_nodes, d_node_keys, d_pool, d_pool_keys;
+    DBuf d_nodes, d_node_keys, d_pool, d_pool_keys, d_chunks, d_patch_dead, d_patch_rows, d_patch_recs;
     DBuf d_pn, d_rm, d_pallocs, d_pkeys, d_big, d_scratch, d_reason;
 
     int fail(int code, const std::string& m) { err = m; return code; }
@@ -331,8 +334,9 @@ struct pe_planner {
                          [&](uint32_t a, uint32_t b) { return allocs[a].row < allocs[b].row; });
         pool.assign(order.size(), pa::AllocRec{});
         pool_keys.clear();
+        chunks.clear();
         pool_of.assign(allocs.size(), pa::kNone);
-        for (auto& nd : nodes) { nd.alloc_off = 0; nd.alloc_cnt = 0; nd.alloc_keys = 0; }
+        for (auto& nd : nodes) { nd.alloc_off = 0; nd.alloc_cnt = 0; nd.alloc_keys = 0; nd.ext_head = pa::kNone; }
         for (uint32_t q = 0; q < order.size(); q++) {
             const HAlloc& h = allocs[order[q]];
             pool_of[order[q]] = q;
@@ -349,13 +353,28 @@ struct pe_planner {
             nd.alloc_keys += ar.n_keys;
         }
         hipError_t e;
-        if ((e = upload(d_nodes, nodes.data(), nodes.size() * sizeof(pa::NodeRec))) != hipSuccess ||
+        // headroom for the commits that append to the pool before the next compaction
+        const size_t room = std::max<size_t>(pool.size(), 4096);
+        const size_t key_room = std::max<size_t>(pool_keys.size(), 16384);
+        if ((e = d_pool.reserve((pool.size() + room) * sizeof(pa::AllocRec))) != hipSuccess ||
+            (e = d_pool_keys.reserve((pool_keys.size() + key_room) * 8)) != hipSuccess ||
+            (e = d_chunks.reserve(std::max<size_t>(nodes.size() / 2, 4096) * sizeof(pa::Chunk))) != hipSuccess ||
+            (e = upload(d_nodes, nodes.data(), nodes.size() * sizeof(pa::NodeRec))) != hipSuccess ||
             (e = upload(d_node_keys, node_keys.data(), node_keys.size() * 8)) != hipSuccess ||
             (e = upload(d_pool, pool.data(), pool.size() * sizeof(pa::AllocRec))) != hipSuccess ||
             (e = upload(d_pool_keys, pool_keys.data(), pool_keys.size() * 8)) != hipSuccess ||
             (e = hipStreamSynchronize(stream)) != hipSuccess)
             return fail(PE_EHIP, std::string("planner upload: ") + hipGetErrorString(e));
         return PE_OK;
+    }
+
+    // Copy into an existing device buffer at an offset; false when it does not fit.
+    bool upload_at(DBuf& b, size_t off, const void* src, size_t bytes, hipError_t* e) {
+        *e = hipSuccess;
+        if (bytes == 0) return true;
+        if (off + bytes > b.cap) return false;
+        *e = hipMemcpyAsync((char*)b.p + off, src, bytes, hipMemcpyHostToDevice, stream);
+        return true;
     }
 
     hipError_t upload(DBuf& b, const void* src, size_t bytes) {
@@ -475,9 +494,16 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
         if (!nd.ready || !nd.eligible) continue;
         uint64_t bound = (uint64_t)nd.n_keys + nd.alloc_keys;
         bytes += 8ull * nd.n_keys + sizeof(pa::AllocRec) * (uint64_t)nd.alloc_cnt + 4ull * r.rm_cnt;
-        for (uint32_t q = nd.alloc_off; q < nd.alloc_off + nd.alloc_cnt; q++) {
-            const bool gone = std::binary_search(rm.begin() + r.rm_off, rm.end(), q);
-            if (!gone) bytes += 8ull * p->pool[q].n_keys;
+        auto count_range = [&](uint32_t off, uint32_t cnt) {
+            for (uint32_t q = off; q < off + cnt; q++) {
+                const bool gone = p->pool[q].terminal || std::binary_search(rm.begin() + r.rm_off, rm.end(), q);
+                if (!gone) bytes += 8ull * p->pool[q].n_keys;
+            }
+        };
+        count_range(nd.alloc_off, nd.alloc_cnt);
+        for (uint32_t c = nd.ext_head; c != pa::kNone; c = p->chunks[c].next) {
+            bytes += sizeof(pa::Chunk) + sizeof(pa::AllocRec) * (uint64_t)p->chunks[c].cnt;
+            count_range(p->chunks[c].off, p->chunks[c].cnt);
         }
         for (uint32_t j = r.place_off; j < r.place_off + r.place_cnt; j++) {
             bound += pa_recs[j].n_keys;
@@ -502,6 +528,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
         return p->fail(PE_EHIP, std::string("planner plan upload: ") + hipGetErrorString(e));
     pa::PlanArgs a{};
     a.nodes = (const pa::NodeRec*)p->d_nodes.p;
+    a.chunks = (const pa::Chunk*)p->d_chunks.p;
     a.pool = (const pa::AllocRec*)p->d_pool.p;
     a.node_keys = (const uint64_t*)p->d_node_keys.p;
     a.pool_keys = (const uint64_t*)p->d_pool_keys.p;
@@ -536,28 +563,79 @@ int pe_planner_commit(pe_planner* p, const pe_strtab* strs, const pe_plan* plan,
     int rc = p->map_strings(strs);
     if (rc) return rc;
     const pe_plan_alloc_table& pt = plan->allocs;
-    std::vector<HAlloc> add;
+    for (uint32_t i = 0; i < plan->n_nodes; i++) {   // validate before changing anything
+        if (!keep[i]) continue;
+        const uint32_t row = plan->node_row[i];
+        if (plan->place_off[i + 1] > plan->place_off[i] && (row == pa::kNone || row >= p->nodes.size()))
+            return p->fail(PE_EINVAL, "commit places allocs on a node outside the snapshot");
+        if (plan->remove_off)
+            for (uint32_t j = plan->remove_off[i]; j < plan->remove_off[i + 1]; j++)
+                if (plan->remove_alloc[j] >= p->allocs.size()) return p->fail(PE_EINVAL, "remove_alloc out of range");
+    }
+    // Incremental: removed allocs turn terminal in place, placed allocs are
+    // appended to the pool as one chunk per node (chained from the node's
+    // record); the device gets the appended records and a small patch.
+    const size_t pool0 = p->pool.size(), keys0 = p->pool_keys.size(), chunks0 = p->chunks.size();
+    std::vector<uint32_t> dead, rows;
+    HAlloc h;
     for (uint32_t i = 0; i < plan->n_nodes; i++) {
         if (!keep[i]) continue;
         const uint32_t row = plan->node_row[i];
-        const uint32_t b = plan->place_off[i], e = plan->place_off[i + 1];
-        if (e > b && (row == pa::kNone || row >= p->nodes.size()))
-            return p->fail(PE_EINVAL, "commit places allocs on a node outside the snapshot");
         if (plan->remove_off)
             for (uint32_t j = plan->remove_off[i]; j < plan->remove_off[i + 1]; j++) {
                 const uint32_t a = plan->remove_alloc[j];
-                if (a >= p->allocs.size()) return p->fail(PE_EINVAL, "remove_alloc out of range");
+                if (p->allocs[a].terminal) continue;
                 p->allocs[a].terminal = 1;
+                if (p->pool_of[a] != pa::kNone) {
+                    dead.push_back(p->pool_of[a]);
+                    p->pool[p->pool_of[a]].terminal = 1;
+                }
             }
+        const uint32_t b = plan->place_off[i], e = plan->place_off[i + 1];
+        if (e == b) continue;
+        pa::NodeRec& nd = p->nodes[row];
+        pa::Chunk ch{(uint32_t)p->pool.size(), e - b, nd.ext_head, 0};
         for (uint32_t j = b; j < e; j++) {
-            HAlloc h;
-            if ((rc = p->flatten(&pt, j, &h))) return rc;
+            if ((rc = p->flatten(&pt, j, &h))) return rc;   // validated by the evaluate of this plan
             h.row = row;
-            add.push_back(std::move(h));
+            pa::AllocRec ar{};
+            ar.cpu = h.cpu; ar.mem = h.mem; ar.disk = h.disk;
+            ar.key_off = (uint32_t)p->pool_keys.size();
+            ar.n_keys = (uint16_t)h.keys.size();
+            ar.terminal = h.terminal;
+            ar.bad_port = h.bad_port;
+            p->pool_keys.insert(p->pool_keys.end(), h.keys.begin(), h.keys.end());
+            nd.alloc_keys += ar.n_keys;
+            p->pool_of.push_back((uint32_t)p->pool.size());
+            p->pool.push_back(ar);
+            p->allocs.push_back(h);
         }
+        if (nd.ext_head == ch.next) rows.push_back(row);   // first chunk of this commit for the row
+        nd.ext_head = (uint32_t)p->chunks.size();
+        p->chunks.push_back(ch);
     }
-    for (auto& h : add) p->allocs.push_back(std::move(h));
-    return p->rebuild_pool();
+    hipError_t e = hipSuccess;
+    const bool fits =
+        p->upload_at(p->d_pool, pool0 * sizeof(pa::AllocRec), p->pool.data() + pool0,
+                     (p->pool.size() - pool0) * sizeof(pa::AllocRec), &e) && e == hipSuccess &&
+        p->upload_at(p->d_pool_keys, keys0 * 8, p->pool_keys.data() + keys0, (p->pool_keys.size() - keys0) * 8, &e) &&
+        e == hipSuccess &&
+        p->upload_at(p->d_chunks, chunks0 * sizeof(pa::Chunk), p->chunks.data() + chunks0,
+                     (p->chunks.size() - chunks0) * sizeof(pa::Chunk), &e) && e == hipSuccess;
+    if (e != hipSuccess) return p->fail(PE_EHIP, std::string("planner commit upload: ") + hipGetErrorString(e));
+    if (!fits) return p->rebuild_pool();   // append room used up: compact
+    std::vector<pa::NodeRec> recs(rows.size());
+    for (size_t k = 0; k < rows.size(); k++) recs[k] = p->nodes[rows[k]];
+    if ((e = p->upload(p->d_patch_dead, dead.data(), dead.size() * 4)) != hipSuccess ||
+        (e = p->upload(p->d_patch_rows, rows.data(), rows.size() * 4)) != hipSuccess ||
+        (e = p->upload(p->d_patch_recs, recs.data(), recs.size() * sizeof(pa::NodeRec))) != hipSuccess ||
+        (e = pe_launch_plan_patch((pa::NodeRec*)p->d_nodes.p, (pa::AllocRec*)p->d_pool.p,
+                                  (const uint32_t*)p->d_patch_dead.p, (uint32_t)dead.size(),
+                                  (const uint32_t*)p->d_patch_rows.p, (const pa::NodeRec*)p->d_patch_recs.p,
+                                  (uint32_t)rows.size(), p->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(p->stream)) != hipSuccess)
+        return p->fail(PE_EHIP, std::string("planner commit patch: ") + hipGetErrorString(e));
+    return PE_OK;
 }
 
 double pe_planner_kernel_ms(const pe_planner* p) { return p ? p->last_ms : 0; }

@@ -114,6 +114,16 @@ __device__ __forceinline__ uint8_t fit_node(const PlanArgs& a, const PlanNodeRec
         if (ar.terminal || (pn.rm_cnt && removed(rm, pn.rm_cnt, q))) continue;
         take(ar, a.pool_keys, buf, fill, cmask, nd.core_mask, acc);
     }
+    for (uint32_t c = nd.ext_head; c != kNone;) {   // allocs committed since the last compaction
+        const Chunk ch = a.chunks[c];
+        for (uint32_t i = gl; i < ch.cnt; i += G) {
+            const uint32_t q = ch.off + i;
+            const AllocRec ar = a.pool[q];
+            if (ar.terminal || (pn.rm_cnt && removed(rm, pn.rm_cnt, q))) continue;
+            take(ar, a.pool_keys, buf, fill, cmask, nd.core_mask, acc);
+        }
+        c = ch.next;
+    }
     for (uint32_t i = gl; i < pn.place_cnt; i += G) {
         const AllocRec ar = a.pallocs[pn.place_off + i];
         if (ar.terminal) continue;
@@ -211,7 +221,25 @@ __global__ void __launch_bounds__(64) k_plan_eval_big(PlanArgs a) {
     if (lane == 0) a.reason[p] = r;
 }
 
+// pe_planner_commit patch: removed allocs stop counting (terminal byte) and
+// the touched nodes get their new records (chain heads, key bounds).
+__global__ void __launch_bounds__(256) k_plan_patch(NodeRec* nodes, AllocRec* pool, const uint32_t* dead, uint32_t n_dead,
+                                                    const uint32_t* rows, const NodeRec* recs, uint32_t n_rows) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_dead) pool[dead[i]].terminal = 1;
+    if (i < n_rows) nodes[rows[i]] = recs[i];
+}
+
 }  // namespace pa
+
+hipError_t pe_launch_plan_patch(pa::NodeRec* nodes, pa::AllocRec* pool, const uint32_t* dead, uint32_t n_dead,
+                                const uint32_t* rows, const pa::NodeRec* recs, uint32_t n_rows, hipStream_t st) {
+    const uint32_t n = n_dead > n_rows ? n_dead : n_rows;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pa::k_plan_patch, dim3((n + 255) / 256), dim3(256), 0, st, nodes, pool, dead, n_dead, rows, recs,
+                       n_rows);
+    return hipGetLastError();
+}
 
 template <int G>
 static void launch_group(const pa::PlanArgs* a, hipStream_t st) {

@@ -40,9 +40,16 @@ struct alignas(16) NodeRec {      // 64 B, one per snapshot node
     uint32_t alloc_off, alloc_cnt;// contiguous snapshot allocs of this node in the pool
     uint32_t alloc_keys;          // Σ keys of those allocs (sizes the scratch fallback)
     uint8_t ready, eligible, setnode_collide, has_cores;
-    uint32_t _pad[2];
+    uint32_t ext_head;            // first chunk of allocs appended by commits (kNone: none)
+    uint32_t _pad;
 };
 static_assert(sizeof(NodeRec) == 64, "NodeRec is 64 bytes");
+
+// Allocs appended to a node by pe_planner_commit since the last compaction:
+// pool[off, off + cnt), chained newest first.
+struct alignas(16) Chunk {
+    uint32_t off, cnt, next, _pad;
+};
 
 struct alignas(16) AllocRec {     // 32 B, snapshot pool entry or plan alloc
     int64_t cpu, mem, disk;
@@ -74,6 +81,7 @@ constexpr uint64_t kHole = ~0ull;                       // staged slot of a mask
 
 struct PlanArgs {
     const NodeRec* nodes;
+    const Chunk* chunks;
     const AllocRec* pool;            // snapshot allocs, grouped by node
     const uint64_t* node_keys;
     const uint64_t* pool_keys;

@@ -395,3 +395,31 @@ def test_planner_matches_golden():
     ep = pl.encode(plan)
     got = [[nid, f, w] for nid, (f, w) in zip(ep.node_ids, _codes_to_pairs(pl.evaluate(ep)))]
     assert got == sp["outcomes"]
+
+
+@pytest.mark.gpu
+def test_planner_incremental_commit_and_compaction():
+    # commits append chunks per node; once the append room is used up the pool
+    # is compacted. Every evaluation in between equals the oracle.
+    nodes, allocs, plan = system_plan(3000, seed=21)
+    pl = _planner()
+    pl.set_state(nodes, allocs)
+    snap = O.Snapshot(nodes, allocs)
+    for step in range(4):
+        res = pl.evaluate_plan_placements(plan)
+        ref = assemble_result(plan, *O.evaluate_plan_placements(snap, plan), snap.alloc_by_id)
+        assert res == ref, step
+        pl.apply(plan, res)
+        snap.apply(plan, ref)
+        # next plan: another system alloc per node (ports move on), and every
+        # third node stops one of its allocs
+        nxt = Plan()
+        for i, nd in enumerate(nodes):
+            mine = snap.by_node.get(nd.id, [])
+            a = PlanAlloc(id="%s-s%d" % (nd.id, step), node_id=nd.id, cpu_shares=250, memory_mb=128, disk_mb=150,
+                          shared_ports=[Port(21000 + 7 * step + i % 5, nd.addresses[0].address)])
+            nxt.node_allocation[nd.id] = [a]
+            if mine and i % 3 == 0:
+                nxt.node_update[nd.id] = [mine[0]]
+        plan = nxt
+    assert pl.lib.pe_planner_snapshot_allocs(pl.h) == len(pl.allocs)
