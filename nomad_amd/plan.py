@@ -332,6 +332,7 @@ class Planner:
         self.row_of: Dict[str, int] = {}
         self.allocs: List[PlanAlloc] = []
         self.alloc_index: Dict[str, int] = {}   # live alloc id -> snapshot index
+        self.interner = Interner()
 
     def close(self):
         if getattr(self, "h", None):

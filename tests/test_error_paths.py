@@ -1,0 +1,49 @@
+"""Error behaviour at the C ABI (include/nomad_pe.h conventions): negative
+PE_E* codes with a message, no partial results, and state that stays usable
+or is reported unusable (GPU: the handles need a device)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from nomad_amd import abi, synth
+from nomad_amd.plan import Plan, PlannerError
+from nomad_amd.structs import Allocation
+from nomad_amd.synth_plan import mock_alloc, mock_node
+
+
+@pytest.mark.gpu
+def test_planner_call_order_and_bad_rows():
+    from nomad_amd.plan import Planner
+    pl = Planner()
+    with pytest.raises(PlannerError, match="set_state"):
+        pl.evaluate(pl.encode(Plan(node_allocation={"x": [mock_alloc("a")]})))
+    pl.set_state([mock_node("n1")], [])
+    ep = pl.encode(Plan(node_allocation={"n1": [mock_alloc("a", "n1")]}))
+    ep.rows[0] = 7                      # a row outside the snapshot
+    with pytest.raises(PlannerError, match="out of range"):
+        pl.evaluate(ep)
+    ep.rows[0] = 0
+    assert list(pl.evaluate(ep)) == [abi.PE_PLAN_FIT]
+    # commit keeping a node that does not exist is refused before any change
+    ep2 = pl.encode(Plan(node_allocation={"ghost": [mock_alloc("b", "ghost")]}))
+    keep = np.ones(1, dtype=np.uint8)
+    rc = pl.lib.pe_planner_commit(pl.h, C.byref(ep2.strtab), C.byref(ep2.c), keep.ctypes.data_as(abi.u8p))
+    assert rc == abi.PE_EINVAL
+    assert pl.lib.pe_planner_snapshot_allocs(pl.h) == 0
+
+
+@pytest.mark.gpu
+def test_update_allocs_bad_index_requires_reload():
+    from nomad_amd.stack import EngineError, GenericStack
+    nodes, allocs = synth.cluster_c1(20, seed=3)
+    st = GenericStack()
+    st.SetState(nodes, allocs)
+    with pytest.raises(EngineError, match="index out of range"):
+        st.UpdateAllocs([Allocation(node_id=nodes[0].id, job_id="j", task_group="g", cpu_shares=100)], [5])
+    with pytest.raises(EngineError, match="pe_set_state"):
+        st.SetJob(synth.mock_job())     # partially applied delta: the snapshot must be reloaded
+    st.SetState(nodes, allocs)
+    st.SetJob(synth.mock_job())
+    st.SetNodes(nodes)
+    assert st.Select(0) is not None
