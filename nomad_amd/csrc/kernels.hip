@@ -1751,7 +1751,7 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t of
 // u32 per node (k_fold_aux) and resolve against LDS copies of the affinity
 // values and the spread boosts, so an option costs no dependent table load.
 template <int BLOCK, bool PF, int PROBE = 0, bool AUX = false>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AUX ? 4 : 5))) k_sweep(SweepArgs A) {
+__device__ __forceinline__ void sweep_block(const SweepArgs& A) {
     constexpr int W = BLOCK / 64;
     constexpr uint32_t kQueue = 128;
     __shared__ SweepRec red[W];
@@ -1866,6 +1866,11 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AUX 
     if (threadIdx.x == 0) A.recs[blockIdx.x] = r;
 }
 
+template <int BLOCK, bool PF, int PROBE = 0, bool AUX = false>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AUX ? 4 : 5))) k_sweep(SweepArgs A) {
+    sweep_block<BLOCK, PF, PROBE, AUX>(A);
+}
+
 // Bound probes for the sweep (PE_SWEEP_VARIANT 5 / 6): 5 streams exactly the
 // sweep's bytes with trivial arithmetic; 6 runs the scoring arithmetic on
 // register-synthesised inputs without touching memory.
@@ -1952,8 +1957,8 @@ __global__ void k_node_record(SweepArgs A, uint32_t row, pe_ranked_node* out) {
 // offers); then the workgroup rebuilds the spread table for the next
 // placement from the updated counts (k_spread_table). state[0]: a nil Select
 // ended the loop (later steps do nothing); state[1]: placements so far.
-__global__ void __launch_bounds__(256) k_sweep_step(SweepArgs A, uint32_t nrecs, const uint32_t* visit, uint32_t n,
-                                                    uint32_t offset, pe_ranked_node* out, uint32_t* state) {
+__device__ __forceinline__ void step_block(const SweepArgs& A, uint32_t nrecs, const uint32_t* visit, uint32_t n,
+                                           uint32_t offset, pe_ranked_node* out, uint32_t* state) {
     __shared__ uint32_t counts[kMaxPsets * kMaxValues];
     __shared__ uint32_t scratch[4];
     __shared__ SweepRec red[4];
@@ -2010,6 +2015,69 @@ __global__ void __launch_bounds__(256) k_sweep_step(SweepArgs A, uint32_t nrecs,
         for (int v = threadIdx.x; v < t.pset_nvals[p]; v += 256) counts[p * kMaxValues + v] = t.pset_counts[p][v];
     __syncthreads();
     build_spread_table<256>(t, counts, const_cast<double*>(A.spread_tab), scratch);
+}
+
+__global__ void __launch_bounds__(256) k_sweep_step(SweepArgs A, uint32_t nrecs, const uint32_t* visit, uint32_t n,
+                                                    uint32_t offset, pe_ranked_node* out, uint32_t* state) {
+    step_block(A, nrecs, visit, n, offset, out, state);
+}
+
+// Grid-wide barrier of the persistent count loop (every workgroup resident;
+// the host launches at most one per CU). Stores of the whole workgroup are
+// released at agent scope before the arrival and acquired after it, so rows
+// committed by workgroup 0 on one XCD are seen by the sweeps on the others
+// (MI355X_MICROARCH.md, inter-workgroup visibility). The wait is bounded: on
+// timeout the workgroup sets state[4] and every workgroup leaves the loop.
+__device__ __forceinline__ bool grid_sync(uint32_t* state, uint32_t nblocks, uint32_t* gen) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __shared__ uint32_t ok;
+    if (threadIdx.x == 0) {
+        ok = 1;
+        const uint32_t g = *gen;
+        const uint32_t arrived = __hip_atomic_fetch_add(&state[2], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        if (arrived == nblocks) {
+            __hip_atomic_store(&state[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&state[3], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            uint32_t spins = 0;
+            while (__hip_atomic_load(&state[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                if (++spins > (1u << 20) ||
+                    __hip_atomic_load(&state[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                    __hip_atomic_store(&state[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        *gen = g + 1;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return ok != 0;
+}
+
+// Persistent full-pass count loop: every placement is sweep_block on all
+// workgroups, a grid barrier, step_block on workgroup 0 (merge, record,
+// commit, next spread table), a grid barrier. state: [0] stopped, [1] placed,
+// [2] barrier arrivals, [3] barrier generation, [4] barrier timeout.
+template <bool AUX>
+__global__ void __launch_bounds__(256) k_sweep_loop(SweepArgs A, uint32_t count, const uint32_t* visit, uint32_t n,
+                                                    uint32_t offset, pe_ranked_node* out, uint32_t* state) {
+    __shared__ uint32_t gen;
+    __shared__ uint32_t stop;
+    if (threadIdx.x == 0) gen = __hip_atomic_load(&state[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    for (uint32_t k = 0; k < count; k++) {
+        sweep_block<256, false, 0, AUX>(A);
+        if (!grid_sync(state, gridDim.x, &gen)) return;
+        if (blockIdx.x == 0) step_block(A, gridDim.x, visit, n, offset, out, state);
+        if (!grid_sync(state, gridDim.x, &gen)) return;
+        if (threadIdx.x == 0) stop = __hip_atomic_load(&state[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (stop) return;
+    }
 }
 
 // node_feas[row] = class_ok[cls] && node_ok[row]: one verdict byte per node so
@@ -2248,5 +2316,17 @@ hipError_t pe_launch_sweep_step(const pe::SweepArgs* a, uint32_t blocks, const u
     if (a->node_aux) hipLaunchKernelGGL((pe::k_sweep<256, false, 0, true>), dim3(blocks), dim3(256), 0, st, *a);
     else hipLaunchKernelGGL((pe::k_sweep<256, false>), dim3(blocks), dim3(256), 0, st, *a);
     hipLaunchKernelGGL(pe::k_sweep_step, dim3(1), dim3(256), 0, st, *a, blocks, visit, n, offset, out, state);
+    return hipGetLastError();
+}
+
+// The persistent loop; `blocks` must all be resident (the host keeps it at
+// most one workgroup per CU). state[0..4] zeroed by the caller.
+hipError_t pe_launch_sweep_loop(const pe::SweepArgs* a, uint32_t blocks, uint32_t count, const uint32_t* visit,
+                                uint32_t n, uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st) {
+    if (a->node_aux)
+        hipLaunchKernelGGL(pe::k_sweep_loop<true>, dim3(blocks), dim3(256), 0, st, *a, count, visit, n, offset, out, state);
+    else
+        hipLaunchKernelGGL(pe::k_sweep_loop<false>, dim3(blocks), dim3(256), 0, st, *a, count, visit, n, offset, out,
+                           state);
     return hipGetLastError();
 }

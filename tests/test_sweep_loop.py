@@ -60,3 +60,18 @@ def test_sweep_count_loop_devices():
     _, _, want = run_place(OracleGenericStack, nodes, allocs, job, perm)
     assert_same_placements(got, want)
     assert [g.device_offers for g in got] == [w.device_offers for w in want]
+
+
+@pytest.mark.gpu
+def test_persistent_count_loop_matches_oracle():
+    # the opt-in persistent variant (one launch, grid barriers) gives the same placements
+    os.environ["PE_LOOP_PERSISTENT"] = "1"
+    try:
+        nodes, allocs = synth.cluster_c3(2500, seed=11)
+        job = synth.job_c3(100)
+        perm = synth.shuffle(2500, 12)
+        _, _, got = run_place(_engine_low_threshold, nodes, allocs, job, perm)
+    finally:
+        del os.environ["PE_LOOP_PERSISTENT"]
+    _, _, want = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    assert_same_placements(got, want)
