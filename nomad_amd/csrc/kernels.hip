@@ -1691,10 +1691,18 @@ __global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts, u
             score[j] = ev.status == kOption ? ev.score : 0.0;
         }
     }
+    // one atomic per workgroup and counter (not per wave): fewer same-address
+    // atomics queueing at one L2 channel
+    __shared__ uint32_t red[3][4];
     for (int k = 0; k < 3; k++) {
         uint32_t x = c[k];
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&counts[k], x);
+        if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const uint32_t x = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+        if (x) atomicAdd(&counts[threadIdx.x], x);
     }
 }
 
