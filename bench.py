@@ -4,20 +4,24 @@ Workload (BASELINE.json configs[1]): 10,000 heterogeneous
 synthetic nodes (seed 42) with 0-3 foreign allocs each, a count=1000 binpack
 service job (cpu 500 / mem 256 / disk 150), limit = ceil(log2 n) = 14.
 
-A step = one batch of E concurrent evaluations of that job (the NumSchedulers
-worker model, nomad/config.go:468: each worker evaluates against its own
-snapshot with its own shuffle), each placing all 1000 allocations with the exact
-reference semantics (fused count loop, one workgroup per eval, pe_place_batch).
-The snapshot and the E visit orders are resident in HBM before timing; result
-records come back to the host inside the timed region.
-value = E * placements / step time. The single-eval latency path (pe_place) is
-reported beside it.
+A step = one evaluation driven exactly as the unchanged Go caller drives a
+Stack (GenericScheduler.computePlacements, generic_sched.go:472-652): ResetPlan
+(fresh EvalContext), SetJob, SetNodes(a shuffled node list), then 1000 x
+(pe_select with empty options, pe_commit of the option). The loop runs in C
+(tools/libdropin.so, the cgo caller's shape) against the C ABI; the engine
+answers from its speculative device count loop. The snapshot is
+resident in HBM before timing. value = placements / timed seconds. The CPU
+baseline is the oracle (C++ restatement of the reference chain) driven by the
+same C loop on one host core.
 
 Multi-GPU: the windowed binpack path does not shard; each rank
-runs its own batches on its own GPU (replicas, weak scaling).
+runs its own evaluations on its own GPU (replicas, weak scaling).
 
 Beside the headline line's C2 numbers, the JSON carries one object per other
 BASELINE.json config (sections, --sections to choose):
+  c2_batch    4096 concurrent evaluations per launch sharing one k_base pass
+  c2_workers  NumSchedulers-style worker threads, one engine handle each, each
+              running the caller loop on its own evaluations
   c3          spread + affinity + semver/regexp job, count=1000 on 10k nodes in 3
               DCs: one evaluation's full-pass count loop on one GPU
   c4          system job on a 100k-node cluster sharded over the ranks (contiguous
@@ -57,16 +61,17 @@ BYTES_PER_NODE_EVAL = 60
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--nodes", type=int, default=10000)
     p.add_argument("--count", type=int, default=1000)
-    p.add_argument("--evals", type=int, default=4096, help="concurrent evaluations per step")
+    p.add_argument("--evals", type=int, default=4096, help="concurrent evaluations per launch (c2_batch)")
+    p.add_argument("--workers", type=int, default=8, help="worker threads of the c2_workers section")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--sweep-nodes", type=int, default=1 << 24,
                    help="nodes of the scoring-sweep roofline measurement (0 = skip)")
-    p.add_argument("--sections", default="c3,c4,c5,c3_sharded,plan_apply,ingest",
+    p.add_argument("--sections", default="c2_batch,c2_workers,c3,c4,c5,c3_sharded,plan_apply,ingest",
                    help="comma list of extra config sections (empty = none)")
     return p.parse_args()
 
@@ -551,6 +556,73 @@ def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
     return out
 
 
+def section_c2_batch(device, nodes, allocs, job, count, evals, steps=10, warmup=2):
+    """Secondary C2 figure: E concurrent evaluations per launch (NumSchedulers
+    workers, nomad/config.go:468), each its own shuffled order, all sharing one
+    k_base pass of the snapshot (pe_place_batch)."""
+    from nomad_amd import synth
+    from nomad_amd.stack import GenericStack
+    orders = np.stack([synth.shuffle(len(nodes), 1000 + e) if e < 64 else
+                       np.random.Generator(np.random.PCG64(1000 + e)).permutation(len(nodes)).astype(np.uint32)
+                       for e in range(evals)])
+    st = GenericStack(device=device)
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.StageOrders(orders)
+    for _ in range(warmup):
+        st.PlaceBatch(0, count, copy=False)
+    t0 = time.perf_counter()
+    placed, kernel_ms = 0, 0.0
+    for _ in range(steps):
+        placed += int(st.PlaceBatch(0, count, copy=False)[3].sum())
+        kernel_ms += st.last_kernel_ms()
+    elapsed = time.perf_counter() - t0
+    evaluated = float(st.PlaceBatch(0, count, copy=False)[2].sum(dtype=np.uint64))
+    st.close()
+    avg_kernel_s = kernel_ms / 1000.0 / steps
+    achieved = evaluated * BYTES_PER_NODE_EVAL / avg_kernel_s / 1e9
+    return {"workload": "C2: %d concurrent evals per launch x count=%d on %d nodes (one k_base pass shared)"
+                        % (evals, count, len(nodes)),
+            "placements_per_s": placed / elapsed, "ms_per_launch": elapsed / steps * 1e3,
+            "roofline": {"bound": "cache", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": chain_traffic(evaluated),
+                         "note": "cache-resident equivalent bytes: 60 B per node-evaluation the reference chain "
+                                 "would read; the 10k-node table sits in L2/MALL, PMC HBM traffic is far lower",
+                         "kernel": "k_base + k_chain", "kernel_ms": avg_kernel_s * 1e3,
+                         "node_evals_per_launch": evaluated}}
+
+
+def section_c2_workers(device, nodes, allocs, job, count, workers, seconds=3.0):
+    """NumSchedulers workers (nomad/config.go:468) on one GPU: each thread owns
+    an engine handle (its own HIP stream) and runs the caller loop of
+    tools/libdropin.so on its own evaluations, like the Go workers would."""
+    from nomad_amd import synth
+    from nomad_amd.stack import GenericStack
+    from tools import dropin
+    orders = np.stack([synth.shuffle(len(nodes), 7000 + e) for e in range(16)])
+    stacks = []
+    for _ in range(workers):
+        st = GenericStack(device=device)
+        st.SetState(nodes, allocs)
+        stacks.append(st)
+    for st in stacks:
+        dropin.run(st, job, orders[:1], count, n_evals=1)
+
+    def work(i):
+        return dropin.run(stacks[i], job, np.roll(orders, i, axis=0), count, n_evals=1 << 30,
+                          max_seconds=seconds)
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(workers) as ex:
+        res = list(ex.map(work, range(workers)))
+    wall = time.perf_counter() - t0
+    for st in stacks:
+        st.close()
+    placed = sum(r[0] for r in res)
+    return {"workload": "C2: %d worker threads x sequential evals (count=%d, %d nodes), one engine handle "
+                        "each, caller loop in C" % (workers, count, len(nodes)),
+            "workers": workers, "placements_per_s": placed / wall, "evals": sum(r[1] for r in res)}
+
+
 def main():
     args = parse()
     # Native libraries (gloo, RCCL) print banners on stdout; the contract is one
@@ -560,65 +632,53 @@ def main():
     rank, world, local, pg = dist_init()
     from nomad_amd import synth
     from nomad_amd.stack import GenericStack
+    from tools import dropin
+    try:
+        import torch
+        sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    except ImportError:
+        sync = lambda: None   # noqa: E731
 
     nodes, allocs = synth.cluster_c2(args.nodes, seed=42)
     job = synth.job_c2(args.count)
-    E = args.evals
+    # one shuffled SetNodes list per evaluation (shuffleNodes, util.go:366-372)
     rng_base = 1000 + 104729 * rank
-    orders = np.stack([synth.shuffle(len(nodes), rng_base + e) if e < 64 else
-                       np.random.Generator(np.random.PCG64(rng_base + e)).permutation(len(nodes)).astype(np.uint32)
-                       for e in range(E)])
+    orders = np.stack([synth.shuffle(len(nodes), rng_base + e) for e in range(32)])
 
+    # Headline: the unchanged caller's protocol through the C ABI. A step is
+    # one evaluation: ResetPlan, SetJob, SetNodes(shuffled list), then count x
+    # (Select, Commit) exactly as computePlacements drives a Stack
+    # (generic_sched.go:485-627), the loop in C (tools/libdropin.so, the cgo
+    # caller's shape). The engine answers from its speculative device loop.
     st = GenericStack(device=local)
     st.SetState(nodes, allocs)
-    st.SetJob(job)
-    st.StageOrders(orders)
-
-    def step():
-        # results land in the engine's page-locked buffer (zero-copy views)
-        rows, scores, evaluated, placed = st.PlaceBatch(0, args.count, copy=False)
-        return int(placed.sum()), st.last_kernel_ms(), st.last_phase_ms()
-
-    for _ in range(args.warmup):
-        step()
+    dropin.run(st, job, orders, args.count, n_evals=max(1, args.warmup))
+    spec0 = st.SpeculationStats()
     barrier(pg)
+    sync()
     t0 = time.perf_counter()
-    placed = 0
-    kernel_ms = 0.0
-    phases = np.zeros(4)
-    for _ in range(args.steps):
-        p, k, ph = step()
-        placed += p
-        kernel_ms += k
-        phases += ph
+    placed, evals, selects, c_secs, rows = dropin.run(st, job, np.roll(orders, -args.warmup, axis=0), args.count,
+                                                      n_evals=args.steps)
+    sync()
     elapsed = time.perf_counter() - t0
-    # every step evaluates the same staged orders: node evaluations per launch
-    # from the last step's records (outside the timed region)
-    evaluated = int(st.PlaceBatch(0, args.count, copy=False)[2].sum(dtype=np.uint64)) * args.steps
     barrier(pg)
+    spec1 = st.SpeculationStats()
     elapsed = reduce(pg, elapsed, lambda d: d.ReduceOp.MAX)
     total_placed = reduce(pg, placed, lambda d: d.ReduceOp.SUM)
 
-    # single-evaluation latency (pe_place on the stack's own plan)
-    lat = GenericStack(device=local)
-    lat.SetState(nodes, allocs)
-    lat_times = []
-    for i in range(5):
-        lat.ResetPlan()
-        lat.SetJob(job)
-        lat.SetNodes(orders[i % E])
-        t1 = time.perf_counter()
-        lat.PlaceArrays(0, args.count)
-        lat_times.append(time.perf_counter() - t1)
-    single = args.count / float(np.median(lat_times[1:]))
-    single_kernel_ms = lat.last_kernel_ms()
+    # the dominant kernel of a step: the speculative count loop (k_base + k_chain),
+    # timed with HIP events on the engine's stream by the same call path
+    st.ResetPlan()
+    st.SetJob(job)
+    st.SetNodes(orders[0])
+    _, _, p1, recs = st.PlaceArrays(0, args.count)
+    loop_kernel_ms = st.last_kernel_ms()
+    node_evals = float(recs["nodes_evaluated"][:p1].sum(dtype=np.uint64))
+    st.close()
 
     if rank == 0:
         value = total_placed / elapsed
-        avg_kernel_s = kernel_ms / 1000.0 / args.steps
-        evals_per_launch = evaluated / args.steps
-        algo_bytes = evals_per_launch * BYTES_PER_NODE_EVAL
-        achieved = algo_bytes / avg_kernel_s / 1e9
+        achieved = node_evals * BYTES_PER_NODE_EVAL / (loop_kernel_ms / 1000.0) / 1e9
         line = {
             "metric": "placements/sec (count=1000 service job, 10k nodes, binpack)",
             "value": value,
@@ -632,28 +692,40 @@ def main():
             "vs_baseline": None,
             "dtype": "int64+f64",
             "data": "synthetic (seeded 10k-node cluster, SURVEY.md §8d C2)",
-            "config": {"workload": "C2: %d concurrent evals/step x service job count=%d, %d heterogeneous "
-                                   "nodes, binpack, limit 14" % (E, args.count, args.nodes),
-                       "evals_per_step": E,
+            "config": {"workload": "C2 drop-in: per step one evaluation of a count=%d binpack service job on %d "
+                                   "heterogeneous nodes (limit 14): ResetPlan + SetJob + SetNodes + %d x "
+                                   "(pe_select, pe_commit) from a C caller loop" % (args.count, args.nodes,
+                                                                                   args.count),
+                       "evals_per_step": 1,
                        "parallelism": "replicas x%d (windowed binpack does not shard)" % world},
-            "step_phases_ms": dict(zip(("host_prep", "kernel", "d2h_results", "call_total"),
-                                       (phases / args.steps).round(4).tolist())),
-            "single_eval": {"placements_per_s": single, "kernel_ms": single_kernel_ms,
-                            "note": "one eval, pe_place fused count loop, host call included"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": chain_traffic(evals_per_launch),
-                         "traffic_note": "FETCH_SIZE x 2 + WRITE_SIZE per k_chain launch (the 10k-node table "
-                                         "is L2/MALL resident, so HBM traffic sits far below the algorithmic "
-                                         "bytes the lanes read)",
-                         "kernel": "k_base + k_chain", "kernel_ms": avg_kernel_s * 1000.0,
-                         "node_evals_per_launch": evals_per_launch,
-                         "bytes_per_node_eval": BYTES_PER_NODE_EVAL},
+            "drop_in": {"placements": placed, "evaluations": evals, "selects": selects,
+                        "c_loop_seconds": c_secs,
+                        "speculation": dict(zip(("runs", "served", "rollbacks", "records"),
+                                                (b - a for a, b in zip(spec0, spec1)))),
+                        "us_per_placement": elapsed / max(1, placed) * 1e6},
+            "roofline": {"bound": "cache", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "note": "k_base + k_chain of one evaluation (the step's device work): cache-resident "
+                                 "equivalent bytes, 60 B per node-evaluation the reference chain reads; the "
+                                 "10k-node table is L2/MALL resident and the loop is latency-bound. The HBM "
+                                 "roofline of SURVEY.md §8(d) is sweep_roofline",
+                         "kernel": "k_base + k_chain", "kernel_ms": loop_kernel_ms,
+                         "node_evals_per_launch": node_evals, "bytes_per_node_eval": BYTES_PER_NODE_EVAL},
         }
         if args.sweep_nodes > 0:
             line["sweep_roofline"] = sweep_roofline(args.sweep_nodes, local)
         if not args.no_cpu:
-            one, multi = cpu_baseline(nodes, allocs, job, args.cpu_seconds)
-            line["cpu_baseline"] = one
+            from oracle.oracle import OracleGenericStack
+            o = OracleGenericStack()
+            o.SetState(nodes, allocs)
+            op, oe, _, osecs, _ = dropin.run(o, job, orders, args.count, n_evals=1 << 30,
+                                             max_seconds=args.cpu_seconds)
+            line["cpu_baseline"] = {"value": op / osecs, "unit": "placements/s", "cores": 1, "kind": "port",
+                                    "sample": "%d evaluations x count=%d on the %d-node cluster in %.1f s through the "
+                                              "same C caller loop, 1 thread (oracle/liboracle.so: C++ restatement "
+                                              "of the reference iterator chain; Go toolchain unavailable)"
+                                              % (oe, args.count, len(nodes), osecs)}
+            _, multi = cpu_baseline(nodes, allocs, job, args.cpu_seconds)
             line["cpu_baseline_multicore"] = multi
     sections = [x for x in args.sections.split(",") if x]
     cpu_s = 0.0 if args.no_cpu else 8.0
@@ -663,6 +735,12 @@ def main():
             if sec in ("c3", "c5"):
                 if rank == 0:
                     extra[sec] = section_c3(local, cpu_s) if sec == "c3" else section_c5(local, cpu_s)
+            elif sec == "c2_batch":
+                if rank == 0:
+                    extra[sec] = section_c2_batch(local, nodes, allocs, job, args.count, args.evals)
+            elif sec == "c2_workers":
+                if rank == 0:
+                    extra[sec] = section_c2_workers(local, nodes, allocs, job, args.count, args.workers)
             elif sec == "c4":
                 extra[sec] = section_c4(local, rank, world, pg, cpu_s)
             elif sec == "c3_sharded":
@@ -679,8 +757,6 @@ def main():
         line["configs"] = extra
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
-    st.close()
-    lat.close()
     if pg is not None:
         pg.destroy_process_group()
 

@@ -275,8 +275,20 @@ int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_
 int pe_select(pe_stack* s, uint32_t tg_index, const pe_select_options* opts,
               pe_ranked_node* out);
 /* Plan.AppendAlloc (structs.go:10707-10714) of an allocation of task group
- * `tg_index` on node `row`: the proposed state seen by later Selects. */
+ * `tg_index` on node `row`: the proposed state seen by later Selects.
+ *
+ * Speculation (transparent to the caller): the first plain Select of a task
+ * group (no preferred / penalty nodes, no Preempt, metrics off) runs the
+ * device count loop for the group's remaining placements and returns its first
+ * record; while every pe_commit names the row the previous Select returned,
+ * later plain Selects of that group are answered from the loop's records with
+ * no device work. Any other call first restores the device state to the
+ * committed prefix, so results always equal one-at-a-time Selects.
+ * PE_SPECULATE=0 in the environment disables it. */
 int pe_commit(pe_stack* s, uint32_t tg_index, int32_t row);
+/* Counters of the speculative loop: out[0] runs started, [1] Selects answered
+ * from records, [2] rollbacks (the caller deviated), [3] records computed. */
+int pe_speculation_stats(const pe_stack* s, uint64_t* out4);
 /* Plan.AppendAlloc plus Plan.AppendPreemptedAlloc of each preempted alloc
  * (handlePreemptions, generic_sched.go:794-816): `preempted` are alloc-table
  * rows, as returned in pe_ranked_node.preempted by a Select with Preempt. */

@@ -193,7 +193,7 @@ ENGINE_SYMBOLS = [
     "pe_reset_plan", "pe_set_job", "pe_set_nodes", "pe_select", "pe_commit", "pe_commit_preempt", "pe_place", "pe_system_place",
     "pe_last_kernel_ms", "pe_stage_orders", "pe_place_batch", "pe_batch_results", "pe_last_phase_ms",
     "pe_check_constraint", "pe_last_sweep_bytes", "pe_select_shard", "pe_select_merge",
-    "pe_set_metrics", "pe_last_metrics", "pe_update_allocs",
+    "pe_set_metrics", "pe_last_metrics", "pe_update_allocs", "pe_speculation_stats",
 ]
 
 

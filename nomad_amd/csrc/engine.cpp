@@ -39,6 +39,8 @@ hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
                             uint32_t offers, hipStream_t st);
 hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs* r, hipStream_t st);
+hipError_t pe_launch_apply_commits(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
+                                   const uint32_t* offers, uint32_t n, hipStream_t st);
 hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ranked_node* out, uint32_t* mask,
                                   hipStream_t st);
 hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
@@ -383,6 +385,25 @@ struct pe_stack {
     std::string metrics_text;
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
+
+    // Speculative count loop behind pe_select / pe_commit: the
+    // first plain Select of a task group runs the device count loop for the
+    // group's remaining placements, committing into HBM after a checkpoint of
+    // the dynamic columns; later Selects are served from the records while each
+    // pe_commit matches the predicted row. Any other call first flushes: the
+    // device state is rolled back to the checkpoint plus the confirmed commits.
+    struct Spec {
+        bool active = false;
+        bool pending = false;          // a served option awaits its pe_commit
+        uint32_t tgi = 0;
+        std::vector<pe_ranked_node> recs;
+        uint32_t n_rec = 0, placed = 0, served = 0, confirmed = 0;
+        uint32_t grow = 1;             // minimum run length, grows while runs get used up
+    } spec;
+    bool spec_on = true;               // PE_SPECULATE=0: every Select runs on its own
+    uint64_t spec_stats[4] = {0, 0, 0, 0};   // runs, Selects served, rollbacks, records computed
+    DevMem ck_rec, ck_coll_job, ck_coll_tg, ck_dev_free, ck_pset[pe::kMaxPsets];
+    DevMem d_commit_rows, d_commit_offers;
 
     // visit order
     std::vector<uint32_t> visit;
@@ -979,6 +1000,19 @@ int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index) 
 int build_alloc_state(pe_stack* s) {
     const uint32_t n = (uint32_t)s->nodes.size();
     s->h_base_rec = s->h_node_rec;
+    {
+        // compact the device-entry pool to the live allocs' ranges: entries
+        // overwritten by pe_update_allocs leave dead ranges behind
+        std::vector<std::pair<uint32_t, uint32_t>> live;
+        live.reserve(s->alloc_dev.size());
+        for (HostAlloc& a : s->allocs) {
+            const uint32_t b = (uint32_t)live.size();
+            for (uint32_t k = a.dev_begin; k < a.dev_end; k++) live.push_back(s->alloc_dev[k]);
+            a.dev_begin = b;
+            a.dev_end = (uint32_t)live.size();
+        }
+        s->alloc_dev.swap(live);
+    }
     std::vector<int64_t> dev_used(s->dev_groups.size(), 0);
     for (const HostAlloc& a : s->allocs) {
         if (a.terminal) continue;
@@ -1960,6 +1994,12 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
 
 extern "C" {
 
+static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out);
+static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* opts);
+static int spec_flush(pe_stack* s);
+static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out);
+static void spec_drop(pe_stack* s);
+
 uint32_t pe_abi_version(void) { return PE_ABI_VERSION; }
 
 pe_stack* pe_stack_create(const pe_config* cfg) {
@@ -1991,6 +2031,7 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     if (const char* e = std::getenv("PE_LOOP_SWEEP_MIN")) s->loop_sweep_min = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("PE_RESULTS_VIA_COPY")) s->results_via_copy = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_WINDOW_LAZY")) s->use_base = std::atoi(e) == 0;
+    if (const char* e = std::getenv("PE_SPECULATE")) s->spec_on = std::atoi(e) != 0;
     return s;
 }
 
@@ -2022,6 +2063,7 @@ int pe_check_constraint(const char* op, const char* l, int ls, const char* r, in
 
 int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
     if (!s || !strs || !nodes) return PE_EINVAL;
+    spec_drop(s);
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     s->strs.clear();
@@ -2049,6 +2091,7 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
 int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index) {
     if (!s || !allocs) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    spec_drop(s);
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     s->add_strings(strs);
@@ -2083,6 +2126,7 @@ int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* a
 int pe_reset_plan(pe_stack* s) {
     if (!s) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    spec_drop(s);
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     const size_t n = s->nodes.size();
@@ -2117,6 +2161,10 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     s->add_strings(strs);
     const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
     if (generic && s->have_job_version && s->job_version == j->version) return PE_OK;   // stack.go:94-96
+    {
+        const int frc = spec_flush(s);   // a different job: the plan so far goes to HBM first
+        if (frc) return frc;
+    }
     s->have_job_version = true;
     s->job_version = j->version;
     s->job_id = j->id;
@@ -2248,10 +2296,17 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
 int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
     if (!s) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    if (!rows && n) return s->fail(PE_EINVAL, "null rows");
+    // validate before touching any state: a rejected list leaves the previous one in place
+    for (uint32_t i = 0; i < n; i++)
+        if (rows[i] >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range");
+    {
+        const int frc = spec_flush(s);
+        if (frc) return frc;
+    }
     s->gen++;
     s->visit.assign(rows, rows + n);
     s->d_visit_is_visit = false;
-    for (uint32_t r : s->visit) if (r >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range");
     s->offset = 0;
     uint32_t lim = 2;
     if (s->cfg.stack_kind == PE_STACK_GENERIC && !s->cfg.batch && n > 0) {
@@ -2516,8 +2571,14 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
 }
 
 int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
-    const int rc = select_impl(s, tgi, opts, out);
-    if (rc == PE_OK && s && out) {
+    if (!s || !out) return PE_EINVAL;
+    int rc = PE_OK;
+    if (!spec_serve(s, tgi, opts, out)) {
+        rc = spec_flush(s);
+        if (rc) return rc;
+        rc = spec_eligible(s, tgi, opts) ? spec_start(s, tgi, out) : select_impl(s, tgi, opts, out);
+    }
+    if (rc == PE_OK) {
         s->offer_row = out->row;
         s->offers = pack_offers(out);
     }
@@ -2599,7 +2660,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     return rc;
 }
 
-int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
+static int commit_impl(pe_stack* s, uint32_t tgi, int32_t row) {
     if (!s) return PE_EINVAL;
     if (!s->have_job || tgi >= s->tgs.size() || row < 0 || (size_t)row >= s->nodes.size())
         return s->fail(PE_EINVAL, "bad commit");
@@ -2647,6 +2708,10 @@ static int shard_prepare(pe_stack* s, uint32_t tgi, TgPlan** gp) {
 
 int pe_select_shard(pe_stack* s, uint32_t tgi, uint32_t row_begin, uint32_t row_end, pe_shard_rec* out) {
     if (!s || !out) return PE_EINVAL;
+    {
+        const int frc = spec_flush(s);
+        if (frc) return frc;
+    }
     if (row_begin > row_end || row_end > s->nodes.size()) return s->fail(PE_EINVAL, "bad shard row range");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
@@ -2664,6 +2729,10 @@ int pe_select_shard(pe_stack* s, uint32_t tgi, uint32_t row_begin, uint32_t row_
 
 int pe_select_merge(pe_stack* s, uint32_t tgi, const pe_shard_rec* recs, uint32_t n_recs, pe_ranked_node* out) {
     if (!s || !out || (!recs && n_recs)) return PE_EINVAL;
+    {
+        const int frc = spec_flush(s);
+        if (frc) return frc;
+    }
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     TgPlan* g = nullptr;
@@ -2687,9 +2756,10 @@ int pe_select_merge(pe_stack* s, uint32_t tgi, const pe_shard_rec* recs, uint32_
     return PE_OK;
 }
 
-int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
+static int commit_preempt_impl(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted,
+                               uint32_t n_preempted) {
     if (!s) return PE_EINVAL;
-    if (n_preempted == 0) return pe_commit(s, tgi, row);
+    if (n_preempted == 0) return commit_impl(s, tgi, row);
     if (!preempted || !s->have_job || tgi >= s->tgs.size() || row < 0 || (size_t)row >= s->nodes.size())
         return s->fail(PE_EINVAL, "bad commit");
     if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
@@ -2708,7 +2778,7 @@ int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* pr
     HIP_TRY(s, pe_launch_commit_preempt(&P, (uint32_t)row, mask, s->d_preempted.as<uint8_t>(),
                                         s->d_pcount.as<uint32_t>(), s->d_dev_free.as<uint32_t>(), s->stream));
     for (uint32_t i = 0; i < n_preempted; i++) s->h_preempted[s->alloc_slot[preempted[i]]] = 1;
-    return pe_commit(s, tgi, row);
+    return commit_impl(s, tgi, row);
 }
 
 static double now_us() {
@@ -2782,7 +2852,13 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     return PE_OK;
 }
 
-int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+// The count loop of computePlacements on the device (pe_place). With
+// `retry_preempt` a nil Select is retried with Preempt=true (selectNextOption,
+// generic_sched.go:773-792) when the configuration enables preemption; without
+// it the loop stops at the first nil Select (the speculative loop behind
+// pe_select leaves the retry to the caller).
+static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed,
+                      bool retry_preempt) {
     const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
     const double t_enter = prof ? now_us() : 0.0;
     if (!s || (!out && count)) return PE_EINVAL;
@@ -2793,6 +2869,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;
+    const bool retry = retry_preempt && s->cfg.preempt;
     uint32_t p = 0, no = s->offset;
     // Sparse options (a saturated cluster): a windowed Select would walk
     // ~limit * n / options positions with one wave. Then every Select
@@ -2815,12 +2892,12 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
             if (out[p].row >= 0) {
                 s->offer_row = out[p].row;
                 s->offers = pack_offers(&out[p]);
-                rc = pe_commit(s, tgi, out[p].row);
+                rc = commit_impl(s, tgi, out[p].row);
                 if (rc) return rc;
                 p++;
                 continue;
             }
-            if (!s->cfg.preempt) break;
+            if (!retry) break;
             pe_select_options o;   // selectNextOption: retry with Preempt=true
             std::memset(&o, 0, sizeof(o));
             o.preempt = 1;
@@ -2830,7 +2907,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
             if (out[p].row < 0) break;
             s->offer_row = out[p].row;
             s->offers = pack_offers(&out[p]);
-            rc = pe_commit_preempt(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
+            rc = commit_preempt_impl(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
             if (rc) return rc;
             p++;
         }
@@ -2839,7 +2916,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     }
     bool same_name = false;   // pe_commit would rebuild other task groups' collision counts
     for (size_t k = 0; k < s->tgs.size(); k++) same_name = same_name || (k != tgi && s->tgs[k]->name == g.name);
-    if (count && !parallel && !s->cfg.preempt && s->limit >= nv && nv >= s->loop_sweep_min && s->visit_unique &&
+    if (count && !parallel && !retry && s->limit >= nv && nv >= s->loop_sweep_min && s->visit_unique &&
         g.n_spread == (int)g.psets.size() && !same_name) {
         // A whole pass per placement over a long list: k_place would sweep it
         // with one workgroup. Here every placement is a multi-CU sweep +
@@ -2857,7 +2934,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
         s->offset = no;
         // selectNextOption (generic_sched.go:773-792): a nil Select is retried
         // with Preempt=true; the placement then evicts (handlePreemptions)
-        while (s->cfg.preempt && p < count) {
+        while (retry && p < count) {
             pe_select_options o;
             std::memset(&o, 0, sizeof(o));
             o.preempt = 1;
@@ -2867,7 +2944,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
             if (out[p].row < 0) break;
             s->offer_row = out[p].row;
             s->offers = pack_offers(&out[p]);
-            rc = pe_commit_preempt(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
+            rc = commit_preempt_impl(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
             if (rc) return rc;
             p++;
             if (p == count) break;
@@ -2889,7 +2966,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
                 if (out[p].row < 0) break;
                 s->offer_row = out[p].row;
                 s->offers = pack_offers(&out[p]);
-                rc = pe_commit(s, tgi, out[p].row);
+                rc = commit_impl(s, tgi, out[p].row);
                 if (rc) return rc;
                 p++;
             }
@@ -2908,8 +2985,197 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     return PE_OK;
 }
 
+// ---- speculative count loop behind pe_select / pe_commit --------------------
+//
+// GenericScheduler.computePlacements drives the stack one placement at a time:
+// Select, build the alloc, Plan.AppendAlloc (generic_sched.go:552-627); the
+// shim mirrors the append with pe_commit. Every fresh placement of a task
+// group has the same empty SelectOptions, so the results of the next k
+// Select/commit pairs are a pure function of the current state: exactly the
+// device count loop (place_impl). The first plain Select therefore runs that
+// loop for the group's remaining count and serves the first record; each
+// later plain Select is served from the records as long as every commit named
+// the predicted row. The loop commits into HBM after a checkpoint of the
+// dynamic columns; when the caller deviates (another row, options, another
+// task group, SetJob, SetNodes, ...) the columns are restored and the
+// confirmed prefix is replayed (k_apply_commits), so the device state is
+// always what the sequential calls would have produced.
+
+static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
+    pe_stack::Spec& sp = s->spec;
+    if (!sp.active || sp.pending || tgi != sp.tgi || sp.served >= sp.n_rec || s->metrics_on) return false;
+    if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
+    s->gen++;
+    *out = sp.recs[sp.served++];
+    sp.pending = out->row >= 0;
+    s->offset = out->new_offset;   // the StaticIterator cursor after this Select
+    s->metrics_valid = false;
+    s->spec_stats[1]++;
+    return true;
+}
+
+static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* opts) {
+    if (!s->spec_on || s->cfg.stack_kind != PE_STACK_GENERIC || s->metrics_on) return false;
+    if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
+    if (!s->have_state || !s->have_job || tgi >= s->tgs.size()) return false;
+    for (size_t k = 0; k < s->tgs.size(); k++)   // commits would rebuild a sibling's collision counts
+        if (k != tgi && s->tgs[k]->name == s->tgs[tgi]->name) return false;
+    return true;
+}
+
+// Copies between the live dynamic columns and the checkpoint (to_ckpt: save).
+static int spec_copy(pe_stack* s, TgPlan& g, bool to_ckpt) {
+    const size_t n = s->nodes.size();
+    auto cp = [&](DevMem& live, DevMem& ck, size_t bytes) -> hipError_t {
+        if (!bytes || !live.p) return hipSuccess;
+        if (to_ckpt) {
+            hipError_t e = ck.ensure(bytes);
+            if (e != hipSuccess) return e;
+            return hipMemcpyAsync(ck.p, live.p, bytes, hipMemcpyDeviceToDevice, s->stream);
+        }
+        return hipMemcpyAsync(live.p, ck.p, bytes, hipMemcpyDeviceToDevice, s->stream);
+    };
+    HIP_TRY(s, cp(s->d_rec, s->ck_rec, n * sizeof(pe::NodeRec)));
+    HIP_TRY(s, cp(s->d_coll_job, s->ck_coll_job, n * sizeof(uint32_t)));
+    HIP_TRY(s, cp(g.coll_tg, s->ck_coll_tg, n * sizeof(uint32_t)));
+    HIP_TRY(s, cp(s->d_dev_free, s->ck_dev_free, n * sizeof(uint32_t)));
+    for (size_t p = 0; p < g.psets.size() && p < (size_t)pe::kMaxPsets; p++)
+        HIP_TRY(s, cp(g.psets[p]->counts, s->ck_pset[p], std::max<size_t>(g.psets[p]->value_str.size(), 1) * 4));
+    return PE_OK;
+}
+
+static int spec_flush(pe_stack* s) {
+    pe_stack::Spec& sp = s->spec;
+    if (!sp.active) return PE_OK;
+    sp.active = false;
+    sp.pending = false;
+    if (sp.served == sp.n_rec && sp.confirmed == sp.placed && sp.placed == sp.n_rec)
+        sp.grow = std::min<uint32_t>(std::max<uint32_t>(16, 2 * sp.grow), 4096);   // used up: run longer next time
+    if (sp.confirmed == sp.placed) return PE_OK;   // HBM holds exactly the confirmed placements
+    HIP_TRY(s, hipSetDevice(s->device));
+    TgPlan& g = *s->tgs[sp.tgi];
+    int rc = spec_copy(s, g, false);
+    if (rc) return rc;
+    s->spec_stats[2]++;
+    if (sp.confirmed == 0) return PE_OK;
+    pe::Ask a = ask_for(s, g);
+    std::vector<uint32_t> rows(sp.confirmed), offers(sp.confirmed);
+    bool ordered_only = false;   // a device ask without a recorded offer: replay one by one
+    for (uint32_t i = 0; i < sp.confirmed; i++) {
+        rows[i] = (uint32_t)sp.recs[i].row;
+        offers[i] = pack_offers(&sp.recs[i]);
+        if (a.n_dev > 0 && offers[i] == 0xFFFFFFFFu) ordered_only = true;
+    }
+    if (ordered_only) {
+        pe::NodeSoA soa = soa_of(s);
+        pe::TgTables t = tables_of(g);
+        for (uint32_t i = 0; i < sp.confirmed; i++)
+            HIP_TRY(s, pe_launch_commit(&soa, &t, &a, rows[i], offers[i], s->stream));
+    } else {
+        HIP_TRY(s, upload(s->d_commit_rows, rows));
+        HIP_TRY(s, upload(s->d_commit_offers, offers));
+        pe::NodeSoA soa = soa_of(s);
+        pe::TgTables t = tables_of(g);
+        HIP_TRY(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
+                                           s->d_commit_offers.as<uint32_t>(), sp.confirmed, s->stream));
+    }
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    return PE_OK;
+}
+
+// Drop the speculation without touching the device (the state is being reset).
+static void spec_drop(pe_stack* s) {
+    s->spec.active = false;
+    s->spec.pending = false;
+    s->spec.grow = 1;
+}
+
+static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
+    s->gen++;
+    HIP_TRY(s, hipSetDevice(s->device));
+    int rc = prepare_tg(s, tgi, s->visit, s->offset);
+    if (rc) return rc;
+    TgPlan& g = *s->tgs[tgi];
+    pe_stack::Spec& sp = s->spec;
+    // placements of the group still to come in this evaluation (tg.Count minus
+    // the plan's), at least the run length grown from earlier used-up runs
+    uint32_t done = 0;
+    for (auto& p : s->plan) done += p.first == g.name;
+    uint32_t count = g.count > 0 && (uint32_t)g.count > done ? (uint32_t)g.count - done : 0u;
+    count = std::min<uint32_t>(std::max(count, sp.grow), 1u << 16);
+    rc = spec_copy(s, g, true);
+    if (rc) return rc;
+    const size_t plan0 = s->plan.size();
+    if (sp.recs.size() < count) sp.recs.resize(count);
+    uint32_t placed = 0;
+    rc = place_impl(s, tgi, count, sp.recs.data(), &placed, false);
+    s->plan.resize(plan0);   // the plan holds confirmed placements only
+    if (rc) {
+        const int rc2 = spec_copy(s, g, false);   // leave the device as the caller last saw it
+        (void)rc2;
+        (void)hipStreamSynchronize(s->stream);
+        return rc;
+    }
+    sp.active = true;
+    sp.pending = false;
+    sp.tgi = tgi;
+    sp.placed = placed;
+    sp.n_rec = placed < count ? placed + 1 : placed;
+    sp.served = 0;
+    sp.confirmed = 0;
+    s->spec_stats[0]++;
+    s->spec_stats[3] += sp.n_rec;
+    s->offer_row = -1;
+    if (!spec_serve(s, tgi, nullptr, out)) return s->fail(PE_ESTATE, "speculative loop produced no record");
+    s->spec_stats[1]--;   // the first record is the Select that started the run
+    return PE_OK;
+}
+
+int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+    if (!s) return PE_EINVAL;
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    return place_impl(s, tgi, count, out, placed, true);
+}
+
+int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
+    if (!s) return PE_EINVAL;
+    pe_stack::Spec& sp = s->spec;
+    if (sp.active && sp.pending && tgi == sp.tgi && row == sp.recs[sp.served - 1].row) {
+        // the predicted Plan.AppendAlloc: already in HBM
+        sp.pending = false;
+        sp.confirmed = sp.served;
+        s->gen++;
+        s->plan.emplace_back(s->tgs[tgi]->name, (uint32_t)row);
+        invalidate_job_distinct(s, tgi);
+        s->offer_row = -1;
+        return PE_OK;
+    }
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    return commit_impl(s, tgi, row);
+}
+
+int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
+    if (!s) return PE_EINVAL;
+    if (n_preempted == 0) return pe_commit(s, tgi, row);
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    return commit_preempt_impl(s, tgi, row, preempted, n_preempted);
+}
+
+int pe_speculation_stats(const pe_stack* s, uint64_t* out4) {
+    if (!s || !out4) return PE_EINVAL;
+    for (int i = 0; i < 4; i++) out4[i] = s->spec_stats[i];
+    return PE_OK;
+}
+
 int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint32_t n) {
     if (!s || (!orders && n_evals && n)) return PE_EINVAL;
+    {
+        const int frc = spec_flush(s);
+        if (frc) return frc;
+    }
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
@@ -3031,6 +3297,10 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
 
 int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out, uint32_t* placed) {
     if (!s) return PE_EINVAL;
+    {
+        const int frc = spec_flush(s);
+        if (frc) return frc;
+    }
     if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place_batch needs a generic stack");
     if (!s->plan.empty()) return s->fail(PE_ESTATE, "batch evaluations start from a fresh plan (pe_reset_plan)");
     if (!s->have_job || tgi >= s->tgs.size()) return s->fail(PE_ESTATE, "pe_set_job not called / bad task group");
@@ -3106,6 +3376,10 @@ void pe_last_phase_ms(const pe_stack* s, double* out4) {
 
 int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     if (!s || !out_score || !out_status) return PE_EINVAL;
+    {
+        const int frc = spec_flush(s);
+        if (frc) return frc;
+    }
     if (s->cfg.stack_kind != PE_STACK_SYSTEM) return s->fail(PE_ESTATE, "pe_system_place needs a system stack");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
@@ -3177,7 +3451,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
                     if (r.row < 0) continue;
                     s->offer_row = r.row;
                     s->offers = pack_offers(&r);
-                    rc = pe_commit_preempt(s, tgi, r.row, r.preempted, r.n_preempted);
+                    rc = commit_preempt_impl(s, tgi, r.row, r.preempted, r.n_preempted);
                     if (rc) { s->limit = saved; return rc; }
                     out_status[pos[k]] = 0;
                     out_score[pos[k]] = r.final_score;
@@ -3246,6 +3520,10 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
 
 extern "C" int pe_set_metrics(pe_stack* s, int on) {
     if (!s) return PE_EINVAL;
+    {
+        const int frc = spec_flush(s);
+        if (frc) return frc;
+    }
     s->metrics_on = on != 0;
     s->metrics_valid = false;
     return PE_OK;

@@ -1744,6 +1744,38 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t of
     commit_row(s, t, a, row, offers);
 }
 
+// Replay of a speculative loop's confirmed placements after a rollback to its
+// checkpoint (pe_commit / pe_select, engine.cpp): one thread per placement,
+// every update an integer atomic add, so repeated rows sum exactly as the
+// sequential commit_row calls would. Each offer was assigned on the state that
+// already held every earlier placement, so no free count underflows and the
+// packed u8 subtractions never borrow.
+__global__ void __launch_bounds__(256) k_apply_commits(NodeSoA s, TgTables t, Ask a, const uint32_t* rows,
+                                                      const uint32_t* offers, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t row = rows[i];
+    NodeRec& r = s.rec[row];
+    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_cpu), (unsigned long long)a.cpu);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_mem), (unsigned long long)a.mem);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_disk), (unsigned long long)a.disk);
+    atomicAdd(reinterpret_cast<unsigned int*>(&r.used_mbits), (unsigned int)a.commit_mbits);
+    atomicAdd(reinterpret_cast<unsigned int*>(&r.used_dyn), (unsigned int)a.commit_dyn);
+    atomicAdd(&s.coll_job[row], 1u);
+    atomicAdd(&t.coll_tg[row], 1u);
+    const uint32_t c = r.cls;
+    if (a.n_dev > 0) {
+        const uint32_t o = offers[i];
+        uint32_t sub = 0;
+        for (int q = 0; q < kMaxDevReq && q < a.n_dev; q++) sub += (uint32_t)a.dev_cnt[q] << (8 * ((o >> (8 * q)) & 255u));
+        atomicSub(&t.dev_free[row], sub);
+    }
+    for (int p = 0; p < t.n_psets; p++) {
+        const uint32_t v = pset_value(t, p, row, c);
+        if (v != kMissing) atomicAdd(&t.pset_counts[p][v], 1u);
+    }
+}
+
 // One pass of the scoring sweep over rows [row_begin, row_end), one tile of
 // BLOCK rows per workgroup iteration (grid-stride), 64 rows per wave. Every
 // lane streams its row (64-byte record, collision count, verdict, visit rank),
@@ -2183,6 +2215,13 @@ hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st) {
 hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
                             uint32_t offers, hipStream_t st) {
     hipLaunchKernelGGL(pe::k_commit, dim3(1), dim3(64), 0, st, *s, *t, *a, row, offers);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_apply_commits(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
+                                   const uint32_t* offers, uint32_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_apply_commits, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, offers, n);
     return hipGetLastError();
 }
 

@@ -64,6 +64,8 @@ def load_engine():
         lib.pe_select_shard.restype = C.c_int
         lib.pe_select_shard.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.POINTER(abi.pe_shard_rec)]
+        lib.pe_speculation_stats.restype = C.c_int
+        lib.pe_speculation_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         lib.pe_select_merge.restype = C.c_int
         lib.pe_select_merge.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(abi.pe_shard_rec), C.c_uint32,
                                         C.POINTER(abi.pe_ranked_node)]
@@ -381,6 +383,13 @@ class GenericStack(_Stack):
         out = abi.pe_ranked_node()
         self._check(self._lib.pe_select_merge(self._h, self._tg_index(tg), arr, len(recs), C.byref(out)))
         return RankedNode.from_c(out, self.nodes)
+
+    def SpeculationStats(self):
+        """(runs, Selects answered from records, rollbacks, records computed) of
+        the speculative count loop behind Select / Commit (pe_speculation_stats)."""
+        buf = (C.c_uint64 * 4)()
+        self._check(self._lib.pe_speculation_stats(self._h, buf))
+        return tuple(int(x) for x in buf)
 
     def last_phase_ms(self):
         """[host prep, kernel, D2H copy, total] of the last PlaceBatch, ms."""

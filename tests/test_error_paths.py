@@ -47,3 +47,36 @@ def test_update_allocs_bad_index_requires_reload():
     st.SetJob(synth.mock_job())
     st.SetNodes(nodes)
     assert st.Select(0) is not None
+
+
+@pytest.mark.gpu
+def test_bad_set_nodes_keeps_previous_list():
+    """A SetNodes with an out-of-range row is refused before any state changes
+    (ADVICE r1): the next Select runs on the previous list, never on bad rows."""
+    from nomad_amd.stack import EngineError, GenericStack
+    from oracle.oracle import OracleGenericStack
+    nodes, allocs = synth.cluster_c1(30, seed=5)
+    job = synth.mock_job(count=3)
+    perm = synth.shuffle(len(nodes), 2)
+    st = GenericStack()
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(perm)
+    bad = np.array(list(perm[:5]) + [len(nodes) + 3], dtype=np.uint32)
+    with pytest.raises(EngineError, match="out of range"):
+        st.SetNodes(bad)
+    got = st.Select(0)
+    o = OracleGenericStack()
+    o.SetState(nodes, allocs)
+    o.SetJob(job)
+    o.SetNodes(perm)
+    want = o.Select(0)
+    assert got is not None and want is not None
+    assert (got.row, got.final_score, got.new_offset) == (want.row, want.final_score, want.new_offset)
+    # a fresh stack whose only SetNodes was refused selects over an empty list
+    st2 = GenericStack()
+    st2.SetState(nodes, allocs)
+    st2.SetJob(job)
+    with pytest.raises(EngineError):
+        st2.SetNodes(bad)
+    assert st2.Select(0) is None

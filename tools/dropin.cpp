@@ -1,0 +1,99 @@
+// Caller-side harness (bench / tests only, not the product): the loop the
+// unchanged Go caller runs against a Stack, written in C so the measured time
+// is the C ABI's and not an interpreter's. GenericScheduler.computePlacements
+// (generic_sched.go:472-652) per evaluation: SetNodes once, then per placement
+// Select with empty options, on nil a retry with Preempt=true when preemption
+// is enabled (selectNextOption, :773-792), and on an option the plan append
+// the cgo shim mirrors with Commit (AppendAlloc :627 + handlePreemptions
+// :794-816). A nil after the retry ends the task group (failedTGAllocs,
+// :519-523). Evaluations start from a fresh EvalContext (ResetPlan) and SetJob.
+//
+// The same loop drives the engine (pe_*) and the CPU oracle (oracle_*): the
+// caller passes the entry points.
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+
+#include "../include/nomad_pe.h"
+
+extern "C" {
+
+struct dropin_api {
+    int (*reset_plan)(void*);
+    int (*set_job)(void*, const pe_strtab*, const pe_job*);
+    int (*set_nodes)(void*, const uint32_t*, uint32_t, uint32_t*);
+    int (*select)(void*, uint32_t, const pe_select_options*, pe_ranked_node*);
+    int (*commit)(void*, uint32_t, int32_t);
+    int (*commit_preempt)(void*, uint32_t, int32_t, const uint32_t*, uint32_t);
+};
+
+// One evaluation's placements of task group `tg`; rows[count] (may be null)
+// receives the chosen rows, -1 after the loop stopped. Returns 0 or the first
+// failing call's status.
+int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, int preempt, int32_t* rows,
+                 uint32_t* placed, uint64_t* selects) {
+    pe_select_options none;
+    std::memset(&none, 0, sizeof(none));
+    pe_select_options pre = none;
+    pre.preempt = 1;
+    pe_ranked_node opt;
+    uint32_t p = 0;
+    uint64_t sel = 0;
+    int rc = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        rc = api->select(h, tg, &none, &opt);
+        sel++;
+        if (rc) break;
+        if (opt.row < 0 && preempt) {
+            rc = api->select(h, tg, &pre, &opt);
+            sel++;
+            if (rc) break;
+        }
+        if (opt.row < 0) break;
+        rc = opt.n_preempted ? api->commit_preempt(h, tg, opt.row, opt.preempted, opt.n_preempted)
+                             : api->commit(h, tg, opt.row);
+        if (rc) break;
+        if (rows) rows[p] = opt.row;
+        p++;
+    }
+    for (uint32_t i = p; rows && i < count; i++) rows[i] = -1;
+    *placed = p;
+    if (selects) *selects += sel;
+    return rc;
+}
+
+// Sequential evaluations, one visit order each (orders[e * n ...]), cycling
+// through n_orders orders, until n_evals are done or max_seconds have passed
+// (0: no time limit). out[0] placements, out[1] evaluations, out[2] Selects;
+// *seconds the wall time of the loop. rows_last[count] gets the last
+// evaluation's rows (may be null).
+int dropin_evals(const dropin_api* api, void* h, const pe_strtab* strs, const pe_job* job, const uint32_t* orders,
+                 uint32_t n_orders, uint32_t n, uint32_t tg, uint32_t count, int preempt, uint32_t n_evals,
+                 double max_seconds, int32_t* rows_last, uint64_t* out, double* seconds) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    uint64_t placed_total = 0, evals = 0, selects = 0;
+    int rc = 0;
+    for (uint32_t e = 0; e < n_evals; e++) {
+        rc = api->reset_plan(h);
+        if (rc) break;
+        rc = api->set_job(h, strs, job);
+        if (rc) break;
+        uint32_t limit = 0;
+        rc = api->set_nodes(h, orders + (size_t)(e % n_orders) * n, n, &limit);
+        if (rc) break;
+        uint32_t p = 0;
+        rc = dropin_place(api, h, tg, count, preempt, rows_last, &p, &selects);
+        if (rc) break;
+        placed_total += p;
+        evals++;
+        if (max_seconds > 0 && std::chrono::duration<double>(clk::now() - t0).count() >= max_seconds) break;
+    }
+    *seconds = std::chrono::duration<double>(clk::now() - t0).count();
+    out[0] = placed_total;
+    out[1] = evals;
+    out[2] = selects;
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+"""Caller-side harness (bench / tests only): runs tools/libdropin.so, the Go
+caller's Select -> Commit loop in C (generic_sched.go:472-652, 773-816),
+against an engine GenericStack or an OracleGenericStack that already holds a
+snapshot (SetState). Evaluations: ResetPlan, SetJob, SetNodes(order), then
+count x (Select [, Select Preempt] , Commit)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from nomad_amd import abi
+from nomad_amd.encode import EncodedJob
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libdropin.so")
+_lib = None
+
+
+class dropin_api(C.Structure):
+    _fields_ = [(name, C.c_void_p) for name in
+                ("reset_plan", "set_job", "set_nodes", "select", "commit", "commit_preempt")]
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        lib = C.CDLL(LIB)
+        lib.dropin_evals.restype = C.c_int
+        lib.dropin_evals.argtypes = [C.POINTER(dropin_api), C.c_void_p, C.POINTER(abi.pe_strtab),
+                                     C.POINTER(abi.pe_job), abi.u32p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                     C.c_uint32, C.c_int, C.c_uint32, C.c_double, abi.i32p,
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        _lib = lib
+    return _lib
+
+
+def _api(stack):
+    lib, p = stack._lib, stack._p
+    a = dropin_api()
+    for name, _ in dropin_api._fields_:
+        setattr(a, name, C.cast(getattr(lib, p + name), C.c_void_p).value)
+    return a
+
+
+def run(stack, job, orders, count, tg=0, preempt=False, n_evals=None, max_seconds=0.0):
+    """Sequential evaluations of `job` through the C loop. orders: (k, n) visit
+    orders, evaluation e uses orders[e % k]. Returns (placements, evals,
+    selects, seconds, rows of the last evaluation)."""
+    lib = load()
+    o = np.ascontiguousarray(np.atleast_2d(np.asarray(orders, dtype=np.uint32)))
+    enc = EncodedJob(job, stack.state.interner)
+    tab = enc.strtab()
+    api = _api(stack)
+    rows = np.full(max(1, count), -1, dtype=np.int32)
+    out = (C.c_uint64 * 3)()
+    secs = C.c_double(0.0)
+    ne = o.shape[0] if n_evals is None else n_evals
+    rc = lib.dropin_evals(C.byref(api), stack._h, C.byref(tab), C.byref(enc.job), o.ctypes.data_as(abi.u32p),
+                          o.shape[0], o.shape[1], tg, count, int(preempt), ne, max_seconds,
+                          rows.ctypes.data_as(abi.i32p), out, C.byref(secs))
+    stack._check(rc)
+    stack._job = job
+    return int(out[0]), int(out[1]), int(out[2]), secs.value, rows[:count]
