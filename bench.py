@@ -202,7 +202,12 @@ def sweep_roofline(n, device, selects=6):
     from nomad_amd.stack import GenericStack
     t0 = time.perf_counter()
     cs = synth_columnar.ColumnarState(n, seed=7, kind="c3")
-    st = GenericStack(device=device)
+    # plain Selects, one at a time (no speculative count loop behind them)
+    os.environ["PE_SPECULATE"] = "0"
+    try:
+        st = GenericStack(device=device)
+    finally:
+        os.environ.pop("PE_SPECULATE", None)
     st.SetStateColumnar(cs)
     st.SetJob(synth.job_c3(1000))
     perm = np.random.Generator(np.random.PCG64(3)).permutation(n).astype(np.uint32)
@@ -652,17 +657,20 @@ def main():
     # caller's shape). The engine answers from its speculative device loop.
     st = GenericStack(device=local)
     st.SetState(nodes, allocs)
-    dropin.run(st, job, orders, args.count, n_evals=max(1, args.warmup))
+    caller = dropin.prepare(st, job)   # the shim's job encoding, once per job
+    caller(orders, args.count, n_evals=max(1, args.warmup))
+    timed_orders = np.roll(orders, -args.warmup, axis=0)
     spec0 = st.SpeculationStats()
+    dropin.phase_seconds(reset=True)
     barrier(pg)
     sync()
     t0 = time.perf_counter()
-    placed, evals, selects, c_secs, rows = dropin.run(st, job, np.roll(orders, -args.warmup, axis=0), args.count,
-                                                      n_evals=args.steps)
+    placed, evals, selects, c_secs, rows = caller(timed_orders, args.count, n_evals=args.steps)
     sync()
     elapsed = time.perf_counter() - t0
     barrier(pg)
     spec1 = st.SpeculationStats()
+    phases = dropin.phase_seconds(reset=True)
     elapsed = reduce(pg, elapsed, lambda d: d.ReduceOp.MAX)
     total_placed = reduce(pg, placed, lambda d: d.ReduceOp.SUM)
 
@@ -702,7 +710,8 @@ def main():
                         "c_loop_seconds": c_secs,
                         "speculation": dict(zip(("runs", "served", "rollbacks", "records"),
                                                 (b - a for a, b in zip(spec0, spec1)))),
-                        "us_per_placement": elapsed / max(1, placed) * 1e6},
+                        "us_per_placement": elapsed / max(1, placed) * 1e6,
+                        "us_per_eval_by_phase": {k: v / max(1, evals) * 1e6 for k, v in phases.items()}},
             "roofline": {"bound": "cache", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "note": "k_base + k_chain of one evaluation (the step's device work): cache-resident "

@@ -36,11 +36,14 @@
 size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
+hipError_t pe_launch_reset_plan(pe::NodeRec* rec, const pe::NodeRec* base_rec, uint32_t* dev_free,
+                                const uint32_t* dev_free_base, uint32_t n, uint8_t* preempted, uint32_t m,
+                                uint32_t* pcount, uint32_t keys, hipStream_t st);
 hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, uint32_t row,
                             uint32_t offers, hipStream_t st);
 hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs* r, hipStream_t st);
 hipError_t pe_launch_apply_commits(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
-                                   const uint32_t* offers, uint32_t n, hipStream_t st);
+                                   const uint32_t* offers, uint32_t n, int sign, hipStream_t st);
 hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ranked_node* out, uint32_t* mask,
                                   hipStream_t st);
 hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
@@ -281,6 +284,9 @@ struct pe_stack {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double last_ms = 0;
+    bool last_ms_pending = false;      // last_ms still to be read from ev0 / ev1
+    bool spin_wait = true;             // PE_SPIN_WAIT=0: chain launches wait with a stream sync
+    uint32_t place_seq = 0;            // completion word sequence (run_place)
     int n_cu = 256;
     int sweep_per_cu = 4, sweep_per_cu_aux = 4;
     uint32_t last_sweep_bytes = 0;   // algorithmic bytes per node of the last sweep
@@ -332,6 +338,9 @@ struct pe_stack {
     uint32_t sweep_min = 1u << 15;     // visit lists at least this long use the multi-CU sweep
     uint32_t loop_sweep_min = 8192;    // full-pass count loops this long run device-resident sweeps
     bool visit_unique = true;
+    bool rank_of_valid = false;        // d_rank_of holds the current SetNodes list's positions
+    std::vector<uint32_t> seen_stamp;  // SetNodes duplicate check
+    uint32_t seen_gen = 0;
     double last_sweep_ms = 0;
     std::vector<uint32_t> h_orders;
     uint32_t staged_evals = 0, staged_n = 0;
@@ -344,11 +353,15 @@ struct pe_stack {
     pe::BatchArgs batch_A{};
     PinnedMem h_batch_out, h_batch_status;
     PinnedMem h_place_out, h_place_status;   // single-evaluation count loop results (mapped)
+    PinnedMem h_stage;                 // upload staging ring (upload_s)
+    DevMem d_emit, d_emit_ov, d_emit_n;   // k_chain deferred records (k_emit)
+    size_t stage_off = 0;
     double phase_ms[4] = {0, 0, 0, 0};   // host prep, kernels, result copy, total (last batch)
     std::vector<pe::NodeRec> h_base_rec;     // snapshot proposed state (no plan)
     std::vector<pe::NodeRec> h_node_rec;     // node-only part (capacities, class, reserved ports)
     DevMem d_rec, d_base_rec, d_coll_job;
     DevMem d_base;                     // windowed loops: per-row base value table
+    DevMem d_base1;                    // the same with one placement on the row
     DevMem d_prof;                     // k_chain step profile (PE_CHAIN_PROF)
     bool orders_unique = true;         // every staged order lists each row at most once
     bool use_base = true;              // PE_WINDOW_LAZY=1: lazy per-position evaluation (k_window)
@@ -398,7 +411,8 @@ struct pe_stack {
         uint32_t tgi = 0;
         std::vector<pe_ranked_node> recs;
         uint32_t n_rec = 0, placed = 0, served = 0, confirmed = 0;
-        uint32_t grow = 1;             // minimum run length, grows while runs get used up
+        uint32_t grow = 1;             // run length on costly paths, doubles while runs get used up
+        bool checkpoint = false;       // dynamic columns saved at the start (device asks)
     } spec;
     bool spec_on = true;               // PE_SPECULATE=0: every Select runs on its own
     uint64_t spec_stats[4] = {0, 0, 0, 0};   // runs, Selects served, rollbacks, records computed
@@ -413,8 +427,15 @@ struct pe_stack {
     uint32_t limit = 2;
     double log10 = 0;
 
+    std::unordered_map<uint32_t, std::vector<uint32_t>> job_allocs;   // job -> non-terminal alloc indices
+
     // ---- helpers --------------------------------------------------------
     int fail(int code, const std::string& m) { err = m; return code; }
+    const std::vector<uint32_t>& own_allocs() const {
+        static const std::vector<uint32_t> none;
+        auto it = job_allocs.find(job_id);
+        return it == job_allocs.end() ? none : it->second;
+    }
     const std::string& S(uint32_t id) const {
         static const std::string empty;
         return id < strs.size() ? strs[id] : empty;
@@ -452,19 +473,44 @@ namespace {
                                                hipGetErrorString(_e));                  \
     } while (0)
 
+// Host -> device upload ordered on the engine stream: the bytes are staged in
+// a page-locked ring and copied asynchronously, so an entry point does not
+// wait for the device; the ring restarts after a stream synchronisation when
+// it is full. Large uploads synchronise and copy directly.
+constexpr size_t kStageBytes = 8u << 20;
+
 template <class T>
-hipError_t upload(DevMem& m, const std::vector<T>& h) {
-    hipError_t e = m.ensure(h.size() * sizeof(T));
-    if (e != hipSuccess) return e;
-    if (h.empty()) return hipSuccess;
-    return hipMemcpy(m.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+hipError_t upload_s(pe_stack* s, DevMem& m, const std::vector<T>& h) {
+    const size_t b = h.size() * sizeof(T);
+    hipError_t e = m.ensure(b);
+    if (e != hipSuccess || b == 0) return e;
+    if (b > kStageBytes / 4) {
+        e = hipStreamSynchronize(s->stream);
+        if (e != hipSuccess) return e;
+        s->stage_off = 0;
+        return hipMemcpy(m.p, h.data(), b, hipMemcpyHostToDevice);
+    }
+    if (!s->h_stage.p) {
+        e = s->h_stage.ensure(kStageBytes);
+        if (e != hipSuccess) return e;
+    }
+    size_t off = (s->stage_off + 255) & ~size_t(255);
+    if (off + b > kStageBytes) {
+        e = hipStreamSynchronize(s->stream);
+        if (e != hipSuccess) return e;
+        off = 0;
+    }
+    unsigned char* dst = s->h_stage.as<unsigned char>() + off;
+    std::memcpy(dst, h.data(), b);
+    s->stage_off = off + b;
+    return hipMemcpyAsync(m.p, dst, b, hipMemcpyHostToDevice, s->stream);
 }
 
 // Visit order into d_visit; the SetNodes list itself is uploaded once per SetNodes.
 hipError_t upload_visit(pe_stack* s, const std::vector<uint32_t>& order) {
     const bool is_visit = &order == &s->visit;
     if (is_visit && s->d_visit_is_visit) return hipSuccess;
-    hipError_t e = upload(s->d_visit, order);
+    hipError_t e = upload_s(s, s->d_visit, order);
     s->d_visit_is_visit = is_visit && e == hipSuccess;
     return e;
 }
@@ -680,7 +726,7 @@ int build_dev_classes(pe_stack* s, TgPlan& g) {
             }
         }
     }
-    HIP_TRY(s, upload(g.dev_cls, tab));
+    HIP_TRY(s, upload_s(s, g.dev_cls, tab));
     g.dev_cls_valid = true;
     g.dev_free = s->d_dev_free.as<uint32_t>();
     return PE_OK;
@@ -1013,6 +1059,11 @@ int build_alloc_state(pe_stack* s) {
         }
         s->alloc_dev.swap(live);
     }
+    // non-terminal allocs per job (SetJob and the collision / property counts
+    // touch only the job's own allocs)
+    s->job_allocs.clear();
+    for (uint32_t i = 0; i < (uint32_t)s->allocs.size(); i++)
+        if (!s->allocs[i].terminal) s->job_allocs[s->allocs[i].job].push_back(i);
     std::vector<int64_t> dev_used(s->dev_groups.size(), 0);
     for (const HostAlloc& a : s->allocs) {
         if (a.terminal) continue;
@@ -1027,8 +1078,8 @@ int build_alloc_state(pe_stack* s) {
         r.used_mbits += a.mbits;
         r.used_dyn += a.dyn;
     }
-    HIP_TRY(s, upload(s->d_base_rec, s->h_base_rec));
-    HIP_TRY(s, upload(s->d_rec, s->h_base_rec));
+    HIP_TRY(s, upload_s(s, s->d_base_rec, s->h_base_rec));
+    HIP_TRY(s, upload_s(s, s->d_rec, s->h_base_rec));
     // DeviceAccounter free counts (devices.go:25-100) packed 4 x u8 per node
     s->h_dev_free.assign(n, 0);
     if (s->dev_packable)
@@ -1038,8 +1089,8 @@ int build_alloc_state(pe_stack* s) {
                 const int64_t f = std::max<int64_t>(0, (int64_t)s->dev_groups[g].healthy - dev_used[g]);
                 s->h_dev_free[i] |= (uint32_t)f << (8 * k);
             }
-    HIP_TRY(s, upload(s->d_dev_free_base, s->h_dev_free));
-    HIP_TRY(s, upload(s->d_dev_free, s->h_dev_free));
+    HIP_TRY(s, upload_s(s, s->d_dev_free_base, s->h_dev_free));
+    HIP_TRY(s, upload_s(s, s->d_dev_free, s->h_dev_free));
     // Preemptor inputs (preemption.go:96-154): non-terminal allocs per node in table order
     {
         s->preempt_unsupported.clear();
@@ -1086,13 +1137,13 @@ int build_alloc_state(pe_stack* s) {
         }
         s->n_jtg_keys = (uint32_t)jtg.size();
         s->h_preempted.assign(std::max<uint32_t>(m, 1), 0);
-        HIP_TRY(s, upload(s->d_node_alloc_off, s->h_node_alloc_off));
-        HIP_TRY(s, upload(s->d_palloc, pa));
-        HIP_TRY(s, upload(s->d_preempted, s->h_preempted));
-        HIP_TRY(s, upload(s->d_pcount, std::vector<uint32_t>(std::max<uint32_t>(s->n_jtg_keys, 1), 0)));
+        HIP_TRY(s, upload_s(s, s->d_node_alloc_off, s->h_node_alloc_off));
+        HIP_TRY(s, upload_s(s, s->d_palloc, pa));
+        HIP_TRY(s, upload_s(s, s->d_preempted, s->h_preempted));
+        HIP_TRY(s, upload_s(s, s->d_pcount, std::vector<uint32_t>(std::max<uint32_t>(s->n_jtg_keys, 1), 0)));
     }
     std::vector<uint32_t> zeros(n, 0);
-    HIP_TRY(s, upload(s->d_coll_job, zeros));
+    HIP_TRY(s, upload_s(s, s->d_coll_job, zeros));
     return PE_OK;
 }
 
@@ -1113,10 +1164,10 @@ int build_collisions(pe_stack* s) {
         job[row]++;
         for (size_t g = 0; g < s->tgs.size(); g++) if (s->tgs[g]->name == tgname) tg[g][row]++;
     };
-    for (auto& a : s->allocs) if (!a.terminal && a.job == s->job_id) add(a.row, a.tg);
+    for (uint32_t i : s->own_allocs()) add(s->allocs[i].row, s->allocs[i].tg);
     for (auto& p : s->plan) add(p.second, p.first);
-    HIP_TRY(s, upload(s->d_coll_job, job));
-    for (size_t g = 0; g < s->tgs.size(); g++) HIP_TRY(s, upload(s->tgs[g]->coll_tg, tg[g]));
+    HIP_TRY(s, upload_s(s, s->d_coll_job, job));
+    for (size_t g = 0; g < s->tgs.size(); g++) HIP_TRY(s, upload_s(s, s->tgs[g]->coll_tg, tg[g]));
     return PE_OK;
 }
 
@@ -1166,8 +1217,8 @@ int build_psets(pe_stack* s, TgPlan& g) {
             return ps->per_node ? by_node[row] : by_class[s->nodes[row].cls];
         };
         ps->h_counts.assign(ps->value_str.size(), 0);
-        for (auto& a : s->allocs)
-            if (!a.terminal && a.ns == s->job_ns && a.job == s->job_id && a.tg == g.name) {
+        for (uint32_t ai : s->own_allocs())
+            if (const HostAlloc& a = s->allocs[ai]; a.ns == s->job_ns && a.tg == g.name) {
                 uint32_t v = node_val(a.row);
                 if (v != pe::kMissing) ps->h_counts[v]++;
             }
@@ -1199,14 +1250,14 @@ int build_psets(pe_stack* s, TgPlan& g) {
             else if (has_star) ps->h_desired[v] = star;
         }
         ps->weight_frac = (double)(int8_t)si->weight / (double)s->sum_spread_weights;
-        HIP_TRY(s, upload(ps->val_class, by_class));
-        if (ps->per_node) HIP_TRY(s, upload(ps->val_node, by_node));
+        HIP_TRY(s, upload_s(s, ps->val_class, by_class));
+        if (ps->per_node) HIP_TRY(s, upload_s(s, ps->val_node, by_node));
         std::vector<uint32_t> cnt = ps->h_counts;
         if (cnt.empty()) cnt.push_back(0);
-        HIP_TRY(s, upload(ps->counts, cnt));
+        HIP_TRY(s, upload_s(s, ps->counts, cnt));
         std::vector<double> des = ps->h_desired;
         if (des.empty()) des.push_back(0);
-        HIP_TRY(s, upload(ps->desired, des));
+        HIP_TRY(s, upload_s(s, ps->desired, des));
         g.psets.push_back(std::move(ps));
     }
     g.n_spread = (int)g.psets.size();
@@ -1262,8 +1313,8 @@ int build_psets(pe_stack* s, TgPlan& g) {
         if (ps->value_str.size() > (size_t)pe::kMaxValues) { g.unsupported = "distinct_property with > 256 values"; return PE_OK; }
         auto node_val = [&](uint32_t row) { return ps->per_node ? by_node[row] : by_class[s->nodes[row].cls]; };
         ps->h_counts.assign(ps->value_str.size(), 0);
-        for (auto& a : s->allocs)
-            if (!a.terminal && a.ns == s->job_ns && a.job == s->job_id && (job_level || a.tg == g.name)) {
+        for (uint32_t ai : s->own_allocs())
+            if (const HostAlloc& a = s->allocs[ai]; a.ns == s->job_ns && (job_level || a.tg == g.name)) {
                 const uint32_t v = node_val(a.row);
                 if (v != pe::kMissing) ps->h_counts[v]++;
             }
@@ -1272,12 +1323,12 @@ int build_psets(pe_stack* s, TgPlan& g) {
                 const uint32_t v = node_val(p.second);
                 if (v != pe::kMissing) ps->h_counts[v]++;
             }
-        HIP_TRY(s, upload(ps->val_class, by_class));
-        if (ps->per_node) HIP_TRY(s, upload(ps->val_node, by_node));
+        HIP_TRY(s, upload_s(s, ps->val_class, by_class));
+        if (ps->per_node) HIP_TRY(s, upload_s(s, ps->val_node, by_node));
         std::vector<uint32_t> cnt = ps->h_counts;
         if (cnt.empty()) cnt.push_back(0);
-        HIP_TRY(s, upload(ps->counts, cnt));
-        HIP_TRY(s, upload(ps->desired, std::vector<double>(1, 0.0)));
+        HIP_TRY(s, upload_s(s, ps->counts, cnt));
+        HIP_TRY(s, upload_s(s, ps->desired, std::vector<double>(1, 0.0)));
         g.psets.push_back(std::move(ps));
     }
     g.psets_built = true;
@@ -1365,9 +1416,9 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         class_ok = class_verdicts(s, g, memo);
         if (s->job_escaped) node_ok = g.job_ok_node;
     }
-    HIP_TRY(s, upload(g.class_ok, class_ok));
+    HIP_TRY(s, upload_s(s, g.class_ok, class_ok));
     g.node_ok_used = !node_ok.empty();
-    if (g.node_ok_used) HIP_TRY(s, upload(g.node_ok, node_ok));
+    if (g.node_ok_used) HIP_TRY(s, upload_s(s, g.node_ok, node_ok));
     {
         // fold the class verdict into one byte per node (single round trip per node)
         pe::NodeSoA soa = soa_of(s);
@@ -1396,14 +1447,14 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         if (escapes) {
             std::vector<double> na(n);
             for (size_t i = 0; i < n; i++) na[i] = score(s->view((uint32_t)i));
-            HIP_TRY(s, upload(g.node_aff, na));
+            HIP_TRY(s, upload_s(s, g.node_aff, na));
             g.node_aff_used = true;
             g.h_aff_node = std::move(na);
             g.h_aff_class.clear();
         } else {
             std::vector<double> ca(s->ncls);
             for (uint32_t c = 0; c < s->ncls; c++) ca[c] = score(s->view(s->class_rep[c]));
-            HIP_TRY(s, upload(g.class_aff, ca));
+            HIP_TRY(s, upload_s(s, g.class_aff, ca));
             g.h_aff_class = std::move(ca);
             g.h_aff_node.clear();
         }
@@ -1421,7 +1472,7 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
             const auto a = s->view((uint32_t)i).aliases;
             al[i] = std::find(a.begin(), a.end(), want) != a.end();
         }
-        HIP_TRY(s, upload(g.alias_ok, al));
+        HIP_TRY(s, upload_s(s, g.alias_ok, al));
         g.alias_used = true;
     }
     g.tables_valid = true;
@@ -1563,8 +1614,8 @@ int build_aux(pe_stack* s, TgPlan& g, const pe::TgTables& t) {
         idx[i] = it->second;
     }
     vals.resize(pe::kAuxValues, 0.0);
-    HIP_TRY(s, upload(g.aff_vals, vals));
-    if (!idx.empty()) HIP_TRY(s, upload(g.aff_idx, idx));
+    HIP_TRY(s, upload_s(s, g.aff_vals, vals));
+    if (!idx.empty()) HIP_TRY(s, upload_s(s, g.aff_idx, idx));
     const size_t n = s->nodes.size();
     HIP_TRY(s, g.node_aux.ensure(sizeof(uint32_t) * std::max<size_t>(n, 1)));
     pe::NodeSoA soa = soa_of(s);
@@ -1581,6 +1632,16 @@ bool full_scan_kernel(pe_stack* s, TgPlan& g, uint32_t n) {
 
 // Full-scan Select (limit >= n) as a multi-CU sweep: every workgroup reduces
 // its rows to a SweepRec, one merge yields the winner.
+// Visit position of every row (PE_NONE: not listed) for the sweep paths.
+int ensure_rank_of(pe_stack* s) {
+    if (s->rank_of_valid) return PE_OK;
+    std::vector<uint32_t> rank_of(s->nodes.size(), PE_NONE);
+    for (uint32_t i = 0; i < (uint32_t)s->visit.size(); i++) rank_of[s->visit[i]] = i;
+    HIP_TRY(s, upload_s(s, s->d_rank_of, rank_of));
+    s->rank_of_valid = true;
+    return PE_OK;
+}
+
 // The sweep over snapshot rows [row_begin, row_end) (one GPU's shard, or all
 // rows): per-workgroup SweepRec records merged into *rec.
 // SweepArgs and grid of one full-pass Select over rows [row_begin, row_end)
@@ -1593,6 +1654,10 @@ int sweep_setup(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_t 
     A.soa = soa_of(s);
     A.tg = tables_of(g);
     A.ask = ask_for(s, g);
+    {
+        const int rc = ensure_rank_of(s);
+        if (rc) return rc;
+    }
     A.rank_of = s->d_rank_of.as<uint32_t>();
     A.n_visit = n;
     A.offset = s->offset;
@@ -1605,7 +1670,7 @@ int sweep_setup(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_t 
             uint32_t r = opts->penalty_rows[i];
             if (r < s->nodes.size()) bits[r >> 5] |= 1u << (r & 31);
         }
-        HIP_TRY(s, upload(s->d_penalty, bits));
+        HIP_TRY(s, upload_s(s, s->d_penalty, bits));
         A.penalty_bits = s->d_penalty.as<uint32_t>();
     }
     if (!g.psets.empty()) {
@@ -1647,6 +1712,7 @@ int sweep_partial(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_
     if (row_end <= row_begin) {   // an empty shard contributes the identity record
         pe_rec_init(rec);
         s->last_ms = s->last_sweep_ms = 0;
+        s->last_ms_pending = false;
         return PE_OK;
     }
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
@@ -1657,6 +1723,7 @@ int sweep_partial(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
+    s->last_ms_pending = false;
     s->last_sweep_ms = ms;
     return PE_OK;
 }
@@ -1819,7 +1886,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
             uint32_t r = opts->penalty_rows[i];
             if (r < s->nodes.size()) bits[r >> 5] |= 1u << (r & 31);
         }
-        HIP_TRY(s, upload(s->d_penalty, bits));
+        HIP_TRY(s, upload_s(s, s->d_penalty, bits));
         P.penalty_bits = s->d_penalty.as<uint32_t>();
     }
     if (!g.psets.empty()) {
@@ -1855,6 +1922,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
+    s->last_ms_pending = false;
     if (flags & 1u)
         return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the on-device "
                                         "alloc limits");
@@ -1892,6 +1960,10 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
 // One evaluation on the stack's plan (pe_select / pe_place): the fused count
 // loop in launches of at most H/2 placements, each merging its overlay back
 // into the HBM SoA so the plan persists.
+double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::vector<uint32_t>& order,
               uint32_t offset, const pe_select_options* opts, pe_ranked_node* out, uint32_t* placed,
               uint32_t* new_offset) {
@@ -1915,7 +1987,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             uint32_t r = opts->penalty_rows[i];
             if (r < s->nodes.size()) bits[r >> 5] |= 1u << (r & 31);
         }
-        HIP_TRY(s, upload(s->d_penalty, bits));
+        HIP_TRY(s, upload_s(s, s->d_penalty, bits));
         A.penalty_bits = s->d_penalty.as<uint32_t>();
     }
     A.hash_bits = hash_bits_for(count, full);
@@ -1935,11 +2007,15 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             }
         }
         if (chain) {
-            HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));
+            // one evaluation: values in visit order (coalesced window reads)
+            HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(std::max<size_t>(s->nodes.size(), n), 1)));
             A.base = s->d_base.as<double>();
+            A.base_by_pos = 1;
+            HIP_TRY(s, s->d_base1.ensure(sizeof(double) * std::max<size_t>(n, 1)));
+            A.base1 = s->d_base1.as<double>();
             if (std::getenv("PE_CHAIN_PROF")) {
-                HIP_TRY(s, s->d_prof.ensure(8 * sizeof(unsigned long long)));
-                HIP_TRY(s, hipMemset(s->d_prof.p, 0, 8 * sizeof(unsigned long long)));
+                HIP_TRY(s, s->d_prof.ensure(32 * sizeof(unsigned long long)));
+                HIP_TRY(s, hipMemset(s->d_prof.p, 0, 32 * sizeof(unsigned long long)));
                 A.prof = s->d_prof.as<unsigned long long>();
             }
         }
@@ -1954,38 +2030,106 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     A.full_out = s->h_place_out.dev<pe_ranked_node>();
     A.eval_status = s->h_place_status.dev<uint32_t>();
     if (!A.full_out || !A.eval_status) return s->fail(PE_EHIP, "mapped result buffers unavailable");
+    if (chain) {
+        // k_chain writes one compact entry per Select; k_emit (many workgroups)
+        // builds the full records and writes the placements back
+        const size_t cap = std::min(count, chunk);
+        HIP_TRY(s, s->d_emit.ensure(sizeof(pe::ChainEmit) * cap));
+        HIP_TRY(s, s->d_emit_ov.ensure(sizeof(uint2) * cap));
+        if (!s->d_emit_n.p) {
+            HIP_TRY(s, s->d_emit_n.ensure(4 * sizeof(uint32_t)));
+            HIP_TRY(s, hipMemsetAsync(s->d_emit_n.p, 0, 4 * sizeof(uint32_t), s->stream));
+        }
+        A.emit = s->d_emit.as<pe::ChainEmit>();
+        A.emit_ov = s->d_emit_ov.as<uint2>();
+        A.emit_n = s->d_emit_n.as<uint32_t>();
+    }
     double total_ms = 0;
     uint32_t done = 0;
+    const bool hprof = std::getenv("PE_PLACE_PROF") != nullptr;
+    double h_launch = 0, h_sync = 0, h_copy = 0;
+    // The chain path ends with k_emit, whose last workgroup raises a completion
+    // word in the mapped status block: the host spins on it instead of waking
+    // from a stream synchronisation; the launch's event timing is resolved
+    // when it is asked for (pe_last_kernel_ms).
+    const bool spin = chain && s->spin_wait;
+    volatile uint32_t* flag = s->h_place_status.as<uint32_t>() + 3;
+    if (spin) {
+        A.done_flag = s->h_place_status.dev<uint32_t>() + 3;
+        HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    }
     while (done < count) {
         const uint32_t c = std::min(chunk, count - done);
         A.count = c;
         A.offset0 = *new_offset;
-        HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+        const double t0 = hprof ? now_us() : 0.0;
+        if (spin) {
+            A.done_seq = ++s->place_seq;
+        } else {
+            HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+        }
         if (chain) HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream));
         else HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
         HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
-        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        const double t1 = hprof ? now_us() : 0.0;
+        if (spin) {
+            const double t_spin = now_us();
+            while (*flag != A.done_seq && now_us() - t_spin < 2000.0) __builtin_ia32_pause();
+            if (*flag != A.done_seq) {
+                HIP_TRY(s, hipStreamSynchronize(s->stream));
+                if (*flag != A.done_seq) return s->fail(PE_EHIP, "k_emit completion word missing");
+            }
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        } else {
+            HIP_TRY(s, hipStreamSynchronize(s->stream));
+            float ms = 0;
+            HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+            total_ms += ms;
+        }
+        const double t2 = hprof ? now_us() : 0.0;
         uint32_t st[2];
-        std::memcpy(st, s->h_place_status.as<uint32_t>(), sizeof(st));
-        float ms = 0;
-        HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
-        total_ms += ms;
+        std::memcpy(st, const_cast<const uint32_t*>(s->h_place_status.as<uint32_t>()), sizeof(st));
         const uint32_t got = std::min(c, st[0] + 1);   // placed + the failing Select
         std::memcpy(out + done, s->h_place_out.as<pe_ranked_node>(), sizeof(pe_ranked_node) * got);
         if (commit)
             for (uint32_t i = 0; i < st[0]; i++) s->plan.emplace_back(g.name, (uint32_t)out[done + i].row);
+        if (hprof) {
+            const double t3 = now_us();
+            h_launch += t1 - t0;
+            h_sync += t2 - t1;
+            h_copy += t3 - t2;
+        }
         *placed += st[0];
         *new_offset = st[1];
         done += c;
         if (st[0] < c) break;
     }
-    s->last_ms = total_ms;
+    s->last_ms_pending = false;
+    if (spin) {
+        s->last_ms_pending = true;   // ev0 .. ev1 bracket the loop's launches
+        if (hprof || A.prof) {
+            HIP_TRY(s, hipEventSynchronize(s->ev1));
+            float ms = 0;
+            HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+            total_ms = ms;
+            s->last_ms_pending = false;
+        }
+    }
+    if (hprof)
+        std::fprintf(stderr, "run_place: launch %.1f us, sync %.1f us (kernels %.1f us), copy %.1f us\n", h_launch,
+                     h_sync, total_ms * 1e3, h_copy);
+    s->last_ms = total_ms;   // (pending when the spin path left it to the events)
     if (A.prof) {
-        unsigned long long pr[8];
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        unsigned long long pr[32];
         HIP_TRY(s, hipMemcpy(pr, A.prof, sizeof(pr), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "k_chain step clocks: setup %llu values %llu scan %llu index %llu select-bounds %llu "
-                             "argmax %llu emit+commit %llu (thread 0, summed over phases; kernels %.3f ms)\n",
-                     pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], total_ms);
+        for (int ph = 0; ph < 4; ph++) {
+            const unsigned long long* p = pr + 8 * ph;
+            if (!p[1]) continue;
+            std::fprintf(stderr, "k_chain phase %d clocks: top %llu values %llu scan %llu index %llu select-bounds %llu "
+                                 "argmax %llu emit+commit %llu\n", ph, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+        }
+        std::fprintf(stderr, "k_chain kernels %.3f ms\n", total_ms);
     }
     return PE_OK;
 }
@@ -2032,6 +2176,7 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     if (const char* e = std::getenv("PE_RESULTS_VIA_COPY")) s->results_via_copy = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_WINDOW_LAZY")) s->use_base = std::atoi(e) == 0;
     if (const char* e = std::getenv("PE_SPECULATE")) s->spec_on = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PE_SPIN_WAIT")) s->spin_wait = std::atoi(e) != 0;
     return s;
 }
 
@@ -2049,7 +2194,17 @@ void pe_stack_destroy(pe_stack* s) {
 
 const char* pe_last_error(const pe_stack* s) { return s ? s->err.c_str() : g_error.c_str(); }
 
-double pe_last_kernel_ms(const pe_stack* s) { return s ? s->last_ms : 0.0; }
+double pe_last_kernel_ms(const pe_stack* s) {
+    if (!s) return 0.0;
+    if (s->last_ms_pending) {
+        pe_stack* m = const_cast<pe_stack*>(s);
+        float ms = 0;
+        if (hipEventSynchronize(m->ev1) == hipSuccess && hipEventElapsedTime(&ms, m->ev0, m->ev1) == hipSuccess)
+            m->last_ms = ms;
+        m->last_ms_pending = false;
+    }
+    return s->last_ms;
+}
 
 uint32_t pe_last_sweep_bytes(const pe_stack* s) { return s ? s->last_sweep_bytes : 0u; }
 
@@ -2130,15 +2285,12 @@ int pe_reset_plan(pe_stack* s) {
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     const size_t n = s->nodes.size();
-    HIP_TRY(s, hipMemcpyAsync(s->d_rec.p, s->d_base_rec.p, n * sizeof(pe::NodeRec), hipMemcpyDeviceToDevice,
-                              s->stream));
-    HIP_TRY(s, hipMemcpyAsync(s->d_dev_free.p, s->d_dev_free_base.p, n * sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                              s->stream));
+    HIP_TRY(s, pe_launch_reset_plan(s->d_rec.as<pe::NodeRec>(), s->d_base_rec.as<pe::NodeRec>(),
+                                    s->d_dev_free.as<uint32_t>(), s->d_dev_free_base.as<uint32_t>(), (uint32_t)n,
+                                    s->d_preempted.as<uint8_t>(), (uint32_t)s->h_preempted.size(),
+                                    s->d_pcount.as<uint32_t>(), std::max<uint32_t>(s->n_jtg_keys, 1), s->stream));
     std::fill(s->h_preempted.begin(), s->h_preempted.end(), 0);
-    HIP_TRY(s, hipMemsetAsync(s->d_preempted.p, 0, s->h_preempted.size(), s->stream));
-    HIP_TRY(s, hipMemsetAsync(s->d_pcount.p, 0, sizeof(uint32_t) * std::max<uint32_t>(s->n_jtg_keys, 1), s->stream));
-    s->offer_row = -1;
-    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    s->offer_row = -1;   // stream-ordered: later launches and uploads see the reset state
     s->plan.clear();
     s->tg_memo.clear();
     s->job_memo.clear();
@@ -2282,8 +2434,8 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     s->have_job = true;
     {   // the job's own state allocs per node (ProposedAllocs minus plan placements)
         std::vector<uint32_t> own(s->nodes.size(), 0);
-        for (auto& a : s->allocs) if (!a.terminal && a.job == s->job_id) own[a.row]++;
-        HIP_TRY(s, upload(s->d_own_existing, own));
+        for (uint32_t i : s->own_allocs()) own[s->allocs[i].row]++;
+        HIP_TRY(s, upload_s(s, s->d_own_existing, own));
         auto it = s->job_keys.find(std::make_pair(s->job_id, s->job_ns));
         s->job_key = it == s->job_keys.end() ? PE_NONE : it->second;
     }
@@ -2316,14 +2468,23 @@ int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_
     s->limit = lim;
     if (limit_out) *limit_out = lim;
     invalidate_tables(s);
-    // visit position of every row (sweep path ranks rows without a gather)
-    std::vector<uint32_t> rank_of(s->nodes.size(), PE_NONE);
+    // a list without repeated rows (the chain and sweep loops need one); the
+    // visit position of every row (rank_of) is built when a sweep needs it
+    if (s->seen_stamp.size() != s->nodes.size()) {
+        s->seen_stamp.assign(s->nodes.size(), 0);
+        s->seen_gen = 0;
+    }
+    if (++s->seen_gen == 0) {
+        std::fill(s->seen_stamp.begin(), s->seen_stamp.end(), 0);
+        s->seen_gen = 1;
+    }
     s->visit_unique = true;
     for (uint32_t i = 0; i < n; i++) {
-        if (rank_of[s->visit[i]] != PE_NONE) s->visit_unique = false;
-        rank_of[s->visit[i]] = i;
+        uint32_t& st = s->seen_stamp[s->visit[i]];
+        if (st == s->seen_gen) s->visit_unique = false;
+        st = s->seen_gen;
     }
-    HIP_TRY(s, upload(s->d_rank_of, rank_of));
+    s->rank_of_valid = false;
     return PE_OK;
 }
 
@@ -2452,7 +2613,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
     }
     ScoreHeap heap;
     if (!rows.empty()) {
-        HIP_TRY(s, upload(s->d_trace_rows, rows));
+        HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
         HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
         HIP_TRY(s, s->d_trace_scores.ensure(rows.size() * 6 * sizeof(double)));
         pe::NodeSoA soa = soa_of(s);
@@ -2465,7 +2626,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                 const uint32_t r = opts->penalty_rows[i];
                 if (r < s->nodes.size()) bits[r >> 5] |= 1u << (r & 31);
             }
-            HIP_TRY(s, upload(s->d_penalty, bits));
+            HIP_TRY(s, upload_s(s, s->d_penalty, bits));
             pbits = s->d_penalty.as<uint32_t>();
         }
         const double* stab = nullptr;
@@ -2522,7 +2683,9 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                         auto& cnt = counts[p];
                         if (cnt.empty()) {
                             cnt.resize(std::max<size_t>(ps.value_str.size(), 1));
-                            HIP_TRY(s, hipMemcpy(cnt.data(), ps.counts.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+                            HIP_TRY(s, hipMemcpyAsync(cnt.data(), ps.counts.p, cnt.size() * 4, hipMemcpyDeviceToHost,
+                                                      s->stream));
+                            HIP_TRY(s, hipStreamSynchronize(s->stream));
                         }
                         used = cnt[it->second];
                     }
@@ -2781,9 +2944,6 @@ static int commit_preempt_impl(pe_stack* s, uint32_t tgi, int32_t row, const uin
     return commit_impl(s, tgi, row);
 }
 
-static double now_us() {
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 // Device-resident full-pass count loop (see pe_place). Same results as
 // `count` x (run_sweep_select + pe_commit).
@@ -2846,6 +3006,7 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
+    s->last_ms_pending = false;
     for (uint32_t i = 0; i < p; i++) s->plan.emplace_back(g.name, (uint32_t)out[i].row);   // Plan.AppendAlloc
     s->offer_row = -1;
     *placed = p;
@@ -3014,6 +3175,13 @@ static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     return true;
 }
 
+// Whether place_impl runs this group's loop as the phase-static chain.
+static bool spec_chain_path(pe_stack* s, TgPlan& g) {
+    const uint32_t nv = (uint32_t)s->visit.size();
+    return !tg_full_scan(s, g) && !s->cfg.preempt && s->use_base && s->visit_unique && nv <= pe_chain_max_n() &&
+           s->limit <= pe_chain_max_limit();
+}
+
 static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* opts) {
     if (!s->spec_on || s->cfg.stack_kind != PE_STACK_GENERIC || s->metrics_on) return false;
     if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
@@ -3049,16 +3217,33 @@ static int spec_flush(pe_stack* s) {
     if (!sp.active) return PE_OK;
     sp.active = false;
     sp.pending = false;
-    if (sp.served == sp.n_rec && sp.confirmed == sp.placed && sp.placed == sp.n_rec)
-        sp.grow = std::min<uint32_t>(std::max<uint32_t>(16, 2 * sp.grow), 4096);   // used up: run longer next time
+    const bool used_up = sp.served == sp.n_rec && sp.confirmed == sp.placed && sp.placed == sp.n_rec;
+    // run length of the next run on a costly path: doubles while runs get used
+    // up, back to one placement after a deviation
+    sp.grow = used_up ? std::min<uint32_t>(2 * sp.grow, 4096) : 1;
     if (sp.confirmed == sp.placed) return PE_OK;   // HBM holds exactly the confirmed placements
     HIP_TRY(s, hipSetDevice(s->device));
     TgPlan& g = *s->tgs[sp.tgi];
+    s->spec_stats[2]++;
+    pe::Ask a = ask_for(s, g);
+    pe::NodeSoA soa = soa_of(s);
+    pe::TgTables t = tables_of(g);
+    if (!sp.checkpoint) {
+        // no device ask: every commit added the same ask to its row, so the
+        // unconfirmed placements are taken back by subtracting them again
+        std::vector<uint32_t> rows(sp.placed - sp.confirmed), offers(rows.size(), 0xFFFFFFFFu);
+        for (uint32_t i = sp.confirmed; i < sp.placed; i++) rows[i - sp.confirmed] = (uint32_t)sp.recs[i].row;
+        HIP_TRY(s, upload_s(s, s->d_commit_rows, rows));
+        HIP_TRY(s, upload_s(s, s->d_commit_offers, offers));
+        HIP_TRY(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
+                                           s->d_commit_offers.as<uint32_t>(), (uint32_t)rows.size(), -1,
+                                           s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        return PE_OK;
+    }
     int rc = spec_copy(s, g, false);
     if (rc) return rc;
-    s->spec_stats[2]++;
     if (sp.confirmed == 0) return PE_OK;
-    pe::Ask a = ask_for(s, g);
     std::vector<uint32_t> rows(sp.confirmed), offers(sp.confirmed);
     bool ordered_only = false;   // a device ask without a recorded offer: replay one by one
     for (uint32_t i = 0; i < sp.confirmed; i++) {
@@ -3067,17 +3252,13 @@ static int spec_flush(pe_stack* s) {
         if (a.n_dev > 0 && offers[i] == 0xFFFFFFFFu) ordered_only = true;
     }
     if (ordered_only) {
-        pe::NodeSoA soa = soa_of(s);
-        pe::TgTables t = tables_of(g);
         for (uint32_t i = 0; i < sp.confirmed; i++)
             HIP_TRY(s, pe_launch_commit(&soa, &t, &a, rows[i], offers[i], s->stream));
     } else {
-        HIP_TRY(s, upload(s->d_commit_rows, rows));
-        HIP_TRY(s, upload(s->d_commit_offers, offers));
-        pe::NodeSoA soa = soa_of(s);
-        pe::TgTables t = tables_of(g);
+        HIP_TRY(s, upload_s(s, s->d_commit_rows, rows));
+        HIP_TRY(s, upload_s(s, s->d_commit_offers, offers));
         HIP_TRY(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
-                                           s->d_commit_offers.as<uint32_t>(), sp.confirmed, s->stream));
+                                           s->d_commit_offers.as<uint32_t>(), sp.confirmed, 1, s->stream));
     }
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     return PE_OK;
@@ -3102,17 +3283,27 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     uint32_t done = 0;
     for (auto& p : s->plan) done += p.first == g.name;
     uint32_t count = g.count > 0 && (uint32_t)g.count > done ? (uint32_t)g.count - done : 0u;
-    count = std::min<uint32_t>(std::max(count, sp.grow), 1u << 16);
-    rc = spec_copy(s, g, true);
-    if (rc) return rc;
+    // The phase-static chain (k_base + k_chain) costs about the same for one
+    // placement as for the whole count: run the group's remaining count. Every
+    // other loop pays per placement: start with one and double while the runs
+    // get used up (spec_flush).
+    count = spec_chain_path(s, g) ? std::max<uint32_t>(count, 1u) : std::max<uint32_t>(std::min(count, sp.grow), 1u);
+    count = std::min<uint32_t>(count, 1u << 16);
+    sp.checkpoint = ask_for(s, g).n_dev > 0;   // device offers are not undone by subtraction
+    if (sp.checkpoint) {
+        rc = spec_copy(s, g, true);
+        if (rc) return rc;
+    }
     const size_t plan0 = s->plan.size();
     if (sp.recs.size() < count) sp.recs.resize(count);
     uint32_t placed = 0;
     rc = place_impl(s, tgi, count, sp.recs.data(), &placed, false);
     s->plan.resize(plan0);   // the plan holds confirmed placements only
     if (rc) {
-        const int rc2 = spec_copy(s, g, false);   // leave the device as the caller last saw it
-        (void)rc2;
+        if (sp.checkpoint) {
+            const int rc2 = spec_copy(s, g, false);   // leave the device as the caller last saw it
+            (void)rc2;
+        }
         (void)hipStreamSynchronize(s->stream);
         return rc;
     }
@@ -3183,7 +3374,7 @@ int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint3
     for (size_t i = 0; i < total; i++)
         if (orders[i] >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range in staged order");
     s->h_orders.assign(orders, orders + total);
-    HIP_TRY(s, upload(s->d_orders, s->h_orders));
+    HIP_TRY(s, upload_s(s, s->d_orders, s->h_orders));
     {
         // generation-stamped duplicate check over every staged order
         std::vector<uint32_t> stamp(s->nodes.size(), 0);
@@ -3246,7 +3437,7 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
             auto ok = class_verdicts(s, g, memo);
             std::copy(ok.begin(), ok.end(), tabs.begin() + (size_t)e * s->ncls);
         }
-        HIP_TRY(s, upload(g.class_ok_batch, tabs));
+        HIP_TRY(s, upload_s(s, g.class_ok_batch, tabs));
         A.tg.class_ok = g.class_ok_batch.as<uint8_t>();
         A.tg.node_feas = nullptr;
         A.class_ok_stride = s->ncls;
@@ -3264,6 +3455,8 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
         // one base pass shared by every evaluation, then k_chain (persistent grid)
         HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));
         A.base = s->d_base.as<double>();
+        HIP_TRY(s, s->d_base1.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));
+        A.base1 = s->d_base1.as<double>();
         s->batch_chain = true;
         const size_t lds = pe_chain_lds_bytes(A.hash_bits, A.packed_overlay != 0, n);
         s->chain_grid = (uint32_t)(pe_chain_blocks_per_cu(lds) * s->n_cu);
@@ -3347,6 +3540,7 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     HIP_TRY(s, hipEventElapsedTime(&copy_ms, s->ev1, s->ev2));
     s->last_ms = ms;
+    s->last_ms_pending = false;
     const uint32_t* st = s->h_batch_status.as<uint32_t>();
     if (placed)
         for (uint32_t e = 0; e < E; e++) placed[e] = st[2 * e];
@@ -3424,6 +3618,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
+    s->last_ms_pending = false;
     for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) s->plan.emplace_back(g.name, s->visit[i]);
     if (s->cfg.preempt) {
         // BinPack with evict (stack.go:267-278) on the nodes the plain fit exhausted
@@ -3461,7 +3656,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
             } else {
                 const uint32_t E = (uint32_t)rows.size();
                 pe::PreemptArgs P = preempt_args(s, g);
-                HIP_TRY(s, upload(s->d_ev_rows, rows));
+                HIP_TRY(s, upload_s(s, s->d_ev_rows, rows));
                 HIP_TRY(s, s->d_ev_status.ensure(E));
                 HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * E));
                 HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * E));
@@ -3499,6 +3694,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
                 float ms2 = 0;
                 HIP_TRY(s, hipEventElapsedTime(&ms2, s->ev0, s->ev1));
                 s->last_ms += ms2;
+                s->last_ms_pending = false;
                 for (uint32_t k = 0; k < E; k++) {
                     if (st[k] != 0) continue;   // exhausted / skipped nodes stay exhausted
                     out_status[pos[k]] = 0;

@@ -98,6 +98,14 @@ struct Ask {
     double dev_tw;                // Σ |affinity weight| over requests with affinities (0: no score)
 };
 
+// One Select of a deferred-record k_chain launch (BatchArgs::emit).
+struct ChainEmit {
+    int32_t row;                  // winner, -1 = nil
+    uint32_t dk;                  // placements of the launch on the row before this one
+    uint32_t consumed, filtered, exhausted, new_offset;
+    double score;                 // FinalScore
+};
+
 // One launch = n_evals independent evaluations (one workgroup each) of the same
 // task group over the same snapshot; eval e visits perms + e*perm_stride.
 struct BatchArgs {
@@ -124,6 +132,21 @@ struct BatchArgs {
     // filtered, +inf exhausted), computed once per launch by k_base for all
     // evaluations. Null: the lazy per-position loop (k_window).
     double* base;
+    // base_by_pos: one evaluation; base[j] is the value of visit position j
+    // (k_base walks the visit list, k_chain then reads the window coalesced)
+    int base_by_pos;
+    // base1 (or null): the same with one placement of this launch on the row
+    // (a row's value in the phase after its first placement)
+    double* base1;
+    // Single-evaluation k_chain with deferred records (or null): k_chain writes
+    // one ChainEmit per Select and dumps its overlay (row, placements) into
+    // emit_ov; k_emit builds the full records and writes the placements back.
+    // emit_n: [0] entries, [1] overlay rows to write back, [2] k_emit ticket.
+    ChainEmit* emit;
+    uint2* emit_ov;
+    uint32_t* emit_n;
+    uint32_t* done_flag;          // or null: k_emit's last workgroup stores done_seq here (system scope)
+    uint32_t done_seq;
     unsigned long long* prof;     // k_chain step clocks (PE_CHAIN_PROF), or null
     pe_ranked_node* full_out;     // [n_evals][count] full records, or null
     pe_placement* out;            // [n_evals][count] compact records, or null

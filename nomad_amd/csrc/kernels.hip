@@ -72,20 +72,40 @@ __device__ __forceinline__ uint32_t ov_count(const Overlay& o, uint32_t row) {
     }
 }
 
-__device__ __forceinline__ void ov_add(const Overlay& o, uint32_t row) {
+// Plan.AppendAlloc into the overlay (one lane); returns the row's slot.
+__device__ __forceinline__ uint32_t ov_add(const Overlay& o, uint32_t row) {
     uint32_t h = ov_hash(o, row);
     if (!o.k) {
         for (;;) {
             const uint32_t e = o.keys[h];
-            if (e == kEmpty) { o.keys[h] = (row << o.kshift) | 1u; return; }
-            if ((e >> o.kshift) == row) { o.keys[h] = e + 1u; return; }
+            if (e == kEmpty) { o.keys[h] = (row << o.kshift) | 1u; return h; }
+            if ((e >> o.kshift) == row) { o.keys[h] = e + 1u; return h; }
             h = (h + 1) & o.mask;
         }
     }
     for (;;) {
         const uint32_t key = o.keys[h];
-        if (key == row) { o.k[h] += 1; return; }
-        if (key == kEmpty) { o.keys[h] = row; o.k[h] = 1; return; }
+        if (key == row) { o.k[h] += 1; return h; }
+        if (key == kEmpty) { o.keys[h] = row; o.k[h] = 1; return h; }
+        h = (h + 1) & o.mask;
+    }
+}
+
+// Slot of `row` in the overlay, or -1 when the row holds no placement.
+__device__ __forceinline__ int ov_slot(const Overlay& o, uint32_t row) {
+    uint32_t h = ov_hash(o, row);
+    if (!o.k) {
+        for (;;) {
+            const uint32_t e = o.keys[h];
+            if (e == kEmpty) return -1;
+            if ((e >> o.kshift) == row) return (int)h;
+            h = (h + 1) & o.mask;
+        }
+    }
+    for (;;) {
+        const uint32_t key = o.keys[h];
+        if (key == row) return (int)h;
+        if (key == kEmpty) return -1;
         h = (h + 1) & o.mask;
     }
 }
@@ -1127,13 +1147,22 @@ __device__ __forceinline__ double encode_eval(const NodeEval& ev) {
 // serves every evaluation of a batch.
 __global__ void __launch_bounds__(256) k_base(BatchArgs A) {
     const uint32_t stride = gridDim.x * 256;
-    for (uint32_t row = blockIdx.x * 256 + threadIdx.x; row < A.soa.n; row += stride) {
+    const uint32_t m = A.base_by_pos ? A.n_visit : A.soa.n;
+    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < m; j += stride) {
+        const uint32_t row = A.base_by_pos ? A.perms[j] : j;
         NodeIn in;
         load_node(A.soa, A.tg, row, in);
         NodeEval ev;
         ev.score = 0.0;
         eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, A.penalty_bits, A.log10, nullptr, row, in, &ev);
-        A.base[row] = encode_eval(ev);
+        A.base[j] = encode_eval(ev);
+        if (A.base1) {
+            NodeEval ev1;
+            ev1.score = 0.0;
+            eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, 1u, A.penalty_bits, A.log10, nullptr, row, in,
+                               &ev1);
+            A.base1[j] = encode_eval(ev1);
+        }
     }
 }
 
@@ -1188,13 +1217,16 @@ struct ChainShared {
     uint32_t sel_arg[kChainMaxSel];                        // option index of the first maximum
     uint32_t sel_row[kChainMaxSel];                        // the winner's row
     uint32_t sel_f[kChainMaxSel], sel_x[kChainMaxSel];     // filtered / exhausted positions (metrics)
-    uint2 redo[kChainMaxRedo];                             // (row, placements) to re-evaluate; then the value
-    uint16_t seg_tab[kChainSegs][kSegE];                  // per segment and entry offset: count | exit << 16
-    uint16_t seg_exit[kChainSegs][kSegE];
+    uint32_t seg_tab[kChainSegs][kSegE];                  // per segment and entry offset: count | exit << 16
     uint16_t seg_entry[kChainSegs], seg_base[kChainSegs];
+    uint2 redo[kChainMaxRedo];                             // (row, placements) to re-evaluate; then the value
+    uint16_t sel_pos[kChainMaxSel];                        // the winner's visit position (relative)
+    // visit positions (mod n) whose row holds >= 1 / >= 2 placements of this
+    // launch: later phases find their values without probing the overlay
+    uint32_t bm1[kChainMaxN / 32], bm2[kChainMaxN / 32];
     double aside_v[kMaxSkip];
     uint32_t aside_row[kMaxSkip];
-    uint32_t tot_o, tot_n, nsel, mode, n_redo, n_seg;
+    uint32_t tot_o, tot_n, nsel, mode, n_redo, n_seg, slow, n_emit, n_ov;
 };
 
 __device__ __forceinline__ unsigned long long order_key(double x) {
@@ -1210,7 +1242,7 @@ __device__ __forceinline__ uint32_t wrap_pos(uint32_t x, uint32_t n) {
 
 // Plan.AppendAlloc into the overlay from many threads at once; the rows are
 // distinct, so no two threads race on one key.
-__device__ __forceinline__ void ov_add_atomic(const Overlay& o, uint32_t row) {
+__device__ __forceinline__ uint32_t ov_add_atomic(const Overlay& o, uint32_t row) {
     uint32_t h = ov_hash(o, row);
     if (!o.k) {
         const uint32_t fresh = (row << o.kshift) | 1u;
@@ -1218,9 +1250,9 @@ __device__ __forceinline__ void ov_add_atomic(const Overlay& o, uint32_t row) {
             uint32_t e = o.keys[h];
             if (e == kEmpty) {
                 e = atomicCAS(&o.keys[h], kEmpty, fresh);
-                if (e == kEmpty) return;
+                if (e == kEmpty) return h;
             }
-            if ((e >> o.kshift) == row) { atomicAdd(&o.keys[h], 1u); return; }
+            if ((e >> o.kshift) == row) { atomicAdd(&o.keys[h], 1u); return h; }
             h = (h + 1) & o.mask;
         }
     }
@@ -1228,9 +1260,9 @@ __device__ __forceinline__ void ov_add_atomic(const Overlay& o, uint32_t row) {
         uint32_t key = o.keys[h];
         if (key == kEmpty) {
             key = atomicCAS(&o.keys[h], kEmpty, row);
-            if (key == kEmpty) { atomicAdd(&o.k[h], 1u); return; }
+            if (key == kEmpty) { atomicAdd(&o.k[h], 1u); return h; }
         }
-        if (key == row) { atomicAdd(&o.k[h], 1u); return; }
+        if (key == row) { atomicAdd(&o.k[h], 1u); return h; }
         h = (h + 1) & o.mask;
     }
 }
@@ -1252,12 +1284,14 @@ __device__ __forceinline__ uint32_t lower_bound_lds(const uint32_t* a, uint32_t 
 constexpr uint32_t kIdxBits = 14, kIdxMask = (1u << kIdxBits) - 1u;
 
 // Optional step profile (PE_CHAIN_PROF): thread 0 accumulates shader clocks
-// per step into A.prof[0..7]; marks follow the block barriers.
+// per step into A.prof[phase * 8 + step] (phases 0..3, the last one
+// accumulating the rest); marks follow the block barriers. Step 0 of phase 0
+// includes the kernel's start and the overlay initialisation.
 #define PE_PROF_MARK(k)                                                   \
     do {                                                                  \
         if (A.prof && tid == 0) {                                         \
             const uint64_t now_ = __builtin_readcyclecounter();           \
-            A.prof[(k)] += now_ - prof_t;                                 \
+            A.prof[prof_ph * 8 + (k)] += now_ - prof_t;                   \
             prof_t = now_;                                                \
         }                                                                 \
     } while (0)
@@ -1282,11 +1316,20 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     uint16_t* nx = nb + ((n + 2 + 1) & ~1u);   // [n + 2]: next Select start per option, then Select id per option
 
     uint64_t prof_t = A.prof ? __builtin_readcyclecounter() : 0;
+    int prof_ph = 0;   // profile slot group: phase (capped at 3)
     for (uint32_t e = blockIdx.x; e < n_evals; e += gridDim.x) {
         const uint32_t* __restrict__ perm = A.perms + (size_t)e * A.perm_stride;
         for (uint32_t i = tid; i < H; i += kChainBlock) {
             ov.keys[i] = kEmpty;
             if (ov.k) ov.k[i] = 0;
+        }
+        for (uint32_t i = tid; i < kChainMaxN / 32; i += kChainBlock) {
+            sh.bm1[i] = 0;
+            sh.bm2[i] = 0;
+        }
+        if (tid == 0) {
+            sh.slow = 0;
+            sh.n_emit = 0;
         }
         uint32_t cur = wrap_pos(A.offsets ? A.offsets[e] : A.offset0, n);
         uint32_t placed = 0;
@@ -1298,7 +1341,8 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
         __syncthreads();
         while (!done) {
             PE_PROF_MARK(0);
-            // 1. values of the window [cur, cur + n): base, or queued for re-evaluation
+            // 1. values of the window [cur, cur + n): base (no placement of this
+            //    launch on the row), base1 (one), or queued for re-evaluation
             uint32_t row[kChainItems];
             double v[kChainItems];
             if (tid == 0) sh.n_redo = 0;
@@ -1307,23 +1351,45 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                 row[q] = j < n ? perm[wrap_pos(cur + j, n)] : 0u;
             }
-#pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
-                const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                v[q] = j < n ? A.base[row[q]] : -__builtin_inf();
-            }
-            __syncthreads();
-            uint32_t redo_mask = 0;
+            // rows holding placements of this launch: one (base1) from the
+            // position bitmaps, two or more re-evaluated (ov_count)
+            uint32_t one_mask = 0, redo_mask = 0;
+            const bool use_bm = placed && sh.slow == 0;
             if (placed) {
 #pragma unroll
                 for (int q = 0; q < kChainItems; q++) {
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                    const uint32_t dk = j < n ? ov_count(ov, row[q]) : 0u;
-                    if (dk) {
+                    if (j < n) {
+                        uint32_t b1 = 1, b2 = 1;
+                        if (use_bm) {
+                            const uint32_t p = wrap_pos(cur + j, n), bit = 1u << (p & 31);
+                            b1 = sh.bm1[p >> 5] & bit;
+                            b2 = sh.bm2[p >> 5] & bit;
+                        }
+                        if (b1 && b2) {
+                            const uint32_t dk = ov_count(ov, row[q]);
+                            if (dk == 1u && A.base1) one_mask |= 1u << q;
+                            else if (dk) redo_mask |= 1u << q;
+                        } else if (b1) {
+                            if (A.base1) one_mask |= 1u << q;
+                            else redo_mask |= 1u << q;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++) {
+                const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                const double* src = ((one_mask >> q) & 1u) ? A.base1 : A.base;
+                v[q] = j < n ? src[A.base_by_pos ? wrap_pos(cur + j, n) : row[q]] : -__builtin_inf();
+            }
+            if (__syncthreads_or(redo_mask != 0)) {
+#pragma unroll
+                for (int q = 0; q < kChainItems; q++) {
+                    if ((redo_mask >> q) & 1u) {
                         const uint32_t slot = atomicAdd(&sh.n_redo, 1u);
-                        sh.redo[slot] = make_uint2(row[q], dk);
+                        sh.redo[slot] = make_uint2(row[q], ov_count(ov, row[q]));
                         v[q] = gm::u2f((unsigned long long)slot);   // slot index until the value is back
-                        redo_mask |= 1u << q;
                     }
                 }
                 __syncthreads();
@@ -1459,15 +1525,14 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     cnt++;
                     i = x;
                 }
-                sh.seg_tab[g][o] = (uint16_t)cnt;
-                sh.seg_exit[g][o] = (uint16_t)ex;
+                sh.seg_tab[g][o] = cnt | (ex << 16);
             }
             __syncthreads();
             if (tid == 0) {
                 const uint32_t want = min(A.count - placed, (uint32_t)kChainMaxSel);
                 uint32_t total = 0, o = 0, used = 0;
                 for (uint32_t g = 0; g < n_seg; g++) {
-                    const uint32_t cnt = sh.seg_tab[g][o], ex = sh.seg_exit[g][o];
+                    const uint32_t te = sh.seg_tab[g][o], cnt = te & 0xFFFFu, ex = te >> 16;
                     sh.seg_entry[g] = (uint16_t)o;
                     sh.seg_base[g] = (uint16_t)total;
                     used = g + 1;
@@ -1569,6 +1634,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     const uint32_t s = pk[q] >> kIdxBits;
                     if (sh.sel_arg[s] == (pk[q] & kIdxMask)) {
                         sh.sel_row[s] = row[q];
+                        sh.sel_pos[s] = (uint16_t)(q * kChainBlock + tid);
                         sh.sel_max[s] = (unsigned long long)gm::f2u(v[q]);
                     }
                 }
@@ -1583,9 +1649,20 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     const int win_row = (int)sh.sel_row[s];
                     const double score = gm::u2f(sh.sel_max[s]);
                     const uint32_t it = placed + s;
-                    if (A.full_out)
+                    const uint32_t next_off = wrap_pos(cur + sh.sel_end[s] + 1u, n);
+                    if (A.emit) {
+                        ChainEmit& m = A.emit[it];
+                        m.row = win_row;
+                        m.dk = ov_count(ov, (uint32_t)win_row);
+                        m.consumed = consumed;
+                        m.filtered = sh.sel_f[s];
+                        m.exhausted = sh.sel_x[s];
+                        m.new_offset = next_off;
+                        m.score = score;
+                    } else if (A.full_out) {
                         emit_placement(A, A.tg.class_ok, ov, nullptr, e, it, win_row, score, consumed, sh.sel_f[s],
-                                       sh.sel_x[s], wrap_pos(cur + sh.sel_end[s] + 1u, n));
+                                       sh.sel_x[s], next_off);
+                    }
                     if (A.out) {
                         pe_placement& o = A.out[(size_t)e * A.count + it];
                         o.row = win_row;
@@ -1593,9 +1670,15 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                         o.final_score = score;
                     }
                 }
-                __syncthreads();   // emit_placement reads the overlay before the commits
-                if (A.commit)
-                    for (uint32_t s = tid; s < nsel; s += kChainBlock) ov_add_atomic(ov, sh.sel_row[s]);
+                __syncthreads();   // the records read the overlay before the commits
+                if (A.commit) {
+                    for (uint32_t s = tid; s < nsel; s += kChainBlock) {
+                        ov_add_atomic(ov, sh.sel_row[s]);
+                        const uint32_t p = wrap_pos(cur + sh.sel_pos[s], n), bit = 1u << (p & 31);
+                        if (atomicOr(&sh.bm1[p >> 5], bit) & bit) atomicOr(&sh.bm2[p >> 5], bit);
+                    }
+                }
+                if (tid == 0) sh.n_emit = placed + nsel;
                 placed += nsel;
                 cur = wrap_pos(cur + sh.sel_end[nsel - 1] + 1u, n);
                 done = mode == kPhaseCount;
@@ -1611,9 +1694,21 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     const uint32_t take = min(a, L > r ? L - r : 0u);
                     for (uint32_t k = 0; k < take; k++)
                         if (sh.aside_v[k] > best) { best = sh.aside_v[k]; win_row = (int)sh.aside_row[k]; }
-                    if (A.full_out)
+                    if (A.emit) {
+                        ChainEmit& m = A.emit[placed];
+                        m.row = win_row;
+                        m.dk = win_row >= 0 ? ov_count(ov, (uint32_t)win_row) : 0u;
+                        m.consumed = n;
+                        m.filtered = sh.sel_f[0];
+                        m.exhausted = sh.sel_x[0];
+                        m.new_offset = cur;
+                        m.score = best;
+                    } else if (A.full_out) {
                         emit_placement(A, A.tg.class_ok, ov, nullptr, e, placed, win_row, best, n, sh.sel_f[0],
                                        sh.sel_x[0], cur);
+                    }
+                    sh.n_emit = placed + 1;
+                    sh.slow = 1;   // the winner's position is not tracked: later phases probe the overlay
                     if (A.out) {
                         pe_placement& o = A.out[(size_t)e * A.count + placed];
                         o.row = win_row;
@@ -1629,14 +1724,101 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 if (placed >= A.count) done = true;
             }
             __syncthreads();
+            PE_PROF_MARK(6);
+            prof_ph = prof_ph < 3 ? prof_ph + 1 : 3;
         }
         if (tid == 0) {
             A.eval_status[2 * e] = placed;
             A.eval_status[2 * e + 1] = cur;
         }
-        PE_PROF_MARK(6);
-        if (A.writeback) writeback_overlay<kChainBlock, false>(A, ov, H, nullptr);
+        if (A.emit) {
+            // records and the HBM writeback are k_emit's: dump the overlay
+            if (tid == 0) sh.n_ov = 0;
+            __syncthreads();
+            for (uint32_t h = tid; h < H; h += kChainBlock) {
+                const uint32_t key = ov.keys[h];
+                if (key == kEmpty) continue;
+                const uint32_t r = ov.k ? key : key >> ov.kshift;
+                const uint32_t kk = ov.k ? ov.k[h] : key & ov.kmask;
+                A.emit_ov[atomicAdd(&sh.n_ov, 1u)] = make_uint2(r, kk);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                A.emit_n[0] = sh.n_emit;
+                A.emit_n[1] = A.writeback ? sh.n_ov : 0u;
+            }
+        } else if (A.writeback) {
+            writeback_overlay<kChainBlock, false>(A, ov, H, nullptr);
+        }
         __syncthreads();
+    }
+}
+
+// Records of a single-evaluation k_chain launch (A.emit): the full Select
+// result of every entry, evaluated on the state the launch started from (the
+// entry's dk = placements on the row before it), then, by the last workgroup
+// to finish, the launch's placements written back to the HBM SoA.
+__global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
+    __shared__ uint32_t last;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < A.emit_n[0]) {
+        const ChainEmit m = A.emit[i];
+        pe_ranked_node& o = A.full_out[i];
+        o.row = m.row;
+        o.nodes_evaluated = m.consumed;
+        o.nodes_filtered = m.filtered;
+        o.nodes_exhausted = m.exhausted;
+        o.new_offset = m.new_offset;
+        o.final_score = 0.0;
+        o.n_scores = 0;
+        o.n_preempted = 0;
+        o.n_device_offers = 0;
+        double parts[PE_MAX_SCORES];
+        uint32_t nsc = 0;
+        for (int q = 0; q < PE_MAX_SCORES; q++) parts[q] = 0.0;
+        if (m.row >= 0) {
+            const uint32_t row = (uint32_t)m.row;
+            NodeIn in;
+            load_node(A.soa, A.tg, row, in);
+            NodeEval ev;
+            ev.score = 0.0;
+            eval_loaded<true>(A.soa, A.tg, A.tg.class_ok, A.ask, m.dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+            o.final_score = ev.score;
+            nsc = ev.nscores;
+            for (int q = 0; q < PE_MAX_SCORES; q++) if (q < (int)ev.nscores) parts[q] = ev.parts[q];
+            record_offers(A.soa, A.ask, A.tg, row, m.dk, &o);
+        }
+        o.n_scores = nsc;
+        for (int q = 0; q < PE_MAX_SCORES; q++) o.scores[q] = parts[q];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&A.emit_n[2], 1u) == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const uint32_t nov = A.emit_n[1];
+    for (uint32_t x = threadIdx.x; x < nov; x += 256) {
+        const uint2 e = A.emit_ov[x];
+        NodeRec& r = A.soa.rec[e.x];
+        r.used_cpu += (int64_t)e.y * A.ask.cpu;
+        r.used_mem += (int64_t)e.y * A.ask.mem;
+        r.used_disk += (int64_t)e.y * A.ask.disk;
+        r.used_mbits += (int32_t)e.y * A.ask.commit_mbits;
+        r.used_dyn += (int32_t)e.y * A.ask.commit_dyn;
+        A.soa.coll_job[e.x] += e.y;
+        A.tg.coll_tg[e.x] += e.y;
+        if (A.ask.n_dev > 0) A.tg.dev_free[e.x] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[e.x], e.y);
+    }
+    if (threadIdx.x == 0) A.emit_n[2] = 0;   // the ticket of the next launch
+    if (A.done_flag) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(A.done_flag, A.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -1744,27 +1926,30 @@ __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t of
     commit_row(s, t, a, row, offers);
 }
 
-// Replay of a speculative loop's confirmed placements after a rollback to its
-// checkpoint (pe_commit / pe_select, engine.cpp): one thread per placement,
-// every update an integer atomic add, so repeated rows sum exactly as the
-// sequential commit_row calls would. Each offer was assigned on the state that
-// already held every earlier placement, so no free count underflows and the
-// packed u8 subtractions never borrow.
+// Replay (sign +1) of a speculative loop's confirmed placements after a
+// rollback to its checkpoint, or removal (sign -1) of its unconfirmed ones
+// (pe_commit / pe_select, engine.cpp): one thread per placement, every update
+// an integer atomic add, so repeated rows sum exactly as the sequential
+// commit_row calls would. Each offer was assigned on the state that already
+// held every earlier placement, so no free count underflows and the packed u8
+// subtractions never borrow. Removal is only used without device asks.
 __global__ void __launch_bounds__(256) k_apply_commits(NodeSoA s, TgTables t, Ask a, const uint32_t* rows,
-                                                      const uint32_t* offers, uint32_t n) {
+                                                      const uint32_t* offers, uint32_t n, int sign) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint32_t row = rows[i];
     NodeRec& r = s.rec[row];
-    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_cpu), (unsigned long long)a.cpu);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_mem), (unsigned long long)a.mem);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_disk), (unsigned long long)a.disk);
-    atomicAdd(reinterpret_cast<unsigned int*>(&r.used_mbits), (unsigned int)a.commit_mbits);
-    atomicAdd(reinterpret_cast<unsigned int*>(&r.used_dyn), (unsigned int)a.commit_dyn);
-    atomicAdd(&s.coll_job[row], 1u);
-    atomicAdd(&t.coll_tg[row], 1u);
+    const unsigned long long s64 = (unsigned long long)(long long)sign;
+    const unsigned int s32 = (unsigned int)sign;
+    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_cpu), (unsigned long long)a.cpu * s64);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_mem), (unsigned long long)a.mem * s64);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&r.used_disk), (unsigned long long)a.disk * s64);
+    atomicAdd(reinterpret_cast<unsigned int*>(&r.used_mbits), (unsigned int)a.commit_mbits * s32);
+    atomicAdd(reinterpret_cast<unsigned int*>(&r.used_dyn), (unsigned int)a.commit_dyn * s32);
+    atomicAdd(&s.coll_job[row], s32);
+    atomicAdd(&t.coll_tg[row], s32);
     const uint32_t c = r.cls;
-    if (a.n_dev > 0) {
+    if (a.n_dev > 0 && sign > 0) {
         const uint32_t o = offers[i];
         uint32_t sub = 0;
         for (int q = 0; q < kMaxDevReq && q < a.n_dev; q++) sub += (uint32_t)a.dev_cnt[q] << (8 * ((o >> (8 * q)) & 255u));
@@ -1772,7 +1957,7 @@ __global__ void __launch_bounds__(256) k_apply_commits(NodeSoA s, TgTables t, As
     }
     for (int p = 0; p < t.n_psets; p++) {
         const uint32_t v = pset_value(t, p, row, c);
-        if (v != kMissing) atomicAdd(&t.pset_counts[p][v], 1u);
+        if (v != kMissing) atomicAdd(&t.pset_counts[p][v], s32);
     }
 }
 
@@ -2122,6 +2307,20 @@ __global__ void __launch_bounds__(256) k_sweep_loop(SweepArgs A, uint32_t count,
 
 // node_feas[row] = class_ok[cls] && node_ok[row]: one verdict byte per node so
 // the count loop issues a single dependent round trip per node.
+// ResetPlan in one launch: the proposed state back to the snapshot (node
+// records, device free counts), no plan preemptions.
+__global__ void __launch_bounds__(256) k_reset_plan(NodeRec* rec, const NodeRec* base_rec, uint32_t* dev_free,
+                                                   const uint32_t* dev_free_base, uint32_t n, uint8_t* preempted,
+                                                   uint32_t m, uint32_t* pcount, uint32_t keys) {
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        rec[i] = base_rec[i];
+        dev_free[i] = dev_free_base[i];
+    }
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < m; i += stride) preempted[i] = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < keys; i += stride) pcount[i] = 0;
+}
+
 __global__ void __launch_bounds__(256) k_fold_feas(NodeSoA s, const uint8_t* class_ok, const uint8_t* node_ok,
                                                    uint8_t* feas) {
     for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < s.n; row += gridDim.x * blockDim.x) {
@@ -2193,7 +2392,8 @@ int pe_chain_blocks_per_cu(size_t lds) {
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st) {
     if (!a->base || a->n_visit > pe::kChainMaxN || a->class_ok_stride || a->limit > pe::kMaxChainLimit)
         return hipErrorInvalidValue;
-    uint32_t blocks = (a->soa.n + 255) / 256;
+    if (a->base_by_pos && n_evals != 1) return hipErrorInvalidValue;
+    uint32_t blocks = ((a->base_by_pos ? a->n_visit : a->soa.n) + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(pe::k_base, dim3(blocks), dim3(256), 0, st, *a);
@@ -2201,6 +2401,11 @@ hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t ma
     uint32_t grid = n_evals < max_blocks ? n_evals : max_blocks;
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL(pe::k_chain, dim3(grid), dim3(pe::kChainBlock), lds, st, *a, n_evals);
+    if (a->emit) {
+        if (n_evals != 1 || !a->full_out || !a->emit_ov || !a->emit_n) return hipErrorInvalidValue;
+        const uint32_t eb = (a->count + 255) / 256;
+        hipLaunchKernelGGL(pe::k_emit, dim3(eb ? eb : 1), dim3(256), 0, st, *a);
+    }
     return hipGetLastError();
 }
 
@@ -2219,9 +2424,9 @@ hipError_t pe_launch_commit(const pe::NodeSoA* s, const pe::TgTables* t, const p
 }
 
 hipError_t pe_launch_apply_commits(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
-                                   const uint32_t* offers, uint32_t n, hipStream_t st) {
+                                   const uint32_t* offers, uint32_t n, int sign, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(pe::k_apply_commits, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, offers, n);
+    hipLaunchKernelGGL(pe::k_apply_commits, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, offers, n, sign);
     return hipGetLastError();
 }
 
@@ -2275,6 +2480,19 @@ hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted
 hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
                                     uint32_t* pcount, uint32_t* dev_free, hipStream_t st) {
     hipLaunchKernelGGL(pe::k_commit_preempt, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount, dev_free);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_reset_plan(pe::NodeRec* rec, const pe::NodeRec* base_rec, uint32_t* dev_free,
+                                const uint32_t* dev_free_base, uint32_t n, uint8_t* preempted, uint32_t m,
+                                uint32_t* pcount, uint32_t keys, hipStream_t st) {
+    uint32_t w = n > m ? n : m;
+    w = w > keys ? w : keys;
+    uint32_t blocks = (w + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_reset_plan, dim3(blocks), dim3(256), 0, st, rec, base_rec, dev_free, dev_free_base, n,
+                       preempted, m, pcount, keys);
     return hipGetLastError();
 }
 

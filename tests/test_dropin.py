@@ -172,3 +172,28 @@ def test_speculation_off_matches_on():
     off, _, eng = both(nodes, allocs, job, perm, env={"PE_SPECULATE": "0"}, count=400)
     assert eng.SpeculationStats()[0] == 0
     assert_equal_runs(on, off)
+
+
+def test_device_asks_deviation_restores_checkpoint():
+    # device asks: the speculative run checkpoints the dynamic columns; a
+    # deviating commit restores them and replays the confirmed offers
+    nodes, allocs = synth.cluster_c5(900, seed=6, busy=0.3)
+    job = synth.job_c5(80)
+    perm = synth.shuffle(900, 21)
+
+    def deviate(i, opt):
+        return int(opt.row) if i != 17 else int(perm[(i * 11) % len(perm)])
+    a, b, eng = both(nodes, allocs, job, perm, count=80, deviate=deviate)
+    assert_equal_runs(a, b)
+    assert eng.SpeculationStats()[2] >= 1
+
+
+def test_costly_paths_grow_run_length():
+    # a full-pass loop pays per placement: runs start at one placement and
+    # double while they get used up (1 + 2 + ... + 64 = 127 >= 100)
+    nodes, allocs = synth.cluster_c3(1500, seed=8)
+    job = synth.job_c3(100)
+    a, b, eng = both(nodes, allocs, job, synth.shuffle(1500, 3), env={"PE_LOOP_SWEEP_MIN": "256"}, count=100)
+    assert_equal_runs(a, b)
+    runs, served, rollbacks, recs = eng.SpeculationStats()
+    assert runs == 7 and rollbacks == 0, eng.SpeculationStats()

@@ -18,6 +18,18 @@
 
 extern "C" {
 
+// Wall time per phase over every dropin_evals call since the last reset:
+// reset_plan, set_job, set_nodes, the first Select of an evaluation, the rest
+// of the Select/Commit loop.
+static double g_phase[5];
+
+void dropin_phase_seconds(double* out5, int reset) {
+    for (int i = 0; i < 5; i++) {
+        out5[i] = g_phase[i];
+        if (reset) g_phase[i] = 0.0;
+    }
+}
+
 struct dropin_api {
     int (*reset_plan)(void*);
     int (*set_job)(void*, const pe_strtab*, const pe_job*);
@@ -40,9 +52,16 @@ int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, in
     uint32_t p = 0;
     uint64_t sel = 0;
     int rc = 0;
+    using clk = std::chrono::steady_clock;
+    auto t_first = clk::now();
     for (uint32_t i = 0; i < count; i++) {
         rc = api->select(h, tg, &none, &opt);
         sel++;
+        if (i == 0) {
+            const auto t = clk::now();
+            g_phase[3] += std::chrono::duration<double>(t - t_first).count();
+            t_first = t;
+        }
         if (rc) break;
         if (opt.row < 0 && preempt) {
             rc = api->select(h, tg, &pre, &opt);
@@ -56,6 +75,7 @@ int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, in
         if (rows) rows[p] = opt.row;
         p++;
     }
+    g_phase[4] += std::chrono::duration<double>(clk::now() - t_first).count();
     for (uint32_t i = p; rows && i < count; i++) rows[i] = -1;
     *placed = p;
     if (selects) *selects += sel;
@@ -75,13 +95,19 @@ int dropin_evals(const dropin_api* api, void* h, const pe_strtab* strs, const pe
     uint64_t placed_total = 0, evals = 0, selects = 0;
     int rc = 0;
     for (uint32_t e = 0; e < n_evals; e++) {
+        auto ta = clk::now();
         rc = api->reset_plan(h);
         if (rc) break;
+        auto tb = clk::now();
+        g_phase[0] += std::chrono::duration<double>(tb - ta).count();
         rc = api->set_job(h, strs, job);
         if (rc) break;
+        ta = clk::now();
+        g_phase[1] += std::chrono::duration<double>(ta - tb).count();
         uint32_t limit = 0;
         rc = api->set_nodes(h, orders + (size_t)(e % n_orders) * n, n, &limit);
         if (rc) break;
+        g_phase[2] += std::chrono::duration<double>(clk::now() - ta).count();
         uint32_t p = 0;
         rc = dropin_place(api, h, tg, count, preempt, rows_last, &p, &selects);
         if (rc) break;

@@ -28,6 +28,8 @@ def load():
         if not os.path.exists(LIB):
             subprocess.check_call(["make", "-s", "-C", HERE])
         lib = C.CDLL(LIB)
+        lib.dropin_phase_seconds.restype = None
+        lib.dropin_phase_seconds.argtypes = [C.POINTER(C.c_double), C.c_int]
         lib.dropin_evals.restype = C.c_int
         lib.dropin_evals.argtypes = [C.POINTER(dropin_api), C.c_void_p, C.POINTER(abi.pe_strtab),
                                      C.POINTER(abi.pe_job), abi.u32p, C.c_uint32, C.c_uint32, C.c_uint32,
@@ -45,22 +47,43 @@ def _api(stack):
     return a
 
 
-def run(stack, job, orders, count, tg=0, preempt=False, n_evals=None, max_seconds=0.0):
-    """Sequential evaluations of `job` through the C loop. orders: (k, n) visit
-    orders, evaluation e uses orders[e % k]. Returns (placements, evals,
-    selects, seconds, rows of the last evaluation)."""
+def prepare(stack, job):
+    """Encode `job` for `stack` once (what a cgo shim does when the job comes
+    in) and return run(orders, count, tg=0, preempt=False, n_evals=None,
+    max_seconds=0.0): sequential evaluations through the C loop. orders: (k, n)
+    visit orders, evaluation e uses orders[e % k]. run returns (placements,
+    evals, selects, seconds, rows of the last evaluation)."""
     lib = load()
-    o = np.ascontiguousarray(np.atleast_2d(np.asarray(orders, dtype=np.uint32)))
     enc = EncodedJob(job, stack.state.interner)
     tab = enc.strtab()
     api = _api(stack)
-    rows = np.full(max(1, count), -1, dtype=np.int32)
     out = (C.c_uint64 * 3)()
     secs = C.c_double(0.0)
-    ne = o.shape[0] if n_evals is None else n_evals
-    rc = lib.dropin_evals(C.byref(api), stack._h, C.byref(tab), C.byref(enc.job), o.ctypes.data_as(abi.u32p),
-                          o.shape[0], o.shape[1], tg, count, int(preempt), ne, max_seconds,
-                          rows.ctypes.data_as(abi.i32p), out, C.byref(secs))
-    stack._check(rc)
-    stack._job = job
-    return int(out[0]), int(out[1]), int(out[2]), secs.value, rows[:count]
+
+    def run(orders, count, tg=0, preempt=False, n_evals=None, max_seconds=0.0):
+        o = np.ascontiguousarray(np.atleast_2d(np.asarray(orders, dtype=np.uint32)))
+        rows = np.full(max(1, count), -1, dtype=np.int32)
+        ne = o.shape[0] if n_evals is None else n_evals
+        rc = lib.dropin_evals(C.byref(api), stack._h, C.byref(tab), C.byref(enc.job), o.ctypes.data_as(abi.u32p),
+                              o.shape[0], o.shape[1], tg, count, int(preempt), ne, max_seconds,
+                              rows.ctypes.data_as(abi.i32p), out, C.byref(secs))
+        stack._check(rc)
+        stack._job = job
+        return int(out[0]), int(out[1]), int(out[2]), secs.value, rows[:count]
+    run.keep = (enc, tab, api)   # the C structs point into these
+    return run
+
+
+def run(stack, job, orders, count, tg=0, preempt=False, n_evals=None, max_seconds=0.0):
+    """Sequential evaluations of `job` through the C loop (see prepare)."""
+    return prepare(stack, job)(orders, count, tg=tg, preempt=preempt, n_evals=n_evals, max_seconds=max_seconds)
+
+
+PHASES = ("reset_plan", "set_job", "set_nodes", "first_select", "loop")
+
+
+def phase_seconds(reset=True):
+    """Wall seconds per caller phase summed over dropin_evals calls."""
+    out = (C.c_double * 5)()
+    load().dropin_phase_seconds(out, int(reset))
+    return dict(zip(PHASES, list(out)))
