@@ -36,6 +36,7 @@
 size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
+hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
 hipError_t pe_launch_reset_plan(pe::NodeRec* rec, const pe::NodeRec* base_rec, uint32_t* dev_free,
                                 const uint32_t* dev_free_base, uint32_t n, uint8_t* preempted, uint32_t m,
                                 uint32_t* pcount, uint32_t keys, hipStream_t st);
@@ -354,6 +355,7 @@ struct pe_stack {
     PinnedMem h_batch_out, h_batch_status;
     PinnedMem h_place_out, h_place_status;   // single-evaluation count loop results (mapped)
     PinnedMem h_stage;                 // upload staging ring (upload_s)
+    unsigned char* stage_dev = nullptr;   // the ring as seen from the device (k_upload reads it)
     DevMem d_emit, d_emit_ov, d_emit_n;   // k_chain deferred records (k_emit)
     size_t stage_off = 0;
     double phase_ms[4] = {0, 0, 0, 0};   // host prep, kernels, result copy, total (last batch)
@@ -429,6 +431,10 @@ struct pe_stack {
 
     std::unordered_map<uint32_t, std::vector<uint32_t>> job_allocs;   // job -> non-terminal alloc indices
 
+    // PE_API_PROF=1: wall time per named host step, printed at pe_stack_destroy
+    bool api_prof = false;
+    std::map<std::string, std::pair<double, uint64_t>> api_acc;
+
     // ---- helpers --------------------------------------------------------
     int fail(int code, const std::string& m) { err = m; return code; }
     const std::vector<uint32_t>& own_allocs() const {
@@ -465,6 +471,25 @@ struct pe_stack {
 };
 
 namespace {
+
+double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Accumulates the enclosing scope's wall time under `name` (PE_API_PROF).
+struct ApiScope {
+    pe_stack* s;
+    const char* name;
+    double t0;
+    ApiScope(pe_stack* st, const char* n) : s(st), name(n), t0(st && st->api_prof ? now_us() : 0.0) {}
+    ~ApiScope() {
+        if (s && s->api_prof) {
+            auto& a = s->api_acc[name];
+            a.first += now_us() - t0;
+            a.second++;
+        }
+    }
+};
 
 #define HIP_TRY(s, expr)                                                                \
     do {                                                                                \
@@ -503,6 +528,8 @@ hipError_t upload_s(pe_stack* s, DevMem& m, const std::vector<T>& h) {
     unsigned char* dst = s->h_stage.as<unsigned char>() + off;
     std::memcpy(dst, h.data(), b);
     s->stage_off = off + b;
+    if (!s->stage_dev) s->stage_dev = s->h_stage.dev<unsigned char>();
+    if (s->stage_dev) return pe_launch_upload(m.p, s->stage_dev + off, b, s->stream);
     return hipMemcpyAsync(m.p, dst, b, hipMemcpyHostToDevice, s->stream);
 }
 
@@ -1510,6 +1537,7 @@ pe::TgTables tables_of(TgPlan& g) {
 }
 
 int prepare_tg(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& order, uint32_t start) {
+    ApiScope prof_(s, "prepare_tg");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     if (!s->have_job) return s->fail(PE_ESTATE, "pe_set_job not called");
     if (tgi >= s->tgs.size()) return s->fail(PE_EINVAL, "task group index out of range");
@@ -1960,10 +1988,6 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
 // One evaluation on the stack's plan (pe_select / pe_place): the fused count
 // loop in launches of at most H/2 placements, each merging its overlay back
 // into the HBM SoA so the plan persists.
-double now_us() {
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::vector<uint32_t>& order,
               uint32_t offset, const pe_select_options* opts, pe_ranked_node* out, uint32_t* placed,
               uint32_t* new_offset) {
@@ -1978,7 +2002,10 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     const uint32_t n = (uint32_t)order.size();
     const bool full = full_scan_kernel(s, g, n);
     pe::BatchArgs A = batch_args(s, g);
-    HIP_TRY(s, upload_visit(s, order));
+    {
+        ApiScope prof_up_(s, "run_place.upload_visit");
+        HIP_TRY(s, upload_visit(s, order));
+    }
     A.perms = s->d_visit.as<uint32_t>();
     A.n_visit = n;
     if (opts && opts->penalty_count > 0) {
@@ -2068,10 +2095,14 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         } else {
             HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
         }
-        if (chain) HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream));
-        else HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
-        HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+        {
+            ApiScope prof_l_(s, "run_place.launch");
+            if (chain) HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream));
+            else HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
+            HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+        }
         const double t1 = hprof ? now_us() : 0.0;
+        ApiScope prof_w_(s, "run_place.wait+copy");
         if (spin) {
             const double t_spin = now_us();
             while (*flag != A.done_seq && now_us() - t_spin < 2000.0) __builtin_ia32_pause();
@@ -2177,11 +2208,17 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     if (const char* e = std::getenv("PE_WINDOW_LAZY")) s->use_base = std::atoi(e) == 0;
     if (const char* e = std::getenv("PE_SPECULATE")) s->spec_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_SPIN_WAIT")) s->spin_wait = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PE_API_PROF")) s->api_prof = std::atoi(e) != 0;
     return s;
 }
 
 void pe_stack_destroy(pe_stack* s) {
     if (!s) return;
+    if (s->api_prof)
+        for (auto& kv : s->api_acc)
+            std::fprintf(stderr, "api %-28s %10.1f us total %8llu calls %8.2f us/call\n", kv.first.c_str(),
+                         kv.second.first, (unsigned long long)kv.second.second,
+                         kv.second.first / std::max<uint64_t>(kv.second.second, 1));
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     s->tgs.clear();
@@ -2280,11 +2317,13 @@ int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* a
 
 int pe_reset_plan(pe_stack* s) {
     if (!s) return PE_EINVAL;
+    ApiScope prof_(s, "reset_plan");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     const size_t n = s->nodes.size();
+    ApiScope prof_launch_(s, "reset_plan.launch");
     HIP_TRY(s, pe_launch_reset_plan(s->d_rec.as<pe::NodeRec>(), s->d_base_rec.as<pe::NodeRec>(),
                                     s->d_dev_free.as<uint32_t>(), s->d_dev_free_base.as<uint32_t>(), (uint32_t)n,
                                     s->d_preempted.as<uint8_t>(), (uint32_t)s->h_preempted.size(),
@@ -2307,6 +2346,7 @@ int pe_reset_plan(pe_stack* s) {
 
 int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     if (!s || !j) return PE_EINVAL;
+    ApiScope prof_(s, "set_job");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
@@ -2432,6 +2472,7 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
                 if (nd.n_device_nets > 1) { g->unsupported = "task network asks on multi-device nodes"; break; }
     }
     s->have_job = true;
+    ApiScope prof_own_(s, "set_job.own+collisions");
     {   // the job's own state allocs per node (ProposedAllocs minus plan placements)
         std::vector<uint32_t> own(s->nodes.size(), 0);
         for (uint32_t i : s->own_allocs()) own[s->allocs[i].row]++;
@@ -2447,6 +2488,7 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
 
 int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
     if (!s) return PE_EINVAL;
+    ApiScope prof_(s, "set_nodes");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     if (!rows && n) return s->fail(PE_EINVAL, "null rows");
     // validate before touching any state: a rejected list leaves the previous one in place
@@ -3272,6 +3314,7 @@ static void spec_drop(pe_stack* s) {
 }
 
 static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
+    ApiScope prof_(s, "spec_start");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     int rc = prepare_tg(s, tgi, s->visit, s->offset);

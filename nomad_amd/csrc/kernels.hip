@@ -2307,6 +2307,17 @@ __global__ void __launch_bounds__(256) k_sweep_loop(SweepArgs A, uint32_t count,
 
 // node_feas[row] = class_ok[cls] && node_ok[row]: one verdict byte per node so
 // the count loop issues a single dependent round trip per node.
+// Host -> device upload as a kernel: the source is page-locked mapped host
+// memory read directly over the bus (a DMA copy costs more setup per call than
+// the whole transfer of these small per-evaluation arrays).
+__global__ void __launch_bounds__(256) k_upload(unsigned char* dst, const unsigned char* src, size_t bytes) {
+    const size_t n16 = bytes / 16;
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (size_t i = n16 * 16 + (size_t)blockIdx.x * 256 + threadIdx.x; i < bytes; i += stride) dst[i] = src[i];
+}
+
 // ResetPlan in one launch: the proposed state back to the snapshot (node
 // records, device free counts), no plan preemptions.
 __global__ void __launch_bounds__(256) k_reset_plan(NodeRec* rec, const NodeRec* base_rec, uint32_t* dev_free,
@@ -2480,6 +2491,17 @@ hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted
 hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
                                     uint32_t* pcount, uint32_t* dev_free, hipStream_t st) {
     hipLaunchKernelGGL(pe::k_commit_preempt, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount, dev_free);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st) {
+    if (!bytes) return hipSuccess;
+    if (((uintptr_t)dst | (uintptr_t)src_mapped) & 15) return hipErrorInvalidValue;
+    size_t blocks = (bytes / 16 + 255) / 256;
+    if (blocks > 256) blocks = 256;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_upload, dim3((uint32_t)blocks), dim3(256), 0, st, static_cast<unsigned char*>(dst),
+                       static_cast<const unsigned char*>(src_mapped), bytes);
     return hipGetLastError();
 }
 

@@ -27,7 +27,10 @@ def main():
     nodes, allocs = synth.cluster_c2(n, seed=42)
     job = synth.job_c2(count)
     orders = np.stack([synth.shuffle(n, 1000 + e) for e in range(32)])
+    if os.environ.get("PROBE_NO_SPIN"):
+        os.environ["PE_SPIN_WAIT"] = "0"
     st = GenericStack()
+    os.environ.pop("PE_SPIN_WAIT", None)
     st.SetState(nodes, allocs)
     run = dropin.prepare(st, job)
     run(orders, count, n_evals=5)
@@ -60,6 +63,19 @@ def main():
     timed("pe_set_nodes", lambda: lib.pe_set_nodes(h, rows.ctypes.data_as(C.POINTER(C.c_uint32)), len(rows),
                                                    C.byref(lim)))
     timed("pe_abi_version (ctypes floor)", lambda: lib.pe_abi_version())
+
+    def spin_us(us):
+        t = time.perf_counter()
+        while (time.perf_counter() - t) * 1e6 < us:
+            pass
+    for gap in (20, 100, 200, 1000):
+        tot = 0.0
+        for _ in range(100):
+            spin_us(gap)
+            t = time.perf_counter()
+            lib.pe_reset_plan(h)
+            tot += time.perf_counter() - t
+        print("  pe_reset_plan after %4d us idle  %7.1f us" % (gap, tot / 100 * 1e6))
     st.close()
     os.environ["PE_CHAIN_PROF"] = "1"
     os.environ["PE_PLACE_PROF"] = "1"
