@@ -1760,10 +1760,16 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
 // to finish, the launch's placements written back to the HBM SoA.
 __global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
     __shared__ uint32_t last;
+    // records are built in LDS and stored to the (host-mapped) output as one
+    // contiguous run per workgroup: 8-byte coalesced stores instead of every
+    // lane writing its own 184-byte record field by field over the bus
+    __shared__ pe_ranked_node recs[256];
+    static_assert(sizeof(pe_ranked_node) % 8 == 0, "record copy granule");
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i < A.emit_n[0]) {
+    const uint32_t n_emit = A.emit_n[0];
+    if (i < n_emit) {
         const ChainEmit m = A.emit[i];
-        pe_ranked_node& o = A.full_out[i];
+        pe_ranked_node& o = recs[threadIdx.x];
         o.row = m.row;
         o.nodes_evaluated = m.consumed;
         o.nodes_filtered = m.filtered;
@@ -1773,9 +1779,9 @@ __global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
         o.n_scores = 0;
         o.n_preempted = 0;
         o.n_device_offers = 0;
-        double parts[PE_MAX_SCORES];
-        uint32_t nsc = 0;
-        for (int q = 0; q < PE_MAX_SCORES; q++) parts[q] = 0.0;
+        for (int q = 0; q < PE_MAX_SCORES; q++) o.scores[q] = 0.0;
+        for (int q = 0; q < PE_MAX_PREEMPT; q++) o.preempted[q] = 0;
+        for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o.device_offer_group[q] = 0;
         if (m.row >= 0) {
             const uint32_t row = (uint32_t)m.row;
             NodeIn in;
@@ -1784,12 +1790,19 @@ __global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
             ev.score = 0.0;
             eval_loaded<true>(A.soa, A.tg, A.tg.class_ok, A.ask, m.dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
             o.final_score = ev.score;
-            nsc = ev.nscores;
-            for (int q = 0; q < PE_MAX_SCORES; q++) if (q < (int)ev.nscores) parts[q] = ev.parts[q];
+            o.n_scores = ev.nscores;
+            for (int q = 0; q < PE_MAX_SCORES; q++) if (q < (int)ev.nscores) o.scores[q] = ev.parts[q];
             record_offers(A.soa, A.ask, A.tg, row, m.dk, &o);
         }
-        o.n_scores = nsc;
-        for (int q = 0; q < PE_MAX_SCORES; q++) o.scores[q] = parts[q];
+    }
+    __syncthreads();
+    {
+        const uint32_t first = blockIdx.x * 256;
+        const uint32_t cnt = n_emit > first ? min(256u, n_emit - first) : 0u;
+        constexpr uint32_t W = sizeof(pe_ranked_node) / 8;
+        const uint2* src = reinterpret_cast<const uint2*>(recs);
+        uint2* dst = reinterpret_cast<uint2*>(A.full_out + first);
+        for (uint32_t w = threadIdx.x; w < cnt * W; w += 256) dst[w] = src[w];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
