@@ -294,6 +294,20 @@ int pe_speculation_stats(const pe_stack* s, uint64_t* out4);
  * rows, as returned in pe_ranked_node.preempted by a Select with Preempt. */
 int pe_commit_preempt(pe_stack* s, uint32_t tg_index, int32_t row, const uint32_t* preempted,
                       uint32_t n_preempted);
+/* Plan.AppendStoppedAlloc (structs.go:10628-10660) of `n` snapshot allocs
+ * (alloc-table rows): each becomes a NodeUpdate entry of its node, and a
+ * non-terminal one leaves the proposed state of the node
+ * (EvalContext.ProposedAllocs, context.go:120-157: resources, devices, the
+ * job's collision counts; the property sets count it as cleared,
+ * propertyset.go:159-209). The stops of computeJobAllocs
+ * (generic_sched.go:382), of a destructive update's previous alloc (:546), of
+ * inplaceUpdate / genericAllocUpdateFn (util.go:749, 1037) and of the
+ * SystemScheduler (scheduler_system.go:230-241). Undone by pe_reset_plan. */
+int pe_plan_stop(pe_stack* s, const uint32_t* allocs, uint32_t n);
+/* Plan.PopUpdate (structs.go:10691-10702): drops the last NodeUpdate entry of
+ * the alloc's node when it is this alloc (generic_sched.go:644, util.go:756,
+ * 1043); otherwise nothing happens. */
+int pe_plan_pop_update(pe_stack* s, uint32_t alloc);
 /* Fused count loop of GenericScheduler.computePlacements (generic_sched.go:493-649)
  * for `count` fresh placements of one task group (no preferred / penalty nodes):
  * Select -> AppendAlloc repeated on the device; stops at the first nil option

@@ -183,6 +183,8 @@ def _sigs(prefix, handle):
                                       C.POINTER(pe_ranked_node)]),
         (prefix + "commit", C.c_int, [H, C.c_uint32, C.c_int32]),
         (prefix + "commit_preempt", C.c_int, [H, C.c_uint32, C.c_int32, u32p, C.c_uint32]),
+        (prefix + "plan_stop", C.c_int, [H, u32p, C.c_uint32]),
+        (prefix + "plan_pop_update", C.c_int, [H, C.c_uint32]),
         (prefix + "place", C.c_int, [H, C.c_uint32, C.c_uint32, C.POINTER(pe_ranked_node), u32p]),
         (prefix + "system_place", C.c_int, [H, C.c_uint32, f64p, u8p, u32p]),
     ]
@@ -194,6 +196,7 @@ ENGINE_SYMBOLS = [
     "pe_last_kernel_ms", "pe_stage_orders", "pe_place_batch", "pe_batch_results", "pe_last_phase_ms",
     "pe_check_constraint", "pe_last_sweep_bytes", "pe_select_shard", "pe_select_merge",
     "pe_set_metrics", "pe_last_metrics", "pe_update_allocs", "pe_speculation_stats",
+    "pe_plan_stop", "pe_plan_pop_update",
 ]
 
 

@@ -37,6 +37,9 @@ size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
+hipError_t pe_launch_plan_stop(pe::NodeRec* rec, uint32_t* dev_free, const pe::PreemptAlloc* allocs,
+                               uint8_t* preempted, const uint32_t* slots, const uint32_t* rows, uint32_t n, int sign,
+                               hipStream_t st);
 hipError_t pe_launch_reset_plan(pe::NodeRec* rec, const pe::NodeRec* base_rec, uint32_t* dev_free,
                                 const uint32_t* dev_free_base, uint32_t n, uint8_t* preempted, uint32_t m,
                                 uint32_t* pcount, uint32_t keys, hipStream_t st);
@@ -259,6 +262,7 @@ struct TgPlan {
     bool has_aff_table = false, node_aff_used = false, node_ok_used = false, alias_used = false;
     std::vector<std::unique_ptr<PsetDev>> psets;
     bool psets_built = false;
+    bool psets_dynamic = false;        // plan stops clear values: counts rebuilt on the host after every commit
     int n_spread = 0;                  // psets[0, n_spread) are spreads, the rest distinct_property
     std::vector<ParsedConstraint> distinct_props;   // tg + task distinct_property constraints
     // device requests (tasks in order) and the per-class match table
@@ -430,6 +434,12 @@ struct pe_stack {
     double log10 = 0;
 
     std::unordered_map<uint32_t, std::vector<uint32_t>> job_allocs;   // job -> non-terminal alloc indices
+    // Plan.NodeUpdate (pe_plan_stop): per node the stopped snapshot allocs in
+    // append order, and per alloc its number of entries
+    std::map<uint32_t, std::vector<uint32_t>> node_update;
+    std::vector<uint32_t> stop_count;
+    DevMem d_stop_slots, d_stop_rows;
+    bool stopped(uint32_t ai) const { return ai < stop_count.size() && stop_count[ai] > 0; }
 
     // PE_API_PROF=1: wall time per named host step, printed at pe_stack_destroy
     bool api_prof = false;
@@ -1191,16 +1201,55 @@ int build_collisions(pe_stack* s) {
         job[row]++;
         for (size_t g = 0; g < s->tgs.size(); g++) if (s->tgs[g]->name == tgname) tg[g][row]++;
     };
-    for (uint32_t i : s->own_allocs()) add(s->allocs[i].row, s->allocs[i].tg);
+    for (uint32_t i : s->own_allocs())
+        if (!s->stopped(i)) add(s->allocs[i].row, s->allocs[i].tg);   // ProposedAllocs drops plan stops
     for (auto& p : s->plan) add(p.second, p.first);
     HIP_TRY(s, upload_s(s, s->d_coll_job, job));
     for (size_t g = 0; g < s->tgs.size(); g++) HIP_TRY(s, upload_s(s, s->tgs[g]->coll_tg, tg[g]));
     return PE_OK;
 }
 
+// The job's own proposed state allocs per node (ProposedAllocs minus plan
+// placements and plan stops) and the collision counts.
+int build_job_counts(pe_stack* s) {
+    std::vector<uint32_t> own(s->nodes.size(), 0);
+    for (uint32_t i : s->own_allocs())
+        if (!s->stopped(i)) own[s->allocs[i].row]++;
+    HIP_TRY(s, upload_s(s, s->d_own_existing, own));
+    return build_collisions(s);
+}
+
+// propertySet cleared values (propertyset.go:159-209): the plan's stopped allocs
+// of the job (terminal ones included, filterAllocs(stopping, false)), less one
+// for every value the proposed allocs also use when more than one is cleared.
+// `node_val` maps a row to the set's value index; `tg_filter` limits to a group.
+template <class F>
+std::vector<uint32_t> cleared_counts(pe_stack* s, size_t nvals, F node_val, bool job_level, uint32_t tg_name) {
+    std::vector<uint32_t> cleared(nvals, 0);
+    bool any = false;
+    for (auto& kv : s->node_update)
+        for (uint32_t ai : kv.second) {
+            const HostAlloc& a = s->allocs[ai];
+            if (a.job != s->job_id || a.ns != s->job_ns || (!job_level && a.tg != tg_name)) continue;
+            const uint32_t v = node_val(a.row);
+            if (v != pe::kMissing) { cleared[v]++; any = true; }
+        }
+    if (!any) return {};
+    std::vector<uint8_t> prop(nvals, 0);
+    for (auto& p : s->plan)
+        if (job_level || p.first == tg_name) {
+            const uint32_t v = node_val(p.second);
+            if (v != pe::kMissing) prop[v] = 1;
+        }
+    for (size_t v = 0; v < nvals; v++)
+        if (prop[v] && cleared[v] > 1) cleared[v]--;
+    return cleared;
+}
+
 // Spread property sets for a task group (spread.go:76-104, propertyset.go).
 int build_psets(pe_stack* s, TgPlan& g) {
     g.psets.clear();
+    g.psets_dynamic = false;
     std::vector<const SpreadSpec*> specs;
     for (auto& sp : s->job_spreads) specs.push_back(&sp);
     for (auto& sp : g.spreads) specs.push_back(&sp);
@@ -1254,6 +1303,13 @@ int build_psets(pe_stack* s, TgPlan& g) {
                 uint32_t v = node_val(p.second);
                 if (v != pe::kMissing) ps->h_counts[v]++;
             }
+        {   // GetCombinedUseMap: existing + proposed - cleared, not below 0
+            const auto cl = cleared_counts(s, ps->value_str.size(), node_val, false, g.name);
+            for (size_t v = 0; v < cl.size(); v++) {
+                ps->h_counts[v] = ps->h_counts[v] >= cl[v] ? ps->h_counts[v] - cl[v] : 0u;
+                if (cl[v]) g.psets_dynamic = true;
+            }
+        }
         if (ps->value_str.size() > (size_t)pe::kMaxValues) { g.unsupported = "spread attribute with > 256 values"; return PE_OK; }
         const SpreadSpec* si = info[sp->attribute];
         const double total = (double)g.count;
@@ -1350,6 +1406,13 @@ int build_psets(pe_stack* s, TgPlan& g) {
                 const uint32_t v = node_val(p.second);
                 if (v != pe::kMissing) ps->h_counts[v]++;
             }
+        {
+            const auto cl = cleared_counts(s, ps->value_str.size(), node_val, job_level, g.name);
+            for (size_t v = 0; v < cl.size(); v++) {
+                ps->h_counts[v] = ps->h_counts[v] >= cl[v] ? ps->h_counts[v] - cl[v] : 0u;
+                if (cl[v]) g.psets_dynamic = true;
+            }
+        }
         HIP_TRY(s, upload_s(s, ps->val_class, by_class));
         if (ps->per_node) HIP_TRY(s, upload_s(s, ps->val_node, by_node));
         std::vector<uint32_t> cnt = ps->h_counts;
@@ -2256,6 +2319,8 @@ int pe_check_constraint(const char* op, const char* l, int ls, const char* r, in
 int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
     if (!s || !strs || !nodes) return PE_EINVAL;
     spec_drop(s);
+    s->node_update.clear();   // a new evaluation context: no plan stops
+    s->stop_count.clear();
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     s->strs.clear();
@@ -2284,6 +2349,8 @@ int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* a
     if (!s || !allocs) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
+    s->node_update.clear();   // a new evaluation context: no plan stops
+    s->stop_count.clear();
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     s->add_strings(strs);
@@ -2320,6 +2387,8 @@ int pe_reset_plan(pe_stack* s) {
     ApiScope prof_(s, "reset_plan");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
+    s->node_update.clear();   // a new evaluation context: no plan stops
+    s->stop_count.clear();
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
     const size_t n = s->nodes.size();
@@ -2329,6 +2398,8 @@ int pe_reset_plan(pe_stack* s) {
                                     s->d_preempted.as<uint8_t>(), (uint32_t)s->h_preempted.size(),
                                     s->d_pcount.as<uint32_t>(), std::max<uint32_t>(s->n_jtg_keys, 1), s->stream));
     std::fill(s->h_preempted.begin(), s->h_preempted.end(), 0);
+    s->node_update.clear();
+    s->stop_count.assign(s->allocs.size(), 0);
     s->offer_row = -1;   // stream-ordered: later launches and uploads see the reset state
     s->plan.clear();
     s->tg_memo.clear();
@@ -2473,17 +2544,12 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     }
     s->have_job = true;
     ApiScope prof_own_(s, "set_job.own+collisions");
-    {   // the job's own state allocs per node (ProposedAllocs minus plan placements)
-        std::vector<uint32_t> own(s->nodes.size(), 0);
-        for (uint32_t i : s->own_allocs()) own[s->allocs[i].row]++;
-        HIP_TRY(s, upload_s(s, s->d_own_existing, own));
+    {
         auto it = s->job_keys.find(std::make_pair(s->job_id, s->job_ns));
         s->job_key = it == s->job_keys.end() ? PE_NONE : it->second;
     }
     s->offer_row = -1;
-    int rc = build_collisions(s);
-    if (rc) return rc;
-    return PE_OK;
+    return build_job_counts(s);
 }
 
 int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
@@ -2886,6 +2952,7 @@ static int commit_impl(pe_stack* s, uint32_t tgi, int32_t row) {
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     s->plan.emplace_back(g.name, (uint32_t)row);
     invalidate_job_distinct(s, tgi);
+    if (g.psets_dynamic) g.psets_built = false;   // cleared values: GetCombinedUseMap is not additive
     // the coll_tg of other task groups with the same name also see this alloc
     for (size_t k = 0; k < s->tgs.size(); k++)
         if (k != tgi && s->tgs[k]->name == g.name) {
@@ -3074,6 +3141,36 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
     if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;
     const bool retry = retry_preempt && s->cfg.preempt;
     uint32_t p = 0, no = s->offset;
+    if (g.psets_dynamic) {
+        // plan stops clear property values: one Select at a time, the counts
+        // rebuilt on the host after every commit
+        while (p < count) {
+            rc = select_impl(s, tgi, nullptr, &out[p]);
+            if (rc) return rc;
+            if (out[p].row < 0) {
+                if (!retry) break;
+                pe_select_options o;   // selectNextOption: retry with Preempt=true
+                std::memset(&o, 0, sizeof(o));
+                o.preempt = 1;
+                rc = select_impl(s, tgi, &o, &out[p]);
+                if (rc) return rc;
+                if (out[p].row < 0) break;
+                s->offer_row = out[p].row;
+                s->offers = pack_offers(&out[p]);
+                rc = commit_preempt_impl(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
+                if (rc) return rc;
+                p++;
+                continue;
+            }
+            s->offer_row = out[p].row;
+            s->offers = pack_offers(&out[p]);
+            rc = commit_impl(s, tgi, out[p].row);
+            if (rc) return rc;
+            p++;
+        }
+        if (placed) *placed = p;
+        return PE_OK;
+    }
     // Sparse options (a saturated cluster): a windowed Select would walk
     // ~limit * n / options positions with one wave. Then every Select
     // evaluates the list in parallel and resolves the window on the device.
@@ -3320,6 +3417,7 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     int rc = prepare_tg(s, tgi, s->visit, s->offset);
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
+    if (g.psets_dynamic) return select_impl(s, tgi, nullptr, out);   // counts rebuilt per commit: no run
     pe_stack::Spec& sp = s->spec;
     // placements of the group still to come in this evaluation (tg.Count minus
     // the plan's), at least the run length grown from earlier used-up runs
@@ -3396,6 +3494,71 @@ int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* pr
     int rc = spec_flush(s);
     if (rc) return rc;
     return commit_preempt_impl(s, tgi, row, preempted, n_preempted);
+}
+
+// Plan.NodeUpdate bookkeeping shared by pe_plan_stop / pe_plan_pop_update:
+// allocs whose entry count crossed 0 <-> 1 leave / rejoin the proposed state.
+static int apply_stop_delta(pe_stack* s, const std::vector<uint32_t>& allocs, int sign) {
+    std::vector<uint32_t> slots, rows;
+    for (uint32_t ai : allocs) {
+        const HostAlloc& a = s->allocs[ai];
+        const uint32_t slot = s->alloc_slot[ai];
+        if (a.terminal || slot == PE_NONE) continue;   // not in AllocsByNodeTerminal(false)
+        uint8_t& f = s->h_preempted[slot];
+        if (sign > 0 ? f != 0 : f != 2) continue;        // already out via a plan preemption
+        f = sign > 0 ? 2 : 0;
+        slots.push_back(slot);
+        rows.push_back(a.row);
+    }
+    if (!slots.empty()) {
+        HIP_TRY(s, upload_s(s, s->d_stop_slots, slots));
+        HIP_TRY(s, upload_s(s, s->d_stop_rows, rows));
+        HIP_TRY(s, pe_launch_plan_stop(s->d_rec.as<pe::NodeRec>(), s->dev_packable ? s->d_dev_free.as<uint32_t>() : nullptr,
+                                       s->d_palloc.as<pe::PreemptAlloc>(), s->d_preempted.as<uint8_t>(),
+                                       s->d_stop_slots.as<uint32_t>(), s->d_stop_rows.as<uint32_t>(),
+                                       (uint32_t)slots.size(), sign, s->stream));
+    }
+    // the job's own allocs feed the collision counts and the property sets
+    for (auto& g : s->tgs) g->psets_built = false;
+    if (s->have_job) return build_job_counts(s);
+    return PE_OK;
+}
+
+int pe_plan_stop(pe_stack* s, const uint32_t* allocs, uint32_t n) {
+    if (!s || (!allocs && n)) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    for (uint32_t i = 0; i < n; i++)
+        if (allocs[i] >= s->allocs.size()) return s->fail(PE_EINVAL, "alloc index out of range");
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    s->gen++;
+    HIP_TRY(s, hipSetDevice(s->device));
+    if (s->stop_count.size() != s->allocs.size()) s->stop_count.assign(s->allocs.size(), 0);
+    std::vector<uint32_t> fresh;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t ai = allocs[i];
+        s->node_update[s->allocs[ai].row].push_back(ai);   // AppendStoppedAlloc: NodeUpdate[node] += alloc
+        if (s->stop_count[ai]++ == 0) fresh.push_back(ai);
+    }
+    return apply_stop_delta(s, fresh, +1);
+}
+
+int pe_plan_pop_update(pe_stack* s, uint32_t alloc) {
+    if (!s) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    if (alloc >= s->allocs.size()) return s->fail(PE_EINVAL, "alloc index out of range");
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    auto it = s->node_update.find(s->allocs[alloc].row);
+    // PopUpdate (structs.go:10691-10702): only the node's last entry, by ID
+    if (it == s->node_update.end() || it->second.empty() || it->second.back() != alloc) return PE_OK;
+    s->gen++;
+    HIP_TRY(s, hipSetDevice(s->device));
+    it->second.pop_back();
+    if (it->second.empty()) s->node_update.erase(it);
+    std::vector<uint32_t> gone;
+    if (--s->stop_count[alloc] == 0) gone.push_back(alloc);
+    return apply_stop_delta(s, gone, -1);
 }
 
 int pe_speculation_stats(const pe_stack* s, uint64_t* out4) {

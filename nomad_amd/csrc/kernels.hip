@@ -2518,6 +2518,15 @@ hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hip
     return hipGetLastError();
 }
 
+hipError_t pe_launch_plan_stop(pe::NodeRec* rec, uint32_t* dev_free, const pe::PreemptAlloc* allocs,
+                               uint8_t* preempted, const uint32_t* slots, const uint32_t* rows, uint32_t n, int sign,
+                               hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_plan_stop, dim3((n + 63) / 64), dim3(64), 0, st, rec, dev_free, allocs, preempted, slots,
+                       rows, n, sign);
+    return hipGetLastError();
+}
+
 hipError_t pe_launch_reset_plan(pe::NodeRec* rec, const pe::NodeRec* base_rec, uint32_t* dev_free,
                                 const uint32_t* dev_free_base, uint32_t n, uint8_t* preempted, uint32_t m,
                                 uint32_t* pcount, uint32_t keys, hipStream_t st) {

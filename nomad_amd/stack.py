@@ -296,6 +296,15 @@ class _Stack:
         else:
             self._check(self._fn("commit")(self._h, self._tg_index(tg), int(row)))
 
+    def StopAllocs(self, allocs: Sequence[int]):
+        """Plan.AppendStoppedAlloc of snapshot allocs (alloc-table rows)."""
+        a = np.ascontiguousarray(np.asarray(list(allocs) or [0], dtype=np.uint32))
+        self._check(self._fn("plan_stop")(self._h, a.ctypes.data_as(abi.u32p), len(allocs)))
+
+    def PopUpdate(self, alloc: int):
+        """Plan.PopUpdate of a snapshot alloc (alloc-table row)."""
+        self._check(self._fn("plan_pop_update")(self._h, int(alloc)))
+
     def Place(self, tg, count: int) -> List[RankedNode]:
         out = (abi.pe_ranked_node * max(1, count))()
         placed = C.c_uint32(0)

@@ -2033,6 +2033,28 @@ int oracle_commit_preempt(oracle_stack* s, uint32_t tgi, int32_t row, const uint
     return oracle_commit(s, tgi, row);
 }
 
+// Plan.AppendStoppedAlloc (structs.go:10628-10660): NodeUpdate[node] += alloc
+int oracle_plan_stop(oracle_stack* s, const uint32_t* allocs, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++)
+        if (allocs[i] >= s->state.allocs.size()) { s->err = "alloc index out of range"; return PE_EINVAL; }
+    for (uint32_t i = 0; i < n; i++) {
+        const OAlloc& a = s->state.allocs[allocs[i]];
+        s->ctx.plan.node_update[a.node_row].push_back(a);
+    }
+    return PE_OK;
+}
+
+// Plan.PopUpdate (structs.go:10691-10702): the node's last entry, when it is this alloc
+int oracle_plan_pop_update(oracle_stack* s, uint32_t alloc) {
+    if (alloc >= s->state.allocs.size()) { s->err = "alloc index out of range"; return PE_EINVAL; }
+    const OAlloc& a = s->state.allocs[alloc];
+    auto it = s->ctx.plan.node_update.find(a.node_row);
+    if (it == s->ctx.plan.node_update.end() || it->second.empty() || it->second.back().id != a.id) return PE_OK;
+    it->second.pop_back();
+    if (it->second.empty()) s->ctx.plan.node_update.erase(it);
+    return PE_OK;
+}
+
 int oracle_place(oracle_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
     uint32_t p = 0;
     for (uint32_t i = 0; i < count; i++) {
