@@ -37,6 +37,8 @@ size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
+hipError_t pe_launch_evict_trace(const pe::PreemptArgs* a, const uint32_t* rows, uint32_t n, uint32_t* code,
+                                 double* named, hipStream_t st);
 hipError_t pe_launch_plan_stop(pe::NodeRec* rec, uint32_t* dev_free, const pe::PreemptAlloc* allocs,
                                uint8_t* preempted, const uint32_t* slots, const uint32_t* rows, uint32_t n, int sign,
                                hipStream_t st);
@@ -324,7 +326,7 @@ struct pe_stack {
     uint32_t n_jtg_keys = 0;
     std::string preempt_unsupported;           // snapshot outside the on-device limits
     DevMem d_node_alloc_off, d_palloc, d_preempted, d_pcount, d_own_existing;
-    DevMem d_ev_status, d_ev_score, d_ev_flags, d_ev_out, d_ev_mask, d_ev_rows, d_ev_masks, d_ev_offers;
+    DevMem d_ev_status, d_ev_score, d_ev_flags, d_ev_out, d_ev_mask, d_ev_rows, d_ev_masks, d_ev_offers, d_ev_named, d_ev_tcodes;
     uint32_t job_key = PE_NONE;
     // device offers of the last Select's pick (committed as chosen)
     int32_t offer_row = -1;
@@ -2672,7 +2674,7 @@ struct ScoreHeap {
 };
 
 static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
-                           uint32_t evaluated, const pe_select_options* opts) {
+                           uint32_t evaluated, const pe_select_options* opts, bool evict = false) {
     s->metrics_valid = false;
     const size_t m = order.size();
     std::map<std::string, int> cf, kf, ce, de;
@@ -2750,12 +2752,66 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         std::vector<double> sc(rows.size() * 6);
         HIP_TRY(s, hipMemcpyAsync(codes.data(), s->d_trace_out.p, codes.size() * 4, hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipMemcpyAsync(sc.data(), s->d_trace_scores.p, sc.size() * 8, hipMemcpyDeviceToHost, s->stream));
+        // Select with Preempt: BinPack with evict per row (rank.go:480-503) and
+        // the ScoreNode values of the options, preemption score included
+        std::vector<uint32_t> ecodes;
+        std::vector<double> named;
+        if (evict) {
+            pe::PreemptArgs P = preempt_args(s, g);
+            P.penalty_bits = pbits;
+            P.spread_tab = stab;
+            if (!stab && !g.psets.empty()) {
+                HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
+                HIP_TRY(s, pe_launch_spread_table(&P.tg, s->d_spread_tab.as<double>(), s->stream));
+                P.spread_tab = s->d_spread_tab.as<double>();
+            }
+            HIP_TRY(s, s->d_ev_tcodes.ensure(rows.size() * sizeof(uint32_t)));
+            HIP_TRY(s, s->d_ev_named.ensure(rows.size() * 7 * sizeof(double)));
+            HIP_TRY(s, pe_launch_evict_trace(&P, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
+                                             s->d_ev_tcodes.as<uint32_t>(), s->d_ev_named.as<double>(), s->stream));
+            ecodes.resize(rows.size());
+            named.resize(rows.size() * 7);
+            HIP_TRY(s, hipMemcpyAsync(ecodes.data(), s->d_ev_tcodes.p, ecodes.size() * 4, hipMemcpyDeviceToHost,
+                                      s->stream));
+            HIP_TRY(s, hipMemcpyAsync(named.data(), s->d_ev_named.p, named.size() * 8, hipMemcpyDeviceToHost,
+                                      s->stream));
+        }
         HIP_TRY(s, hipStreamSynchronize(s->stream));
         const bool has_aff = !g.affinities.empty();
         const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
         std::map<int, std::vector<uint32_t>> counts;   // distinct_property use counts, read on demand
         for (size_t i = 0; i < rows.size(); i++) {
             const uint32_t row = rows[i], code = codes[i];
+            const uint32_t base = code & 255u;
+            if (evict && base != pe::kTrDistinctHosts && base != pe::kTrDistinctProp) {
+                const uint32_t ec = ecodes[i], st = ec & 255u;
+                if (ec >> 24) return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or "
+                                                              "exceeds the on-device alloc limits");
+                if (st == 0) {   // option (kOption), preempting or not
+                    const double* o = &named[i * 7];
+                    const uint32_t fl = (ec >> 16) & 255u;
+                    ScoreMeta sm;
+                    sm.row = row;
+                    sm.scores.emplace_back("binpack", o[0]);
+                    if (a.dev_tw != 0.0) sm.scores.emplace_back("devices", o[1]);
+                    if (generic) {
+                        if (a.anti_aff) sm.scores.emplace_back("job-anti-affinity", o[2]);
+                        sm.scores.emplace_back("node-reschedule-penalty", (fl & 1u) ? -1.0 : 0.0);
+                        if (!has_aff) sm.scores.emplace_back("node-affinity", 0.0);
+                        else if (o[3] != 0.0) sm.scores.emplace_back("node-affinity", o[3]);
+                        if (o[4] != 0.0) sm.scores.emplace_back("allocation-spread", o[4]);
+                        if (fl & 2u) sm.scores.emplace_back("preemption", o[5]);
+                    }
+                    sm.norm = o[6];
+                    heap.push(std::move(sm));
+                } else if (st == 2) {   // kExhausted: no preemption frees enough (ExhaustedNode(dim))
+                    const uint32_t d = (ec >> 8) & 255u;
+                    exhaust(row, d == pe::kTrCpu ? "cpu" : (d == pe::kTrMemory ? "memory" : "disk"));
+                } else if (st != 3) {   // kSkipped (device preemption failed) records nothing
+                    return s->fail(PE_EHIP, "k_evict_trace: outcome differs from the host walk");
+                }
+                continue;
+            }
             switch (code & 255u) {
                 case pe::kTrOption: {   // ScoreNode calls in chain order, then the NormScore push
                     const double* o = &sc[i * 6];
@@ -2872,8 +2928,8 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         if (s->cfg.preempt) rc = run_evict_select(s, *s->tgs[tgi], s->visit, 0, nullptr, out, &no);
         else rc = run_place(s, tgi, 1, 0, s->visit, 0, nullptr, out, &placed, &no);
         s->limit = saved;
-        if (rc == PE_OK && !s->cfg.preempt && s->metrics_on)
-            rc = compute_metrics(s, *s->tgs[tgi], s->visit, 0, out->nodes_evaluated, nullptr);
+        if (rc == PE_OK && s->metrics_on)
+            rc = compute_metrics(s, *s->tgs[tgi], s->visit, 0, out->nodes_evaluated, nullptr, s->cfg.preempt != 0);
         return rc;
     }
     if (opts && opts->preferred_count > 0) {
@@ -2895,8 +2951,8 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         if (rc) return rc;
         // the inner Select over the preferred list has its own AllocMetric
         // (ctx.Reset per Select); its walk also advances the memo shadow
-        if (!opts->preempt && s->metrics_on) {
-            rc = compute_metrics(s, g, pref, 0, out->nodes_evaluated, &o2);
+        if (s->metrics_on) {
+            rc = compute_metrics(s, g, pref, 0, out->nodes_evaluated, &o2, opts->preempt != 0);
             if (rc) return rc;
         }
         s->offset = 0;
@@ -2910,10 +2966,12 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;   // never reset until SetNodes (stack.go:165-167)
     if (opts && opts->preempt) {
         uint32_t no;
+        const uint32_t start0 = s->offset;
         rc = run_evict_select(s, g, s->visit, s->offset, opts, out, &no);
         if (rc) return rc;
         s->offset = no;
-        return PE_OK;
+        if (s->metrics_on) rc = compute_metrics(s, g, s->visit, start0, out->nodes_evaluated, opts, true);
+        return rc;
     }
     const uint32_t start = s->offset;
     if (s->limit >= s->visit.size() && s->visit.size() >= s->sweep_min && g.n_spread == (int)g.psets.size() &&

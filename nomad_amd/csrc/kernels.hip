@@ -2527,6 +2527,13 @@ hipError_t pe_launch_plan_stop(pe::NodeRec* rec, uint32_t* dev_free, const pe::P
     return hipGetLastError();
 }
 
+hipError_t pe_launch_evict_trace(const pe::PreemptArgs* a, const uint32_t* rows, uint32_t n, uint32_t* code,
+                                 double* named, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_evict_trace, dim3((n + 63) / 64), dim3(64), 0, st, *a, rows, n, code, named);
+    return hipGetLastError();
+}
+
 hipError_t pe_launch_reset_plan(pe::NodeRec* rec, const pe::NodeRec* base_rec, uint32_t* dev_free,
                                 const uint32_t* dev_free_base, uint32_t n, uint8_t* preempted, uint32_t m,
                                 uint32_t* pcount, uint32_t keys, hipStream_t st) {

@@ -228,3 +228,64 @@ def test_metrics_system_stack():
             eng.Commit(0, re.row)
             ora.Commit(0, ro.row)
     assert seen
+
+
+def _preempt_loop(nodes, allocs, job, perm, placements, config, system=False):
+    """computePlacements with selectNextOption's Preempt retry (generic_sched.go:
+    773-792): every Select's maps equal, the Preempt ones included (BinPack with
+    evict: ExhaustedNode when no preemption frees enough, rank.go:480-503;
+    ScoreNode("preemption"), rank.go:793-806)."""
+    from nomad_amd.stack import GenericStack, SelectOptions
+    sts = []
+    for cls in (GenericStack, OracleGenericStack):
+        st = cls(config=config)
+        st.EnableMetrics()
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(perm)
+        sts.append(st)
+    eng, ora = sts
+    seen = {"preemption": 0, "exhausted": set()}
+    for k in range(placements):
+        for opts in (None, SelectOptions(preempt=True)):
+            re, ro = eng.SelectRaw(0, opts), ora.SelectRaw(0, opts)
+            assert (re.row, re.nodes_evaluated, re.nodes_filtered, re.nodes_exhausted, re.preempted) == \
+                (ro.row, ro.nodes_evaluated, ro.nodes_filtered, ro.nodes_exhausted, ro.preempted), (k, opts)
+            me, mo = eng.LastMetrics(), ora.LastMetrics()
+            assert me == mo, (k, opts, me, mo)
+            seen["exhausted"] |= set(mo["DimensionExhausted"])
+            seen["preemption"] += sum(1 for x in mo["ScoreMetaData"] if "preemption" in x[2])
+            if ro.row >= 0:
+                break
+        if ro.row < 0:
+            break
+        eng.Commit(0, re.row, re.preempted)
+        ora.Commit(0, ro.row, ro.preempted)
+    return seen
+
+
+@pytest.mark.gpu
+def test_metrics_preempt_selects():
+    from nomad_amd.structs import SchedulerConfig
+    nodes, allocs = synth.cluster_c5(700, seed=21, busy=0.95)
+    job = synth.job_c5(120)
+    seen = _preempt_loop(nodes, allocs, job, synth.shuffle(len(nodes), 4), 120,
+                         SchedulerConfig(preempt_service=True))
+    assert seen["preemption"] > 0
+
+
+@pytest.mark.gpu
+def test_metrics_preempt_selects_cpu_memory():
+    # no devices: PreemptForTaskGroup frees cpu / memory; nodes where it cannot
+    # are ExhaustedNode(dim)
+    from nomad_amd.structs import Allocation, SchedulerConfig
+    nodes, allocs = synth.cluster_c2(500, seed=22)
+    for i, nd in enumerate(nodes):
+        allocs.append(Allocation(node_id=nd.id, job_id="low-%d" % (i % 5), task_group="tg",
+                                 cpu_shares=max(0, nd.cpu_shares - 100 - 600 - (i % 3) * 200), memory_mb=64,
+                                 disk_mb=10, priority=10 + (i % 4) * 10))
+    job = synth.job_c2(200)
+    job.priority = 70
+    seen = _preempt_loop(nodes, allocs, job, synth.shuffle(len(nodes), 5), 200,
+                         SchedulerConfig(preempt_service=True))
+    assert seen["preemption"] > 0
