@@ -37,6 +37,8 @@ size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
+hipError_t pe_launch_commit_rows(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
+                                 uint32_t n, hipStream_t st);
 hipError_t pe_launch_evict_trace(const pe::PreemptArgs* a, const uint32_t* rows, uint32_t n, uint32_t* code,
                                  double* named, hipStream_t st);
 hipError_t pe_launch_plan_stop(pe::NodeRec* rec, uint32_t* dev_free, const pe::PreemptAlloc* allocs,
@@ -242,6 +244,7 @@ struct PsetDev {
     bool distinct = false;         // distinct_property set (filter) instead of a spread (score)
     uint32_t allowed = 1;
     std::string target_text;       // LTarget of the distinct_property constraint (metrics reasons)
+    std::vector<uint32_t> h_val_class, h_val_node;   // value index per class / per node (host copies)
 };
 
 struct TgPlan {
@@ -1397,6 +1400,8 @@ int build_psets(pe_stack* s, TgPlan& g) {
         }
         if (ps->value_str.size() > (size_t)pe::kMaxValues) { g.unsupported = "distinct_property with > 256 values"; return PE_OK; }
         auto node_val = [&](uint32_t row) { return ps->per_node ? by_node[row] : by_class[s->nodes[row].cls]; };
+        ps->h_val_class = by_class;
+        ps->h_val_node = by_node;
         ps->h_counts.assign(ps->value_str.size(), 0);
         for (uint32_t ai : s->own_allocs())
             if (const HostAlloc& a = s->allocs[ai]; a.ns == s->job_ns && (job_level || a.tg == g.name)) {
@@ -2462,9 +2467,7 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     };
     s->job_spreads = conv_spreads(j->spread_off, j->spread_count);
     std::string job_unsupported;
-    for (auto& c : s->job_constraints)
-        if (c.op == "distinct_property" && !generic)
-            job_unsupported = "distinct_property on a system stack (placements couple through the value counts)";
+
     s->tgs.clear();
     for (uint32_t gi = 0; gi < j->tg_count; gi++) {
         const pe_task_group& t = j->task_groups[gi];
@@ -2478,10 +2481,7 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
         for (uint32_t k = 0; k < t.constraint_count; k++) {
             g->constraints.push_back(parse_constraint(s, j->constraints[t.constraint_off + k]));
             if (g->constraints.back().op == "distinct_hosts") g->ask.distinct_tg = 1;
-            if (g->constraints.back().op == "distinct_property") {
-                if (!generic) g->unsupported = "distinct_property on a system stack (placements couple through the value counts)";
-                g->distinct_props.push_back(g->constraints.back());
-            }
+            if (g->constraints.back().op == "distinct_property") g->distinct_props.push_back(g->constraints.back());
         }
         for (uint32_t k = 0; k < t.task_count; k++) {
             const pe_task& x = j->tasks[t.task_off + k];
@@ -3832,6 +3832,77 @@ void pe_last_phase_ms(const pe_stack* s, double* out4) {
     for (int i = 0; i < 4; i++) out4[i] = s->phase_ms[i];
 }
 
+// SystemScheduler placements of a task group with distinct_property sets
+// (scheduler_system.go:283-425; stack.go:252 DistinctPropertyIterator): the
+// nodes in list order, each passing when every set's combined use of its value
+// is below the allowed count, then the plain fit (decided by k_system) or, when
+// it is exhausted, BinPack with evict; every placement grows the counts.
+static int system_place_distinct(pe_stack* s, uint32_t tgi, TgPlan& g, double* out_score, uint8_t* out_status,
+                                 uint32_t* placed) {
+    std::vector<PsetDev*> ds;
+    std::vector<std::vector<uint32_t>> cnt;
+    for (size_t q = (size_t)g.n_spread; q < g.psets.size(); q++) {
+        ds.push_back(g.psets[q].get());
+        cnt.push_back(g.psets[q]->h_counts);
+    }
+    auto value = [&](const PsetDev* ps, uint32_t row) {
+        return ps->per_node ? ps->h_val_node[row] : ps->h_val_class[s->nodes[row].cls];
+    };
+    std::vector<uint32_t> accepted;
+    uint32_t p = 0;
+    const uint32_t saved = s->limit;
+    s->limit = 1;
+    int rc = PE_OK;
+    for (uint32_t i = 0; i < (uint32_t)s->visit.size() && rc == PE_OK; i++) {
+        const uint32_t row = s->visit[i];
+        if (out_status[i] == 1) continue;
+        bool ok = true;
+        for (size_t k = 0; k < ds.size() && ok; k++) {
+            const uint32_t v = value(ds[k], row);
+            ok = v != pe::kMissing && cnt[k][v] < ds[k]->allowed;
+        }
+        if (!ok) {
+            out_status[i] = 1;
+            out_score[i] = std::nan("");
+            continue;
+        }
+        if (out_status[i] != 0) {   // exhausted: BinPack with evict on this node alone
+            if (!s->cfg.preempt) continue;
+            pe_ranked_node r;
+            uint32_t no;
+            rc = run_evict_select(s, g, std::vector<uint32_t>{row}, 0, nullptr, &r, &no);
+            if (rc || r.row < 0) continue;
+            s->offer_row = r.row;
+            s->offers = pack_offers(&r);
+            rc = commit_preempt_impl(s, tgi, r.row, r.preempted, r.n_preempted);
+            if (rc) continue;
+            out_status[i] = 0;
+            out_score[i] = r.final_score;
+        } else {
+            accepted.push_back(row);
+        }
+        for (size_t k = 0; k < ds.size(); k++) cnt[k][value(ds[k], row)]++;
+        p++;
+    }
+    s->limit = saved;
+    if (rc) return rc;
+    if (!accepted.empty()) {
+        HIP_TRY(s, upload_s(s, s->d_commit_rows, accepted));
+        pe::NodeSoA soa = soa_of(s);
+        pe::TgTables t = tables_of(g);
+        pe::Ask a = ask_for(s, g);
+        HIP_TRY(s, pe_launch_commit_rows(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(), (uint32_t)accepted.size(),
+                                         s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        for (uint32_t r : accepted) s->plan.emplace_back(g.name, r);
+    }
+    for (auto& q : g.psets) q->h_counts.clear();   // stale: the next Select rebuilds the sets
+    g.psets_built = false;
+    invalidate_job_distinct(s, tgi);
+    *placed = p;
+    return PE_OK;
+}
+
 int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     if (!s || !out_score || !out_status) return PE_EINVAL;
     {
@@ -3871,6 +3942,12 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     A.out_score = d_score.as<double>();
     A.out_status = d_st.as<uint8_t>();
     A.placed = s->d_status.as<uint32_t>();
+    // distinct_property couples the nodes through the value counts: the kernel
+    // evaluates every node without it and without committing, the host then
+    // walks the list in order (DistinctPropertyIterator before BinPack)
+    const bool distinct = g.psets.size() > (size_t)g.n_spread;
+    A.commit = distinct ? 0 : 1;
+    if (distinct) A.tg.n_psets = A.tg.n_spread;
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     HIP_TRY(s, pe_launch_system(&A, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
@@ -3883,6 +3960,12 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
     s->last_ms_pending = false;
+    if (distinct) {
+        rc = system_place_distinct(s, tgi, g, out_score, out_status, &p);
+        if (rc) return rc;
+        if (placed) *placed = p;
+        return PE_OK;
+    }
     for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) s->plan.emplace_back(g.name, s->visit[i]);
     if (s->cfg.preempt) {
         // BinPack with evict (stack.go:267-278) on the nodes the plain fit exhausted

@@ -252,6 +252,7 @@ struct SystemArgs {
     double* out_score;            // [n_list]
     uint8_t* out_status;          // [n_list] 0 placed 1 filtered 2 exhausted
     uint32_t* placed;             // [1] atomic counter
+    int commit;                   // Plan.AppendAlloc of the options in the kernel (0: the caller commits)
 };
 
 }  // namespace pe

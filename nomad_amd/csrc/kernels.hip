@@ -1848,6 +1848,8 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
         if (ev.status == kOption) {
             A.out_score[i] = ev.score;
             A.out_status[i] = 0;
+            local++;
+            if (!A.commit) continue;
             // Plan.AppendAlloc: rows are unique in the list, so no races
             NodeRec& r = A.soa.rec[row];
             r.used_cpu += A.ask.cpu;
@@ -1858,7 +1860,6 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
             A.soa.coll_job[row] += 1;
             A.tg.coll_tg[row] += 1;
             if (A.ask.n_dev > 0) A.tg.dev_free[row] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[row], 1);
-            local++;
         } else {
             A.out_score[i] = __builtin_nan("");
             A.out_status[i] = (uint8_t)ev.status;
@@ -1937,6 +1938,28 @@ __device__ __forceinline__ void commit_row(const NodeSoA& s, const TgTables& t, 
 __global__ void k_commit(NodeSoA s, TgTables t, Ask a, uint32_t row, uint32_t offers) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     commit_row(s, t, a, row, offers);
+}
+
+// Plan.AppendAlloc of distinct rows chosen on the host (SystemScheduler
+// placements resolved against distinct_property counts): commit_row per
+// thread, the shared property-set counts by atomics.
+__global__ void __launch_bounds__(256) k_commit_rows(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t row = rows[i];
+    NodeRec& r = s.rec[row];
+    r.used_cpu += a.cpu;
+    r.used_mem += a.mem;
+    r.used_disk += a.disk;
+    r.used_mbits += a.commit_mbits;
+    r.used_dyn += a.commit_dyn;
+    s.coll_job[row] += 1;
+    t.coll_tg[row] += 1;
+    if (a.n_dev > 0) t.dev_free[row] = dev_after(a, t.dev_cls[r.cls], t.dev_free[row], 1);
+    for (int p = 0; p < t.n_psets; p++) {
+        const uint32_t v = pset_value(t, p, row, r.cls);
+        if (v != kMissing) atomicAdd(&t.pset_counts[p][v], 1u);
+    }
 }
 
 // Replay (sign +1) of a speculative loop's confirmed placements after a
@@ -2531,6 +2554,13 @@ hipError_t pe_launch_evict_trace(const pe::PreemptArgs* a, const uint32_t* rows,
                                  double* named, hipStream_t st) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(pe::k_evict_trace, dim3((n + 63) / 64), dim3(64), 0, st, *a, rows, n, code, named);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_commit_rows(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
+                                 uint32_t n, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_commit_rows, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, n);
     return hipGetLastError();
 }
 
