@@ -19,6 +19,7 @@ runs its own evaluations on its own GPU (replicas, weak scaling).
 
 Beside the headline line's C2 numbers, the JSON carries one object per other
 BASELINE.json config (sections, --sections to choose):
+  c2_100k     the drop-in protocol on a 100k-node cluster (the metric's second size)
   c2_batch    4096 concurrent evaluations per launch sharing one k_base pass
   c2_workers  NumSchedulers-style worker threads, one engine handle each, each
               running the caller loop on its own evaluations
@@ -71,7 +72,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--sweep-nodes", type=int, default=1 << 24,
                    help="nodes of the scoring-sweep roofline measurement (0 = skip)")
-    p.add_argument("--sections", default="c2_batch,c2_workers,c3,c4,c5,c3_sharded,plan_apply,ingest",
+    p.add_argument("--sections", default="c2_100k,c2_batch,c2_workers,c3,c4,c5,c3_sharded,plan_apply,ingest",
                    help="comma list of extra config sections (empty = none)")
     return p.parse_args()
 
@@ -597,6 +598,45 @@ def section_c2_batch(device, nodes, allocs, job, count, evals, steps=10, warmup=
                          "node_evals_per_launch": evaluated}}
 
 
+def section_c2_100k(device, cpu_s, count=1000, n=100000, evals=20):
+    """The metric's 100k-node case: the C2 drop-in protocol (ResetPlan, SetJob,
+    SetNodes, count x (Select, Commit) from the C caller loop) on a 100k-node
+    cluster, limit 17 (stack.go:83-90)."""
+    from nomad_amd import synth
+    from nomad_amd.stack import GenericStack
+    from tools import dropin
+    nodes, allocs = synth.cluster_c2(n, seed=42)
+    job = synth.job_c2(count)
+    orders = np.stack([synth.shuffle(n, 5000 + e) for e in range(8)])
+    st = GenericStack(device=device)
+    st.SetState(nodes, allocs)
+    caller = dropin.prepare(st, job)
+    caller(orders, count, n_evals=2)
+    t0 = time.perf_counter()
+    placed, ne, _, _, _ = caller(orders, count, n_evals=evals)
+    wall = time.perf_counter() - t0
+    st.ResetPlan()
+    st.SetJob(job)
+    st.SetNodes(orders[0])
+    _, _, p1, recs = st.PlaceArrays(0, count)
+    kernel_ms = st.last_kernel_ms()
+    node_evals = float(recs["nodes_evaluated"][:p1].sum(dtype=np.uint64))
+    st.close()
+    out = {"workload": "C2 drop-in on %d nodes: count=%d binpack, limit 17, one evaluation per step" % (n, count),
+           "placements_per_s": placed / wall, "ms_per_eval": wall / ne * 1e3, "evals": ne,
+           "nodes_scored_per_s": node_evals * ne / wall, "kernel_ms": kernel_ms,
+           "node_evals_per_eval": node_evals}
+    if cpu_s > 0:
+        from oracle.oracle import OracleGenericStack
+        o = OracleGenericStack()
+        o.SetState(nodes, allocs)
+        op, oe, _, osecs, _ = dropin.run(o, job, orders, count, n_evals=1 << 30, max_seconds=cpu_s)
+        out["cpu_baseline"] = {"value": op / osecs, "unit": "placements/s", "cores": 1, "kind": "port",
+                               "sample": "%d evaluations x count=%d on the %d-node cluster through the same C caller "
+                                         "loop, 1 thread" % (oe, count, n)}
+    return out
+
+
 def section_c2_workers(device, nodes, allocs, job, count, workers, seconds=3.0):
     """NumSchedulers workers (nomad/config.go:468) on one GPU: each thread owns
     an engine handle (its own HIP stream) and runs the caller loop of
@@ -747,6 +787,9 @@ def main():
             elif sec == "c2_batch":
                 if rank == 0:
                     extra[sec] = section_c2_batch(local, nodes, allocs, job, args.count, args.evals)
+            elif sec == "c2_100k":
+                if rank == 0:
+                    extra[sec] = section_c2_100k(local, cpu_s)
             elif sec == "c2_workers":
                 if rank == 0:
                     extra[sec] = section_c2_workers(local, nodes, allocs, job, args.count, args.workers)

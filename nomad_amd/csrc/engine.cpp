@@ -487,6 +487,8 @@ struct pe_stack {
 
 namespace {
 
+constexpr uint32_t kStalledFlag = 0x80000000u;   // k_chain cursor flag (kChainStalled)
+
 double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -2090,7 +2092,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     A.hash_bits = hash_bits_for(count, full);
     A.packed_overlay = packed_kbits(s, 1u << A.hash_bits, full);
     bool chain = false;
-    if (!full && s->use_base && count > 1 && n <= pe_chain_max_n() && A.limit <= pe_chain_max_limit()) {
+    if (!full && s->use_base && count > 1 && A.limit <= pe_chain_max_limit()) {
         // count loop over one rotation at a time (k_base + k_chain): needs a
         // visit list without repeated rows
         chain = true;
@@ -2149,7 +2151,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     // word in the mapped status block: the host spins on it instead of waking
     // from a stream synchronisation; the launch's event timing is resolved
     // when it is asked for (pe_last_kernel_ms).
-    const bool spin = chain && s->spin_wait;
+    bool spin = chain && s->spin_wait;
     volatile uint32_t* flag = s->h_place_status.as<uint32_t>() + 3;
     if (spin) {
         A.done_flag = s->h_place_status.dev<uint32_t>() + 3;
@@ -2201,7 +2203,20 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             h_copy += t3 - t2;
         }
         *placed += st[0];
-        *new_offset = st[1];
+        *new_offset = st[1] & ~kStalledFlag;
+        if (chain && (st[1] & kStalledFlag)) {
+            // a Select needs more than the chain's window of a long list (sparse
+            // options): the lazy per-position loop places the rest
+            done += st[0];
+            chain = false;
+            A.base = nullptr;
+            A.base1 = nullptr;
+            A.base_by_pos = 0;
+            A.emit = nullptr;
+            A.done_flag = nullptr;
+            spin = false;
+            continue;
+        }
         done += c;
         if (st[0] < c) break;
     }
@@ -3235,7 +3250,7 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
     bool parallel = false;
     const uint32_t nv = (uint32_t)s->visit.size();
     const double t_prep = prof ? now_us() : 0.0;
-    const bool chain_ok = nv <= pe_chain_max_n() && s->limit <= pe_chain_max_limit();
+    const bool chain_ok = s->limit <= pe_chain_max_limit();
     if (count && g.psets.empty() && nv >= kParallelMinNodes && (s->cfg.preempt || !chain_ok)) {
         uint32_t cnt[3];
         rc = census(s, g, cnt);
@@ -3375,7 +3390,8 @@ static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
 // Whether place_impl runs this group's loop as the phase-static chain.
 static bool spec_chain_path(pe_stack* s, TgPlan& g) {
     const uint32_t nv = (uint32_t)s->visit.size();
-    return !tg_full_scan(s, g) && !s->cfg.preempt && s->use_base && s->visit_unique && nv <= pe_chain_max_n() &&
+    (void)nv;
+    return !tg_full_scan(s, g) && !s->cfg.preempt && s->use_base && s->visit_unique &&
            s->limit <= pe_chain_max_limit();
 }
 

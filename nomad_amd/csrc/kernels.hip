@@ -1200,8 +1200,9 @@ constexpr int kChainMaxSel = 1024;                            // Selects resolve
 constexpr int kChainTiles = kChainMaxN / 64;
 constexpr uint32_t kChainMaxRedo = 2048;                      // rows re-evaluated per phase (<= placements per launch)
 
-enum : int { kPhaseMore = 0, kPhaseCount = 1, kPhaseExhausted = 2 };
-constexpr int kSegE = 17;                 // entry offsets into a segment: a Select spans <= limit + 3 options
+enum : int { kPhaseMore = 0, kPhaseCount = 1, kPhaseExhausted = 2, kPhaseStall = 3 };
+constexpr uint32_t kChainStalled = 0x80000000u;   // eval_status cursor flag: continue with the lazy loop
+constexpr int kSegE = 21;                 // entry offsets into a segment: a Select spans <= limit + 3 options
 constexpr uint32_t kSegLen = 256;         // options per segment of the boundary walk
 constexpr int kChainSegs = kChainMaxN / kSegLen;
 constexpr uint32_t kMaxChainLimit = kSegE - 3;
@@ -1303,6 +1304,9 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = A.n_visit;
+    // positions per phase: one rotation, or its first kChainMaxN positions on a
+    // longer list (every Select of the phase still stops inside the window)
+    const uint32_t W = n < kChainMaxN ? n : kChainMaxN;
     const uint32_t L = A.limit;
     const uint32_t H = 1u << A.hash_bits;
     Overlay ov;
@@ -1313,7 +1317,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     ov.kshift = A.packed_overlay;
     ov.kmask = A.packed_overlay ? (1u << A.packed_overlay) - 1u : 0u;
     uint16_t* nb = reinterpret_cast<uint16_t*>(ov.keys + (A.packed_overlay ? H : 2 * H));   // [n + 2]
-    uint16_t* nx = nb + ((n + 2 + 1) & ~1u);   // [n + 2]: next Select start per option, then Select id per option
+    uint16_t* nx = nb + ((W + 2 + 1) & ~1u);   // [W + 2]: next Select start per option, then Select id per option
 
     uint64_t prof_t = A.prof ? __builtin_readcyclecounter() : 0;
     int prof_ph = 0;   // profile slot group: phase (capped at 3)
@@ -1328,11 +1332,12 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             sh.bm2[i] = 0;
         }
         if (tid == 0) {
-            sh.slow = 0;
+            sh.slow = n > kChainMaxN ? 1u : 0u;   // the position bitmaps cover one window of the list
             sh.n_emit = 0;
         }
         uint32_t cur = wrap_pos(A.offsets ? A.offsets[e] : A.offset0, n);
         uint32_t placed = 0;
+        bool stalled = false;
         bool done = n == 0 || A.count == 0;
         if (n == 0 && A.count && tid == 0 && A.out) {
             pe_placement& o = A.out[(size_t)e * A.count];
@@ -1349,7 +1354,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
 #pragma unroll
             for (int q = 0; q < kChainItems; q++) {
                 const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                row[q] = j < n ? perm[wrap_pos(cur + j, n)] : 0u;
+                row[q] = j < W ? perm[wrap_pos(cur + j, n)] : 0u;
             }
             // rows holding placements of this launch: one (base1) from the
             // position bitmaps, two or more re-evaluated (ov_count)
@@ -1359,7 +1364,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
 #pragma unroll
                 for (int q = 0; q < kChainItems; q++) {
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                    if (j < n) {
+                    if (j < W) {
                         uint32_t b1 = 1, b2 = 1;
                         if (use_bm) {
                             const uint32_t p = wrap_pos(cur + j, n), bit = 1u << (p & 31);
@@ -1381,7 +1386,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             for (int q = 0; q < kChainItems; q++) {
                 const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                 const double* src = ((one_mask >> q) & 1u) ? A.base1 : A.base;
-                v[q] = j < n ? src[A.base_by_pos ? wrap_pos(cur + j, n) : row[q]] : -__builtin_inf();
+                v[q] = j < W ? src[A.base_by_pos ? wrap_pos(cur + j, n) : row[q]] : -__builtin_inf();
             }
             if (__syncthreads_or(redo_mask != 0)) {
 #pragma unroll
@@ -1418,12 +1423,12 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
 #pragma unroll
             for (int q = 0; q < kChainItems; q++) {
                 const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                const bool is_o = j < n && v[q] > -__builtin_inf() && v[q] < __builtin_inf();
+                const bool is_o = j < W && v[q] > -__builtin_inf() && v[q] < __builtin_inf();
                 const bool is_n = is_o && v[q] <= 0.0;
                 optmask |= (uint32_t)is_o << q;
                 nmask |= (uint32_t)is_n << q;
                 const uint64_t bo = __ballot(is_o), bn = __ballot(is_n);
-                if (lane == 0 && q * kChainBlock < (int)n) {
+                if (lane == 0 && q * kChainBlock < (int)W) {
                     sh.tile_o[q * (kChainBlock / 64) + wave] = (uint32_t)__popcll(bo);
                     sh.tile_n[q * (kChainBlock / 64) + wave] = (uint32_t)__popcll(bn);
                 }
@@ -1437,7 +1442,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             __syncthreads();
             PE_PROF_MARK(1);
             // 2. exclusive scan of the tile counts (wave 0)
-            const uint32_t ntiles = (n + 63) / 64;
+            const uint32_t ntiles = (W + 63) / 64;
             if (wave == 0) {
                 constexpr int PER = kChainTiles / 64;
                 uint32_t so = 0, sn = 0, lo[PER], ln[PER];
@@ -1473,7 +1478,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             for (int q = 0; q < kChainItems; q++) {
                 const uint64_t bo = __ballot((optmask >> q) & 1u), bn = __ballot((nmask >> q) & 1u);
                 const uint32_t t = (uint32_t)(q * (kChainBlock / 64) + wave);
-                const bool live = (uint32_t)(q * kChainBlock) < n;
+                const bool live = (uint32_t)(q * kChainBlock) < W;
                 const uint32_t k = (live ? sh.tile_o[t] : 0u) + lanes_below(bo, lane);
                 const uint32_t nbk = (live ? sh.tile_n[t] : 0u) + lanes_below(bn, lane);
                 pk[q] = (k & kIdxMask) | ((nbk & kIdxMask) << kIdxBits);
@@ -1543,7 +1548,11 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 int mode = kPhaseMore;
                 uint32_t ns = total;
-                if (ns == 0) {
+                if (ns == 0 && W < n) {
+                    // a Select needs more than the window: the lazy loop goes on from here
+                    mode = kPhaseStall;
+                    used = 0;
+                } else if (ns == 0) {
                     // the first Select saw the whole list without reaching the limit
                     mode = kPhaseExhausted;
                     ns = tot_o ? 1u : 0u;
@@ -1580,6 +1589,10 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             __syncthreads();
             const uint32_t nsel = sh.nsel;
             const int mode = (int)sh.mode;
+            if (mode == kPhaseStall) {
+                stalled = true;
+                break;
+            }
             const uint32_t last_b = nsel ? sh.sel_b[nsel - 1] : 0u;
             PE_PROF_MARK(4);
             // 5. per-Select maxima over the returned options (a Select sets its
@@ -1615,11 +1628,11 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             }
             if (A.full_out && (nsel || mode == kPhaseExhausted)) {
                 // AllocMetric counters: filtered / exhausted positions pulled by each Select
-                const uint32_t end = mode == kPhaseExhausted ? n - 1 : sh.sel_end[nsel - 1];
+                const uint32_t end = mode == kPhaseExhausted ? W - 1 : sh.sel_end[nsel - 1];
 #pragma unroll
                 for (int q = 0; q < kChainItems; q++) {
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                    if (j <= end && j < n && !((optmask >> q) & 1u)) {
+                    if (j <= end && j < W && !((optmask >> q) & 1u)) {
                         // pulled by the Select of the next option after j
                         const uint32_t s = mode == kPhaseExhausted ? 0u : (uint32_t)nx[pk[q] & kIdxMask];
                         atomicAdd(v[q] == -__builtin_inf() ? &sh.sel_f[s] : &sh.sel_x[s], 1u);
@@ -1674,8 +1687,10 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 if (A.commit) {
                     for (uint32_t s = tid; s < nsel; s += kChainBlock) {
                         ov_add_atomic(ov, sh.sel_row[s]);
-                        const uint32_t p = wrap_pos(cur + sh.sel_pos[s], n), bit = 1u << (p & 31);
-                        if (atomicOr(&sh.bm1[p >> 5], bit) & bit) atomicOr(&sh.bm2[p >> 5], bit);
+                        if (n <= kChainMaxN) {   // the bitmaps cover lists of one window only
+                            const uint32_t p = wrap_pos(cur + sh.sel_pos[s], n), bit = 1u << (p & 31);
+                            if (atomicOr(&sh.bm1[p >> 5], bit) & bit) atomicOr(&sh.bm2[p >> 5], bit);
+                        }
                     }
                 }
                 if (tid == 0) sh.n_emit = placed + nsel;
@@ -1729,7 +1744,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
         }
         if (tid == 0) {
             A.eval_status[2 * e] = placed;
-            A.eval_status[2 * e + 1] = cur;
+            A.eval_status[2 * e + 1] = cur | (stalled ? kChainStalled : 0u);
         }
         if (A.emit) {
             // records and the HBM writeback are k_emit's: dump the overlay
@@ -2426,6 +2441,7 @@ uint32_t pe_chain_max_n() { return pe::kChainMaxN; }
 uint32_t pe_chain_max_limit() { return pe::kMaxChainLimit; }
 
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n) {
+    if (n > pe::kChainMaxN) n = pe::kChainMaxN;   // nb / nx cover one window
     return (size_t)(packed ? 4u : 8u) * ((size_t)1 << hash_bits) + 4u * (((size_t)n + 3u) & ~(size_t)1);
 }
 
@@ -2437,7 +2453,8 @@ int pe_chain_blocks_per_cu(size_t lds) {
 }
 
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st) {
-    if (!a->base || a->n_visit > pe::kChainMaxN || a->class_ok_stride || a->limit > pe::kMaxChainLimit)
+    if (!a->base || (a->n_visit > pe::kChainMaxN && n_evals != 1) || a->class_ok_stride ||
+        a->limit > pe::kMaxChainLimit)
         return hipErrorInvalidValue;
     if (a->base_by_pos && n_evals != 1) return hipErrorInvalidValue;
     uint32_t blocks = ((a->base_by_pos ? a->n_visit : a->soa.n) + 255) / 256;

@@ -119,3 +119,54 @@ def test_c2_10k_caller_protocol_count_1000():
         st.SetNodes(perm)
         res.append(compute_placements(st, 1000))
     assert len(res[0]) == 1000 and res[0] == res[1]
+
+
+@pytest.mark.gpu
+def test_c2_100k_nodes_count_1000():
+    # the metric's 100k-node case (BASELINE.json: "count=1000 job on 10k/100k
+    # nodes"), limit 17 (stack.go:83-90): the phase-static chain over windows
+    # of the long list, speculative behind Select / Commit
+    import numpy as np
+    from nomad_amd.stack import GenericStack
+    from oracle.oracle import OracleGenericStack
+    nodes, allocs = synth.cluster_c2(100000, seed=42)
+    job = synth.job_c2(1000)
+    perm = synth.shuffle(100000, 77)
+    got = []
+    for st in (GenericStack(), OracleGenericStack()):
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        assert st.SetNodes(perm) == 17
+        seq = []
+        for _ in range(1000):
+            r = st.Select(0)
+            seq.append(None if r is None else (r.row, r.final_score, r.nodes_evaluated, r.new_offset))
+            if r is None:
+                break
+            st.Commit(0, r.row)
+        got.append(seq)
+    assert got[0] == got[1]
+
+
+@pytest.mark.gpu
+def test_chain_window_stall_on_sparse_long_list():
+    # 40k nodes of which only a few hundred fit: a Select walks more than the
+    # chain's 16384-position window, so the launch hands over to the lazy loop
+    import numpy as np
+    from nomad_amd.stack import GenericStack
+    from oracle.oracle import OracleGenericStack
+    from nomad_amd.structs import Allocation
+    nodes, allocs = synth.cluster_c2(40000, seed=5, other_allocs=False)
+    for i, nd in enumerate(nodes):
+        if i % 150:
+            allocs.append(Allocation(node_id=nd.id, job_id="filler", task_group="tg",
+                                     cpu_shares=nd.cpu_shares - 100 - 200, memory_mb=64, disk_mb=10))
+    job = synth.job_c2(400)
+    perm = synth.shuffle(40000, 78)
+    got = []
+    for st in (GenericStack(), OracleGenericStack()):
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(perm)
+        got.append([(r.row, r.final_score, r.nodes_evaluated, r.new_offset) for r in st.Place(0, 400)])
+    assert got[0] == got[1]
