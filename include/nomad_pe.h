@@ -264,6 +264,14 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
  * reset (a state change starts a new evaluation). */
 int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index);
 int pe_reset_plan(pe_stack* s);
+/* Node upserts into the resident snapshot (state_store.go UpsertNode and the
+ * node_endpoint.go Register / UpdateStatus / UpdateDrain paths, with
+ * Node.ComputeClass computed by the caller, node_class.go:31-104): row i of
+ * `nodes` replaces snapshot row index[i], or is appended when index is NULL
+ * or index[i] == PE_NONE (appended rows take the next row numbers in order).
+ * The allocs stay; a node's allocs keep their rows. Like pe_update_allocs it
+ * starts a new evaluation context (pe_set_job / pe_set_nodes again). */
+int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const uint32_t* index);
 /* Stack.SetJob (stack.go:93-115 / 290-299). `strs` extends the table given to
  * pe_set_state (same ids for its first entries, job strings appended). */
 int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* job);

@@ -335,7 +335,9 @@ struct pe_stack {
     int32_t offer_row = -1;
     uint32_t offers = 0xFFFFFFFFu;
     uint32_t ncls = 0;
-    std::vector<uint32_t> class_rep;   // first row of each class
+    std::vector<uint32_t> class_rep;   // a member row of each class (the first, unless it changed)
+    std::unordered_map<uint32_t, uint32_t> cls_of;                   // ComputedClass str id -> dense class
+    std::unordered_map<uint64_t, std::vector<uint32_t>> sig_of;      // checker-input hash -> signatures
     // Nodes with equal ComputedClass AND equal non-hashed checker inputs
     // (drivers, networks, host-network aliases, host volumes, device count)
     // share a signature: every FeasibilityChecker verdict is a function of it.
@@ -900,56 +902,123 @@ void tg_ask(const pe_job* j, const pe_task_group& t, pe::Ask* a) {
 int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index);
 int build_alloc_state(pe_stack* s);
 
-int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) {
-    const uint32_t n = nt->n;
-    s->nodes.assign(n, HostNode());
-    std::unordered_map<uint32_t, uint32_t> cls_of;
-    s->class_rep.clear();
-    s->h_base_rec.assign(n, pe::NodeRec());
-    std::memset(s->h_base_rec.data(), 0, sizeof(pe::NodeRec) * n);
-    // variable-length node maps: copied once into CSR arrays, sorted per node
-    auto copy_off = [&](std::vector<uint32_t>& dst, const uint32_t* off) {
-        dst.assign(n + 1, 0);
-        if (off) for (uint32_t i = 0; i <= n; i++) dst[i] = off[i] - off[0];
-    };
-    copy_off(s->attr_off, nt->attr_off);
-    copy_off(s->meta_off, nt->meta_off);
-    copy_off(s->drv_off, nt->drv_off);
-    copy_off(s->net_off, nt->net_off);
-    copy_off(s->alias_off, nt->alias_off);
-    copy_off(s->hv_off, nt->hv_off);
-    s->attr_kv.resize(s->attr_off[n]);
-    s->meta_kv.resize(s->meta_off[n]);
-    s->drv_kf.resize(s->drv_off[n]);
-    s->net_mode_ids.resize(s->net_off[n]);
-    s->alias_ids.resize(s->alias_off[n]);
-    s->hv_kf.resize(s->hv_off[n]);
-    const uint32_t a0 = nt->attr_off[0], m0 = nt->meta_off[0], d0 = nt->drv_off[0];
-    const uint32_t w0 = nt->net_off[0], l0 = nt->alias_off[0], v0 = nt->hv_off ? nt->hv_off[0] : 0;
-    for (size_t k = 0; k < s->attr_kv.size(); k++) s->attr_kv[k] = KV(nt->attr_key[a0 + k], nt->attr_val[a0 + k]);
-    for (size_t k = 0; k < s->meta_kv.size(); k++) s->meta_kv[k] = KV(nt->meta_key[m0 + k], nt->meta_val[m0 + k]);
-    for (size_t k = 0; k < s->drv_kf.size(); k++) s->drv_kf[k] = KF(nt->drv_name[d0 + k], nt->drv_flags[d0 + k]);
-    for (size_t k = 0; k < s->net_mode_ids.size(); k++) s->net_mode_ids[k] = nt->net_mode[w0 + k];
-    for (size_t k = 0; k < s->alias_ids.size(); k++) s->alias_ids[k] = nt->alias_name[l0 + k];
-    for (size_t k = 0; k < s->hv_kf.size(); k++) s->hv_kf[k] = KF(nt->hv_name[v0 + k], nt->hv_read_only[v0 + k]);
-    for (uint32_t i = 0; i < n; i++) {
-        std::sort(s->attr_kv.begin() + s->attr_off[i], s->attr_kv.begin() + s->attr_off[i + 1]);
-        std::sort(s->meta_kv.begin() + s->meta_off[i], s->meta_kv.begin() + s->meta_off[i + 1]);
-        std::sort(s->drv_kf.begin() + s->drv_off[i], s->drv_kf.begin() + s->drv_off[i + 1]);
-        std::sort(s->alias_ids.begin() + s->alias_off[i], s->alias_ids.begin() + s->alias_off[i + 1]);
-        std::sort(s->hv_kf.begin() + s->hv_off[i], s->hv_kf.begin() + s->hv_off[i + 1]);
+// Node rows of a pe_node_table into the host mirror (build_state, and the
+// node upserts of pe_update_nodes): source row i of `nt` becomes row
+// target[i]; rows not targeted keep their data; the list grows to n_new rows.
+// The variable-length maps and the device groups are rebuilt as one pass of
+// copies; ComputedClass and checker signatures are interned into the persistent
+// maps, and a class / signature whose representative row changed gets another
+// member as its representative.
+int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t>& target, uint32_t n_new) {
+    const uint32_t n_old = (uint32_t)s->nodes.size();
+    const uint32_t m = nt->n;
+    std::vector<int32_t> src_of(n_new, -1);
+    for (uint32_t i = 0; i < m; i++) {
+        if (target[i] >= n_new || src_of[target[i]] >= 0) return s->fail(PE_EINVAL, "bad node row");
+        src_of[target[i]] = (int32_t)i;
     }
-    for (uint32_t i = 0; i < n; i++) {
-        HostNode& h = s->nodes[i];
+    for (uint32_t r = n_old; r < n_new; r++)
+        if (src_of[r] < 0) return s->fail(PE_EINVAL, "appended node rows must be contiguous");
+    // variable-length node maps: copied into CSR arrays, sorted per node
+    auto rebuild = [&](auto& items, std::vector<uint32_t>& off, const uint32_t* noff, auto item_of, bool sorted) {
+        using T = typename std::decay_t<decltype(items)>::value_type;
+        std::vector<T> out;
+        std::vector<uint32_t> o(n_new + 1, 0);
+        out.reserve(items.size() + (noff ? noff[m] - noff[0] : 0));
+        for (uint32_t r = 0; r < n_new; r++) {
+            const size_t b = out.size();
+            if (src_of[r] >= 0) {
+                const uint32_t i = (uint32_t)src_of[r];
+                for (uint32_t k = noff ? noff[i] : 0; noff && k < noff[i + 1]; k++) out.push_back(item_of(k));
+                if (sorted) std::sort(out.begin() + (long)b, out.end());
+            } else {
+                out.insert(out.end(), items.begin() + off[r], items.begin() + off[r + 1]);
+            }
+            o[r + 1] = (uint32_t)out.size();
+        }
+        items.swap(out);
+        off.swap(o);
+    };
+    if (s->attr_off.size() != n_old + 1) {   // a fresh mirror
+        for (auto* off : {&s->attr_off, &s->meta_off, &s->drv_off, &s->net_off, &s->alias_off, &s->hv_off, &s->dev_off})
+            off->assign(n_old + 1, 0);
+    }
+    rebuild(s->attr_kv, s->attr_off, nt->attr_off, [&](uint32_t k) { return KV(nt->attr_key[k], nt->attr_val[k]); }, true);
+    rebuild(s->meta_kv, s->meta_off, nt->meta_off, [&](uint32_t k) { return KV(nt->meta_key[k], nt->meta_val[k]); }, true);
+    rebuild(s->drv_kf, s->drv_off, nt->drv_off, [&](uint32_t k) { return KF(nt->drv_name[k], nt->drv_flags[k]); }, true);
+    rebuild(s->net_mode_ids, s->net_off, nt->net_off, [&](uint32_t k) { return nt->net_mode[k]; }, false);
+    rebuild(s->alias_ids, s->alias_off, nt->alias_off, [&](uint32_t k) { return nt->alias_name[k]; }, true);
+    rebuild(s->hv_kf, s->hv_off, nt->hv_off, [&](uint32_t k) { return KF(nt->hv_name[k], nt->hv_read_only[k]); }, true);
+    // device groups (NodeResources.Devices) with typed attributes
+    {
+        std::vector<uint32_t> doff(n_new + 1, 0);
+        std::vector<HostDevGroup> groups;
+        std::vector<std::pair<uint32_t, pe::DevAttr>> attrs;
+        for (uint32_t r = 0; r < n_new; r++) {
+            if (src_of[r] >= 0) {
+                const uint32_t i = (uint32_t)src_of[r];
+                const uint32_t g0 = nt->dev_off ? nt->dev_off[i] : 0, g1 = nt->dev_off ? nt->dev_off[i + 1] : 0;
+                for (uint32_t g = g0; g < g1; g++) {
+                    HostDevGroup d{nt->dev_vendor[g], nt->dev_type[g], nt->dev_name[g], nt->dev_healthy[g], 0, 0};
+                    d.attr_begin = (uint32_t)attrs.size();
+                    for (uint32_t q = nt->dev_attr_off ? nt->dev_attr_off[g] : 0;
+                         nt->dev_attr_off && q < nt->dev_attr_off[g + 1]; q++) {
+                        const pe_attr& pa = nt->dev_attr_val[q];
+                        pe::DevAttr at;
+                        switch (pa.kind) {
+                            case PE_ATTR_INT: at.kind = pe::DevAttr::kInt; at.i = pa.i; at.unit = s->S(pa.unit); break;
+                            case PE_ATTR_FLOAT: at.kind = pe::DevAttr::kFloat; at.f = pa.f; at.unit = s->S(pa.unit); break;
+                            case PE_ATTR_BOOL: at.kind = pe::DevAttr::kBool; at.b = pa.i != 0; break;
+                            default: at.kind = pe::DevAttr::kString; at.s = s->S(pa.s); break;
+                        }
+                        attrs.emplace_back(nt->dev_attr_key[q], at);
+                    }
+                    d.attr_end = (uint32_t)attrs.size();
+                    std::sort(attrs.begin() + d.attr_begin, attrs.begin() + d.attr_end,
+                              [](const auto& x, const auto& y) { return x.first < y.first; });
+                    groups.push_back(d);
+                }
+            } else {
+                for (uint32_t g = s->dev_off[r]; g < s->dev_off[r + 1]; g++) {
+                    HostDevGroup d = s->dev_groups[g];
+                    const uint32_t b = (uint32_t)attrs.size();
+                    attrs.insert(attrs.end(), s->dev_attr.begin() + d.attr_begin, s->dev_attr.begin() + d.attr_end);
+                    d.attr_begin = b;
+                    d.attr_end = (uint32_t)attrs.size();
+                    groups.push_back(d);
+                }
+            }
+            doff[r + 1] = (uint32_t)groups.size();
+        }
+        s->dev_off.swap(doff);
+        s->dev_groups.swap(groups);
+        s->dev_attr.swap(attrs);
+        s->max_dev_groups = 0;
+        s->dev_packable = true;
+        for (uint32_t r = 0; r < n_new; r++) s->max_dev_groups = std::max(s->max_dev_groups, s->dev_off[r + 1] - s->dev_off[r]);
+        for (const HostDevGroup& d : s->dev_groups) if (d.healthy > 255) s->dev_packable = false;
+        if (s->max_dev_groups > (uint32_t)pe::kMaxDevGroups) s->dev_packable = false;
+    }
+    // fixed per-node fields, ComputedClass interning
+    s->nodes.resize(n_new);
+    s->h_node_rec.resize(n_new);
+    std::vector<uint32_t> old_cls(n_new, PE_NONE), old_sig(n_new, PE_NONE);
+    for (uint32_t r = 0; r < n_old; r++)
+        if (src_of[r] >= 0) { old_cls[r] = s->nodes[r].cls; old_sig[r] = s->nodes[r].sig; }
+    for (uint32_t r = 0; r < n_new; r++) {
+        if (src_of[r] < 0) continue;
+        const uint32_t i = (uint32_t)src_of[r];
+        HostNode& h = s->nodes[r];
+        h = HostNode();
         h.id = nt->id[i]; h.name = nt->name[i]; h.dc = nt->datacenter[i];
         h.node_class = nt->node_class[i]; h.cclass = nt->computed_class[i];
-        auto it = cls_of.find(h.cclass);
-        if (it == cls_of.end()) {
-            it = cls_of.emplace(h.cclass, (uint32_t)s->class_rep.size()).first;
-            s->class_rep.push_back(i);
+        auto it = s->cls_of.find(h.cclass);
+        if (it == s->cls_of.end()) {
+            it = s->cls_of.emplace(h.cclass, (uint32_t)s->class_rep.size()).first;
+            s->class_rep.push_back(r);
+            s->class_sigs.emplace_back();
         }
         h.cls = it->second;
-        s->h_base_rec[i].cls = h.cls;
         h.n_device_nets = 0;
         h.first_mbits = -1;
         for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++) {
@@ -958,100 +1027,116 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
                 h.n_device_nets++;
             }
         }
-        h.n_devices = nt->dev_off ? (uint16_t)(nt->dev_off[i + 1] - nt->dev_off[i]) : 0;
-        pe::NodeRec& r = s->h_base_rec[i];
-        r.cap_cpu = nt->cpu_shares[i] - nt->reserved_cpu[i];
-        r.cap_mem = nt->memory_mb[i] - nt->reserved_memory_mb[i];
-        r.cap_disk = nt->disk_mb[i] - nt->reserved_disk_mb[i];
-        r.avail_mbits = h.first_mbits;
-        r.used_dyn = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
+        h.n_devices = (uint16_t)(s->dev_off[r + 1] - s->dev_off[r]);
+        pe::NodeRec& rec = s->h_node_rec[r];
+        std::memset(&rec, 0, sizeof(rec));
+        rec.cls = h.cls;
+        rec.cap_cpu = nt->cpu_shares[i] - nt->reserved_cpu[i];
+        rec.cap_mem = nt->memory_mb[i] - nt->reserved_memory_mb[i];
+        rec.cap_disk = nt->disk_mb[i] - nt->reserved_disk_mb[i];
+        rec.avail_mbits = h.first_mbits;
+        rec.used_dyn = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
     }
     s->ncls = (uint32_t)s->class_rep.size();
-    // device groups (NodeResources.Devices) with typed attributes
-    s->dev_off.assign(n + 1, 0);
-    s->dev_groups.clear();
-    s->dev_attr.clear();
-    s->max_dev_groups = 0;
-    s->dev_packable = true;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint32_t g0 = nt->dev_off ? nt->dev_off[i] : 0, g1 = nt->dev_off ? nt->dev_off[i + 1] : 0;
-        for (uint32_t g = g0; g < g1; g++) {
-            HostDevGroup d{nt->dev_vendor[g], nt->dev_type[g], nt->dev_name[g], nt->dev_healthy[g], 0, 0};
-            d.attr_begin = (uint32_t)s->dev_attr.size();
-            for (uint32_t q = nt->dev_attr_off ? nt->dev_attr_off[g] : 0;
-                 nt->dev_attr_off && q < nt->dev_attr_off[g + 1]; q++) {
-                const pe_attr& pa = nt->dev_attr_val[q];
-                pe::DevAttr a;
-                switch (pa.kind) {
-                    case PE_ATTR_INT: a.kind = pe::DevAttr::kInt; a.i = pa.i; a.unit = s->S(pa.unit); break;
-                    case PE_ATTR_FLOAT: a.kind = pe::DevAttr::kFloat; a.f = pa.f; a.unit = s->S(pa.unit); break;
-                    case PE_ATTR_BOOL: a.kind = pe::DevAttr::kBool; a.b = pa.i != 0; break;
-                    default: a.kind = pe::DevAttr::kString; a.s = s->S(pa.s); break;
-                }
-                s->dev_attr.emplace_back(nt->dev_attr_key[q], a);
-            }
-            d.attr_end = (uint32_t)s->dev_attr.size();
-            std::sort(s->dev_attr.begin() + d.attr_begin, s->dev_attr.begin() + d.attr_end,
-                      [](const auto& x, const auto& y) { return x.first < y.first; });
-            if (d.healthy > 255) s->dev_packable = false;
-            s->dev_groups.push_back(d);
-        }
-        s->dev_off[i + 1] = (uint32_t)s->dev_groups.size();
-        s->max_dev_groups = std::max(s->max_dev_groups, g1 - g0);
-    }
-    if (s->max_dev_groups > (uint32_t)pe::kMaxDevGroups) s->dev_packable = false;
-    // checker-input signatures
+    // checker-input signatures: nodes with equal ComputedClass AND equal
+    // non-hashed checker inputs (drivers, networks, aliases, volumes, device
+    // health). A 64-bit hash of the inputs; equal hashes are verified exactly
+    // against the signature's representative before being merged.
+    auto same_inputs = [&](uint32_t a_row, uint32_t b_row) {
+        const NodeView x = s->view(a_row), y = s->view(b_row);
+        auto eq = [](auto u, auto v) { return u.size() == v.size() && std::equal(u.begin(), u.end(), v.begin()); };
+        if (x.h->n_devices != y.h->n_devices) return false;
+        for (uint32_t k = 0; k < x.h->n_devices; k++)   // DeviceChecker reads healthy counts
+            if (s->dev_groups[s->dev_off[a_row] + k].healthy != s->dev_groups[s->dev_off[b_row] + k].healthy)
+                return false;
+        return x.h->cls == y.h->cls && eq(x.drivers, y.drivers) &&
+               eq(x.net_modes, y.net_modes) && eq(x.aliases, y.aliases) && eq(x.volumes, y.volumes);
+    };
+    auto sig_hash = [&](uint32_t r) {
+        const HostNode& h = s->nodes[r];
+        const NodeView v = s->view(r);
+        uint64_t x = 1469598103934665603ull;
+        auto mix = [&](uint64_t y) { x = (x ^ y) * 1099511628211ull; x ^= x >> 29; };
+        mix(h.cls);
+        mix(h.n_devices);
+        for (uint32_t k = s->dev_off[r]; k < s->dev_off[r + 1]; k++) mix(s->dev_groups[k].healthy);
+        mix(v.drivers.size());
+        for (auto& d : v.drivers) { mix(d.first); mix(d.second); }
+        mix(v.net_modes.size());
+        for (uint32_t mm : v.net_modes) mix(mm);
+        mix(v.aliases.size());
+        for (uint32_t al : v.aliases) mix(al);
+        mix(v.volumes.size());
+        for (auto& vv : v.volumes) { mix(vv.first); mix(vv.second); }
+        return x;
+    };
+    // representatives of changed rows move to another member first
     {
-        // 64-bit hash of the checker inputs; equal hashes are verified exactly
-        // against the signature's representative before being merged.
-        std::unordered_map<uint64_t, std::vector<uint32_t>> sig_of;
-        s->sig_rep.clear();
-        s->sig_cls.clear();
-        s->class_sigs.assign(s->ncls, {});
-        auto same_inputs = [&](uint32_t a_row, uint32_t b_row) {
-            const NodeView x = s->view(a_row), y = s->view(b_row);
-            auto eq = [](auto u, auto v) { return u.size() == v.size() && std::equal(u.begin(), u.end(), v.begin()); };
-            if (x.h->n_devices != y.h->n_devices) return false;
-            for (uint32_t k = 0; k < x.h->n_devices; k++)   // DeviceChecker reads healthy counts
-                if (s->dev_groups[s->dev_off[a_row] + k].healthy != s->dev_groups[s->dev_off[b_row] + k].healthy)
-                    return false;
-            return x.h->cls == y.h->cls && eq(x.drivers, y.drivers) &&
-                   eq(x.net_modes, y.net_modes) && eq(x.aliases, y.aliases) && eq(x.volumes, y.volumes);
-        };
-        for (uint32_t i = 0; i < n; i++) {
-            HostNode& h = s->nodes[i];
-            const NodeView v = s->view(i);
-            uint64_t x = 1469598103934665603ull;
-            auto mix = [&](uint64_t y) { x = (x ^ y) * 1099511628211ull; x ^= x >> 29; };
-            mix(h.cls);
-            mix(h.n_devices);
-            for (uint32_t k = s->dev_off[i]; k < s->dev_off[i + 1]; k++) mix(s->dev_groups[k].healthy);
-            mix(v.drivers.size());
-            for (auto& d : v.drivers) { mix(d.first); mix(d.second); }
-            mix(v.net_modes.size());
-            for (uint32_t m : v.net_modes) mix(m);
-            mix(v.aliases.size());
-            for (uint32_t al : v.aliases) mix(al);
-            mix(v.volumes.size());
-            for (auto& vv : v.volumes) { mix(vv.first); mix(vv.second); }
-            auto& bucket = sig_of[x];
-            uint32_t found = PE_NONE;
-            for (uint32_t sg : bucket)
-                if (same_inputs(s->sig_rep[sg], i)) { found = sg; break; }
-            if (found == PE_NONE) {
-                found = (uint32_t)s->sig_rep.size();
-                bucket.push_back(found);
-                s->sig_rep.push_back(i);
-                s->sig_cls.push_back(h.cls);
-                s->class_sigs[h.cls].push_back(found);
+        std::vector<uint8_t> changed(n_new, 0);
+        for (uint32_t r = 0; r < n_new; r++) changed[r] = src_of[r] >= 0;
+        std::vector<uint32_t> cls_fix, sig_fix;
+        for (uint32_t c = 0; c < (uint32_t)s->class_rep.size(); c++)
+            if (s->class_rep[c] < n_old && changed[s->class_rep[c]] && old_cls[s->class_rep[c]] == c) cls_fix.push_back(c);
+        for (uint32_t g = 0; g < (uint32_t)s->sig_rep.size(); g++)
+            if (changed[s->sig_rep[g]]) sig_fix.push_back(g);
+        if (!cls_fix.empty() || !sig_fix.empty()) {
+            std::unordered_map<uint32_t, uint32_t> cnew, snew;
+            for (uint32_t r = 0; r < n_new; r++) {
+                if (changed[r]) continue;
+                cnew.emplace(s->nodes[r].cls, r);
+                snew.emplace(s->nodes[r].sig, r);
             }
-            h.sig = found;
+            for (uint32_t c : cls_fix) {
+                auto it = cnew.find(c);
+                if (it != cnew.end()) s->class_rep[c] = it->second;   // else the class keeps no member
+            }
+            for (uint32_t g : sig_fix) {
+                auto it = snew.find(g);
+                if (it != snew.end()) { s->sig_rep[g] = it->second; continue; }
+                s->sig_rep[g] = PE_NONE;   // no member left: never matched again
+            }
         }
     }
-    s->h_node_rec = s->h_base_rec;
+    for (uint32_t r = 0; r < n_new; r++) {
+        if (src_of[r] < 0) continue;
+        HostNode& h = s->nodes[r];
+        auto& bucket = s->sig_of[sig_hash(r)];
+        uint32_t found = PE_NONE;
+        for (uint32_t sg : bucket)
+            if (s->sig_rep[sg] != PE_NONE && same_inputs(s->sig_rep[sg], r)) { found = sg; break; }
+        if (found == PE_NONE) {
+            found = (uint32_t)s->sig_rep.size();
+            bucket.push_back(found);
+            s->sig_rep.push_back(r);
+            s->sig_cls.push_back(h.cls);
+            s->class_sigs[h.cls].push_back(found);
+        }
+        h.sig = found;
+    }
+    return PE_OK;
+}
+
+int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) {
+    s->nodes.clear();
+    s->h_node_rec.clear();
+    s->cls_of.clear();
+    s->class_rep.clear();
+    s->class_sigs.clear();
+    s->sig_of.clear();
+    s->sig_rep.clear();
+    s->sig_cls.clear();
+    for (auto* off : {&s->attr_off, &s->meta_off, &s->drv_off, &s->net_off, &s->alias_off, &s->hv_off, &s->dev_off})
+        off->assign(1, 0);
+    s->attr_kv.clear(); s->meta_kv.clear(); s->drv_kf.clear(); s->hv_kf.clear();
+    s->net_mode_ids.clear(); s->alias_ids.clear();
+    s->dev_groups.clear(); s->dev_attr.clear();
+    std::vector<uint32_t> target(nt->n);
+    for (uint32_t i = 0; i < nt->n; i++) target[i] = i;
+    int rc = apply_nodes(s, nt, target, nt->n);
+    if (rc) return rc;
     s->allocs.clear();
     s->alloc_dev.clear();
-    int rc = append_allocs(s, at, nullptr);
+    rc = append_allocs(s, at, nullptr);
     if (rc) return rc;
     return build_alloc_state(s);
 }
@@ -2402,6 +2487,45 @@ int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* a
     s->offset = 0;
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     return PE_OK;
+}
+
+int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const uint32_t* index) {
+    if (!s || !nodes) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    spec_drop(s);
+    s->node_update.clear();   // a new evaluation context: no plan stops
+    s->stop_count.clear();
+    s->gen++;
+    HIP_TRY(s, hipSetDevice(s->device));
+    s->add_strings(strs);
+    const uint32_t n_old = (uint32_t)s->nodes.size();
+    std::vector<uint32_t> target(nodes->n);
+    uint32_t n_new = n_old;
+    for (uint32_t i = 0; i < nodes->n; i++) {
+        const uint32_t r = index ? index[i] : PE_NONE;
+        if (r != PE_NONE && r >= n_old) return s->fail(PE_EINVAL, "node index out of range");
+        target[i] = r == PE_NONE ? n_new++ : r;
+    }
+    int rc = apply_nodes(s, nodes, target, n_new);
+    if (rc) {   // the mirror may be half updated: a reload is required
+        s->have_state = false;
+        return rc;
+    }
+    s->plan.clear();
+    s->tg_memo.clear();
+    s->job_memo.clear();
+    s->ref_tg_memo.clear();
+    s->ref_job_memo.clear();
+    s->spread_info_done.clear();
+    s->sum_spread_weights = 0;
+    s->have_job = false;
+    s->have_job_version = false;
+    s->tgs.clear();
+    s->visit.clear();
+    s->offset = 0;
+    rc = build_alloc_state(s);
+    if (rc) s->have_state = false;
+    return rc;
 }
 
 int pe_reset_plan(pe_stack* s) {

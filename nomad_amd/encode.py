@@ -69,12 +69,39 @@ class EncodedState:
     """pe_node_table + pe_alloc_table over one Interner."""
 
     def __init__(self, nodes: Sequence[Node], allocs: Sequence[Allocation], interner: Interner = None):
-        it = self.interner = interner or Interner()
+        self.interner = interner or Interner()
         self.nodes = list(nodes)
-        n = len(nodes)
         self.row_of = {nd.id: i for i, nd in enumerate(nodes)}
-        keep = []
-        self.keep = keep
+        self.keep = []
+        self.node_table = self.encode_node_table(self.nodes)
+        self.alloc_table = self.encode_alloc_table(allocs)
+
+    def update_nodes(self, nodes: Sequence[Node], index=None):
+        """pe_node_table of node upserts (pe_update_nodes): nodes[i] replaces
+        row index[i], or is appended when index[i] is None; the mirror's node
+        list and row map follow."""
+        idx = []
+        for i, nd in enumerate(nodes):
+            r = None if index is None else index[i]
+            if r is None or r < 0:
+                r = len(self.nodes)
+                self.nodes.append(nd)
+                idx.append(abi.PE_NONE)
+            else:
+                old = self.nodes[r]
+                if self.row_of.get(old.id) == r and old.id != nd.id:
+                    del self.row_of[old.id]
+                self.nodes[r] = nd
+                idx.append(r)
+            self.row_of[nd.id] = r
+        return self.encode_node_table(list(nodes)), _u32(idx or [0])
+
+    def encode_node_table(self, nodes: Sequence[Node]) -> abi.pe_node_table:
+        """pe_node_table of `nodes` over this state's interner (the arrays stay
+        alive with this object)."""
+        it = self.interner
+        n = len(nodes)
+        keep = self.keep
 
         def col(f, conv):
             a = conv([f(nd) for nd in nodes])
@@ -145,9 +172,7 @@ class EncodedState:
         keep.extend([aoff, akeys_a, avals_a])
         nt.dev_attr_off, nt.dev_attr_key = _ptr(aoff, abi.u32p), _ptr(akeys_a, abi.u32p)
         nt.dev_attr_val = C.cast(avals_a, C.POINTER(abi.pe_attr))
-        self.node_table = nt
-
-        self.alloc_table = self.encode_alloc_table(allocs)
+        return nt
 
     def encode_alloc_table(self, allocs: Sequence[Allocation]) -> abi.pe_alloc_table:
         """pe_alloc_table over this state's interner and node rows (the arrays

@@ -223,6 +223,19 @@ class _Stack:
         self._check(fn(self._h, C.byref(t), C.byref(at), idx.ctypes.data_as(abi.u32p)))
         self._job = None
 
+    def UpdateNodes(self, nodes: Sequence[Node], index: Optional[Sequence[int]] = None):
+        """Node upserts without a reload (pe_update_nodes): nodes[i] replaces
+        snapshot row index[i] (None / -1: appended)."""
+        fn = self._fn("update_nodes")
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.POINTER(abi.pe_strtab), C.POINTER(abi.pe_node_table), abi.u32p]
+        nt, idx = self.state.update_nodes(nodes, index)
+        if self.nodes is not None:
+            self.nodes = list(self.state.nodes)
+        t = self.state.strtab()
+        self._check(fn(self._h, C.byref(t), C.byref(nt), idx.ctypes.data_as(abi.u32p)))
+        self._job = None
+
     def ResetPlan(self):
         """New evaluation on the resident snapshot (fresh EvalContext)."""
         self._check(self._fn("reset_plan")(self._h))

@@ -96,10 +96,20 @@ class Node:
         put("|class"); put(self.node_class)
         for d in self.devices:
             put(d.vendor); put(d.type); put(d.name)
-            for k in sorted(d.attributes):
-                put(k); put(repr(d.attributes[k]))
+            for k in sorted(d.attributes):   # NodeDeviceResource.HashIncludeMap: no unique.* keys
+                if not k.startswith("unique."):
+                    put(k); put(repr(d.attributes[k]))
         self.computed_class = "v1:%d" % int.from_bytes(h.digest(), "little")
         return self.computed_class
+
+
+def escaped_constraints(constraints):
+    """EscapedConstraints (node_class.go:108-132): the constraints whose LTarget
+    or RTarget escapes the computed class (${node.unique.*}, ${attr.unique.*},
+    ${meta.unique.*})."""
+    def escapes(t):
+        return t.startswith("${node.unique.") or t.startswith("${attr.unique.") or t.startswith("${meta.unique.")
+    return [c for c in constraints if escapes(c.ltarget) or escapes(c.rtarget)]
 
 
 @dataclass

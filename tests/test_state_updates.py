@@ -98,3 +98,96 @@ def test_update_allocs_devices_and_preemption():
     _, _, want = run_place(OracleGenericStack, nodes, updated, job, perm, config=cfg)
     assert_same_placements(got, want)
     assert [g.preempted for g in got] == [w.preempted for w in want]
+
+
+def _node_delta(nodes, seed, n_changed=120, n_new=40, devices=False):
+    """Node upserts: capacity, attribute (class), driver and device changes on
+    existing rows, plus new nodes appended."""
+    rng = random.Random(seed)
+    changed, index = [], []
+    for r in rng.sample(range(len(nodes)), n_changed):
+        nd = copy.deepcopy(nodes[r])
+        k = rng.randrange(4)
+        if k == 0:
+            nd.cpu_shares = rng.choice([8000, 16000])
+        elif k == 1:
+            nd.attributes["kernel.name"] = rng.choice(["linux", "windows"])
+            nd.node_class = "class-%d" % rng.randrange(12)
+        elif k == 2:
+            nd.drivers = {}
+            nd.attributes.pop("driver.exec", None)
+        elif devices and nd.devices:
+            nd.devices[0].healthy = max(0, nd.devices[0].healthy - 2)
+        else:
+            nd.meta["rack"] = "r%d" % rng.randrange(5)
+        nd.compute_class()
+        changed.append(nd)
+        index.append(r)
+    base = synth.cluster_c5(n_new, seed=seed + 100)[0] if devices else synth.cluster_c2(n_new, seed=seed + 100)[0]
+    for nd in base:
+        nd.id = "new-" + nd.id
+        nd.compute_class()
+        changed.append(nd)
+        index.append(None)
+    updated = list(nodes)
+    for nd, r in zip(changed, index):
+        if r is None:
+            updated.append(nd)
+        else:
+            updated[r] = nd
+    return changed, index, updated
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["c2", "c3"])
+def test_update_nodes_equals_fresh_state(kind):
+    from nomad_amd.stack import GenericStack
+    if kind == "c2":
+        nodes, allocs = synth.cluster_c2(1500, seed=31)
+        job = synth.job_c2(300)
+    else:
+        nodes, allocs = synth.cluster_c3(1500, seed=32)
+        job = synth.job_c3(200)
+    changed, index, updated = _node_delta(nodes, 3)
+    st = GenericStack()
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(synth.shuffle(len(nodes), 5))
+    st.Place(0, 40)                       # an evaluation on the old snapshot
+    st.UpdateNodes(changed, index)        # node upserts: rows replaced and appended
+    perm = synth.shuffle(len(updated), 6)
+    st.SetJob(job)
+    st.SetNodes(list(perm))
+    got = st.Place(0, job.task_groups[0].count)
+    _, _, want = run_place(OracleGenericStack, updated, allocs, job, perm)
+    assert_same_placements(got, want)
+    # then an alloc delta on the updated snapshot, and a second node delta
+    changed2, index2, updated2 = _delta(updated, allocs, 4, frac_terminal=0.2, n_new=60)
+    st.UpdateAllocs(changed2, index2)
+    changed3, index3, updated3 = _node_delta(updated, 7, n_changed=60, n_new=10)
+    st.UpdateNodes(changed3, index3)
+    perm3 = synth.shuffle(len(updated3), 8)
+    st.SetJob(job)
+    st.SetNodes(list(perm3))
+    got3 = st.Place(0, job.task_groups[0].count)
+    _, _, want3 = run_place(OracleGenericStack, updated3, updated2, job, perm3)
+    assert_same_placements(got3, want3)
+
+
+@pytest.mark.gpu
+def test_update_nodes_devices_and_preemption():
+    from nomad_amd.stack import GenericStack
+    cfg = SchedulerConfig(preempt_service=True)
+    nodes, allocs = synth.cluster_c5(700, seed=33, busy=0.8)
+    changed, index, updated = _node_delta(nodes, 9, n_changed=150, n_new=30, devices=True)
+    job = synth.job_c5(100)
+    perm = synth.shuffle(len(updated), 10)
+    st = GenericStack(config=cfg)
+    st.SetState(nodes, allocs)
+    st.UpdateNodes(changed, index)
+    st.SetJob(job)
+    st.SetNodes(list(perm))
+    got = st.Place(0, 100)
+    _, _, want = run_place(OracleGenericStack, updated, allocs, job, perm, config=cfg)
+    assert_same_placements(got, want)
+    assert [g.preempted for g in got] == [w.preempted for w in want]
