@@ -337,7 +337,8 @@ struct pe_stack {
     uint32_t ncls = 0;
     std::vector<uint32_t> class_rep;   // a member row of each class (the first, unless it changed)
     std::unordered_map<uint32_t, uint32_t> cls_of;                   // ComputedClass str id -> dense class
-    std::unordered_map<uint64_t, std::vector<uint32_t>> sig_of;      // checker-input hash -> signatures
+    std::unordered_map<uint64_t, std::vector<uint32_t>> sig_of;      // checker-input hash -> live signatures
+    std::vector<uint64_t> sig_hash;                                   // per signature
     // Nodes with equal ComputedClass AND equal non-hashed checker inputs
     // (drivers, networks, host-network aliases, host volumes, device count)
     // share a signature: every FeasibilityChecker verdict is a function of it.
@@ -1093,25 +1094,46 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
             for (uint32_t g : sig_fix) {
                 auto it = snew.find(g);
                 if (it != snew.end()) { s->sig_rep[g] = it->second; continue; }
-                s->sig_rep[g] = PE_NONE;   // no member left: never matched again
+                // no member left: out of its class and of the hash buckets (the
+                // representative row index stays valid for the tables)
+                auto& cs = s->class_sigs[s->sig_cls[g]];
+                cs.erase(std::remove(cs.begin(), cs.end(), g), cs.end());
+                auto& bk = s->sig_of[s->sig_hash[g]];
+                bk.erase(std::remove(bk.begin(), bk.end(), g), bk.end());
             }
         }
     }
     for (uint32_t r = 0; r < n_new; r++) {
         if (src_of[r] < 0) continue;
         HostNode& h = s->nodes[r];
-        auto& bucket = s->sig_of[sig_hash(r)];
+        const uint64_t hv = sig_hash(r);
+        auto& bucket = s->sig_of[hv];
         uint32_t found = PE_NONE;
         for (uint32_t sg : bucket)
-            if (s->sig_rep[sg] != PE_NONE && same_inputs(s->sig_rep[sg], r)) { found = sg; break; }
+            if (same_inputs(s->sig_rep[sg], r)) { found = sg; break; }
         if (found == PE_NONE) {
             found = (uint32_t)s->sig_rep.size();
             bucket.push_back(found);
             s->sig_rep.push_back(r);
             s->sig_cls.push_back(h.cls);
+            s->sig_hash.push_back(hv);
             s->class_sigs[h.cls].push_back(found);
         }
         h.sig = found;
+    }
+    // a class whose representative left it (and had no other member then) takes
+    // a member that joined it later
+    {
+        std::vector<uint32_t> stale;
+        for (uint32_t c = 0; c < s->ncls; c++)
+            if (s->nodes[s->class_rep[c]].cls != c) stale.push_back(c);
+        if (!stale.empty()) {
+            std::vector<uint32_t> first(s->ncls, PE_NONE);
+            for (uint32_t r = 0; r < n_new; r++)
+                if (first[s->nodes[r].cls] == PE_NONE) first[s->nodes[r].cls] = r;
+            for (uint32_t c : stale)
+                if (first[c] != PE_NONE) s->class_rep[c] = first[c];
+        }
     }
     return PE_OK;
 }
@@ -1123,6 +1145,7 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     s->class_rep.clear();
     s->class_sigs.clear();
     s->sig_of.clear();
+    s->sig_hash.clear();
     s->sig_rep.clear();
     s->sig_cls.clear();
     for (auto* off : {&s->attr_off, &s->meta_off, &s->drv_off, &s->net_off, &s->alias_off, &s->hv_off, &s->dev_off})
@@ -1532,7 +1555,7 @@ void classify_classes(pe_stack* s, TgPlan& g, pe::ConstraintEvaluator& ev) {
     if (s->job_memo.size() != s->ncls) s->job_memo.assign(s->ncls, -1);
     for (uint32_t c = 0; c < s->ncls; c++) {
         const auto& sigs = s->class_sigs[c];
-        g.class_verdict[c] = g.sig_tg[sigs[0]];
+        g.class_verdict[c] = sigs.empty() ? 0 : g.sig_tg[sigs[0]];   // a class left without members: no node reads it
         for (uint32_t sg : sigs) if (g.sig_tg[sg] != g.class_verdict[c]) g.class_uniform[c] = 0;
         if (!s->job_escaped && s->job_memo[c] == -1)
             s->job_memo[c] = job_feasible(s, ev, s->view(s->class_rep[c])) ? 1 : 0;
