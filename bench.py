@@ -493,12 +493,43 @@ def section_ingest(device, n=100000, reps=5):
         rc = lib.pe_update_allocs(h, C.byref(tab), C.byref(at), idx.ctypes.data_as(abi.u32p))
         t_upd.append(time.perf_counter() - t0)
         assert rc == 0
+    # node upserts (pe_update_nodes): n/100 nodes change capacity or class, n/1000 join
+    lib.pe_update_nodes.restype = C.c_int
+    lib.pe_update_nodes.argtypes = [C.c_void_p, C.POINTER(abi.pe_strtab), C.POINTER(abi.pe_node_table), abi.u32p]
+    t_nodes = []
+    for rep in range(reps):
+        tab = es.strtab()
+        rc = lib.pe_set_state(h, C.byref(tab), C.byref(es.node_table), C.byref(es.alloc_table))
+        assert rc == 0
+        upd_nodes, upd_idx = [], []
+        for r in rng.sample(range(n), n // 100):
+            nd = copy.deepcopy(nodes[r])
+            nd.cpu_shares *= 2
+            if r % 3 == 0:
+                nd.attributes["kernel.version"] = "6.%d" % (rep % 3)
+            nd.compute_class()
+            upd_nodes.append(nd)
+            upd_idx.append(r)
+        for k in range(n // 1000):
+            nd = copy.deepcopy(nodes[k])
+            nd.id = "joined-%d-%d" % (rep, k)
+            upd_nodes.append(nd)
+            upd_idx.append(abi.PE_NONE)
+        nt = es.encode_node_table(upd_nodes)
+        ix = np.asarray(upd_idx, dtype=np.uint32)
+        tab = es.strtab()
+        t0 = time.perf_counter()
+        rc = lib.pe_update_nodes(h, C.byref(tab), C.byref(nt), ix.ctypes.data_as(abi.u32p))
+        t_nodes.append(time.perf_counter() - t0)
+        assert rc == 0
     st.close()
-    full, upd = float(np.median(t_full)), float(np.median(t_upd))
-    return {"workload": "C2-shaped cluster of %d nodes, %d allocs; delta: %d allocs terminal + %d new"
+    full, upd, unodes = float(np.median(t_full)), float(np.median(t_upd)), float(np.median(t_nodes))
+    return {"workload": "C2-shaped cluster of %d nodes, %d allocs; delta: %d allocs terminal + %d new; node "
+                        "upserts: %d changed + %d joined"
                         % (n, len(allocs), sum(1 for i in index if i != abi.PE_NONE),
-                           sum(1 for i in index if i == abi.PE_NONE)),
-            "set_state_ms": full * 1e3, "update_allocs_ms": upd * 1e3, "speedup": full / upd}
+                           sum(1 for i in index if i == abi.PE_NONE), n // 100, n // 1000),
+            "set_state_ms": full * 1e3, "update_allocs_ms": upd * 1e3, "speedup": full / upd,
+            "update_nodes_ms": unodes * 1e3}
 
 
 def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
