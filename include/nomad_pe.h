@@ -294,6 +294,23 @@ int pe_select(pe_stack* s, uint32_t tg_index, const pe_select_options* opts,
  * committed prefix, so results always equal one-at-a-time Selects.
  * PE_SPECULATE=0 in the environment disables it. */
 int pe_commit(pe_stack* s, uint32_t tg_index, int32_t row);
+/* Multi-GPU: one engine handle per GPU and process, joined by
+ * an RCCL communicator (ncclGetUniqueId on one rank, the 128 bytes shared by
+ * the caller, ncclCommInitRank on every rank). */
+int pe_comm_unique_id(uint8_t* out, size_t cap);
+int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id);
+/* The full-pass count loop (task groups with affinities / spreads, limit >=
+ * list) sharded over the ranks: every rank holds the whole snapshot, job and
+ * SetNodes list and sweeps its rows [row_begin, row_end); per placement one
+ * ncclAllGather of the ranks' 80-byte records on the engine stream, then every
+ * rank resolves and commits the same winner (the gather carries every
+ * workgroup's record: blocks x 80 B per rank). Every rank receives the same
+ * records. Windowed task groups return PE_EUNSUPPORTED (replicas only). */
+int pe_place_sharded(pe_stack* s, uint32_t tg_index, uint32_t count, uint32_t row_begin, uint32_t row_end,
+                     pe_ranked_node* out, uint32_t* placed);
+/* Device time of one all-gather in the last pe_place_sharded (microseconds,
+ * mean over one sampled placement per 64; includes waiting for peer ranks). */
+double pe_last_exchange_us(const pe_stack* s);
 /* Counters of the speculative loop: out[0] runs started, [1] Selects answered
  * from records, [2] rollbacks (the caller deviated), [3] records computed. */
 int pe_speculation_stats(const pe_stack* s, uint64_t* out4);

@@ -196,7 +196,8 @@ ENGINE_SYMBOLS = [
     "pe_last_kernel_ms", "pe_stage_orders", "pe_place_batch", "pe_batch_results", "pe_last_phase_ms",
     "pe_check_constraint", "pe_last_sweep_bytes", "pe_select_shard", "pe_select_merge",
     "pe_set_metrics", "pe_last_metrics", "pe_update_allocs", "pe_speculation_stats",
-    "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes",
+    "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
+    "pe_place_sharded", "pe_last_exchange_us",
 ]
 
 

@@ -28,6 +28,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/nomad_pe.h"
 #include "constraint_eval.h"
 #include "engine_types.h"
@@ -37,6 +39,9 @@ size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
+hipError_t pe_launch_sweep_only(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t pe_launch_step_only(const pe::SweepArgs* a, uint32_t nrecs, const uint32_t* visit, uint32_t n,
+                               uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_commit_rows(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
                                  uint32_t n, hipStream_t st);
 hipError_t pe_launch_evict_trace(const pe::PreemptArgs* a, const uint32_t* rows, uint32_t n, uint32_t* code,
@@ -448,6 +453,14 @@ struct pe_stack {
     std::vector<uint32_t> stop_count;
     DevMem d_stop_slots, d_stop_rows;
     bool stopped(uint32_t ai) const { return ai < stop_count.size() && stop_count[ai] > 0; }
+
+    // multi-GPU handle (pe_comm_init): an RCCL communicator over the ranks'
+    // engines, one GPU each; the sharded count loop gathers per-rank records
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    DevMem d_gather;
+    hipEvent_t ev_x0 = nullptr, ev_x1 = nullptr;   // around one sampled all-gather per chunk
+    double last_exchange_us = 0;
 
     // PE_API_PROF=1: wall time per named host step, printed at pe_stack_destroy
     bool api_prof = false;
@@ -2414,6 +2427,9 @@ void pe_stack_destroy(pe_stack* s) {
                          kv.second.first / std::max<uint64_t>(kv.second.second, 1));
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->comm) (void)ncclCommDestroy(s->comm);
+    if (s->ev_x0) (void)hipEventDestroy(s->ev_x0);
+    if (s->ev_x1) (void)hipEventDestroy(s->ev_x1);
     s->tgs.clear();
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -3781,6 +3797,138 @@ int pe_plan_pop_update(pe_stack* s, uint32_t alloc) {
     if (--s->stop_count[alloc] == 0) gone.push_back(alloc);
     return apply_stop_delta(s, gone, -1);
 }
+
+// ---- multi-GPU ------------------------------------------------
+
+int pe_comm_unique_id(uint8_t* out, size_t cap) {
+    if (!out || cap < NCCL_UNIQUE_ID_BYTES) return PE_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return PE_EHIP;
+    std::memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return PE_OK;
+}
+
+int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id) {
+    if (!s || !id || nranks < 1 || rank < 0 || rank >= nranks) return PE_EINVAL;
+    HIP_TRY(s, hipSetDevice(s->device));
+    if (s->comm) {
+        (void)ncclCommDestroy(s->comm);
+        s->comm = nullptr;
+    }
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    const ncclResult_t r = ncclCommInitRank(&s->comm, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        s->comm = nullptr;
+        return s->fail(PE_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    s->nranks = nranks;
+    s->rank = rank;
+    if (!s->ev_x0) HIP_TRY(s, hipEventCreate(&s->ev_x0));
+    if (!s->ev_x1) HIP_TRY(s, hipEventCreate(&s->ev_x1));
+    return PE_OK;
+}
+
+// The full-pass count loop (limit >= list, affinity / spread task groups)
+// sharded over the communicator's ranks: every rank holds the whole snapshot
+// and sweeps rows [row_begin, row_end); per placement k_sweep writes the
+// rank's per-workgroup 80-byte records, one in-place ncclAllGather of them
+// over xGMI runs on the engine stream (an identity at one rank, skipped), and
+// k_sweep_step merges every rank's records,
+// resolves the winner, writes its record and commits
+// it on every rank. Nothing returns to the host between placements; the stop
+// flag is read every 64 placements.
+int pe_place_sharded(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_begin, uint32_t row_end,
+                     pe_ranked_node* out, uint32_t* placed) {
+    if (!s || (!out && count)) return PE_EINVAL;
+    if (!s->comm) return s->fail(PE_ESTATE, "pe_comm_init not called");
+    if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "sharded placement needs a generic stack");
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    s->gen++;
+    HIP_TRY(s, hipSetDevice(s->device));
+    if (row_begin > row_end || row_end > s->nodes.size()) return s->fail(PE_EINVAL, "bad shard row range");
+    rc = prepare_tg(s, tgi, s->visit, s->offset);
+    if (rc) return rc;
+    TgPlan& g = *s->tgs[tgi];
+    if (!tg_full_scan(s, g)) return s->fail(PE_EUNSUPPORTED, "sharded placement: a windowed task group (replicas only)");
+    if (!s->visit_unique) return s->fail(PE_EUNSUPPORTED, "sharded placement needs a list without repeated rows");
+    if (g.n_spread != (int)g.psets.size() || g.psets_dynamic)
+        return s->fail(PE_EUNSUPPORTED, "sharded placement with distinct_property or cleared property values");
+    for (size_t k = 0; k < s->tgs.size(); k++)
+        if (k != tgi && s->tgs[k]->name == g.name)
+            return s->fail(PE_EUNSUPPORTED, "sharded placement: task groups sharing a name");
+    s->limit = 0x7FFFFFFF;
+    const uint32_t n = (uint32_t)s->visit.size();
+    pe::SweepArgs A;
+    uint32_t blocks = 0;
+    rc = sweep_setup(s, g, nullptr, row_begin, row_end, &A, &blocks);
+    if (rc) return rc;
+    // every rank launches the same number of workgroups (sized for the
+    // largest range) so that the all-gather moves equal slices: rank r's
+    // workgroup records land in d_gather[r * blocks ...] and the step merges
+    // all nranks * blocks of them (no separate merge launch)
+    const uint32_t rows_max = (uint32_t)((s->nodes.size() + (size_t)s->nranks - 1) / (size_t)s->nranks);
+    blocks = std::max<uint32_t>(1, std::min<uint32_t>((rows_max + 255) / 256,
+                                                      (uint32_t)s->n_cu * (uint32_t)s->sweep_per_cu_aux));
+    const size_t slice = sizeof(pe::SweepRec) * blocks;
+    HIP_TRY(s, s->d_gather.ensure(slice * (size_t)s->nranks));
+    A.recs = reinterpret_cast<pe::SweepRec*>(static_cast<char*>(s->d_gather.p) + slice * (size_t)s->rank);
+    pe::SweepArgs A2 = A;   // the step merges the gathered records
+    A2.recs = s->d_gather.as<pe::SweepRec>();
+    const uint32_t nrecs = blocks * (uint32_t)s->nranks;
+    HIP_TRY(s, upload_visit(s, s->visit));
+    HIP_TRY(s, s->d_loop_out.ensure(sizeof(pe_ranked_node) * (size_t)(count + 1)));
+    HIP_TRY(s, s->d_loop_state.ensure(8 * sizeof(uint32_t)));
+    HIP_TRY(s, hipMemsetAsync(s->d_loop_state.p, 0, 8 * sizeof(uint32_t), s->stream));
+    uint32_t* state = s->d_loop_state.as<uint32_t>();
+    uint32_t h_state[5] = {0, 0, 0, 0, 0};
+    const uint32_t chunk = 64;
+    double x_us = 0;
+    uint32_t x_n = 0;
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    if (A.spread_tab) HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
+    for (uint32_t k = 0; k < count && !h_state[0]; k += chunk) {
+        const uint32_t m = std::min(chunk, count - k);
+        for (uint32_t j = 0; j < m; j++) {
+            HIP_TRY(s, pe_launch_sweep_only(&A, blocks, s->stream));
+            if (s->nranks > 1) {   // in place: this rank's slice already sits at its offset
+                if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x0, s->stream));
+                const ncclResult_t r = ncclAllGather(A.recs, s->d_gather.p, slice, ncclUint8, s->comm, s->stream);
+                if (r != ncclSuccess) return s->fail(PE_EHIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+                if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x1, s->stream));
+            }
+            HIP_TRY(s, pe_launch_step_only(&A2, nrecs, s->d_visit.as<uint32_t>(), n, s->offset,
+                                           s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
+        }
+        HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        float xms = 0;
+        if (m && s->nranks > 1 && hipEventElapsedTime(&xms, s->ev_x0, s->ev_x1) == hipSuccess) {
+            x_us += xms * 1e3;
+            x_n++;
+        }
+    }
+    s->last_exchange_us = x_n ? x_us / x_n : 0.0;
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    const uint32_t p = h_state[1];
+    const uint32_t nrec = std::min(count, p + (h_state[0] ? 1u : 0u));
+    if (nrec)
+        HIP_TRY(s, hipMemcpyAsync(out, s->d_loop_out.p, sizeof(pe_ranked_node) * nrec, hipMemcpyDeviceToHost,
+                                  s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    s->last_ms_pending = false;
+    for (uint32_t i = 0; i < p; i++) s->plan.emplace_back(g.name, (uint32_t)out[i].row);   // Plan.AppendAlloc
+    invalidate_job_distinct(s, tgi);
+    s->offer_row = -1;
+    if (placed) *placed = p;
+    return PE_OK;
+}
+
+double pe_last_exchange_us(const pe_stack* s) { return s ? s->last_exchange_us : 0.0; }
 
 int pe_speculation_stats(const pe_stack* s, uint64_t* out4) {
     if (!s || !out4) return PE_EINVAL;

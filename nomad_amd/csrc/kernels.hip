@@ -2682,6 +2682,20 @@ hipError_t pe_launch_sweep_step(const pe::SweepArgs* a, uint32_t blocks, const u
     return hipGetLastError();
 }
 
+// The sweep alone (per-workgroup records into a->recs, no merge).
+hipError_t pe_launch_sweep_only(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st) {
+    if (a->node_aux) hipLaunchKernelGGL((pe::k_sweep<256, false, 0, true>), dim3(blocks), dim3(256), 0, st, *a);
+    else hipLaunchKernelGGL((pe::k_sweep<256, false>), dim3(blocks), dim3(256), 0, st, *a);
+    return hipGetLastError();
+}
+
+// The step alone (sharded loop: its records are the ranks' gathered ones).
+hipError_t pe_launch_step_only(const pe::SweepArgs* a, uint32_t nrecs, const uint32_t* visit, uint32_t n,
+                               uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st) {
+    hipLaunchKernelGGL(pe::k_sweep_step, dim3(1), dim3(256), 0, st, *a, nrecs, visit, n, offset, out, state);
+    return hipGetLastError();
+}
+
 // The persistent loop; `blocks` must all be resident (the host keeps it at
 // most one workgroup per CU). state[0..4] zeroed by the caller.
 hipError_t pe_launch_sweep_loop(const pe::SweepArgs* a, uint32_t blocks, uint32_t count, const uint32_t* visit,

@@ -15,7 +15,11 @@ state, ~64 B per node in HBM); what is split is the work:
 * Windowed binpack (limit = ceil(log2 n)) does not shard: ranks run replicas.
 
 The collective is torch.distributed's all_gather: RCCL over xGMI on GPU tensors
-(backend "nccl"), gloo on CPU tensors for the multi-process CPU tests.
+(backend "nccl"), gloo on CPU tensors for the multi-process CPU tests. On GPUs
+the whole sharded count loop also runs inside the engine (`device_place`,
+pe_place_sharded): the engine's own RCCL communicator all-gathers the records
+on the engine stream between k_sweep and k_sweep_step, so no placement returns
+to the host.
 """
 from __future__ import annotations
 
@@ -80,6 +84,27 @@ class ShardedFullScan:
                 break
             self.stack.Commit(tg, r.row)
         return out
+
+
+def comm_init(stack, dist=None):
+    """Join every rank's engine into one RCCL communicator: rank 0 draws the
+    unique id (pe_comm_unique_id) and torch.distributed broadcasts it."""
+    from .stack import comm_unique_id
+    world = dist.get_world_size() if dist is not None else 1
+    rank = dist.get_rank() if dist is not None else 0
+    uid = comm_unique_id() if rank == 0 else bytes(128)
+    if world > 1:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    stack.CommInit(world, rank, uid)
+    return rank, world
+
+
+def device_place(stack, tg, count: int, n_rows: int, rank: int, world: int):
+    """The sharded full-pass count loop inside the engine (pe_place_sharded)."""
+    b, e = shard_range(n_rows, rank, world)
+    return stack.PlaceSharded(tg, count, b, e)
 
 
 def system_place_sharded(stack, rows: Sequence[int], rank: int, world: int, tg=0):

@@ -66,6 +66,15 @@ def load_engine():
                                         C.POINTER(abi.pe_shard_rec)]
         lib.pe_speculation_stats.restype = C.c_int
         lib.pe_speculation_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        lib.pe_comm_unique_id.restype = C.c_int
+        lib.pe_comm_unique_id.argtypes = [abi.u8p, C.c_size_t]
+        lib.pe_comm_init.restype = C.c_int
+        lib.pe_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, abi.u8p]
+        lib.pe_place_sharded.restype = C.c_int
+        lib.pe_place_sharded.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.POINTER(abi.pe_ranked_node), abi.u32p]
+        lib.pe_last_exchange_us.restype = C.c_double
+        lib.pe_last_exchange_us.argtypes = [C.c_void_p]
         lib.pe_select_merge.restype = C.c_int
         lib.pe_select_merge.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(abi.pe_shard_rec), C.c_uint32,
                                         C.POINTER(abi.pe_ranked_node)]
@@ -406,6 +415,27 @@ class GenericStack(_Stack):
         self._check(self._lib.pe_select_merge(self._h, self._tg_index(tg), arr, len(recs), C.byref(out)))
         return RankedNode.from_c(out, self.nodes)
 
+    def CommInit(self, nranks: int, rank: int, unique_id: bytes):
+        """Join the RCCL communicator of `nranks` engines (pe_comm_init); every
+        rank passes the same 128-byte id (comm_unique_id on one rank)."""
+        buf = np.frombuffer(bytes(unique_id), dtype=np.uint8).copy()
+        self._check(self._lib.pe_comm_init(self._h, nranks, rank, buf.ctypes.data_as(abi.u8p)))
+
+    def PlaceSharded(self, tg, count: int, row_begin: int, row_end: int) -> List[RankedNode]:
+        """The full-pass count loop over the communicator's ranks, this rank
+        sweeping snapshot rows [row_begin, row_end) (pe_place_sharded); every
+        rank returns the same records."""
+        out = (abi.pe_ranked_node * max(1, count))()
+        placed = C.c_uint32(0)
+        self._check(self._lib.pe_place_sharded(self._h, self._tg_index(tg), count, row_begin, row_end, out,
+                                               C.byref(placed)))
+        n = min(count, placed.value + 1)
+        return [RankedNode.from_c(out[i], self.nodes) for i in range(n)]
+
+    def last_exchange_us(self) -> float:
+        """Device time of one all-gather in the last PlaceSharded (us)."""
+        return self._lib.pe_last_exchange_us(self._h)
+
     def SpeculationStats(self):
         """(runs, Selects answered from records, rollbacks, records computed) of
         the speculative count loop behind Select / Commit (pe_speculation_stats)."""
@@ -425,6 +455,16 @@ class GenericStack(_Stack):
     def last_sweep_bytes(self) -> int:
         """Algorithmic bytes per node of the last full-scan sweep Select."""
         return self._lib.pe_last_sweep_bytes(self._h)
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId through the engine (pe_comm_unique_id): 128 bytes that
+    rank 0 hands to every rank's CommInit."""
+    buf = np.zeros(128, dtype=np.uint8)
+    rc = load_engine().pe_comm_unique_id(buf.ctypes.data_as(abi.u8p), 128)
+    if rc:
+        raise RuntimeError("pe_comm_unique_id failed (%d)" % rc)
+    return buf.tobytes()
 
 
 class SystemStack(_Stack):

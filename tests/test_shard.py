@@ -184,3 +184,38 @@ def test_plan_apply_sharded_equals_single():
     ids, fits, why = O.evaluate_plan_placements(O.Snapshot(nodes, allocs), plan)
     assert merged == {nid: (f, w) for nid, f, w in zip(ids, fits, why)}
     assert sum(len(part) for part in got) == len(ids)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,count", [(5000, 300), (20000, 120)])
+def test_engine_rccl_sharded_loop_matches_place(n, count):
+    """pe_place_sharded (RCCL all-gather of the records on the engine stream
+    between k_sweep and k_sweep_step) at one rank == pe_place's device loop ==
+    the oracle, record by record."""
+    from nomad_amd.stack import GenericStack
+    from oracle.oracle import OracleGenericStack
+    nodes, allocs = synth.cluster_c3(n, seed=23)
+    job = synth.job_c3(count)
+    perm = synth.shuffle(len(nodes), 9)
+    a, b = GenericStack(), GenericStack()
+    for st in (a, b):
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(list(perm))
+    rank, world = shard.comm_init(a)
+    assert (rank, world) == (0, 1)
+    got = shard.device_place(a, 0, count, len(nodes), rank, world)
+    ref = b.Place(0, count)
+
+    def key(r):
+        return (r.row, r.final_score, tuple(r.scores), r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted)
+    assert [key(r) for r in got] == [key(r) for r in ref]
+    if n <= 5000:
+        o = OracleGenericStack()
+        o.SetState(nodes, allocs)
+        o.SetJob(job)
+        o.SetNodes(list(perm))
+        assert [(r.row, r.final_score) for r in got] == [(r.row, r.final_score) for r in o.Place(0, count)]
+    # the plan is shared: the next Select on both handles agrees
+    x, y = a.SelectRaw(0), b.SelectRaw(0)
+    assert (x.row, x.final_score) == (y.row, y.final_score)
