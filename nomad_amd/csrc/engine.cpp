@@ -39,6 +39,10 @@ size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
+size_t pe_fullpass_lds_bytes(uint32_t n);
+hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
+                                  uint32_t count, pe_ranked_node* out, uint32_t* state, unsigned long long* prof,
+                                  hipStream_t st);
 hipError_t pe_launch_sweep_only(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t pe_launch_step_only(const pe::SweepArgs* a, uint32_t nrecs, const uint32_t* visit, uint32_t n,
                                uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
@@ -459,6 +463,8 @@ struct pe_stack {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     DevMem d_gather;
+    pe::SweepArgs h_full_args;   // k_fullpass_lds arguments (read through d_full_args)
+    DevMem d_full_args;
     hipEvent_t ev_x0 = nullptr, ev_x1 = nullptr;   // around one sampled all-gather per chunk
     double last_exchange_us = 0;
 
@@ -503,6 +509,7 @@ struct pe_stack {
 
 namespace {
 
+constexpr uint32_t kFullLdsMaxN = 32768;          // k_fullpass_lds tried up to this list length
 constexpr uint32_t kStalledFlag = 0x80000000u;   // k_chain cursor flag (kChainStalled)
 
 double now_us() {
@@ -3311,17 +3318,47 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, s->d_loop_state.ensure(8 * sizeof(uint32_t)));
     HIP_TRY(s, hipMemsetAsync(s->d_loop_state.p, 0, 8 * sizeof(uint32_t), s->stream));
     uint32_t* state = s->d_loop_state.as<uint32_t>();
-    uint32_t h_state[5] = {0, 0, 0, 0, 0};
+    uint32_t h_state[6] = {0, 0, 0, 0, 0, 0};
     const uint32_t chunk = 64;
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     // the first placement's spread table; each step rebuilds it for the next
     if (A.spread_tab) HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
+    // lists whose options fit one workgroup's LDS: the whole loop in one
+    // launch (k_fullpass_lds: 16 B of LDS per option, only the committed
+    // node refreshed); more options than entries -> state[5], the loops below
+    bool lds_loop = A.node_aux != nullptr && n <= kFullLdsMaxN && count > 0;
+    if (const char* e = std::getenv("PE_FULL_LDS")) lds_loop = lds_loop && std::atoi(e) != 0;
+    if (lds_loop) {
+        const bool fprof = std::getenv("PE_FULL_PROF") != nullptr;   // per-phase clocks of the loop
+        DevMem d_prof;
+        if (fprof) HIP_TRY(s, d_prof.ensure(8 * sizeof(unsigned long long)));
+        HIP_TRY(s, hipMemsetAsync(s->d_loop_out.p, 0, sizeof(pe_ranked_node) * (size_t)count, s->stream));
+        s->h_full_args = A;
+        HIP_TRY(s, s->d_full_args.ensure(sizeof(pe::SweepArgs)));
+        HIP_TRY(s, hipMemcpyAsync(s->d_full_args.p, &s->h_full_args, sizeof(pe::SweepArgs), hipMemcpyHostToDevice,
+                                  s->stream));
+        HIP_TRY(s, pe_launch_fullpass_lds(s->d_full_args.as<pe::SweepArgs>(), A.spread_tab ? A.tg.n_psets : 0,
+                                          s->d_visit.as<uint32_t>(), n, count, s->d_loop_out.as<pe_ranked_node>(),
+                                          state, fprof ? d_prof.as<unsigned long long>() : nullptr, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        if (fprof) {
+            unsigned long long h[8];
+            HIP_TRY(s, hipMemcpy(h, d_prof.p, sizeof(h), hipMemcpyDeviceToHost));
+            const double p = std::max<uint32_t>(1, h_state[1]);
+            std::fprintf(stderr, "k_fullpass_lds us/placement (wave 0): approx %.2f amax-reduce %.2f exact %.2f "
+                         "best-reduce %.2f barrier %.2f resolve %.2f winner+commit %.2f table %.2f\n",
+                         h[4] / 100.0 / p, h[5] / 100.0 / p, h[6] / 100.0 / p, h[7] / 100.0 / p, h[0] / 100.0 / p,
+                         h[1] / 100.0 / p, h[2] / 100.0 / p, h[3] / 100.0 / p);
+        }
+        if (h_state[5]) lds_loop = false;
+    }
     const char* pe_env = std::getenv("PE_LOOP_PERSISTENT");
     // measured slower than back-to-back launches (10k nodes: 38.4 vs 34.6 us,
     // 100k: 145 vs 91 us per placement: the agent-scope barrier fences cost
     // more than the launch gaps they remove), so it is opt-in
     const bool persistent = pe_env ? std::atoi(pe_env) != 0 : false;
-    if (persistent && count) {
+    if (persistent && count && !lds_loop) {
         // one launch for the whole loop: grid barriers between the sweep and
         // the step; at most one workgroup per CU so that all are resident
         const uint32_t pb = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)s->n_cu));
@@ -3335,7 +3372,7 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
             return s->fail(PE_EHIP, "persistent count loop: grid barrier timed out");
         }
     }
-    for (uint32_t k = 0; !persistent && k < count && !h_state[0]; k += chunk) {
+    for (uint32_t k = 0; !persistent && !lds_loop && k < count && !h_state[0]; k += chunk) {
         const uint32_t m = std::min(chunk, count - k);
         for (uint32_t j = 0; j < m; j++)
             HIP_TRY(s, pe_launch_sweep_step(&A, blocks, s->d_visit.as<uint32_t>(), n, s->offset,

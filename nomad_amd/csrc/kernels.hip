@@ -273,34 +273,60 @@ __device__ __forceinline__ void lookup_scores(const TgTables& t, const uint32_t*
 
 // Scoring half: scores in append order, summed left to
 // right, then ScoreNormalizationIterator.
+// The scores before the spread one, summed left to right; k = how many.
 template <bool kKeepParts>
-__device__ __forceinline__ void score_option(const Ask& a, double log10, const ScoreIn& si, NodeEval* out) {
+__device__ __forceinline__ double score_head(const Ask& a, double log10, const ScoreIn& si, double* parts,
+                                             uint32_t& k_out) {
     const uint32_t coll = si.coll;
     const double fit = gm::fit_score(si.ccpu, si.cmem, si.ucpu, si.umem, a.algo_spread, log10);
     double sum = fit;
     uint32_t k = 1;
-    if (kKeepParts) out->parts[0] = fit;
+    if (kKeepParts) parts[0] = fit;
     if (a.dev_tw != 0.0) {   // device affinity (rank.go:518-523)
         sum += si.dev_aff;
-        if (kKeepParts) out->parts[k] = si.dev_aff;
+        if (kKeepParts) parts[k] = si.dev_aff;
         k++;
     }
     if (a.anti_aff && coll > 0) {   // JobAntiAffinityIterator (rank.go:588-591)
         const double pen = -1 * (double)(coll + 1) / (double)a.desired_count;
         sum += pen;
-        if (kKeepParts) out->parts[k] = pen;
+        if (kKeepParts) parts[k] = pen;
         k++;
     }
     if (si.penalty) {   // NodeReschedulingPenaltyIterator (rank.go:632-635)
         sum += -1.0;
-        if (kKeepParts) out->parts[k] = -1.0;
+        if (kKeepParts) parts[k] = -1.0;
         k++;
     }
     if (si.aff != 0.0) {   // NodeAffinityIterator (rank.go:698-725)
         sum += si.aff;
-        if (kKeepParts) out->parts[k] = si.aff;
+        if (kKeepParts) parts[k] = si.aff;
         k++;
     }
+    k_out = k;
+    return sum;
+}
+
+// The normalised score; with kKeepParts the parts go to `parts` (any
+// address space: a runtime index into a stack array would live in scratch).
+template <bool kKeepParts>
+__device__ __forceinline__ double score_into(const Ask& a, double log10, const ScoreIn& si, double* parts,
+                                             uint32_t* nscores) {
+    uint32_t k;
+    double sum = score_head<kKeepParts>(a, log10, si, parts, k);
+    if (si.spread != 0.0) {   // SpreadIterator (spread.go:110-174)
+        sum += si.spread;
+        if (kKeepParts) parts[k] = si.spread;
+        k++;
+    }
+    *nscores = k;
+    return sum / (double)k;   // ScoreNormalizationIterator (rank.go:762-767)
+}
+
+template <bool kKeepParts>
+__device__ __forceinline__ void score_option(const Ask& a, double log10, const ScoreIn& si, NodeEval* out) {
+    uint32_t k;
+    double sum = score_head<kKeepParts>(a, log10, si, out->parts, k);
     if (si.spread != 0.0) {   // SpreadIterator (spread.go:110-174)
         sum += si.spread;
         if (kKeepParts) out->parts[k] = si.spread;
@@ -2213,16 +2239,24 @@ __global__ void __launch_bounds__(256) k_spread_table(TgTables t, double* tab) {
     build_spread_table<256>(t, counts, tab, scratch);
 }
 
+// Score parts of the winner straight into its record (eval_node<true> with
+// the parts in the record, not in a stack array, which would live in scratch).
+__device__ __forceinline__ void record_winner(const SweepArgs& A, uint32_t row, pe_ranked_node* o) {
+    NodeIn in;
+    load_node(A.soa, A.tg, row, in);
+    ScoreIn si;
+    (void)status_loaded(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, row, in, &si, A.spread_tab);
+    lookup_scores(A.tg, A.penalty_bits, A.spread_tab, row, in.r.cls, &si);
+    for (int k = 0; k < PE_MAX_SCORES; k++) o->scores[k] = 0.0;
+    uint32_t ns;
+    o->final_score = score_into<true>(A.ask, A.log10, si, o->scores, &ns);
+    o->n_scores = ns;
+}
+
 // Score parts of one node (the winner's RankedNode record).
 __global__ void k_node_record(SweepArgs A, uint32_t row, pe_ranked_node* out) {
     if (threadIdx.x != 0) return;
-    Overlay none;
-    none.keys = nullptr;
-    NodeEval ev;
-    eval_node<true>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, A.spread_tab, row, &ev);
-    out->final_score = ev.score;
-    out->n_scores = ev.nscores;
-    for (int k = 0; k < PE_MAX_SCORES; k++) out->scores[k] = k < (int)ev.nscores ? ev.parts[k] : 0.0;
+    record_winner(A, row, out);
     record_offers(A.soa, A.ask, A.tg, row, 0u, out);
 }
 
@@ -2262,15 +2296,8 @@ __device__ __forceinline__ void step_block(const SweepArgs& A, uint32_t nrecs, c
                 uint32_t pos = offset + rank;
                 if (pos >= n) pos -= n;
                 const uint32_t row = visit[pos];
-                Overlay none;
-                none.keys = nullptr;
-                NodeEval ev;
-                eval_node<true>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, A.spread_tab, row,
-                                &ev);
                 o->row = (int32_t)row;
-                o->final_score = ev.score;
-                o->n_scores = ev.nscores;
-                for (int k = 0; k < PE_MAX_SCORES; k++) o->scores[k] = k < (int)ev.nscores ? ev.parts[k] : 0.0;
+                record_winner(A, row, o);
                 record_offers(A.soa, A.ask, A.tg, row, 0u, o);
                 uint32_t offers = 0xFFFFFFFFu;
                 if (o->n_device_offers) {
@@ -2296,6 +2323,358 @@ __device__ __forceinline__ void step_block(const SweepArgs& A, uint32_t nrecs, c
 __global__ void __launch_bounds__(256) k_sweep_step(SweepArgs A, uint32_t nrecs, const uint32_t* visit, uint32_t n,
                                                     uint32_t offset, pe_ranked_node* out, uint32_t* state) {
     step_block(A, nrecs, visit, n, offset, out, state);
+}
+
+// The whole full-pass count loop in one workgroup, for lists whose options
+// fit LDS. A commit changes only the committed node's own inputs (use,
+// collisions, devices, distinct_hosts) and the spread boosts (one value per
+// property value), and a node that is filtered or exhausted stays so while
+// the loop only adds allocations. So the workgroup evaluates the list once
+// and keeps one LDS entry per option: its visit position, status, the sum of
+// its scores before the spread one (score_head: binpack, device affinity,
+// anti-affinity, penalty, affinity, summed left to right) and its spread
+// property values. A placement then reads 16 bytes of LDS per option, adds
+// the spread boost and normalises exactly as score_option does. The maximum
+// is found on approximate scores (sum x 1/k, within 2^-52 relative of
+// sum / k): only the options within a 2^-48 margin of a wave's maximum take
+// the exact quotient, and (max score, earliest rank) is reduced over those;
+// a non-positive maximum takes the exact LimitIterator skip record instead
+// (rec_add / rec_winner). Two lanes of wave 0 then
+// load the winner once and evaluate it side by side: lane 0 as it stands
+// (dk = 0: the placement's record, parts written straight into it), lane 1
+// with the placement added (dk = 1: the option's new entry, as the overlay
+// chain does); lane 0 commits to the SoA and, for target spreads, refreshes
+// the one boost per property whose count moved (even spreads rebuild the
+// table). One launch for the whole loop; results equal `count` x (k_sweep +
+// k_sweep_step). More options than entries: state[5] = 1 before any commit
+// and the host runs the multi-workgroup loop instead. The arguments come
+// through a device buffer: the TgTables arrays are indexed by property at
+// run time, which would copy a by-value argument to scratch.
+}  // namespace pe
+// ROCm device library wave reduction (DPP), also behind __reduce_max_sync
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_max_f64(double);
+namespace pe {
+
+constexpr int kFullThreads = 1024;
+constexpr int kFullWaves = kFullThreads / 64;
+constexpr int kFullPer = 9;                               // entries per thread
+constexpr uint32_t kFullCap = kFullThreads * kFullPer;    // LDS entries (16 B each)
+
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const unsigned long long u = __double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+template <int NP>   // spread properties scored (A.spread_tab ? n_psets : 0), at most kAuxPsets
+__global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* __restrict__ Ap, const uint32_t* visit,
+                                                               uint32_t n, uint32_t count, pe_ranked_node* out,
+                                                               uint32_t* state, unsigned long long* prof) {
+    const SweepArgs& A = *Ap;
+    extern __shared__ double ent_sum[];                                    // [kFullCap] score_head sums
+    uint32_t* ent_meta = reinterpret_cast<uint32_t*>(ent_sum + kFullCap);   // status | k << 2 | spread values
+    uint32_t* ent_pos = ent_meta + kFullCap;                                // visit position
+    __shared__ double tab[kAuxPsets * (kMaxValues + 1)];
+    __shared__ double desired[kAuxPsets * kMaxValues];
+    __shared__ uint32_t counts[kAuxPsets * kMaxValues];
+    __shared__ double aff_lds[kAuxValues];
+    __shared__ double red_s[kFullWaves];
+    __shared__ uint32_t red_r[kFullWaves];
+    __shared__ uint32_t red_f[kFullWaves], red_e[kFullWaves];
+    __shared__ SweepRec red[kFullWaves];
+    __shared__ uint32_t scratch[4];
+    __shared__ uint32_t sh_nf, sh_ne, sh_stop, sh_win, sh_m;
+    __shared__ double parts1[PE_MAX_SCORES];   // lane 1's parts (unused)
+    __shared__ double rcp_k[8];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const TgTables& t = A.tg;
+    constexpr int np = NP;
+    const uint32_t off = A.offset;
+    bool any_even = false;
+    for (int p = 0; p < np; p++) any_even = any_even || t.pset_even[p];
+    for (int i = tid; i < kAuxValues; i += kFullThreads) aff_lds[i] = A.aff_vals[i];
+    if (tid < 8) rcp_k[tid] = tid ? 1.0 / (double)tid : 0.0;
+    if (tid == 0) sh_m = 0;
+    for (int p = 0; p < np; p++)
+        for (int v = tid; v < t.pset_nvals[p]; v += kFullThreads) {
+            counts[p * kMaxValues + v] = t.pset_counts[p][v];
+            desired[p * kMaxValues + v] = t.pset_even[p] ? 0.0 : t.pset_desired[p][v];
+        }
+    __syncthreads();
+    if (np) build_spread_table<kFullThreads>(t, counts, tab, scratch);
+    auto spread_of = [&](uint32_t meta) __attribute__((always_inline)) -> double {   // lookup_scores' total
+        double sp = 0.0;
+#pragma unroll
+        for (int p = 0; p < np; p++) {
+            const uint32_t v = (meta >> (8 + 8 * p)) & 255u;
+            sp += (v == kAuxMissing) ? -1.0 : tab[p * (kMaxValues + 1) + v];
+        }
+        return sp;
+    };
+    auto load = [&](uint32_t row, NodeIn& in) __attribute__((always_inline)) -> uint32_t {   // the sweep's AUX fetch
+        in.r = A.soa.rec[row];
+        in.coll_tg = t.coll_tg[row];
+        in.dev_free = t.dev_free ? t.dev_free[row] : 0u;
+        const uint32_t aux = A.node_aux[row];
+        in.feas = aux >> 31;
+        return aux;
+    };
+    // status and score_head of a loaded node with dk placements of this loop
+    // added; with a `parts` pointer the parts are written there
+    auto head = [&](uint32_t row, const NodeIn& in, uint32_t aux, uint32_t dk, double* parts, double* sum,
+                    uint32_t* kk) __attribute__((always_inline)) -> int {
+        ScoreIn si;
+        const int st = status_loaded(A.soa, t, t.class_ok, A.ask, dk, row, in, &si);
+        *kk = 0;
+        *sum = 0.0;
+        if (st == kOption) {
+            si.penalty = A.penalty_bits ? (A.penalty_bits[row >> 5] >> (row & 31)) & 1u : 0u;
+            si.aff = aff_lds[aux & 255u];
+            si.spread = 0.0;
+            *sum = parts ? score_head<true>(A.ask, A.log10, si, parts, *kk)
+                         : score_head<false>(A.ask, A.log10, si, nullptr, *kk);
+        }
+        return st;
+    };
+    // the final score of an entry (score_option's tail)
+    auto final_sum = [&](uint32_t e, uint32_t* kk_out) __attribute__((always_inline)) -> double {
+        const uint32_t meta = ent_meta[e];
+        double sum = ent_sum[e];
+        const double sp = spread_of(meta);
+        uint32_t kk = (meta >> 2) & 7u;
+        if (sp != 0.0) { sum += sp; kk++; }
+        *kk_out = kk;
+        return sum;
+    };
+    uint32_t nf = 0, ne = 0;
+    for (uint32_t pos = tid; pos < n; pos += kFullThreads) {
+        const uint32_t row = visit[pos];
+        NodeIn in;
+        const uint32_t aux = load(row, in);
+        double s;
+        uint32_t kk;
+        const int st = head(row, in, aux, 0u, nullptr, &s, &kk);
+        nf += st == kFiltered;
+        ne += st == kExhausted;
+        if (st == kOption) {
+            const uint32_t e = atomicAdd(&sh_m, 1u);
+            if (e < kFullCap) {
+                ent_sum[e] = s;
+                ent_meta[e] = (uint32_t)st | (kk << 2) | (aux & 0x00FFFF00u);
+                ent_pos[e] = pos;
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        nf += (uint32_t)__shfl_xor((int)nf, o);
+        ne += (uint32_t)__shfl_xor((int)ne, o);
+    }
+    if (lane == 0) { red_f[wid] = nf; red_e[wid] = ne; }
+    __syncthreads();
+    const uint32_t m = sh_m;
+    if (m > kFullCap) {   // uniform: nothing committed yet, the host takes the other loop
+        if (tid == 0) state[5] = 1;
+        return;
+    }
+    if (tid == 0) {
+        uint32_t a = 0, b = 0;
+        for (int w = 0; w < kFullWaves; w++) { a += red_f[w]; b += red_e[w]; }
+        sh_nf = a;
+        sh_ne = b;
+        sh_stop = 0;
+    }
+    __syncthreads();
+    auto rank_of_pos = [&](uint32_t pos) __attribute__((always_inline)) -> uint32_t {
+        return pos >= off ? pos - off : pos + n - off;
+    };
+    unsigned long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = prof ? wall_clock64() : 0;
+    auto mark = [&](int i) __attribute__((always_inline)) {
+        if (prof && tid == 0) {
+            const unsigned long long x = wall_clock64();
+            tp[i] += x - tl;
+            tl = x;
+        }
+    };
+    for (uint32_t it = 0; it < count; it++) {
+        double ap[kFullPer];
+        double amax = -__builtin_inff();
+#pragma unroll
+        for (int j = 0; j < kFullPer; j++) {
+            const uint32_t e = (uint32_t)tid + (uint32_t)j * kFullThreads;
+            ap[j] = -__builtin_inff();
+            if (e < m) {
+                uint32_t kk;
+                const double sum = final_sum(e, &kk);
+                if ((ent_meta[e] & 3u) == (uint32_t)kOption) ap[j] = sum * rcp_k[kk];
+            }
+            amax = ap[j] > amax ? ap[j] : amax;
+        }
+        mark(4);
+        amax = __ockl_wfred_max_f64(amax);
+        mark(5);
+        const double cut = amax - (__builtin_fabs(amax) * 0x1p-48 + 0x1p-1000);
+        double best = -__builtin_inff();
+        uint32_t best_rank = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < kFullPer; j++) {
+            const bool near = ap[j] >= cut && ap[j] != -__builtin_inff();   // options only
+            if (__ballot(near)) {
+                if (near) {
+                    const uint32_t e = (uint32_t)tid + (uint32_t)j * kFullThreads;
+                    uint32_t kk;
+                    const double sc = final_sum(e, &kk) / (double)kk;
+                    const uint32_t rk = rank_of_pos(ent_pos[e]);
+                    if (sc > best || (sc == best && rk < best_rank)) { best = sc; best_rank = rk; }
+                }
+            }
+        }
+        mark(6);
+        {   // the wave's (max, earliest rank) over its few candidate lanes
+            uint64_t cand = __ballot(best_rank != 0xFFFFFFFFu);
+            double wb = -__builtin_inff();
+            uint32_t wr = 0xFFFFFFFFu;
+            while (cand) {
+                const int l = __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const double b = readlane_f64(best, l);
+                const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)best_rank, l);
+                if (b > wb || (b == wb && r < wr)) { wb = b; wr = r; }
+            }
+            best = wb;
+            best_rank = wr;
+        }
+        mark(7);
+        if (lane == 0) { red_s[wid] = best; red_r[wid] = best_rank; }
+        __syncthreads();
+        mark(0);
+        // every wave resolves the block's winner itself (no second barrier)
+        best = lane < kFullWaves ? red_s[lane] : -__builtin_inff();
+        best_rank = lane < kFullWaves ? red_r[lane] : 0xFFFFFFFFu;
+        for (int o = kFullWaves / 2; o > 0; o >>= 1) {
+            const double ob = __shfl_xor(best, o);
+            const uint32_t orank = (uint32_t)__shfl_xor((int)best_rank, o);
+            if (ob > best || (ob == best && orank < best_rank)) { best = ob; best_rank = orank; }
+        }
+        best = __shfl(best, 0);
+        uint32_t win = (uint32_t)__shfl((int)best_rank, 0);
+        if (win != 0xFFFFFFFFu && !(best > 0.0)) {   // every option non-positive: the skip rule decides (rare)
+            SweepRec r;
+            rec_init(r);
+            for (uint32_t e = tid; e < m; e += kFullThreads) {
+                if ((ent_meta[e] & 3u) != (uint32_t)kOption) continue;
+                uint32_t kk;
+                const double sum = final_sum(e, &kk);
+                rec_add(r, rank_of_pos(ent_pos[e]), sum / (double)kk);
+            }
+            rec_block_reduce<kFullThreads>(r, red);
+            if (tid == 0) sh_win = rec_winner(r);
+            __syncthreads();
+            win = sh_win;
+        }
+        mark(1);
+        pe_ranked_node* o = out + it;
+        if (wid == 0 && win == 0xFFFFFFFFu) {
+            if (lane == 0) {
+                o->row = -1;
+                o->nodes_evaluated = n;            // a full pass pulls every node
+                o->nodes_filtered = sh_nf;
+                o->nodes_exhausted = sh_ne;
+                o->new_offset = off;
+                state[0] = 1;
+                sh_stop = 1;
+            }
+        } else if (wid == 0 && lane < 2) {
+            uint32_t pos = off + win;
+            if (pos >= n) pos -= n;
+            const uint32_t row = visit[pos];
+            // the winner's entry (the options are few per lane: scan for it)
+            NodeIn in;
+            const uint32_t aux = load(row, in);
+            double s;
+            uint32_t kk;
+            const int st = head(row, in, aux, (uint32_t)lane, lane == 0 ? o->scores : parts1, &s, &kk);
+            const int st1 = __shfl(st, 1);
+            const uint32_t meta0 = (aux & 0x00FFFF00u);   // spread values: the entry's
+            if (lane == 1) {
+                sh_win = (uint32_t)st | (kk << 2) | meta0;
+                parts1[0] = s;
+            } else {           // the placement's record, then the commit
+                const double sp = spread_of(meta0);
+                if (sp != 0.0) {   // SpreadIterator (spread.go:110-174)
+                    s += sp;
+                    o->scores[kk] = sp;
+                    kk++;
+                }
+                o->row = (int32_t)row;
+                o->final_score = s / (double)kk;   // ScoreNormalizationIterator (rank.go:762-767)
+                o->n_scores = kk;
+                o->nodes_evaluated = n;            // a full pass pulls every node
+                o->nodes_filtered = sh_nf;
+                o->nodes_exhausted = sh_ne;
+                o->new_offset = off;               // and leaves the cursor where it is
+                record_offers(A.soa, A.ask, t, row, 0u, o);
+                uint32_t offers = 0xFFFFFFFFu;
+                if (o->n_device_offers) {
+                    offers = 0;
+                    for (uint32_t q = 0; q < o->n_device_offers && q < 4; q++)
+                        offers |= (o->device_offer_group[q] & 255u) << (8 * q);
+                }
+                const bool fast = A.ask.n_dev == 0 && np == t.n_psets;
+                if (fast) {   // commit_row from the loaded values: stores only
+                    NodeRec& r = A.soa.rec[row];
+                    r.used_cpu = in.r.used_cpu + A.ask.cpu;
+                    r.used_mem = in.r.used_mem + A.ask.mem;
+                    r.used_disk = in.r.used_disk + A.ask.disk;
+                    r.used_mbits = in.r.used_mbits + A.ask.commit_mbits;
+                    r.used_dyn = in.r.used_dyn + A.ask.commit_dyn;
+                    A.soa.coll_job[row] += 1;
+                    t.coll_tg[row] = in.coll_tg + 1;
+                } else {
+                    commit_row(A.soa, t, A.ask, row, offers);
+                }
+#pragma unroll
+                for (int p = 0; p < np; p++) {
+                    const uint32_t v = (meta0 >> (8 + 8 * p)) & 255u;
+                    if (v == kAuxMissing) continue;
+                    const uint32_t c = ++counts[p * kMaxValues + v];
+                    if (fast) t.pset_counts[p][v] = c;
+                    if (!t.pset_even[p]) {       // build_spread_table's target boost of this value
+                        const double d = desired[p * kMaxValues + v];
+                        tab[p * (kMaxValues + 1) + v] = d != d ? -1.0 : ((d - (double)(c + 1u)) / d) *
+                                                                        t.pset_weight_frac[p];
+                    }
+                }
+                state[1] = it + 1;
+                sh_nf += st1 == kFiltered;
+                sh_ne += st1 == kExhausted;
+            }
+        }
+        mark(2);
+        __syncthreads();
+        if (sh_stop) break;
+        if (win != 0xFFFFFFFFu) {   // the winner's entry with this placement added
+            uint32_t pos = off + win;
+            if (pos >= n) pos -= n;
+#pragma unroll
+            for (int j = 0; j < kFullPer; j++) {
+                const uint32_t e = (uint32_t)tid + (uint32_t)j * kFullThreads;
+                if (e < m && ent_pos[e] == pos) {
+                    ent_sum[e] = parts1[0];
+                    ent_meta[e] = sh_win;
+                }
+            }
+        }
+        if (any_even) build_spread_table<kFullThreads>(t, counts, tab, scratch);
+        __syncthreads();
+        mark(3);
+    }
+    if (prof && tid == 0)
+        for (int i = 0; i < 8; i++) prof[i] = tp[i];
+    // the HBM table the next Select starts from
+    for (int p = 0; p < np; p++)
+        for (int v = tid; v < t.pset_nvals[p]; v += kFullThreads)
+            const_cast<double*>(A.spread_tab)[p * (kMaxValues + 1) + v] = tab[p * (kMaxValues + 1) + v];
 }
 
 // Grid-wide barrier of the persistent count loop (every workgroup resident;
@@ -2679,6 +3058,41 @@ hipError_t pe_launch_sweep_step(const pe::SweepArgs* a, uint32_t blocks, const u
     if (a->node_aux) hipLaunchKernelGGL((pe::k_sweep<256, false, 0, true>), dim3(blocks), dim3(256), 0, st, *a);
     else hipLaunchKernelGGL((pe::k_sweep<256, false>), dim3(blocks), dim3(256), 0, st, *a);
     hipLaunchKernelGGL(pe::k_sweep_step, dim3(1), dim3(256), 0, st, *a, blocks, visit, n, offset, out, state);
+    return hipGetLastError();
+}
+
+// The LDS-resident full-pass loop (one workgroup); dynamic LDS = 12 B per node.
+size_t pe_fullpass_lds_bytes(uint32_t) { return (size_t)pe::kFullCap * (sizeof(double) + 2 * sizeof(uint32_t)); }
+
+hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
+                                  uint32_t count, pe_ranked_node* out, uint32_t* state, unsigned long long* prof,
+                                  hipStream_t st) {
+    const size_t lds = pe_fullpass_lds_bytes(n);
+    static bool attr = false;
+    if (!attr) {
+        for (const void* f : {reinterpret_cast<const void*>(&pe::k_fullpass_lds<0>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_lds<1>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_lds<2>)}) {
+            const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)pe_fullpass_lds_bytes(0));
+            if (e != hipSuccess) return e;
+        }
+        attr = true;
+    }
+    switch (np) {
+        case 0:
+            hipLaunchKernelGGL(pe::k_fullpass_lds<0>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
+                               out, state, prof);
+            break;
+        case 1:
+            hipLaunchKernelGGL(pe::k_fullpass_lds<1>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
+                               out, state, prof);
+            break;
+        default:
+            hipLaunchKernelGGL(pe::k_fullpass_lds<2>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
+                               out, state, prof);
+            break;
+    }
     return hipGetLastError();
 }
 
