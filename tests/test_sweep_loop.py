@@ -66,6 +66,7 @@ def test_sweep_count_loop_devices():
 def test_persistent_count_loop_matches_oracle():
     # the opt-in persistent variant (one launch, grid barriers) gives the same placements
     os.environ["PE_LOOP_PERSISTENT"] = "1"
+    os.environ["PE_FULL_LDS"] = "0"   # the one-workgroup loop would take it first
     try:
         nodes, allocs = synth.cluster_c3(2500, seed=11)
         job = synth.job_c3(100)
@@ -73,5 +74,57 @@ def test_persistent_count_loop_matches_oracle():
         _, _, got = run_place(_engine_low_threshold, nodes, allocs, job, perm)
     finally:
         del os.environ["PE_LOOP_PERSISTENT"]
+        del os.environ["PE_FULL_LDS"]
+    _, _, want = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    assert_same_placements(got, want)
+
+
+# ---- the one-workgroup loop (k_fullpass_lds) against the oracle and the
+# multi-workgroup loop, over the job shapes that take its different branches
+
+def _c3_variant(kind, count):
+    from nomad_amd.structs import Affinity, Constraint, Spread, SpreadTarget
+    job = synth.job_c3(count)
+    if kind == "even":          # evenSpreadScoreBoost: the table is rebuilt every placement
+        job.spreads = [Spread("${node.datacenter}", 100, [])]
+    elif kind == "two":         # two spread properties (NP = 2)
+        job.spreads.append(Spread("${node.class}", 50, [SpreadTarget("c1", 40), SpreadTarget("c2", 20)]))
+    elif kind == "affinity":    # no spread (NP = 0)
+        job.spreads = []
+    elif kind == "distinct":    # distinct_hosts: a committed node leaves the options
+        job.constraints.append(Constraint("", "", "distinct_hosts"))
+    elif kind == "negative":    # every score <= 0: the LimitIterator skip rule decides
+        job.spreads = [Spread("${node.datacenter}", 100, [SpreadTarget("dc9", 100)])]
+        job.affinities = [Affinity("${node.class}", "c3", "!=", -100)]
+    return job
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["even", "two", "affinity", "distinct", "negative"])
+def test_one_workgroup_loop_variants(kind):
+    nodes, allocs = synth.cluster_c3(3000, seed=21)
+    job = _c3_variant(kind, 150)
+    perm = synth.shuffle(3000, 22)
+    _, _, got = run_place(_engine_low_threshold, nodes, allocs, job, perm)
+    _, _, want = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    assert_same_placements(got, want)
+    os.environ["PE_FULL_LDS"] = "0"
+    try:
+        _, _, multi = run_place(_engine_low_threshold, nodes, allocs, job, perm)
+    finally:
+        del os.environ["PE_FULL_LDS"]
+    assert_same_placements(multi, want)
+
+
+@pytest.mark.gpu
+def test_one_workgroup_loop_option_overflow():
+    # more options than LDS entries (9216): the kernel stops before any commit
+    # and the multi-workgroup loop places instead
+    from nomad_amd.structs import Affinity
+    nodes, allocs = synth.cluster_c2(12000, seed=23)
+    job = synth.job_c2(40)
+    job.affinities = [Affinity("${node.datacenter}", "dc1", "=", 30)]   # full pass
+    perm = synth.shuffle(12000, 24)
+    _, _, got = run_place(_engine_low_threshold, nodes, allocs, job, perm)
     _, _, want = run_place(OracleGenericStack, nodes, allocs, job, perm)
     assert_same_placements(got, want)
