@@ -227,6 +227,9 @@ struct ParsedConstraint {
     std::string op;
     bool escapes;
     std::string ltext, text;   // LTarget, Constraint.String() "l op r" (structs.go:8292)
+    // checkConstraint outcome per (left value, right value) pair of interned
+    // node values (see meets): nodes and classes share a handful of values
+    mutable std::unordered_map<uint64_t, uint8_t> memo;
 };
 
 struct ParsedAffinity {
@@ -646,9 +649,36 @@ ParsedConstraint parse_constraint(const pe_stack* s, const pe_constraint& c) {
     return p;
 }
 
+// The resolved target as a code: the interned value id, or a marker for a
+// literal (fixed per constraint), an absent value and a nil target.
+uint32_t target_code(const ParsedTarget& p, const NodeView& n) {
+    constexpr uint32_t kLiteral = 0xFFFFFFFCu, kAbsent = 0xFFFFFFFDu, kNil = 0xFFFFFFFEu;
+    switch (p.kind) {
+        case T_LITERAL: return kLiteral;
+        case T_ID: return n.h->id == PE_NONE ? kAbsent : n.h->id;
+        case T_DC: return n.h->dc == PE_NONE ? kAbsent : n.h->dc;
+        case T_NAME: return n.h->name == PE_NONE ? kAbsent : n.h->name;
+        case T_CLASS: return n.h->node_class == PE_NONE ? kAbsent : n.h->node_class;
+        case T_ATTR:
+        case T_META: {
+            uint32_t x;
+            if (p.key != PE_NONE && find_kv(p.kind == T_ATTR ? n.attrs : n.meta, p.key, &x)) return x;
+            return kAbsent;
+        }
+        default: return kNil;
+    }
+}
+
+// checkConstraint (feasible.go:783-846) on a node, memoised per pair of
+// resolved values: the outcome is a function of the two targets alone.
 bool meets(const pe_stack* s, pe::ConstraintEvaluator& ev, const ParsedConstraint& c, const NodeView& n) {
+    const uint64_t key = ((uint64_t)target_code(c.l, n) << 32) | target_code(c.r, n);
+    auto it = c.memo.find(key);
+    if (it != c.memo.end()) return it->second != 0;
     Target l = resolve(s, c.l, n), r = resolve(s, c.r, n);
-    return ev.check(c.op, l, r);
+    const bool ok = ev.check(c.op, l, r);
+    c.memo.emplace(key, ok ? 1 : 0);
+    return ok;
 }
 
 // ---- devices (host side) ------------------------------------------------------
