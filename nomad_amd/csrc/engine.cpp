@@ -69,6 +69,8 @@ hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st);
 hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* status, double* score,
                             hipStream_t st);
 hipError_t pe_launch_resolve(const pe::EvictResolveArgs* r, hipStream_t st);
+hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st);
+uint32_t pe_ploop_max_n();
 hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
                                     uint32_t* dev_free, uint32_t* placed, hipStream_t st);
 hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
@@ -424,6 +426,7 @@ struct pe_stack {
     std::string metrics_text;
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
+    DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;  // device-resident parallel count loop (k_ploop)
 
     // Speculative count loop behind pe_select / pe_commit: the
     // first plain Select of a task group runs the device count loop for the
@@ -3327,6 +3330,116 @@ static int commit_preempt_impl(pe_stack* s, uint32_t tgi, int32_t row, const uin
 }
 
 
+// Device-resident count loop over sparse options (k_ploop): the parallel
+// Select loop of place_impl (plain Select, Preempt retry on nil, commit) as
+// one single-workgroup launch. Valid while a commit changes the outcome of
+// its own row only: no property sets (spread / distinct_property), a visit
+// list without repeated rows, no max_parallel penalty (the plan's preemption
+// counts would reach other nodes' eviction choices). *handled = false leaves
+// the loop to the host-driven path (nothing committed).
+static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count, bool retry,
+                            pe_ranked_node* out, uint32_t* placed, bool* handled) {
+    *handled = false;
+    *placed = 0;
+    const uint32_t n = (uint32_t)s->visit.size();
+    if (!count || (std::getenv("PE_PLOOP") && std::getenv("PE_PLOOP")[0] == '0')) return PE_OK;
+    if (!g.psets.empty() || g.psets_dynamic || !s->visit_unique || n == 0 || n > pe_ploop_max_n()) return PE_OK;
+    for (size_t k = 0; k < s->tgs.size(); k++)
+        if (k != tgi && s->tgs[k]->name == g.name) return PE_OK;
+    if (retry && !s->preempt_unsupported.empty()) return PE_OK;
+    pe::BatchArgs A = batch_args(s, g);
+    HIP_TRY(s, upload_visit(s, s->visit));
+    A.perms = s->d_visit.as<uint32_t>();
+    A.n_visit = n;
+    HIP_TRY(s, s->d_ev_status_p.ensure(n));
+    HIP_TRY(s, s->d_ev_score_p.ensure(sizeof(double) * n));
+    HIP_TRY(s, s->d_ev_status.ensure(n));
+    HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * n));
+    HIP_TRY(s, s->d_ev_out.ensure(16));
+    HIP_TRY(s, s->d_ev_flags.ensure(16));
+    HIP_TRY(s, s->d_loop_out.ensure(sizeof(pe_ranked_node) * (size_t)count));
+    HIP_TRY(s, s->d_ploop_mask.ensure(sizeof(uint32_t) * (size_t)count));
+    HIP_TRY(s, s->d_loop_state.ensure(8 * sizeof(uint32_t)));
+    HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
+    HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
+    HIP_TRY(s, hipMemsetAsync(s->d_loop_state.p, 0, 8 * sizeof(uint32_t), s->stream));
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->d_ev_status_p.as<uint8_t>(),
+                                s->d_ev_score_p.as<double>(), s->stream));
+    pe::PLoopArgs L;
+    std::memset(&L, 0, sizeof(L));
+    L.P = preempt_args(s, g);
+    L.P.visit = s->d_visit.as<uint32_t>();
+    L.P.n_visit = n;
+    L.P.status = s->d_ev_status.as<uint8_t>();
+    L.P.score = s->d_ev_score.as<double>();
+    L.P.flags = s->d_ev_flags.as<uint32_t>();
+    if (retry) {
+        HIP_TRY(s, s->d_ev_dep.ensure(n));
+        L.P.dep_out = s->d_ev_dep.as<uint8_t>();
+        L.dep_init = L.P.dep_out;
+        HIP_TRY(s, pe_launch_evict_only(&L.P, s->stream));
+        L.P.dep_out = nullptr;
+        uint32_t flags = 0;
+        HIP_TRY(s, hipMemcpyAsync(&flags, L.P.flags, sizeof(flags), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        if (flags & 1u) return PE_OK;   // a node outside the device limits: the host path reports it when reached
+    } else {
+        HIP_TRY(s, hipMemsetAsync(L.P.status, 3, n, s->stream));
+    }
+    L.st_plain = s->d_ev_status_p.as<uint8_t>();
+    L.sc_plain = s->d_ev_score_p.as<double>();
+    L.preempted = s->d_preempted.as<uint8_t>();
+    L.pcount = s->d_pcount.as<uint32_t>();
+    L.dev_free = s->d_dev_free.as<uint32_t>();
+    L.offset = s->offset % n;
+    L.limit = s->limit;
+    L.count = count;
+    L.retry = retry ? 1 : 0;
+    L.out = s->d_loop_out.as<pe_ranked_node>();
+    L.out_mask = s->d_ploop_mask.as<uint32_t>();
+    L.state = s->d_loop_state.as<uint32_t>();
+    HIP_TRY(s, pe_launch_ploop(&L, s->stream));
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    uint32_t st[4];
+    HIP_TRY(s, hipMemcpyAsync(st, L.state, sizeof(st), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    const uint32_t recs = std::min(st[3], count);
+    std::vector<uint32_t> masks(recs);
+    if (recs) {
+        HIP_TRY(s, hipMemcpyAsync(out, L.out, sizeof(pe_ranked_node) * recs, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(masks.data(), L.out_mask, sizeof(uint32_t) * recs, hipMemcpyDeviceToHost,
+                                  s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+    }
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    s->last_ms_pending = false;
+    *handled = true;
+    const uint32_t p = std::min(st[0], count);
+    for (uint32_t k = 0; k < recs; k++) std::memset(out[k].preempted, 0, sizeof(out[k].preempted));
+    for (uint32_t k = 0; k < p; k++) {
+        const uint32_t row = (uint32_t)out[k].row;
+        s->plan.emplace_back(g.name, row);
+        const uint32_t b = s->h_node_alloc_off[row];
+        for (uint32_t i = 0; i < 32; i++)
+            if ((masks[k] >> i) & 1u) {
+                if (out[k].n_preempted >= PE_MAX_PREEMPT)
+                    return s->fail(PE_EUNSUPPORTED, "more than PE_MAX_PREEMPT preempted allocs");
+                out[k].preempted[out[k].n_preempted++] = s->h_palloc_index[b + i];
+                s->h_preempted[b + i] = 1;
+            }
+    }
+    *placed = p;
+    s->offset = st[1];
+    if (st[2] == 1)
+        return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the on-device "
+                                        "alloc limits");
+    if (st[2] == 2) return s->fail(PE_EHIP, "k_ploop: the resolved winner is not an option");
+    return PE_OK;
+}
+
 // Device-resident full-pass count loop (see pe_place). Same results as
 // `count` x (run_sweep_select + pe_commit).
 static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count, pe_ranked_node* out,
@@ -3488,7 +3601,10 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
         parallel = cnt[0] == 0 || (uint64_t)std::min<uint32_t>(s->limit, nv) * nv / cnt[0] > kParallelWalk;
     }
     if (parallel) {
-        while (p < count) {
+        bool handled = false;
+        rc = ploop_count_loop(s, g, tgi, count, retry, out, &p, &handled);
+        if (rc) return rc;
+        while (!handled && p < count) {
             rc = run_parallel_select(s, g, &out[p], &no);
             if (rc) return rc;
             s->offset = no;

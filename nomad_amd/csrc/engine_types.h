@@ -232,6 +232,7 @@ struct PreemptArgs {
     uint32_t* mask_out;               // or null: preempted allocs (bits over the node's allocs)
     uint32_t* offers_out;             // or null: device offers, one byte per request
     uint32_t* flags;                  // [1] bit 0: a node exceeded the on-device limits
+    uint8_t* dep_out;                 // or null: per position, the outcome read the plan's preemption counts
 };
 
 // LimitIterator + MaxScoreIterator over per-position results.
@@ -240,6 +241,24 @@ struct EvictResolveArgs {
     const double* score;
     uint32_t n, offset, limit;
     int32_t* out;                     // [0] winner position (relative) or -1, [1] consumed, [2] filtered, [3] exhausted
+};
+
+// Device-resident count loop over sparse options (k_ploop): the plain Select
+// and its Preempt retry of every placement resolved in one workgroup from
+// per-position outcomes kept in LDS; only committed rows are re-evaluated.
+struct PLoopArgs {
+    PreemptArgs P;                    // P.status / P.score: evict outcomes by position (k_evict, refreshed lazily)
+    const uint8_t* st_plain;          // [n] plain outcomes by position (k_census)
+    const uint8_t* dep_init;          // [n] or null: Preempt outcomes that read the preemption counts (k_evict)
+    double* sc_plain;                 // [n] plain scores by position (rewritten for committed rows)
+    uint8_t* preempted;               // Plan.NodePreemptions flags (apply_preempt)
+    uint32_t* pcount;
+    uint32_t* dev_free;
+    uint32_t offset, limit, count;
+    int32_t retry;                    // selectNextOption: a nil plain Select retries with Preempt
+    pe_ranked_node* out;              // [count] records (a nil record ends the loop)
+    uint32_t* out_mask;               // [count] preempted allocs of each placement (bits over the node's allocs)
+    uint32_t* state;                  // [0] placements, [1] cursor, [2] error (1: node outside the device limits), [3] records
 };
 
 struct SystemArgs {

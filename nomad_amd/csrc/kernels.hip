@@ -3121,3 +3121,25 @@ hipError_t pe_launch_sweep_loop(const pe::SweepArgs* a, uint32_t blocks, uint32_
                            state);
     return hipGetLastError();
 }
+
+// Device-resident count loop over sparse options (one workgroup); dynamic LDS
+// = 2 bits per position for each of the two outcome passes.
+constexpr uint32_t kPLoopMaxN = 229376;   // 2 x 2 bits + 1 bit per position in 160 KB of LDS
+uint32_t pe_ploop_max_n() { return kPLoopMaxN; }
+static size_t pe_ploop_lds_bytes(uint32_t n) { return (2u * ((n + 15u) / 16u) + (n + 31u) / 32u) * sizeof(uint32_t); }
+
+hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st) {
+    const uint32_t n = a->P.n_visit;
+    if (n == 0 || n > kPLoopMaxN) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&pe::k_ploop),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)pe_ploop_lds_bytes(kPLoopMaxN));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const size_t lds = pe_ploop_lds_bytes(n);
+    hipLaunchKernelGGL(pe::k_ploop, dim3(1), dim3(pe::kPLoopBlock), lds, st, *a);
+    return hipGetLastError();
+}
