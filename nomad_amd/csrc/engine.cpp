@@ -359,7 +359,7 @@ struct pe_stack {
     std::vector<uint32_t> sig_rep, sig_cls;
     std::vector<std::vector<uint32_t>> class_sigs;
     // staged visit orders for pe_place_batch
-    DevMem d_orders, d_batch_out, d_batch_status, d_sys_score, d_sys_status;
+    DevMem d_orders, d_batch_out, d_batch_status, d_sys_out;
     // full-scan sweep path
     DevMem d_rank_of, d_sweep_recs, d_sweep_merged, d_spread_tab, d_record;
     uint32_t sweep_min = 1u << 15;     // visit lists at least this long use the multi-CU sweep
@@ -379,6 +379,7 @@ struct pe_stack {
     bool results_via_copy = false;     // PE_RESULTS_VIA_COPY=1: device buffer + one D2H copy
     pe::BatchArgs batch_A{};
     PinnedMem h_batch_out, h_batch_status;
+    PinnedMem h_sys_out;   // SystemStack results, staged for the caller's arrays
     PinnedMem h_place_out, h_place_status;   // single-evaluation count loop results (mapped)
     PinnedMem h_stage;                 // upload staging ring (upload_s)
     unsigned char* stage_dev = nullptr;   // the ring as seen from the device (k_upload reads it)
@@ -2777,9 +2778,28 @@ int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_
     ApiScope prof_(s, "set_nodes");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     if (!rows && n) return s->fail(PE_EINVAL, "null rows");
-    // validate before touching any state: a rejected list leaves the previous one in place
-    for (uint32_t i = 0; i < n; i++)
-        if (rows[i] >= s->nodes.size()) return s->fail(PE_EINVAL, "row out of range");
+    // validate before touching any state: a rejected list leaves the previous one
+    // in place. The same pass finds repeated rows (the chain and sweep loops and
+    // the system placement need a list without them).
+    if (s->seen_stamp.size() != s->nodes.size()) {
+        s->seen_stamp.assign(s->nodes.size(), 0);
+        s->seen_gen = 0;
+    }
+    if (++s->seen_gen == 0) {
+        std::fill(s->seen_stamp.begin(), s->seen_stamp.end(), 0);
+        s->seen_gen = 1;
+    }
+    bool unique = true;
+    {
+        const uint32_t nn = (uint32_t)s->nodes.size(), gen = s->seen_gen;
+        uint32_t* stamp = s->seen_stamp.data();
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t r = rows[i];
+            if (r >= nn) return s->fail(PE_EINVAL, "row out of range");
+            unique = unique && stamp[r] != gen;
+            stamp[r] = gen;
+        }
+    }
     {
         const int frc = spec_flush(s);
         if (frc) return frc;
@@ -2796,22 +2816,8 @@ int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_
     s->limit = lim;
     if (limit_out) *limit_out = lim;
     invalidate_tables(s);
-    // a list without repeated rows (the chain and sweep loops need one); the
-    // visit position of every row (rank_of) is built when a sweep needs it
-    if (s->seen_stamp.size() != s->nodes.size()) {
-        s->seen_stamp.assign(s->nodes.size(), 0);
-        s->seen_gen = 0;
-    }
-    if (++s->seen_gen == 0) {
-        std::fill(s->seen_stamp.begin(), s->seen_stamp.end(), 0);
-        s->seen_gen = 1;
-    }
-    s->visit_unique = true;
-    for (uint32_t i = 0; i < n; i++) {
-        uint32_t& st = s->seen_stamp[s->visit[i]];
-        if (st == s->seen_gen) s->visit_unique = false;
-        st = s->seen_gen;
-    }
+    // the visit position of every row (rank_of) is built when a sweep needs it
+    s->visit_unique = unique;
     s->rank_of_valid = false;
     return PE_OK;
 }
@@ -3399,6 +3405,12 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     L.out = s->d_loop_out.as<pe_ranked_node>();
     L.out_mask = s->d_ploop_mask.as<uint32_t>();
     L.state = s->d_loop_state.as<uint32_t>();
+    const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
+    if (prof) {
+        HIP_TRY(s, s->d_prof.ensure(8 * sizeof(unsigned long long)));
+        HIP_TRY(s, hipMemsetAsync(s->d_prof.p, 0, 8 * sizeof(unsigned long long), s->stream));
+        L.prof = s->d_prof.as<unsigned long long>();
+    }
     HIP_TRY(s, pe_launch_ploop(&L, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     uint32_t st[4];
@@ -3416,6 +3428,13 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
     s->last_ms_pending = false;
+    if (prof) {
+        unsigned long long h[8];
+        HIP_TRY(s, hipMemcpy(h, L.prof, sizeof(h), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "k_ploop: %u placements, %.3f ms total; us: plain resolve %.1f, refresh %.1f, preempt "
+                             "resolve %.1f, winner %.1f; refreshed %llu dirty + %llu pcount readers\n",
+                     st[0], ms, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[4], h[5]);
+    }
     *handled = true;
     const uint32_t p = std::min(st[0], count);
     for (uint32_t k = 0; k < recs; k++) std::memset(out[k].preempted, 0, sizeof(out[k].preempted));
@@ -4406,25 +4425,27 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     if (s->cfg.stack_kind != PE_STACK_SYSTEM) return s->fail(PE_ESTATE, "pe_system_place needs a system stack");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
+    // every node appears once (checked by SetNodes): the single-node Selects are independent
+    if (!s->visit_unique) return s->fail(PE_EUNSUPPORTED, "duplicate rows in the system placement list");
+    int rc;
     {
-        // every node appears once: the single-node Selects are independent
-        std::vector<uint8_t> seen(s->nodes.size(), 0);
-        for (uint32_t r : s->visit) {
-            if (seen[r]) return s->fail(PE_EUNSUPPORTED, "duplicate rows in the system placement list");
-            seen[r] = 1;
-        }
+        ApiScope prof_(s, "system.prepare_tg");
+        rc = prepare_tg(s, tgi, s->visit, 0);
     }
-    int rc = prepare_tg(s, tgi, s->visit, 0);
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     const uint32_t n = (uint32_t)s->visit.size();
+    ApiScope prof_run_(s, "system.upload+kernel+results");
     HIP_TRY(s, upload_visit(s, s->visit));
-    DevMem& d_score = s->d_sys_score;
-    DevMem& d_st = s->d_sys_status;
-    HIP_TRY(s, d_score.ensure(sizeof(double) * std::max<uint32_t>(n, 1)));
-    HIP_TRY(s, d_st.ensure(std::max<uint32_t>(n, 1)));
-    HIP_TRY(s, s->d_status.ensure(16));
-    HIP_TRY(s, hipMemsetAsync(s->d_status.p, 0, 16, s->stream));
+    // results: device buffers, one DMA each into page-locked staging (a kernel
+    // storing into mapped host memory runs 50x slower), then copied out
+    // one device block [scores | outcomes | placed], one DMA into page-locked staging
+    const size_t st_off = sizeof(double) * (size_t)n;
+    const size_t placed_off = st_off + (((size_t)n + 3) & ~(size_t)3);
+    HIP_TRY(s, s->d_sys_out.ensure(placed_off + 4));
+    HIP_TRY(s, s->h_sys_out.ensure(placed_off + 4));
+    uint8_t* dsys = s->d_sys_out.as<uint8_t>();
+    HIP_TRY(s, hipMemsetAsync(dsys + placed_off, 0, 4, s->stream));
     pe::SystemArgs A;
     std::memset(&A, 0, sizeof(A));
     A.soa = soa_of(s);
@@ -4433,9 +4454,9 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     A.list = s->d_visit.as<uint32_t>();
     A.n_list = n;
     A.log10 = s->log10;
-    A.out_score = d_score.as<double>();
-    A.out_status = d_st.as<uint8_t>();
-    A.placed = s->d_status.as<uint32_t>();
+    A.out_score = reinterpret_cast<double*>(dsys);
+    A.out_status = dsys + st_off;
+    A.placed = reinterpret_cast<uint32_t*>(dsys + placed_off);
     // distinct_property couples the nodes through the value counts: the kernel
     // evaluates every node without it and without committing, the host then
     // walks the list in order (DistinctPropertyIterator before BinPack)
@@ -4445,11 +4466,24 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     HIP_TRY(s, pe_launch_system(&A, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
-    uint32_t p = 0;
-    HIP_TRY(s, hipMemcpyAsync(&p, A.placed, sizeof(p), hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(s, hipMemcpyAsync(out_score, A.out_score, sizeof(double) * n, hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(s, hipMemcpyAsync(out_status, A.out_status, n, hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    {
+        ApiScope prof_k_(s, "system.kernel_sync");
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+    }
+    {
+        ApiScope prof_d_(s, "system.d2h");
+        HIP_TRY(s, hipMemcpyAsync(s->h_sys_out.p, dsys, placed_off + 4, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+    }
+    uint32_t p;
+    {
+        ApiScope prof_c_(s, "system.copy_out");
+        const uint8_t* h = s->h_sys_out.as<uint8_t>();
+        std::memcpy(&p, h + placed_off, 4);
+        std::memcpy(out_score, h, sizeof(double) * n);
+        std::memcpy(out_status, h + st_off, n);
+    }
+    ApiScope prof_p_(s, "system.plan");
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
@@ -4460,7 +4494,19 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
         if (placed) *placed = p;
         return PE_OK;
     }
-    for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) s->plan.emplace_back(g.name, s->visit[i]);
+    {
+        // Plan.AppendAlloc of every placed node, branch-free (one slot of slack)
+        const size_t base = s->plan.size();
+        s->plan.resize(base + p + 1);
+        std::pair<uint32_t, uint32_t>* w = s->plan.data() + base;
+        const uint32_t nm = g.name;
+        for (uint32_t i = 0; i < n; i++) {
+            w->first = nm;
+            w->second = s->visit[i];
+            w += out_status[i] == 0;
+        }
+        s->plan.resize(base + p);
+    }
     if (s->cfg.preempt) {
         // BinPack with evict (stack.go:267-278) on the nodes the plain fit exhausted
         std::vector<uint32_t> pos, rows;
@@ -4504,6 +4550,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
                 HIP_TRY(s, s->d_ev_offers.ensure(sizeof(uint32_t) * E));
                 HIP_TRY(s, s->d_ev_flags.ensure(16));
                 HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
+                HIP_TRY(s, s->d_status.ensure(16));
                 HIP_TRY(s, hipMemsetAsync(s->d_status.p, 0, 16, s->stream));
                 P.visit = s->d_ev_rows.as<uint32_t>();
                 P.n_visit = E;

@@ -259,6 +259,8 @@ struct PLoopArgs {
     pe_ranked_node* out;              // [count] records (a nil record ends the loop)
     uint32_t* out_mask;               // [count] preempted allocs of each placement (bits over the node's allocs)
     uint32_t* state;                  // [0] placements, [1] cursor, [2] error (1: node outside the device limits), [3] records
+    unsigned long long* prof;         // [6] or null (PE_PLACE_PROF): wall-clock ticks of the plain resolve, refresh,
+                                      // Preempt resolve, winner; refreshed dirty rows, refreshed pcount readers
 };
 
 struct SystemArgs {

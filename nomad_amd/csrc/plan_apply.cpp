@@ -9,6 +9,7 @@
 // SetNode emulation (its collide flag and the reserved (IP, port) set), and the
 // flattening of allocs into 32-byte records plus 64-bit keys. Every fit
 // decision is made by k_plan_eval on the device (plan_kernels.hip).
+#include <chrono>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -446,8 +447,12 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     if (!p || !plan || (plan->n_nodes && (!reason || !plan->node_row || !plan->place_off))) return PE_EINVAL;
     if (!p->have_state) return p->fail(PE_ESTATE, "pe_planner_set_state not called");
     if (hipSetDevice(p->device) != hipSuccess) return p->fail(PE_EHIP, "hipSetDevice");
+    const bool prof = getenv("PE_PLAN_PROF") != nullptr;
+    auto tnow = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double t[6] = {tnow(), 0, 0, 0, 0, 0};
     int rc = p->map_strings(strs);
     if (rc) return rc;
+    t[1] = tnow();
     const uint32_t np = plan->n_nodes;
     const pe_plan_alloc_table& pt = plan->allocs;
     if (np && plan->place_off[np] > pt.count) return p->fail(PE_EINVAL, "place_off exceeds plan allocs");
@@ -467,6 +472,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
         ar.bad_port = h.bad_port;
         pkeys.insert(pkeys.end(), h.keys.begin(), h.keys.end());
     }
+    t[2] = tnow();
     uint64_t scratch = 0, bytes = 0;
     for (uint32_t i = 0; i < np; i++) {
         pa::PlanNodeRec& r = pn[i];
@@ -517,6 +523,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
             if (scratch > 0xFFFFFFF0ull) return p->fail(PE_ENOMEM, "plan key scratch too large");
         }
     }
+    t[3] = tnow();
     hipError_t e;
     if ((e = p->upload(p->d_pn, pn.data(), pn.size() * sizeof(pa::PlanNodeRec))) != hipSuccess ||
         (e = p->upload(p->d_rm, rm.data(), rm.size() * 4)) != hipSuccess ||
@@ -526,6 +533,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
         (e = p->d_scratch.reserve(std::max<uint64_t>(scratch, 1) * 8)) != hipSuccess ||
         (e = p->d_reason.reserve(std::max<uint32_t>(np, 1))) != hipSuccess)
         return p->fail(PE_EHIP, std::string("planner plan upload: ") + hipGetErrorString(e));
+    t[4] = tnow();
     pa::PlanArgs a{};
     a.nodes = (const pa::NodeRec*)p->d_nodes.p;
     a.chunks = (const pa::Chunk*)p->d_chunks.p;
@@ -550,6 +558,11 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     (void)hipEventElapsedTime(&ms, p->e0, p->e1);
     p->last_ms = ms;
     p->last_bytes = bytes;
+    if (prof) {
+        t[5] = tnow();
+        fprintf(stderr, "planner evaluate us: strings %.1f flatten %.1f nodes %.1f upload %.1f kernel+reasons %.1f "
+                        "(kernel %.1f)\n", t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], ms * 1e3);
+    }
     uint32_t fit = 0;
     for (uint32_t i = 0; i < np; i++) fit += reason[i] == PE_PLAN_FIT;
     if (n_fit) *n_fit = fit;

@@ -348,8 +348,8 @@ class _Stack:
 
     def SystemPlace(self, tg):
         n = len(self._visit)
-        score = np.zeros(max(1, n), dtype=np.float64)
-        status = np.zeros(max(1, n), dtype=np.uint8)
+        score = np.empty(max(1, n), dtype=np.float64)
+        status = np.empty(max(1, n), dtype=np.uint8)
         placed = C.c_uint32(0)
         self._check(self._fn("system_place")(self._h, self._tg_index(tg), score.ctypes.data_as(abi.f64p),
                                              status.ctypes.data_as(abi.u8p), C.byref(placed)))
