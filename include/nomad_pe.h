@@ -510,7 +510,8 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
  * `keep[i]` != 0 selects plan node i (the caller passes the result it applied). */
 int pe_planner_commit(pe_planner* p, const pe_strtab* strs, const pe_plan* plan, const uint8_t* keep);
 /* Device time of the last evaluate (HIP events around the kernel) and its
- * algorithmic bytes (records and keys read + reasons written). */
+ * algorithmic bytes (records and keys read + reasons written), computed when
+ * asked against the current snapshot: ask before pe_planner_commit. */
 double pe_planner_kernel_ms(const pe_planner* p);
 uint64_t pe_planner_last_bytes(const pe_planner* p);
 uint32_t pe_planner_snapshot_allocs(const pe_planner* p);

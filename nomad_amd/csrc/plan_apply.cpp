@@ -127,7 +127,13 @@ struct pe_planner {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     std::string err;
     double last_ms = 0;
-    uint64_t last_bytes = 0;
+    // algorithmic bytes of the last evaluate, computed on request (pe_planner_last_bytes)
+    mutable uint64_t last_bytes = 0;
+    mutable bool bytes_valid = true;
+    std::vector<pa::PlanNodeRec> last_pn;
+    std::vector<uint32_t> last_rm;
+    std::vector<pa::AllocRec> last_pa;
+    uint64_t plan_bytes() const;
     bool have_state = false;
     int group = 4;    // lanes per plan node in k_plan_eval (PE_PLAN_GROUP: 4 / 8 / 16 / 64; 4 measured fastest)
 
@@ -168,6 +174,7 @@ struct pe_planner {
         if (have && t->count >= have && memcmp(t->offsets, xl_off.data(), (have + 1) * 4) == 0 &&
             memcmp(t->bytes, xl_bytes.data(), xl_bytes.size()) == 0)
             keep = have;
+        if (keep == t->count && have) return PE_OK;   // the same table as last call
         xl.resize(keep);
         xl.reserve(t->count);
         for (uint32_t i = (uint32_t)keep; i < t->count; i++)
@@ -385,6 +392,39 @@ struct pe_planner {
     }
 };
 
+// What k_plan_eval reads and writes for the last evaluated plan: 32 B plan
+// node record + 1 reason byte per plan node; with a placement on a known node
+// its 64 B record; when the fit check runs the node's static keys, every
+// snapshot / chunk alloc record of the node (32 B), the keys of those still
+// counted, 4 B per removal and each plan alloc with its keys.
+// Computed on the host when asked, against the current snapshot.
+uint64_t pe_planner::plan_bytes() const {
+    uint64_t bytes = 0;
+    for (const pa::PlanNodeRec& r : last_pn) {
+        bytes += sizeof(pa::PlanNodeRec) + 1;
+        if (r.place_cnt == 0 || r.row == pa::kNone || r.row >= nodes.size()) continue;
+        const pa::NodeRec& nd = nodes[r.row];
+        bytes += sizeof(pa::NodeRec);
+        if (!nd.ready || !nd.eligible) continue;
+        bytes += 8ull * nd.n_keys + sizeof(pa::AllocRec) * (uint64_t)nd.alloc_cnt + 4ull * r.rm_cnt;
+        auto count_range = [&](uint32_t off, uint32_t cnt) {
+            for (uint32_t q = off; q < off + cnt && q < pool.size(); q++) {
+                const bool gone = pool[q].terminal ||
+                                  std::binary_search(last_rm.begin() + r.rm_off, last_rm.begin() + r.rm_off + r.rm_cnt, q);
+                if (!gone) bytes += 8ull * pool[q].n_keys;
+            }
+        };
+        count_range(nd.alloc_off, nd.alloc_cnt);
+        for (uint32_t c = nd.ext_head; c != pa::kNone && c < chunks.size(); c = chunks[c].next) {
+            bytes += sizeof(pa::Chunk) + sizeof(pa::AllocRec) * (uint64_t)chunks[c].cnt;
+            count_range(chunks[c].off, chunks[c].cnt);
+        }
+        for (uint32_t j = r.place_off; j < r.place_off + r.place_cnt && j < last_pa.size(); j++)
+            bytes += sizeof(pa::AllocRec) + (last_pa[j].terminal ? 0 : 8ull * last_pa[j].n_keys);
+    }
+    return bytes;
+}
+
 extern "C" {
 
 pe_planner* pe_planner_create(int device) {
@@ -473,7 +513,7 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
         pkeys.insert(pkeys.end(), h.keys.begin(), h.keys.end());
     }
     t[2] = tnow();
-    uint64_t scratch = 0, bytes = 0;
+    uint64_t scratch = 0;
     for (uint32_t i = 0; i < np; i++) {
         pa::PlanNodeRec& r = pn[i];
         r.row = plan->node_row[i];
@@ -493,28 +533,11 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
         }
         r.rm_cnt = (uint32_t)rm.size() - r.rm_off;
         r.scratch_off = pa::kNone;
-        bytes += sizeof(pa::PlanNodeRec) + 1;
         if (r.place_cnt == 0 || r.row == pa::kNone) continue;
         const pa::NodeRec& nd = p->nodes[r.row];
-        bytes += sizeof(pa::NodeRec);
         if (!nd.ready || !nd.eligible) continue;
         uint64_t bound = (uint64_t)nd.n_keys + nd.alloc_keys;
-        bytes += 8ull * nd.n_keys + sizeof(pa::AllocRec) * (uint64_t)nd.alloc_cnt + 4ull * r.rm_cnt;
-        auto count_range = [&](uint32_t off, uint32_t cnt) {
-            for (uint32_t q = off; q < off + cnt; q++) {
-                const bool gone = p->pool[q].terminal || std::binary_search(rm.begin() + r.rm_off, rm.end(), q);
-                if (!gone) bytes += 8ull * p->pool[q].n_keys;
-            }
-        };
-        count_range(nd.alloc_off, nd.alloc_cnt);
-        for (uint32_t c = nd.ext_head; c != pa::kNone; c = p->chunks[c].next) {
-            bytes += sizeof(pa::Chunk) + sizeof(pa::AllocRec) * (uint64_t)p->chunks[c].cnt;
-            count_range(p->chunks[c].off, p->chunks[c].cnt);
-        }
-        for (uint32_t j = r.place_off; j < r.place_off + r.place_cnt; j++) {
-            bound += pa_recs[j].n_keys;
-            bytes += sizeof(pa::AllocRec) + (pa_recs[j].terminal ? 0 : 8ull * pa_recs[j].n_keys);
-        }
+        for (uint32_t j = r.place_off; j < r.place_off + r.place_cnt; j++) bound += pa_recs[j].n_keys;
         r.key_bound = (uint32_t)std::min<uint64_t>(bound, 0xFFFFFFFFull);
         if (bound > pa::lds_keys(p->group)) {
             big.push_back(i);
@@ -557,7 +580,10 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     float ms = 0;
     (void)hipEventElapsedTime(&ms, p->e0, p->e1);
     p->last_ms = ms;
-    p->last_bytes = bytes;
+    p->last_pn = std::move(pn);
+    p->last_rm = std::move(rm);
+    p->last_pa = std::move(pa_recs);
+    p->bytes_valid = false;
     if (prof) {
         t[5] = tnow();
         fprintf(stderr, "planner evaluate us: strings %.1f flatten %.1f nodes %.1f upload %.1f kernel+reasons %.1f "
@@ -652,7 +678,14 @@ int pe_planner_commit(pe_planner* p, const pe_strtab* strs, const pe_plan* plan,
 }
 
 double pe_planner_kernel_ms(const pe_planner* p) { return p ? p->last_ms : 0; }
-uint64_t pe_planner_last_bytes(const pe_planner* p) { return p ? p->last_bytes : 0; }
+uint64_t pe_planner_last_bytes(const pe_planner* p) {
+    if (!p) return 0;
+    if (!p->bytes_valid) {
+        p->last_bytes = p->plan_bytes();
+        p->bytes_valid = true;
+    }
+    return p->last_bytes;
+}
 uint32_t pe_planner_snapshot_allocs(const pe_planner* p) { return p ? (uint32_t)p->allocs.size() : 0; }
 
 }  // extern "C"
