@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 2u
+#define PE_ABI_VERSION 3u
 #define PE_NONE 0xFFFFFFFFu
 #define PE_MAX_SCORES 8
 #define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried per RankedNode */
@@ -103,6 +103,11 @@ typedef struct pe_node_table {
     const uint32_t* dev_healthy;     /* healthy instance count */
     const uint32_t* dev_attr_off;    /* CSR over device groups */
     const uint32_t* dev_attr_key; const pe_attr* dev_attr_val;
+    /* NodeResources.Cpu.ReservableCpuCores (CSR over nodes) and TotalCpuCores;
+       ReservedResources.Cpu.ReservedCpuCores (CSR). NULL: no core sets */
+    const uint32_t* core_off; const uint16_t* core_id;
+    const uint32_t* total_cores;
+    const uint32_t* rsv_core_off; const uint16_t* rsv_core_id;
 } pe_node_table;
 
 /* ---- existing allocations of the snapshot (state AllocsByNode) ---------- */
@@ -124,6 +129,8 @@ typedef struct pe_alloc_table {
     /* TaskGroup.Migrate.MaxParallel of the alloc's job, or NULL = 0 for every
        alloc (Preemptor.SetCandidates, scheduler/preemption.go:141-154) */
     const int32_t* max_parallel;
+    /* ComparableResources().Flattened.Cpu.ReservedCores (CSR over allocs), or NULL */
+    const uint32_t* core_off; const uint16_t* core_id;
 } pe_alloc_table;
 
 /* ---- job specification (structs.Job / TaskGroup / Task) ----------------- */
@@ -147,7 +154,7 @@ typedef struct pe_device_request {           /* structs.RequestedDevice */
 typedef struct pe_task {
     uint32_t name, driver;
     int64_t cpu, memory_mb, memory_max_mb;
-    int32_t cores;                            /* reserved cores (not on device path) */
+    int32_t cores;                            /* Resources.Cores: reserved cores (rank.go:437-466) */
     uint32_t lifecycle;                       /* PE_LC_* */
     int32_t has_network, net_mbits, net_dyn_ports, net_reserved_ports;
     uint32_t constraint_off, constraint_count;
@@ -230,6 +237,9 @@ typedef struct pe_ranked_node {                 /* RankedNode, rank.go:21-36 */
        task group (tasks in order), the index of the chosen device group on the node */
     uint32_t n_device_offers;
     uint32_t device_offer_group[PE_MAX_DEVICE_REQ];
+    /* Cpu.ReservedCores of the task group's tasks (rank.go:437-466): bit c =
+       core c; tasks asking cores take them in task order, lowest ids first */
+    uint64_t reserved_cores[4];
 } pe_ranked_node;
 
 typedef struct pe_placement {                   /* compact per-placement record (batches) */

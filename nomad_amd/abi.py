@@ -8,6 +8,7 @@ import ctypes as C
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
+u16p = C.POINTER(C.c_uint16)
 i32p = C.POINTER(C.c_int32)
 i64p = C.POINTER(C.c_int64)
 f64p = C.POINTER(C.c_double)
@@ -51,6 +52,8 @@ class pe_node_table(C.Structure):
         ("dev_off", u32p), ("dev_vendor", u32p), ("dev_type", u32p), ("dev_name", u32p),
         ("dev_healthy", u32p),
         ("dev_attr_off", u32p), ("dev_attr_key", u32p), ("dev_attr_val", C.POINTER(pe_attr)),
+        ("core_off", u32p), ("core_id", u16p), ("total_cores", u32p),
+        ("rsv_core_off", u32p), ("rsv_core_id", u16p),
     ]
 
 
@@ -63,6 +66,7 @@ class pe_alloc_table(C.Structure):
         ("net_mbits", i32p), ("dyn_ports", i32p),
         ("dev_off", u32p), ("dev_group", u32p), ("dev_count", u32p),
         ("max_parallel", i32p),
+        ("core_off", u32p), ("core_id", u16p),
     ]
 
 
@@ -159,7 +163,8 @@ class pe_ranked_node(C.Structure):
                 ("nodes_evaluated", C.c_uint32), ("nodes_filtered", C.c_uint32),
                 ("nodes_exhausted", C.c_uint32), ("new_offset", C.c_uint32),
                 ("n_preempted", C.c_uint32), ("preempted", C.c_uint32 * PE_MAX_PREEMPT),
-                ("n_device_offers", C.c_uint32), ("device_offer_group", C.c_uint32 * PE_MAX_DEVICE_REQ)]
+                ("n_device_offers", C.c_uint32), ("device_offer_group", C.c_uint32 * PE_MAX_DEVICE_REQ),
+                ("reserved_cores", C.c_uint64 * 4)]
 
 
 class pe_shard_rec(C.Structure):

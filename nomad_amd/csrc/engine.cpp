@@ -52,7 +52,7 @@ hipError_t pe_launch_evict_trace(const pe::PreemptArgs* a, const uint32_t* rows,
                                  double* named, hipStream_t st);
 hipError_t pe_launch_plan_stop(pe::NodeRec* rec, uint32_t* dev_free, const pe::PreemptAlloc* allocs,
                                uint8_t* preempted, const uint32_t* slots, const uint32_t* rows, uint32_t n, int sign,
-                               hipStream_t st);
+                               uint64_t* core_used, const uint64_t* palloc_cores, hipStream_t st);
 hipError_t pe_launch_reset_plan(pe::NodeRec* rec, const pe::NodeRec* base_rec, uint32_t* dev_free,
                                 const uint32_t* dev_free_base, uint32_t n, uint8_t* preempted, uint32_t m,
                                 uint32_t* pcount, uint32_t keys, hipStream_t st);
@@ -194,6 +194,8 @@ struct HostAlloc {
     int64_t cpu = 0, mem = 0, disk = 0;
     int32_t mbits = 0, dyn = 0;            // network use on the node's host device
     uint32_t dev_begin = 0, dev_end = 0;   // into pe_stack::alloc_dev
+    uint64_t cores[4] = {0, 0, 0, 0};      // Flattened.Cpu.ReservedCores (ids < 256)
+    bool cores_beyond = false;             // a reserved core id >= 256
 };
 
 // One device group of a node (NodeResources.Devices[i], structs.go:2980-3010).
@@ -342,6 +344,14 @@ struct pe_stack {
     std::map<std::pair<uint32_t, uint32_t>, uint32_t> job_keys;   // (job, ns) -> key
     uint32_t n_jtg_keys = 0;
     std::string preempt_unsupported;           // snapshot outside the on-device limits
+    // reserved cores (rank.go:437-466): 4 x u64 masks per node over core ids < 256
+    bool has_cores = false;                    // some node has ReservableCpuCores / ReservedCpuCores
+    std::string cores_tg_unsupported;          // why task groups asking cores stay on the host path
+    std::string cores_unsupported;             // alloc core sets that fail every AllocsFit (overlap, outside)
+    std::vector<uint64_t> h_core_rsvable, h_core_avail, h_core_base, h_core_used;   // used: host mirror of the plan
+    std::vector<int64_t> h_core_spc;
+    std::vector<uint8_t> h_core_bad;           // per node: ids >= 256, or reservable cores with TotalCpuCores 0
+    DevMem d_core_rsvable, d_core_avail, d_core_base, d_core_used, d_core_spc, d_palloc_cores;
     DevMem d_node_alloc_off, d_palloc, d_preempted, d_pcount, d_own_existing;
     DevMem d_ev_status, d_ev_score, d_ev_flags, d_ev_out, d_ev_mask, d_ev_rows, d_ev_masks, d_ev_offers, d_ev_named, d_ev_tcodes;
     uint32_t job_key = PE_NONE;
@@ -922,13 +932,18 @@ bool tg_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g
 void tg_ask(const pe_job* j, const pe_task_group& t, pe::Ask* a) {
     int64_t sc_c = 0, sc_m = 0, eph_c = 0, eph_m = 0, main_c = 0, main_m = 0, ps_c = 0, ps_m = 0;
     a->task_mbits = 0; a->task_dyn = 0; a->has_task_net = 0;
+    a->cores = 0;
     for (uint32_t k = 0; k < t.task_count; k++) {
         const pe_task& x = j->tasks[t.task_off + k];
+        // a task with reserved cores holds SharesPerCore x cores CpuShares on the
+        // chosen node (rank.go:461-463): its cpu is the per-node part of the ask
+        const int64_t cpu = x.cores > 0 ? 0 : x.cpu;
+        if (x.cores > 0) a->cores += x.cores;
         switch (x.lifecycle) {
-            case PE_LC_MAIN: main_c += x.cpu; main_m += x.memory_mb; break;
-            case PE_LC_PRESTART: eph_c += x.cpu; eph_m += x.memory_mb; break;
-            case PE_LC_PRESTART_SIDECAR: sc_c += x.cpu; sc_m += x.memory_mb; break;
-            case PE_LC_POSTSTOP: ps_c += x.cpu; ps_m += x.memory_mb; break;
+            case PE_LC_MAIN: main_c += cpu; main_m += x.memory_mb; break;
+            case PE_LC_PRESTART: eph_c += cpu; eph_m += x.memory_mb; break;
+            case PE_LC_PRESTART_SIDECAR: sc_c += cpu; sc_m += x.memory_mb; break;
+            case PE_LC_POSTSTOP: ps_c += cpu; ps_m += x.memory_mb; break;
             default: break;
         }
         if (x.has_network) {
@@ -1092,6 +1107,46 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         rec.avail_mbits = h.first_mbits;
         rec.used_dyn = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
     }
+    // reserved cores (rank.go:437-466, structs.go:3891-3906): reservable and
+    // AllocsFit-available (reservable - node reserved) masks, SharesPerCore
+    s->h_core_rsvable.resize(4 * (size_t)n_new, 0);
+    s->h_core_avail.resize(4 * (size_t)n_new, 0);
+    s->h_core_spc.resize(n_new, 0);
+    s->h_core_bad.resize(n_new, 0);
+    for (uint32_t r = 0; r < n_new; r++) {
+        if (src_of[r] < 0) continue;
+        const uint32_t i = (uint32_t)src_of[r];
+        uint64_t* rs = &s->h_core_rsvable[4 * (size_t)r];
+        uint64_t* av = &s->h_core_avail[4 * (size_t)r];
+        uint64_t rsv[4] = {0, 0, 0, 0};
+        for (int w = 0; w < 4; w++) rs[w] = av[w] = 0;
+        uint8_t bad = 0;
+        for (uint32_t k = nt->core_off ? nt->core_off[i] : 0; nt->core_off && k < nt->core_off[i + 1]; k++) {
+            const uint16_t c = nt->core_id[k];
+            if (c >= 256) { bad = 1; continue; }
+            rs[c >> 6] |= 1ull << (c & 63);
+        }
+        for (uint32_t k = nt->rsv_core_off ? nt->rsv_core_off[i] : 0; nt->rsv_core_off && k < nt->rsv_core_off[i + 1]; k++) {
+            const uint16_t c = nt->rsv_core_id[k];
+            if (c < 256) rsv[c >> 6] |= 1ull << (c & 63);
+        }
+        for (int w = 0; w < 4; w++) av[w] = rs[w] & ~rsv[w];
+        const uint32_t total = nt->total_cores ? nt->total_cores[i] : 0;
+        s->h_core_spc[r] = total ? nt->cpu_shares[i] / (int64_t)total : 0;
+        if (total == 0 && (rs[0] | rs[1] | rs[2] | rs[3])) bad = 1;
+        s->h_core_bad[r] = bad;
+    }
+    s->has_cores = false;
+    s->cores_tg_unsupported.clear();
+    for (uint32_t r = 0; r < n_new; r++) {
+        if (s->h_core_bad[r]) s->cores_tg_unsupported = "core ids >= 256, or reservable cores with TotalCpuCores 0";
+        for (int w = 0; w < 4 && !s->has_cores; w++) s->has_cores = s->h_core_rsvable[4 * (size_t)r + w] != 0;
+    }
+    if (s->has_cores) {
+        HIP_TRY(s, upload_s(s, s->d_core_rsvable, s->h_core_rsvable));
+        HIP_TRY(s, upload_s(s, s->d_core_avail, s->h_core_avail));
+        HIP_TRY(s, upload_s(s, s->d_core_spc, s->h_core_spc));
+    }
     s->ncls = (uint32_t)s->class_rep.size();
     // checker-input signatures: nodes with equal ComputedClass AND equal
     // non-hashed checker inputs (drivers, networks, aliases, volumes, device
@@ -1236,6 +1291,11 @@ int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index) 
         for (uint32_t k = at->dev_off ? at->dev_off[i] : 0; at->dev_off && k < at->dev_off[i + 1]; k++)
             s->alloc_dev.emplace_back(at->dev_group[k], at->dev_count[k]);
         a.dev_end = (uint32_t)s->alloc_dev.size();
+        for (uint32_t k = at->core_off ? at->core_off[i] : 0; at->core_off && k < at->core_off[i + 1]; k++) {
+            const uint16_t c = at->core_id[k];
+            if (c >= 256) a.cores_beyond = true;
+            else a.cores[c >> 6] |= 1ull << (c & 63);
+        }
         const uint32_t at_index = index ? index[i] : PE_NONE;
         if (at_index == PE_NONE) {
             s->allocs.push_back(a);
@@ -1350,6 +1410,50 @@ int build_alloc_state(pe_stack* s) {
     }
     std::vector<uint32_t> zeros(n, 0);
     HIP_TRY(s, upload_s(s, s->d_coll_job, zeros));
+    // reserved cores held by the snapshot's allocs. Overlapping sets, or cores
+    // outside a node's AllocsFit-available set, fail every AllocsFit on that
+    // node ("cores", funcs.go:158-180): not modelled on the device.
+    s->cores_unsupported.clear();
+    s->h_core_base.assign(4 * (size_t)n, 0);
+    bool any_alloc_cores = false;
+    for (const HostAlloc& a : s->allocs) {
+        if (a.terminal) continue;
+        if (a.cores_beyond) s->cores_unsupported = "allocs holding core ids >= 256";
+        uint64_t* u = &s->h_core_base[4 * (size_t)a.row];
+        for (int w = 0; w < 4; w++) {
+            if (!a.cores[w]) continue;
+            any_alloc_cores = true;
+            if (u[w] & a.cores[w]) s->cores_unsupported = "allocs holding overlapping reserved cores";
+            u[w] |= a.cores[w];
+        }
+    }
+    if (any_alloc_cores)
+        for (uint32_t r = 0; r < n; r++) {
+            const uint64_t* u = &s->h_core_base[4 * (size_t)r];
+            const uint64_t* av = r < s->h_core_avail.size() / 4 ? &s->h_core_avail[4 * (size_t)r] : nullptr;
+            const bool any = av && (av[0] | av[1] | av[2] | av[3]);
+            for (int w = 0; w < 4 && any; w++)
+                if (u[w] & ~av[w]) s->cores_unsupported = "allocs holding reserved cores outside the node's available set";
+        }
+    s->h_core_used = s->h_core_base;
+    if (s->has_cores || any_alloc_cores) {
+        if (!s->has_cores) {   // core sets on allocs only: empty reservable masks
+            s->h_core_rsvable.assign(4 * (size_t)n, 0);
+            s->h_core_avail.assign(4 * (size_t)n, 0);
+            s->h_core_spc.assign(n, 0);
+            s->has_cores = true;
+            HIP_TRY(s, upload_s(s, s->d_core_rsvable, s->h_core_rsvable));
+            HIP_TRY(s, upload_s(s, s->d_core_avail, s->h_core_avail));
+            HIP_TRY(s, upload_s(s, s->d_core_spc, s->h_core_spc));
+        }
+        HIP_TRY(s, upload_s(s, s->d_core_base, s->h_core_base));
+        HIP_TRY(s, upload_s(s, s->d_core_used, s->h_core_base));
+        const uint32_t m = s->h_node_alloc_off[n];
+        std::vector<uint64_t> pc(4 * (size_t)std::max<uint32_t>(m, 1), 0);
+        for (uint32_t slot = 0; slot < m; slot++)
+            for (int w = 0; w < 4; w++) pc[4 * (size_t)slot + w] = s->allocs[s->h_palloc_index[slot]].cores[w];
+        HIP_TRY(s, upload_s(s, s->d_palloc_cores, pc));
+    }
     return PE_OK;
 }
 
@@ -1358,7 +1462,36 @@ pe::NodeSoA soa_of(pe_stack* s) {
     a.n = (uint32_t)s->nodes.size();
     a.rec = s->d_rec.as<pe::NodeRec>();
     a.coll_job = s->d_coll_job.as<uint32_t>();
+    a.core_rsvable = s->has_cores ? s->d_core_rsvable.as<uint64_t>() : nullptr;
+    a.core_avail = s->has_cores ? s->d_core_avail.as<uint64_t>() : nullptr;
+    a.core_used = s->has_cores ? s->d_core_used.as<uint64_t>() : nullptr;
+    a.core_spc = s->has_cores ? s->d_core_spc.as<int64_t>() : nullptr;
     return a;
+}
+
+// Reserved cores the next placement of the group takes on `row` (the lowest
+// free ones, rank.go:437-466), from the host mirror of the plan's used sets;
+// with `take` they become used (Plan.AppendAlloc).
+void core_record(pe_stack* s, const TgPlan& g, int32_t row, bool take, uint64_t out[4]) {
+    for (int w = 0; w < 4; w++) out[w] = 0;
+    if (g.ask.cores <= 0 || !s->has_cores || row < 0 || (size_t)row >= s->nodes.size()) return;
+    uint32_t need = (uint32_t)g.ask.cores;
+    for (int w = 0; w < 4 && need; w++) {
+        uint64_t f = s->h_core_rsvable[4 * (size_t)row + w] & ~s->h_core_used[4 * (size_t)row + w];
+        for (; f && need; need--) { out[w] |= f & (~f + 1); f &= f - 1; }
+        if (take) s->h_core_used[4 * (size_t)row + w] |= out[w];
+    }
+}
+
+// A snapshot alloc's reserved cores leave (hold = false: plan stop or
+// preemption) or rejoin (PopUpdate) its node's used set in the host mirror.
+void core_hold(pe_stack* s, uint32_t alloc, bool hold) {
+    if (!s->has_cores || alloc >= s->allocs.size()) return;
+    const HostAlloc& a = s->allocs[alloc];
+    for (int w = 0; w < 4; w++) {
+        uint64_t& u = s->h_core_used[4 * (size_t)a.row + w];
+        u = hold ? (u | a.cores[w]) : (u & ~a.cores[w]);
+    }
 }
 
 // Job-dependent per-node collision counts from the snapshot + the plan.
@@ -1777,6 +1910,8 @@ int prepare_tg(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& order, ui
     if (tgi >= s->tgs.size()) return s->fail(PE_EINVAL, "task group index out of range");
     TgPlan& g = *s->tgs[tgi];
     if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
+    if (!s->cores_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, s->cores_unsupported);
+    if (g.ask.cores > 0 && !s->cores_tg_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, s->cores_tg_unsupported);
     if (!g.psets_built) {
         int rc = build_psets(s, g);
         if (rc) return rc;
@@ -2065,6 +2200,7 @@ pe::PreemptArgs preempt_args(pe_stack* s, TgPlan& g) {
     P.job_priority = s->job_priority;
     P.log10 = s->log10;
     P.score_preemption = s->cfg.stack_kind == PE_STACK_GENERIC ? 1 : 0;
+    P.palloc_cores = s->has_cores ? s->d_palloc_cores.as<uint64_t>() : nullptr;
     return P;
 }
 
@@ -2137,6 +2273,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     const uint32_t n = (uint32_t)order.size();
     *new_offset = n ? offset % n : 0;
     if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
+    if (g.ask.cores > 0) return s->fail(PE_EUNSUPPORTED, "reserved cores with preemption");
     if (n == 0) return PE_OK;
     pe::PreemptArgs P = preempt_args(s, g);
     HIP_TRY(s, upload_visit(s, order));
@@ -2624,6 +2761,11 @@ int pe_reset_plan(pe_stack* s) {
                                     s->d_preempted.as<uint8_t>(), (uint32_t)s->h_preempted.size(),
                                     s->d_pcount.as<uint32_t>(), std::max<uint32_t>(s->n_jtg_keys, 1), s->stream));
     std::fill(s->h_preempted.begin(), s->h_preempted.end(), 0);
+    if (s->has_cores) {   // reserved cores back to the snapshot's
+        HIP_TRY(s, hipMemcpyAsync(s->d_core_used.p, s->d_core_base.p, sizeof(uint64_t) * 4 * n, hipMemcpyDeviceToDevice,
+                                  s->stream));
+        s->h_core_used = s->h_core_base;
+    }
     s->node_update.clear();
     s->stop_count.assign(s->allocs.size(), 0);
     s->offer_row = -1;   // stream-ordered: later launches and uploads see the reset state
@@ -2708,9 +2850,14 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
             for (uint32_t c = 0; c < x.constraint_count; c++) g->constraints.push_back(parse_constraint(s, j->constraints[x.constraint_off + c]));
             for (uint32_t d = 0; d < x.device_count; d++)
                 g->dev_reqs.push_back(parse_dev_request(s, j, j->devices[x.device_off + d]));
-            if (x.cores > 0) g->unsupported = "reserved cores";
+            if (x.cores > 0 && x.lifecycle != PE_LC_MAIN) g->unsupported = "reserved cores on a lifecycle hook task";
             if (x.has_network && x.net_reserved_ports > 0) g->unsupported = "static port asks";
         }
+        if (g->ask.cores > 0)   // the per-node ask is Σ main tasks + SharesPerCore x cores (no max over hooks)
+            for (uint32_t k = 0; k < t.task_count; k++) {
+                const uint32_t lc = j->tasks[t.task_off + k].lifecycle;
+                if (lc == PE_LC_PRESTART || lc == PE_LC_POSTSTOP) g->unsupported = "reserved cores beside prestart / poststop tasks";
+            }
         for (auto& c : g->constraints) g->escaped = g->escaped || c.escapes;
         for (uint32_t k = 0; k < t.volume_count; k++)
             g->volumes.emplace_back(j->volume_source[t.volume_off + k], j->volume_read_only[t.volume_off + k] != 0);
@@ -3090,6 +3237,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                 case pe::kTrDevZero: exhaust(row, "devices: invalid request of zero devices"); break;
                 case pe::kTrDevNoMatch: exhaust(row, "devices: no devices match request"); break;
                 case pe::kTrCpu: exhaust(row, "cpu"); break;
+                case pe::kTrCores: exhaust(row, "cores"); break;
                 case pe::kTrMemory: exhaust(row, "memory"); break;
                 case pe::kTrDisk: exhaust(row, "disk"); break;
                 case pe::kTrMismatch: return s->fail(PE_EHIP, "k_trace: device verdict differs from the host walk");
@@ -3132,6 +3280,7 @@ int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranke
     if (rc == PE_OK) {
         s->offer_row = out->row;
         s->offers = pack_offers(out);
+        if (tgi < s->tgs.size()) core_record(s, *s->tgs[tgi], out->row, false, out->reserved_cores);
     }
     return rc;
 }
@@ -3331,7 +3480,10 @@ static int commit_preempt_impl(pe_stack* s, uint32_t tgi, int32_t row, const uin
     pe::PreemptArgs P = preempt_args(s, g);
     HIP_TRY(s, pe_launch_commit_preempt(&P, (uint32_t)row, mask, s->d_preempted.as<uint8_t>(),
                                         s->d_pcount.as<uint32_t>(), s->d_dev_free.as<uint32_t>(), s->stream));
-    for (uint32_t i = 0; i < n_preempted; i++) s->h_preempted[s->alloc_slot[preempted[i]]] = 1;
+    for (uint32_t i = 0; i < n_preempted; i++) {
+        s->h_preempted[s->alloc_slot[preempted[i]]] = 1;
+        core_hold(s, preempted[i], false);
+    }
     return commit_impl(s, tgi, row);
 }
 
@@ -3448,6 +3600,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
                     return s->fail(PE_EUNSUPPORTED, "more than PE_MAX_PREEMPT preempted allocs");
                 out[k].preempted[out[k].n_preempted++] = s->h_palloc_index[b + i];
                 s->h_preempted[b + i] = 1;
+                core_hold(s, s->h_palloc_index[b + i], false);
             }
     }
     *placed = p;
@@ -3764,6 +3917,7 @@ static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* op
     if (!s->spec_on || s->cfg.stack_kind != PE_STACK_GENERIC || s->metrics_on) return false;
     if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
     if (!s->have_state || !s->have_job || tgi >= s->tgs.size()) return false;
+    if (s->tgs[tgi]->ask.cores > 0) return false;   // the rollback kernel does not return reserved cores
     for (size_t k = 0; k < s->tgs.size(); k++)   // commits would rebuild a sibling's collision counts
         if (k != tgi && s->tgs[k]->name == s->tgs[tgi]->name) return false;
     return true;
@@ -3906,7 +4060,12 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     if (!s) return PE_EINVAL;
     int rc = spec_flush(s);
     if (rc) return rc;
-    return place_impl(s, tgi, count, out, placed, true);
+    uint32_t p = 0;
+    rc = place_impl(s, tgi, count, out, &p, true);
+    if (placed) *placed = p;
+    if (tgi < s->tgs.size() && s->tgs[tgi]->ask.cores > 0)   // the placements' reserved cores, in order
+        for (uint32_t k = 0; k < p && k < count; k++) core_record(s, *s->tgs[tgi], out[k].row, true, out[k].reserved_cores);
+    return rc;
 }
 
 int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
@@ -3924,7 +4083,10 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
     }
     int rc = spec_flush(s);
     if (rc) return rc;
-    return commit_impl(s, tgi, row);
+    rc = commit_impl(s, tgi, row);
+    uint64_t cores[4];
+    if (rc == PE_OK) core_record(s, *s->tgs[tgi], row, true, cores);
+    return rc;
 }
 
 int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
@@ -3932,7 +4094,10 @@ int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* pr
     if (n_preempted == 0) return pe_commit(s, tgi, row);
     int rc = spec_flush(s);
     if (rc) return rc;
-    return commit_preempt_impl(s, tgi, row, preempted, n_preempted);
+    rc = commit_preempt_impl(s, tgi, row, preempted, n_preempted);
+    uint64_t cores[4];
+    if (rc == PE_OK) core_record(s, *s->tgs[tgi], row, true, cores);
+    return rc;
 }
 
 // Plan.NodeUpdate bookkeeping shared by pe_plan_stop / pe_plan_pop_update:
@@ -3948,6 +4113,7 @@ static int apply_stop_delta(pe_stack* s, const std::vector<uint32_t>& allocs, in
         f = sign > 0 ? 2 : 0;
         slots.push_back(slot);
         rows.push_back(a.row);
+        core_hold(s, ai, sign < 0);   // its reserved cores leave (rejoin) the node's used set
     }
     if (!slots.empty()) {
         HIP_TRY(s, upload_s(s, s->d_stop_slots, slots));
@@ -3955,7 +4121,8 @@ static int apply_stop_delta(pe_stack* s, const std::vector<uint32_t>& allocs, in
         HIP_TRY(s, pe_launch_plan_stop(s->d_rec.as<pe::NodeRec>(), s->dev_packable ? s->d_dev_free.as<uint32_t>() : nullptr,
                                        s->d_palloc.as<pe::PreemptAlloc>(), s->d_preempted.as<uint8_t>(),
                                        s->d_stop_slots.as<uint32_t>(), s->d_stop_rows.as<uint32_t>(),
-                                       (uint32_t)slots.size(), sign, s->stream));
+                                       (uint32_t)slots.size(), sign, s->has_cores ? s->d_core_used.as<uint64_t>() : nullptr,
+                                       s->has_cores ? s->d_palloc_cores.as<uint64_t>() : nullptr, s->stream));
     }
     // the job's own allocs feed the collision counts and the property sets
     for (auto& g : s->tgs) g->psets_built = false;
@@ -4492,6 +4659,9 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
         rc = system_place_distinct(s, tgi, g, out_score, out_status, &p);
         if (rc) return rc;
         if (placed) *placed = p;
+        uint64_t cores[4];
+        if (g.ask.cores > 0)   // the host mirror of the placements' reserved cores
+            for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) core_record(s, g, (int32_t)s->visit[i], true, cores);
         return PE_OK;
     }
     {
@@ -4506,6 +4676,9 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
             w += out_status[i] == 0;
         }
         s->plan.resize(base + p);
+        uint64_t cores[4];
+        if (g.ask.cores > 0)   // the host mirror of the placements' reserved cores
+            for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) core_record(s, g, (int32_t)s->visit[i], true, cores);
     }
     if (s->cfg.preempt) {
         // BinPack with evict (stack.go:267-278) on the nodes the plain fit exhausted
@@ -4514,6 +4687,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
             if (out_status[i] == 2) { pos.push_back(i); rows.push_back(s->visit[i]); }
         if (!rows.empty()) {
             if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
+            if (g.ask.cores > 0) return s->fail(PE_EUNSUPPORTED, "reserved cores with preemption");
             // the max_parallel penalty reads the plan's preemption counts, which
             // earlier nodes grow: then the nodes go one at a time in list order
             bool serial = false;
@@ -4590,7 +4764,10 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
                     s->plan.emplace_back(g.name, rows[k]);
                     const uint32_t b = s->h_node_alloc_off[rows[k]];
                     for (uint32_t i = 0; i < 32; i++)
-                        if ((masks[k] >> i) & 1u) s->h_preempted[b + i] = 1;
+                        if ((masks[k] >> i) & 1u) {
+                            s->h_preempted[b + i] = 1;
+                            core_hold(s, s->h_palloc_index[b + i], false);
+                        }
                     p++;
                 }
             }

@@ -26,7 +26,7 @@ enum : uint32_t {
     kTrOption = 0, kTrDistinctHosts = 1, kTrDistinctProp = 2,
     kTrNoAddr = 10, kTrDynPorts = 11, kTrNoNetworks = 12, kTrBandwidth = 13, kTrTaskDyn = 14,
     kTrDevNone = 20, kTrDevZero = 21, kTrDevNoMatch = 22,
-    kTrCpu = 30, kTrMemory = 31, kTrDisk = 32,
+    kTrCpu = 30, kTrMemory = 31, kTrDisk = 32, kTrCores = 33,
     kTrMismatch = 254,          // device verdict disagrees with the host walk (bug guard)
     kTrPenalty = 1u << 16,      // option: node in the rescheduling penalty set
 };
@@ -56,6 +56,12 @@ struct NodeSoA {
     uint32_t n;
     NodeRec* rec;                // [n], row order of the snapshot (job independent)
     uint32_t* coll_job;          // [n] proposed allocs of the job (distinct_hosts only)
+    // reserved cores (rank.go:437-466), null when no node has core sets: per
+    // node 4 x u64 masks over core ids < 256
+    const uint64_t* core_rsvable;   // ReservableCpuCores
+    const uint64_t* core_avail;     // ReservableCpuCores - ReservedCpuCores (AllocsFit Superset)
+    uint64_t* core_used;            // Σ proposed allocs' ReservedCores
+    const int64_t* core_spc;        // [n] SharesPerCore = CpuShares / TotalCpuCores
 };
 
 // Per (job, task group) feasibility / affinity / spread tables for a Select.
@@ -92,6 +98,7 @@ struct Ask {
     int32_t distinct_job, distinct_tg;
     int32_t algo_spread;
     int32_t anti_aff;             // JobAntiAffinityIterator present (GenericStack only)
+    int32_t cores;                // Σ Resources.Cores of the tasks (cpu: the other tasks' CpuShares)
     int32_t n_dev;                // device requests of the task group (tasks in order)
     uint32_t dev_aff;             // bit q: request q has affinities
     int32_t dev_cnt[kMaxDevReq];  // RequestedDevice.Count
@@ -233,6 +240,7 @@ struct PreemptArgs {
     uint32_t* offers_out;             // or null: device offers, one byte per request
     uint32_t* flags;                  // [1] bit 0: a node exceeded the on-device limits
     uint8_t* dep_out;                 // or null: per position, the outcome read the plan's preemption counts
+    const uint64_t* palloc_cores;     // [m x 4] or null: reserved cores held by each alloc (by CSR slot)
 };
 
 // LimitIterator + MaxScoreIterator over per-position results.

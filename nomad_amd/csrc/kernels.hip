@@ -174,6 +174,41 @@ __device__ __forceinline__ uint32_t dev_after(const Ask& a, const DevClass& dc, 
     return free;
 }
 
+// Reserved cores (BinPackIterator, rank.go:437-466): every placement of the
+// task group on a node takes the lowest free cores (cpuset ToSlice order), so
+// the (dk+1)-th placement of an evaluation holds the free cores of rank
+// [dk*cores, (dk+1)*cores). False when fewer are free ("cores" exhausted).
+__device__ __forceinline__ bool core_pick(const NodeSoA& s, uint32_t row, uint32_t cores, uint32_t dk,
+                                          uint64_t ch[4]) {
+    uint32_t skip = dk * cores, need = cores;
+    for (int w = 0; w < 4; w++) {
+        uint64_t f = s.core_rsvable[4 * row + w] & ~s.core_used[4 * row + w];
+        ch[w] = 0;
+        const uint32_t c = (uint32_t)__popcll(f);
+        if (skip >= c) { skip -= c; continue; }
+        for (; skip; skip--) f &= f - 1;
+        for (; f && need; need--) { ch[w] |= f & (~f + 1); f &= f - 1; }
+    }
+    return need == 0;
+}
+
+// CpuShares of one placement on the row: tasks with cores hold SharesPerCore x
+// cores (rank.go:461-463).
+__device__ __forceinline__ int64_t ask_cpu(const NodeSoA& s, const Ask& a, uint32_t row) {
+    return a.cores > 0 ? a.cpu + (int64_t)a.cores * s.core_spc[row] : a.cpu;
+}
+
+// Plan.AppendAlloc of k placements on the row: their cores leave the free set.
+__device__ __forceinline__ void core_take(const NodeSoA& s, const Ask& a, uint32_t row, uint32_t k) {
+    if (a.cores <= 0 || !s.core_rsvable) return;
+    uint32_t need = k * (uint32_t)a.cores;
+    for (int w = 0; w < 4 && need; w++) {
+        uint64_t f = s.core_rsvable[4 * row + w] & ~s.core_used[4 * row + w], t = 0;
+        for (; f && need; need--) { t |= f & (~f + 1); f &= f - 1; }
+        s.core_used[4 * row + w] |= t;
+    }
+}
+
 // Inputs of the scoring half of the pipeline (everything after AllocsFit).
 // The table lookups (affinity, spread, penalty) are resolved by
 // lookup_scores so that their loads issue with the node's own loads; the
@@ -245,10 +280,20 @@ __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t
         if (!dev_assign(a, dc, fr, &m)) return kExhausted;
         if (a.dev_tw != 0.0) si->dev_aff = m / a.dev_tw;
     }
-    const int64_t ucpu = r.used_cpu + (int64_t)(dk + 1) * a.cpu;
+    int64_t acpu = a.cpu;
+    bool core_out = false;
+    if (a.cores > 0) {   // reserved cores (rank.go:437-466), then AllocsFit's Superset check
+        uint64_t ch[4];
+        if (!s.core_rsvable || !core_pick(s, row, (uint32_t)a.cores, dk, ch)) return kExhausted;
+        acpu += (int64_t)a.cores * s.core_spc[row];
+        const uint64_t* av = s.core_avail + 4 * row;
+        if (av[0] | av[1] | av[2] | av[3])
+            core_out = ((ch[0] & ~av[0]) | (ch[1] & ~av[1]) | (ch[2] & ~av[2]) | (ch[3] & ~av[3])) != 0;
+    }
+    const int64_t ucpu = r.used_cpu + (int64_t)(dk + 1) * acpu;
     const int64_t umem = r.used_mem + (int64_t)(dk + 1) * a.mem;
     const int64_t udisk = r.used_disk + (int64_t)(dk + 1) * a.disk;
-    if (r.cap_cpu < ucpu || r.cap_mem < umem || r.cap_disk < udisk) return kExhausted;
+    if (r.cap_cpu < ucpu || core_out || r.cap_mem < umem || r.cap_disk < udisk) return kExhausted;
     si->ccpu = r.cap_cpu;
     si->cmem = r.cap_mem;
     si->ucpu = ucpu;
@@ -422,8 +467,19 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
             free -= cnt << (8 * best);
         }
     }
+    bool core_out = false;
+    if (code == kTrOption && a.cores > 0) {                         // reserved cores (rank.go:437-466)
+        uint64_t ch[4];
+        if (!s.core_rsvable || !core_pick(s, row, (uint32_t)a.cores, 0, ch)) code = kTrCores;
+        else {
+            const uint64_t* av = s.core_avail + 4 * row;
+            if (av[0] | av[1] | av[2] | av[3])
+                core_out = ((ch[0] & ~av[0]) | (ch[1] & ~av[1]) | (ch[2] & ~av[2]) | (ch[3] & ~av[3])) != 0;
+        }
+    }
     if (code == kTrOption) {                                        // AllocsFit → Superset order
-        if (r.cap_cpu < r.used_cpu + a.cpu) code = kTrCpu;
+        if (r.cap_cpu < r.used_cpu + ask_cpu(s, a, row)) code = kTrCpu;
+        else if (core_out) code = kTrCores;
         else if (r.cap_mem < r.used_mem + a.mem) code = kTrMemory;
         else if (r.cap_disk < r.used_disk + a.disk) code = kTrDisk;
     }
@@ -778,7 +834,8 @@ __device__ void writeback_overlay(const BatchArgs& A, const Overlay& ov, uint32_
         const uint32_t row = ov.k ? e : e >> ov.kshift;
         const uint32_t k = ov.k ? ov.k[h] : e & ov.kmask;
         NodeRec& r = A.soa.rec[row];
-        r.used_cpu += (int64_t)k * A.ask.cpu;
+        r.used_cpu += (int64_t)k * ask_cpu(A.soa, A.ask, row);
+        core_take(A.soa, A.ask, row, k);
         r.used_mem += (int64_t)k * A.ask.mem;
         r.used_disk += (int64_t)k * A.ask.disk;
         r.used_mbits += (int32_t)k * A.ask.commit_mbits;
@@ -1857,7 +1914,8 @@ __global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
     for (uint32_t x = threadIdx.x; x < nov; x += 256) {
         const uint2 e = A.emit_ov[x];
         NodeRec& r = A.soa.rec[e.x];
-        r.used_cpu += (int64_t)e.y * A.ask.cpu;
+        r.used_cpu += (int64_t)e.y * ask_cpu(A.soa, A.ask, e.x);
+        core_take(A.soa, A.ask, e.x, e.y);
         r.used_mem += (int64_t)e.y * A.ask.mem;
         r.used_disk += (int64_t)e.y * A.ask.disk;
         r.used_mbits += (int32_t)e.y * A.ask.commit_mbits;
@@ -1893,7 +1951,8 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
             if (!A.commit) continue;
             // Plan.AppendAlloc: rows are unique in the list, so no races
             NodeRec& r = A.soa.rec[row];
-            r.used_cpu += A.ask.cpu;
+            r.used_cpu += ask_cpu(A.soa, A.ask, row);
+            core_take(A.soa, A.ask, row, 1);
             r.used_mem += A.ask.mem;
             r.used_disk += A.ask.disk;
             r.used_mbits += A.ask.commit_mbits;
@@ -1949,7 +2008,8 @@ __global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts, u
 __device__ __forceinline__ void commit_row(const NodeSoA& s, const TgTables& t, const Ask& a, uint32_t row,
                                            uint32_t offers) {
     NodeRec& r = s.rec[row];
-    r.used_cpu += a.cpu;
+    r.used_cpu += ask_cpu(s, a, row);
+    core_take(s, a, row, 1);
     r.used_mem += a.mem;
     r.used_disk += a.disk;
     r.used_mbits += a.commit_mbits;
@@ -1989,7 +2049,8 @@ __global__ void __launch_bounds__(256) k_commit_rows(NodeSoA s, TgTables t, Ask 
     if (i >= n) return;
     const uint32_t row = rows[i];
     NodeRec& r = s.rec[row];
-    r.used_cpu += a.cpu;
+    r.used_cpu += ask_cpu(s, a, row);
+    core_take(s, a, row, 1);
     r.used_mem += a.mem;
     r.used_disk += a.disk;
     r.used_mbits += a.commit_mbits;
@@ -2620,7 +2681,7 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
                     for (uint32_t q = 0; q < o->n_device_offers && q < 4; q++)
                         offers |= (o->device_offer_group[q] & 255u) << (8 * q);
                 }
-                const bool fast = A.ask.n_dev == 0 && np == t.n_psets;
+                const bool fast = A.ask.n_dev == 0 && A.ask.cores == 0 && np == t.n_psets;
                 if (fast) {   // commit_row from the loaded values: stores only
                     NodeRec& r = A.soa.rec[row];
                     r.used_cpu = in.r.used_cpu + A.ask.cpu;
@@ -2939,10 +3000,10 @@ hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hip
 
 hipError_t pe_launch_plan_stop(pe::NodeRec* rec, uint32_t* dev_free, const pe::PreemptAlloc* allocs,
                                uint8_t* preempted, const uint32_t* slots, const uint32_t* rows, uint32_t n, int sign,
-                               hipStream_t st) {
+                               uint64_t* core_used, const uint64_t* palloc_cores, hipStream_t st) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(pe::k_plan_stop, dim3((n + 63) / 64), dim3(64), 0, st, rec, dev_free, allocs, preempted, slots,
-                       rows, n, sign);
+                       rows, n, sign, core_used, palloc_cores);
     return hipGetLastError();
 }
 

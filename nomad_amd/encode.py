@@ -65,6 +65,10 @@ def _u8(x):
     return np.ascontiguousarray(np.asarray(x, dtype=np.uint8))
 
 
+def _u16(x):
+    return np.ascontiguousarray(np.asarray(x, dtype=np.uint16))
+
+
 class EncodedState:
     """pe_node_table + pe_alloc_table over one Interner."""
 
@@ -172,6 +176,12 @@ class EncodedState:
         keep.extend([aoff, akeys_a, avals_a])
         nt.dev_attr_off, nt.dev_attr_key = _ptr(aoff, abi.u32p), _ptr(akeys_a, abi.u32p)
         nt.dev_attr_val = C.cast(avals_a, C.POINTER(abi.pe_attr))
+        if any(nd.reservable_cores or nd.reserved_cores or nd.total_cores for nd in nodes):
+            off, cid = csr(lambda x: [(c,) for c in x.reservable_cores], [_u16])
+            nt.core_off, nt.core_id = _ptr(off, abi.u32p), _ptr(cid, abi.u16p)
+            nt.total_cores = _ptr(col(lambda x: x.total_cores, _u32), abi.u32p)
+            off, rid = csr(lambda x: [(c,) for c in x.reserved_cores], [_u16])
+            nt.rsv_core_off, nt.rsv_core_id = _ptr(off, abi.u32p), _ptr(rid, abi.u16p)
         return nt
 
     def encode_alloc_table(self, allocs: Sequence[Allocation]) -> abi.pe_alloc_table:
@@ -211,6 +221,15 @@ class EncodedState:
         at.dev_group = _ptr(dgrp_a, abi.u32p)
         at.dev_count = _ptr(dcnt_a, abi.u32p)
         at.max_parallel = _ptr(acol(lambda a: a.max_parallel, _i32), abi.i32p)
+        if any(a.reserved_cores for a in live):
+            coff = np.zeros(len(live) + 1, dtype=np.uint32)
+            cid = []
+            for i, a in enumerate(live):
+                cid.extend(a.reserved_cores)
+                coff[i + 1] = len(cid)
+            cid_a = _u16(cid if cid else [0])
+            keep.extend([coff, cid_a])
+            at.core_off, at.core_id = _ptr(coff, abi.u32p), _ptr(cid_a, abi.u16p)
         return at
 
     def strtab(self):

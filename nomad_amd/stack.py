@@ -104,6 +104,7 @@ class RankedNode:
     new_offset: int = 0
     preempted: List[int] = field(default_factory=list)   # PreemptedAllocs: alloc-table rows
     device_offers: List[int] = field(default_factory=list)   # chosen device group per request
+    reserved_cores: List[int] = field(default_factory=list)  # Cpu.ReservedCores of the tasks, ascending
 
     @classmethod
     def from_c(cls, r: abi.pe_ranked_node, nodes):
@@ -112,7 +113,9 @@ class RankedNode:
                    scores=[r.scores[i] for i in range(r.n_scores)], nodes_evaluated=r.nodes_evaluated,
                    nodes_filtered=r.nodes_filtered, nodes_exhausted=r.nodes_exhausted,
                    new_offset=r.new_offset, preempted=[r.preempted[i] for i in range(r.n_preempted)],
-                   device_offers=[r.device_offer_group[i] for i in range(r.n_device_offers)])
+                   device_offers=[r.device_offer_group[i] for i in range(r.n_device_offers)],
+                   reserved_cores=[64 * w + b for w in range(4) for b in range(64)
+                                   if (r.reserved_cores[w] >> b) & 1])
 
 
 class _Stack:

@@ -69,6 +69,9 @@ class Node:
     reserved_host_ports: List[int] = field(default_factory=list)
     host_volumes: Dict[str, bool] = field(default_factory=dict)   # name -> read only
     devices: List[DeviceGroup] = field(default_factory=list)
+    reservable_cores: List[int] = field(default_factory=list)   # NodeResources.Cpu.ReservableCpuCores
+    total_cores: int = 0                                        # NodeResources.Cpu.TotalCpuCores
+    reserved_cores: List[int] = field(default_factory=list)     # ReservedResources.Cpu.ReservedCpuCores
     status: str = "ready"
     drain: bool = False
     eligible: bool = True
@@ -129,6 +132,7 @@ class Allocation:
     # DeviceIDs counted per group (nomad/structs/devices.go:62-100)
     devices: List[Tuple[int, int]] = field(default_factory=list)
     max_parallel: int = 0         # TaskGroup.Migrate.MaxParallel of the alloc's job (preemption.go:146-150)
+    reserved_cores: List[int] = field(default_factory=list)   # Flattened.Cpu.ReservedCores
 
 
 @dataclass

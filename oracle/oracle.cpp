@@ -72,6 +72,8 @@ struct ONode {
     std::map<std::string, bool> host_volumes;   // name -> read only
     int n_devices;
     std::vector<ODev> devs;
+    std::vector<uint16_t> rcores, nrsv_cores;   // ReservableCpuCores, ReservedResources.Cpu.ReservedCpuCores
+    uint32_t total_cores = 0;                   // TotalCpuCores
 };
 
 struct OAlloc {
@@ -85,6 +87,7 @@ struct OAlloc {
     std::vector<std::pair<int, int>> devs;   // (device group on the node, instances held)
     int32_t max_parallel = 0;
     int state_index = -1;                    // row of the state alloc table (-1: plan alloc)
+    std::vector<uint16_t> cores;             // Flattened.Cpu.ReservedCores (a set)
 };
 
 struct OConstraint { std::string l, r, op; };
@@ -902,6 +905,8 @@ struct RankedNode {
     std::vector<double> scores;
     std::vector<const OAlloc*> preempted;   // PreemptedAllocs
     std::vector<std::pair<int, int>> offers; // device offers (group, instances) per request
+    std::vector<uint16_t> cores;             // Cpu.ReservedCores of the tasks, in task order
+    int64_t cpu = 0;                         // the alloc's CpuShares (SharesPerCore x cores for core tasks)
 };
 
 struct RankIterator { virtual ~RankIterator() {} virtual RankedNode* Next() = 0; virtual void Reset() = 0; };
@@ -922,15 +927,18 @@ struct FeasibleRankIterator : RankIterator {
 
 // The task group's resource ask: AllocatedResources.Comparable() (structs.go:3445-3487)
 struct Ask { int64_t cpu, mem, disk; };
-static Ask tg_ask(const OTaskGroup& tg, bool oversub) {
+// spc >= 0: tasks asking reserved cores hold SharesPerCore x cores CpuShares
+// (rank.go:461-463); spc < 0: their Resources.CPU (a commit without a Select)
+static Ask tg_ask(const OTaskGroup& tg, bool oversub, int64_t spc = -1) {
     (void)oversub;
     int64_t sc_cpu = 0, sc_mem = 0, eph_cpu = 0, eph_mem = 0, main_cpu = 0, main_mem = 0, ps_cpu = 0, ps_mem = 0;
     for (auto& t : tg.tasks) {
+        const int64_t cpu = (t.cores > 0 && spc >= 0) ? spc * t.cores : t.cpu;
         switch (t.lifecycle) {
-            case PE_LC_MAIN: main_cpu += t.cpu; main_mem += t.mem; break;
-            case PE_LC_PRESTART: eph_cpu += t.cpu; eph_mem += t.mem; break;
-            case PE_LC_PRESTART_SIDECAR: sc_cpu += t.cpu; sc_mem += t.mem; break;
-            case PE_LC_POSTSTOP: ps_cpu += t.cpu; ps_mem += t.mem; break;
+            case PE_LC_MAIN: main_cpu += cpu; main_mem += t.mem; break;
+            case PE_LC_PRESTART: eph_cpu += cpu; eph_mem += t.mem; break;
+            case PE_LC_PRESTART_SIDECAR: sc_cpu += cpu; sc_mem += t.mem; break;
+            case PE_LC_POSTSTOP: ps_cpu += cpu; ps_mem += t.mem; break;
             default: break;   // poststart hooks are not counted by Comparable()
         }
     }
@@ -1286,6 +1294,8 @@ struct BinPackIterator : RankIterator {
             }
             bool skip = false;
             option->offers.clear();
+            option->cores.clear();
+            int64_t spc = -1;
             for (auto& t : tg->tasks) {
                 if (t.has_network) {
                     // AssignNetwork over the node's AvailNetworks (device != "")
@@ -1326,16 +1336,50 @@ struct BinPackIterator : RankIterator {
                     }
                 }
                 if (skip) break;
-                if (t.cores > 0) throw Unsupported("reserved cores");
+                if (t.cores > 0) {   // reserved cores (rank.go:437-466)
+                    std::set<uint16_t> allocated(option->cores.begin(), option->cores.end());
+                    for (const OAlloc* a : proposed) allocated.insert(a->cores.begin(), a->cores.end());
+                    std::vector<uint16_t> avail;   // cpuset ToSlice: ascending
+                    for (uint16_t c : std::set<uint16_t>(n.rcores.begin(), n.rcores.end()))
+                        if (!allocated.count(c)) avail.push_back(c);
+                    if ((int64_t)avail.size() < (int64_t)t.cores) {   // no preemption for cores ("TODO")
+                        ctx->metrics.ExhaustedNode(&n, "cores");
+                        skip = true;
+                        break;
+                    }
+                    option->cores.insert(option->cores.end(), avail.begin(), avail.begin() + t.cores);
+                    if (n.total_cores == 0) throw Unsupported("TotalCpuCores = 0 (SharesPerCore divides by it)");
+                    spc = n.cpu / (int64_t)n.total_cores;   // SharesPerCore (structs.go:3047-3049)
+                }
             }
             if (skip) continue;
-            Ask ask = tg_ask(*tg, oversub);
+            Ask ask = tg_ask(*tg, oversub, spc);
+            option->cpu = ask.cpu;
             // AllocsFit(node, proposed + ask): used over non-terminal allocs
             int64_t ucpu = ask.cpu, umem = ask.mem, udisk = ask.disk;
             for (const OAlloc* a : proposed) { if (a->terminal) continue; ucpu += a->cpu; umem += a->mem; udisk += a->disk; }
             int64_t acpu = n.cpu - n.rcpu, amem = n.mem - n.rmem, adisk = n.disk - n.rdisk;
             const char* dim = nullptr;
-            if (acpu < ucpu) dim = "cpu";
+            // reserved cores: overlap between allocs, then Superset's cores
+            // check against ReservableCpuCores - ReservedCpuCores (funcs.go:148-180,
+            // structs.go:3891-3906)
+            bool core_overlap = false, core_outside = false;
+            {
+                std::set<uint16_t> used;
+                auto add = [&](const std::vector<uint16_t>& cs) {
+                    for (uint16_t c : std::set<uint16_t>(cs.begin(), cs.end()))
+                        if (!used.insert(c).second) core_overlap = true;
+                };
+                for (const OAlloc* a : proposed) if (!a->terminal) add(a->cores);
+                add(option->cores);
+                std::set<uint16_t> av(n.rcores.begin(), n.rcores.end());
+                for (uint16_t c : n.nrsv_cores) av.erase(c);
+                if (!av.empty())
+                    for (uint16_t c : used) core_outside = core_outside || !av.count(c);
+            }
+            if (core_overlap) dim = "cores";
+            else if (acpu < ucpu) dim = "cpu";
+            else if (core_outside) dim = "cores";
             else if (amem < umem) dim = "memory";
             else if (adisk < udisk) dim = "disk";
             if (dim) {
@@ -1662,6 +1706,8 @@ struct oracle_stack {
     bool have_job_version = false; uint64_t job_version = 0;
     int offer_row = -1;                                // device offers of the last Select's pick
     std::vector<std::pair<int, int>> offers;
+    std::vector<uint16_t> offer_cores;                 // and its reserved cores / CpuShares
+    int64_t offer_cpu = 0;
 
     explicit oracle_stack(const pe_config& c) : cfg(c) {
         ctx.state = &state;
@@ -1752,6 +1798,11 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
             }
             n.devs.push_back(d);
         }
+        if (nt->core_off)
+            n.rcores.assign(nt->core_id + nt->core_off[i], nt->core_id + nt->core_off[i + 1]);
+        if (nt->rsv_core_off)
+            n.nrsv_cores.assign(nt->rsv_core_id + nt->rsv_core_off[i], nt->rsv_core_id + nt->rsv_core_off[i + 1]);
+        n.total_cores = nt->total_cores ? nt->total_cores[i] : 0;
     }
     st.allocs.resize(at ? at->count : 0);
     st.allocs_by_node.assign(nt->n, {});
@@ -1769,6 +1820,7 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
         if (at->dev_off)
             for (uint32_t k = at->dev_off[i]; k < at->dev_off[i + 1]; k++)
                 a.devs.push_back({(int)at->dev_group[k], (int)at->dev_count[k]});
+        if (at->core_off) a.cores.assign(at->core_id + at->core_off[i], at->core_id + at->core_off[i + 1]);
         st.allocs_by_node[a.node_row].push_back((int)i);
     }
     s->ctx.plan = Plan();
@@ -1941,6 +1993,8 @@ static void fill_out(pe_ranked_node* out, RankedNode* o, const oracle_stack* s) 
         if (o->offers.size() > PE_MAX_DEVICE_REQ) throw Unsupported("more than PE_MAX_DEVICE_REQ device requests");
         out->n_device_offers = (uint32_t)o->offers.size();
         for (size_t i = 0; i < o->offers.size(); i++) out->device_offer_group[i] = (uint32_t)o->offers[i].first;
+        for (uint16_t c : o->cores)
+            if (c < 256) out->reserved_cores[c >> 6] |= 1ull << (c & 63);
     }
 }
 
@@ -1983,7 +2037,7 @@ int oracle_select(oracle_stack* s, uint32_t tgi, const pe_select_options* opts, 
         RankedNode* o = s->cfg.stack_kind == PE_STACK_GENERIC ? generic_select(s, tgi, opts) : system_select(s, tgi);
         fill_out(out, o, s);
         s->offer_row = o ? o->node->row : -1;
-        if (o) s->offers = o->offers;
+        if (o) { s->offers = o->offers; s->offer_cores = o->cores; s->offer_cpu = o->cpu; }
     } catch (const Unsupported& e) {
         s->err = std::string("unsupported: ") + e.what();
         return PE_EUNSUPPORTED;
@@ -2006,6 +2060,8 @@ int oracle_commit(oracle_stack* s, uint32_t tgi, int32_t row) {
     tg_net_contrib(tg, &a.mbits, &a.dyn_ports);
     if (row == s->offer_row) {
         a.devs = s->offers;
+        a.cores = s->offer_cores;
+        a.cpu = s->offer_cpu;
     } else {   // commit without a Select of this node: assign on the proposed state
         const ONode& n = s->state.nodes[(size_t)row];
         DevAlloc dev(&n);
@@ -2017,6 +2073,16 @@ int oracle_commit(oracle_stack* s, uint32_t tgi, int32_t row) {
                 dev.AddReserved(g, (int64_t)r.count);
                 a.devs.push_back({g, (int)r.count});
             }
+        // reserved cores: the lowest free ones of the node, as BinPack picks them
+        int64_t need = 0;
+        for (auto& t : tg.tasks) need += t.cores > 0 ? t.cores : 0;
+        if (need > 0) {
+            std::set<uint16_t> allocated;
+            for (const OAlloc* p : s->ctx.ProposedAllocs(row)) allocated.insert(p->cores.begin(), p->cores.end());
+            for (uint16_t c : std::set<uint16_t>(n.rcores.begin(), n.rcores.end()))
+                if (!allocated.count(c) && (int64_t)a.cores.size() < need) a.cores.push_back(c);
+            a.cpu = tg_ask(tg, s->bin_pack.oversub, n.total_cores ? n.cpu / (int64_t)n.total_cores : 0).cpu;
+        }
     }
     s->offer_row = -1;
     s->ctx.plan.node_allocation[row].push_back(a);

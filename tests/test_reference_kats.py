@@ -181,3 +181,32 @@ def test_drivers_and_distinct_hosts(stack_cls):
     st.SetNodes(nodes)
     r = st.SelectRaw(0)
     assert r.row == -1 and r.nodes_filtered == 3
+
+
+def _core_node(nid, reservable=(0, 1)):
+    n = plain_node(nid, 2048, 2048, 0, 0)
+    n.total_cores = 2
+    n.reservable_cores = list(reservable)
+    n.compute_class()
+    return n
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_binpack_reserved_cores(stack_cls):
+    """rank_test.go:950-1065 TestBinPackIterator_ReservedCores: the node whose
+    cores are both held is exhausted ("cores"); the other one is picked and the
+    task gets core 1."""
+    nodes = [_core_node("n0"), _core_node("n1")]
+    allocs = [Allocation(node_id="n0", job_id="j1", task_group="web", cpu_shares=2048, memory_mb=2048,
+                         reserved_cores=[0, 1]),
+              Allocation(node_id="n1", job_id="j2", task_group="web", cpu_shares=1024, memory_mb=1024,
+                         reserved_cores=[0])]
+    job = Job(id="kat", task_groups=[TaskGroup(name="web", count=1, ephemeral_disk_mb=0, tasks=[
+        Task(name="web", driver="exec", cpu=0, memory_mb=1024, cores=1)])])
+    st = mk(stack_cls, nodes, allocs, job)
+    st.SetNodes(nodes)
+    r = st.SelectRaw(0)
+    assert r.row == 1 and r.reserved_cores == [1]
+    assert r.nodes_exhausted == 1
+    st.SetNodes([nodes[0]])
+    assert st.SelectRaw(0).row == -1
