@@ -418,6 +418,9 @@ struct pe_stack {
     std::vector<ParsedAffinity> job_affinities;
     std::vector<SpreadSpec> job_spreads;
     std::vector<std::unique_ptr<TgPlan>> tgs;
+    // retired task groups whose device tables the next SetJob reuses: freeing
+    // them (hipFree) would synchronise the device on every evaluation
+    std::vector<std::unique_ptr<TgPlan>> tg_pool;
     std::vector<std::pair<uint32_t, uint32_t>> plan;   // committed (tg name id, row)
 
     // SpreadIterator bookkeeping (spread.go:99-102, 254)
@@ -1457,6 +1460,36 @@ int build_alloc_state(pe_stack* s) {
     return PE_OK;
 }
 
+// Task groups of the previous job go to a small pool; a new one takes a
+// retired group's device buffers (same stream: later uploads are ordered after
+// the kernels that read them).
+void retire_tgs(pe_stack* s) {
+    for (auto& g : s->tgs)
+        if (s->tg_pool.size() < 16) s->tg_pool.push_back(std::move(g));
+    s->tgs.clear();
+}
+
+std::unique_ptr<TgPlan> new_tg(pe_stack* s) {
+    auto g = std::make_unique<TgPlan>();
+    if (s->tg_pool.empty()) return g;
+    std::unique_ptr<TgPlan> old = std::move(s->tg_pool.back());
+    s->tg_pool.pop_back();
+    auto take = [](DevMem& dst, DevMem& src) { std::swap(dst.p, src.p); std::swap(dst.bytes, src.bytes); };
+    take(g->class_ok, old->class_ok);
+    take(g->node_ok, old->node_ok);
+    take(g->class_aff, old->class_aff);
+    take(g->node_aff, old->node_aff);
+    take(g->alias_ok, old->alias_ok);
+    take(g->coll_tg, old->coll_tg);
+    take(g->dev_cls, old->dev_cls);
+    take(g->class_ok_batch, old->class_ok_batch);
+    take(g->node_feas, old->node_feas);
+    take(g->node_aux, old->node_aux);
+    take(g->aff_vals, old->aff_vals);
+    take(g->aff_idx, old->aff_idx);
+    return g;
+}
+
 pe::NodeSoA soa_of(pe_stack* s) {
     pe::NodeSoA a;
     a.n = (uint32_t)s->nodes.size();
@@ -2391,7 +2424,8 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     A.hash_bits = hash_bits_for(count, full);
     A.packed_overlay = packed_kbits(s, 1u << A.hash_bits, full);
     bool chain = false;
-    if (!full && s->use_base && count > 1 && A.limit <= pe_chain_max_limit()) {
+    // the phase-static chain is compiled without reserved cores (k_chain's registers)
+    if (!full && s->use_base && count > 1 && A.limit <= pe_chain_max_limit() && g.ask.cores == 0) {
         // count loop over one rotation at a time (k_base + k_chain): needs a
         // visit list without repeated rows
         chain = true;
@@ -2608,7 +2642,7 @@ void pe_stack_destroy(pe_stack* s) {
     if (s->comm) (void)ncclCommDestroy(s->comm);
     if (s->ev_x0) (void)hipEventDestroy(s->ev_x0);
     if (s->ev_x1) (void)hipEventDestroy(s->ev_x1);
-    s->tgs.clear();
+    retire_tgs(s);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->ev2) (void)hipEventDestroy(s->ev2);
@@ -2663,7 +2697,7 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
     s->have_state = true;
     s->have_job = false;
     s->have_job_version = false;
-    s->tgs.clear();
+    retire_tgs(s);
     s->visit.clear();
     s->offset = 0;
     return PE_OK;
@@ -2699,7 +2733,7 @@ int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* a
     s->sum_spread_weights = 0;
     s->have_job = false;
     s->have_job_version = false;
-    s->tgs.clear();
+    retire_tgs(s);
     s->visit.clear();
     s->offset = 0;
     HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -2737,7 +2771,7 @@ int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nod
     s->sum_spread_weights = 0;
     s->have_job = false;
     s->have_job_version = false;
-    s->tgs.clear();
+    retire_tgs(s);
     s->visit.clear();
     s->offset = 0;
     rc = build_alloc_state(s);
@@ -2778,7 +2812,7 @@ int pe_reset_plan(pe_stack* s) {
     s->sum_spread_weights = 0;
     s->have_job = false;
     s->have_job_version = false;
-    s->tgs.clear();
+    retire_tgs(s);
     s->offset = 0;
     return PE_OK;
 }
@@ -2829,10 +2863,10 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     s->job_spreads = conv_spreads(j->spread_off, j->spread_count);
     std::string job_unsupported;
 
-    s->tgs.clear();
+    retire_tgs(s);
     for (uint32_t gi = 0; gi < j->tg_count; gi++) {
         const pe_task_group& t = j->task_groups[gi];
-        auto g = std::make_unique<TgPlan>();
+        auto g = new_tg(s);
         g->name = t.name;
         g->count = t.count;
         g->unsupported = job_unsupported;
@@ -3502,6 +3536,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     const uint32_t n = (uint32_t)s->visit.size();
     if (!count || (std::getenv("PE_PLOOP") && std::getenv("PE_PLOOP")[0] == '0')) return PE_OK;
     if (!g.psets.empty() || g.psets_dynamic || !s->visit_unique || n == 0 || n > pe_ploop_max_n()) return PE_OK;
+    if (g.ask.cores > 0) return PE_OK;   // k_ploop is compiled without reserved cores
     for (size_t k = 0; k < s->tgs.size(); k++)
         if (k != tgi && s->tgs[k]->name == g.name) return PE_OK;
     if (retry && !s->preempt_unsupported.empty()) return PE_OK;
@@ -3910,7 +3945,7 @@ static bool spec_chain_path(pe_stack* s, TgPlan& g) {
     const uint32_t nv = (uint32_t)s->visit.size();
     (void)nv;
     return !tg_full_scan(s, g) && !s->cfg.preempt && s->use_base && s->visit_unique &&
-           s->limit <= pe_chain_max_limit();
+           s->limit <= pe_chain_max_limit() && g.ask.cores == 0;
 }
 
 static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* opts) {
@@ -4394,7 +4429,7 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
     A.commit = 1;
     A.writeback = 0;
     s->batch_chain = false;
-    if (!full && s->use_base && A.class_ok_stride == 0 && s->orders_unique && n <= pe_chain_max_n() &&
+    if (!full && s->use_base && A.class_ok_stride == 0 && s->orders_unique && n <= pe_chain_max_n() && g.ask.cores == 0 &&
         A.limit <= pe_chain_max_limit()) {
         // one base pass shared by every evaluation, then k_chain (persistent grid)
         HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(s->nodes.size(), 1)));

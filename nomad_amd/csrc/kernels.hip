@@ -1,6 +1,6 @@
 // HIP kernels of the MI355X placement engine (gfx950, wave64).
 //
-// k_place<BLOCK, FULL>  persistent count loop, one workgroup per evaluation.
+// k_place<BLOCK, FULL, CORES>  persistent count loop, one workgroup per evaluation.
 //   The node SoA in HBM is the snapshot's proposed state and is read-only
 //   during the loop; each evaluation keeps the allocs it places in a private
 //   LDS overlay (open-addressed hash keyed by node row: cpu/mem/disk/collision/
@@ -174,22 +174,36 @@ __device__ __forceinline__ uint32_t dev_after(const Ask& a, const DevClass& dc, 
     return free;
 }
 
-// Reserved cores (BinPackIterator, rank.go:437-466): every placement of the
-// task group on a node takes the lowest free cores (cpuset ToSlice order), so
-// the (dk+1)-th placement of an evaluation holds the free cores of rank
-// [dk*cores, (dk+1)*cores). False when fewer are free ("cores" exhausted).
-__device__ __forceinline__ bool core_pick(const NodeSoA& s, uint32_t row, uint32_t cores, uint32_t dk,
-                                          uint64_t ch[4]) {
+// Reserved cores of the (dk+1)-th placement on the row, out of line so that
+// the hot pipeline keeps its registers: status 1 when too few cores are free
+// ("cores"), 2 when a chosen core is outside the AllocsFit-available set;
+// cpu = the cores' CpuShares (SharesPerCore x cores).
+struct CoreFit {
+    int64_t cpu;
+    int32_t status;
+};
+
+__device__ __forceinline__ CoreFit core_fit(const uint64_t* rsvable, const uint64_t* used, const uint64_t* avail,
+                                         const int64_t* spc, uint32_t cores, uint32_t row, uint32_t dk) {
+    CoreFit f{0, 1};
+    if (!rsvable) return f;
     uint32_t skip = dk * cores, need = cores;
+    uint64_t out = 0, any_av = 0;
+#pragma unroll 1
     for (int w = 0; w < 4; w++) {
-        uint64_t f = s.core_rsvable[4 * row + w] & ~s.core_used[4 * row + w];
-        ch[w] = 0;
-        const uint32_t c = (uint32_t)__popcll(f);
+        any_av |= avail[4 * row + w];
+        uint64_t fr = rsvable[4 * row + w] & ~used[4 * row + w];
+        const uint32_t c = (uint32_t)__popcll(fr);
         if (skip >= c) { skip -= c; continue; }
-        for (; skip; skip--) f &= f - 1;
-        for (; f && need; need--) { ch[w] |= f & (~f + 1); f &= f - 1; }
+        for (; skip; skip--) fr &= fr - 1;
+        uint64_t ch = 0;
+        for (; fr && need; need--) { ch |= fr & (~fr + 1); fr &= fr - 1; }
+        out |= ch & ~avail[4 * row + w];
     }
-    return need == 0;
+    if (need) return f;
+    f.status = (any_av && out) ? 2 : 0;
+    f.cpu = (int64_t)cores * spc[row];
+    return f;
 }
 
 // CpuShares of one placement on the row: tasks with cores hold SharesPerCore x
@@ -199,14 +213,17 @@ __device__ __forceinline__ int64_t ask_cpu(const NodeSoA& s, const Ask& a, uint3
 }
 
 // Plan.AppendAlloc of k placements on the row: their cores leave the free set.
-__device__ __forceinline__ void core_take(const NodeSoA& s, const Ask& a, uint32_t row, uint32_t k) {
-    if (a.cores <= 0 || !s.core_rsvable) return;
-    uint32_t need = k * (uint32_t)a.cores;
+__device__ __forceinline__ void core_take_rows(const uint64_t* rsvable, uint64_t* used, uint32_t row, uint32_t need) {
+#pragma unroll 1
     for (int w = 0; w < 4 && need; w++) {
-        uint64_t f = s.core_rsvable[4 * row + w] & ~s.core_used[4 * row + w], t = 0;
+        uint64_t f = rsvable[4 * row + w] & ~used[4 * row + w], t = 0;
         for (; f && need; need--) { t |= f & (~f + 1); f &= f - 1; }
-        s.core_used[4 * row + w] |= t;
+        used[4 * row + w] |= t;
     }
+}
+
+__device__ __forceinline__ void core_take(const NodeSoA& s, const Ask& a, uint32_t row, uint32_t k) {
+    if (a.cores > 0 && s.core_rsvable) core_take_rows(s.core_rsvable, s.core_used, row, k * (uint32_t)a.cores);
 }
 
 // Inputs of the scoring half of the pipeline (everything after AllocsFit).
@@ -239,6 +256,7 @@ __device__ __forceinline__ bool distinct_ok(const TgTables& t, const double* tab
     return true;
 }
 
+template <bool kCores = true>
 __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
                                              const Ask& a, uint32_t dk, uint32_t row, const NodeIn& in,
                                              ScoreIn* si, const double* ptab = nullptr) {
@@ -282,13 +300,11 @@ __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t
     }
     int64_t acpu = a.cpu;
     bool core_out = false;
-    if (a.cores > 0) {   // reserved cores (rank.go:437-466), then AllocsFit's Superset check
-        uint64_t ch[4];
-        if (!s.core_rsvable || !core_pick(s, row, (uint32_t)a.cores, dk, ch)) return kExhausted;
-        acpu += (int64_t)a.cores * s.core_spc[row];
-        const uint64_t* av = s.core_avail + 4 * row;
-        if (av[0] | av[1] | av[2] | av[3])
-            core_out = ((ch[0] & ~av[0]) | (ch[1] & ~av[1]) | (ch[2] & ~av[2]) | (ch[3] & ~av[3])) != 0;
+    if (kCores && a.cores > 0) {   // reserved cores (rank.go:437-466), then AllocsFit's Superset check
+        const CoreFit f = core_fit(s.core_rsvable, s.core_used, s.core_avail, s.core_spc, (uint32_t)a.cores, row, dk);
+        if (f.status == 1) return kExhausted;
+        acpu += f.cpu;
+        core_out = f.status == 2;
     }
     const int64_t ucpu = r.used_cpu + (int64_t)(dk + 1) * acpu;
     const int64_t umem = r.used_mem + (int64_t)(dk + 1) * a.mem;
@@ -383,26 +399,26 @@ __device__ __forceinline__ void score_option(const Ask& a, double log10, const S
 }
 
 // The whole fused per-node pipeline.
-template <bool kKeepParts>
+template <bool kKeepParts, bool kCores = true>
 __device__ __forceinline__ void eval_loaded(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
                                             const Ask& a, uint32_t dk, const uint32_t* penalty_bits,
                                             double log10, const double* spread_tab, uint32_t row,
                                             const NodeIn& in, NodeEval* out) {
     ScoreIn si;
-    const int st = status_loaded(s, t, class_ok, a, dk, row, in, &si, spread_tab);
+    const int st = status_loaded<kCores>(s, t, class_ok, a, dk, row, in, &si, spread_tab);
     if (st != kOption) { out->status = st; return; }
     lookup_scores(t, penalty_bits, spread_tab, row, in.r.cls, &si);
     score_option<kKeepParts>(a, log10, si, out);
 }
 
-template <bool kKeepParts>
+template <bool kKeepParts, bool kCores = true>
 __device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, const uint8_t* class_ok,
                                           const Ask& a, const Overlay& ov, const uint32_t* penalty_bits,
                                           double log10, const double* spread_tab, uint32_t row,
                                           NodeEval* out) {
     NodeIn in;
     load_node(s, t, row, in);
-    eval_loaded<kKeepParts>(s, t, class_ok, a, ov_count(ov, row), penalty_bits, log10, spread_tab, row, in,
+    eval_loaded<kKeepParts, kCores>(s, t, class_ok, a, ov_count(ov, row), penalty_bits, log10, spread_tab, row, in,
                             out);
 }
 
@@ -469,13 +485,9 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
     }
     bool core_out = false;
     if (code == kTrOption && a.cores > 0) {                         // reserved cores (rank.go:437-466)
-        uint64_t ch[4];
-        if (!s.core_rsvable || !core_pick(s, row, (uint32_t)a.cores, 0, ch)) code = kTrCores;
-        else {
-            const uint64_t* av = s.core_avail + 4 * row;
-            if (av[0] | av[1] | av[2] | av[3])
-                core_out = ((ch[0] & ~av[0]) | (ch[1] & ~av[1]) | (ch[2] & ~av[2]) | (ch[3] & ~av[3])) != 0;
-        }
+        const CoreFit f = core_fit(s.core_rsvable, s.core_used, s.core_avail, s.core_spc, (uint32_t)a.cores, row, 0);
+        if (f.status == 1) code = kTrCores;
+        core_out = f.status == 2;
     }
     if (code == kTrOption) {                                        // AllocsFit → Superset order
         if (r.cap_cpu < r.used_cpu + ask_cpu(s, a, row)) code = kTrCpu;
@@ -685,6 +697,7 @@ __device__ __forceinline__ void record_offers(const NodeSoA& s, const Ask& a, co
 }
 
 // Result records of placement `it` of evaluation e (one lane).
+template <bool kCores = true>
 __device__ __forceinline__ void emit_placement(const BatchArgs& A, const uint8_t* class_ok, const Overlay& ov,
                                             const double* spread_tab, uint32_t e, uint32_t it, int win_row,
                                             double best_score, uint32_t consumed, uint32_t n_filtered,
@@ -703,8 +716,8 @@ __device__ __forceinline__ void emit_placement(const BatchArgs& A, const uint8_t
         for (int k = 0; k < PE_MAX_SCORES; k++) o.scores[k] = 0.0;
         if (win_row >= 0) {
             NodeEval ev;
-            eval_node<true>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab,
-                            (uint32_t)win_row, &ev);
+            eval_node<true, kCores>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab,
+                                    (uint32_t)win_row, &ev);
             o.final_score = ev.score;
             o.n_scores = ev.nscores;
             for (int k = 0; k < (int)ev.nscores && k < PE_MAX_SCORES; k++) o.scores[k] = ev.parts[k];
@@ -826,7 +839,7 @@ __device__ __forceinline__ void rec_block_reduce(SweepRec& r, SweepRec* red) {
 }
 
 // Merge an evaluation's overlay into the HBM SoA (the stack's plan persists).
-template <int BLOCK, bool FULL>
+template <int BLOCK, bool FULL, bool kCores = true>
 __device__ void writeback_overlay(const BatchArgs& A, const Overlay& ov, uint32_t H, const uint32_t* counts) {
     for (uint32_t h = threadIdx.x; h < H; h += BLOCK) {
         const uint32_t e = ov.keys[h];
@@ -834,8 +847,12 @@ __device__ void writeback_overlay(const BatchArgs& A, const Overlay& ov, uint32_
         const uint32_t row = ov.k ? e : e >> ov.kshift;
         const uint32_t k = ov.k ? ov.k[h] : e & ov.kmask;
         NodeRec& r = A.soa.rec[row];
-        r.used_cpu += (int64_t)k * ask_cpu(A.soa, A.ask, row);
-        core_take(A.soa, A.ask, row, k);
+        if (kCores) {
+            r.used_cpu += (int64_t)k * ask_cpu(A.soa, A.ask, row);
+            core_take(A.soa, A.ask, row, k);
+        } else {
+            r.used_cpu += (int64_t)k * A.ask.cpu;
+        }
         r.used_mem += (int64_t)k * A.ask.mem;
         r.used_disk += (int64_t)k * A.ask.disk;
         r.used_mbits += (int32_t)k * A.ask.commit_mbits;
@@ -851,7 +868,7 @@ __device__ void writeback_overlay(const BatchArgs& A, const Overlay& ov, uint32_
     }
 }
 
-template <int BLOCK, bool FULL>
+template <int BLOCK, bool FULL, bool CORES>
 __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
     __shared__ LoopShared<BLOCK> sh;
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
@@ -909,7 +926,7 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
                 uint32_t pos = offset + j;
                 if (pos >= n) pos -= n;
                 NodeEval ev;
-                eval_node<false>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab, perm[pos], &ev);
+                eval_node<false, CORES>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab, perm[pos], &ev);
                 if (ev.status == kFiltered) rec.filtered++;
                 else if (ev.status == kExhausted) rec.exhausted++;
                 else rec_add(rec, j, ev.score);
@@ -942,7 +959,7 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
                 uint32_t pos = offset + j;
                 if (pos >= n) pos -= n;
                 const uint32_t row = perm[pos];
-                eval_node<false>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab, row, &ev);
+                eval_node<false, CORES>(A.soa, A.tg, class_ok, A.ask, ov, A.penalty_bits, A.log10, spread_tab, row, &ev);
             }
             const bool is_opt = valid && ev.status == kOption;
             const bool is_np = is_opt && ev.score <= 0.0;
@@ -1007,7 +1024,7 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
         uint32_t no = n ? offset + (consumed % n) : 0u;
         if (no >= n) no -= n;
         if (tid == 0) {
-            emit_placement(A, class_ok, ov, spread_tab, e, it, win_row, best_score, consumed, n_filtered,
+            emit_placement<CORES>(A, class_ok, ov, spread_tab, e, it, win_row, best_score, consumed, n_filtered,
                            n_exhausted, no);
             if (win_row >= 0 && A.commit) commit_overlay(A.soa, A.tg, ov, counts, (uint32_t)win_row);
         }
@@ -1020,7 +1037,7 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
         A.eval_status[2 * e] = placed;
         A.eval_status[2 * e + 1] = offset;
     }
-    if (A.writeback) writeback_overlay<BLOCK, FULL>(A, ov, H, counts);
+    if (A.writeback) writeback_overlay<BLOCK, FULL, CORES>(A, ov, H, counts);
 }
 
 // Windowed count loop (limit < n: no affinities or spreads, so a node's result
@@ -1237,12 +1254,12 @@ __global__ void __launch_bounds__(256) k_base(BatchArgs A) {
         load_node(A.soa, A.tg, row, in);
         NodeEval ev;
         ev.score = 0.0;
-        eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+        eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, A.penalty_bits, A.log10, nullptr, row, in, &ev);
         A.base[j] = encode_eval(ev);
         if (A.base1) {
             NodeEval ev1;
             ev1.score = 0.0;
-            eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, 1u, A.penalty_bits, A.log10, nullptr, row, in,
+            eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, 1u, A.penalty_bits, A.log10, nullptr, row, in,
                                &ev1);
             A.base1[j] = encode_eval(ev1);
         }
@@ -1488,7 +1505,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     load_node(A.soa, A.tg, rd.x, in);
                     NodeEval ev;
                     ev.score = 0.0;
-                    eval_loaded<false>(A.soa, A.tg, A.tg.class_ok, A.ask, rd.y, A.penalty_bits, A.log10, nullptr,
+                    eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, rd.y, A.penalty_bits, A.log10, nullptr,
                                        rd.x, in, &ev);
                     const unsigned long long bits = (unsigned long long)gm::f2u(encode_eval(ev));
                     sh.redo[w] = make_uint2((uint32_t)bits, (uint32_t)(bits >> 32));
@@ -1756,7 +1773,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                         m.new_offset = next_off;
                         m.score = score;
                     } else if (A.full_out) {
-                        emit_placement(A, A.tg.class_ok, ov, nullptr, e, it, win_row, score, consumed, sh.sel_f[s],
+                        emit_placement<false>(A, A.tg.class_ok, ov, nullptr, e, it, win_row, score, consumed, sh.sel_f[s],
                                        sh.sel_x[s], next_off);
                     }
                     if (A.out) {
@@ -1802,7 +1819,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                         m.new_offset = cur;
                         m.score = best;
                     } else if (A.full_out) {
-                        emit_placement(A, A.tg.class_ok, ov, nullptr, e, placed, win_row, best, n, sh.sel_f[0],
+                        emit_placement<false>(A, A.tg.class_ok, ov, nullptr, e, placed, win_row, best, n, sh.sel_f[0],
                                        sh.sel_x[0], cur);
                     }
                     sh.n_emit = placed + 1;
@@ -1846,7 +1863,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 A.emit_n[1] = A.writeback ? sh.n_ov : 0u;
             }
         } else if (A.writeback) {
-            writeback_overlay<kChainBlock, false>(A, ov, H, nullptr);
+            writeback_overlay<kChainBlock, false, false>(A, ov, H, nullptr);   // no cores on the chain path
         }
         __syncthreads();
     }
@@ -1886,7 +1903,7 @@ __global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
             load_node(A.soa, A.tg, row, in);
             NodeEval ev;
             ev.score = 0.0;
-            eval_loaded<true>(A.soa, A.tg, A.tg.class_ok, A.ask, m.dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+            eval_loaded<true, false>(A.soa, A.tg, A.tg.class_ok, A.ask, m.dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
             o.final_score = ev.score;
             o.n_scores = ev.nscores;
             for (int q = 0; q < PE_MAX_SCORES; q++) if (q < (int)ev.nscores) o.scores[q] = ev.parts[q];
@@ -2005,11 +2022,16 @@ __global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts, u
 // Host-driven Plan.AppendAlloc on the HBM SoA (pe_commit). `offers`: the
 // device offers of the Select that chose the node (one byte per request), or
 // ~0u to assign them on the current state.
+template <bool kCores = true>
 __device__ __forceinline__ void commit_row(const NodeSoA& s, const TgTables& t, const Ask& a, uint32_t row,
                                            uint32_t offers) {
     NodeRec& r = s.rec[row];
-    r.used_cpu += ask_cpu(s, a, row);
-    core_take(s, a, row, 1);
+    if (kCores) {
+        r.used_cpu += ask_cpu(s, a, row);
+        core_take(s, a, row, 1);
+    } else {
+        r.used_cpu += a.cpu;
+    }
     r.used_mem += a.mem;
     r.used_disk += a.disk;
     r.used_mbits += a.commit_mbits;
@@ -2867,8 +2889,15 @@ hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, 
     const size_t lds = pe_place_lds_bytes(full, a->hash_bits, a->packed_overlay != 0);
     if (full) {
         // few evaluations: 1024-lane workgroups keep more rows in flight per pass
-        if (n_evals <= 64) hipLaunchKernelGGL((pe::k_place<1024, true>), dim3(n_evals), dim3(1024), lds, st, *a);
-        else hipLaunchKernelGGL((pe::k_place<256, true>), dim3(n_evals), dim3(256), lds, st, *a);
+        // reserved cores are a separate instantiation (their code costs the others registers)
+        const bool cores = a->ask.cores > 0;
+        if (n_evals <= 64) {
+            if (cores) hipLaunchKernelGGL((pe::k_place<1024, true, true>), dim3(n_evals), dim3(1024), lds, st, *a);
+            else hipLaunchKernelGGL((pe::k_place<1024, true, false>), dim3(n_evals), dim3(1024), lds, st, *a);
+        } else {
+            if (cores) hipLaunchKernelGGL((pe::k_place<256, true, true>), dim3(n_evals), dim3(256), lds, st, *a);
+            else hipLaunchKernelGGL((pe::k_place<256, true, false>), dim3(n_evals), dim3(256), lds, st, *a);
+        }
     } else {
         hipLaunchKernelGGL(pe::k_window, dim3(n_evals), dim3(64), lds, st, *a);
     }

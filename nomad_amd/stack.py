@@ -91,6 +91,18 @@ class SelectOptions:
     alloc_name: str = ""
 
 
+def _core_ids(mask) -> List[int]:
+    """Core ids of a 256-bit pe_ranked_node.reserved_cores mask, ascending."""
+    out = []
+    for w in range(4):
+        m = int(mask[w])
+        while m:
+            low = m & -m
+            out.append(64 * w + low.bit_length() - 1)
+            m ^= low
+    return out
+
+
 @dataclass
 class RankedNode:
     """RankedNode (rank.go:21-36) plus the AllocMetric counters."""
@@ -114,8 +126,7 @@ class RankedNode:
                    nodes_filtered=r.nodes_filtered, nodes_exhausted=r.nodes_exhausted,
                    new_offset=r.new_offset, preempted=[r.preempted[i] for i in range(r.n_preempted)],
                    device_offers=[r.device_offer_group[i] for i in range(r.n_device_offers)],
-                   reserved_cores=[64 * w + b for w in range(4) for b in range(64)
-                                   if (r.reserved_cores[w] >> b) & 1])
+                   reserved_cores=_core_ids(r.reserved_cores))
 
 
 class _Stack:
