@@ -108,6 +108,13 @@ typedef struct pe_node_table {
     const uint32_t* core_off; const uint16_t* core_id;
     const uint32_t* total_cores;
     const uint32_t* rsv_core_off; const uint16_t* rsv_core_id;
+    /* NodeResources.NodeNetworks[*].Addresses[*] in node order (CSR): Alias,
+       Address and its ReservedPorts spec (ParsePortRanges syntax, PE_NONE =
+       none); ReservedResources.Networks.ReservedHostPorts per node (PE_NONE =
+       none). NULL: no addresses (static port asks then find none) */
+    const uint32_t* addr_off; const uint32_t* addr_alias; const uint32_t* addr_ip;
+    const uint32_t* addr_rsv_ports;
+    const uint32_t* rsv_host_ports;
 } pe_node_table;
 
 /* ---- existing allocations of the snapshot (state AllocsByNode) ---------- */
@@ -131,6 +138,9 @@ typedef struct pe_alloc_table {
     const int32_t* max_parallel;
     /* ComparableResources().Flattened.Cpu.ReservedCores (CSR over allocs), or NULL */
     const uint32_t* core_off; const uint16_t* core_id;
+    /* ports the alloc holds (NetworkIndex.AddAllocs: AllocatedPorts HostIP /
+       Value, or the pre-0.12 networks' IP and ports), CSR over allocs, or NULL */
+    const uint32_t* port_off; const uint32_t* port_ip; const int32_t* port_value;
 } pe_alloc_table;
 
 /* ---- job specification (structs.Job / TaskGroup / Task) ----------------- */
@@ -173,6 +183,8 @@ typedef struct pe_task_group {
     uint32_t net_host_network;                /* host network alias of the ports ("default") */
     uint32_t volume_off, volume_count;        /* host volume requests */
     int32_t has_csi_volumes;                  /* CSI: not on the device path */
+    uint32_t rport_off, rport_count;          /* tg network ReservedPorts (static ports): into
+                                                 pe_job.rport_value / rport_label */
 } pe_task_group;
 #define PE_JOB_SERVICE 0
 #define PE_JOB_BATCH 1
@@ -196,6 +208,8 @@ typedef struct pe_job {
     const pe_affinity* device_affinities;
     const uint32_t* volume_source;           /* host volume requests: source name */
     const uint8_t* volume_read_only;
+    const int32_t* rport_value;              /* static ports: Port.Value and Port.Label */
+    const uint32_t* rport_label;
 } pe_job;
 
 /* ---- stack configuration (SchedulerConfiguration, operator.go:128-210) --- */

@@ -54,6 +54,8 @@ class pe_node_table(C.Structure):
         ("dev_attr_off", u32p), ("dev_attr_key", u32p), ("dev_attr_val", C.POINTER(pe_attr)),
         ("core_off", u32p), ("core_id", u16p), ("total_cores", u32p),
         ("rsv_core_off", u32p), ("rsv_core_id", u16p),
+        ("addr_off", u32p), ("addr_alias", u32p), ("addr_ip", u32p), ("addr_rsv_ports", u32p),
+        ("rsv_host_ports", u32p),
     ]
 
 
@@ -67,6 +69,7 @@ class pe_alloc_table(C.Structure):
         ("dev_off", u32p), ("dev_group", u32p), ("dev_count", u32p),
         ("max_parallel", i32p),
         ("core_off", u32p), ("core_id", u16p),
+        ("port_off", u32p), ("port_ip", u32p), ("port_value", i32p),
     ]
 
 
@@ -120,6 +123,7 @@ class pe_task_group(C.Structure):
         ("net_host_network", C.c_uint32),
         ("volume_off", C.c_uint32), ("volume_count", C.c_uint32),
         ("has_csi_volumes", C.c_int32),
+        ("rport_off", C.c_uint32), ("rport_count", C.c_uint32),
     ]
 
 
@@ -142,6 +146,8 @@ class pe_job(C.Structure):
         ("device_affinities", C.POINTER(pe_affinity)),
         ("volume_source", u32p),
         ("volume_read_only", u8p),
+        ("rport_value", i32p),
+        ("rport_label", u32p),
     ]
 
 

@@ -70,6 +70,8 @@ hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* s
                             hipStream_t st);
 hipError_t pe_launch_resolve(const pe::EvictResolveArgs* r, hipStream_t st);
 hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st);
+hipError_t pe_launch_static_gate(const uint8_t* blocked, const uint32_t* coll_tg, uint32_t* gate, uint32_t n,
+                                 hipStream_t st);
 uint32_t pe_ploop_max_n();
 hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
                                     uint32_t* dev_free, uint32_t* placed, hipStream_t st);
@@ -196,6 +198,13 @@ struct HostAlloc {
     uint32_t dev_begin = 0, dev_end = 0;   // into pe_stack::alloc_dev
     uint64_t cores[4] = {0, 0, 0, 0};      // Flattened.Cpu.ReservedCores (ids < 256)
     bool cores_beyond = false;             // a reserved core id >= 256
+    uint32_t port_begin = 0, port_end = 0; // into pe_stack::alloc_ports: (HostIP str id, port) held
+};
+
+// One NodeNetworks address (NetworkIndex.SetNode, network.go:92-141).
+struct HostAddr {
+    uint32_t alias, ip;
+    std::vector<int> reserved;             // its ReservedPorts, parsed
 };
 
 // One device group of a node (NodeResources.Devices[i], structs.go:2980-3010).
@@ -281,6 +290,9 @@ struct TgPlan {
     DevMem class_ok, node_ok, class_aff, node_aff, alias_ok, coll_tg;
     bool tables_valid = false;
     bool has_aff_table = false, node_aff_used = false, node_ok_used = false, alias_used = false;
+    // static port asks (tg network ReservedPorts): (value, label) and the per-node gate
+    std::vector<std::pair<int32_t, uint32_t>> rports;
+    DevMem static_gate, static_blocked;
     std::vector<std::unique_ptr<PsetDev>> psets;
     bool psets_built = false;
     bool psets_dynamic = false;        // plan stops clear values: counts rebuilt on the host after every commit
@@ -329,6 +341,9 @@ struct pe_stack {
     std::vector<uint32_t> net_mode_ids, alias_ids;
     std::vector<HostAlloc> allocs;
     std::vector<std::pair<uint32_t, uint32_t>> alloc_dev;   // (device group on the node, instances held)
+    std::vector<std::pair<uint32_t, int32_t>> alloc_ports;  // (HostIP, port) held by allocs
+    std::vector<std::vector<HostAddr>> node_addrs;          // per node, node order
+    std::vector<std::vector<int>> node_rhp;                 // per node ReservedHostPorts, parsed
     // device groups per node (CSR) and their attributes
     std::vector<uint32_t> dev_off;
     std::vector<HostDevGroup> dev_groups;
@@ -961,10 +976,15 @@ void tg_ask(const pe_job* j, const pe_task_group& t, pe::Ask* a) {
     a->mem = sc_m + eph_m;
     a->disk = t.ephemeral_disk_mb;
     a->tg_dyn = t.has_network ? t.net_dyn_ports : 0;
+    a->static_dyn = 0;   // static ports in [MinDynamicPort, MaxDynamicPort]: the dynamic picks skip them
+    for (uint32_t k = 0; t.has_network && j->rport_value && k < t.rport_count; k++) {
+        const int32_t v = j->rport_value[t.rport_off + k];
+        a->static_dyn += (v >= 20000 && v <= 32000) ? 1 : 0;
+    }
     // NetworkIndex.AddAllocs contribution of the placed alloc (network.go:144-193)
     if (t.has_network && t.net_dyn_ports + t.net_reserved_ports > 0) {
         a->commit_mbits = 0;
-        a->commit_dyn = t.net_dyn_ports;
+        a->commit_dyn = t.net_dyn_ports + a->static_dyn;
     } else {
         a->commit_mbits = a->task_mbits;
         a->commit_dyn = a->task_dyn;
@@ -982,6 +1002,43 @@ int build_alloc_state(pe_stack* s);
 // copies; ComputedClass and checker signatures are interned into the persistent
 // maps, and a class / signature whose representative row changed gets another
 // member as its representative.
+// structs.ParsePortRanges (funcs.go:495-548) as NetworkIndex uses it: a spec
+// that does not parse reserves nothing; ports >= 65536 are dropped (the
+// reference stops at the first one in map order; ascending is one legal order).
+std::vector<int> parse_port_ranges(const std::string& spec) {
+    std::vector<int> out;
+    if (spec.empty()) return out;
+    size_t b = 0;
+    while (b <= spec.size()) {
+        size_t e = spec.find(',', b);
+        if (e == std::string::npos) e = spec.size();
+        std::string part = spec.substr(b, e - b);
+        while (!part.empty() && part.front() == ' ') part.erase(part.begin());
+        while (!part.empty() && part.back() == ' ') part.pop_back();
+        auto num = [](const std::string& x, uint64_t* v) {
+            if (x.empty() || x.size() > 19) return false;
+            uint64_t r = 0;
+            for (char c : x) { if (c < '0' || c > '9') return false; r = r * 10 + (uint64_t)(c - '0'); }
+            *v = r;
+            return true;
+        };
+        const size_t dash = part.find('-');
+        uint64_t lo, hi;
+        if (dash == std::string::npos) {
+            if (!num(part, &lo)) return {};
+            hi = lo;
+        } else {
+            if (part.find('-', dash + 1) != std::string::npos) return {};
+            if (!num(part.substr(0, dash), &lo) || !num(part.substr(dash + 1), &hi) || hi < lo) return {};
+        }
+        for (uint64_t v = lo; v <= hi && v < 65536; v++) out.push_back((int)v);
+        b = e + 1;
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+}
+
 int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t>& target, uint32_t n_new) {
     const uint32_t n_old = (uint32_t)s->nodes.size();
     const uint32_t m = nt->n;
@@ -1139,6 +1196,24 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         if (total == 0 && (rs[0] | rs[1] | rs[2] | rs[3])) bad = 1;
         s->h_core_bad[r] = bad;
     }
+    // NodeNetworks addresses and ReservedHostPorts (static port asks)
+    s->node_addrs.resize(n_new);
+    s->node_rhp.resize(n_new);
+    for (uint32_t r = 0; r < n_new; r++) {
+        if (src_of[r] < 0) continue;
+        const uint32_t i = (uint32_t)src_of[r];
+        auto& av = s->node_addrs[r];
+        av.clear();
+        for (uint32_t k = nt->addr_off ? nt->addr_off[i] : 0; nt->addr_off && k < nt->addr_off[i + 1]; k++) {
+            HostAddr a;
+            a.alias = nt->addr_alias[k];
+            a.ip = nt->addr_ip[k];
+            if (nt->addr_rsv_ports && nt->addr_rsv_ports[k] != PE_NONE) a.reserved = parse_port_ranges(s->S(nt->addr_rsv_ports[k]));
+            av.push_back(std::move(a));
+        }
+        s->node_rhp[r].clear();
+        if (nt->rsv_host_ports && nt->rsv_host_ports[i] != PE_NONE) s->node_rhp[r] = parse_port_ranges(s->S(nt->rsv_host_ports[i]));
+    }
     s->has_cores = false;
     s->cores_tg_unsupported.clear();
     for (uint32_t r = 0; r < n_new; r++) {
@@ -1271,6 +1346,7 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     if (rc) return rc;
     s->allocs.clear();
     s->alloc_dev.clear();
+    s->alloc_ports.clear();
     rc = append_allocs(s, at, nullptr);
     if (rc) return rc;
     return build_alloc_state(s);
@@ -1294,6 +1370,10 @@ int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index) 
         for (uint32_t k = at->dev_off ? at->dev_off[i] : 0; at->dev_off && k < at->dev_off[i + 1]; k++)
             s->alloc_dev.emplace_back(at->dev_group[k], at->dev_count[k]);
         a.dev_end = (uint32_t)s->alloc_dev.size();
+        a.port_begin = (uint32_t)s->alloc_ports.size();
+        for (uint32_t k = at->port_off ? at->port_off[i] : 0; at->port_off && k < at->port_off[i + 1]; k++)
+            s->alloc_ports.emplace_back(at->port_ip[k], at->port_value[k]);
+        a.port_end = (uint32_t)s->alloc_ports.size();
         for (uint32_t k = at->core_off ? at->core_off[i] : 0; at->core_off && k < at->core_off[i + 1]; k++) {
             const uint16_t c = at->core_id[k];
             if (c >= 256) a.cores_beyond = true;
@@ -1327,6 +1407,15 @@ int build_alloc_state(pe_stack* s) {
             a.dev_end = (uint32_t)live.size();
         }
         s->alloc_dev.swap(live);
+        std::vector<std::pair<uint32_t, int32_t>> lp;
+        lp.reserve(s->alloc_ports.size());
+        for (HostAlloc& a : s->allocs) {
+            const uint32_t b = (uint32_t)lp.size();
+            for (uint32_t k = a.port_begin; k < a.port_end; k++) lp.push_back(s->alloc_ports[k]);
+            a.port_begin = b;
+            a.port_end = (uint32_t)lp.size();
+        }
+        s->alloc_ports.swap(lp);
     }
     // non-terminal allocs per job (SetJob and the collision / property counts
     // touch only the job's own allocs)
@@ -1487,7 +1576,60 @@ std::unique_ptr<TgPlan> new_tg(pe_stack* s) {
     take(g->node_aux, old->node_aux);
     take(g->aff_vals, old->aff_vals);
     take(g->aff_idx, old->aff_idx);
+    take(g->static_gate, old->static_gate);
+    take(g->static_blocked, old->static_blocked);
     return g;
+}
+
+// Why the group's static ports cannot go on `row` under the current plan
+// (AssignPorts, network.go:317-363; the reference's error text in *why), or
+// false when they fit. The used ports of an address: the node's reservations
+// for its IP, ReservedHostPorts, the ports the proposed snapshot allocs hold
+// on it (plan stops and preemptions excluded).
+bool static_port_reason(pe_stack* s, const TgPlan& g, uint32_t row, std::string* why) {
+    const HostAddr* ad = nullptr;
+    if (row < s->node_addrs.size())
+        for (const HostAddr& a : s->node_addrs[row]) if (a.alias == g.net_host) { ad = &a; break; }
+    for (const auto& rp : g.rports) {
+        if (!ad) {
+            if (why) *why = "no addresses available for \"" + s->S(g.net_host) + "\" network";
+            return true;
+        }
+        if (rp.first < 0 || rp.first >= 65536) {
+            if (why) *why = "invalid port " + std::to_string(rp.first) + " (out of range)";
+            return true;
+        }
+        bool used = false;
+        for (const HostAddr& a : s->node_addrs[row])
+            if (a.ip == ad->ip) used = used || std::binary_search(a.reserved.begin(), a.reserved.end(), rp.first);
+        if (row < s->node_rhp.size())
+            used = used || std::binary_search(s->node_rhp[row].begin(), s->node_rhp[row].end(), rp.first);
+        for (uint32_t k = s->h_node_alloc_off[row]; k < s->h_node_alloc_off[row + 1] && !used; k++) {
+            if (s->h_preempted[k]) continue;   // a plan stop (2) or preemption (1)
+            const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+            for (uint32_t q = a.port_begin; q < a.port_end; q++)
+                used = used || (s->alloc_ports[q].first == ad->ip && s->alloc_ports[q].second == rp.first);
+        }
+        if (used) {
+            if (why) *why = "reserved port collision " + (rp.second == PE_NONE ? std::string() : s->S(rp.second)) + "=" +
+                            std::to_string(rp.first);
+            return true;
+        }
+    }
+    return false;
+}
+
+// The collision text when the group's own placement holds the ports (its first static port).
+std::string static_port_collision(pe_stack* s, const TgPlan& g) {
+    if (g.rports.empty()) return "reserved port collision";
+    const auto& rp = g.rports.front();
+    return "reserved port collision " + (rp.second == PE_NONE ? std::string() : s->S(rp.second)) + "=" +
+           std::to_string(rp.first);
+}
+
+// Static port gates follow ProposedAllocs: stops and evictions free ports.
+void invalidate_static(pe_stack* s) {
+    for (auto& g : s->tgs) if (!g->rports.empty()) g->tables_valid = false;
 }
 
 pe::NodeSoA soa_of(pe_stack* s) {
@@ -1902,6 +2044,21 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         HIP_TRY(s, upload_s(s, g.alias_ok, al));
         g.alias_used = true;
     }
+    if (!g.rports.empty()) {
+        // AssignPorts' static ports (network.go:317-363) on the current plan: a
+        // node is blocked when a port is invalid, its host network has no
+        // address, or the port is used on that address (the node's reservations,
+        // ReservedHostPorts, the proposed snapshot allocs, this group's
+        // placements). The device adds the group's later placements (gate).
+        std::vector<uint8_t> blocked(n, 0);
+        for (uint32_t r = 0; r < (uint32_t)n; r++) blocked[r] = static_port_reason(s, g, r, nullptr) ? 1 : 0;
+        for (auto& p : s->plan)
+            if (p.first == g.name && p.second < n) blocked[p.second] = 1;
+        HIP_TRY(s, upload_s(s, g.static_blocked, blocked));
+        HIP_TRY(s, g.static_gate.ensure(sizeof(uint32_t) * std::max<size_t>(n, 1)));
+        HIP_TRY(s, pe_launch_static_gate(g.static_blocked.as<uint8_t>(), g.coll_tg.as<uint32_t>(),
+                                         g.static_gate.as<uint32_t>(), (uint32_t)n, s->stream));
+    }
     g.tables_valid = true;
     return PE_OK;
 }
@@ -1915,6 +2072,7 @@ pe::TgTables tables_of(TgPlan& g) {
     t.class_aff = (g.has_aff_table && !g.node_aff_used) ? g.class_aff.as<double>() : nullptr;
     t.node_aff = g.node_aff_used ? g.node_aff.as<double>() : nullptr;
     t.alias_ok = g.alias_used ? g.alias_ok.as<uint8_t>() : nullptr;
+    t.static_gate = g.rports.empty() ? nullptr : g.static_gate.as<uint32_t>();
     t.coll_tg = g.coll_tg.as<uint32_t>();
     if (!g.dev_reqs.empty()) {
         t.dev_free = g.dev_free;
@@ -2307,6 +2465,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     *new_offset = n ? offset % n : 0;
     if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
     if (g.ask.cores > 0) return s->fail(PE_EUNSUPPORTED, "reserved cores with preemption");
+    if (!g.rports.empty()) return s->fail(PE_EUNSUPPORTED, "static port asks with preemption (PreemptForNetwork)");
     if (n == 0) return PE_OK;
     pe::PreemptArgs P = preempt_args(s, g);
     HIP_TRY(s, upload_visit(s, order));
@@ -2900,7 +3059,10 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
         g->net_mode = t.has_network ? t.net_mode : s->lookup("host");
         g->net_host = t.net_host_network;
         g->net_ports = t.net_dyn_ports + t.net_reserved_ports;
-        if (t.has_network && t.net_reserved_ports > 0) g->unsupported = "static port asks";
+        for (uint32_t k = 0; t.has_network && j->rport_value && k < t.rport_count; k++)
+            g->rports.emplace_back(j->rport_value[t.rport_off + k], j->rport_label ? j->rport_label[t.rport_off + k] : PE_NONE);
+        if (t.has_network && (int64_t)g->rports.size() != (int64_t)t.net_reserved_ports)
+            g->unsupported = "static port asks without their values (pe_task_group.rport_*)";
         // affinities: job, task group, tasks (rank.go:671-686)
         g->affinities = s->job_affinities;
         for (uint32_t k = 0; k < t.affinity_count; k++)
@@ -2936,6 +3098,13 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
         if (!generic && (!g->spreads.empty() || !s->job_spreads.empty())) g->spreads.clear();
         if (!generic) g->affinities.clear();
         s->tgs.push_back(std::move(g));
+    }
+    {   // static ports of one group only: a sibling's placements would hold them too
+        int with_static = 0;
+        for (auto& g : s->tgs) with_static += g->rports.empty() ? 0 : 1;
+        if (with_static > 1)
+            for (auto& g : s->tgs)
+                if (!g->rports.empty()) g->unsupported = "static port asks in several task groups of a job";
     }
     if (!generic) s->job_spreads.clear();
     // task networks must resolve against a single host device network on every node
@@ -3263,6 +3432,12 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                     break;
                 }
                 case pe::kTrNoAddr: exhaust(row, "network: no addresses available"); break;
+                case pe::kTrStaticPort: {
+                    std::string why;
+                    if (!static_port_reason(s, g, row, &why)) why = static_port_collision(s, g);
+                    exhaust(row, "network: " + why);
+                    break;
+                }
                 case pe::kTrDynPorts: exhaust(row, "network: dynamic port selection failed"); break;
                 case pe::kTrNoNetworks: exhaust(row, "network: no networks available"); break;
                 case pe::kTrBandwidth: exhaust(row, "network: bandwidth exceeded"); break;
@@ -3516,6 +3691,7 @@ static int commit_preempt_impl(pe_stack* s, uint32_t tgi, int32_t row, const uin
                                         s->d_pcount.as<uint32_t>(), s->d_dev_free.as<uint32_t>(), s->stream));
     for (uint32_t i = 0; i < n_preempted; i++) {
         s->h_preempted[s->alloc_slot[preempted[i]]] = 1;
+        invalidate_static(s);
         core_hold(s, preempted[i], false);
     }
     return commit_impl(s, tgi, row);
@@ -3537,6 +3713,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     if (!count || (std::getenv("PE_PLOOP") && std::getenv("PE_PLOOP")[0] == '0')) return PE_OK;
     if (!g.psets.empty() || g.psets_dynamic || !s->visit_unique || n == 0 || n > pe_ploop_max_n()) return PE_OK;
     if (g.ask.cores > 0) return PE_OK;   // k_ploop is compiled without reserved cores
+    if (!g.rports.empty()) return PE_OK;  // the static port gate is rebuilt on the host after evictions
     for (size_t k = 0; k < s->tgs.size(); k++)
         if (k != tgi && s->tgs[k]->name == g.name) return PE_OK;
     if (retry && !s->preempt_unsupported.empty()) return PE_OK;
@@ -3636,6 +3813,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
                 out[k].preempted[out[k].n_preempted++] = s->h_palloc_index[b + i];
                 s->h_preempted[b + i] = 1;
                 core_hold(s, s->h_palloc_index[b + i], false);
+                invalidate_static(s);
             }
     }
     *placed = p;
@@ -4149,6 +4327,7 @@ static int apply_stop_delta(pe_stack* s, const std::vector<uint32_t>& allocs, in
         slots.push_back(slot);
         rows.push_back(a.row);
         core_hold(s, ai, sign < 0);   // its reserved cores leave (rejoin) the node's used set
+        invalidate_static(s);         // and its ports
     }
     if (!slots.empty()) {
         HIP_TRY(s, upload_s(s, s->d_stop_slots, slots));
@@ -4723,6 +4902,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
         if (!rows.empty()) {
             if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
             if (g.ask.cores > 0) return s->fail(PE_EUNSUPPORTED, "reserved cores with preemption");
+            if (!g.rports.empty()) return s->fail(PE_EUNSUPPORTED, "static port asks with preemption (PreemptForNetwork)");
             // the max_parallel penalty reads the plan's preemption counts, which
             // earlier nodes grow: then the nodes go one at a time in list order
             bool serial = false;
@@ -4802,6 +4982,7 @@ int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_s
                         if ((masks[k] >> i) & 1u) {
                             s->h_preempted[b + i] = 1;
                             core_hold(s, s->h_palloc_index[b + i], false);
+                            invalidate_static(s);
                         }
                     p++;
                 }

@@ -25,6 +25,7 @@ constexpr int kMaxDevGroups = 4;      // device groups per node on device (u8 fr
 enum : uint32_t {
     kTrOption = 0, kTrDistinctHosts = 1, kTrDistinctProp = 2,
     kTrNoAddr = 10, kTrDynPorts = 11, kTrNoNetworks = 12, kTrBandwidth = 13, kTrTaskDyn = 14,
+    kTrStaticPort = 15,         // the reason string is rebuilt on the host (static_port_reason)
     kTrDevNone = 20, kTrDevZero = 21, kTrDevNoMatch = 22,
     kTrCpu = 30, kTrMemory = 31, kTrDisk = 32, kTrCores = 33,
     kTrMismatch = 254,          // device verdict disagrees with the host walk (bug guard)
@@ -73,6 +74,8 @@ struct TgTables {
     const double* node_aff;      // [n] or null
     const uint8_t* alias_ok;     // [n] or null: node has an address for the tg's port network
     uint32_t* coll_tg;           // [n] proposed allocs of (job, tg) per node
+    const uint32_t* static_gate; // [n] or null: static port asks; 0 = a port is taken (or no address), else
+                                 // coll_tg + 1 when the gate was built (a later placement of the group holds them)
     int n_psets;                                 // spread property sets first, then distinct_property sets
     int n_spread;                                // psets [0, n_spread) score, [n_spread, n_psets) filter
     uint32_t pset_allowed[kMaxPsets];            // distinct_property: allowed use count per value
@@ -99,6 +102,7 @@ struct Ask {
     int32_t algo_spread;
     int32_t anti_aff;             // JobAntiAffinityIterator present (GenericStack only)
     int32_t cores;                // Σ Resources.Cores of the tasks (cpu: the other tasks' CpuShares)
+    int32_t static_dyn;           // static ports of the ask inside the dynamic range (skipped by the dynamic picks)
     int32_t n_dev;                // device requests of the task group (tasks in order)
     uint32_t dev_aff;             // bit q: request q has affinities
     int32_t dev_cnt[kMaxDevReq];  // RequestedDevice.Count

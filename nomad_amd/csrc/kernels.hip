@@ -277,12 +277,18 @@ __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t
     }
     if (ok && t.n_psets > t.n_spread) ok = distinct_ok(t, ptab, row, c);
     if (!ok) return kFiltered;
-    // BinPackIterator (rank.go:193-527): network offers, then AllocsFit
+    // BinPackIterator (rank.go:193-527): network offers, then AllocsFit.
+    // AssignPorts' static ports first (network.go:317-363): the host-built gate
+    // (free on the node's address, no placement of the group since)
+    if (t.static_gate) {
+        const uint32_t gt = t.static_gate[row];
+        if (gt == 0u || in.coll_tg + dk + 1u != gt) return kExhausted;
+    }
     if (a.tg_dyn > 0 || a.has_task_net) {
         int32_t dyn = r.used_dyn + (int32_t)dk * a.commit_dyn;
         if (a.tg_dyn > 0) {
-            if ((t.alias_ok && !t.alias_ok[row]) || kDynPortCapacity - dyn < 1) return kExhausted;
-            dyn += a.tg_dyn;
+            if ((t.alias_ok && !t.alias_ok[row]) || kDynPortCapacity - dyn - a.static_dyn < 1) return kExhausted;
+            dyn += a.tg_dyn + a.static_dyn;
         }
         if (a.has_task_net) {
             const int32_t avail = r.avail_mbits;
@@ -447,12 +453,15 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
             if (v == kMissing || t.pset_counts[p][v] >= t.pset_allowed[p]) code = kTrDistinctProp | ((uint32_t)p << 8);
         }
     }
+    if (code == kTrOption && t.static_gate &&                      // AssignPorts static ports (network.go:317-363)
+        (t.static_gate[row] == 0u || in.coll_tg + 1u != t.static_gate[row]))
+        code = kTrStaticPort;
     if (code == kTrOption && (a.tg_dyn > 0 || a.has_task_net)) {   // rank.go:231-295
         int32_t dyn = r.used_dyn;
         if (a.tg_dyn > 0) {
             if (t.alias_ok && !t.alias_ok[row]) code = kTrNoAddr;
-            else if (kDynPortCapacity - dyn < 1) code = kTrDynPorts;
-            dyn += a.tg_dyn;
+            else if (kDynPortCapacity - dyn - a.static_dyn < 1) code = kTrDynPorts;
+            dyn += a.tg_dyn + a.static_dyn;
         }
         if (code == kTrOption && a.has_task_net) {
             if (r.avail_mbits < 0) code = kTrNoNetworks;
@@ -2873,11 +2882,21 @@ __global__ void __launch_bounds__(256) k_fold_aux(NodeSoA s, TgTables t, const u
     }
 }
 
+// Static port gate of a task group (status_loaded): blocked rows stay 0, the
+// others hold the group's collision count + 1 at build time.
+__global__ void __launch_bounds__(256) k_static_gate(const uint8_t* blocked, const uint32_t* coll_tg, uint32_t* gate,
+                                                     uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) gate[i] = blocked[i] ? 0u : coll_tg[i] + 1u;
+}
+
 #include "evict.inc"
 
 }  // namespace pe
 
 // ---- launch wrappers (host) ------------------------------------------------
+hipError_t pe_launch_static_gate(const uint8_t* blocked, const uint32_t* coll_tg, uint32_t* gate, uint32_t n,
+                                 hipStream_t st);
 size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed) {
     size_t b = (size_t)(packed ? 4u : 8u) * ((size_t)1 << hash_bits);
     if (full) b += sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1) + 4u * pe::kMaxPsets * pe::kMaxValues;
@@ -3231,5 +3250,12 @@ hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st) {
     }
     const size_t lds = pe_ploop_lds_bytes(n);
     hipLaunchKernelGGL(pe::k_ploop, dim3(1), dim3(pe::kPLoopBlock), lds, st, *a);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_static_gate(const uint8_t* blocked, const uint32_t* coll_tg, uint32_t* gate, uint32_t n,
+                                 hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_static_gate, dim3((n + 255) / 256), dim3(256), 0, st, blocked, coll_tg, gate, n);
     return hipGetLastError();
 }

@@ -176,6 +176,13 @@ class EncodedState:
         keep.extend([aoff, akeys_a, avals_a])
         nt.dev_attr_off, nt.dev_attr_key = _ptr(aoff, abi.u32p), _ptr(akeys_a, abi.u32p)
         nt.dev_attr_val = C.cast(avals_a, C.POINTER(abi.pe_attr))
+        # NodeNetworks addresses and the node's reserved host ports (static port asks)
+        NONE = abi.PE_NONE
+        off, al, ip, rp = csr(lambda x: [(I(a), I(b), I(c) if c else NONE) for a, b, c in x.node_addresses()],
+                              [_u32, _u32, _u32])
+        nt.addr_off, nt.addr_alias, nt.addr_ip, nt.addr_rsv_ports = (_ptr(a, abi.u32p) for a in (off, al, ip, rp))
+        nt.rsv_host_ports = _ptr(col(lambda x: I(",".join(str(p) for p in x.reserved_host_ports))
+                                     if x.reserved_host_ports else NONE, _u32), abi.u32p)
         if any(nd.reservable_cores or nd.reserved_cores or nd.total_cores for nd in nodes):
             off, cid = csr(lambda x: [(c,) for c in x.reservable_cores], [_u16])
             nt.core_off, nt.core_id = _ptr(off, abi.u32p), _ptr(cid, abi.u16p)
@@ -221,6 +228,17 @@ class EncodedState:
         at.dev_group = _ptr(dgrp_a, abi.u32p)
         at.dev_count = _ptr(dcnt_a, abi.u32p)
         at.max_parallel = _ptr(acol(lambda a: a.max_parallel, _i32), abi.i32p)
+        if any(a.ports for a in live):
+            poff = np.zeros(len(live) + 1, dtype=np.uint32)
+            pip, pval = [], []
+            for i, a in enumerate(live):
+                for h, v in a.ports:
+                    pip.append(I(h))
+                    pval.append(v)
+                poff[i + 1] = len(pip)
+            pip_a, pval_a = _u32(pip), _i32(pval)
+            keep.extend([poff, pip_a, pval_a])
+            at.port_off, at.port_ip, at.port_value = _ptr(poff, abi.u32p), _ptr(pip_a, abi.u32p), _ptr(pval_a, abi.i32p)
         if any(a.reserved_cores for a in live):
             coff = np.zeros(len(live) + 1, dtype=np.uint32)
             cid = []
@@ -264,6 +282,7 @@ class EncodedJob:
         cons, affs, spreads, targets, tasks, tgs = [], [], [], [], [], []
         devs, dcons, daffs = [], [], []
         vol_src, vol_ro = [], []
+        rport_val, rport_lab = [], []
 
         def add_cons(cs):
             off = len(cons)
@@ -325,6 +344,11 @@ class EncodedJob:
                 g.has_network, g.net_mode = 1, I(tg.network.mode)
                 g.net_dyn_ports, g.net_reserved_ports = tg.network.dynamic_ports, len(tg.network.reserved_ports)
                 g.net_host_network = I(tg.network.host_network)
+                g.rport_off, g.rport_count = len(rport_val), len(tg.network.reserved_ports)
+                for k, v in enumerate(tg.network.reserved_ports):
+                    rport_val.append(v)
+                    lab = tg.network.port_labels[k] if k < len(tg.network.port_labels) else ""
+                    rport_lab.append(I(lab))
             else:
                 g.net_mode = I("host")
                 g.net_host_network = I("default")
@@ -349,6 +373,10 @@ class EncodedJob:
         self._vr = _u8(vol_ro if vol_ro else [0])
         pj.volume_source = _ptr(self._vs, abi.u32p)
         pj.volume_read_only = _ptr(self._vr, abi.u8p)
+        self._rv = _i32(rport_val if rport_val else [0])
+        self._rl = _u32(rport_lab if rport_lab else [0])
+        pj.rport_value = _ptr(self._rv, abi.i32p)
+        pj.rport_label = _ptr(self._rl, abi.u32p)
         self.job = pj
         self.interner = interner
 

@@ -37,6 +37,7 @@ class NetworkResource:
     mbits: int = 0
     dynamic_ports: int = 0          # number of DynamicPorts in an ask
     reserved_ports: List[int] = field(default_factory=list)
+    port_labels: List[str] = field(default_factory=list)   # Port.Label of each reserved port (ask side)
     host_network: str = "default"   # Port.HostNetwork after Canonicalize()
 
 
@@ -72,10 +73,24 @@ class Node:
     reservable_cores: List[int] = field(default_factory=list)   # NodeResources.Cpu.ReservableCpuCores
     total_cores: int = 0                                        # NodeResources.Cpu.TotalCpuCores
     reserved_cores: List[int] = field(default_factory=list)     # ReservedResources.Cpu.ReservedCpuCores
+    # NodeNetworks[*].Addresses[*]: (alias, address, ReservedPorts spec); empty:
+    # one address per host_network_aliases entry at the first network's IP
+    addresses: List[Tuple[str, str, str]] = field(default_factory=list)
     status: str = "ready"
     drain: bool = False
     eligible: bool = True
     computed_class: str = ""
+
+    def node_addresses(self) -> List[Tuple[str, str, str]]:
+        """NodeNetworks addresses (alias, address, ReservedPorts spec) in node order."""
+        if self.addresses:
+            return list(self.addresses)
+        ip = ""
+        for w in self.networks:
+            ip = w.ip or (w.cidr.split("/")[0] if w.cidr else "")
+            if ip:
+                break
+        return [(a, ip, "") for a in self.host_network_aliases]
 
     def ready(self) -> bool:
         """Node.Ready (structs.go:1935-1937)."""
@@ -133,6 +148,7 @@ class Allocation:
     devices: List[Tuple[int, int]] = field(default_factory=list)
     max_parallel: int = 0         # TaskGroup.Migrate.MaxParallel of the alloc's job (preemption.go:146-150)
     reserved_cores: List[int] = field(default_factory=list)   # Flattened.Cpu.ReservedCores
+    ports: List[Tuple[str, int]] = field(default_factory=list)   # (HostIP, port) the alloc holds
 
 
 @dataclass

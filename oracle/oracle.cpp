@@ -74,6 +74,9 @@ struct ONode {
     std::vector<ODev> devs;
     std::vector<uint16_t> rcores, nrsv_cores;   // ReservableCpuCores, ReservedResources.Cpu.ReservedCpuCores
     uint32_t total_cores = 0;                   // TotalCpuCores
+    struct Addr { std::string alias, ip; std::vector<int> reserved; };
+    std::vector<Addr> addrs;                    // NodeNetworks[*].Addresses[*] in node order
+    std::vector<int> reserved_host_ports;       // ReservedResources.Networks.ReservedHostPorts
 };
 
 struct OAlloc {
@@ -88,6 +91,7 @@ struct OAlloc {
     int32_t max_parallel = 0;
     int state_index = -1;                    // row of the state alloc table (-1: plan alloc)
     std::vector<uint16_t> cores;             // Flattened.Cpu.ReservedCores (a set)
+    std::vector<std::pair<std::string, int>> ports;   // (HostIP, port) held (NetworkIndex.AddAllocs)
 };
 
 struct OConstraint { std::string l, r, op; };
@@ -125,6 +129,7 @@ struct OTaskGroup {
     std::vector<std::vector<OAffinity>> task_affinities;
     bool has_network; std::string net_mode, net_host_network;
     int32_t net_dyn, net_reserved;
+    std::vector<std::pair<int, std::string>> rports;     // ReservedPorts (Value, Label)
     std::vector<std::pair<std::string, bool>> volumes;   // host volume requests (source, read only)
     bool csi;
 };
@@ -907,6 +912,7 @@ struct RankedNode {
     std::vector<std::pair<int, int>> offers; // device offers (group, instances) per request
     std::vector<uint16_t> cores;             // Cpu.ReservedCores of the tasks, in task order
     int64_t cpu = 0;                         // the alloc's CpuShares (SharesPerCore x cores for core tasks)
+    std::vector<std::pair<std::string, int>> ports;   // static ports of the offer (HostIP, value)
 };
 
 struct RankIterator { virtual ~RankIterator() {} virtual RankedNode* Next() = 0; virtual void Reset() = 0; };
@@ -947,11 +953,50 @@ static Ask tg_ask(const OTaskGroup& tg, bool oversub, int64_t spc = -1) {
     return Ask{sc_cpu + eph_cpu, sc_mem + eph_mem, tg.disk};
 }
 
+// structs.ParsePortRanges (funcs.go:495-548) as NetworkIndex uses it: a spec
+// that does not parse reserves nothing; ports >= 65536 are dropped (the
+// reference stops at the first one in map order; ascending is one legal order).
+static std::vector<int> parse_port_ranges(const std::string& spec) {
+    std::set<int> ports;
+    if (spec.empty()) return {};
+    size_t b = 0;
+    while (b <= spec.size()) {
+        size_t e = spec.find(',', b);
+        if (e == std::string::npos) e = spec.size();
+        std::string part = spec.substr(b, e - b);
+        while (!part.empty() && part.front() == ' ') part.erase(part.begin());
+        while (!part.empty() && part.back() == ' ') part.pop_back();
+        auto num = [](const std::string& x, uint64_t* v) {
+            if (x.empty() || x.size() > 19) return false;
+            uint64_t r = 0;
+            for (char c : x) { if (c < '0' || c > '9') return false; r = r * 10 + (uint64_t)(c - '0'); }
+            *v = r;
+            return true;
+        };
+        const size_t dash = part.find('-');
+        uint64_t lo, hi;
+        if (dash == std::string::npos) {
+            if (!num(part, &lo)) return {};
+            hi = lo;
+        } else {
+            if (part.find('-', dash + 1) != std::string::npos) return {};
+            if (!num(part.substr(0, dash), &lo) || !num(part.substr(dash + 1), &hi) || hi < lo) return {};
+        }
+        for (uint64_t v = lo; v <= hi && v < 65536; v++) ports.insert((int)v);
+        b = e + 1;
+    }
+    return std::vector<int>(ports.begin(), ports.end());
+}
+
 // NetworkIndex contribution of an alloc of this task group (network.go:144-193):
 // allocs with task-group ports only count their ports; otherwise task networks.
 static void tg_net_contrib(const OTaskGroup& tg, int32_t* mbits, int32_t* dyn) {
     *mbits = 0; *dyn = 0;
-    if (tg.has_network && tg.net_dyn + tg.net_reserved > 0) { *dyn = tg.net_dyn; return; }
+    if (tg.has_network && tg.net_dyn + tg.net_reserved > 0) {
+        *dyn = tg.net_dyn;
+        for (auto& p : tg.rports) *dyn += (p.first >= 20000 && p.first <= 32000) ? 1 : 0;
+        return;
+    }
     for (auto& t : tg.tasks) if (t.has_network) { *mbits += t.net_mbits; *dyn += t.net_dyn; }
 }
 
@@ -1276,8 +1321,37 @@ struct BinPackIterator : RankIterator {
             pre.job_priority = priority; pre.job_id = job_id; pre.job_ns = job_ns;
             pre.SetNode(n);
             pre.SetPreemptions(ctx->plan);
+            option->ports.clear();
             if (tg->has_network) {
-                if (tg->net_reserved > 0) throw Unsupported("static port asks");
+                // AssignPorts, ReservedPorts first (network.go:317-363): the first
+                // address of the port's host network; the port must be free on it
+                int32_t static_dyn = 0;
+                std::string perr;
+                for (auto& rp : tg->rports) {
+                    const ONode::Addr* ad = nullptr;
+                    for (auto& a : n.addrs) if (a.alias == tg->net_host_network) { ad = &a; break; }
+                    if (!ad) { perr = "no addresses available for \"" + tg->net_host_network + "\" network"; break; }
+                    if (rp.first < 0 || rp.first >= 65536) { perr = "invalid port " + std::to_string(rp.first) + " (out of range)"; break; }
+                    // used ports of the address: the node's reservations for that IP,
+                    // ReservedHostPorts (every address), the proposed allocs' ports
+                    bool used = false;
+                    for (auto& a : n.addrs)
+                        if (a.ip == ad->ip) for (int v : a.reserved) used = used || v == rp.first;
+                    for (int v : n.reserved_host_ports) used = used || v == rp.first;
+                    for (const OAlloc* a : proposed) {
+                        if (a->terminal) continue;
+                        for (auto& pp : a->ports) used = used || (pp.first == ad->ip && pp.second == rp.first);
+                    }
+                    if (used) { perr = "reserved port collision " + rp.second + "=" + std::to_string(rp.first); break; }
+                    option->ports.push_back({ad->ip, rp.first});
+                    static_dyn += (rp.first >= 20000 && rp.first <= 32000) ? 1 : 0;
+                }
+                if (!perr.empty()) {
+                    if (evict) throw Unsupported("network preemption");   // PreemptForNetwork path
+                    ctx->metrics.ExhaustedNode(&n, "network: " + perr);
+                    continue;
+                }
+                used_dyn += static_dyn;   // reservedIdx: the dynamic picks skip them
                 // AssignPorts: each dynamic port needs an address of its host network
                 // and one free port in [MinDynamicPort, MaxDynamicPort].
                 if (tg->net_dyn > 0) {
@@ -1706,8 +1780,9 @@ struct oracle_stack {
     bool have_job_version = false; uint64_t job_version = 0;
     int offer_row = -1;                                // device offers of the last Select's pick
     std::vector<std::pair<int, int>> offers;
-    std::vector<uint16_t> offer_cores;                 // and its reserved cores / CpuShares
+    std::vector<uint16_t> offer_cores;                 // and its reserved cores / CpuShares / static ports
     int64_t offer_cpu = 0;
+    std::vector<std::pair<std::string, int>> offer_ports;
 
     explicit oracle_stack(const pe_config& c) : cfg(c) {
         ctx.state = &state;
@@ -1803,6 +1878,15 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
         if (nt->rsv_core_off)
             n.nrsv_cores.assign(nt->rsv_core_id + nt->rsv_core_off[i], nt->rsv_core_id + nt->rsv_core_off[i + 1]);
         n.total_cores = nt->total_cores ? nt->total_cores[i] : 0;
+        for (uint32_t k = nt->addr_off ? nt->addr_off[i] : 0; nt->addr_off && k < nt->addr_off[i + 1]; k++) {
+            ONode::Addr a;
+            a.alias = S(st, nt->addr_alias[k]);
+            a.ip = S(st, nt->addr_ip[k]);
+            if (nt->addr_rsv_ports && nt->addr_rsv_ports[k] != PE_NONE) a.reserved = parse_port_ranges(S(st, nt->addr_rsv_ports[k]));
+            n.addrs.push_back(a);
+        }
+        if (nt->rsv_host_ports && nt->rsv_host_ports[i] != PE_NONE)
+            n.reserved_host_ports = parse_port_ranges(S(st, nt->rsv_host_ports[i]));
     }
     st.allocs.resize(at ? at->count : 0);
     st.allocs_by_node.assign(nt->n, {});
@@ -1821,6 +1905,8 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
             for (uint32_t k = at->dev_off[i]; k < at->dev_off[i + 1]; k++)
                 a.devs.push_back({(int)at->dev_group[k], (int)at->dev_count[k]});
         if (at->core_off) a.cores.assign(at->core_id + at->core_off[i], at->core_id + at->core_off[i + 1]);
+        if (at->port_off)
+            for (uint32_t k = at->port_off[i]; k < at->port_off[i + 1]; k++) a.ports.push_back({S(st, at->port_ip[k]), at->port_value[k]});
         st.allocs_by_node[a.node_row].push_back((int)i);
     }
     s->ctx.plan = Plan();
@@ -1887,6 +1973,8 @@ int oracle_set_job(oracle_stack* s, const pe_strtab* strs, const pe_job* j) {
         tg.net_host_network = S(st, t.net_host_network);
         if (tg.net_host_network.empty()) tg.net_host_network = "default";
         tg.net_dyn = t.net_dyn_ports; tg.net_reserved = t.net_reserved_ports;
+        for (uint32_t k = 0; k < t.rport_count && j->rport_value; k++)
+            tg.rports.push_back({j->rport_value[t.rport_off + k], S(st, j->rport_label[t.rport_off + k])});
         for (uint32_t k = 0; k < t.volume_count; k++)
             tg.volumes.push_back({S(st, j->volume_source[t.volume_off + k]), j->volume_read_only[t.volume_off + k] != 0});
         tg.csi = t.has_csi_volumes != 0;
@@ -2037,7 +2125,7 @@ int oracle_select(oracle_stack* s, uint32_t tgi, const pe_select_options* opts, 
         RankedNode* o = s->cfg.stack_kind == PE_STACK_GENERIC ? generic_select(s, tgi, opts) : system_select(s, tgi);
         fill_out(out, o, s);
         s->offer_row = o ? o->node->row : -1;
-        if (o) { s->offers = o->offers; s->offer_cores = o->cores; s->offer_cpu = o->cpu; }
+        if (o) { s->offers = o->offers; s->offer_cores = o->cores; s->offer_cpu = o->cpu; s->offer_ports = o->ports; }
     } catch (const Unsupported& e) {
         s->err = std::string("unsupported: ") + e.what();
         return PE_EUNSUPPORTED;
@@ -2062,6 +2150,7 @@ int oracle_commit(oracle_stack* s, uint32_t tgi, int32_t row) {
         a.devs = s->offers;
         a.cores = s->offer_cores;
         a.cpu = s->offer_cpu;
+        a.ports = s->offer_ports;
     } else {   // commit without a Select of this node: assign on the proposed state
         const ONode& n = s->state.nodes[(size_t)row];
         DevAlloc dev(&n);
