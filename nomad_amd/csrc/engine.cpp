@@ -4435,6 +4435,8 @@ int pe_place_sharded(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_beg
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     if (!tg_full_scan(s, g)) return s->fail(PE_EUNSUPPORTED, "sharded placement: a windowed task group (replicas only)");
+    if (g.ask.cores > 0 || !g.rports.empty())
+        return s->fail(PE_EUNSUPPORTED, "sharded placement with reserved cores or static ports");
     if (!s->visit_unique) return s->fail(PE_EUNSUPPORTED, "sharded placement needs a list without repeated rows");
     if (g.n_spread != (int)g.psets.size() || g.psets_dynamic)
         return s->fail(PE_EUNSUPPORTED, "sharded placement with distinct_property or cleared property values");

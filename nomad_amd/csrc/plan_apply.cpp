@@ -194,13 +194,17 @@ struct pe_planner {
         tmp->assign(t->bytes + t->offsets[caller], t->offsets[caller + 1] - t->offsets[caller]);
         return tmp;
     }
+    std::array<uint32_t, 3> last_tuple{{PE_NONE, PE_NONE, PE_NONE}};
+    uint32_t last_tuple_id = 0;
     uint32_t tuple(uint32_t v, uint32_t ty, uint32_t n) {
         auto key = std::array<uint32_t, 3>{v, ty, n};
+        if (key == last_tuple) return last_tuple_id;   // allocs of a node repeat their device type
+        last_tuple = key;
         auto it = tuple_id.find(key);
-        if (it != tuple_id.end()) return it->second;
+        if (it != tuple_id.end()) return last_tuple_id = it->second;
         const uint32_t id = (uint32_t)tuple_id.size();
         tuple_id.emplace(key, id);
-        return id;
+        return last_tuple_id = id;
     }
 
     // Flatten one alloc of a pe_plan_alloc_table (strings already mapped).

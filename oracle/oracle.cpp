@@ -1358,7 +1358,16 @@ struct BinPackIterator : RankIterator {
                     bool has_addr = false;
                     for (auto& a : n.aliases) if (a == tg->net_host_network) { has_addr = true; break; }
                     if (!has_addr || kDynPortCapacity - used_dyn < 1) {
-                        if (evict) throw Unsupported("network preemption");   // PreemptForNetwork path
+                        if (evict) {
+                            // PreemptForNetwork(ask) with no static ports and no MBits
+                            // (preemption.go:270-455): no candidate with a network, or
+                            // free bandwidth >= 0, returns nil; BinPack then skips the
+                            // node without an ExhaustedNode (rank.go:265-272)
+                            int32_t avail = 0;
+                            for (auto& nw : n.nets) if (!nw.device.empty()) { avail = std::max(nw.mbits, 0); break; }
+                            if (used_mbits > avail) throw Unsupported("network preemption");
+                            continue;
+                        }
                         ctx->metrics.ExhaustedNode(&n, !has_addr ? "network: no addresses available"
                                                                  : "network: dynamic port selection failed");
                         continue;

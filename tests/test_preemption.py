@@ -236,3 +236,29 @@ def test_c5_sparse_parallel_count_loop(preempt):
     _, _, re = run_place(_engine, nodes, allocs, job, perm, config=cfg)
     assert_same_placements(re, ro)
     assert [sorted(x.preempted) for x in re] == [sorted(x.preempted) for x in ro]
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_preempt_skips_nodes_without_dynamic_ports(stack_cls):
+    """BinPack with evict on a task-group port ask that a node cannot meet:
+    PreemptForNetwork (preemption.go:270-455) finds nothing to evict while the
+    node's bandwidth is not overcommitted, and the node is skipped
+    (rank.go:265-272) -- neither filtered nor exhausted."""
+    nodes = [synth.mock_node("n%d" % i) for i in range(6)]
+    for nd in nodes:
+        nd.compute_class()
+    allocs = []
+    for i, nd in enumerate(nodes):
+        # low-priority work fills cpu everywhere; nodes 0, 2, 4 also hold every dynamic port
+        allocs.append(Allocation(node_id=nd.id, job_id="batch-%d" % i, task_group="t", cpu_shares=3800,
+                                 memory_mb=256, priority=20, dyn_ports=12001 if i % 2 == 0 else 0))
+    job = synth.mock_job(count=3)
+    job.priority = 70
+    st = stack_cls(config=SchedulerConfig(preempt_service=True))
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(list(range(len(nodes))))
+    r = st.SelectRaw(0, SelectOptions(preempt=True))
+    # nodes 0, 2, 4 are skipped; 1, 3, 5 evict their batch alloc (limit 3); the first wins the tie
+    assert (r.row, r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted) == (1, 6, 0, 0)
+    assert r.preempted == [1]
