@@ -39,6 +39,8 @@ size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
+hipError_t pe_launch_counts(const pe::CountDsts* d, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
+                            hipStream_t st);
 size_t pe_fullpass_lds_bytes(uint32_t n);
 hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
                                   uint32_t count, pe_ranked_node* out, uint32_t* state, unsigned long long* prof,
@@ -386,6 +388,7 @@ struct pe_stack {
     // staged visit orders for pe_place_batch
     DevMem d_orders, d_batch_out, d_batch_status, d_sys_out;
     // full-scan sweep path
+    DevMem d_count_ents;   // sparse per-node counts (build_collisions)
     DevMem d_rank_of, d_sweep_recs, d_sweep_merged, d_spread_tab, d_record;
     uint32_t sweep_min = 1u << 15;     // visit lists at least this long use the multi-CU sweep
     uint32_t loop_sweep_min = 8192;    // full-pass count loops this long run device-resident sweeps
@@ -406,6 +409,7 @@ struct pe_stack {
     PinnedMem h_batch_out, h_batch_status;
     PinnedMem h_sys_out;   // SystemStack results, staged for the caller's arrays
     PinnedMem h_place_out, h_place_status;   // single-evaluation count loop results (mapped)
+    PinnedMem h_emit_out;                    // k_emit's compact records (mapped)
     PinnedMem h_stage;                 // upload staging ring (upload_s)
     unsigned char* stage_dev = nullptr;   // the ring as seen from the device (k_upload reads it)
     DevMem d_emit, d_emit_ov, d_emit_n;   // k_chain deferred records (k_emit)
@@ -1669,32 +1673,68 @@ void core_hold(pe_stack* s, uint32_t alloc, bool hold) {
     }
 }
 
-// Job-dependent per-node collision counts from the snapshot + the plan.
-int build_collisions(pe_stack* s) {
+// Job-dependent per-node collision counts from the snapshot + the plan, and
+// with `own` the job's own proposed state allocs per node (ProposedAllocs
+// minus plan placements and plan stops). The counts are mostly zero (a new
+// job, a short plan): the nonzero ones go up as a sorted sparse list and one
+// launch rewrites every array, instead of one dense upload per array.
+int build_collisions(pe_stack* s, bool own = false) {
     const size_t n = s->nodes.size();
-    std::vector<uint32_t> job(n, 0);
-    std::vector<std::vector<uint32_t>> tg(s->tgs.size(), std::vector<uint32_t>(n, 0));
-    auto add = [&](uint32_t row, uint32_t tgname) {
-        job[row]++;
-        for (size_t g = 0; g < s->tgs.size(); g++) if (s->tgs[g]->name == tgname) tg[g][row]++;
+    const uint32_t ntg = (uint32_t)s->tgs.size();
+    const uint32_t nd = ntg + 2;   // dst 0: own, 1: job, 2 + g: task group g
+    if (nd > (uint32_t)pe::kMaxCountDst || n >= (size_t(1) << 27)) {
+        std::vector<uint32_t> job(n, 0), mine(own ? n : 0, 0);
+        std::vector<std::vector<uint32_t>> tg(ntg, std::vector<uint32_t>(n, 0));
+        auto add = [&](uint32_t row, uint32_t tgname) {
+            job[row]++;
+            for (uint32_t g = 0; g < ntg; g++) if (s->tgs[g]->name == tgname) tg[g][row]++;
+        };
+        for (uint32_t i : s->own_allocs())
+            if (!s->stopped(i)) { add(s->allocs[i].row, s->allocs[i].tg); if (own) mine[s->allocs[i].row]++; }
+        for (auto& p : s->plan) add(p.second, p.first);
+        if (own) HIP_TRY(s, upload_s(s, s->d_own_existing, mine));
+        HIP_TRY(s, upload_s(s, s->d_coll_job, job));
+        for (uint32_t g = 0; g < ntg; g++) HIP_TRY(s, upload_s(s, s->tgs[g]->coll_tg, tg[g]));
+        return PE_OK;
+    }
+    std::vector<uint32_t> keys;
+    auto add = [&](uint32_t row, uint32_t tgname, bool is_own) {
+        const uint32_t base = row << 5;
+        if (is_own) keys.push_back(base);
+        keys.push_back(base | 1u);
+        for (uint32_t g = 0; g < ntg; g++) if (s->tgs[g]->name == tgname) keys.push_back(base | (2u + g));
     };
     for (uint32_t i : s->own_allocs())
-        if (!s->stopped(i)) add(s->allocs[i].row, s->allocs[i].tg);   // ProposedAllocs drops plan stops
-    for (auto& p : s->plan) add(p.second, p.first);
-    HIP_TRY(s, upload_s(s, s->d_coll_job, job));
-    for (size_t g = 0; g < s->tgs.size(); g++) HIP_TRY(s, upload_s(s, s->tgs[g]->coll_tg, tg[g]));
+        if (!s->stopped(i)) add(s->allocs[i].row, s->allocs[i].tg, own);   // ProposedAllocs drops plan stops
+    for (auto& p : s->plan) add(p.second, p.first, false);
+    std::sort(keys.begin(), keys.end());
+    std::vector<uint2> ents;
+    for (size_t i = 0; i < keys.size();) {
+        size_t j = i;
+        while (j < keys.size() && keys[j] == keys[i]) j++;
+        ents.push_back(make_uint2(keys[i], (uint32_t)(j - i)));
+        i = j;
+    }
+    pe::CountDsts D;
+    std::memset(&D, 0, sizeof(D));
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(uint32_t);
+    if (own) {
+        HIP_TRY(s, s->d_own_existing.ensure(bytes));
+        D.d[0] = s->d_own_existing.as<uint32_t>();
+    }
+    HIP_TRY(s, s->d_coll_job.ensure(bytes));
+    D.d[1] = s->d_coll_job.as<uint32_t>();
+    for (uint32_t g = 0; g < ntg; g++) {
+        HIP_TRY(s, s->tgs[g]->coll_tg.ensure(bytes));
+        D.d[2 + g] = s->tgs[g]->coll_tg.as<uint32_t>();
+    }
+    if (!ents.empty()) HIP_TRY(s, upload_s(s, s->d_count_ents, ents));
+    HIP_TRY(s, pe_launch_counts(&D, nd, (uint32_t)n, ents.empty() ? nullptr : s->d_count_ents.as<uint2>(),
+                                (uint32_t)ents.size(), s->stream));
     return PE_OK;
 }
 
-// The job's own proposed state allocs per node (ProposedAllocs minus plan
-// placements and plan stops) and the collision counts.
-int build_job_counts(pe_stack* s) {
-    std::vector<uint32_t> own(s->nodes.size(), 0);
-    for (uint32_t i : s->own_allocs())
-        if (!s->stopped(i)) own[s->allocs[i].row]++;
-    HIP_TRY(s, upload_s(s, s->d_own_existing, own));
-    return build_collisions(s);
-}
+int build_job_counts(pe_stack* s) { return build_collisions(s, true); }
 
 // propertySet cleared values (propertyset.go:159-209): the plan's stopped allocs
 // of the job (terminal ones included, filterAllocs(stopping, false)), less one
@@ -2634,6 +2674,10 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         A.emit = s->d_emit.as<pe::ChainEmit>();
         A.emit_ov = s->d_emit_ov.as<uint2>();
         A.emit_n = s->d_emit_n.as<uint32_t>();
+        HIP_TRY(s, s->h_emit_out.ensure(sizeof(pe::EmitRec) * cap));
+        A.emit_out = s->h_emit_out.dev<pe::EmitRec>();
+        if (!A.emit_out) return s->fail(PE_EHIP, "mapped result buffers unavailable");
+        A.full_out = nullptr;
     }
     double total_ms = 0;
     uint32_t done = 0;
@@ -2685,7 +2729,20 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         uint32_t st[2];
         std::memcpy(st, const_cast<const uint32_t*>(s->h_place_status.as<uint32_t>()), sizeof(st));
         const uint32_t got = std::min(c, st[0] + 1);   // placed + the failing Select
-        std::memcpy(out + done, s->h_place_out.as<pe_ranked_node>(), sizeof(pe_ranked_node) * got);
+        if (chain) {
+            // widen k_emit's compact records: the leading fields are byte-identical
+            const pe::EmitRec* er = s->h_emit_out.as<pe::EmitRec>();
+            for (uint32_t i = 0; i < got; i++) {
+                pe_ranked_node& o = out[done + i];
+                std::memcpy(&o, &er[i], offsetof(pe::EmitRec, n_device_offers));
+                std::memset(reinterpret_cast<char*>(&o) + offsetof(pe_ranked_node, n_preempted), 0,
+                            sizeof(pe_ranked_node) - offsetof(pe_ranked_node, n_preempted));
+                o.n_device_offers = er[i].n_device_offers;
+                for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o.device_offer_group[q] = er[i].device_offer_group[q];
+            }
+        } else {
+            std::memcpy(out + done, s->h_place_out.as<pe_ranked_node>(), sizeof(pe_ranked_node) * got);
+        }
         if (commit)
             for (uint32_t i = 0; i < st[0]; i++) s->plan.emplace_back(g.name, (uint32_t)out[done + i].row);
         if (hprof) {
@@ -2705,6 +2762,8 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             A.base1 = nullptr;
             A.base_by_pos = 0;
             A.emit = nullptr;
+            A.emit_out = nullptr;
+            A.full_out = s->h_place_out.dev<pe_ranked_node>();
             A.done_flag = nullptr;
             spin = false;
             continue;

@@ -1,6 +1,7 @@
 // Shared host/device layout of the placement engine's HBM state and the
 // per-launch parameter block.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 #include "../../include/nomad_pe.h"
 
@@ -117,6 +118,30 @@ struct ChainEmit {
     double score;                 // FinalScore
 };
 
+// Per-node count arrays rewritten by one k_counts launch (own allocs, job and
+// task-group collisions); null entries are skipped.
+constexpr int kMaxCountDst = 32;
+struct CountDsts {
+    uint32_t* d[kMaxCountDst];
+};
+
+// Select result as k_emit hands it to the host: the leading fields of
+// pe_ranked_node (row .. new_offset, byte-identical) and the device offers;
+// the host widens it (no preemptions or reserved cores on the chain path).
+struct EmitRec {
+    int32_t row;
+    uint32_t n_scores;
+    double final_score;
+    double scores[PE_MAX_SCORES];
+    uint32_t nodes_evaluated, nodes_filtered, nodes_exhausted, new_offset;
+    uint32_t n_device_offers;
+    uint16_t device_offer_group[PE_MAX_DEVICE_REQ];
+    uint32_t pad;
+};
+static_assert(sizeof(EmitRec) % 8 == 0, "record copy granule");
+static_assert(offsetof(EmitRec, n_device_offers) == offsetof(pe_ranked_node, n_preempted),
+              "EmitRec shares pe_ranked_node's leading fields");
+
 // One launch = n_evals independent evaluations (one workgroup each) of the same
 // task group over the same snapshot; eval e visits perms + e*perm_stride.
 struct BatchArgs {
@@ -160,6 +185,7 @@ struct BatchArgs {
     uint32_t done_seq;
     unsigned long long* prof;     // k_chain step clocks (PE_CHAIN_PROF), or null
     pe_ranked_node* full_out;     // [n_evals][count] full records, or null
+    EmitRec* emit_out;            // k_emit's records (single-evaluation chain), or null
     pe_placement* out;            // [n_evals][count] compact records, or null
     uint32_t* eval_status;        // [n_evals][2]: placed, final cursor
 };

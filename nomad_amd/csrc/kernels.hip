@@ -1735,7 +1735,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     if (order_key(v[q]) == sh.sel_max[s]) atomicMin(&sh.sel_arg[s], pk[q] & kIdxMask);
                 }
             }
-            if (A.full_out && (nsel || mode == kPhaseExhausted)) {
+            if ((A.full_out || A.emit) && (nsel || mode == kPhaseExhausted)) {
                 // AllocMetric counters: filtered / exhausted positions pulled by each Select
                 const uint32_t end = mode == kPhaseExhausted ? W - 1 : sh.sel_end[nsel - 1];
 #pragma unroll
@@ -1878,22 +1878,24 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     }
 }
 
+constexpr uint32_t kEmitBlock = 64;
+
 // Records of a single-evaluation k_chain launch (A.emit): the full Select
 // result of every entry, evaluated on the state the launch started from (the
-// entry's dk = placements on the row before it), then, by the last workgroup
-// to finish, the launch's placements written back to the HBM SoA.
-__global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
+// entry's dk = placements on the row before it); k_emit_writeback then
+// writes the launch's placements back to the HBM SoA.
+__global__ void __launch_bounds__(kEmitBlock) k_emit(BatchArgs A) {
     __shared__ uint32_t last;
     // records are built in LDS and stored to the (host-mapped) output as one
-    // contiguous run per workgroup: 8-byte coalesced stores instead of every
-    // lane writing its own 184-byte record field by field over the bus
-    __shared__ pe_ranked_node recs[256];
-    static_assert(sizeof(pe_ranked_node) % 8 == 0, "record copy granule");
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    // contiguous run per workgroup: 8-byte coalesced stores of compact records
+    // instead of every lane writing its own record field by field over the
+    // bus; small workgroups spread the bus writes over more CUs
+    __shared__ EmitRec recs[kEmitBlock];
+    const uint32_t i = blockIdx.x * kEmitBlock + threadIdx.x;
     const uint32_t n_emit = A.emit_n[0];
     if (i < n_emit) {
         const ChainEmit m = A.emit[i];
-        pe_ranked_node& o = recs[threadIdx.x];
+        EmitRec& o = recs[threadIdx.x];
         o.row = m.row;
         o.nodes_evaluated = m.consumed;
         o.nodes_filtered = m.filtered;
@@ -1901,10 +1903,9 @@ __global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
         o.new_offset = m.new_offset;
         o.final_score = 0.0;
         o.n_scores = 0;
-        o.n_preempted = 0;
         o.n_device_offers = 0;
+        o.pad = 0;
         for (int q = 0; q < PE_MAX_SCORES; q++) o.scores[q] = 0.0;
-        for (int q = 0; q < PE_MAX_PREEMPT; q++) o.preempted[q] = 0;
         for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o.device_offer_group[q] = 0;
         if (m.row >= 0) {
             const uint32_t row = (uint32_t)m.row;
@@ -1916,48 +1917,59 @@ __global__ void __launch_bounds__(256) k_emit(BatchArgs A) {
             o.final_score = ev.score;
             o.n_scores = ev.nscores;
             for (int q = 0; q < PE_MAX_SCORES; q++) if (q < (int)ev.nscores) o.scores[q] = ev.parts[q];
-            record_offers(A.soa, A.ask, A.tg, row, m.dk, &o);
+            if (A.ask.n_dev > 0) {
+                const DevClass& dc = A.tg.dev_cls[A.soa.rec[row].cls];
+                uint32_t fr = dev_after(A.ask, dc, A.tg.dev_free[row], m.dk);
+                double mm;
+                uint32_t groups[kMaxDevReq];
+                if (dev_assign(A.ask, dc, fr, &mm, groups)) {
+                    o.n_device_offers = (uint32_t)A.ask.n_dev;
+                    for (int q = 0; q < kMaxDevReq; q++)
+                        if (q < A.ask.n_dev) o.device_offer_group[q] = (uint16_t)groups[q];
+                }
+            }
         }
     }
     __syncthreads();
     {
-        const uint32_t first = blockIdx.x * 256;
-        const uint32_t cnt = n_emit > first ? min(256u, n_emit - first) : 0u;
-        constexpr uint32_t W = sizeof(pe_ranked_node) / 8;
+        const uint32_t first = blockIdx.x * kEmitBlock;
+        const uint32_t cnt = n_emit > first ? min(kEmitBlock, n_emit - first) : 0u;
+        constexpr uint32_t W = sizeof(EmitRec) / 8;
         const uint2* src = reinterpret_cast<const uint2*>(recs);
-        uint2* dst = reinterpret_cast<uint2*>(A.full_out + first);
-        for (uint32_t w = threadIdx.x; w < cnt * W; w += 256) dst[w] = src[w];
+        uint2* dst = reinterpret_cast<uint2*>(A.emit_out + first);
+        for (uint32_t w = threadIdx.x; w < cnt * W; w += kEmitBlock) dst[w] = src[w];
     }
+    if (!A.done_flag) return;
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
+        __threadfence_system();
         last = atomicAdd(&A.emit_n[2], 1u) == gridDim.x - 1 ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const uint32_t nov = A.emit_n[1];
-    for (uint32_t x = threadIdx.x; x < nov; x += 256) {
-        const uint2 e = A.emit_ov[x];
-        NodeRec& r = A.soa.rec[e.x];
-        r.used_cpu += (int64_t)e.y * ask_cpu(A.soa, A.ask, e.x);
-        core_take(A.soa, A.ask, e.x, e.y);
-        r.used_mem += (int64_t)e.y * A.ask.mem;
-        r.used_disk += (int64_t)e.y * A.ask.disk;
-        r.used_mbits += (int32_t)e.y * A.ask.commit_mbits;
-        r.used_dyn += (int32_t)e.y * A.ask.commit_dyn;
-        A.soa.coll_job[e.x] += e.y;
-        A.tg.coll_tg[e.x] += e.y;
-        if (A.ask.n_dev > 0) A.tg.dev_free[e.x] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[e.x], e.y);
-    }
-    if (threadIdx.x == 0) A.emit_n[2] = 0;   // the ticket of the next launch
-    if (A.done_flag) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
+        // the last workgroup to finish tells the spinning host the records are in
+        if (last) {
             __threadfence_system();
             __hip_atomic_store(A.done_flag, A.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+}
+
+// The launch's placements written back to the HBM SoA, one overlay entry
+// (row, placements) per thread; runs after k_emit on the stream (the records
+// read the state the launch started from), off the host's critical path.
+__global__ void __launch_bounds__(256) k_emit_writeback(BatchArgs A) {
+    const uint32_t x = blockIdx.x * 256 + threadIdx.x;
+    if (x == 0) A.emit_n[2] = 0;   // k_emit's ticket for the next launch
+    if (x >= A.emit_n[1]) return;
+    const uint2 e = A.emit_ov[x];
+    NodeRec& r = A.soa.rec[e.x];
+    r.used_cpu += (int64_t)e.y * ask_cpu(A.soa, A.ask, e.x);
+    core_take(A.soa, A.ask, e.x, e.y);
+    r.used_mem += (int64_t)e.y * A.ask.mem;
+    r.used_disk += (int64_t)e.y * A.ask.disk;
+    r.used_mbits += (int32_t)e.y * A.ask.commit_mbits;
+    r.used_dyn += (int32_t)e.y * A.ask.commit_dyn;
+    A.soa.coll_job[e.x] += e.y;
+    A.tg.coll_tg[e.x] += e.y;
+    if (A.ask.n_dev > 0) A.tg.dev_free[e.x] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[e.x], e.y);
 }
 
 // SystemStack: every list entry is an independent single-node Select.
@@ -2840,6 +2852,28 @@ __global__ void __launch_bounds__(256) k_upload(unsigned char* dst, const unsign
     for (size_t i = n16 * 16 + (size_t)blockIdx.x * 256 + threadIdx.x; i < bytes; i += stride) dst[i] = src[i];
 }
 
+// Per-node count arrays from a sorted sparse list (key = row << 5 | array,
+// value = count): each thread owns one row, zeroes it in every array and
+// writes the row's entries found by binary search.
+__global__ void __launch_bounds__(256) k_counts(CountDsts D, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m) {
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t row = blockIdx.x * 256 + threadIdx.x; row < n; row += stride) {
+        uint32_t lo = 0, hi = m;
+        const uint32_t k0 = row << 5;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ents[mid].x < k0) lo = mid + 1;
+            else hi = mid;
+        }
+        for (uint32_t d = 0; d < nd; d++) {
+            if (!D.d[d]) continue;
+            uint32_t v = 0;
+            if (lo < m && ents[lo].x == (k0 | d)) v = ents[lo++].y;
+            D.d[d][row] = v;
+        }
+    }
+}
+
 // ResetPlan in one launch: the proposed state back to the snapshot (node
 // records, device free counts), no plan preemptions.
 __global__ void __launch_bounds__(256) k_reset_plan(NodeRec* rec, const NodeRec* base_rec, uint32_t* dev_free,
@@ -2954,9 +2988,11 @@ hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t ma
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL(pe::k_chain, dim3(grid), dim3(pe::kChainBlock), lds, st, *a, n_evals);
     if (a->emit) {
-        if (n_evals != 1 || !a->full_out || !a->emit_ov || !a->emit_n) return hipErrorInvalidValue;
-        const uint32_t eb = (a->count + 255) / 256;
-        hipLaunchKernelGGL(pe::k_emit, dim3(eb ? eb : 1), dim3(256), 0, st, *a);
+        if (n_evals != 1 || !a->emit_out || !a->emit_ov || !a->emit_n) return hipErrorInvalidValue;
+        const uint32_t eb = (a->count + pe::kEmitBlock - 1) / pe::kEmitBlock;
+        hipLaunchKernelGGL(pe::k_emit, dim3(eb ? eb : 1), dim3(pe::kEmitBlock), 0, st, *a);
+        const uint32_t wb = (a->count + 255) / 256;   // overlay rows <= placements
+        hipLaunchKernelGGL(pe::k_emit_writeback, dim3(wb ? wb : 1), dim3(256), 0, st, *a);
     }
     return hipGetLastError();
 }
@@ -3043,6 +3079,16 @@ hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hip
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(pe::k_upload, dim3((uint32_t)blocks), dim3(256), 0, st, static_cast<unsigned char*>(dst),
                        static_cast<const unsigned char*>(src_mapped), bytes);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_counts(const pe::CountDsts* d, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
+                            hipStream_t st) {
+    if (nd > (uint32_t)pe::kMaxCountDst || (m && !ents) || n >= (1u << 27)) return hipErrorInvalidValue;
+    if (!n) return hipSuccess;
+    uint32_t blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(pe::k_counts, dim3(blocks), dim3(256), 0, st, *d, nd, n, ents, m);
     return hipGetLastError();
 }
 
