@@ -142,6 +142,7 @@ struct PinnedMem {
         if (p) (void)hipHostFree(p);
         p = nullptr;
         bytes = 0;
+        dp_of = nullptr;
     }
     hipError_t ensure(size_t b) {
         if (b <= bytes && p) return hipSuccess;
@@ -151,12 +152,20 @@ struct PinnedMem {
         return e;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }
-    // the same bytes as seen from the device (kernels store results directly)
+    // the same bytes as seen from the device (kernels store results directly);
+    // looked up once per allocation
     template <class T> T* dev() const {
-        void* d = nullptr;
-        if (!p || hipHostGetDevicePointer(&d, p, 0) != hipSuccess) return nullptr;
-        return static_cast<T*>(d);
+        if (!p) return nullptr;
+        if (dp_of != p) {
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) return nullptr;
+            dp = d;
+            dp_of = p;
+        }
+        return static_cast<T*>(dp);
     }
+    mutable void* dp = nullptr;
+    mutable void* dp_of = nullptr;
 };
 
 // Fixed per-node fields; the variable-length maps live in stack-owned CSR
@@ -472,10 +481,14 @@ struct pe_stack {
         bool pending = false;          // a served option awaits its pe_commit
         uint32_t tgi = 0;
         std::vector<pe_ranked_node> recs;
+        std::vector<pe::EmitRec> crecs;   // the chain's compact records (compact = true), widened when served
+        bool compact = false;
         uint32_t n_rec = 0, placed = 0, served = 0, confirmed = 0;
         uint32_t grow = 1;             // run length on costly paths, doubles while runs get used up
         bool checkpoint = false;       // dynamic columns saved at the start (device asks)
     } spec;
+    std::vector<pe::EmitRec>* emit_sink = nullptr;   // run_place: keep chain records compact here
+    bool emit_sunk = false;                          // ... and it did
     bool spec_on = true;               // PE_SPECULATE=0: every Select runs on its own
     uint64_t spec_stats[4] = {0, 0, 0, 0};   // runs, Selects served, rollbacks, records computed
     DevMem ck_rec, ck_coll_job, ck_coll_tg, ck_dev_free, ck_pset[pe::kMaxPsets];
@@ -2588,6 +2601,16 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     return PE_OK;
 }
 
+// A compact chain record as the full RankedNode (the leading fields are
+// byte-identical; no preemptions or reserved cores on the chain path).
+static inline void widen_rec(const pe::EmitRec& e, pe_ranked_node* o) {
+    std::memcpy(o, &e, offsetof(pe::EmitRec, n_device_offers));
+    std::memset(reinterpret_cast<char*>(o) + offsetof(pe_ranked_node, n_preempted), 0,
+                sizeof(pe_ranked_node) - offsetof(pe_ranked_node, n_preempted));
+    o->n_device_offers = e.n_device_offers;
+    for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o->device_offer_group[q] = e.device_offer_group[q];
+}
+
 // One evaluation on the stack's plan (pe_select / pe_place): the fused count
 // loop in launches of at most H/2 placements, each merging its overlay back
 // into the HBM SoA so the plan persists.
@@ -2604,6 +2627,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     }
     const uint32_t n = (uint32_t)order.size();
     const bool full = full_scan_kernel(s, g, n);
+    std::vector<pe::EmitRec>* sink = s->emit_sink;
     pe::BatchArgs A = batch_args(s, g);
     {
         ApiScope prof_up_(s, "run_place.upload_visit");
@@ -2730,21 +2754,21 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         std::memcpy(st, const_cast<const uint32_t*>(s->h_place_status.as<uint32_t>()), sizeof(st));
         const uint32_t got = std::min(c, st[0] + 1);   // placed + the failing Select
         if (chain) {
-            // widen k_emit's compact records: the leading fields are byte-identical
             const pe::EmitRec* er = s->h_emit_out.as<pe::EmitRec>();
-            for (uint32_t i = 0; i < got; i++) {
-                pe_ranked_node& o = out[done + i];
-                std::memcpy(&o, &er[i], offsetof(pe::EmitRec, n_device_offers));
-                std::memset(reinterpret_cast<char*>(&o) + offsetof(pe_ranked_node, n_preempted), 0,
-                            sizeof(pe_ranked_node) - offsetof(pe_ranked_node, n_preempted));
-                o.n_device_offers = er[i].n_device_offers;
-                for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o.device_offer_group[q] = er[i].device_offer_group[q];
+            if (sink) {
+                // the caller serves them one by one (speculation): stay compact
+                if (sink->size() < done + got) sink->resize(done + got);
+                std::memcpy(sink->data() + done, er, sizeof(pe::EmitRec) * got);
+                s->emit_sunk = true;
+            } else {
+                for (uint32_t i = 0; i < got; i++) widen_rec(er[i], &out[done + i]);
             }
         } else {
             std::memcpy(out + done, s->h_place_out.as<pe_ranked_node>(), sizeof(pe_ranked_node) * got);
         }
         if (commit)
-            for (uint32_t i = 0; i < st[0]; i++) s->plan.emplace_back(g.name, (uint32_t)out[done + i].row);
+            for (uint32_t i = 0; i < st[0]; i++)
+                s->plan.emplace_back(g.name, (uint32_t)(chain && sink ? (*sink)[done + i].row : out[done + i].row));
         if (hprof) {
             const double t3 = now_us();
             h_launch += t1 - t0;
@@ -2757,6 +2781,11 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             // a Select needs more than the chain's window of a long list (sparse
             // options): the lazy per-position loop places the rest
             done += st[0];
+            if (sink) {   // full records from here on: widen the compact ones
+                for (uint32_t i = 0; i < done; i++) widen_rec((*sink)[i], &out[i]);
+                s->emit_sunk = false;
+                sink = nullptr;
+            }
             chain = false;
             A.base = nullptr;
             A.base1 = nullptr;
@@ -2804,6 +2833,10 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
 }  // namespace
 
 extern "C" {
+
+static inline int32_t spec_row(const pe_stack::Spec& sp, uint32_t i) {
+    return sp.compact ? sp.crecs[i].row : sp.recs[i].row;
+}
 
 static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out);
 static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* opts);
@@ -3992,6 +4025,10 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
     const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
     const double t_enter = prof ? now_us() : 0.0;
     if (!s || (!out && count)) return PE_EINVAL;
+    // compact chain records for the speculation (spec_start), honoured by the
+    // plain count loop below only
+    std::vector<pe::EmitRec>* sink = s->emit_sink;
+    s->emit_sink = nullptr;
     if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place needs a generic stack");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
@@ -4092,7 +4129,9 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
         no = s->offset;
     }
     if (count) {
+        s->emit_sink = retry ? nullptr : sink;   // nothing below reads the records without a retry
         rc = run_place(s, tgi, count, 1, s->visit, s->offset, nullptr, out, &p, &no);
+        s->emit_sink = nullptr;
         if (rc) return rc;
         s->offset = no;
         // selectNextOption (generic_sched.go:773-792): a nil Select is retried
@@ -4169,7 +4208,8 @@ static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     if (!sp.active || sp.pending || tgi != sp.tgi || sp.served >= sp.n_rec || s->metrics_on) return false;
     if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
     s->gen++;
-    *out = sp.recs[sp.served++];
+    if (sp.compact) widen_rec(sp.crecs[sp.served++], out);
+    else *out = sp.recs[sp.served++];
     sp.pending = out->row >= 0;
     s->offset = out->new_offset;   // the StaticIterator cursor after this Select
     s->metrics_valid = false;
@@ -4236,7 +4276,7 @@ static int spec_flush(pe_stack* s) {
         // no device ask: every commit added the same ask to its row, so the
         // unconfirmed placements are taken back by subtracting them again
         std::vector<uint32_t> rows(sp.placed - sp.confirmed), offers(rows.size(), 0xFFFFFFFFu);
-        for (uint32_t i = sp.confirmed; i < sp.placed; i++) rows[i - sp.confirmed] = (uint32_t)sp.recs[i].row;
+        for (uint32_t i = sp.confirmed; i < sp.placed; i++) rows[i - sp.confirmed] = (uint32_t)spec_row(sp, i);
         HIP_TRY(s, upload_s(s, s->d_commit_rows, rows));
         HIP_TRY(s, upload_s(s, s->d_commit_offers, offers));
         HIP_TRY(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
@@ -4251,8 +4291,14 @@ static int spec_flush(pe_stack* s) {
     std::vector<uint32_t> rows(sp.confirmed), offers(sp.confirmed);
     bool ordered_only = false;   // a device ask without a recorded offer: replay one by one
     for (uint32_t i = 0; i < sp.confirmed; i++) {
-        rows[i] = (uint32_t)sp.recs[i].row;
-        offers[i] = pack_offers(&sp.recs[i]);
+        rows[i] = (uint32_t)spec_row(sp, i);
+        if (sp.compact) {
+            pe_ranked_node r;
+            widen_rec(sp.crecs[i], &r);
+            offers[i] = pack_offers(&r);
+        } else {
+            offers[i] = pack_offers(&sp.recs[i]);
+        }
         if (a.n_dev > 0 && offers[i] == 0xFFFFFFFFu) ordered_only = true;
     }
     if (ordered_only) {
@@ -4303,7 +4349,11 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     const size_t plan0 = s->plan.size();
     if (sp.recs.size() < count) sp.recs.resize(count);
     uint32_t placed = 0;
+    s->emit_sink = &sp.crecs;
+    s->emit_sunk = false;
     rc = place_impl(s, tgi, count, sp.recs.data(), &placed, false);
+    s->emit_sink = nullptr;
+    sp.compact = s->emit_sunk;
     s->plan.resize(plan0);   // the plan holds confirmed placements only
     if (rc) {
         if (sp.checkpoint) {
@@ -4343,7 +4393,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
 int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
     if (!s) return PE_EINVAL;
     pe_stack::Spec& sp = s->spec;
-    if (sp.active && sp.pending && tgi == sp.tgi && row == sp.recs[sp.served - 1].row) {
+    if (sp.active && sp.pending && tgi == sp.tgi && row == spec_row(sp, sp.served - 1)) {
         // the predicted Plan.AppendAlloc: already in HBM
         sp.pending = false;
         sp.confirmed = sp.served;
