@@ -1309,7 +1309,7 @@ constexpr int kChainMaxSel = 1024;                            // Selects resolve
 constexpr int kChainTiles = kChainMaxN / 64;
 constexpr uint32_t kChainMaxRedo = 2048;                      // rows re-evaluated per phase (<= placements per launch)
 
-enum : int { kPhaseMore = 0, kPhaseCount = 1, kPhaseExhausted = 2, kPhaseStall = 3 };
+enum : int { kPhaseMore = 0, kPhaseCount = 1, kPhaseExhausted = 2, kPhaseStall = 3, kPhaseRetry = 4 };
 constexpr uint32_t kChainStalled = 0x80000000u;   // eval_status cursor flag: continue with the lazy loop
 constexpr int kSegE = 21;                 // entry offsets into a segment: a Select spans <= limit + 3 options
 constexpr uint32_t kSegLen = 256;         // options per segment of the boundary walk
@@ -1415,7 +1415,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     const uint32_t n = A.n_visit;
     // positions per phase: one rotation, or its first kChainMaxN positions on a
     // longer list (every Select of the phase still stops inside the window)
-    const uint32_t W = n < kChainMaxN ? n : kChainMaxN;
+    const uint32_t Wfull = n < kChainMaxN ? n : kChainMaxN;
     const uint32_t L = A.limit;
     const uint32_t H = 1u << A.hash_bits;
     Overlay ov;
@@ -1426,7 +1426,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     ov.kshift = A.packed_overlay;
     ov.kmask = A.packed_overlay ? (1u << A.packed_overlay) - 1u : 0u;
     uint16_t* nb = reinterpret_cast<uint16_t*>(ov.keys + (A.packed_overlay ? H : 2 * H));   // [n + 2]
-    uint16_t* nx = nb + ((W + 2 + 1) & ~1u);   // [W + 2]: next Select start per option, then Select id per option
+    uint16_t* nx = nb + ((Wfull + 2 + 1) & ~1u);   // [W + 2]: next Select start per option, then Select id per option
 
     uint64_t prof_t = A.prof ? __builtin_readcyclecounter() : 0;
     int prof_ph = 0;   // profile slot group: phase (capped at 3)
@@ -1448,6 +1448,8 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
         uint32_t placed = 0;
         bool stalled = false;
         bool done = n == 0 || A.count == 0;
+        uint32_t pos_used = 0;      // visit positions the resolved Selects consumed so far
+        bool force_full = false;    // a shortened window held no whole Select: use the full one
         if (n == 0 && A.count && tid == 0 && A.out) {
             pe_placement& o = A.out[(size_t)e * A.count];
             o.row = -1; o.nodes_evaluated = 0; o.final_score = 0.0;
@@ -1455,6 +1457,16 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
         __syncthreads();
         while (!done) {
             PE_PROF_MARK(0);
+            // positions of this phase: the full window, or after the first
+            // phase what the remaining Selects need at the observed positions
+            // per Select with a margin (the per-position steps scale with it)
+            uint32_t W = Wfull;
+            if (placed && !force_full) {
+                const uint64_t need = (uint64_t)(A.count - placed) * pos_used * 3u / (2u * placed) + 1024u;
+                if (need < W) W = (uint32_t)((need + kChainBlock - 1) / kChainBlock * kChainBlock);
+                if (W > Wfull) W = Wfull;
+            }
+            force_full = false;
             // 1. values of the window [cur, cur + n): base (no placement of this
             //    launch on the row), base1 (one), or queued for re-evaluation
             uint32_t row[kChainItems];
@@ -1657,7 +1669,11 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 int mode = kPhaseMore;
                 uint32_t ns = total;
-                if (ns == 0 && W < n) {
+                if (ns == 0 && W < Wfull) {
+                    // the shortened window held no whole Select: again with the full one
+                    mode = kPhaseRetry;
+                    used = 0;
+                } else if (ns == 0 && W < n) {
                     // a Select needs more than the window: the lazy loop goes on from here
                     mode = kPhaseStall;
                     used = 0;
@@ -1701,6 +1717,10 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             if (mode == kPhaseStall) {
                 stalled = true;
                 break;
+            }
+            if (mode == kPhaseRetry) {
+                force_full = true;
+                continue;
             }
             const uint32_t last_b = nsel ? sh.sel_b[nsel - 1] : 0u;
             PE_PROF_MARK(4);
@@ -1804,6 +1824,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 if (tid == 0) sh.n_emit = placed + nsel;
                 placed += nsel;
+                pos_used += sh.sel_end[nsel - 1] + 1u;
                 cur = wrap_pos(cur + sh.sel_end[nsel - 1] + 1u, n);
                 done = mode == kPhaseCount;
             } else {

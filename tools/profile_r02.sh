@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-2 profile on the GPU box: the default bench line (CPU baselines
 # included), rocprofv3 kernel stats of the bench's headline loop, of the C5
-# loop (k_ploop) and of the C3 count loop, and the PMC traffic passes
+# loop (k_ploop) and of the C3 count loop, the device timeline of three
+# headline evaluations (tools/timeline.py), and the PMC traffic passes
 # (FETCH_SIZE, WRITE_SIZE in separate runs) of the 2^24-node scoring sweep.
 # Every GPU step has its own time limit; the script stops at the first
 # failure. Outputs land in gpurun_out/<tag>/.
@@ -17,6 +18,8 @@ cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
   python3 "$ROOT/bench.py" --no-cpu --steps 10 --warmup 2 --sweep-nodes 0 --sections "" > "$OUT/trace.log" 2>&1
+T=$(find "$OUT/trace" -name "*kernel_trace.csv" -print -quit)
+python3 "$ROOT/tools/timeline.py" "$T" k_emit_writeback 3 > "$OUT/headline_timeline.txt"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5" -o c5 -- \
   python3 "$ROOT/tools/c5_prof.py" > "$OUT/c5.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c3" -o c3 -- \
