@@ -57,3 +57,22 @@ def test_chain_fills_cluster(n, extra):
     assert placed == min(n, n + extra)
     if extra > 0:
         assert re[-1].row < 0
+
+
+def test_dropin_chain_stall_on_sparse_options():
+    """The caller's Select/Commit protocol on a list longer than one chain
+    window whose options thin out: the speculative run starts on the chain
+    (compact records) and hands over to the lazy loop when a Select no longer
+    stops inside the window; every Select must still equal the oracle's."""
+    from nomad_amd.structs import Constraint
+    from tests.test_dropin import assert_equal_runs, both
+    n = 20000
+    nodes = one_slot_cluster(n, seed=77)
+    for k, nd in enumerate(nodes):
+        nd.datacenter = "dc1" if (k < 200 or k % 997 == 0) else "dc2"
+        nd.compute_class()
+    job = big_job(260)
+    job.constraints = [Constraint("${node.datacenter}", "dc1", "=")]
+    a, b, eng = both(nodes, [], job, list(range(n)), count=260)
+    assert_equal_runs(a, b)
+    assert a[-1] is None and sum(1 for x in a if x is not None) == 220
