@@ -181,6 +181,22 @@ def chain_traffic(evals_per_launch):
     return t["bytes_per_launch"]
 
 
+HEADLINE_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02", "headline_traffic.json")
+
+
+def headline_traffic(node_evals):
+    """HBM bytes of one headline evaluation's k_base + k_chain from the
+    committed PMC passes over this same workload (tools/headline_pmc.sh), or None."""
+    try:
+        with open(HEADLINE_TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("node_evals") != int(node_evals) or t.get("bytes_per_node_eval") != BYTES_PER_NODE_EVAL:
+        return None, None
+    return t["bytes_per_launch"], os.path.relpath(HEADLINE_TRAFFIC_FILE, ROOT)
+
+
 def sweep_traffic(n, bytes_per_node):
     """HBM bytes per sweep launch from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md
@@ -818,7 +834,8 @@ def main():
                         "us_per_placement": elapsed / max(1, placed) * 1e6,
                         "us_per_eval_by_phase": {k: v / max(1, evals) * 1e6 for k, v in phases.items()}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": headline_traffic(node_evals)[0],
+                         "traffic_source": headline_traffic(node_evals)[1],
                          "note": "k_base + k_chain of one evaluation (the step's device work): cache-resident "
                                  "equivalent bytes, 60 B per node-evaluation the reference chain reads; the "
                                  "10k-node table is L2/MALL resident and the loop is latency-bound. The HBM "
