@@ -77,6 +77,9 @@ hipError_t pe_launch_static_gate(const uint8_t* blocked, const uint32_t* coll_tg
 uint32_t pe_ploop_max_n();
 hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
                                     uint32_t* dev_free, uint32_t* placed, hipStream_t st);
+size_t pe_fold_feas_max_classes();
+hipError_t pe_launch_fold_feas_staged(const pe::NodeSoA* s, const unsigned char* class_src, uint8_t* class_dst,
+                                      uint32_t ncls, const uint8_t* node_ok, uint8_t* feas, hipStream_t st);
 hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, const uint8_t* node_ok, uint8_t* feas,
                                hipStream_t st);
 hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec* merged, hipStream_t st);
@@ -623,6 +626,26 @@ hipError_t upload_s(pe_stack* s, DevMem& m, const std::vector<T>& h) {
     if (!s->stage_dev) s->stage_dev = s->h_stage.dev<unsigned char>();
     if (s->stage_dev) return pe_launch_upload(m.p, s->stage_dev + off, b, s->stream);
     return hipMemcpyAsync(m.p, dst, b, hipMemcpyHostToDevice, s->stream);
+}
+
+// Copies `h` into the page-locked staging ring without a copy launch and
+// returns the staged bytes as the device sees them (a kernel that consumes a
+// small table reads it from there itself), or null when it does not fit.
+template <class T>
+const unsigned char* stage_only(pe_stack* s, const std::vector<T>& h) {
+    const size_t b = h.size() * sizeof(T);
+    if (b == 0 || b > kStageBytes / 4) return nullptr;
+    if (!s->h_stage.p && s->h_stage.ensure(kStageBytes) != hipSuccess) return nullptr;
+    size_t off = (s->stage_off + 255) & ~size_t(255);
+    if (off + b > kStageBytes) {
+        if (hipStreamSynchronize(s->stream) != hipSuccess) return nullptr;
+        off = 0;
+    }
+    if (!s->stage_dev) s->stage_dev = s->h_stage.dev<unsigned char>();
+    if (!s->stage_dev) return nullptr;
+    std::memcpy(s->h_stage.as<unsigned char>() + off, h.data(), b);
+    s->stage_off = off + b;
+    return s->stage_dev + off;
 }
 
 // Visit order into d_visit; the SetNodes list itself is uploaded once per SetNodes.
@@ -2038,16 +2061,26 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         class_ok = class_verdicts(s, g, memo);
         if (s->job_escaped) node_ok = g.job_ok_node;
     }
-    HIP_TRY(s, upload_s(s, g.class_ok, class_ok));
     g.node_ok_used = !node_ok.empty();
     if (g.node_ok_used) HIP_TRY(s, upload_s(s, g.node_ok, node_ok));
     {
-        // fold the class verdict into one byte per node (single round trip per node)
+        // fold the class verdict into one byte per node (single round trip per
+        // node); the class table goes up with the same launch when it is small
         pe::NodeSoA soa = soa_of(s);
         HIP_TRY(s, g.node_feas.ensure(std::max<size_t>(n, 1)));
-        HIP_TRY(s, pe_launch_fold_feas(&soa, g.class_ok.as<uint8_t>(),
-                                       g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr,
-                                       g.node_feas.as<uint8_t>(), s->stream));
+        HIP_TRY(s, g.class_ok.ensure(std::max<size_t>(class_ok.size(), 1)));
+        const unsigned char* staged =
+            class_ok.size() <= pe_fold_feas_max_classes() ? stage_only(s, class_ok) : nullptr;
+        if (staged) {
+            HIP_TRY(s, pe_launch_fold_feas_staged(&soa, staged, g.class_ok.as<uint8_t>(), (uint32_t)class_ok.size(),
+                                                  g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr,
+                                                  g.node_feas.as<uint8_t>(), s->stream));
+        } else {
+            HIP_TRY(s, upload_s(s, g.class_ok, class_ok));
+            HIP_TRY(s, pe_launch_fold_feas(&soa, g.class_ok.as<uint8_t>(),
+                                           g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr,
+                                           g.node_feas.as<uint8_t>(), s->stream));
+        }
     }
 
     // NodeAffinityIterator score per class (rank.go:698-725)

@@ -2918,6 +2918,28 @@ __global__ void __launch_bounds__(256) k_fold_feas(NodeSoA s, const uint8_t* cla
     }
 }
 
+// k_fold_feas with the class table read from the page-locked staging ring:
+// every workgroup pulls the (small) table over the bus into LDS, workgroup 0
+// also stores it to its device copy for the later kernels; saves the
+// separate upload launch.
+constexpr uint32_t kFoldMaxClasses = 16384;
+__global__ void __launch_bounds__(256) k_fold_feas_staged(NodeSoA s, const uint8_t* class_src, uint8_t* class_dst,
+                                                          uint32_t ncls, const uint8_t* node_ok, uint8_t* feas) {
+    __shared__ uint8_t cls_ok[kFoldMaxClasses];
+    for (uint32_t c = threadIdx.x; c < ncls; c += blockDim.x) {
+        const uint8_t v = class_src[c];
+        cls_ok[c] = v;
+        if (blockIdx.x == 0) class_dst[c] = v;
+    }
+    __syncthreads();
+    for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < s.n; row += gridDim.x * blockDim.x) {
+        const uint32_t c = s.rec[row].cls;
+        bool ok = c < ncls && cls_ok[c] != 0;
+        if (node_ok) ok = ok && node_ok[row] != 0;
+        feas[row] = ok ? 1 : 0;
+    }
+}
+
 // node_aux[row] (SweepArgs): verdict bit, affinity index (per class, or per
 // node when the affinities escape the class), spread values of the first
 // kAuxPsets properties. Built once per (job, task group) tables.
@@ -3155,6 +3177,19 @@ hipError_t pe_launch_fold_feas(const pe::NodeSoA* s, const uint8_t* class_ok, co
     if (blocks > 4096) blocks = 4096;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(pe::k_fold_feas, dim3(blocks), dim3(256), 0, st, *s, class_ok, node_ok, feas);
+    return hipGetLastError();
+}
+
+size_t pe_fold_feas_max_classes() { return pe::kFoldMaxClasses; }
+
+hipError_t pe_launch_fold_feas_staged(const pe::NodeSoA* s, const unsigned char* class_src, uint8_t* class_dst,
+                                      uint32_t ncls, const uint8_t* node_ok, uint8_t* feas, hipStream_t st) {
+    if (ncls > pe::kFoldMaxClasses || !class_src || !class_dst) return hipErrorInvalidValue;
+    uint32_t blocks = (s->n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(pe::k_fold_feas_staged, dim3(blocks), dim3(256), 0, st, *s, class_src, class_dst, ncls,
+                       node_ok, feas);
     return hipGetLastError();
 }
 
