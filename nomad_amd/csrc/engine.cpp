@@ -2662,12 +2662,6 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     const bool full = full_scan_kernel(s, g, n);
     std::vector<pe::EmitRec>* sink = s->emit_sink;
     pe::BatchArgs A = batch_args(s, g);
-    {
-        ApiScope prof_up_(s, "run_place.upload_visit");
-        HIP_TRY(s, upload_visit(s, order));
-    }
-    A.perms = s->d_visit.as<uint32_t>();
-    A.n_visit = n;
     if (opts && opts->penalty_count > 0) {
         std::vector<uint32_t> bits((s->nodes.size() + 31) / 32, 0);
         for (uint32_t i = 0; i < opts->penalty_count; i++) {
@@ -2708,6 +2702,28 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             }
         }
     }
+    bool staged_is_visit = false;
+    {
+        // the visit order: k_base of the chain reads a new list straight from
+        // the staging ring and stores it to d_visit itself (no copy launch)
+        ApiScope prof_up_(s, "run_place.upload_visit");
+        const bool is_visit = &order == &s->visit;
+        const unsigned char* src = nullptr;
+        if (chain && !(is_visit && s->d_visit_is_visit)) {
+            HIP_TRY(s, s->d_visit.ensure(sizeof(uint32_t) * (size_t)n));
+            src = stage_only(s, order);
+        }
+        if (src) {
+            A.perm_src = reinterpret_cast<const uint32_t*>(src);
+            A.perm_dst = s->d_visit.as<uint32_t>();
+            s->d_visit_is_visit = false;   // until the launch that stores it is queued
+            staged_is_visit = is_visit;
+        } else {
+            HIP_TRY(s, upload_visit(s, order));
+        }
+    }
+    A.perms = s->d_visit.as<uint32_t>();
+    A.n_visit = n;
     const uint32_t chunk = std::max<uint32_t>(1, (1u << A.hash_bits) / 2);
     // records and status land in mapped page-locked memory: the kernel writes
     // them over PCIe while it runs, one stream sync per launch
@@ -2764,6 +2780,11 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             ApiScope prof_l_(s, "run_place.launch");
             if (chain) HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream));
             else HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
+            if (A.perm_src) {   // d_visit now holds the list (stream order)
+                s->d_visit_is_visit = staged_is_visit;
+                A.perm_src = nullptr;
+                A.perm_dst = nullptr;
+            }
             HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
         }
         const double t1 = hprof ? now_us() : 0.0;

@@ -149,6 +149,10 @@ struct BatchArgs {
     TgTables tg;
     Ask ask;
     const uint32_t* perms;        // visit orders (SetNodes lists after shuffle)
+    // single-evaluation chain: k_base reads the visit order from the staging
+    // ring (perm_src, mapped) and stores it to perm_dst (= perms), or null
+    const uint32_t* perm_src;
+    uint32_t* perm_dst;
     uint32_t perm_stride;         // 0: all evals share one order
     uint32_t class_ok_stride;     // 0: shared class table, else per-eval tables
     const uint32_t* offsets;      // per-eval StaticIterator cursor, or null -> offset0

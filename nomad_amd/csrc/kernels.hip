@@ -1258,7 +1258,15 @@ __global__ void __launch_bounds__(256) k_base(BatchArgs A) {
     const uint32_t stride = gridDim.x * 256;
     const uint32_t m = A.base_by_pos ? A.n_visit : A.soa.n;
     for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < m; j += stride) {
-        const uint32_t row = A.base_by_pos ? A.perms[j] : j;
+        uint32_t row = j;
+        if (A.base_by_pos) {
+            if (A.perm_src) {
+                row = A.perm_src[j];
+                A.perm_dst[j] = row;
+            } else {
+                row = A.perms[j];
+            }
+        }
         NodeIn in;
         load_node(A.soa, A.tg, row, in);
         NodeEval ev;
@@ -3022,6 +3030,7 @@ hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t ma
         a->limit > pe::kMaxChainLimit)
         return hipErrorInvalidValue;
     if (a->base_by_pos && n_evals != 1) return hipErrorInvalidValue;
+    if (a->perm_src && (!a->base_by_pos || !a->perm_dst)) return hipErrorInvalidValue;
     uint32_t blocks = ((a->base_by_pos ? a->n_visit : a->soa.n) + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
