@@ -247,19 +247,15 @@ bool ConstraintEvaluator::version_match(bool semver, const Target& l, const Targ
     return check_version_constraints(*it->second, v, semver);
 }
 
+// checkRegexpMatch (feasible.go:931-960): Go's regexp (RE2 syntax), see go_regexp.h.
 bool ConstraintEvaluator::regexp_match(const Target& l, const Target& r) {
     if (l.nil || r.nil) return false;
-    if (re_bad_.count(r.value)) return false;
     auto it = re_cache_.find(r.value);
     if (it == re_cache_.end()) {
-        try {
-            it = re_cache_.emplace(r.value, std::make_shared<std::regex>(r.value, std::regex::ECMAScript)).first;
-        } catch (const std::regex_error&) {
-            re_bad_[r.value] = true;
-            return false;
-        }
+        int status;
+        it = re_cache_.emplace(r.value, gore::compile(r.value, &status)).first;
     }
-    return std::regex_search(l.value, *it->second);
+    return it->second && gore::match(*it->second, l.value);
 }
 
 static bool set_contains(const Target& l, const Target& r, bool all) {

@@ -14,7 +14,8 @@
 #include <vector>
 #include <unordered_map>
 #include <memory>
-#include <regex>
+
+#include "go_regexp.h"
 
 namespace pe {
 
@@ -68,8 +69,9 @@ private:
     bool version_match(bool semver, const Target& l, const Target& r);
     bool regexp_match(const Target& l, const Target& r);
     std::unordered_map<std::string, std::shared_ptr<std::vector<VersionConstraint>>> ver_cache_[2];
-    std::unordered_map<std::string, std::shared_ptr<std::regex>> re_cache_;
-    std::unordered_map<std::string, bool> re_bad_;
+    // regexp.Compile results per pattern (ctx.RegexpCache(), feasible.go:945-957);
+    // null = the pattern does not compile (Go returns false for it)
+    std::unordered_map<std::string, std::shared_ptr<const gore::Prog>> re_cache_;
 };
 
 bool target_escapes(const std::string& t);   // node_class.go:120-132

@@ -8,10 +8,7 @@
 //     comparePrereleases, Constraint operators incl. prereleaseCheck and "~>".
 //   helper/constraints/semver/constraints.go (semver operand: Semver 2.0 ordering,
 //     no "~>" operator).
-// Regexp: Go's RE2 is restated with std::regex (ECMAScript). The two agree on
-// the pattern class used by the reference KATs (feasible_test.go:1194-1229) and
-// the configs (anchors, classes, alternation, repetition); RE2-only syntax
-// (e.g. (?P<name>..), \pL) is outside the pinned set ("parity unpinned").
+// Regexp: Go 1.16's regexp package (RE2 syntax) is restated in go_regexp.h.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -24,6 +21,8 @@
 #include <memory>
 #include <cctype>
 #include <climits>
+
+#include "go_regexp.h"
 
 namespace orasem {
 
@@ -263,7 +262,8 @@ static inline bool parse_constraints(const std::string& str, bool semver, std::v
 }
 
 struct Caches {
-    std::map<std::string, std::shared_ptr<std::regex>> re;
+    struct Compiled { bool ok = false; std::vector<orare::Re> pool; int root = 0; };
+    std::map<std::string, std::shared_ptr<Compiled>> re;
     std::map<std::string, std::shared_ptr<std::vector<VConstraint>>> ver, semver;
 };
 
@@ -287,17 +287,16 @@ static inline bool check_version_match(Caches& c, bool semver, const Val& l, con
     return true;
 }
 
+// checkRegexpMatch (feasible.go:931-960)
 static inline bool check_regexp_match(Caches& c, const Val& l, const Val& r) {
     if (l.is_nil || r.is_nil) return false;
     auto it = c.re.find(r.s);
-    std::shared_ptr<std::regex> re;
-    if (it != c.re.end()) re = it->second;
-    else {
-        try { re = std::make_shared<std::regex>(r.s, std::regex::ECMAScript); }
-        catch (...) { return false; }
-        c.re[r.s] = re;
+    if (it == c.re.end()) {
+        auto k = std::make_shared<Caches::Compiled>();
+        k->ok = orare::compile(r.s, &k->pool, &k->root);
+        it = c.re.emplace(r.s, k).first;
     }
-    return std::regex_search(l.s, *re);
+    return it->second->ok && orare::match_string(it->second->pool, it->second->root, l.s);
 }
 
 static inline bool check_set_contains_all(const Val& l, const Val& r) {
