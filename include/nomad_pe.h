@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 3u
+#define PE_ABI_VERSION 4u
 #define PE_NONE 0xFFFFFFFFu
 #define PE_MAX_SCORES 8
 #define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried per RankedNode */
@@ -423,6 +423,39 @@ int pe_set_metrics(pe_stack* s, int on);
  * CF / KF / CE / DE, keys sorted. Writes at most cap bytes (NUL-terminated) and
  * returns the bytes needed, or PE_ESTATE when the last Select has none. */
 int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap);
+/* EvalEligibility (scheduler/context.go:190-356) as the reference chain would
+ * hold it after this evaluation's Selects: the job-level and per task group
+ * ComputedClassFeasibility entries FeasibilityWrapper.Next writes for every
+ * node the chain pulls (feasible.go:1061-1153). createBlockedEval /
+ * ReblockEval read GetClasses() and HasEscaped() from it
+ * (generic_sched.go:177-181, 193-203); the shim mirrors the entries into
+ * ctx.Eligibility() after each Select (changed_only = 1 returns the entries
+ * set or changed since the last call that fit in `cap`). *n receives the
+ * number of entries; *flags bit PE_ELIG_ESCAPED = HasEscaped(). */
+#define PE_CLASS_INELIGIBLE 1   /* EvalComputedClassIneligible */
+#define PE_CLASS_ELIGIBLE 2     /* EvalComputedClassEligible */
+#define PE_ELIG_ESCAPED 1u
+typedef struct pe_class_feas {
+    uint32_t task_group;      /* PE_NONE: EvalEligibility.job; else the task group name (str id) */
+    uint32_t computed_class;  /* Node.ComputedClass (str id, as in pe_node_table.computed_class) */
+    uint32_t status;          /* PE_CLASS_INELIGIBLE / PE_CLASS_ELIGIBLE */
+} pe_class_feas;
+int pe_get_eligibility(pe_stack* s, uint32_t changed_only, pe_class_feas* out, uint32_t cap, uint32_t* n,
+                       uint32_t* flags);
+/* After the Go chain answered a Select (PE_EUNSUPPORTED): its ctx.Eligibility()
+ * entries become the engine's memo, so later Selects filter and decide classes
+ * exactly as the chain would (EvalEligibility is shared by the two stacks). */
+int pe_put_eligibility(pe_stack* s, const pe_class_feas* in, uint32_t n);
+/* The GenericStack iterator state that persists between Selects:
+ * StaticIterator.offset (feasible.go:75-117) and the LimitIterator limit
+ * (stack.go:81-90; latched to MaxInt32 by task groups with affinities or
+ * spreads, stack.go:165-167). Before the shim's fallback GenericStack answers
+ * a PE_EUNSUPPORTED Select it takes both from pe_get_cursor; afterwards
+ * pe_set_cursor hands the chain's offset and limit back, with the task group
+ * it selected for (its SpreadIterator.SetTaskGroup adds the group's spread
+ * weights to sumSpreadWeights, spread.go:232-257), or PE_NONE. */
+int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit);
+int pe_set_cursor(pe_stack* s, uint32_t tg_index, uint32_t offset, uint32_t limit);
 /* Host-side constraint semantics used for pre-resolution (checkConstraint,
  * feasible.go:785-820), exposed for known-answer tests; needs no device.
  * l_state / r_state: 0 nil (unknown ${...} target), 1 found, 2 missing ("", false). */

@@ -181,6 +181,14 @@ class pe_placement(C.Structure):
     _fields_ = [("row", C.c_int32), ("nodes_evaluated", C.c_uint32), ("final_score", C.c_double)]
 
 
+PE_CLASS_INELIGIBLE, PE_CLASS_ELIGIBLE = 1, 2
+PE_ELIG_ESCAPED = 1
+
+
+class pe_class_feas(C.Structure):
+    _fields_ = [("task_group", C.c_uint32), ("computed_class", C.c_uint32), ("status", C.c_uint32)]
+
+
 # Entry points declared in include/nomad_pe.h: (name, restype, argtypes)
 def _sigs(prefix, handle):
     H = C.c_void_p
@@ -198,6 +206,10 @@ def _sigs(prefix, handle):
         (prefix + "plan_pop_update", C.c_int, [H, C.c_uint32]),
         (prefix + "place", C.c_int, [H, C.c_uint32, C.c_uint32, C.POINTER(pe_ranked_node), u32p]),
         (prefix + "system_place", C.c_int, [H, C.c_uint32, f64p, u8p, u32p]),
+        (prefix + "get_eligibility", C.c_int, [H, C.c_uint32, C.POINTER(pe_class_feas), C.c_uint32, u32p, u32p]),
+        (prefix + "put_eligibility", C.c_int, [H, C.POINTER(pe_class_feas), C.c_uint32]),
+        (prefix + "get_cursor", C.c_int, [H, u32p, u32p]),
+        (prefix + "set_cursor", C.c_int, [H, C.c_uint32, C.c_uint32, C.c_uint32]),
     ]
 
 
@@ -208,7 +220,8 @@ ENGINE_SYMBOLS = [
     "pe_check_constraint", "pe_last_sweep_bytes", "pe_select_shard", "pe_select_merge",
     "pe_set_metrics", "pe_last_metrics", "pe_update_allocs", "pe_speculation_stats",
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
-    "pe_place_sharded", "pe_last_exchange_us",
+    "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
+    "pe_set_cursor",
 ]
 
 

@@ -469,6 +469,25 @@ struct pe_stack {
     std::map<uint32_t, std::vector<int8_t>> ref_tg_memo;
     std::vector<int8_t> ref_job_memo;
     std::string metrics_text;
+
+    // EvalEligibility as the reference chain holds it (pe_get_eligibility,
+    // context.go:190-356): every Select logs the visit-list span its chain
+    // pulled; spans resolve in visit order into the job-level and per task
+    // group class maps (the memo entries FeasibilityWrapper.Next writes,
+    // feasible.go:1061-1153). Resolution is lazy (SetNodes, SetJob, a get) and
+    // stops as soon as every class has been seen.
+    struct EligSpan { uint32_t tgi, begin, len; };
+    struct ExTg { std::vector<int8_t> st; std::vector<uint8_t> seen; uint32_t unseen = 0; };
+    std::vector<EligSpan> elig_log;
+    std::vector<int8_t> ex_job;                          // per dense class: -1 unknown / 0 / 1
+    std::vector<uint8_t> ex_job_seen;
+    uint32_t ex_job_unseen = 0;
+    std::map<uint32_t, ExTg> ex_tg;                      // task group name -> class map
+    std::map<uint32_t, bool> ex_tg_escaped;              // tgEscapedConstraints (kept across SetJob)
+    std::vector<std::pair<uint32_t, uint32_t>> ex_dirty; // (tg name or PE_NONE, class) since the last get
+    std::vector<uint32_t> cls_str;                       // dense class -> ComputedClass str id
+    bool elig_mute = false;                              // place_impl inside pe_place / spec_start
+    uint64_t test_fallback_every = 0, test_select_calls = 0;   // PE_TEST_FALLBACK_EVERY
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
     DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;  // device-resident parallel count loop (k_ploop)
@@ -1810,8 +1829,14 @@ int build_psets(pe_stack* s, TgPlan& g) {
     // computeSpreadInfo once per task group name; weights accumulate (spread.go:254)
     if (!s->spread_info_done.count(g.name)) {
         s->spread_info_done.insert(g.name);
+        const int32_t before = s->sum_spread_weights;
         for (auto& sp : g.spreads) s->sum_spread_weights += (int32_t)(int8_t)sp.weight;
         for (auto& sp : s->job_spreads) s->sum_spread_weights += (int32_t)(int8_t)sp.weight;
+        // SpreadIterator.Next divides by the running sum (spread.go:157): the
+        // other groups' spread weights change with it
+        if (s->sum_spread_weights != before)
+            for (auto& o : s->tgs)
+                if (o.get() != &g) o->psets_built = false;
     }
     // combined list for desired counts: tg spreads then job spreads, keyed by attribute
     std::map<uint32_t, const SpreadSpec*> info;
@@ -2932,6 +2957,7 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     if (const char* e = std::getenv("PE_SPECULATE")) s->spec_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_SPIN_WAIT")) s->spin_wait = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_API_PROF")) s->api_prof = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PE_TEST_FALLBACK_EVERY")) s->test_fallback_every = std::strtoull(e, nullptr, 10);
     return s;
 }
 
@@ -2979,6 +3005,125 @@ int pe_check_constraint(const char* op, const char* l, int ls, const char* r, in
     return ev.check(op ? op : "", lt, rt) ? 1 : 0;
 }
 
+// ---- EvalEligibility export (context.go:190-356) ---------------------------
+
+static void elig_reset(pe_stack* s) {
+    s->elig_log.clear();
+    s->ex_job.clear();
+    s->ex_job_seen.clear();
+    s->ex_job_unseen = 0;
+    s->ex_tg.clear();
+    s->ex_tg_escaped.clear();
+    s->ex_dirty.clear();
+    s->cls_str.clear();
+}
+
+static void elig_size(pe_stack* s) {
+    if (s->ex_job.size() != s->ncls) {
+        s->ex_job.assign(s->ncls, -1);
+        s->ex_job_seen.assign(s->ncls, 0);
+        s->ex_job_unseen = s->ncls;
+    }
+}
+
+static pe_stack::ExTg& elig_tg(pe_stack* s, uint32_t name) {
+    pe_stack::ExTg& e = s->ex_tg[name];
+    if (e.st.size() != s->ncls) {
+        e.st.assign(s->ncls, -1);
+        e.seen.assign(s->ncls, 0);
+        e.unseen = s->ncls;
+    }
+    return e;
+}
+
+static void elig_set(pe_stack* s, uint32_t map, std::vector<int8_t>& st, uint32_t c, int8_t v) {
+    if (st[c] == v) return;
+    st[c] = v;
+    s->ex_dirty.emplace_back(map, c);
+}
+
+// One row the chain pulled for a Select of task group g, in visit order
+// (FeasibilityWrapper.Next, feasible.go:1061-1153): the job-level entry of its
+// class is written unless the job escaped; the task group's entry is decided
+// by the first visited node of the class that passes the job checks.
+static void elig_visit(pe_stack* s, TgPlan& g, pe::ConstraintEvaluator& ev, uint32_t row) {
+    const HostNode& nd = s->nodes[row];
+    const uint32_t c = nd.cls;
+    bool jr;
+    if (s->job_escaped) {
+        jr = g.job_ok_node.size() == s->nodes.size() ? g.job_ok_node[row] != 0 : job_feasible(s, ev, s->view(row));
+    } else {
+        if (s->job_memo.size() != s->ncls) s->job_memo.assign(s->ncls, -1);
+        if (s->job_memo[c] == -1) s->job_memo[c] = job_feasible(s, ev, s->view(row)) ? 1 : 0;
+        jr = s->job_memo[c] == 1;
+        if (!s->ex_job_seen[c]) { s->ex_job_seen[c] = 1; s->ex_job_unseen--; }
+        elig_set(s, PE_NONE, s->ex_job, c, jr ? 1 : 0);
+    }
+    if (g.escaped) return;
+    pe_stack::ExTg& e = elig_tg(s, g.name);
+    if (e.seen[c]) return;
+    if (!jr) {
+        // a class-exact job failure: no node of the class reaches the tg checks
+        if (!s->job_escaped) { e.seen[c] = 1; e.unseen--; }
+        return;
+    }
+    e.seen[c] = 1;
+    e.unseen--;
+    if (g.sig_tg.size() != s->sig_rep.size()) {
+        g.sig_tg.clear();
+        classify_classes(s, g, ev);
+    }
+    elig_set(s, g.name, e.st, c, g.sig_tg[nd.sig] ? 1 : 0);
+}
+
+static void elig_walk(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& list, uint32_t begin, uint32_t len,
+                      pe::ConstraintEvaluator& ev) {
+    const size_t m = list.size();
+    if (tgi >= s->tgs.size() || !m) return;
+    TgPlan& g = *s->tgs[tgi];
+    elig_size(s);
+    pe_stack::ExTg* e = g.escaped ? nullptr : &elig_tg(s, g.name);
+    len = (uint32_t)std::min<uint64_t>(len, m);
+    for (uint32_t k = 0; k < len; k++) {
+        if ((!e || e->unseen == 0) && (s->job_escaped || s->ex_job_unseen == 0)) break;   // nothing left to learn
+        elig_visit(s, g, ev, list[(begin + k) % m]);
+    }
+}
+
+static void elig_resolve(pe_stack* s) {
+    if (s->elig_log.empty()) return;
+    pe::ConstraintEvaluator ev;
+    for (const auto& sp : s->elig_log) elig_walk(s, sp.tgi, s->visit, sp.begin, sp.len, ev);
+    s->elig_log.clear();
+}
+
+// A Select of task group tgi pulled `len` rows of the SetNodes list from
+// position `begin` (its StaticIterator window). Consecutive windows of one
+// group merge, so the speculative count loop logs one span.
+static void elig_log_span(pe_stack* s, uint32_t tgi, uint32_t begin, uint32_t len) {
+    if (s->elig_mute || !len) return;
+    const uint32_t m = (uint32_t)s->visit.size();
+    if (!m) return;
+    begin %= m;
+    if (!s->elig_log.empty()) {
+        pe_stack::EligSpan& last = s->elig_log.back();
+        if (last.tgi == tgi && last.len < m && (uint32_t)(((uint64_t)last.begin + last.len) % m) == begin) {
+            last.len = (uint32_t)std::min<uint64_t>((uint64_t)last.len + len, m);
+            return;
+        }
+        if (last.tgi == tgi && last.len >= m) return;   // the whole list already
+    }
+    s->elig_log.push_back(pe_stack::EligSpan{tgi, begin, std::min(len, m)});
+}
+
+// A Select over another list (the preferred nodes): resolve in order now.
+static void elig_visit_list(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& list, uint32_t len) {
+    if (s->elig_mute || !len) return;
+    elig_resolve(s);
+    pe::ConstraintEvaluator ev;
+    elig_walk(s, tgi, list, 0, len, ev);
+}
+
 int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
     if (!s || !strs || !nodes) return PE_EINVAL;
     spec_drop(s);
@@ -2997,6 +3142,7 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
     s->ref_job_memo.clear();
     s->spread_info_done.clear();
     s->sum_spread_weights = 0;
+    elig_reset(s);
     int rc = build_state(s, nodes, allocs);
     if (rc) return rc;
     s->have_state = true;
@@ -3036,6 +3182,7 @@ int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* a
     s->ref_job_memo.clear();
     s->spread_info_done.clear();
     s->sum_spread_weights = 0;
+    elig_reset(s);
     s->have_job = false;
     s->have_job_version = false;
     retire_tgs(s);
@@ -3074,6 +3221,7 @@ int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nod
     s->ref_job_memo.clear();
     s->spread_info_done.clear();
     s->sum_spread_weights = 0;
+    elig_reset(s);
     s->have_job = false;
     s->have_job_version = false;
     retire_tgs(s);
@@ -3115,6 +3263,7 @@ int pe_reset_plan(pe_stack* s) {
     s->ref_job_memo.clear();
     s->spread_info_done.clear();
     s->sum_spread_weights = 0;
+    elig_reset(s);
     s->have_job = false;
     s->have_job_version = false;
     retire_tgs(s);
@@ -3131,6 +3280,7 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     s->add_strings(strs);
     const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
     if (generic && s->have_job_version && s->job_version == j->version) return PE_OK;   // stack.go:94-96
+    elig_resolve(s);   // the windows so far belong to the current job's task groups
     {
         const int frc = spec_flush(s);   // a different job: the plan so far goes to HBM first
         if (frc) return frc;
@@ -3260,6 +3410,7 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
                 if (nd.n_device_nets > 1) { g->unsupported = "task network asks on multi-device nodes"; break; }
     }
     s->have_job = true;
+    for (auto& g : s->tgs) s->ex_tg_escaped[g->name] = g->escaped;   // EvalEligibility.SetJob (context.go:221-234)
     ApiScope prof_own_(s, "set_job.own+collisions");
     {
         auto it = s->job_keys.find(std::make_pair(s->job_id, s->job_ns));
@@ -3301,6 +3452,7 @@ int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_
         if (frc) return frc;
     }
     s->gen++;
+    elig_resolve(s);   // logged spans index the old list
     s->visit.assign(rows, rows + n);
     s->d_visit_is_visit = false;
     s->offset = 0;
@@ -3627,6 +3779,13 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
 int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
     if (!s || !out) return PE_EINVAL;
     int rc = PE_OK;
+    if (s->test_fallback_every && ++s->test_select_calls % s->test_fallback_every == 0) {
+        // test hook: this Select is answered by the caller's Go chain (the
+        // shim's PE_EUNSUPPORTED path); the engine state is the committed prefix
+        rc = spec_flush(s);
+        if (rc) return rc;
+        return s->fail(PE_EUNSUPPORTED, "PE_TEST_FALLBACK_EVERY");
+    }
     if (!spec_serve(s, tgi, opts, out)) {
         rc = spec_flush(s);
         if (rc) return rc;
@@ -3656,6 +3815,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         if (s->cfg.preempt) rc = run_evict_select(s, *s->tgs[tgi], s->visit, 0, nullptr, out, &no);
         else rc = run_place(s, tgi, 1, 0, s->visit, 0, nullptr, out, &placed, &no);
         s->limit = saved;
+        if (rc == PE_OK) elig_log_span(s, tgi, 0, out->nodes_evaluated);
         if (rc == PE_OK && s->metrics_on)
             rc = compute_metrics(s, *s->tgs[tgi], s->visit, 0, out->nodes_evaluated, nullptr, s->cfg.preempt != 0);
         return rc;
@@ -3677,6 +3837,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         if (opts->preempt) rc = run_evict_select(s, g, pref, 0, &o2, out, &no);
         else rc = run_place(s, tgi, 1, 0, pref, 0, &o2, out, &placed, &no);
         if (rc) return rc;
+        elig_visit_list(s, tgi, pref, out->nodes_evaluated);
         // the inner Select over the preferred list has its own AllocMetric
         // (ctx.Reset per Select); its walk also advances the memo shadow
         if (s->metrics_on) {
@@ -3698,6 +3859,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         rc = run_evict_select(s, g, s->visit, s->offset, opts, out, &no);
         if (rc) return rc;
         s->offset = no;
+        elig_log_span(s, tgi, start0, out->nodes_evaluated);
         if (s->metrics_on) rc = compute_metrics(s, g, s->visit, start0, out->nodes_evaluated, opts, true);
         return rc;
     }
@@ -3706,6 +3868,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         s->visit_unique) {
         // a whole pass over a large list: multi-CU sweep instead of one workgroup
         rc = run_sweep_select(s, g, opts, out);
+        if (rc == PE_OK) elig_log_span(s, tgi, start, out->nodes_evaluated);
         if (rc == PE_OK && s->metrics_on) rc = compute_metrics(s, g, s->visit, start, out->nodes_evaluated, opts);
         return rc;
     }
@@ -3713,6 +3876,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     rc = run_place(s, tgi, 1, 0, s->visit, s->offset, opts, out, &placed, &no);
     if (rc) return rc;
     s->offset = no;
+    elig_log_span(s, tgi, start, out->nodes_evaluated);
     if (s->metrics_on) rc = compute_metrics(s, g, s->visit, start, out->nodes_evaluated, opts);
     return rc;
 }
@@ -3811,6 +3975,7 @@ int pe_select_merge(pe_stack* s, uint32_t tgi, const pe_shard_rec* recs, uint32_
     if (rc) return rc;
     s->offer_row = out->row;
     s->offers = pack_offers(out);
+    elig_log_span(s, tgi, s->offset, (uint32_t)s->visit.size());   // a full pass
     return PE_OK;
 }
 
@@ -4265,6 +4430,7 @@ static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     if (sp.compact) widen_rec(sp.crecs[sp.served++], out);
     else *out = sp.recs[sp.served++];
     sp.pending = out->row >= 0;
+    elig_log_span(s, tgi, s->offset, out->nodes_evaluated);
     s->offset = out->new_offset;   // the StaticIterator cursor after this Select
     s->metrics_valid = false;
     s->spec_stats[1]++;
@@ -4405,7 +4571,9 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     uint32_t placed = 0;
     s->emit_sink = &sp.crecs;
     s->emit_sunk = false;
+    s->elig_mute = true;   // records are logged when served
     rc = place_impl(s, tgi, count, sp.recs.data(), &placed, false);
+    s->elig_mute = false;
     s->emit_sink = nullptr;
     sp.compact = s->emit_sunk;
     s->plan.resize(plan0);   // the plan holds confirmed placements only
@@ -4437,8 +4605,24 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     int rc = spec_flush(s);
     if (rc) return rc;
     uint32_t p = 0;
+    const uint32_t start = s->offset;
+    s->elig_mute = true;   // the windows are logged from the records below
     rc = place_impl(s, tgi, count, out, &p, true);
+    s->elig_mute = false;
     if (placed) *placed = p;
+    if (rc == PE_OK && count) {
+        // Consecutive windows continue the cursor. A nil Select (the last
+        // record when p < count, or the plain Select before a Preempt retry,
+        // whose placement then evicts) pulled the whole list.
+        uint64_t pulled = 0;
+        bool whole = p < count;
+        for (uint32_t k = 0; k < std::min(p + 1, count); k++) {
+            pulled += out[k].nodes_evaluated;
+            whole = whole || (k < p && out[k].n_preempted > 0);
+        }
+        elig_log_span(s, tgi, start, whole ? (uint32_t)s->visit.size()
+                                           : (uint32_t)std::min<uint64_t>(pulled, s->visit.size()));
+    }
     if (tgi < s->tgs.size() && s->tgs[tgi]->ask.cores > 0)   // the placements' reserved cores, in order
         for (uint32_t k = 0; k < p && k < count; k++) core_record(s, *s->tgs[tgi], out[k].row, true, out[k].reserved_cores);
     return rc;
@@ -4584,7 +4768,7 @@ int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id) {
 // resolves the winner, writes its record and commits
 // it on every rank. Nothing returns to the host between placements; the stop
 // flag is read every 64 placements.
-int pe_place_sharded(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_begin, uint32_t row_end,
+static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_begin, uint32_t row_end,
                      pe_ranked_node* out, uint32_t* placed) {
     if (!s || (!out && count)) return PE_EINVAL;
     if (!s->comm) return s->fail(PE_ESTATE, "pe_comm_init not called");
@@ -4962,7 +5146,7 @@ static int system_place_distinct(pe_stack* s, uint32_t tgi, TgPlan& g, double* o
     return PE_OK;
 }
 
-int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
+static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     if (!s || !out_score || !out_status) return PE_EINVAL;
     {
         const int frc = spec_flush(s);
@@ -5180,4 +5364,130 @@ extern "C" int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap) {
         buf[k] = 0;
     }
     return (int64_t)s->metrics_text.size() + 1;
+}
+
+// ---- wrappers that log the chain's visits for EvalEligibility -----------------
+
+int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
+    const int rc = system_place_impl(s, tgi, out_score, out_status, placed);
+    // one single-node Select per row of the list (scheduler_system.go:290-422)
+    if (rc == PE_OK) elig_log_span(s, tgi, 0, (uint32_t)s->visit.size());
+    return rc;
+}
+
+int pe_place_sharded(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_begin, uint32_t row_end,
+                     pe_ranked_node* out, uint32_t* placed) {
+    const int rc = place_sharded_impl(s, tgi, count, row_begin, row_end, out, placed);
+    if (rc == PE_OK && count) elig_log_span(s, tgi, s->offset, (uint32_t)s->visit.size());   // full passes
+    return rc;
+}
+
+int pe_get_eligibility(pe_stack* s, uint32_t changed_only, pe_class_feas* out, uint32_t cap, uint32_t* n_out,
+                       uint32_t* flags) {
+    if (!s || !n_out) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    elig_resolve(s);
+    elig_size(s);
+    if (s->cls_str.size() != s->ncls) {
+        s->cls_str.assign(s->ncls, PE_NONE);
+        for (const auto& kv : s->cls_of)
+            if (kv.second < s->ncls) s->cls_str[kv.second] = kv.first;
+    }
+    std::vector<pe_class_feas> ents;
+    auto push = [&](uint32_t map, uint32_t c, int8_t v) {
+        if (v < 0) return;
+        ents.push_back(pe_class_feas{map, s->cls_str[c], v ? (uint32_t)PE_CLASS_ELIGIBLE : (uint32_t)PE_CLASS_INELIGIBLE});
+    };
+    if (changed_only) {
+        std::sort(s->ex_dirty.begin(), s->ex_dirty.end());
+        s->ex_dirty.erase(std::unique(s->ex_dirty.begin(), s->ex_dirty.end()), s->ex_dirty.end());
+        for (const auto& d : s->ex_dirty) {
+            if (d.first == PE_NONE) push(PE_NONE, d.second, s->ex_job[d.second]);
+            else push(d.first, d.second, s->ex_tg[d.first].st[d.second]);
+        }
+    } else {
+        for (uint32_t c = 0; c < s->ncls; c++) push(PE_NONE, c, s->ex_job[c]);
+        for (const auto& kv : s->ex_tg)
+            for (uint32_t c = 0; c < (uint32_t)kv.second.st.size(); c++) push(kv.first, c, kv.second.st[c]);
+    }
+    *n_out = (uint32_t)ents.size();
+    if (out && cap) std::memcpy(out, ents.data(), sizeof(pe_class_feas) * std::min<size_t>(cap, ents.size()));
+    if (ents.size() <= cap) s->ex_dirty.clear();
+    if (flags) {
+        bool esc = s->job_escaped;   // HasEscaped (context.go:237-251)
+        for (const auto& kv : s->ex_tg_escaped) esc = esc || kv.second;
+        *flags = esc ? PE_ELIG_ESCAPED : 0u;
+    }
+    return PE_OK;
+}
+
+int pe_put_eligibility(pe_stack* s, const pe_class_feas* in, uint32_t n) {
+    if (!s || (!in && n)) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    s->gen++;
+    elig_resolve(s);
+    elig_size(s);
+    if (s->job_memo.size() != s->ncls) s->job_memo.assign(s->ncls, -1);
+    if (s->ref_job_memo.size() != s->ncls) s->ref_job_memo.assign(s->ncls, -1);
+    bool changed = false;
+    for (uint32_t i = 0; i < n; i++) {
+        const auto it = s->cls_of.find(in[i].computed_class);
+        if (it == s->cls_of.end() || it->second >= s->ncls) continue;   // a class without nodes here
+        const uint32_t c = it->second;
+        if (in[i].status != PE_CLASS_ELIGIBLE && in[i].status != PE_CLASS_INELIGIBLE) continue;
+        const int8_t v = in[i].status == PE_CLASS_ELIGIBLE ? 1 : 0;
+        if (in[i].task_group == PE_NONE) {
+            s->ex_job[c] = v;
+            if (!s->ex_job_seen[c]) { s->ex_job_seen[c] = 1; s->ex_job_unseen--; }
+            if (s->job_memo[c] != v) { s->job_memo[c] = v; changed = true; }
+            s->ref_job_memo[c] = v;
+        } else {
+            const uint32_t name = in[i].task_group;
+            pe_stack::ExTg& e = elig_tg(s, name);
+            e.st[c] = v;
+            if (!e.seen[c]) { e.seen[c] = 1; e.unseen--; }
+            auto& memo = s->tg_memo[name];
+            if (memo.size() != s->ncls) memo.assign(s->ncls, -1);
+            if (memo[c] != v) { memo[c] = v; changed = true; }
+            auto& rt = s->ref_tg_memo[name];
+            if (rt.size() != s->ncls) rt.assign(s->ncls, -1);
+            rt[c] = v;
+        }
+    }
+    if (changed) invalidate_tables(s);
+    return PE_OK;
+}
+
+int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit) {
+    if (!s) return PE_EINVAL;
+    if (offset) *offset = s->offset;
+    if (limit) *limit = s->limit;
+    return PE_OK;
+}
+
+int pe_set_cursor(pe_stack* s, uint32_t tgi, uint32_t offset, uint32_t limit) {
+    if (!s) return PE_EINVAL;
+    if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
+    if (!s->visit.empty() && offset >= s->visit.size()) return s->fail(PE_EINVAL, "cursor beyond the SetNodes list");
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    s->gen++;
+    elig_resolve(s);   // windows before the Go chain's Select, in order
+    s->offset = s->visit.empty() ? 0 : offset;
+    s->limit = limit;
+    if (tgi != PE_NONE) {
+        if (!s->have_job || tgi >= s->tgs.size()) return s->fail(PE_EINVAL, "task group index out of range");
+        // the Go chain's SpreadIterator.SetTaskGroup ran for this group (spread.go:76-104)
+        TgPlan& g = *s->tgs[tgi];
+        if (s->cfg.stack_kind == PE_STACK_GENERIC && !s->spread_info_done.count(g.name)) {
+            s->spread_info_done.insert(g.name);
+            for (auto& sp : g.spreads) s->sum_spread_weights += (int32_t)(int8_t)sp.weight;
+            for (auto& sp : s->job_spreads) s->sum_spread_weights += (int32_t)(int8_t)sp.weight;
+            for (auto& o : s->tgs) o->psets_built = false;   // every spread weight is over the new sum
+        }
+    }
+    invalidate_tables(s);
+    return PE_OK;
 }

@@ -17,15 +17,34 @@ stack call, replays the plan's changes since then:
 
 A placement is committed before the next Select, which is exactly when the
 engine's speculative count loop expects it, so the unchanged
-caller gets the device loop. `Plan` here is the subset of structs.Plan
-(structs.go:10540-10714) the protocol reads.
+caller gets the device loop. structs.Plan keeps NodeAllocation as a map of
+per-node lists, so plan order across nodes is not recoverable; new placements
+are replayed node by node, in list order within a node. Commits of different
+nodes commute (resource sums, collision counts, device and core picks are per
+node), and between two Selects the caller appends at most the last Select's
+placement, which is the one the speculation checks.
+
+EvalEligibility: the Go EvalContext's memo is read by the caller after the
+Selects (createBlockedEval, generic_sched.go:177-203), so after every engine
+Select the shim mirrors the entries that changed (pe_get_eligibility with
+changed_only) into `ctx_eligibility`.
+
+PE_EUNSUPPORTED: the Select is answered by `fallback`, the reference chain on
+the same EvalContext (here the oracle restatement). Before it runs, the
+fallback takes the engine's StaticIterator offset and LimitIterator limit
+(pe_get_cursor), the SpreadIterator.SetTaskGroup of every group the engine
+has selected for, and the ctx memo; afterwards the engine takes the chain's
+offset, limit, group and memo back (pe_set_cursor, pe_put_eligibility), so
+later Selects continue exactly where the reference chain would be.
+`Plan` here is the subset of structs.Plan (structs.go:10540-10714) the
+protocol reads.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
-from .stack import GenericStack, SelectOptions
+from .stack import GenericStack, SelectOptions, Unsupported
 
 
 @dataclass
@@ -65,22 +84,32 @@ class Plan:
 class DeviceStack:
     """scheduler.Stack on the engine, driven by an unchanged caller that only
     mutates `plan`. One handle per worker: the snapshot stays resident across
-    evaluations (`new_eval` = NewEvalContext)."""
+    evaluations (`new_eval` = NewEvalContext). `fallback`: the reference chain
+    (a stack with the same interface, given the same snapshot) that answers
+    PE_EUNSUPPORTED Selects."""
 
-    def __init__(self, engine: GenericStack, plan: Plan):
+    def __init__(self, engine: GenericStack, plan: Plan, fallback=None):
         self.eng = engine
+        self.fallback = fallback
         self.plan = plan
         self._tg_names: List[str] = []
+        self.fallback_selects = 0
         self._reset_mirror()
 
     def _reset_mirror(self):
         self._upd: Dict[int, List[int]] = {}
         self._alloc_seen: Dict[int, int] = {}
-        self._pre_seen: Dict[int, int] = {}
+        self.ctx_eligibility = {"job": {}, "tgs": {}}
+        self._seen_tgs: List[str] = []     # groups the engine selected for, in order
+        self._fb_tgs = set()               # groups the fallback's SpreadIterator has seen
+
+    def _stacks(self):
+        return (self.eng,) if self.fallback is None else (self.eng, self.fallback)
 
     def new_eval(self, plan: Plan):
         """A new evaluation on the resident snapshot (pe_reset_plan)."""
-        self.eng.ResetPlan()
+        for st in self._stacks():
+            st.ResetPlan()
         self.plan = plan
         self._reset_mirror()
 
@@ -93,28 +122,73 @@ class DeviceStack:
             while k < len(have) and k < len(want) and have[k] == want[k]:
                 k += 1
             for a in reversed(have[k:]):
-                self.eng.PopUpdate(a)
+                for st in self._stacks():
+                    st.PopUpdate(a)
             if want[k:]:
-                self.eng.StopAllocs(want[k:])
+                for st in self._stacks():
+                    st.StopAllocs(want[k:])
             self._upd[node] = list(want)
         for node, allocs in p.node_allocation.items():
             seen = self._alloc_seen.get(node, 0)
             pre = p.node_preemptions.get(node, [])
             for a in allocs[seen:]:
                 by = [r for r, pid in pre if pid == a.id]
-                self.eng.Commit(self._tg_names.index(a.task_group), a.node_row, by)
+                for st in self._stacks():
+                    st.Commit(self._tg_names.index(a.task_group), a.node_row, by)
             self._alloc_seen[node] = len(allocs)
+
+    def _mirror_eligibility(self, delta):
+        self.ctx_eligibility["job"].update(delta["job"])
+        for tg, m in delta["tgs"].items():
+            self.ctx_eligibility["tgs"].setdefault(tg, {}).update(m)
 
     # -- scheduler.Stack (stack.go:23-32) ------------------------------------
     def SetNodes(self, rows):
         self._sync()
+        if self.fallback is not None:
+            self.fallback.SetNodes(rows)
         return self.eng.SetNodes(rows)
 
     def SetJob(self, job):
         self._sync()
         self._tg_names = [g.name for g in job.task_groups]
+        if self.fallback is not None:
+            self.fallback.SetJob(job)
         self.eng.SetJob(job)
 
     def Select(self, tg, options: Optional[SelectOptions] = None):
         self._sync()
-        return self.eng.Select(tg, options)
+        name = tg if isinstance(tg, str) else self._tg_names[tg]
+        try:
+            r = self.eng.Select(tg, options)
+        except Unsupported:
+            if self.fallback is None:
+                raise
+            return self._fallback_select(tg, name, options)
+        if name not in self._seen_tgs:
+            self._seen_tgs.append(name)
+        self._mirror_eligibility(self.eng.Eligibility(changed_only=True))
+        return r
+
+    def _fallback_select(self, tg, name, options):
+        """The reference chain answers; both sides then hold the same iterator
+        state, plan and memo (pe_get_cursor / pe_set_cursor / pe_put_eligibility)."""
+        fb = self.fallback
+        off, lim = self.eng.GetCursor()
+        fb.SetCursor(off, lim)
+        for g in self._seen_tgs:            # SpreadIterator.SetTaskGroup the engine has done
+            if g not in self._fb_tgs:
+                fb.SetCursor(off, lim, g)
+                self._fb_tgs.add(g)
+        fb.PutEligibility(self.ctx_eligibility)
+        r = fb.Select(tg, options)
+        self.fallback_selects += 1
+        self._fb_tgs.add(name)
+        self.ctx_eligibility = fb.Eligibility()
+        self.ctx_eligibility.pop("escaped", None)
+        self.eng.PutEligibility(self.ctx_eligibility)
+        off, lim = fb.GetCursor()
+        self.eng.SetCursor(off, lim, name)
+        if name not in self._seen_tgs:
+            self._seen_tgs.append(name)
+        return r

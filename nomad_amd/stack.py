@@ -216,6 +216,67 @@ class _Stack:
             out[names[kind]][key] = int(cnt)
         return out
 
+    # -- EvalEligibility and iterator state (context.go:190-356) -------------
+    def Eligibility(self, changed_only: bool = False) -> Dict:
+        """The evaluation's EvalEligibility maps as the reference chain holds
+        them: {"job": {class: eligible}, "tgs": {tg name: {class: eligible}},
+        "escaped": HasEscaped()} (pe_get_eligibility)."""
+        fn = self._fn("get_eligibility")
+        n, flags = C.c_uint32(0), C.c_uint32(0)
+        self._check(fn(self._h, int(changed_only), None, 0, C.byref(n), C.byref(flags)))
+        buf = (abi.pe_class_feas * max(1, n.value))()
+        self._check(fn(self._h, int(changed_only), buf, n.value, C.byref(n), C.byref(flags)))
+        strs = self.state.interner.strs
+        out = {"job": {}, "tgs": {}, "escaped": bool(flags.value & abi.PE_ELIG_ESCAPED)}
+        for e in buf[:n.value]:
+            cls, ok = strs[e.computed_class], e.status == abi.PE_CLASS_ELIGIBLE
+            if e.task_group == abi.PE_NONE:
+                out["job"][cls] = ok
+            else:
+                out["tgs"].setdefault(strs[e.task_group], {})[cls] = ok
+        return out
+
+    def PutEligibility(self, elig: Dict):
+        """Load EvalEligibility maps ({"job": ..., "tgs": ...}) into this stack's memo."""
+        it = self.state.interner
+        ents = [(abi.PE_NONE, it.intern(c), ok) for c, ok in elig.get("job", {}).items()]
+        for tg, m in elig.get("tgs", {}).items():
+            ents += [(it.intern(tg), it.intern(c), ok) for c, ok in m.items()]
+        buf = (abi.pe_class_feas * max(1, len(ents)))()
+        for k, (tg, c, ok) in enumerate(ents):
+            buf[k].task_group, buf[k].computed_class = tg, c
+            buf[k].status = abi.PE_CLASS_ELIGIBLE if ok else abi.PE_CLASS_INELIGIBLE
+        self._check(self._fn("put_eligibility")(self._h, buf, len(ents)))
+
+    @staticmethod
+    def GetClasses(elig: Dict) -> Dict[str, bool]:
+        """EvalEligibility.GetClasses (context.go:253-290) over Eligibility()'s maps."""
+        out: Dict[str, bool] = {}
+        for classes in elig["tgs"].values():
+            for cls, ok in classes.items():
+                if ok:
+                    out[cls] = True
+                elif cls not in out:
+                    out[cls] = False
+        for cls, ok in elig["job"].items():
+            if ok:
+                out.setdefault(cls, True)
+            else:
+                out[cls] = False
+        return out
+
+    def GetCursor(self):
+        """(StaticIterator offset, LimitIterator limit)."""
+        off, lim = C.c_uint32(0), C.c_uint32(0)
+        self._check(self._fn("get_cursor")(self._h, C.byref(off), C.byref(lim)))
+        return off.value, lim.value
+
+    def SetCursor(self, offset: int, limit: int, tg=None):
+        """Adopt another chain's cursor and limit; `tg`: the task group it
+        selected for (its SpreadIterator.SetTaskGroup ran)."""
+        tgi = abi.PE_NONE if tg is None else self._tg_index(tg)
+        self._check(self._fn("set_cursor")(self._h, tgi, int(offset), int(limit)))
+
     # -- scheduler.State snapshot -------------------------------------------
     def SetState(self, nodes: Sequence[Node], allocs: Sequence[Allocation] = ()):
         self.nodes = list(nodes)

@@ -2313,6 +2313,66 @@ int oracle_limit_iter(const double* scores, int n, int limit, double threshold, 
 
 }  // extern "C"
 
+// ---- the iterator state a fallback GenericStack shares with the engine -----
+// (test mirror of what the cgo shim reads and writes on the Go chain: the
+// StaticIterator cursor, the LimitIterator limit, SpreadIterator.SetTaskGroup
+// and the EvalEligibility maps of the shared EvalContext)
+
+static uint32_t str_id(const State& st, const std::string& v) {
+    for (uint32_t i = 0; i < st.strs.size(); i++)
+        if (st.strs[i] == v) return i;
+    return PE_NONE;
+}
+
+extern "C" int oracle_get_eligibility(oracle_stack* s, uint32_t changed_only, pe_class_feas* out, uint32_t cap,
+                                      uint32_t* n, uint32_t* flags) {
+    (void)changed_only;   // the oracle always reports the whole memo
+    std::vector<pe_class_feas> ents;
+    auto status = [](int f) { return f == kEligible ? (uint32_t)PE_CLASS_ELIGIBLE : (uint32_t)PE_CLASS_INELIGIBLE; };
+    for (auto& kv : s->ctx.elig.job)
+        if (kv.second == kEligible || kv.second == kIneligible)
+            ents.push_back(pe_class_feas{PE_NONE, str_id(s->state, kv.first), status(kv.second)});
+    for (auto& tg : s->ctx.elig.tgs)
+        for (auto& kv : tg.second)
+            if (kv.second == kEligible || kv.second == kIneligible)
+                ents.push_back(pe_class_feas{str_id(s->state, tg.first), str_id(s->state, kv.first), status(kv.second)});
+    *n = (uint32_t)ents.size();
+    if (out) std::memcpy(out, ents.data(), sizeof(pe_class_feas) * std::min<size_t>(cap, ents.size()));
+    if (flags) {   // HasEscaped (context.go:237-251)
+        bool esc = s->ctx.elig.job_escaped;
+        for (auto& kv : s->ctx.elig.tg_escaped) esc = esc || kv.second;
+        *flags = esc ? PE_ELIG_ESCAPED : 0u;
+    }
+    return PE_OK;
+}
+
+extern "C" int oracle_put_eligibility(oracle_stack* s, const pe_class_feas* in, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        const std::string cls = S(s->state, in[i].computed_class);
+        const bool e = in[i].status == PE_CLASS_ELIGIBLE;
+        if (in[i].task_group == PE_NONE) s->ctx.elig.SetJobEligibility(e, cls);
+        else s->ctx.elig.SetTaskGroupEligibility(e, S(s->state, in[i].task_group), cls);
+    }
+    return PE_OK;
+}
+
+extern "C" int oracle_get_cursor(const oracle_stack* s, uint32_t* offset, uint32_t* limit) {
+    const int m = (int)s->source.nodes.size();
+    if (offset) *offset = m ? (uint32_t)(s->source.offset % m) : 0u;
+    if (limit) *limit = (uint32_t)s->limit.limit;
+    return PE_OK;
+}
+
+extern "C" int oracle_set_cursor(oracle_stack* s, uint32_t tgi, uint32_t offset, uint32_t limit) {
+    s->source.offset = (int)offset;
+    s->limit.limit = (int)limit;
+    if (tgi != PE_NONE && s->cfg.stack_kind == PE_STACK_GENERIC) {
+        if (!s->have_job || tgi >= s->job.tgs.size()) { s->err = "bad task group"; return PE_EINVAL; }
+        s->spread.SetTaskGroup(&s->tg(tgi));
+    }
+    return PE_OK;
+}
+
 /* AllocMetric maps of the last Select (ClassFiltered, ConstraintFiltered,
  * ClassExhausted, DimensionExhausted) as text; returns the bytes needed. */
 extern "C" size_t oracle_last_metrics(const oracle_stack* s, char* buf, size_t cap) {

@@ -34,12 +34,12 @@ def test_every_declared_symbol_is_exported():
 def test_abi_version():
     lib = C.CDLL(LIB)
     lib.pe_abi_version.restype = C.c_uint32
-    assert lib.pe_abi_version() == 3
+    assert lib.pe_abi_version() == 4
 
 
 STRUCTS = ["pe_strtab", "pe_attr", "pe_node_table", "pe_alloc_table", "pe_constraint", "pe_affinity",
            "pe_spread_target", "pe_spread", "pe_device_request", "pe_task", "pe_task_group", "pe_job",
-           "pe_config", "pe_select_options", "pe_ranked_node", "pe_placement",
+           "pe_config", "pe_select_options", "pe_ranked_node", "pe_placement", "pe_class_feas",
            "pe_plan_node_table", "pe_plan_alloc_table", "pe_plan"]
 
 
