@@ -318,6 +318,14 @@ int pe_select(pe_stack* s, uint32_t tg_index, const pe_select_options* opts,
  * committed prefix, so results always equal one-at-a-time Selects.
  * PE_SPECULATE=0 in the environment disables it. */
 int pe_commit(pe_stack* s, uint32_t tg_index, int32_t row);
+/* Apply queued device work now: the speculative count loop's confirmed
+ * placements and the SystemScheduler fast path's queued commits (every entry
+ * point that reads the device state does this itself; callers use it to
+ * settle the device at a point of their choosing). */
+int pe_flush(pe_stack* s);
+/* SystemStack fast path counters: out[0] k_system passes over the snapshot
+ * that filled the per-row cache, out[1] single-node Selects answered from it. */
+int pe_system_spec_stats(const pe_stack* s, uint64_t* out2);
 /* Multi-GPU: one engine handle per GPU and process, joined by
  * an RCCL communicator (ncclGetUniqueId on one rank, the 128 bytes shared by
  * the caller, ncclCommInitRank on every rank). */

@@ -221,7 +221,7 @@ ENGINE_SYMBOLS = [
     "pe_set_metrics", "pe_last_metrics", "pe_update_allocs", "pe_speculation_stats",
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
-    "pe_set_cursor",
+    "pe_set_cursor", "pe_flush", "pe_system_spec_stats",
 ]
 
 

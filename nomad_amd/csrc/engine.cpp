@@ -309,6 +309,7 @@ struct TgPlan {
     DevMem static_gate, static_blocked;
     std::vector<std::unique_ptr<PsetDev>> psets;
     bool psets_built = false;
+    bool elig_complete = false;   // every class's EvalEligibility entries are known (pe_get_eligibility)
     bool psets_dynamic = false;        // plan stops clear values: counts rebuilt on the host after every commit
     int n_spread = 0;                  // psets[0, n_spread) are spreads, the rest distinct_property
     std::vector<ParsedConstraint> distinct_props;   // tg + task distinct_property constraints
@@ -487,6 +488,25 @@ struct pe_stack {
     std::vector<std::pair<uint32_t, uint32_t>> ex_dirty; // (tg name or PE_NONE, class) since the last get
     std::vector<uint32_t> cls_str;                       // dense class -> ComputedClass str id
     bool elig_mute = false;                              // place_impl inside pe_place / spec_start
+
+    // The unchanged SystemScheduler caller (scheduler_system.go:289-302):
+    // SetNodes([node]) then Select for every node. From the third single-node
+    // Select of a task group on, one k_system pass over every snapshot row
+    // (no commit) answers the rest from a per-row cache; the caller's commits
+    // queue on the host and reach HBM in one k_commit_rows launch when any
+    // other call needs the device state (sys_flush). Rows a commit, stop or
+    // preemption touched since the pass are answered by the single Select.
+    struct SysSpec {
+        bool active = false;
+        uint32_t tgi = 0, singles = 0, singles_tgi = PE_NONE;
+        int32_t served_row = -1;          // the last served Select's pick, awaiting its commit
+        std::vector<uint32_t> pending;    // committed rows not yet in HBM
+        uint64_t passes = 0, served = 0;
+    } sys;
+    PinnedMem h_sys_cache;                // [FinalScore per row | outcome per row]
+    std::vector<uint8_t> sys_dirty;
+    DevMem d_identity;
+    uint32_t identity_n = 0;
     uint64_t test_fallback_every = 0, test_select_calls = 0;   // PE_TEST_FALLBACK_EVERY
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
@@ -2922,6 +2942,9 @@ static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* op
 static int spec_flush(pe_stack* s);
 static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out);
 static void spec_drop(pe_stack* s);
+static int sys_flush(pe_stack* s);
+static bool sys_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out, int* rc);
+static void sys_touch(pe_stack* s, uint32_t row);
 
 uint32_t pe_abi_version(void) { return PE_ABI_VERSION; }
 
@@ -3085,7 +3108,10 @@ static void elig_walk(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& li
     pe_stack::ExTg* e = g.escaped ? nullptr : &elig_tg(s, g.name);
     len = (uint32_t)std::min<uint64_t>(len, m);
     for (uint32_t k = 0; k < len; k++) {
-        if ((!e || e->unseen == 0) && (s->job_escaped || s->ex_job_unseen == 0)) break;   // nothing left to learn
+        if ((!e || e->unseen == 0) && (s->job_escaped || s->ex_job_unseen == 0)) {   // nothing left to learn
+            g.elig_complete = true;
+            break;
+        }
         elig_visit(s, g, ev, list[(begin + k) % m]);
     }
 }
@@ -3101,7 +3127,7 @@ static void elig_resolve(pe_stack* s) {
 // position `begin` (its StaticIterator window). Consecutive windows of one
 // group merge, so the speculative count loop logs one span.
 static void elig_log_span(pe_stack* s, uint32_t tgi, uint32_t begin, uint32_t len) {
-    if (s->elig_mute || !len) return;
+    if (s->elig_mute || !len || (tgi < s->tgs.size() && s->tgs[tgi]->elig_complete)) return;
     const uint32_t m = (uint32_t)s->visit.size();
     if (!m) return;
     begin %= m;
@@ -3118,7 +3144,7 @@ static void elig_log_span(pe_stack* s, uint32_t tgi, uint32_t begin, uint32_t le
 
 // A Select over another list (the preferred nodes): resolve in order now.
 static void elig_visit_list(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& list, uint32_t len) {
-    if (s->elig_mute || !len) return;
+    if (s->elig_mute || !len || (tgi < s->tgs.size() && s->tgs[tgi]->elig_complete)) return;
     elig_resolve(s);
     pe::ConstraintEvaluator ev;
     elig_walk(s, tgi, list, 0, len, ev);
@@ -3285,6 +3311,9 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
         const int frc = spec_flush(s);   // a different job: the plan so far goes to HBM first
         if (frc) return frc;
     }
+    s->sys.active = false;   // per-row outcomes of the previous job's groups
+    s->sys.singles = 0;
+    s->sys.singles_tgi = PE_NONE;
     s->have_job_version = true;
     s->job_version = j->version;
     s->job_id = j->id;
@@ -3422,6 +3451,21 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
 
 int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
     if (!s) return PE_EINVAL;
+    if (n == 1 && rows && s->sys.active && s->visit.size() == 1 && rows[0] < s->nodes.size()) {
+        // SystemScheduler's per-node SetNodes while the per-row cache answers:
+        // the task group's tables do not depend on the list (every class's
+        // memo verdict is uniform), so only the list changes
+        if (!s->elig_log.empty()) elig_resolve(s);
+        s->gen++;
+        s->visit[0] = rows[0];
+        s->d_visit_is_visit = false;
+        s->rank_of_valid = false;
+        s->visit_unique = true;
+        s->offset = 0;
+        s->limit = 2;
+        if (limit_out) *limit_out = 2;
+        return PE_OK;
+    }
     ApiScope prof_(s, "set_nodes");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     if (!rows && n) return s->fail(PE_EINVAL, "null rows");
@@ -3776,9 +3820,139 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
     return PE_OK;
 }
 
+// ---- SystemScheduler per-node Selects from a per-row cache ------------------
+
+static void sys_touch(pe_stack* s, uint32_t row) {
+    if (row < s->sys_dirty.size()) s->sys_dirty[row] = 1;
+}
+
+// The queued Plan.AppendAllocs of served system Selects, into HBM at once.
+static int sys_flush(pe_stack* s) {
+    pe_stack::SysSpec& y = s->sys;
+    if (y.pending.empty()) return PE_OK;
+    if (y.tgi >= s->tgs.size()) { y.pending.clear(); return s->fail(PE_ESTATE, "queued system commits lost their task group"); }
+    HIP_TRY(s, hipSetDevice(s->device));
+    TgPlan& g = *s->tgs[y.tgi];
+    HIP_TRY(s, upload_s(s, s->d_commit_rows, y.pending));
+    pe::NodeSoA soa = soa_of(s);
+    pe::TgTables t = tables_of(g);
+    pe::Ask a = ask_for(s, g);
+    HIP_TRY(s, pe_launch_commit_rows(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(), (uint32_t)y.pending.size(),
+                                     s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    y.pending.clear();
+    return PE_OK;
+}
+
+// Whether one k_system pass can stand in for this group's single-node Selects:
+// outcomes must be per row (no distinct_property value counts), the memo
+// verdict of every class independent of the visit order (uniform classes or
+// an escaped group), and the result record the cache holds complete (no
+// device offers, reserved cores or static ports to return).
+static bool sys_cacheable(pe_stack* s, TgPlan& g) {
+    return g.unsupported.empty() && g.psets.empty() && g.dev_reqs.empty() && g.ask.cores == 0 && g.rports.empty() &&
+           (g.escaped || g.nonuniform.empty()) && s->visit_unique;
+}
+
+static int sys_start(pe_stack* s, uint32_t tgi) {
+    ApiScope prof_(s, "sys_start");
+    pe_stack::SysSpec& y = s->sys;
+    int rc = spec_flush(s);
+    if (rc) return rc;
+    HIP_TRY(s, hipSetDevice(s->device));
+    rc = prepare_tg(s, tgi, s->visit, 0);
+    if (rc) return rc;
+    TgPlan& g = *s->tgs[tgi];
+    if (!sys_cacheable(s, g)) return PE_EUNSUPPORTED;   // the single Select path answers
+    const uint32_t n = (uint32_t)s->nodes.size();
+    if (s->identity_n != n) {
+        std::vector<uint32_t> id(n);
+        for (uint32_t i = 0; i < n; i++) id[i] = i;
+        HIP_TRY(s, s->d_identity.ensure(sizeof(uint32_t) * (size_t)std::max<uint32_t>(n, 1)));
+        HIP_TRY(s, hipMemcpyAsync(s->d_identity.p, id.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, s->stream));
+        s->identity_n = n;
+    }
+    const size_t st_off = sizeof(double) * (size_t)n;
+    const size_t bytes = st_off + (((size_t)n + 3) & ~(size_t)3) + 4;
+    HIP_TRY(s, s->d_sys_out.ensure(bytes));
+    HIP_TRY(s, s->h_sys_cache.ensure(bytes));
+    uint8_t* dsys = s->d_sys_out.as<uint8_t>();
+    pe::SystemArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.soa = soa_of(s);
+    A.tg = tables_of(g);
+    A.ask = ask_for(s, g);
+    A.list = s->d_identity.as<uint32_t>();
+    A.n_list = n;
+    A.log10 = s->log10;
+    A.out_score = reinterpret_cast<double*>(dsys);
+    A.out_status = dsys + st_off;
+    A.placed = reinterpret_cast<uint32_t*>(dsys + bytes - 4);
+    A.commit = 0;
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, pe_launch_system(&A, s->stream));
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(s->h_sys_cache.p, dsys, bytes - 4, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    s->last_ms_pending = false;
+    s->sys_dirty.assign(n, 0);
+    y.active = true;
+    y.tgi = tgi;
+    y.served_row = -1;
+    y.passes++;
+    return PE_OK;
+}
+
+// A plain single-node SystemStack.Select (stack.go:301-333) answered from the
+// per-row cache. Returns false when the caller must take the single Select path.
+static bool sys_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out, int* rc) {
+    pe_stack::SysSpec& y = s->sys;
+    if (s->visit.size() != 1 || s->metrics_on || !s->have_job || tgi >= s->tgs.size()) return false;
+    if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
+    if (!y.active || y.tgi != tgi) {
+        // start after the group's second single-node Select: one pass over the
+        // snapshot costs about as much as a handful of single Selects
+        if (y.singles_tgi != tgi) { y.singles_tgi = tgi; y.singles = 0; }
+        if (++y.singles < 3) return false;
+        const int r = sys_start(s, tgi);
+        if (r == PE_EUNSUPPORTED) { y.singles = 0; s->err.clear(); return false; }
+        if (r) { *rc = r; return true; }
+    }
+    const uint32_t row = s->visit[0];
+    if (s->sys_dirty[row]) return false;
+    const uint32_t n = (uint32_t)s->nodes.size();
+    const uint8_t st = s->h_sys_cache.as<uint8_t>()[sizeof(double) * (size_t)n + row];
+    if (st == 2 && s->cfg.preempt) return false;   // BinPack with evict: the single Select path
+    const double sc = s->h_sys_cache.as<double>()[row];
+    out->row = st == 0 ? (int32_t)row : -1;
+    out->n_scores = st == 0 ? 1u : 0u;
+    out->final_score = st == 0 ? sc : 0.0;
+    out->scores[0] = out->final_score;
+    out->nodes_evaluated = 1;
+    out->nodes_filtered = st == 1;
+    out->nodes_exhausted = st == 2;
+    out->new_offset = 0;
+    out->n_preempted = 0;
+    out->n_device_offers = 0;
+    out->reserved_cores[0] = out->reserved_cores[1] = out->reserved_cores[2] = out->reserved_cores[3] = 0;
+    y.served_row = out->row;
+    y.served++;
+    s->offer_row = out->row;
+    s->offers = 0xFFFFFFFFu;
+    s->metrics_valid = false;
+    elig_log_span(s, tgi, 0, 1);
+    *rc = PE_OK;
+    return true;
+}
+
 int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
     if (!s || !out) return PE_EINVAL;
     int rc = PE_OK;
+    if (s->cfg.stack_kind == PE_STACK_SYSTEM && !s->test_fallback_every && sys_serve(s, tgi, opts, out, &rc))
+        return rc;
     if (s->test_fallback_every && ++s->test_select_calls % s->test_fallback_every == 0) {
         // test hook: this Select is answered by the caller's Go chain (the
         // shim's PE_EUNSUPPORTED path); the engine state is the committed prefix
@@ -4477,6 +4651,10 @@ static int spec_copy(pe_stack* s, TgPlan& g, bool to_ckpt) {
 }
 
 static int spec_flush(pe_stack* s) {
+    if (!s->sys.pending.empty()) {
+        const int rc = sys_flush(s);
+        if (rc) return rc;
+    }
     pe_stack::Spec& sp = s->spec;
     if (!sp.active) return PE_OK;
     sp.active = false;
@@ -4539,6 +4717,11 @@ static void spec_drop(pe_stack* s) {
     s->spec.active = false;
     s->spec.pending = false;
     s->spec.grow = 1;
+    s->sys.active = false;   // a new evaluation context: queued commits are moot
+    s->sys.pending.clear();
+    s->sys.singles = 0;
+    s->sys.singles_tgi = PE_NONE;
+    s->sys.served_row = -1;
 }
 
 static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
@@ -4630,6 +4813,16 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
 
 int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
     if (!s) return PE_EINVAL;
+    if (s->sys.active && tgi == s->sys.tgi && row >= 0 && row == s->sys.served_row) {
+        // the served single-node Select's Plan.AppendAlloc: queued for HBM
+        s->sys.served_row = -1;
+        s->sys.pending.push_back((uint32_t)row);
+        s->sys_dirty[(uint32_t)row] = 1;
+        s->plan.emplace_back(s->tgs[tgi]->name, (uint32_t)row);
+        s->offer_row = -1;
+        return PE_OK;
+    }
+    if (s->sys.active && row >= 0 && (size_t)row < s->sys_dirty.size()) sys_touch(s, (uint32_t)row);
     pe_stack::Spec& sp = s->spec;
     if (sp.active && sp.pending && tgi == sp.tgi && row == spec_row(sp, sp.served - 1)) {
         // the predicted Plan.AppendAlloc: already in HBM
@@ -4654,6 +4847,7 @@ int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* pr
     if (n_preempted == 0) return pe_commit(s, tgi, row);
     int rc = spec_flush(s);
     if (rc) return rc;
+    if (s->sys.active && row >= 0 && (size_t)row < s->sys_dirty.size()) sys_touch(s, (uint32_t)row);
     rc = commit_preempt_impl(s, tgi, row, preempted, n_preempted);
     uint64_t cores[4];
     if (rc == PE_OK) core_record(s, *s->tgs[tgi], row, true, cores);
@@ -4673,6 +4867,7 @@ static int apply_stop_delta(pe_stack* s, const std::vector<uint32_t>& allocs, in
         f = sign > 0 ? 2 : 0;
         slots.push_back(slot);
         rows.push_back(a.row);
+        if (s->sys.active) sys_touch(s, a.row);   // its node's cached outcome is stale
         core_hold(s, ai, sign < 0);   // its reserved cores leave (rejoin) the node's used set
         invalidate_static(s);         // and its ports
     }
@@ -5370,6 +5565,7 @@ extern "C" int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap) {
 
 int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     const int rc = system_place_impl(s, tgi, out_score, out_status, placed);
+    if (s) s->sys.active = false;   // rows committed on the device: the per-row cache is stale
     // one single-node Select per row of the list (scheduler_system.go:290-422)
     if (rc == PE_OK) elig_log_span(s, tgi, 0, (uint32_t)s->visit.size());
     return rc;
@@ -5456,7 +5652,10 @@ int pe_put_eligibility(pe_stack* s, const pe_class_feas* in, uint32_t n) {
             rt[c] = v;
         }
     }
-    if (changed) invalidate_tables(s);
+    if (changed) {
+        invalidate_tables(s);
+        s->sys.active = false;   // class verdicts changed under the per-row cache
+    }
     return PE_OK;
 }
 
@@ -5489,5 +5688,17 @@ int pe_set_cursor(pe_stack* s, uint32_t tgi, uint32_t offset, uint32_t limit) {
         }
     }
     invalidate_tables(s);
+    return PE_OK;
+}
+
+int pe_flush(pe_stack* s) {
+    if (!s) return PE_EINVAL;
+    return spec_flush(s);
+}
+
+int pe_system_spec_stats(const pe_stack* s, uint64_t* out2) {
+    if (!s || !out2) return PE_EINVAL;
+    out2[0] = s->sys.passes;
+    out2[1] = s->sys.served;
     return PE_OK;
 }

@@ -1,0 +1,106 @@
+"""The unchanged SystemScheduler caller through the C ABI.
+
+SystemScheduler.computePlacements (scheduler_system.go:283-425) calls, for
+every node it places on, SetNodes([node]) then Select and appends a placed
+option to the plan. tools/dropin.cpp runs exactly that loop in C against the
+engine and against the oracle. From a task group's third single-node Select
+the engine answers from a per-row cache filled by one k_system pass (no
+commit) and queues the commits (pe_flush / any later device call applies
+them). Results must equal the oracle's Select by Select, and the pe_system_place
+batch path's (VERDICT r02 missing 5).
+"""
+import numpy as np
+import pytest
+
+from nomad_amd import synth
+from nomad_amd.structs import Allocation, SchedulerConfig
+from oracle.oracle import OracleSystemStack
+from tools import dropin
+
+pytestmark = pytest.mark.gpu
+
+
+def engine_system(**kw):
+    from nomad_amd.stack import SystemStack
+    return SystemStack(**kw)
+
+
+def _stacks(nodes, allocs, job, cfg=None):
+    e, o = engine_system(config=cfg), OracleSystemStack(config=cfg)
+    for st in (e, o):
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+    return e, o
+
+
+def _stats(e):
+    import ctypes as C
+    out = (C.c_uint64 * 2)()
+    e._check(e._lib.pe_system_spec_stats(C.c_void_p(e._h), out))
+    return int(out[0]), int(out[1])
+
+
+def _same(a, b):
+    sa, ca, pa, _ = a
+    sb, cb, pb, _ = b
+    assert pa == pb
+    assert np.array_equal(sa, sb)
+    both = sa == 0
+    assert np.array_equal(ca[both], cb[both])   # bit-exact FinalScores
+
+
+@pytest.mark.parametrize("n", [20000, 100000])
+def test_system_caller_protocol_matches_oracle(n):
+    nodes, allocs = synth.cluster_c4(n, seed=11)
+    job = synth.mock_system_job()
+    e, o = _stacks(nodes, allocs, job)
+    rows = np.arange(n, dtype=np.uint32)
+    re_ = dropin.system_loop(e, 0, rows)
+    ro = dropin.system_loop(o, 0, rows)
+    _same(re_, ro)
+    passes, served = _stats(e)
+    assert passes == 1 and served == n - 2
+    assert re_[2] > 0.8 * n
+    # the batch path on a fresh evaluation gives the same outcomes
+    e.ResetPlan()
+    e.SetJob(job)
+    e.SetNodes(rows)
+    sc, st, placed = e.SystemPlace(0)
+    assert placed == re_[2]
+    assert np.array_equal(st, re_[0])
+    assert np.array_equal(sc[st == 0], re_[1][st == 0])
+    # EvalEligibility after the per-node Selects
+    e2, o2 = _stacks(nodes[:3000], [a for a in allocs if a.node_id in {x.id for x in nodes[:3000]}], job)
+    r3 = np.arange(3000, dtype=np.uint32)
+    dropin.system_loop(e2, 0, r3)
+    dropin.system_loop(o2, 0, r3)
+    ee, oe = e2.Eligibility(), o2.Eligibility()
+    assert ee["job"] == oe["job"] and ee["tgs"] == oe["tgs"]
+
+
+def test_system_revisits_stops_and_preemption():
+    """Rows touched after the cache pass (a second pass over placed rows, plan
+    stops, preempting placements) take the single Select path."""
+    n = 8000
+    nodes, allocs = synth.cluster_c4(n, seed=5)
+    job = synth.mock_system_job()
+    job.priority = 90
+    rng = np.random.Generator(np.random.PCG64(3))
+    for k in rng.choice(n, size=600, replace=False):   # low-priority fillers: eviction candidates
+        nd = nodes[int(k)]
+        allocs.append(Allocation(node_id=nd.id, job_id="low-%d" % (k % 7), task_group="tg",
+                                 cpu_shares=nd.cpu_shares - 300, memory_mb=512, disk_mb=100, priority=20))
+    cfg = SchedulerConfig(preempt_system=True)
+    e, o = _stacks(nodes, allocs, job, cfg)
+    order = rng.permutation(n).astype(np.uint32)
+    _same(dropin.system_loop(e, 0, order[:5000]), dropin.system_loop(o, 0, order[:5000]))
+    # stop some snapshot allocs of nodes not visited yet, then the rest + a revisit
+    stop = [i for i, a in enumerate(allocs) if a.job_id.startswith("low")][:40]
+    for st in (e, o):
+        st.StopAllocs(stop)
+    tail = np.concatenate([order[5000:], order[:300]])
+    _same(dropin.system_loop(e, 0, tail), dropin.system_loop(o, 0, tail))
+    passes, served = _stats(e)
+    assert passes == 1 and served > 4000
+    ee, oe = e.Eligibility(), o.Eligibility()
+    assert ee["job"] == oe["job"] and ee["tgs"] == oe["tgs"]

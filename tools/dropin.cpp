@@ -122,4 +122,45 @@ int dropin_evals(const dropin_api* api, void* h, const pe_strtab* strs, const pe
     return rc;
 }
 
+// SystemScheduler.computePlacements (scheduler_system.go:283-425) for one task
+// group: for every node of `rows`, SetNodes([node]) then Select with empty
+// options (BinPack evicts inside the Select when preemption is enabled); an
+// option is appended to the plan (Commit, with its preempted allocs). Per node
+// out: status 0 placed / 1 filtered / 2 exhausted, score (FinalScore or NaN).
+// `flush` (may be null) is called once at the end, inside the timed region:
+// the entry point that forces queued device work (e.g. the next call that
+// reads the device state). Returns 0 or the first failing status.
+int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* rows, uint32_t n, uint8_t* status,
+                  double* score, uint32_t* placed, int (*flush)(void*), double* seconds) {
+    pe_select_options none;
+    std::memset(&none, 0, sizeof(none));
+    pe_ranked_node opt;
+    uint32_t p = 0;
+    int rc = 0;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t limit;
+        rc = api->set_nodes(h, rows + i, 1, &limit);
+        if (rc) break;
+        rc = api->select(h, tg, &none, &opt);
+        if (rc) break;
+        if (opt.row < 0) {
+            status[i] = opt.nodes_filtered > 0 ? 1 : 2;
+            score[i] = __builtin_nan("");
+            continue;
+        }
+        rc = opt.n_preempted ? api->commit_preempt(h, tg, opt.row, opt.preempted, opt.n_preempted)
+                             : api->commit(h, tg, opt.row);
+        if (rc) break;
+        status[i] = 0;
+        score[i] = opt.final_score;
+        p++;
+    }
+    if (!rc && flush) rc = flush(h);
+    *seconds = std::chrono::duration<double>(clk::now() - t0).count();
+    *placed = p;
+    return rc;
+}
+
 }  // extern "C"

@@ -35,6 +35,9 @@ def load():
                                      C.POINTER(abi.pe_job), abi.u32p, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.c_int, C.c_uint32, C.c_double, abi.i32p,
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        lib.dropin_system.restype = C.c_int
+        lib.dropin_system.argtypes = [C.POINTER(dropin_api), C.c_void_p, C.c_uint32, abi.u32p, C.c_uint32,
+                                      abi.u8p, abi.f64p, abi.u32p, C.c_void_p, C.POINTER(C.c_double)]
         _lib = lib
     return _lib
 
@@ -87,3 +90,23 @@ def phase_seconds(reset=True):
     out = (C.c_double * 5)()
     load().dropin_phase_seconds(out, int(reset))
     return dict(zip(PHASES, list(out)))
+
+
+def system_loop(stack, tg, rows, flush=True):
+    """SystemScheduler.computePlacements' per-node loop through the C harness
+    (SetNodes([node]) + Select + Commit for every node of `rows`) on a
+    SystemStack that holds the snapshot and the job. Returns (status, score,
+    placed, seconds); `flush` times pe_flush (queued commits into HBM) too."""
+    lib = load()
+    r = np.ascontiguousarray(np.asarray(rows, dtype=np.uint32))
+    st = np.zeros(max(1, len(r)), dtype=np.uint8)
+    sc = np.zeros(max(1, len(r)), dtype=np.float64)
+    placed, secs = C.c_uint32(0), C.c_double(0.0)
+    fl = C.cast(getattr(stack._lib, stack._p + "flush"), C.c_void_p).value \
+        if flush and hasattr(stack._lib, stack._p + "flush") else None
+    api = _api(stack)
+    rc = lib.dropin_system(C.byref(api), stack._h, tg, r.ctypes.data_as(abi.u32p), len(r),
+                           st.ctypes.data_as(abi.u8p), sc.ctypes.data_as(abi.f64p), C.byref(placed), fl,
+                           C.byref(secs))
+    stack._check(rc)
+    return st[:len(r)], sc[:len(r)], placed.value, secs.value
