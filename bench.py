@@ -72,7 +72,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--sweep-nodes", type=int, default=1 << 24,
                    help="nodes of the scoring-sweep roofline measurement (0 = skip)")
-    p.add_argument("--sections", default="c2_100k,c2_batch,c2_workers,c3,c4,c5,c3_sharded,plan_apply,ingest",
+    p.add_argument("--sections", default="c1,c2_100k,c2_batch,c2_workers,c3,c4,c4_drop_in,c5,c3_sharded,plan_apply,ingest",
                    help="comma list of extra config sections (empty = none)")
     return p.parse_args()
 
@@ -350,6 +350,50 @@ def section_c4(device, rank, world, pg, cpu_s):
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port",
                                "sample": "system placements over a %d-node C4 cluster in %.2f s" % (ns, dt)}
+    return out
+
+
+def section_c4_drop_in(device, cpu_s):
+    """C4 through the unchanged SystemScheduler caller: for every node of the
+    list SetNodes([node]) + Select + Commit (scheduler_system.go:289-302) from a
+    C loop over the C ABI (tools/dropin.cpp), 100k nodes. The timed region
+    includes the per-row cache pass (k_system over the snapshot) and pe_flush
+    (the queued commits into HBM)."""
+    from nomad_amd import synth, synth_columnar
+    from nomad_amd.stack import SystemStack
+    from tools import dropin
+    import ctypes as C
+    n = 100000
+    cs = synth_columnar.ColumnarState(n, seed=11, kind="c4", prefill=0.05)
+    job = synth.mock_system_job()
+    rows = np.random.Generator(np.random.PCG64(5)).permutation(n).astype(np.uint32)
+    st = SystemStack(device=device)
+    st.SetStateColumnar(cs)
+    times, placed = [], 0
+    for i in range(4):
+        st.ResetPlan()
+        st.SetJob(job)
+        _, _, placed, secs = dropin.system_loop(st, 0, rows)
+        times.append(secs)
+    stats = (C.c_uint64 * 2)()
+    st._lib.pe_system_spec_stats(C.c_void_p(st._h), stats)
+    kms = st.last_kernel_ms()
+    st.close()
+    wall = float(np.median(times[1:]))
+    out = {"workload": "C4 caller protocol: mock.SystemJob on %d nodes, SetNodes([node]) + Select + Commit per "
+                       "node from a C loop (one evaluation)" % n,
+           "placed": int(placed), "nodes_per_s": n / wall, "wall_ms": wall * 1e3, "cache_kernel_ms": kms,
+           "cache_passes": int(stats[0]), "served_selects": int(stats[1])}
+    if cpu_s > 0:
+        from oracle.oracle import OracleSystemStack
+        ns = 20000
+        small = synth_columnar.ColumnarState(ns, seed=11, kind="c4", prefill=0.05)
+        o = OracleSystemStack()
+        o.SetStateColumnar(small)
+        o.SetJob(job)
+        _, _, _, dt = dropin.system_loop(o, 0, np.arange(ns, dtype=np.uint32))
+        out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port",
+                               "sample": "the same C caller loop over a %d-node C4 cluster in %.3f s" % (ns, dt)}
     return out
 
 
@@ -674,6 +718,41 @@ def section_c2_batch(device, nodes, allocs, job, count, evals, steps=10, warmup=
                          "node_evals_per_launch": evaluated}}
 
 
+def section_c1(device, cpu_s, evals=2000):
+    """C1: the scheduler.Harness shape, mock.Job() count=10 on 100
+    mock.Node() nodes, limit 7, through the C caller loop (ResetPlan, SetJob,
+    SetNodes, 10 x (Select, Commit)) per evaluation."""
+    from nomad_amd import synth
+    from nomad_amd.stack import GenericStack
+    from tools import dropin
+    nodes, allocs = synth.cluster_c1(100, seed=42)
+    job = synth.mock_job(count=10)
+    orders = np.stack([synth.shuffle(len(nodes), 1 + e) for e in range(16)])
+    st = GenericStack(device=device)
+    st.SetState(nodes, allocs)
+    caller = dropin.prepare(st, job)
+    caller(orders, 10, n_evals=50)
+    placed, ne, _, secs, _ = caller(orders, 10, n_evals=evals)
+    st.ResetPlan()
+    st.SetJob(job)
+    st.SetNodes(orders[0])
+    _, _, p1, recs = st.PlaceArrays(0, 10)
+    node_evals = float(recs["nodes_evaluated"][:p1].sum(dtype=np.uint64))
+    st.close()
+    out = {"workload": "C1: mock.Job() count=10 on 100 mock.Node() nodes (limit 7), one evaluation per step",
+           "placements_per_s": placed / secs, "ms_per_eval": secs / ne * 1e3, "evals": ne,
+           "nodes_scored_per_s": node_evals * ne / secs, "node_evals_per_eval": node_evals}
+    if cpu_s > 0:
+        from oracle.oracle import OracleGenericStack
+        o = OracleGenericStack()
+        o.SetState(nodes, allocs)
+        op, oe, _, osecs, _ = dropin.run(o, job, orders, 10, n_evals=1 << 30, max_seconds=min(cpu_s, 3.0))
+        out["cpu_baseline"] = {"value": op / osecs, "unit": "placements/s", "cores": 1, "kind": "port",
+                               "sample": "%d evaluations x count=10 through the same C caller loop, 1 thread"
+                                         % oe}
+    return out
+
+
 def section_c2_100k(device, cpu_s, count=1000, n=100000, evals=20):
     """The metric's 100k-node case: the C2 drop-in protocol (ResetPlan, SetJob,
     SetNodes, count x (Select, Commit) from the C caller loop) on a 100k-node
@@ -794,6 +873,7 @@ def main():
     phases = dropin.phase_seconds(reset=True)
     elapsed = reduce(pg, elapsed, lambda d: d.ReduceOp.MAX)
     total_placed = reduce(pg, placed, lambda d: d.ReduceOp.SUM)
+    total_evals = reduce(pg, evals, lambda d: d.ReduceOp.SUM)
 
     # the dominant kernel of a step: the speculative count loop (k_base + k_chain),
     # timed with HIP events on the engine's stream by the same call path
@@ -816,6 +896,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1000.0,
+            "nodes_scored_per_s": node_evals * total_evals / elapsed,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -849,13 +930,23 @@ def main():
             from oracle.oracle import OracleGenericStack
             o = OracleGenericStack()
             o.SetState(nodes, allocs)
-            op, oe, _, osecs, _ = dropin.run(o, job, orders, args.count, n_evals=1 << 30,
-                                             max_seconds=args.cpu_seconds)
-            line["cpu_baseline"] = {"value": op / osecs, "unit": "placements/s", "cores": 1, "kind": "port",
-                                    "sample": "%d evaluations x count=%d on the %d-node cluster in %.1f s through the "
-                                              "same C caller loop, 1 thread (oracle/liboracle.so: C++ restatement "
-                                              "of the reference iterator chain; Go toolchain unavailable)"
-                                              % (oe, args.count, len(nodes), osecs)}
+            # three runs of a third of the budget each: the median is the
+            # reported value, the fastest bounds the speedup conservatively
+            runs = []
+            for _ in range(3):
+                op, oe, _, osecs, _ = dropin.run(o, job, orders, args.count, n_evals=1 << 30,
+                                                 max_seconds=args.cpu_seconds / 3.0)
+                runs.append((op / osecs, oe, osecs))
+            rates = sorted(r[0] for r in runs)
+            oe_all, secs_all = sum(r[1] for r in runs), sum(r[2] for r in runs)
+            line["cpu_baseline"] = {"value": rates[1], "unit": "placements/s", "cores": 1, "kind": "port",
+                                    "runs": [r[0] for r in runs], "fastest": rates[-1],
+                                    "sample": "median of 3 runs, %d evaluations x count=%d on the %d-node cluster in "
+                                              "%.1f s in all, through the same C caller loop, 1 thread "
+                                              "(oracle/liboracle.so: C++ restatement of the reference iterator "
+                                              "chain; Go toolchain unavailable)"
+                                              % (oe_all, args.count, len(nodes), secs_all)}
+            line["speedup_vs_fastest_cpu_run"] = value / rates[-1]
             _, multi = cpu_baseline(nodes, allocs, job, args.cpu_seconds)
             line["cpu_baseline_multicore"] = multi
     sections = [x for x in args.sections.split(",") if x]
@@ -878,6 +969,12 @@ def main():
                     extra[sec] = section_c2_workers(local, nodes, allocs, job, args.count, args.workers)
             elif sec == "c4":
                 extra[sec] = section_c4(local, rank, world, pg, cpu_s)
+            elif sec == "c4_drop_in":
+                if rank == 0:
+                    extra[sec] = section_c4_drop_in(local, cpu_s)
+            elif sec == "c1":
+                if rank == 0:
+                    extra[sec] = section_c1(local, cpu_s)
             elif sec == "c3_sharded":
                 extra[sec] = section_c3_sharded(local, rank, world, pg)
             elif sec == "plan_apply":

@@ -36,6 +36,7 @@ extern "C" {
 #define PE_MAX_SCORES 8
 #define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried per RankedNode */
 #define PE_MAX_DEVICE_REQ 4 /* device requests of a task group on the device path */
+#define PE_MAX_DEVICES 8    /* GPUs one handle drives (pe_config.device_ids) */
 
 /* ---- status codes ------------------------------------------------------ */
 #define PE_OK 0
@@ -226,7 +227,17 @@ typedef struct pe_config {
                                  GenericStack: PreemptionConfig.{Service,Batch}SchedulerEnabled:
                                  pe_place retries a nil Select with Preempt=true
                                  (selectNextOption, generic_sched.go:773-792) */
-    int32_t device;           /* HIP device ordinal */
+    int32_t device;           /* HIP device ordinal (device_count <= 1) */
+    /* One handle over several GPUs of this process (SURVEY.md §8b "device
+     * count/ids"): device_ids[0] holds the handle's own state, the others
+     * replicas of it; full-pass count loops (pe_place of task groups with
+     * affinities / spreads) and pe_system_place split the rows over all of
+     * them, exchanging per-placement records with ncclAllGather over
+     * communicators from ncclCommInitAll. Ids that all name one GPU run the
+     * same split with device copies instead of RCCL (loopback, for tests).
+     * 0 or 1: the single `device`. */
+    uint32_t device_count;
+    int32_t device_ids[PE_MAX_DEVICES];
 } pe_config;
 
 typedef struct pe_select_options {              /* SelectOptions, stack.go:34-39 */
@@ -326,6 +337,8 @@ int pe_flush(pe_stack* s);
 /* SystemStack fast path counters: out[0] k_system passes over the snapshot
  * that filled the per-row cache, out[1] single-node Selects answered from it. */
 int pe_system_spec_stats(const pe_stack* s, uint64_t* out2);
+/* GPUs this handle drives (pe_config.device_count; 1 for a single device). */
+uint32_t pe_device_count(const pe_stack* s);
 /* Multi-GPU: one engine handle per GPU and process, joined by
  * an RCCL communicator (ncclGetUniqueId on one rank, the 128 bytes shared by
  * the caller, ncclCommInitRank on every rank). */

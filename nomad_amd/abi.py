@@ -154,7 +154,7 @@ class pe_job(C.Structure):
 class pe_config(C.Structure):
     _fields_ = [("stack_kind", C.c_uint32), ("batch", C.c_uint32), ("algorithm", C.c_uint32),
                 ("memory_oversubscription", C.c_uint32), ("preempt", C.c_uint32),
-                ("device", C.c_int32)]
+                ("device", C.c_int32), ("device_count", C.c_uint32), ("device_ids", C.c_int32 * 8)]
 
 
 class pe_select_options(C.Structure):
@@ -221,7 +221,7 @@ ENGINE_SYMBOLS = [
     "pe_set_metrics", "pe_last_metrics", "pe_update_allocs", "pe_speculation_stats",
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
-    "pe_set_cursor", "pe_flush", "pe_system_spec_stats",
+    "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count",
 ]
 
 

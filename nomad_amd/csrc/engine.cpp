@@ -556,6 +556,22 @@ struct pe_stack {
     // engines, one GPU each; the sharded count loop gathers per-rank records
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+
+    // One handle over several devices (pe_config.device_count > 1): `kids`
+    // hold replicas of the snapshot, job and plan on the other devices. The
+    // per-evaluation calls (state, job) are forwarded as they come; the plan
+    // mutations (commits, preemptions, stops) are logged and replayed into the
+    // kids before a sharded call, which also copies the cursor, limit, spread
+    // bookkeeping and class memo. Sharded full-pass count loops exchange their
+    // records with ncclAllGather over `group_comms` (ncclCommInitAll), or with
+    // device copies when every id names one GPU (loopback). A root-only call
+    // the log cannot replay (a batch system placement with evictions) marks
+    // the kids stale until the next evaluation context.
+    struct ReplayOp { uint8_t kind; uint32_t tgi; int32_t row; std::vector<uint32_t> a; };
+    std::vector<pe_stack*> kids;
+    std::vector<ncclComm_t> group_comms;
+    bool loopback = false, kids_valid = true;
+    std::vector<ReplayOp> replay;
     DevMem d_gather;
     pe::SweepArgs h_full_args;   // k_fullpass_lds arguments (read through d_full_args)
     DevMem d_full_args;
@@ -2956,10 +2972,16 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
         g_error = "no HIP device available: the placement engine runs only on the GPU";
         return nullptr;
     }
-    if (cfg->device < 0 || cfg->device >= ndev) { g_error = "device ordinal out of range"; return nullptr; }
+    if (cfg->device_count > PE_MAX_DEVICES) { g_error = "device_count above PE_MAX_DEVICES"; return nullptr; }
+    const int root_dev = cfg->device_count > 1 ? cfg->device_ids[0] : cfg->device;
+    if (root_dev < 0 || root_dev >= ndev) { g_error = "device ordinal out of range"; return nullptr; }
+    for (uint32_t k = 1; k < cfg->device_count; k++)
+        if (cfg->device_ids[k] < 0 || cfg->device_ids[k] >= ndev) { g_error = "device ordinal out of range"; return nullptr; }
     auto* s = new pe_stack();
     s->cfg = *cfg;
-    s->device = cfg->device;
+    s->cfg.device = root_dev;
+    s->cfg.device_count = 0;
+    s->device = root_dev;
     if (hipSetDevice(s->device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
         hipEventCreate(&s->ev2) != hipSuccess) {
@@ -2981,11 +3003,40 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     if (const char* e = std::getenv("PE_SPIN_WAIT")) s->spin_wait = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_API_PROF")) s->api_prof = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_TEST_FALLBACK_EVERY")) s->test_fallback_every = std::strtoull(e, nullptr, 10);
+    if (cfg->device_count > 1) {
+        // replicas on the other devices, and the communicators of the group
+        bool same = true;
+        for (uint32_t k = 1; k < cfg->device_count; k++) {
+            pe_config kc = s->cfg;
+            kc.device = cfg->device_ids[k];
+            pe_stack* kid = pe_stack_create(&kc);
+            if (!kid) { pe_stack_destroy(s); return nullptr; }
+            kid->test_fallback_every = 0;
+            s->kids.push_back(kid);
+            same = same && cfg->device_ids[k] == root_dev;
+        }
+        s->loopback = same;
+        if (!same) {
+            std::vector<int> devs(cfg->device_ids, cfg->device_ids + cfg->device_count);
+            s->group_comms.assign(devs.size(), nullptr);
+            const ncclResult_t r = ncclCommInitAll(s->group_comms.data(), (int)devs.size(), devs.data());
+            if (r != ncclSuccess) {
+                g_error = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+                s->group_comms.clear();
+                pe_stack_destroy(s);
+                return nullptr;
+            }
+        }
+        (void)hipSetDevice(s->device);
+    }
     return s;
 }
 
 void pe_stack_destroy(pe_stack* s) {
     if (!s) return;
+    for (pe_stack* k : s->kids) pe_stack_destroy(k);
+    for (ncclComm_t c : s->group_comms)
+        if (c) (void)ncclCommDestroy(c);
     if (s->api_prof)
         for (auto& kv : s->api_acc)
             std::fprintf(stderr, "api %-28s %10.1f us total %8llu calls %8.2f us/call\n", kv.first.c_str(),
@@ -3150,7 +3201,7 @@ static void elig_visit_list(pe_stack* s, uint32_t tgi, const std::vector<uint32_
     elig_walk(s, tgi, list, 0, len, ev);
 }
 
-int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
+static int set_state_one(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
     if (!s || !strs || !nodes) return PE_EINVAL;
     spec_drop(s);
     s->node_update.clear();   // a new evaluation context: no plan stops
@@ -3180,7 +3231,7 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
     return PE_OK;
 }
 
-int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index) {
+static int update_allocs_one(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index) {
     if (!s || !allocs) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
@@ -3218,7 +3269,7 @@ int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* a
     return PE_OK;
 }
 
-int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const uint32_t* index) {
+static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const uint32_t* index) {
     if (!s || !nodes) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
@@ -3258,7 +3309,7 @@ int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nod
     return rc;
 }
 
-int pe_reset_plan(pe_stack* s) {
+static int reset_plan_one(pe_stack* s) {
     if (!s) return PE_EINVAL;
     ApiScope prof_(s, "reset_plan");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
@@ -3297,7 +3348,7 @@ int pe_reset_plan(pe_stack* s) {
     return PE_OK;
 }
 
-int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
+static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     if (!s || !j) return PE_EINVAL;
     ApiScope prof_(s, "set_job");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
@@ -4754,6 +4805,7 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     uint32_t placed = 0;
     s->emit_sink = &sp.crecs;
     s->emit_sunk = false;
+    const uint32_t off0 = s->offset;
     s->elig_mute = true;   // records are logged when served
     rc = place_impl(s, tgi, count, sp.recs.data(), &placed, false);
     s->elig_mute = false;
@@ -4778,12 +4830,13 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     s->spec_stats[0]++;
     s->spec_stats[3] += sp.n_rec;
     s->offer_row = -1;
+    s->offset = off0;   // the run left the cursor at its end: serving advances it record by record
     if (!spec_serve(s, tgi, nullptr, out)) return s->fail(PE_ESTATE, "speculative loop produced no record");
     s->spec_stats[1]--;   // the first record is the Select that started the run
     return PE_OK;
 }
 
-int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+static int place_one(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
     if (!s) return PE_EINVAL;
     int rc = spec_flush(s);
     if (rc) return rc;
@@ -4811,7 +4864,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     return rc;
 }
 
-int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
+static int commit_one(pe_stack* s, uint32_t tgi, int32_t row) {
     if (!s) return PE_EINVAL;
     if (s->sys.active && tgi == s->sys.tgi && row >= 0 && row == s->sys.served_row) {
         // the served single-node Select's Plan.AppendAlloc: queued for HBM
@@ -4842,9 +4895,9 @@ int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
     return rc;
 }
 
-int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
+static int commit_preempt_one(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
     if (!s) return PE_EINVAL;
-    if (n_preempted == 0) return pe_commit(s, tgi, row);
+    if (n_preempted == 0) return commit_one(s, tgi, row);
     int rc = spec_flush(s);
     if (rc) return rc;
     if (s->sys.active && row >= 0 && (size_t)row < s->sys_dirty.size()) sys_touch(s, (uint32_t)row);
@@ -4886,7 +4939,7 @@ static int apply_stop_delta(pe_stack* s, const std::vector<uint32_t>& allocs, in
     return PE_OK;
 }
 
-int pe_plan_stop(pe_stack* s, const uint32_t* allocs, uint32_t n) {
+static int plan_stop_one(pe_stack* s, const uint32_t* allocs, uint32_t n) {
     if (!s || (!allocs && n)) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     for (uint32_t i = 0; i < n; i++)
@@ -4905,7 +4958,7 @@ int pe_plan_stop(pe_stack* s, const uint32_t* allocs, uint32_t n) {
     return apply_stop_delta(s, fresh, +1);
 }
 
-int pe_plan_pop_update(pe_stack* s, uint32_t alloc) {
+static int plan_pop_update_one(pe_stack* s, uint32_t alloc) {
     if (!s) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     if (alloc >= s->allocs.size()) return s->fail(PE_EINVAL, "alloc index out of range");
@@ -5563,7 +5616,7 @@ extern "C" int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap) {
 
 // ---- wrappers that log the chain's visits for EvalEligibility -----------------
 
-int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
+static int system_place_one(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     const int rc = system_place_impl(s, tgi, out_score, out_status, placed);
     if (s) s->sys.active = false;   // rows committed on the device: the per-row cache is stale
     // one single-node Select per row of the list (scheduler_system.go:290-422)
@@ -5702,3 +5755,394 @@ int pe_system_spec_stats(const pe_stack* s, uint64_t* out2) {
     out2[1] = s->sys.served;
     return PE_OK;
 }
+
+// ---- one handle over several devices (pe_config.device_count) ---------------
+
+static void kid_log(pe_stack* s, uint8_t kind, uint32_t tgi, int32_t row, const uint32_t* a, uint32_t n) {
+    if (s->kids.empty() || !s->kids_valid) return;
+    s->replay.push_back(pe_stack::ReplayOp{kind, tgi, row, std::vector<uint32_t>(a, a + n)});
+}
+
+// The kids take the plan mutations logged since the last sync, in order, and
+// the root's iterator state: they then hold exactly the root's plan.
+static int kids_sync(pe_stack* s) {
+    if (s->kids.empty()) return PE_OK;
+    if (!s->kids_valid) return PE_EUNSUPPORTED;
+    for (pe_stack* k : s->kids) {
+        int rc = PE_OK;
+        if (k->visit != s->visit) rc = pe_set_nodes(k, s->visit.data(), (uint32_t)s->visit.size(), nullptr);
+        for (size_t i = 0; i < s->replay.size() && rc == PE_OK; i++) {
+            const pe_stack::ReplayOp& op = s->replay[i];
+            switch (op.kind) {
+                case 0: rc = commit_one(k, op.tgi, op.row); break;
+                case 1: rc = commit_preempt_one(k, op.tgi, op.row, op.a.data(), (uint32_t)op.a.size()); break;
+                case 2: rc = plan_stop_one(k, op.a.data(), (uint32_t)op.a.size()); break;
+                default: rc = plan_pop_update_one(k, op.a[0]); break;
+            }
+        }
+        if (rc == PE_OK) rc = spec_flush(k);
+        if (rc) {
+            s->kids_valid = false;
+            s->replay.clear();
+            return PE_EUNSUPPORTED;
+        }
+        k->offset = s->offset;
+        k->limit = s->limit;
+        k->tg_memo = s->tg_memo;
+        k->job_memo = s->job_memo;
+        if (k->spread_info_done != s->spread_info_done || k->sum_spread_weights != s->sum_spread_weights) {
+            k->spread_info_done = s->spread_info_done;
+            k->sum_spread_weights = s->sum_spread_weights;
+            for (auto& g : k->tgs) g->psets_built = false;
+        }
+        invalidate_tables(k);
+    }
+    s->replay.clear();
+    return PE_OK;
+}
+
+// After a call that starts a new evaluation context on every replica.
+static void kids_fresh(pe_stack* s, bool all_ok) {
+    s->replay.clear();
+    s->kids_valid = all_ok;
+}
+
+// The full-pass count loop split over the handle's devices: rows
+// [n k / N, n (k+1) / N) on replica k, per placement one k_sweep per replica,
+// the records exchanged (ncclAllGather over the group's communicators, or
+// device copies in loopback), then every replica's k_sweep_step merges all
+// N x blocks records and commits the same winner.
+static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+    std::vector<pe_stack*> st{s};
+    st.insert(st.end(), s->kids.begin(), s->kids.end());
+    const uint32_t N = (uint32_t)st.size();
+    const uint32_t n = (uint32_t)s->visit.size(), nn = (uint32_t)s->nodes.size();
+    std::vector<pe::SweepArgs> A(N), A2(N);
+    const uint32_t rows_max = (nn + N - 1) / N;
+    const uint32_t blocks = std::max<uint32_t>(
+        1, std::min<uint32_t>((rows_max + 255) / 256, (uint32_t)s->n_cu * (uint32_t)s->sweep_per_cu_aux));
+    const size_t slice = sizeof(pe::SweepRec) * blocks;
+    auto strm = [&](uint32_t k) { return s->loopback ? s->stream : st[k]->stream; };
+    for (uint32_t k = 0; k < N; k++) {
+        pe_stack* x = st[k];
+        HIP_TRY(s, hipSetDevice(x->device));
+        int rc = prepare_tg(x, tgi, x->visit, x->offset);
+        if (rc) return k ? s->fail(rc, "replica: " + x->err) : rc;
+        x->limit = 0x7FFFFFFF;
+        uint32_t b_unused = 0;
+        rc = sweep_setup(x, *x->tgs[tgi], nullptr, (uint32_t)((uint64_t)nn * k / N),
+                         (uint32_t)((uint64_t)nn * (k + 1) / N), &A[k], &b_unused);
+        if (rc) return k ? s->fail(rc, "replica: " + x->err) : rc;
+        HIP_TRY(s, x->d_gather.ensure(slice * N));
+        A[k].recs = reinterpret_cast<pe::SweepRec*>(static_cast<char*>(x->d_gather.p) + slice * k);
+        A2[k] = A[k];
+        A2[k].recs = x->d_gather.as<pe::SweepRec>();
+        HIP_TRY(s, upload_visit(x, x->visit));
+        HIP_TRY(s, x->d_loop_out.ensure(sizeof(pe_ranked_node) * (size_t)(count + 1)));
+        HIP_TRY(s, x->d_loop_state.ensure(8 * sizeof(uint32_t)));
+        HIP_TRY(s, hipStreamSynchronize(x->stream));   // uploads on the replica's own stream
+        HIP_TRY(s, hipMemsetAsync(x->d_loop_state.p, 0, 8 * sizeof(uint32_t), strm(k)));
+        if (A[k].spread_tab) HIP_TRY(s, pe_launch_spread_table(&A[k].tg, x->d_spread_tab.as<double>(), strm(k)));
+    }
+    uint32_t h_state[5] = {0, 0, 0, 0, 0};
+    const uint32_t chunk = 64;
+    double x_us = 0;
+    uint32_t x_n = 0;
+    if (!s->ev_x0) HIP_TRY(s, hipEventCreate(&s->ev_x0));
+    if (!s->ev_x1) HIP_TRY(s, hipEventCreate(&s->ev_x1));
+    HIP_TRY(s, hipSetDevice(s->device));
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    for (uint32_t p0 = 0; p0 < count && !h_state[0]; p0 += chunk) {
+        const uint32_t m = std::min(chunk, count - p0);
+        for (uint32_t j = 0; j < m; j++) {
+            for (uint32_t k = 0; k < N; k++) {
+                HIP_TRY(s, hipSetDevice(st[k]->device));
+                HIP_TRY(s, pe_launch_sweep_only(&A[k], blocks, strm(k)));
+            }
+            HIP_TRY(s, hipSetDevice(s->device));
+            if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x0, s->stream));
+            if (s->loopback) {
+                // every replica's slice into every other replica's gather buffer
+                for (uint32_t k = 0; k < N; k++)
+                    for (uint32_t e = 0; e < N; e++)
+                        if (e != k)
+                            HIP_TRY(s, hipMemcpyAsync(static_cast<char*>(st[k]->d_gather.p) + slice * e,
+                                                      static_cast<char*>(st[e]->d_gather.p) + slice * e, slice,
+                                                      hipMemcpyDeviceToDevice, s->stream));
+            } else {
+                ncclResult_t r = ncclGroupStart();
+                for (uint32_t k = 0; k < N && r == ncclSuccess; k++)
+                    r = ncclAllGather(A[k].recs, st[k]->d_gather.p, slice, ncclUint8, s->group_comms[k], st[k]->stream);
+                const ncclResult_t r2 = ncclGroupEnd();
+                if (r != ncclSuccess || r2 != ncclSuccess)
+                    return s->fail(PE_EHIP, std::string("ncclAllGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+            }
+            if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x1, s->stream));
+            for (uint32_t k = 0; k < N; k++) {
+                HIP_TRY(s, hipSetDevice(st[k]->device));
+                HIP_TRY(s, pe_launch_step_only(&A2[k], blocks * N, st[k]->d_visit.as<uint32_t>(), n, st[k]->offset,
+                                               st[k]->d_loop_out.as<pe_ranked_node>(),
+                                               st[k]->d_loop_state.as<uint32_t>(), strm(k)));
+            }
+        }
+        HIP_TRY(s, hipSetDevice(s->device));
+        HIP_TRY(s, hipMemcpyAsync(h_state, s->d_loop_state.p, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        float xms = 0;
+        if (m && hipEventElapsedTime(&xms, s->ev_x0, s->ev_x1) == hipSuccess) {
+            x_us += xms * 1e3;
+            x_n++;
+        }
+    }
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    for (uint32_t k = 1; k < N; k++) {
+        HIP_TRY(s, hipSetDevice(st[k]->device));
+        HIP_TRY(s, hipStreamSynchronize(strm(k)));
+    }
+    HIP_TRY(s, hipSetDevice(s->device));
+    s->last_exchange_us = x_n ? x_us / x_n : 0.0;
+    const uint32_t p = h_state[1];
+    const uint32_t nrec = std::min(count, p + (h_state[0] ? 1u : 0u));
+    if (nrec)
+        HIP_TRY(s, hipMemcpyAsync(out, s->d_loop_out.p, sizeof(pe_ranked_node) * nrec, hipMemcpyDeviceToHost,
+                                  s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    s->last_ms_pending = false;
+    for (pe_stack* x : st) {
+        for (uint32_t i = 0; i < p; i++) x->plan.emplace_back(x->tgs[tgi]->name, (uint32_t)out[i].row);
+        invalidate_job_distinct(x, tgi);
+        x->offer_row = -1;
+        x->gen++;
+    }
+    elig_log_span(s, tgi, s->offset, n);   // full passes
+    if (placed) *placed = p;
+    return PE_OK;
+}
+
+// Whether tgi's count loop can run split over the replicas (as pe_place_sharded).
+static bool multi_place_ok(pe_stack* s, uint32_t tgi, uint32_t count) {
+    if (s->kids.empty() || !s->kids_valid || !count || s->cfg.stack_kind != PE_STACK_GENERIC || s->metrics_on)
+        return false;
+    if (prepare_tg(s, tgi, s->visit, s->offset) != PE_OK) { s->err.clear(); return false; }
+    TgPlan& g = *s->tgs[tgi];
+    if (!tg_full_scan(s, g) || g.ask.cores > 0 || !g.rports.empty() || !s->visit_unique) return false;
+    if (g.n_spread != (int)g.psets.size() || g.psets_dynamic || s->cfg.preempt) return false;
+    for (size_t k = 0; k < s->tgs.size(); k++)
+        if (k != tgi && s->tgs[k]->name == g.name) return false;
+    return s->visit.size() >= 2 * (s->kids.size() + 1);
+}
+
+// pe_system_place split over the replicas: contiguous ranges of the list, each
+// evaluated and committed by its replica; then every replica commits the
+// others' placements, so all of them hold the same plan.
+static int multi_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
+    std::vector<pe_stack*> st{s};
+    st.insert(st.end(), s->kids.begin(), s->kids.end());
+    const uint32_t N = (uint32_t)st.size(), n = (uint32_t)s->visit.size();
+    std::vector<uint32_t> lo(N), hi(N);
+    for (uint32_t k = 0; k < N; k++) {
+        lo[k] = (uint32_t)((uint64_t)n * k / N);
+        hi[k] = (uint32_t)((uint64_t)n * (k + 1) / N);
+    }
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    for (uint32_t k = 0; k < N; k++) {
+        pe_stack* x = st[k];
+        HIP_TRY(s, hipSetDevice(x->device));
+        int rc = prepare_tg(x, tgi, x->visit, 0);
+        if (rc) return k ? s->fail(rc, "replica: " + x->err) : rc;
+        TgPlan& g = *x->tgs[tgi];
+        HIP_TRY(s, upload_visit(x, x->visit));
+        const uint32_t m = hi[k] - lo[k];
+        const size_t st_off = sizeof(double) * (size_t)m;
+        const size_t bytes = st_off + (((size_t)m + 3) & ~(size_t)3) + 4;
+        HIP_TRY(s, x->d_sys_out.ensure(bytes));
+        HIP_TRY(s, x->h_sys_out.ensure(bytes));
+        uint8_t* dsys = x->d_sys_out.as<uint8_t>();
+        HIP_TRY(s, hipMemsetAsync(dsys + bytes - 4, 0, 4, x->stream));
+        pe::SystemArgs Sa;
+        std::memset(&Sa, 0, sizeof(Sa));
+        Sa.soa = soa_of(x);
+        Sa.tg = tables_of(g);
+        Sa.ask = ask_for(x, g);
+        Sa.list = x->d_visit.as<uint32_t>() + lo[k];
+        Sa.n_list = m;
+        Sa.log10 = x->log10;
+        Sa.out_score = reinterpret_cast<double*>(dsys);
+        Sa.out_status = dsys + st_off;
+        Sa.placed = reinterpret_cast<uint32_t*>(dsys + bytes - 4);
+        Sa.commit = 1;
+        if (m) HIP_TRY(s, pe_launch_system(&Sa, x->stream));
+        HIP_TRY(s, hipMemcpyAsync(x->h_sys_out.p, dsys, bytes, hipMemcpyDeviceToHost, x->stream));
+    }
+    std::vector<std::vector<uint32_t>> rows(N);
+    uint32_t p = 0;
+    for (uint32_t k = 0; k < N; k++) {
+        pe_stack* x = st[k];
+        HIP_TRY(s, hipSetDevice(x->device));
+        HIP_TRY(s, hipStreamSynchronize(x->stream));
+        const uint32_t m = hi[k] - lo[k];
+        const uint8_t* h = x->h_sys_out.as<uint8_t>();
+        const size_t st_off = sizeof(double) * (size_t)m;
+        std::memcpy(out_score + lo[k], h, sizeof(double) * m);
+        std::memcpy(out_status + lo[k], h + st_off, m);
+        for (uint32_t i = 0; i < m; i++)
+            if (out_status[lo[k] + i] == 0) rows[k].push_back(s->visit[lo[k] + i]);
+        p += (uint32_t)rows[k].size();
+    }
+    // every replica commits the other ranges' placements
+    for (uint32_t k = 0; k < N; k++) {
+        pe_stack* x = st[k];
+        std::vector<uint32_t> others;
+        for (uint32_t e = 0; e < N; e++)
+            if (e != k) others.insert(others.end(), rows[e].begin(), rows[e].end());
+        HIP_TRY(s, hipSetDevice(x->device));
+        if (!others.empty()) {
+            TgPlan& g = *x->tgs[tgi];
+            HIP_TRY(s, upload_s(x, x->d_commit_rows, others));
+            pe::NodeSoA soa = soa_of(x);
+            pe::TgTables t = tables_of(g);
+            pe::Ask a = ask_for(x, g);
+            HIP_TRY(s, pe_launch_commit_rows(&soa, &t, &a, x->d_commit_rows.as<uint32_t>(), (uint32_t)others.size(),
+                                             x->stream));
+        }
+    }
+    for (uint32_t k = 0; k < N; k++) {
+        pe_stack* x = st[k];
+        HIP_TRY(s, hipSetDevice(x->device));
+        HIP_TRY(s, hipStreamSynchronize(x->stream));
+        for (uint32_t e = 0; e < N; e++)
+            for (uint32_t r : rows[e]) x->plan.emplace_back(x->tgs[tgi]->name, r);   // list order
+        x->sys.active = false;
+        x->gen++;
+    }
+    HIP_TRY(s, hipSetDevice(s->device));
+    HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
+    HIP_TRY(s, hipEventSynchronize(s->ev1));
+    float ms = 0;
+    HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    s->last_ms_pending = false;
+    elig_log_span(s, tgi, 0, n);
+    if (placed) *placed = p;
+    return PE_OK;
+}
+
+static bool multi_system_ok(pe_stack* s, uint32_t tgi) {
+    if (s->kids.empty() || !s->kids_valid || s->cfg.stack_kind != PE_STACK_SYSTEM || s->cfg.preempt) return false;
+    if (!s->visit_unique || s->visit.size() < s->kids.size() + 1) return false;
+    if (prepare_tg(s, tgi, s->visit, 0) != PE_OK) { s->err.clear(); return false; }
+    TgPlan& g = *s->tgs[tgi];
+    return g.psets.size() == (size_t)g.n_spread && g.ask.cores == 0;
+}
+
+int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
+    const int rc = set_state_one(s, strs, nodes, allocs);
+    if (rc || !s || s->kids.empty()) return rc;
+    bool ok = true;
+    for (pe_stack* k : s->kids) ok = set_state_one(k, strs, nodes, allocs) == PE_OK && ok;
+    kids_fresh(s, ok);
+    return rc;
+}
+
+int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index) {
+    const int rc = update_allocs_one(s, strs, allocs, index);
+    if (rc || !s || s->kids.empty()) return rc;
+    bool ok = true;
+    for (pe_stack* k : s->kids) ok = update_allocs_one(k, strs, allocs, index) == PE_OK && ok;
+    kids_fresh(s, ok);
+    return rc;
+}
+
+int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const uint32_t* index) {
+    const int rc = update_nodes_one(s, strs, nodes, index);
+    if (rc || !s || s->kids.empty()) return rc;
+    bool ok = true;
+    for (pe_stack* k : s->kids) ok = update_nodes_one(k, strs, nodes, index) == PE_OK && ok;
+    kids_fresh(s, ok);
+    return rc;
+}
+
+int pe_reset_plan(pe_stack* s) {
+    const int rc = reset_plan_one(s);
+    if (rc || !s || s->kids.empty()) return rc;
+    bool ok = true;
+    for (pe_stack* k : s->kids) ok = reset_plan_one(k) == PE_OK && ok;
+    kids_fresh(s, ok);
+    return rc;
+}
+
+int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
+    if (s && !s->kids.empty()) (void)kids_sync(s);   // the logged commits name the current job's groups
+    const int rc = set_job_one(s, strs, j);
+    if (rc || !s || s->kids.empty() || !s->kids_valid) return rc;
+    for (pe_stack* k : s->kids)
+        if (set_job_one(k, strs, j) != PE_OK) s->kids_valid = false;
+    return rc;
+}
+
+int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
+    const int rc = commit_one(s, tgi, row);
+    if (rc == PE_OK && !s->kids.empty()) kid_log(s, 0, tgi, row, nullptr, 0);
+    return rc;
+}
+
+int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
+    const int rc = commit_preempt_one(s, tgi, row, preempted, n_preempted);
+    if (rc == PE_OK && !s->kids.empty()) kid_log(s, 1, tgi, row, preempted, n_preempted);
+    return rc;
+}
+
+int pe_plan_stop(pe_stack* s, const uint32_t* allocs, uint32_t n) {
+    const int rc = plan_stop_one(s, allocs, n);
+    if (rc == PE_OK && !s->kids.empty()) kid_log(s, 2, 0, 0, allocs, n);
+    return rc;
+}
+
+int pe_plan_pop_update(pe_stack* s, uint32_t alloc) {
+    const int rc = plan_pop_update_one(s, alloc);
+    if (rc == PE_OK && !s->kids.empty()) kid_log(s, 3, 0, 0, &alloc, 1);
+    return rc;
+}
+
+int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+    if (!s) return PE_EINVAL;
+    if (!s->kids.empty() && s->kids_valid) {
+        int rc = spec_flush(s);
+        if (rc) return rc;
+        if (multi_place_ok(s, tgi, count) && kids_sync(s) == PE_OK) {
+            s->gen++;
+            rc = multi_place(s, tgi, count, out, placed);
+            if (rc) s->kids_valid = false;
+            return rc;
+        }
+    }
+    uint32_t p = 0;
+    const int rc = place_one(s, tgi, count, out, &p);
+    if (placed) *placed = p;
+    if (rc == PE_OK && !s->kids.empty())   // the placements, as the caller's commits would replay them
+        for (uint32_t k = 0; k < p && k < count; k++)
+            kid_log(s, 1, tgi, out[k].row, out[k].preempted, out[k].n_preempted);
+    return rc;
+}
+
+int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
+    if (!s || !out_score || !out_status) return PE_EINVAL;
+    if (!s->kids.empty() && s->kids_valid) {
+        int rc = spec_flush(s);
+        if (rc) return rc;
+        if (multi_system_ok(s, tgi) && kids_sync(s) == PE_OK) {
+            s->gen++;
+            rc = multi_system_place(s, tgi, out_score, out_status, placed);
+            if (rc) s->kids_valid = false;
+            return rc;
+        }
+    }
+    const int rc = system_place_one(s, tgi, out_score, out_status, placed);
+    if (!s->kids.empty()) s->kids_valid = false;   // evictions / distinct_property: not replayable
+    return rc;
+}
+
+uint32_t pe_device_count(const pe_stack* s) { return s ? (uint32_t)s->kids.size() + 1u : 0u; }

@@ -135,7 +135,7 @@ class _Stack:
     stack_kind = abi.PE_STACK_GENERIC
 
     def __init__(self, lib, prefix: str, batch: bool = False, config: SchedulerConfig = None,
-                 device: int = 0):
+                 device: int = 0, devices: Optional[Sequence[int]] = None):
         self._lib = lib
         self._p = prefix
         config = config or SchedulerConfig()
@@ -147,6 +147,12 @@ class _Stack:
         cfg.preempt = int(config.preempt_system if self.stack_kind == abi.PE_STACK_SYSTEM
                           else config.preempt_service)
         cfg.device = device
+        if devices is not None and len(devices) > 1:   # one handle over several GPUs (pe_config.device_ids)
+            if len(devices) > 8:
+                raise ValueError("at most 8 devices per handle")
+            cfg.device_count = len(devices)
+            for k, d in enumerate(devices):
+                cfg.device_ids[k] = int(d)
         self._cfg = cfg
         create = getattr(lib, prefix + ("stack_create" if prefix == "pe_" else "create"))
         self._h = create(C.byref(cfg))
@@ -435,8 +441,9 @@ class GenericStack(_Stack):
     """NewGenericStack (stack.go:336-431) on the MI355X engine."""
     stack_kind = abi.PE_STACK_GENERIC
 
-    def __init__(self, batch: bool = False, config: SchedulerConfig = None, device: int = 0):
-        super().__init__(load_engine(), "pe_", batch, config, device)
+    def __init__(self, batch: bool = False, config: SchedulerConfig = None, device: int = 0,
+                 devices: Optional[Sequence[int]] = None):
+        super().__init__(load_engine(), "pe_", batch, config, device, devices)
 
     def StageOrders(self, orders: np.ndarray):
         """Stage E visit orders (E x n rows, each a shuffled SetNodes list) in HBM."""
@@ -546,8 +553,9 @@ class SystemStack(_Stack):
     """NewSystemStack (stack.go:207-283) on the MI355X engine."""
     stack_kind = abi.PE_STACK_SYSTEM
 
-    def __init__(self, sysbatch: bool = False, config: SchedulerConfig = None, device: int = 0):
-        super().__init__(load_engine(), "pe_", False, config, device)
+    def __init__(self, sysbatch: bool = False, config: SchedulerConfig = None, device: int = 0,
+                 devices: Optional[Sequence[int]] = None):
+        super().__init__(load_engine(), "pe_", False, config, device, devices)
 
     def last_kernel_ms(self) -> float:
         return self._lib.pe_last_kernel_ms(self._h)
