@@ -142,6 +142,10 @@ typedef struct pe_alloc_table {
     /* ports the alloc holds (NetworkIndex.AddAllocs: AllocatedPorts HostIP /
        Value, or the pre-0.12 networks' IP and ports), CSR over allocs, or NULL */
     const uint32_t* port_off; const uint32_t* port_ip; const int32_t* port_value;
+    /* ComparableResources().Flattened.Networks is non-empty (the alloc takes
+       part in PreemptForNetwork, preemption.go:302-331), or NULL: derived as
+       net_mbits > 0 || dyn_ports > 0 || the alloc holds ports */
+    const uint8_t* has_network;
 } pe_alloc_table;
 
 /* ---- job specification (structs.Job / TaskGroup / Task) ----------------- */

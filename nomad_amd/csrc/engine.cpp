@@ -38,6 +38,7 @@
 size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
+hipError_t pe_launch_rank_of(const uint32_t* list, uint32_t n_list, uint32_t* rank_of, uint32_t n_rows, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
 hipError_t pe_launch_counts(const pe::CountDsts* d, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
                             hipStream_t st);
@@ -209,6 +210,7 @@ struct HostAlloc {
     int32_t priority = 0, max_parallel = 0;
     int64_t cpu = 0, mem = 0, disk = 0;
     int32_t mbits = 0, dyn = 0;            // network use on the node's host device
+    bool has_net = false;                  // Flattened.Networks non-empty (PreemptForNetwork candidates)
     uint32_t dev_begin = 0, dev_end = 0;   // into pe_stack::alloc_dev
     uint64_t cores[4] = {0, 0, 0, 0};      // Flattened.Cpu.ReservedCores (ids < 256)
     bool cores_beyond = false;             // a reserved core id >= 256
@@ -503,10 +505,10 @@ struct pe_stack {
         std::vector<uint32_t> pending;    // committed rows not yet in HBM
         uint64_t passes = 0, served = 0;
     } sys;
-    PinnedMem h_sys_cache;                // [FinalScore per row | outcome per row]
-    std::vector<uint8_t> sys_dirty;
+    PinnedMem h_sys_cache;                // per row: FinalScore, or a NaN carrying the outcome (kSysDirty: stale)
     DevMem d_identity;
     uint32_t identity_n = 0;
+    DevMem d_sys_res;                     // k_system_rows outcomes by row
     uint64_t test_fallback_every = 0, test_select_calls = 0;   // PE_TEST_FALLBACK_EVERY
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
@@ -1060,7 +1062,7 @@ void tg_ask(const pe_job* j, const pe_task_group& t, pe::Ask* a) {
             default: break;
         }
         if (x.has_network) {
-            a->has_task_net = 1;
+            a->has_task_net += 1;   // the number of task networks (AssignNetwork per task)
             a->task_mbits += x.net_mbits;
             a->task_dyn += x.net_dyn_ports;
         }
@@ -1469,6 +1471,7 @@ int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index) 
         for (uint32_t k = at->port_off ? at->port_off[i] : 0; at->port_off && k < at->port_off[i + 1]; k++)
             s->alloc_ports.emplace_back(at->port_ip[k], at->port_value[k]);
         a.port_end = (uint32_t)s->alloc_ports.size();
+        a.has_net = at->has_network ? at->has_network[i] != 0 : (a.mbits > 0 || a.dyn > 0 || a.port_end > a.port_begin);
         for (uint32_t k = at->core_off ? at->core_off[i] : 0; at->core_off && k < at->core_off[i + 1]; k++) {
             const uint16_t c = at->core_id[k];
             if (c >= 256) a.cores_beyond = true;
@@ -1577,7 +1580,7 @@ int build_alloc_state(pe_stack* s) {
             x.jtg_key = jtg.emplace(std::make_tuple(a.job, a.ns, a.tg), (uint32_t)jtg.size()).first->second;
             x.mbits = a.mbits;
             x.dyn = a.dyn;
-            x.state_index = i;
+            x.state_index = i | (a.has_net ? pe::kAllocHasNet : 0u);
             const uint32_t ng = s->dev_off[a.row + 1] - s->dev_off[a.row];
             for (uint32_t k = a.dev_begin; k < a.dev_end; k++) {
                 const uint32_t g = s->alloc_dev[k].first, c = s->alloc_dev[k].second;
@@ -3873,8 +3876,11 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
 
 // ---- SystemScheduler per-node Selects from a per-row cache ------------------
 
+constexpr uint64_t kSysNaN = 0x7FF8000000000000ull;
+constexpr uint64_t kSysDirty = kSysNaN | 3u;   // a row changed since the cache pass
+
 static void sys_touch(pe_stack* s, uint32_t row) {
-    if (row < s->sys_dirty.size()) s->sys_dirty[row] = 1;
+    if (s->sys.active && row < s->nodes.size()) s->h_sys_cache.as<uint64_t>()[row] = kSysDirty;
 }
 
 // The queued Plan.AppendAllocs of served system Selects, into HBM at once.
@@ -3923,33 +3929,28 @@ static int sys_start(pe_stack* s, uint32_t tgi) {
         HIP_TRY(s, hipMemcpyAsync(s->d_identity.p, id.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, s->stream));
         s->identity_n = n;
     }
-    const size_t st_off = sizeof(double) * (size_t)n;
-    const size_t bytes = st_off + (((size_t)n + 3) & ~(size_t)3) + 4;
-    HIP_TRY(s, s->d_sys_out.ensure(bytes));
-    HIP_TRY(s, s->h_sys_cache.ensure(bytes));
-    uint8_t* dsys = s->d_sys_out.as<uint8_t>();
+    HIP_TRY(s, s->d_sys_res.ensure(sizeof(uint64_t) * (size_t)std::max<uint32_t>(n, 1)));
+    HIP_TRY(s, s->h_sys_cache.ensure(sizeof(uint64_t) * (size_t)std::max<uint32_t>(n, 1)));
     pe::SystemArgs A;
     std::memset(&A, 0, sizeof(A));
     A.soa = soa_of(s);
     A.tg = tables_of(g);
     A.ask = ask_for(s, g);
-    A.list = s->d_identity.as<uint32_t>();
-    A.n_list = n;
     A.log10 = s->log10;
-    A.out_score = reinterpret_cast<double*>(dsys);
-    A.out_status = dsys + st_off;
-    A.placed = reinterpret_cast<uint32_t*>(dsys + bytes - 4);
     A.commit = 0;
+    A.rank_of = s->d_identity.as<uint32_t>();   // every row, at its own position
+    A.res = s->d_sys_res.as<uint64_t>();
+    A.n_rows = n;
+    A.n_list = 0;                                // outcomes stay in res, by row
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     HIP_TRY(s, pe_launch_system(&A, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
-    HIP_TRY(s, hipMemcpyAsync(s->h_sys_cache.p, dsys, bytes - 4, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(s, hipMemcpyAsync(s->h_sys_cache.p, s->d_sys_res.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
     s->last_ms_pending = false;
-    s->sys_dirty.assign(n, 0);
     y.active = true;
     y.tgi = tgi;
     y.served_row = -1;
@@ -3973,11 +3974,13 @@ static bool sys_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, 
         if (r) { *rc = r; return true; }
     }
     const uint32_t row = s->visit[0];
-    if (s->sys_dirty[row]) return false;
-    const uint32_t n = (uint32_t)s->nodes.size();
-    const uint8_t st = s->h_sys_cache.as<uint8_t>()[sizeof(double) * (size_t)n + row];
+    const uint64_t v = s->h_sys_cache.as<uint64_t>()[row];
+    if (v == kSysDirty) return false;
+    const bool nan = (v & kSysNaN) == kSysNaN;
+    const uint8_t st = nan ? (uint8_t)(v & 3u) : 0;
     if (st == 2 && s->cfg.preempt) return false;   // BinPack with evict: the single Select path
-    const double sc = s->h_sys_cache.as<double>()[row];
+    double sc;
+    std::memcpy(&sc, &v, sizeof(sc));
     out->row = st == 0 ? (int32_t)row : -1;
     out->n_scores = st == 0 ? 1u : 0u;
     out->final_score = st == 0 ? sc : 0.0;
@@ -4870,12 +4873,12 @@ static int commit_one(pe_stack* s, uint32_t tgi, int32_t row) {
         // the served single-node Select's Plan.AppendAlloc: queued for HBM
         s->sys.served_row = -1;
         s->sys.pending.push_back((uint32_t)row);
-        s->sys_dirty[(uint32_t)row] = 1;
+        s->h_sys_cache.as<uint64_t>()[(uint32_t)row] = kSysDirty;
         s->plan.emplace_back(s->tgs[tgi]->name, (uint32_t)row);
         s->offer_row = -1;
         return PE_OK;
     }
-    if (s->sys.active && row >= 0 && (size_t)row < s->sys_dirty.size()) sys_touch(s, (uint32_t)row);
+    if (s->sys.active && row >= 0) sys_touch(s, (uint32_t)row);
     pe_stack::Spec& sp = s->spec;
     if (sp.active && sp.pending && tgi == sp.tgi && row == spec_row(sp, sp.served - 1)) {
         // the predicted Plan.AppendAlloc: already in HBM
@@ -4900,7 +4903,7 @@ static int commit_preempt_one(pe_stack* s, uint32_t tgi, int32_t row, const uint
     if (n_preempted == 0) return commit_one(s, tgi, row);
     int rc = spec_flush(s);
     if (rc) return rc;
-    if (s->sys.active && row >= 0 && (size_t)row < s->sys_dirty.size()) sys_touch(s, (uint32_t)row);
+    if (s->sys.active && row >= 0) sys_touch(s, (uint32_t)row);
     rc = commit_preempt_impl(s, tgi, row, preempted, n_preempted);
     uint64_t cores[4];
     if (rc == PE_OK) core_record(s, *s->tgs[tgi], row, true, cores);
@@ -5435,6 +5438,17 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
     A.out_score = reinterpret_cast<double*>(dsys);
     A.out_status = dsys + st_off;
     A.placed = reinterpret_cast<uint32_t*>(dsys + placed_off);
+    if ((uint64_t)n * 4 >= s->nodes.size()) {
+        // a list covering much of the snapshot: row-order evaluation (coalesced)
+        const uint32_t nn = (uint32_t)s->nodes.size();
+        HIP_TRY(s, s->d_rank_of.ensure(sizeof(uint32_t) * (size_t)std::max<uint32_t>(nn, 1)));
+        HIP_TRY(s, s->d_sys_res.ensure(sizeof(uint64_t) * (size_t)std::max<uint32_t>(nn, 1)));
+        HIP_TRY(s, pe_launch_rank_of(s->d_visit.as<uint32_t>(), n, s->d_rank_of.as<uint32_t>(), nn, s->stream));
+        s->rank_of_valid = true;   // the same table ensure_rank_of would build
+        A.rank_of = s->d_rank_of.as<uint32_t>();
+        A.res = s->d_sys_res.as<uint64_t>();
+        A.n_rows = nn;
+    }
     // distinct_property couples the nodes through the value counts: the kernel
     // evaluates every node without it and without committing, the host then
     // walks the list in order (DistinctPropertyIterator before BinPack)

@@ -95,7 +95,7 @@ struct TgTables {
 struct Ask {
     int64_t cpu, mem, disk;       // AllocatedResources.Comparable() of the task group
     int32_t tg_dyn;               // tg network dynamic ports (AssignPorts)
-    int32_t has_task_net;         // task-level network asks present
+    int32_t has_task_net;         // task-level network asks (the number of tasks with a network)
     int32_t task_mbits, task_dyn; // Σ over task networks
     int32_t commit_mbits, commit_dyn;   // NetworkIndex contribution of the placed alloc
     int32_t desired_count;        // tg.Count for job anti-affinity
@@ -246,8 +246,9 @@ struct PreemptAlloc {
     int32_t mbits, dyn;      // NetworkIndex contribution (released on eviction)
     uint32_t dev_g, dev_c;   // device entries: group / instances, one byte each
     uint32_t n_dev;          // device entries (<= 4)
-    uint32_t state_index;    // row of the pe_alloc_table snapshot
+    uint32_t state_index;    // row of the pe_alloc_table snapshot; bit 31 kAllocHasNet
 };
+constexpr uint32_t kAllocHasNet = 1u << 31;   // Flattened.Networks non-empty (PreemptForNetwork)
 static_assert(sizeof(PreemptAlloc) == 64, "PreemptAlloc is one 64-byte line");
 
 struct PreemptArgs {
@@ -316,6 +317,14 @@ struct SystemArgs {
     uint8_t* out_status;          // [n_list] 0 placed 1 filtered 2 exhausted
     uint32_t* placed;             // [1] atomic counter
     int commit;                   // Plan.AppendAlloc of the options in the kernel (0: the caller commits)
+    // Row-order form (a list that covers a large part of the snapshot): the
+    // kernel walks rows 0..n_rows-1 (coalesced NodeRec / count / verdict
+    // accesses; the list's rows found through rank_of) and stores each
+    // outcome at the row's list position, or with n_list == 0 into res[row]
+    // (the FinalScore, or a NaN whose payload is the outcome).
+    const uint32_t* rank_of;      // [n_rows] list position of each row, or PE_NONE; null: list-order kernel
+    uint64_t* res;                // [n_rows]
+    uint32_t n_rows;
 };
 
 }  // namespace pe

@@ -2036,6 +2036,55 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(A.placed, local);
 }
 
+// k_system in row order, phase one: every row of the list evaluated (and
+// committed) with coalesced accesses; the outcome lands in res[row].
+__device__ __forceinline__ uint64_t sys_box(int status, double score) {
+    if (status == kOption) return (uint64_t)__double_as_longlong(score);
+    return 0x7FF8000000000000ull | (uint64_t)status;   // a quiet NaN carrying the outcome
+}
+
+__global__ void __launch_bounds__(256) k_system_rows(SystemArgs A) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t local = 0;
+    Overlay none;
+    none.keys = nullptr;
+    for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < A.n_rows; row += stride) {
+        const uint32_t pos = A.rank_of[row];
+        if (pos == 0xFFFFFFFFu) continue;
+        NodeEval ev;
+        eval_node<false>(A.soa, A.tg, A.tg.class_ok, A.ask, none, nullptr, A.log10, nullptr, row, &ev);
+        if (A.n_list) {   // the outcome at the row's list position (scattered stores, nothing waits on them)
+            A.out_score[pos] = ev.status == kOption ? ev.score : __builtin_nan("");
+            A.out_status[pos] = (uint8_t)ev.status;
+        } else {
+            A.res[row] = sys_box(ev.status, ev.score);
+        }
+        if (ev.status != kOption) continue;
+        local++;
+        if (!A.commit) continue;
+        NodeRec& r = A.soa.rec[row];
+        r.used_cpu += ask_cpu(A.soa, A.ask, row);
+        core_take(A.soa, A.ask, row, 1);
+        r.used_mem += A.ask.mem;
+        r.used_disk += A.ask.disk;
+        r.used_mbits += A.ask.commit_mbits;
+        r.used_dyn += A.ask.commit_dyn;
+        A.soa.coll_job[row] += 1;
+        A.tg.coll_tg[row] += 1;
+        if (A.ask.n_dev > 0) A.tg.dev_free[row] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[row], 1);
+    }
+    if (A.placed) {
+        for (int off = 32; off > 0; off >>= 1) local += __shfl_xor(local, off);
+        if ((threadIdx.x & 63) == 0 && local) atomicAdd(A.placed, local);
+    }
+}
+
+// rank_of[row] = position of row in the list (rows absent: PE_NONE, set by the caller's memset)
+__global__ void __launch_bounds__(256) k_rank_of(const uint32_t* list, uint32_t n_list, uint32_t* rank_of) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n_list) rank_of[list[i]] = i;
+}
+
 // Outcome census of one Select pass over the visit list on the HBM state
 // (no overlay): counts[0] options, [1] filtered, [2] exhausted. With no option
 // the Select is nil after pulling every node, which the count loop's
@@ -3049,7 +3098,21 @@ hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t ma
     return hipGetLastError();
 }
 
+hipError_t pe_launch_rank_of(const uint32_t* list, uint32_t n_list, uint32_t* rank_of, uint32_t n_rows, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(rank_of, 0xFF, sizeof(uint32_t) * (size_t)n_rows, st);
+    if (e != hipSuccess || !n_list) return e;
+    hipLaunchKernelGGL(pe::k_rank_of, dim3((n_list + 255) / 256), dim3(256), 0, st, list, n_list, rank_of);
+    return hipGetLastError();
+}
+
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st) {
+    if (a->rank_of && a->res) {   // row order: coalesced evaluation, then the list-order gather
+        uint32_t b1 = (a->n_rows + 255) / 256;
+        if (b1 > 8192) b1 = 8192;
+        if (b1 == 0) b1 = 1;
+        hipLaunchKernelGGL(pe::k_system_rows, dim3(b1), dim3(256), 0, st, *a);
+        return hipGetLastError();
+    }
     uint32_t blocks = (a->n_list + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;

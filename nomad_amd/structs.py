@@ -140,6 +140,7 @@ class Allocation:
     memory_mb: int = 0
     disk_mb: int = 0
     net_mbits: int = 0
+    has_network: Optional[bool] = None   # Flattened.Networks non-empty (None: net_mbits/dyn_ports/ports > 0)
     dyn_ports: int = 0
     priority: int = 50
     terminal: bool = False

@@ -92,6 +92,7 @@ struct OAlloc {
     int state_index = -1;                    // row of the state alloc table (-1: plan alloc)
     std::vector<uint16_t> cores;             // Flattened.Cpu.ReservedCores (a set)
     std::vector<std::pair<std::string, int>> ports;   // (HostIP, port) held (NetworkIndex.AddAllocs)
+    bool has_net = false;                    // Flattened.Networks non-empty (on the node's first device)
 };
 
 struct OConstraint { std::string l, r, op; };
@@ -1217,6 +1218,61 @@ struct Preemptor {
         return out;
     }
 
+    // PreemptForNetwork (preemption.go:270-455) for an ask of `needed` MBits
+    // without reserved ports, every candidate's network on the node's device
+    // (total: AvailBandwidth, used: the NetworkIndex's UsedBandwidth).
+    std::vector<const OAlloc*> ForNetwork(int32_t needed, int32_t total, int32_t used) {
+        if (current.empty()) return {};
+        std::vector<const OAlloc*> dev;
+        for (const OAlloc* a : current) {
+            if (!a->has_net) continue;
+            if (job_priority - a->priority < 10) continue;
+            dev.push_back(a);
+        }
+        if (dev.empty()) return {};
+        if (total < needed) return {};
+        const int32_t free_bw = total - used;
+        int32_t pbw = 0;
+        std::vector<const OAlloc*> best;
+        bool met = pbw + free_bw >= needed;
+        auto distance = [&](const OAlloc* a) {   // networkResourceDistance (preemption.go:627-635)
+            return std::fabs((double)((int64_t)needed - (int64_t)a->mbits) / (double)needed);
+        };
+        if (!met) {
+            for (auto& grp : group_preemptible(job_priority, dev)) {
+                auto v = grp.second;
+                go_sort_slice(v, [&](const OAlloc* x, const OAlloc* y) {   // distanceComparatorForNetwork
+                    auto score = [&](const OAlloc* a) {                   // scoreForNetwork
+                        double pen = 0.0;
+                        const int num = num_preemptions(a);
+                        if (a->max_parallel > 0 && num >= a->max_parallel)
+                            pen = (double)((num + 1) - a->max_parallel) * 50.0;
+                        return distance(a) + pen;
+                    };
+                    return score(x) < score(y);
+                });
+                for (const OAlloc* a : v) {
+                    pbw += a->mbits;
+                    best.push_back(a);
+                    if (pbw + free_bw >= needed) { met = true; break; }
+                }
+                if (met) break;
+            }
+        }
+        if (!met) return {};
+        // filterSuperset with the network resource (MeetsRequirements is false
+        // while either MBits figure is 0)
+        go_sort_slice(best, [&](const OAlloc* x, const OAlloc* y) { return distance(x) > distance(y); });
+        int32_t avail = free_bw;
+        std::vector<const OAlloc*> out;
+        for (const OAlloc* a : best) {
+            out.push_back(a);
+            avail += a->mbits;
+            if (avail != 0 && needed != 0 && avail >= needed) break;
+        }
+        return out;
+    }
+
     // PreemptForDevice + selectBestAllocs (preemption.go:472-601); device groups
     // in node order (a map in the reference).
     std::vector<const OAlloc*> ForDevice(orasem::Caches& c, const ONode& n, const ODevReq& req, const DevAlloc& da) {
@@ -1293,6 +1349,19 @@ struct BinPackIterator : RankIterator {
     const OTaskGroup* tg = nullptr;
     bool spread_algo = false, oversub = false;
 
+    // NetworkIndex SetNode + AddAllocs: dynamic-range ports in use and the
+    // bandwidth used on the device (network.go:92-200)
+    static void index_usage(const ONode& n, const std::vector<const OAlloc*>& proposed, int32_t* dyn, int32_t* mbits) {
+        *dyn = n.reserved_dyn;
+        *mbits = 0;
+        for (const OAlloc* a : proposed) { if (a->terminal) continue; *dyn += a->dyn_ports; *mbits += a->mbits; }
+    }
+    // AvailBandwidth of the node's (first) host network device
+    static int32_t device_bandwidth(const ONode& n) {
+        for (auto& nw : n.nets) if (!nw.device.empty()) return nw.mbits;
+        return 0;
+    }
+
     static double score_fit(bool spread, const ONode& n, int64_t ucpu, int64_t umem) {
         double node_cpu = (double)n.cpu, node_mem = (double)n.mem;
         node_cpu -= (double)n.rcpu; node_mem -= (double)n.rmem;
@@ -1311,8 +1380,8 @@ struct BinPackIterator : RankIterator {
             const ONode& n = *option->node;
             auto proposed = ctx->ProposedAllocs(n.row);
             // NetworkIndex: SetNode + AddAllocs
-            int32_t used_dyn = n.reserved_dyn, used_mbits = 0;
-            for (const OAlloc* a : proposed) { if (a->terminal) continue; used_dyn += a->dyn_ports; used_mbits += a->mbits; }
+            int32_t used_dyn = 0, used_mbits = 0;
+            index_usage(n, proposed, &used_dyn, &used_mbits);
             DevAlloc dev(&n);
             dev.AddAllocs(proposed);
             double total_dev_w = 0.0, sum_dev_match = 0.0;
@@ -1358,19 +1427,21 @@ struct BinPackIterator : RankIterator {
                     bool has_addr = false;
                     for (auto& a : n.aliases) if (a == tg->net_host_network) { has_addr = true; break; }
                     if (!has_addr || kDynPortCapacity - used_dyn < 1) {
-                        if (evict) {
-                            // PreemptForNetwork(ask) with no static ports and no MBits
-                            // (preemption.go:270-455): no candidate with a network, or
-                            // free bandwidth >= 0, returns nil; BinPack then skips the
-                            // node without an ExhaustedNode (rank.go:265-272)
-                            int32_t avail = 0;
-                            for (auto& nw : n.nets) if (!nw.device.empty()) { avail = std::max(nw.mbits, 0); break; }
-                            if (used_mbits > avail) throw Unsupported("network preemption");
+                        if (!evict) {
+                            ctx->metrics.ExhaustedNode(&n, !has_addr ? "network: no addresses available"
+                                                                     : "network: dynamic port selection failed");
                             continue;
                         }
-                        ctx->metrics.ExhaustedNode(&n, !has_addr ? "network: no addresses available"
-                                                                 : "network: dynamic port selection failed");
-                        continue;
+                        // PreemptForNetwork on the group's ask (rank.go:273-300); nil
+                        // skips the node without an ExhaustedNode
+                        if (!tg->rports.empty()) throw Unsupported("static port asks with preemption");
+                        pre.SetCandidates(proposed);
+                        auto np = pre.ForNetwork(0, device_bandwidth(n), used_mbits);
+                        if (np.empty()) continue;
+                        to_preempt.insert(to_preempt.end(), np.begin(), np.end());
+                        proposed = remove_allocs(proposed, np);
+                        index_usage(n, proposed, &used_dyn, &used_mbits);   // a new NetworkIndex
+                        if (!has_addr || kDynPortCapacity - used_dyn < 1) continue;
                     }
                     used_dyn += tg->net_dyn;   // AddReservedPorts(offer)
                 }
@@ -1390,10 +1461,29 @@ struct BinPackIterator : RankIterator {
                         if (kDynPortCapacity - used_dyn < t.net_dyn) { err = "dynamic port selection failed"; continue; }
                         ok = true; break;
                     }
-                    if (!ok) {
-                        if (evict) throw Unsupported("network preemption");   // PreemptForNetwork path
-                        ctx->metrics.ExhaustedNode(&n, "network: " + err); skip = true; break;
+                    if (!ok && evict) {
+                        // PreemptForNetwork on the task's ask (rank.go:343-379); the
+                        // rebuilt index holds the remaining proposed allocs only
+                        int ndev = 0;
+                        for (auto& nw : n.nets) ndev += nw.device.empty() ? 0 : 1;
+                        if (ndev > 1) throw Unsupported("network preemption on a node with several network devices");
+                        if (t.net_reserved > 0) throw Unsupported("static port asks with preemption");
+                        pre.SetCandidates(proposed);
+                        auto np = pre.ForNetwork(t.net_mbits, device_bandwidth(n), used_mbits);
+                        if (np.empty()) { skip = true; break; }
+                        to_preempt.insert(to_preempt.end(), np.begin(), np.end());
+                        proposed = remove_allocs(proposed, np);
+                        index_usage(n, proposed, &used_dyn, &used_mbits);
+                        for (auto& nw : n.nets) {
+                            if (nw.device.empty()) continue;
+                            if (used_mbits + t.net_mbits > nw.mbits) continue;
+                            if (kDynPortCapacity - used_dyn < t.net_dyn) continue;
+                            ok = true;
+                            break;
+                        }
+                        if (!ok) { skip = true; break; }
                     }
+                    if (!ok) { ctx->metrics.ExhaustedNode(&n, "network: " + err); skip = true; break; }
                     used_mbits += t.net_mbits; used_dyn += t.net_dyn;   // AddReserved(offer)
                 }
                 // devices (rank.go:366-414)
@@ -1909,6 +1999,8 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
         a.cpu = at->cpu_shares[i]; a.mem = at->memory_mb[i]; a.disk = at->disk_mb[i];
         a.mbits = at->net_mbits[i]; a.dyn_ports = at->dyn_ports[i];
         a.state_index = (int)i;
+        const bool held_ports = at->port_off && at->port_off[i + 1] > at->port_off[i];
+        a.has_net = at->has_network ? at->has_network[i] != 0 : (a.mbits > 0 || a.dyn_ports > 0 || held_ports);
         a.max_parallel = at->max_parallel ? at->max_parallel[i] : 0;
         if (at->dev_off)
             for (uint32_t k = at->dev_off[i]; k < at->dev_off[i + 1]; k++)

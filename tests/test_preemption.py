@@ -2,11 +2,18 @@
 PreemptForDevice, scheduler/preemption.go:194-601) and the
 PreemptionScoringIterator score (rank.go:773-844).
 
-Known-answer tests are the reference's TestPreemption cases without network
-preemption (scheduler/preemption_test.go:983-1324), rebuilt at the Stack
-boundary: one node, Select with Preempt=true, the set of preempted allocs.
-createAlloc gives allocs cpu / memory (and task networks) but no shared disk,
-and the ask has an empty EphemeralDisk, so disk is 0 on both sides.
+Known-answer tests are the reference's TestPreemption cases
+(scheduler/preemption_test.go:286-1324), rebuilt at the Stack boundary: one
+node, Select with Preempt=true, the set of preempted allocs. createAlloc gives
+allocs cpu / memory (and task networks) but no shared disk, and the ask has an
+empty EphemeralDisk, so disk is 0 on both sides. The cases whose ask holds a
+static port ("No preemption because existing allocs are not low priority",
+"Preempting low priority allocs not enough ...", "preemption impossible -
+static port ...", "preempt only from device that has allocation with unused
+reserved port", "one alloc meets static port need ...", "alloc that meets
+static port need ...") are outside the device path: task static ports are
+refused with PE_EUNSUPPORTED and left to the reference chain
+(test_static_port_network_preemption_is_refused).
 """
 import math
 
@@ -47,9 +54,12 @@ def preemption_node():
     return nd
 
 
-def alloc(i, prio, cpu, mem, devices=(), mbits=0):
+def alloc(i, prio, cpu, mem, devices=(), mbits=0, node="node-0"):
+    """createAlloc; `mbits` is the bandwidth of the alloc's eth0 networks (task
+    and group networks on one device add up in Flattened.Networks[0] and in
+    NetworkIndex.UsedBandwidth alike)."""
     job = {LOW: "low", LOW2: "low2", HIGH: "high"}[prio]
-    return Allocation(node_id="node-0", job_id=job, task_group="web", cpu_shares=cpu, memory_mb=mem,
+    return Allocation(node_id=node, job_id=job, task_group="web", cpu_shares=cpu, memory_mb=mem,
                       disk_mb=0, priority=prio, devices=list(devices), net_mbits=mbits)
 
 
@@ -80,6 +90,22 @@ CASES = {
     "device preemption not possible": (
         [alloc(0, LOW, 500, 512, [(0, 4)]), alloc(1, LOW, 200, 512, [(2, 1)])],
         ask_job(1000, 512, RequestedDevice("gpu", 6)), None),
+    # PreemptForNetwork (preemption.go:270-455) from BinPack's AssignNetwork failure
+    "Combination of high/low priority allocs, without static ports": (
+        [alloc(0, HIGH, 2800, 2256, mbits=150), alloc(1, LOW, 200, 256, mbits=200 + 300),
+         alloc(2, LOW, 200, 256, mbits=300), alloc(3, LOW, 700, 256)],
+        ask_job(1100, 1000, mbits=840), {1, 2, 3}),
+    "preempt allocs with network devices": (
+        [alloc(0, LOW, 2800, 2256), alloc(1, LOW, 200, 256, mbits=800)],
+        ask_job(1100, 1000, mbits=840), {1}),
+    "Preemption needed for all resources except network": (
+        [alloc(0, HIGH, 2800, 2256, mbits=150), alloc(1, LOW, 200, 256, mbits=50),
+         alloc(2, LOW, 200, 512), alloc(3, LOW, 700, 276)],
+        ask_job(1000, 3000, mbits=50), {1, 2, 3}),
+    "Only one low priority alloc needs to be preempted": (
+        [alloc(0, HIGH, 1200, 2256, mbits=150), alloc(1, LOW, 200, 256, mbits=500),
+         alloc(2, LOW, 200, 256, mbits=320)],
+        ask_job(300, 500, mbits=320), {2}),
     "filter out superset allocs": (
         [alloc(0, HIGH, 1800, 2256, mbits=150), alloc(1, LOW, 1500, 256, mbits=100),
          alloc(2, LOW, 600, 256, mbits=300)],
@@ -113,6 +139,93 @@ def test_preemption_kat(stack_cls, case):
     prios = [allocs[i].priority for i in r.preempted]
     want = 1.0 / (1.0 + math.exp(0.0048 * (net_priority(prios) - 2048.0)))
     assert abs(r.scores[-1] - want) <= 1e-12 * want
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_network_preemption_close_priority(stack_cls):
+    """"ignore allocs with close enough priority for network devices": a job
+    5 above the allocs finds no network candidate and the node is skipped."""
+    node = preemption_node()
+    allocs = [alloc(0, LOW, 2800, 2256), alloc(1, LOW, 200, 256, mbits=800)]
+    job = ask_job(1100, 1000, mbits=840)
+    job.priority = LOW + 5
+    st = stack_cls()
+    st.SetState([node], allocs)
+    st.SetJob(job)
+    st.SetNodes([node])
+    r = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert r.row == -1 and r.nodes_exhausted == 0
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_network_preemption_existing_evictions(stack_cls):
+    """"alloc from job that has existing evictions not chosen for preemption":
+    the plan already preempts an alloc of the priority-40 job (here on a second
+    node), the priority-30 alloc goes first and alone meets the bandwidth."""
+    node = preemption_node()
+    other = synth.mock_node("node-1")
+    other.reserved_host_ports = []
+    allocs = [alloc(0, HIGH, 1200, 2256, mbits=150), alloc(1, LOW, 200, 256, mbits=500),
+              alloc(2, LOW2, 200, 256, mbits=300),
+              alloc(3, LOW2, 3700, 256, mbits=300, node="node-1")]
+    job = ask_job(300, 500, mbits=320)
+    job.task_groups[0].count = 2
+    st = stack_cls()
+    st.SetState([node, other], allocs)
+    st.SetJob(job)
+    st.SetNodes([other])
+    r1 = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert r1.row == 1 and r1.preempted == [3]
+    st.Commit(0, r1.row, r1.preempted)
+    st.SetNodes([node])
+    r2 = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert r2.row == 0 and r2.preempted == [1]
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_group_port_preemption_frees_dynamic_ports(stack_cls):
+    """AssignPorts failing on a task-group dynamic port ask with eviction
+    (rank.go:273-300): PreemptForNetwork with an ask of 0 MBits keeps every
+    alloc it collected (MeetsRequirements is false for 0 MBits), and only
+    runs when the device's bandwidth is overcommitted; after the evictions
+    the rebuilt index frees the dynamic ports."""
+    nodes = [synth.mock_node("n%d" % i) for i in range(4)]
+    for nd in nodes:
+        nd.compute_class()
+    allocs = []
+    for i, nd in enumerate(nodes):
+        allocs.append(Allocation(node_id=nd.id, job_id="batch-%d" % i, task_group="t", cpu_shares=600,
+                                 memory_mb=256, priority=20, dyn_ports=12001, net_mbits=700))
+        allocs.append(Allocation(node_id=nd.id, job_id="svc-%d" % i, task_group="t", cpu_shares=600,
+                                 memory_mb=256, priority=30, net_mbits=400 if i % 2 else 200))
+    job = synth.mock_job(count=3)
+    job.priority = 70
+    st = stack_cls(config=SchedulerConfig(preempt_service=True))
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(list(range(len(nodes))))
+    r = st.SelectRaw(0, SelectOptions(preempt=True))
+    # nodes 1, 3 are overcommitted (1100 > 1000 MBits): the priority-20 alloc
+    # goes first and is enough; nodes 0, 2 are skipped
+    assert (r.row, r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted) == (1, 4, 0, 0)
+    assert r.preempted == [2]
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_static_port_network_preemption_is_refused(stack_cls):
+    """A task static port ask is outside the device path: the engine refuses
+    the task group (PE_EUNSUPPORTED, the shim hands it to the reference chain)
+    and the oracle raises on it."""
+    node = preemption_node()
+    allocs = [alloc(0, HIGH, 1200, 2256, mbits=150), alloc(1, LOW, 200, 256, mbits=600)]
+    job = ask_job(600, 1000, mbits=700)
+    job.task_groups[0].tasks[0].network.reserved_ports = [88]
+    st = stack_cls()
+    st.SetState([node], allocs)
+    with pytest.raises(Exception, match="(?i)unsupported|static port"):
+        st.SetJob(job)
+        st.SetNodes([node])
+        st.SelectRaw(0, SelectOptions(preempt=True))
 
 
 @pytest.mark.parametrize("stack_cls", STACKS)
