@@ -146,6 +146,12 @@ typedef struct pe_alloc_table {
        part in PreemptForNetwork, preemption.go:302-331), or NULL: derived as
        net_mbits > 0 || dyn_ports > 0 || the alloc holds ports */
     const uint8_t* has_network;
+    /* the Device of the alloc's networks (NetworkResource.Device; string id),
+       or PE_NONE / NULL: the node's first host network device. Bandwidth is
+       kept per node on that device (NetworkIndex.UsedBandwidth[device],
+       network.go:196-230): a network ask on a node holding an alloc on another
+       device is refused (PE_EUNSUPPORTED) */
+    const uint32_t* net_device;
 } pe_alloc_table;
 
 /* ---- job specification (structs.Job / TaskGroup / Task) ----------------- */

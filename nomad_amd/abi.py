@@ -71,6 +71,7 @@ class pe_alloc_table(C.Structure):
         ("core_off", u32p), ("core_id", u16p),
         ("port_off", u32p), ("port_ip", u32p), ("port_value", i32p),
         ("has_network", u8p),
+        ("net_device", u32p),
     ]
 
 

@@ -179,6 +179,7 @@ struct HostNode {
     uint32_t cls;
     uint32_t sig;          // (class, drivers, networks, aliases, volumes, devices) signature
     int32_t first_mbits;
+    uint32_t first_dev;    // string id of the first host network device (PE_NONE: none)
     uint16_t n_device_nets, n_devices;
 };
 
@@ -379,6 +380,7 @@ struct pe_stack {
     // reserved cores (rank.go:437-466): 4 x u64 masks per node over core ids < 256
     bool has_cores = false;                    // some node has ReservableCpuCores / ReservedCpuCores
     std::string cores_tg_unsupported;          // why task groups asking cores stay on the host path
+    uint64_t net_other_dev = 0;                // allocs on a network device other than their node's first
     std::string cores_unsupported;             // alloc core sets that fail every AllocsFit (overlap, outside)
     std::vector<uint64_t> h_core_rsvable, h_core_avail, h_core_base, h_core_used;   // used: host mirror of the plan
     std::vector<int64_t> h_core_spc;
@@ -1248,9 +1250,10 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         h.cls = it->second;
         h.n_device_nets = 0;
         h.first_mbits = -1;
+        h.first_dev = PE_NONE;
         for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++) {
             if (!s->S(nt->net_device[k]).empty()) {
-                if (h.n_device_nets == 0) h.first_mbits = nt->net_mbits[k];
+                if (h.n_device_nets == 0) { h.first_mbits = nt->net_mbits[k]; h.first_dev = nt->net_device[k]; }
                 h.n_device_nets++;
             }
         }
@@ -1444,6 +1447,7 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     s->allocs.clear();
     s->alloc_dev.clear();
     s->alloc_ports.clear();
+    s->net_other_dev = 0;
     rc = append_allocs(s, at, nullptr);
     if (rc) return rc;
     return build_alloc_state(s);
@@ -1472,6 +1476,9 @@ int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index) 
             s->alloc_ports.emplace_back(at->port_ip[k], at->port_value[k]);
         a.port_end = (uint32_t)s->alloc_ports.size();
         a.has_net = at->has_network ? at->has_network[i] != 0 : (a.mbits > 0 || a.dyn > 0 || a.port_end > a.port_begin);
+        if (at->net_device && at->net_device[i] != PE_NONE && a.has_net &&
+            (s->nodes[row].first_dev == PE_NONE || s->S(at->net_device[i]) != s->S(s->nodes[row].first_dev)))
+            s->net_other_dev++;   // its bandwidth is not on the device the engine keeps per node
         for (uint32_t k = at->core_off ? at->core_off[i] : 0; at->core_off && k < at->core_off[i + 1]; k++) {
             const uint16_t c = at->core_id[k];
             if (c >= 256) a.cores_beyond = true;
@@ -2129,12 +2136,18 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
     if (g.node_ok_used) HIP_TRY(s, upload_s(s, g.node_ok, node_ok));
     {
         // fold the class verdict into one byte per node (single round trip per
-        // node); the class table goes up with the same launch when it is small
+        // node); the class table goes up with the same launch when every
+        // workgroup's pull of it over the bus stays small (blocks x classes
+        // bytes, at most kStagedFoldBusBytes), else one upload + k_fold_feas
         pe::NodeSoA soa = soa_of(s);
         HIP_TRY(s, g.node_feas.ensure(std::max<size_t>(n, 1)));
         HIP_TRY(s, g.class_ok.ensure(std::max<size_t>(class_ok.size(), 1)));
-        const unsigned char* staged =
-            class_ok.size() <= pe_fold_feas_max_classes() ? stage_only(s, class_ok) : nullptr;
+        constexpr size_t kStagedFoldBusBytes = 256 * 1024;
+        const size_t fold_blocks = std::min<size_t>(4096, std::max<size_t>(1, ((size_t)n + 255) / 256));
+        const unsigned char* staged = class_ok.size() <= pe_fold_feas_max_classes() &&
+                                              class_ok.size() * fold_blocks <= kStagedFoldBusBytes
+                                          ? stage_only(s, class_ok)
+                                          : nullptr;
         if (staged) {
             HIP_TRY(s, pe_launch_fold_feas_staged(&soa, staged, g.class_ok.as<uint8_t>(), (uint32_t)class_ok.size(),
                                                   g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr,
@@ -2253,6 +2266,8 @@ int prepare_tg(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& order, ui
     if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
     if (!s->cores_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, s->cores_unsupported);
     if (g.ask.cores > 0 && !s->cores_tg_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, s->cores_tg_unsupported);
+    if ((g.ask.tg_dyn > 0 || g.ask.has_task_net) && s->net_other_dev)
+        return s->fail(PE_EUNSUPPORTED, "network asks with allocs on a node's other network device");
     if (!g.psets_built) {
         int rc = build_psets(s, g);
         if (rc) return rc;

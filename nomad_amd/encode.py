@@ -230,6 +230,8 @@ class EncodedState:
         at.max_parallel = _ptr(acol(lambda a: a.max_parallel, _i32), abi.i32p)
         at.has_network = _ptr(acol(lambda a: int(bool(a.net_mbits > 0 or a.dyn_ports > 0 or a.ports)
                                                   if a.has_network is None else a.has_network), _u8), abi.u8p)
+        at.net_device = _ptr(acol(lambda a: abi.PE_NONE if a.net_device is None else I(a.net_device), _u32),
+                             abi.u32p)
         if any(a.ports for a in live):
             poff = np.zeros(len(live) + 1, dtype=np.uint32)
             pip, pval = [], []

@@ -141,6 +141,7 @@ class Allocation:
     disk_mb: int = 0
     net_mbits: int = 0
     has_network: Optional[bool] = None   # Flattened.Networks non-empty (None: net_mbits/dyn_ports/ports > 0)
+    net_device: Optional[str] = None     # NetworkResource.Device (None: the node's first device network)
     dyn_ports: int = 0
     priority: int = 50
     terminal: bool = False

@@ -93,6 +93,7 @@ struct OAlloc {
     std::vector<uint16_t> cores;             // Flattened.Cpu.ReservedCores (a set)
     std::vector<std::pair<std::string, int>> ports;   // (HostIP, port) held (NetworkIndex.AddAllocs)
     bool has_net = false;                    // Flattened.Networks non-empty (on the node's first device)
+    bool other_dev = false;                  // its networks are on another device than the node's first
 };
 
 struct OConstraint { std::string l, r, op; };
@@ -1379,6 +1380,11 @@ struct BinPackIterator : RankIterator {
             if (!option) return nullptr;
             const ONode& n = *option->node;
             auto proposed = ctx->ProposedAllocs(n.row);
+            bool net_ask = tg->has_network;
+            for (auto& t : tg->tasks) net_ask = net_ask || t.has_network;
+            if (net_ask)   // UsedBandwidth is per device (network.go:196-230); kept for the first only
+                for (const OAlloc* a : proposed)
+                    if (a->other_dev && !a->terminal) throw Unsupported("allocs on another network device");
             // NetworkIndex: SetNode + AddAllocs
             int32_t used_dyn = 0, used_mbits = 0;
             index_usage(n, proposed, &used_dyn, &used_mbits);
@@ -2001,6 +2007,12 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
         a.state_index = (int)i;
         const bool held_ports = at->port_off && at->port_off[i + 1] > at->port_off[i];
         a.has_net = at->has_network ? at->has_network[i] != 0 : (a.mbits > 0 || a.dyn_ports > 0 || held_ports);
+        if (at->net_device && at->net_device[i] != PE_NONE && a.has_net) {
+            std::string first;
+            const ONode& nd = st.nodes[(size_t)a.node_row];
+            for (auto& nw : nd.nets) if (!nw.device.empty()) { first = nw.device; break; }
+            a.other_dev = S(st, at->net_device[i]) != first;
+        }
         a.max_parallel = at->max_parallel ? at->max_parallel[i] : 0;
         if (at->dev_off)
             for (uint32_t k = at->dev_off[i]; k < at->dev_off[i + 1]; k++)

@@ -375,3 +375,29 @@ def test_preempt_skips_nodes_without_dynamic_ports(stack_cls):
     # nodes 0, 2, 4 are skipped; 1, 3, 5 evict their batch alloc (limit 3); the first wins the tie
     assert (r.row, r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted) == (1, 6, 0, 0)
     assert r.preempted == [1]
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_alloc_on_other_network_device_is_refused(stack_cls):
+    """NetworkIndex keeps bandwidth per device (UsedBandwidth[device],
+    network.go:196-230) and PreemptForNetwork groups candidates by their
+    network's device (preemption.go:302-331). Both sides keep it for the node's
+    first device only, so a network ask on a node holding an alloc on another
+    device is refused (PE_EUNSUPPORTED / oracle Unsupported) rather than
+    answered from the wrong device's figures; with the alloc on eth0 the same
+    case places and preempts."""
+    node = preemption_node()
+    job = ask_job(1100, 1000, mbits=840)
+    for dev, refused in (("eth1", True), ("eth0", False)):
+        allocs = [alloc(0, LOW, 2800, 2256), alloc(1, LOW, 200, 256, mbits=800)]
+        allocs[1].net_device = dev
+        st = stack_cls()
+        st.SetState([node], allocs)
+        st.SetJob(job)
+        st.SetNodes([node])
+        if refused:
+            with pytest.raises(Exception, match="(?i)unsupported|network device"):
+                st.SelectRaw(0, SelectOptions(preempt=True))
+        else:
+            r = st.SelectRaw(0, SelectOptions(preempt=True))
+            assert r.row == 0 and r.preempted == [1]
