@@ -5438,10 +5438,11 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
     // one device block [scores | outcomes | placed], one DMA into page-locked staging
     const size_t st_off = sizeof(double) * (size_t)n;
     const size_t placed_off = st_off + (((size_t)n + 3) & ~(size_t)3);
-    HIP_TRY(s, s->d_sys_out.ensure(placed_off + 4));
-    HIP_TRY(s, s->h_sys_out.ensure(placed_off + 4));
+    const size_t placed_bytes = sizeof(uint32_t) * pe::kPlacedSlots;
+    HIP_TRY(s, s->d_sys_out.ensure(placed_off + placed_bytes));
+    HIP_TRY(s, s->h_sys_out.ensure(placed_off + placed_bytes));
     uint8_t* dsys = s->d_sys_out.as<uint8_t>();
-    HIP_TRY(s, hipMemsetAsync(dsys + placed_off, 0, 4, s->stream));
+    HIP_TRY(s, hipMemsetAsync(dsys + placed_off, 0, placed_bytes, s->stream));
     pe::SystemArgs A;
     std::memset(&A, 0, sizeof(A));
     A.soa = soa_of(s);
@@ -5453,6 +5454,7 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
     A.out_score = reinterpret_cast<double*>(dsys);
     A.out_status = dsys + st_off;
     A.placed = reinterpret_cast<uint32_t*>(dsys + placed_off);
+    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));   // the timed device work: rank_of + k_system
     if ((uint64_t)n * 4 >= s->nodes.size()) {
         // a list covering much of the snapshot: row-order evaluation (coalesced)
         const uint32_t nn = (uint32_t)s->nodes.size();
@@ -5470,7 +5472,6 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
     const bool distinct = g.psets.size() > (size_t)g.n_spread;
     A.commit = distinct ? 0 : 1;
     if (distinct) A.tg.n_psets = A.tg.n_spread;
-    HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     HIP_TRY(s, pe_launch_system(&A, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     {
@@ -5479,14 +5480,19 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
     }
     {
         ApiScope prof_d_(s, "system.d2h");
-        HIP_TRY(s, hipMemcpyAsync(s->h_sys_out.p, dsys, placed_off + 4, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(s->h_sys_out.p, dsys, placed_off + placed_bytes, hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
     }
     uint32_t p;
     {
         ApiScope prof_c_(s, "system.copy_out");
         const uint8_t* h = s->h_sys_out.as<uint8_t>();
-        std::memcpy(&p, h + placed_off, 4);
+        p = 0;
+        for (uint32_t k = 0; k < pe::kPlacedSlots; k++) {
+            uint32_t v;
+            std::memcpy(&v, h + placed_off + 4 * k, 4);
+            p += v;
+        }
         std::memcpy(out_score, h, sizeof(double) * n);
         std::memcpy(out_status, h + st_off, n);
     }
@@ -6001,7 +6007,7 @@ static int multi_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint
         Sa.log10 = x->log10;
         Sa.out_score = reinterpret_cast<double*>(dsys);
         Sa.out_status = dsys + st_off;
-        Sa.placed = reinterpret_cast<uint32_t*>(dsys + bytes - 4);
+        Sa.placed = nullptr;   // counted from the outcomes below
         Sa.commit = 1;
         if (m) HIP_TRY(s, pe_launch_system(&Sa, x->stream));
         HIP_TRY(s, hipMemcpyAsync(x->h_sys_out.p, dsys, bytes, hipMemcpyDeviceToHost, x->stream));

@@ -249,6 +249,7 @@ struct PreemptAlloc {
     uint32_t state_index;    // row of the pe_alloc_table snapshot; bit 31 kAllocHasNet
 };
 constexpr uint32_t kAllocHasNet = 1u << 31;   // Flattened.Networks non-empty (PreemptForNetwork)
+constexpr uint32_t kPlacedSlots = 64;          // SystemArgs.placed: counters the host sums
 static_assert(sizeof(PreemptAlloc) == 64, "PreemptAlloc is one 64-byte line");
 
 struct PreemptArgs {

@@ -2001,6 +2001,21 @@ __global__ void __launch_bounds__(256) k_emit_writeback(BatchArgs A) {
     if (A.ask.n_dev > 0) A.tg.dev_free[e.x] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[e.x], e.y);
 }
 
+// The placed count of a 256-lane workgroup, one atomic per workgroup into one
+// of kPlacedSlots counters (the host sums them): same-address atomics from
+// every wave serialise at one L2 channel (32k of them at 6.4M rows cost more
+// than the evaluation).
+__device__ __forceinline__ void add_placed(uint32_t local, uint32_t* slots) {
+    __shared__ uint32_t red[4];
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_xor(local, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = local;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t x = red[0] + red[1] + red[2] + red[3];
+        if (x) atomicAdd(&slots[blockIdx.x % kPlacedSlots], x);
+    }
+}
+
 // SystemStack: every list entry is an independent single-node Select.
 __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -2032,8 +2047,7 @@ __global__ void __launch_bounds__(256) k_system(SystemArgs A) {
             A.out_status[i] = (uint8_t)ev.status;
         }
     }
-    for (int off = 32; off > 0; off >>= 1) local += __shfl_xor(local, off);
-    if ((threadIdx.x & 63) == 0 && local) atomicAdd(A.placed, local);
+    if (A.placed) add_placed(local, A.placed);
 }
 
 // k_system in row order, phase one: every row of the list evaluated (and
@@ -2073,10 +2087,21 @@ __global__ void __launch_bounds__(256) k_system_rows(SystemArgs A) {
         A.tg.coll_tg[row] += 1;
         if (A.ask.n_dev > 0) A.tg.dev_free[row] = dev_after(A.ask, A.tg.dev_cls[r.cls], A.tg.dev_free[row], 1);
     }
-    if (A.placed) {
-        for (int off = 32; off > 0; off >>= 1) local += __shfl_xor(local, off);
-        if ((threadIdx.x & 63) == 0 && local) atomicAdd(A.placed, local);
-    }
+    if (A.placed) add_placed(local, A.placed);
+}
+
+// Phase two of the row-order pass: the outcomes back in list order. Reads the
+// list coalesced and res[list[pos]] (8 B per row, L2 / MALL resident), writes
+// FinalScore and the outcome coalesced; random 8-byte stores into the outputs
+// would cost a 64-byte line write each.
+__global__ void __launch_bounds__(256) k_system_gather(const uint32_t* list, uint32_t n_list, const uint64_t* res,
+                                                      double* out_score, uint8_t* out_status) {
+    const uint32_t pos = blockIdx.x * 256 + threadIdx.x;
+    if (pos >= n_list) return;
+    const uint64_t v = res[list[pos]];
+    const bool boxed = (v & 0xFFFFFFFFFFFFFFF0ull) == 0x7FF8000000000000ull;
+    out_score[pos] = boxed ? __builtin_nan("") : __longlong_as_double((long long)v);
+    out_status[pos] = boxed ? (uint8_t)(v & 15u) : (uint8_t)kOption;
 }
 
 // rank_of[row] = position of row in the list (rows absent: PE_NONE, set by the caller's memset)
@@ -3110,7 +3135,19 @@ hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st) {
         uint32_t b1 = (a->n_rows + 255) / 256;
         if (b1 > 8192) b1 = 8192;
         if (b1 == 0) b1 = 1;
-        hipLaunchKernelGGL(pe::k_system_rows, dim3(b1), dim3(256), 0, st, *a);
+        static const bool scatter = [] {
+            const char* e = std::getenv("PE_SYS_SCATTER");
+            return e && e[0] == '1';
+        }();
+        if (scatter || !a->n_list) {   // outcomes stored at list positions directly (or kept by row)
+            hipLaunchKernelGGL(pe::k_system_rows, dim3(b1), dim3(256), 0, st, *a);
+            return hipGetLastError();
+        }
+        pe::SystemArgs r = *a;
+        r.n_list = 0;   // outcomes by row into res
+        hipLaunchKernelGGL(pe::k_system_rows, dim3(b1), dim3(256), 0, st, r);
+        hipLaunchKernelGGL(pe::k_system_gather, dim3((a->n_list + 255) / 256), dim3(256), 0, st, a->list, a->n_list,
+                           a->res, a->out_score, a->out_status);
         return hipGetLastError();
     }
     uint32_t blocks = (a->n_list + 255) / 256;

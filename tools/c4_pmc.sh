@@ -18,7 +18,8 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/writ
 cd "$ROOT"
 F=$(find "$OUT/fetch" -name "*counter_collection.csv" -print -quit)
 W=$(find "$OUT/write" -name "*counter_collection.csv" -print -quit)
-python3 tools/pmc_traffic.py "$F" "$W" "k_system" 100000 73 "$OUT/system_traffic.json"
+python3 tools/pmc_traffic.py "$F" "$W" "k_system_rows" 100000 73 "$OUT/system_rows_traffic.json"
+python3 tools/pmc_traffic.py "$F" "$W" "k_system_gather" 100000 21 "$OUT/system_gather_traffic.json" || true
 cat "$OUT/sizes.jsonl"
 find "$OUT/stats" -name "*kernel_stats.csv" -exec cp {} "$OUT/c4_kernel_stats.csv" \;
 head -5 "$OUT/c4_kernel_stats.csv"
