@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 4u
+#define PE_ABI_VERSION 5u
 #define PE_NONE 0xFFFFFFFFu
 #define PE_MAX_SCORES 8
 #define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried per RankedNode */
@@ -116,6 +116,12 @@ typedef struct pe_node_table {
     const uint32_t* addr_off; const uint32_t* addr_alias; const uint32_t* addr_ip;
     const uint32_t* addr_rsv_ports;
     const uint32_t* rsv_host_ports;
+    /* NodeResources.Networks[*] addresses (str ids, per net_off entry): the IP
+       field (PE_NONE = "") and the one address AssignNetwork yields from the
+       CIDR (yieldIP, network.go:294-315; PE_NONE when the CIDR does not parse
+       or holds more than one address). NULL: unknown (task-level static ports
+       are then not on the device path) */
+    const uint32_t* net_ip; const uint32_t* net_cidr_ip;
 } pe_node_table;
 
 /* ---- existing allocations of the snapshot (state AllocsByNode) ---------- */
@@ -181,6 +187,9 @@ typedef struct pe_task {
     uint32_t constraint_off, constraint_count;
     uint32_t affinity_off, affinity_count;
     uint32_t device_off, device_count;
+    uint32_t rport_off;                       /* the task network's ReservedPorts (static ports):
+                                                 pe_job.rport_value / rport_label [rport_off,
+                                                 rport_off + net_reserved_ports) */
 } pe_task;
 typedef struct pe_task_group {
     uint32_t name; int32_t count;

@@ -56,6 +56,7 @@ class pe_node_table(C.Structure):
         ("rsv_core_off", u32p), ("rsv_core_id", u16p),
         ("addr_off", u32p), ("addr_alias", u32p), ("addr_ip", u32p), ("addr_rsv_ports", u32p),
         ("rsv_host_ports", u32p),
+        ("net_ip", u32p), ("net_cidr_ip", u32p),
     ]
 
 
@@ -109,6 +110,7 @@ class pe_task(C.Structure):
         ("constraint_off", C.c_uint32), ("constraint_count", C.c_uint32),
         ("affinity_off", C.c_uint32), ("affinity_count", C.c_uint32),
         ("device_off", C.c_uint32), ("device_count", C.c_uint32),
+        ("rport_off", C.c_uint32),
     ]
 
 

@@ -181,6 +181,10 @@ struct HostNode {
     int32_t first_mbits;
     uint32_t first_dev;    // string id of the first host network device (PE_NONE: none)
     uint16_t n_device_nets, n_devices;
+    // that network's IP field and the one address AssignNetwork yields from its
+    // CIDR (PE_NONE: none, or not known / not one address)
+    uint32_t first_ipfield = PE_NONE, first_yield = PE_NONE;
+    bool yield_known = false;
 };
 
 template <class T>
@@ -310,6 +314,13 @@ struct TgPlan {
     // static port asks (tg network ReservedPorts): (value, label) and the per-node gate
     std::vector<std::pair<int32_t, uint32_t>> rports;
     DevMem static_gate, static_blocked;
+    // the task network's ReservedPorts (AssignNetwork, network.go:407-442) and their gate
+    std::vector<std::pair<int32_t, uint32_t>> trports;
+    DevMem task_gate, task_blocked;
+    // PreemptForNetwork's reserved-port step per node (host-built, preemption.go:
+    // 309-342): the holders to preempt first (CSR-relative alloc indices, one
+    // byte each, in ask order) and flags (kPort*)
+    DevMem port_list, port_info, port_block;
     std::vector<std::unique_ptr<PsetDev>> psets;
     bool psets_built = false;
     bool elig_complete = false;   // every class's EvalEligibility entries are known (pe_get_eligibility)
@@ -330,6 +341,8 @@ struct TgPlan {
     DevMem node_aux, aff_vals, aff_idx;
     bool aux_valid = false, aux_ok = false;
 };
+
+static inline bool has_static(const TgPlan& g) { return !g.rports.empty() || !g.trports.empty(); }
 
 }  // namespace
 
@@ -437,6 +450,7 @@ struct pe_stack {
     DevMem d_rec, d_base_rec, d_coll_job;
     DevMem d_base;                     // windowed loops: per-row base value table
     DevMem d_base1;                    // the same with one placement on the row
+    DevMem d_chain_vs;                 // k_chain per-workgroup scratch (window values by position)
     DevMem d_prof;                     // k_chain step profile (PE_CHAIN_PROF)
     bool orders_unique = true;         // every staged order lists each row at most once
     bool use_base = true;              // PE_WINDOW_LAZY=1: lazy per-position evaluation (k_window)
@@ -515,6 +529,7 @@ struct pe_stack {
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
     DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;  // device-resident parallel count loop (k_ploop)
+    DevMem d_ploop_parts, d_ploop_nparts;   // k_ploop: Preempt records per position (parts, count)
 
     // Speculative count loop behind pe_select / pe_commit: the
     // first plain Select of a task group runs the device count loop for the
@@ -1251,9 +1266,16 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         h.n_device_nets = 0;
         h.first_mbits = -1;
         h.first_dev = PE_NONE;
+        h.first_ipfield = h.first_yield = PE_NONE;
+        h.yield_known = false;
         for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++) {
             if (!s->S(nt->net_device[k]).empty()) {
-                if (h.n_device_nets == 0) { h.first_mbits = nt->net_mbits[k]; h.first_dev = nt->net_device[k]; }
+                if (h.n_device_nets == 0) {
+                    h.first_mbits = nt->net_mbits[k];
+                    h.first_dev = nt->net_device[k];
+                    if (nt->net_ip) h.first_ipfield = nt->net_ip[k];
+                    if (nt->net_cidr_ip) { h.first_yield = nt->net_cidr_ip[k]; h.yield_known = h.first_yield != PE_NONE; }
+                }
                 h.n_device_nets++;
             }
         }
@@ -1691,7 +1713,7 @@ std::unique_ptr<TgPlan> new_tg(pe_stack* s) {
 // false when they fit. The used ports of an address: the node's reservations
 // for its IP, ReservedHostPorts, the ports the proposed snapshot allocs hold
 // on it (plan stops and preemptions excluded).
-bool static_port_reason(pe_stack* s, const TgPlan& g, uint32_t row, std::string* why) {
+bool static_port_reason(pe_stack* s, const TgPlan& g, uint32_t row, std::string* why, uint32_t excl = 0) {
     const HostAddr* ad = nullptr;
     if (row < s->node_addrs.size())
         for (const HostAddr& a : s->node_addrs[row]) if (a.alias == g.net_host) { ad = &a; break; }
@@ -1711,6 +1733,8 @@ bool static_port_reason(pe_stack* s, const TgPlan& g, uint32_t row, std::string*
             used = used || std::binary_search(s->node_rhp[row].begin(), s->node_rhp[row].end(), rp.first);
         for (uint32_t k = s->h_node_alloc_off[row]; k < s->h_node_alloc_off[row + 1] && !used; k++) {
             if (s->h_preempted[k]) continue;   // a plan stop (2) or preemption (1)
+            const uint32_t rel = k - s->h_node_alloc_off[row];
+            if (rel < 32 && ((excl >> rel) & 1u)) continue;   // preempted by the Select being evaluated
             const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
             for (uint32_t q = a.port_begin; q < a.port_end; q++)
                 used = used || (s->alloc_ports[q].first == ad->ip && s->alloc_ports[q].second == rp.first);
@@ -1726,15 +1750,149 @@ bool static_port_reason(pe_stack* s, const TgPlan& g, uint32_t row, std::string*
 
 // The collision text when the group's own placement holds the ports (its first static port).
 std::string static_port_collision(pe_stack* s, const TgPlan& g) {
-    if (g.rports.empty()) return "reserved port collision";
-    const auto& rp = g.rports.front();
+    const auto& ports = g.rports.empty() ? g.trports : g.rports;
+    if (ports.empty()) return "reserved port collision";
+    const auto& rp = ports.front();
     return "reserved port collision " + (rp.second == PE_NONE ? std::string() : s->S(rp.second)) + "=" +
            std::to_string(rp.first);
 }
 
+// AssignNetwork's ReservedPorts check (network.go:407-442) for the task
+// network's static ports on the node's one device network: the address yieldIP
+// gives from its CIDR. UsedPorts[ip] holds the ReservedPorts of node addresses
+// with that IP, ReservedHostPorts when the IP is a key SetNode created (the
+// network's IP field or an address, network.go:92-141, 238-265), and the ports
+// the proposed allocs hold on it (minus `excl`, CSR-relative).
+bool task_port_reason(pe_stack* s, const TgPlan& g, uint32_t row, std::string* why, uint32_t excl = 0) {
+    const HostNode& h = s->nodes[row];
+    if (h.n_device_nets == 0 || g.trports.empty()) return false;   // "no networks available" is the device's
+    const uint32_t ip = h.first_yield;
+    bool keyed = ip == h.first_ipfield;
+    if (row < s->node_addrs.size())
+        for (const HostAddr& a : s->node_addrs[row]) keyed = keyed || a.ip == ip;
+    for (const auto& rp : g.trports) {
+        if (rp.first < 0 || rp.first >= 65536) {
+            if (why) *why = "invalid port " + std::to_string(rp.first) + " (out of range)";
+            return true;
+        }
+        bool used = false;
+        if (row < s->node_addrs.size())
+            for (const HostAddr& a : s->node_addrs[row])
+                if (a.ip == ip) used = used || std::binary_search(a.reserved.begin(), a.reserved.end(), rp.first);
+        if (keyed && row < s->node_rhp.size())
+            used = used || std::binary_search(s->node_rhp[row].begin(), s->node_rhp[row].end(), rp.first);
+        for (uint32_t k = s->h_node_alloc_off[row]; k < s->h_node_alloc_off[row + 1] && !used; k++) {
+            if (s->h_preempted[k]) continue;
+            const uint32_t rel = k - s->h_node_alloc_off[row];
+            if (rel < 32 && ((excl >> rel) & 1u)) continue;
+            const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+            for (uint32_t q = a.port_begin; q < a.port_end; q++)
+                used = used || (s->alloc_ports[q].first == ip && s->alloc_ports[q].second == rp.first);
+        }
+        if (used) {
+            if (why) *why = "reserved port collision " + (rp.second == PE_NONE ? std::string() : s->S(rp.second)) + "=" +
+                            std::to_string(rp.first);
+            return true;
+        }
+    }
+    return false;
+}
+
+// PreemptForNetwork's reserved-port step (preemption.go:302-342) for the
+// static ask of `g` on one node, as the device's preempt_for_network consumes
+// it: candidates are the node's proposed state allocs outside the job;
+// usedPortToAlloc maps every ReservedPorts value of a preemptible candidate with
+// a network to its last holder in candidate order, filteredReservedPorts the
+// values of the others with a network. Then whether the static ports still
+// collide once the listed holders leave (node reservations, remaining allocs,
+// this group's own placements).
+// The static ports' blockers on the node for the retried offer: allocs of the
+// node (CSR-relative bits) that hold a needed port on the address the ask
+// takes, and whether anything that no preemption removes blocks one (a node
+// reservation, an invalid port, no address, an alloc of the job itself).
+static uint32_t port_blockers(pe_stack* s, const TgPlan& g, uint32_t row, bool* permanent) {
+    *permanent = false;
+    const bool task = g.rports.empty();
+    uint32_t ip = PE_NONE;
+    bool keyed = true;   // ReservedHostPorts apply (always for an address)
+    if (task) {
+        const HostNode& h = s->nodes[row];
+        if (h.n_device_nets == 0) return 0;
+        ip = h.first_yield;
+        keyed = ip == h.first_ipfield;
+        if (row < s->node_addrs.size())
+            for (const HostAddr& a : s->node_addrs[row]) keyed = keyed || a.ip == ip;
+    } else {
+        if (row < s->node_addrs.size())
+            for (const HostAddr& a : s->node_addrs[row]) if (a.alias == g.net_host) { ip = a.ip; break; }
+        if (ip == PE_NONE) { *permanent = true; return 0; }
+    }
+    const auto& ports = task ? g.trports : g.rports;
+    const uint32_t b = s->h_node_alloc_off[row], e = s->h_node_alloc_off[row + 1];
+    uint32_t mask = 0;
+    for (const auto& rp : ports) {
+        if (rp.first < 0 || rp.first >= 65536) { *permanent = true; continue; }
+        if (row < s->node_addrs.size())
+            for (const HostAddr& a : s->node_addrs[row])
+                if (a.ip == ip && std::binary_search(a.reserved.begin(), a.reserved.end(), rp.first)) *permanent = true;
+        if (keyed && row < s->node_rhp.size() &&
+            std::binary_search(s->node_rhp[row].begin(), s->node_rhp[row].end(), rp.first))
+            *permanent = true;
+        for (uint32_t k = b; k < e; k++) {
+            if (s->h_preempted[k]) continue;
+            const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+            bool holds = false;
+            for (uint32_t q = a.port_begin; q < a.port_end; q++)
+                holds = holds || (s->alloc_ports[q].first == ip && s->alloc_ports[q].second == rp.first);
+            if (!holds) continue;
+            if ((a.job == s->job_id && a.ns == s->job_ns) || k - b >= 32) *permanent = true;
+            else mask |= 1u << (k - b);
+        }
+    }
+    return mask;
+}
+
+static void port_step(pe_stack* s, const TgPlan& g, uint32_t row, bool own_placed, uint64_t* list, uint8_t* info,
+                      uint32_t* blockers) {
+    *list = ~0ull;
+    *info = 0;
+    *blockers = 0;
+    const auto& ports = g.rports.empty() ? g.trports : g.rports;
+    const uint32_t b = s->h_node_alloc_off[row], e = s->h_node_alloc_off[row + 1];
+    if (e - b > (uint32_t)pe::kMaxNodeAllocs) return;   // the device refuses the node itself
+    std::map<int32_t, uint32_t> holder;
+    std::set<int32_t> filtered;
+    for (uint32_t k = b; k < e; k++) {
+        if (s->h_preempted[k]) continue;
+        const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+        if ((a.job == s->job_id && a.ns == s->job_ns) || !a.has_net) continue;
+        const bool pre = s->job_priority - a.priority >= 10;
+        for (uint32_t q = a.port_begin; q < a.port_end; q++) {
+            if (pre) holder[s->alloc_ports[q].second] = k - b;
+            else filtered.insert(s->alloc_ports[q].second);
+        }
+    }
+    uint32_t n = 0, mask = 0;
+    for (const auto& rp : ports) {
+        auto it = holder.find(rp.first);
+        if (it != holder.end()) {
+            if (((mask >> it->second) & 1u) || n >= 8) { *info = pe::kPortUnsup; return; }
+            mask |= 1u << it->second;
+            *list = (*list & ~(0xFFull << (8 * n))) | ((uint64_t)it->second << (8 * n));
+            n++;
+        } else if (filtered.count(rp.first)) {
+            *info = pe::kPortFail;
+            return;
+        }
+    }
+    bool permanent = false;
+    *blockers = port_blockers(s, g, row, &permanent);
+    *info = (uint8_t)(n | ((own_placed || permanent) ? pe::kPortBlocked : 0u));
+}
+
 // Static port gates follow ProposedAllocs: stops and evictions free ports.
 void invalidate_static(pe_stack* s) {
-    for (auto& g : s->tgs) if (!g->rports.empty()) g->tables_valid = false;
+    for (auto& g : s->tgs) if (has_static(*g)) g->tables_valid = false;
 }
 
 pe::NodeSoA soa_of(pe_stack* s) {
@@ -2207,20 +2365,34 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         HIP_TRY(s, upload_s(s, g.alias_ok, al));
         g.alias_used = true;
     }
-    if (!g.rports.empty()) {
-        // AssignPorts' static ports (network.go:317-363) on the current plan: a
-        // node is blocked when a port is invalid, its host network has no
-        // address, or the port is used on that address (the node's reservations,
-        // ReservedHostPorts, the proposed snapshot allocs, this group's
-        // placements). The device adds the group's later placements (gate).
-        std::vector<uint8_t> blocked(n, 0);
-        for (uint32_t r = 0; r < (uint32_t)n; r++) blocked[r] = static_port_reason(s, g, r, nullptr) ? 1 : 0;
+    if (has_static(g)) {
+        // AssignPorts' static ports (network.go:317-363) or the task network's
+        // (AssignNetwork, :407-442) on the current plan: a node is blocked when a
+        // port is invalid, its host network has no address, or the port is used
+        // on that address (the node's reservations, ReservedHostPorts, the
+        // proposed snapshot allocs, this group's placements). The device adds
+        // the group's later placements (gate).
+        std::vector<uint8_t> own(n, 0), blocked(n, 0);
         for (auto& p : s->plan)
-            if (p.first == g.name && p.second < n) blocked[p.second] = 1;
-        HIP_TRY(s, upload_s(s, g.static_blocked, blocked));
-        HIP_TRY(s, g.static_gate.ensure(sizeof(uint32_t) * std::max<size_t>(n, 1)));
-        HIP_TRY(s, pe_launch_static_gate(g.static_blocked.as<uint8_t>(), g.coll_tg.as<uint32_t>(),
-                                         g.static_gate.as<uint32_t>(), (uint32_t)n, s->stream));
+            if (p.first == g.name && p.second < n) own[p.second] = 1;
+        const bool task = g.rports.empty();
+        for (uint32_t r = 0; r < (uint32_t)n; r++)
+            blocked[r] = (own[r] || (task ? task_port_reason(s, g, r, nullptr) : static_port_reason(s, g, r, nullptr)))
+                             ? 1 : 0;
+        DevMem& gate = task ? g.task_gate : g.static_gate;
+        DevMem& bl = task ? g.task_blocked : g.static_blocked;
+        HIP_TRY(s, upload_s(s, bl, blocked));
+        HIP_TRY(s, gate.ensure(sizeof(uint32_t) * std::max<size_t>(n, 1)));
+        HIP_TRY(s, pe_launch_static_gate(bl.as<uint8_t>(), g.coll_tg.as<uint32_t>(), gate.as<uint32_t>(), (uint32_t)n,
+                                         s->stream));
+        // PreemptForNetwork's reserved-port step per node, for Selects with Preempt
+        std::vector<uint64_t> plist(n);
+        std::vector<uint8_t> pinfo(n);
+        std::vector<uint32_t> pblock(n);
+        for (uint32_t r = 0; r < (uint32_t)n; r++) port_step(s, g, r, own[r] != 0, &plist[r], &pinfo[r], &pblock[r]);
+        HIP_TRY(s, upload_s(s, g.port_list, plist));
+        HIP_TRY(s, upload_s(s, g.port_info, pinfo));
+        HIP_TRY(s, upload_s(s, g.port_block, pblock));
     }
     g.tables_valid = true;
     return PE_OK;
@@ -2236,6 +2408,10 @@ pe::TgTables tables_of(TgPlan& g) {
     t.node_aff = g.node_aff_used ? g.node_aff.as<double>() : nullptr;
     t.alias_ok = g.alias_used ? g.alias_ok.as<uint8_t>() : nullptr;
     t.static_gate = g.rports.empty() ? nullptr : g.static_gate.as<uint32_t>();
+    t.task_gate = g.trports.empty() ? nullptr : g.task_gate.as<uint32_t>();
+    t.port_list = has_static(g) ? g.port_list.as<uint64_t>() : nullptr;
+    t.port_info = has_static(g) ? g.port_info.as<uint8_t>() : nullptr;
+    t.port_block = has_static(g) ? g.port_block.as<uint32_t>() : nullptr;
     t.coll_tg = g.coll_tg.as<uint32_t>();
     if (!g.dev_reqs.empty()) {
         t.dev_free = g.dev_free;
@@ -2630,7 +2806,6 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     *new_offset = n ? offset % n : 0;
     if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
     if (g.ask.cores > 0) return s->fail(PE_EUNSUPPORTED, "reserved cores with preemption");
-    if (!g.rports.empty()) return s->fail(PE_EUNSUPPORTED, "static port asks with preemption (PreemptForNetwork)");
     if (n == 0) return PE_OK;
     pe::PreemptArgs P = preempt_args(s, g);
     HIP_TRY(s, upload_visit(s, order));
@@ -2774,6 +2949,8 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             A.base_by_pos = 1;
             HIP_TRY(s, s->d_base1.ensure(sizeof(double) * std::max<size_t>(n, 1)));
             A.base1 = s->d_base1.as<double>();
+            HIP_TRY(s, s->d_chain_vs.ensure(sizeof(double) * (size_t)pe_chain_max_n()));
+            A.chain_vs = s->d_chain_vs.as<double>();
             if (std::getenv("PE_CHAIN_PROF")) {
                 HIP_TRY(s, s->d_prof.ensure(32 * sizeof(unsigned long long)));
                 HIP_TRY(s, hipMemset(s->d_prof.p, 0, 32 * sizeof(unsigned long long)));
@@ -3438,7 +3615,17 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
             for (uint32_t d = 0; d < x.device_count; d++)
                 g->dev_reqs.push_back(parse_dev_request(s, j, j->devices[x.device_off + d]));
             if (x.cores > 0 && x.lifecycle != PE_LC_MAIN) g->unsupported = "reserved cores on a lifecycle hook task";
-            if (x.has_network && x.net_reserved_ports > 0) g->unsupported = "static port asks";
+            if (x.has_network && x.net_reserved_ports > 0) {
+                if (!g->trports.empty()) g->unsupported = "static ports in several task networks";
+                else if (!j->rport_value) g->unsupported = "task static ports without their values (pe_task.rport_off)";
+                else
+                    for (int32_t q = 0; q < x.net_reserved_ports; q++) {
+                        const int32_t v = j->rport_value[x.rport_off + (uint32_t)q];
+                        // a static port in the dynamic range shrinks the task's dynamic picks: not modelled
+                        if (v >= 20000 && v <= 32000) g->unsupported = "task static ports in the dynamic port range";
+                        g->trports.emplace_back(v, j->rport_label ? j->rport_label[x.rport_off + (uint32_t)q] : PE_NONE);
+                    }
+            }
         }
         if (g->ask.cores > 0)   // the per-node ask is Σ main tasks + SharesPerCore x cores (no max over hooks)
             for (uint32_t k = 0; k < t.task_count; k++) {
@@ -3457,6 +3644,8 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
             g->rports.emplace_back(j->rport_value[t.rport_off + k], j->rport_label ? j->rport_label[t.rport_off + k] : PE_NONE);
         if (t.has_network && (int64_t)g->rports.size() != (int64_t)t.net_reserved_ports)
             g->unsupported = "static port asks without their values (pe_task_group.rport_*)";
+        if (!g->rports.empty() && !g->trports.empty())
+            g->unsupported = "static ports in the task group network and a task network";
         // affinities: job, task group, tasks (rank.go:671-686)
         g->affinities = s->job_affinities;
         for (uint32_t k = 0; k < t.affinity_count; k++)
@@ -3495,10 +3684,18 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     }
     {   // static ports of one group only: a sibling's placements would hold them too
         int with_static = 0;
-        for (auto& g : s->tgs) with_static += g->rports.empty() ? 0 : 1;
+        for (auto& g : s->tgs) with_static += has_static(*g) ? 1 : 0;
         if (with_static > 1)
             for (auto& g : s->tgs)
-                if (!g->rports.empty()) g->unsupported = "static port asks in several task groups of a job";
+                if (has_static(*g)) g->unsupported = "static port asks in several task groups of a job";
+    }
+    for (auto& g : s->tgs) {   // AssignNetwork's address: the network CIDR's one address on every node
+        if (g->trports.empty()) continue;
+        for (auto& nd : s->nodes)
+            if (nd.n_device_nets > 0 && !nd.yield_known) {
+                g->unsupported = "task static ports on a network whose CIDR is not one known address";
+                break;
+            }
     }
     if (!generic) s->job_spreads.clear();
     // task networks must resolve against a single host device network on every node
@@ -3849,6 +4046,12 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                     exhaust(row, "network: " + why);
                     break;
                 }
+                case pe::kTrTaskStatic: {
+                    std::string why;
+                    if (!task_port_reason(s, g, row, &why)) why = static_port_collision(s, g);
+                    exhaust(row, "network: " + why);
+                    break;
+                }
                 case pe::kTrDynPorts: exhaust(row, "network: dynamic port selection failed"); break;
                 case pe::kTrNoNetworks: exhaust(row, "network: no networks available"); break;
                 case pe::kTrBandwidth: exhaust(row, "network: bandwidth exceeded"); break;
@@ -3922,7 +4125,7 @@ static int sys_flush(pe_stack* s) {
 // an escaped group), and the result record the cache holds complete (no
 // device offers, reserved cores or static ports to return).
 static bool sys_cacheable(pe_stack* s, TgPlan& g) {
-    return g.unsupported.empty() && g.psets.empty() && g.dev_reqs.empty() && g.ask.cores == 0 && g.rports.empty() &&
+    return g.unsupported.empty() && g.psets.empty() && g.dev_reqs.empty() && g.ask.cores == 0 && !has_static(g) &&
            (g.escaped || g.nonuniform.empty()) && s->visit_unique;
 }
 
@@ -4267,7 +4470,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     if (!count || (std::getenv("PE_PLOOP") && std::getenv("PE_PLOOP")[0] == '0')) return PE_OK;
     if (!g.psets.empty() || g.psets_dynamic || !s->visit_unique || n == 0 || n > pe_ploop_max_n()) return PE_OK;
     if (g.ask.cores > 0) return PE_OK;   // k_ploop is compiled without reserved cores
-    if (!g.rports.empty()) return PE_OK;  // the static port gate is rebuilt on the host after evictions
+    if (has_static(g)) return PE_OK;  // the static port gate is rebuilt on the host after evictions
     for (size_t k = 0; k < s->tgs.size(); k++)
         if (k != tgi && s->tgs[k]->name == g.name) return PE_OK;
     if (retry && !s->preempt_unsupported.empty()) return PE_OK;
@@ -4302,6 +4505,16 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         HIP_TRY(s, s->d_ev_dep.ensure(n));
         L.P.dep_out = s->d_ev_dep.as<uint8_t>();
         L.dep_init = L.P.dep_out;
+        // the Preempt record of every position is kept (and refreshed with its
+        // outcome): a Preempt winner's record is then read, not re-evaluated
+        HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * (size_t)n));
+        HIP_TRY(s, s->d_ev_offers.ensure(sizeof(uint32_t) * (size_t)n));
+        HIP_TRY(s, s->d_ploop_parts.ensure(sizeof(double) * PE_MAX_SCORES * (size_t)n));
+        HIP_TRY(s, s->d_ploop_nparts.ensure(n));
+        L.P.mask_out = s->d_ev_masks.as<uint32_t>();
+        L.P.offers_out = s->d_ev_offers.as<uint32_t>();
+        L.P.parts_out = s->d_ploop_parts.as<double>();
+        L.P.nparts_out = s->d_ploop_nparts.as<uint8_t>();
         HIP_TRY(s, pe_launch_evict_only(&L.P, s->stream));
         L.P.dep_out = nullptr;
         uint32_t flags = 0;
@@ -4350,8 +4563,10 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         unsigned long long h[8];
         HIP_TRY(s, hipMemcpy(h, L.prof, sizeof(h), hipMemcpyDeviceToHost));
         std::fprintf(stderr, "k_ploop: %u placements, %.3f ms total; us: plain resolve %.1f, refresh %.1f, preempt "
-                             "resolve %.1f, winner %.1f; refreshed %llu dirty + %llu pcount readers\n",
-                     st[0], ms, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[4], h[5]);
+                             "resolve %.1f, winner %.1f (its evict_eval %.1f, commit %.1f); refreshed %llu dirty + %llu pcount "
+                             "readers\n",
+                     st[0], ms, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[6] / 100.0, h[7] / 100.0, h[4],
+                     h[5]);
     }
     *handled = true;
     const uint32_t p = std::min(st[0], count);
@@ -4571,6 +4786,10 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
             s->offers = pack_offers(&out[p]);
             rc = commit_preempt_impl(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
             if (rc) return rc;
+            if (has_static(g)) {   // the evictions freed ports: the gates and port records again
+                rc = prepare_tg(s, tgi, s->visit, s->offset);
+                if (rc) return rc;
+            }
             p++;
         }
         count = 0;   // done: skip the fused loop below
@@ -4610,6 +4829,10 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
             s->offers = pack_offers(&out[p]);
             rc = commit_preempt_impl(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
             if (rc) return rc;
+            if (has_static(g)) {   // the evictions freed ports: the gates and port records again
+                rc = prepare_tg(s, tgi, s->visit, s->offset);
+                if (rc) return rc;
+            }
             p++;
             if (p == count) break;
             if (!g.psets.empty()) {   // spread / distinct counts: the fused count loop
@@ -5048,7 +5271,7 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     if (!tg_full_scan(s, g)) return s->fail(PE_EUNSUPPORTED, "sharded placement: a windowed task group (replicas only)");
-    if (g.ask.cores > 0 || !g.rports.empty())
+    if (g.ask.cores > 0 || has_static(g))
         return s->fail(PE_EUNSUPPORTED, "sharded placement with reserved cores or static ports");
     if (!s->visit_unique) return s->fail(PE_EUNSUPPORTED, "sharded placement needs a list without repeated rows");
     if (g.n_spread != (int)g.psets.size() || g.psets_dynamic)
@@ -5233,6 +5456,8 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
         s->batch_chain = true;
         const size_t lds = pe_chain_lds_bytes(A.hash_bits, A.packed_overlay != 0, n);
         s->chain_grid = (uint32_t)(pe_chain_blocks_per_cu(lds) * s->n_cu);
+        HIP_TRY(s, s->d_chain_vs.ensure(sizeof(double) * (size_t)pe_chain_max_n() * s->chain_grid));
+        A.chain_vs = s->d_chain_vs.as<double>();
     }
     HIP_TRY(s, s->d_batch_out.ensure(sizeof(pe_placement) * (size_t)E * std::max<uint32_t>(count, 1)));
     HIP_TRY(s, s->d_batch_status.ensure(sizeof(uint32_t) * 2 * (size_t)E));
@@ -5534,7 +5759,6 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
         if (!rows.empty()) {
             if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
             if (g.ask.cores > 0) return s->fail(PE_EUNSUPPORTED, "reserved cores with preemption");
-            if (!g.rports.empty()) return s->fail(PE_EUNSUPPORTED, "static port asks with preemption (PreemptForNetwork)");
             // the max_parallel penalty reads the plan's preemption counts, which
             // earlier nodes grow: then the nodes go one at a time in list order
             bool serial = false;
@@ -5963,7 +6187,7 @@ static bool multi_place_ok(pe_stack* s, uint32_t tgi, uint32_t count) {
         return false;
     if (prepare_tg(s, tgi, s->visit, s->offset) != PE_OK) { s->err.clear(); return false; }
     TgPlan& g = *s->tgs[tgi];
-    if (!tg_full_scan(s, g) || g.ask.cores > 0 || !g.rports.empty() || !s->visit_unique) return false;
+    if (!tg_full_scan(s, g) || g.ask.cores > 0 || has_static(g) || !s->visit_unique) return false;
     if (g.n_spread != (int)g.psets.size() || g.psets_dynamic || s->cfg.preempt) return false;
     for (size_t k = 0; k < s->tgs.size(); k++)
         if (k != tgi && s->tgs[k]->name == g.name) return false;

@@ -27,6 +27,7 @@ enum : uint32_t {
     kTrOption = 0, kTrDistinctHosts = 1, kTrDistinctProp = 2,
     kTrNoAddr = 10, kTrDynPorts = 11, kTrNoNetworks = 12, kTrBandwidth = 13, kTrTaskDyn = 14,
     kTrStaticPort = 15,         // the reason string is rebuilt on the host (static_port_reason)
+    kTrTaskStatic = 16,         // the task network's static ports (task_port_reason)
     kTrDevNone = 20, kTrDevZero = 21, kTrDevNoMatch = 22,
     kTrCpu = 30, kTrMemory = 31, kTrDisk = 32, kTrCores = 33,
     kTrMismatch = 254,          // device verdict disagrees with the host walk (bug guard)
@@ -67,6 +68,12 @@ struct NodeSoA {
 };
 
 // Per (job, task group) feasibility / affinity / spread tables for a Select.
+// kPort* flags of TgTables.port_info
+constexpr uint8_t kPortCount = 0x0F;     // holders listed
+constexpr uint8_t kPortFail = 0x10;      // a needed port is held by an alloc too close in priority: nil
+constexpr uint8_t kPortBlocked = 0x20;   // a needed port is blocked by what no preemption removes
+constexpr uint8_t kPortUnsup = 0x40;     // one alloc holds two ports of the ask, or too many holders
+
 struct TgTables {
     const uint8_t* class_ok;     // [ncls] memoised job+tg feasibility per class
     const uint8_t* node_ok;      // [n] or null: per-node verdict (escaped constraints)
@@ -77,6 +84,13 @@ struct TgTables {
     uint32_t* coll_tg;           // [n] proposed allocs of (job, tg) per node
     const uint32_t* static_gate; // [n] or null: static port asks; 0 = a port is taken (or no address), else
                                  // coll_tg + 1 when the gate was built (a later placement of the group holds them)
+    const uint32_t* task_gate;   // [n] or null: the same for the task network's static ports (AssignNetwork)
+    // [n] or null: PreemptForNetwork's reserved-port step of the static ask
+    // (group or task network): holders to preempt first (CSR-relative alloc
+    // indices, one byte each, ask order) and kPort* flags
+    const uint64_t* port_list;
+    const uint8_t* port_info;
+    const uint32_t* port_block;  // [n] or null: allocs (CSR-relative bits) holding a needed port on the ask's address
     int n_psets;                                 // spread property sets first, then distinct_property sets
     int n_spread;                                // psets [0, n_spread) score, [n_spread, n_psets) filter
     uint32_t pset_allowed[kMaxPsets];            // distinct_property: allowed use count per value
@@ -188,6 +202,9 @@ struct BatchArgs {
     uint32_t* done_flag;          // or null: k_emit's last workgroup stores done_seq here (system scope)
     uint32_t done_seq;
     unsigned long long* prof;     // k_chain step clocks (PE_CHAIN_PROF), or null
+    // k_chain scratch, kChainMaxN doubles per workgroup: the window's values
+    // by relative position (one thread per Select walks its own positions)
+    double* chain_vs;
     pe_ranked_node* full_out;     // [n_evals][count] full records, or null
     EmitRec* emit_out;            // k_emit's records (single-evaluation chain), or null
     pe_placement* out;            // [n_evals][count] compact records, or null
@@ -277,6 +294,11 @@ struct PreemptArgs {
     uint32_t* flags;                  // [1] bit 0: a node exceeded the on-device limits
     uint8_t* dep_out;                 // or null: per position, the outcome read the plan's preemption counts
     const uint64_t* palloc_cores;     // [m x 4] or null: reserved cores held by each alloc (by CSR slot)
+    // or null: per position the option's score parts (PE_MAX_SCORES each) and
+    // their count, kept with mask_out / offers_out so the loop's winner record
+    // is read instead of re-evaluated (k_ploop)
+    double* parts_out;
+    uint8_t* nparts_out;
 };
 
 // LimitIterator + MaxScoreIterator over per-position results.

@@ -294,6 +294,10 @@ __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t
             const int32_t avail = r.avail_mbits;
             const int32_t mb = r.used_mbits + (int32_t)dk * a.commit_mbits;
             if (avail < 0 || mb + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) return kExhausted;
+            if (t.task_gate) {   // AssignNetwork's static ports (network.go:419-431), host-built gate
+                const uint32_t gt = t.task_gate[row];
+                if (gt == 0u || in.coll_tg + dk + 1u != gt) return kExhausted;
+            }
         }
     }
     si->dev_aff = 0.0;
@@ -466,6 +470,7 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
         if (code == kTrOption && a.has_task_net) {
             if (r.avail_mbits < 0) code = kTrNoNetworks;
             else if (r.used_mbits + a.task_mbits > r.avail_mbits) code = kTrBandwidth;
+            else if (t.task_gate && (t.task_gate[row] == 0u || in.coll_tg + 1u != t.task_gate[row])) code = kTrTaskStatic;
             else if (kDynPortCapacity - dyn < a.task_dyn) code = kTrTaskDyn;
         }
     }
@@ -1253,16 +1258,23 @@ __device__ __forceinline__ double encode_eval(const NodeEval& ev) {
 
 // base[row]: the fused pipeline of every row of the snapshot with no placement
 // of this launch on it. It does not depend on the visit order, so one pass
-// serves every evaluation of a batch.
-__global__ void __launch_bounds__(256) k_base(BatchArgs A) {
-    const uint32_t stride = gridDim.x * 256;
+// serves every evaluation of a batch. base1 (one placement on the row) is
+// computed by a second set of lanes rather than after base in the same lane:
+// the pass is one dependent load + evaluate chain per lane, so the two tables
+// finish in the time of one; 64-lane workgroups spread it over more CUs.
+constexpr int kBaseBlock = 64;
+__global__ void __launch_bounds__(kBaseBlock) k_base(BatchArgs A) {
+    const uint32_t stride = gridDim.x * kBaseBlock;
     const uint32_t m = A.base_by_pos ? A.n_visit : A.soa.n;
-    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < m; j += stride) {
+    const uint32_t total = A.base1 ? 2u * m : m;
+    for (uint32_t t = blockIdx.x * kBaseBlock + threadIdx.x; t < total; t += stride) {
+        const uint32_t dk = t >= m ? 1u : 0u;
+        const uint32_t j = t - dk * m;
         uint32_t row = j;
         if (A.base_by_pos) {
             if (A.perm_src) {
                 row = A.perm_src[j];
-                A.perm_dst[j] = row;
+                if (!dk) A.perm_dst[j] = row;
             } else {
                 row = A.perms[j];
             }
@@ -1271,15 +1283,8 @@ __global__ void __launch_bounds__(256) k_base(BatchArgs A) {
         load_node(A.soa, A.tg, row, in);
         NodeEval ev;
         ev.score = 0.0;
-        eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, A.penalty_bits, A.log10, nullptr, row, in, &ev);
-        A.base[j] = encode_eval(ev);
-        if (A.base1) {
-            NodeEval ev1;
-            ev1.score = 0.0;
-            eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, 1u, A.penalty_bits, A.log10, nullptr, row, in,
-                               &ev1);
-            A.base1[j] = encode_eval(ev1);
-        }
+        eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+        (dk ? A.base1 : A.base)[j] = encode_eval(ev);
     }
 }
 
@@ -1414,6 +1419,41 @@ constexpr uint32_t kIdxBits = 14, kIdxMask = (1u << kIdxBits) - 1u;
         }                                                                 \
     } while (0)
 
+
+// Step 5 of k_chain (out of line: its loads would otherwise raise the whole
+// kernel's register pressure).
+template <class Sh>
+__device__ __noinline__ void chain_walk(Sh& sh, const uint16_t* nb, const double* vs, const uint32_t* perm,
+                                        uint32_t cur, uint32_t n, uint32_t nsel, int tid) {
+    for (uint32_t s = (uint32_t)tid; s < nsel; s += kChainBlock) {
+        const uint32_t p0 = s ? (uint32_t)nb[sh.sel_b[s - 1]] + 1u : 0u;
+        const uint32_t p1 = nb[sh.sel_b[s]];
+        uint32_t n_aside = 0, f = 0, x = 0;
+        int bp = -1;
+        double best = 0.0;
+        for (uint32_t pb = p0; pb <= p1; pb += 8u) {
+            double y[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) y[k] = vs[min(pb + (uint32_t)k, p1)];   // one round of loads
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (pb + (uint32_t)k > p1) break;
+                const double yk = y[k];
+                if (yk == -__builtin_inf()) { f++; continue; }
+                if (yk == __builtin_inf()) { x++; continue; }
+                if (yk <= 0.0 && n_aside < (uint32_t)kMaxSkip) { n_aside++; continue; }
+                if (bp < 0 || yk > best) { best = yk; bp = (int)(pb + (uint32_t)k); }
+            }
+        }
+        sh.sel_end[s] = p1;
+        sh.sel_pos[s] = (uint16_t)bp;
+        sh.sel_max[s] = (unsigned long long)gm::f2u(best);
+        sh.sel_row[s] = perm[wrap_pos(cur + (uint32_t)bp, n)];
+        sh.sel_f[s] = f;
+        sh.sel_x[s] = x;
+    }
+}
+
 __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_evals) {
     static_assert(kChainMaxN <= (1u << kIdxBits), "option index packing");
     static_assert(kChainMaxSel <= (1 << (32 - 2 * kIdxBits + kIdxBits)), "select id packing");
@@ -1440,6 +1480,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     int prof_ph = 0;   // profile slot group: phase (capped at 3)
     for (uint32_t e = blockIdx.x; e < n_evals; e += gridDim.x) {
         const uint32_t* __restrict__ perm = A.perms + (size_t)e * A.perm_stride;
+        double* __restrict__ vs = A.chain_vs + (size_t)blockIdx.x * kChainMaxN;   // values by relative position
         for (uint32_t i = tid; i < H; i += kChainBlock) {
             ov.keys[i] = kEmpty;
             if (ov.k) ov.k[i] = 0;
@@ -1552,6 +1593,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
 #pragma unroll
             for (int q = 0; q < kChainItems; q++) {
                 const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                if (j < W) vs[j] = v[q];   // read back by the Select walks of step 5 (after the barriers)
                 const bool is_o = j < W && v[q] > -__builtin_inf() && v[q] < __builtin_inf();
                 const bool is_n = is_o && v[q] <= 0.0;
                 optmask |= (uint32_t)is_o << q;
@@ -1645,6 +1687,10 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             }
             if (tid == 0) nx[tot_o] = kNxFail;
             __syncthreads();
+            // nb is free from here on: the relative position of every option
+#pragma unroll
+            for (int q = 0; q < kChainItems; q++)
+                if ((optmask >> q) & 1u) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
             const uint32_t n_seg = (tot_o + kSegLen - 1) / kSegLen;
             const uint32_t E = L + 3;
             for (uint32_t t = tid; t < n_seg * E; t += kChainBlock) {
@@ -1711,15 +1757,6 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
             }
             __syncthreads();
-            {
-                // Select id of every option of a resolved Select (nx is free now)
-                const uint32_t ns = sh.nsel;
-                for (uint32_t sel = tid; sel < ns; sel += kChainBlock) {
-                    const uint32_t i0 = sel ? sh.sel_b[sel - 1] + 1u : 0u;
-                    for (uint32_t k = i0; k <= sh.sel_b[sel]; k++) nx[k] = (uint16_t)sel;
-                }
-            }
-            __syncthreads();
             const uint32_t nsel = sh.nsel;
             const int mode = (int)sh.mode;
             if (mode == kPhaseStall) {
@@ -1730,62 +1767,51 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 force_full = true;
                 continue;
             }
-            const uint32_t last_b = nsel ? sh.sel_b[nsel - 1] : 0u;
             PE_PROF_MARK(4);
-            // 5. per-Select maxima over the returned options (a Select sets its
-            //    first three N options aside)
-            uint32_t retmask = 0;
-#pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
-                const uint32_t k = pk[q] & kIdxMask;
-                uint32_t s = 0;
-                if (((optmask >> q) & 1u) && nsel && k <= last_b) {
-                    s = nx[k];
-                    const uint32_t i0 = s ? sh.sel_b[s - 1] + 1u : 0u;
-                    const uint32_t nrank = (pk[q] >> kIdxBits) - nb[i0];
-                    const bool aside = ((nmask >> q) & 1u) && nrank < (uint32_t)kMaxSkip;
-                    if (!aside) {
-                        retmask |= 1u << q;
-                        atomicMax(&sh.sel_max[s], order_key(v[q]));
-                    } else if (mode == kPhaseExhausted) {
-                        sh.aside_v[nrank] = v[q];
-                        sh.aside_row[nrank] = row[q];
-                    }
-                    if (k == sh.sel_b[s]) sh.sel_end[s] = (uint32_t)(q * kChainBlock + tid);
-                }
-                pk[q] = k | (s << kIdxBits);
-            }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
-                if ((retmask >> q) & 1u) {
-                    const uint32_t s = pk[q] >> kIdxBits;
-                    if (order_key(v[q]) == sh.sel_max[s]) atomicMin(&sh.sel_arg[s], pk[q] & kIdxMask);
-                }
-            }
-            if ((A.full_out || A.emit) && (nsel || mode == kPhaseExhausted)) {
-                // AllocMetric counters: filtered / exhausted positions pulled by each Select
-                const uint32_t end = mode == kPhaseExhausted ? W - 1 : sh.sel_end[nsel - 1];
+            if (mode != kPhaseExhausted) {
+                // 5. one thread per Select walks its positions (previous stop + 1
+                //    .. its stop) in the scratch copy of the values: the first
+                //    kMaxSkip non-positive options are set aside, MaxScoreIterator
+                //    keeps the first strict maximum of the rest (select.go:79-116);
+                //    filtered / exhausted positions are the Select's metrics
+                chain_walk(sh, nb, vs, perm, cur, n, nsel, tid);
+            } else {
+                // the one Select of an exhausted stream: every option of the
+                // window (atomics over one key), its first kMaxSkip N's set aside
+                uint32_t retmask = 0;
 #pragma unroll
                 for (int q = 0; q < kChainItems; q++) {
-                    const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                    if (j <= end && j < W && !((optmask >> q) & 1u)) {
-                        // pulled by the Select of the next option after j
-                        const uint32_t s = mode == kPhaseExhausted ? 0u : (uint32_t)nx[pk[q] & kIdxMask];
-                        atomicAdd(v[q] == -__builtin_inf() ? &sh.sel_f[s] : &sh.sel_x[s], 1u);
+                    if ((optmask >> q) & 1u) {
+                        const uint32_t nrank = pk[q] >> kIdxBits;   // N options before this one
+                        const bool aside = ((nmask >> q) & 1u) && nrank < (uint32_t)kMaxSkip;
+                        if (!aside) {
+                            retmask |= 1u << q;
+                            atomicMax(&sh.sel_max[0], order_key(v[q]));
+                        } else {
+                            sh.aside_v[nrank] = v[q];
+                            sh.aside_row[nrank] = row[q];
+                        }
                     }
                 }
-            }
-            __syncthreads();
-            // the first maximum of each Select publishes its row and FinalScore
+                __syncthreads();
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
-                if ((retmask >> q) & 1u) {
-                    const uint32_t s = pk[q] >> kIdxBits;
-                    if (sh.sel_arg[s] == (pk[q] & kIdxMask)) {
-                        sh.sel_row[s] = row[q];
-                        sh.sel_pos[s] = (uint16_t)(q * kChainBlock + tid);
-                        sh.sel_max[s] = (unsigned long long)gm::f2u(v[q]);
+                for (int q = 0; q < kChainItems; q++)
+                    if (((retmask >> q) & 1u) && order_key(v[q]) == sh.sel_max[0])
+                        atomicMin(&sh.sel_arg[0], pk[q] & kIdxMask);
+                if (A.full_out || A.emit) {
+#pragma unroll
+                    for (int q = 0; q < kChainItems; q++) {
+                        const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                        if (j < W && !((optmask >> q) & 1u))
+                            atomicAdd(v[q] == -__builtin_inf() ? &sh.sel_f[0] : &sh.sel_x[0], 1u);
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < kChainItems; q++) {
+                    if (((retmask >> q) & 1u) && sh.sel_arg[0] == (pk[q] & kIdxMask)) {
+                        sh.sel_row[0] = row[q];
+                        sh.sel_max[0] = (unsigned long long)gm::f2u(v[q]);
                     }
                 }
             }
@@ -3100,15 +3126,16 @@ int pe_chain_blocks_per_cu(size_t lds) {
 }
 
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st) {
-    if (!a->base || (a->n_visit > pe::kChainMaxN && n_evals != 1) || a->class_ok_stride ||
+    if (!a->base || !a->chain_vs || (a->n_visit > pe::kChainMaxN && n_evals != 1) || a->class_ok_stride ||
         a->limit > pe::kMaxChainLimit)
         return hipErrorInvalidValue;
     if (a->base_by_pos && n_evals != 1) return hipErrorInvalidValue;
     if (a->perm_src && (!a->base_by_pos || !a->perm_dst)) return hipErrorInvalidValue;
-    uint32_t blocks = ((a->base_by_pos ? a->n_visit : a->soa.n) + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
+    const uint32_t m = a->base_by_pos ? a->n_visit : a->soa.n;
+    uint32_t blocks = ((a->base1 ? 2u * m : m) + pe::kBaseBlock - 1) / pe::kBaseBlock;
+    if (blocks > 8192) blocks = 8192;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(pe::k_base, dim3(blocks), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(pe::k_base, dim3(blocks), dim3(pe::kBaseBlock), 0, st, *a);
     const size_t lds = pe_chain_lds_bytes(a->hash_bits, a->packed_overlay != 0, a->n_visit);
     uint32_t grid = n_evals < max_blocks ? n_evals : max_blocks;
     if (grid == 0) grid = 1;
@@ -3180,7 +3207,7 @@ hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs*
     uint32_t blocks = (a->n_visit + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(pe::k_evict, dim3(blocks), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(pe::k_evict<false>, dim3(blocks), dim3(256), 0, st, *a);
     hipLaunchKernelGGL(pe::k_evict_resolve, dim3(1), dim3(pe::kResolveBlock), 0, st, *r);
     return hipGetLastError();
 }
@@ -3198,7 +3225,12 @@ hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st) {
     uint32_t blocks = (a->n_visit + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(pe::k_evict, dim3(blocks), dim3(256), 0, st, *a);
+    if (a->parts_out) {
+        if (!a->nparts_out || !a->mask_out || !a->offers_out) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(pe::k_evict<true>, dim3(blocks), dim3(256), 0, st, *a);
+    } else {
+        hipLaunchKernelGGL(pe::k_evict<false>, dim3(blocks), dim3(256), 0, st, *a);
+    }
     return hipGetLastError();
 }
 

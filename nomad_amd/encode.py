@@ -152,6 +152,11 @@ class EncodedState:
                                        for w in x.networks], [_u32, _u32, _i32])
         nt.net_off, nt.net_mode, nt.net_device = (_ptr(a, abi.u32p) for a in (off, m, d))
         nt.net_mbits = _ptr(mb, abi.i32p)
+        # the network's IP field and the one address yieldIP gives from its
+        # CIDR (AssignNetwork, network.go:294-315), PE_NONE: none / several
+        off, nip, cip = csr(lambda x: [(I(w.ip) if w.ip else abi.PE_NONE, _cidr_single(w.cidr, I))
+                                       for w in x.networks], [_u32, _u32])
+        nt.net_ip, nt.net_cidr_ip = _ptr(nip, abi.u32p), _ptr(cip, abi.u32p)
         off, al = csr(lambda x: [(I(a),) for a in x.host_network_aliases], [_u32])
         nt.alias_off, nt.alias_name = _ptr(off, abi.u32p), _ptr(al, abi.u32p)
         nt.reserved_dyn_ports = _ptr(col(lambda x: sum(1 for p in x.reserved_host_ports
@@ -260,6 +265,19 @@ class EncodedState:
         return t
 
 
+def _cidr_single(cidr: str, intern) -> int:
+    """The only address of a CIDR block, interned (PE_NONE when the CIDR does
+    not parse or holds more than one address)."""
+    import ipaddress
+    try:
+        net = ipaddress.ip_network(cidr, strict=False)
+    except ValueError:
+        return abi.PE_NONE
+    if net.num_addresses != 1:
+        return abi.PE_NONE
+    return intern(str(net.network_address))
+
+
 def encode_attr(val, it: Interner) -> abi.pe_attr:
     """psstructs.Attribute: (kind, value, unit). Accepts python scalars or (value, unit)."""
     a = abi.pe_attr()
@@ -329,6 +347,11 @@ class EncodedJob:
                 if t.network is not None:
                     pt.has_network, pt.net_mbits = 1, t.network.mbits
                     pt.net_dyn_ports, pt.net_reserved_ports = t.network.dynamic_ports, len(t.network.reserved_ports)
+                    pt.rport_off = len(rport_val)
+                    for k, v in enumerate(t.network.reserved_ports):
+                        rport_val.append(v)
+                        lab = t.network.port_labels[k] if k < len(t.network.port_labels) else ""
+                        rport_lab.append(I(lab))
                 pt.constraint_off, pt.constraint_count = add_cons(t.constraints)
                 pt.affinity_off, pt.affinity_count = add_affs(t.affinities)
                 pt.device_off, pt.device_count = len(devs), len(t.devices)

@@ -52,7 +52,7 @@ struct Unsupported : std::runtime_error {
 static const int32_t kDynPortCapacity = 32000 - 20000 + 1;   // IndexesInRange is inclusive
 
 struct DriverInfo { bool detected, healthy, nil; };
-struct NetRes { std::string mode, device; int32_t mbits; };
+struct NetRes { std::string mode, device; int32_t mbits; std::string ip, cidr_ip; };   // cidr_ip: yieldIP's one address
 
 struct ODev {
     std::string vendor, type, name;
@@ -111,6 +111,7 @@ struct OTask {
     int32_t cores;
     uint32_t lifecycle;
     bool has_network; int32_t net_mbits, net_dyn, net_reserved;
+    std::vector<std::pair<int, std::string>> rports;   // the task network's ReservedPorts (Value, Label)
     std::vector<const pe_constraint*> constraints;
     std::vector<const pe_affinity*> affinities;
     int n_devices;
@@ -1219,15 +1220,21 @@ struct Preemptor {
         return out;
     }
 
-    // PreemptForNetwork (preemption.go:270-455) for an ask of `needed` MBits
-    // without reserved ports, every candidate's network on the node's device
-    // (total: AvailBandwidth, used: the NetworkIndex's UsedBandwidth).
-    std::vector<const OAlloc*> ForNetwork(int32_t needed, int32_t total, int32_t used) {
+    // PreemptForNetwork (preemption.go:270-455) for an ask of `needed` MBits and
+    // the ReservedPorts values `ports`, every candidate's network on the node's
+    // device (total: AvailBandwidth, used: the NetworkIndex's UsedBandwidth).
+    // An alloc's ReservedPorts are the values of the ports it holds.
+    std::vector<const OAlloc*> ForNetwork(int32_t needed, int32_t total, int32_t used,
+                                          const std::vector<int>& ports = {}) {
         if (current.empty()) return {};
         std::vector<const OAlloc*> dev;
+        std::set<int> filtered;   // filteredReservedPorts: ports of allocs too close in priority
         for (const OAlloc* a : current) {
             if (!a->has_net) continue;
-            if (job_priority - a->priority < 10) continue;
+            if (job_priority - a->priority < 10) {
+                for (auto& pp : a->ports) filtered.insert(pp.second);
+                continue;
+            }
             dev.push_back(a);
         }
         if (dev.empty()) return {};
@@ -1235,6 +1242,25 @@ struct Preemptor {
         const int32_t free_bw = total - used;
         int32_t pbw = 0;
         std::vector<const OAlloc*> best;
+        if (!ports.empty()) {
+            // the reserved ports first: usedPortToAlloc (the last holder in
+            // candidate order wins), a port held by a filtered alloc fails
+            std::map<int, const OAlloc*> holder;
+            for (const OAlloc* a : dev)
+                for (auto& pp : a->ports) holder[pp.second] = a;
+            for (int v : ports) {
+                auto it = holder.find(v);
+                if (it != holder.end()) {
+                    for (const OAlloc* b : best)
+                        if (b == it->second) throw Unsupported("one alloc holding two static ports of the ask");
+                    pbw += it->second->mbits;
+                    best.push_back(it->second);
+                } else if (filtered.count(v)) {
+                    return {};
+                }
+            }
+            dev = remove_allocs(dev, best);
+        }
         bool met = pbw + free_bw >= needed;
         auto distance = [&](const OAlloc* a) {   // networkResourceDistance (preemption.go:627-635)
             return std::fabs((double)((int64_t)needed - (int64_t)a->mbits) / (double)needed);
@@ -1397,60 +1423,76 @@ struct BinPackIterator : RankIterator {
             pre.SetNode(n);
             pre.SetPreemptions(ctx->plan);
             option->ports.clear();
+            // UsedPorts[ip] of the NetworkIndex (network.go:92-293): SetNode keys the
+            // AvailNetworks' IP fields and the addresses (their ReservedPorts), then
+            // marks ReservedHostPorts on every key; AddAllocs marks the proposed
+            // allocs' ports; this BinPack's offers so far (option->ports) are added
+            // by AddReservedPorts / AddReserved (idx_offers; a rebuilt index drops them).
+            std::vector<std::pair<std::string, int>> idx_offers;
+            auto port_used = [&](const std::vector<const OAlloc*>& prop, const std::string& ip, int v) {
+                bool keyed = false;
+                for (auto& nw : n.nets) if (!nw.device.empty() && nw.ip == ip) keyed = true;
+                for (auto& ad : n.addrs)
+                    if (ad.ip == ip) {
+                        keyed = true;
+                        for (int r : ad.reserved) if (r == v) return true;
+                    }
+                if (keyed) for (int r : n.reserved_host_ports) if (r == v) return true;
+                for (const OAlloc* x : prop) {
+                    if (x->terminal) continue;
+                    for (auto& pp : x->ports) if (pp.first == ip && pp.second == v) return true;
+                }
+                for (auto& o : idx_offers) if (o.first == ip && o.second == v) return true;
+                return false;
+            };
             if (tg->has_network) {
-                // AssignPorts, ReservedPorts first (network.go:317-363): the first
-                // address of the port's host network; the port must be free on it
+                // AssignPorts (network.go:317-404): ReservedPorts first, on the first
+                // address of the port's host network, then one free port in
+                // [MinDynamicPort, MaxDynamicPort] per dynamic port; "" = an offer
+                std::vector<int> rport_values;
+                for (auto& rp : tg->rports) rport_values.push_back(rp.first);
+                std::vector<std::pair<std::string, int>> offer;
                 int32_t static_dyn = 0;
-                std::string perr;
-                for (auto& rp : tg->rports) {
-                    const ONode::Addr* ad = nullptr;
-                    for (auto& a : n.addrs) if (a.alias == tg->net_host_network) { ad = &a; break; }
-                    if (!ad) { perr = "no addresses available for \"" + tg->net_host_network + "\" network"; break; }
-                    if (rp.first < 0 || rp.first >= 65536) { perr = "invalid port " + std::to_string(rp.first) + " (out of range)"; break; }
-                    // used ports of the address: the node's reservations for that IP,
-                    // ReservedHostPorts (every address), the proposed allocs' ports
-                    bool used = false;
-                    for (auto& a : n.addrs)
-                        if (a.ip == ad->ip) for (int v : a.reserved) used = used || v == rp.first;
-                    for (int v : n.reserved_host_ports) used = used || v == rp.first;
-                    for (const OAlloc* a : proposed) {
-                        if (a->terminal) continue;
-                        for (auto& pp : a->ports) used = used || (pp.first == ad->ip && pp.second == rp.first);
+                auto assign_ports = [&](const std::vector<const OAlloc*>& prop) -> std::string {
+                    offer.clear();
+                    static_dyn = 0;
+                    for (auto& rp : tg->rports) {
+                        const ONode::Addr* ad = nullptr;
+                        for (auto& x : n.addrs) if (x.alias == tg->net_host_network) { ad = &x; break; }
+                        if (!ad) return "no addresses available for \"" + tg->net_host_network + "\" network";
+                        if (rp.first < 0 || rp.first >= 65536) return "invalid port " + std::to_string(rp.first) + " (out of range)";
+                        if (port_used(prop, ad->ip, rp.first))
+                            return "reserved port collision " + rp.second + "=" + std::to_string(rp.first);
+                        offer.push_back({ad->ip, rp.first});
+                        static_dyn += (rp.first >= 20000 && rp.first <= 32000) ? 1 : 0;
                     }
-                    if (used) { perr = "reserved port collision " + rp.second + "=" + std::to_string(rp.first); break; }
-                    option->ports.push_back({ad->ip, rp.first});
-                    static_dyn += (rp.first >= 20000 && rp.first <= 32000) ? 1 : 0;
-                }
+                    if (tg->net_dyn > 0) {   // reservedIdx: the dynamic picks skip the static ones
+                        bool has_addr = false;
+                        for (auto& x : n.aliases) if (x == tg->net_host_network) { has_addr = true; break; }
+                        if (!has_addr) return "no addresses available";
+                        if (kDynPortCapacity - used_dyn - static_dyn < 1) return "dynamic port selection failed";
+                    }
+                    return "";
+                };
+                std::string perr = assign_ports(proposed);
                 if (!perr.empty()) {
-                    if (evict) throw Unsupported("network preemption");   // PreemptForNetwork path
-                    ctx->metrics.ExhaustedNode(&n, "network: " + perr);
-                    continue;
-                }
-                used_dyn += static_dyn;   // reservedIdx: the dynamic picks skip them
-                // AssignPorts: each dynamic port needs an address of its host network
-                // and one free port in [MinDynamicPort, MaxDynamicPort].
-                if (tg->net_dyn > 0) {
-                    bool has_addr = false;
-                    for (auto& a : n.aliases) if (a == tg->net_host_network) { has_addr = true; break; }
-                    if (!has_addr || kDynPortCapacity - used_dyn < 1) {
-                        if (!evict) {
-                            ctx->metrics.ExhaustedNode(&n, !has_addr ? "network: no addresses available"
-                                                                     : "network: dynamic port selection failed");
-                            continue;
-                        }
-                        // PreemptForNetwork on the group's ask (rank.go:273-300); nil
-                        // skips the node without an ExhaustedNode
-                        if (!tg->rports.empty()) throw Unsupported("static port asks with preemption");
-                        pre.SetCandidates(proposed);
-                        auto np = pre.ForNetwork(0, device_bandwidth(n), used_mbits);
-                        if (np.empty()) continue;
-                        to_preempt.insert(to_preempt.end(), np.begin(), np.end());
-                        proposed = remove_allocs(proposed, np);
-                        index_usage(n, proposed, &used_dyn, &used_mbits);   // a new NetworkIndex
-                        if (!has_addr || kDynPortCapacity - used_dyn < 1) continue;
+                    if (!evict) {
+                        ctx->metrics.ExhaustedNode(&n, "network: " + perr);
+                        continue;
                     }
-                    used_dyn += tg->net_dyn;   // AddReservedPorts(offer)
+                    // PreemptForNetwork on the group's ask (rank.go:273-300); nil skips
+                    // the node without an ExhaustedNode, and so does a failed retry
+                    pre.SetCandidates(proposed);
+                    auto np = pre.ForNetwork(0, device_bandwidth(n), used_mbits, rport_values);
+                    if (np.empty()) continue;
+                    to_preempt.insert(to_preempt.end(), np.begin(), np.end());
+                    proposed = remove_allocs(proposed, np);
+                    index_usage(n, proposed, &used_dyn, &used_mbits);   // a new NetworkIndex
+                    if (!assign_ports(proposed).empty()) continue;
                 }
+                used_dyn += static_dyn + tg->net_dyn;   // AddReservedPorts(offer)
+                option->ports.insert(option->ports.end(), offer.begin(), offer.end());
+                idx_offers.insert(idx_offers.end(), offer.begin(), offer.end());
             }
             bool skip = false;
             option->offers.clear();
@@ -1458,39 +1500,63 @@ struct BinPackIterator : RankIterator {
             int64_t spc = -1;
             for (auto& t : tg->tasks) {
                 if (t.has_network) {
-                    // AssignNetwork over the node's AvailNetworks (device != "")
-                    bool ok = false; std::string err = "no networks available";
-                    for (auto& nw : n.nets) {
-                        if (nw.device.empty()) continue;
-                        if (used_mbits + t.net_mbits > nw.mbits) { err = "bandwidth exceeded"; continue; }
-                        if (t.net_reserved > 0) throw Unsupported("static port asks");
-                        if (kDynPortCapacity - used_dyn < t.net_dyn) { err = "dynamic port selection failed"; continue; }
-                        ok = true; break;
-                    }
+                    // AssignNetwork over the node's AvailNetworks (device != "", yieldIP
+                    // over the CIDR): bandwidth, ReservedPorts on the address, dynamic
+                    std::vector<int> rport_values;
+                    for (auto& rp : t.rports) rport_values.push_back(rp.first);
+                    const std::string* yield_ip = nullptr;
+                    auto assign_network = [&](const std::vector<const OAlloc*>& prop, std::string* err) {
+                        *err = "no networks available";
+                        for (auto& nw : n.nets) {
+                            if (nw.device.empty()) continue;
+                            if (used_mbits + t.net_mbits > nw.mbits) { *err = "bandwidth exceeded"; continue; }
+                            if (!t.rports.empty()) {
+                                if (nw.cidr_ip.empty()) throw Unsupported("task static ports on a network that is not one address");
+                                bool bad = false;
+                                for (auto& rp : t.rports) {
+                                    if (rp.first < 0 || rp.first >= 65536) {
+                                        *err = "invalid port " + std::to_string(rp.first) + " (out of range)";
+                                        bad = true;
+                                        break;
+                                    }
+                                    if (port_used(prop, nw.cidr_ip, rp.first)) {
+                                        *err = "reserved port collision " + rp.second + "=" + std::to_string(rp.first);
+                                        bad = true;
+                                        break;
+                                    }
+                                }
+                                if (bad) continue;
+                            }
+                            if (kDynPortCapacity - used_dyn < t.net_dyn) { *err = "dynamic port selection failed"; continue; }
+                            yield_ip = &nw.cidr_ip;
+                            return true;
+                        }
+                        return false;
+                    };
+                    std::string err;
+                    bool ok = assign_network(proposed, &err);
                     if (!ok && evict) {
                         // PreemptForNetwork on the task's ask (rank.go:343-379); the
                         // rebuilt index holds the remaining proposed allocs only
                         int ndev = 0;
                         for (auto& nw : n.nets) ndev += nw.device.empty() ? 0 : 1;
                         if (ndev > 1) throw Unsupported("network preemption on a node with several network devices");
-                        if (t.net_reserved > 0) throw Unsupported("static port asks with preemption");
                         pre.SetCandidates(proposed);
-                        auto np = pre.ForNetwork(t.net_mbits, device_bandwidth(n), used_mbits);
+                        auto np = pre.ForNetwork(t.net_mbits, device_bandwidth(n), used_mbits, rport_values);
                         if (np.empty()) { skip = true; break; }
                         to_preempt.insert(to_preempt.end(), np.begin(), np.end());
                         proposed = remove_allocs(proposed, np);
                         index_usage(n, proposed, &used_dyn, &used_mbits);
-                        for (auto& nw : n.nets) {
-                            if (nw.device.empty()) continue;
-                            if (used_mbits + t.net_mbits > nw.mbits) continue;
-                            if (kDynPortCapacity - used_dyn < t.net_dyn) continue;
-                            ok = true;
-                            break;
-                        }
-                        if (!ok) { skip = true; break; }
+                        idx_offers.clear();   // the rebuilt index holds no earlier offers
+                        std::string err2;
+                        if (!assign_network(proposed, &err2)) { skip = true; break; }
                     }
-                    if (!ok) { ctx->metrics.ExhaustedNode(&n, "network: " + err); skip = true; break; }
+                    if (!ok && !evict) { ctx->metrics.ExhaustedNode(&n, "network: " + err); skip = true; break; }
                     used_mbits += t.net_mbits; used_dyn += t.net_dyn;   // AddReserved(offer)
+                    for (auto& rp : t.rports) {
+                        option->ports.push_back({*yield_ip, rp.first});
+                        idx_offers.push_back({*yield_ip, rp.first});
+                    }
                 }
                 // devices (rank.go:366-414)
                 for (auto& req : t.devices) {
@@ -1952,8 +2018,13 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
             uint8_t f = nt->drv_flags[k];
             n.drivers[S(st, nt->drv_name[k])] = DriverInfo{(f & 1) != 0, (f & 2) != 0, (f & 4) != 0};
         }
-        for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++)
-            n.nets.push_back(NetRes{S(st, nt->net_mode[k]), S(st, nt->net_device[k]), nt->net_mbits[k]});
+        for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++) {
+            auto ip_of = [&](const uint32_t* col) {
+                return (col && col[k] != PE_NONE) ? S(st, col[k]) : std::string();
+            };
+            n.nets.push_back(NetRes{S(st, nt->net_mode[k]), S(st, nt->net_device[k]), nt->net_mbits[k],
+                                    ip_of(nt->net_ip), ip_of(nt->net_cidr_ip)});
+        }
         for (uint32_t k = nt->alias_off[i]; k < nt->alias_off[i + 1]; k++) n.aliases.push_back(S(st, nt->alias_name[k]));
         n.reserved_dyn = nt->reserved_dyn_ports ? nt->reserved_dyn_ports[i] : 0;
         if (nt->hv_off)
@@ -2098,6 +2169,11 @@ int oracle_set_job(oracle_stack* s, const pe_strtab* strs, const pe_job* j) {
             ot.cpu = pt.cpu; ot.mem = pt.memory_mb; ot.mem_max = pt.memory_max_mb; ot.cores = pt.cores;
             ot.lifecycle = pt.lifecycle;
             ot.has_network = pt.has_network != 0; ot.net_mbits = pt.net_mbits; ot.net_dyn = pt.net_dyn_ports; ot.net_reserved = pt.net_reserved_ports;
+            for (int32_t q = 0; ot.has_network && q < pt.net_reserved_ports; q++) {
+                if (!j->rport_value) throw Unsupported("task static ports without their values");
+                ot.rports.push_back({j->rport_value[pt.rport_off + (uint32_t)q],
+                                     j->rport_label ? S(st, j->rport_label[pt.rport_off + (uint32_t)q]) : std::string()});
+            }
             ot.n_devices = (int)pt.device_count;
             for (uint32_t q = 0; q < pt.device_count; q++) {
                 const pe_device_request& r = j->devices[pt.device_off + q];

@@ -9,11 +9,11 @@ allocs cpu / memory (and task networks) but no shared disk, and the ask has an
 empty EphemeralDisk, so disk is 0 on both sides. The cases whose ask holds a
 static port ("No preemption because existing allocs are not low priority",
 "Preempting low priority allocs not enough ...", "preemption impossible -
-static port ...", "preempt only from device that has allocation with unused
-reserved port", "one alloc meets static port need ...", "alloc that meets
-static port need ...") are outside the device path: task static ports are
-refused with PE_EUNSUPPORTED and left to the reference chain
-(test_static_port_network_preemption_is_refused).
+static port ...", "one alloc meets static port need ...", "alloc that meets
+static port need ...") ask static ports in a task network (AssignNetwork's
+ReservedPorts and PreemptForNetwork's reserved-port step); "preempt only from
+device that has allocation with unused reserved port" needs a second network
+device and is refused (PE_EUNSUPPORTED, the reference chain answers).
 """
 import math
 
@@ -54,17 +54,19 @@ def preemption_node():
     return nd
 
 
-def alloc(i, prio, cpu, mem, devices=(), mbits=0, node="node-0"):
+def alloc(i, prio, cpu, mem, devices=(), mbits=0, node="node-0", ports=()):
     """createAlloc; `mbits` is the bandwidth of the alloc's eth0 networks (task
     and group networks on one device add up in Flattened.Networks[0] and in
-    NetworkIndex.UsedBandwidth alike)."""
+    NetworkIndex.UsedBandwidth alike); `ports` the (IP, value) ReservedPorts of
+    its networks."""
     job = {LOW: "low", LOW2: "low2", HIGH: "high"}[prio]
     return Allocation(node_id=node, job_id=job, task_group="web", cpu_shares=cpu, memory_mb=mem,
-                      disk_mb=0, priority=prio, devices=list(devices), net_mbits=mbits)
+                      disk_mb=0, priority=prio, devices=list(devices), net_mbits=mbits, ports=list(ports))
 
 
-def ask_job(cpu, mem, device=None, mbits=0):
-    net = NetworkResource(mbits=mbits) if mbits else None
+def ask_job(cpu, mem, device=None, mbits=0, ports=()):
+    net = NetworkResource(mbits=mbits, reserved_ports=[v for _, v in ports],
+                          port_labels=[lab for lab, _ in ports]) if (mbits or ports) else None
     return Job(id="preemptor", priority=100, task_groups=[TaskGroup(name="web", count=1, ephemeral_disk_mb=0, tasks=[
         Task(name="web", driver="exec", cpu=cpu, memory_mb=mem, network=net,
              devices=[device] if device else [])])])
@@ -110,6 +112,28 @@ CASES = {
         [alloc(0, HIGH, 1800, 2256, mbits=150), alloc(1, LOW, 1500, 256, mbits=100),
          alloc(2, LOW, 600, 256, mbits=300)],
         ask_job(1000, 256, mbits=50), {1}),
+    # the task network asks static ports (AssignNetwork's ReservedPorts,
+    # network.go:407-442; PreemptForNetwork's reserved-port step,
+    # preemption.go:309-342). The reference node also carries mock.Node()'s
+    # COMPAT Node.Reserved network (port 22 on 192.168.0.100), which is not
+    # modelled; it changes no expected outcome below.
+    "No preemption because existing allocs are not low priority": (
+        [alloc(0, HIGH, 3200, 7256, mbits=50)],
+        ask_job(2000, 256, mbits=1, ports=[("ssh", 22)]), None),
+    "Preempting low priority allocs not enough to meet resource ask": (
+        [alloc(0, LOW, 3200, 7256, mbits=50)],
+        ask_job(4000, 8192, mbits=1, ports=[("ssh", 22)]), None),
+    "preemption impossible - static port needed is used by higher priority alloc": (
+        [alloc(0, HIGH, 1200, 2256, mbits=150), alloc(1, HIGH, 200, 256, mbits=600, ports=[("192.168.0.200", 88)])],
+        ask_job(600, 1000, mbits=700, ports=[("db", 88)]), None),
+    "one alloc meets static port need, another meets remaining mbits needed": (
+        [alloc(0, HIGH, 1200, 2256, mbits=150), alloc(1, LOW, 200, 256, mbits=500, ports=[("192.168.0.200", 88)]),
+         alloc(2, LOW, 200, 256, mbits=200)],
+        ask_job(2700, 1000, mbits=800, ports=[("db", 88)]), {1, 2}),
+    "alloc that meets static port need also meets other needs": (
+        [alloc(0, HIGH, 1200, 2256, mbits=150), alloc(1, LOW, 200, 256, mbits=600, ports=[("192.168.0.200", 88)]),
+         alloc(2, LOW, 200, 256, mbits=100)],
+        ask_job(600, 1000, mbits=700, ports=[("db", 88)]), {1}),
 }
 
 
@@ -212,20 +236,67 @@ def test_group_port_preemption_frees_dynamic_ports(stack_cls):
 
 
 @pytest.mark.parametrize("stack_cls", STACKS)
-def test_static_port_network_preemption_is_refused(stack_cls):
-    """A task static port ask is outside the device path: the engine refuses
-    the task group (PE_EUNSUPPORTED, the shim hands it to the reference chain)
-    and the oracle raises on it."""
+def test_static_port_holder_on_the_address_is_preempted(stack_cls):
+    """A task static port held on the node's address by a low-priority alloc:
+    AssignNetwork fails, PreemptForNetwork takes the port holder first
+    (usedPortToAlloc), which also frees enough bandwidth; the retried offer
+    gets the port."""
     node = preemption_node()
-    allocs = [alloc(0, HIGH, 1200, 2256, mbits=150), alloc(1, LOW, 200, 256, mbits=600)]
-    job = ask_job(600, 1000, mbits=700)
-    job.task_groups[0].tasks[0].network.reserved_ports = [88]
+    allocs = [alloc(0, HIGH, 1200, 2256, mbits=150),
+              alloc(1, LOW, 200, 256, mbits=600, ports=[("192.168.0.100", 88)]),
+              alloc(2, LOW, 200, 256, mbits=50)]
+    job = ask_job(600, 1000, mbits=100, ports=[("db", 88)])
     st = stack_cls()
     st.SetState([node], allocs)
-    with pytest.raises(Exception, match="(?i)unsupported|static port"):
-        st.SetJob(job)
-        st.SetNodes([node])
-        st.SelectRaw(0, SelectOptions(preempt=True))
+    st.SetJob(job)
+    st.SetNodes([node])
+    assert st.SelectRaw(0).row == -1          # reserved port collision db=88
+    r = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert r.row == 0 and r.preempted == [1]
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_static_port_held_by_a_close_priority_alloc(stack_cls):
+    """filteredReservedPorts: the port is held by an alloc too close in
+    priority; no preemption even though another candidate would free
+    bandwidth."""
+    node = preemption_node()
+    allocs = [alloc(0, LOW, 1200, 2256, mbits=300),
+              alloc(1, HIGH, 200, 256, mbits=100, ports=[("192.168.0.100", 88)])]
+    job = ask_job(600, 1000, mbits=100, ports=[("db", 88)])
+    st = stack_cls()
+    st.SetState([node], allocs)
+    st.SetJob(job)
+    st.SetNodes([node])
+    assert st.SelectRaw(0, SelectOptions(preempt=True)).row == -1
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_group_static_port_preemption(stack_cls):
+    """Task-group static ports (AssignPorts, rank.go:265-300): the holder of the
+    port on the host network's address is preempted; a node whose port is a
+    node reservation stays skipped."""
+    nodes = [synth.mock_node("n%d" % i) for i in range(3)]
+    nodes[2].reserved_host_ports = [22, 8080]
+    for nd in nodes:
+        nd.compute_class()
+    allocs = [Allocation(node_id="n0", job_id="svc", task_group="t", cpu_shares=3000, memory_mb=512,
+                         priority=80, ports=[("192.168.0.100", 8080)], net_mbits=10),
+              Allocation(node_id="n1", job_id="batch", task_group="t", cpu_shares=500, memory_mb=512,
+                         priority=20, ports=[("192.168.0.100", 8080)], net_mbits=10),
+              Allocation(node_id="n1", job_id="batch2", task_group="t", cpu_shares=500, memory_mb=512,
+                         priority=20, net_mbits=10)]
+    job = synth.mock_job(count=2)
+    job.priority = 70
+    job.task_groups[0].network = NetworkResource(mode="host", dynamic_ports=1, reserved_ports=[8080],
+                                                 port_labels=["http"])
+    st = stack_cls(config=SchedulerConfig(preempt_service=True))
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes([0, 1, 2])
+    assert st.SelectRaw(0).row == -1
+    r = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert (r.row, r.preempted, r.nodes_evaluated) == (1, [1], 3)
 
 
 @pytest.mark.parametrize("stack_cls", STACKS)

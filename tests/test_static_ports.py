@@ -175,3 +175,107 @@ def test_static_ports_system_stack():
     assert po == pe and (to == te).all()
     m = to == 0
     assert (so[m] == se[m]).all()
+
+
+# ---- task network static ports (AssignNetwork, network.go:407-442) and
+# PreemptForNetwork's reserved-port step (preemption.go:302-342) ------------
+
+def task_static_job(ports, mbits=10, dyn=0, count=1, job_id="tstatic", priority=50, cpu=100):
+    net = NetworkResource(mode="host", mbits=mbits, dynamic_ports=dyn, reserved_ports=list(ports),
+                          port_labels=["p%d" % p for p in ports])
+    return Job(id=job_id, priority=priority, task_groups=[TaskGroup(
+        name="web", count=count, ephemeral_disk_mb=100,
+        tasks=[Task(name="web", driver="exec", cpu=cpu, memory_mb=64, network=net)])])
+
+
+def task_port_cluster(n, seed, busy=0.0):
+    """Nodes whose eth0 CIDR is the node's one address (yieldIP), allocs holding
+    static ports and bandwidth on it; `busy` of the nodes nearly full of
+    low-priority work (preemption candidates)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    ids = sorted(synth.uuids(n, seed))
+    nodes, allocs = [], []
+    for k, nid in enumerate(ids):
+        ip = "10.%d.%d.%d" % (k >> 16, (k >> 8) & 255, k & 255)
+        nd = _node(nid, [("default", ip, "22" if rng.random() < 0.2 else "")],
+                   reserved_host_ports=(9000,) if rng.random() < 0.3 else ())
+        nd.networks = [NetworkResource(mode="host", device="eth0", cidr=ip + "/32", mbits=1000)]
+        nd.name = "node-%05d" % k
+        nd.compute_class()
+        nodes.append(nd)
+        full = rng.random() < busy
+        for q in range(int(rng.integers(0, 3)) + (2 if full else 0)):
+            port = int(rng.choice([8080, 443, 5000, 9000]))
+            prio = int(rng.choice([20, 30, 95] if full else [50, 95]))
+            allocs.append(Allocation(node_id=nid, job_id="svc-%d" % (k % 7 + q), task_group="web",
+                                     cpu_shares=1600 if full else 200, memory_mb=128, disk_mb=50,
+                                     priority=prio, net_mbits=int(rng.choice([50, 300, 600])),
+                                     ports=[(ip if rng.random() < 0.8 else "172.16.0.1", port)]))
+    return nodes, allocs
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_task_static_port_reasons(stack_cls):
+    """mock.Node(): the address 192.168.0.100 is the CIDR's one address, so
+    ReservedHostPorts 22 collides on it; a port held by an alloc on that IP
+    collides, one held on another IP does not; invalid ports fail; bandwidth
+    is checked before the ports."""
+    nodes = [_node("n0"), _node("n1"), _node("n2")]
+    allocs = [Allocation(node_id="n1", job_id="other", task_group="web", cpu_shares=100, memory_mb=64,
+                         ports=[("192.168.0.100", 8080)], net_mbits=10),
+              Allocation(node_id="n2", job_id="other", task_group="web", cpu_shares=100, memory_mb=64,
+                         ports=[("10.9.9.9", 8080)], net_mbits=10)]
+    cases = [
+        (task_static_job([22]), [None, None, None], "network: reserved port collision p22=22"),
+        (task_static_job([8080]), [0, None, 2], "network: reserved port collision p8080=8080"),
+        (task_static_job([70000]), [None, None, None], "network: invalid port 70000 (out of range)"),
+        (task_static_job([8080], mbits=2000), [None, None, None], "network: bandwidth exceeded"),
+    ]
+    for job, want, reason in cases:
+        for row, w in enumerate(want):
+            st = stack_cls()
+            st.SetState(nodes, allocs)
+            st.SetJob(job)
+            st.EnableMetrics(True)
+            st.SetNodes([row])
+            r = st.SelectRaw(0)
+            assert (r.row if r.row >= 0 else None) == w, (job.task_groups[0].tasks[0].network.reserved_ports, row)
+            if w is None and reason and row in (0, 1) and "p8080" not in reason:
+                assert st.LastMetrics()["DimensionExhausted"] == {reason: 1}
+            if w is None and "p8080" in reason:
+                assert st.LastMetrics()["DimensionExhausted"] == {reason: 1}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,count,ports", [(900, 900, [8080]), (4000, 3000, [443, 5000])])
+def test_task_static_ports_count_loop(n, count, ports):
+    nodes, allocs = task_port_cluster(n, seed=n)
+    job = task_static_job(ports, count=count)
+    perm = synth.shuffle(len(nodes), 3)
+    _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, perm)
+    _, _, re = run_place(_engine, nodes, allocs, job, perm)
+    assert_same_placements(re, ro)
+    assert 0 < sum(1 for x in re if x.row >= 0) < count
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("task", [True, False])
+def test_static_port_preemption_count_loop(task):
+    """Saturated cluster, preemption on: nil Selects retried with Preempt=true
+    evict the static port's holders (and bandwidth for task networks),
+    placement by placement equal to the oracle, with the preempted sets."""
+    from nomad_amd.structs import SchedulerConfig
+    nodes, allocs = task_port_cluster(1500, seed=77, busy=0.9)
+    if task:
+        job = task_static_job([8080], mbits=500, count=400, priority=70, cpu=1500)
+    else:
+        job = static_job([8080], dyn=0, count=400)
+        job.priority = 70
+        job.task_groups[0].tasks[0].cpu = 1500
+    cfg = SchedulerConfig(preempt_service=True)
+    perm = synth.shuffle(len(nodes), 9)
+    _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, perm, config=cfg)
+    _, _, re = run_place(_engine, nodes, allocs, job, perm, config=cfg)
+    assert_same_placements(re, ro)
+    assert [sorted(x.preempted) for x in re] == [sorted(x.preempted) for x in ro]
+    assert sum(1 for x in re if x.preempted) > 5

@@ -12,3 +12,7 @@ timeout -k 10 120 python -u tools/chain_prof.py > "$OUT/chain_prof.txt" 2>&1 || 
 cat "$OUT/chain_prof.txt"
 PE_API_PROF=1 timeout -k 10 120 python -u tools/dropin_probe.py > "$OUT/dropin_probe.txt" 2>&1 || { tail -30 "$OUT/dropin_probe.txt"; exit 1; }
 tail -40 "$OUT/dropin_probe.txt"
+PE_PLACE_PROF=1 timeout -k 10 180 python -u tools/c5_prof.py > "$OUT/c5_prof.txt" 2>&1 || { tail -30 "$OUT/c5_prof.txt"; exit 1; }
+cat "$OUT/c5_prof.txt"
+PE_API_PROF=1 timeout -k 10 120 python -u tools/dropin_probe.py 100 10 2000 > "$OUT/dropin_probe_c1.txt" 2>&1 || { tail -30 "$OUT/dropin_probe_c1.txt"; exit 1; }
+tail -40 "$OUT/dropin_probe_c1.txt"
