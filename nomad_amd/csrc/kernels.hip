@@ -1516,13 +1516,15 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 if (W > Wfull) W = Wfull;
             }
             force_full = false;
+            // items a lane holds this phase (wave-uniform): the rest lie past the window
+            const int qn = (int)((W + kChainBlock - 1) / kChainBlock);
             // 1. values of the window [cur, cur + n): base (no placement of this
             //    launch on the row), base1 (one), or queued for re-evaluation
             uint32_t row[kChainItems];
             double v[kChainItems];
             if (tid == 0) sh.n_redo = 0;
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
+            for (int q = 0; q < kChainItems && q < qn; q++) {
                 const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                 row[q] = j < W ? perm[wrap_pos(cur + j, n)] : 0u;
             }
@@ -1532,7 +1534,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             const bool use_bm = placed && sh.slow == 0;
             if (placed) {
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < kChainItems && q < qn; q++) {
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                     if (j < W) {
                         uint32_t b1 = 1, b2 = 1;
@@ -1553,14 +1555,14 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
             }
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
+            for (int q = 0; q < kChainItems && q < qn; q++) {
                 const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                 const double* src = ((one_mask >> q) & 1u) ? A.base1 : A.base;
                 v[q] = j < W ? src[A.base_by_pos ? wrap_pos(cur + j, n) : row[q]] : -__builtin_inf();
             }
             if (__syncthreads_or(redo_mask != 0)) {
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < kChainItems && q < qn; q++) {
                     if ((redo_mask >> q) & 1u) {
                         const uint32_t slot = atomicAdd(&sh.n_redo, 1u);
                         sh.redo[slot] = make_uint2(row[q], ov_count(ov, row[q]));
@@ -1582,7 +1584,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < kChainItems && q < qn; q++) {
                     if ((redo_mask >> q) & 1u) {
                         const uint2 r2 = sh.redo[(uint32_t)gm::f2u(v[q])];
                         v[q] = gm::u2f(((unsigned long long)r2.y << 32) | r2.x);
@@ -1591,7 +1593,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             }
             uint32_t optmask = 0, nmask = 0;   // bit q: position holds an option / a non-positive option
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
+            for (int q = 0; q < kChainItems && q < qn; q++) {
                 const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                 if (j < W) vs[j] = v[q];   // read back by the Select walks of step 5 (after the barriers)
                 const bool is_o = j < W && v[q] > -__builtin_inf() && v[q] < __builtin_inf();
@@ -1646,7 +1648,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             // 3. option index and N prefix of every option; nb[k] = N options before option k
             uint32_t pk[kChainItems];
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
+            for (int q = 0; q < kChainItems && q < qn; q++) {
                 const uint64_t bo = __ballot((optmask >> q) & 1u), bn = __ballot((nmask >> q) & 1u);
                 const uint32_t t = (uint32_t)(q * (kChainBlock / 64) + wave);
                 const bool live = (uint32_t)(q * kChainBlock) < W;
@@ -1666,97 +1668,123 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             //    option in parallel; 4b: per 64-option segment and entry offset the
             //    Selects inside and the exit offset; 4c: one lane walks the
             //    segments; 4d: the Selects are written out in parallel.
+            if (tot_n == 0) {
+                // no non-positive option in the window: every Select returns
+                // exactly L options (m = 0 above), so Select s stops at option
+                // (s + 1) L - 1; nb takes the options' positions at once
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
-                if ((optmask >> q) & 1u) {
-                    const uint32_t i = pk[q] & kIdxMask;
-                    const uint32_t a0 = pk[q] >> kIdxBits;
-                    uint32_t nxt = kNxFail;
-                    if (i + L - 1 < tot_o) {
-                        if (nb[min(i + L, tot_o)] - a0 == 0) nxt = i + L;
-                        else if (i + L < tot_o) {
-                            if (nb[i + L + 1] - a0 == 1) nxt = i + L + 1;
-                            else if (i + L + 1 < tot_o) {
-                                if (nb[i + L + 2] - a0 == 2) nxt = i + L + 2;
-                                else if (i + L + 2 < tot_o) nxt = i + L + 3;
+                for (int q = 0; q < kChainItems && q < qn; q++)
+                    if ((optmask >> q) & 1u) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
+                if (tid == 0) {
+                    const uint32_t want = min(A.count - placed, (uint32_t)kChainMaxSel);
+                    const uint32_t fit = tot_o / L;
+                    uint32_t ns = fit < want ? fit : want;
+                    int fmode = kPhaseMore;
+                    if (ns == 0 && W < Wfull) fmode = kPhaseRetry;
+                    else if (ns == 0 && W < n) fmode = kPhaseStall;
+                    else if (ns == 0) { fmode = kPhaseExhausted; ns = tot_o ? 1u : 0u; if (ns) sh.sel_b[0] = tot_o - 1; }
+                    else if (ns == A.count - placed) fmode = kPhaseCount;
+                    sh.nsel = ns;
+                    sh.mode = (uint32_t)fmode;
+                    sh.n_seg = 0;
+                }
+                __syncthreads();
+                if (sh.mode == (uint32_t)kPhaseMore || sh.mode == (uint32_t)kPhaseCount)
+                    for (uint32_t sel = tid; sel < sh.nsel; sel += kChainBlock) sh.sel_b[sel] = (sel + 1) * L - 1;
+                __syncthreads();
+            } else {
+#pragma unroll
+                for (int q = 0; q < kChainItems && q < qn; q++) {
+                    if ((optmask >> q) & 1u) {
+                        const uint32_t i = pk[q] & kIdxMask;
+                        const uint32_t a0 = pk[q] >> kIdxBits;
+                        uint32_t nxt = kNxFail;
+                        if (i + L - 1 < tot_o) {
+                            if (nb[min(i + L, tot_o)] - a0 == 0) nxt = i + L;
+                            else if (i + L < tot_o) {
+                                if (nb[i + L + 1] - a0 == 1) nxt = i + L + 1;
+                                else if (i + L + 1 < tot_o) {
+                                    if (nb[i + L + 2] - a0 == 2) nxt = i + L + 2;
+                                    else if (i + L + 2 < tot_o) nxt = i + L + 3;
+                                }
                             }
                         }
+                        nx[i] = (uint16_t)nxt;
                     }
-                    nx[i] = (uint16_t)nxt;
                 }
-            }
-            if (tid == 0) nx[tot_o] = kNxFail;
-            __syncthreads();
-            // nb is free from here on: the relative position of every option
+                if (tid == 0) nx[tot_o] = kNxFail;
+                __syncthreads();
+                // nb is free from here on: the relative position of every option
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++)
-                if ((optmask >> q) & 1u) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
-            const uint32_t n_seg = (tot_o + kSegLen - 1) / kSegLen;
-            const uint32_t E = L + 3;
-            for (uint32_t t = tid; t < n_seg * E; t += kChainBlock) {
-                const uint32_t g = t / E, o = t - g * E;
-                const uint32_t end = kSegLen * (g + 1);
-                uint32_t i = kSegLen * g + o, cnt = 0, ex = kExFail;
-                for (;;) {
-                    if (i >= end) { ex = i - end; break; }
-                    if (i >= tot_o) break;
-                    const uint32_t x = nx[i];
-                    if (x == kNxFail) break;
-                    cnt++;
-                    i = x;
-                }
-                sh.seg_tab[g][o] = cnt | (ex << 16);
-            }
-            __syncthreads();
-            if (tid == 0) {
-                const uint32_t want = min(A.count - placed, (uint32_t)kChainMaxSel);
-                uint32_t total = 0, o = 0, used = 0;
-                for (uint32_t g = 0; g < n_seg; g++) {
-                    const uint32_t te = sh.seg_tab[g][o], cnt = te & 0xFFFFu, ex = te >> 16;
-                    sh.seg_entry[g] = (uint16_t)o;
-                    sh.seg_base[g] = (uint16_t)total;
-                    used = g + 1;
-                    if (total + cnt >= want) { total = want; break; }
-                    total += cnt;
-                    if (ex == kExFail) break;
-                    o = ex;
-                }
-                int mode = kPhaseMore;
-                uint32_t ns = total;
-                if (ns == 0 && W < Wfull) {
-                    // the shortened window held no whole Select: again with the full one
-                    mode = kPhaseRetry;
-                    used = 0;
-                } else if (ns == 0 && W < n) {
-                    // a Select needs more than the window: the lazy loop goes on from here
-                    mode = kPhaseStall;
-                    used = 0;
-                } else if (ns == 0) {
-                    // the first Select saw the whole list without reaching the limit
-                    mode = kPhaseExhausted;
-                    ns = tot_o ? 1u : 0u;
-                    if (ns) sh.sel_b[0] = tot_o - 1;
-                    used = 0;
-                } else if (ns == A.count - placed) {
-                    mode = kPhaseCount;
-                }
-                sh.nsel = ns;
-                sh.mode = (uint32_t)mode;
-                sh.n_seg = used;
-            }
-            __syncthreads();
-            {
-                const uint32_t ns = sh.nsel, used = sh.n_seg;
-                for (uint32_t g = tid; g < used; g += kChainBlock) {
-                    uint32_t i = kSegLen * g + sh.seg_entry[g], sel = sh.seg_base[g];
-                    while (sel < ns && i < kSegLen * (g + 1)) {
+                for (int q = 0; q < kChainItems && q < qn; q++)
+                    if ((optmask >> q) & 1u) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
+                const uint32_t n_seg = (tot_o + kSegLen - 1) / kSegLen;
+                const uint32_t E = L + 3;
+                for (uint32_t t = tid; t < n_seg * E; t += kChainBlock) {
+                    const uint32_t g = t / E, o = t - g * E;
+                    const uint32_t end = kSegLen * (g + 1);
+                    uint32_t i = kSegLen * g + o, cnt = 0, ex = kExFail;
+                    for (;;) {
+                        if (i >= end) { ex = i - end; break; }
+                        if (i >= tot_o) break;
                         const uint32_t x = nx[i];
-                        sh.sel_b[sel++] = x - 1u;
+                        if (x == kNxFail) break;
+                        cnt++;
                         i = x;
                     }
+                    sh.seg_tab[g][o] = cnt | (ex << 16);
                 }
+                __syncthreads();
+                if (tid == 0) {
+                    const uint32_t want = min(A.count - placed, (uint32_t)kChainMaxSel);
+                    uint32_t total = 0, o = 0, used = 0;
+                    for (uint32_t g = 0; g < n_seg; g++) {
+                        const uint32_t te = sh.seg_tab[g][o], cnt = te & 0xFFFFu, ex = te >> 16;
+                        sh.seg_entry[g] = (uint16_t)o;
+                        sh.seg_base[g] = (uint16_t)total;
+                        used = g + 1;
+                        if (total + cnt >= want) { total = want; break; }
+                        total += cnt;
+                        if (ex == kExFail) break;
+                        o = ex;
+                    }
+                    int mode = kPhaseMore;
+                    uint32_t ns = total;
+                    if (ns == 0 && W < Wfull) {
+                        // the shortened window held no whole Select: again with the full one
+                        mode = kPhaseRetry;
+                        used = 0;
+                    } else if (ns == 0 && W < n) {
+                        // a Select needs more than the window: the lazy loop goes on from here
+                        mode = kPhaseStall;
+                        used = 0;
+                    } else if (ns == 0) {
+                        // the first Select saw the whole list without reaching the limit
+                        mode = kPhaseExhausted;
+                        ns = tot_o ? 1u : 0u;
+                        if (ns) sh.sel_b[0] = tot_o - 1;
+                        used = 0;
+                    } else if (ns == A.count - placed) {
+                        mode = kPhaseCount;
+                    }
+                    sh.nsel = ns;
+                    sh.mode = (uint32_t)mode;
+                    sh.n_seg = used;
+                }
+                __syncthreads();
+                {
+                    const uint32_t ns = sh.nsel, used = sh.n_seg;
+                    for (uint32_t g = tid; g < used; g += kChainBlock) {
+                        uint32_t i = kSegLen * g + sh.seg_entry[g], sel = sh.seg_base[g];
+                        while (sel < ns && i < kSegLen * (g + 1)) {
+                            const uint32_t x = nx[i];
+                            sh.sel_b[sel++] = x - 1u;
+                            i = x;
+                        }
+                    }
+                }
+                __syncthreads();
             }
-            __syncthreads();
             const uint32_t nsel = sh.nsel;
             const int mode = (int)sh.mode;
             if (mode == kPhaseStall) {
@@ -1780,7 +1808,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 // window (atomics over one key), its first kMaxSkip N's set aside
                 uint32_t retmask = 0;
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < kChainItems && q < qn; q++) {
                     if ((optmask >> q) & 1u) {
                         const uint32_t nrank = pk[q] >> kIdxBits;   // N options before this one
                         const bool aside = ((nmask >> q) & 1u) && nrank < (uint32_t)kMaxSkip;
@@ -1795,12 +1823,12 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++)
+                for (int q = 0; q < kChainItems && q < qn; q++)
                     if (((retmask >> q) & 1u) && order_key(v[q]) == sh.sel_max[0])
                         atomicMin(&sh.sel_arg[0], pk[q] & kIdxMask);
                 if (A.full_out || A.emit) {
 #pragma unroll
-                    for (int q = 0; q < kChainItems; q++) {
+                    for (int q = 0; q < kChainItems && q < qn; q++) {
                         const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                         if (j < W && !((optmask >> q) & 1u))
                             atomicAdd(v[q] == -__builtin_inf() ? &sh.sel_f[0] : &sh.sel_x[0], 1u);
@@ -1808,7 +1836,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < kChainItems && q < qn; q++) {
                     if (((retmask >> q) & 1u) && sh.sel_arg[0] == (pk[q] & kIdxMask)) {
                         sh.sel_row[0] = row[q];
                         sh.sel_max[0] = (unsigned long long)gm::f2u(v[q]);
