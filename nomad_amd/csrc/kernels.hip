@@ -1261,15 +1261,19 @@ __device__ __forceinline__ double encode_eval(const NodeEval& ev) {
 // serves every evaluation of a batch. base1 (one placement on the row) is
 // computed by a second set of lanes rather than after base in the same lane:
 // the pass is one dependent load + evaluate chain per lane, so the two tables
-// finish in the time of one; 64-lane workgroups spread it over more CUs.
+// finish in the time of one; 64-lane workgroups spread it over more CUs. The
+// two lanes of one position are neighbours in a wave, so the row's column
+// lines are fetched once for both (halves in separate workgroups landed on
+// separate XCDs and fetched every line twice).
 constexpr int kBaseBlock = 64;
 __global__ void __launch_bounds__(kBaseBlock) k_base(BatchArgs A) {
     const uint32_t stride = gridDim.x * kBaseBlock;
     const uint32_t m = A.base_by_pos ? A.n_visit : A.soa.n;
-    const uint32_t total = A.base1 ? 2u * m : m;
+    const uint32_t sh = A.base1 ? 1u : 0u;
+    const uint32_t total = m << sh;
     for (uint32_t t = blockIdx.x * kBaseBlock + threadIdx.x; t < total; t += stride) {
-        const uint32_t dk = t >= m ? 1u : 0u;
-        const uint32_t j = t - dk * m;
+        const uint32_t dk = t & sh;
+        const uint32_t j = t >> sh;
         uint32_t row = j;
         if (A.base_by_pos) {
             if (A.perm_src) {
