@@ -1424,6 +1424,24 @@ constexpr uint32_t kIdxBits = 14, kIdxMask = (1u << kIdxBits) - 1u;
     } while (0)
 
 
+// The chain's rare heavy paths out of line: inlined, the table and ask fields
+// they read were hoisted to the kernel's start and held (spilled) for its
+// whole run.
+__device__ __noinline__ void chain_emit_full(const BatchArgs& A, Overlay ov, uint32_t e, uint32_t it, int win_row,
+                                             double score, uint32_t consumed, uint32_t f, uint32_t x, uint32_t next_off) {
+    emit_placement<false>(A, A.tg.class_ok, ov, nullptr, e, it, win_row, score, consumed, f, x, next_off);
+}
+
+// value of (row, placements) re-evaluated: the k_base pipeline with dk placements
+__device__ __noinline__ double chain_reeval(const BatchArgs& A, uint32_t row, uint32_t dk) {
+    NodeIn in;
+    load_node(A.soa, A.tg, row, in);
+    NodeEval ev;
+    ev.score = 0.0;
+    eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+    return encode_eval(ev);
+}
+
 // Step 5 of k_chain (out of line: its loads would otherwise raise the whole
 // kernel's register pressure).
 template <class Sh>
@@ -1470,6 +1488,9 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
     const uint32_t Wfull = n < kChainMaxN ? n : kChainMaxN;
     const uint32_t L = A.limit;
     const uint32_t H = 1u << A.hash_bits;
+    // A in the kernel-argument segment, for the out-of-line helpers (taking the
+    // parameter's address would copy the whole struct to scratch)
+    const BatchArgs& Ak = *(const BatchArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     Overlay ov;
     ov.bits = A.hash_bits;
     ov.mask = H - 1;
@@ -1524,87 +1545,95 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             const int qn = (int)((W + kChainBlock - 1) / kChainBlock);
             // 1. values of the window [cur, cur + n): base (no placement of this
             //    launch on the row), base1 (one), or queued for re-evaluation
-            uint32_t row[kChainItems];
-            double v[kChainItems];
             if (tid == 0) sh.n_redo = 0;
-#pragma unroll
-            for (int q = 0; q < kChainItems && q < qn; q++) {
-                const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                row[q] = j < W ? perm[wrap_pos(cur + j, n)] : 0u;
-            }
             // rows holding placements of this launch: one (base1) from the
             // position bitmaps, two or more re-evaluated (ov_count)
-            uint32_t one_mask = 0, redo_mask = 0;
             const bool use_bm = placed && sh.slow == 0;
-            if (placed) {
+            uint32_t optmask = 0, nmask = 0, redo_mask = 0;   // bit q: option / non-positive option / re-evaluate
+            {
+                // rows are read only where the value needs them: every position
+                // without the bitmaps (overlay probes) or for a row-indexed base,
+                // else none (the first phase reads base, later ones base / base1
+                // by position and re-evaluate the bitmaps' rows from the list)
+                const bool rows_all = !A.base_by_pos || (placed && !use_bm);
+                uint32_t row[kChainItems];
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++) {
+                for (int q = 0; q < kChainItems; q++) {
+                    if (q >= qn) break;
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                    if (j < W) {
-                        uint32_t b1 = 1, b2 = 1;
-                        if (use_bm) {
-                            const uint32_t p = wrap_pos(cur + j, n), bit = 1u << (p & 31);
-                            b1 = sh.bm1[p >> 5] & bit;
-                            b2 = sh.bm2[p >> 5] & bit;
-                        }
-                        if (b1 && b2) {
-                            const uint32_t dk = ov_count(ov, row[q]);
-                            if (dk == 1u && A.base1) one_mask |= 1u << q;
-                            else if (dk) redo_mask |= 1u << q;
-                        } else if (b1) {
-                            if (A.base1) one_mask |= 1u << q;
-                            else redo_mask |= 1u << q;
+                    row[q] = rows_all && j < W ? perm[wrap_pos(cur + j, n)] : 0u;
+                }
+                uint32_t one_mask = 0;
+                if (placed) {
+#pragma unroll
+                    for (int q = 0; q < kChainItems; q++) {
+                        if (q >= qn) break;
+                        const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                        if (j < W) {
+                            uint32_t b1 = 1, b2 = 1;
+                            if (use_bm) {
+                                const uint32_t p = wrap_pos(cur + j, n), bit = 1u << (p & 31);
+                                b1 = sh.bm1[p >> 5] & bit;
+                                b2 = sh.bm2[p >> 5] & bit;
+                                if (b1 && (b2 || !A.base1)) redo_mask |= 1u << q;
+                                else if (b1) one_mask |= 1u << q;
+                            } else {
+                                const uint32_t dk = ov_count(ov, row[q]);
+                                if (dk == 1u && A.base1) one_mask |= 1u << q;
+                                else if (dk) redo_mask |= 1u << q;
+                            }
                         }
                     }
                 }
-            }
 #pragma unroll
-            for (int q = 0; q < kChainItems && q < qn; q++) {
-                const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                const double* src = ((one_mask >> q) & 1u) ? A.base1 : A.base;
-                v[q] = j < W ? src[A.base_by_pos ? wrap_pos(cur + j, n) : row[q]] : -__builtin_inf();
+                for (int q = 0; q < kChainItems; q++) {
+                    if (q >= qn) break;
+                    const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                    if (j < W && !((redo_mask >> q) & 1u)) {
+                        const double* src = ((one_mask >> q) & 1u) ? A.base1 : A.base;
+                        const double v = src[A.base_by_pos ? wrap_pos(cur + j, n) : row[q]];
+                        vs[j] = v;   // read back by the Select walks of step 5 (after the barriers)
+                        const bool is_o = v > -__builtin_inf() && v < __builtin_inf();
+                        optmask |= (uint32_t)is_o << q;
+                        nmask |= (uint32_t)(is_o && v <= 0.0) << q;
+                    }
+                }
             }
             if (__syncthreads_or(redo_mask != 0)) {
+                // rows with placements of this launch the tables do not cover:
+                // evaluated in parallel, the value stored at its window position
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++) {
+                for (int q = 0; q < kChainItems; q++) {
+                    if (q >= qn) break;
                     if ((redo_mask >> q) & 1u) {
+                        const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                        const uint32_t r = perm[wrap_pos(cur + j, n)];
                         const uint32_t slot = atomicAdd(&sh.n_redo, 1u);
-                        sh.redo[slot] = make_uint2(row[q], ov_count(ov, row[q]));
-                        v[q] = gm::u2f((unsigned long long)slot);   // slot index until the value is back
+                        sh.redo[slot] = make_uint2(r, ov_count(ov, r) | (j << 18));
                     }
                 }
                 __syncthreads();
                 const uint32_t nr = sh.n_redo;
                 for (uint32_t w = tid; w < nr; w += kChainBlock) {
                     const uint2 rd = sh.redo[w];
-                    NodeIn in;
-                    load_node(A.soa, A.tg, rd.x, in);
-                    NodeEval ev;
-                    ev.score = 0.0;
-                    eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, rd.y, A.penalty_bits, A.log10, nullptr,
-                                       rd.x, in, &ev);
-                    const unsigned long long bits = (unsigned long long)gm::f2u(encode_eval(ev));
-                    sh.redo[w] = make_uint2((uint32_t)bits, (uint32_t)(bits >> 32));
+                    vs[rd.y >> 18] = chain_reeval(Ak, rd.x, rd.y & 0x3FFFFu);
                 }
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++) {
+                for (int q = 0; q < kChainItems; q++) {
+                    if (q >= qn) break;
                     if ((redo_mask >> q) & 1u) {
-                        const uint2 r2 = sh.redo[(uint32_t)gm::f2u(v[q])];
-                        v[q] = gm::u2f(((unsigned long long)r2.y << 32) | r2.x);
+                        const double v = vs[q * kChainBlock + tid];
+                        const bool is_o = v > -__builtin_inf() && v < __builtin_inf();
+                        optmask |= (uint32_t)is_o << q;
+                        nmask |= (uint32_t)(is_o && v <= 0.0) << q;
                     }
                 }
             }
-            uint32_t optmask = 0, nmask = 0;   // bit q: position holds an option / a non-positive option
 #pragma unroll
-            for (int q = 0; q < kChainItems && q < qn; q++) {
-                const uint32_t j = (uint32_t)(q * kChainBlock + tid);
-                if (j < W) vs[j] = v[q];   // read back by the Select walks of step 5 (after the barriers)
-                const bool is_o = j < W && v[q] > -__builtin_inf() && v[q] < __builtin_inf();
-                const bool is_n = is_o && v[q] <= 0.0;
-                optmask |= (uint32_t)is_o << q;
-                nmask |= (uint32_t)is_n << q;
-                const uint64_t bo = __ballot(is_o), bn = __ballot(is_n);
+            for (int q = 0; q < kChainItems; q++) {
+                if (q >= qn) break;
+                const uint64_t bo = __ballot((optmask >> q) & 1u), bn = __ballot((nmask >> q) & 1u);
                 if (lane == 0 && q * kChainBlock < (int)W) {
                     sh.tile_o[q * (kChainBlock / 64) + wave] = (uint32_t)__popcll(bo);
                     sh.tile_n[q * (kChainBlock / 64) + wave] = (uint32_t)__popcll(bn);
@@ -1652,7 +1681,8 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             // 3. option index and N prefix of every option; nb[k] = N options before option k
             uint32_t pk[kChainItems];
 #pragma unroll
-            for (int q = 0; q < kChainItems && q < qn; q++) {
+            for (int q = 0; q < kChainItems; q++) {
+                if (q >= qn) break;
                 const uint64_t bo = __ballot((optmask >> q) & 1u), bn = __ballot((nmask >> q) & 1u);
                 const uint32_t t = (uint32_t)(q * (kChainBlock / 64) + wave);
                 const bool live = (uint32_t)(q * kChainBlock) < W;
@@ -1677,8 +1707,8 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 // exactly L options (m = 0 above), so Select s stops at option
                 // (s + 1) L - 1; nb takes the options' positions at once
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++)
-                    if ((optmask >> q) & 1u) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
+                for (int q = 0; q < kChainItems; q++)
+                    if (q < qn && ((optmask >> q) & 1u)) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
                 if (tid == 0) {
                     const uint32_t want = min(A.count - placed, (uint32_t)kChainMaxSel);
                     const uint32_t fit = tot_o / L;
@@ -1698,7 +1728,8 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 __syncthreads();
             } else {
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++) {
+                for (int q = 0; q < kChainItems; q++) {
+                    if (q >= qn) break;
                     if ((optmask >> q) & 1u) {
                         const uint32_t i = pk[q] & kIdxMask;
                         const uint32_t a0 = pk[q] >> kIdxBits;
@@ -1720,8 +1751,8 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 __syncthreads();
                 // nb is free from here on: the relative position of every option
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++)
-                    if ((optmask >> q) & 1u) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
+                for (int q = 0; q < kChainItems; q++)
+                    if (q < qn && ((optmask >> q) & 1u)) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
                 const uint32_t n_seg = (tot_o + kSegLen - 1) / kSegLen;
                 const uint32_t E = L + 3;
                 for (uint32_t t = tid; t < n_seg * E; t += kChainBlock) {
@@ -1812,38 +1843,49 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 // window (atomics over one key), its first kMaxSkip N's set aside
                 uint32_t retmask = 0;
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++) {
+                for (int q = 0; q < kChainItems; q++) {
+                    if (q >= qn) break;
                     if ((optmask >> q) & 1u) {
+                        const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                        const double vq = vs[j];
                         const uint32_t nrank = pk[q] >> kIdxBits;   // N options before this one
                         const bool aside = ((nmask >> q) & 1u) && nrank < (uint32_t)kMaxSkip;
                         if (!aside) {
                             retmask |= 1u << q;
-                            atomicMax(&sh.sel_max[0], order_key(v[q]));
+                            atomicMax(&sh.sel_max[0], order_key(vq));
                         } else {
-                            sh.aside_v[nrank] = v[q];
-                            sh.aside_row[nrank] = row[q];
+                            sh.aside_v[nrank] = vq;
+                            sh.aside_row[nrank] = perm[wrap_pos(cur + j, n)];
                         }
                     }
                 }
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++)
-                    if (((retmask >> q) & 1u) && order_key(v[q]) == sh.sel_max[0])
+                for (int q = 0; q < kChainItems; q++) {
+                    if (q >= qn) break;
+                    const uint32_t j = (uint32_t)(q * kChainBlock + tid);
+                    if (((retmask >> q) & 1u) &&
+                        order_key(vs[j]) == sh.sel_max[0])
                         atomicMin(&sh.sel_arg[0], pk[q] & kIdxMask);
+                }
                 if (A.full_out || A.emit) {
 #pragma unroll
-                    for (int q = 0; q < kChainItems && q < qn; q++) {
+                    for (int q = 0; q < kChainItems; q++) {
+                        if (q >= qn) break;
                         const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                         if (j < W && !((optmask >> q) & 1u))
-                            atomicAdd(v[q] == -__builtin_inf() ? &sh.sel_f[0] : &sh.sel_x[0], 1u);
+                            atomicAdd(vs[j] == -__builtin_inf()
+                                          ? &sh.sel_f[0] : &sh.sel_x[0], 1u);
                     }
                 }
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kChainItems && q < qn; q++) {
+                for (int q = 0; q < kChainItems; q++) {
+                    if (q >= qn) break;
+                    const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                     if (((retmask >> q) & 1u) && sh.sel_arg[0] == (pk[q] & kIdxMask)) {
-                        sh.sel_row[0] = row[q];
-                        sh.sel_max[0] = (unsigned long long)gm::f2u(v[q]);
+                        sh.sel_row[0] = perm[wrap_pos(cur + j, n)];
+                        sh.sel_max[0] = (unsigned long long)gm::f2u(vs[j]);
                     }
                 }
             }
@@ -1868,8 +1910,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                         m.new_offset = next_off;
                         m.score = score;
                     } else if (A.full_out) {
-                        emit_placement<false>(A, A.tg.class_ok, ov, nullptr, e, it, win_row, score, consumed, sh.sel_f[s],
-                                       sh.sel_x[s], next_off);
+                        chain_emit_full(Ak, ov, e, it, win_row, score, consumed, sh.sel_f[s], sh.sel_x[s], next_off);
                     }
                     if (A.out) {
                         pe_placement& o = A.out[(size_t)e * A.count + it];
@@ -1915,8 +1956,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                         m.new_offset = cur;
                         m.score = best;
                     } else if (A.full_out) {
-                        emit_placement<false>(A, A.tg.class_ok, ov, nullptr, e, placed, win_row, best, n, sh.sel_f[0],
-                                       sh.sel_x[0], cur);
+                        chain_emit_full(Ak, ov, e, placed, win_row, best, n, sh.sel_f[0], sh.sel_x[0], cur);
                     }
                     sh.n_emit = placed + 1;
                     sh.slow = 1;   // the winner's position is not tracked: later phases probe the overlay
@@ -3159,7 +3199,7 @@ int pe_chain_blocks_per_cu(size_t lds) {
 
 hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st) {
     if (!a->base || !a->chain_vs || (a->n_visit > pe::kChainMaxN && n_evals != 1) || a->class_ok_stride ||
-        a->limit > pe::kMaxChainLimit)
+        a->limit > pe::kMaxChainLimit || a->count >= (1u << 18))   // redo entries pack count | position << 18
         return hipErrorInvalidValue;
     if (a->base_by_pos && n_evals != 1) return hipErrorInvalidValue;
     if (a->perm_src && (!a->base_by_pos || !a->perm_dst)) return hipErrorInvalidValue;
