@@ -41,7 +41,7 @@ hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_rank_of(const uint32_t* list, uint32_t n_list, uint32_t* rank_of, uint32_t n_rows, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
 hipError_t pe_launch_counts(const pe::CountDsts* d, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
-                            hipStream_t st);
+                            const pe::ResetArgs* r, hipStream_t st);
 size_t pe_fullpass_lds_bytes(uint32_t n);
 hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
                                   uint32_t count, pe_ranked_node* out, uint32_t* state, unsigned long long* prof,
@@ -383,6 +383,9 @@ struct pe_stack {
     bool dev_packable = true;          // every node fits the packed 4 x u8 free-count column
     std::vector<uint32_t> h_dev_free;  // snapshot free healthy instances per group (no plan)
     DevMem d_dev_free, d_dev_free_base;
+    // ResetPlan's state copy not launched yet: it rides in SetJob's k_counts
+    // launch, any other call launches it first (flush_reset)
+    bool reset_pending = false;
     // preemption: non-terminal state allocs per node (CSR, table order) as PreemptAlloc
     std::vector<uint32_t> h_node_alloc_off, h_palloc_index;   // CSR; slot -> alloc-table row
     std::vector<uint32_t> alloc_slot;          // alloc-table row -> slot (PE_NONE: terminal)
@@ -1937,11 +1940,46 @@ void core_hold(pe_stack* s, uint32_t alloc, bool hold) {
 // minus plan placements and plan stops). The counts are mostly zero (a new
 // job, a short plan): the nonzero ones go up as a sorted sparse list and one
 // launch rewrites every array, instead of one dense upload per array.
+static pe::ResetArgs reset_args(pe_stack* s) {
+    pe::ResetArgs R;
+    R.rec = s->d_rec.as<pe::NodeRec>();
+    R.base_rec = s->d_base_rec.as<pe::NodeRec>();
+    R.dev_free = s->d_dev_free.as<uint32_t>();
+    R.dev_free_base = s->d_dev_free_base.as<uint32_t>();
+    R.n = (uint32_t)s->nodes.size();
+    R.preempted = s->d_preempted.as<uint8_t>();
+    R.m = (uint32_t)s->h_preempted.size();
+    R.pcount = s->d_pcount.as<uint32_t>();
+    R.keys = std::max<uint32_t>(s->n_jtg_keys, 1);
+    return R;
+}
+
+// The deferred ResetPlan launch, before any other device work of the handle.
+static int flush_reset(pe_stack* s) {
+    if (!s->reset_pending) return PE_OK;
+    s->reset_pending = false;
+    HIP_TRY(s, hipSetDevice(s->device));
+    const pe::ResetArgs R = reset_args(s);
+    HIP_TRY(s, pe_launch_reset_plan(R.rec, R.base_rec, R.dev_free, R.dev_free_base, R.n, R.preempted, R.m, R.pcount,
+                                    R.keys, s->stream));
+    return PE_OK;
+}
+
+
+#define PE_FLUSH_RESET(s)                             \
+    do {                                              \
+        if ((s) && (s)->reset_pending) {              \
+            const int frc_ = flush_reset(s);          \
+            if (frc_) return frc_;                    \
+        }                                             \
+    } while (0)
+
 int build_collisions(pe_stack* s, bool own = false) {
     const size_t n = s->nodes.size();
     const uint32_t ntg = (uint32_t)s->tgs.size();
     const uint32_t nd = ntg + 2;   // dst 0: own, 1: job, 2 + g: task group g
     if (nd > (uint32_t)pe::kMaxCountDst || n >= (size_t(1) << 27)) {
+        PE_FLUSH_RESET(s);
         std::vector<uint32_t> job(n, 0), mine(own ? n : 0, 0);
         std::vector<std::vector<uint32_t>> tg(ntg, std::vector<uint32_t>(n, 0));
         auto add = [&](uint32_t row, uint32_t tgname) {
@@ -1988,8 +2026,10 @@ int build_collisions(pe_stack* s, bool own = false) {
         D.d[2 + g] = s->tgs[g]->coll_tg.as<uint32_t>();
     }
     if (!ents.empty()) HIP_TRY(s, upload_s(s, s->d_count_ents, ents));
+    const pe::ResetArgs R = s->reset_pending ? reset_args(s) : pe::ResetArgs{};
+    s->reset_pending = false;
     HIP_TRY(s, pe_launch_counts(&D, nd, (uint32_t)n, ents.empty() ? nullptr : s->d_count_ents.as<uint2>(),
-                                (uint32_t)ents.size(), s->stream));
+                                (uint32_t)ents.size(), R.rec ? &R : nullptr, s->stream));
     return PE_OK;
 }
 
@@ -3504,7 +3544,9 @@ static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_ta
     return rc;
 }
 
-static int reset_plan_one(pe_stack* s) {
+// may_defer: a handle without child devices leaves the state copy to the next
+// SetJob's k_counts launch (one launch less per evaluation)
+static int reset_plan_one(pe_stack* s, bool may_defer) {
     if (!s) return PE_EINVAL;
     ApiScope prof_(s, "reset_plan");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
@@ -3515,10 +3557,11 @@ static int reset_plan_one(pe_stack* s) {
     HIP_TRY(s, hipSetDevice(s->device));
     const size_t n = s->nodes.size();
     ApiScope prof_launch_(s, "reset_plan.launch");
-    HIP_TRY(s, pe_launch_reset_plan(s->d_rec.as<pe::NodeRec>(), s->d_base_rec.as<pe::NodeRec>(),
-                                    s->d_dev_free.as<uint32_t>(), s->d_dev_free_base.as<uint32_t>(), (uint32_t)n,
-                                    s->d_preempted.as<uint8_t>(), (uint32_t)s->h_preempted.size(),
-                                    s->d_pcount.as<uint32_t>(), std::max<uint32_t>(s->n_jtg_keys, 1), s->stream));
+    s->reset_pending = true;
+    if (!may_defer) {
+        const int frc = flush_reset(s);
+        if (frc) return frc;
+    }
     std::fill(s->h_preempted.begin(), s->h_preempted.end(), 0);
     if (s->has_cores) {   // reserved cores back to the snapshot's
         HIP_TRY(s, hipMemcpyAsync(s->d_core_used.p, s->d_core_base.p, sizeof(uint64_t) * 4 * n, hipMemcpyDeviceToDevice,
@@ -4221,6 +4264,7 @@ static bool sys_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, 
 }
 
 int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
+    PE_FLUSH_RESET(s);
     if (!s || !out) return PE_EINVAL;
     int rc = PE_OK;
     if (s->cfg.stack_kind == PE_STACK_SYSTEM && !s->test_fallback_every && sys_serve(s, tgi, opts, out, &rc))
@@ -4375,6 +4419,7 @@ static int shard_prepare(pe_stack* s, uint32_t tgi, TgPlan** gp) {
 }
 
 int pe_select_shard(pe_stack* s, uint32_t tgi, uint32_t row_begin, uint32_t row_end, pe_shard_rec* out) {
+    PE_FLUSH_RESET(s);
     if (!s || !out) return PE_EINVAL;
     {
         const int frc = spec_flush(s);
@@ -4396,6 +4441,7 @@ int pe_select_shard(pe_stack* s, uint32_t tgi, uint32_t row_begin, uint32_t row_
 }
 
 int pe_select_merge(pe_stack* s, uint32_t tgi, const pe_shard_rec* recs, uint32_t n_recs, pe_ranked_node* out) {
+    PE_FLUSH_RESET(s);
     if (!s || !out || (!recs && n_recs)) return PE_EINVAL;
     {
         const int frc = spec_flush(s);
@@ -5228,6 +5274,7 @@ int pe_comm_unique_id(uint8_t* out, size_t cap) {
 }
 
 int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id) {
+    PE_FLUSH_RESET(s);
     if (!s || !id || nranks < 1 || rank < 0 || rank >= nranks) return PE_EINVAL;
     HIP_TRY(s, hipSetDevice(s->device));
     if (s->comm) {
@@ -5358,6 +5405,7 @@ int pe_speculation_stats(const pe_stack* s, uint64_t* out4) {
 }
 
 int pe_stage_orders(pe_stack* s, const uint32_t* orders, uint32_t n_evals, uint32_t n) {
+    PE_FLUSH_RESET(s);
     if (!s || (!orders && n_evals && n)) return PE_EINVAL;
     {
         const int frc = spec_flush(s);
@@ -5487,6 +5535,7 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
 }  // namespace
 
 int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out, uint32_t* placed) {
+    PE_FLUSH_RESET(s);
     if (!s) return PE_EINVAL;
     {
         const int frc = spec_flush(s);
@@ -5885,6 +5934,7 @@ static int system_place_one(pe_stack* s, uint32_t tgi, double* out_score, uint8_
 
 int pe_place_sharded(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_begin, uint32_t row_end,
                      pe_ranked_node* out, uint32_t* placed) {
+    PE_FLUSH_RESET(s);
     const int rc = place_sharded_impl(s, tgi, count, row_begin, row_end, out, placed);
     if (rc == PE_OK && count) elig_log_span(s, tgi, s->offset, (uint32_t)s->visit.size());   // full passes
     return rc;
@@ -5892,6 +5942,7 @@ int pe_place_sharded(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_beg
 
 int pe_get_eligibility(pe_stack* s, uint32_t changed_only, pe_class_feas* out, uint32_t cap, uint32_t* n_out,
                        uint32_t* flags) {
+    PE_FLUSH_RESET(s);
     if (!s || !n_out) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     elig_resolve(s);
@@ -5930,6 +5981,7 @@ int pe_get_eligibility(pe_stack* s, uint32_t changed_only, pe_class_feas* out, u
 }
 
 int pe_put_eligibility(pe_stack* s, const pe_class_feas* in, uint32_t n) {
+    PE_FLUSH_RESET(s);
     if (!s || (!in && n)) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     int rc = spec_flush(s);
@@ -5979,6 +6031,7 @@ int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit) {
 }
 
 int pe_set_cursor(pe_stack* s, uint32_t tgi, uint32_t offset, uint32_t limit) {
+    PE_FLUSH_RESET(s);
     if (!s) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     if (!s->visit.empty() && offset >= s->visit.size()) return s->fail(PE_EINVAL, "cursor beyond the SetNodes list");
@@ -6004,6 +6057,7 @@ int pe_set_cursor(pe_stack* s, uint32_t tgi, uint32_t offset, uint32_t limit) {
 }
 
 int pe_flush(pe_stack* s) {
+    PE_FLUSH_RESET(s);
     if (!s) return PE_EINVAL;
     return spec_flush(s);
 }
@@ -6298,6 +6352,7 @@ static bool multi_system_ok(pe_stack* s, uint32_t tgi) {
 }
 
 int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
+    PE_FLUSH_RESET(s);
     const int rc = set_state_one(s, strs, nodes, allocs);
     if (rc || !s || s->kids.empty()) return rc;
     bool ok = true;
@@ -6307,6 +6362,7 @@ int pe_set_state(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes,
 }
 
 int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index) {
+    PE_FLUSH_RESET(s);
     const int rc = update_allocs_one(s, strs, allocs, index);
     if (rc || !s || s->kids.empty()) return rc;
     bool ok = true;
@@ -6316,6 +6372,7 @@ int pe_update_allocs(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* a
 }
 
 int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const uint32_t* index) {
+    PE_FLUSH_RESET(s);
     const int rc = update_nodes_one(s, strs, nodes, index);
     if (rc || !s || s->kids.empty()) return rc;
     bool ok = true;
@@ -6325,10 +6382,10 @@ int pe_update_nodes(pe_stack* s, const pe_strtab* strs, const pe_node_table* nod
 }
 
 int pe_reset_plan(pe_stack* s) {
-    const int rc = reset_plan_one(s);
+    const int rc = reset_plan_one(s, s && s->kids.empty());
     if (rc || !s || s->kids.empty()) return rc;
     bool ok = true;
-    for (pe_stack* k : s->kids) ok = reset_plan_one(k) == PE_OK && ok;
+    for (pe_stack* k : s->kids) ok = reset_plan_one(k, false) == PE_OK && ok;
     kids_fresh(s, ok);
     return rc;
 }
@@ -6343,30 +6400,35 @@ int pe_set_job(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
 }
 
 int pe_commit(pe_stack* s, uint32_t tgi, int32_t row) {
+    PE_FLUSH_RESET(s);
     const int rc = commit_one(s, tgi, row);
     if (rc == PE_OK && !s->kids.empty()) kid_log(s, 0, tgi, row, nullptr, 0);
     return rc;
 }
 
 int pe_commit_preempt(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
+    PE_FLUSH_RESET(s);
     const int rc = commit_preempt_one(s, tgi, row, preempted, n_preempted);
     if (rc == PE_OK && !s->kids.empty()) kid_log(s, 1, tgi, row, preempted, n_preempted);
     return rc;
 }
 
 int pe_plan_stop(pe_stack* s, const uint32_t* allocs, uint32_t n) {
+    PE_FLUSH_RESET(s);
     const int rc = plan_stop_one(s, allocs, n);
     if (rc == PE_OK && !s->kids.empty()) kid_log(s, 2, 0, 0, allocs, n);
     return rc;
 }
 
 int pe_plan_pop_update(pe_stack* s, uint32_t alloc) {
+    PE_FLUSH_RESET(s);
     const int rc = plan_pop_update_one(s, alloc);
     if (rc == PE_OK && !s->kids.empty()) kid_log(s, 3, 0, 0, &alloc, 1);
     return rc;
 }
 
 int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
+    PE_FLUSH_RESET(s);
     if (!s) return PE_EINVAL;
     if (!s->kids.empty() && s->kids_valid) {
         int rc = spec_flush(s);
@@ -6388,6 +6450,7 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
 }
 
 int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
+    PE_FLUSH_RESET(s);
     if (!s || !out_score || !out_status) return PE_EINVAL;
     if (!s->kids.empty() && s->kids_valid) {
         int rc = spec_flush(s);

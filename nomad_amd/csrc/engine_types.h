@@ -139,6 +139,20 @@ struct CountDsts {
     uint32_t* d[kMaxCountDst];
 };
 
+// ResetPlan's state copy (proposed state back to the snapshot) when it rides in
+// the next k_counts launch (rec null: none)
+struct ResetArgs {
+    NodeRec* rec;
+    const NodeRec* base_rec;
+    uint32_t* dev_free;
+    const uint32_t* dev_free_base;
+    uint32_t n;
+    uint8_t* preempted;
+    uint32_t m;
+    uint32_t* pcount;
+    uint32_t keys;
+};
+
 // Select result as k_emit hands it to the host: the leading fields of
 // pe_ranked_node (row .. new_offset, byte-identical) and the device offers;
 // the host widens it (no preemptions or reserved cores on the chain path).

@@ -20,7 +20,9 @@
 // k_system              SystemStack: independent single-node Selects, grid-stride.
 // k_commit              one Plan.AppendAlloc on the HBM SoA (pe_commit).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include "engine_types.h"
 #include "gomath_dev.h"
 
@@ -3055,9 +3057,19 @@ __global__ void __launch_bounds__(256) k_upload(unsigned char* dst, const unsign
 
 // Per-node count arrays from a sorted sparse list (key = row << 5 | array,
 // value = count): each thread owns one row, zeroes it in every array and
-// writes the row's entries found by binary search.
-__global__ void __launch_bounds__(256) k_counts(CountDsts D, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m) {
+// writes the row's entries found by binary search. A deferred ResetPlan (R.rec)
+// rides in the same launch: its arrays are disjoint from the counts.
+__global__ void __launch_bounds__(256) k_counts(CountDsts D, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
+                                                ResetArgs R) {
     const uint32_t stride = gridDim.x * 256;
+    if (R.rec) {
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < R.n; i += stride) {
+            R.rec[i] = R.base_rec[i];
+            R.dev_free[i] = R.dev_free_base[i];
+        }
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < R.m; i += stride) R.preempted[i] = 0;
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < R.keys; i += stride) R.pcount[i] = 0;
+    }
     for (uint32_t row = blockIdx.x * 256 + threadIdx.x; row < n; row += stride) {
         uint32_t lo = 0, hi = m;
         const uint32_t k0 = row << 5;
@@ -3339,12 +3351,20 @@ hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hip
 }
 
 hipError_t pe_launch_counts(const pe::CountDsts* d, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
-                            hipStream_t st) {
+                            const pe::ResetArgs* r, hipStream_t st) {
     if (nd > (uint32_t)pe::kMaxCountDst || (m && !ents) || n >= (1u << 27)) return hipErrorInvalidValue;
-    if (!n) return hipSuccess;
-    uint32_t blocks = (n + 255) / 256;
+    pe::ResetArgs R;
+    std::memset(&R, 0, sizeof(R));
+    if (r && r->rec) {
+        if (!r->base_rec || !r->dev_free || !r->dev_free_base || (r->m && !r->preempted) || (r->keys && !r->pcount))
+            return hipErrorInvalidValue;
+        R = *r;
+    }
+    const uint32_t span = std::max(n, std::max(R.n, std::max(R.m, R.keys)));
+    if (!span) return hipSuccess;
+    uint32_t blocks = (span + 255) / 256;
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(pe::k_counts, dim3(blocks), dim3(256), 0, st, *d, nd, n, ents, m);
+    hipLaunchKernelGGL(pe::k_counts, dim3(blocks), dim3(256), 0, st, *d, nd, n, ents, m, R);
     return hipGetLastError();
 }
 
