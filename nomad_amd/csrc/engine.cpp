@@ -93,6 +93,7 @@ int pe_sweep_blocks_per_cu(bool aux);
 hipError_t pe_launch_fold_aux(const pe::NodeSoA* s, const pe::TgTables* t, const uint8_t* aff_idx_class,
                               const uint8_t* aff_idx_node, uint32_t* aux, hipStream_t st);
 uint32_t pe_chain_max_n();
+uint32_t pe_emit_grid(uint32_t count);
 uint32_t pe_chain_max_limit();
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n);
 int pe_chain_blocks_per_cu(size_t lds);
@@ -442,6 +443,7 @@ struct pe_stack {
     PinnedMem h_batch_out, h_batch_status;
     PinnedMem h_sys_out;   // SystemStack results, staged for the caller's arrays
     PinnedMem h_place_out, h_place_status;   // single-evaluation count loop results (mapped)
+    PinnedMem h_emit_done;                   // k_emit's per-workgroup completion words (mapped)
     PinnedMem h_emit_out;                    // k_emit's compact records (mapped)
     PinnedMem h_stage;                 // upload staging ring (upload_s)
     unsigned char* stage_dev = nullptr;   // the ring as seen from the device (k_upload reads it)
@@ -3057,9 +3059,15 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     // from a stream synchronisation; the launch's event timing is resolved
     // when it is asked for (pe_last_kernel_ms).
     bool spin = chain && s->spin_wait;
-    volatile uint32_t* flag = s->h_place_status.as<uint32_t>() + 3;
+    volatile uint32_t* flag = nullptr;
     if (spin) {
-        A.done_flag = s->h_place_status.dev<uint32_t>() + 3;
+        const size_t fb = sizeof(uint32_t) * pe_emit_grid(chunk);
+        if (s->h_emit_done.bytes < fb) {
+            HIP_TRY(s, s->h_emit_done.ensure(fb));
+            std::memset(s->h_emit_done.p, 0, s->h_emit_done.bytes);
+        }
+        flag = s->h_emit_done.as<uint32_t>();
+        A.done_flag = s->h_emit_done.dev<uint32_t>();
         HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     }
     while (done < count) {
@@ -3087,10 +3095,17 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         ApiScope prof_w_(s, "run_place.wait+copy");
         if (spin) {
             const double t_spin = now_us();
-            while (*flag != A.done_seq && now_us() - t_spin < 2000.0) __builtin_ia32_pause();
-            if (*flag != A.done_seq) {
+            const uint32_t nwg = pe_emit_grid(c);
+            uint32_t w = 0;   // completion words seen so far (in order)
+            while (w < nwg) {
+                if (flag[w] == A.done_seq) { w++; continue; }
+                if (now_us() - t_spin >= 2000.0) break;
+                __builtin_ia32_pause();
+            }
+            if (w < nwg) {
                 HIP_TRY(s, hipStreamSynchronize(s->stream));
-                if (*flag != A.done_seq) return s->fail(PE_EHIP, "k_emit completion word missing");
+                while (w < nwg && flag[w] == A.done_seq) w++;
+                if (w < nwg) return s->fail(PE_EHIP, "k_emit completion word missing");
             }
             __atomic_thread_fence(__ATOMIC_ACQUIRE);
         } else {

@@ -213,7 +213,7 @@ struct BatchArgs {
     ChainEmit* emit;
     uint2* emit_ov;
     uint32_t* emit_n;
-    uint32_t* done_flag;          // or null: k_emit's last workgroup stores done_seq here (system scope)
+    uint32_t* done_flag;          // or null: k_emit's workgroup b stores done_seq to done_flag[b] (system scope)
     uint32_t done_seq;
     unsigned long long* prof;     // k_chain step clocks (PE_CHAIN_PROF), or null
     // k_chain scratch, kChainMaxN doubles per workgroup: the window's values

@@ -2014,7 +2014,6 @@ constexpr uint32_t kEmitBlock = 64;
 // entry's dk = placements on the row before it); k_emit_writeback then
 // writes the launch's placements back to the HBM SoA.
 __global__ void __launch_bounds__(kEmitBlock) k_emit(BatchArgs A) {
-    __shared__ uint32_t last;
     // records are built in LDS and stored to the (host-mapped) output as one
     // contiguous run per workgroup: 8-byte coalesced stores of compact records
     // instead of every lane writing its own record field by field over the
@@ -2070,14 +2069,12 @@ __global__ void __launch_bounds__(kEmitBlock) k_emit(BatchArgs A) {
     }
     if (!A.done_flag) return;
     __syncthreads();
+    // every workgroup raises its own completion word once its records are out:
+    // the spinning host checks them all (no ticket atomic round trip and one
+    // system fence per workgroup instead of two)
     if (threadIdx.x == 0) {
         __threadfence_system();
-        last = atomicAdd(&A.emit_n[2], 1u) == gridDim.x - 1 ? 1u : 0u;
-        // the last workgroup to finish tells the spinning host the records are in
-        if (last) {
-            __threadfence_system();
-            __hip_atomic_store(A.done_flag, A.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        __hip_atomic_store(A.done_flag + blockIdx.x, A.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -3195,6 +3192,7 @@ hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, 
 // Phase-static windowed loop: k_base over the snapshot, then k_chain with a
 // persistent grid of at most `max_blocks` workgroups (one evaluation each at a time).
 uint32_t pe_chain_max_n() { return pe::kChainMaxN; }
+uint32_t pe_emit_grid(uint32_t count) { return count ? (count + pe::kEmitBlock - 1) / pe::kEmitBlock : 1u; }
 uint32_t pe_chain_max_limit() { return pe::kMaxChainLimit; }
 
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n) {
@@ -3226,8 +3224,7 @@ hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t ma
     hipLaunchKernelGGL(pe::k_chain, dim3(grid), dim3(pe::kChainBlock), lds, st, *a, n_evals);
     if (a->emit) {
         if (n_evals != 1 || !a->emit_out || !a->emit_ov || !a->emit_n) return hipErrorInvalidValue;
-        const uint32_t eb = (a->count + pe::kEmitBlock - 1) / pe::kEmitBlock;
-        hipLaunchKernelGGL(pe::k_emit, dim3(eb ? eb : 1), dim3(pe::kEmitBlock), 0, st, *a);
+        hipLaunchKernelGGL(pe::k_emit, dim3(pe_emit_grid(a->count)), dim3(pe::kEmitBlock), 0, st, *a);
         const uint32_t wb = (a->count + 255) / 256;   // overlay rows <= placements
         hipLaunchKernelGGL(pe::k_emit_writeback, dim3(wb ? wb : 1), dim3(256), 0, st, *a);
     }
