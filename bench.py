@@ -111,6 +111,25 @@ def reduce(pg, x, op):
     return float(t.item())
 
 
+def cpu_model():
+    """The host CPU the baseline ran on: model name, logical CPUs of the
+    machine, CPUs this process may run on."""
+    name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    name = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 0
+    return {"model": name, "nproc": os.cpu_count() or 0, "affinity_cpus": avail}
+
+
 def cpu_eval_loop(nodes, allocs, job, seconds, seed0):
     from oracle.oracle import OracleGenericStack
     from nomad_amd import synth
@@ -135,7 +154,7 @@ def cpu_eval_loop(nodes, allocs, job, seconds, seed0):
 def cpu_baseline(nodes, allocs, job, seconds):
     """oracle/liboracle.so (C++ restatement of the reference chain) on host cores."""
     placed, evals, dt = cpu_eval_loop(nodes, allocs, job, seconds, 1000)
-    one = {"value": placed / dt, "unit": "placements/s", "cores": 1, "kind": "port",
+    one = {"value": placed / dt, "unit": "placements/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
            "sample": "%d evals x count=%d on the %d-node cluster in %.1f s, 1 thread "
                      "(oracle/liboracle.so: C++ restatement of the reference iterator chain; "
                      "Go toolchain unavailable)" % (evals, job.task_groups[0].count, len(nodes), dt)}
@@ -145,7 +164,7 @@ def cpu_baseline(nodes, allocs, job, seconds):
         res = [f.result() for f in futs]
     tot = sum(r[0] for r in res)
     wall = max(r[2] for r in res)
-    multi = {"value": tot / wall, "unit": "placements/s", "cores": threads, "kind": "port",
+    multi = {"value": tot / wall, "unit": "placements/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
              "sample": "%d threads x independent evals for %.1f s (box CPU share)" % (threads, wall)}
     return one, multi
 
@@ -304,7 +323,7 @@ def section_c3(device, cpu_s):
             o.SetNodes(perm)
             return o
         rate, k, dt = _oracle_rate(mk, lambda o, k: o.PlaceArrays(0, k)[2], cpu_s)
-        out["cpu_baseline"] = {"value": rate, "unit": "placements/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": rate, "unit": "placements/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
                                "sample": "first %d placements of the same evaluation in %.2f s" % (k, dt)}
     return out
 
@@ -348,7 +367,7 @@ def section_c4(device, rank, world, pg, cpu_s):
         t0 = time.perf_counter()
         o.SystemPlace(0)
         dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
                                "sample": "system placements over a %d-node C4 cluster in %.2f s" % (ns, dt)}
     return out
 
@@ -392,7 +411,7 @@ def section_c4_drop_in(device, cpu_s):
         o.SetStateColumnar(small)
         o.SetJob(job)
         _, _, _, dt = dropin.system_loop(o, 0, np.arange(ns, dtype=np.uint32))
-        out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
                                "sample": "the same C caller loop over a %d-node C4 cluster in %.3f s" % (ns, dt)}
     return out
 
@@ -420,6 +439,7 @@ def section_c5(device, cpu_s):
         t0 = time.perf_counter()
         rows, _, placed, recs = st.PlaceArrays(0, 1000)   # records stay in a numpy view (no per-record objects)
         times.append(time.perf_counter() - t0)
+    rows, recs = np.array(rows[:placed]), np.array(recs[:placed])   # outlive the handle
     st.close()
     wall = float(np.median(times[1:]))
     pre = int((recs["n_preempted"][:placed] > 0).sum())
@@ -427,32 +447,59 @@ def section_c5(device, cpu_s):
                        "preemption enabled, 99 % of GPU nodes busy", "placements": placed,
            "preempting_placements": pre, "placements_per_s": placed / wall, "wall_ms": wall * 1e3}
     if cpu_s > 0:
+        # The same evaluation on the oracle through the caller's loop (Select,
+        # the Preempt retry on nil, Commit with the preempted set). The whole
+        # run is ~10 CPU-minutes (628 Selects with Preempt over 50k nodes), so
+        # two bounded windows of it are timed: its first placements, and the
+        # placements from the middle on after the engine's records up to there
+        # are replayed into the oracle's plan untimed (they are bit-identical
+        # to the oracle's own: tests/test_full_size.py c5_bench_shape). The
+        # evaluation's CPU time = each placement kind's mean time over the
+        # windows (plain / evicting) x this evaluation's count of that kind.
         from oracle.oracle import OracleGenericStack
+        from nomad_amd.stack import SelectOptions
 
-        def mk(ns, al):
+        def fresh():
             o = OracleGenericStack(config=cfg)
-            o.SetState(ns, al)
+            o.SetState(nodes, allocs)
             o.SetJob(job)
             o.SetNodes(perm)
             return o
-        # free-GPU regime: the evaluation's first placements
-        o = mk(nodes, allocs)
-        t0 = time.perf_counter()
-        k_free = o.PlaceArrays(0, 128)[2]
-        dt_free = time.perf_counter() - t0
-        # eviction regime: every GPU node held, so each placement fails its plain
-        # Select and evicts (a bounded sample of 3 placements)
-        bnodes, ballocs = synth.cluster_c5(50000, seed=5, busy=1.0)
-        o = mk(bnodes, ballocs)
-        t0 = time.perf_counter()
-        k_pre = o.PlaceArrays(0, 3)[2]
-        dt_pre = time.perf_counter() - t0
-        est = (placed - pre) * dt_free / max(1, k_free) + pre * dt_pre / max(1, k_pre)
+
+        def window(o, j, budget):
+            ts = {False: [], True: []}
+            t0 = time.perf_counter()
+            while j < placed and time.perf_counter() - t0 < budget:
+                t1 = time.perf_counter()
+                r = o.Select(0)
+                if r is None:
+                    r = o.Select(0, SelectOptions(preempt=True))
+                if r is None:
+                    break
+                o.Commit(0, r.row, r.preempted)
+                ts[bool(r.preempted)].append(time.perf_counter() - t1)
+                j += 1
+            return ts
+        w1 = window(fresh(), 0, cpu_s / 2)
+        j0 = placed // 2
+        o = fresh()
+        for i in range(j0):
+            o.Commit(0, int(rows[i]), [int(x) for x in recs["preempted"][i][:int(recs["n_preempted"][i])]])
+        w2 = window(o, j0, cpu_s / 2)
+        plain = w1[False] + w2[False]
+        evict = w1[True] + w2[True]
+        t_plain = float(np.mean(plain)) if plain else 0.0
+        t_evict = float(np.mean(evict)) if evict else 0.0
+        est = (placed - pre) * t_plain + pre * t_evict
         out["cpu_baseline"] = {"value": placed / est if est > 0 else 0.0, "unit": "placements/s", "cores": 1,
-                               "kind": "port",
-                               "sample": "%d free-GPU placements in %.2f s and %d evicting placements (all GPU "
-                                         "nodes busy) in %.2f s, weighted by this run's %d / %d split"
-                                         % (k_free, dt_free, k_pre, dt_pre, placed - pre, pre)}
+                               "kind": "port", "cpu": cpu_model(),
+                               "sample": "this evaluation on the oracle through the caller's loop, 1 thread: its "
+                                         "placements 0-%d (%d plain, %d evicting) and %d-%d (%d plain, %d evicting, "
+                                         "after replaying the first %d records untimed); mean %.1f ms per plain and "
+                                         "%.1f ms per evicting placement x this evaluation's %d / %d"
+                                         % (len(w1[False]) + len(w1[True]) - 1, len(w1[False]), len(w1[True]), j0,
+                                            j0 + len(w2[False]) + len(w2[True]) - 1, len(w2[False]), len(w2[True]),
+                                            j0, t_plain * 1e3, t_evict * 1e3, placed - pre, pre)}
     return out
 
 
@@ -676,7 +723,7 @@ def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
             O.evaluate_node_plan(snap, my_plan, ids[k])
             k += 1
         dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": k / dt, "unit": "plan nodes/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": k / dt, "unit": "plan nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
                                "sample": "evaluateNodePlan on the first %d plan nodes in %.2f s (oracle/plan_apply.py, "
                                          "Python restatement; Go toolchain unavailable)" % (k, dt)}
     return out
@@ -747,7 +794,7 @@ def section_c1(device, cpu_s, evals=2000):
         o = OracleGenericStack()
         o.SetState(nodes, allocs)
         op, oe, _, osecs, _ = dropin.run(o, job, orders, 10, n_evals=1 << 30, max_seconds=min(cpu_s, 3.0))
-        out["cpu_baseline"] = {"value": op / osecs, "unit": "placements/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": op / osecs, "unit": "placements/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
                                "sample": "%d evaluations x count=10 through the same C caller loop, 1 thread"
                                          % oe}
     return out
@@ -786,7 +833,7 @@ def section_c2_100k(device, cpu_s, count=1000, n=100000, evals=20):
         o = OracleGenericStack()
         o.SetState(nodes, allocs)
         op, oe, _, osecs, _ = dropin.run(o, job, orders, count, n_evals=1 << 30, max_seconds=cpu_s)
-        out["cpu_baseline"] = {"value": op / osecs, "unit": "placements/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": op / osecs, "unit": "placements/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
                                "sample": "%d evaluations x count=%d on the %d-node cluster through the same C caller "
                                          "loop, 1 thread" % (oe, count, n)}
     return out
@@ -877,11 +924,20 @@ def main():
 
     # the dominant kernel of a step: the speculative count loop (k_base + k_chain),
     # timed with HIP events on the engine's stream by the same call path
-    st.ResetPlan()
-    st.SetJob(job)
-    st.SetNodes(orders[0])
-    _, _, p1, recs = st.PlaceArrays(0, args.count)
-    loop_kernel_ms = st.last_kernel_ms()
+    # HIP events between the chain's kernels (k_base, k_chain, k_emit,
+    # k_emit_writeback): the roofline's kernel_ms is exactly k_base + k_chain,
+    # the median over a few evaluations outside the timed region
+    st.SetKernelSplit(True)
+    splits = []
+    for i in range(5):
+        st.ResetPlan()
+        st.SetJob(job)
+        st.SetNodes(orders[i % len(orders)])
+        _, _, p1, recs = st.PlaceArrays(0, args.count)
+        splits.append(st.last_kernel_split())
+        loop_all_ms = st.last_kernel_ms()
+    split_ms = {k: float(np.median([d[k] for d in splits])) for k in splits[0]}
+    loop_kernel_ms = split_ms["k_base"] + split_ms["k_chain"]
     node_evals = float(recs["nodes_evaluated"][:p1].sum(dtype=np.uint64))
     st.close()
 
@@ -922,6 +978,9 @@ def main():
                                  "10k-node table is L2/MALL resident and the loop is latency-bound. The HBM "
                                  "roofline of SURVEY.md §8(d) is sweep_roofline",
                          "kernel": "k_base + k_chain", "kernel_ms": loop_kernel_ms,
+                         "kernel_ms_source": "HIP events on the engine stream around k_base and k_chain "
+                                             "(pe_last_kernel_split), median of 5 evaluations",
+                         "evaluation_kernels_ms": dict(split_ms, all_launches=loop_all_ms),
                          "node_evals_per_launch": node_evals, "bytes_per_node_eval": BYTES_PER_NODE_EVAL},
         }
         if args.sweep_nodes > 0:
@@ -939,7 +998,7 @@ def main():
                 runs.append((op / osecs, oe, osecs))
             rates = sorted(r[0] for r in runs)
             oe_all, secs_all = sum(r[1] for r in runs), sum(r[2] for r in runs)
-            line["cpu_baseline"] = {"value": rates[1], "unit": "placements/s", "cores": 1, "kind": "port",
+            line["cpu_baseline"] = {"value": rates[1], "unit": "placements/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
                                     "runs": [r[0] for r in runs], "fastest": rates[-1],
                                     "sample": "median of 3 runs, %d evaluations x count=%d on the %d-node cluster in "
                                               "%.1f s in all, through the same C caller loop, 1 thread "

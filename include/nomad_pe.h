@@ -46,6 +46,8 @@ extern "C" {
 #define PE_EUNSUPPORTED (-4) /* feature not on the device path (CSI, cores, ...):
                                 the shim falls back to the Go chain for this Select */
 #define PE_ENOMEM (-5)
+#define PE_EINTERNAL (-6)    /* an engine invariant failed on the device (a kernel bounds guard tripped);
+                                the call is abandoned, the handle must be reset (pe_set_state) */
 
 /* ---- interned strings -------------------------------------------------- */
 typedef struct pe_strtab {
@@ -452,6 +454,13 @@ double pe_last_kernel_ms(const pe_stack* s);
 /* Algorithmic HBM bytes per node of the last full-scan sweep Select (73 with
  * the verdict byte, 76 with the folded per-node score word), 0 if none ran. */
 uint32_t pe_last_sweep_bytes(const pe_stack* s);
+/* Per-kernel device time of the windowed count loop (measurement aid; off by
+ * default, or PE_KERNEL_SPLIT=1 in the environment at pe_stack_create): with it
+ * on, the chain path records HIP events between its kernels and
+ * pe_last_kernel_split writes the last launch's ms4 = {k_base, k_chain, k_emit,
+ * k_emit_writeback}; PE_ESTATE when the last pe_place / Select ran no chain. */
+int pe_set_kernel_split(pe_stack* s, int on);
+int pe_last_kernel_split(const pe_stack* s, double* ms4);
 /* AllocMetric maps (structs.go:9826-10026) of Selects: ClassFiltered,
  * ConstraintFiltered, ClassExhausted, DimensionExhausted — what
  * `ctx.Metrics()` holds after GenericStack.Select (FilterNode / ExhaustedNode,

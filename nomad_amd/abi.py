@@ -17,7 +17,7 @@ PE_NONE = 0xFFFFFFFF
 PE_MAX_SCORES = 8
 PE_MAX_PREEMPT = 16
 PE_MAX_DEVICE_REQ = 4
-PE_OK, PE_EINVAL, PE_ESTATE, PE_EHIP, PE_EUNSUPPORTED, PE_ENOMEM = 0, -1, -2, -3, -4, -5
+PE_OK, PE_EINVAL, PE_ESTATE, PE_EHIP, PE_EUNSUPPORTED, PE_ENOMEM, PE_EINTERNAL = 0, -1, -2, -3, -4, -5, -6
 
 PE_ATTR_INT, PE_ATTR_FLOAT, PE_ATTR_STRING, PE_ATTR_BOOL = 1, 2, 3, 4
 PE_LC_MAIN, PE_LC_PRESTART, PE_LC_PRESTART_SIDECAR, PE_LC_POSTSTOP, PE_LC_POSTSTART = 0, 1, 2, 3, 4
@@ -225,7 +225,8 @@ ENGINE_SYMBOLS = [
     "pe_set_metrics", "pe_last_metrics", "pe_update_allocs", "pe_speculation_stats",
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
-    "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count",
+    "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
+    "pe_last_kernel_split",
 ]
 
 

@@ -93,11 +93,16 @@ int pe_sweep_blocks_per_cu(bool aux);
 hipError_t pe_launch_fold_aux(const pe::NodeSoA* s, const pe::TgTables* t, const uint8_t* aff_idx_class,
                               const uint8_t* aff_idx_node, uint32_t* aux, hipStream_t st);
 uint32_t pe_chain_max_n();
+uint32_t pe_chain_fused_max_n();
+int pe_chain_shape(uint32_t n_visit);
+uint32_t pe_chain_fused_max_count();
+uint32_t pe_chain_fused_max_classes();
 uint32_t pe_emit_grid(uint32_t count);
 uint32_t pe_chain_max_limit();
 size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n);
 int pe_chain_blocks_per_cu(size_t lds);
-hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st);
+hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st,
+                           hipEvent_t* split = nullptr);
 hipError_t pe_launch_sweep_step(const pe::SweepArgs* a, uint32_t blocks, const uint32_t* visit, uint32_t n,
                                 uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_sweep_loop(const pe::SweepArgs* a, uint32_t blocks, uint32_t count, const uint32_t* visit,
@@ -353,6 +358,11 @@ struct pe_stack {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    // per-kernel events of the windowed chain (PE_KERNEL_SPLIT / pe_set_kernel_split):
+    // before k_base, after k_base, k_chain, k_emit, k_emit_writeback of the last launch
+    bool kernel_split = false;
+    bool split_valid = false;
+    hipEvent_t ev_split[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     double last_ms = 0;
     bool last_ms_pending = false;      // last_ms still to be read from ev0 / ev1
     bool spin_wait = true;             // PE_SPIN_WAIT=0: chain launches wait with a stream sync
@@ -387,6 +397,13 @@ struct pe_stack {
     // ResetPlan's state copy not launched yet: it rides in SetJob's k_counts
     // launch, any other call launches it first (flush_reset)
     bool reset_pending = false;
+    // The FeasibilityWrapper fold of the last build_tables, not launched yet:
+    // place_impl lets it ride in the windowed chain's first launch (k_base, or
+    // the fused k_chain) and launches it on its own on every other path
+    // (flush_fold); nothing leaves place_impl with it pending.
+    bool fold_defer_ok = false;
+    bool fold_pending = false;
+    pe::FoldArgs pending_fold{};
     // preemption: non-terminal state allocs per node (CSR, table order) as PreemptAlloc
     std::vector<uint32_t> h_node_alloc_off, h_palloc_index;   // CSR; slot -> alloc-table row
     std::vector<uint32_t> alloc_slot;          // alloc-table row -> slot (PE_NONE: terminal)
@@ -645,6 +662,7 @@ namespace {
 
 constexpr uint32_t kFullLdsMaxN = 32768;          // k_fullpass_lds tried up to this list length
 constexpr uint32_t kStalledFlag = 0x80000000u;   // k_chain cursor flag (kChainStalled)
+constexpr uint32_t kChainErrFlag = 0x40000000u;   // k_chain bounds guard tripped (kChainError)
 
 double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -677,6 +695,7 @@ struct ApiScope {
 // wait for the device; the ring restarts after a stream synchronisation when
 // it is full. Large uploads synchronise and copy directly.
 constexpr size_t kStageBytes = 8u << 20;
+static int flush_fold(pe_stack* s);
 
 template <class T>
 hipError_t upload_s(pe_stack* s, DevMem& m, const std::vector<T>& h) {
@@ -684,6 +703,7 @@ hipError_t upload_s(pe_stack* s, DevMem& m, const std::vector<T>& h) {
     hipError_t e = m.ensure(b);
     if (e != hipSuccess || b == 0) return e;
     if (b > kStageBytes / 4) {
+        if (s->fold_pending && flush_fold(s) != PE_OK) return hipErrorLaunchFailure;   // it reads its staged table
         e = hipStreamSynchronize(s->stream);
         if (e != hipSuccess) return e;
         s->stage_off = 0;
@@ -695,6 +715,8 @@ hipError_t upload_s(pe_stack* s, DevMem& m, const std::vector<T>& h) {
     }
     size_t off = (s->stage_off + 255) & ~size_t(255);
     if (off + b > kStageBytes) {
+        // the ring restarts: a pending fold still reads its staged table
+        if (s->fold_pending && flush_fold(s) != PE_OK) return hipErrorLaunchFailure;
         e = hipStreamSynchronize(s->stream);
         if (e != hipSuccess) return e;
         off = 0;
@@ -717,6 +739,7 @@ const unsigned char* stage_only(pe_stack* s, const std::vector<T>& h) {
     if (!s->h_stage.p && s->h_stage.ensure(kStageBytes) != hipSuccess) return nullptr;
     size_t off = (s->stage_off + 255) & ~size_t(255);
     if (off + b > kStageBytes) {
+        if (s->fold_pending && flush_fold(s) != PE_OK) return nullptr;   // it reads its staged table
         if (hipStreamSynchronize(s->stream) != hipSuccess) return nullptr;
         off = 0;
     }
@@ -1956,8 +1979,22 @@ static pe::ResetArgs reset_args(pe_stack* s) {
     return R;
 }
 
+// A pending fold (pe_stack::fold_pending) as its own launch.
+static int flush_fold(pe_stack* s) {
+    if (!s->fold_pending) return PE_OK;
+    s->fold_pending = false;
+    const pe::FoldArgs F = s->pending_fold;
+    const pe::NodeSoA soa = soa_of(s);
+    HIP_TRY(s, pe_launch_fold_feas_staged(&soa, F.class_src, F.class_dst, F.ncls, F.node_ok, F.feas, s->stream));
+    return PE_OK;
+}
+
 // The deferred ResetPlan launch, before any other device work of the handle.
 static int flush_reset(pe_stack* s) {
+    if (s->fold_pending) {
+        const int rc = flush_fold(s);
+        if (rc) return rc;
+    }
     if (!s->reset_pending) return PE_OK;
     s->reset_pending = false;
     HIP_TRY(s, hipSetDevice(s->device));
@@ -1970,7 +2007,7 @@ static int flush_reset(pe_stack* s) {
 
 #define PE_FLUSH_RESET(s)                             \
     do {                                              \
-        if ((s) && (s)->reset_pending) {              \
+        if ((s) && ((s)->reset_pending || (s)->fold_pending)) { \
             const int frc_ = flush_reset(s);          \
             if (frc_) return frc_;                    \
         }                                             \
@@ -2348,10 +2385,23 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
                                               class_ok.size() * fold_blocks <= kStagedFoldBusBytes
                                           ? stage_only(s, class_ok)
                                           : nullptr;
+        {
+            const int rc = flush_fold(s);   // an earlier table's fold first (stream order)
+            if (rc) return rc;
+        }
         if (staged) {
-            HIP_TRY(s, pe_launch_fold_feas_staged(&soa, staged, g.class_ok.as<uint8_t>(), (uint32_t)class_ok.size(),
-                                                  g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr,
-                                                  g.node_feas.as<uint8_t>(), s->stream));
+            pe::FoldArgs F;
+            F.class_src = staged;
+            F.class_dst = g.class_ok.as<uint8_t>();
+            F.ncls = (uint32_t)class_ok.size();
+            F.node_ok = g.node_ok_used ? g.node_ok.as<uint8_t>() : nullptr;
+            F.feas = g.node_feas.as<uint8_t>();
+            s->pending_fold = F;
+            s->fold_pending = true;
+            if (!s->fold_defer_ok) {
+                const int rc = flush_fold(s);
+                if (rc) return rc;
+            }
         } else {
             HIP_TRY(s, upload_s(s, g.class_ok, class_ok));
             HIP_TRY(s, pe_launch_fold_feas(&soa, g.class_ok.as<uint8_t>(),
@@ -3032,9 +3082,33 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     A.full_out = s->h_place_out.dev<pe_ranked_node>();
     A.eval_status = s->h_place_status.dev<uint32_t>();
     if (!A.full_out || !A.eval_status) return s->fail(PE_EHIP, "mapped result buffers unavailable");
+    // the table build's pending fold: carried by the chain's first launch
+    // (k_base pulls the class table into LDS per workgroup while that stays
+    // small on the bus, the fused k_chain for short lists), else its own launch
+    bool fused = false;
+    if (chain) {
+        const uint32_t base_blocks = (2u * (uint32_t)n + 63u) / 64u;
+        fused = (uint32_t)n <= pe_chain_fused_max_n() && pe_chain_shape(n) <= 4 &&
+                count <= pe_chain_fused_max_count() && count <= chunk &&
+                s->nodes.size() <= 16384 && std::getenv("PE_CHAIN_FUSED") == nullptr;
+        if (fused && s->fold_pending && s->pending_fold.ncls > pe_chain_fused_max_classes()) fused = false;
+        if (s->fold_pending && (fused || (size_t)s->pending_fold.ncls * base_blocks <= 256u * 1024u)) {
+            A.fold = s->pending_fold;
+            s->fold_pending = false;
+        }
+    }
+    {
+        const int frc = flush_fold(s);
+        if (frc) return frc;
+    }
     if (chain) {
         // k_chain writes one compact entry per Select; k_emit (many workgroups)
-        // builds the full records and writes the placements back
+        // builds the full records and writes the placements back (or, fused,
+        // k_chain itself)
+        if (fused) {
+            A.fused = 1;
+            A.base1 = nullptr;   // later phases re-evaluate rows holding placements
+        }
         const size_t cap = std::min(count, chunk);
         HIP_TRY(s, s->d_emit.ensure(sizeof(pe::ChainEmit) * cap));
         HIP_TRY(s, s->d_emit_ov.ensure(sizeof(uint2) * cap));
@@ -3082,20 +3156,32 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         }
         {
             ApiScope prof_l_(s, "run_place.launch");
-            if (chain) HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream));
-            else HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
+            if (chain) {
+                hipEvent_t* split = nullptr;
+                if (s->kernel_split) {
+                    for (auto& ev : s->ev_split)
+                        if (!ev) HIP_TRY(s, hipEventCreate(&ev));
+                    split = s->ev_split;
+                }
+                HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream, split));
+                s->split_valid = split != nullptr;
+            } else {
+                s->split_valid = false;
+                HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
+            }
             if (A.perm_src) {   // d_visit now holds the list (stream order)
                 s->d_visit_is_visit = staged_is_visit;
                 A.perm_src = nullptr;
                 A.perm_dst = nullptr;
             }
+            A.fold = pe::FoldArgs{};   // the first launch carried it
             HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
         }
         const double t1 = hprof ? now_us() : 0.0;
         ApiScope prof_w_(s, "run_place.wait+copy");
         if (spin) {
             const double t_spin = now_us();
-            const uint32_t nwg = pe_emit_grid(c);
+            const uint32_t nwg = A.fused ? 1u : pe_emit_grid(c);
             uint32_t w = 0;   // completion words seen so far (in order)
             while (w < nwg) {
                 if (flag[w] == A.done_seq) { w++; continue; }
@@ -3140,6 +3226,8 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             h_sync += t2 - t1;
             h_copy += t3 - t2;
         }
+        if (chain && (st[1] & kChainErrFlag))
+            return s->fail(PE_EINTERNAL, "k_chain: a bounds guard tripped (evaluation stopped)");
         *placed += st[0];
         *new_offset = st[1] & ~kStalledFlag;
         if (chain && (st[1] & kStalledFlag)) {
@@ -3152,6 +3240,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
                 sink = nullptr;
             }
             chain = false;
+            A.fused = 0;
             A.base = nullptr;
             A.base1 = nullptr;
             A.base_by_pos = 0;
@@ -3252,6 +3341,7 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     if (const char* e = std::getenv("PE_SPECULATE")) s->spec_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_SPIN_WAIT")) s->spin_wait = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_API_PROF")) s->api_prof = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PE_KERNEL_SPLIT")) s->kernel_split = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_TEST_FALLBACK_EVERY")) s->test_fallback_every = std::strtoull(e, nullptr, 10);
     if (cfg->device_count > 1) {
         // replicas on the other devices, and the communicators of the group
@@ -3298,6 +3388,8 @@ void pe_stack_destroy(pe_stack* s) {
     if (s->ev_x0) (void)hipEventDestroy(s->ev_x0);
     if (s->ev_x1) (void)hipEventDestroy(s->ev_x1);
     retire_tgs(s);
+    for (hipEvent_t ev : s->ev_split)
+        if (ev) (void)hipEventDestroy(ev);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->ev2) (void)hipEventDestroy(s->ev2);
@@ -3317,6 +3409,27 @@ double pe_last_kernel_ms(const pe_stack* s) {
         m->last_ms_pending = false;
     }
     return s->last_ms;
+}
+
+int pe_set_kernel_split(pe_stack* s, int on) {
+    if (!s) return PE_EINVAL;
+    s->kernel_split = on != 0;
+    s->split_valid = false;
+    return PE_OK;
+}
+
+int pe_last_kernel_split(const pe_stack* s, double* ms4) {
+    if (!s || !ms4) return PE_EINVAL;
+    if (!s->split_valid) return PE_ESTATE;
+    pe_stack* m = const_cast<pe_stack*>(s);
+    if (hipEventSynchronize(m->ev_split[4]) != hipSuccess) return m->fail(PE_EHIP, "kernel split events");
+    for (int k = 0; k < 4; k++) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, m->ev_split[k], m->ev_split[k + 1]) != hipSuccess)
+            return m->fail(PE_EHIP, "kernel split events");
+        ms4[k] = ms;
+    }
+    return PE_OK;
 }
 
 uint32_t pe_last_sweep_bytes(const pe_stack* s) { return s ? s->last_sweep_bytes : 0u; }
@@ -4770,12 +4883,29 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
     if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place needs a generic stack");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
+    // The table build's fold may ride in the windowed chain's first launch
+    // (run_place); every other path below launches it first, and nothing
+    // leaves this function with it pending.
+    struct FoldGuard {
+        pe_stack* s;
+        ~FoldGuard() {
+            s->fold_defer_ok = false;
+            if (s->fold_pending) (void)flush_fold(s);
+        }
+    } fold_guard{s};
+    s->fold_defer_ok = true;
     int rc = prepare_tg(s, tgi, s->visit, s->offset);
+    s->fold_defer_ok = false;
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;
     const bool retry = retry_preempt && s->cfg.preempt;
     uint32_t p = 0, no = s->offset;
+    if (g.psets_dynamic || retry || tg_full_scan(s, g)) {
+        // no windowed chain launch first on these paths
+        rc = flush_fold(s);
+        if (rc) return rc;
+    }
     if (g.psets_dynamic) {
         // plan stops clear property values: one Select at a time, the counts
         // rebuilt on the host after every commit
@@ -4815,6 +4945,8 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
     const bool chain_ok = s->limit <= pe_chain_max_limit();
     if (count && g.psets.empty() && nv >= kParallelMinNodes && (s->cfg.preempt || !chain_ok)) {
         uint32_t cnt[3];
+        rc = flush_fold(s);
+        if (rc) return rc;
         rc = census(s, g, cnt);
         if (rc) return rc;
         parallel = cnt[0] == 0 || (uint64_t)std::min<uint32_t>(s->limit, nv) * nv / cnt[0] > kParallelWalk;
@@ -4865,6 +4997,8 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
         // merge followed by k_sweep_step (winner record + commit on the
         // device), queued back to back with no host round trip; the host only
         // checks the stop flag between chunks. A full pass leaves the cursor.
+        rc = flush_fold(s);
+        if (rc) return rc;
         rc = sweep_count_loop(s, g, tgi, count, out, &p);
         if (rc) return rc;
         count = 0;
@@ -5604,6 +5738,10 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
     s->last_ms = ms;
     s->last_ms_pending = false;
     const uint32_t* st = s->h_batch_status.as<uint32_t>();
+    if (s->batch_chain)
+        for (uint32_t e = 0; e < E; e++)
+            if (st[2 * e + 1] & kChainErrFlag)
+                return s->fail(PE_EINTERNAL, "k_chain: a bounds guard tripped (batch evaluation stopped)");
     if (placed)
         for (uint32_t e = 0; e < E; e++) placed[e] = st[2 * e];
     if (out) std::memcpy(out, s->h_batch_out.p, sizeof(pe_placement) * (size_t)E * count);

@@ -170,6 +170,18 @@ static_assert(sizeof(EmitRec) % 8 == 0, "record copy granule");
 static_assert(offsetof(EmitRec, n_device_offers) == offsetof(pe_ranked_node, n_preempted),
               "EmitRec shares pe_ranked_node's leading fields");
 
+// The FeasibilityWrapper verdicts folded into one byte per node (k_fold_feas_staged's
+// work) carried by the next windowed-chain launch instead of a launch of its
+// own: k_base (or a fused k_chain) pulls the class table from the staging ring
+// into LDS, stores node_feas for every row and evaluates with the table.
+struct FoldArgs {
+    const uint8_t* class_src;    // class verdict table in the mapped staging ring
+    uint8_t* class_dst;          // its device copy (written by one workgroup)
+    uint32_t ncls;
+    const uint8_t* node_ok;      // [n] or null
+    uint8_t* feas;               // [n] node_feas; null: no fold carried
+};
+
 // One launch = n_evals independent evaluations (one workgroup each) of the same
 // task group over the same snapshot; eval e visits perms + e*perm_stride.
 struct BatchArgs {
@@ -209,7 +221,7 @@ struct BatchArgs {
     // Single-evaluation k_chain with deferred records (or null): k_chain writes
     // one ChainEmit per Select and dumps its overlay (row, placements) into
     // emit_ov; k_emit builds the full records and writes the placements back.
-    // emit_n: [0] entries, [1] overlay rows to write back, [2] k_emit ticket.
+    // emit_n: [0] entries, [1] overlay rows to write back.
     ChainEmit* emit;
     uint2* emit_ov;
     uint32_t* emit_n;
@@ -219,6 +231,11 @@ struct BatchArgs {
     // k_chain scratch, kChainMaxN doubles per workgroup: the window's values
     // by relative position (one thread per Select walks its own positions)
     double* chain_vs;
+    FoldArgs fold;                // a fold carried by this launch (fold.feas null: none)
+    // Short lists, one evaluation: k_chain alone (no k_base / k_emit /
+    // k_emit_writeback launches) evaluates the first phase's positions itself,
+    // builds the records, writes the placements back and raises done_flag[0]
+    int fused;
     pe_ranked_node* full_out;     // [n_evals][count] full records, or null
     EmitRec* emit_out;            // k_emit's records (single-evaluation chain), or null
     pe_placement* out;            // [n_evals][count] compact records, or null

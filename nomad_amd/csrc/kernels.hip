@@ -30,6 +30,7 @@ namespace pe {
 
 enum : int { kOption = 0, kFiltered = 1, kExhausted = 2 };
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kFoldMaxClasses = 16384;   // class verdict table staged in LDS by a fold
 
 struct NodeEval {
     int status;
@@ -1267,9 +1268,35 @@ __device__ __forceinline__ double encode_eval(const NodeEval& ev) {
 // two lanes of one position are neighbours in a wave, so the row's column
 // lines are fetched once for both (halves in separate workgroups landed on
 // separate XCDs and fetched every line twice).
+// With FOLD the launch also carries the FeasibilityWrapper fold (FoldArgs):
+// each workgroup pulls the class verdict table from the staging ring into LDS,
+// the grid stores node_feas for every row (the later kernels read it), and the
+// evaluation reads the verdict from the table (no dependency on another
+// workgroup's stores).
 constexpr int kBaseBlock = 64;
+template <bool FOLD>
 __global__ void __launch_bounds__(kBaseBlock) k_base(BatchArgs A) {
+    __shared__ uint8_t cls_ok[FOLD ? kFoldMaxClasses : 1];
     const uint32_t stride = gridDim.x * kBaseBlock;
+    TgTables tg = A.tg;
+    const uint8_t* class_ok = A.tg.class_ok;
+    if (FOLD) {
+        const FoldArgs& F = A.fold;
+        for (uint32_t c = threadIdx.x; c < F.ncls; c += kBaseBlock) {
+            const uint8_t v = F.class_src[c];
+            cls_ok[c] = v;
+            if (blockIdx.x == 0) F.class_dst[c] = v;
+        }
+        __syncthreads();
+        for (uint32_t row = blockIdx.x * kBaseBlock + threadIdx.x; row < A.soa.n; row += stride) {
+            const uint32_t c = A.soa.rec[row].cls;
+            bool ok = c < F.ncls && cls_ok[c] != 0;
+            if (F.node_ok) ok = ok && F.node_ok[row] != 0;
+            F.feas[row] = ok ? 1 : 0;
+        }
+        class_ok = cls_ok;
+        tg.node_feas = nullptr;   // status_loaded: class_ok[cls] && node_ok[row]
+    }
     const uint32_t m = A.base_by_pos ? A.n_visit : A.soa.n;
     const uint32_t sh = A.base1 ? 1u : 0u;
     const uint32_t total = m << sh;
@@ -1286,10 +1313,10 @@ __global__ void __launch_bounds__(kBaseBlock) k_base(BatchArgs A) {
             }
         }
         NodeIn in;
-        load_node(A.soa, A.tg, row, in);
+        load_node(A.soa, tg, row, in);
         NodeEval ev;
         ev.score = 0.0;
-        eval_loaded<false, false>(A.soa, A.tg, A.tg.class_ok, A.ask, dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+        eval_loaded<false, false>(A.soa, tg, class_ok, A.ask, dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
         (dk ? A.base1 : A.base)[j] = encode_eval(ev);
     }
 }
@@ -1321,24 +1348,82 @@ __global__ void __launch_bounds__(kBaseBlock) k_base(BatchArgs A) {
 // the window ends the phase early; if it is the phase's first one it has seen
 // the whole list: the stream is exhausted, set-aside options are appended
 // (at most `limit` in total) and the cursor stays (feasible.go:90-107).
+// One record of a deferred-record k_chain launch: the full Select result of
+// the entry, evaluated on the state the launch started from (the entry's dk =
+// placements of the launch on the row before it).
+__device__ __forceinline__ void build_emit_rec(const BatchArgs& A, const ChainEmit& m, EmitRec& o) {
+    o.row = m.row;
+    o.nodes_evaluated = m.consumed;
+    o.nodes_filtered = m.filtered;
+    o.nodes_exhausted = m.exhausted;
+    o.new_offset = m.new_offset;
+    o.final_score = 0.0;
+    o.n_scores = 0;
+    o.n_device_offers = 0;
+    o.pad = 0;
+    for (int q = 0; q < PE_MAX_SCORES; q++) o.scores[q] = 0.0;
+    for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o.device_offer_group[q] = 0;
+    if (m.row < 0) return;
+    const uint32_t row = (uint32_t)m.row;
+    NodeIn in;
+    load_node(A.soa, A.tg, row, in);
+    NodeEval ev;
+    ev.score = 0.0;
+    eval_loaded<true, false>(A.soa, A.tg, A.tg.class_ok, A.ask, m.dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+    o.final_score = ev.score;
+    o.n_scores = ev.nscores;
+    for (int q = 0; q < PE_MAX_SCORES; q++) if (q < (int)ev.nscores) o.scores[q] = ev.parts[q];
+    if (A.ask.n_dev > 0) {
+        const DevClass& dc = A.tg.dev_cls[A.soa.rec[row].cls];
+        uint32_t fr = dev_after(A.ask, dc, A.tg.dev_free[row], m.dk);
+        double mm;
+        uint32_t groups[kMaxDevReq];
+        if (dev_assign(A.ask, dc, fr, &mm, groups)) {
+            o.n_device_offers = (uint32_t)A.ask.n_dev;
+            for (int q = 0; q < kMaxDevReq; q++)
+                if (q < A.ask.n_dev) o.device_offer_group[q] = (uint16_t)groups[q];
+        }
+    }
+}
+
 constexpr int kChainBlock = 1024;
-constexpr int kChainItems = 16;
-constexpr uint32_t kChainMaxN = kChainBlock * kChainItems;   // positions per phase held in registers
+constexpr int kChainItems = 16;                               // positions per lane of the largest shape
+constexpr uint32_t kChainMaxN = kChainBlock * kChainItems;   // positions per phase held in registers (largest shape)
 constexpr int kChainMaxSel = 1024;                            // Selects resolved per phase
-constexpr int kChainTiles = kChainMaxN / 64;
 constexpr uint32_t kChainMaxRedo = 2048;                      // rows re-evaluated per phase (<= placements per launch)
 
 enum : int { kPhaseMore = 0, kPhaseCount = 1, kPhaseExhausted = 2, kPhaseStall = 3, kPhaseRetry = 4 };
 constexpr uint32_t kChainStalled = 0x80000000u;   // eval_status cursor flag: continue with the lazy loop
 constexpr int kSegE = 21;                 // entry offsets into a segment: a Select spans <= limit + 3 options
 constexpr uint32_t kSegLen = 256;         // options per segment of the boundary walk
-constexpr int kChainSegs = kChainMaxN / kSegLen;
 constexpr uint32_t kMaxChainLimit = kSegE - 3;
 constexpr uint16_t kNxFail = 0xFFFF;      // the Select starting at this option cannot stop in the window
 constexpr uint32_t kExFail = 0xFF;
+// k_chain error flags (eval_status cursor word, beside kChainStalled): an
+// index the shape's arrays do not cover. The kernel stops the evaluation
+// instead of storing out of bounds and the host fails the call.
+constexpr uint32_t kChainError = 0x40000000u;
 
+// Per-instantiation shape of k_chain: ITEMS visit positions per lane, so one
+// phase covers kMaxN = 1024 * ITEMS positions. Every array and loop bound below
+// derives from it, including the wave-0 tile scan (kScanPer tiles per lane,
+// at least one: a shape with fewer than 64 tiles still scans all of them).
+template <int ITEMS>
+struct ChainShape {
+    static constexpr int kItems = ITEMS;
+    static constexpr uint32_t kMaxN = (uint32_t)kChainBlock * ITEMS;
+    static constexpr int kTiles = (int)(kMaxN / 64);
+    static constexpr int kSegs = (int)((kMaxN + kSegLen - 1) / kSegLen);
+    static constexpr int kScanPer = (kTiles + 63) / 64;
+    static_assert(kScanPer * 64 >= kTiles, "the tile scan covers every tile");
+    static_assert(kMaxN <= kChainMaxN, "the host sizes scratch for the largest shape");
+    static_assert(kMaxN % 32 == 0, "position bitmaps");
+};
+
+template <int ITEMS>
 struct ChainShared {
-    uint32_t tile_o[kChainTiles], tile_n[kChainTiles];    // per 64-position tile counts, then exclusive offsets
+    using Shp = ChainShape<ITEMS>;
+    uint32_t tile_o[Shp::kTiles], tile_n[Shp::kTiles];    // per 64-position tile counts, then exclusive offsets
     uint32_t sel_b[kChainMaxSel];                          // option index of each Select's stop
     uint32_t sel_end[kChainMaxSel];                        // its visit position (relative to the phase start)
     unsigned long long sel_max[kChainMaxSel];              // order-preserving key of the max returned score,
@@ -1346,16 +1431,17 @@ struct ChainShared {
     uint32_t sel_arg[kChainMaxSel];                        // option index of the first maximum
     uint32_t sel_row[kChainMaxSel];                        // the winner's row
     uint32_t sel_f[kChainMaxSel], sel_x[kChainMaxSel];     // filtered / exhausted positions (metrics)
-    uint32_t seg_tab[kChainSegs][kSegE];                  // per segment and entry offset: count | exit << 16
-    uint16_t seg_entry[kChainSegs], seg_base[kChainSegs];
+    uint32_t seg_tab[Shp::kSegs][kSegE];                  // per segment and entry offset: count | exit << 16
+    uint16_t seg_entry[Shp::kSegs], seg_base[Shp::kSegs];
     uint2 redo[kChainMaxRedo];                             // (row, placements) to re-evaluate; then the value
     uint16_t sel_pos[kChainMaxSel];                        // the winner's visit position (relative)
     // visit positions (mod n) whose row holds >= 1 / >= 2 placements of this
     // launch: later phases find their values without probing the overlay
-    uint32_t bm1[kChainMaxN / 32], bm2[kChainMaxN / 32];
+    uint32_t bm1[Shp::kMaxN / 32], bm2[Shp::kMaxN / 32];
     double aside_v[kMaxSkip];
     uint32_t aside_row[kMaxSkip];
     uint32_t tot_o, tot_n, nsel, mode, n_redo, n_seg, slow, n_emit, n_ov;
+    uint32_t err;                                          // a bounds guard tripped (kChainError)
 };
 
 __device__ __forceinline__ unsigned long long order_key(double x) {
@@ -1469,6 +1555,10 @@ __device__ __noinline__ void chain_walk(Sh& sh, const uint16_t* nb, const double
                 if (bp < 0 || yk > best) { best = yk; bp = (int)(pb + (uint32_t)k); }
             }
         }
+        if (bp < 0) {   // every Select returns at least one option past its set-aside ones
+            sh.err = 1u;
+            bp = (int)p1;
+        }
         sh.sel_end[s] = p1;
         sh.sel_pos[s] = (uint16_t)bp;
         sh.sel_max[s] = (unsigned long long)gm::f2u(best);
@@ -1478,16 +1568,25 @@ __device__ __noinline__ void chain_walk(Sh& sh, const uint16_t* nb, const double
     }
 }
 
+// FUSED (short lists of one evaluation, BatchArgs::fused): no k_base, k_emit
+// or k_emit_writeback launch; the kernel carries the fold (FoldArgs), evaluates
+// its first phase's positions itself (storing them as the base table of the
+// later phases, whose rows with placements are re-evaluated: no base1), builds
+// the records into the mapped output, writes the placements back and raises
+// done_flag[0].
+constexpr uint32_t kFusedMaxClasses = 4096;
+template <int ITEMS, bool FUSED>
 __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_evals) {
-    static_assert(kChainMaxN <= (1u << kIdxBits), "option index packing");
+    using Shp = ChainShape<ITEMS>;
+    static_assert(Shp::kMaxN <= (1u << kIdxBits), "option index packing");
     static_assert(kChainMaxSel <= (1 << (32 - 2 * kIdxBits + kIdxBits)), "select id packing");
-    __shared__ ChainShared sh;
+    __shared__ ChainShared<ITEMS> sh;
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = A.n_visit;
-    // positions per phase: one rotation, or its first kChainMaxN positions on a
+    // positions per phase: one rotation, or its first Shp::kMaxN positions on a
     // longer list (every Select of the phase still stops inside the window)
-    const uint32_t Wfull = n < kChainMaxN ? n : kChainMaxN;
+    const uint32_t Wfull = n < Shp::kMaxN ? n : Shp::kMaxN;
     const uint32_t L = A.limit;
     const uint32_t H = 1u << A.hash_bits;
     // A in the kernel-argument segment, for the out-of-line helpers (taking the
@@ -1505,6 +1604,24 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
 
     uint64_t prof_t = A.prof ? __builtin_readcyclecounter() : 0;
     int prof_ph = 0;   // profile slot group: phase (capped at 3)
+    if (FUSED && A.fold.feas) {
+        // the FeasibilityWrapper fold of every row, before any evaluation
+        __shared__ uint8_t fcls[FUSED ? kFusedMaxClasses : 1];
+        const FoldArgs& F = A.fold;
+        for (uint32_t c = tid; c < F.ncls; c += kChainBlock) {
+            const uint8_t v = F.class_src[c];
+            fcls[c] = v;
+            F.class_dst[c] = v;
+        }
+        __syncthreads();
+        for (uint32_t row = tid; row < A.soa.n; row += kChainBlock) {
+            const uint32_t c = A.soa.rec[row].cls;
+            bool ok = c < F.ncls && fcls[c] != 0;
+            if (F.node_ok) ok = ok && F.node_ok[row] != 0;
+            F.feas[row] = ok ? 1 : 0;
+        }
+        __syncthreads();
+    }
     for (uint32_t e = blockIdx.x; e < n_evals; e += gridDim.x) {
         const uint32_t* __restrict__ perm = A.perms + (size_t)e * A.perm_stride;
         double* __restrict__ vs = A.chain_vs + (size_t)blockIdx.x * kChainMaxN;   // values by relative position
@@ -1512,13 +1629,14 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             ov.keys[i] = kEmpty;
             if (ov.k) ov.k[i] = 0;
         }
-        for (uint32_t i = tid; i < kChainMaxN / 32; i += kChainBlock) {
+        for (uint32_t i = tid; i < Shp::kMaxN / 32; i += kChainBlock) {
             sh.bm1[i] = 0;
             sh.bm2[i] = 0;
         }
         if (tid == 0) {
-            sh.slow = n > kChainMaxN ? 1u : 0u;   // the position bitmaps cover one window of the list
+            sh.slow = n > Shp::kMaxN ? 1u : 0u;   // the position bitmaps cover one window of the list
             sh.n_emit = 0;
+            sh.err = 0;
         }
         uint32_t cur = wrap_pos(A.offsets ? A.offsets[e] : A.offset0, n);
         uint32_t placed = 0;
@@ -1558,9 +1676,9 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 // else none (the first phase reads base, later ones base / base1
                 // by position and re-evaluate the bitmaps' rows from the list)
                 const bool rows_all = !A.base_by_pos || (placed && !use_bm);
-                uint32_t row[kChainItems];
+                uint32_t row[ITEMS];
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < ITEMS; q++) {
                     if (q >= qn) break;
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                     row[q] = rows_all && j < W ? perm[wrap_pos(cur + j, n)] : 0u;
@@ -1568,7 +1686,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 uint32_t one_mask = 0;
                 if (placed) {
 #pragma unroll
-                    for (int q = 0; q < kChainItems; q++) {
+                    for (int q = 0; q < ITEMS; q++) {
                         if (q >= qn) break;
                         const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                         if (j < W) {
@@ -1588,12 +1706,28 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     }
                 }
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < ITEMS; q++) {
                     if (q >= qn) break;
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                     if (j < W && !((redo_mask >> q) & 1u)) {
-                        const double* src = ((one_mask >> q) & 1u) ? A.base1 : A.base;
-                        const double v = src[A.base_by_pos ? wrap_pos(cur + j, n) : row[q]];
+                        double v;
+                        if (FUSED && !placed) {
+                            // the first phase evaluates its positions (and
+                            // stores the visit order when it came staged)
+                            const uint32_t p = wrap_pos(cur + j, n);
+                            uint32_t r;
+                            if (A.perm_src) {
+                                r = A.perm_src[p];
+                                A.perm_dst[p] = r;
+                            } else {
+                                r = perm[p];
+                            }
+                            v = chain_reeval(Ak, r, 0u);
+                            A.base[p] = v;
+                        } else {
+                            const double* src = ((one_mask >> q) & 1u) ? A.base1 : A.base;
+                            v = src[A.base_by_pos ? wrap_pos(cur + j, n) : row[q]];
+                        }
                         vs[j] = v;   // read back by the Select walks of step 5 (after the barriers)
                         const bool is_o = v > -__builtin_inf() && v < __builtin_inf();
                         optmask |= (uint32_t)is_o << q;
@@ -1605,24 +1739,26 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 // rows with placements of this launch the tables do not cover:
                 // evaluated in parallel, the value stored at its window position
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < ITEMS; q++) {
                     if (q >= qn) break;
                     if ((redo_mask >> q) & 1u) {
                         const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                         const uint32_t r = perm[wrap_pos(cur + j, n)];
                         const uint32_t slot = atomicAdd(&sh.n_redo, 1u);
-                        sh.redo[slot] = make_uint2(r, ov_count(ov, r) | (j << 18));
+                        if (slot < kChainMaxRedo) sh.redo[slot] = make_uint2(r, ov_count(ov, r) | (j << 18));
+                        else sh.err = 1u;
                     }
                 }
                 __syncthreads();
-                const uint32_t nr = sh.n_redo;
+                const uint32_t nr = min(sh.n_redo, kChainMaxRedo);
                 for (uint32_t w = tid; w < nr; w += kChainBlock) {
                     const uint2 rd = sh.redo[w];
                     vs[rd.y >> 18] = chain_reeval(Ak, rd.x, rd.y & 0x3FFFFu);
                 }
                 __syncthreads();
+                if (sh.err) break;
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < ITEMS; q++) {
                     if (q >= qn) break;
                     if ((redo_mask >> q) & 1u) {
                         const double v = vs[q * kChainBlock + tid];
@@ -1633,7 +1769,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
             }
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
+            for (int q = 0; q < ITEMS; q++) {
                 if (q >= qn) break;
                 const uint64_t bo = __ballot((optmask >> q) & 1u), bn = __ballot((nmask >> q) & 1u);
                 if (lane == 0 && q * kChainBlock < (int)W) {
@@ -1652,7 +1788,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             // 2. exclusive scan of the tile counts (wave 0)
             const uint32_t ntiles = (W + 63) / 64;
             if (wave == 0) {
-                constexpr int PER = kChainTiles / 64;
+                constexpr int PER = Shp::kScanPer;
                 uint32_t so = 0, sn = 0, lo[PER], ln[PER];
 #pragma unroll
                 for (int k = 0; k < PER; k++) {
@@ -1681,9 +1817,9 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             __syncthreads();
             PE_PROF_MARK(2);
             // 3. option index and N prefix of every option; nb[k] = N options before option k
-            uint32_t pk[kChainItems];
+            uint32_t pk[ITEMS];
 #pragma unroll
-            for (int q = 0; q < kChainItems; q++) {
+            for (int q = 0; q < ITEMS; q++) {
                 if (q >= qn) break;
                 const uint64_t bo = __ballot((optmask >> q) & 1u), bn = __ballot((nmask >> q) & 1u);
                 const uint32_t t = (uint32_t)(q * (kChainBlock / 64) + wave);
@@ -1691,11 +1827,18 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 const uint32_t k = (live ? sh.tile_o[t] : 0u) + lanes_below(bo, lane);
                 const uint32_t nbk = (live ? sh.tile_n[t] : 0u) + lanes_below(bn, lane);
                 pk[q] = (k & kIdxMask) | ((nbk & kIdxMask) << kIdxBits);
-                if ((optmask >> q) & 1u) nb[k] = (uint16_t)nbk;
+                if ((optmask >> q) & 1u) {
+                    if (k < W) nb[k] = (uint16_t)nbk;
+                    else sh.err = 1u;   // an option index past the window: the scan is wrong
+                }
             }
             const uint32_t tot_o = sh.tot_o, tot_n = sh.tot_n;
-            if (tid == 0) nb[tot_o] = (uint16_t)tot_n;
+            if (tid == 0) {
+                if (tot_o <= W) nb[tot_o] = (uint16_t)tot_n;
+                else sh.err = 1u;
+            }
             __syncthreads();
+            if (sh.err) break;   // stop the evaluation before any index built on the scan is used
             PE_PROF_MARK(3);
             // 4. Select boundaries. A Select starting at option i stops at option
             //    i + L - 1 + m for the smallest m in {0, 1, 2} with exactly m N's
@@ -1709,7 +1852,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 // exactly L options (m = 0 above), so Select s stops at option
                 // (s + 1) L - 1; nb takes the options' positions at once
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++)
+                for (int q = 0; q < ITEMS; q++)
                     if (q < qn && ((optmask >> q) & 1u)) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
                 if (tid == 0) {
                     const uint32_t want = min(A.count - placed, (uint32_t)kChainMaxSel);
@@ -1730,7 +1873,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 __syncthreads();
             } else {
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < ITEMS; q++) {
                     if (q >= qn) break;
                     if ((optmask >> q) & 1u) {
                         const uint32_t i = pk[q] & kIdxMask;
@@ -1753,7 +1896,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 __syncthreads();
                 // nb is free from here on: the relative position of every option
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++)
+                for (int q = 0; q < ITEMS; q++)
                     if (q < qn && ((optmask >> q) & 1u)) nb[pk[q] & kIdxMask] = (uint16_t)(q * kChainBlock + tid);
                 const uint32_t n_seg = (tot_o + kSegLen - 1) / kSegLen;
                 const uint32_t E = L + 3;
@@ -1845,7 +1988,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 // window (atomics over one key), its first kMaxSkip N's set aside
                 uint32_t retmask = 0;
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < ITEMS; q++) {
                     if (q >= qn) break;
                     if ((optmask >> q) & 1u) {
                         const uint32_t j = (uint32_t)(q * kChainBlock + tid);
@@ -1863,7 +2006,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < ITEMS; q++) {
                     if (q >= qn) break;
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                     if (((retmask >> q) & 1u) &&
@@ -1872,7 +2015,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 if (A.full_out || A.emit) {
 #pragma unroll
-                    for (int q = 0; q < kChainItems; q++) {
+                    for (int q = 0; q < ITEMS; q++) {
                         if (q >= qn) break;
                         const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                         if (j < W && !((optmask >> q) & 1u))
@@ -1882,7 +2025,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kChainItems; q++) {
+                for (int q = 0; q < ITEMS; q++) {
                     if (q >= qn) break;
                     const uint32_t j = (uint32_t)(q * kChainBlock + tid);
                     if (((retmask >> q) & 1u) && sh.sel_arg[0] == (pk[q] & kIdxMask)) {
@@ -1892,6 +2035,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 }
             }
             __syncthreads();
+            if (sh.err) break;
             PE_PROF_MARK(5);
             // 6. emit the winners and commit them (Plan.AppendAlloc), one Select per thread
             if (mode != kPhaseExhausted) {
@@ -1902,6 +2046,10 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     const double score = gm::u2f(sh.sel_max[s]);
                     const uint32_t it = placed + s;
                     const uint32_t next_off = wrap_pos(cur + sh.sel_end[s] + 1u, n);
+                    if (it >= A.count) {   // nsel <= count - placed by construction
+                        sh.err = 1u;
+                        continue;
+                    }
                     if (A.emit) {
                         ChainEmit& m = A.emit[it];
                         m.row = win_row;
@@ -1925,7 +2073,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 if (A.commit) {
                     for (uint32_t s = tid; s < nsel; s += kChainBlock) {
                         ov_add_atomic(ov, sh.sel_row[s]);
-                        if (n <= kChainMaxN) {   // the bitmaps cover lists of one window only
+                        if (n <= Shp::kMaxN) {   // the bitmaps cover lists of one window only
                             const uint32_t p = wrap_pos(cur + sh.sel_pos[s], n), bit = 1u << (p & 31);
                             if (atomicOr(&sh.bm1[p >> 5], bit) & bit) atomicOr(&sh.bm2[p >> 5], bit);
                         }
@@ -1980,11 +2128,25 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
             PE_PROF_MARK(6);
             prof_ph = prof_ph < 3 ? prof_ph + 1 : 3;
         }
+        __syncthreads();
         if (tid == 0) {
             A.eval_status[2 * e] = placed;
-            A.eval_status[2 * e + 1] = cur | (stalled ? kChainStalled : 0u);
+            A.eval_status[2 * e + 1] = cur | (stalled ? kChainStalled : 0u) | (sh.err ? kChainError : 0u);
         }
-        if (A.emit) {
+        if (FUSED) {
+            // the records, on the state the launch started from, then the
+            // placements into HBM, then the completion word
+            __syncthreads();
+            const uint32_t ne = min(sh.n_emit, A.count);
+            for (uint32_t i = tid; i < ne; i += kChainBlock) build_emit_rec(Ak, A.emit[i], A.emit_out[i]);
+            __syncthreads();
+            if (A.writeback) writeback_overlay<kChainBlock, false, false>(A, ov, H, nullptr);
+            __syncthreads();
+            if (tid == 0 && A.done_flag) {
+                __threadfence_system();
+                __hip_atomic_store(A.done_flag, A.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else if (A.emit) {
             // records and the HBM writeback are k_emit's: dump the overlay
             if (tid == 0) sh.n_ov = 0;
             __syncthreads();
@@ -1993,12 +2155,15 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                 if (key == kEmpty) continue;
                 const uint32_t r = ov.k ? key : key >> ov.kshift;
                 const uint32_t kk = ov.k ? ov.k[h] : key & ov.kmask;
-                A.emit_ov[atomicAdd(&sh.n_ov, 1u)] = make_uint2(r, kk);
+                const uint32_t slot = atomicAdd(&sh.n_ov, 1u);
+                if (slot < A.count) A.emit_ov[slot] = make_uint2(r, kk);   // overlay rows <= placements
+                else sh.err = 1u;
             }
             __syncthreads();
             if (tid == 0) {
-                A.emit_n[0] = sh.n_emit;
-                A.emit_n[1] = A.writeback ? sh.n_ov : 0u;
+                A.emit_n[0] = min(sh.n_emit, A.count);
+                A.emit_n[1] = A.writeback ? min(sh.n_ov, A.count) : 0u;
+                if (sh.err) A.eval_status[2 * e + 1] |= kChainError;
             }
         } else if (A.writeback) {
             writeback_overlay<kChainBlock, false, false>(A, ov, H, nullptr);   // no cores on the chain path
@@ -2020,44 +2185,8 @@ __global__ void __launch_bounds__(kEmitBlock) k_emit(BatchArgs A) {
     // bus; small workgroups spread the bus writes over more CUs
     __shared__ EmitRec recs[kEmitBlock];
     const uint32_t i = blockIdx.x * kEmitBlock + threadIdx.x;
-    const uint32_t n_emit = A.emit_n[0];
-    if (i < n_emit) {
-        const ChainEmit m = A.emit[i];
-        EmitRec& o = recs[threadIdx.x];
-        o.row = m.row;
-        o.nodes_evaluated = m.consumed;
-        o.nodes_filtered = m.filtered;
-        o.nodes_exhausted = m.exhausted;
-        o.new_offset = m.new_offset;
-        o.final_score = 0.0;
-        o.n_scores = 0;
-        o.n_device_offers = 0;
-        o.pad = 0;
-        for (int q = 0; q < PE_MAX_SCORES; q++) o.scores[q] = 0.0;
-        for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o.device_offer_group[q] = 0;
-        if (m.row >= 0) {
-            const uint32_t row = (uint32_t)m.row;
-            NodeIn in;
-            load_node(A.soa, A.tg, row, in);
-            NodeEval ev;
-            ev.score = 0.0;
-            eval_loaded<true, false>(A.soa, A.tg, A.tg.class_ok, A.ask, m.dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
-            o.final_score = ev.score;
-            o.n_scores = ev.nscores;
-            for (int q = 0; q < PE_MAX_SCORES; q++) if (q < (int)ev.nscores) o.scores[q] = ev.parts[q];
-            if (A.ask.n_dev > 0) {
-                const DevClass& dc = A.tg.dev_cls[A.soa.rec[row].cls];
-                uint32_t fr = dev_after(A.ask, dc, A.tg.dev_free[row], m.dk);
-                double mm;
-                uint32_t groups[kMaxDevReq];
-                if (dev_assign(A.ask, dc, fr, &mm, groups)) {
-                    o.n_device_offers = (uint32_t)A.ask.n_dev;
-                    for (int q = 0; q < kMaxDevReq; q++)
-                        if (q < A.ask.n_dev) o.device_offer_group[q] = (uint16_t)groups[q];
-                }
-            }
-        }
-    }
+    const uint32_t n_emit = min(A.emit_n[0], A.count);
+    if (i < n_emit) build_emit_rec(A, A.emit[i], recs[threadIdx.x]);
     __syncthreads();
     {
         const uint32_t first = blockIdx.x * kEmitBlock;
@@ -2083,7 +2212,6 @@ __global__ void __launch_bounds__(kEmitBlock) k_emit(BatchArgs A) {
 // read the state the launch started from), off the host's critical path.
 __global__ void __launch_bounds__(256) k_emit_writeback(BatchArgs A) {
     const uint32_t x = blockIdx.x * 256 + threadIdx.x;
-    if (x == 0) A.emit_n[2] = 0;   // k_emit's ticket for the next launch
     if (x >= A.emit_n[1]) return;
     const uint2 e = A.emit_ov[x];
     NodeRec& r = A.soa.rec[e.x];
@@ -3111,7 +3239,6 @@ __global__ void __launch_bounds__(256) k_fold_feas(NodeSoA s, const uint8_t* cla
 // every workgroup pulls the (small) table over the bus into LDS, workgroup 0
 // also stores it to its device copy for the later kernels; saves the
 // separate upload launch.
-constexpr uint32_t kFoldMaxClasses = 16384;
 __global__ void __launch_bounds__(256) k_fold_feas_staged(NodeSoA s, const uint8_t* class_src, uint8_t* class_dst,
                                                           uint32_t ncls, const uint8_t* node_ok, uint8_t* feas) {
     __shared__ uint8_t cls_ok[kFoldMaxClasses];
@@ -3202,32 +3329,83 @@ size_t pe_chain_lds_bytes(int hash_bits, bool packed, uint32_t n) {
 
 int pe_chain_blocks_per_cu(size_t lds) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pe::k_chain, pe::kChainBlock, lds) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pe::k_chain<pe::kChainItems, false>, pe::kChainBlock, lds) !=
+            hipSuccess || nb <= 0)
         nb = 1;
     return nb;
 }
 
-hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st) {
+// Shape of a launch: the fewest positions per lane that hold one window of
+// the list. PE_CHAIN_ITEMS=4 / 16 asks for a larger shape (tests run every
+// shape on the same list); a smaller one than the list needs is never used.
+static int chain_items(uint32_t n_visit) {
+    int items = n_visit > pe::kChainBlock * 4u ? 16 : (n_visit > pe::kChainBlock ? 4 : 1);
+    if (const char* e = std::getenv("PE_CHAIN_ITEMS")) {
+        const int forced = std::atoi(e);
+        if (forced > items) items = forced >= 16 ? 16 : 4;
+    }
+    return items;
+}
+
+int pe_chain_shape(uint32_t n_visit) { return chain_items(n_visit); }
+
+// Largest list / count / class table a fused launch (BatchArgs::fused) takes.
+uint32_t pe_chain_fused_max_n() { return pe::kChainBlock * 4u; }
+uint32_t pe_chain_fused_max_count() { return 256u; }
+uint32_t pe_chain_fused_max_classes() { return pe::kFusedMaxClasses; }
+
+// split (or null): five events recorded before k_base and after k_base,
+// k_chain, k_emit and k_emit_writeback (per-kernel device time, PE_KERNEL_SPLIT)
+hipError_t pe_launch_chain(const pe::BatchArgs* a, uint32_t n_evals, uint32_t max_blocks, hipStream_t st,
+                           hipEvent_t* split) {
     if (!a->base || !a->chain_vs || (a->n_visit > pe::kChainMaxN && n_evals != 1) || a->class_ok_stride ||
         a->limit > pe::kMaxChainLimit || a->count >= (1u << 18))   // redo entries pack count | position << 18
         return hipErrorInvalidValue;
     if (a->base_by_pos && n_evals != 1) return hipErrorInvalidValue;
     if (a->perm_src && (!a->base_by_pos || !a->perm_dst)) return hipErrorInvalidValue;
+    if (a->fold.feas && (!a->fold.class_src || !a->fold.class_dst || a->fold.ncls > pe::kFoldMaxClasses))
+        return hipErrorInvalidValue;
+    const size_t lds = pe_chain_lds_bytes(a->hash_bits, a->packed_overlay != 0, a->n_visit);
+    uint32_t grid = n_evals < max_blocks ? n_evals : max_blocks;
+    if (grid == 0) grid = 1;
+    const int items = chain_items(a->n_visit);
+    if (a->fused) {
+        // one launch: fold, first-phase values, chain, records, writeback
+        if (n_evals != 1 || !a->base_by_pos || a->base1 || !a->emit || !a->emit_out || items > 4 ||
+            a->count > pe_chain_fused_max_count() || (a->fold.feas && a->fold.ncls > pe::kFusedMaxClasses))
+            return hipErrorInvalidValue;
+        if (split) for (int k = 0; k < 2; k++) (void)hipEventRecord(split[k], st);
+        if (items == 1) hipLaunchKernelGGL((pe::k_chain<1, true>), dim3(1), dim3(pe::kChainBlock), lds, st, *a, 1u);
+        else hipLaunchKernelGGL((pe::k_chain<4, true>), dim3(1), dim3(pe::kChainBlock), lds, st, *a, 1u);
+        if (split) for (int k = 2; k < 5; k++) (void)hipEventRecord(split[k], st);
+        return hipGetLastError();
+    }
     const uint32_t m = a->base_by_pos ? a->n_visit : a->soa.n;
     uint32_t blocks = ((a->base1 ? 2u * m : m) + pe::kBaseBlock - 1) / pe::kBaseBlock;
     if (blocks > 8192) blocks = 8192;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(pe::k_base, dim3(blocks), dim3(pe::kBaseBlock), 0, st, *a);
-    const size_t lds = pe_chain_lds_bytes(a->hash_bits, a->packed_overlay != 0, a->n_visit);
-    uint32_t grid = n_evals < max_blocks ? n_evals : max_blocks;
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(pe::k_chain, dim3(grid), dim3(pe::kChainBlock), lds, st, *a, n_evals);
+    if (split) (void)hipEventRecord(split[0], st);
+    if (a->fold.feas) hipLaunchKernelGGL(pe::k_base<true>, dim3(blocks), dim3(pe::kBaseBlock), 0, st, *a);
+    else hipLaunchKernelGGL(pe::k_base<false>, dim3(blocks), dim3(pe::kBaseBlock), 0, st, *a);
+    if (split) (void)hipEventRecord(split[1], st);
+    switch (items) {
+    case 1: hipLaunchKernelGGL((pe::k_chain<1, false>), dim3(grid), dim3(pe::kChainBlock), lds, st, *a, n_evals); break;
+    case 4: hipLaunchKernelGGL((pe::k_chain<4, false>), dim3(grid), dim3(pe::kChainBlock), lds, st, *a, n_evals); break;
+    default:
+        hipLaunchKernelGGL((pe::k_chain<pe::kChainItems, false>), dim3(grid), dim3(pe::kChainBlock), lds, st, *a,
+                           n_evals);
+    }
+    if (split) (void)hipEventRecord(split[2], st);
     if (a->emit) {
         if (n_evals != 1 || !a->emit_out || !a->emit_ov || !a->emit_n) return hipErrorInvalidValue;
         hipLaunchKernelGGL(pe::k_emit, dim3(pe_emit_grid(a->count)), dim3(pe::kEmitBlock), 0, st, *a);
+        if (split) (void)hipEventRecord(split[3], st);
         const uint32_t wb = (a->count + 255) / 256;   // overlay rows <= placements
         hipLaunchKernelGGL(pe::k_emit_writeback, dim3(wb ? wb : 1), dim3(256), 0, st, *a);
+    } else if (split) {
+        (void)hipEventRecord(split[3], st);
     }
+    if (split) (void)hipEventRecord(split[4], st);
     return hipGetLastError();
 }
 

@@ -52,6 +52,10 @@ def load_engine():
         lib.pe_last_kernel_ms.argtypes = [C.c_void_p]
         lib.pe_last_sweep_bytes.restype = C.c_uint32
         lib.pe_last_sweep_bytes.argtypes = [C.c_void_p]
+        lib.pe_set_kernel_split.restype = C.c_int
+        lib.pe_set_kernel_split.argtypes = [C.c_void_p, C.c_int]
+        lib.pe_last_kernel_split.restype = C.c_int
+        lib.pe_last_kernel_split.argtypes = [C.c_void_p, abi.f64p]
         lib.pe_stage_orders.restype = C.c_int
         lib.pe_stage_orders.argtypes = [C.c_void_p, abi.u32p, C.c_uint32, C.c_uint32]
         lib.pe_place_batch.restype = C.c_int
@@ -537,6 +541,16 @@ class GenericStack(_Stack):
     def last_sweep_bytes(self) -> int:
         """Algorithmic bytes per node of the last full-scan sweep Select."""
         return self._lib.pe_last_sweep_bytes(self._h)
+
+    def SetKernelSplit(self, on: bool = True):
+        """Record HIP events between the windowed chain's kernels (measurement aid)."""
+        self._check(self._lib.pe_set_kernel_split(self._h, 1 if on else 0))
+
+    def last_kernel_split(self):
+        """{k_base, k_chain, k_emit, k_emit_writeback} device ms of the last chain launch."""
+        buf = (C.c_double * 4)()
+        self._check(self._lib.pe_last_kernel_split(self._h, C.cast(buf, abi.f64p)))
+        return dict(zip(("k_base", "k_chain", "k_emit", "k_emit_writeback"), list(buf)))
 
 
 def comm_unique_id() -> bytes:

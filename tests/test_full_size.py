@@ -105,6 +105,71 @@ def test_c5_50k_caller_protocol(c5_cluster):
     assert sum(1 for x in res[0] if x is not None and x[7]) >= 30
 
 
+@pytest.fixture(scope="module")
+def c5_bench_shape():
+    """bench.py's C5 workload exactly (section_c5): 50k nodes, busy=0.99,
+    job_c5(1000), shuffle(.., 77), service preemption on, and the oracle's
+    1000 placements of it frozen in tests/golden/c5_bench_shape.json.gz
+    (tools/make_c5_golden.py: ~10 minutes of oracle time, too long for a GPU
+    test; tests/test_golden.py re-derives its first placements on the CPU).
+    The oracle's Place is the caller's loop itself (oracle.cpp oracle_place:
+    Select, Preempt retry on nil as generic_sched.go:773-792, commit with the
+    preempted set), so the one fixture answers both engine protocols below."""
+    from tools.make_c5_golden import OUT, build
+    import gzip
+    import json
+    with gzip.open(OUT, "rt") as f:
+        g = json.load(f)
+    nodes, allocs, job, perm, cfg = build(g["case"])
+    return nodes, allocs, job, perm, cfg, g
+
+
+def _c5_key(r):
+    # the record fields the fixture holds, as tests/test_dropin._key orders them
+    return (r.row, r.final_score.hex(), tuple(s.hex() for s in r.scores), r.nodes_evaluated, r.nodes_filtered,
+            r.nodes_exhausted, r.new_offset, tuple(r.preempted), tuple(r.device_offers))
+
+
+def _c5_want(g):
+    return [(w["row"], w["final_score"], tuple(w["scores"]), w["evaluated"], w["filtered"], w["exhausted"],
+             w["offset"], tuple(w["preempted"]), tuple(w["device_offers"])) for w in g["placements"]]
+
+
+def test_c5_bench_shape_count_loop(c5_bench_shape):
+    # the engine's device count loop (k_ploop) over all 1000 placements
+    from nomad_amd.stack import GenericStack
+    nodes, allocs, job, perm, cfg, g = c5_bench_shape
+    st = GenericStack(config=cfg)
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    assert st.SetNodes(perm) == g["limit"]
+    got = [_c5_key(r) for r in st.Place(0, 1000)]
+    want = _c5_want(g)
+    assert len(got) == len(want) == 1000
+    for i, (x, y) in enumerate(zip(got, want)):
+        assert x == y, ("placement %d" % i, x, y)
+    assert sum(1 for w in want if w[7]) == 628
+
+
+def test_c5_bench_shape_caller_protocol(c5_bench_shape):
+    # the same evaluation through Select / Commit with the Preempt retry
+    from nomad_amd.stack import GenericStack, SelectOptions
+    nodes, allocs, job, perm, cfg, g = c5_bench_shape
+    st = GenericStack(config=cfg)
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(perm)
+    want = _c5_want(g)
+    for i, w in enumerate(want):
+        r = st.Select(0)
+        if r is None:
+            r = st.Select(0, SelectOptions(preempt=True))
+        assert r is not None, "placement %d: nil" % i
+        got = _c5_key(r)
+        assert got == w, ("placement %d" % i, got, w)
+        st.Commit(0, r.row, r.preempted)
+
+
 def test_c2_10k_caller_protocol_count_1000():
     from nomad_amd.stack import GenericStack
     from tests.test_dropin import compute_placements
