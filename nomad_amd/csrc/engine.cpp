@@ -690,6 +690,18 @@ struct ApiScope {
                                                hipGetErrorString(_e));                  \
     } while (0)
 
+// A launch that reads the plan's device state (node records, device free
+// counts, preemptions): the deferred ResetPlan copy must have been launched
+// before it (every entry point starts with PE_FLUSH_RESET); a launch that
+// would read the previous evaluation's state fails instead.
+#define HIP_TRY_STATE(s, expr)                                                          \
+    do {                                                                                \
+        if ((s)->reset_pending)                                                         \
+            return (s)->fail(PE_EINTERNAL, std::string(#expr ": the deferred ResetPlan " \
+                                                       "copy was not launched first")); \
+        HIP_TRY(s, expr);                                                               \
+    } while (0)
+
 // Host -> device upload ordered on the engine stream: the bytes are staged in
 // a page-locked ring and copied asynchronously, so an entry point does not
 // wait for the device; the ring restarts after a stream synchronisation when
@@ -1996,11 +2008,13 @@ static int flush_reset(pe_stack* s) {
         if (rc) return rc;
     }
     if (!s->reset_pending) return PE_OK;
-    s->reset_pending = false;
     HIP_TRY(s, hipSetDevice(s->device));
     const pe::ResetArgs R = reset_args(s);
     HIP_TRY(s, pe_launch_reset_plan(R.rec, R.base_rec, R.dev_free, R.dev_free_base, R.n, R.preempted, R.m, R.pcount,
                                     R.keys, s->stream));
+    // only a launched copy clears the flag: a failed launch is retried by the
+    // next entry point instead of leaving the previous evaluation's state
+    s->reset_pending = false;
     return PE_OK;
 }
 
@@ -2066,9 +2080,9 @@ int build_collisions(pe_stack* s, bool own = false) {
     }
     if (!ents.empty()) HIP_TRY(s, upload_s(s, s->d_count_ents, ents));
     const pe::ResetArgs R = s->reset_pending ? reset_args(s) : pe::ResetArgs{};
-    s->reset_pending = false;
     HIP_TRY(s, pe_launch_counts(&D, nd, (uint32_t)n, ents.empty() ? nullptr : s->d_count_ents.as<uint2>(),
                                 (uint32_t)ents.size(), R.rec ? &R : nullptr, s->stream));
+    s->reset_pending = false;   // the copy rode in this launch (cleared only once it launched)
     return PE_OK;
 }
 
@@ -2737,7 +2751,7 @@ int sweep_partial(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_
         return PE_OK;
     }
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-    HIP_TRY(s, pe_launch_sweep(&A, blocks, s->d_sweep_merged.as<pe::SweepRec>(), s->stream));
+    HIP_TRY_STATE(s, pe_launch_sweep(&A, blocks, s->d_sweep_merged.as<pe::SweepRec>(), s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     HIP_TRY(s, hipMemcpyAsync(rec, s->d_sweep_merged.p, sizeof(*rec), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -2764,7 +2778,7 @@ int sweep_finish(pe_stack* s, pe::SweepArgs& A, const pe::SweepRec& rec, pe_rank
         uint32_t pos = s->offset + rank;
         if (pos >= n) pos -= n;
         const uint32_t row = s->visit[pos];
-        HIP_TRY(s, pe_launch_node_record(&A, row, s->d_record.as<pe_ranked_node>(), s->stream));
+        HIP_TRY_STATE(s, pe_launch_node_record(&A, row, s->d_record.as<pe_ranked_node>(), s->stream));
         pe_ranked_node rr;
         HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -2794,7 +2808,7 @@ int census(pe_stack* s, TgPlan& g, uint32_t* cnt) {
     A.n_visit = (uint32_t)s->visit.size();
     HIP_TRY(s, s->d_ev_out.ensure(16));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
-    HIP_TRY(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), nullptr, nullptr, s->stream));
+    HIP_TRY_STATE(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), nullptr, nullptr, s->stream));
     HIP_TRY(s, hipMemcpyAsync(cnt, s->d_ev_out.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     return PE_OK;
@@ -2845,7 +2859,7 @@ int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* n
     HIP_TRY(s, s->d_ev_flags.ensure(16));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
-    HIP_TRY(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->d_ev_status.as<uint8_t>(),
+    HIP_TRY_STATE(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->d_ev_status.as<uint8_t>(),
                                 s->d_ev_score.as<double>(), s->stream));
     pe::EvictResolveArgs R;
     R.status = s->d_ev_status.as<uint8_t>();
@@ -2854,7 +2868,7 @@ int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* n
     R.offset = s->offset % n;
     R.limit = s->limit;
     R.out = s->d_ev_out.as<int32_t>();
-    HIP_TRY(s, pe_launch_resolve(&R, s->stream));
+    HIP_TRY_STATE(s, pe_launch_resolve(&R, s->stream));
     int32_t res[4];
     HIP_TRY(s, hipMemcpyAsync(res, R.out, sizeof(res), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -2872,7 +2886,7 @@ int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* n
         P.visit = s->d_visit.as<uint32_t>();
         P.n_visit = n;
         P.flags = s->d_ev_flags.as<uint32_t>();
-        HIP_TRY(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
+        HIP_TRY_STATE(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
                                           s->stream));
         pe_ranked_node rr;
         HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
@@ -2935,7 +2949,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     R.limit = s->limit;
     R.out = s->d_ev_out.as<int32_t>();
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-    HIP_TRY(s, pe_launch_evict(&P, &R, s->stream));
+    HIP_TRY_STATE(s, pe_launch_evict(&P, &R, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     int32_t res[4];
     uint32_t flags = 0;
@@ -2957,7 +2971,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     out->new_offset = *new_offset;
     if (res[0] >= 0) {
         const uint32_t row = order[(uint32_t)(((uint64_t)(offset % n) + (uint32_t)res[0]) % n)];
-        HIP_TRY(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
+        HIP_TRY_STATE(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
                                           s->stream));
         pe_ranked_node rr;
         uint32_t mask = 0;
@@ -3128,8 +3142,9 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     uint32_t done = 0;
     const bool hprof = std::getenv("PE_PLACE_PROF") != nullptr;
     double h_launch = 0, h_sync = 0, h_copy = 0;
-    // The chain path ends with k_emit, whose last workgroup raises a completion
-    // word in the mapped status block: the host spins on it instead of waking
+    // The chain path ends with k_emit (or the fused k_chain), each of whose
+    // workgroups raises its own completion word in the mapped h_emit_done
+    // block (sequence place_seq): the host spins on them instead of waking
     // from a stream synchronisation; the launch's event timing is resolved
     // when it is asked for (pe_last_kernel_ms).
     bool spin = chain && s->spin_wait;
@@ -3163,11 +3178,11 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
                         if (!ev) HIP_TRY(s, hipEventCreate(&ev));
                     split = s->ev_split;
                 }
-                HIP_TRY(s, pe_launch_chain(&A, 1, 1, s->stream, split));
+                HIP_TRY_STATE(s, pe_launch_chain(&A, 1, 1, s->stream, split));
                 s->split_valid = split != nullptr;
             } else {
                 s->split_valid = false;
-                HIP_TRY(s, pe_launch_place(&A, 1, full, s->stream));
+                HIP_TRY_STATE(s, pe_launch_place(&A, 1, full, s->stream));
             }
             if (A.perm_src) {   // d_visit now holds the list (stream order)
                 s->d_visit_is_visit = staged_is_visit;
@@ -4098,7 +4113,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             HIP_TRY(s, pe_launch_spread_table(&t, s->d_spread_tab.as<double>(), s->stream));
             stab = s->d_spread_tab.as<double>();
         }
-        HIP_TRY(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
+        HIP_TRY_STATE(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
                                    s->d_trace_out.as<uint32_t>(), pbits, s->log10, stab,
                                    s->d_trace_scores.as<double>(), s->stream));
         std::vector<uint32_t> codes(rows.size());
@@ -4120,7 +4135,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             }
             HIP_TRY(s, s->d_ev_tcodes.ensure(rows.size() * sizeof(uint32_t)));
             HIP_TRY(s, s->d_ev_named.ensure(rows.size() * 7 * sizeof(double)));
-            HIP_TRY(s, pe_launch_evict_trace(&P, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
+            HIP_TRY_STATE(s, pe_launch_evict_trace(&P, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
                                              s->d_ev_tcodes.as<uint32_t>(), s->d_ev_named.as<double>(), s->stream));
             ecodes.resize(rows.size());
             named.resize(rows.size() * 7);
@@ -4283,7 +4298,7 @@ static int sys_flush(pe_stack* s) {
     pe::NodeSoA soa = soa_of(s);
     pe::TgTables t = tables_of(g);
     pe::Ask a = ask_for(s, g);
-    HIP_TRY(s, pe_launch_commit_rows(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(), (uint32_t)y.pending.size(),
+    HIP_TRY_STATE(s, pe_launch_commit_rows(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(), (uint32_t)y.pending.size(),
                                      s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     y.pending.clear();
@@ -4332,7 +4347,7 @@ static int sys_start(pe_stack* s, uint32_t tgi) {
     A.n_rows = n;
     A.n_list = 0;                                // outcomes stay in res, by row
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-    HIP_TRY(s, pe_launch_system(&A, s->stream));
+    HIP_TRY_STATE(s, pe_launch_system(&A, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     HIP_TRY(s, hipMemcpyAsync(s->h_sys_cache.p, s->d_sys_res.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -4516,7 +4531,7 @@ static int commit_impl(pe_stack* s, uint32_t tgi, int32_t row) {
     // the Select's own device offers when it chose this node (rank.go:404-405)
     const uint32_t offers = row == s->offer_row ? s->offers : 0xFFFFFFFFu;
     s->offer_row = -1;
-    HIP_TRY(s, pe_launch_commit(&soa, &t, &a, (uint32_t)row, offers, s->stream));
+    HIP_TRY_STATE(s, pe_launch_commit(&soa, &t, &a, (uint32_t)row, offers, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     s->plan.emplace_back(g.name, (uint32_t)row);
     invalidate_job_distinct(s, tgi);
@@ -4618,7 +4633,7 @@ static int commit_preempt_impl(pe_stack* s, uint32_t tgi, int32_t row, const uin
     HIP_TRY(s, hipSetDevice(s->device));
     TgPlan& g = *s->tgs[tgi];
     pe::PreemptArgs P = preempt_args(s, g);
-    HIP_TRY(s, pe_launch_commit_preempt(&P, (uint32_t)row, mask, s->d_preempted.as<uint8_t>(),
+    HIP_TRY_STATE(s, pe_launch_commit_preempt(&P, (uint32_t)row, mask, s->d_preempted.as<uint8_t>(),
                                         s->d_pcount.as<uint32_t>(), s->d_dev_free.as<uint32_t>(), s->stream));
     for (uint32_t i = 0; i < n_preempted; i++) {
         s->h_preempted[s->alloc_slot[preempted[i]]] = 1;
@@ -4665,7 +4680,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
     HIP_TRY(s, hipMemsetAsync(s->d_loop_state.p, 0, 8 * sizeof(uint32_t), s->stream));
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-    HIP_TRY(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->d_ev_status_p.as<uint8_t>(),
+    HIP_TRY_STATE(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->d_ev_status_p.as<uint8_t>(),
                                 s->d_ev_score_p.as<double>(), s->stream));
     pe::PLoopArgs L;
     std::memset(&L, 0, sizeof(L));
@@ -4689,7 +4704,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         L.P.offers_out = s->d_ev_offers.as<uint32_t>();
         L.P.parts_out = s->d_ploop_parts.as<double>();
         L.P.nparts_out = s->d_ploop_nparts.as<uint8_t>();
-        HIP_TRY(s, pe_launch_evict_only(&L.P, s->stream));
+        HIP_TRY_STATE(s, pe_launch_evict_only(&L.P, s->stream));
         L.P.dep_out = nullptr;
         uint32_t flags = 0;
         HIP_TRY(s, hipMemcpyAsync(&flags, L.P.flags, sizeof(flags), hipMemcpyDeviceToHost, s->stream));
@@ -4707,6 +4722,10 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     L.limit = s->limit;
     L.count = count;
     L.retry = retry ? 1 : 0;
+    {
+        const char* cd = std::getenv("PE_PLOOP_CHECK_DEAD");
+        L.check_dead = (cd && cd[0] && cd[0] != '0') ? 1 : 0;
+    }
     L.out = s->d_loop_out.as<pe_ranked_node>();
     L.out_mask = s->d_ploop_mask.as<uint32_t>();
     L.state = s->d_loop_state.as<uint32_t>();
@@ -4716,7 +4735,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         HIP_TRY(s, hipMemsetAsync(s->d_prof.p, 0, 8 * sizeof(unsigned long long), s->stream));
         L.prof = s->d_prof.as<unsigned long long>();
     }
-    HIP_TRY(s, pe_launch_ploop(&L, s->stream));
+    HIP_TRY_STATE(s, pe_launch_ploop(&L, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     uint32_t st[4];
     HIP_TRY(s, hipMemcpyAsync(st, L.state, sizeof(st), hipMemcpyDeviceToHost, s->stream));
@@ -4764,7 +4783,9 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     if (st[2] == 1)
         return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the on-device "
                                         "alloc limits");
-    if (st[2] == 2) return s->fail(PE_EHIP, "k_ploop: the resolved winner is not an option");
+    if (st[2] == 2) return s->fail(PE_EINTERNAL, "k_ploop: the resolved winner is not an option");
+    if (st[2] == 3)
+        return s->fail(PE_EINTERNAL, "k_ploop: a plain Select skipped as provably failing found a winner");
     return PE_OK;
 }
 
@@ -4808,7 +4829,7 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         HIP_TRY(s, s->d_full_args.ensure(sizeof(pe::SweepArgs)));
         HIP_TRY(s, hipMemcpyAsync(s->d_full_args.p, &s->h_full_args, sizeof(pe::SweepArgs), hipMemcpyHostToDevice,
                                   s->stream));
-        HIP_TRY(s, pe_launch_fullpass_lds(s->d_full_args.as<pe::SweepArgs>(), A.spread_tab ? A.tg.n_psets : 0,
+        HIP_TRY_STATE(s, pe_launch_fullpass_lds(s->d_full_args.as<pe::SweepArgs>(), A.spread_tab ? A.tg.n_psets : 0,
                                           s->d_visit.as<uint32_t>(), n, count, s->d_loop_out.as<pe_ranked_node>(),
                                           state, fprof ? d_prof.as<unsigned long long>() : nullptr, s->stream));
         HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
@@ -4834,7 +4855,7 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         // the step; at most one workgroup per CU so that all are resident
         const uint32_t pb = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)s->n_cu));
         A.recs = s->d_sweep_recs.as<pe::SweepRec>();
-        HIP_TRY(s, pe_launch_sweep_loop(&A, pb, count, s->d_visit.as<uint32_t>(), n, s->offset,
+        HIP_TRY_STATE(s, pe_launch_sweep_loop(&A, pb, count, s->d_visit.as<uint32_t>(), n, s->offset,
                                         s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
         HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -4846,7 +4867,7 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     for (uint32_t k = 0; !persistent && !lds_loop && k < count && !h_state[0]; k += chunk) {
         const uint32_t m = std::min(chunk, count - k);
         for (uint32_t j = 0; j < m; j++)
-            HIP_TRY(s, pe_launch_sweep_step(&A, blocks, s->d_visit.as<uint32_t>(), n, s->offset,
+            HIP_TRY_STATE(s, pe_launch_sweep_step(&A, blocks, s->d_visit.as<uint32_t>(), n, s->offset,
                                             s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
         HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -5164,7 +5185,7 @@ static int spec_flush(pe_stack* s) {
         for (uint32_t i = sp.confirmed; i < sp.placed; i++) rows[i - sp.confirmed] = (uint32_t)spec_row(sp, i);
         HIP_TRY(s, upload_s(s, s->d_commit_rows, rows));
         HIP_TRY(s, upload_s(s, s->d_commit_offers, offers));
-        HIP_TRY(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
+        HIP_TRY_STATE(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
                                            s->d_commit_offers.as<uint32_t>(), (uint32_t)rows.size(), -1,
                                            s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -5188,11 +5209,11 @@ static int spec_flush(pe_stack* s) {
     }
     if (ordered_only) {
         for (uint32_t i = 0; i < sp.confirmed; i++)
-            HIP_TRY(s, pe_launch_commit(&soa, &t, &a, rows[i], offers[i], s->stream));
+            HIP_TRY_STATE(s, pe_launch_commit(&soa, &t, &a, rows[i], offers[i], s->stream));
     } else {
         HIP_TRY(s, upload_s(s, s->d_commit_rows, rows));
         HIP_TRY(s, upload_s(s, s->d_commit_offers, offers));
-        HIP_TRY(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
+        HIP_TRY_STATE(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
                                            s->d_commit_offers.as<uint32_t>(), sp.confirmed, 1, s->stream));
     }
     HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -5508,14 +5529,14 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
     for (uint32_t k = 0; k < count && !h_state[0]; k += chunk) {
         const uint32_t m = std::min(chunk, count - k);
         for (uint32_t j = 0; j < m; j++) {
-            HIP_TRY(s, pe_launch_sweep_only(&A, blocks, s->stream));
+            HIP_TRY_STATE(s, pe_launch_sweep_only(&A, blocks, s->stream));
             if (s->nranks > 1) {   // in place: this rank's slice already sits at its offset
                 if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x0, s->stream));
                 const ncclResult_t r = ncclAllGather(A.recs, s->d_gather.p, slice, ncclUint8, s->comm, s->stream);
                 if (r != ncclSuccess) return s->fail(PE_EHIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
                 if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x1, s->stream));
             }
-            HIP_TRY(s, pe_launch_step_only(&A2, nrecs, s->d_visit.as<uint32_t>(), n, s->offset,
+            HIP_TRY_STATE(s, pe_launch_step_only(&A2, nrecs, s->d_visit.as<uint32_t>(), n, s->offset,
                                            s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
         }
         HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
@@ -5721,8 +5742,8 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
     const pe::BatchArgs& A = s->batch_A;
     const auto t1 = std::chrono::steady_clock::now();
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-    if (s->batch_chain) HIP_TRY(s, pe_launch_chain(&A, E, s->chain_grid, s->stream));
-    else HIP_TRY(s, pe_launch_place(&A, E, s->batch_full, s->stream));
+    if (s->batch_chain) HIP_TRY_STATE(s, pe_launch_chain(&A, E, s->chain_grid, s->stream));
+    else HIP_TRY_STATE(s, pe_launch_place(&A, E, s->batch_full, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     if (!s->batch_direct) {
         HIP_TRY(s, hipMemcpyAsync(s->h_batch_status.p, A.eval_status, sizeof(uint32_t) * 2 * (size_t)E,
@@ -5827,7 +5848,7 @@ static int system_place_distinct(pe_stack* s, uint32_t tgi, TgPlan& g, double* o
         pe::NodeSoA soa = soa_of(s);
         pe::TgTables t = tables_of(g);
         pe::Ask a = ask_for(s, g);
-        HIP_TRY(s, pe_launch_commit_rows(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(), (uint32_t)accepted.size(),
+        HIP_TRY_STATE(s, pe_launch_commit_rows(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(), (uint32_t)accepted.size(),
                                          s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
         for (uint32_t r : accepted) s->plan.emplace_back(g.name, r);
@@ -5899,7 +5920,7 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
     const bool distinct = g.psets.size() > (size_t)g.n_spread;
     A.commit = distinct ? 0 : 1;
     if (distinct) A.tg.n_psets = A.tg.n_spread;
-    HIP_TRY(s, pe_launch_system(&A, s->stream));
+    HIP_TRY_STATE(s, pe_launch_system(&A, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     {
         ApiScope prof_k_(s, "system.kernel_sync");
@@ -6007,14 +6028,14 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
                 P.offers_out = s->d_ev_offers.as<uint32_t>();
                 P.flags = s->d_ev_flags.as<uint32_t>();
                 HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-                HIP_TRY(s, pe_launch_evict_only(&P, s->stream));
+                HIP_TRY_STATE(s, pe_launch_evict_only(&P, s->stream));
                 uint32_t flags = 0;
                 HIP_TRY(s, hipMemcpyAsync(&flags, P.flags, sizeof(flags), hipMemcpyDeviceToHost, s->stream));
                 HIP_TRY(s, hipStreamSynchronize(s->stream));
                 if (flags & 1u)
                     return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the "
                                                     "on-device alloc limits");
-                HIP_TRY(s, pe_launch_commit_evicted(&P, s->d_preempted.as<uint8_t>(), s->d_pcount.as<uint32_t>(),
+                HIP_TRY_STATE(s, pe_launch_commit_evicted(&P, s->d_preempted.as<uint8_t>(), s->d_pcount.as<uint32_t>(),
                                                     s->d_dev_free.as<uint32_t>(), s->d_status.as<uint32_t>(),
                                                     s->stream));
                 HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
@@ -6323,7 +6344,7 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
         for (uint32_t j = 0; j < m; j++) {
             for (uint32_t k = 0; k < N; k++) {
                 HIP_TRY(s, hipSetDevice(st[k]->device));
-                HIP_TRY(s, pe_launch_sweep_only(&A[k], blocks, strm(k)));
+                HIP_TRY_STATE(s, pe_launch_sweep_only(&A[k], blocks, strm(k)));
             }
             HIP_TRY(s, hipSetDevice(s->device));
             if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x0, s->stream));
@@ -6346,7 +6367,7 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
             if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x1, s->stream));
             for (uint32_t k = 0; k < N; k++) {
                 HIP_TRY(s, hipSetDevice(st[k]->device));
-                HIP_TRY(s, pe_launch_step_only(&A2[k], blocks * N, st[k]->d_visit.as<uint32_t>(), n, st[k]->offset,
+                HIP_TRY_STATE(s, pe_launch_step_only(&A2[k], blocks * N, st[k]->d_visit.as<uint32_t>(), n, st[k]->offset,
                                                st[k]->d_loop_out.as<pe_ranked_node>(),
                                                st[k]->d_loop_state.as<uint32_t>(), strm(k)));
             }
@@ -6440,7 +6461,7 @@ static int multi_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint
         Sa.out_status = dsys + st_off;
         Sa.placed = nullptr;   // counted from the outcomes below
         Sa.commit = 1;
-        if (m) HIP_TRY(s, pe_launch_system(&Sa, x->stream));
+        if (m) HIP_TRY_STATE(s, pe_launch_system(&Sa, x->stream));
         HIP_TRY(s, hipMemcpyAsync(x->h_sys_out.p, dsys, bytes, hipMemcpyDeviceToHost, x->stream));
     }
     std::vector<std::vector<uint32_t>> rows(N);
@@ -6471,7 +6492,7 @@ static int multi_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint
             pe::NodeSoA soa = soa_of(x);
             pe::TgTables t = tables_of(g);
             pe::Ask a = ask_for(x, g);
-            HIP_TRY(s, pe_launch_commit_rows(&soa, &t, &a, x->d_commit_rows.as<uint32_t>(), (uint32_t)others.size(),
+            HIP_TRY_STATE(s, pe_launch_commit_rows(&soa, &t, &a, x->d_commit_rows.as<uint32_t>(), (uint32_t)others.size(),
                                              x->stream));
         }
     }

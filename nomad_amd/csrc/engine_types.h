@@ -353,9 +353,12 @@ struct PLoopArgs {
     uint32_t* dev_free;
     uint32_t offset, limit, count;
     int32_t retry;                    // selectNextOption: a nil plain Select retries with Preempt
+    int32_t check_dead;               // PE_PLOOP_CHECK_DEAD: run the plain resolves the loop skips as provably
+                                      // failing anyway and stop with error 3 if one finds a winner
     pe_ranked_node* out;              // [count] records (a nil record ends the loop)
     uint32_t* out_mask;               // [count] preempted allocs of each placement (bits over the node's allocs)
-    uint32_t* state;                  // [0] placements, [1] cursor, [2] error (1: node outside the device limits), [3] records
+    uint32_t* state;                  // [0] placements, [1] cursor, [2] error (1: node outside the device limits,
+                                      // 2: winner not an option, 3: a skipped plain resolve had a winner), [3] records
     unsigned long long* prof;         // [6] or null (PE_PLACE_PROF): wall-clock ticks of the plain resolve, refresh,
                                       // Preempt resolve, winner; refreshed dirty rows, refreshed pcount readers
 };

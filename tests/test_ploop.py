@@ -109,3 +109,36 @@ def test_ploop_cluster_exhausted():
     assert dev[-1].row < 0 and 2000 < len(dev) < 20000
     assert_same_placements(dev, host)
     assert [sorted(x.preempted) for x in dev] == [sorted(x.preempted) for x in host]
+
+
+@pytest.mark.parametrize("variant", ["max_parallel", "distinct_property", "job_counts"])
+def test_ploop_skipped_plain_resolves_fail(variant, monkeypatch):
+    """k_ploop skips a plain Select after a failed one whose placement left its
+    row without a plain option. PE_PLOOP_CHECK_DEAD runs every
+    skipped resolve anyway and fails the call (PE_EINTERNAL) if one finds a
+    winner. Every GPU node is full (busy=1.0), so the plain Select stays dead
+    across all the Preempt placements, with max_parallel penalties, a
+    distinct_property constraint over a 40-rack meta key, or a job that
+    already holds allocs (job-level collision counts) in play."""
+    import random
+    nodes, allocs = synth.cluster_c5(4000, seed=29, busy=1.0)
+    rng = random.Random(3)
+    for nd in nodes:
+        nd.meta["rack"] = "r%02d" % rng.randrange(40)
+        nd.compute_class()
+    job = synth.job_c5(120)
+    if variant == "max_parallel":
+        for a in allocs:
+            a.max_parallel = 1
+    elif variant == "distinct_property":
+        from nomad_amd.structs import Constraint
+        job.task_groups[0].constraints.append(Constraint("${meta.rack}", "3", "distinct_property"))
+    else:
+        gpu = [nd for nd in nodes if nd.devices][:30]
+        for nd in gpu:
+            allocs.append(Allocation(node_id=nd.id, job_id=job.id, task_group="infer", cpu_shares=100,
+                                     memory_mb=64, disk_mb=10, priority=80))
+    perm = synth.shuffle(len(nodes), 6)
+    monkeypatch.setenv("PE_PLOOP_CHECK_DEAD", "1")
+    re, _ = _run_both(nodes, allocs, job, perm, SchedulerConfig(preempt_service=True))
+    assert sum(1 for x in re if x.preempted) > 20

@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round-4 GPU pass: the -m gpu suite, the default bench line, then rocprofv3
+# kernel stats of the headline loop (with its device timeline), of the 2^24-node
+# scoring sweep and of the C5 loop. Every GPU step has its own time limit; the
+# script stops at the first failure. Outputs in gpurun_out/<tag>/ (copied into
+# profiles/r04/ by hand afterwards). SKIP_TESTS=1 skips the suite.
+set -eo pipefail
+TAG=${1:-r04p}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations 20 \
+    > "$OUT/gpu_pytest.log" 2>&1 || { tail -60 "$OUT/gpu_pytest.log"; exit 1; }
+  tail -1 "$OUT/gpu_pytest.log"
+fi
+timeout -k 10 500 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
+python3 -c "import json;d=json.load(open('$OUT/bench.json'));r=d['roofline'];print('value %.4g' % d['value'], 'us/eval %.1f' % (d['ms_per_step']*1e3), 'cpu', d['cpu_baseline']['value'], 'frac', r['frac'], 'traffic', r['traffic']); print(' '.join('%s %.4g' % (k, v.get('placements_per_s', v.get('nodes_per_s', 0))) for k, v in d['configs'].items() if isinstance(v, dict)))"
+cd /tmp
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
+  python3 "$ROOT/bench.py" --no-cpu --steps 10 --warmup 2 --sweep-nodes 0 --sections "" > "$OUT/trace.log" 2>&1
+T=$(find "$OUT/trace" -name "*kernel_trace.csv" -print -quit)
+python3 "$ROOT/tools/timeline.py" "$T" k_emit_writeback 3 > "$OUT/headline_timeline.txt" || true
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/sweep" -o sweep -- \
+  python3 "$ROOT/tools/sweep_variants.py" 16777216 0 0 > "$OUT/sweep.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5" -o c5 -- \
+  python3 "$ROOT/tools/c5_prof.py" > "$OUT/c5.log" 2>&1
+cat "$OUT/sweep.log" "$OUT/c5.log" | tail -20
+find "$OUT" -name "*kernel_stats.csv" | sort
