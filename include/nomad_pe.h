@@ -31,10 +31,11 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 5u
+#define PE_ABI_VERSION 6u
 #define PE_NONE 0xFFFFFFFFu
 #define PE_MAX_SCORES 8
-#define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried per RankedNode */
+#define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried inline per RankedNode (the
+                               full list of a longer one: pe_preempted_of) */
 #define PE_MAX_DEVICE_REQ 4 /* device requests of a task group on the device path */
 #define PE_MAX_DEVICES 8    /* GPUs one handle drives (pe_config.device_ids) */
 
@@ -276,7 +277,8 @@ typedef struct pe_ranked_node {                 /* RankedNode, rank.go:21-36 */
     /* AllocMetric side outputs (structs.go:9826-10026) */
     uint32_t nodes_evaluated, nodes_filtered, nodes_exhausted;
     uint32_t new_offset;      /* StaticIterator cursor after the Select */
-    /* PreemptedAllocs (rank.go:511-513): rows of the pe_alloc_table snapshot */
+    /* PreemptedAllocs (rank.go:511-513): rows of the pe_alloc_table snapshot;
+       n_preempted is the whole count, the first PE_MAX_PREEMPT are inline */
     uint32_t n_preempted;
     uint32_t preempted[PE_MAX_PREEMPT];
     /* TaskResources device offers (rank.go:404-405): per device request of the
@@ -385,6 +387,15 @@ int pe_speculation_stats(const pe_stack* s, uint64_t* out4);
  * rows, as returned in pe_ranked_node.preempted by a Select with Preempt. */
 int pe_commit_preempt(pe_stack* s, uint32_t tg_index, int32_t row, const uint32_t* preempted,
                       uint32_t n_preempted);
+/* The full PreemptedAllocs of record `record` of the last pe_select (record 0)
+ * or pe_place (record k) when it holds more than PE_MAX_PREEMPT (rank.go:511-513
+ * has no cap): writes min(cap, n) alloc-table rows, the first PE_MAX_PREEMPT
+ * equal to the inline ones, and returns n; PE_ESTATE when that record carries
+ * its whole list inline. Valid until the next pe_select / pe_place /
+ * pe_system_place. The Go shim calls it when n_preempted > PE_MAX_PREEMPT,
+ * before pe_commit_preempt(row, list, n). Replaces reading
+ * RankedNode.PreemptedAllocs past the inline array (rank.go:511-513). */
+int pe_preempted_of(const pe_stack* s, uint32_t record, uint32_t* out, uint32_t cap);
 /* Plan.AppendStoppedAlloc (structs.go:10628-10660) of `n` snapshot allocs
  * (alloc-table rows): each becomes a NodeUpdate entry of its node, and a
  * non-terminal one leaves the proposed state of the node

@@ -206,6 +206,7 @@ def _sigs(prefix, handle):
                                       C.POINTER(pe_ranked_node)]),
         (prefix + "commit", C.c_int, [H, C.c_uint32, C.c_int32]),
         (prefix + "commit_preempt", C.c_int, [H, C.c_uint32, C.c_int32, u32p, C.c_uint32]),
+        (prefix + "preempted_of", C.c_int, [H, C.c_uint32, u32p, C.c_uint32]),
         (prefix + "plan_stop", C.c_int, [H, u32p, C.c_uint32]),
         (prefix + "plan_pop_update", C.c_int, [H, C.c_uint32]),
         (prefix + "place", C.c_int, [H, C.c_uint32, C.c_uint32, C.POINTER(pe_ranked_node), u32p]),
@@ -226,7 +227,7 @@ ENGINE_SYMBOLS = [
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
     "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
-    "pe_last_kernel_split",
+    "pe_last_kernel_split", "pe_preempted_of",
 ]
 
 

@@ -66,7 +66,7 @@ hipError_t pe_launch_apply_commits(const pe::NodeSoA* s, const pe::TgTables* t, 
                                    const uint32_t* offers, uint32_t n, int sign, hipStream_t st);
 hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ranked_node* out, uint32_t* mask,
                                   hipStream_t st);
-hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
+hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, const uint32_t* mask, uint8_t* preempted,
                                     uint32_t* pcount, uint32_t* dev_free, hipStream_t st);
 hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st);
 hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* status, double* score,
@@ -411,6 +411,12 @@ struct pe_stack {
     std::map<std::pair<uint32_t, uint32_t>, uint32_t> job_keys;   // (job, ns) -> key
     uint32_t n_jtg_keys = 0;
     std::string preempt_unsupported;           // snapshot outside the on-device limits
+    // eviction width of the snapshot (PreemptArgs::mask_words, evict.inc): 1
+    // while every node holds <= 32 non-terminal allocs, else 8 (<= 256)
+    uint32_t evict_words = 1;
+    // PreemptedAllocs past the PE_MAX_PREEMPT a record carries inline, of the
+    // last record-producing call: (record index, the full list)
+    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> pre_overflow;
     // reserved cores (rank.go:437-466): 4 x u64 masks per node over core ids < 256
     bool has_cores = false;                    // some node has ReservableCpuCores / ReservedCpuCores
     std::string cores_tg_unsupported;          // why task groups asking cores stay on the host path
@@ -550,7 +556,8 @@ struct pe_stack {
     uint64_t test_fallback_every = 0, test_select_calls = 0;   // PE_TEST_FALLBACK_EVERY
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
-    DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;  // device-resident parallel count loop (k_ploop)
+    DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;
+    DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)  // device-resident parallel count loop (k_ploop)
     DevMem d_ploop_parts, d_ploop_nparts;   // k_ploop: Preempt records per position (parts, count)
 
     // Speculative count loop behind pe_select / pe_commit: the
@@ -1634,11 +1641,13 @@ int build_alloc_state(pe_stack* s) {
         s->h_palloc_index.assign(m, 0);
         s->alloc_slot.assign(s->allocs.size(), PE_NONE);
         std::vector<uint32_t> fill(s->h_node_alloc_off.begin(), s->h_node_alloc_off.end() - 1);
+        uint32_t max_m = 0;
+        for (uint32_t i = 0; i < n; i++) max_m = std::max(max_m, cnt[i + 1]);
+        s->evict_words = max_m <= 32u ? 1u : 8u;
+        if (max_m > pe::kEvictMaxAllocs) s->preempt_unsupported = "more than 256 allocs on a node";
         for (uint32_t i = 0; i < s->allocs.size(); i++) {
             const HostAlloc& a = s->allocs[i];
             if (a.terminal) continue;
-            if (cnt[a.row + 1] > (uint32_t)pe::kMaxNodeAllocs)
-                s->preempt_unsupported = "more than 32 allocs on a node";
             const uint32_t slot = fill[a.row]++;
             s->h_palloc_index[slot] = i;
             s->alloc_slot[i] = slot;
@@ -1899,7 +1908,9 @@ static void port_step(pe_stack* s, const TgPlan& g, uint32_t row, bool own_place
     *blockers = 0;
     const auto& ports = g.rports.empty() ? g.trports : g.rports;
     const uint32_t b = s->h_node_alloc_off[row], e = s->h_node_alloc_off[row + 1];
-    if (e - b > (uint32_t)pe::kMaxNodeAllocs) return;   // the device refuses the node itself
+    // the holder list and blocker bits index the node's first 32 allocs: a
+    // wider node's reserved-port preemption stays on the host path
+    if (e - b > (uint32_t)pe::kMaxNodeAllocs) { *info = pe::kPortUnsup; return; }
     std::map<int32_t, uint32_t> holder;
     std::set<int32_t> filtered;
     for (uint32_t k = b; k < e; k++) {
@@ -2839,7 +2850,53 @@ pe::PreemptArgs preempt_args(pe_stack* s, TgPlan& g) {
     P.log10 = s->log10;
     P.score_preemption = s->cfg.stack_kind == PE_STACK_GENERIC ? 1 : 0;
     P.palloc_cores = s->has_cores ? s->d_palloc_cores.as<uint64_t>() : nullptr;
+    P.mask_words = s->evict_words;
     return P;
+}
+
+// The next wider eviction width after a launch flagged kEvictWider (a node's
+// ProposedAllocs outgrew it), or 0 when none is left.
+static uint32_t wider_words(uint32_t w) {
+    for (uint32_t x : pe::kEvictWidths)
+        if (x > w) return x;
+    return 0;
+}
+
+// Record `o`'s PreemptedAllocs from the preempted set of its node (`mask`, W
+// words over the node's CSR slots): inline up to PE_MAX_PREEMPT, the full
+// list kept under record index `rec` beyond that (pe_preempted_of). With
+// `commit` the allocs also join the host mirror of Plan.NodePreemptions (the
+// device loop already applied them).
+static void set_preempted(pe_stack* s, pe_ranked_node& o, uint32_t rec, uint32_t row, const uint32_t* mask,
+                          uint32_t words, bool commit) {
+    const uint32_t b = s->h_node_alloc_off[row], m = s->h_node_alloc_off[row + 1] - b;
+    o.n_preempted = 0;
+    std::vector<uint32_t> full;
+    for (uint32_t i = 0; i < m && i < 32u * words; i++) {
+        if (!((mask[i >> 5] >> (i & 31u)) & 1u)) continue;
+        const uint32_t a = s->h_palloc_index[b + i];
+        if (o.n_preempted < PE_MAX_PREEMPT) o.preempted[o.n_preempted] = a;
+        o.n_preempted++;
+        full.push_back(a);
+        if (commit) {
+            s->h_preempted[b + i] = 1;
+            core_hold(s, a, false);
+            invalidate_static(s);
+        }
+    }
+    if (o.n_preempted > PE_MAX_PREEMPT) {
+        for (auto& e : s->pre_overflow)
+            if (e.first == rec) { e.second = std::move(full); return; }
+        s->pre_overflow.emplace_back(rec, std::move(full));
+    }
+}
+
+// The full PreemptedAllocs of record `rec` of the current call.
+static const uint32_t* preempted_list(const pe_stack* s, uint32_t rec, const pe_ranked_node& o) {
+    if (o.n_preempted <= PE_MAX_PREEMPT) return o.preempted;
+    for (auto& e : s->pre_overflow)
+        if (e.first == rec && e.second.size() == o.n_preempted) return e.second.data();
+    return nullptr;
 }
 
 int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* new_offset) {
@@ -2855,7 +2912,7 @@ int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* n
     HIP_TRY(s, s->d_ev_status.ensure(n));
     HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * n));
     HIP_TRY(s, s->d_ev_out.ensure(16));
-    HIP_TRY(s, s->d_ev_mask.ensure(16));
+    HIP_TRY(s, s->d_ev_mask.ensure(sizeof(uint32_t) * (pe::kEvictWidths[1] + 1)));
     HIP_TRY(s, s->d_ev_flags.ensure(16));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
@@ -2905,7 +2962,8 @@ int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* n
 // over `order` from cursor `offset`: every position evaluated in parallel, then
 // the LimitIterator window resolved on the device.
 int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t offset,
-                     const pe_select_options* opts, pe_ranked_node* out, uint32_t* new_offset) {
+                     const pe_select_options* opts, pe_ranked_node* out, uint32_t* new_offset, uint32_t rec = 0,
+                     uint32_t words = 0) {
     std::memset(out, 0, sizeof(*out));
     out->row = -1;
     const uint32_t n = (uint32_t)order.size();
@@ -2914,6 +2972,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     if (g.ask.cores > 0) return s->fail(PE_EUNSUPPORTED, "reserved cores with preemption");
     if (n == 0) return PE_OK;
     pe::PreemptArgs P = preempt_args(s, g);
+    if (words) P.mask_words = words;
     HIP_TRY(s, upload_visit(s, order));
     P.visit = s->d_visit.as<uint32_t>();
     P.n_visit = n;
@@ -2935,7 +2994,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * n));
     HIP_TRY(s, s->d_ev_flags.ensure(16));
     HIP_TRY(s, s->d_ev_out.ensure(16));
-    HIP_TRY(s, s->d_ev_mask.ensure(16));
+    HIP_TRY(s, s->d_ev_mask.ensure(sizeof(uint32_t) * (pe::kEvictWidths[1] + 1)));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
     P.status = s->d_ev_status.as<uint8_t>();
@@ -2960,9 +3019,14 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
     s->last_ms_pending = false;
-    if (flags & 1u)
-        return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the on-device "
-                                        "alloc limits");
+    if (flags & pe::kEvictUnsup)
+        return s->fail(PE_EUNSUPPORTED, "preemption: a node outside the device path (several network devices, "
+                                        "static ports on a node of more than 32 allocs, reserved cores)");
+    if (flags & pe::kEvictWider) {   // a node's ProposedAllocs outgrew the width: the same Select wider
+        const uint32_t w = wider_words(P.mask_words);
+        if (!w) return s->fail(PE_EUNSUPPORTED, "preemption: a node's proposed allocs exceed the widest eviction width");
+        return run_evict_select(s, g, order, offset, opts, out, new_offset, rec, w);
+    }
     const uint32_t consumed = (uint32_t)res[1];
     out->nodes_evaluated = consumed;
     out->nodes_filtered = (uint32_t)res[2];
@@ -2974,9 +3038,10 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
         HIP_TRY_STATE(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
                                           s->stream));
         pe_ranked_node rr;
-        uint32_t mask = 0;
+        uint32_t mask[pe::kEvictWidths[1] + 1];
         HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(s, hipMemcpyAsync(&mask, s->d_ev_mask.p, sizeof(mask), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(mask, s->d_ev_mask.p, sizeof(uint32_t) * (P.mask_words + 1), hipMemcpyDeviceToHost,
+                                  s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
         out->row = (int32_t)row;
         out->final_score = rr.final_score;
@@ -2984,12 +3049,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
         std::memcpy(out->scores, rr.scores, sizeof(out->scores));
         out->n_device_offers = rr.n_device_offers;
         std::memcpy(out->device_offer_group, rr.device_offer_group, sizeof(out->device_offer_group));
-        const uint32_t b = s->h_node_alloc_off[row];
-        for (uint32_t i = 0; i < 32; i++)
-            if ((mask >> i) & 1u) {
-                if (out->n_preempted >= PE_MAX_PREEMPT) return s->fail(PE_EUNSUPPORTED, "more than PE_MAX_PREEMPT preempted allocs");
-                out->preempted[out->n_preempted++] = s->h_palloc_index[b + i];
-            }
+        set_preempted(s, *out, rec, row, mask, P.mask_words, false);
     }
     return PE_OK;
 }
@@ -3978,7 +4038,8 @@ static uint32_t pack_offers(const pe_ranked_node* out) {
     return w;
 }
 
-static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out);
+static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out,
+                       uint32_t rec = 0);
 
 // AllocMetric maps of one plain Select (structs.go:9903-9937): the rows the
 // chain pulled (visit order from the Select's cursor), FeasibilityWrapper
@@ -4135,14 +4196,25 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             }
             HIP_TRY(s, s->d_ev_tcodes.ensure(rows.size() * sizeof(uint32_t)));
             HIP_TRY(s, s->d_ev_named.ensure(rows.size() * 7 * sizeof(double)));
-            HIP_TRY_STATE(s, pe_launch_evict_trace(&P, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
-                                             s->d_ev_tcodes.as<uint32_t>(), s->d_ev_named.as<double>(), s->stream));
             ecodes.resize(rows.size());
             named.resize(rows.size() * 7);
-            HIP_TRY(s, hipMemcpyAsync(ecodes.data(), s->d_ev_tcodes.p, ecodes.size() * 4, hipMemcpyDeviceToHost,
-                                      s->stream));
-            HIP_TRY(s, hipMemcpyAsync(named.data(), s->d_ev_named.p, named.size() * 8, hipMemcpyDeviceToHost,
-                                      s->stream));
+            for (;;) {   // a row wider than the launch: the trace again, wider
+                HIP_TRY_STATE(s, pe_launch_evict_trace(&P, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
+                                                       s->d_ev_tcodes.as<uint32_t>(), s->d_ev_named.as<double>(),
+                                                       s->stream));
+                HIP_TRY(s, hipMemcpyAsync(ecodes.data(), s->d_ev_tcodes.p, ecodes.size() * 4, hipMemcpyDeviceToHost,
+                                          s->stream));
+                HIP_TRY(s, hipMemcpyAsync(named.data(), s->d_ev_named.p, named.size() * 8, hipMemcpyDeviceToHost,
+                                          s->stream));
+                HIP_TRY(s, hipStreamSynchronize(s->stream));
+                bool wider = false;
+                for (uint32_t ec : ecodes) wider = wider || (((ec >> 24) & pe::kEvictWider) != 0u);
+                if (!wider) break;
+                P.mask_words = wider_words(P.mask_words);
+                if (!P.mask_words)
+                    return s->fail(PE_EUNSUPPORTED, "preemption: a node's proposed allocs exceed the widest eviction "
+                                                    "width");
+            }
         }
         HIP_TRY(s, hipStreamSynchronize(s->stream));
         const bool has_aff = !g.affinities.empty();
@@ -4153,8 +4225,8 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             const uint32_t base = code & 255u;
             if (evict && base != pe::kTrDistinctHosts && base != pe::kTrDistinctProp) {
                 const uint32_t ec = ecodes[i], st = ec & 255u;
-                if (ec >> 24) return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or "
-                                                              "exceeds the on-device alloc limits");
+                if (ec >> 24) return s->fail(PE_EUNSUPPORTED, "preemption: a node outside the device path (several "
+                                                              "network devices, reserved cores)");
                 if (st == 0) {   // option (kOption), preempting or not
                     const double* o = &named[i * 7];
                     const uint32_t fl = (ec >> 16) & 255u;
@@ -4409,6 +4481,7 @@ static bool sys_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, 
 int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
     PE_FLUSH_RESET(s);
     if (!s || !out) return PE_EINVAL;
+    s->pre_overflow.clear();
     int rc = PE_OK;
     if (s->cfg.stack_kind == PE_STACK_SYSTEM && !s->test_fallback_every && sys_serve(s, tgi, opts, out, &rc))
         return rc;
@@ -4432,7 +4505,8 @@ int pe_select(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranke
     return rc;
 }
 
-static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
+// `rec`: the record's index in the call's output (PreemptedAllocs overflow).
+static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out, uint32_t rec) {
     if (!s || !out) return PE_EINVAL;
     s->gen++;
     s->metrics_valid = false;
@@ -4445,7 +4519,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         uint32_t placed, no;
         const uint32_t saved = s->limit;
         s->limit = 1;
-        if (s->cfg.preempt) rc = run_evict_select(s, *s->tgs[tgi], s->visit, 0, nullptr, out, &no);
+        if (s->cfg.preempt) rc = run_evict_select(s, *s->tgs[tgi], s->visit, 0, nullptr, out, &no, rec);
         else rc = run_place(s, tgi, 1, 0, s->visit, 0, nullptr, out, &placed, &no);
         s->limit = saved;
         if (rc == PE_OK) elig_log_span(s, tgi, 0, out->nodes_evaluated);
@@ -4467,7 +4541,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         pe_select_options o2 = *opts;
         o2.preferred_count = 0;
         uint32_t placed, no;
-        if (opts->preempt) rc = run_evict_select(s, g, pref, 0, &o2, out, &no);
+        if (opts->preempt) rc = run_evict_select(s, g, pref, 0, &o2, out, &no, rec);
         else rc = run_place(s, tgi, 1, 0, pref, 0, &o2, out, &placed, &no);
         if (rc) return rc;
         elig_visit_list(s, tgi, pref, out->nodes_evaluated);
@@ -4480,7 +4554,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         s->offset = 0;
         invalidate_tables(s);
         if (out->row >= 0) return PE_OK;
-        return select_impl(s, tgi, &o2, out);
+        return select_impl(s, tgi, &o2, out, rec);
     }
     int rc = prepare_tg(s, tgi, s->visit, s->offset);
     if (rc) return rc;
@@ -4489,7 +4563,7 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     if (opts && opts->preempt) {
         uint32_t no;
         const uint32_t start0 = s->offset;
-        rc = run_evict_select(s, g, s->visit, s->offset, opts, out, &no);
+        rc = run_evict_select(s, g, s->visit, s->offset, opts, out, &no, rec);
         if (rc) return rc;
         s->offset = no;
         elig_log_span(s, tgi, start0, out->nodes_evaluated);
@@ -4622,19 +4696,24 @@ static int commit_preempt_impl(pe_stack* s, uint32_t tgi, int32_t row, const uin
         return s->fail(PE_EINVAL, "bad commit");
     if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
     // Plan.AppendPreemptedAlloc (structs.go:10664-10680) of allocs on the chosen node
-    uint32_t mask = 0;
+    const uint32_t words = s->evict_words;
+    std::vector<uint32_t> mask(words, 0u);
     const uint32_t b = s->h_node_alloc_off[(uint32_t)row];
     for (uint32_t i = 0; i < n_preempted; i++) {
         const uint32_t a = preempted[i];
         if (a >= s->allocs.size() || s->alloc_slot[a] == PE_NONE || s->allocs[a].row != (uint32_t)row)
             return s->fail(PE_EINVAL, "preempted alloc is not a live alloc of the node");
-        mask |= 1u << (s->alloc_slot[a] - b);
+        const uint32_t k = s->alloc_slot[a] - b;
+        if (k >= 32u * words) return s->fail(PE_EINTERNAL, "preempted alloc past the eviction width");
+        mask[k >> 5] |= 1u << (k & 31u);
     }
     HIP_TRY(s, hipSetDevice(s->device));
     TgPlan& g = *s->tgs[tgi];
     pe::PreemptArgs P = preempt_args(s, g);
-    HIP_TRY_STATE(s, pe_launch_commit_preempt(&P, (uint32_t)row, mask, s->d_preempted.as<uint8_t>(),
-                                        s->d_pcount.as<uint32_t>(), s->d_dev_free.as<uint32_t>(), s->stream));
+    HIP_TRY(s, upload_s(s, s->d_pre_mask, mask));
+    HIP_TRY_STATE(s, pe_launch_commit_preempt(&P, (uint32_t)row, s->d_pre_mask.as<uint32_t>(),
+                                              s->d_preempted.as<uint8_t>(), s->d_pcount.as<uint32_t>(),
+                                              s->d_dev_free.as<uint32_t>(), s->stream));
     for (uint32_t i = 0; i < n_preempted; i++) {
         s->h_preempted[s->alloc_slot[preempted[i]]] = 1;
         invalidate_static(s);
@@ -4651,8 +4730,12 @@ static int commit_preempt_impl(pe_stack* s, uint32_t tgi, int32_t row, const uin
 // list without repeated rows, no max_parallel penalty (the plan's preemption
 // counts would reach other nodes' eviction choices). *handled = false leaves
 // the loop to the host-driven path (nothing committed).
+// `rec0`: index of out[0] in the call's records; `words`: eviction width
+// (0: the snapshot's). A launch that meets a node wider than its width stops
+// there (the placements before it are committed) and the rest reruns wider.
 static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count, bool retry,
-                            pe_ranked_node* out, uint32_t* placed, bool* handled) {
+                            pe_ranked_node* out, uint32_t* placed, bool* handled, uint32_t rec0 = 0,
+                            uint32_t words = 0) {
     *handled = false;
     *placed = 0;
     const uint32_t n = (uint32_t)s->visit.size();
@@ -4673,8 +4756,9 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * n));
     HIP_TRY(s, s->d_ev_out.ensure(16));
     HIP_TRY(s, s->d_ev_flags.ensure(16));
+    if (!words) words = s->evict_words;
     HIP_TRY(s, s->d_loop_out.ensure(sizeof(pe_ranked_node) * (size_t)count));
-    HIP_TRY(s, s->d_ploop_mask.ensure(sizeof(uint32_t) * (size_t)count));
+    HIP_TRY(s, s->d_ploop_mask.ensure(sizeof(uint32_t) * words * (size_t)count));
     HIP_TRY(s, s->d_loop_state.ensure(8 * sizeof(uint32_t)));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
@@ -4685,6 +4769,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     pe::PLoopArgs L;
     std::memset(&L, 0, sizeof(L));
     L.P = preempt_args(s, g);
+    L.P.mask_words = words;
     L.P.visit = s->d_visit.as<uint32_t>();
     L.P.n_visit = n;
     L.P.status = s->d_ev_status.as<uint8_t>();
@@ -4696,7 +4781,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         L.dep_init = L.P.dep_out;
         // the Preempt record of every position is kept (and refreshed with its
         // outcome): a Preempt winner's record is then read, not re-evaluated
-        HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * (size_t)n));
+        HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * words * (size_t)n));
         HIP_TRY(s, s->d_ev_offers.ensure(sizeof(uint32_t) * (size_t)n));
         HIP_TRY(s, s->d_ploop_parts.ensure(sizeof(double) * PE_MAX_SCORES * (size_t)n));
         HIP_TRY(s, s->d_ploop_nparts.ensure(n));
@@ -4709,7 +4794,12 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         uint32_t flags = 0;
         HIP_TRY(s, hipMemcpyAsync(&flags, L.P.flags, sizeof(flags), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
-        if (flags & 1u) return PE_OK;   // a node outside the device limits: the host path reports it when reached
+        if (flags & pe::kEvictUnsup) return PE_OK;   // outside the device path: the host loop reports it when reached
+        if (flags & pe::kEvictWider) {   // nothing committed yet: the whole loop wider
+            const uint32_t w = wider_words(words);
+            if (!w) return PE_OK;
+            return ploop_count_loop(s, g, tgi, count, retry, out, placed, handled, rec0, w);
+        }
     } else {
         HIP_TRY(s, hipMemsetAsync(L.P.status, 3, n, s->stream));
     }
@@ -4741,10 +4831,10 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, hipMemcpyAsync(st, L.state, sizeof(st), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     const uint32_t recs = std::min(st[3], count);
-    std::vector<uint32_t> masks(recs);
+    std::vector<uint32_t> masks((size_t)recs * words);
     if (recs) {
         HIP_TRY(s, hipMemcpyAsync(out, L.out, sizeof(pe_ranked_node) * recs, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(s, hipMemcpyAsync(masks.data(), L.out_mask, sizeof(uint32_t) * recs, hipMemcpyDeviceToHost,
+        HIP_TRY(s, hipMemcpyAsync(masks.data(), L.out_mask, sizeof(uint32_t) * words * recs, hipMemcpyDeviceToHost,
                                   s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
     }
@@ -4767,22 +4857,24 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     for (uint32_t k = 0; k < p; k++) {
         const uint32_t row = (uint32_t)out[k].row;
         s->plan.emplace_back(g.name, row);
-        const uint32_t b = s->h_node_alloc_off[row];
-        for (uint32_t i = 0; i < 32; i++)
-            if ((masks[k] >> i) & 1u) {
-                if (out[k].n_preempted >= PE_MAX_PREEMPT)
-                    return s->fail(PE_EUNSUPPORTED, "more than PE_MAX_PREEMPT preempted allocs");
-                out[k].preempted[out[k].n_preempted++] = s->h_palloc_index[b + i];
-                s->h_preempted[b + i] = 1;
-                core_hold(s, s->h_palloc_index[b + i], false);
-                invalidate_static(s);
-            }
+        set_preempted(s, out[k], rec0 + k, row, masks.data() + (size_t)k * words, words, true);
     }
     *placed = p;
     s->offset = st[1];
+    if (st[2] == 4) {   // a node wider than this launch: the remaining placements wider
+        const uint32_t w = wider_words(words);
+        if (!w) return s->fail(PE_EUNSUPPORTED, "preemption: a node's proposed allocs exceed the widest eviction width");
+        uint32_t p2 = 0;
+        bool h2 = false;
+        const int rc = ploop_count_loop(s, g, tgi, count - p, retry, out + p, &p2, &h2, rec0 + p, w);
+        *placed = p + p2;
+        if (rc) return rc;
+        *handled = h2;   // not handled: the host loop continues from *placed
+        return PE_OK;
+    }
     if (st[2] == 1)
-        return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the on-device "
-                                        "alloc limits");
+        return s->fail(PE_EUNSUPPORTED, "preemption: a node outside the device path (several network devices, "
+                                        "reserved cores)");
     if (st[2] == 2) return s->fail(PE_EINTERNAL, "k_ploop: the resolved winner is not an option");
     if (st[2] == 3)
         return s->fail(PE_EINTERNAL, "k_ploop: a plain Select skipped as provably failing found a winner");
@@ -4931,19 +5023,19 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
         // plan stops clear property values: one Select at a time, the counts
         // rebuilt on the host after every commit
         while (p < count) {
-            rc = select_impl(s, tgi, nullptr, &out[p]);
+            rc = select_impl(s, tgi, nullptr, &out[p], p);
             if (rc) return rc;
             if (out[p].row < 0) {
                 if (!retry) break;
                 pe_select_options o;   // selectNextOption: retry with Preempt=true
                 std::memset(&o, 0, sizeof(o));
                 o.preempt = 1;
-                rc = select_impl(s, tgi, &o, &out[p]);
+                rc = select_impl(s, tgi, &o, &out[p], p);
                 if (rc) return rc;
                 if (out[p].row < 0) break;
                 s->offer_row = out[p].row;
                 s->offers = pack_offers(&out[p]);
-                rc = commit_preempt_impl(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
+                rc = commit_preempt_impl(s, tgi, out[p].row, preempted_list(s, p, out[p]), out[p].n_preempted);
                 if (rc) return rc;
                 p++;
                 continue;
@@ -4992,13 +5084,13 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
             pe_select_options o;   // selectNextOption: retry with Preempt=true
             std::memset(&o, 0, sizeof(o));
             o.preempt = 1;
-            rc = run_evict_select(s, g, s->visit, s->offset, &o, &out[p], &no);
+            rc = run_evict_select(s, g, s->visit, s->offset, &o, &out[p], &no, p);
             if (rc) return rc;
             s->offset = no;
             if (out[p].row < 0) break;
             s->offer_row = out[p].row;
             s->offers = pack_offers(&out[p]);
-            rc = commit_preempt_impl(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
+            rc = commit_preempt_impl(s, tgi, out[p].row, preempted_list(s, p, out[p]), out[p].n_preempted);
             if (rc) return rc;
             if (has_static(g)) {   // the evictions freed ports: the gates and port records again
                 rc = prepare_tg(s, tgi, s->visit, s->offset);
@@ -5037,13 +5129,13 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
             pe_select_options o;
             std::memset(&o, 0, sizeof(o));
             o.preempt = 1;
-            rc = run_evict_select(s, g, s->visit, s->offset, &o, &out[p], &no);
+            rc = run_evict_select(s, g, s->visit, s->offset, &o, &out[p], &no, p);
             if (rc) return rc;
             s->offset = no;
             if (out[p].row < 0) break;
             s->offer_row = out[p].row;
             s->offers = pack_offers(&out[p]);
-            rc = commit_preempt_impl(s, tgi, out[p].row, out[p].preempted, out[p].n_preempted);
+            rc = commit_preempt_impl(s, tgi, out[p].row, preempted_list(s, p, out[p]), out[p].n_preempted);
             if (rc) return rc;
             if (has_static(g)) {   // the evictions freed ports: the gates and port records again
                 rc = prepare_tg(s, tgi, s->visit, s->offset);
@@ -5831,7 +5923,7 @@ static int system_place_distinct(pe_stack* s, uint32_t tgi, TgPlan& g, double* o
             if (rc || r.row < 0) continue;
             s->offer_row = r.row;
             s->offers = pack_offers(&r);
-            rc = commit_preempt_impl(s, tgi, r.row, r.preempted, r.n_preempted);
+            rc = commit_preempt_impl(s, tgi, r.row, preempted_list(s, 0, r), r.n_preempted);
             if (rc) continue;
             out_status[i] = 0;
             out_score[i] = r.final_score;
@@ -6001,7 +6093,7 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
                     if (r.row < 0) continue;
                     s->offer_row = r.row;
                     s->offers = pack_offers(&r);
-                    rc = commit_preempt_impl(s, tgi, r.row, r.preempted, r.n_preempted);
+                    rc = commit_preempt_impl(s, tgi, r.row, preempted_list(s, 0, r), r.n_preempted);
                     if (rc) { s->limit = saved; return rc; }
                     out_status[pos[k]] = 0;
                     out_score[pos[k]] = r.final_score;
@@ -6011,10 +6103,11 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
             } else {
                 const uint32_t E = (uint32_t)rows.size();
                 pe::PreemptArgs P = preempt_args(s, g);
+                const uint32_t W8 = pe::kEvictWidths[1];
                 HIP_TRY(s, upload_s(s, s->d_ev_rows, rows));
                 HIP_TRY(s, s->d_ev_status.ensure(E));
                 HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * E));
-                HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * E));
+                HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * W8 * E));
                 HIP_TRY(s, s->d_ev_offers.ensure(sizeof(uint32_t) * E));
                 HIP_TRY(s, s->d_ev_flags.ensure(16));
                 HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
@@ -6028,23 +6121,33 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
                 P.offers_out = s->d_ev_offers.as<uint32_t>();
                 P.flags = s->d_ev_flags.as<uint32_t>();
                 HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
-                HIP_TRY_STATE(s, pe_launch_evict_only(&P, s->stream));
                 uint32_t flags = 0;
-                HIP_TRY(s, hipMemcpyAsync(&flags, P.flags, sizeof(flags), hipMemcpyDeviceToHost, s->stream));
-                HIP_TRY(s, hipStreamSynchronize(s->stream));
-                if (flags & 1u)
-                    return s->fail(PE_EUNSUPPORTED, "preemption: a node needs network preemption or exceeds the "
-                                                    "on-device alloc limits");
+                for (;;) {   // nothing is committed before the launch that covers every node
+                    HIP_TRY_STATE(s, pe_launch_evict_only(&P, s->stream));
+                    HIP_TRY(s, hipMemcpyAsync(&flags, P.flags, sizeof(flags), hipMemcpyDeviceToHost, s->stream));
+                    HIP_TRY(s, hipStreamSynchronize(s->stream));
+                    if ((flags & pe::kEvictUnsup) || !(flags & pe::kEvictWider)) break;
+                    P.mask_words = wider_words(P.mask_words);
+                    if (!P.mask_words) break;
+                    HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
+                }
+                if (flags & pe::kEvictUnsup)
+                    return s->fail(PE_EUNSUPPORTED, "preemption: a node outside the device path (several network "
+                                                    "devices, reserved cores)");
+                if (!P.mask_words)
+                    return s->fail(PE_EUNSUPPORTED, "preemption: a node's proposed allocs exceed the widest eviction "
+                                                    "width");
                 HIP_TRY_STATE(s, pe_launch_commit_evicted(&P, s->d_preempted.as<uint8_t>(), s->d_pcount.as<uint32_t>(),
                                                     s->d_dev_free.as<uint32_t>(), s->d_status.as<uint32_t>(),
                                                     s->stream));
                 HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
                 std::vector<uint8_t> st(E);
                 std::vector<double> sc(E);
-                std::vector<uint32_t> masks(E);
+                const uint32_t W = P.mask_words;
+                std::vector<uint32_t> masks((size_t)W * E);
                 HIP_TRY(s, hipMemcpyAsync(st.data(), P.status, E, hipMemcpyDeviceToHost, s->stream));
                 HIP_TRY(s, hipMemcpyAsync(sc.data(), P.score, sizeof(double) * E, hipMemcpyDeviceToHost, s->stream));
-                HIP_TRY(s, hipMemcpyAsync(masks.data(), P.mask_out, sizeof(uint32_t) * E, hipMemcpyDeviceToHost,
+                HIP_TRY(s, hipMemcpyAsync(masks.data(), P.mask_out, sizeof(uint32_t) * W * E, hipMemcpyDeviceToHost,
                                           s->stream));
                 HIP_TRY(s, hipStreamSynchronize(s->stream));
                 float ms2 = 0;
@@ -6056,13 +6159,8 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
                     out_status[pos[k]] = 0;
                     out_score[pos[k]] = sc[k];
                     s->plan.emplace_back(g.name, rows[k]);
-                    const uint32_t b = s->h_node_alloc_off[rows[k]];
-                    for (uint32_t i = 0; i < 32; i++)
-                        if ((masks[k] >> i) & 1u) {
-                            s->h_preempted[b + i] = 1;
-                            core_hold(s, s->h_palloc_index[b + i], false);
-                            invalidate_static(s);
-                        }
+                    pe_ranked_node r;   // the host mirrors of the evictions k_commit_evicted applied
+                    set_preempted(s, r, k, rows[k], masks.data() + (size_t)k * W, W, true);
                     p++;
                 }
             }
@@ -6604,6 +6702,7 @@ int pe_plan_pop_update(pe_stack* s, uint32_t alloc) {
 int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
     PE_FLUSH_RESET(s);
     if (!s) return PE_EINVAL;
+    s->pre_overflow.clear();
     if (!s->kids.empty() && s->kids_valid) {
         int rc = spec_flush(s);
         if (rc) return rc;
@@ -6619,13 +6718,26 @@ int pe_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uin
     if (placed) *placed = p;
     if (rc == PE_OK && !s->kids.empty())   // the placements, as the caller's commits would replay them
         for (uint32_t k = 0; k < p && k < count; k++)
-            kid_log(s, 1, tgi, out[k].row, out[k].preempted, out[k].n_preempted);
+            kid_log(s, 1, tgi, out[k].row, preempted_list(s, k, out[k]), out[k].n_preempted);
     return rc;
+}
+
+int pe_preempted_of(const pe_stack* s, uint32_t record, uint32_t* out, uint32_t cap) {
+    if (!s) return PE_EINVAL;
+    for (auto& e : s->pre_overflow)
+        if (e.first == record) {
+            const uint32_t k = std::min<uint32_t>(cap, (uint32_t)e.second.size());
+            if (k && !out) return PE_EINVAL;
+            if (k) std::memcpy(out, e.second.data(), sizeof(uint32_t) * k);
+            return (int)e.second.size();
+        }
+    return PE_ESTATE;
 }
 
 int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     PE_FLUSH_RESET(s);
     if (!s || !out_score || !out_status) return PE_EINVAL;
+    s->pre_overflow.clear();
     if (!s->kids.empty() && s->kids_valid) {
         int rc = spec_flush(s);
         if (rc) return rc;

@@ -281,7 +281,7 @@ constexpr int kAuxValues = 256;
 constexpr uint32_t kAuxMissing = 255;
 
 // ---- preemption (BinPack with eviction, scheduler/preemption.go) -------------
-constexpr int kMaxNodeAllocs = 32;    // allocs of one node considered for eviction on device
+constexpr int kMaxNodeAllocs = 32;    // allocs of one node staged in LDS by k_ploop (the narrow width)
 constexpr int kMaxProposed = 64;      // ProposedAllocs list length (state allocs + plan placements)
 
 // A non-terminal state alloc as the Preemptor sees it (Allocation.ComparableResources,
@@ -320,9 +320,10 @@ struct PreemptArgs {
     // per visit position
     uint8_t* status;                  // kOption / kFiltered / kExhausted / kSkipped
     double* score;
-    uint32_t* mask_out;               // or null: preempted allocs (bits over the node's allocs)
+    uint32_t* mask_out;               // or null: preempted allocs (mask_words words of bits over the node's allocs)
     uint32_t* offers_out;             // or null: device offers, one byte per request
-    uint32_t* flags;                  // [1] bit 0: a node exceeded the on-device limits
+    uint32_t* flags;                  // [1] bit 0: a node outside the modelled surface; bit 1: a node wider
+                                      // than mask_words (rerun wider)
     uint8_t* dep_out;                 // or null: per position, the outcome read the plan's preemption counts
     const uint64_t* palloc_cores;     // [m x 4] or null: reserved cores held by each alloc (by CSR slot)
     // or null: per position the option's score parts (PE_MAX_SCORES each) and
@@ -330,7 +331,15 @@ struct PreemptArgs {
     // is read instead of re-evaluated (k_ploop)
     double* parts_out;
     uint8_t* nparts_out;
+    // eviction width (evict.inc): preempted sets are mask_words x 32 bits over a
+    // node's allocs; the launch evaluates nodes of up to 32 x mask_words allocs
+    // and ProposedAllocs lists of up to 64 x mask_words (kEvictWidths)
+    uint32_t mask_words;
 };
+constexpr uint32_t kEvictWidths[2] = {1u, 8u};   // instantiated widths, narrowest first
+constexpr uint32_t kEvictUnsup = 1u;   // PreemptArgs::flags: a node outside what the device path models
+constexpr uint32_t kEvictWider = 2u;   // a node's alloc list exceeds the launch's eviction width
+constexpr uint32_t kEvictMaxAllocs = 32u * 8u;    // node allocs the widest launch evaluates
 
 // LimitIterator + MaxScoreIterator over per-position results.
 struct EvictResolveArgs {

@@ -21,6 +21,7 @@
 // k_commit              one Plan.AppendAlloc on the HBM SoA (pe_commit).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 #include "engine_types.h"
@@ -3462,11 +3463,22 @@ hipError_t pe_launch_resolve(const pe::EvictResolveArgs* r, hipStream_t st) {
     return hipGetLastError();
 }
 
+// Eviction widths (evict.inc): W = 1 (<= 32 allocs per node) or 8 (<= 256).
+// A wide launch keeps its per-lane lists in scratch: the grid is capped lower
+// so that its scratch reservation stays small.
+static inline bool evict_width_ok(uint32_t w) { return w == 1u || w == 8u; }
+static inline uint32_t evict_blocks(uint32_t n, uint32_t w) {
+    uint32_t blocks = (n + 255) / 256;
+    const uint32_t cap = w == 1u ? 2048u : 256u;
+    if (blocks > cap) blocks = cap;
+    return blocks ? blocks : 1u;
+}
+
 hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs* r, hipStream_t st) {
-    uint32_t blocks = (a->n_visit + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(pe::k_evict<false>, dim3(blocks), dim3(256), 0, st, *a);
+    if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
+    const uint32_t blocks = evict_blocks(a->n_visit, a->mask_words);
+    if (a->mask_words == 1u) hipLaunchKernelGGL((pe::k_evict<false, 1>), dim3(blocks), dim3(256), 0, st, *a);
+    else hipLaunchKernelGGL((pe::k_evict<false, 8>), dim3(blocks), dim3(256), 0, st, *a);
     hipLaunchKernelGGL(pe::k_evict_resolve, dim3(1), dim3(pe::kResolveBlock), 0, st, *r);
     return hipGetLastError();
 }
@@ -3481,36 +3493,54 @@ hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* s
 }
 
 hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st) {
-    uint32_t blocks = (a->n_visit + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    if (blocks == 0) blocks = 1;
+    if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
+    const uint32_t blocks = evict_blocks(a->n_visit, a->mask_words);
+    const bool w1 = a->mask_words == 1u;
     if (a->parts_out) {
         if (!a->nparts_out || !a->mask_out || !a->offers_out) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(pe::k_evict<true>, dim3(blocks), dim3(256), 0, st, *a);
+        if (w1) hipLaunchKernelGGL((pe::k_evict<true, 1>), dim3(blocks), dim3(256), 0, st, *a);
+        else hipLaunchKernelGGL((pe::k_evict<true, 8>), dim3(blocks), dim3(256), 0, st, *a);
     } else {
-        hipLaunchKernelGGL(pe::k_evict<false>, dim3(blocks), dim3(256), 0, st, *a);
+        if (w1) hipLaunchKernelGGL((pe::k_evict<false, 1>), dim3(blocks), dim3(256), 0, st, *a);
+        else hipLaunchKernelGGL((pe::k_evict<false, 8>), dim3(blocks), dim3(256), 0, st, *a);
     }
     return hipGetLastError();
 }
 
+// mask: mask_words + 1 words (the preempted set, then the kEvict* flags)
 hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ranked_node* out, uint32_t* mask,
                                   hipStream_t st) {
-    hipLaunchKernelGGL(pe::k_evict_record, dim3(1), dim3(64), 0, st, *a, row, out, mask);
+    if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
+    if (a->mask_words == 1u) hipLaunchKernelGGL(pe::k_evict_record<1>, dim3(1), dim3(64), 0, st, *a, row, out, mask);
+    else hipLaunchKernelGGL(pe::k_evict_record<8>, dim3(1), dim3(64), 0, st, *a, row, out, mask);
     return hipGetLastError();
 }
 
 hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
                                     uint32_t* dev_free, uint32_t* placed, hipStream_t st) {
+    if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
     uint32_t blocks = (a->n_visit + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(pe::k_commit_evicted, dim3(blocks), dim3(256), 0, st, *a, preempted, pcount, dev_free, placed);
+    if (a->mask_words == 1u)
+        hipLaunchKernelGGL(pe::k_commit_evicted<1>, dim3(blocks), dim3(256), 0, st, *a, preempted, pcount, dev_free,
+                           placed);
+    else
+        hipLaunchKernelGGL(pe::k_commit_evicted<8>, dim3(blocks), dim3(256), 0, st, *a, preempted, pcount, dev_free,
+                           placed);
     return hipGetLastError();
 }
 
-hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, uint32_t mask, uint8_t* preempted,
+// mask: mask_words words in device memory
+hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, const uint32_t* mask, uint8_t* preempted,
                                     uint32_t* pcount, uint32_t* dev_free, hipStream_t st) {
-    hipLaunchKernelGGL(pe::k_commit_preempt, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount, dev_free);
+    if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
+    if (a->mask_words == 1u)
+        hipLaunchKernelGGL(pe::k_commit_preempt<1>, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount,
+                           dev_free);
+    else
+        hipLaunchKernelGGL(pe::k_commit_preempt<8>, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount,
+                           dev_free);
     return hipGetLastError();
 }
 
@@ -3555,7 +3585,11 @@ hipError_t pe_launch_plan_stop(pe::NodeRec* rec, uint32_t* dev_free, const pe::P
 hipError_t pe_launch_evict_trace(const pe::PreemptArgs* a, const uint32_t* rows, uint32_t n, uint32_t* code,
                                  double* named, hipStream_t st) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(pe::k_evict_trace, dim3((n + 63) / 64), dim3(64), 0, st, *a, rows, n, code, named);
+    if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
+    if (a->mask_words == 1u)
+        hipLaunchKernelGGL(pe::k_evict_trace<1>, dim3((n + 63) / 64), dim3(64), 0, st, *a, rows, n, code, named);
+    else
+        hipLaunchKernelGGL(pe::k_evict_trace<8>, dim3((n + 63) / 64), dim3(64), 0, st, *a, rows, n, code, named);
     return hipGetLastError();
 }
 
@@ -3749,17 +3783,20 @@ static size_t pe_ploop_lds_bytes(uint32_t n) { return (2u * ((n + 15u) / 16u) + 
 
 hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st) {
     const uint32_t n = a->P.n_visit;
-    if (n == 0 || n > kPLoopMaxN) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&pe::k_ploop),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (n == 0 || n > kPLoopMaxN || !evict_width_ok(a->P.mask_words)) return hipErrorInvalidValue;
+    static bool attr[2] = {false, false};
+    const int wi = a->P.mask_words == 1u ? 0 : 1;
+    if (!attr[wi]) {
+        const void* fn = wi == 0 ? reinterpret_cast<const void*>(&pe::k_ploop<1>)
+                                 : reinterpret_cast<const void*>(&pe::k_ploop<8>);
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)pe_ploop_lds_bytes(kPLoopMaxN));
         if (e != hipSuccess) return e;
-        attr = true;
+        attr[wi] = true;
     }
     const size_t lds = pe_ploop_lds_bytes(n);
-    hipLaunchKernelGGL(pe::k_ploop, dim3(1), dim3(pe::kPLoopBlock), lds, st, *a);
+    if (wi == 0) hipLaunchKernelGGL(pe::k_ploop<1>, dim3(1), dim3(pe::kPLoopBlock), lds, st, *a);
+    else hipLaunchKernelGGL(pe::k_ploop<8>, dim3(1), dim3(pe::kPLoopBlock), lds, st, *a);
     return hipGetLastError();
 }
 

@@ -123,12 +123,16 @@ class RankedNode:
     reserved_cores: List[int] = field(default_factory=list)  # Cpu.ReservedCores of the tasks, ascending
 
     @classmethod
-    def from_c(cls, r: abi.pe_ranked_node, nodes):
+    def from_c(cls, r: abi.pe_ranked_node, nodes, full_preempted=None):
+        """`full_preempted`: the whole PreemptedAllocs list when the record
+        carries more than PE_MAX_PREEMPT (pe_preempted_of)."""
+        pre = list(full_preempted) if full_preempted is not None else \
+            [r.preempted[i] for i in range(min(r.n_preempted, abi.PE_MAX_PREEMPT))]
         return cls(row=r.row, node=nodes[r.row] if (nodes is not None and r.row >= 0) else None,
                    final_score=r.final_score,
                    scores=[r.scores[i] for i in range(r.n_scores)], nodes_evaluated=r.nodes_evaluated,
                    nodes_filtered=r.nodes_filtered, nodes_exhausted=r.nodes_exhausted,
-                   new_offset=r.new_offset, preempted=[r.preempted[i] for i in range(r.n_preempted)],
+                   new_offset=r.new_offset, preempted=pre,
                    device_offers=[r.device_offer_group[i] for i in range(r.n_device_offers)],
                    reserved_cores=_core_ids(r.reserved_cores))
 
@@ -381,8 +385,19 @@ class _Stack:
             opts.preempt = int(options.preempt)
         out = abi.pe_ranked_node()
         self._check(self._fn("select")(self._h, self._tg_index(tg), C.byref(opts), C.byref(out)))
-        r = RankedNode.from_c(out, self.nodes)
+        r = RankedNode.from_c(out, self.nodes, self._full_preempted(0, out))
         return r if r.row >= 0 else None
+
+    def _full_preempted(self, record, r):
+        """PreemptedAllocs of record `record` of the last call when the record
+        holds more than PE_MAX_PREEMPT inline (else None)."""
+        if r.n_preempted <= abi.PE_MAX_PREEMPT:
+            return None
+        buf = (C.c_uint32 * r.n_preempted)()
+        n = self._fn("preempted_of")(self._h, record, buf, r.n_preempted)
+        if n != r.n_preempted:
+            raise RuntimeError("preempted_of(%d) returned %d for %d allocs" % (record, n, r.n_preempted))
+        return list(buf)
 
     def SelectRaw(self, tg, options: SelectOptions = None) -> RankedNode:
         """Select, but also returns the metrics when no node was found."""
@@ -391,7 +406,7 @@ class _Stack:
         if options is not None:
             opts.preempt = int(options.preempt)
         self._check(self._fn("select")(self._h, self._tg_index(tg), C.byref(opts), C.byref(out)))
-        return RankedNode.from_c(out, self.nodes)
+        return RankedNode.from_c(out, self.nodes, self._full_preempted(0, out))
 
     def Commit(self, tg, node_or_row, preempted: Sequence[int] = ()):
         """Plan.AppendAlloc (+ AppendPreemptedAlloc of `preempted` alloc-table rows)."""
@@ -417,7 +432,7 @@ class _Stack:
         placed = C.c_uint32(0)
         self._check(self._fn("place")(self._h, self._tg_index(tg), count, out, C.byref(placed)))
         n = min(count, placed.value + 1)
-        return [RankedNode.from_c(out[i], self.nodes) for i in range(n)]
+        return [RankedNode.from_c(out[i], self.nodes, self._full_preempted(i, out[i])) for i in range(n)]
 
     def PlaceArrays(self, tg, count: int):
         """Fused count loop returning (rows, final_scores, placed, records) as numpy

@@ -1923,6 +1923,10 @@ struct StaticRankIterator : RankIterator {
 struct oracle_stack {
     pe_config cfg;
     std::string err;
+    // PreemptedAllocs past PE_MAX_PREEMPT of the last record-producing call:
+    // (record index, full list), as the engine's pe_preempted_of
+    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> pre_overflow;
+    uint32_t cur_rec = 0;
     State state;
     EvalContext ctx;
     OJob job; bool have_job = false;
@@ -2251,7 +2255,7 @@ static void set_task_group(oracle_stack* s, const OTaskGroup& tg, bool system) {
     s->bin_pack.tg = &tg;
 }
 
-static void fill_out(pe_ranked_node* out, RankedNode* o, const oracle_stack* s) {
+static void fill_out(pe_ranked_node* out, RankedNode* o, oracle_stack* s) {
     std::memset(out, 0, sizeof(*out));
     out->row = o ? o->node->row : -1;
     if (o) {
@@ -2264,9 +2268,14 @@ static void fill_out(pe_ranked_node* out, RankedNode* o, const oracle_stack* s) 
     out->nodes_exhausted = s->ctx.metrics.exhausted;
     out->new_offset = s->source.nodes.empty() ? 0 : (uint32_t)(s->source.offset % (int)s->source.nodes.size());
     if (o) {
-        if (o->preempted.size() > PE_MAX_PREEMPT) throw Unsupported("more than PE_MAX_PREEMPT preempted allocs");
         out->n_preempted = (uint32_t)o->preempted.size();
-        for (size_t i = 0; i < o->preempted.size(); i++) out->preempted[i] = (uint32_t)o->preempted[i]->state_index;
+        std::vector<uint32_t> full;
+        for (size_t i = 0; i < o->preempted.size(); i++) {
+            const uint32_t a = (uint32_t)o->preempted[i]->state_index;
+            if (i < PE_MAX_PREEMPT) out->preempted[i] = a;
+            full.push_back(a);
+        }
+        if (full.size() > PE_MAX_PREEMPT) s->pre_overflow.emplace_back(s->cur_rec, std::move(full));
         if (o->offers.size() > PE_MAX_DEVICE_REQ) throw Unsupported("more than PE_MAX_DEVICE_REQ device requests");
         out->n_device_offers = (uint32_t)o->offers.size();
         for (size_t i = 0; i < o->offers.size(); i++) out->device_offer_group[i] = (uint32_t)o->offers[i].first;
@@ -2308,7 +2317,35 @@ static RankedNode* system_select(oracle_stack* s, uint32_t tgi) {
     return s->score_norm.Next();
 }
 
+static int select_rec(oracle_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out,
+                      uint32_t rec);
+
 int oracle_select(oracle_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
+    s->pre_overflow.clear();
+    return select_rec(s, tgi, opts, out, 0);
+}
+
+// The full PreemptedAllocs of record `rec` of the last call (engine: pe_preempted_of).
+int oracle_preempted_of(const oracle_stack* s, uint32_t rec, uint32_t* out, uint32_t cap) {
+    for (auto& e : s->pre_overflow)
+        if (e.first == rec) {
+            const size_t k = std::min<size_t>(cap, e.second.size());
+            for (size_t i = 0; i < k; i++) out[i] = e.second[i];
+            return (int)e.second.size();
+        }
+    return PE_ESTATE;
+}
+
+static const uint32_t* full_preempted(const oracle_stack* s, uint32_t rec, const pe_ranked_node& r) {
+    if (r.n_preempted <= PE_MAX_PREEMPT) return r.preempted;
+    for (auto& e : s->pre_overflow)
+        if (e.first == rec && e.second.size() == r.n_preempted) return e.second.data();
+    return nullptr;
+}
+
+static int select_rec(oracle_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out,
+                      uint32_t rec) {
+    s->cur_rec = rec;
     if (!s->have_job || tgi >= s->job.tgs.size()) { s->err = "select before set_job / bad tg"; return PE_ESTATE; }
     try {
         RankedNode* o = s->cfg.stack_kind == PE_STACK_GENERIC ? generic_select(s, tgi, opts) : system_select(s, tgi);
@@ -2401,17 +2438,18 @@ int oracle_plan_pop_update(oracle_stack* s, uint32_t alloc) {
 
 int oracle_place(oracle_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
     uint32_t p = 0;
+    s->pre_overflow.clear();
     for (uint32_t i = 0; i < count; i++) {
         pe_select_options opts; std::memset(&opts, 0, sizeof(opts));
-        int rc = oracle_select(s, tgi, &opts, &out[i]);
+        int rc = select_rec(s, tgi, &opts, &out[i], i);
         if (rc != PE_OK) return rc;
         if (out[i].row < 0 && s->cfg.preempt && s->cfg.stack_kind == PE_STACK_GENERIC) {
             opts.preempt = 1;   // selectNextOption (generic_sched.go:786-790)
-            rc = oracle_select(s, tgi, &opts, &out[i]);
+            rc = select_rec(s, tgi, &opts, &out[i], i);
             if (rc != PE_OK) return rc;
         }
         if (out[i].row < 0) break;   // failedTGAllocs: the rest of the tg is coalesced
-        oracle_commit_preempt(s, tgi, out[i].row, out[i].preempted, out[i].n_preempted);
+        oracle_commit_preempt(s, tgi, out[i].row, full_preempted(s, i, out[i]), out[i].n_preempted);
         p++;
     }
     if (placed) *placed = p;
@@ -2425,7 +2463,8 @@ int oracle_system_place(oracle_stack* s, uint32_t tgi, double* out_score, uint8_
     for (size_t i = 0; i < all.size(); i++) {
         s->source.SetNodes(std::vector<const ONode*>{all[i]});
         pe_ranked_node r;
-        int rc = oracle_select(s, tgi, nullptr, &r);
+        s->pre_overflow.clear();
+        int rc = select_rec(s, tgi, nullptr, &r, 0);
         if (rc != PE_OK) return rc;
         if (r.row < 0) {
             out_score[i] = NAN;
@@ -2433,7 +2472,7 @@ int oracle_system_place(oracle_stack* s, uint32_t tgi, double* out_score, uint8_
             continue;
         }
         out_score[i] = r.final_score; out_status[i] = 0;
-        oracle_commit_preempt(s, tgi, r.row, r.preempted, r.n_preempted);
+        oracle_commit_preempt(s, tgi, r.row, full_preempted(s, 0, r), r.n_preempted);
         p++;
     }
     s->source.SetNodes(all);

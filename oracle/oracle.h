@@ -26,6 +26,7 @@ int oracle_select(oracle_stack* s, uint32_t tg_index, const pe_select_options* o
 int oracle_commit(oracle_stack* s, uint32_t tg_index, int32_t row);
 int oracle_commit_preempt(oracle_stack* s, uint32_t tg_index, int32_t row, const uint32_t* preempted,
                           uint32_t n_preempted);
+int oracle_preempted_of(const oracle_stack* s, uint32_t record, uint32_t* out, uint32_t cap);
 int oracle_plan_stop(oracle_stack* s, const uint32_t* allocs, uint32_t n);
 int oracle_plan_pop_update(oracle_stack* s, uint32_t alloc);
 int oracle_place(oracle_stack* s, uint32_t tg_index, uint32_t count, pe_ranked_node* out,

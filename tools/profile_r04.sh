@@ -15,6 +15,17 @@ if [ -z "$SKIP_TESTS" ]; then
     > "$OUT/gpu_pytest.log" 2>&1 || { tail -60 "$OUT/gpu_pytest.log"; exit 1; }
   tail -1 "$OUT/gpu_pytest.log"
 fi
+cd /tmp
+export TMPDIR=/tmp
+for R in 10000 1048576; do
+  timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_f$R" -o f -- \
+    "$ROOT/tools/fetch_calib" $R > "$OUT/calib_$R.txt" 2> "$OUT/calib_f$R.err"
+  timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib_w$R" -o w -- \
+    "$ROOT/tools/fetch_calib" $R > /dev/null 2> "$OUT/calib_w$R.err"
+  python3 "$ROOT/tools/fetch_calib.py" $(find "$OUT/calib_f$R" -name "*counter_collection.csv" -print -quit) \
+    $(find "$OUT/calib_w$R" -name "*counter_collection.csv" -print -quit) "$OUT/calib_$R.txt" "$OUT/fetch_calib_$R.json" > /dev/null
+done
+cd "$ROOT"
 timeout -k 10 500 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
 python3 -c "import json;d=json.load(open('$OUT/bench.json'));r=d['roofline'];print('value %.4g' % d['value'], 'us/eval %.1f' % (d['ms_per_step']*1e3), 'cpu', d['cpu_baseline']['value'], 'frac', r['frac'], 'traffic', r['traffic']); print(' '.join('%s %.4g' % (k, v.get('placements_per_s', v.get('nodes_per_s', 0))) for k, v in d['configs'].items() if isinstance(v, dict)))"
 cd /tmp
