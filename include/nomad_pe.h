@@ -515,6 +515,48 @@ int pe_put_eligibility(pe_stack* s, const pe_class_feas* in, uint32_t n);
  * it selected for (its SpreadIterator.SetTaskGroup adds the group's spread
  * weights to sumSpreadWeights, spread.go:232-257), or PE_NONE. */
 int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit);
+/* ---- zero-crossing served Selects --------------------------------------------
+ * GenericScheduler.computePlacements (generic_sched.go:552-627) calls Select
+ * once per placement and the shim commits each option (Plan.AppendAlloc): two
+ * cgo crossings per placement. After the first plain Select of a task group
+ * the engine already holds the records of the group's whole remaining count
+ * loop; this view lets the caller answer the following plain
+ * Select / Commit pairs from host memory and cross into C only when it
+ * deviates. One view per handle, used from the handle's thread.
+ *
+ *   Select(tg) with no options, when v->n_rec > 0, tg == v->tg_index,
+ *     v->served == v->confirmed and v->served < v->n_rec:
+ *       the result is v->recs[v->served] (row < 0: nil, the count loop is
+ *       over; no Commit follows), then v->served++;
+ *   Commit(tg, row), when v->served == v->confirmed + 1, tg == v->tg_index
+ *     and row == v->recs[v->served - 1].row: v->confirmed++;
+ *   anything else goes through the entry points below, which first take the
+ *     counters over, so the engine state is exactly what the sequential calls
+ *     would have produced; they may replace or withdraw the records (v->epoch
+ *     changes; v->n_rec 0: nothing to serve).
+ * A served record is the leading part of pe_ranked_node (row .. new_offset)
+ * plus the device offers; served Selects never preempt or reserve cores.
+ * Replaces: the Select / Commit crossings of computePlacements' loop. */
+typedef struct pe_spec_rec {
+    int32_t row;
+    uint32_t n_scores;
+    double final_score;
+    double scores[PE_MAX_SCORES];
+    uint32_t nodes_evaluated, nodes_filtered, nodes_exhausted, new_offset;
+    uint32_t n_device_offers;
+    uint16_t device_offer_group[PE_MAX_DEVICE_REQ];
+    uint32_t pad;
+} pe_spec_rec;
+typedef struct pe_spec_view {
+    uint32_t epoch;               /* engine: changes whenever recs / n_rec / tg_index change */
+    uint32_t tg_index;            /* the task group the records answer */
+    uint32_t n_rec;               /* records [0, n_rec) are valid */
+    uint32_t pad0;
+    const pe_spec_rec* recs;      /* the run's records in Select order */
+    uint32_t served;              /* caller and engine: Selects answered from recs */
+    uint32_t confirmed;           /* caller and engine: Commits that named the answered row */
+} pe_spec_view;
+pe_spec_view* pe_spec_view_get(pe_stack* s);
 int pe_set_cursor(pe_stack* s, uint32_t tg_index, uint32_t offset, uint32_t limit);
 /* Host-side constraint semantics used for pre-resolution (checkConstraint,
  * feasible.go:785-820), exposed for known-answer tests; needs no device.

@@ -227,8 +227,21 @@ ENGINE_SYMBOLS = [
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
     "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
-    "pe_last_kernel_split", "pe_preempted_of",
+    "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get",
 ]
+
+
+class pe_spec_rec(C.Structure):   # nomad_pe.h: a served-Select record
+    _fields_ = [("row", C.c_int32), ("n_scores", C.c_uint32), ("final_score", C.c_double),
+                ("scores", C.c_double * PE_MAX_SCORES), ("nodes_evaluated", C.c_uint32),
+                ("nodes_filtered", C.c_uint32), ("nodes_exhausted", C.c_uint32), ("new_offset", C.c_uint32),
+                ("n_device_offers", C.c_uint32), ("device_offer_group", C.c_uint16 * PE_MAX_DEVICE_REQ),
+                ("pad", C.c_uint32)]
+
+
+class pe_spec_view(C.Structure):
+    _fields_ = [("epoch", C.c_uint32), ("tg_index", C.c_uint32), ("n_rec", C.c_uint32), ("pad0", C.c_uint32),
+                ("recs", C.POINTER(pe_spec_rec)), ("served", C.c_uint32), ("confirmed", C.c_uint32)]
 
 
 def bind(lib, prefix, create_name, destroy_name, error_name):

@@ -572,6 +572,7 @@ struct pe_stack {
         uint32_t tgi = 0;
         std::vector<pe_ranked_node> recs;
         std::vector<pe::EmitRec> crecs;   // the chain's compact records (compact = true), widened when served
+        std::vector<pe::EmitRec> vrecs;   // recs narrowed for the served-Select view (compact = false)
         bool compact = false;
         uint32_t n_rec = 0, placed = 0, served = 0, confirmed = 0;
         uint32_t grow = 1;             // run length on costly paths, doubles while runs get used up
@@ -579,6 +580,7 @@ struct pe_stack {
     } spec;
     std::vector<pe::EmitRec>* emit_sink = nullptr;   // run_place: keep chain records compact here
     bool emit_sunk = false;                          // ... and it did
+    pe_spec_view sview{};              // the run's records for caller-served Selects (pe_spec_view_get)
     bool spec_on = true;               // PE_SPECULATE=0: every Select runs on its own
     uint64_t spec_stats[4] = {0, 0, 0, 0};   // runs, Selects served, rollbacks, records computed
     DevMem ck_rec, ck_coll_job, ck_coll_tg, ck_dev_free, ck_pset[pe::kMaxPsets];
@@ -664,6 +666,11 @@ struct pe_stack {
         }
     }
 };
+
+extern "C" {
+static void elig_log_span(pe_stack* s, uint32_t tgi, uint32_t begin, uint32_t len);
+static void kid_log(pe_stack* s, uint8_t kind, uint32_t tgi, int32_t row, const uint32_t* a, uint32_t n);
+}
 
 namespace {
 
@@ -2030,8 +2037,81 @@ static int flush_reset(pe_stack* s) {
 }
 
 
+void invalidate_job_distinct(pe_stack* s, uint32_t tgi);
+
+// ---- the served-Select view (pe_spec_view) ----------------------------------
+// The records of the active run, published for the caller; its counters mirror
+// sp.served / sp.confirmed. What the caller served or confirmed from the view
+// is taken over exactly as spec_serve / commit_one would have done it.
+static const pe::EmitRec& spec_rec(const pe_stack::Spec& sp, uint32_t k) {
+    return sp.compact ? sp.crecs[k] : sp.vrecs[k];
+}
+
+static void view_take(pe_stack* s) {
+    pe_spec_view& v = s->sview;
+    pe_stack::Spec& sp = s->spec;
+    if (!v.n_rec || !sp.active) return;
+    if (v.served == sp.served && v.confirmed == sp.confirmed) return;
+    const uint32_t served = std::min(v.served, sp.n_rec), confirmed = std::min(v.confirmed, served);
+    const auto name = s->tgs[sp.tgi]->name;
+    for (uint32_t k = sp.served; k < served; k++) {   // spec_serve of record k, then its commit
+        const pe::EmitRec& r = spec_rec(sp, k);
+        s->gen++;
+        elig_log_span(s, sp.tgi, s->offset, r.nodes_evaluated);
+        s->offset = r.new_offset;
+        s->metrics_valid = false;
+        s->spec_stats[1]++;
+        if (k < confirmed && r.row >= 0) {
+            s->gen++;
+            s->plan.emplace_back(name, (uint32_t)r.row);
+            invalidate_job_distinct(s, sp.tgi);
+            if (!s->kids.empty()) kid_log(s, 0, sp.tgi, r.row, nullptr, 0);   // as pe_commit logs it
+        }
+    }
+    sp.served = served;
+    sp.confirmed = std::max(sp.confirmed, confirmed);
+    sp.pending = sp.served > sp.confirmed && spec_rec(sp, sp.served - 1).row >= 0;
+    s->offer_row = -1;
+    v.served = sp.served;
+    v.confirmed = sp.confirmed;
+}
+
+static void view_publish(pe_stack* s) {
+    pe_stack::Spec& sp = s->spec;
+    pe_spec_view& v = s->sview;
+    if (!sp.compact) {   // served Selects carry no preemptions / reserved cores: the leading fields
+        sp.vrecs.resize(sp.n_rec);
+        for (uint32_t k = 0; k < sp.n_rec; k++) {
+            const pe_ranked_node& r = sp.recs[k];
+            pe::EmitRec& e = sp.vrecs[k];
+            std::memset(&e, 0, sizeof(e));
+            std::memcpy(&e, &r, offsetof(pe::EmitRec, n_device_offers));
+            e.n_device_offers = r.n_device_offers;
+            for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) e.device_offer_group[q] = (uint16_t)r.device_offer_group[q];
+        }
+    }
+    v.epoch++;
+    v.tg_index = sp.tgi;
+    v.recs = sp.compact ? sp.crecs.data() : sp.vrecs.data();
+    v.served = sp.served;
+    v.confirmed = sp.confirmed;
+    v.n_rec = s->metrics_on ? 0u : sp.n_rec;
+}
+
+static void view_withdraw(pe_stack* s) {
+    pe_spec_view& v = s->sview;
+    if (!v.n_rec && !v.recs) return;
+    v.epoch++;
+    v.n_rec = 0;
+    v.recs = nullptr;
+    v.served = v.confirmed = 0;
+}
+
+// Every entry point first takes over the Selects / Commits the caller served
+// from the view, then launches a deferred ResetPlan copy.
 #define PE_FLUSH_RESET(s)                             \
     do {                                              \
+        if (s) view_take(s);                          \
         if ((s) && ((s)->reset_pending || (s)->fold_pending)) { \
             const int frc_ = flush_reset(s);          \
             if (frc_) return frc_;                    \
@@ -2943,11 +3023,20 @@ int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* n
         P.visit = s->d_visit.as<uint32_t>();
         P.n_visit = n;
         P.flags = s->d_ev_flags.as<uint32_t>();
-        HIP_TRY_STATE(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
-                                          s->stream));
         pe_ranked_node rr;
-        HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        for (;;) {   // the node's ProposedAllocs may have outgrown the width: the record wider
+            HIP_TRY_STATE(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(),
+                                                    s->d_ev_mask.as<uint32_t>(), s->stream));
+            uint32_t fl = 0;
+            HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(s, hipMemcpyAsync(&fl, s->d_ev_mask.as<uint32_t>() + P.mask_words, sizeof(fl),
+                                      hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(s, hipStreamSynchronize(s->stream));
+            if (!(fl & pe::kEvictWider)) break;
+            P.mask_words = wider_words(P.mask_words);
+            if (!P.mask_words) return s->fail(PE_EUNSUPPORTED, "preemption: a node's proposed allocs exceed the "
+                                                                "widest eviction width");
+        }
         out->row = (int32_t)row;
         out->final_score = rr.final_score;
         out->n_scores = rr.n_scores;
@@ -5197,6 +5286,7 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
 // always what the sequential calls would have produced.
 
 static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
+    view_take(s);
     pe_stack::Spec& sp = s->spec;
     if (!sp.active || sp.pending || tgi != sp.tgi || sp.served >= sp.n_rec || s->metrics_on) return false;
     if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
@@ -5208,6 +5298,8 @@ static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     s->offset = out->new_offset;   // the StaticIterator cursor after this Select
     s->metrics_valid = false;
     s->spec_stats[1]++;
+    s->sview.served = sp.served;
+    s->sview.confirmed = sp.confirmed;
     return true;
 }
 
@@ -5255,8 +5347,10 @@ static int spec_flush(pe_stack* s) {
         const int rc = sys_flush(s);
         if (rc) return rc;
     }
+    view_take(s);
     pe_stack::Spec& sp = s->spec;
     if (!sp.active) return PE_OK;
+    view_withdraw(s);
     sp.active = false;
     sp.pending = false;
     const bool used_up = sp.served == sp.n_rec && sp.confirmed == sp.placed && sp.placed == sp.n_rec;
@@ -5314,6 +5408,7 @@ static int spec_flush(pe_stack* s) {
 
 // Drop the speculation without touching the device (the state is being reset).
 static void spec_drop(pe_stack* s) {
+    view_withdraw(s);
     s->spec.active = false;
     s->spec.pending = false;
     s->spec.grow = 1;
@@ -5382,6 +5477,7 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     s->offset = off0;   // the run left the cursor at its end: serving advances it record by record
     if (!spec_serve(s, tgi, nullptr, out)) return s->fail(PE_ESTATE, "speculative loop produced no record");
     s->spec_stats[1]--;   // the first record is the Select that started the run
+    view_publish(s);
     return PE_OK;
 }
 
@@ -5425,11 +5521,13 @@ static int commit_one(pe_stack* s, uint32_t tgi, int32_t row) {
         return PE_OK;
     }
     if (s->sys.active && row >= 0) sys_touch(s, (uint32_t)row);
+    view_take(s);
     pe_stack::Spec& sp = s->spec;
     if (sp.active && sp.pending && tgi == sp.tgi && row == spec_row(sp, sp.served - 1)) {
         // the predicted Plan.AppendAlloc: already in HBM
         sp.pending = false;
         sp.confirmed = sp.served;
+        s->sview.confirmed = sp.confirmed;
         s->gen++;
         s->plan.emplace_back(s->tgs[tgi]->name, (uint32_t)row);
         invalidate_job_distinct(s, tgi);
@@ -5662,6 +5760,7 @@ double pe_last_exchange_us(const pe_stack* s) { return s ? s->last_exchange_us :
 
 int pe_speculation_stats(const pe_stack* s, uint64_t* out4) {
     if (!s || !out4) return PE_EINVAL;
+    view_take(const_cast<pe_stack*>(s));
     for (int i = 0; i < 4; i++) out4[i] = s->spec_stats[i];
     return PE_OK;
 }
@@ -6295,8 +6394,11 @@ int pe_put_eligibility(pe_stack* s, const pe_class_feas* in, uint32_t n) {
     return PE_OK;
 }
 
+pe_spec_view* pe_spec_view_get(pe_stack* s) { return s ? &s->sview : nullptr; }
+
 int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit) {
     if (!s) return PE_EINVAL;
+    view_take(const_cast<pe_stack*>(s));   // Selects the caller served from the view moved the cursor
     if (offset) *offset = s->offset;
     if (limit) *limit = s->limit;
     return PE_OK;

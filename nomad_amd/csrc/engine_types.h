@@ -156,16 +156,8 @@ struct ResetArgs {
 // Select result as k_emit hands it to the host: the leading fields of
 // pe_ranked_node (row .. new_offset, byte-identical) and the device offers;
 // the host widens it (no preemptions or reserved cores on the chain path).
-struct EmitRec {
-    int32_t row;
-    uint32_t n_scores;
-    double final_score;
-    double scores[PE_MAX_SCORES];
-    uint32_t nodes_evaluated, nodes_filtered, nodes_exhausted, new_offset;
-    uint32_t n_device_offers;
-    uint16_t device_offer_group[PE_MAX_DEVICE_REQ];
-    uint32_t pad;
-};
+// It is the public pe_spec_rec (the served-Select view, nomad_pe.h).
+using EmitRec = pe_spec_rec;
 static_assert(sizeof(EmitRec) % 8 == 0, "record copy granule");
 static_assert(offsetof(EmitRec, n_device_offers) == offsetof(pe_ranked_node, n_preempted),
               "EmitRec shares pe_ranked_node's leading fields");

@@ -23,7 +23,8 @@ from .encode import EncodedJob, EncodedState, Interner
 from .structs import Allocation, Job, Node, SchedulerConfig
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ENGINE_LIB = os.path.join(_HERE, "libnomadpe.so")
+# PE_ENGINE_LIB: an A/B build of the same sources (measurement runs only)
+ENGINE_LIB = os.environ.get("PE_ENGINE_LIB") or os.path.join(_HERE, "libnomadpe.so")
 
 
 class EngineError(RuntimeError):

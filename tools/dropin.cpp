@@ -9,7 +9,11 @@
 // :519-523). Evaluations start from a fresh EvalContext (ResetPlan) and SetJob.
 //
 // The same loop drives the engine (pe_*) and the CPU oracle (oracle_*): the
-// caller passes the entry points.
+// caller passes the entry points. With the engine's served-Select view
+// (pe_spec_view_get, nomad_pe.h) the loop answers plain Select / Commit pairs
+// from the view and calls C only when it deviates, as the Go shim does; a
+// record with more than PE_MAX_PREEMPT preempted allocs is read in full with
+// preempted_of before its Commit.
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -37,7 +41,29 @@ struct dropin_api {
     int (*select)(void*, uint32_t, const pe_select_options*, pe_ranked_node*);
     int (*commit)(void*, uint32_t, int32_t);
     int (*commit_preempt)(void*, uint32_t, int32_t, const uint32_t*, uint32_t);
+    int (*preempted_of)(const void*, uint32_t, uint32_t*, uint32_t);
+    pe_spec_view* (*spec_view_get)(void*);   // null: every Select and Commit crosses
 };
+
+static int g_use_view = 1;
+void dropin_use_view(int on) { g_use_view = on; }
+static uint64_t g_view_served = 0;   // Selects answered from the view since the last read
+uint64_t dropin_view_served(int reset) {
+    const uint64_t x = g_view_served;
+    if (reset) g_view_served = 0;
+    return x;
+}
+
+// Commit of a Select's option, with its whole PreemptedAllocs list.
+static int commit_opt(const dropin_api* api, void* h, uint32_t tg, const pe_ranked_node& opt, uint32_t rec) {
+    if (!opt.n_preempted) return api->commit(h, tg, opt.row);
+    if (opt.n_preempted <= PE_MAX_PREEMPT) return api->commit_preempt(h, tg, opt.row, opt.preempted, opt.n_preempted);
+    uint32_t buf[1024];
+    if (opt.n_preempted > 1024 || !api->preempted_of) return PE_EUNSUPPORTED;
+    const int n = api->preempted_of(h, rec, buf, opt.n_preempted);
+    if (n != (int)opt.n_preempted) return n < 0 ? n : PE_ESTATE;
+    return api->commit_preempt(h, tg, opt.row, buf, opt.n_preempted);
+}
 
 // One evaluation's placements of task group `tg`; rows[count] (may be null)
 // receives the chosen rows, -1 after the loop stopped. Returns 0 or the first
@@ -54,7 +80,20 @@ int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, in
     int rc = 0;
     using clk = std::chrono::steady_clock;
     auto t_first = clk::now();
+    pe_spec_view* v = (g_use_view && api->spec_view_get) ? api->spec_view_get(h) : nullptr;
     for (uint32_t i = 0; i < count; i++) {
+        if (v && v->n_rec && v->tg_index == tg && v->served == v->confirmed && v->served < v->n_rec &&
+            v->recs[v->served].row >= 0) {
+            // a plain Select answered from the view and its Commit confirmed there
+            const int32_t row = v->recs[v->served].row;
+            v->served++;
+            v->confirmed++;
+            sel++;
+            g_view_served++;
+            if (rows) rows[p] = row;
+            p++;
+            continue;
+        }
         rc = api->select(h, tg, &none, &opt);
         sel++;
         if (i == 0) {
@@ -69,8 +108,7 @@ int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, in
             if (rc) break;
         }
         if (opt.row < 0) break;
-        rc = opt.n_preempted ? api->commit_preempt(h, tg, opt.row, opt.preempted, opt.n_preempted)
-                             : api->commit(h, tg, opt.row);
+        rc = commit_opt(api, h, tg, opt, 0);
         if (rc) break;
         if (rows) rows[p] = opt.row;
         p++;
@@ -150,8 +188,7 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
             score[i] = __builtin_nan("");
             continue;
         }
-        rc = opt.n_preempted ? api->commit_preempt(h, tg, opt.row, opt.preempted, opt.n_preempted)
-                             : api->commit(h, tg, opt.row);
+        rc = commit_opt(api, h, tg, opt, 0);
         if (rc) break;
         status[i] = 0;
         score[i] = opt.final_score;

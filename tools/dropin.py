@@ -19,7 +19,8 @@ _lib = None
 
 class dropin_api(C.Structure):
     _fields_ = [(name, C.c_void_p) for name in
-                ("reset_plan", "set_job", "set_nodes", "select", "commit", "commit_preempt")]
+                ("reset_plan", "set_job", "set_nodes", "select", "commit", "commit_preempt", "preempted_of",
+                 "spec_view_get")]
 
 
 def load():
@@ -35,6 +36,10 @@ def load():
                                      C.POINTER(abi.pe_job), abi.u32p, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.c_int, C.c_uint32, C.c_double, abi.i32p,
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        lib.dropin_use_view.restype = None
+        lib.dropin_use_view.argtypes = [C.c_int]
+        lib.dropin_view_served.restype = C.c_uint64
+        lib.dropin_view_served.argtypes = [C.c_int]
         lib.dropin_system.restype = C.c_int
         lib.dropin_system.argtypes = [C.POINTER(dropin_api), C.c_void_p, C.c_uint32, abi.u32p, C.c_uint32,
                                       abi.u8p, abi.f64p, abi.u32p, C.c_void_p, C.POINTER(C.c_double)]
@@ -46,8 +51,19 @@ def _api(stack):
     lib, p = stack._lib, stack._p
     a = dropin_api()
     for name, _ in dropin_api._fields_:
-        setattr(a, name, C.cast(getattr(lib, p + name), C.c_void_p).value)
+        fn = getattr(lib, p + name, None)   # the oracle has no served-Select view
+        setattr(a, name, C.cast(fn, C.c_void_p).value if fn is not None else None)
     return a
+
+
+def use_view(on):
+    """Whether the C loop answers plain Select / Commit pairs from the
+    engine's served-Select view (the Go shim's shape) or crosses every time."""
+    load().dropin_use_view(1 if on else 0)
+
+
+def view_served(reset=False):
+    return int(load().dropin_view_served(1 if reset else 0))
 
 
 def prepare(stack, job):

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-4 GPU check: new tests first (-k $2 or the files in $3), then the whole
+# -m gpu suite, then a short bench of the sections in $SECTIONS. Every GPU step
+# has its own time limit; the script stops at the first failure. Outputs in
+# gpurun_out/<tag>/.
+set -eo pipefail
+TAG=${1:-r04c}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+ARGS=(-m gpu -x -v --timeout 300 --timeout-method thread --durations 15)
+if [ -n "$FIRST" ]; then
+  timeout -k 10 600 python -u -m pytest $FIRST "${ARGS[@]}" > "$OUT/first.log" 2>&1 || { tail -80 "$OUT/first.log"; exit 1; }
+  grep -E "passed|failed" "$OUT/first.log" | tail -1
+fi
+if [ -z "$NO_SUITE" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations 20 \
+    > "$OUT/gpu_pytest.log" 2>&1 || { tail -80 "$OUT/gpu_pytest.log"; exit 1; }
+  tail -1 "$OUT/gpu_pytest.log"
+fi
+if [ -n "$SECTIONS" ]; then
+  timeout -k 10 400 python -u bench.py --no-cpu --sweep-nodes 0 --sections "$SECTIONS" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
+  python3 -c "import json;d=json.load(open('$OUT/bench.json'));print('C2 %.4g' % d['value'], 'us/eval %.1f' % (d['ms_per_step']*1e3)); print(' '.join('%s %.4g' % (k, v.get('placements_per_s', v.get('nodes_per_s', 0))) for k, v in d['configs'].items() if isinstance(v, dict)))"
+fi
+if [ -n "$AB_LIBS" ]; then   # A/B of engine builds: the C5 loop (tools/c5_prof.py) with each
+  for LIB in $AB_LIBS; do
+    if [ "$LIB" = default ]; then unset PE_ENGINE_LIB; else export PE_ENGINE_LIB=$ROOT/$LIB; fi
+    echo "== $LIB"
+    PE_PLACE_PROF=1 timeout -k 10 300 python -u tools/c5_prof.py > "$OUT/ab_$(basename $LIB).txt" 2>&1 || { tail -20 "$OUT/ab_$(basename $LIB).txt"; exit 1; }
+    grep -E "^run|k_ploop:" "$OUT/ab_$(basename $LIB).txt" | tail -4
+  done
+  unset PE_ENGINE_LIB
+fi
