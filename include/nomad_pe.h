@@ -477,7 +477,8 @@ int pe_last_kernel_split(const pe_stack* s, double* ms4);
  * `ctx.Metrics()` holds after GenericStack.Select (FilterNode / ExhaustedNode,
  * structs.go:9907-9937). Off by default; switch on before the first Select of
  * an evaluation (the maps depend on the EvalEligibility memo history).
- * Available for plain Selects (no preferred nodes, no Preempt). */
+ * Available for every Select: plain, with preferred nodes, and with Preempt
+ * (BinPack with evict per visited row, k_evict_trace). */
 int pe_set_metrics(pe_stack* s, int on);
 /* The last Select's maps as text lines "KIND\tKEY\tCOUNT\n", KIND one of
  * CF / KF / CE / DE, keys sorted. Writes at most cap bytes (NUL-terminated) and

@@ -35,7 +35,7 @@
 #include "engine_types.h"
 #include "gomath_dev.h"
 
-size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed);
+size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed, size_t pset_bytes);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_rank_of(const uint32_t* list, uint32_t n_list, uint32_t* rank_of, uint32_t n_rows, hipStream_t st);
@@ -366,6 +366,7 @@ struct pe_stack {
     double last_ms = 0;
     bool last_ms_pending = false;      // last_ms still to be read from ev0 / ev1
     bool spin_wait = true;             // PE_SPIN_WAIT=0: chain launches wait with a stream sync
+    bool counts_defer_ok = true;       // PE_COUNTS_DEFER=0: SetJob launches its counts at once
     uint32_t place_seq = 0;            // completion word sequence (run_place)
     int n_cu = 256;
     int sweep_per_cu = 4, sweep_per_cu_aux = 4;
@@ -404,6 +405,12 @@ struct pe_stack {
     bool fold_defer_ok = false;
     bool fold_pending = false;
     pe::FoldArgs pending_fold{};
+    // SetJob's collision counts (with a deferred ResetPlan copy) not launched
+    // yet: a short list's fused k_chain carries them (one launch per
+    // evaluation); the first other launch that reads the plan's state
+    // launches them first (HIP_TRY_STATE, flush_counts)
+    bool counts_pending = false;
+    pe::CountArgs pending_counts{};
     // preemption: non-terminal state allocs per node (CSR, table order) as PreemptAlloc
     std::vector<uint32_t> h_node_alloc_off, h_palloc_index;   // CSR; slot -> alloc-table row
     std::vector<uint32_t> alloc_slot;          // alloc-table row -> slot (PE_NONE: terminal)
@@ -557,7 +564,8 @@ struct pe_stack {
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
     DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;
-    DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)  // device-resident parallel count loop (k_ploop)
+    DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)
+    DevMem d_pset_g, d_pset_gb;              // FULL k_place per-value tables beyond the LDS budget (batch: gb)  // device-resident parallel count loop (k_ploop)
     DevMem d_ploop_parts, d_ploop_nparts;   // k_ploop: Preempt records per position (parts, count)
 
     // Speculative count loop behind pe_select / pe_commit: the
@@ -708,8 +716,13 @@ struct ApiScope {
 // counts, preemptions): the deferred ResetPlan copy must have been launched
 // before it (every entry point starts with PE_FLUSH_RESET); a launch that
 // would read the previous evaluation's state fails instead.
+static int flush_counts(pe_stack* s);
 #define HIP_TRY_STATE(s, expr)                                                          \
     do {                                                                                \
+        if ((s)->counts_pending) {                                                      \
+            const int crc_ = flush_counts(s);                                           \
+            if (crc_) return crc_;                                                      \
+        }                                                                               \
         if ((s)->reset_pending)                                                         \
             return (s)->fail(PE_EINTERNAL, std::string(#expr ": the deferred ResetPlan " \
                                                        "copy was not launched first")); \
@@ -730,6 +743,7 @@ hipError_t upload_s(pe_stack* s, DevMem& m, const std::vector<T>& h) {
     if (e != hipSuccess || b == 0) return e;
     if (b > kStageBytes / 4) {
         if (s->fold_pending && flush_fold(s) != PE_OK) return hipErrorLaunchFailure;   // it reads its staged table
+        if (s->counts_pending && flush_counts(s) != PE_OK) return hipErrorLaunchFailure;   // its staged entries
         e = hipStreamSynchronize(s->stream);
         if (e != hipSuccess) return e;
         s->stage_off = 0;
@@ -741,8 +755,9 @@ hipError_t upload_s(pe_stack* s, DevMem& m, const std::vector<T>& h) {
     }
     size_t off = (s->stage_off + 255) & ~size_t(255);
     if (off + b > kStageBytes) {
-        // the ring restarts: a pending fold still reads its staged table
+        // the ring restarts: a pending fold / count launch still reads its staged table
         if (s->fold_pending && flush_fold(s) != PE_OK) return hipErrorLaunchFailure;
+        if (s->counts_pending && flush_counts(s) != PE_OK) return hipErrorLaunchFailure;
         e = hipStreamSynchronize(s->stream);
         if (e != hipSuccess) return e;
         off = 0;
@@ -766,6 +781,7 @@ const unsigned char* stage_only(pe_stack* s, const std::vector<T>& h) {
     size_t off = (s->stage_off + 255) & ~size_t(255);
     if (off + b > kStageBytes) {
         if (s->fold_pending && flush_fold(s) != PE_OK) return nullptr;   // it reads its staged table
+        if (s->counts_pending && flush_counts(s) != PE_OK) return nullptr;
         if (hipStreamSynchronize(s->stream) != hipSuccess) return nullptr;
         off = 0;
     }
@@ -2010,6 +2026,14 @@ static pe::ResetArgs reset_args(pe_stack* s) {
 }
 
 // A pending fold (pe_stack::fold_pending) as its own launch.
+static int flush_counts(pe_stack* s) {
+    if (!s->counts_pending) return PE_OK;
+    const pe::CountArgs C = s->pending_counts;
+    HIP_TRY(s, pe_launch_counts(&C.D, C.nd, C.n, C.ents, C.m, C.R.rec ? &C.R : nullptr, s->stream));
+    s->counts_pending = false;
+    return PE_OK;
+}
+
 static int flush_fold(pe_stack* s) {
     if (!s->fold_pending) return PE_OK;
     s->fold_pending = false;
@@ -2118,7 +2142,12 @@ static void view_withdraw(pe_stack* s) {
         }                                             \
     } while (0)
 
-int build_collisions(pe_stack* s, bool own = false) {
+// `defer` (SetJob): the counts may wait for the next launch (counts_pending).
+int build_collisions(pe_stack* s, bool own = false, bool defer = false) {
+    if (s->counts_pending) {   // an earlier SetJob's counts first: launches keep their order
+        const int frc = flush_counts(s);
+        if (frc) return frc;
+    }
     const size_t n = s->nodes.size();
     const uint32_t ntg = (uint32_t)s->tgs.size();
     const uint32_t nd = ntg + 2;   // dst 0: own, 1: job, 2 + g: task group g
@@ -2169,15 +2198,32 @@ int build_collisions(pe_stack* s, bool own = false) {
         HIP_TRY(s, s->tgs[g]->coll_tg.ensure(bytes));
         D.d[2 + g] = s->tgs[g]->coll_tg.as<uint32_t>();
     }
-    if (!ents.empty()) HIP_TRY(s, upload_s(s, s->d_count_ents, ents));
     const pe::ResetArgs R = s->reset_pending ? reset_args(s) : pe::ResetArgs{};
+    if (defer && s->counts_defer_ok) {
+        // the entries stay in the mapped staging ring: the launch that carries
+        // them reads them from there
+        const uint2* staged = ents.empty() ? nullptr : reinterpret_cast<const uint2*>(stage_only(s, ents));
+        if (ents.empty() || staged) {
+            pe::CountArgs& C = s->pending_counts;
+            C.D = D;
+            C.nd = nd;
+            C.n = (uint32_t)n;
+            C.ents = staged;
+            C.m = (uint32_t)ents.size();
+            C.R = R;
+            s->counts_pending = true;
+            s->reset_pending = false;   // the copy rides with the counts
+            return PE_OK;
+        }
+    }
+    if (!ents.empty()) HIP_TRY(s, upload_s(s, s->d_count_ents, ents));
     HIP_TRY(s, pe_launch_counts(&D, nd, (uint32_t)n, ents.empty() ? nullptr : s->d_count_ents.as<uint2>(),
                                 (uint32_t)ents.size(), R.rec ? &R : nullptr, s->stream));
     s->reset_pending = false;   // the copy rode in this launch (cleared only once it launched)
     return PE_OK;
 }
 
-int build_job_counts(pe_stack* s) { return build_collisions(s, true); }
+int build_job_counts(pe_stack* s, bool defer = false) { return build_collisions(s, true, defer); }
 
 // propertySet cleared values (propertyset.go:159-209): the plan's stopped allocs
 // of the job (terminal ones included, filterAllocs(stopping, false)), less one
@@ -2213,7 +2259,7 @@ int build_psets(pe_stack* s, TgPlan& g) {
     std::vector<const SpreadSpec*> specs;
     for (auto& sp : s->job_spreads) specs.push_back(&sp);
     for (auto& sp : g.spreads) specs.push_back(&sp);
-    if (specs.size() > (size_t)pe::kMaxPsets) { g.unsupported = "more than 4 spread stanzas"; return PE_OK; }
+    if (specs.size() > (size_t)pe::kMaxPsets) { g.unsupported = "more than 8 spread stanzas"; return PE_OK; }
     // computeSpreadInfo once per task group name; weights accumulate (spread.go:254)
     if (!s->spread_info_done.count(g.name)) {
         s->spread_info_done.insert(g.name);
@@ -2276,7 +2322,6 @@ int build_psets(pe_stack* s, TgPlan& g) {
                 if (cl[v]) g.psets_dynamic = true;
             }
         }
-        if (ps->value_str.size() > (size_t)pe::kMaxValues) { g.unsupported = "spread attribute with > 256 values"; return PE_OK; }
         const SpreadSpec* si = info[sp->attribute];
         const double total = (double)g.count;
         std::map<uint32_t, double> desired;
@@ -2316,7 +2361,7 @@ int build_psets(pe_stack* s, TgPlan& g) {
     for (auto& c : s->job_constraints) if (c.op == "distinct_property") dps.emplace_back(&c, true);
     for (auto& c : g.distinct_props) dps.emplace_back(&c, false);
     if (g.psets.size() + dps.size() > (size_t)pe::kMaxPsets) {
-        g.unsupported = "more than 4 spread and distinct_property sets";
+        g.unsupported = "more than 8 spread and distinct_property sets";
         return PE_OK;
     }
     for (auto& dp : dps) {
@@ -2359,7 +2404,6 @@ int build_psets(pe_stack* s, TgPlan& g) {
         } else {
             for (uint32_t c2 = 0; c2 < s->ncls; c2++) by_class[c2] = value_of(s->view(s->class_rep[c2]));
         }
-        if (ps->value_str.size() > (size_t)pe::kMaxValues) { g.unsupported = "distinct_property with > 256 values"; return PE_OK; }
         auto node_val = [&](uint32_t row) { return ps->per_node ? by_node[row] : by_class[s->nodes[row].cls]; };
         ps->h_val_class = by_class;
         ps->h_val_node = by_node;
@@ -2580,7 +2624,7 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         DevMem& bl = task ? g.task_blocked : g.static_blocked;
         HIP_TRY(s, upload_s(s, bl, blocked));
         HIP_TRY(s, gate.ensure(sizeof(uint32_t) * std::max<size_t>(n, 1)));
-        HIP_TRY(s, pe_launch_static_gate(bl.as<uint8_t>(), g.coll_tg.as<uint32_t>(), gate.as<uint32_t>(), (uint32_t)n,
+        HIP_TRY_STATE(s, pe_launch_static_gate(bl.as<uint8_t>(), g.coll_tg.as<uint32_t>(), gate.as<uint32_t>(), (uint32_t)n,
                                          s->stream));
         // PreemptForNetwork's reserved-port step per node, for Selects with Preempt
         std::vector<uint64_t> plist(n);
@@ -2626,8 +2670,28 @@ pe::TgTables tables_of(TgPlan& g) {
         t.pset_nvals[p] = (int)ps.value_str.size();
         t.pset_even[p] = ps.even ? 1 : 0;
         t.pset_weight_frac[p] = ps.weight_frac;
+        // per-value tables set after set (one spare boost entry per set)
+        t.pset_tab_off[p] = t.pset_tab_total;
+        t.pset_cnt_off[p] = t.pset_cnt_total;
+        t.pset_tab_total += (uint32_t)t.pset_nvals[p] + 1u;
+        t.pset_cnt_total += (uint32_t)t.pset_nvals[p];
     }
     return t;
+}
+
+// Bytes of a task group's spread boost table in HBM (the pset_tab_off layout).
+size_t spread_tab_bytes(const TgPlan& g) {
+    size_t v = 0;
+    for (auto& ps : g.psets) v += ps->value_str.size() + 1;
+    return sizeof(double) * std::max<size_t>(v, 1);
+}
+
+// Bytes of the fused count loop's per-value tables (spread boosts + use
+// counts) in LDS, or 0 when they are kept in HBM instead (beyond the budget).
+constexpr size_t kPsetLdsBudget = 48 * 1024;
+size_t pset_lds_bytes(const pe::TgTables& t) {
+    const size_t b = (sizeof(double) * t.pset_tab_total + 4u * t.pset_cnt_total + 15u) & ~(size_t)15u;
+    return b <= kPsetLdsBudget ? b : 0u;
 }
 
 int prepare_tg(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& order, uint32_t start) {
@@ -2677,16 +2741,31 @@ void invalidate_tables(pe_stack* s) {
 }
 
 // Largest overlay (log2 entries) that fits the LDS budget of one workgroup.
-int max_hash_bits(bool full) {
+// Where a FULL k_place keeps its per-value tables: dynamic LDS (A.pset_lds
+// bytes) while they fit the budget, else one HBM set per evaluation.
+int place_pset_tables(pe_stack* s, pe::BatchArgs& A, uint32_t n_evals, DevMem& buf) {
+    A.pset_g_tab = nullptr;
+    A.pset_g_cnt = nullptr;
+    A.pset_lds = (uint32_t)pset_lds_bytes(A.tg);
+    if (A.pset_lds || A.tg.n_psets == 0) return PE_OK;
+    const size_t tb = sizeof(double) * A.tg.pset_tab_total * (size_t)n_evals;
+    const size_t cb = 4u * A.tg.pset_cnt_total * (size_t)n_evals;
+    HIP_TRY(s, buf.ensure(tb + cb));
+    A.pset_g_tab = buf.as<double>();
+    A.pset_g_cnt = reinterpret_cast<uint32_t*>(buf.as<unsigned char>() + tb);
+    return PE_OK;
+}
+
+int max_hash_bits(bool full, size_t pset_bytes) {
     int bits = 12;
-    while (bits > 6 && pe_place_lds_bytes(full, bits, false) > 96 * 1024) bits--;
+    while (bits > 6 && pe_place_lds_bytes(full, bits, false, pset_bytes) > 96 * 1024) bits--;
     return bits;
 }
 
-int hash_bits_for(uint32_t count, bool full) {
+int hash_bits_for(uint32_t count, bool full, size_t pset_bytes) {
     int bits = 6;
     while (bits < 30 && (1u << bits) < 2u * std::max<uint32_t>(count, 1)) bits++;
-    return std::min(bits, max_hash_bits(full));
+    return std::min(bits, max_hash_bits(full, pset_bytes));
 }
 
 // Count bits of a packed windowed-kernel overlay entry (row << kbits | k), or 0
@@ -2800,7 +2879,7 @@ int sweep_setup(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_t 
         A.penalty_bits = s->d_penalty.as<uint32_t>();
     }
     if (!g.psets.empty()) {
-        HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
+        HIP_TRY(s, s->d_spread_tab.ensure(spread_tab_bytes(g)));
         A.spread_tab = s->d_spread_tab.as<double>();
     }
     if (!g.aux_valid) {
@@ -3075,7 +3154,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
         P.penalty_bits = s->d_penalty.as<uint32_t>();
     }
     if (!g.psets.empty()) {
-        HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
+        HIP_TRY(s, s->d_spread_tab.ensure(spread_tab_bytes(g)));
         HIP_TRY(s, pe_launch_spread_table(&P.tg, s->d_spread_tab.as<double>(), s->stream));
         P.spread_tab = s->d_spread_tab.as<double>();
     }
@@ -3180,7 +3259,11 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         HIP_TRY(s, upload_s(s, s->d_penalty, bits));
         A.penalty_bits = s->d_penalty.as<uint32_t>();
     }
-    A.hash_bits = hash_bits_for(count, full);
+    if (full) {
+        const int rc = place_pset_tables(s, A, 1, s->d_pset_g);
+        if (rc) return rc;
+    }
+    A.hash_bits = hash_bits_for(count, full, A.pset_lds);
     A.packed_overlay = packed_kbits(s, 1u << A.hash_bits, full);
     bool chain = false;
     // the phase-static chain is compiled without reserved cores (k_chain's registers)
@@ -3271,6 +3354,10 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         if (fused) {
             A.fused = 1;
             A.base1 = nullptr;   // later phases re-evaluate rows holding placements
+            if (s->counts_pending) {   // SetJob's counts ride in this launch
+                A.counts = s->pending_counts;
+                s->counts_pending = false;
+            }
         }
         const size_t cap = std::min(count, chunk);
         HIP_TRY(s, s->d_emit.ensure(sizeof(pe::ChainEmit) * cap));
@@ -3504,6 +3591,7 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
     if (const char* e = std::getenv("PE_WINDOW_LAZY")) s->use_base = std::atoi(e) == 0;
     if (const char* e = std::getenv("PE_SPECULATE")) s->spec_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_SPIN_WAIT")) s->spin_wait = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PE_COUNTS_DEFER")) s->counts_defer_ok = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_API_PROF")) s->api_prof = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_KERNEL_SPLIT")) s->kernel_split = std::atoi(e) != 0;
     if (const char* e = std::getenv("PE_TEST_FALLBACK_EVERY")) s->test_fallback_every = std::strtoull(e, nullptr, 10);
@@ -3731,6 +3819,7 @@ static void elig_visit_list(pe_stack* s, uint32_t tgi, const std::vector<uint32_
 static int set_state_one(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
     if (!s || !strs || !nodes) return PE_EINVAL;
     spec_drop(s);
+    s->counts_pending = false;   // a new snapshot: its arrays are rebuilt (the job's counts by the next SetJob)
     s->node_update.clear();   // a new evaluation context: no plan stops
     s->stop_count.clear();
     s->gen++;
@@ -3762,6 +3851,10 @@ static int update_allocs_one(pe_stack* s, const pe_strtab* strs, const pe_alloc_
     if (!s || !allocs) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
+    {
+        const int frc = flush_counts(s);   // before any array is resized
+        if (frc) return frc;
+    }
     s->node_update.clear();   // a new evaluation context: no plan stops
     s->stop_count.clear();
     s->gen++;
@@ -3800,6 +3893,10 @@ static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_ta
     if (!s || !nodes) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
+    {
+        const int frc = flush_counts(s);   // before any array is resized
+        if (frc) return frc;
+    }
     s->node_update.clear();   // a new evaluation context: no plan stops
     s->stop_count.clear();
     s->gen++;
@@ -4047,7 +4144,7 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
         s->job_key = it == s->job_keys.end() ? PE_NONE : it->second;
     }
     s->offer_row = -1;
-    return build_job_counts(s);
+    return build_job_counts(s, true);
 }
 
 int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
@@ -4259,7 +4356,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         }
         const double* stab = nullptr;
         if (t.n_spread > 0) {
-            HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
+            HIP_TRY(s, s->d_spread_tab.ensure(spread_tab_bytes(g)));
             HIP_TRY(s, pe_launch_spread_table(&t, s->d_spread_tab.as<double>(), s->stream));
             stab = s->d_spread_tab.as<double>();
         }
@@ -4279,7 +4376,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             P.penalty_bits = pbits;
             P.spread_tab = stab;
             if (!stab && !g.psets.empty()) {
-                HIP_TRY(s, s->d_spread_tab.ensure(sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1)));
+                HIP_TRY(s, s->d_spread_tab.ensure(spread_tab_bytes(g)));
                 HIP_TRY(s, pe_launch_spread_table(&P.tg, s->d_spread_tab.as<double>(), s->stream));
                 P.spread_tab = s->d_spread_tab.as<double>();
             }
@@ -5323,6 +5420,10 @@ static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* op
 
 // Copies between the live dynamic columns and the checkpoint (to_ckpt: save).
 static int spec_copy(pe_stack* s, TgPlan& g, bool to_ckpt) {
+    {
+        const int frc = flush_counts(s);   // the checkpoint copies the count arrays
+        if (frc) return frc;
+    }
     const size_t n = s->nodes.size();
     auto cp = [&](DevMem& live, DevMem& ck, size_t bytes) -> hipError_t {
         if (!bytes || !live.p) return hipSuccess;
@@ -5828,7 +5929,11 @@ int prepare_batch(pe_stack* s, uint32_t tgi, uint32_t count) {
     pe::BatchArgs A = batch_args(s, g);
     s->limit = saved_limit;
     const bool full = !g.psets.empty() || lim >= n;
-    A.hash_bits = hash_bits_for(count, full);
+    if (full) {
+        const int prc = place_pset_tables(s, A, E, s->d_pset_gb);   // kept with batch_A
+        if (prc) return prc;
+    }
+    A.hash_bits = hash_bits_for(count, full, A.pset_lds);
     A.packed_overlay = packed_kbits(s, count, full);
     if ((1u << A.hash_bits) < 2u * count)
         return s->fail(PE_EUNSUPPORTED, "count too large for the per-eval LDS overlay in batch mode");
@@ -6513,7 +6618,10 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
     for (uint32_t k = 0; k < N; k++) {
         pe_stack* x = st[k];
         HIP_TRY(s, hipSetDevice(x->device));
-        int rc = prepare_tg(x, tgi, x->visit, x->offset);
+        int rc = flush_counts(x);   // the launches below check the root's pending state only
+        if (!rc && x->reset_pending) rc = flush_reset(x);
+        if (rc) return k ? s->fail(rc, "replica: " + x->err) : rc;
+        rc = prepare_tg(x, tgi, x->visit, x->offset);
         if (rc) return k ? s->fail(rc, "replica: " + x->err) : rc;
         x->limit = 0x7FFFFFFF;
         uint32_t b_unused = 0;
@@ -6638,7 +6746,10 @@ static int multi_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint
     for (uint32_t k = 0; k < N; k++) {
         pe_stack* x = st[k];
         HIP_TRY(s, hipSetDevice(x->device));
-        int rc = prepare_tg(x, tgi, x->visit, 0);
+        int rc = flush_counts(x);   // the launches below check the root's pending state only
+        if (!rc && x->reset_pending) rc = flush_reset(x);
+        if (rc) return k ? s->fail(rc, "replica: " + x->err) : rc;
+        rc = prepare_tg(x, tgi, x->visit, 0);
         if (rc) return k ? s->fail(rc, "replica: " + x->err) : rc;
         TgPlan& g = *x->tgs[tgi];
         HIP_TRY(s, upload_visit(x, x->visit));

@@ -7,8 +7,12 @@
 
 namespace pe {
 
-constexpr int kMaxPsets = 4;          // spread property sets handled on device
-constexpr int kMaxValues = 256;       // distinct values per spread property on device
+constexpr int kMaxPsets = 8;          // spread + distinct_property sets of a task group on the device
+// Per-value tables (spread boosts, use counts) are laid out set after set
+// (TgTables::pset_tab_off / pset_cnt_off), so a set may hold any number of
+// values. Kernels stage them in LDS while they fit kLdsPsetValues entries in
+// all and read them from HBM otherwise.
+constexpr int kLdsPsetValues = 2048;
 constexpr uint32_t kMissing = 0xFFFFFFFFu;   // node has no value for the property
 constexpr int32_t kDynPortCapacity = 32000 - 20000 + 1;   // IndexesInRange is inclusive
 constexpr int kMaxSkip = 3;           // stack.go:17 maxSkip
@@ -101,6 +105,10 @@ struct TgTables {
     int pset_nvals[kMaxPsets];
     int pset_even[kMaxPsets];                    // no targets: evenSpreadScoreBoost
     double pset_weight_frac[kMaxPsets];          // float64(weight) / float64(sumSpreadWeights)
+    // table layout: set p's boosts at spread table entries [tab_off[p], tab_off[p] + nvals + 1)
+    // (one spare entry per set), its counts at [cnt_off[p], cnt_off[p] + nvals)
+    uint32_t pset_tab_off[kMaxPsets], pset_cnt_off[kMaxPsets];
+    uint32_t pset_tab_total, pset_cnt_total;
     // devices (only when the task group requests devices, else null)
     uint32_t* dev_free;                          // [n] free healthy instances per group, 4 x u8
     const DevClass* dev_cls;                     // [ncls]
@@ -153,6 +161,17 @@ struct ResetArgs {
     uint32_t keys;
 };
 
+// SetJob's collision counts (and a deferred ResetPlan copy) as a launch
+// carries them: the k_counts launch, or the fused k_chain of a short list
+// (BatchArgs::counts, nd 0: none)
+struct CountArgs {
+    CountDsts D;
+    uint32_t nd, n;
+    const uint2* ents;            // sorted (row << 5 | array, count), possibly in the mapped staging ring
+    uint32_t m;
+    ResetArgs R;
+};
+
 // Select result as k_emit hands it to the host: the leading fields of
 // pe_ranked_node (row .. new_offset, byte-identical) and the device offers;
 // the host widens it (no preemptions or reserved cores on the chain path).
@@ -177,6 +196,12 @@ struct FoldArgs {
 // One launch = n_evals independent evaluations (one workgroup each) of the same
 // task group over the same snapshot; eval e visits perms + e*perm_stride.
 struct BatchArgs {
+    // FULL k_place: the per-value tables in HBM, one set per evaluation
+    // (pset_tab_total doubles / pset_cnt_total counts each), when they exceed
+    // the LDS budget; null: in dynamic LDS (pset_lds bytes)
+    double* pset_g_tab;
+    uint32_t* pset_g_cnt;
+    uint32_t pset_lds;
     NodeSoA soa;
     TgTables tg;
     Ask ask;
@@ -224,6 +249,7 @@ struct BatchArgs {
     // by relative position (one thread per Select walks its own positions)
     double* chain_vs;
     FoldArgs fold;                // a fold carried by this launch (fold.feas null: none)
+    CountArgs counts;             // SetJob's counts carried by a fused k_chain (counts.nd 0: none)
     // Short lists, one evaluation: k_chain alone (no k_base / k_emit /
     // k_emit_writeback launches) evaluates the first phase's positions itself,
     // builds the records, writes the placements back and raises done_flag[0]

@@ -254,7 +254,7 @@ __device__ __forceinline__ bool distinct_ok(const TgTables& t, const double* tab
     for (int p = t.n_spread; p < t.n_psets; p++) {
         const uint32_t v = pset_value(t, p, row, c);
         if (v == kMissing) return false;
-        const bool blocked = tab ? tab[p * (kMaxValues + 1) + v] != 0.0 : t.pset_counts[p][v] >= t.pset_allowed[p];
+        const bool blocked = tab ? tab[t.pset_tab_off[p] + v] != 0.0 : t.pset_counts[p][v] >= t.pset_allowed[p];
         if (blocked) return false;
     }
     return true;
@@ -341,7 +341,7 @@ __device__ __forceinline__ void lookup_scores(const TgTables& t, const uint32_t*
     double total = 0.0;
     for (int p = 0; p < t.n_spread; p++) {
         const uint32_t v = pset_value(t, p, row, c);
-        total += (v == kMissing) ? -1.0 : spread_tab[p * (kMaxValues + 1) + v];
+        total += (v == kMissing) ? -1.0 : spread_tab[t.pset_tab_off[p] + v];
     }
     si->spread = total;
 }
@@ -536,29 +536,45 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
 }
 
 // evenSpreadScoreBoost (spread.go:178-228) / target boost (spread.go:143-164)
-// per value of each property set, from the eval's LDS use counts.
+// per value of each property set, from the eval's use counts: `counts` in the
+// pset_cnt_off layout (an LDS copy, or the loop's own counts), or null to read
+// each set's HBM counts. `tab` in the pset_tab_off layout.
 template <int BLOCK>
 __device__ void build_spread_table(const TgTables& t, const uint32_t* counts, double* tab, uint32_t* scratch) {
     const int tid = threadIdx.x;
     for (int p = 0; p < t.n_psets; p++) {
         const int nv = t.pset_nvals[p];
-        const uint32_t* cnt = counts + p * kMaxValues;
+        const uint32_t* cnt = counts ? counts + t.pset_cnt_off[p] : t.pset_counts[p];
+        double* tb = tab + t.pset_tab_off[p];
         if (p >= t.n_spread) {   // distinct_property: 1.0 marks a value at its allowed count
-            for (int v = tid; v < nv; v += BLOCK) tab[p * (kMaxValues + 1) + v] = cnt[v] >= t.pset_allowed[p] ? 1.0 : 0.0;
+            for (int v = tid; v < nv; v += BLOCK) tb[v] = cnt[v] >= t.pset_allowed[p] ? 1.0 : 0.0;
             continue;
         }
         if (t.pset_even[p]) {
-            if (tid == 0) {
-                uint32_t mn = 0, mx = 0, present = 0;
-                for (int v = 0; v < nv; v++) {
-                    const uint32_t x = cnt[v];
-                    if (x == 0) continue;
-                    present++;
-                    if (mn == 0 || x < mn) mn = x;
-                    if (mx == 0 || x > mx) mx = x;
-                }
-                scratch[0] = mn; scratch[1] = mx; scratch[2] = present;
+            // min / max / number of the used values (any count of values: a
+            // block reduction, the same integers as the reference's map walk)
+            uint32_t lmn = 0xFFFFFFFFu, lmx = 0, lpr = 0;
+            for (int v = tid; v < nv; v += BLOCK) {
+                const uint32_t x = cnt[v];
+                if (x == 0) continue;
+                lpr++;
+                lmn = x < lmn ? x : lmn;
+                lmx = x > lmx ? x : lmx;
             }
+            for (int off = 32; off > 0; off >>= 1) {
+                lmn = min(lmn, (uint32_t)__shfl_xor((int)lmn, off));
+                lmx = max(lmx, (uint32_t)__shfl_xor((int)lmx, off));
+                lpr += (uint32_t)__shfl_xor((int)lpr, off);
+            }
+            if (tid == 0) { scratch[0] = 0xFFFFFFFFu; scratch[1] = 0; scratch[2] = 0; }
+            __syncthreads();
+            if ((tid & 63) == 0) {
+                atomicMin(&scratch[0], lmn);
+                atomicMax(&scratch[1], lmx);
+                atomicAdd(&scratch[2], lpr);
+            }
+            __syncthreads();
+            if (tid == 0 && scratch[2] == 0) { scratch[0] = 0; }   // no used value: min = max = 0
             __syncthreads();
             const uint32_t mn = scratch[0], mx = scratch[1], present = scratch[2];
             for (int v = tid; v < nv; v += BLOCK) {
@@ -574,7 +590,7 @@ __device__ void build_spread_table(const TgTables& t, const uint32_t* counts, do
                     else if (mn == 0) b = 1.0;
                     else b = (double)(int)(mx - mn) / (double)mn;
                 }
-                tab[p * (kMaxValues + 1) + v] = b;
+                tb[v] = b;
             }
             __syncthreads();
         } else {
@@ -586,7 +602,7 @@ __device__ void build_spread_table(const TgTables& t, const uint32_t* counts, do
                     const double used = (double)(cnt[v] + 1u);
                     b = ((desired - used) / desired) * t.pset_weight_frac[p];
                 }
-                tab[p * (kMaxValues + 1) + v] = b;
+                tb[v] = b;
             }
         }
     }
@@ -693,7 +709,7 @@ __device__ __forceinline__ void commit_overlay(const NodeSoA& s, const TgTables&
         const uint32_t c = s.rec[row].cls;
         for (int p = 0; p < t.n_psets; p++) {
             const uint32_t v = pset_value(t, p, row, c);
-            if (v != kMissing) counts[p * kMaxValues + v] += 1;
+            if (v != kMissing) counts[t.pset_cnt_off[p] + v] += 1;
         }
     }
 }
@@ -882,7 +898,7 @@ __device__ void writeback_overlay(const BatchArgs& A, const Overlay& ov, uint32_
     if constexpr (FULL) {
         for (int q = 0; q < A.tg.n_psets; q++)
             for (int v = threadIdx.x; v < A.tg.pset_nvals[q]; v += BLOCK)
-                A.tg.pset_counts[q][v] = counts[q * kMaxValues + v];
+                A.tg.pset_counts[q][v] = counts[A.tg.pset_cnt_off[q] + v];
     }
 }
 
@@ -902,10 +918,14 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
     double* spread_tab = nullptr;
     uint32_t* counts = nullptr;
     if constexpr (FULL) {
-        spread_tab = reinterpret_cast<double*>(p);
-        p += sizeof(double) * kMaxPsets * (kMaxValues + 1);
-        counts = reinterpret_cast<uint32_t*>(p);
-        p += sizeof(uint32_t) * kMaxPsets * kMaxValues;
+        if (A.pset_g_tab) {   // tables beyond the LDS budget: this evaluation's HBM copy
+            spread_tab = A.pset_g_tab + (size_t)e * A.tg.pset_tab_total;
+            counts = A.pset_g_cnt + (size_t)e * A.tg.pset_cnt_total;
+        } else {
+            spread_tab = reinterpret_cast<double*>(p);
+            counts = reinterpret_cast<uint32_t*>(p + sizeof(double) * A.tg.pset_tab_total);
+            p += A.pset_lds;
+        }
     }
     Overlay ov;
     ov.bits = A.hash_bits;
@@ -915,7 +935,7 @@ __global__ void __launch_bounds__(BLOCK) k_place(BatchArgs A) {
     for (uint32_t i = tid; i < H; i += BLOCK) ov.keys[i] = kEmpty;
     if constexpr (FULL) {
         for (int q = 0; q < A.tg.n_psets; q++)
-            for (int v = tid; v < A.tg.pset_nvals[q]; v += BLOCK) counts[q * kMaxValues + v] = A.tg.pset_counts[q][v];
+            for (int v = tid; v < A.tg.pset_nvals[q]; v += BLOCK) counts[A.tg.pset_cnt_off[q] + v] = A.tg.pset_counts[q][v];
     }
     __syncthreads();
 
@@ -1569,6 +1589,38 @@ __device__ __noinline__ void chain_walk(Sh& sh, const uint16_t* nb, const double
     }
 }
 
+// Per-node count arrays from a sorted sparse list (key = row << 5 | array,
+// value = count): each thread owns one row, zeroes it in every array and
+// writes the row's entries found by binary search. A deferred ResetPlan (R.rec)
+// rides along: its arrays are disjoint from the counts.
+// `first` / `stride`: this thread's first index and the launch's thread count.
+__device__ __forceinline__ void counts_apply(const CountDsts& D, uint32_t nd, uint32_t n, const uint2* ents,
+                                             uint32_t m, const ResetArgs& R, uint32_t first, uint32_t stride) {
+    if (R.rec) {
+        for (uint32_t i = first; i < R.n; i += stride) {
+            R.rec[i] = R.base_rec[i];
+            R.dev_free[i] = R.dev_free_base[i];
+        }
+        for (uint32_t i = first; i < R.m; i += stride) R.preempted[i] = 0;
+        for (uint32_t i = first; i < R.keys; i += stride) R.pcount[i] = 0;
+    }
+    for (uint32_t row = first; row < n; row += stride) {
+        uint32_t lo = 0, hi = m;
+        const uint32_t k0 = row << 5;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ents[mid].x < k0) lo = mid + 1;
+            else hi = mid;
+        }
+        for (uint32_t d = 0; d < nd; d++) {
+            if (!D.d[d]) continue;
+            uint32_t v = 0;
+            if (lo < m && ents[lo].x == (k0 | d)) v = ents[lo++].y;
+            D.d[d][row] = v;
+        }
+    }
+}
+
 // FUSED (short lists of one evaluation, BatchArgs::fused): no k_base, k_emit
 // or k_emit_writeback launch; the kernel carries the fold (FoldArgs), evaluates
 // its first phase's positions itself (storing them as the base table of the
@@ -1605,6 +1657,13 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
 
     uint64_t prof_t = A.prof ? __builtin_readcyclecounter() : 0;
     int prof_ph = 0;   // profile slot group: phase (capped at 3)
+    if (FUSED && A.counts.nd) {
+        // SetJob's collision counts (and the deferred ResetPlan copy) carried
+        // by this launch instead of a k_counts launch of their own
+        const CountArgs& C = A.counts;
+        counts_apply(C.D, C.nd, C.n, C.ents, C.m, C.R, (uint32_t)tid, kChainBlock);
+        __syncthreads();
+    }
     if (FUSED && A.fold.feas) {
         // the FeasibilityWrapper fold of every row, before any evaluation
         __shared__ uint8_t fcls[FUSED ? kFusedMaxClasses : 1];
@@ -2501,7 +2560,7 @@ __device__ __forceinline__ void sweep_block(const SweepArgs& A) {
         for (int i = tid; i < kAuxValues; i += BLOCK) aff_lds[i] = A.aff_vals[i];
         for (int p = 0; p < A.tg.n_psets; p++)
             for (int i = tid; i < kAuxValues; i += BLOCK)
-                sp_lds[p][i] = i < A.tg.pset_nvals[p] ? A.spread_tab[p * (kMaxValues + 1) + i] : 0.0;
+                sp_lds[p][i] = i < A.tg.pset_nvals[p] ? A.spread_tab[A.tg.pset_tab_off[p] + i] : 0.0;
         __syncthreads();
     }
     const uint32_t n = A.n_visit;
@@ -2664,12 +2723,14 @@ __global__ void __launch_bounds__(512) k_sweep_merge(const SweepRec* recs, uint3
 // Spread contribution table in HBM for the sweep path (same code as the
 // persistent loop's LDS table, so both paths are bit-identical).
 __global__ void __launch_bounds__(256) k_spread_table(TgTables t, double* tab) {
-    __shared__ uint32_t counts[kMaxPsets * kMaxValues];
+    __shared__ uint32_t counts[kLdsPsetValues];
     __shared__ uint32_t scratch[4];
-    for (int p = 0; p < t.n_psets; p++)
-        for (int v = threadIdx.x; v < t.pset_nvals[p]; v += 256) counts[p * kMaxValues + v] = t.pset_counts[p][v];
+    const bool lds = t.pset_cnt_total <= (uint32_t)kLdsPsetValues;   // else the HBM counts
+    if (lds)
+        for (int p = 0; p < t.n_psets; p++)
+            for (int v = threadIdx.x; v < t.pset_nvals[p]; v += 256) counts[t.pset_cnt_off[p] + v] = t.pset_counts[p][v];
     __syncthreads();
-    build_spread_table<256>(t, counts, tab, scratch);
+    build_spread_table<256>(t, lds ? counts : nullptr, tab, scratch);
 }
 
 // Score parts of the winner straight into its record (eval_node<true> with
@@ -2702,7 +2763,7 @@ __global__ void k_node_record(SweepArgs A, uint32_t row, pe_ranked_node* out) {
 // ended the loop (later steps do nothing); state[1]: placements so far.
 __device__ __forceinline__ void step_block(const SweepArgs& A, uint32_t nrecs, const uint32_t* visit, uint32_t n,
                                            uint32_t offset, pe_ranked_node* out, uint32_t* state) {
-    __shared__ uint32_t counts[kMaxPsets * kMaxValues];
+    __shared__ uint32_t counts[kLdsPsetValues];
     __shared__ uint32_t scratch[4];
     __shared__ SweepRec red[4];
     __shared__ uint32_t go;
@@ -2747,10 +2808,12 @@ __device__ __forceinline__ void step_block(const SweepArgs& A, uint32_t nrecs, c
     __syncthreads();
     if (!go) return;   // workgroup-uniform
     const TgTables& t = A.tg;
-    for (int p = 0; p < t.n_psets; p++)
-        for (int v = threadIdx.x; v < t.pset_nvals[p]; v += 256) counts[p * kMaxValues + v] = t.pset_counts[p][v];
+    const bool lds = t.pset_cnt_total <= (uint32_t)kLdsPsetValues;   // else the HBM counts
+    if (lds)
+        for (int p = 0; p < t.n_psets; p++)
+            for (int v = threadIdx.x; v < t.pset_nvals[p]; v += 256) counts[t.pset_cnt_off[p] + v] = t.pset_counts[p][v];
     __syncthreads();
-    build_spread_table<256>(t, counts, const_cast<double*>(A.spread_tab), scratch);
+    build_spread_table<256>(t, lds ? counts : nullptr, const_cast<double*>(A.spread_tab), scratch);
 }
 
 __global__ void __launch_bounds__(256) k_sweep_step(SweepArgs A, uint32_t nrecs, const uint32_t* visit, uint32_t n,
@@ -2808,9 +2871,10 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
     extern __shared__ double ent_sum[];                                    // [kFullCap] score_head sums
     uint32_t* ent_meta = reinterpret_cast<uint32_t*>(ent_sum + kFullCap);   // status | k << 2 | spread values
     uint32_t* ent_pos = ent_meta + kFullCap;                                // visit position
-    __shared__ double tab[kAuxPsets * (kMaxValues + 1)];
-    __shared__ double desired[kAuxPsets * kMaxValues];
-    __shared__ uint32_t counts[kAuxPsets * kMaxValues];
+    // the pset_tab_off / pset_cnt_off layout of at most kAuxPsets sets of < kAuxValues values
+    __shared__ double tab[kAuxPsets * (kAuxValues + 1)];
+    __shared__ double desired[kAuxPsets * kAuxValues];
+    __shared__ uint32_t counts[kAuxPsets * kAuxValues];
     __shared__ double aff_lds[kAuxValues];
     __shared__ double red_s[kFullWaves];
     __shared__ uint32_t red_r[kFullWaves];
@@ -2831,8 +2895,8 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
     if (tid == 0) sh_m = 0;
     for (int p = 0; p < np; p++)
         for (int v = tid; v < t.pset_nvals[p]; v += kFullThreads) {
-            counts[p * kMaxValues + v] = t.pset_counts[p][v];
-            desired[p * kMaxValues + v] = t.pset_even[p] ? 0.0 : t.pset_desired[p][v];
+            counts[t.pset_cnt_off[p] + v] = t.pset_counts[p][v];
+            desired[t.pset_cnt_off[p] + v] = t.pset_even[p] ? 0.0 : t.pset_desired[p][v];
         }
     __syncthreads();
     if (np) build_spread_table<kFullThreads>(t, counts, tab, scratch);
@@ -2841,7 +2905,7 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
 #pragma unroll
         for (int p = 0; p < np; p++) {
             const uint32_t v = (meta >> (8 + 8 * p)) & 255u;
-            sp += (v == kAuxMissing) ? -1.0 : tab[p * (kMaxValues + 1) + v];
+            sp += (v == kAuxMissing) ? -1.0 : tab[t.pset_tab_off[p] + v];
         }
         return sp;
     };
@@ -3070,12 +3134,12 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
                 for (int p = 0; p < np; p++) {
                     const uint32_t v = (meta0 >> (8 + 8 * p)) & 255u;
                     if (v == kAuxMissing) continue;
-                    const uint32_t c = ++counts[p * kMaxValues + v];
+                    const uint32_t c = ++counts[t.pset_cnt_off[p] + v];
                     if (fast) t.pset_counts[p][v] = c;
                     if (!t.pset_even[p]) {       // build_spread_table's target boost of this value
-                        const double d = desired[p * kMaxValues + v];
-                        tab[p * (kMaxValues + 1) + v] = d != d ? -1.0 : ((d - (double)(c + 1u)) / d) *
-                                                                        t.pset_weight_frac[p];
+                        const double d = desired[t.pset_cnt_off[p] + v];
+                        tab[t.pset_tab_off[p] + v] = d != d ? -1.0 : ((d - (double)(c + 1u)) / d) *
+                                                                     t.pset_weight_frac[p];
                     }
                 }
                 state[1] = it + 1;
@@ -3107,7 +3171,7 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
     // the HBM table the next Select starts from
     for (int p = 0; p < np; p++)
         for (int v = tid; v < t.pset_nvals[p]; v += kFullThreads)
-            const_cast<double*>(A.spread_tab)[p * (kMaxValues + 1) + v] = tab[p * (kMaxValues + 1) + v];
+            const_cast<double*>(A.spread_tab)[t.pset_tab_off[p] + v] = tab[t.pset_tab_off[p] + v];
 }
 
 // Grid-wide barrier of the persistent count loop (every workgroup resident;
@@ -3187,30 +3251,7 @@ __global__ void __launch_bounds__(256) k_upload(unsigned char* dst, const unsign
 // rides in the same launch: its arrays are disjoint from the counts.
 __global__ void __launch_bounds__(256) k_counts(CountDsts D, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
                                                 ResetArgs R) {
-    const uint32_t stride = gridDim.x * 256;
-    if (R.rec) {
-        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < R.n; i += stride) {
-            R.rec[i] = R.base_rec[i];
-            R.dev_free[i] = R.dev_free_base[i];
-        }
-        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < R.m; i += stride) R.preempted[i] = 0;
-        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < R.keys; i += stride) R.pcount[i] = 0;
-    }
-    for (uint32_t row = blockIdx.x * 256 + threadIdx.x; row < n; row += stride) {
-        uint32_t lo = 0, hi = m;
-        const uint32_t k0 = row << 5;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (ents[mid].x < k0) lo = mid + 1;
-            else hi = mid;
-        }
-        for (uint32_t d = 0; d < nd; d++) {
-            if (!D.d[d]) continue;
-            uint32_t v = 0;
-            if (lo < m && ents[lo].x == (k0 | d)) v = ents[lo++].y;
-            D.d[d][row] = v;
-        }
-    }
+    counts_apply(D, nd, n, ents, m, R, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256);
 }
 
 // ResetPlan in one launch: the proposed state back to the snapshot (node
@@ -3291,15 +3332,15 @@ __global__ void __launch_bounds__(256) k_static_gate(const uint8_t* blocked, con
 // ---- launch wrappers (host) ------------------------------------------------
 hipError_t pe_launch_static_gate(const uint8_t* blocked, const uint32_t* coll_tg, uint32_t* gate, uint32_t n,
                                  hipStream_t st);
-size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed) {
+size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed, size_t pset_bytes) {
     size_t b = (size_t)(packed ? 4u : 8u) * ((size_t)1 << hash_bits);
-    if (full) b += sizeof(double) * pe::kMaxPsets * (pe::kMaxValues + 1) + 4u * pe::kMaxPsets * pe::kMaxValues;
+    if (full) b += pset_bytes;
     return b;
 }
 
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st) {
     if (full && a->packed_overlay) return hipErrorInvalidValue;   // packed entries: windowed kernel only
-    const size_t lds = pe_place_lds_bytes(full, a->hash_bits, a->packed_overlay != 0);
+    const size_t lds = pe_place_lds_bytes(full, a->hash_bits, a->packed_overlay != 0, a->pset_lds);
     if (full) {
         // few evaluations: 1024-lane workgroups keep more rows in flight per pass
         // reserved cores are a separate instantiation (their code costs the others registers)

@@ -22,8 +22,10 @@
 // groups) is replaced by a fixed order: allocs by ascending id (state table
 // order, then plan order), device groups in node order.
 // sort.Slice is Go 1.16's quickSort_func (go.mod: go 1.16), restated below.
-// Out of the oracle's scope (returns PE_EUNSUPPORTED): network preemption
-// (PreemptForNetwork), reserved cores, CSI volumes, static reserved port asks.
+// Modelled as the reference does: PreemptForNetwork (bandwidth, dynamic and
+// static ports), reserved cores, static reserved port asks, nodes and
+// preempted lists of any length (pe_preempted_of). Out of the oracle's scope
+// (returns PE_EUNSUPPORTED): CSI volumes.
 #include "oracle.h"
 #include "gomath.h"
 #include "semantics.h"

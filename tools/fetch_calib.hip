@@ -90,6 +90,14 @@ __global__ void __launch_bounds__(64) c_rows4(const uint32_t* col, uint32_t rows
     keep(acc, sink);
 }
 
+// 8-byte values read in order (k_chain's base / base1 by visit position)
+__global__ void __launch_bounds__(64) c_rows8(const double* col, uint32_t rows, uint32_t* sink) {
+    const uint32_t stride = gridDim.x * 64;
+    double acc = 0.0;
+    for (uint32_t t = blockIdx.x * 64 + threadIdx.x; t < rows; t += stride) acc += col[t];
+    keep(acc == 12345.678 ? 0xDEADBEEFu : 0u, sink);
+}
+
 // 8-byte values stored in order / scattered through the permutation
 __global__ void __launch_bounds__(64) c_store8(double* dst, uint32_t rows) {
     const uint32_t stride = gridDim.x * 64;
@@ -131,6 +139,7 @@ int main(int argc, char** argv) {
         c_gather64<true><<<blocks(2 * rows), 64>>>((const Rec64*)d_tab, (const uint32_t*)d_perm, rows, sink);
         c_gather4<<<blocks(rows), 64>>>((const uint32_t*)d_col, (const uint32_t*)d_perm, rows, sink);
         c_rows4<<<blocks(rows), 64>>>((const uint32_t*)d_col, rows, sink);
+        c_rows8<<<blocks(rows), 64>>>((const double*)d_out, rows, sink);
         c_store8<<<blocks(rows), 64>>>((double*)d_out, rows);
         c_scatter8<<<blocks(rows), 64>>>((double*)d_out, (const uint32_t*)d_perm, rows);
         CK(hipDeviceSynchronize());
@@ -138,10 +147,10 @@ int main(int argc, char** argv) {
     // unique bytes per pattern (reads / writes)
     std::printf("{\"rows\": %u, \"unique\": {\"c_stream16\": [%llu, 0], \"c_rows64\": [%llu, 0], "
                 "\"c_gather64<false>\": [%llu, 0], \"c_gather64<true>\": [%llu, 0], \"c_gather4\": [%llu, 0], "
-                "\"c_rows4\": [%llu, 0], \"c_store8\": [0, %llu], \"c_scatter8\": [%llu, %llu]}}\n",
+                "\"c_rows4\": [%llu, 0], \"c_rows8\": [%llu, 0], \"c_store8\": [0, %llu], \"c_scatter8\": [%llu, %llu]}}\n",
                 rows, (unsigned long long)n16 * 16, (unsigned long long)rows * 64,
                 (unsigned long long)rows * 68, (unsigned long long)rows * 68, (unsigned long long)rows * 8,
-                (unsigned long long)rows * 4, (unsigned long long)rows * 8, (unsigned long long)rows * 4,
-                (unsigned long long)rows * 8);
+                (unsigned long long)rows * 4, (unsigned long long)rows * 8, (unsigned long long)rows * 8,
+                (unsigned long long)rows * 4, (unsigned long long)rows * 8);
     return 0;
 }

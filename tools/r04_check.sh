@@ -32,3 +32,17 @@ if [ -n "$AB_LIBS" ]; then   # A/B of engine builds: the C5 loop (tools/c5_prof.
   done
   unset PE_ENGINE_LIB
 fi
+if [ -n "$CHAIN_PROF" ]; then   # k_chain per-step clock profile of the C2 loop
+  timeout -k 10 200 python -u tools/chain_prof.py > "$OUT/chain_prof.txt" 2>&1 || { tail -20 "$OUT/chain_prof.txt"; exit 1; }
+  tail -12 "$OUT/chain_prof.txt"
+fi
+if [ -n "$C1_TRACE" ]; then   # device timeline of the C1 evaluation loop
+  cd /tmp
+  export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c1trace" -o c1 -- \
+    python3 "$ROOT/bench.py" --no-cpu --steps 3 --warmup 1 --sweep-nodes 0 --sections c1 > "$OUT/c1trace.log" 2>&1
+  cd "$ROOT"
+  T=$(find "$OUT/c1trace" -name "*kernel_trace.csv" -print -quit)
+  python3 tools/timeline.py "$T" k_chain 4 > "$OUT/c1_timeline.txt" || true
+  tail -24 "$OUT/c1_timeline.txt"
+fi
