@@ -7,9 +7,12 @@ service job (cpu 500 / mem 256 / disk 150), limit = ceil(log2 n) = 14.
 A step = one evaluation driven exactly as the unchanged Go caller drives a
 Stack (GenericScheduler.computePlacements, generic_sched.go:472-652): ResetPlan
 (fresh EvalContext), SetJob, SetNodes(a shuffled node list), then 1000 x
-(pe_select with empty options, pe_commit of the option). The loop runs in C
+(Select with empty options, Commit of the option). The loop runs in C
 (tools/libdropin.so, the cgo caller's shape) against the C ABI; the engine
-answers from its speculative device count loop. The snapshot is
+answers from its speculative device count loop, and the loop
+answers the Selects / Commits that follow the prediction from the engine's
+served-Select view (pe_spec_view_get) without a C call, as the Go shim does
+(INTEGRATION.md); --no-view crosses on every call. The snapshot is
 resident in HBM before timing. value = placements / timed seconds. The CPU
 baseline is the oracle (C++ restatement of the reference chain) driven by the
 same C loop on one host core.
@@ -31,6 +34,7 @@ BASELINE.json config (sections, --sections to choose):
               nodes whose GPUs are mostly held by priority-20 work
   c3_sharded  full-pass Selects over a 100k-node C3 cluster split across the
               ranks: one 80-byte record all-gather (RCCL) per placement
+  c3_sharded_1m  the same over 2^20 nodes (64 placements)
   plan_apply  plan applier fit check (evaluatePlanPlacements) of a system-job plan
               over a 100k-node snapshot, node ranges sharded over the ranks
   ingest      full snapshot upload (pe_set_state) vs an alloc delta
@@ -70,9 +74,12 @@ def parse():
     p.add_argument("--workers", type=int, default=8, help="worker threads of the c2_workers section")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-view", action="store_true",
+                   help="the C caller loop calls pe_select / pe_commit for every placement")
     p.add_argument("--sweep-nodes", type=int, default=1 << 24,
                    help="nodes of the scoring-sweep roofline measurement (0 = skip)")
-    p.add_argument("--sections", default="c1,c2_100k,c2_batch,c2_workers,c3,c4,c4_drop_in,c5,c3_sharded,plan_apply,ingest",
+    p.add_argument("--sections", default="c1,c2_100k,c2_batch,c2_workers,c3,c4,c4_drop_in,c5,c3_sharded,c3_sharded_1m,"
+                                         "plan_apply,ingest",
                    help="comma list of extra config sections (empty = none)")
     return p.parse_args()
 
@@ -503,7 +510,7 @@ def section_c5(device, cpu_s):
     return out
 
 
-def section_c3_sharded(device, rank, world, pg, placements=256, host_placements=64):
+def section_c3_sharded(device, rank, world, pg, placements=256, host_placements=64, n=100000):
     """Full-pass Selects of a C3 job over a 100k-node cluster split across the
     ranks. Device loop (pe_place_sharded): per placement each GPU sweeps its
     rows into an 80-byte record, the engine's RCCL communicator all-gathers the
@@ -513,7 +520,6 @@ def section_c3_sharded(device, rank, world, pg, placements=256, host_placements=
     one rank the unsharded device loop (pe_place) it must stay within 10 % of."""
     from nomad_amd import shard, synth, synth_columnar
     from nomad_amd.stack import GenericStack
-    n = 100000
     cs = synth_columnar.ColumnarState(n, seed=7, kind="c3")
     job = synth.job_c3(placements)
     perm = np.random.Generator(np.random.PCG64(3)).permutation(n).astype(np.uint32)
@@ -531,7 +537,9 @@ def section_c3_sharded(device, rank, world, pg, placements=256, host_placements=
         dt = time.perf_counter() - t0
         barrier(pg)
         walls.append(reduce(pg, dt, lambda d: d.ReduceOp.MAX))
-        xs.append(st.last_exchange_us())
+        # every rank times its own exchange (the all-gather's events on its
+        # engine stream); the line reports the slowest rank's
+        xs.append(reduce(pg, st.last_exchange_us(), lambda d: d.ReduceOp.MAX))
     placed = sum(1 for r in res if r.row >= 0)
     wall = min(walls[1:])
     out = {"workload": "C3 job on %d nodes, full-pass Selects sharded over %d GPUs, %d placements"
@@ -904,11 +912,13 @@ def main():
     # caller's shape). The engine answers from its speculative device loop.
     st = GenericStack(device=local)
     st.SetState(nodes, allocs)
+    dropin.use_view(not args.no_view)   # predicted Select / Commit pairs from the served-Select view
     caller = dropin.prepare(st, job)   # the shim's job encoding, once per job
     caller(orders, args.count, n_evals=max(1, args.warmup))
     timed_orders = np.roll(orders, -args.warmup, axis=0)
     spec0 = st.SpeculationStats()
     dropin.phase_seconds(reset=True)
+    dropin.view_served(reset=True)
     barrier(pg)
     sync()
     t0 = time.perf_counter()
@@ -918,6 +928,7 @@ def main():
     barrier(pg)
     spec1 = st.SpeculationStats()
     phases = dropin.phase_seconds(reset=True)
+    view_served = dropin.view_served(reset=True)
     elapsed = reduce(pg, elapsed, lambda d: d.ReduceOp.MAX)
     total_placed = reduce(pg, placed, lambda d: d.ReduceOp.SUM)
     total_evals = reduce(pg, evals, lambda d: d.ReduceOp.SUM)
@@ -960,11 +971,14 @@ def main():
             "data": "synthetic (seeded 10k-node cluster, SURVEY.md §8d C2)",
             "config": {"workload": "C2 drop-in: per step one evaluation of a count=%d binpack service job on %d "
                                    "heterogeneous nodes (limit 14): ResetPlan + SetJob + SetNodes + %d x "
-                                   "(pe_select, pe_commit) from a C caller loop" % (args.count, args.nodes,
-                                                                                   args.count),
+                                   "(Select, Commit) from a C caller loop, %s"
+                                   % (args.count, args.nodes, args.count,
+                                      "every call through the C ABI" if args.no_view else
+                                      "predicted pairs from the served-Select view (pe_spec_view)"),
                        "evals_per_step": 1,
                        "parallelism": "replicas x%d (windowed binpack does not shard)" % world},
             "drop_in": {"placements": placed, "evaluations": evals, "selects": selects,
+                        "selects_from_view": view_served,
                         "c_loop_seconds": c_secs,
                         "speculation": dict(zip(("runs", "served", "rollbacks", "records"),
                                                 (b - a for a, b in zip(spec0, spec1)))),
@@ -1036,6 +1050,11 @@ def main():
                     extra[sec] = section_c1(local, cpu_s)
             elif sec == "c3_sharded":
                 extra[sec] = section_c3_sharded(local, rank, world, pg)
+            elif sec == "c3_sharded_1m":
+                # 2^20 nodes: one GPU's sweep per placement is long enough for
+                # the split to pay for the per-placement exchange
+                extra[sec] = section_c3_sharded(local, rank, world, pg, placements=64, host_placements=16,
+                                                n=1 << 20)
             elif sec == "plan_apply":
                 extra[sec] = section_plan_apply(local, rank, world, pg, cpu_s)
             elif sec == "ingest":

@@ -317,6 +317,10 @@ struct TgPlan {
     DevMem class_ok, node_ok, class_aff, node_aff, alias_ok, coll_tg;
     bool tables_valid = false;
     bool has_aff_table = false, node_aff_used = false, node_ok_used = false, alias_used = false;
+    // what alias_ok holds: the host network it was built for and the node
+    // table generation (it travels with the buffer when the plan is recycled)
+    uint32_t alias_for = 0xFFFFFFFFu;
+    uint64_t alias_gen = 0;
     // static port asks (tg network ReservedPorts): (value, label) and the per-node gate
     std::vector<std::pair<int32_t, uint32_t>> rports;
     DevMem static_gate, static_blocked;
@@ -367,6 +371,7 @@ struct pe_stack {
     bool last_ms_pending = false;      // last_ms still to be read from ev0 / ev1
     bool spin_wait = true;             // PE_SPIN_WAIT=0: chain launches wait with a stream sync
     bool counts_defer_ok = true;       // PE_COUNTS_DEFER=0: SetJob launches its counts at once
+    uint64_t nodes_gen = 1;            // bumped whenever the node table changes (apply_nodes)
     uint32_t place_seq = 0;            // completion word sequence (run_place)
     int n_cu = 256;
     int sweep_per_cu = 4, sweep_per_cu_aux = 4;
@@ -722,6 +727,10 @@ static int flush_counts(pe_stack* s);
         if ((s)->counts_pending) {                                                      \
             const int crc_ = flush_counts(s);                                           \
             if (crc_) return crc_;                                                      \
+        }                                                                               \
+        if ((s)->fold_pending) {                                                        \
+            const int frc_ = flush_fold(s);                                             \
+            if (frc_) return frc_;                                                      \
         }                                                                               \
         if ((s)->reset_pending)                                                         \
             return (s)->fail(PE_EINTERNAL, std::string(#expr ": the deferred ResetPlan " \
@@ -1224,6 +1233,7 @@ std::vector<int> parse_port_ranges(const std::string& spec) {
 }
 
 int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t>& target, uint32_t n_new) {
+    s->nodes_gen++;   // node-table-derived device buffers (alias_ok) are stale
     const uint32_t n_old = (uint32_t)s->nodes.size();
     const uint32_t m = nt->n;
     std::vector<int32_t> src_of(n_new, -1);
@@ -1768,6 +1778,8 @@ std::unique_ptr<TgPlan> new_tg(pe_stack* s) {
     take(g->class_aff, old->class_aff);
     take(g->node_aff, old->node_aff);
     take(g->alias_ok, old->alias_ok);
+    g->alias_for = old->alias_for;
+    g->alias_gen = old->alias_gen;
     take(g->coll_tg, old->coll_tg);
     take(g->dev_cls, old->dev_cls);
     take(g->class_ok_batch, old->class_ok_batch);
@@ -2199,7 +2211,9 @@ int build_collisions(pe_stack* s, bool own = false, bool defer = false) {
         D.d[2 + g] = s->tgs[g]->coll_tg.as<uint32_t>();
     }
     const pe::ResetArgs R = s->reset_pending ? reset_args(s) : pe::ResetArgs{};
-    if (defer && s->counts_defer_ok) {
+    // only where the next launch can be a fused k_chain (a short list): else
+    // the counts launch now and run while the host prepares the first Select
+    if (defer && s->counts_defer_ok && n <= pe_chain_fused_max_n()) {
         // the entries stay in the mapped staging ring: the launch that carries
         // them reads them from there
         const uint2* staged = ents.empty() ? nullptr : reinterpret_cast<const uint2*>(stage_only(s, ents));
@@ -2597,13 +2611,19 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
     // AssignPorts needs an address of the ports' host network on the node
     g.alias_used = false;
     if (g.ask.tg_dyn > 0) {
-        std::vector<uint8_t> al(n, 0);
         const uint32_t want = g.net_host;
-        for (size_t i = 0; i < n; i++) {
-            const auto a = s->view((uint32_t)i).aliases;
-            al[i] = std::find(a.begin(), a.end(), want) != a.end();
+        // a property of the node table alone: a recycled plan's buffer built for
+        // the same host network on the same node table is reused (no upload)
+        if (g.alias_for != want || g.alias_gen != s->nodes_gen || g.alias_ok.bytes < n) {
+            std::vector<uint8_t> al(n, 0);
+            for (size_t i = 0; i < n; i++) {
+                const auto a = s->view((uint32_t)i).aliases;
+                al[i] = std::find(a.begin(), a.end(), want) != a.end();
+            }
+            HIP_TRY(s, upload_s(s, g.alias_ok, al));
+            g.alias_for = want;
+            g.alias_gen = s->nodes_gen;
         }
-        HIP_TRY(s, upload_s(s, g.alias_ok, al));
         g.alias_used = true;
     }
     if (has_static(g)) {
@@ -5524,7 +5544,18 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     ApiScope prof_(s, "spec_start");
     s->gen++;
     HIP_TRY(s, hipSetDevice(s->device));
+    // the table build's fold may ride in the run's first launch (place_impl,
+    // run_place); nothing leaves spec_start with it pending
+    struct FoldGuard {
+        pe_stack* s;
+        ~FoldGuard() {
+            s->fold_defer_ok = false;
+            if (s->fold_pending) (void)flush_fold(s);
+        }
+    } fold_guard{s};
+    s->fold_defer_ok = true;
     int rc = prepare_tg(s, tgi, s->visit, s->offset);
+    s->fold_defer_ok = false;
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
     if (g.psets_dynamic) return select_impl(s, tgi, nullptr, out);   // counts rebuilt per commit: no run
