@@ -14,11 +14,17 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -26,6 +32,7 @@
 #include "plan_types.h"
 
 hipError_t pe_launch_plan_eval(const pa::PlanArgs* a, int group, hipStream_t st);
+hipError_t pe_launch_plan_stage_copy(const void* host_mapped, void* dst, uint64_t bytes, hipStream_t st);
 hipError_t pe_launch_plan_patch(pa::NodeRec* nodes, pa::AllocRec* pool, const uint32_t* dead, uint32_t n_dead,
                                 const uint32_t* rows, const pa::NodeRec* recs, uint32_t n_rows, hipStream_t st);
 
@@ -119,6 +126,109 @@ struct HAlloc {
     std::vector<uint64_t> keys;
 };
 
+// Page-locked staging for the per-call uploads: the flattening writes its
+// records straight here and the copy engine reads them without the runtime's
+// pageable bounce.
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~PinBuf() { if (p) (void)hipHostFree(p); }
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+};
+
+// Persistent host workers for the per-call flattening (PE_PLAN_THREADS,
+// default min(16, cores)). run(fn) calls fn(k) for k in [0, size()), the
+// caller taking k = 0. Idle workers spin ~100 us before sleeping, so the
+// phases of one call hand over without a futex wake.
+class WorkerPool {
+  public:
+    explicit WorkerPool(int n, int spin_us) : spin_us_(spin_us) {
+        for (int k = 1; k < n; k++) workers_.emplace_back([this, k] { loop(k); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_.store(true);
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    int size() const { return (int)workers_.size() + 1; }
+    void run(const std::function<void(int)>& fn) {
+        if (workers_.empty()) { fn(0); return; }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &fn;
+            pending_.store((int)workers_.size(), std::memory_order_relaxed);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        fn(0);
+        while (pending_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+    }
+
+  private:
+    void loop(int k) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g;
+            auto t0 = std::chrono::steady_clock::now();
+            int spins = 0;
+            while ((g = gen_.load(std::memory_order_acquire)) == seen && !stop_.load()) {
+                __builtin_ia32_pause();
+                if ((++spins & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
+                    std::unique_lock<std::mutex> l(mu_);
+                    cv_.wait(l, [&] { return gen_.load() != seen || stop_.load(); });
+                }
+            }
+            if (stop_.load()) return;
+            seen = g;
+            (*job_)(k);
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
+    std::atomic<bool> stop_{false};
+    const std::function<void(int)>* job_ = nullptr;
+    int spin_us_;
+};
+
+// Per-worker memo of DeviceIdTuple ids (allocs of neighbouring nodes repeat a
+// handful of tuples); misses go to the planner's map under its lock.
+struct TupleMemo {
+    std::array<uint32_t, 3> key[8];
+    uint32_t id[8];
+    int n = 0, next = 0;
+};
+
+// One worker's share of a plan: a contiguous range of plan nodes and their
+// placed allocs, keys and removals gathered locally, offsets made global in a
+// second pass.
+struct PlanPart {
+    uint32_t n0 = 0, n1 = 0;
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> rm;
+    std::vector<pa::BigNode> big;
+    std::vector<pa::PlanRes> res;   // distinct resource triples of the part's allocs
+    uint64_t scratch = 0;
+    uint64_t key_base = 0, rm_base = 0, scratch_base = 0, res_base = 0;
+    int rc = PE_OK, node_rc = PE_OK;
+    const char* msg = nullptr;
+    const char* node_msg = nullptr;
+    TupleMemo memo;
+};
+
 }  // namespace
 
 struct pe_planner {
@@ -130,10 +240,22 @@ struct pe_planner {
     // algorithmic bytes of the last evaluate, computed on request (pe_planner_last_bytes)
     mutable uint64_t last_bytes = 0;
     mutable bool bytes_valid = true;
-    std::vector<pa::PlanNodeRec> last_pn;
-    std::vector<uint32_t> last_rm;
-    std::vector<pa::AllocRec> last_pa;
+    // the last evaluate's plan columns, removals, plan allocs and resource
+    // table (in the pinned staging, valid until the next evaluate)
+    const uint32_t *last_row = nullptr, *last_poff = nullptr, *last_rmoff = nullptr, *last_rm = nullptr;
+    const pa::PlanAllocRec* last_pa = nullptr;
+    const pa::PlanRes* last_res = nullptr;
+    uint32_t last_np = 0, last_npa = 0, last_nres = 0;
     uint64_t plan_bytes() const;
+    PinBuf h_stage;   // plan node records | plan allocs | keys | removals, one region
+    DBuf d_stage;
+    std::vector<PlanPart> parts;
+    std::unique_ptr<WorkerPool> pool_w;
+    int threads = 1, spin_us = 100, copy_kernel = 0;
+    WorkerPool& workers() {
+        if (!pool_w) pool_w.reset(new WorkerPool(threads, spin_us));
+        return *pool_w;
+    }
     bool have_state = false;
     int group = 4;    // lanes per plan node in k_plan_eval (PE_PLAN_GROUP: 4 / 8 / 16 / 64; 4 measured fastest)
 
@@ -150,7 +272,7 @@ struct pe_planner {
     std::vector<pa::Chunk> chunks;     // allocs appended by commits since the last compaction
 
     DBuf d_nodes, d_node_keys, d_pool, d_pool_keys, d_chunks, d_patch_dead, d_patch_rows, d_patch_recs;
-    DBuf d_pn, d_rm, d_pallocs, d_pkeys, d_big, d_scratch, d_reason;
+    DBuf d_big, d_scratch, d_reason;
 
     int fail(int code, const std::string& m) { err = m; return code; }
 
@@ -171,9 +293,7 @@ struct pe_planner {
         if (t->count && (!t->offsets || !t->bytes)) return fail(PE_EINVAL, "bad string table");
         size_t keep = 0;
         const size_t have = xl.size();
-        if (have && t->count >= have && memcmp(t->offsets, xl_off.data(), (have + 1) * 4) == 0 &&
-            memcmp(t->bytes, xl_bytes.data(), xl_bytes.size()) == 0)
-            keep = have;
+        if (have && t->count >= have && same_prefix(t, have)) keep = have;
         if (keep == t->count && have) return PE_OK;   // the same table as last call
         xl.resize(keep);
         xl.reserve(t->count);
@@ -183,6 +303,22 @@ struct pe_planner {
         xl_bytes.assign(t->bytes, t->count ? t->offsets[t->count] : 0);
         if (t->count == 0) xl_off.assign(1, 0);
         return PE_OK;
+    }
+    // The caller's first `have` strings equal the mapped ones (offsets and
+    // bytes); tables past 1 MiB are compared by the workers in slices.
+    bool same_prefix(const pe_strtab* t, size_t have) {
+        const size_t ob = (have + 1) * 4, bb = xl_bytes.size();
+        if (t->offsets[have] != bb) return false;
+        const int T = (ob + bb > (1u << 20)) ? threads : 1;
+        if (T == 1) return memcmp(t->offsets, xl_off.data(), ob) == 0 && memcmp(t->bytes, xl_bytes.data(), bb) == 0;
+        std::atomic<bool> same{true};
+        workers().run([&](int k) {
+            const size_t o0 = ob * k / T, o1 = ob * (k + 1) / T, b0 = bb * k / T, b1 = bb * (k + 1) / T;
+            if (memcmp((const char*)t->offsets + o0, (const char*)xl_off.data() + o0, o1 - o0) != 0 ||
+                memcmp(t->bytes + b0, xl_bytes.data() + b0, b1 - b0) != 0)
+                same.store(false, std::memory_order_relaxed);
+        });
+        return same.load();
     }
     bool str(uint32_t caller, uint32_t* out) const {
         if (caller >= xl.size()) return false;
@@ -194,57 +330,86 @@ struct pe_planner {
         tmp->assign(t->bytes + t->offsets[caller], t->offsets[caller + 1] - t->offsets[caller]);
         return tmp;
     }
-    std::array<uint32_t, 3> last_tuple{{PE_NONE, PE_NONE, PE_NONE}};
-    uint32_t last_tuple_id = 0;
-    uint32_t tuple(uint32_t v, uint32_t ty, uint32_t n) {
-        auto key = std::array<uint32_t, 3>{v, ty, n};
-        if (key == last_tuple) return last_tuple_id;   // allocs of a node repeat their device type
-        last_tuple = key;
-        auto it = tuple_id.find(key);
-        if (it != tuple_id.end()) return last_tuple_id = it->second;
-        const uint32_t id = (uint32_t)tuple_id.size();
-        tuple_id.emplace(key, id);
-        return last_tuple_id = id;
+    std::mutex tuple_mu;
+    TupleMemo memo;   // the single-threaded callers' memo
+    uint32_t tuple(uint32_t v, uint32_t ty, uint32_t n, TupleMemo* m) {
+        const auto key = std::array<uint32_t, 3>{v, ty, n};
+        for (int k = 0; k < m->n; k++)
+            if (m->key[k] == key) return m->id[k];
+        uint32_t id;
+        {
+            std::lock_guard<std::mutex> g(tuple_mu);
+            auto it = tuple_id.find(key);
+            if (it != tuple_id.end()) {
+                id = it->second;
+            } else {
+                id = (uint32_t)tuple_id.size();
+                tuple_id.emplace(key, id);
+            }
+        }
+        const int slot = m->n < 8 ? m->n++ : (m->next++ & 7);
+        m->key[slot] = key;
+        m->id[slot] = id;
+        return id;
     }
 
-    // Flatten one alloc of a pe_plan_alloc_table (strings already mapped).
-    int flatten(const pe_plan_alloc_table* t, uint32_t i, HAlloc* h) {
-        h->row = t->node_row ? t->node_row[i] : pa::kNone;
-        h->terminal = t->terminal ? (t->terminal[i] != 0) : 0;
-        h->cpu = t->cpu_shares ? t->cpu_shares[i] : 0;
-        h->mem = t->memory_mb ? t->memory_mb[i] : 0;
-        h->disk = t->disk_mb ? t->disk_mb[i] : 0;
-        h->bad_port = 0;
-        h->keys.clear();
+    // Flatten one alloc of a pe_plan_alloc_table (strings already mapped):
+    // resources and flags into *ar, its keys appended to *keys. Thread-safe;
+    // an error returns its code and message without touching `err`.
+    int flatten_into(const pe_plan_alloc_table* t, uint32_t i, pa::AllocRec* ar, std::vector<uint64_t>* keys,
+                     TupleMemo* m, const char** msg) {
+        const size_t k0 = keys->size();
+        ar->cpu = t->cpu_shares ? t->cpu_shares[i] : 0;
+        ar->mem = t->memory_mb ? t->memory_mb[i] : 0;
+        ar->disk = t->disk_mb ? t->disk_mb[i] : 0;
+        ar->terminal = t->terminal ? (t->terminal[i] != 0) : 0;
+        ar->bad_port = 0;
         if (t->core_off && t->core_off[i + 1] > t->core_off[i]) {
             // Flattened.Cpu.ReservedCores is a set (cpuset union, structs.go:3711-3719)
-            const size_t b = h->keys.size();
             for (uint32_t j = t->core_off[i]; j < t->core_off[i + 1]; j++)
-                h->keys.push_back(pa::make_key(pa::K_CORE_USED, t->core_id[j]));
-            std::sort(h->keys.begin() + b, h->keys.end());
-            h->keys.erase(std::unique(h->keys.begin() + b, h->keys.end()), h->keys.end());
+                keys->push_back(pa::make_key(pa::K_CORE_USED, t->core_id[j]));
+            std::sort(keys->begin() + k0, keys->end());
+            keys->erase(std::unique(keys->begin() + k0, keys->end()), keys->end());
         }
         if (t->port_off) {
             for (uint32_t j = t->port_off[i]; j < t->port_off[i + 1]; j++) {
                 const int64_t v = t->port_value[j];
-                if (v < 0 || (uint64_t)v >= kMaxValidPort) { h->bad_port = 1; continue; }   // network.go:203-205, 222-224
+                if (v < 0 || (uint64_t)v >= kMaxValidPort) { ar->bad_port = 1; continue; }   // network.go:203-205, 222-224
                 uint32_t ip;
-                if (!str(t->port_ip[j], &ip)) return fail(PE_EINVAL, "port ip string id out of range");
-                h->keys.push_back(pa::make_key(pa::K_PORT_USED, (uint64_t)ip << 16 | (uint64_t)v));
+                if (!str(t->port_ip[j], &ip)) { *msg = "port ip string id out of range"; return PE_EINVAL; }
+                keys->push_back(pa::make_key(pa::K_PORT_USED, (uint64_t)ip << 16 | (uint64_t)v));
             }
         }
         if (t->dev_off) {
             for (uint32_t j = t->dev_off[i]; j < t->dev_off[i + 1]; j++) {
                 uint32_t v, ty, n, inst;
                 if (!str(t->dev_vendor[j], &v) || !str(t->dev_type[j], &ty) || !str(t->dev_name[j], &n) ||
-                    !str(t->dev_instance[j], &inst))
-                    return fail(PE_EINVAL, "device string id out of range");
-                h->keys.push_back(pa::make_key(pa::K_DEV_USED, (uint64_t)inst << 24 | tuple(v, ty, n)));
+                    !str(t->dev_instance[j], &inst)) {
+                    *msg = "device string id out of range";
+                    return PE_EINVAL;
+                }
+                keys->push_back(pa::make_key(pa::K_DEV_USED, (uint64_t)inst << 24 | tuple(v, ty, n, m)));
             }
         }
-        if (h->keys.size() > 0xFFFF) return fail(PE_EINVAL, "alloc holds more than 65535 cores/ports/devices");
+        const size_t nk = keys->size() - k0;
+        if (nk > 0xFFFF) { *msg = "alloc holds more than 65535 cores/ports/devices"; return PE_EINVAL; }
+        ar->key_off = (uint32_t)k0;
+        ar->n_keys = (uint16_t)nk;
         return PE_OK;
     }
+    int flatten(const pe_plan_alloc_table* t, uint32_t i, HAlloc* h) {
+        pa::AllocRec ar{};
+        const char* msg = nullptr;
+        h->keys.clear();
+        const int rc = flatten_into(t, i, &ar, &h->keys, &memo, &msg);
+        if (rc) return fail(rc, msg);
+        h->row = t->node_row ? t->node_row[i] : pa::kNone;
+        h->terminal = ar.terminal;
+        h->bad_port = ar.bad_port;
+        h->cpu = ar.cpu; h->mem = ar.mem; h->disk = ar.disk;
+        return PE_OK;
+    }
+    int plan_part(const pe_plan* plan, PlanPart* w, uint32_t* prow, uint32_t* rmoff, pa::PlanAllocRec* pa_recs);
 
     // Node static keys and the SetNode collide flag (network.go:92-141).
     int build_node(const pe_plan_node_table* t, const pe_strtab* strs, uint32_t r, pa::NodeRec* nd) {
@@ -319,7 +484,7 @@ struct pe_planner {
                 uint32_t v, ty, n;
                 if (!str(t->dev_vendor[g], &v) || !str(t->dev_type[g], &ty) || !str(t->dev_name[g], &n))
                     return fail(PE_EINVAL, "device string id out of range");
-                auto& s = inst[tuple(v, ty, n)];
+                auto& s = inst[tuple(v, ty, n, &memo)];
                 s.clear();
                 for (uint32_t k = t->inst_off[g]; k < t->inst_off[g + 1]; k++) {
                     if (!t->inst_healthy[k]) continue;
@@ -396,25 +561,29 @@ struct pe_planner {
     }
 };
 
-// What k_plan_eval reads and writes for the last evaluated plan: 32 B plan
-// node record + 1 reason byte per plan node; with a placement on a known node
-// its 64 B record; when the fit check runs the node's static keys, every
-// snapshot / chunk alloc record of the node (32 B), the keys of those still
-// counted, 4 B per removal and each plan alloc with its keys.
-// Computed on the host when asked, against the current snapshot.
+// What k_plan_eval reads and writes for the last evaluated plan: per plan node
+// its row and place_off (4 + 4 B; + 4 B rm_off when the plan removes allocs) and
+// 1 reason byte; with a placement on a known node its 64 B record; when the fit
+// check runs the node's static keys, every snapshot / chunk alloc record of the
+// node (32 B), the keys of those still counted, 4 B per removal and each plan
+// alloc (16 B) with its keys; the distinct resource triples once (24 B each)
+// (DESIGN.md §9). Computed on the host when asked, against the current snapshot.
 uint64_t pe_planner::plan_bytes() const {
-    uint64_t bytes = 0;
-    for (const pa::PlanNodeRec& r : last_pn) {
-        bytes += sizeof(pa::PlanNodeRec) + 1;
-        if (r.place_cnt == 0 || r.row == pa::kNone || r.row >= nodes.size()) continue;
-        const pa::NodeRec& nd = nodes[r.row];
+    std::set<std::array<int64_t, 3>> distinct;   // the parts' tables may repeat a triple
+    for (uint32_t k = 0; k < last_nres; k++) distinct.insert({last_res[k].cpu, last_res[k].mem, last_res[k].disk});
+    uint64_t bytes = sizeof(pa::PlanRes) * (uint64_t)distinct.size();
+    for (uint32_t i = 0; i < last_np; i++) {
+        const uint32_t row = last_row[i], place_off = last_poff[i], place_cnt = last_poff[i + 1] - last_poff[i];
+        const uint32_t rm_off = last_rmoff ? last_rmoff[i] : 0, rm_cnt = last_rmoff ? last_rmoff[i + 1] - rm_off : 0;
+        bytes += 8 + (last_rmoff ? 4 : 0) + 1;
+        if (place_cnt == 0 || row == pa::kNone || (row & ~pa::kBigRow) >= nodes.size()) continue;
+        const pa::NodeRec& nd = nodes[row & ~pa::kBigRow];
         bytes += sizeof(pa::NodeRec);
         if (!nd.ready || !nd.eligible) continue;
-        bytes += 8ull * nd.n_keys + sizeof(pa::AllocRec) * (uint64_t)nd.alloc_cnt + 4ull * r.rm_cnt;
+        bytes += 8ull * nd.n_keys + sizeof(pa::AllocRec) * (uint64_t)nd.alloc_cnt + 4ull * rm_cnt;
         auto count_range = [&](uint32_t off, uint32_t cnt) {
             for (uint32_t q = off; q < off + cnt && q < pool.size(); q++) {
-                const bool gone = pool[q].terminal ||
-                                  std::binary_search(last_rm.begin() + r.rm_off, last_rm.begin() + r.rm_off + r.rm_cnt, q);
+                const bool gone = pool[q].terminal || std::binary_search(last_rm + rm_off, last_rm + rm_off + rm_cnt, q);
                 if (!gone) bytes += 8ull * pool[q].n_keys;
             }
         };
@@ -423,10 +592,84 @@ uint64_t pe_planner::plan_bytes() const {
             bytes += sizeof(pa::Chunk) + sizeof(pa::AllocRec) * (uint64_t)chunks[c].cnt;
             count_range(chunks[c].off, chunks[c].cnt);
         }
-        for (uint32_t j = r.place_off; j < r.place_off + r.place_cnt && j < last_pa.size(); j++)
-            bytes += sizeof(pa::AllocRec) + (last_pa[j].terminal ? 0 : 8ull * last_pa[j].n_keys);
+        for (uint32_t j = place_off; j < place_off + place_cnt && j < last_npa; j++)
+            bytes += sizeof(pa::PlanAllocRec) + (last_pa[j].terminal ? 0 : 8ull * last_pa[j].n_keys);
     }
     return bytes;
+}
+
+// Plan nodes [w->n0, w->n1) and their placed allocs: plan alloc records into
+// pa_recs (key and resource offsets local to the part), rows into prow and
+// removal offsets into rmoff (local to the part), k_plan_eval_big's nodes with
+// part-local scratch offsets. Alloc errors take precedence over plan node
+// errors, the serial order of evaluate.
+int pe_planner::plan_part(const pe_plan* plan, PlanPart* w, uint32_t* prow, uint32_t* rmoff, pa::PlanAllocRec* pa_recs) {
+    const pe_plan_alloc_table& pt = plan->allocs;
+    w->keys.clear();
+    w->rm.clear();
+    w->big.clear();
+    w->res.clear();
+    w->scratch = 0;
+    w->rc = w->node_rc = PE_OK;
+    for (uint32_t i = w->n0; i < w->n1; i++)
+        if (plan->place_off[i + 1] < plan->place_off[i]) {
+            w->msg = "place_off not ascending";
+            return w->rc = PE_EINVAL;
+        }
+    const uint32_t a0 = plan->place_off[w->n0], a1 = plan->place_off[w->n1];
+    pa::AllocRec ar;
+    for (uint32_t j = a0; j < a1; j++) {
+        if ((w->rc = flatten_into(&pt, j, &ar, &w->keys, &w->memo, &w->msg))) return w->rc;
+        pa::PlanAllocRec& pr = pa_recs[j];
+        pr.key_off = ar.key_off;
+        pr.n_keys = ar.n_keys;
+        pr.terminal = ar.terminal;
+        pr.bad_port = ar.bad_port;
+        pr._pad = 0;
+        // the task group's allocs repeat one triple: compare with the last few
+        const size_t nr = w->res.size();
+        uint32_t idx = (uint32_t)nr;
+        for (size_t k = nr; k > 0 && k + 4 > nr; k--) {
+            const pa::PlanRes& r = w->res[k - 1];
+            if (r.cpu == ar.cpu && r.mem == ar.mem && r.disk == ar.disk) { idx = (uint32_t)(k - 1); break; }
+        }
+        if (idx == nr) w->res.push_back(pa::PlanRes{ar.cpu, ar.mem, ar.disk});
+        pr.res = idx;
+    }
+    for (uint32_t i = w->n0; i < w->n1; i++) {
+        const uint32_t row = plan->node_row[i];
+        if (row != pa::kNone && row >= nodes.size()) {
+            w->node_msg = "plan node_row out of range";
+            return w->node_rc = PE_EINVAL;
+        }
+        prow[i] = row;
+        const uint32_t place_off = plan->place_off[i], place_cnt = plan->place_off[i + 1] - place_off;
+        if (rmoff) {
+            rmoff[i] = (uint32_t)w->rm.size();
+            const size_t b = w->rm.size();
+            for (uint32_t j = plan->remove_off[i]; j < plan->remove_off[i + 1]; j++) {
+                const uint32_t a = plan->remove_alloc[j];
+                if (a >= allocs.size()) {
+                    w->node_msg = "remove_alloc out of range";
+                    return w->node_rc = PE_EINVAL;
+                }
+                if (pool_of[a] != pa::kNone) w->rm.push_back(pool_of[a]);
+            }
+            std::sort(w->rm.begin() + b, w->rm.end());
+            w->rm.erase(std::unique(w->rm.begin() + b, w->rm.end()), w->rm.end());
+        }
+        if (place_cnt == 0 || row == pa::kNone) continue;
+        const pa::NodeRec& nd = nodes[row];
+        if (!nd.ready || !nd.eligible) continue;
+        uint64_t bound = (uint64_t)nd.n_keys + nd.alloc_keys;   // k_plan_eval's sum
+        for (uint32_t j = place_off; j < place_off + place_cnt; j++) bound += pa_recs[j].n_keys;
+        if (bound > pa::lds_keys(group)) {
+            prow[i] = row | pa::kBigRow;
+            w->big.push_back(pa::BigNode{i, (uint32_t)std::min<uint64_t>(w->scratch, 0xFFFFFFFFull)});
+            w->scratch += bound;
+        }
+    }
+    return PE_OK;
 }
 
 extern "C" {
@@ -441,6 +684,10 @@ pe_planner* pe_planner_create(int device) {
         const int v = atoi(g);
         if (v == 4 || v == 8 || v == 16 || v == 64) p->group = v;
     }
+    p->threads = (int)std::min<unsigned>(16, std::max<unsigned>(1, std::thread::hardware_concurrency()));
+    if (const char* g = getenv("PE_PLAN_THREADS")) p->threads = std::max(1, std::min(64, atoi(g)));
+    if (const char* g = getenv("PE_PLAN_SPIN_US")) p->spin_us = std::max(0, atoi(g));
+    if (const char* g = getenv("PE_PLAN_COPY")) p->copy_kernel = strcmp(g, "kernel") == 0;
     if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&p->e0) != hipSuccess || hipEventCreate(&p->e1) != hipSuccess) {
         delete p;
@@ -467,6 +714,7 @@ int pe_planner_set_state(pe_planner* p, const pe_strtab* strs, const pe_plan_nod
     if (t->n && (!t->cpu_shares || !t->memory_mb || !t->disk_mb)) return p->fail(PE_EINVAL, "node resources missing");
     if (hipSetDevice(p->device) != hipSuccess) return p->fail(PE_EHIP, "hipSetDevice");
     p->have_state = false;
+    if (t->n >= pa::kBigRow) return p->fail(PE_EINVAL, "snapshot of 2^31 nodes or more");
     int rc = p->map_strings(strs);
     if (rc) return rc;
     p->nodes.assign(t->n, pa::NodeRec{});
@@ -500,66 +748,126 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     const uint32_t np = plan->n_nodes;
     const pe_plan_alloc_table& pt = plan->allocs;
     if (np && plan->place_off[np] > pt.count) return p->fail(PE_EINVAL, "place_off exceeds plan allocs");
+    const uint32_t na = np ? plan->place_off[np] : 0;
 
-    std::vector<pa::PlanNodeRec> pn(np);
-    std::vector<uint32_t> rm, big;
-    std::vector<pa::AllocRec> pa_recs(pt.count);
-    std::vector<uint64_t> pkeys;
-    HAlloc h;
-    for (uint32_t i = 0; i < pt.count; i++) {
-        if ((rc = p->flatten(&pt, i, &h))) return rc;
-        pa::AllocRec& ar = pa_recs[i];
-        ar.cpu = h.cpu; ar.mem = h.mem; ar.disk = h.disk;
-        ar.key_off = (uint32_t)pkeys.size();
-        ar.n_keys = (uint16_t)h.keys.size();
-        ar.terminal = h.terminal;
-        ar.bad_port = h.bad_port;
-        pkeys.insert(pkeys.end(), h.keys.begin(), h.keys.end());
-    }
-    t[2] = tnow();
-    uint64_t scratch = 0;
-    for (uint32_t i = 0; i < np; i++) {
-        pa::PlanNodeRec& r = pn[i];
-        r.row = plan->node_row[i];
-        if (r.row != pa::kNone && r.row >= p->nodes.size()) return p->fail(PE_EINVAL, "plan node_row out of range");
-        r.place_off = plan->place_off[i];
-        r.place_cnt = plan->place_off[i + 1] - plan->place_off[i];
-        r.rm_off = (uint32_t)rm.size();
-        if (plan->remove_off) {
-            const size_t b = rm.size();
-            for (uint32_t j = plan->remove_off[i]; j < plan->remove_off[i + 1]; j++) {
-                const uint32_t a = plan->remove_alloc[j];
-                if (a >= p->allocs.size()) return p->fail(PE_EINVAL, "remove_alloc out of range");
-                if (p->pool_of[a] != pa::kNone) rm.push_back(p->pool_of[a]);
-            }
-            std::sort(rm.begin() + b, rm.end());
-            rm.erase(std::unique(rm.begin() + b, rm.end()), rm.end());
-        }
-        r.rm_cnt = (uint32_t)rm.size() - r.rm_off;
-        r.scratch_off = pa::kNone;
-        if (r.place_cnt == 0 || r.row == pa::kNone) continue;
-        const pa::NodeRec& nd = p->nodes[r.row];
-        if (!nd.ready || !nd.eligible) continue;
-        uint64_t bound = (uint64_t)nd.n_keys + nd.alloc_keys;
-        for (uint32_t j = r.place_off; j < r.place_off + r.place_cnt; j++) bound += pa_recs[j].n_keys;
-        r.key_bound = (uint32_t)std::min<uint64_t>(bound, 0xFFFFFFFFull);
-        if (bound > pa::lds_keys(p->group)) {
-            big.push_back(i);
-            r.scratch_off = (uint32_t)scratch;
-            scratch += bound;
-            if (scratch > 0xFFFFFFF0ull) return p->fail(PE_ENOMEM, "plan key scratch too large");
-        }
-    }
-    t[3] = tnow();
+    // Flatten into one pinned staging region, one part per worker over
+    // contiguous plan node ranges (balanced by plan nodes + placed allocs);
+    // the parts' key / removal / scratch / resource offsets are then made
+    // global and their keys, removals and resource triples gathered behind
+    // each other; one copy to the device. Alloc errors take precedence over
+    // plan node errors (the serial order: every alloc is flattened before the
+    // plan nodes are walked).
+    auto span = [](const uint32_t* off, uint32_t n) -> uint64_t {
+        return off && n && off[n] > off[0] ? off[n] - off[0] : 0;
+    };
+    const uint64_t key_cap = span(pt.core_off, na) + span(pt.port_off, na) + span(pt.dev_off, na);
+    const uint64_t rm_cap = plan->remove_off ? span(plan->remove_off, np) : 0;
+    if (key_cap > 0xFFFFFFFFull || rm_cap > 0xFFFFFFFFull) return p->fail(PE_ENOMEM, "plan too large");
+    const bool has_rm = rm_cap > 0;
+    // staging layout (host and device alike, 256-B aligned parts): rows,
+    // place_off, rm_off (plans with removals), plan allocs, keys (up to the
+    // offsets' bound), resource triples, removals
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    const uint64_t o_poff = al(4ull * np);
+    const uint64_t o_rmoff = al(o_poff + 4ull * (np + 1));
+    const uint64_t o_pa = al(o_rmoff + (has_rm ? 4ull * (np + 1) : 0));
+    const uint64_t o_keys = al(o_pa + (uint64_t)na * sizeof(pa::PlanAllocRec));
+    const uint64_t o_res = al(o_keys + key_cap * 8);
+    const uint64_t o_rm = al(o_res + (uint64_t)std::max<uint32_t>(na, 1) * sizeof(pa::PlanRes));
+    const uint64_t stage_bytes = al(o_rm + rm_cap * 4) + 256;
     hipError_t e;
-    if ((e = p->upload(p->d_pn, pn.data(), pn.size() * sizeof(pa::PlanNodeRec))) != hipSuccess ||
-        (e = p->upload(p->d_rm, rm.data(), rm.size() * 4)) != hipSuccess ||
-        (e = p->upload(p->d_pallocs, pa_recs.data(), pa_recs.size() * sizeof(pa::AllocRec))) != hipSuccess ||
-        (e = p->upload(p->d_pkeys, pkeys.data(), pkeys.size() * 8)) != hipSuccess ||
-        (e = p->upload(p->d_big, big.data(), big.size() * 4)) != hipSuccess ||
-        (e = p->d_scratch.reserve(std::max<uint64_t>(scratch, 1) * 8)) != hipSuccess ||
+    if ((e = p->h_stage.reserve(stage_bytes)) != hipSuccess || (e = p->d_stage.reserve(stage_bytes)) != hipSuccess ||
         (e = p->d_reason.reserve(std::max<uint32_t>(np, 1))) != hipSuccess)
+        return p->fail(PE_EHIP, std::string("planner staging: ") + hipGetErrorString(e));
+    char* const hs = (char*)p->h_stage.p;
+    char* const ds = (char*)p->d_stage.p;
+    auto* prow = (uint32_t*)hs;
+    auto* poff = (uint32_t*)(hs + o_poff);
+    auto* rmoff = has_rm ? (uint32_t*)(hs + o_rmoff) : nullptr;
+    auto* pa_recs = (pa::PlanAllocRec*)(hs + o_pa);
+    auto* pkeys = (uint64_t*)(hs + o_keys);
+    auto* pres = (pa::PlanRes*)(hs + o_res);
+    auto* rm = (uint32_t*)(hs + o_rm);
+    // ranges of [0, np) balanced by plan nodes + placed allocs
+    auto split = [&](int k, int parts) -> uint32_t {
+        if (k == parts) return np;
+        const uint64_t goal = ((uint64_t)np + plan->place_off[np]) * k / parts;
+        uint32_t a = 0, b = np;   // first i with i + place_off[i] >= goal (binary search)
+        while (a < b) {
+            const uint32_t m = a + (b - a) / 2;
+            if ((uint64_t)m + plan->place_off[m] < goal) a = m + 1;
+            else b = m;
+        }
+        return a;
+    };
+    const int T = np == 0 ? 0 : (np + na >= 8192) ? p->threads : 1;
+    if ((int)p->parts.size() < T) p->parts.resize(T);
+    for (int k = 0; k < T; k++) {
+        p->parts[k].n0 = split(k, T);
+        p->parts[k].n1 = split(k + 1, T);
+    }
+    auto part = [&](int k) { if (k < T) p->plan_part(plan, &p->parts[k], prow, rmoff, pa_recs); };
+    if (T > 1) p->workers().run(part);
+    else if (T == 1) part(0);
+    for (int k = 0; k < T; k++)
+        if (p->parts[k].rc) return p->fail(p->parts[k].rc, p->parts[k].msg);
+    for (int k = 0; k < T; k++)
+        if (p->parts[k].node_rc) return p->fail(p->parts[k].node_rc, p->parts[k].node_msg);
+    t[2] = tnow();
+    uint64_t nkeys = 0, nrm = 0, scratch = 0, nres = 0;
+    std::vector<pa::BigNode> big;
+    for (int k = 0; k < T; k++) {
+        PlanPart& w = p->parts[k];
+        w.key_base = nkeys;
+        w.rm_base = nrm;
+        w.scratch_base = scratch;
+        w.res_base = nres;
+        nkeys += w.keys.size();
+        nrm += w.rm.size();
+        nres += w.res.size();
+        for (const pa::BigNode& b : w.big) big.push_back(pa::BigNode{b.p, (uint32_t)(b.scratch_off + scratch)});
+        scratch += w.scratch;
+    }
+    if (scratch > 0xFFFFFFF0ull) return p->fail(PE_ENOMEM, "plan key scratch too large");
+    if (nkeys > key_cap || nrm > rm_cap) return p->fail(PE_EINVAL, "plan offsets not ascending");
+    auto gather = [&](int k) {
+        if (k >= T) return;
+        const PlanPart& w = p->parts[k];
+        if (w.n0 == w.n1) return;
+        const uint32_t kb = (uint32_t)w.key_base, rb = (uint32_t)w.rm_base, resb = (uint32_t)w.res_base;
+        for (uint32_t j = plan->place_off[w.n0]; j < plan->place_off[w.n1]; j++) {
+            pa_recs[j].key_off += kb;
+            pa_recs[j].res += resb;
+        }
+        memcpy(poff + w.n0, plan->place_off + w.n0, 4ull * (w.n1 - w.n0));
+        if (rmoff)
+            for (uint32_t i = w.n0; i < w.n1; i++) rmoff[i] += rb;
+        if (!w.keys.empty()) memcpy(pkeys + kb, w.keys.data(), w.keys.size() * 8);
+        if (!w.res.empty()) memcpy(pres + resb, w.res.data(), w.res.size() * sizeof(pa::PlanRes));
+        if (!w.rm.empty()) memcpy(rm + rb, w.rm.data(), w.rm.size() * 4);
+    };
+    if (T > 1) p->workers().run(gather);
+    else if (T == 1) gather(0);
+    poff[np] = np ? plan->place_off[np] : 0;
+    if (rmoff) rmoff[np] = (uint32_t)nrm;
+    t[3] = tnow();
+    // host -> device: one copy-engine transfer of everything up to the last
+    // resource triple (+ the removals), or k_plan_stage_copy reading the
+    // mapped staging (PE_PLAN_COPY=kernel)
+    void* hs_dev = nullptr;
+    if (p->copy_kernel && hipHostGetDevicePointer(&hs_dev, hs, 0) != hipSuccess) hs_dev = nullptr;
+    auto h2d = [&](uint64_t off, uint64_t bytes) -> hipError_t {
+        if (!bytes) return hipSuccess;
+        if (hs_dev) return pe_launch_plan_stage_copy((const char*)hs_dev + off, ds + off, bytes, p->stream);
+        return hipMemcpyAsync(ds + off, hs + off, bytes, hipMemcpyHostToDevice, p->stream);
+    };
+    if ((np && (e = h2d(0, o_res + nres * sizeof(pa::PlanRes))) != hipSuccess) ||
+        (e = h2d(o_rm, nrm * 4)) != hipSuccess ||
+        (e = p->upload(p->d_big, big.data(), big.size() * sizeof(pa::BigNode))) != hipSuccess ||
+        (e = p->d_scratch.reserve(std::max<uint64_t>(scratch, 1) * 8)) != hipSuccess) {
+        (void)hipStreamSynchronize(p->stream);
         return p->fail(PE_EHIP, std::string("planner plan upload: ") + hipGetErrorString(e));
+    }
     t[4] = tnow();
     pa::PlanArgs a{};
     a.nodes = (const pa::NodeRec*)p->d_nodes.p;
@@ -567,13 +875,16 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     a.pool = (const pa::AllocRec*)p->d_pool.p;
     a.node_keys = (const uint64_t*)p->d_node_keys.p;
     a.pool_keys = (const uint64_t*)p->d_pool_keys.p;
-    a.pn = (const pa::PlanNodeRec*)p->d_pn.p;
+    a.prow = (const uint32_t*)ds;
+    a.poff = (const uint32_t*)(ds + o_poff);
+    a.rmoff = rmoff ? (const uint32_t*)(ds + o_rmoff) : nullptr;
     a.n_plan = np;
-    a.rm = (const uint32_t*)p->d_rm.p;
-    a.pallocs = (const pa::AllocRec*)p->d_pallocs.p;
-    a.pkeys = (const uint64_t*)p->d_pkeys.p;
+    a.rm = (const uint32_t*)(ds + o_rm);
+    a.pallocs = (const pa::PlanAllocRec*)(ds + o_pa);
+    a.pres = (const pa::PlanRes*)(ds + o_res);
+    a.pkeys = (const uint64_t*)(ds + o_keys);
     a.scratch = (uint64_t*)p->d_scratch.p;
-    a.big = (const uint32_t*)p->d_big.p;
+    a.big = (const pa::BigNode*)p->d_big.p;
     a.n_big = (uint32_t)big.size();
     a.reason = (uint8_t*)p->d_reason.p;
     if ((e = hipEventRecord(p->e0, p->stream)) != hipSuccess || (e = pe_launch_plan_eval(&a, p->group, p->stream)) != hipSuccess ||
@@ -584,14 +895,21 @@ int pe_planner_evaluate(pe_planner* p, const pe_strtab* strs, const pe_plan* pla
     float ms = 0;
     (void)hipEventElapsedTime(&ms, p->e0, p->e1);
     p->last_ms = ms;
-    p->last_pn = std::move(pn);
-    p->last_rm = std::move(rm);
-    p->last_pa = std::move(pa_recs);
+    p->last_row = prow;
+    p->last_poff = poff;
+    p->last_rmoff = rmoff;
+    p->last_rm = rm;
+    p->last_pa = pa_recs;
+    p->last_np = np;
+    p->last_npa = na;
+    p->last_nres = (uint32_t)nres;
+    p->last_res = pres;
     p->bytes_valid = false;
     if (prof) {
         t[5] = tnow();
-        fprintf(stderr, "planner evaluate us: strings %.1f flatten %.1f nodes %.1f upload %.1f kernel+reasons %.1f "
-                        "(kernel %.1f)\n", t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], ms * 1e3);
+        fprintf(stderr, "planner evaluate us: strings %.1f flatten %.1f gather %.1f upload %.1f "
+                        "kernel+reasons %.1f (kernel %.1f, %d threads)\n", t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4],
+                ms * 1e3, T);
     }
     uint32_t fit = 0;
     for (uint32_t i = 0; i < np; i++) fit += reason[i] == PE_PLAN_FIT;

@@ -74,18 +74,14 @@ struct Acc {
     bool bad = false, core_dup = false, core_missing = false;
 };
 
-// Stage one counted alloc: sums, masked cores, keys.
+// Stage one counted alloc's keys: cores < 64 into the mask, the rest into buf.
 template <typename Buf>
-__device__ __forceinline__ void take(const AllocRec& ar, const uint64_t* keys, Buf buf, uint32_t* fill,
-                                     unsigned long long* cmask, uint64_t node_mask, Acc& acc) {
-    acc.cpu += ar.cpu;
-    acc.mem += ar.mem;
-    acc.disk += ar.disk;
-    acc.bad |= ar.bad_port != 0;
-    if (!ar.n_keys) return;
-    const uint32_t base = atomicAdd(fill, (uint32_t)ar.n_keys);
-    for (uint32_t k = 0; k < ar.n_keys; k++) {
-        uint64_t key = keys[ar.key_off + k];
+__device__ __forceinline__ void take_keys(uint32_t key_off, uint32_t n_keys, const uint64_t* keys, Buf buf,
+                                          uint32_t* fill, unsigned long long* cmask, uint64_t node_mask, Acc& acc) {
+    if (!n_keys) return;
+    const uint32_t base = atomicAdd(fill, n_keys);
+    for (uint32_t k = 0; k < n_keys; k++) {
+        uint64_t key = keys[key_off + k];
         const uint64_t v = key & kValMask;
         if ((uint32_t)(key >> 60) == K_CORE_USED && v < 64) {
             const unsigned long long bit = 1ull << v;
@@ -98,8 +94,37 @@ __device__ __forceinline__ void take(const AllocRec& ar, const uint64_t* keys, B
     }
 }
 
+// A snapshot alloc: sums, masked cores, keys.
+template <typename Buf>
+__device__ __forceinline__ void take(const AllocRec& ar, const uint64_t* keys, Buf buf, uint32_t* fill,
+                                     unsigned long long* cmask, uint64_t node_mask, Acc& acc) {
+    acc.cpu += ar.cpu;
+    acc.mem += ar.mem;
+    acc.disk += ar.disk;
+    acc.bad |= ar.bad_port != 0;
+    take_keys(ar.key_off, ar.n_keys, keys, buf, fill, cmask, node_mask, acc);
+}
+
+// One plan node as the kernel sees it.
+struct PlanNode {
+    uint32_t row, place_off, place_cnt, rm_off, rm_cnt;
+    bool big;
+};
+
+__device__ __forceinline__ PlanNode plan_node(const PlanArgs& a, uint32_t p) {
+    PlanNode n;
+    const uint32_t row = a.prow[p];
+    n.big = row != kNone && (row & kBigRow) != 0;
+    n.row = row == kNone ? kNone : row & ~kBigRow;
+    n.place_off = a.poff[p];
+    n.place_cnt = a.poff[p + 1] - n.place_off;
+    n.rm_off = a.rmoff ? a.rmoff[p] : 0;
+    n.rm_cnt = a.rmoff ? a.rmoff[p + 1] - n.rm_off : 0;
+    return n;
+}
+
 template <int G, bool GLOBAL, typename Buf>
-__device__ __forceinline__ uint8_t fit_node(const PlanArgs& a, const PlanNodeRec& pn, const NodeRec& nd,
+__device__ __forceinline__ uint8_t fit_node(const PlanArgs& a, const PlanNode& pn, const NodeRec& nd,
                                             uint32_t lane, Buf buf, uint32_t* fill, unsigned long long* cmask) {
     const uint32_t gl = lane & (G - 1);
     for (uint32_t i = gl; i < nd.n_keys; i += G) buf[i] = a.node_keys[nd.key_off + i];
@@ -125,9 +150,14 @@ __device__ __forceinline__ uint8_t fit_node(const PlanArgs& a, const PlanNodeRec
         c = ch.next;
     }
     for (uint32_t i = gl; i < pn.place_cnt; i += G) {
-        const AllocRec ar = a.pallocs[pn.place_off + i];
+        const PlanAllocRec ar = a.pallocs[pn.place_off + i];
         if (ar.terminal) continue;
-        take(ar, a.pkeys, buf, fill, cmask, nd.core_mask, acc);
+        const PlanRes r = a.pres[ar.res];
+        acc.cpu += r.cpu;
+        acc.mem += r.mem;
+        acc.disk += r.disk;
+        acc.bad |= ar.bad_port != 0;
+        take_keys(ar.key_off, ar.n_keys, a.pkeys, buf, fill, cmask, nd.core_mask, acc);
     }
     if (GLOBAL) wave_sync_global(); else wave_sync_lds();
     const uint32_t k = *fill;
@@ -177,7 +207,7 @@ __device__ __forceinline__ uint8_t fit_node(const PlanArgs& a, const PlanNodeRec
 }
 
 // Node checks ahead of AllocsFit; returns true when the fit check must run.
-__device__ __forceinline__ bool precheck(const PlanArgs& a, const PlanNodeRec& pn, NodeRec* nd, uint8_t* r) {
+__device__ __forceinline__ bool precheck(const PlanArgs& a, const PlanNode& pn, NodeRec* nd, uint8_t* r) {
     if (pn.place_cnt == 0) { *r = PE_PLAN_FIT; return false; }            // evict-only (plan_apply.go:614-616)
     if (pn.row == kNone) { *r = PE_PLAN_NODE_MISSING; return false; }
     *nd = a.nodes[pn.row];
@@ -199,10 +229,10 @@ __global__ void __launch_bounds__(64 * kWaves) k_plan_eval(PlanArgs a) {
     if (first >= a.n_plan) return;   // whole wave idle; no workgroup barrier below
     const uint32_t p = blockIdx.x * NB + slot;
     if (p >= a.n_plan) return;       // group-uniform: the group's lanes leave together
-    const PlanNodeRec pn = a.pn[p];
-    if (pn.scratch_off != kNone) return;   // k_plan_eval_big
+    const PlanNode pn = plan_node(a, p);
     NodeRec nd;
     uint8_t r;
+    if (pn.big) return;              // k_plan_eval_big writes this node's reason
     if (precheck(a, pn, &nd, &r))
         r = fit_node<G, false>(a, pn, nd, lane, keys[slot], &fill[slot], &cmask[slot]);
     if ((lane & (G - 1)) == 0) a.reason[p] = r;
@@ -212,13 +242,13 @@ __global__ void __launch_bounds__(64) k_plan_eval_big(PlanArgs a) {
     __shared__ uint32_t fill;
     __shared__ unsigned long long cmask;
     const uint32_t lane = threadIdx.x;
-    const uint32_t p = a.big[blockIdx.x];
-    const PlanNodeRec pn = a.pn[p];
+    const BigNode b = a.big[blockIdx.x];
+    const PlanNode pn = plan_node(a, b.p);
     NodeRec nd;
     uint8_t r;
     if (precheck(a, pn, &nd, &r))
-        r = fit_node<64, true>(a, pn, nd, lane, a.scratch + pn.scratch_off, &fill, &cmask);
-    if (lane == 0) a.reason[p] = r;
+        r = fit_node<64, true>(a, pn, nd, lane, a.scratch + b.scratch_off, &fill, &cmask);
+    if (lane == 0) a.reason[b.p] = r;
 }
 
 // pe_planner_commit patch: removed allocs stop counting (terminal byte) and
@@ -230,7 +260,26 @@ __global__ void __launch_bounds__(256) k_plan_patch(NodeRec* nodes, AllocRec* po
     if (i < n_rows) nodes[rows[i]] = recs[i];
 }
 
+// The plan's staging copied from page-locked host memory by the CUs (each
+// lane reads 16 B over PCIe per step, many workgroups in flight), instead of
+// one copy-engine transfer (PE_PLAN_COPY=kernel).
+__global__ void __launch_bounds__(256) k_plan_stage_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                         uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+}
+
 }  // namespace pa
+
+hipError_t pe_launch_plan_stage_copy(const void* host_mapped, void* dst, uint64_t bytes, hipStream_t st) {
+    const uint64_t n16 = (bytes + 15) / 16;
+    if (n16 == 0) return hipSuccess;
+    const uint64_t want = (n16 + 255) / 256;
+    const uint32_t blocks = (uint32_t)(want < 2048 ? want : 2048);
+    hipLaunchKernelGGL(pa::k_plan_stage_copy, dim3(blocks), dim3(256), 0, st, (const uint4*)host_mapped, (uint4*)dst,
+                       n16);
+    return hipGetLastError();
+}
 
 hipError_t pe_launch_plan_patch(pa::NodeRec* nodes, pa::AllocRec* pool, const uint32_t* dead, uint32_t n_dead,
                                 const uint32_t* rows, const pa::NodeRec* recs, uint32_t n_rows, hipStream_t st) {

@@ -19,6 +19,7 @@
 namespace pa {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kBigRow = 0x80000000u;   // plan row column: the node is k_plan_eval_big's
 
 // key = kind << 60 | value
 enum : uint32_t {
@@ -60,20 +61,37 @@ struct alignas(16) AllocRec {     // 32 B, snapshot pool entry or plan alloc
 };
 static_assert(sizeof(AllocRec) == 32, "AllocRec is 32 bytes");
 
-struct alignas(16) PlanNodeRec {  // 32 B, one per plan node
-    uint32_t row;                 // snapshot row or kNone
-    uint32_t place_off, place_cnt;// plan allocs
-    uint32_t rm_off, rm_cnt;      // removed pool indices (sorted ascending)
-    uint32_t scratch_off;         // kNone: keys fit the wave's LDS buffer
-    uint32_t key_bound;           // upper bound of staged keys
+// A plan alloc (16 B): its keys and its resources, an index into the plan's
+// table of distinct (cpu, memory, disk) triples (the allocs of one task group
+// share one). Plan nodes travel as three u32 columns: snapshot row (kNone:
+// unknown; | kBigRow when the node's key bound passes the LDS budget),
+// place_off[n + 1] (the caller's own column) and, when the plan removes live
+// allocs, rm_off[n + 1] into the sorted removal lists.
+struct alignas(16) PlanAllocRec {
+    uint32_t key_off;
+    uint16_t n_keys;
+    uint8_t terminal;
+    uint8_t bad_port;
+    uint32_t res;
     uint32_t _pad;
 };
-static_assert(sizeof(PlanNodeRec) == 32, "PlanNodeRec is 32 bytes");
+static_assert(sizeof(PlanAllocRec) == 16, "PlanAllocRec is 16 bytes");
+
+struct PlanRes {
+    int64_t cpu, mem, disk;
+};
+static_assert(sizeof(PlanRes) == 24, "PlanRes is 24 bytes");
+
+struct BigNode {                  // a plan node past the LDS budget (k_plan_eval_big)
+    uint32_t p;                   // plan node index
+    uint32_t scratch_off;         // its global key scratch
+};
 
 // k_plan_eval<G>: a group of G lanes per plan node (64/G nodes per wavefront),
 // keys staged in a per-node LDS buffer of lds_keys(G) (16 KiB per workgroup);
-// plan nodes whose key bound exceeds it go to k_plan_eval_big (one wavefront
-// each, global scratch). The host picks G (pe_planner, PE_PLAN_GROUP).
+// plan nodes whose key bound (node keys + snapshot alloc keys + plan alloc
+// keys, the same sum on host and device) exceeds it go to k_plan_eval_big (one
+// wavefront each, global scratch). The host picks G (pe_planner, PE_PLAN_GROUP).
 constexpr int kWaves = 4;                               // waves per workgroup
 __host__ __device__ constexpr int nodes_per_block(int g) { return kWaves * (64 / g); }
 __host__ __device__ constexpr uint32_t lds_keys(int g) { return 2048u / (uint32_t)(kWaves * (64 / g)); }
@@ -85,13 +103,16 @@ struct PlanArgs {
     const AllocRec* pool;            // snapshot allocs, grouped by node
     const uint64_t* node_keys;
     const uint64_t* pool_keys;
-    const PlanNodeRec* pn;
+    const uint32_t* prow;            // plan node -> snapshot row (kNone: unknown node)
+    const uint32_t* poff;            // [n_plan + 1] plan allocs of each plan node
+    const uint32_t* rmoff;           // [n_plan + 1] removals of each plan node (null: none)
     uint32_t n_plan;
-    const uint32_t* rm;              // removed pool indices
-    const AllocRec* pallocs;         // plan allocs
+    const uint32_t* rm;              // removed pool indices, sorted per plan node
+    const PlanAllocRec* pallocs;     // plan allocs
+    const PlanRes* pres;             // their distinct resource triples
     const uint64_t* pkeys;
     uint64_t* scratch;
-    const uint32_t* big;             // plan nodes past the LDS budget
+    const BigNode* big;              // plan nodes past the LDS budget
     uint32_t n_big;
     uint8_t* reason;
 };

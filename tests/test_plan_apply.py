@@ -423,3 +423,33 @@ def test_planner_incremental_commit_and_compaction():
                 nxt.node_update[nd.id] = [mine[0]]
         plan = nxt
     assert pl.lib.pe_planner_snapshot_allocs(pl.h) == len(pl.allocs)
+
+
+@pytest.mark.gpu
+def test_planner_threaded_flatten_matches_serial(monkeypatch):
+    """The plan's flattening runs in per-worker parts (contiguous plan node
+    ranges, offsets made global afterwards); with one worker it is the serial
+    loop. Same codes and the same algorithmic bytes either way, with removals
+    (node_update of live allocs) spread over every part, and against the
+    oracle on nodes taken from every part."""
+    nodes, allocs, plan = system_plan(12000, seed=17)
+    snap = O.Snapshot(nodes, allocs)
+    rng = random.Random(5)
+    for nd in rng.sample(nodes, 3000):
+        mine = snap.by_node.get(nd.id, [])
+        if mine:
+            plan.node_update[nd.id] = [mine[0]]
+    got = []
+    for threads in ("1", "5", "16"):
+        monkeypatch.setenv("PE_PLAN_THREADS", threads)
+        pl = _planner()
+        pl.set_state(nodes, allocs)
+        ep = pl.encode(plan)
+        got.append((pl.evaluate(ep).copy(), pl.last_bytes()))
+        pl.close()
+    for codes, nbytes in got[1:]:
+        assert np.array_equal(codes, got[0][0])
+        assert nbytes == got[0][1]
+    for i in range(0, len(ep.node_ids), 97):
+        nid = ep.node_ids[i]
+        assert _codes_to_pairs([got[2][0][i]])[0] == O.evaluate_node_plan(snap, plan, nid), nid

@@ -46,3 +46,10 @@ if [ -n "$C1_TRACE" ]; then   # device timeline of the C1 evaluation loop
   python3 tools/timeline.py "$T" k_chain 4 > "$OUT/c1_timeline.txt" || true
   tail -24 "$OUT/c1_timeline.txt"
 fi
+if [ -n "$AB_ENV" ]; then   # headline bench A/B: default vs the environment settings in $AB_ENV
+  for V in default "$AB_ENV"; do
+    if [ "$V" = default ]; then E=""; else E="$V"; fi
+    env $E timeout -k 10 300 python -u bench.py --no-cpu --sweep-nodes 0 --sections "" > "$OUT/ab_env.json" 2> "$OUT/ab_env.err" || { tail -20 "$OUT/ab_env.err"; exit 1; }
+    python3 -c "import json;d=json.load(open('$OUT/ab_env.json'));print('$V', 'C2 %.4g' % d['value'], 'us/eval %.1f' % (d['ms_per_step']*1e3), d['drop_in']['us_per_eval_by_phase'])"
+  done
+fi
