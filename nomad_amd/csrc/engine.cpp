@@ -26,6 +26,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -40,6 +41,7 @@ hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, 
 hipError_t pe_launch_system(const pe::SystemArgs* a, hipStream_t st);
 hipError_t pe_launch_rank_of(const uint32_t* list, uint32_t n_list, uint32_t* rank_of, uint32_t n_rows, hipStream_t st);
 hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t st);
+hipError_t pe_launch_scatter_rows(void* dst, uint32_t words, const void* payload_mapped, uint32_t n, hipStream_t st);
 hipError_t pe_launch_counts(const pe::CountDsts* d, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
                             const pe::ResetArgs* r, hipStream_t st);
 size_t pe_fullpass_lds_bytes(uint32_t n);
@@ -137,6 +139,24 @@ struct DevMem {
         return e;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }
+    // at least b bytes, the first `keep` bytes kept (device copy on `st`);
+    // 25 % headroom so rows appended one update at a time do not copy each time
+    hipError_t grow(size_t b, size_t keep, hipStream_t st) {
+        if (b <= bytes && p) return hipSuccess;
+        void* q = nullptr;
+        const size_t want = b + b / 4;
+        hipError_t e = hipMalloc(&q, want ? want : 16);
+        if (e != hipSuccess) return e;
+        if (p && keep) {
+            e = hipMemcpyAsync(q, p, std::min(keep, bytes), hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);   // before the old block is freed
+        }
+        if (e != hipSuccess) { (void)hipFree(q); return e; }
+        release();
+        p = q;
+        bytes = want ? want : 16;
+        return hipSuccess;
+    }
 };
 
 // Page-locked host buffer: device-to-host result copies run at DMA rate and the
@@ -239,6 +259,51 @@ struct HostDevGroup {
     uint32_t vendor, type, name, healthy;
     uint32_t attr_begin, attr_end;          // into pe_stack::dev_attr
 };
+
+// Where each node's variable-length list sits in its item vector: items
+// [off[r], off[r] + cnt[r]). A row rewritten with at most as many items keeps
+// its place; a longer one moves to the end of the vector (its old range turns
+// dead); the vector is compacted into row order once dead items outnumber the
+// live ones. pe_update_nodes then costs O(changed rows), not O(table).
+struct RowIndex {
+    std::vector<uint32_t> off, cnt;
+    size_t dead = 0;
+    uint32_t b(uint32_t r) const { return off[r]; }
+    uint32_t e(uint32_t r) const { return off[r] + cnt[r]; }
+    uint32_t n(uint32_t r) const { return cnt[r]; }
+    void clear() { off.clear(); cnt.clear(); dead = 0; }
+    void rows(uint32_t n_rows) { off.resize(n_rows, 0); cnt.resize(n_rows, 0); }
+};
+
+// Row r of `ix` becomes k items written by fill(T* dst) (rows() covers r).
+template <typename T, typename Fill>
+void row_set(RowIndex& ix, std::vector<T>& items, uint32_t r, uint32_t k, Fill fill) {
+    if (k <= ix.cnt[r]) {
+        ix.dead += ix.cnt[r] - k;
+        fill(items.data() + ix.off[r]);
+        ix.cnt[r] = k;
+        return;
+    }
+    ix.dead += ix.cnt[r];
+    ix.off[r] = (uint32_t)items.size();
+    items.resize(items.size() + k);
+    fill(items.data() + ix.off[r]);
+    ix.cnt[r] = k;
+}
+
+template <typename T>
+void row_compact(RowIndex& ix, std::vector<T>& items) {
+    if (ix.dead == 0 || ix.dead * 2 <= items.size()) return;
+    std::vector<T> out;
+    out.reserve(items.size() - ix.dead);
+    for (size_t r = 0; r < ix.off.size(); r++) {
+        const uint32_t b = (uint32_t)out.size();
+        out.insert(out.end(), items.begin() + ix.off[r], items.begin() + ix.off[r] + ix.cnt[r]);
+        ix.off[r] = b;
+    }
+    items.swap(out);
+    ix.dead = 0;
+}
 
 // A device-request target parsed once (resolveDeviceTarget, feasible.go:1304-1330).
 struct DevTarget {
@@ -383,7 +448,7 @@ struct pe_stack {
 
     // state
     std::vector<HostNode> nodes;
-    std::vector<uint32_t> attr_off, meta_off, drv_off, net_off, alias_off, hv_off;
+    RowIndex attr_ix, meta_ix, drv_ix, net_ix, alias_ix, hv_ix;
     std::vector<KV> attr_kv, meta_kv;
     std::vector<KF> drv_kf, hv_kf;
     std::vector<uint32_t> net_mode_ids, alias_ids;
@@ -392,10 +457,12 @@ struct pe_stack {
     std::vector<std::pair<uint32_t, int32_t>> alloc_ports;  // (HostIP, port) held by allocs
     std::vector<std::vector<HostAddr>> node_addrs;          // per node, node order
     std::vector<std::vector<int>> node_rhp;                 // per node ReservedHostPorts, parsed
-    // device groups per node (CSR) and their attributes
-    std::vector<uint32_t> dev_off;
+    // device groups per node and their attributes
+    RowIndex dev_ix;
     std::vector<HostDevGroup> dev_groups;
     std::vector<std::pair<uint32_t, pe::DevAttr>> dev_attr;   // sorted by key per group
+    size_t dev_attr_dead = 0;          // attributes of groups rewritten since the last compaction
+    uint32_t n_dev_big = 0;            // live groups with more than 255 healthy instances
     uint32_t max_dev_groups = 0;
     bool dev_packable = true;          // every node fits the packed 4 x u8 free-count column
     std::vector<uint32_t> h_dev_free;  // snapshot free healthy instances per group (no plan)
@@ -423,6 +490,14 @@ struct pe_stack {
     std::map<std::pair<uint32_t, uint32_t>, uint32_t> job_keys;   // (job, ns) -> key
     uint32_t n_jtg_keys = 0;
     std::string preempt_unsupported;           // snapshot outside the on-device limits
+    // what build_alloc_state found, kept so that a node upsert recomputes only
+    // its rows: per-row reasons (kRow*) with their counts, the allocation-only
+    // reasons, the Preemptor records
+    std::vector<uint8_t> row_flags;
+    uint32_t n_row_overheld = 0, n_row_devent = 0, n_row_core_out = 0;
+    bool evict_too_many = false, any_alloc_cores = false, alloc_state_ok = false;
+    std::string cores_unsup_allocs;
+    std::vector<pe::PreemptAlloc> h_palloc;
     // eviction width of the snapshot (PreemptArgs::mask_words, evict.inc): 1
     // while every node holds <= 32 non-terminal allocs, else 8 (<= 256)
     uint32_t evict_words = 1;
@@ -437,6 +512,7 @@ struct pe_stack {
     std::vector<uint64_t> h_core_rsvable, h_core_avail, h_core_base, h_core_used;   // used: host mirror of the plan
     std::vector<int64_t> h_core_spc;
     std::vector<uint8_t> h_core_bad;           // per node: ids >= 256, or reservable cores with TotalCpuCores 0
+    uint32_t n_core_bad = 0, n_core_rows = 0;  // rows with h_core_bad / with reservable cores
     DevMem d_core_rsvable, d_core_avail, d_core_base, d_core_used, d_core_spc, d_palloc_cores;
     DevMem d_node_alloc_off, d_palloc, d_preempted, d_pcount, d_own_existing;
     DevMem d_ev_status, d_ev_score, d_ev_flags, d_ev_out, d_ev_mask, d_ev_rows, d_ev_masks, d_ev_offers, d_ev_named, d_ev_tcodes;
@@ -660,12 +736,12 @@ struct pe_stack {
         NodeView v;
         v.h = &nodes[row];
         v.row = row;
-        v.attrs = {attr_kv.data() + attr_off[row], attr_off[row + 1] - attr_off[row]};
-        v.meta = {meta_kv.data() + meta_off[row], meta_off[row + 1] - meta_off[row]};
-        v.drivers = {drv_kf.data() + drv_off[row], drv_off[row + 1] - drv_off[row]};
-        v.volumes = {hv_kf.data() + hv_off[row], hv_off[row + 1] - hv_off[row]};
-        v.net_modes = {net_mode_ids.data() + net_off[row], net_off[row + 1] - net_off[row]};
-        v.aliases = {alias_ids.data() + alias_off[row], alias_off[row + 1] - alias_off[row]};
+        v.attrs = {attr_kv.data() + attr_ix.b(row), attr_ix.n(row)};
+        v.meta = {meta_kv.data() + meta_ix.b(row), meta_ix.n(row)};
+        v.drivers = {drv_kf.data() + drv_ix.b(row), drv_ix.n(row)};
+        v.volumes = {hv_kf.data() + hv_ix.b(row), hv_ix.n(row)};
+        v.net_modes = {net_mode_ids.data() + net_ix.b(row), net_ix.n(row)};
+        v.aliases = {alias_ids.data() + alias_ix.b(row), alias_ix.n(row)};
         return v;
     }
     uint32_t lookup(const std::string& s) const {
@@ -964,7 +1040,7 @@ bool dev_matches(const pe_stack* s, pe::ConstraintEvaluator& ev, const DevReqSpe
 // DeviceChecker.hasDevices (feasible.go:1206-1274): healthy instances, groups in node order.
 bool has_devices(const pe_stack* s, pe::ConstraintEvaluator& ev, const TgPlan& g, uint32_t row) {
     if (g.dev_reqs.empty()) return true;
-    const uint32_t b = s->dev_off[row], e = s->dev_off[row + 1];
+    const uint32_t b = s->dev_ix.b(row), e = s->dev_ix.e(row);
     if (b == e) return false;
     std::vector<int64_t> avail(e - b);
     for (uint32_t k = b; k < e; k++) avail[k - b] = s->dev_groups[k].healthy;
@@ -1023,7 +1099,7 @@ int build_dev_classes(pe_stack* s, TgPlan& g) {
     std::memset(tab.data(), 0, sizeof(pe::DevClass) * tab.size());
     for (uint32_t c = 0; c < s->ncls; c++) {
         const uint32_t row = s->class_rep[c];
-        const uint32_t b = s->dev_off[row], e = s->dev_off[row + 1];
+        const uint32_t b = s->dev_ix.b(row), e = s->dev_ix.e(row);
         pe::DevClass& d = tab[c];
         d.n_groups = e - b;
         for (size_t q = 0; q < g.dev_reqs.size(); q++) {
@@ -1236,55 +1312,61 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
     s->nodes_gen++;   // node-table-derived device buffers (alias_ok) are stale
     const uint32_t n_old = (uint32_t)s->nodes.size();
     const uint32_t m = nt->n;
-    std::vector<int32_t> src_of(n_new, -1);
-    for (uint32_t i = 0; i < m; i++) {
-        if (target[i] >= n_new || src_of[target[i]] >= 0) return s->fail(PE_EINVAL, "bad node row");
-        src_of[target[i]] = (int32_t)i;
+    // the source rows in target-row order (classes and signatures are interned
+    // in row order, as a full build does); every target once, appended rows
+    // exactly n_old .. n_new - 1
+    std::vector<uint32_t> order(m);
+    for (uint32_t i = 0; i < m; i++) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return target[x] < target[y]; });
+    for (uint32_t j = 0; j < m; j++) {
+        const uint32_t t = target[order[j]];
+        if (t >= n_new || (j && t == target[order[j - 1]])) return s->fail(PE_EINVAL, "bad node row");
     }
-    for (uint32_t r = n_old; r < n_new; r++)
-        if (src_of[r] < 0) return s->fail(PE_EINVAL, "appended node rows must be contiguous");
-    // variable-length node maps: copied into CSR arrays, sorted per node
-    auto rebuild = [&](auto& items, std::vector<uint32_t>& off, const uint32_t* noff, auto item_of, bool sorted) {
-        using T = typename std::decay_t<decltype(items)>::value_type;
-        std::vector<T> out;
-        std::vector<uint32_t> o(n_new + 1, 0);
-        out.reserve(items.size() + (noff ? noff[m] - noff[0] : 0));
-        for (uint32_t r = 0; r < n_new; r++) {
-            const size_t b = out.size();
-            if (src_of[r] >= 0) {
-                const uint32_t i = (uint32_t)src_of[r];
-                for (uint32_t k = noff ? noff[i] : 0; noff && k < noff[i + 1]; k++) out.push_back(item_of(k));
-                if (sorted) std::sort(out.begin() + (long)b, out.end());
-            } else {
-                out.insert(out.end(), items.begin() + off[r], items.begin() + off[r + 1]);
-            }
-            o[r + 1] = (uint32_t)out.size();
-        }
-        items.swap(out);
-        off.swap(o);
+    {
+        uint32_t n_app = 0;
+        for (uint32_t j = 0; j < m; j++) n_app += target[order[j]] >= n_old;
+        if (n_app != n_new - n_old) return s->fail(PE_EINVAL, "appended node rows must be contiguous");
+    }
+    // variable-length node maps, rewritten row by row (sorted per node)
+    auto span = [](const uint32_t* off, uint32_t i) -> uint32_t {
+        return off && off[i + 1] > off[i] ? off[i + 1] - off[i] : 0;
     };
-    if (s->attr_off.size() != n_old + 1) {   // a fresh mirror
-        for (auto* off : {&s->attr_off, &s->meta_off, &s->drv_off, &s->net_off, &s->alias_off, &s->hv_off, &s->dev_off})
-            off->assign(n_old + 1, 0);
-    }
-    rebuild(s->attr_kv, s->attr_off, nt->attr_off, [&](uint32_t k) { return KV(nt->attr_key[k], nt->attr_val[k]); }, true);
-    rebuild(s->meta_kv, s->meta_off, nt->meta_off, [&](uint32_t k) { return KV(nt->meta_key[k], nt->meta_val[k]); }, true);
-    rebuild(s->drv_kf, s->drv_off, nt->drv_off, [&](uint32_t k) { return KF(nt->drv_name[k], nt->drv_flags[k]); }, true);
-    rebuild(s->net_mode_ids, s->net_off, nt->net_off, [&](uint32_t k) { return nt->net_mode[k]; }, false);
-    rebuild(s->alias_ids, s->alias_off, nt->alias_off, [&](uint32_t k) { return nt->alias_name[k]; }, true);
-    rebuild(s->hv_kf, s->hv_off, nt->hv_off, [&](uint32_t k) { return KF(nt->hv_name[k], nt->hv_read_only[k]); }, true);
+    auto put = [&](RowIndex& ix, auto& items, const uint32_t* noff, auto item_of, bool sorted) {
+        ix.rows(n_new);
+        for (uint32_t j = 0; j < m; j++) {
+            const uint32_t i = order[j];
+            const uint32_t k = span(noff, i), k0 = k ? noff[i] : 0;
+            row_set(ix, items, target[i], k, [&](auto* dst) {
+                for (uint32_t q = 0; q < k; q++) dst[q] = item_of(k0 + q);
+                if (sorted) std::sort(dst, dst + k);
+            });
+        }
+        row_compact(ix, items);
+    };
+    put(s->attr_ix, s->attr_kv, nt->attr_off, [&](uint32_t k) { return KV(nt->attr_key[k], nt->attr_val[k]); }, true);
+    put(s->meta_ix, s->meta_kv, nt->meta_off, [&](uint32_t k) { return KV(nt->meta_key[k], nt->meta_val[k]); }, true);
+    put(s->drv_ix, s->drv_kf, nt->drv_off, [&](uint32_t k) { return KF(nt->drv_name[k], nt->drv_flags[k]); }, true);
+    put(s->net_ix, s->net_mode_ids, nt->net_off, [&](uint32_t k) { return nt->net_mode[k]; }, false);
+    put(s->alias_ix, s->alias_ids, nt->alias_off, [&](uint32_t k) { return nt->alias_name[k]; }, true);
+    put(s->hv_ix, s->hv_kf, nt->hv_off, [&](uint32_t k) { return KF(nt->hv_name[k], nt->hv_read_only[k]); }, true);
     // device groups (NodeResources.Devices) with typed attributes
     {
-        std::vector<uint32_t> doff(n_new + 1, 0);
-        std::vector<HostDevGroup> groups;
-        std::vector<std::pair<uint32_t, pe::DevAttr>> attrs;
-        for (uint32_t r = 0; r < n_new; r++) {
-            if (src_of[r] >= 0) {
-                const uint32_t i = (uint32_t)src_of[r];
-                const uint32_t g0 = nt->dev_off ? nt->dev_off[i] : 0, g1 = nt->dev_off ? nt->dev_off[i + 1] : 0;
-                for (uint32_t g = g0; g < g1; g++) {
+        s->dev_ix.rows(n_new);
+        bool max_dirty = false;
+        for (uint32_t j = 0; j < m; j++) {
+            const uint32_t i = order[j], r = target[i];
+            for (uint32_t g = s->dev_ix.b(r); g < s->dev_ix.e(r); g++) {   // the row's old groups leave
+                const HostDevGroup& d = s->dev_groups[g];
+                s->n_dev_big -= d.healthy > 255;
+                s->dev_attr_dead += d.attr_end - d.attr_begin;
+            }
+            if (s->dev_ix.n(r) && s->dev_ix.n(r) == s->max_dev_groups) max_dirty = true;
+            const uint32_t k = span(nt->dev_off, i), g0 = k ? nt->dev_off[i] : 0;
+            row_set(s->dev_ix, s->dev_groups, r, k, [&](HostDevGroup* dst) {
+                for (uint32_t j = 0; j < k; j++) {
+                    const uint32_t g = g0 + j;
                     HostDevGroup d{nt->dev_vendor[g], nt->dev_type[g], nt->dev_name[g], nt->dev_healthy[g], 0, 0};
-                    d.attr_begin = (uint32_t)attrs.size();
+                    d.attr_begin = (uint32_t)s->dev_attr.size();
                     for (uint32_t q = nt->dev_attr_off ? nt->dev_attr_off[g] : 0;
                          nt->dev_attr_off && q < nt->dev_attr_off[g + 1]; q++) {
                         const pe_attr& pa = nt->dev_attr_val[q];
@@ -1295,43 +1377,49 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
                             case PE_ATTR_BOOL: at.kind = pe::DevAttr::kBool; at.b = pa.i != 0; break;
                             default: at.kind = pe::DevAttr::kString; at.s = s->S(pa.s); break;
                         }
-                        attrs.emplace_back(nt->dev_attr_key[q], at);
+                        s->dev_attr.emplace_back(nt->dev_attr_key[q], at);
                     }
-                    d.attr_end = (uint32_t)attrs.size();
-                    std::sort(attrs.begin() + d.attr_begin, attrs.begin() + d.attr_end,
+                    d.attr_end = (uint32_t)s->dev_attr.size();
+                    std::sort(s->dev_attr.begin() + d.attr_begin, s->dev_attr.begin() + d.attr_end,
                               [](const auto& x, const auto& y) { return x.first < y.first; });
-                    groups.push_back(d);
+                    s->n_dev_big += d.healthy > 255;
+                    dst[j] = d;
                 }
-            } else {
-                for (uint32_t g = s->dev_off[r]; g < s->dev_off[r + 1]; g++) {
-                    HostDevGroup d = s->dev_groups[g];
+            });
+            s->max_dev_groups = std::max(s->max_dev_groups, k);
+        }
+        row_compact(s->dev_ix, s->dev_groups);
+        if (s->dev_attr_dead && s->dev_attr_dead * 2 > s->dev_attr.size()) {   // attributes back into group order
+            std::vector<std::pair<uint32_t, pe::DevAttr>> attrs;
+            attrs.reserve(s->dev_attr.size() - s->dev_attr_dead);
+            for (uint32_t r = 0; r < n_new; r++)
+                for (uint32_t g = s->dev_ix.b(r); g < s->dev_ix.e(r); g++) {
+                    HostDevGroup& d = s->dev_groups[g];
                     const uint32_t b = (uint32_t)attrs.size();
                     attrs.insert(attrs.end(), s->dev_attr.begin() + d.attr_begin, s->dev_attr.begin() + d.attr_end);
                     d.attr_begin = b;
                     d.attr_end = (uint32_t)attrs.size();
-                    groups.push_back(d);
                 }
-            }
-            doff[r + 1] = (uint32_t)groups.size();
+            s->dev_attr.swap(attrs);
+            s->dev_attr_dead = 0;
         }
-        s->dev_off.swap(doff);
-        s->dev_groups.swap(groups);
-        s->dev_attr.swap(attrs);
-        s->max_dev_groups = 0;
-        s->dev_packable = true;
-        for (uint32_t r = 0; r < n_new; r++) s->max_dev_groups = std::max(s->max_dev_groups, s->dev_off[r + 1] - s->dev_off[r]);
-        for (const HostDevGroup& d : s->dev_groups) if (d.healthy > 255) s->dev_packable = false;
-        if (s->max_dev_groups > (uint32_t)pe::kMaxDevGroups) s->dev_packable = false;
+        if (max_dirty) {   // a row that held the maximum changed: the exact maximum again
+            s->max_dev_groups = 0;
+            for (uint32_t r = 0; r < n_new; r++) s->max_dev_groups = std::max(s->max_dev_groups, s->dev_ix.n(r));
+        }
+        s->dev_packable = s->n_dev_big == 0 && s->max_dev_groups <= (uint32_t)pe::kMaxDevGroups;
     }
-    // fixed per-node fields, ComputedClass interning
+    // fixed per-node fields, ComputedClass interning; the changed rows' old
+    // class and signature (representatives of those move to another member)
     s->nodes.resize(n_new);
     s->h_node_rec.resize(n_new);
-    std::vector<uint32_t> old_cls(n_new, PE_NONE), old_sig(n_new, PE_NONE);
-    for (uint32_t r = 0; r < n_old; r++)
-        if (src_of[r] >= 0) { old_cls[r] = s->nodes[r].cls; old_sig[r] = s->nodes[r].sig; }
-    for (uint32_t r = 0; r < n_new; r++) {
-        if (src_of[r] < 0) continue;
-        const uint32_t i = (uint32_t)src_of[r];
+    std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> old_of;
+    old_of.reserve(m * 2);
+    for (uint32_t i = 0; i < m; i++)
+        if (target[i] < n_old) old_of.emplace(target[i], std::make_pair(s->nodes[target[i]].cls, s->nodes[target[i]].sig));
+    auto changed = [&](uint32_t r) { return r >= n_old || old_of.count(r) != 0; };
+    for (uint32_t j = 0; j < m; j++) {
+        const uint32_t i = order[j], r = target[i];
         HostNode& h = s->nodes[r];
         h = HostNode();
         h.id = nt->id[i]; h.name = nt->name[i]; h.dc = nt->datacenter[i];
@@ -1359,7 +1447,7 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
                 h.n_device_nets++;
             }
         }
-        h.n_devices = (uint16_t)(s->dev_off[r + 1] - s->dev_off[r]);
+        h.n_devices = (uint16_t)s->dev_ix.n(r);
         pe::NodeRec& rec = s->h_node_rec[r];
         std::memset(&rec, 0, sizeof(rec));
         rec.cls = h.cls;
@@ -1375,11 +1463,12 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
     s->h_core_avail.resize(4 * (size_t)n_new, 0);
     s->h_core_spc.resize(n_new, 0);
     s->h_core_bad.resize(n_new, 0);
-    for (uint32_t r = 0; r < n_new; r++) {
-        if (src_of[r] < 0) continue;
-        const uint32_t i = (uint32_t)src_of[r];
+    for (uint32_t j = 0; j < m; j++) {
+        const uint32_t i = order[j], r = target[i];
         uint64_t* rs = &s->h_core_rsvable[4 * (size_t)r];
         uint64_t* av = &s->h_core_avail[4 * (size_t)r];
+        s->n_core_bad -= s->h_core_bad[r];
+        s->n_core_rows -= (rs[0] | rs[1] | rs[2] | rs[3]) != 0;
         uint64_t rsv[4] = {0, 0, 0, 0};
         for (int w = 0; w < 4; w++) rs[w] = av[w] = 0;
         uint8_t bad = 0;
@@ -1397,13 +1486,14 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         s->h_core_spc[r] = total ? nt->cpu_shares[i] / (int64_t)total : 0;
         if (total == 0 && (rs[0] | rs[1] | rs[2] | rs[3])) bad = 1;
         s->h_core_bad[r] = bad;
+        s->n_core_bad += bad;
+        s->n_core_rows += (rs[0] | rs[1] | rs[2] | rs[3]) != 0;
     }
     // NodeNetworks addresses and ReservedHostPorts (static port asks)
     s->node_addrs.resize(n_new);
     s->node_rhp.resize(n_new);
-    for (uint32_t r = 0; r < n_new; r++) {
-        if (src_of[r] < 0) continue;
-        const uint32_t i = (uint32_t)src_of[r];
+    for (uint32_t j = 0; j < m; j++) {
+        const uint32_t i = order[j], r = target[i];
         auto& av = s->node_addrs[r];
         av.clear();
         for (uint32_t k = nt->addr_off ? nt->addr_off[i] : 0; nt->addr_off && k < nt->addr_off[i + 1]; k++) {
@@ -1416,17 +1506,10 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         s->node_rhp[r].clear();
         if (nt->rsv_host_ports && nt->rsv_host_ports[i] != PE_NONE) s->node_rhp[r] = parse_port_ranges(s->S(nt->rsv_host_ports[i]));
     }
-    s->has_cores = false;
-    s->cores_tg_unsupported.clear();
-    for (uint32_t r = 0; r < n_new; r++) {
-        if (s->h_core_bad[r]) s->cores_tg_unsupported = "core ids >= 256, or reservable cores with TotalCpuCores 0";
-        for (int w = 0; w < 4 && !s->has_cores; w++) s->has_cores = s->h_core_rsvable[4 * (size_t)r + w] != 0;
-    }
-    if (s->has_cores) {
-        HIP_TRY(s, upload_s(s, s->d_core_rsvable, s->h_core_rsvable));
-        HIP_TRY(s, upload_s(s, s->d_core_avail, s->h_core_avail));
-        HIP_TRY(s, upload_s(s, s->d_core_spc, s->h_core_spc));
-    }
+    // the device copies of the core masks are made by build_alloc_state /
+    // refresh_node_rows (whole, or the changed rows)
+    s->has_cores = s->n_core_rows > 0;
+    s->cores_tg_unsupported = s->n_core_bad ? "core ids >= 256, or reservable cores with TotalCpuCores 0" : "";
     s->ncls = (uint32_t)s->class_rep.size();
     // checker-input signatures: nodes with equal ComputedClass AND equal
     // non-hashed checker inputs (drivers, networks, aliases, volumes, device
@@ -1437,7 +1520,7 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         auto eq = [](auto u, auto v) { return u.size() == v.size() && std::equal(u.begin(), u.end(), v.begin()); };
         if (x.h->n_devices != y.h->n_devices) return false;
         for (uint32_t k = 0; k < x.h->n_devices; k++)   // DeviceChecker reads healthy counts
-            if (s->dev_groups[s->dev_off[a_row] + k].healthy != s->dev_groups[s->dev_off[b_row] + k].healthy)
+            if (s->dev_groups[s->dev_ix.b(a_row) + k].healthy != s->dev_groups[s->dev_ix.b(b_row) + k].healthy)
                 return false;
         return x.h->cls == y.h->cls && eq(x.drivers, y.drivers) &&
                eq(x.net_modes, y.net_modes) && eq(x.aliases, y.aliases) && eq(x.volumes, y.volumes);
@@ -1449,7 +1532,7 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         auto mix = [&](uint64_t y) { x = (x ^ y) * 1099511628211ull; x ^= x >> 29; };
         mix(h.cls);
         mix(h.n_devices);
-        for (uint32_t k = s->dev_off[r]; k < s->dev_off[r + 1]; k++) mix(s->dev_groups[k].healthy);
+        for (uint32_t k = s->dev_ix.b(r); k < s->dev_ix.e(r); k++) mix(s->dev_groups[k].healthy);
         mix(v.drivers.size());
         for (auto& d : v.drivers) { mix(d.first); mix(d.second); }
         mix(v.net_modes.size());
@@ -1460,29 +1543,29 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
         for (auto& vv : v.volumes) { mix(vv.first); mix(vv.second); }
         return x;
     };
-    // representatives of changed rows move to another member first
+    // representatives of changed rows move to another member first: the first
+    // unchanged member in row order (a scan from row 0 that stops once every
+    // such class and signature has one)
     {
-        std::vector<uint8_t> changed(n_new, 0);
-        for (uint32_t r = 0; r < n_new; r++) changed[r] = src_of[r] >= 0;
-        std::vector<uint32_t> cls_fix, sig_fix;
-        for (uint32_t c = 0; c < (uint32_t)s->class_rep.size(); c++)
-            if (s->class_rep[c] < n_old && changed[s->class_rep[c]] && old_cls[s->class_rep[c]] == c) cls_fix.push_back(c);
+        std::unordered_set<uint32_t> need_cls, need_sig;
+        for (uint32_t c = 0; c < (uint32_t)s->class_rep.size(); c++) {
+            const uint32_t rep = s->class_rep[c];
+            auto it = old_of.find(rep);
+            if (rep < n_old && it != old_of.end() && it->second.first == c) need_cls.insert(c);
+        }
         for (uint32_t g = 0; g < (uint32_t)s->sig_rep.size(); g++)
-            if (changed[s->sig_rep[g]]) sig_fix.push_back(g);
-        if (!cls_fix.empty() || !sig_fix.empty()) {
-            std::unordered_map<uint32_t, uint32_t> cnew, snew;
-            for (uint32_t r = 0; r < n_new; r++) {
-                if (changed[r]) continue;
-                cnew.emplace(s->nodes[r].cls, r);
-                snew.emplace(s->nodes[r].sig, r);
+            if (changed(s->sig_rep[g])) need_sig.insert(g);
+        if (!need_cls.empty() || !need_sig.empty()) {
+            std::unordered_set<uint32_t> got_cls, got_sig;
+            for (uint32_t r = 0; r < n_new && (got_cls.size() < need_cls.size() || got_sig.size() < need_sig.size()); r++) {
+                if (changed(r)) continue;
+                const uint32_t c = s->nodes[r].cls, g = s->nodes[r].sig;
+                if (need_cls.count(c) && got_cls.insert(c).second) s->class_rep[c] = r;
+                if (need_sig.count(g) && got_sig.insert(g).second) s->sig_rep[g] = r;
             }
-            for (uint32_t c : cls_fix) {
-                auto it = cnew.find(c);
-                if (it != cnew.end()) s->class_rep[c] = it->second;   // else the class keeps no member
-            }
-            for (uint32_t g : sig_fix) {
-                auto it = snew.find(g);
-                if (it != snew.end()) { s->sig_rep[g] = it->second; continue; }
+            // a class with no member left keeps its representative index
+            for (uint32_t g : need_sig) {
+                if (got_sig.count(g)) continue;
                 // no member left: out of its class and of the hash buckets (the
                 // representative row index stays valid for the tables)
                 auto& cs = s->class_sigs[s->sig_cls[g]];
@@ -1492,8 +1575,8 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
             }
         }
     }
-    for (uint32_t r = 0; r < n_new; r++) {
-        if (src_of[r] < 0) continue;
+    for (uint32_t j = 0; j < m; j++) {
+        const uint32_t i = order[j], r = target[i];
         HostNode& h = s->nodes[r];
         const uint64_t hv = sig_hash(r);
         auto& bucket = s->sig_of[hv];
@@ -1537,11 +1620,16 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     s->sig_hash.clear();
     s->sig_rep.clear();
     s->sig_cls.clear();
-    for (auto* off : {&s->attr_off, &s->meta_off, &s->drv_off, &s->net_off, &s->alias_off, &s->hv_off, &s->dev_off})
-        off->assign(1, 0);
+    for (RowIndex* ix : {&s->attr_ix, &s->meta_ix, &s->drv_ix, &s->net_ix, &s->alias_ix, &s->hv_ix, &s->dev_ix})
+        ix->clear();
     s->attr_kv.clear(); s->meta_kv.clear(); s->drv_kf.clear(); s->hv_kf.clear();
     s->net_mode_ids.clear(); s->alias_ids.clear();
     s->dev_groups.clear(); s->dev_attr.clear();
+    s->dev_attr_dead = 0;
+    s->n_dev_big = 0;
+    s->max_dev_groups = 0;
+    s->h_core_rsvable.clear(); s->h_core_avail.clear(); s->h_core_spc.clear(); s->h_core_bad.clear();
+    s->n_core_bad = s->n_core_rows = 0;
     std::vector<uint32_t> target(nt->n);
     for (uint32_t i = 0; i < nt->n; i++) target[i] = i;
     int rc = apply_nodes(s, nt, target, nt->n);
@@ -1599,9 +1687,82 @@ int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index) 
 
 // Everything derived from the snapshot's allocations: base proposed usage,
 // device free counts, the Preemptor's per-node candidate lists.
+constexpr uint8_t kRowOverheld = 1;   // device instances held beyond a group's healthy count
+constexpr uint8_t kRowDevEnt = 2;     // an alloc's device entries beyond the packed 4 x 255
+constexpr uint8_t kRowCoreOut = 4;    // allocs hold cores outside the node's available set
+
+// The unsupported-snapshot reasons from the per-row counts, in the order the
+// full build assigns them (the last assignment wins there).
+static void alloc_state_reasons(pe_stack* s) {
+    s->preempt_unsupported = s->n_row_devent ? "alloc device entries beyond 4 x 255"
+                             : s->evict_too_many ? "more than 256 allocs on a node"
+                             : s->n_row_overheld ? "device instances held beyond the healthy count"
+                                                 : "";
+    s->cores_unsupported = s->n_row_core_out ? "allocs holding reserved cores outside the node's available set"
+                                             : s->cores_unsup_allocs;
+}
+
+// Base record, device usage and Preemptor device fields of one row from the
+// row's non-terminal allocs (slots h_node_alloc_off[r] .. [r + 1]); returns
+// the row's kRow* flags. `slots_changed` collects the Preemptor slots whose
+// device fields were rewritten (null: not needed).
+static uint8_t alloc_row(pe_stack* s, uint32_t r, std::vector<uint32_t>* slots_changed) {
+    uint8_t flags = 0;
+    pe::NodeRec rec = s->h_node_rec[r];
+    const uint32_t ng = s->dev_ix.n(r), g0 = s->dev_ix.b(r);
+    int64_t used[pe::kMaxDevGroups + 1] = {0};
+    std::vector<int64_t> used_big(ng > pe::kMaxDevGroups ? ng : 0, 0);
+    int64_t* du = ng > pe::kMaxDevGroups ? used_big.data() : used;
+    const uint32_t sb = r + 1 < s->h_node_alloc_off.size() ? s->h_node_alloc_off[r] : 0;
+    const uint32_t se = r + 1 < s->h_node_alloc_off.size() ? s->h_node_alloc_off[r + 1] : 0;
+    for (uint32_t slot = sb; slot < se; slot++) {
+        const HostAlloc& a = s->allocs[s->h_palloc_index[slot]];
+        rec.used_cpu += a.cpu;
+        rec.used_mem += a.mem;
+        rec.used_disk += a.disk;
+        rec.used_mbits += a.mbits;
+        rec.used_dyn += a.dyn;
+        pe::PreemptAlloc& x = s->h_palloc[slot];
+        x.dev_g = x.dev_c = 0;
+        x.n_dev = 0;
+        for (uint32_t k = a.dev_begin; k < a.dev_end; k++) {
+            const uint32_t g = s->alloc_dev[k].first, c = s->alloc_dev[k].second;
+            if (g >= ng) continue;   // the group is no longer fingerprinted (devices.go:88-99)
+            du[g] += c;
+            if (x.n_dev >= 4 || g >= 4 || c > 255) { flags |= kRowDevEnt; continue; }
+            x.dev_g |= g << (8 * x.n_dev);
+            x.dev_c |= c << (8 * x.n_dev);
+            x.n_dev++;
+        }
+        if (slots_changed) slots_changed->push_back(slot);
+    }
+    s->h_base_rec[r] = rec;
+    uint32_t packed = 0;
+    for (uint32_t k = 0; k < ng; k++) {
+        const int64_t healthy = (int64_t)s->dev_groups[g0 + k].healthy;
+        if (du[k] > healthy) flags |= kRowOverheld;
+        if (s->dev_packable) packed |= (uint32_t)std::max<int64_t>(0, healthy - du[k]) << (8 * k);
+    }
+    s->h_dev_free[r] = packed;
+    const uint64_t* u = &s->h_core_base[4 * (size_t)r];
+    const uint64_t* av = r < s->h_core_avail.size() / 4 ? &s->h_core_avail[4 * (size_t)r] : nullptr;
+    if (av && (av[0] | av[1] | av[2] | av[3]))
+        for (int w = 0; w < 4; w++)
+            if (u[w] & ~av[w]) flags |= kRowCoreOut;
+    return flags;
+}
+
+static void count_row_flags(pe_stack* s, uint8_t f, int sign) {
+    s->n_row_overheld += sign * ((f & kRowOverheld) != 0);
+    s->n_row_devent += sign * ((f & kRowDevEnt) != 0);
+    s->n_row_core_out += sign * ((f & kRowCoreOut) != 0);
+}
+
+// Everything derived from the snapshot's allocations: base proposed usage,
+// device free counts, the Preemptor's per-node candidate lists.
 int build_alloc_state(pe_stack* s) {
     const uint32_t n = (uint32_t)s->nodes.size();
-    s->h_base_rec = s->h_node_rec;
+    s->alloc_state_ok = false;
     {
         // compact the device-entry pool to the live allocs' ranges: entries
         // overwritten by pe_update_allocs leave dead ranges behind
@@ -1629,62 +1790,48 @@ int build_alloc_state(pe_stack* s) {
     s->job_allocs.clear();
     for (uint32_t i = 0; i < (uint32_t)s->allocs.size(); i++)
         if (!s->allocs[i].terminal) s->job_allocs[s->allocs[i].job].push_back(i);
-    std::vector<int64_t> dev_used(s->dev_groups.size(), 0);
+    // reserved cores held by the snapshot's allocs. Overlapping sets, or cores
+    // outside a node's AllocsFit-available set, fail every AllocsFit on that
+    // node ("cores", funcs.go:158-180): not modelled on the device.
+    s->cores_unsup_allocs.clear();
+    s->h_core_base.assign(4 * (size_t)n, 0);
+    s->any_alloc_cores = false;
     for (const HostAlloc& a : s->allocs) {
         if (a.terminal) continue;
-        for (uint32_t k = a.dev_begin; k < a.dev_end; k++) {
-            const uint32_t g = s->alloc_dev[k].first;
-            if (g < s->dev_off[a.row + 1] - s->dev_off[a.row]) dev_used[s->dev_off[a.row] + g] += s->alloc_dev[k].second;
+        if (a.cores_beyond) s->cores_unsup_allocs = "allocs holding core ids >= 256";
+        uint64_t* u = &s->h_core_base[4 * (size_t)a.row];
+        for (int w = 0; w < 4; w++) {
+            if (!a.cores[w]) continue;
+            s->any_alloc_cores = true;
+            if (u[w] & a.cores[w]) s->cores_unsup_allocs = "allocs holding overlapping reserved cores";
+            u[w] |= a.cores[w];
         }
-        pe::NodeRec& r = s->h_base_rec[a.row];
-        r.used_cpu += a.cpu;
-        r.used_mem += a.mem;
-        r.used_disk += a.disk;
-        r.used_mbits += a.mbits;
-        r.used_dyn += a.dyn;
     }
-    HIP_TRY(s, upload_s(s, s->d_base_rec, s->h_base_rec));
-    HIP_TRY(s, upload_s(s, s->d_rec, s->h_base_rec));
-    // DeviceAccounter free counts (devices.go:25-100) packed 4 x u8 per node
-    s->h_dev_free.assign(n, 0);
-    if (s->dev_packable)
-        for (uint32_t i = 0; i < n; i++)
-            for (uint32_t k = 0; k < s->dev_off[i + 1] - s->dev_off[i]; k++) {
-                const uint32_t g = s->dev_off[i] + k;
-                const int64_t f = std::max<int64_t>(0, (int64_t)s->dev_groups[g].healthy - dev_used[g]);
-                s->h_dev_free[i] |= (uint32_t)f << (8 * k);
-            }
-    HIP_TRY(s, upload_s(s, s->d_dev_free_base, s->h_dev_free));
-    HIP_TRY(s, upload_s(s, s->d_dev_free, s->h_dev_free));
     // Preemptor inputs (preemption.go:96-154): non-terminal allocs per node in table order
+    s->job_keys.clear();
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> jtg;
+    std::vector<uint32_t> cnt(n + 1, 0);
+    for (auto& a : s->allocs) if (!a.terminal) cnt[a.row + 1]++;
+    s->h_node_alloc_off.assign(n + 1, 0);
+    for (uint32_t i = 0; i < n; i++) s->h_node_alloc_off[i + 1] = s->h_node_alloc_off[i] + cnt[i + 1];
+    const uint32_t m = s->h_node_alloc_off[n];
+    s->h_palloc.assign(std::max<uint32_t>(m, 1), pe::PreemptAlloc{});
+    std::memset(s->h_palloc.data(), 0, sizeof(pe::PreemptAlloc) * s->h_palloc.size());
+    s->h_palloc_index.assign(m, 0);
+    s->alloc_slot.assign(s->allocs.size(), PE_NONE);
     {
-        s->preempt_unsupported.clear();
-        for (size_t g = 0; g < dev_used.size(); g++)
-            if (dev_used[g] > (int64_t)s->dev_groups[g].healthy)
-                s->preempt_unsupported = "device instances held beyond the healthy count";
-        s->job_keys.clear();
-        std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> jtg;
-        std::vector<uint32_t> cnt(n + 1, 0);
-        for (auto& a : s->allocs) if (!a.terminal) cnt[a.row + 1]++;
-        s->h_node_alloc_off.assign(n + 1, 0);
-        for (uint32_t i = 0; i < n; i++) s->h_node_alloc_off[i + 1] = s->h_node_alloc_off[i] + cnt[i + 1];
-        const uint32_t m = s->h_node_alloc_off[n];
-        std::vector<pe::PreemptAlloc> pa(std::max<uint32_t>(m, 1));
-        std::memset(pa.data(), 0, sizeof(pe::PreemptAlloc) * pa.size());
-        s->h_palloc_index.assign(m, 0);
-        s->alloc_slot.assign(s->allocs.size(), PE_NONE);
         std::vector<uint32_t> fill(s->h_node_alloc_off.begin(), s->h_node_alloc_off.end() - 1);
         uint32_t max_m = 0;
         for (uint32_t i = 0; i < n; i++) max_m = std::max(max_m, cnt[i + 1]);
         s->evict_words = max_m <= 32u ? 1u : 8u;
-        if (max_m > pe::kEvictMaxAllocs) s->preempt_unsupported = "more than 256 allocs on a node";
+        s->evict_too_many = max_m > pe::kEvictMaxAllocs;
         for (uint32_t i = 0; i < s->allocs.size(); i++) {
             const HostAlloc& a = s->allocs[i];
             if (a.terminal) continue;
             const uint32_t slot = fill[a.row]++;
             s->h_palloc_index[slot] = i;
             s->alloc_slot[i] = slot;
-            pe::PreemptAlloc& x = pa[slot];
+            pe::PreemptAlloc& x = s->h_palloc[slot];
             x.cpu = a.cpu; x.mem = a.mem; x.disk = a.disk;
             x.priority = a.priority; x.max_parallel = a.max_parallel;
             x.job_key = s->job_keys.emplace(std::make_pair(a.job, a.ns), (uint32_t)s->job_keys.size()).first->second;
@@ -1692,69 +1839,145 @@ int build_alloc_state(pe_stack* s) {
             x.mbits = a.mbits;
             x.dyn = a.dyn;
             x.state_index = i | (a.has_net ? pe::kAllocHasNet : 0u);
-            const uint32_t ng = s->dev_off[a.row + 1] - s->dev_off[a.row];
-            for (uint32_t k = a.dev_begin; k < a.dev_end; k++) {
-                const uint32_t g = s->alloc_dev[k].first, c = s->alloc_dev[k].second;
-                if (g >= ng) continue;   // the group is no longer fingerprinted (devices.go:88-99)
-                if (x.n_dev >= 4 || g >= 4 || c > 255) { s->preempt_unsupported = "alloc device entries beyond 4 x 255"; continue; }
-                x.dev_g |= g << (8 * x.n_dev);
-                x.dev_c |= c << (8 * x.n_dev);
-                x.n_dev++;
-            }
         }
-        s->n_jtg_keys = (uint32_t)jtg.size();
-        s->h_preempted.assign(std::max<uint32_t>(m, 1), 0);
-        HIP_TRY(s, upload_s(s, s->d_node_alloc_off, s->h_node_alloc_off));
-        HIP_TRY(s, upload_s(s, s->d_palloc, pa));
-        HIP_TRY(s, upload_s(s, s->d_preempted, s->h_preempted));
-        HIP_TRY(s, upload_s(s, s->d_pcount, std::vector<uint32_t>(std::max<uint32_t>(s->n_jtg_keys, 1), 0)));
     }
+    // per row: base record, device free counts (DeviceAccounter, devices.go:25-100,
+    // packed 4 x u8 per node), the Preemptor's device fields, the row reasons
+    s->h_base_rec = s->h_node_rec;
+    s->h_dev_free.assign(n, 0);
+    s->row_flags.assign(n, 0);
+    s->n_row_overheld = s->n_row_devent = s->n_row_core_out = 0;
+    for (uint32_t r = 0; r < n; r++) {
+        s->row_flags[r] = alloc_row(s, r, nullptr);
+        count_row_flags(s, s->row_flags[r], +1);
+    }
+    alloc_state_reasons(s);
+    HIP_TRY(s, upload_s(s, s->d_base_rec, s->h_base_rec));
+    HIP_TRY(s, upload_s(s, s->d_rec, s->h_base_rec));
+    HIP_TRY(s, upload_s(s, s->d_dev_free_base, s->h_dev_free));
+    HIP_TRY(s, upload_s(s, s->d_dev_free, s->h_dev_free));
+    s->n_jtg_keys = (uint32_t)jtg.size();
+    s->h_preempted.assign(std::max<uint32_t>(m, 1), 0);
+    HIP_TRY(s, upload_s(s, s->d_node_alloc_off, s->h_node_alloc_off));
+    HIP_TRY(s, upload_s(s, s->d_palloc, s->h_palloc));
+    HIP_TRY(s, upload_s(s, s->d_preempted, s->h_preempted));
+    HIP_TRY(s, upload_s(s, s->d_pcount, std::vector<uint32_t>(std::max<uint32_t>(s->n_jtg_keys, 1), 0)));
     std::vector<uint32_t> zeros(n, 0);
     HIP_TRY(s, upload_s(s, s->d_coll_job, zeros));
-    // reserved cores held by the snapshot's allocs. Overlapping sets, or cores
-    // outside a node's AllocsFit-available set, fail every AllocsFit on that
-    // node ("cores", funcs.go:158-180): not modelled on the device.
-    s->cores_unsupported.clear();
-    s->h_core_base.assign(4 * (size_t)n, 0);
-    bool any_alloc_cores = false;
-    for (const HostAlloc& a : s->allocs) {
-        if (a.terminal) continue;
-        if (a.cores_beyond) s->cores_unsupported = "allocs holding core ids >= 256";
-        uint64_t* u = &s->h_core_base[4 * (size_t)a.row];
-        for (int w = 0; w < 4; w++) {
-            if (!a.cores[w]) continue;
-            any_alloc_cores = true;
-            if (u[w] & a.cores[w]) s->cores_unsupported = "allocs holding overlapping reserved cores";
-            u[w] |= a.cores[w];
-        }
-    }
-    if (any_alloc_cores)
-        for (uint32_t r = 0; r < n; r++) {
-            const uint64_t* u = &s->h_core_base[4 * (size_t)r];
-            const uint64_t* av = r < s->h_core_avail.size() / 4 ? &s->h_core_avail[4 * (size_t)r] : nullptr;
-            const bool any = av && (av[0] | av[1] | av[2] | av[3]);
-            for (int w = 0; w < 4 && any; w++)
-                if (u[w] & ~av[w]) s->cores_unsupported = "allocs holding reserved cores outside the node's available set";
-        }
     s->h_core_used = s->h_core_base;
-    if (s->has_cores || any_alloc_cores) {
+    if (s->has_cores || s->any_alloc_cores) {
         if (!s->has_cores) {   // core sets on allocs only: empty reservable masks
             s->h_core_rsvable.assign(4 * (size_t)n, 0);
             s->h_core_avail.assign(4 * (size_t)n, 0);
             s->h_core_spc.assign(n, 0);
             s->has_cores = true;
-            HIP_TRY(s, upload_s(s, s->d_core_rsvable, s->h_core_rsvable));
-            HIP_TRY(s, upload_s(s, s->d_core_avail, s->h_core_avail));
-            HIP_TRY(s, upload_s(s, s->d_core_spc, s->h_core_spc));
         }
+        HIP_TRY(s, upload_s(s, s->d_core_rsvable, s->h_core_rsvable));
+        HIP_TRY(s, upload_s(s, s->d_core_avail, s->h_core_avail));
+        HIP_TRY(s, upload_s(s, s->d_core_spc, s->h_core_spc));
         HIP_TRY(s, upload_s(s, s->d_core_base, s->h_core_base));
         HIP_TRY(s, upload_s(s, s->d_core_used, s->h_core_base));
-        const uint32_t m = s->h_node_alloc_off[n];
         std::vector<uint64_t> pc(4 * (size_t)std::max<uint32_t>(m, 1), 0);
         for (uint32_t slot = 0; slot < m; slot++)
             for (int w = 0; w < 4; w++) pc[4 * (size_t)slot + w] = s->allocs[s->h_palloc_index[slot]].cores[w];
         HIP_TRY(s, upload_s(s, s->d_palloc_cores, pc));
     }
+    s->alloc_state_ok = true;
+    return PE_OK;
+}
+
+// Rows `rows` of a device array from its host mirror `h` (row_elems
+// elements of T per row): one k_scatter_rows launch reading the staging ring,
+// or the whole array when the payload does not fit the ring.
+template <class T>
+int patch_rows(pe_stack* s, DevMem& d, const std::vector<T>& h, const std::vector<uint32_t>& rows, size_t row_elems) {
+    static_assert(sizeof(T) % 4 == 0, "rows of whole 4-byte words");
+    if (rows.empty()) return PE_OK;
+    const uint32_t words = (uint32_t)(row_elems * sizeof(T) / 4);
+    std::vector<uint32_t> payload(rows.size() * (1 + (size_t)words));
+    std::memcpy(payload.data(), rows.data(), rows.size() * 4);
+    uint32_t* dst = payload.data() + rows.size();
+    for (size_t i = 0; i < rows.size(); i++)
+        std::memcpy(dst + i * words, &h[(size_t)rows[i] * row_elems], (size_t)words * 4);
+    const unsigned char* staged = stage_only(s, payload);
+    if (!staged) {
+        HIP_TRY(s, upload_s(s, d, h));
+        return PE_OK;
+    }
+    HIP_TRY(s, pe_launch_scatter_rows(d.p, words, staged, (uint32_t)rows.size(), s->stream));
+    return PE_OK;
+}
+
+// pe_update_nodes' share of build_alloc_state. The snapshot's allocations did
+// not change: only the changed rows and the appended ones (which hold no
+// allocs yet) get their base records, device free counts, Preemptor device
+// fields and row reasons recomputed, and the device arrays are grown (content
+// kept) and patched row by row; the plan then resets as after ResetPlan. A
+// property of the whole snapshot that changed with the update (the packed
+// device column, reserved cores appearing or leaving) takes the full build.
+int refresh_node_rows(pe_stack* s, std::vector<uint32_t> rows, uint32_t n_old, bool packable_before,
+                      bool cores_before) {
+    const uint32_t n = (uint32_t)s->nodes.size();
+    s->has_cores = s->has_cores || s->any_alloc_cores;
+    static const bool force_full = getenv("PE_UPDATE_FULL") != nullptr;   // A/B against the full build
+    if (force_full || !s->alloc_state_ok || s->h_node_alloc_off.size() != (size_t)n_old + 1 ||
+        s->dev_packable != packable_before || s->has_cores != cores_before)
+        return build_alloc_state(s);
+    for (uint32_t r = n_old; r < n; r++) rows.push_back(r);
+    std::sort(rows.begin(), rows.end());
+    const uint32_t m = s->h_node_alloc_off[n_old];
+    s->h_node_alloc_off.resize((size_t)n + 1, m);
+    s->h_base_rec.resize(n);
+    s->h_dev_free.resize(n, 0);
+    s->row_flags.resize(n, 0);
+    s->h_core_base.resize(4 * (size_t)n, 0);
+    std::vector<uint32_t> slots;
+    for (uint32_t r : rows) {
+        count_row_flags(s, s->row_flags[r], -1);
+        s->row_flags[r] = alloc_row(s, r, &slots);
+        count_row_flags(s, s->row_flags[r], +1);
+    }
+    alloc_state_reasons(s);
+    auto grow = [&](DevMem& d, size_t row_bytes, size_t extra) {
+        return d.grow(row_bytes * n + extra, row_bytes * n_old + extra, s->stream);
+    };
+    HIP_TRY(s, grow(s->d_base_rec, sizeof(pe::NodeRec), 0));
+    HIP_TRY(s, grow(s->d_rec, sizeof(pe::NodeRec), 0));
+    HIP_TRY(s, grow(s->d_dev_free_base, 4, 0));
+    HIP_TRY(s, grow(s->d_dev_free, 4, 0));
+    HIP_TRY(s, grow(s->d_node_alloc_off, 4, 4));
+    HIP_TRY(s, grow(s->d_coll_job, 4, 0));
+    int rc;
+    // the working copies too: a launch that reads node fields (class, capacity)
+    // may run before the deferred reset copy lands
+    if ((rc = patch_rows(s, s->d_base_rec, s->h_base_rec, rows, 1))) return rc;
+    if ((rc = patch_rows(s, s->d_rec, s->h_base_rec, rows, 1))) return rc;
+    if ((rc = patch_rows(s, s->d_dev_free_base, s->h_dev_free, rows, 1))) return rc;
+    if ((rc = patch_rows(s, s->d_dev_free, s->h_dev_free, rows, 1))) return rc;
+    if ((rc = patch_rows(s, s->d_palloc, s->h_palloc, slots, 1))) return rc;
+    std::vector<uint32_t> tail;   // node_alloc_off entries of the appended rows
+    for (uint32_t r = n_old; r < n; r++) tail.push_back(r + 1);
+    if ((rc = patch_rows(s, s->d_node_alloc_off, s->h_node_alloc_off, tail, 1))) return rc;
+    HIP_TRY(s, hipMemsetAsync(s->d_coll_job.p, 0, 4 * (size_t)n, s->stream));
+    if (s->has_cores) {
+        HIP_TRY(s, grow(s->d_core_rsvable, 32, 0));
+        HIP_TRY(s, grow(s->d_core_avail, 32, 0));
+        HIP_TRY(s, grow(s->d_core_spc, 8, 0));
+        HIP_TRY(s, grow(s->d_core_base, 32, 0));
+        HIP_TRY(s, grow(s->d_core_used, 32, 0));
+        if ((rc = patch_rows(s, s->d_core_rsvable, s->h_core_rsvable, rows, 4))) return rc;
+        if ((rc = patch_rows(s, s->d_core_avail, s->h_core_avail, rows, 4))) return rc;
+        if ((rc = patch_rows(s, s->d_core_spc, s->h_core_spc, rows, 1))) return rc;
+        std::vector<uint32_t> app(rows.end() - (n - n_old), rows.end());
+        if ((rc = patch_rows(s, s->d_core_base, s->h_core_base, app, 4))) return rc;
+        s->h_core_used = s->h_core_base;
+        HIP_TRY(s, hipMemcpyAsync(s->d_core_used.p, s->d_core_base.p, 32 * (size_t)n, hipMemcpyDeviceToDevice, s->stream));
+    }
+    // a new evaluation context: the deferred ResetPlan copy (rec <- base,
+    // free counts <- base, preempted / pcount zero) runs before the next launch
+    std::fill(s->h_preempted.begin(), s->h_preempted.end(), 0);
+    s->reset_pending = true;
+    s->offer_row = -1;
     return PE_OK;
 }
 
@@ -3930,11 +4153,15 @@ static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_ta
         if (r != PE_NONE && r >= n_old) return s->fail(PE_EINVAL, "node index out of range");
         target[i] = r == PE_NONE ? n_new++ : r;
     }
+    const bool packable_before = s->dev_packable, cores_before = s->has_cores;
     int rc = apply_nodes(s, nodes, target, n_new);
     if (rc) {   // the mirror may be half updated: a reload is required
         s->have_state = false;
         return rc;
     }
+    std::vector<uint32_t> rows;
+    for (uint32_t r : target)
+        if (r < n_old) rows.push_back(r);
     s->plan.clear();
     s->tg_memo.clear();
     s->job_memo.clear();
@@ -3948,7 +4175,7 @@ static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_ta
     retire_tgs(s);
     s->visit.clear();
     s->offset = 0;
-    rc = build_alloc_state(s);
+    rc = refresh_node_rows(s, std::move(rows), n_old, packable_before, cores_before);
     if (rc) s->have_state = false;
     return rc;
 }

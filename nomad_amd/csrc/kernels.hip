@@ -1589,6 +1589,18 @@ __device__ __noinline__ void chain_walk(Sh& sh, const uint16_t* nb, const double
     }
 }
 
+// Row patches (pe_update_nodes): payload = rows[n] then n rows of `words`
+// 4-byte words each, read from the mapped staging; dst row r gets its row.
+__global__ void __launch_bounds__(256) k_scatter_rows(uint32_t* dst, uint32_t words, const uint32_t* payload,
+                                                      uint32_t n) {
+    const uint64_t total = (uint64_t)n * words;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += stride) {
+        const uint32_t i = (uint32_t)(t / words), w = (uint32_t)(t % words);
+        dst[(uint64_t)payload[i] * words + w] = payload[n + t];
+    }
+}
+
 // Per-node count arrays from a sorted sparse list (key = row << 5 | array,
 // value = count): each thread owns one row, zeroes it in every array and
 // writes the row's entries found by binary search. A deferred ResetPlan (R.rec)
@@ -3593,6 +3605,16 @@ hipError_t pe_launch_upload(void* dst, const void* src_mapped, size_t bytes, hip
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(pe::k_upload, dim3((uint32_t)blocks), dim3(256), 0, st, static_cast<unsigned char*>(dst),
                        static_cast<const unsigned char*>(src_mapped), bytes);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_scatter_rows(void* dst, uint32_t words, const void* payload_mapped, uint32_t n, hipStream_t st) {
+    if (!n || !words) return hipSuccess;
+    if (((uintptr_t)dst | (uintptr_t)payload_mapped) & 3) return hipErrorInvalidValue;
+    uint64_t blocks = ((uint64_t)n * words + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(pe::k_scatter_rows, dim3((uint32_t)blocks), dim3(256), 0, st, static_cast<uint32_t*>(dst), words,
+                       static_cast<const uint32_t*>(payload_mapped), n);
     return hipGetLastError();
 }
 

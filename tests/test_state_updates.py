@@ -191,3 +191,59 @@ def test_update_nodes_devices_and_preemption():
     _, _, want = run_place(OracleGenericStack, updated, allocs, job, perm, config=cfg)
     assert_same_placements(got, want)
     assert [g.preempted for g in got] == [w.preempted for w in want]
+
+
+@pytest.mark.gpu
+def test_update_nodes_many_rounds_lists_move_and_compact():
+    """pe_update_nodes rewrites a changed row's lists in place when they do not
+    grow and moves them to the end of their vector when they do; dead ranges
+    are compacted once they outnumber the live ones. Six rounds of upserts
+    that add attributes / meta / drivers (lists grow), drop them (lists
+    shrink), flip classes and append nodes, on one handle; every round equals
+    the oracle on the updated snapshot from scratch."""
+    from nomad_amd.stack import GenericStack
+    nodes, allocs = synth.cluster_c3(1200, seed=41)
+    job = synth.job_c3(60)
+    st = GenericStack()
+    st.SetState(nodes, allocs)
+    cur = list(nodes)
+    rng = random.Random(17)
+    for rnd in range(6):
+        changed, index = [], []
+        for r in rng.sample(range(len(cur)), 400):
+            nd = copy.deepcopy(cur[r])
+            k = (r + rnd) % 4
+            if k == 0:   # longer attribute and meta lists
+                for q in range(rnd + 2):
+                    nd.attributes["extra.%d.%d" % (rnd, q)] = "v%d" % q
+                nd.meta["zone%d" % rnd] = "z%d" % (r % 3)
+            elif k == 1:   # shorter lists
+                for key in [a for a in nd.attributes if a.startswith("extra.")][:3]:
+                    nd.attributes.pop(key)
+                nd.meta.pop("rack", None)
+            elif k == 2:
+                nd.attributes["kernel.name"] = rng.choice(["linux", "windows"])
+                nd.drivers = dict(nd.drivers)
+            else:
+                nd.cpu_shares = rng.choice([4000, 8000, 16000])
+            nd.compute_class()
+            changed.append(nd)
+            index.append(r)
+        for q in range(25):
+            nd = copy.deepcopy(cur[rng.randrange(len(cur))])
+            nd.id = "joined-%d-%d" % (rnd, q)
+            nd.compute_class()
+            changed.append(nd)
+            index.append(None)
+        for nd, r in zip(changed, index):
+            if r is None:
+                cur.append(nd)
+            else:
+                cur[r] = nd
+        st.UpdateNodes(changed, index)
+        perm = synth.shuffle(len(cur), 50 + rnd)
+        st.SetJob(job)
+        st.SetNodes(list(perm))
+        got = st.Place(0, 60)
+        _, _, want = run_place(OracleGenericStack, cur, allocs, job, perm)
+        assert_same_placements(got, want)
