@@ -3525,10 +3525,13 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         }
         if (chain) {
             // one evaluation: values in visit order (coalesced window reads)
+            // PE_BASE_BY_ROW=1: the values by row instead (k_base reads the
+            // records in row order, k_chain gathers the values through the list)
+            static const bool by_row = std::getenv("PE_BASE_BY_ROW") != nullptr;
             HIP_TRY(s, s->d_base.ensure(sizeof(double) * std::max<size_t>(std::max<size_t>(s->nodes.size(), n), 1)));
             A.base = s->d_base.as<double>();
-            A.base_by_pos = 1;
-            HIP_TRY(s, s->d_base1.ensure(sizeof(double) * std::max<size_t>(n, 1)));
+            A.base_by_pos = by_row ? 0 : 1;
+            HIP_TRY(s, s->d_base1.ensure(sizeof(double) * std::max<size_t>(by_row ? s->nodes.size() : n, 1)));
             A.base1 = s->d_base1.as<double>();
             HIP_TRY(s, s->d_chain_vs.ensure(sizeof(double) * (size_t)pe_chain_max_n()));
             A.chain_vs = s->d_chain_vs.as<double>();
@@ -3546,7 +3549,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         ApiScope prof_up_(s, "run_place.upload_visit");
         const bool is_visit = &order == &s->visit;
         const unsigned char* src = nullptr;
-        if (chain && !(is_visit && s->d_visit_is_visit)) {
+        if (chain && A.base_by_pos && !(is_visit && s->d_visit_is_visit)) {
             HIP_TRY(s, s->d_visit.ensure(sizeof(uint32_t) * (size_t)n));
             src = stage_only(s, order);
         }
@@ -3577,7 +3580,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     bool fused = false;
     if (chain) {
         const uint32_t base_blocks = (2u * (uint32_t)n + 63u) / 64u;
-        fused = (uint32_t)n <= pe_chain_fused_max_n() && pe_chain_shape(n) <= 4 &&
+        fused = A.base_by_pos && (uint32_t)n <= pe_chain_fused_max_n() && pe_chain_shape(n) <= 4 &&
                 count <= pe_chain_fused_max_count() && count <= chunk &&
                 s->nodes.size() <= 16384 && std::getenv("PE_CHAIN_FUSED") == nullptr;
         if (fused && s->fold_pending && s->pending_fold.ncls > pe_chain_fused_max_classes()) fused = false;

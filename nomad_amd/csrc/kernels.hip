@@ -1299,8 +1299,16 @@ template <bool FOLD>
 __global__ void __launch_bounds__(kBaseBlock) k_base(BatchArgs A) {
     __shared__ uint8_t cls_ok[FOLD ? kFoldMaxClasses : 1];
     const uint32_t stride = gridDim.x * kBaseBlock;
-    TgTables tg = A.tg;
+    // the tables straight from the kernel arguments: a local copy of TgTables
+    // (its per-set arrays are indexed at run time) lived in scratch, 680 B per
+    // lane written and read back by every launch
+    const TgTables& tg = A.tg;
     const uint8_t* class_ok = A.tg.class_ok;
+    auto fold_ok = [&](uint32_t row, uint32_t c) {
+        bool ok = c < A.fold.ncls && cls_ok[c] != 0;
+        if (A.fold.node_ok) ok = ok && A.fold.node_ok[row] != 0;
+        return ok;
+    };
     if (FOLD) {
         const FoldArgs& F = A.fold;
         for (uint32_t c = threadIdx.x; c < F.ncls; c += kBaseBlock) {
@@ -1309,14 +1317,9 @@ __global__ void __launch_bounds__(kBaseBlock) k_base(BatchArgs A) {
             if (blockIdx.x == 0) F.class_dst[c] = v;
         }
         __syncthreads();
-        for (uint32_t row = blockIdx.x * kBaseBlock + threadIdx.x; row < A.soa.n; row += stride) {
-            const uint32_t c = A.soa.rec[row].cls;
-            bool ok = c < F.ncls && cls_ok[c] != 0;
-            if (F.node_ok) ok = ok && F.node_ok[row] != 0;
-            F.feas[row] = ok ? 1 : 0;
-        }
+        for (uint32_t row = blockIdx.x * kBaseBlock + threadIdx.x; row < A.soa.n; row += stride)
+            F.feas[row] = fold_ok(row, A.soa.rec[row].cls) ? 1 : 0;
         class_ok = cls_ok;
-        tg.node_feas = nullptr;   // status_loaded: class_ok[cls] && node_ok[row]
     }
     const uint32_t m = A.base_by_pos ? A.n_visit : A.soa.n;
     const uint32_t sh = A.base1 ? 1u : 0u;
@@ -1334,7 +1337,14 @@ __global__ void __launch_bounds__(kBaseBlock) k_base(BatchArgs A) {
             }
         }
         NodeIn in;
-        load_node(A.soa, tg, row, in);
+        if (FOLD) {   // the verdict from the LDS table: other workgroups are still storing node_feas
+            in.r = A.soa.rec[row];
+            in.coll_tg = tg.coll_tg[row];
+            in.dev_free = tg.dev_free ? tg.dev_free[row] : 0u;
+            in.feas = fold_ok(row, in.r.cls) ? 1u : 0u;
+        } else {
+            load_node(A.soa, tg, row, in);
+        }
         NodeEval ev;
         ev.score = 0.0;
         eval_loaded<false, false>(A.soa, tg, class_ok, A.ask, dk, A.penalty_bits, A.log10, nullptr, row, in, &ev);
