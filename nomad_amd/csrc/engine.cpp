@@ -5257,8 +5257,8 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     L.state = s->d_loop_state.as<uint32_t>();
     const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
     if (prof) {
-        HIP_TRY(s, s->d_prof.ensure(8 * sizeof(unsigned long long)));
-        HIP_TRY(s, hipMemsetAsync(s->d_prof.p, 0, 8 * sizeof(unsigned long long), s->stream));
+        HIP_TRY(s, s->d_prof.ensure(16 * sizeof(unsigned long long)));
+        HIP_TRY(s, hipMemsetAsync(s->d_prof.p, 0, 16 * sizeof(unsigned long long), s->stream));
         L.prof = s->d_prof.as<unsigned long long>();
     }
     HIP_TRY_STATE(s, pe_launch_ploop(&L, s->stream));
@@ -5279,13 +5279,13 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     s->last_ms = ms;
     s->last_ms_pending = false;
     if (prof) {
-        unsigned long long h[8];
+        unsigned long long h[16];
         HIP_TRY(s, hipMemcpy(h, L.prof, sizeof(h), hipMemcpyDeviceToHost));
         std::fprintf(stderr, "k_ploop: %u placements, %.3f ms total; us: plain resolve %.1f, refresh %.1f, preempt "
                              "resolve %.1f, winner %.1f (its evict_eval %.1f, commit %.1f); refreshed %llu dirty + %llu pcount "
-                             "readers\n",
+                             "readers; winner evict_eval again, cache-warm %.1f (%llu calls)\n",
                      st[0], ms, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[6] / 100.0, h[7] / 100.0, h[4],
-                     h[5]);
+                     h[5], h[8] / 100.0, h[9]);
     }
     *handled = true;
     const uint32_t p = std::min(st[0], count);
