@@ -1,7 +1,9 @@
 #!/bin/bash
-# Round-4 GPU pass: the -m gpu suite, the default bench line, then rocprofv3
-# kernel stats of the headline loop (with its device timeline), of the 2^24-node
-# scoring sweep and of the C5 loop. Every GPU step has its own time limit; the
+# Round-4 GPU pass: the -m gpu suite, the FETCH_SIZE calibration, the default
+# bench line, then rocprofv3 kernel stats of the headline loop (with its device
+# timeline), of the 2^24-node scoring sweep and of the C5 loop, and the PMC
+# traffic passes of the headline evaluation (tools/headline_pmc_r04.sh) and of
+# the sweep (FETCH_SIZE x 2, the calibrated 16-B streaming factor). Every GPU step has its own time limit; the
 # script stops at the first failure. Outputs in gpurun_out/<tag>/ (copied into
 # profiles/r04/ by hand afterwards). SKIP_TESTS=1 skips the suite.
 set -eo pipefail
@@ -39,4 +41,14 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5" -o c5 -- \
   python3 "$ROOT/tools/c5_prof.py" > "$OUT/c5.log" 2>&1
 cat "$OUT/sweep.log" "$OUT/c5.log" | tail -20
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/sweep_f" -o f -- \
+  python3 "$ROOT/tools/sweep_variants.py" 16777216 0 0 > /dev/null 2> "$OUT/sweep_f.err"
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/sweep_w" -o w -- \
+  python3 "$ROOT/tools/sweep_variants.py" 16777216 0 0 > /dev/null 2> "$OUT/sweep_w.err"
+cd "$ROOT"
+python3 tools/pmc_traffic.py $(find "$OUT/sweep_f" -name "*counter_collection.csv" -print -quit) \
+  $(find "$OUT/sweep_w" -name "*counter_collection.csv" -print -quit) "k_sweep<" 16777216 76 "$OUT/sweep_traffic.json" 2.0 \
+  | grep -E "traffic_over|bytes_per_launch"
+bash tools/headline_pmc_r04.sh | grep -E "traffic_over|k_base_bytes|k_chain_bytes"
+cp gpurun_out/headline_pmc/headline_traffic.json "$OUT/headline_traffic.json"
 find "$OUT" -name "*kernel_stats.csv" | sort
