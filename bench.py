@@ -396,20 +396,35 @@ def section_c4_drop_in(device, cpu_s):
     st = SystemStack(device=device)
     st.SetStateColumnar(cs)
     times, placed = [], 0
+    dropin.view_served(reset=True)
     for i in range(4):
         st.ResetPlan()
         st.SetJob(job)
         _, _, placed, secs = dropin.system_loop(st, 0, rows)
         times.append(secs)
+    from_view = dropin.view_served(reset=True) / 4
     stats = (C.c_uint64 * 2)()
     st._lib.pe_system_spec_stats(C.c_void_p(st._h), stats)
     kms = st.last_kernel_ms()
+    # the same loop crossing into C for every triple (no served system-Select view)
+    crossing = []
+    dropin.use_view(False)
+    try:
+        for i in range(3):
+            st.ResetPlan()
+            st.SetJob(job)
+            crossing.append(dropin.system_loop(st, 0, rows)[3])
+    finally:
+        dropin.use_view(True)
     st.close()
     wall = float(np.median(times[1:]))
+    wall_x = float(np.median(crossing[1:]))
     out = {"workload": "C4 caller protocol: mock.SystemJob on %d nodes, SetNodes([node]) + Select + Commit per "
-                       "node from a C loop (one evaluation)" % n,
+                       "node from a C loop (one evaluation), the triples the served system-Select view covers "
+                       "answered from it" % n,
            "placed": int(placed), "nodes_per_s": n / wall, "wall_ms": wall * 1e3, "cache_kernel_ms": kms,
-           "cache_passes": int(stats[0]), "served_selects": int(stats[1])}
+           "cache_passes": int(stats[0]), "served_selects": int(stats[1]), "from_view_per_eval": from_view,
+           "nodes_per_s_crossing": n / wall_x, "wall_ms_crossing": wall_x * 1e3}
     if cpu_s > 0:
         from oracle.oracle import OracleSystemStack
         ns = 20000

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 6u
+#define PE_ABI_VERSION 7u
 #define PE_NONE 0xFFFFFFFFu
 #define PE_MAX_SCORES 8
 #define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried inline per RankedNode (the
@@ -558,6 +558,44 @@ typedef struct pe_spec_view {
     uint32_t confirmed;           /* caller and engine: Commits that named the answered row */
 } pe_spec_view;
 pe_spec_view* pe_spec_view_get(pe_stack* s);
+/* SystemScheduler.computePlacements (scheduler_system.go:283-425) runs, for
+ * every node, SetNodes([node]) + Select + (on an option) Plan.AppendAlloc:
+ * three crossings per node (scheduler_system.go:289-302). From a task group's
+ * third single-node Select the engine answers from a per-row cache filled by
+ * one k_system pass; this view exposes that cache so the
+ * caller answers the triples from host memory and logs them, and crosses into
+ * C only when it deviates. One view per handle, used from its thread.
+ *
+ *   SetNodes([row]) + Select(tg) with no options, when v->n_rows > 0,
+ *     tg == v->tg_index, row < v->n_rows, v->n_log < v->log_cap and
+ *     outcome[row] is servable: a finite double is an option on `row` with
+ *     that FinalScore (one score, nodes_evaluated 1); a NaN whose low two bits
+ *     are 1 (filtered) or 2 (exhausted) is nil with nodes_filtered /
+ *     nodes_exhausted 1 -- unless v->preempt and it is exhausted (BinPack with
+ *     eviction answers: go to C); low bits 3 (PE_SYS_STALE) mean the row
+ *     changed since the pass: go to C. Then v->log[v->n_log++] = row, with
+ *     PE_SYS_NIL set for a nil answer;
+ *   the Commit of that option: v->log[v->n_log - 1] |= PE_SYS_COMMITTED and
+ *     outcome[row] = PE_SYS_STALE (a committed row is not served again);
+ *   anything else goes through the entry points, which first take the log
+ *     over (the engine state is then exactly what the sequential calls would
+ *     have produced); they may withdraw the view (v->epoch changes; v->n_rows 0).
+ * Replaces: the SetNodes / Select / Commit crossings of the per-node loop. */
+#define PE_SYS_NIL (1u << 31)
+#define PE_SYS_COMMITTED (1u << 30)
+#define PE_SYS_ROW_MASK 0x3FFFFFFFu
+#define PE_SYS_STALE 0x7FF8000000000003ull
+typedef struct pe_system_view {
+    uint32_t epoch;               /* engine: changes whenever outcome / n_rows / tg_index change */
+    uint32_t tg_index;            /* the task group the outcomes answer */
+    uint32_t n_rows;              /* 0: nothing to serve */
+    uint32_t log_cap;             /* entries log[] can hold */
+    uint64_t* outcome;            /* [n_rows] per row (bits of a double) */
+    uint32_t* log;                /* [log_cap] served Selects in order, written by the caller */
+    uint32_t n_log;               /* caller and engine: entries written / taken over */
+    uint32_t preempt;             /* nonzero: exhausted rows go to the engine */
+} pe_system_view;
+pe_system_view* pe_system_view_get(pe_stack* s);
 int pe_set_cursor(pe_stack* s, uint32_t tg_index, uint32_t offset, uint32_t limit);
 /* Host-side constraint semantics used for pre-resolution (checkConstraint,
  * feasible.go:785-820), exposed for known-answer tests; needs no device.

@@ -227,7 +227,7 @@ ENGINE_SYMBOLS = [
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
     "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
-    "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get",
+    "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get", "pe_system_view_get",
 ]
 
 
@@ -242,6 +242,18 @@ class pe_spec_rec(C.Structure):   # nomad_pe.h: a served-Select record
 class pe_spec_view(C.Structure):
     _fields_ = [("epoch", C.c_uint32), ("tg_index", C.c_uint32), ("n_rec", C.c_uint32), ("pad0", C.c_uint32),
                 ("recs", C.POINTER(pe_spec_rec)), ("served", C.c_uint32), ("confirmed", C.c_uint32)]
+
+
+PE_SYS_NIL = 1 << 31
+PE_SYS_COMMITTED = 1 << 30
+PE_SYS_ROW_MASK = 0x3FFFFFFF
+PE_SYS_STALE = 0x7FF8000000000003
+
+
+class pe_system_view(C.Structure):   # nomad_pe.h: the served system-Select view
+    _fields_ = [("epoch", C.c_uint32), ("tg_index", C.c_uint32), ("n_rows", C.c_uint32), ("log_cap", C.c_uint32),
+                ("outcome", C.POINTER(C.c_uint64)), ("log", C.POINTER(C.c_uint32)), ("n_log", C.c_uint32),
+                ("preempt", C.c_uint32)]
 
 
 def bind(lib, prefix, create_name, destroy_name, error_name):

@@ -670,6 +670,9 @@ struct pe_stack {
     std::vector<pe::EmitRec>* emit_sink = nullptr;   // run_place: keep chain records compact here
     bool emit_sunk = false;                          // ... and it did
     pe_spec_view sview{};              // the run's records for caller-served Selects (pe_spec_view_get)
+    pe_system_view sysview{};          // the per-row cache for caller-served system Selects (pe_system_view_get)
+    std::vector<uint32_t> sys_log;     // its log
+    uint32_t sys_taken = 0;            // log entries taken over
     bool spec_on = true;               // PE_SPECULATE=0: every Select runs on its own
     uint64_t spec_stats[4] = {0, 0, 0, 0};   // runs, Selects served, rollbacks, records computed
     DevMem ck_rec, ck_coll_job, ck_coll_tg, ck_dev_free, ck_pset[pe::kMaxPsets];
@@ -761,6 +764,7 @@ static void elig_log_span(pe_stack* s, uint32_t tgi, uint32_t begin, uint32_t le
 static void kid_log(pe_stack* s, uint8_t kind, uint32_t tgi, int32_t row, const uint32_t* a, uint32_t n);
 }
 
+static void elig_resolve(pe_stack* s);   // the served system-Select view replays it
 namespace {
 
 constexpr uint32_t kFullLdsMaxN = 32768;          // k_fullpass_lds tried up to this list length
@@ -2306,7 +2310,10 @@ static const pe::EmitRec& spec_rec(const pe_stack::Spec& sp, uint32_t k) {
     return sp.compact ? sp.crecs[k] : sp.vrecs[k];
 }
 
+static void sys_view_take(pe_stack* s);
+
 static void view_take(pe_stack* s) {
+    sys_view_take(s);
     pe_spec_view& v = s->sview;
     pe_stack::Spec& sp = s->spec;
     if (!v.n_rec || !sp.active) return;
@@ -2366,8 +2373,88 @@ static void view_withdraw(pe_stack* s) {
     v.served = v.confirmed = 0;
 }
 
+// ---- the served system-Select view (pe_system_view) --------------------------
+// The per-row cache of the active k_system pass and a log the caller writes
+// for every SetNodes([row]) + Select (+ Commit) it answered from it; taken over
+// exactly as pe_set_nodes' per-node path, sys_serve and commit_one would have
+// done it.
+constexpr uint64_t kSysNaNBits = 0x7FF8000000000000ull;
+constexpr uint64_t kSysStale = kSysNaNBits | 3u;
+static_assert(kSysStale == PE_SYS_STALE, "the view's stale marker is the cache's");
+
+static void sys_view_take(pe_stack* s) {
+    pe_system_view& v = s->sysview;
+    if (!v.n_rows || v.n_log == s->sys_taken) return;
+    pe_stack::SysSpec& y = s->sys;
+    const uint32_t upto = std::min(v.n_log, v.log_cap);
+    if (!y.active || y.tgi >= s->tgs.size() || s->visit.size() != 1) { s->sys_taken = upto; return; }
+    const auto name = s->tgs[y.tgi]->name;
+    uint64_t* cache = s->h_sys_cache.as<uint64_t>();
+    for (uint32_t k = s->sys_taken; k < upto; k++) {
+        const uint32_t e = v.log[k];
+        const uint32_t row = e & PE_SYS_ROW_MASK;
+        if (row >= s->nodes.size()) continue;
+        // SetNodes([row]): the per-node path of pe_set_nodes
+        if (!s->elig_log.empty()) elig_resolve(s);
+        s->gen++;
+        s->visit[0] = row;
+        s->d_visit_is_visit = false;
+        s->rank_of_valid = false;
+        s->visit_unique = true;
+        s->offset = 0;
+        s->limit = 2;
+        // Select: sys_serve
+        const bool nil = (e & PE_SYS_NIL) != 0;
+        y.served_row = nil ? -1 : (int32_t)row;
+        y.served++;
+        s->offer_row = y.served_row;
+        s->offers = 0xFFFFFFFFu;
+        s->metrics_valid = false;
+        elig_log_span(s, y.tgi, 0, 1);
+        // Commit: commit_one's served branch
+        if (!nil && (e & PE_SYS_COMMITTED)) {
+            y.served_row = -1;
+            y.pending.push_back(row);
+            cache[row] = kSysStale;
+            s->plan.emplace_back(name, row);
+            s->offer_row = -1;
+        }
+    }
+    s->sys_taken = upto;
+}
+
+static void sys_view_publish(pe_stack* s) {
+    pe_system_view& v = s->sysview;
+    const uint32_t n = (uint32_t)s->nodes.size();
+    v.epoch++;
+    v.tg_index = s->sys.tgi;
+    s->sys_log.resize(std::max<uint32_t>(n, 1));
+    v.log = s->sys_log.data();
+    v.log_cap = n;
+    v.n_log = 0;
+    s->sys_taken = 0;
+    v.outcome = s->h_sys_cache.as<uint64_t>();
+    v.preempt = s->cfg.preempt ? 1u : 0u;
+    v.n_rows = (s->metrics_on || !s->kids.empty()) ? 0u : n;
+}
+
+static void sys_view_withdraw(pe_stack* s) {
+    pe_system_view& v = s->sysview;
+    if (!v.n_rows && !v.outcome) return;
+    v.epoch++;
+    v.n_rows = 0;
+    v.outcome = nullptr;
+    v.n_log = 0;
+    s->sys_taken = 0;
+}
+
+static void sys_deactivate(pe_stack* s) {
+    s->sys.active = false;
+    sys_view_withdraw(s);
+}
+
 // Every entry point first takes over the Selects / Commits the caller served
-// from the view, then launches a deferred ResetPlan copy.
+// from the views, then launches a deferred ResetPlan copy.
 #define PE_FLUSH_RESET(s)                             \
     do {                                              \
         if (s) view_take(s);                          \
@@ -4239,7 +4326,7 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
         const int frc = spec_flush(s);   // a different job: the plan so far goes to HBM first
         if (frc) return frc;
     }
-    s->sys.active = false;   // per-row outcomes of the previous job's groups
+    sys_deactivate(s);   // per-row outcomes of the previous job's groups
     s->sys.singles = 0;
     s->sys.singles_tgi = PE_NONE;
     s->have_job_version = true;
@@ -4399,6 +4486,7 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
 
 int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
     if (!s) return PE_EINVAL;
+    sys_view_take(s);   // the caller's served system Selects first
     if (n == 1 && rows && s->sys.active && s->visit.size() == 1 && rows[0] < s->nodes.size()) {
         // SystemScheduler's per-node SetNodes while the per-row cache answers:
         // the task group's tables do not depend on the list (every class's
@@ -4867,6 +4955,7 @@ static int sys_start(pe_stack* s, uint32_t tgi) {
     y.tgi = tgi;
     y.served_row = -1;
     y.passes++;
+    sys_view_publish(s);
     return PE_OK;
 }
 
@@ -5763,7 +5852,7 @@ static void spec_drop(pe_stack* s) {
     s->spec.active = false;
     s->spec.pending = false;
     s->spec.grow = 1;
-    s->sys.active = false;   // a new evaluation context: queued commits are moot
+    sys_deactivate(s);   // a new evaluation context: queued commits are moot
     s->sys.pending.clear();
     s->sys.singles = 0;
     s->sys.singles_tgi = PE_NONE;
@@ -6639,11 +6728,13 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
 
 extern "C" int pe_set_metrics(pe_stack* s, int on) {
     if (!s) return PE_EINVAL;
+    view_take(s);
     {
         const int frc = spec_flush(s);
         if (frc) return frc;
     }
     s->metrics_on = on != 0;
+    if (s->metrics_on) sys_view_withdraw(s);   // served Selects would carry no metrics
     s->metrics_valid = false;
     return PE_OK;
 }
@@ -6663,7 +6754,7 @@ extern "C" int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap) {
 
 static int system_place_one(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     const int rc = system_place_impl(s, tgi, out_score, out_status, placed);
-    if (s) s->sys.active = false;   // rows committed on the device: the per-row cache is stale
+    if (s) sys_deactivate(s);   // rows committed on the device: the per-row cache is stale
     // one single-node Select per row of the list (scheduler_system.go:290-422)
     if (rc == PE_OK) elig_log_span(s, tgi, 0, (uint32_t)s->visit.size());
     return rc;
@@ -6755,12 +6846,13 @@ int pe_put_eligibility(pe_stack* s, const pe_class_feas* in, uint32_t n) {
     }
     if (changed) {
         invalidate_tables(s);
-        s->sys.active = false;   // class verdicts changed under the per-row cache
+        sys_deactivate(s);   // class verdicts changed under the per-row cache
     }
     return PE_OK;
 }
 
 pe_spec_view* pe_spec_view_get(pe_stack* s) { return s ? &s->sview : nullptr; }
+pe_system_view* pe_system_view_get(pe_stack* s) { return s ? &s->sysview : nullptr; }
 
 int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit) {
     if (!s) return PE_EINVAL;
@@ -7074,7 +7166,7 @@ static int multi_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint
         HIP_TRY(s, hipStreamSynchronize(x->stream));
         for (uint32_t e = 0; e < N; e++)
             for (uint32_t r : rows[e]) x->plan.emplace_back(x->tgs[tgi]->name, r);   // list order
-        x->sys.active = false;
+        sys_deactivate(x);
         x->gen++;
     }
     HIP_TRY(s, hipSetDevice(s->device));

@@ -43,6 +43,7 @@ struct dropin_api {
     int (*commit_preempt)(void*, uint32_t, int32_t, const uint32_t*, uint32_t);
     int (*preempted_of)(const void*, uint32_t, uint32_t*, uint32_t);
     pe_spec_view* (*spec_view_get)(void*);   // null: every Select and Commit crosses
+    pe_system_view* (*system_view_get)(void*);   // null: every per-node triple crosses
 };
 
 static int g_use_view = 1;
@@ -165,6 +166,9 @@ int dropin_evals(const dropin_api* api, void* h, const pe_strtab* strs, const pe
 // options (BinPack evicts inside the Select when preemption is enabled); an
 // option is appended to the plan (Commit, with its preempted allocs). Per node
 // out: status 0 placed / 1 filtered / 2 exhausted, score (FinalScore or NaN).
+// With the engine's served system-Select view (pe_system_view_get) the triple
+// of a node the view covers is answered from host memory and logged, as the Go
+// shim does; the others cross.
 // `flush` (may be null) is called once at the end, inside the timed region:
 // the entry point that forces queued device work (e.g. the next call that
 // reads the device state). Returns 0 or the first failing status.
@@ -177,7 +181,31 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
     int rc = 0;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
+    pe_system_view* v = (g_use_view && api->system_view_get) ? api->system_view_get(h) : nullptr;
     for (uint32_t i = 0; i < n; i++) {
+        const uint32_t row = rows[i];
+        if (v && v->n_rows && v->tg_index == tg && row < v->n_rows && v->n_log < v->log_cap) {
+            uint64_t bits = v->outcome[row];
+            const bool nan = (bits & 0x7FF8000000000000ull) == 0x7FF8000000000000ull;
+            const uint32_t code = nan ? (uint32_t)(bits & 3u) : 0u;
+            if (code != 3u && !(code == 2u && v->preempt)) {
+                if (code) {   // nil: filtered or exhausted
+                    v->log[v->n_log++] = row | PE_SYS_NIL;
+                    status[i] = (uint8_t)code;
+                    score[i] = __builtin_nan("");
+                } else {      // an option, appended to the plan
+                    double sc;
+                    std::memcpy(&sc, &bits, sizeof(sc));
+                    v->log[v->n_log++] = row | PE_SYS_COMMITTED;
+                    v->outcome[row] = PE_SYS_STALE;
+                    status[i] = 0;
+                    score[i] = sc;
+                    p++;
+                }
+                g_view_served++;
+                continue;
+            }
+        }
         uint32_t limit;
         rc = api->set_nodes(h, rows + i, 1, &limit);
         if (rc) break;
