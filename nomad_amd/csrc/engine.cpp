@@ -2385,11 +2385,53 @@ static_assert(kSysStale == PE_SYS_STALE, "the view's stale marker is the cache's
 static void sys_view_take(pe_stack* s) {
     pe_system_view& v = s->sysview;
     if (!v.n_rows || v.n_log == s->sys_taken) return;
+    ApiScope prof_(s, "sys_view_take");
     pe_stack::SysSpec& y = s->sys;
     const uint32_t upto = std::min(v.n_log, v.log_cap);
     if (!y.active || y.tgi >= s->tgs.size() || s->visit.size() != 1) { s->sys_taken = upto; return; }
     const auto name = s->tgs[y.tgi]->name;
     uint64_t* cache = s->h_sys_cache.as<uint64_t>();
+    if (s->elig_log.empty() && (s->elig_mute || s->tgs[y.tgi]->elig_complete)) {
+        // nothing for EvalEligibility to log: the per-node SetNodes / Select
+        // bookkeeping leaves the last entry's state, and only the commits
+        // need one step each
+        uint32_t last = PE_NONE;
+        bool last_nil = true;
+        uint32_t cnt = 0;
+        y.pending.reserve(y.pending.size() + (upto - s->sys_taken));
+        s->plan.reserve(s->plan.size() + (upto - s->sys_taken));
+        for (uint32_t k = s->sys_taken; k < upto; k++) {
+            const uint32_t e = v.log[k];
+            const uint32_t row = e & PE_SYS_ROW_MASK;
+            if (row >= s->nodes.size()) continue;
+            cnt++;
+            last = row;
+            last_nil = (e & PE_SYS_NIL) != 0;
+            if (!last_nil && (e & PE_SYS_COMMITTED)) {
+                y.pending.push_back(row);
+                cache[row] = kSysStale;
+                s->plan.emplace_back(name, row);
+            }
+        }
+        if (cnt) {
+            const uint32_t le = v.log[upto - 1];
+            const bool committed = !last_nil && (le & PE_SYS_COMMITTED) && (le & PE_SYS_ROW_MASK) == last;
+            s->gen += cnt;   // one per SetNodes, as the per-node path counts
+            s->visit[0] = last;
+            s->d_visit_is_visit = false;
+            s->rank_of_valid = false;
+            s->visit_unique = true;
+            s->offset = 0;
+            s->limit = 2;
+            y.served += cnt;
+            y.served_row = (last_nil || committed) ? -1 : (int32_t)last;
+            s->offer_row = y.served_row;
+            s->offers = 0xFFFFFFFFu;
+            s->metrics_valid = false;
+        }
+        s->sys_taken = upto;
+        return;
+    }
     for (uint32_t k = s->sys_taken; k < upto; k++) {
         const uint32_t e = v.log[k];
         const uint32_t row = e & PE_SYS_ROW_MASK;
@@ -4885,6 +4927,7 @@ static void sys_touch(pe_stack* s, uint32_t row) {
 
 // The queued Plan.AppendAllocs of served system Selects, into HBM at once.
 static int sys_flush(pe_stack* s) {
+    ApiScope prof_(s, "sys_flush");
     pe_stack::SysSpec& y = s->sys;
     if (y.pending.empty()) return PE_OK;
     if (y.tgi >= s->tgs.size()) { y.pending.clear(); return s->fail(PE_ESTATE, "queued system commits lost their task group"); }
