@@ -5415,9 +5415,10 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         HIP_TRY(s, hipMemcpy(h, L.prof, sizeof(h), hipMemcpyDeviceToHost));
         std::fprintf(stderr, "k_ploop: %u placements, %.3f ms total; us: plain resolve %.1f, refresh %.1f, preempt "
                              "resolve %.1f, winner %.1f (its evict_eval %.1f, commit %.1f); refreshed %llu dirty + %llu pcount "
-                             "readers; winner evict_eval again, cache-warm %.1f (%llu calls)\n",
+                             "readers; winner evict_eval again, cache-warm %.1f (%llu calls); the next row's after it, data cold "
+                             "%.1f (%llu calls)\n",
                      st[0], ms, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[6] / 100.0, h[7] / 100.0, h[4],
-                     h[5], h[8] / 100.0, h[9]);
+                     h[5], h[8] / 100.0, h[9], h[10] / 100.0, h[11]);
     }
     *handled = true;
     const uint32_t p = std::min(st[0], count);
