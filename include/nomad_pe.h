@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 7u
+#define PE_ABI_VERSION 8u
 #define PE_NONE 0xFFFFFFFFu
 #define PE_MAX_SCORES 8
 #define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried inline per RankedNode (the
@@ -518,26 +518,38 @@ int pe_put_eligibility(pe_stack* s, const pe_class_feas* in, uint32_t n);
 int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit);
 /* ---- zero-crossing served Selects --------------------------------------------
  * GenericScheduler.computePlacements (generic_sched.go:552-627) calls Select
- * once per placement and the shim commits each option (Plan.AppendAlloc): two
- * cgo crossings per placement. After the first plain Select of a task group
- * the engine already holds the records of the group's whole remaining count
- * loop; this view lets the caller answer the following plain
- * Select / Commit pairs from host memory and cross into C only when it
+ * once per placement, retries a nil one with Preempt=true when preemption is
+ * enabled (selectNextOption, :773-792), and the shim commits each option
+ * (Plan.AppendAlloc + AppendPreemptedAlloc, :627, :794-816): two or three cgo
+ * crossings per placement. After the first plain Select of a task group the
+ * engine already holds the records of the group's count loop (DESIGN.md §12,
+ * §25): with preemption enabled, a placement that evicts is two records, the
+ * plain Select's nil and the Preempt retry's option (flag PE_SPEC_PREEMPT,
+ * its PreemptedAllocs in pre_allocs). This view lets the caller answer those
+ * Selects and Commits from host memory and cross into C only when it
  * deviates. One view per handle, used from the handle's thread.
  *
- *   Select(tg) with no options, when v->n_rec > 0, tg == v->tg_index,
- *     v->served == v->confirmed and v->served < v->n_rec:
- *       the result is v->recs[v->served] (row < 0: nil, the count loop is
- *       over; no Commit follows), then v->served++;
- *   Commit(tg, row), when v->served == v->confirmed + 1, tg == v->tg_index
- *     and row == v->recs[v->served - 1].row: v->confirmed++;
+ *   Select(tg, opts) with no preferred / penalty nodes, when v->n_rec > 0,
+ *     tg == v->tg_index, v->served == v->confirmed, v->served < v->n_rec and
+ *     (v->recs[v->served].flags & PE_SPEC_PREEMPT) is set exactly when
+ *     opts.Preempt is:
+ *       the result is v->recs[v->served], with PreemptedAllocs
+ *       v->pre_allocs[v->pre_off[k] .. v->pre_off[k + 1]) for k = v->served
+ *       (none when v->pre_off is NULL); then v->served++, and for a nil
+ *       result (row < 0, which no Commit follows) also v->confirmed++;
+ *   Commit(tg, row) / CommitPreempt(tg, row, list), when v->served ==
+ *     v->confirmed + 1, tg == v->tg_index, row == v->recs[v->served - 1].row
+ *     and the list is that record's PreemptedAllocs in its order (empty for
+ *     Commit): v->confirmed++;
  *   anything else goes through the entry points below, which first take the
  *     counters over, so the engine state is exactly what the sequential calls
  *     would have produced; they may replace or withdraw the records (v->epoch
  *     changes; v->n_rec 0: nothing to serve).
- * A served record is the leading part of pe_ranked_node (row .. new_offset)
- * plus the device offers; served Selects never preempt or reserve cores.
+ * A record the engine returned through pe_select may be confirmed through the
+ * view as well. A served record is the leading part of pe_ranked_node (row ..
+ * new_offset) plus the device offers; served Selects never reserve cores.
  * Replaces: the Select / Commit crossings of computePlacements' loop. */
+#define PE_SPEC_PREEMPT 1u   /* pe_spec_rec.flags: answers the Select with Preempt=true */
 typedef struct pe_spec_rec {
     int32_t row;
     uint32_t n_scores;
@@ -546,7 +558,7 @@ typedef struct pe_spec_rec {
     uint32_t nodes_evaluated, nodes_filtered, nodes_exhausted, new_offset;
     uint32_t n_device_offers;
     uint16_t device_offer_group[PE_MAX_DEVICE_REQ];
-    uint32_t pad;
+    uint32_t flags;               /* PE_SPEC_* */
 } pe_spec_rec;
 typedef struct pe_spec_view {
     uint32_t epoch;               /* engine: changes whenever recs / n_rec / tg_index change */
@@ -555,7 +567,9 @@ typedef struct pe_spec_view {
     uint32_t pad0;
     const pe_spec_rec* recs;      /* the run's records in Select order */
     uint32_t served;              /* caller and engine: Selects answered from recs */
-    uint32_t confirmed;           /* caller and engine: Commits that named the answered row */
+    uint32_t confirmed;           /* caller and engine: records settled (Commits, nils) */
+    const uint32_t* pre_off;      /* [n_rec + 1] or NULL: record k's PreemptedAllocs ... */
+    const uint32_t* pre_allocs;   /* ... are pre_allocs[pre_off[k] .. pre_off[k + 1]) (alloc-table rows) */
 } pe_spec_view;
 pe_spec_view* pe_spec_view_get(pe_stack* s);
 /* SystemScheduler.computePlacements (scheduler_system.go:283-425) runs, for

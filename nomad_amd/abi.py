@@ -236,12 +236,16 @@ class pe_spec_rec(C.Structure):   # nomad_pe.h: a served-Select record
                 ("scores", C.c_double * PE_MAX_SCORES), ("nodes_evaluated", C.c_uint32),
                 ("nodes_filtered", C.c_uint32), ("nodes_exhausted", C.c_uint32), ("new_offset", C.c_uint32),
                 ("n_device_offers", C.c_uint32), ("device_offer_group", C.c_uint16 * PE_MAX_DEVICE_REQ),
-                ("pad", C.c_uint32)]
+                ("flags", C.c_uint32)]
+
+
+PE_SPEC_PREEMPT = 1   # pe_spec_rec.flags: answers the Select with Preempt=true
 
 
 class pe_spec_view(C.Structure):
     _fields_ = [("epoch", C.c_uint32), ("tg_index", C.c_uint32), ("n_rec", C.c_uint32), ("pad0", C.c_uint32),
-                ("recs", C.POINTER(pe_spec_rec)), ("served", C.c_uint32), ("confirmed", C.c_uint32)]
+                ("recs", C.POINTER(pe_spec_rec)), ("served", C.c_uint32), ("confirmed", C.c_uint32),
+                ("pre_off", C.POINTER(C.c_uint32)), ("pre_allocs", C.POINTER(C.c_uint32))]
 
 
 PE_SYS_NIL = 1 << 31

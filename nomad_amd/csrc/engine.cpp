@@ -15,6 +15,7 @@
 // scoring and selection all run on the device.
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -665,8 +666,23 @@ struct pe_stack {
         bool compact = false;
         uint32_t n_rec = 0, placed = 0, served = 0, confirmed = 0;
         uint32_t grow = 1;             // run length on costly paths, doubles while runs get used up
-        bool checkpoint = false;       // dynamic columns saved at the start (device asks)
+        bool checkpoint = false;       // dynamic columns saved at the start (device asks, evictions)
+        // A run with the Preempt retry (preemption enabled, §25): records are
+        // Select answers, a placement that evicts is two of them (the plain
+        // nil, then the Preempt option), so served / confirmed count records
+        // and these map records to placements.
+        bool evict = false;
+        std::vector<uint32_t> rec_place;   // record -> placement index, PE_NONE for a nil record
+        std::vector<uint32_t> place_rec;   // placement -> its record
+        std::vector<uint32_t> rflags;      // record -> PE_SPEC_* flags
+        std::vector<uint32_t> pre_off, pre_list;   // record -> PreemptedAllocs (CSR, alloc-table rows)
     } spec;
+    // place_impl with the Preempt retry: per placement, the plain nil Select
+    // the retry followed (nodes evaluated / filtered / exhausted, cursor;
+    // evaluated PE_NONE when the placement took no retry)
+    std::vector<std::array<uint32_t, 4>>* nil_sink = nullptr;
+    DevMem d_ploop_nil;
+    DevMem ck_preempted, ck_pcount;
     std::vector<pe::EmitRec>* emit_sink = nullptr;   // run_place: keep chain records compact here
     bool emit_sunk = false;                          // ... and it did
     pe_spec_view sview{};              // the run's records for caller-served Selects (pe_spec_view_get)
@@ -2275,10 +2291,10 @@ static int flush_counts(pe_stack* s) {
 
 static int flush_fold(pe_stack* s) {
     if (!s->fold_pending) return PE_OK;
-    s->fold_pending = false;
     const pe::FoldArgs F = s->pending_fold;
     const pe::NodeSoA soa = soa_of(s);
     HIP_TRY(s, pe_launch_fold_feas_staged(&soa, F.class_src, F.class_dst, F.ncls, F.node_ok, F.feas, s->stream));
+    s->fold_pending = false;   // only a launched fold clears the flag (as flush_reset)
     return PE_OK;
 }
 
@@ -2312,14 +2328,50 @@ static const pe::EmitRec& spec_rec(const pe_stack::Spec& sp, uint32_t k) {
 
 static void sys_view_take(pe_stack* s);
 
+// Record k's row, and its PreemptedAllocs (evicting runs; none otherwise).
+static inline int32_t spec_rec_row(const pe_stack::Spec& sp, uint32_t k) {
+    return sp.compact ? sp.crecs[k].row : sp.recs[k].row;
+}
+static inline uint32_t spec_rec_npre(const pe_stack::Spec& sp, uint32_t k) {
+    return sp.evict ? sp.pre_off[k + 1] - sp.pre_off[k] : 0u;
+}
+static inline const uint32_t* spec_rec_pre(const pe_stack::Spec& sp, uint32_t k) {
+    return sp.evict ? sp.pre_list.data() + sp.pre_off[k] : nullptr;
+}
+
+// A served nil needs no Commit: it is settled as soon as it is served.
+static void spec_settle(pe_stack::Spec& sp) {
+    if (sp.served == sp.confirmed + 1 && spec_rec_row(sp, sp.served - 1) < 0) sp.confirmed = sp.served;
+    sp.pending = sp.served > sp.confirmed;
+}
+
+// Record k's Commit named its row: Plan.AppendAlloc (+ AppendPreemptedAlloc)
+// in the host mirror, as commit_one's predicted branch; `kids` logs it for the
+// replicas as pe_commit / pe_commit_preempt would.
+static void spec_confirm_rec(pe_stack* s, uint32_t k, bool kids) {
+    pe_stack::Spec& sp = s->spec;
+    const int32_t row = spec_rec_row(sp, k);
+    if (row < 0) return;
+    s->gen++;
+    s->plan.emplace_back(s->tgs[sp.tgi]->name, (uint32_t)row);
+    invalidate_job_distinct(s, sp.tgi);
+    if (kids && !s->kids.empty()) {
+        const uint32_t np = spec_rec_npre(sp, k);
+        kid_log(s, np ? 1 : 0, sp.tgi, row, np ? spec_rec_pre(sp, k) : nullptr, np);
+    }
+}
+
 static void view_take(pe_stack* s) {
     sys_view_take(s);
     pe_spec_view& v = s->sview;
     pe_stack::Spec& sp = s->spec;
     if (!v.n_rec || !sp.active) return;
     if (v.served == sp.served && v.confirmed == sp.confirmed) return;
-    const uint32_t served = std::min(v.served, sp.n_rec), confirmed = std::min(v.confirmed, served);
-    const auto name = s->tgs[sp.tgi]->name;
+    const uint32_t served = std::min(std::max(v.served, sp.served), sp.n_rec);
+    const uint32_t confirmed = std::min(std::max(v.confirmed, sp.confirmed), served);
+    // a record pe_select served (spec_start / spec_serve) whose Commit the
+    // caller confirmed through the view
+    if (sp.pending && confirmed >= sp.served) spec_confirm_rec(s, sp.served - 1, true);
     for (uint32_t k = sp.served; k < served; k++) {   // spec_serve of record k, then its commit
         const pe::EmitRec& r = spec_rec(sp, k);
         s->gen++;
@@ -2327,16 +2379,11 @@ static void view_take(pe_stack* s) {
         s->offset = r.new_offset;
         s->metrics_valid = false;
         s->spec_stats[1]++;
-        if (k < confirmed && r.row >= 0) {
-            s->gen++;
-            s->plan.emplace_back(name, (uint32_t)r.row);
-            invalidate_job_distinct(s, sp.tgi);
-            if (!s->kids.empty()) kid_log(s, 0, sp.tgi, r.row, nullptr, 0);   // as pe_commit logs it
-        }
+        if (k < confirmed) spec_confirm_rec(s, k, true);
     }
     sp.served = served;
-    sp.confirmed = std::max(sp.confirmed, confirmed);
-    sp.pending = sp.served > sp.confirmed && spec_rec(sp, sp.served - 1).row >= 0;
+    sp.confirmed = confirmed;
+    spec_settle(sp);
     s->offer_row = -1;
     v.served = sp.served;
     v.confirmed = sp.confirmed;
@@ -2345,7 +2392,7 @@ static void view_take(pe_stack* s) {
 static void view_publish(pe_stack* s) {
     pe_stack::Spec& sp = s->spec;
     pe_spec_view& v = s->sview;
-    if (!sp.compact) {   // served Selects carry no preemptions / reserved cores: the leading fields
+    if (!sp.compact) {   // served Selects carry no reserved cores: the leading fields
         sp.vrecs.resize(sp.n_rec);
         for (uint32_t k = 0; k < sp.n_rec; k++) {
             const pe_ranked_node& r = sp.recs[k];
@@ -2354,11 +2401,14 @@ static void view_publish(pe_stack* s) {
             std::memcpy(&e, &r, offsetof(pe::EmitRec, n_device_offers));
             e.n_device_offers = r.n_device_offers;
             for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) e.device_offer_group[q] = (uint16_t)r.device_offer_group[q];
+            e.flags = sp.evict ? sp.rflags[k] : 0u;
         }
     }
     v.epoch++;
     v.tg_index = sp.tgi;
     v.recs = sp.compact ? sp.crecs.data() : sp.vrecs.data();
+    v.pre_off = sp.evict ? sp.pre_off.data() : nullptr;
+    v.pre_allocs = sp.evict ? sp.pre_list.data() : nullptr;
     v.served = sp.served;
     v.confirmed = sp.confirmed;
     v.n_rec = s->metrics_on ? 0u : sp.n_rec;
@@ -2370,6 +2420,7 @@ static void view_withdraw(pe_stack* s) {
     v.epoch++;
     v.n_rec = 0;
     v.recs = nullptr;
+    v.pre_off = v.pre_allocs = nullptr;
     v.served = v.confirmed = 0;
 }
 
@@ -3707,6 +3758,11 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
     // (k_base pulls the class table into LDS per workgroup while that stays
     // small on the bus, the fused k_chain for short lists), else its own launch
     bool fused = false;
+    // pending work this call's first launch carries: handed back when that
+    // launch fails, so the next entry point still launches it
+    bool fold_taken = false, counts_taken = false;
+    const pe::FoldArgs fold_saved = s->pending_fold;
+    const pe::CountArgs counts_saved = s->pending_counts;
     if (chain) {
         const uint32_t base_blocks = (2u * (uint32_t)n + 63u) / 64u;
         fused = A.base_by_pos && (uint32_t)n <= pe_chain_fused_max_n() && pe_chain_shape(n) <= 4 &&
@@ -3716,6 +3772,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         if (s->fold_pending && (fused || (size_t)s->pending_fold.ncls * base_blocks <= 256u * 1024u)) {
             A.fold = s->pending_fold;
             s->fold_pending = false;
+            fold_taken = true;
         }
     }
     {
@@ -3732,6 +3789,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             if (s->counts_pending) {   // SetJob's counts ride in this launch
                 A.counts = s->pending_counts;
                 s->counts_pending = false;
+                counts_taken = true;
             }
         }
         const size_t cap = std::min(count, chunk);
@@ -3789,7 +3847,13 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
                         if (!ev) HIP_TRY(s, hipEventCreate(&ev));
                     split = s->ev_split;
                 }
-                HIP_TRY_STATE(s, pe_launch_chain(&A, 1, 1, s->stream, split));
+                HIP_TRY_STATE(s, hipSuccess);   // whatever is still pending launches first
+                const hipError_t le = pe_launch_chain(&A, 1, 1, s->stream, split);
+                if (le != hipSuccess && done == 0) {
+                    if (fold_taken) { s->pending_fold = fold_saved; s->fold_pending = true; }
+                    if (counts_taken) { s->pending_counts = counts_saved; s->counts_pending = true; }
+                }
+                HIP_TRY(s, le);
                 s->split_valid = split != nullptr;
             } else {
                 s->split_valid = false;
@@ -3914,8 +3978,17 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
 
 extern "C" {
 
+// The row of placement i of the run (record i, or its record in an evicting run).
 static inline int32_t spec_row(const pe_stack::Spec& sp, uint32_t i) {
-    return sp.compact ? sp.crecs[i].row : sp.recs[i].row;
+    return spec_rec_row(sp, sp.evict ? sp.place_rec[i] : i);
+}
+
+// Placements among the run's settled records: what HBM must hold after a flush.
+static uint32_t spec_conf_placed(const pe_stack::Spec& sp) {
+    if (!sp.evict) return std::min(sp.confirmed, sp.placed);
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < sp.confirmed && k < sp.n_rec; k++) c += sp.rec_place[k] != PE_NONE;
+    return c;
 }
 
 static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out);
@@ -5387,6 +5460,11 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     L.out = s->d_loop_out.as<pe_ranked_node>();
     L.out_mask = s->d_ploop_mask.as<uint32_t>();
     L.state = s->d_loop_state.as<uint32_t>();
+    if (retry && s->nil_sink) {   // the plain nils the Preempt retries follow (speculative run records)
+        HIP_TRY(s, s->d_ploop_nil.ensure(sizeof(uint32_t) * 4 * (size_t)count));
+        HIP_TRY(s, hipMemsetAsync(s->d_ploop_nil.p, 0xFF, sizeof(uint32_t) * 4 * (size_t)count, s->stream));
+        L.nil_out = s->d_ploop_nil.as<uint32_t>();
+    }
     const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
     if (prof) {
         HIP_TRY(s, s->d_prof.ensure(16 * sizeof(unsigned long long)));
@@ -5400,11 +5478,17 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     const uint32_t recs = std::min(st[3], count);
     std::vector<uint32_t> masks((size_t)recs * words);
+    std::vector<std::array<uint32_t, 4>> nils(L.nil_out ? recs : 0u);
     if (recs) {
         HIP_TRY(s, hipMemcpyAsync(out, L.out, sizeof(pe_ranked_node) * recs, hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipMemcpyAsync(masks.data(), L.out_mask, sizeof(uint32_t) * words * recs, hipMemcpyDeviceToHost,
                                   s->stream));
+        if (L.nil_out)
+            HIP_TRY(s, hipMemcpyAsync(nils.data(), L.nil_out, sizeof(uint32_t) * 4 * recs, hipMemcpyDeviceToHost,
+                                      s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
+        for (uint32_t k = 0; k < (uint32_t)nils.size(); k++)
+            if (nils[k][0] != PE_NONE && rec0 + k < s->nil_sink->size()) (*s->nil_sink)[rec0 + k] = nils[k];
     }
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -5553,6 +5637,13 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
 // generic_sched.go:773-792) when the configuration enables preemption; without
 // it the loop stops at the first nil Select (the speculative loop behind
 // pe_select leaves the retry to the caller).
+// The plain nil Select that placement k's Preempt retry follows, for the
+// speculative run's records (nil_sink).
+static inline void note_nil(pe_stack* s, uint32_t k, const pe_ranked_node& r) {
+    if (s->nil_sink && k < s->nil_sink->size())
+        (*s->nil_sink)[k] = {r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted, r.new_offset};
+}
+
 static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed,
                       bool retry_preempt) {
     const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
@@ -5596,6 +5687,7 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
             if (rc) return rc;
             if (out[p].row < 0) {
                 if (!retry) break;
+                note_nil(s, p, out[p]);
                 pe_select_options o;   // selectNextOption: retry with Preempt=true
                 std::memset(&o, 0, sizeof(o));
                 o.preempt = 1;
@@ -5650,6 +5742,7 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
                 continue;
             }
             if (!retry) break;
+            note_nil(s, p, out[p]);
             pe_select_options o;   // selectNextOption: retry with Preempt=true
             std::memset(&o, 0, sizeof(o));
             o.preempt = 1;
@@ -5695,6 +5788,7 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
         // selectNextOption (generic_sched.go:773-792): a nil Select is retried
         // with Preempt=true; the placement then evicts (handlePreemptions)
         while (retry && p < count) {
+            note_nil(s, p, out[p]);   // out[p]: the plain Select's nil
             pe_select_options o;
             std::memset(&o, 0, sizeof(o));
             o.preempt = 1;
@@ -5769,11 +5863,18 @@ static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     view_take(s);
     pe_stack::Spec& sp = s->spec;
     if (!sp.active || sp.pending || tgi != sp.tgi || sp.served >= sp.n_rec || s->metrics_on) return false;
-    if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
+    if (opts && (opts->penalty_count || opts->preferred_count)) return false;
+    // a Preempt retry is answered by a Preempt record only, and vice versa
+    const bool want_pre = opts && opts->preempt;
+    if (want_pre != (sp.evict && (sp.rflags[sp.served] & PE_SPEC_PREEMPT) != 0)) return false;
     s->gen++;
-    if (sp.compact) widen_rec(sp.crecs[sp.served++], out);
-    else *out = sp.recs[sp.served++];
-    sp.pending = out->row >= 0;
+    const uint32_t k = sp.served++;
+    if (sp.compact) widen_rec(sp.crecs[k], out);
+    else *out = sp.recs[k];
+    if (spec_rec_npre(sp, k) > PE_MAX_PREEMPT)   // pe_preempted_of(s, 0, ...) of this Select
+        s->pre_overflow.emplace_back(0u, std::vector<uint32_t>(spec_rec_pre(sp, k),
+                                                                spec_rec_pre(sp, k) + spec_rec_npre(sp, k)));
+    spec_settle(sp);
     elig_log_span(s, tgi, s->offset, out->nodes_evaluated);
     s->offset = out->new_offset;   // the StaticIterator cursor after this Select
     s->metrics_valid = false;
@@ -5823,6 +5924,70 @@ static int spec_copy(pe_stack* s, TgPlan& g, bool to_ckpt) {
     HIP_TRY(s, cp(s->d_dev_free, s->ck_dev_free, n * sizeof(uint32_t)));
     for (size_t p = 0; p < g.psets.size() && p < (size_t)pe::kMaxPsets; p++)
         HIP_TRY(s, cp(g.psets[p]->counts, s->ck_pset[p], std::max<size_t>(g.psets[p]->value_str.size(), 1) * 4));
+    if (s->spec.evict) {   // Plan.NodePreemptions: the preempted flags and the per-(job, tg) counts
+        HIP_TRY(s, cp(s->d_preempted, s->ck_preempted, s->h_preempted.size()));
+        HIP_TRY(s, cp(s->d_pcount, s->ck_pcount, sizeof(uint32_t) * std::max<uint32_t>(s->n_jtg_keys, 1)));
+    }
+    return PE_OK;
+}
+
+// An evicting run (§25) is undone from its checkpoint: the columns, the
+// preempted flags and counts go back, the unconfirmed placements' preempted
+// allocs rejoin the host mirror, and the confirmed prefix is replayed
+// (its evictions, then its commits: both are sums, so their order is free).
+static int spec_rollback_evict(pe_stack* s, uint32_t conf) {
+    pe_stack::Spec& sp = s->spec;
+    TgPlan& g = *s->tgs[sp.tgi];
+    bool freed = false;
+    for (uint32_t i = conf; i < sp.placed; i++) {
+        const uint32_t k = sp.place_rec[i];
+        for (uint32_t j = 0; j < spec_rec_npre(sp, k); j++) {
+            const uint32_t slot = s->alloc_slot[spec_rec_pre(sp, k)[j]];
+            if (slot != PE_NONE) s->h_preempted[slot] = 0;
+            freed = true;
+        }
+    }
+    if (freed) invalidate_static(s);
+    int rc = spec_copy(s, g, false);
+    if (rc) return rc;
+    if (conf == 0) {
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        return PE_OK;
+    }
+    pe::Ask a = ask_for(s, g);
+    pe::NodeSoA soa = soa_of(s);
+    pe::TgTables t = tables_of(g);
+    const uint32_t words = s->evict_words;
+    std::vector<uint32_t> masks, mrows, rows(conf), offers(conf);
+    for (uint32_t i = 0; i < conf; i++) {
+        const uint32_t k = sp.place_rec[i];
+        const uint32_t row = (uint32_t)spec_rec_row(sp, k);
+        rows[i] = row;
+        offers[i] = pack_offers(&sp.recs[k]);
+        if (!spec_rec_npre(sp, k)) continue;
+        const uint32_t b = s->h_node_alloc_off[row];
+        const size_t at = masks.size();
+        masks.resize(at + words, 0u);
+        for (uint32_t j = 0; j < spec_rec_npre(sp, k); j++) {
+            const uint32_t q = s->alloc_slot[spec_rec_pre(sp, k)[j]] - b;
+            if (q >= 32u * words) return s->fail(PE_EINTERNAL, "replayed preemption past the eviction width");
+            masks[at + (q >> 5)] |= 1u << (q & 31u);
+        }
+        mrows.push_back(row);
+    }
+    if (!mrows.empty()) {
+        pe::PreemptArgs P = preempt_args(s, g);
+        HIP_TRY(s, upload_s(s, s->d_pre_mask, masks));
+        for (size_t j = 0; j < mrows.size(); j++)
+            HIP_TRY_STATE(s, pe_launch_commit_preempt(&P, mrows[j], s->d_pre_mask.as<uint32_t>() + j * words,
+                                                      s->d_preempted.as<uint8_t>(), s->d_pcount.as<uint32_t>(),
+                                                      s->d_dev_free.as<uint32_t>(), s->stream));
+    }
+    HIP_TRY(s, upload_s(s, s->d_commit_rows, rows));
+    HIP_TRY(s, upload_s(s, s->d_commit_offers, offers));
+    HIP_TRY_STATE(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
+                                             s->d_commit_offers.as<uint32_t>(), conf, 1, s->stream));
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
     return PE_OK;
 }
 
@@ -5837,22 +6002,25 @@ static int spec_flush(pe_stack* s) {
     view_withdraw(s);
     sp.active = false;
     sp.pending = false;
-    const bool used_up = sp.served == sp.n_rec && sp.confirmed == sp.placed && sp.placed == sp.n_rec;
+    const uint32_t conf = spec_conf_placed(sp);
+    const bool used_up = sp.served == sp.n_rec && conf == sp.placed && sp.n_rec > 0 &&
+                         spec_rec_row(sp, sp.n_rec - 1) >= 0;
     // run length of the next run on a costly path: doubles while runs get used
     // up, back to one placement after a deviation
     sp.grow = used_up ? std::min<uint32_t>(2 * sp.grow, 4096) : 1;
-    if (sp.confirmed == sp.placed) return PE_OK;   // HBM holds exactly the confirmed placements
+    if (conf == sp.placed) return PE_OK;   // HBM holds exactly the confirmed placements
     HIP_TRY(s, hipSetDevice(s->device));
-    TgPlan& g = *s->tgs[sp.tgi];
     s->spec_stats[2]++;
+    if (sp.evict) return spec_rollback_evict(s, conf);
+    TgPlan& g = *s->tgs[sp.tgi];
     pe::Ask a = ask_for(s, g);
     pe::NodeSoA soa = soa_of(s);
     pe::TgTables t = tables_of(g);
     if (!sp.checkpoint) {
         // no device ask: every commit added the same ask to its row, so the
         // unconfirmed placements are taken back by subtracting them again
-        std::vector<uint32_t> rows(sp.placed - sp.confirmed), offers(rows.size(), 0xFFFFFFFFu);
-        for (uint32_t i = sp.confirmed; i < sp.placed; i++) rows[i - sp.confirmed] = (uint32_t)spec_row(sp, i);
+        std::vector<uint32_t> rows(sp.placed - conf), offers(rows.size(), 0xFFFFFFFFu);
+        for (uint32_t i = conf; i < sp.placed; i++) rows[i - conf] = (uint32_t)spec_row(sp, i);
         HIP_TRY(s, upload_s(s, s->d_commit_rows, rows));
         HIP_TRY(s, upload_s(s, s->d_commit_offers, offers));
         HIP_TRY_STATE(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
@@ -5863,10 +6031,10 @@ static int spec_flush(pe_stack* s) {
     }
     int rc = spec_copy(s, g, false);
     if (rc) return rc;
-    if (sp.confirmed == 0) return PE_OK;
-    std::vector<uint32_t> rows(sp.confirmed), offers(sp.confirmed);
+    if (conf == 0) return PE_OK;
+    std::vector<uint32_t> rows(conf), offers(conf);
     bool ordered_only = false;   // a device ask without a recorded offer: replay one by one
-    for (uint32_t i = 0; i < sp.confirmed; i++) {
+    for (uint32_t i = 0; i < conf; i++) {
         rows[i] = (uint32_t)spec_row(sp, i);
         if (sp.compact) {
             pe_ranked_node r;
@@ -5878,13 +6046,13 @@ static int spec_flush(pe_stack* s) {
         if (a.n_dev > 0 && offers[i] == 0xFFFFFFFFu) ordered_only = true;
     }
     if (ordered_only) {
-        for (uint32_t i = 0; i < sp.confirmed; i++)
+        for (uint32_t i = 0; i < conf; i++)
             HIP_TRY_STATE(s, pe_launch_commit(&soa, &t, &a, rows[i], offers[i], s->stream));
     } else {
         HIP_TRY(s, upload_s(s, s->d_commit_rows, rows));
         HIP_TRY(s, upload_s(s, s->d_commit_offers, offers));
         HIP_TRY_STATE(s, pe_launch_apply_commits(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(),
-                                           s->d_commit_offers.as<uint32_t>(), sp.confirmed, 1, s->stream));
+                                           s->d_commit_offers.as<uint32_t>(), conf, 1, s->stream));
     }
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     return PE_OK;
@@ -5934,7 +6102,11 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     // get used up (spec_flush).
     count = spec_chain_path(s, g) ? std::max<uint32_t>(count, 1u) : std::max<uint32_t>(std::min(count, sp.grow), 1u);
     count = std::min<uint32_t>(count, 1u << 16);
-    sp.checkpoint = ask_for(s, g).n_dev > 0;   // device offers are not undone by subtraction
+    // With preemption enabled the run is selectNextOption's loop (generic_sched.go:
+    // 773-792): a nil plain Select retried with Preempt=true, whose placement
+    // evicts (§25). Evictions are not undone by subtraction: checkpoint.
+    sp.evict = s->cfg.preempt != 0;
+    sp.checkpoint = sp.evict || ask_for(s, g).n_dev > 0;   // device offers are not undone by subtraction
     if (sp.checkpoint) {
         rc = spec_copy(s, g, true);
         if (rc) return rc;
@@ -5942,28 +6114,87 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     const size_t plan0 = s->plan.size();
     if (sp.recs.size() < count) sp.recs.resize(count);
     uint32_t placed = 0;
-    s->emit_sink = &sp.crecs;
+    s->emit_sink = sp.evict ? nullptr : &sp.crecs;
     s->emit_sunk = false;
     const uint32_t off0 = s->offset;
+    std::vector<std::array<uint32_t, 4>> nils;
+    if (sp.evict) {
+        nils.assign(count + 1, std::array<uint32_t, 4>{PE_NONE, 0u, 0u, 0u});
+        s->nil_sink = &nils;
+        s->pre_overflow.clear();
+    }
     s->elig_mute = true;   // records are logged when served
-    rc = place_impl(s, tgi, count, sp.recs.data(), &placed, false);
+    rc = place_impl(s, tgi, count, sp.recs.data(), &placed, sp.evict);
     s->elig_mute = false;
     s->emit_sink = nullptr;
-    sp.compact = s->emit_sunk;
+    s->nil_sink = nullptr;
+    sp.compact = !sp.evict && s->emit_sunk;
     s->plan.resize(plan0);   // the plan holds confirmed placements only
-    if (rc) {
+    // A failed run leaves the device as the caller last saw it (and the host
+    // mirror of the preempted allocs: the run's placements are dropped).
+    auto undo_run = [&](int err) {
         if (sp.checkpoint) {
-            const int rc2 = spec_copy(s, g, false);   // leave the device as the caller last saw it
+            if (sp.evict)
+                for (uint32_t k = 0; k < placed && k < count; k++) {
+                    const uint32_t* l = preempted_list(s, k, sp.recs[k]);
+                    for (uint32_t j = 0; l && j < sp.recs[k].n_preempted; j++) {
+                        const uint32_t slot = s->alloc_slot[l[j]];
+                        if (slot != PE_NONE) s->h_preempted[slot] = 0;
+                    }
+                }
+            const int rc2 = spec_copy(s, g, false);
             (void)rc2;
+            if (sp.evict) invalidate_static(s);
         }
         (void)hipStreamSynchronize(s->stream);
-        return rc;
-    }
+        sp.evict = false;
+        return err;
+    };
+    if (rc) return undo_run(rc);
     sp.active = true;
     sp.pending = false;
     sp.tgi = tgi;
     sp.placed = placed;
     sp.n_rec = placed < count ? placed + 1 : placed;
+    if (sp.evict) {
+        // the Select answers in order: an evicting placement is the plain
+        // Select's nil, then the Preempt retry's option
+        std::vector<pe_ranked_node> seq;
+        seq.reserve(2 * (size_t)sp.n_rec);
+        sp.rec_place.clear();
+        sp.place_rec.clear();
+        sp.rflags.clear();
+        sp.pre_off.assign(1, 0u);
+        sp.pre_list.clear();
+        for (uint32_t k = 0; k < sp.n_rec; k++) {
+            const pe_ranked_node& r = sp.recs[k];
+            if (nils[k][0] != PE_NONE) {
+                pe_ranked_node z;
+                std::memset(&z, 0, sizeof(z));
+                z.row = -1;
+                z.nodes_evaluated = nils[k][0];
+                z.nodes_filtered = nils[k][1];
+                z.nodes_exhausted = nils[k][2];
+                z.new_offset = nils[k][3];
+                seq.push_back(z);
+                sp.rec_place.push_back(PE_NONE);
+                sp.rflags.push_back(0u);
+                sp.pre_off.push_back((uint32_t)sp.pre_list.size());
+            }
+            const uint32_t np = r.row >= 0 ? r.n_preempted : 0u;
+            const uint32_t* l = np ? preempted_list(s, k, r) : nullptr;
+            if (np && !l) return undo_run(s->fail(PE_EINTERNAL, "speculative loop: a record's PreemptedAllocs are missing"));
+            if (k < placed) sp.place_rec.push_back((uint32_t)seq.size());
+            seq.push_back(r);
+            sp.rec_place.push_back(k < placed ? k : PE_NONE);
+            sp.rflags.push_back(nils[k][0] != PE_NONE ? PE_SPEC_PREEMPT : 0u);
+            sp.pre_list.insert(sp.pre_list.end(), l, l + np);
+            sp.pre_off.push_back((uint32_t)sp.pre_list.size());
+        }
+        sp.recs.swap(seq);
+        sp.n_rec = (uint32_t)sp.recs.size();
+        s->pre_overflow.clear();
+    }
     sp.served = 0;
     sp.confirmed = 0;
     s->spec_stats[0]++;
@@ -6018,14 +6249,13 @@ static int commit_one(pe_stack* s, uint32_t tgi, int32_t row) {
     if (s->sys.active && row >= 0) sys_touch(s, (uint32_t)row);
     view_take(s);
     pe_stack::Spec& sp = s->spec;
-    if (sp.active && sp.pending && tgi == sp.tgi && row == spec_row(sp, sp.served - 1)) {
+    if (sp.active && sp.pending && tgi == sp.tgi && row == spec_rec_row(sp, sp.served - 1) &&
+        spec_rec_npre(sp, sp.served - 1) == 0) {
         // the predicted Plan.AppendAlloc: already in HBM
         sp.pending = false;
         sp.confirmed = sp.served;
         s->sview.confirmed = sp.confirmed;
-        s->gen++;
-        s->plan.emplace_back(s->tgs[tgi]->name, (uint32_t)row);
-        invalidate_job_distinct(s, tgi);
+        spec_confirm_rec(s, sp.served - 1, false);   // pe_commit logs it for the replicas
         s->offer_row = -1;
         return PE_OK;
     }
@@ -6040,6 +6270,19 @@ static int commit_one(pe_stack* s, uint32_t tgi, int32_t row) {
 static int commit_preempt_one(pe_stack* s, uint32_t tgi, int32_t row, const uint32_t* preempted, uint32_t n_preempted) {
     if (!s) return PE_EINVAL;
     if (n_preempted == 0) return commit_one(s, tgi, row);
+    view_take(s);
+    pe_stack::Spec& sp = s->spec;
+    if (preempted && sp.active && sp.pending && tgi == sp.tgi && row == spec_rec_row(sp, sp.served - 1) &&
+        n_preempted == spec_rec_npre(sp, sp.served - 1) &&
+        std::equal(preempted, preempted + n_preempted, spec_rec_pre(sp, sp.served - 1))) {
+        // the predicted Plan.AppendAlloc + AppendPreemptedAlloc: already in HBM
+        sp.pending = false;
+        sp.confirmed = sp.served;
+        s->sview.confirmed = sp.confirmed;
+        spec_confirm_rec(s, sp.served - 1, false);   // pe_commit_preempt logs it for the replicas
+        s->offer_row = -1;
+        return PE_OK;
+    }
     int rc = spec_flush(s);
     if (rc) return rc;
     if (s->sys.active && row >= 0) sys_touch(s, (uint32_t)row);

@@ -384,6 +384,10 @@ struct PLoopArgs {
                                       // failing anyway and stop with error 3 if one finds a winner
     pe_ranked_node* out;              // [count] records (a nil record ends the loop)
     uint32_t* out_mask;               // [count] preempted allocs of each placement (bits over the node's allocs)
+    // [4 * count] or null: per placement whose plain Select came back nil
+    // (the Preempt retry then answered it), that nil Select's nodes
+    // evaluated / filtered / exhausted and cursor; untouched otherwise
+    uint32_t* nil_out;
     uint32_t* state;                  // [0] placements, [1] cursor, [2] error (1: node outside the device limits,
                                       // 2: winner not an option, 3: a skipped plain resolve had a winner), [3] records
     unsigned long long* prof;         // [6] or null (PE_PLACE_PROF): wall-clock ticks of the plain resolve, refresh,

@@ -1391,7 +1391,7 @@ __device__ __forceinline__ void build_emit_rec(const BatchArgs& A, const ChainEm
     o.final_score = 0.0;
     o.n_scores = 0;
     o.n_device_offers = 0;
-    o.pad = 0;
+    o.flags = 0;
     for (int q = 0; q < PE_MAX_SCORES; q++) o.scores[q] = 0.0;
     for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o.device_offer_group[q] = 0;
     if (m.row < 0) return;

@@ -10,8 +10,9 @@
 //
 // The same loop drives the engine (pe_*) and the CPU oracle (oracle_*): the
 // caller passes the entry points. With the engine's served-Select view
-// (pe_spec_view_get, nomad_pe.h) the loop answers plain Select / Commit pairs
-// from the view and calls C only when it deviates, as the Go shim does; a
+// (pe_spec_view_get, nomad_pe.h) the loop answers Select / Commit pairs (the
+// Preempt retry included) from the view and calls C only when it deviates,
+// as the Go shim does; a
 // record with more than PE_MAX_PREEMPT preempted allocs is read in full with
 // preempted_of before its Commit.
 #include <chrono>
@@ -66,6 +67,13 @@ static int commit_opt(const dropin_api* api, void* h, uint32_t tg, const pe_rank
     return api->commit_preempt(h, tg, opt.row, buf, opt.n_preempted);
 }
 
+// Whether the next Select (plain, or the Preempt retry with `flag` =
+// PE_SPEC_PREEMPT) is answered by the view (nomad_pe.h's rules).
+static bool view_can(const pe_spec_view* v, uint32_t tg, uint32_t flag) {
+    return v && v->n_rec && v->tg_index == tg && v->served == v->confirmed && v->served < v->n_rec &&
+           (v->recs[v->served].flags & PE_SPEC_PREEMPT) == flag;
+}
+
 // One evaluation's placements of task group `tg`; rows[count] (may be null)
 // receives the chosen rows, -1 after the loop stopped. Returns 0 or the first
 // failing call's status.
@@ -81,29 +89,47 @@ int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, in
     int rc = 0;
     using clk = std::chrono::steady_clock;
     auto t_first = clk::now();
+    auto first_done = [&](uint32_t i) {
+        if (i != 0) return;
+        const auto t = clk::now();
+        g_phase[3] += std::chrono::duration<double>(t - t_first).count();
+        t_first = t;
+    };
     pe_spec_view* v = (g_use_view && api->spec_view_get) ? api->spec_view_get(h) : nullptr;
     for (uint32_t i = 0; i < count; i++) {
-        if (v && v->n_rec && v->tg_index == tg && v->served == v->confirmed && v->served < v->n_rec &&
-            v->recs[v->served].row >= 0) {
-            // a plain Select answered from the view and its Commit confirmed there
-            const int32_t row = v->recs[v->served].row;
-            v->served++;
+        if (view_can(v, tg, 0)) {
+            // a plain Select answered from the view; an option's Commit is
+            // confirmed there, a nil is settled at once
+            const pe_spec_rec& r = v->recs[v->served++];
             v->confirmed++;
             sel++;
             g_view_served++;
-            if (rows) rows[p] = row;
-            p++;
-            continue;
+            first_done(i);
+            if (r.row >= 0) {
+                if (rows) rows[p] = r.row;
+                p++;
+                continue;
+            }
+            opt.row = -1;
+        } else {
+            rc = api->select(h, tg, &none, &opt);
+            sel++;
+            first_done(i);
+            if (rc) break;
         }
-        rc = api->select(h, tg, &none, &opt);
-        sel++;
-        if (i == 0) {
-            const auto t = clk::now();
-            g_phase[3] += std::chrono::duration<double>(t - t_first).count();
-            t_first = t;
-        }
-        if (rc) break;
         if (opt.row < 0 && preempt) {
+            if (view_can(v, tg, PE_SPEC_PREEMPT)) {
+                // the Preempt retry from the view; its CommitPreempt names the
+                // record's row and PreemptedAllocs, confirmed there
+                const pe_spec_rec& r = v->recs[v->served++];
+                v->confirmed++;
+                sel++;
+                g_view_served++;
+                if (r.row < 0) break;
+                if (rows) rows[p] = r.row;
+                p++;
+                continue;
+            }
             rc = api->select(h, tg, &pre, &opt);
             sel++;
             if (rc) break;
