@@ -366,6 +366,10 @@ uint32_t pe_device_count(const pe_stack* s);
  * an RCCL communicator (ncclGetUniqueId on one rank, the 128 bytes shared by
  * the caller, ncclCommInitRank on every rank). */
 int pe_comm_unique_id(uint8_t* out, size_t cap);
+/* The RCCL library the collectives call, bound at first use: the one the
+ * process already has mapped (soname librccl.so.1, e.g. torch's), else
+ * /opt/rocm/lib/librccl.so.1; "" when none loads. */
+const char* pe_comm_library(void);
 int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id);
 /* The full-pass count loop (task groups with affinities / spreads, limit >=
  * list) sharded over the ranks: every rank holds the whole snapshot, job and
@@ -546,7 +550,8 @@ int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit);
  *     would have produced; they may replace or withdraw the records (v->epoch
  *     changes; v->n_rec 0: nothing to serve).
  * A record the engine returned through pe_select may be confirmed through the
- * view as well. A served record is the leading part of pe_ranked_node (row ..
+ * view as well. With pe_set_metrics on, windowed runs without property sets or
+ * preemption still publish records, each with its AllocMetric maps. A served record is the leading part of pe_ranked_node (row ..
  * new_offset) plus the device offers; served Selects never reserve cores.
  * Replaces: the Select / Commit crossings of computePlacements' loop. */
 #define PE_SPEC_PREEMPT 1u   /* pe_spec_rec.flags: answers the Select with Preempt=true */
@@ -570,6 +575,11 @@ typedef struct pe_spec_view {
     uint32_t confirmed;           /* caller and engine: records settled (Commits, nils) */
     const uint32_t* pre_off;      /* [n_rec + 1] or NULL: record k's PreemptedAllocs ... */
     const uint32_t* pre_allocs;   /* ... are pre_allocs[pre_off[k] .. pre_off[k + 1]) (alloc-table rows) */
+    /* With pe_set_metrics on: record k's AllocMetric maps, the text pe_last_metrics
+     * would return after that Select, are metrics[metrics_off[k] .. metrics_off[k + 1])
+     * (not NUL-terminated); NULL when the records carry none. */
+    const char* metrics;
+    const uint32_t* metrics_off;
 } pe_spec_view;
 pe_spec_view* pe_spec_view_get(pe_stack* s);
 /* SystemScheduler.computePlacements (scheduler_system.go:283-425) runs, for

@@ -227,7 +227,7 @@ ENGINE_SYMBOLS = [
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
     "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
-    "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get", "pe_system_view_get",
+    "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get", "pe_system_view_get", "pe_comm_library",
 ]
 
 
@@ -245,7 +245,8 @@ PE_SPEC_PREEMPT = 1   # pe_spec_rec.flags: answers the Select with Preempt=true
 class pe_spec_view(C.Structure):
     _fields_ = [("epoch", C.c_uint32), ("tg_index", C.c_uint32), ("n_rec", C.c_uint32), ("pad0", C.c_uint32),
                 ("recs", C.POINTER(pe_spec_rec)), ("served", C.c_uint32), ("confirmed", C.c_uint32),
-                ("pre_off", C.POINTER(C.c_uint32)), ("pre_allocs", C.POINTER(C.c_uint32))]
+                ("pre_off", C.POINTER(C.c_uint32)), ("pre_allocs", C.POINTER(C.c_uint32)),
+                ("metrics", C.c_void_p), ("metrics_off", C.POINTER(C.c_uint32))]
 
 
 PE_SYS_NIL = 1 << 31

@@ -30,12 +30,84 @@
 #include <unordered_set>
 #include <vector>
 
+#include <dlfcn.h>
+#include <mutex>
 #include <rccl/rccl.h>
 
 #include "../../include/nomad_pe.h"
 #include "constraint_eval.h"
 #include "engine_types.h"
 #include "gomath_dev.h"
+
+// ---- RCCL, bound at run time ------------------------------------------------
+// The engine's collectives (pe_comm_init / pe_place_sharded, the one-handle
+// multi-GPU split) call the RCCL the process already has mapped when there is
+// one: a Python caller that imported torch has torch's librccl (soname
+// librccl.so.1) loaded, and a second copy from /opt/rocm would give the process
+// two RCCL instances with separate proxies and shared-memory state. Otherwise
+// /opt/rocm's library is loaded. pe_comm_library() names the one in use.
+namespace {
+struct RcclApi {
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommInitAll) CommInitAll = nullptr;
+    decltype(&ncclAllGather) AllGather = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+    std::string path;
+    bool ok = false;
+};
+
+const RcclApi& rccl() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);   // matches a loaded library by soname
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+#define PE_RCCL_SYM(x) api.x = reinterpret_cast<decltype(api.x)>(dlsym(h, "nccl" #x))
+        PE_RCCL_SYM(GetUniqueId);
+        PE_RCCL_SYM(CommInitRank);
+        PE_RCCL_SYM(CommInitAll);
+        PE_RCCL_SYM(AllGather);
+        PE_RCCL_SYM(CommDestroy);
+        PE_RCCL_SYM(GroupStart);
+        PE_RCCL_SYM(GroupEnd);
+        PE_RCCL_SYM(GetErrorString);
+#undef PE_RCCL_SYM
+        api.ok = api.GetUniqueId && api.CommInitRank && api.CommInitAll && api.AllGather && api.CommDestroy &&
+                 api.GroupStart && api.GroupEnd && api.GetErrorString;
+        Dl_info info;
+        if (api.GetUniqueId && dladdr(reinterpret_cast<void*>(api.GetUniqueId), &info) && info.dli_fname)
+            api.path = info.dli_fname;
+    });
+    return api;
+}
+
+ncclResult_t rc_GetUniqueId(ncclUniqueId* id) {
+    return rccl().ok ? rccl().GetUniqueId(id) : ncclSystemError;
+}
+ncclResult_t rc_CommInitRank(ncclComm_t* c, int n, ncclUniqueId id, int rank) {
+    return rccl().ok ? rccl().CommInitRank(c, n, id, rank) : ncclSystemError;
+}
+ncclResult_t rc_CommInitAll(ncclComm_t* c, int n, const int* devs) {
+    return rccl().ok ? rccl().CommInitAll(c, n, devs) : ncclSystemError;
+}
+ncclResult_t rc_AllGather(const void* src, void* dst, size_t count, ncclDataType_t t, ncclComm_t c,
+                          hipStream_t st) {
+    return rccl().ok ? rccl().AllGather(src, dst, count, t, c, st) : ncclSystemError;
+}
+ncclResult_t rc_CommDestroy(ncclComm_t c) { return rccl().ok ? rccl().CommDestroy(c) : ncclSystemError; }
+ncclResult_t rc_GroupStart() { return rccl().ok ? rccl().GroupStart() : ncclSystemError; }
+ncclResult_t rc_GroupEnd() { return rccl().ok ? rccl().GroupEnd() : ncclSystemError; }
+const char* rc_GetErrorString(ncclResult_t r) {
+    return rccl().ok ? rccl().GetErrorString(r) : "RCCL library unavailable (dlopen librccl.so.1 failed)";
+}
+}  // namespace
 
 size_t pe_place_lds_bytes(bool full, int hash_bits, bool packed, size_t pset_bytes);
 hipError_t pe_launch_place(const pe::BatchArgs* a, uint32_t n_evals, bool full, hipStream_t st);
@@ -112,7 +184,7 @@ hipError_t pe_launch_sweep_loop(const pe::SweepArgs* a, uint32_t blocks, uint32_
                                 uint32_t n, uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
                            uint32_t n, uint32_t* out, const uint32_t* penalty_bits, double log10,
-                           const double* spread_tab, double* scores, hipStream_t st);
+                           const double* spread_tab, double* scores, hipStream_t st, const uint16_t* dks = nullptr);
 
 namespace {
 
@@ -422,6 +494,13 @@ static inline bool has_static(const TgPlan& g) { return !g.rports.empty() || !g.
 
 }  // namespace
 
+// A reference-memo entry the AllocMetric walk set: (task-group memo?, class, value).
+struct MemoDelta {
+    bool tg;
+    uint32_t cls;
+    int8_t v;
+};
+
 struct pe_stack {
     pe_config cfg{};
     std::string err;
@@ -676,12 +755,22 @@ struct pe_stack {
         std::vector<uint32_t> place_rec;   // placement -> its record
         std::vector<uint32_t> rflags;      // record -> PE_SPEC_* flags
         std::vector<uint32_t> pre_off, pre_list;   // record -> PreemptedAllocs (CSR, alloc-table rows)
+        // AllocMetric maps of every record (pe_set_metrics on, §10/§25): the
+        // texts pe_last_metrics returns (CSR), the reference-memo changes each
+        // record's walk made (CSR) and the memo the run started from
+        bool metrics = false;
+        std::string mtext;
+        std::vector<uint32_t> mtext_off;
+        std::vector<MemoDelta> memo_log;
+        std::vector<uint32_t> memo_off;
+        std::vector<int8_t> memo_job0, memo_tg0;
     } spec;
     // place_impl with the Preempt retry: per placement, the plain nil Select
     // the retry followed (nodes evaluated / filtered / exhausted, cursor;
     // evaluated PE_NONE when the placement took no retry)
     std::vector<std::array<uint32_t, 4>>* nil_sink = nullptr;
     DevMem d_ploop_nil;
+    DevMem d_trace_dk;                 // spec_metrics: per traced row, the earlier records' placements
     DevMem ck_preempted, ck_pcount;
     std::vector<pe::EmitRec>* emit_sink = nullptr;   // run_place: keep chain records compact here
     bool emit_sunk = false;                          // ... and it did
@@ -2361,6 +2450,14 @@ static void spec_confirm_rec(pe_stack* s, uint32_t k, bool kids) {
     }
 }
 
+// pe_last_metrics after record k was served.
+static void spec_metrics_served(pe_stack* s, uint32_t k) {
+    const pe_stack::Spec& sp = s->spec;
+    if (!sp.metrics || k + 1 >= sp.mtext_off.size()) return;
+    s->metrics_text.assign(sp.mtext, sp.mtext_off[k], sp.mtext_off[k + 1] - sp.mtext_off[k]);
+    s->metrics_valid = true;
+}
+
 static void view_take(pe_stack* s) {
     sys_view_take(s);
     pe_spec_view& v = s->sview;
@@ -2381,6 +2478,7 @@ static void view_take(pe_stack* s) {
         s->spec_stats[1]++;
         if (k < confirmed) spec_confirm_rec(s, k, true);
     }
+    if (served > sp.served) spec_metrics_served(s, served - 1);
     sp.served = served;
     sp.confirmed = confirmed;
     spec_settle(sp);
@@ -2409,9 +2507,11 @@ static void view_publish(pe_stack* s) {
     v.recs = sp.compact ? sp.crecs.data() : sp.vrecs.data();
     v.pre_off = sp.evict ? sp.pre_off.data() : nullptr;
     v.pre_allocs = sp.evict ? sp.pre_list.data() : nullptr;
+    v.metrics = sp.metrics ? sp.mtext.data() : nullptr;
+    v.metrics_off = sp.metrics ? sp.mtext_off.data() : nullptr;
     v.served = sp.served;
     v.confirmed = sp.confirmed;
-    v.n_rec = s->metrics_on ? 0u : sp.n_rec;
+    v.n_rec = (s->metrics_on && !sp.metrics) ? 0u : sp.n_rec;
 }
 
 static void view_withdraw(pe_stack* s) {
@@ -2421,6 +2521,8 @@ static void view_withdraw(pe_stack* s) {
     v.n_rec = 0;
     v.recs = nullptr;
     v.pre_off = v.pre_allocs = nullptr;
+    v.metrics = nullptr;
+    v.metrics_off = nullptr;
     v.served = v.confirmed = 0;
 }
 
@@ -4002,6 +4104,8 @@ static void sys_touch(pe_stack* s, uint32_t row);
 
 uint32_t pe_abi_version(void) { return PE_ABI_VERSION; }
 
+const char* pe_comm_library(void) { return rccl().ok ? rccl().path.c_str() : ""; }
+
 pe_stack* pe_stack_create(const pe_config* cfg) {
     if (!cfg) { g_error = "null config"; return nullptr; }
     int ndev = 0;
@@ -4059,9 +4163,9 @@ pe_stack* pe_stack_create(const pe_config* cfg) {
         if (!same) {
             std::vector<int> devs(cfg->device_ids, cfg->device_ids + cfg->device_count);
             s->group_comms.assign(devs.size(), nullptr);
-            const ncclResult_t r = ncclCommInitAll(s->group_comms.data(), (int)devs.size(), devs.data());
+            const ncclResult_t r = rc_CommInitAll(s->group_comms.data(), (int)devs.size(), devs.data());
             if (r != ncclSuccess) {
-                g_error = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+                g_error = std::string("ncclCommInitAll: ") + rc_GetErrorString(r);
                 s->group_comms.clear();
                 pe_stack_destroy(s);
                 return nullptr;
@@ -4076,7 +4180,7 @@ void pe_stack_destroy(pe_stack* s) {
     if (!s) return;
     for (pe_stack* k : s->kids) pe_stack_destroy(k);
     for (ncclComm_t c : s->group_comms)
-        if (c) (void)ncclCommDestroy(c);
+        if (c) (void)rc_CommDestroy(c);
     if (s->api_prof)
         for (auto& kv : s->api_acc)
             std::fprintf(stderr, "api %-28s %10.1f us total %8llu calls %8.2f us/call\n", kv.first.c_str(),
@@ -4084,7 +4188,7 @@ void pe_stack_destroy(pe_stack* s) {
                          kv.second.first / std::max<uint64_t>(kv.second.second, 1));
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    if (s->comm) (void)ncclCommDestroy(s->comm);
+    if (s->comm) (void)rc_CommDestroy(s->comm);
     if (s->ev_x0) (void)hipEventDestroy(s->ev_x0);
     if (s->ev_x1) (void)hipEventDestroy(s->ev_x1);
     retire_tgs(s);
@@ -4741,27 +4845,42 @@ struct ScoreHeap {
     }
 };
 
-static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
-                           uint32_t evaluated, const pe_select_options* opts, bool evict = false) {
-    s->metrics_valid = false;
-    const size_t m = order.size();
+// The maps of one Select as they fill (FilterNode / ExhaustedNode, ScoreNode).
+struct MetricAcc {
     std::map<std::string, int> cf, kf, ce, de;
-    auto filter = [&](uint32_t row, const std::string& why) {
+    ScoreHeap heap;
+    void filter(pe_stack* s, uint32_t row, const std::string& why) {
         const uint32_t nc = s->nodes[row].node_class;
         if (nc != PE_NONE && !s->S(nc).empty()) cf[s->S(nc)]++;
         if (!why.empty()) kf[why]++;
-    };
-    auto exhaust = [&](uint32_t row, const std::string& dim) {
+    }
+    void exhaust(pe_stack* s, uint32_t row, const std::string& dim) {
         const uint32_t nc = s->nodes[row].node_class;
         if (nc != PE_NONE && !s->S(nc).empty()) ce[s->S(nc)]++;
         if (!dim.empty()) de[dim]++;
-    };
+    }
+};
+
+// FeasibilityWrapper half of one Select's maps: the window's rows in visit
+// order against the reference memo shadow (feasible.go:1061-1153); rows that
+// pass go to `rows` for k_trace. `log` (or null) receives the memo changes.
+static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
+                         uint32_t evaluated, MetricAcc& acc, std::vector<uint32_t>& rows,
+                         std::vector<MemoDelta>* log = nullptr) {
+    const size_t m = order.size();
     if (s->ref_job_memo.size() != s->ncls) s->ref_job_memo.assign(s->ncls, -1);
     auto& rt = s->ref_tg_memo[g.name];
     if (rt.size() != s->ncls) rt.assign(s->ncls, -1);
     pe::ConstraintEvaluator ev;
-    std::vector<uint32_t> rows;
     static const char* kIneligible = "computed class ineligible";
+    auto set_job = [&](uint32_t c, int8_t v) {
+        if (log) log->push_back({false, c, v});
+        s->ref_job_memo[c] = v;
+    };
+    auto set_tg = [&](uint32_t c, int8_t v) {
+        if (log) log->push_back({true, c, v});
+        rt[c] = v;
+    };
     for (uint32_t k = 0; k < evaluated && m; k++) {
         const uint32_t row = order[(start + k) % m];
         const NodeView v = s->view(row);
@@ -4773,8 +4892,8 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             why = kIneligible;
         } else {
             why = job_fail(s, ev, v);
-            if (why) s->ref_job_memo[c] = 0;
-            else if (s->ref_job_memo[c] == -1) s->ref_job_memo[c] = 1;
+            if (why) set_job(c, 0);
+            else if (s->ref_job_memo[c] == -1) set_job(c, 1);
         }
         if (!why) {
             if (g.escaped) {
@@ -4783,13 +4902,123 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                 why = kIneligible;
             } else if (rt[c] == -1) {
                 why = tg_fail(s, ev, g, v);
-                rt[c] = why ? 0 : 1;
+                set_tg(c, why ? 0 : 1);
             }
         }
-        if (why) filter(row, why);
+        if (why) acc.filter(s, row, why);
         else rows.push_back(row);
     }
-    ScoreHeap heap;
+}
+
+// One k_trace outcome of a plain Select (o: its 6 score values).
+static int metrics_outcome(pe_stack* s, TgPlan& g, const pe::Ask& a, uint32_t row, uint32_t code, const double* o,
+                           MetricAcc& acc, std::map<int, std::vector<uint32_t>>& counts) {
+    const bool has_aff = !g.affinities.empty();
+    const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
+    switch (code & 255u) {
+        case pe::kTrOption: {   // ScoreNode calls in chain order, then the NormScore push
+            ScoreMeta sm;
+            sm.row = row;
+            sm.scores.emplace_back("binpack", o[0]);
+            if (a.dev_tw != 0.0) sm.scores.emplace_back("devices", o[1]);
+            if (generic) {   // the SystemStack ranks with BinPack alone (stack.go:277-281)
+                if (a.anti_aff) sm.scores.emplace_back("job-anti-affinity", o[2]);
+                sm.scores.emplace_back("node-reschedule-penalty", (code & pe::kTrPenalty) ? -1.0 : 0.0);
+                if (!has_aff) sm.scores.emplace_back("node-affinity", 0.0);
+                else if (o[3] != 0.0) sm.scores.emplace_back("node-affinity", o[3]);
+                if (o[4] != 0.0) sm.scores.emplace_back("allocation-spread", o[4]);
+            }
+            sm.norm = o[5];
+            acc.heap.push(std::move(sm));
+            break;
+        }
+        case pe::kTrDistinctHosts: acc.filter(s, row, "distinct_hosts"); break;
+        case pe::kTrDistinctProp: {   // propertyset.go:213-244
+            const int p = (int)(code >> 8);
+            PsetDev& ps = *g.psets[p];
+            uint32_t vid;
+            Target tv = resolve(s, ps.target, s->view(row), &vid);
+            if (!tv.found || tv.nil) {
+                acc.filter(s, row, "missing property \"" + ps.target_text + "\"");
+                break;
+            }
+            if (vid == PE_NONE) vid = s->lookup(tv.value);
+            auto it = ps.value_index.find(vid);
+            uint64_t used = 0;
+            if (it != ps.value_index.end()) {
+                auto& cnt = counts[p];
+                if (cnt.empty()) {
+                    cnt.resize(std::max<size_t>(ps.value_str.size(), 1));
+                    HIP_TRY(s, hipMemcpyAsync(cnt.data(), ps.counts.p, cnt.size() * 4, hipMemcpyDeviceToHost,
+                                              s->stream));
+                    HIP_TRY(s, hipStreamSynchronize(s->stream));
+                }
+                used = cnt[it->second];
+            }
+            acc.filter(s, row, "distinct_property: " + ps.target_text + "=" + tv.value + " used by " +
+                                   std::to_string(used) + " allocs");
+            break;
+        }
+        case pe::kTrNoAddr: acc.exhaust(s, row, "network: no addresses available"); break;
+        case pe::kTrStaticPort: {
+            std::string why;
+            if (!static_port_reason(s, g, row, &why)) why = static_port_collision(s, g);
+            acc.exhaust(s, row, "network: " + why);
+            break;
+        }
+        case pe::kTrTaskStatic: {
+            std::string why;
+            if (!task_port_reason(s, g, row, &why)) why = static_port_collision(s, g);
+            acc.exhaust(s, row, "network: " + why);
+            break;
+        }
+        case pe::kTrDynPorts: acc.exhaust(s, row, "network: dynamic port selection failed"); break;
+        case pe::kTrNoNetworks: acc.exhaust(s, row, "network: no networks available"); break;
+        case pe::kTrBandwidth: acc.exhaust(s, row, "network: bandwidth exceeded"); break;
+        case pe::kTrTaskDyn: acc.exhaust(s, row, "network: dynamic port selection failed"); break;
+        case pe::kTrDevNone: acc.exhaust(s, row, "devices: no devices available"); break;
+        case pe::kTrDevZero: acc.exhaust(s, row, "devices: invalid request of zero devices"); break;
+        case pe::kTrDevNoMatch: acc.exhaust(s, row, "devices: no devices match request"); break;
+        case pe::kTrCpu: acc.exhaust(s, row, "cpu"); break;
+        case pe::kTrCores: acc.exhaust(s, row, "cores"); break;
+        case pe::kTrMemory: acc.exhaust(s, row, "memory"); break;
+        case pe::kTrDisk: acc.exhaust(s, row, "disk"); break;
+        case pe::kTrMismatch: return s->fail(PE_EHIP, "k_trace: device verdict differs from the host walk");
+        default: return s->fail(PE_EHIP, "k_trace: unknown outcome code");
+    }
+    return PE_OK;
+}
+
+// pe_last_metrics' text of one Select's maps.
+static std::string metrics_text(pe_stack* s, MetricAcc& acc) {
+    std::string out;
+    auto put = [&](const char* k, const std::map<std::string, int>& mm) {
+        for (auto& kv : mm) out += std::string(k) + "\t" + kv.first + "\t" + std::to_string(kv.second) + "\n";
+    };
+    put("CF", acc.cf); put("KF", acc.kf); put("CE", acc.ce); put("DE", acc.de);
+    // ScoreMetaData (PopulateScoreMetaData): "SM\trank\tnode id\tnorm\tname=value,..." (%.17g)
+    auto items = acc.heap.reverse_items();
+    char num[64];
+    for (size_t i = 0; i < items.size(); i++) {
+        auto& it = items[i];
+        std::sort(it.scores.begin(), it.scores.end());
+        snprintf(num, sizeof num, "%.17g", it.norm);
+        out += "SM\t" + std::to_string(i) + "\t" + s->S(s->nodes[it.row].id) + "\t" + num + "\t";
+        for (size_t k = 0; k < it.scores.size(); k++) {
+            snprintf(num, sizeof num, "%.17g", it.scores[k].second);
+            out += (k ? "," : "") + it.scores[k].first + "=" + num;
+        }
+        out += "\n";
+    }
+    return out;
+}
+
+static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
+                           uint32_t evaluated, const pe_select_options* opts, bool evict = false) {
+    s->metrics_valid = false;
+    MetricAcc acc;
+    std::vector<uint32_t> rows;
+    metrics_walk(s, g, order, start, evaluated, acc, rows);
     if (!rows.empty()) {
         HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
         HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
@@ -4882,111 +5111,111 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                         if (fl & 2u) sm.scores.emplace_back("preemption", o[5]);
                     }
                     sm.norm = o[6];
-                    heap.push(std::move(sm));
+                    acc.heap.push(std::move(sm));
                 } else if (st == 2) {   // kExhausted: no preemption frees enough (ExhaustedNode(dim))
                     const uint32_t d = (ec >> 8) & 255u;
-                    exhaust(row, d == pe::kTrCpu ? "cpu" : (d == pe::kTrMemory ? "memory" : "disk"));
+                    acc.exhaust(s, row, d == pe::kTrCpu ? "cpu" : (d == pe::kTrMemory ? "memory" : "disk"));
                 } else if (st != 3) {   // kSkipped (device preemption failed) records nothing
                     return s->fail(PE_EHIP, "k_evict_trace: outcome differs from the host walk");
                 }
                 continue;
             }
-            switch (code & 255u) {
-                case pe::kTrOption: {   // ScoreNode calls in chain order, then the NormScore push
-                    const double* o = &sc[i * 6];
-                    ScoreMeta sm;
-                    sm.row = row;
-                    sm.scores.emplace_back("binpack", o[0]);
-                    if (a.dev_tw != 0.0) sm.scores.emplace_back("devices", o[1]);
-                    if (generic) {   // the SystemStack ranks with BinPack alone (stack.go:277-281)
-                        if (a.anti_aff) sm.scores.emplace_back("job-anti-affinity", o[2]);
-                        sm.scores.emplace_back("node-reschedule-penalty", (code & pe::kTrPenalty) ? -1.0 : 0.0);
-                        if (!has_aff) sm.scores.emplace_back("node-affinity", 0.0);
-                        else if (o[3] != 0.0) sm.scores.emplace_back("node-affinity", o[3]);
-                        if (o[4] != 0.0) sm.scores.emplace_back("allocation-spread", o[4]);
-                    }
-                    sm.norm = o[5];
-                    heap.push(std::move(sm));
-                    break;
-                }
-                case pe::kTrDistinctHosts: filter(row, "distinct_hosts"); break;
-                case pe::kTrDistinctProp: {   // propertyset.go:213-244
-                    const int p = (int)(code >> 8);
-                    PsetDev& ps = *g.psets[p];
-                    uint32_t vid;
-                    Target tv = resolve(s, ps.target, s->view(row), &vid);
-                    if (!tv.found || tv.nil) {
-                        filter(row, "missing property \"" + ps.target_text + "\"");
-                        break;
-                    }
-                    if (vid == PE_NONE) vid = s->lookup(tv.value);
-                    auto it = ps.value_index.find(vid);
-                    uint64_t used = 0;
-                    if (it != ps.value_index.end()) {
-                        auto& cnt = counts[p];
-                        if (cnt.empty()) {
-                            cnt.resize(std::max<size_t>(ps.value_str.size(), 1));
-                            HIP_TRY(s, hipMemcpyAsync(cnt.data(), ps.counts.p, cnt.size() * 4, hipMemcpyDeviceToHost,
-                                                      s->stream));
-                            HIP_TRY(s, hipStreamSynchronize(s->stream));
-                        }
-                        used = cnt[it->second];
-                    }
-                    filter(row, "distinct_property: " + ps.target_text + "=" + tv.value + " used by " +
-                                    std::to_string(used) + " allocs");
-                    break;
-                }
-                case pe::kTrNoAddr: exhaust(row, "network: no addresses available"); break;
-                case pe::kTrStaticPort: {
-                    std::string why;
-                    if (!static_port_reason(s, g, row, &why)) why = static_port_collision(s, g);
-                    exhaust(row, "network: " + why);
-                    break;
-                }
-                case pe::kTrTaskStatic: {
-                    std::string why;
-                    if (!task_port_reason(s, g, row, &why)) why = static_port_collision(s, g);
-                    exhaust(row, "network: " + why);
-                    break;
-                }
-                case pe::kTrDynPorts: exhaust(row, "network: dynamic port selection failed"); break;
-                case pe::kTrNoNetworks: exhaust(row, "network: no networks available"); break;
-                case pe::kTrBandwidth: exhaust(row, "network: bandwidth exceeded"); break;
-                case pe::kTrTaskDyn: exhaust(row, "network: dynamic port selection failed"); break;
-                case pe::kTrDevNone: exhaust(row, "devices: no devices available"); break;
-                case pe::kTrDevZero: exhaust(row, "devices: invalid request of zero devices"); break;
-                case pe::kTrDevNoMatch: exhaust(row, "devices: no devices match request"); break;
-                case pe::kTrCpu: exhaust(row, "cpu"); break;
-                case pe::kTrCores: exhaust(row, "cores"); break;
-                case pe::kTrMemory: exhaust(row, "memory"); break;
-                case pe::kTrDisk: exhaust(row, "disk"); break;
-                case pe::kTrMismatch: return s->fail(PE_EHIP, "k_trace: device verdict differs from the host walk");
-                default: return s->fail(PE_EHIP, "k_trace: unknown outcome code");
-            }
+            const int rc = metrics_outcome(s, g, a, row, code, &sc[i * 6], acc, counts);
+            if (rc) return rc;
         }
     }
-    std::string out;
-    auto put = [&](const char* k, const std::map<std::string, int>& mm) {
-        for (auto& kv : mm) out += std::string(k) + "\t" + kv.first + "\t" + std::to_string(kv.second) + "\n";
-    };
-    put("CF", cf); put("KF", kf); put("CE", ce); put("DE", de);
-    // ScoreMetaData (PopulateScoreMetaData): "SM\trank\tnode id\tnorm\tname=value,..." (%.17g)
-    auto items = heap.reverse_items();
-    char num[64];
-    for (size_t i = 0; i < items.size(); i++) {
-        auto& it = items[i];
-        std::sort(it.scores.begin(), it.scores.end());
-        snprintf(num, sizeof num, "%.17g", it.norm);
-        out += "SM\t" + std::to_string(i) + "\t" + s->S(s->nodes[it.row].id) + "\t" + num + "\t";
-        for (size_t k = 0; k < it.scores.size(); k++) {
-            snprintf(num, sizeof num, "%.17g", it.scores[k].second);
-            out += (k ? "," : "") + it.scores[k].first + "=" + num;
-        }
-        out += "\n";
-    }
-    s->metrics_text = out;
+    s->metrics_text = metrics_text(s, acc);
     s->metrics_valid = true;
     return PE_OK;
+}
+
+// AllocMetric maps of every record of a speculative run (§25): record k's
+// Select saw the run's starting state plus the placements of records < k, so
+// its window is walked on the host in record order (the FeasibilityWrapper
+// half, with the reference memo), and every row that passes is traced in one
+// k_trace launch against the checkpoint of the starting state, with dk = the
+// earlier records' placements on the row. Windowed runs without property sets
+// and without evictions only (their state differs by placements alone).
+static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
+    pe_stack::Spec& sp = s->spec;
+    const auto& order = s->visit;
+    auto& rt = s->ref_tg_memo[g.name];
+    if (s->ref_job_memo.size() != s->ncls) s->ref_job_memo.assign(s->ncls, -1);
+    if (rt.size() != s->ncls) rt.assign(s->ncls, -1);
+    sp.memo_job0 = s->ref_job_memo;
+    sp.memo_tg0 = rt;
+    sp.memo_log.clear();
+    sp.memo_off.assign(1, 0u);
+    std::vector<MetricAcc> acc(sp.n_rec);
+    std::vector<uint32_t> rows, rec_end(sp.n_rec);
+    std::vector<uint16_t> dks;
+    std::unordered_map<uint32_t, uint16_t> placed_on;   // row -> placements of earlier records
+    uint32_t off = off0;
+    for (uint32_t k = 0; k < sp.n_rec; k++) {
+        const uint32_t ev = sp.compact ? sp.crecs[k].nodes_evaluated : sp.recs[k].nodes_evaluated;
+        const size_t r0 = rows.size();
+        metrics_walk(s, g, order, off, ev, acc[k], rows, &sp.memo_log);
+        sp.memo_off.push_back((uint32_t)sp.memo_log.size());
+        for (size_t i = r0; i < rows.size(); i++) {
+            auto it = placed_on.find(rows[i]);
+            dks.push_back(it == placed_on.end() ? 0 : it->second);
+        }
+        rec_end[k] = (uint32_t)rows.size();
+        const int32_t row = spec_rec_row(sp, k);
+        if (row >= 0) placed_on[(uint32_t)row]++;
+        off = sp.compact ? sp.crecs[k].new_offset : sp.recs[k].new_offset;
+    }
+    std::vector<uint32_t> codes(rows.size());
+    std::vector<double> sc(rows.size() * 6);
+    pe::Ask a = ask_for(s, g);
+    if (!rows.empty()) {
+        HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
+        HIP_TRY(s, upload_s(s, s->d_trace_dk, dks));
+        HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
+        HIP_TRY(s, s->d_trace_scores.ensure(rows.size() * 6 * sizeof(double)));
+        pe::NodeSoA soa = soa_of(s);   // the run's starting state: the checkpoint
+        pe::TgTables t = tables_of(g);
+        soa.rec = s->ck_rec.as<pe::NodeRec>();
+        soa.coll_job = s->ck_coll_job.as<uint32_t>();
+        t.coll_tg = s->ck_coll_tg.as<uint32_t>();
+        if (t.dev_free) t.dev_free = s->ck_dev_free.as<uint32_t>();
+        HIP_TRY_STATE(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
+                                         s->d_trace_out.as<uint32_t>(), nullptr, s->log10, nullptr,
+                                         s->d_trace_scores.as<double>(), s->stream, s->d_trace_dk.as<uint16_t>()));
+        HIP_TRY(s, hipMemcpyAsync(codes.data(), s->d_trace_out.p, codes.size() * 4, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(sc.data(), s->d_trace_scores.p, sc.size() * 8, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipStreamSynchronize(s->stream));
+    }
+    sp.mtext.clear();
+    sp.mtext_off.assign(1, 0u);
+    std::map<int, std::vector<uint32_t>> counts;
+    size_t i = 0;
+    for (uint32_t k = 0; k < sp.n_rec; k++) {
+        for (; i < rec_end[k]; i++) {
+            const int rc = metrics_outcome(s, g, a, rows[i], codes[i], &sc[i * 6], acc[k], counts);
+            if (rc) return rc;
+        }
+        sp.mtext += metrics_text(s, acc[k]);
+        sp.mtext_off.push_back((uint32_t)sp.mtext.size());
+    }
+    sp.metrics = true;
+    return PE_OK;
+}
+
+// The reference memo after the run's first `served` records: the run's
+// starting memo plus those records' walks.
+static void spec_memo_rewind(pe_stack* s, uint32_t served) {
+    pe_stack::Spec& sp = s->spec;
+    if (!sp.metrics || sp.tgi >= s->tgs.size()) return;
+    auto& rt = s->ref_tg_memo[s->tgs[sp.tgi]->name];
+    s->ref_job_memo = sp.memo_job0;
+    rt = sp.memo_tg0;
+    const uint32_t end = sp.memo_off[std::min<uint32_t>(served, (uint32_t)sp.memo_off.size() - 1)];
+    for (uint32_t j = 0; j < end; j++) {
+        const MemoDelta& d = sp.memo_log[j];
+        if (d.tg) rt[d.cls] = d.v;
+        else s->ref_job_memo[d.cls] = d.v;
+    }
 }
 
 // ---- SystemScheduler per-node Selects from a per-row cache ------------------
@@ -5862,7 +6091,8 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
 static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out) {
     view_take(s);
     pe_stack::Spec& sp = s->spec;
-    if (!sp.active || sp.pending || tgi != sp.tgi || sp.served >= sp.n_rec || s->metrics_on) return false;
+    if (!sp.active || sp.pending || tgi != sp.tgi || sp.served >= sp.n_rec || (s->metrics_on && !sp.metrics))
+        return false;
     if (opts && (opts->penalty_count || opts->preferred_count)) return false;
     // a Preempt retry is answered by a Preempt record only, and vice versa
     const bool want_pre = opts && opts->preempt;
@@ -5878,6 +6108,7 @@ static bool spec_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     elig_log_span(s, tgi, s->offset, out->nodes_evaluated);
     s->offset = out->new_offset;   // the StaticIterator cursor after this Select
     s->metrics_valid = false;
+    spec_metrics_served(s, k);
     s->spec_stats[1]++;
     s->sview.served = sp.served;
     s->sview.confirmed = sp.confirmed;
@@ -5893,12 +6124,19 @@ static bool spec_chain_path(pe_stack* s, TgPlan& g) {
 }
 
 static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* opts) {
-    if (!s->spec_on || s->cfg.stack_kind != PE_STACK_GENERIC || s->metrics_on) return false;
+    if (!s->spec_on || s->cfg.stack_kind != PE_STACK_GENERIC) return false;
     if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
     if (!s->have_state || !s->have_job || tgi >= s->tgs.size()) return false;
     if (s->tgs[tgi]->ask.cores > 0) return false;   // the rollback kernel does not return reserved cores
     for (size_t k = 0; k < s->tgs.size(); k++)   // commits would rebuild a sibling's collision counts
         if (k != tgi && s->tgs[k]->name == s->tgs[tgi]->name) return false;
+    if (s->metrics_on) {
+        // the records' maps are traced against the run's starting state plus
+        // earlier placements (spec_metrics): windowed runs, no property sets,
+        // no evictions
+        TgPlan& g = *s->tgs[tgi];
+        if (s->cfg.preempt || !g.psets.empty() || g.psets_dynamic || tg_full_scan(s, g)) return false;
+    }
     return true;
 }
 
@@ -6002,12 +6240,17 @@ static int spec_flush(pe_stack* s) {
     view_withdraw(s);
     sp.active = false;
     sp.pending = false;
+    if (sp.metrics) {   // the reference memo as the served records' walks left it
+        spec_memo_rewind(s, sp.served);
+        sp.metrics = false;
+    }
     const uint32_t conf = spec_conf_placed(sp);
     const bool used_up = sp.served == sp.n_rec && conf == sp.placed && sp.n_rec > 0 &&
                          spec_rec_row(sp, sp.n_rec - 1) >= 0;
-    // run length of the next run on a costly path: doubles while runs get used
-    // up, back to one placement after a deviation
-    sp.grow = used_up ? std::min<uint32_t>(2 * sp.grow, 4096) : 1;
+    // run length of the next run on a costly path: x4 while runs get used up
+    // (a run's fixed cost, ~0.1-0.4 ms, over fewer runs), back to one
+    // placement after a deviation
+    sp.grow = used_up ? std::min<uint32_t>(4 * sp.grow, 4096) : 1;
     if (conf == sp.placed) return PE_OK;   // HBM holds exactly the confirmed placements
     HIP_TRY(s, hipSetDevice(s->device));
     s->spec_stats[2]++;
@@ -6061,6 +6304,7 @@ static int spec_flush(pe_stack* s) {
 // Drop the speculation without touching the device (the state is being reset).
 static void spec_drop(pe_stack* s) {
     view_withdraw(s);
+    s->spec.metrics = false;
     s->spec.active = false;
     s->spec.pending = false;
     s->spec.grow = 1;
@@ -6106,7 +6350,10 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     // 773-792): a nil plain Select retried with Preempt=true, whose placement
     // evicts (§25). Evictions are not undone by subtraction: checkpoint.
     sp.evict = s->cfg.preempt != 0;
-    sp.checkpoint = sp.evict || ask_for(s, g).n_dev > 0;   // device offers are not undone by subtraction
+    sp.metrics = false;
+    // device offers are not undone by subtraction; the AllocMetric trace reads
+    // the starting state from the checkpoint
+    sp.checkpoint = sp.evict || ask_for(s, g).n_dev > 0 || s->metrics_on;
     if (sp.checkpoint) {
         rc = spec_copy(s, g, true);
         if (rc) return rc;
@@ -6194,6 +6441,17 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
         sp.recs.swap(seq);
         sp.n_rec = (uint32_t)sp.recs.size();
         s->pre_overflow.clear();
+    }
+    if (s->metrics_on) {
+        const int mrc = spec_metrics(s, g, off0);
+        if (mrc) {   // nothing served yet: the device and the memo go back to the run's start
+            sp.active = true;
+            sp.served = sp.confirmed = 0;
+            spec_memo_rewind(s, 0);
+            sp.metrics = false;
+            (void)spec_flush(s);
+            return mrc;
+        }
     }
     sp.served = 0;
     sp.confirmed = 0;
@@ -6366,7 +6624,7 @@ static int plan_pop_update_one(pe_stack* s, uint32_t alloc) {
 int pe_comm_unique_id(uint8_t* out, size_t cap) {
     if (!out || cap < NCCL_UNIQUE_ID_BYTES) return PE_EINVAL;
     ncclUniqueId id;
-    if (ncclGetUniqueId(&id) != ncclSuccess) return PE_EHIP;
+    if (rc_GetUniqueId(&id) != ncclSuccess) return PE_EHIP;
     std::memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
     return PE_OK;
 }
@@ -6376,15 +6634,15 @@ int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id) {
     if (!s || !id || nranks < 1 || rank < 0 || rank >= nranks) return PE_EINVAL;
     HIP_TRY(s, hipSetDevice(s->device));
     if (s->comm) {
-        (void)ncclCommDestroy(s->comm);
+        (void)rc_CommDestroy(s->comm);
         s->comm = nullptr;
     }
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
-    const ncclResult_t r = ncclCommInitRank(&s->comm, nranks, uid, rank);
+    const ncclResult_t r = rc_CommInitRank(&s->comm, nranks, uid, rank);
     if (r != ncclSuccess) {
         s->comm = nullptr;
-        return s->fail(PE_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        return s->fail(PE_EHIP, std::string("ncclCommInitRank: ") + rc_GetErrorString(r));
     }
     s->nranks = nranks;
     s->rank = rank;
@@ -6460,8 +6718,8 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
             HIP_TRY_STATE(s, pe_launch_sweep_only(&A, blocks, s->stream));
             if (s->nranks > 1) {   // in place: this rank's slice already sits at its offset
                 if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x0, s->stream));
-                const ncclResult_t r = ncclAllGather(A.recs, s->d_gather.p, slice, ncclUint8, s->comm, s->stream);
-                if (r != ncclSuccess) return s->fail(PE_EHIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+                const ncclResult_t r = rc_AllGather(A.recs, s->d_gather.p, slice, ncclUint8, s->comm, s->stream);
+                if (r != ncclSuccess) return s->fail(PE_EHIP, std::string("ncclAllGather: ") + rc_GetErrorString(r));
                 if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x1, s->stream));
             }
             HIP_TRY_STATE(s, pe_launch_step_only(&A2, nrecs, s->d_visit.as<uint32_t>(), n, s->offset,
@@ -7028,6 +7286,7 @@ extern "C" int pe_set_metrics(pe_stack* s, int on) {
 
 extern "C" int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap) {
     if (!s) return PE_EINVAL;
+    view_take(const_cast<pe_stack*>(s));   // Selects the caller served from the view: the last one's maps
     if (!s->metrics_valid) return PE_ESTATE;
     if (buf && cap) {
         const size_t k = std::min(cap - 1, s->metrics_text.size());
@@ -7305,12 +7564,12 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
                                                       static_cast<char*>(st[e]->d_gather.p) + slice * e, slice,
                                                       hipMemcpyDeviceToDevice, s->stream));
             } else {
-                ncclResult_t r = ncclGroupStart();
+                ncclResult_t r = rc_GroupStart();
                 for (uint32_t k = 0; k < N && r == ncclSuccess; k++)
-                    r = ncclAllGather(A[k].recs, st[k]->d_gather.p, slice, ncclUint8, s->group_comms[k], st[k]->stream);
-                const ncclResult_t r2 = ncclGroupEnd();
+                    r = rc_AllGather(A[k].recs, st[k]->d_gather.p, slice, ncclUint8, s->group_comms[k], st[k]->stream);
+                const ncclResult_t r2 = rc_GroupEnd();
                 if (r != ncclSuccess || r2 != ncclSuccess)
-                    return s->fail(PE_EHIP, std::string("ncclAllGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+                    return s->fail(PE_EHIP, std::string("ncclAllGather: ") + rc_GetErrorString(r != ncclSuccess ? r : r2));
             }
             if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x1, s->stream));
             for (uint32_t k = 0; k < N; k++) {

@@ -443,17 +443,22 @@ __device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, c
 // Options also get their named scores (ScoreNode calls, rank.go:516-522, 591-593,
 // 635-637, 704-722, spread.go:170, rank.go:769) as 6 doubles: binpack, devices,
 // job-anti-affinity, node-affinity, allocation-spread, normalized-score.
+// `dks` (or null): per entry, placements of this task group on the row that
+// the state lacks (a speculative run's earlier Selects, traced against the
+// run's starting state; no property sets then), applied as status_loaded does.
 __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint32_t n, uint32_t* out,
-                        const uint32_t* penalty_bits, double log10, const double* spread_tab, double* sc) {
+                        const uint32_t* penalty_bits, double log10, const double* spread_tab, double* sc,
+                        const uint16_t* dks) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t row = rows[i];
+    const uint32_t dk = dks ? (uint32_t)dks[i] : 0u;
     NodeIn in;
     load_node(s, t, row, in);
-    const NodeRec& r = in.r;
+    NodeRec& r = in.r;
     const uint32_t c = r.cls;
     uint32_t code = kTrOption;
-    if ((a.distinct_job && s.coll_job[row] > 0) || (a.distinct_tg && in.coll_tg > 0)) {
+    if ((a.distinct_job && s.coll_job[row] + dk > 0) || (a.distinct_tg && in.coll_tg + dk > 0)) {
         code = kTrDistinctHosts;                                   // feasible.go:569-595
     } else {
         for (int p = t.n_spread; p < t.n_psets && code == kTrOption; p++) {
@@ -462,8 +467,12 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
         }
     }
     if (code == kTrOption && t.static_gate &&                      // AssignPorts static ports (network.go:317-363)
-        (t.static_gate[row] == 0u || in.coll_tg + 1u != t.static_gate[row]))
+        (t.static_gate[row] == 0u || in.coll_tg + dk + 1u != t.static_gate[row]))
         code = kTrStaticPort;
+    if (dk) {   // the earlier placements' network use
+        r.used_dyn += (int32_t)dk * a.commit_dyn;
+        r.used_mbits += (int32_t)dk * a.commit_mbits;
+    }
     if (code == kTrOption && (a.tg_dyn > 0 || a.has_task_net)) {   // rank.go:231-295
         int32_t dyn = r.used_dyn;
         if (a.tg_dyn > 0) {
@@ -474,13 +483,13 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
         if (code == kTrOption && a.has_task_net) {
             if (r.avail_mbits < 0) code = kTrNoNetworks;
             else if (r.used_mbits + a.task_mbits > r.avail_mbits) code = kTrBandwidth;
-            else if (t.task_gate && (t.task_gate[row] == 0u || in.coll_tg + 1u != t.task_gate[row])) code = kTrTaskStatic;
+            else if (t.task_gate && (t.task_gate[row] == 0u || in.coll_tg + dk + 1u != t.task_gate[row])) code = kTrTaskStatic;
             else if (kDynPortCapacity - dyn < a.task_dyn) code = kTrTaskDyn;
         }
     }
     if (code == kTrOption && a.n_dev > 0) {                         // AssignDevice errors (device.go:32-131)
         const DevClass& dc = t.dev_cls[c];
-        uint32_t free = in.dev_free;
+        uint32_t free = dk ? dev_after(a, dc, in.dev_free, dk) : in.dev_free;
         if (dc.n_groups == 0) code = kTrDevNone;
         for (int q = 0; q < kMaxDevReq && code == kTrOption; q++) {
             if (q >= a.n_dev) break;
@@ -503,19 +512,24 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
     }
     bool core_out = false;
     if (code == kTrOption && a.cores > 0) {                         // reserved cores (rank.go:437-466)
-        const CoreFit f = core_fit(s.core_rsvable, s.core_used, s.core_avail, s.core_spc, (uint32_t)a.cores, row, 0);
+        const CoreFit f = core_fit(s.core_rsvable, s.core_used, s.core_avail, s.core_spc, (uint32_t)a.cores, row, dk);
         if (f.status == 1) code = kTrCores;
         core_out = f.status == 2;
     }
     if (code == kTrOption) {                                        // AllocsFit → Superset order
-        if (r.cap_cpu < r.used_cpu + ask_cpu(s, a, row)) code = kTrCpu;
+        const int64_t k1 = (int64_t)dk + 1;
+        if (r.cap_cpu < r.used_cpu + k1 * ask_cpu(s, a, row)) code = kTrCpu;
         else if (core_out) code = kTrCores;
-        else if (r.cap_mem < r.used_mem + a.mem) code = kTrMemory;
-        else if (r.cap_disk < r.used_disk + a.disk) code = kTrDisk;
+        else if (r.cap_mem < r.used_mem + k1 * a.mem) code = kTrMemory;
+        else if (r.cap_disk < r.used_disk + k1 * a.disk) code = kTrDisk;
     }
     if (code == kTrOption) {
         ScoreIn si;
-        if (status_loaded(s, t, t.class_ok, a, 0, row, in, &si) != kOption) {
+        if (dk) {   // status_loaded applies dk itself: the network columns as loaded
+            r.used_dyn -= (int32_t)dk * a.commit_dyn;
+            r.used_mbits -= (int32_t)dk * a.commit_mbits;
+        }
+        if (status_loaded(s, t, t.class_ok, a, dk, row, in, &si) != kOption) {
             out[i] = kTrMismatch;
             return;
         }
@@ -3770,10 +3784,10 @@ void pe_rec_init_host(pe::SweepRec* a) { pe::rec_init(*a); }
 
 hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
                            uint32_t n, uint32_t* out, const uint32_t* penalty_bits, double log10,
-                           const double* spread_tab, double* scores, hipStream_t st) {
+                           const double* spread_tab, double* scores, hipStream_t st, const uint16_t* dks) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(pe::k_trace, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, n, out,
-                       penalty_bits, log10, spread_tab, scores);
+                       penalty_bits, log10, spread_tab, scores, dks);
     return hipGetLastError();
 }
 

@@ -87,6 +87,28 @@ def load_engine():
     return _engine
 
 
+def parse_metrics(text: str) -> Dict:
+    """pe_last_metrics' text (also a served record's maps in pe_spec_view) as
+    {"ClassFiltered": {...}, "ConstraintFiltered": {...}, "ClassExhausted":
+    {...}, "DimensionExhausted": {...}, "ScoreMetaData": [(node id, NormScore,
+    {scorer: score}), ...]}."""
+    names = {"CF": "ClassFiltered", "KF": "ConstraintFiltered", "CE": "ClassExhausted",
+             "DE": "DimensionExhausted"}
+    out = {v: {} for v in names.values()}
+    out["ScoreMetaData"] = []
+    for line in text.split("\n"):
+        if not line:
+            continue
+        if line.startswith("SM\t"):   # PopulateScoreMetaData: top 5 by NormScore, descending
+            _, _, node_id, norm, parts = line.split("\t")
+            scores = dict((k, float(v)) for k, v in (p.split("=") for p in parts.split(",") if p))
+            out["ScoreMetaData"].append((node_id, float(norm), scores))
+            continue
+        kind, key, cnt = line.split("\t")
+        out[names[kind]][key] = int(cnt)
+    return out
+
+
 @dataclass
 class SelectOptions:
     """SelectOptions (stack.go:34-39); nodes are given as node IDs or rows."""
@@ -215,21 +237,7 @@ class _Stack:
             self._check(int(need))
         buf = C.create_string_buffer(int(need) + 1)
         fn(self._h, buf, len(buf))
-        names = {"CF": "ClassFiltered", "KF": "ConstraintFiltered", "CE": "ClassExhausted",
-                 "DE": "DimensionExhausted"}
-        out = {v: {} for v in names.values()}
-        out["ScoreMetaData"] = []
-        for line in buf.value.decode().split("\n"):
-            if not line:
-                continue
-            if line.startswith("SM\t"):   # PopulateScoreMetaData: top 5 by NormScore, descending
-                _, _, node_id, norm, parts = line.split("\t")
-                scores = dict((k, float(v)) for k, v in (p.split("=") for p in parts.split(",") if p))
-                out["ScoreMetaData"].append((node_id, float(norm), scores))
-                continue
-            kind, key, cnt = line.split("\t")
-            out[names[kind]][key] = int(cnt)
-        return out
+        return parse_metrics(buf.value.decode())
 
     # -- EvalEligibility and iterator state (context.go:190-356) -------------
     def Eligibility(self, changed_only: bool = False) -> Dict:

@@ -152,7 +152,8 @@ def test_c5_bench_shape_count_loop(c5_bench_shape):
 
 
 def test_c5_bench_shape_caller_protocol(c5_bench_shape):
-    # the same evaluation through Select / Commit with the Preempt retry
+    # the same evaluation through Select / Commit with the Preempt retry, every
+    # Select through C: plain nils and Preempt options both from the run records
     from nomad_amd.stack import GenericStack, SelectOptions
     nodes, allocs, job, perm, cfg, g = c5_bench_shape
     st = GenericStack(config=cfg)
@@ -160,14 +161,47 @@ def test_c5_bench_shape_caller_protocol(c5_bench_shape):
     st.SetJob(job)
     st.SetNodes(perm)
     want = _c5_want(g)
+    nils = {n[0]: tuple(n[1:]) for n in g["plain_nils"]}
     for i, w in enumerate(want):
-        r = st.Select(0)
-        if r is None:
-            r = st.Select(0, SelectOptions(preempt=True))
-        assert r is not None, "placement %d: nil" % i
+        r = st.SelectRaw(0)
+        if r.row < 0:
+            assert (r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted, r.new_offset) == nils[i], i
+            r = st.SelectRaw(0, SelectOptions(preempt=True))
+        else:
+            assert i not in nils, i
+        assert r.row >= 0, "placement %d: nil" % i
         got = _c5_key(r)
         assert got == w, ("placement %d" % i, got, w)
         st.Commit(0, r.row, r.preempted)
+    runs, served, rollbacks, records = st.SpeculationStats()
+    # speculative runs of x4 growing length serve everything; no per-Select path
+    assert rollbacks == 0 and runs <= 6 and served == len(want) + len(nils) - runs, st.SpeculationStats()
+
+
+def test_c5_bench_shape_served_from_the_view(c5_bench_shape):
+    # the Go shim's zero-crossing path: every answer it can take from the
+    # served-Select view, the nils and PreemptedAllocs included
+    from nomad_amd.stack import GenericStack
+    from tests.test_spec_view import ViewAnswers, protocol_answers
+    nodes, allocs, job, perm, cfg, g = c5_bench_shape
+    st = GenericStack(config=cfg)
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(perm)
+    vc = ViewAnswers(st)
+    got = [x if x[0] == "nil" else (x[0], x[1].hex(), tuple(v.hex() for v in x[2])) + tuple(x[3:])
+           for x in protocol_answers(vc, 1000)]
+    want, nils = _c5_want(g), {n[0]: n[1:] for n in g["plain_nils"]}
+    exp = []
+    for i, w in enumerate(want):
+        if i in nils:
+            exp.append(("nil",) + tuple(nils[i]))
+        exp.append(w)
+    assert len(got) == len(exp)
+    for i, (x, y) in enumerate(zip(got, exp)):
+        assert x == y, ("answer %d" % i, x, y)
+    runs, _, rollbacks, _ = st.SpeculationStats()
+    assert rollbacks == 0 and runs <= 6 and vc.served >= len(exp) - runs, (st.SpeculationStats(), vc.served)
 
 
 def test_c2_10k_caller_protocol_count_1000():

@@ -289,3 +289,87 @@ def test_metrics_preempt_selects_cpu_memory():
     seen = _preempt_loop(nodes, allocs, job, synth.shuffle(len(nodes), 5), 200,
                          SchedulerConfig(preempt_service=True))
     assert seen["preemption"] > 0
+
+
+def _view_metrics_loop(nodes, allocs, job, perm, placements, tg=0, deviate=()):
+    """The Go shim's zero-crossing path with metrics on: Selects and Commits
+    from the served-Select view, each served record's maps read from the view
+    (pe_spec_view.metrics), the rest through C; every Select's result and
+    maps equal the oracle's (generic_sched.go:558, 587: Allocation.Metrics)."""
+    import ctypes as C
+    from nomad_amd import abi
+    from nomad_amd.stack import GenericStack, parse_metrics
+    eng, ora = GenericStack(), OracleGenericStack()
+    for st in (eng, ora):
+        st.EnableMetrics()
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(perm)
+    fn = eng._lib.pe_spec_view_get
+    fn.restype = C.POINTER(abi.pe_spec_view)
+    fn.argtypes = [C.c_void_p]
+    v = fn(eng._h).contents
+    from_view = 0
+    for k in range(placements):
+        ro = ora.SelectRaw(tg)
+        mo = ora.LastMetrics()
+        if v.n_rec and v.tg_index == tg and v.served == v.confirmed and v.served < v.n_rec:
+            assert v.metrics and v.metrics_off, "served records carry no maps"
+            i = v.served
+            r = v.recs[i]
+            a, b = v.metrics_off[i], v.metrics_off[i + 1]
+            me = parse_metrics(C.string_at(v.metrics + a, b - a).decode())
+            v.served += 1
+            if r.row < 0:
+                v.confirmed += 1
+            from_view += 1
+            got = (r.row, r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted)
+        else:
+            re = eng.SelectRaw(tg)
+            me = eng.LastMetrics()
+            got = (re.row, re.nodes_evaluated, re.nodes_filtered, re.nodes_exhausted)
+        assert got == (ro.row, ro.nodes_evaluated, ro.nodes_filtered, ro.nodes_exhausted), k
+        assert me == mo, (k, me, mo)
+        if ro.row < 0:
+            break
+        row = ro.row
+        if k in deviate:   # another row: the run is rolled back, the memo rewound
+            row = int(perm[(k * 31) % len(perm)])
+        if k not in deviate and v.n_rec and v.tg_index == tg and v.served == v.confirmed + 1 \
+                and v.recs[v.served - 1].row == row:
+            v.confirmed += 1
+        else:
+            eng.Commit(tg, row)
+        ora.Commit(tg, row)
+    return from_view, eng
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deviate", [(), (3, 4, 57, 120)])
+def test_metrics_served_from_the_view(deviate):
+    nodes, allocs = synth.cluster_c2(600, seed=3)
+    for i, nd in enumerate(nodes):
+        if i % 7 == 0:
+            nd.attributes["kernel.name"] = "windows"
+            nd.compute_class()
+        if i % 11 == 0:
+            nd.drivers = {}
+            nd.attributes.pop("driver.exec", None)
+            nd.compute_class()
+    job = synth.job_c2(300)
+    job.constraints.append(Constraint("${attr.kernel.name}", "linux", "="))
+    job.task_groups[0].tasks[0].cpu = 2500
+    job.task_groups[0].tasks[0].memory_mb = 6000
+    from_view, eng = _view_metrics_loop(nodes, allocs, job, synth.shuffle(len(nodes), 9), 300, deviate=deviate)
+    assert from_view >= 250, from_view
+    runs, served, rollbacks, _ = eng.SpeculationStats()
+    assert runs >= 1 and rollbacks >= (1 if deviate else 0), eng.SpeculationStats()
+
+
+@pytest.mark.gpu
+def test_metrics_served_from_the_view_devices():
+    # device asks: the traced rows' free instances after the earlier records' offers
+    nodes, allocs = synth.cluster_c5(900, seed=4, busy=0.3)
+    job = synth.job_c5(150)
+    from_view, _ = _view_metrics_loop(nodes, allocs, job, synth.shuffle(len(nodes), 5), 150)
+    assert from_view >= 100, from_view

@@ -7,8 +7,9 @@ Self-derived from the oracle (the Go reference cannot run here, SURVEY.md
 this evaluation (628 Selects with Preempt over 50k nodes), too long for a GPU
 test, so the GPU test compares the engine with this frozen oracle output and
 tests/test_golden.py re-derives its first placements on the CPU to catch drift.
-oracle_place is the caller's loop itself (Select, Preempt retry on nil,
-commit with the preempted set), so the fixture answers both engine protocols.
+The loop is the caller's itself (Select, Preempt retry on nil, commit with
+the preempted set); the plain nil before each retry is kept too, so the
+fixture answers both engine protocols, the served records included.
 """
 import gzip
 import json
@@ -46,12 +47,34 @@ def main():
     st.SetState(nodes, allocs)
     st.SetJob(job)
     limit = st.SetNodes(list(perm))
+    # the caller's loop (generic_sched.go:552-627, 773-792), every Select
+    # answer kept: the plain Select's nil before a Preempt retry as well
+    from nomad_amd.stack import SelectOptions
+    res, nils, secs = [], [], []
     t0 = time.time()
-    res = st.Place(0, CASE["count"])
+    for i in range(CASE["count"]):
+        t1 = time.perf_counter()
+        r = st.SelectRaw(0)
+        if r.row < 0:
+            nils.append([i, r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted, r.new_offset])
+            r = st.SelectRaw(0, SelectOptions(preempt=True))
+        if r.row < 0:
+            break
+        st.Commit(0, r.row, r.preempted)
+        secs.append(time.perf_counter() - t1)
+        res.append(r)
     dt = time.time() - t0
-    doc = {"case": CASE, "limit": limit, "oracle_seconds": dt, "placements": [record(r) for r in res]}
+    doc = {"case": CASE, "limit": limit, "oracle_seconds": dt, "placements": [record(r) for r in res],
+           "plain_nils": nils}
     with gzip.open(OUT, "wt") as f:
         json.dump(doc, f, separators=(",", ":"))
+    # where the oracle's time goes, placement by placement (bench.py's C5
+    # cpu_baseline samples windows of this loop)
+    prof = os.path.join(ROOT, "profiles", "r05", "c5_oracle_timing.json")
+    os.makedirs(os.path.dirname(prof), exist_ok=True)
+    with open(prof, "w") as f:
+        json.dump({"case": CASE, "host": os.uname().nodename, "oracle_seconds": dt,
+                   "evicting": [bool(r.preempted) for r in res], "seconds": secs}, f)
     print("wrote %s: %d placements, %d evicting, oracle %.1f s"
           % (OUT, len(res), sum(1 for r in res if r.preempted), dt))
 
