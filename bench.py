@@ -422,17 +422,16 @@ def section_c4(device, rank, world, pg, cpu_s):
            "kernel_ms_rank0": float(np.median(kms[1:]))}
     if cpu_s > 0 and rank == 0:
         from oracle.oracle import OracleSystemStack
-        ns = 20000
-        small = synth_columnar.ColumnarState(ns, seed=11, kind="c4", prefill=0.05)
         o = OracleSystemStack()
-        o.SetStateColumnar(small)
+        o.SetStateColumnar(cs)
         o.SetJob(job)
-        o.SetNodes(np.arange(ns, dtype=np.uint32))
+        o.SetNodes(rows)
         t0 = time.perf_counter()
         o.SystemPlace(0)
         dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
-                               "sample": "system placements over a %d-node C4 cluster in %.2f s" % (ns, dt)}
+        out["cpu_baseline"] = {"value": n / dt, "unit": "nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
+                               "sample": "the same system placement over the same %d-node cluster and list in "
+                                         "%.2f s, 1 thread" % (n, dt)}
     return out
 
 
@@ -484,14 +483,13 @@ def section_c4_drop_in(device, cpu_s):
            "nodes_per_s_crossing": n / wall_x, "wall_ms_crossing": wall_x * 1e3}
     if cpu_s > 0:
         from oracle.oracle import OracleSystemStack
-        ns = 20000
-        small = synth_columnar.ColumnarState(ns, seed=11, kind="c4", prefill=0.05)
         o = OracleSystemStack()
-        o.SetStateColumnar(small)
+        o.SetStateColumnar(cs)
         o.SetJob(job)
-        _, _, _, dt = dropin.system_loop(o, 0, np.arange(ns, dtype=np.uint32))
-        out["cpu_baseline"] = {"value": ns / dt, "unit": "nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
-                               "sample": "the same C caller loop over a %d-node C4 cluster in %.3f s" % (ns, dt)}
+        _, _, _, dt = dropin.system_loop(o, 0, rows)
+        out["cpu_baseline"] = {"value": n / dt, "unit": "nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
+                               "sample": "the same C caller loop over the same %d-node cluster and list in %.3f s, "
+                                         "1 thread" % (n, dt)}
     return out
 
 
@@ -797,19 +795,33 @@ def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
                         "bytes_note": "records and keys read + 1 reason byte per plan node (DESIGN.md §9)"}}
     pl.close()
     if cpu_s > 0 and rank == 0:
-        from oracle import plan_apply as O
-        snap = O.Snapshot(my_nodes, my_allocs)
-        ids = ep.node_ids
-        t0 = time.perf_counter()
-        k = 0
-        while k < len(ids) and time.perf_counter() - t0 < cpu_s:
-            O.evaluate_node_plan(snap, my_plan, ids[k])
-            k += 1
-        dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": k / dt, "unit": "plan nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
-                               "sample": "evaluateNodePlan on the first %d plan nodes in %.2f s (oracle/plan_apply.py, "
-                                         "Python restatement; Go toolchain unavailable)" % (k, dt)}
+        # the C++ restatement (oracle/plan_oracle.cpp, -O3, one thread) over
+        # the same encoded plan: evaluateNodePlan for every plan node
+        from oracle.oracle import OraclePlanner
+        op = OraclePlanner()
+        op.set_state(my_nodes, my_allocs)
+        oep = op.encode(my_plan)
+        secs = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            ocodes = op.evaluate(oep)
+            secs.append(time.perf_counter() - t0)
+            if sum(secs) > cpu_s:
+                break
+        op.close()
+        if not np.array_equal(ocodes, codes):
+            raise RuntimeError("plan_apply: the C++ oracle's reasons differ from the device's")
+        dt = float(np.median(secs))
+        out["cpu_baseline"] = {"value": len(ids_of(oep)) / dt, "unit": "plan nodes/s", "cores": 1, "kind": "port",
+                               "cpu": cpu_model(),
+                               "sample": "evaluateNodePlan over all %d plan nodes of this shard, median of %d runs "
+                                         "of %.3f s (oracle/plan_oracle.cpp, C++ -O3 restatement, 1 thread; its "
+                                         "reasons equal the device's)" % (len(ids_of(oep)), len(secs), dt)}
     return out
+
+
+def ids_of(ep):
+    return ep.node_ids
 
 
 def section_c2_batch(device, nodes, allocs, job, count, evals, steps=10, warmup=2):
@@ -1008,6 +1020,29 @@ def main():
     total_placed = reduce(pg, placed, lambda d: d.ReduceOp.SUM)
     total_evals = reduce(pg, evals, lambda d: d.ReduceOp.SUM)
 
+    # The same caller loop with AllocMetric on: every placement's
+    # Allocation.Metrics (generic_sched.go:558, 587), the maps copied out from
+    # the served records (pe_spec_view.metrics) or through pe_last_metrics.
+    st.EnableMetrics(True)
+    dropin.use_metrics(True)
+    caller(orders, args.count, n_evals=1)
+    dropin.metric_bytes(reset=True)
+    m_evals = max(2, args.steps // 2)
+    sync()
+    t0 = time.perf_counter()
+    m_placed, m_done, _, _, _ = caller(timed_orders, args.count, n_evals=m_evals)
+    sync()
+    m_elapsed = time.perf_counter() - t0
+    m_bytes = dropin.metric_bytes(reset=True)
+    dropin.use_metrics(False)
+    st.EnableMetrics(False)
+    metrics_on = {"value": m_placed / m_elapsed, "unit": "placements/s", "evaluations": m_done,
+                  "ms_per_step": m_elapsed / max(1, m_done) * 1e3,
+                  "metric_bytes_per_eval": m_bytes / max(1, m_done),
+                  "note": "rank-local: the headline loop with pe_set_metrics on, every Select's AllocMetric maps "
+                          "(ClassFiltered / ConstraintFiltered / ClassExhausted / DimensionExhausted / top-5 "
+                          "ScoreMetaData) copied out by the caller"}
+
     # the dominant kernel of a step: the speculative count loop (k_base + k_chain),
     # timed with HIP events on the engine's stream by the same call path
     # HIP events between the chain's kernels (k_base, k_chain, k_emit,
@@ -1052,6 +1087,7 @@ def main():
                                       "predicted pairs from the served-Select view (pe_spec_view)"),
                        "evals_per_step": 1,
                        "parallelism": "replicas x%d (windowed binpack does not shard)" % world},
+            "metrics_on": metrics_on,
             "drop_in": {"placements": placed, "evaluations": evals, "selects": selects,
                         "selects_from_view": view_served,
                         "c_loop_seconds": c_secs,

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <charconv>
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -4791,9 +4792,31 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
 // NodeScoreMeta (structs.go:10030-10035) and the top-K ScoreHeap
 // (lib/kheap/score_heap.go) with Go's container/heap up/down, so ties keep the
 // reference's order.
+// The named scores of one option (at most 7 scorers: binpack, devices,
+// job-anti-affinity, node-reschedule-penalty, node-affinity,
+// allocation-spread, preemption); names are literals, so the heap moves PODs.
+struct ScoreList {
+    const char* name[8];
+    double val[8];
+    uint32_t n = 0;
+    void emplace_back(const char* k, double v) {
+        name[n] = k;
+        val[n] = v;
+        n++;
+    }
+    uint32_t size() const { return n; }
+    void sort_by_name() {   // NodeScoreMeta.Scores is a map: its keys in order
+        for (uint32_t i = 1; i < n; i++)
+            for (uint32_t j = i; j > 0 && std::strcmp(name[j], name[j - 1]) < 0; j--) {
+                std::swap(name[j], name[j - 1]);
+                std::swap(val[j], val[j - 1]);
+            }
+    }
+};
+
 struct ScoreMeta {
     uint32_t row;
-    std::vector<std::pair<std::string, double>> scores;   // sorted by name on output
+    ScoreList scores;   // sorted by name on output
     double norm;
 };
 
@@ -4996,19 +5019,31 @@ static std::string metrics_text(pe_stack* s, MetricAcc& acc) {
         for (auto& kv : mm) out += std::string(k) + "\t" + kv.first + "\t" + std::to_string(kv.second) + "\n";
     };
     put("CF", acc.cf); put("KF", acc.kf); put("CE", acc.ce); put("DE", acc.de);
-    // ScoreMetaData (PopulateScoreMetaData): "SM\trank\tnode id\tnorm\tname=value,..." (%.17g)
+    // ScoreMetaData (PopulateScoreMetaData): "SM\trank\tnode id\tnorm\tname=value,..."
+    // (shortest round-trip decimal: the same doubles when parsed back)
     auto items = acc.heap.reverse_items();
     char num[64];
+    auto put_num = [&](double x) {
+        const auto r = std::to_chars(num, num + sizeof num, x);
+        out.append(num, r.ptr);
+    };
     for (size_t i = 0; i < items.size(); i++) {
         auto& it = items[i];
-        std::sort(it.scores.begin(), it.scores.end());
-        snprintf(num, sizeof num, "%.17g", it.norm);
-        out += "SM\t" + std::to_string(i) + "\t" + s->S(s->nodes[it.row].id) + "\t" + num + "\t";
-        for (size_t k = 0; k < it.scores.size(); k++) {
-            snprintf(num, sizeof num, "%.17g", it.scores[k].second);
-            out += (k ? "," : "") + it.scores[k].first + "=" + num;
+        it.scores.sort_by_name();
+        out += "SM\t";
+        out += (char)('0' + i);
+        out += '\t';
+        out += s->S(s->nodes[it.row].id);
+        out += '\t';
+        put_num(it.norm);
+        out += '\t';
+        for (uint32_t k = 0; k < it.scores.size(); k++) {
+            if (k) out += ',';
+            out += it.scores.name[k];
+            out += '=';
+            put_num(it.scores.val[k]);
         }
-        out += "\n";
+        out += '\n';
     }
     return out;
 }
@@ -5137,6 +5172,8 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
 // earlier records' placements on the row. Windowed runs without property sets
 // and without evictions only (their state differs by placements alone).
 static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
+    static const bool prof = std::getenv("PE_METRICS_PROF") != nullptr;
+    const double t0 = prof ? now_us() : 0.0;
     pe_stack::Spec& sp = s->spec;
     const auto& order = s->visit;
     auto& rt = s->ref_tg_memo[g.name];
@@ -5165,6 +5202,7 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         if (row >= 0) placed_on[(uint32_t)row]++;
         off = sp.compact ? sp.crecs[k].new_offset : sp.recs[k].new_offset;
     }
+    const double t1 = prof ? now_us() : 0.0;
     std::vector<uint32_t> codes(rows.size());
     std::vector<double> sc(rows.size() * 6);
     pe::Ask a = ask_for(s, g);
@@ -5186,6 +5224,7 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         HIP_TRY(s, hipMemcpyAsync(sc.data(), s->d_trace_scores.p, sc.size() * 8, hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
     }
+    const double t2 = prof ? now_us() : 0.0;
     sp.mtext.clear();
     sp.mtext_off.assign(1, 0u);
     std::map<int, std::vector<uint32_t>> counts;
@@ -5199,6 +5238,9 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         sp.mtext_off.push_back((uint32_t)sp.mtext.size());
     }
     sp.metrics = true;
+    if (prof)
+        std::fprintf(stderr, "spec_metrics: %u records, %zu traced rows: walk %.1f us, trace %.1f us, maps+text %.1f us "
+                             "(%zu B)\n", sp.n_rec, rows.size(), t1 - t0, t2 - t1, now_us() - t2, sp.mtext.size());
     return PE_OK;
 }
 
@@ -6135,7 +6177,9 @@ static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* op
         // earlier placements (spec_metrics): windowed runs, no property sets,
         // no evictions
         TgPlan& g = *s->tgs[tgi];
-        if (s->cfg.preempt || !g.psets.empty() || g.psets_dynamic || tg_full_scan(s, g)) return false;
+        if (s->cfg.preempt || tg_full_scan(s, g) || !g.distinct_props.empty()) return false;   // (sets may be unbuilt)
+        for (auto& c : s->job_constraints)
+            if (c.op == "distinct_property") return false;
     }
     return true;
 }

@@ -56,6 +56,16 @@ int oracle_check_constraint(const char* op, const char* l, int l_state, const ch
 int oracle_limit_iter(const double* scores, int n, int limit, double threshold, int max_skip,
                       int* out_order, int* winner, int* pulled);
 
+/* Plan applier fit check (plan_oracle.cpp): pe_planner_* on the CPU. */
+typedef struct oracle_planner oracle_planner;
+oracle_planner* oracle_planner_create(void);
+void oracle_planner_destroy(oracle_planner* p);
+int oracle_planner_set_state(oracle_planner* p, const pe_strtab* strs, const pe_plan_node_table* nodes,
+                             const pe_plan_alloc_table* allocs);
+int oracle_planner_evaluate(oracle_planner* p, const pe_strtab* strs, const pe_plan* plan, uint8_t* reason,
+                            uint32_t* n_fit);
+int oracle_planner_commit(oracle_planner* p, const pe_strtab* strs, const pe_plan* plan, const uint8_t* keep);
+
 #ifdef __cplusplus
 }
 #endif

@@ -98,3 +98,51 @@ def limit_iter(scores, limit, threshold=0.0, max_skip=3):
     k = load().oracle_limit_iter(s.ctypes.data_as(abi.f64p), len(s), limit, threshold, max_skip,
                                  order.ctypes.data_as(abi.i32p), C.byref(w), C.byref(p))
     return list(order[:k]), w.value, p.value
+
+
+class _PlannerAdapter:
+    """pe_planner_* names over liboracle's oracle_planner_* (plan_oracle.cpp)."""
+
+    def __init__(self, lib):
+        H = C.c_void_p
+        sigs = [("create", C.c_void_p, []), ("destroy", None, [H]),
+                ("set_state", C.c_int, [H, C.POINTER(abi.pe_strtab), C.POINTER(abi.pe_plan_node_table),
+                                        C.POINTER(abi.pe_plan_alloc_table)]),
+                ("evaluate", C.c_int, [H, C.POINTER(abi.pe_strtab), C.POINTER(abi.pe_plan), abi.u8p, abi.u32p]),
+                ("commit", C.c_int, [H, C.POINTER(abi.pe_strtab), C.POINTER(abi.pe_plan), abi.u8p])]
+        for name, res, args in sigs:
+            fn = getattr(lib, "oracle_planner_" + name)
+            fn.restype = res
+            fn.argtypes = args
+            setattr(self, "pe_planner_" + name, fn)
+
+    @staticmethod
+    def pe_planner_last_error(h):
+        return b"oracle planner"
+
+
+def OraclePlanner():
+    """nomad_amd.plan.Planner's interface (set_state / encode / evaluate /
+    evaluate_plan_placements / apply) on the C++ restatement: the same
+    encoding of the same plans, evaluated on one CPU core."""
+    from nomad_amd.plan import Interner, Planner
+
+    class _OraclePlanner(Planner):
+        def __init__(self):
+            self.lib = _PlannerAdapter(load())
+            self.h = self.lib.pe_planner_create()
+            self.nodes, self.row_of, self.allocs, self.alloc_index = [], {}, [], {}
+            self.interner = Interner()
+
+        def close(self):
+            if getattr(self, "h", None):
+                self.lib.pe_planner_destroy(self.h)
+                self.h = None
+
+        def kernel_ms(self):
+            return 0.0
+
+        def last_bytes(self):
+            return 0
+
+    return _OraclePlanner()

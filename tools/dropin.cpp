@@ -45,7 +45,35 @@ struct dropin_api {
     int (*preempted_of)(const void*, uint32_t, uint32_t*, uint32_t);
     pe_spec_view* (*spec_view_get)(void*);   // null: every Select and Commit crosses
     pe_system_view* (*system_view_get)(void*);   // null: every per-node triple crosses
+    int64_t (*last_metrics)(const void*, char*, size_t);   // AllocMetric text of the last Select
 };
+
+// With metrics on, every Select's AllocMetric maps are copied out as the shim
+// fills Allocation.Metrics (generic_sched.go:558, 587): from the served
+// record's text in the view, else through last_metrics.
+static int g_metrics = 0;
+void dropin_use_metrics(int on) { g_metrics = on; }
+static uint64_t g_metric_bytes = 0;
+uint64_t dropin_metric_bytes(int reset) {
+    const uint64_t x = g_metric_bytes;
+    if (reset) g_metric_bytes = 0;
+    return x;
+}
+static char g_mbuf[1 << 16];
+static void metrics_from_view(const pe_spec_view* v, uint32_t k) {
+    if (!g_metrics || !v->metrics) return;
+    const uint32_t a = v->metrics_off[k], n = v->metrics_off[k + 1] - a;
+    const uint32_t c = n < sizeof(g_mbuf) ? n : (uint32_t)sizeof(g_mbuf);
+    std::memcpy(g_mbuf, v->metrics + a, c);
+    g_metric_bytes += n;
+}
+static int metrics_from_c(const dropin_api* api, void* h) {
+    if (!g_metrics || !api->last_metrics) return 0;
+    const int64_t n = api->last_metrics(h, g_mbuf, sizeof(g_mbuf));
+    if (n < 0) return (int)n;
+    g_metric_bytes += (uint64_t)n;
+    return 0;
+}
 
 static int g_use_view = 1;
 void dropin_use_view(int on) { g_use_view = on; }
@@ -100,6 +128,7 @@ int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, in
         if (view_can(v, tg, 0)) {
             // a plain Select answered from the view; an option's Commit is
             // confirmed there, a nil is settled at once
+            metrics_from_view(v, v->served);
             const pe_spec_rec& r = v->recs[v->served++];
             v->confirmed++;
             sel++;
@@ -115,12 +144,14 @@ int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, in
             rc = api->select(h, tg, &none, &opt);
             sel++;
             first_done(i);
+            if (!rc) rc = metrics_from_c(api, h);
             if (rc) break;
         }
         if (opt.row < 0 && preempt) {
             if (view_can(v, tg, PE_SPEC_PREEMPT)) {
                 // the Preempt retry from the view; its CommitPreempt names the
                 // record's row and PreemptedAllocs, confirmed there
+                metrics_from_view(v, v->served);
                 const pe_spec_rec& r = v->recs[v->served++];
                 v->confirmed++;
                 sel++;
@@ -132,6 +163,7 @@ int dropin_place(const dropin_api* api, void* h, uint32_t tg, uint32_t count, in
             }
             rc = api->select(h, tg, &pre, &opt);
             sel++;
+            if (!rc) rc = metrics_from_c(api, h);
             if (rc) break;
         }
         if (opt.row < 0) break;

@@ -20,7 +20,7 @@ _lib = None
 class dropin_api(C.Structure):
     _fields_ = [(name, C.c_void_p) for name in
                 ("reset_plan", "set_job", "set_nodes", "select", "commit", "commit_preempt", "preempted_of",
-                 "spec_view_get", "system_view_get")]
+                 "spec_view_get", "system_view_get", "last_metrics")]
 
 
 def load():
@@ -40,6 +40,10 @@ def load():
         lib.dropin_use_view.argtypes = [C.c_int]
         lib.dropin_view_served.restype = C.c_uint64
         lib.dropin_view_served.argtypes = [C.c_int]
+        lib.dropin_use_metrics.restype = None
+        lib.dropin_use_metrics.argtypes = [C.c_int]
+        lib.dropin_metric_bytes.restype = C.c_uint64
+        lib.dropin_metric_bytes.argtypes = [C.c_int]
         lib.dropin_system.restype = C.c_int
         lib.dropin_system.argtypes = [C.POINTER(dropin_api), C.c_void_p, C.c_uint32, abi.u32p, C.c_uint32,
                                       abi.u8p, abi.f64p, abi.u32p, C.c_void_p, C.POINTER(C.c_double)]
@@ -60,6 +64,17 @@ def use_view(on):
     """Whether the C loop answers plain Select / Commit pairs from the
     engine's served-Select view (the Go shim's shape) or crosses every time."""
     load().dropin_use_view(1 if on else 0)
+
+
+def use_metrics(on):
+    """Whether the C loop copies out every Select's AllocMetric maps (the
+    stack must have them on: EnableMetrics), as the shim fills
+    Allocation.Metrics."""
+    load().dropin_use_metrics(1 if on else 0)
+
+
+def metric_bytes(reset=False):
+    return int(load().dropin_metric_bytes(1 if reset else 0))
 
 
 def view_served(reset=False):
