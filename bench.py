@@ -613,6 +613,9 @@ def section_c3_sharded(device, rank, world, pg, placements=256, host_placements=
         # every rank times its own exchange (the all-gather's events on its
         # engine stream); the line reports the slowest rank's
         xs.append(reduce(pg, st.last_exchange_us(), lambda d: d.ReduceOp.MAX))
+    xstats = st.last_exchange_stats()
+    x_min = reduce(pg, xstats[1], lambda d: d.ReduceOp.MAX)
+    x_max = reduce(pg, xstats[2], lambda d: d.ReduceOp.MAX)
     placed = sum(1 for r in res if r.row >= 0)
     wall = min(walls[1:])
     out = {"workload": "C3 job on %d nodes, full-pass Selects sharded over %d GPUs, %d placements"
@@ -620,6 +623,9 @@ def section_c3_sharded(device, rank, world, pg, placements=256, host_placements=
            "placements_per_s": placed / wall, "ms_per_placement": wall / max(1, placed) * 1e3,
            "node_evals_per_s": placed * n / wall,
            "exchange_us_per_placement": xs[-1],
+           "exchange_us_stats": {"mean": xs[-1], "min": x_min, "max": x_max, "timed_placements": xstats[3],
+                                 "note": "HIP events around every placement's all-gather on each rank's stream, "
+                                         "max over ranks (includes waiting for the slowest rank's sweep)"},
            "exchange": ("none (one rank)" if world == 1 else
                         "in-place ncclAllGather of the per-workgroup 80 B records on the engine stream "
                         "(pe_place_sharded)")}

@@ -380,9 +380,12 @@ int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id);
  * records. Windowed task groups return PE_EUNSUPPORTED (replicas only). */
 int pe_place_sharded(pe_stack* s, uint32_t tg_index, uint32_t count, uint32_t row_begin, uint32_t row_end,
                      pe_ranked_node* out, uint32_t* placed);
-/* Device time of one all-gather in the last pe_place_sharded (microseconds,
- * mean over one sampled placement per 64; includes waiting for peer ranks). */
+/* Device time of the all-gather in the last pe_place_sharded (microseconds,
+ * mean over every placement; includes waiting for peer ranks). */
 double pe_last_exchange_us(const pe_stack* s);
+/* The same as out4 = {mean, min, max} microseconds and the placements timed
+ * (0 at one rank: no exchange runs). */
+int pe_last_exchange_stats(const pe_stack* s, double* out4);
 /* Counters of the speculative loop: out[0] runs started, [1] Selects answered
  * from records, [2] rollbacks (the caller deviated), [3] records computed. */
 int pe_speculation_stats(const pe_stack* s, uint64_t* out4);

@@ -227,7 +227,7 @@ ENGINE_SYMBOLS = [
     "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
     "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
-    "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get", "pe_system_view_get", "pe_comm_library",
+    "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get", "pe_system_view_get", "pe_comm_library", "pe_last_exchange_stats",
 ]
 
 

@@ -825,6 +825,8 @@ struct pe_stack {
     DevMem d_full_args;
     hipEvent_t ev_x0 = nullptr, ev_x1 = nullptr;   // around one sampled all-gather per chunk
     double last_exchange_us = 0;
+    double last_exchange_stats[4] = {0, 0, 0, 0};   // mean, min, max us, placements timed
+    std::vector<hipEvent_t> ev_xs;                   // pe_place_sharded: a pair per placement of a chunk
 
     // PE_API_PROF=1: wall time per named host step, printed at pe_stack_destroy
     bool api_prof = false;
@@ -4192,6 +4194,8 @@ void pe_stack_destroy(pe_stack* s) {
     if (s->comm) (void)rc_CommDestroy(s->comm);
     if (s->ev_x0) (void)hipEventDestroy(s->ev_x0);
     if (s->ev_x1) (void)hipEventDestroy(s->ev_x1);
+    for (hipEvent_t ev : s->ev_xs)
+        if (ev) (void)hipEventDestroy(ev);
     retire_tgs(s);
     for (hipEvent_t ev : s->ev_split)
         if (ev) (void)hipEventDestroy(ev);
@@ -6752,8 +6756,12 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
     uint32_t* state = s->d_loop_state.as<uint32_t>();
     uint32_t h_state[5] = {0, 0, 0, 0, 0};
     const uint32_t chunk = 64;
-    double x_us = 0;
+    double x_us = 0, x_min = 1e300, x_max = 0;
     uint32_t x_n = 0;
+    if (s->nranks > 1 && s->ev_xs.empty()) {   // an event pair around every placement's all-gather
+        s->ev_xs.resize(2 * chunk, nullptr);
+        for (auto& e : s->ev_xs) HIP_TRY(s, hipEventCreate(&e));
+    }
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     if (A.spread_tab) HIP_TRY(s, pe_launch_spread_table(&A.tg, s->d_spread_tab.as<double>(), s->stream));
     for (uint32_t k = 0; k < count && !h_state[0]; k += chunk) {
@@ -6761,23 +6769,31 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
         for (uint32_t j = 0; j < m; j++) {
             HIP_TRY_STATE(s, pe_launch_sweep_only(&A, blocks, s->stream));
             if (s->nranks > 1) {   // in place: this rank's slice already sits at its offset
-                if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x0, s->stream));
+                HIP_TRY(s, hipEventRecord(s->ev_xs[2 * j], s->stream));
                 const ncclResult_t r = rc_AllGather(A.recs, s->d_gather.p, slice, ncclUint8, s->comm, s->stream);
                 if (r != ncclSuccess) return s->fail(PE_EHIP, std::string("ncclAllGather: ") + rc_GetErrorString(r));
-                if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x1, s->stream));
+                HIP_TRY(s, hipEventRecord(s->ev_xs[2 * j + 1], s->stream));
             }
             HIP_TRY_STATE(s, pe_launch_step_only(&A2, nrecs, s->d_visit.as<uint32_t>(), n, s->offset,
                                            s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
         }
         HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
-        float xms = 0;
-        if (m && s->nranks > 1 && hipEventElapsedTime(&xms, s->ev_x0, s->ev_x1) == hipSuccess) {
-            x_us += xms * 1e3;
+        for (uint32_t j = 0; s->nranks > 1 && j < m; j++) {   // every placement's all-gather
+            float xms = 0;
+            if (hipEventElapsedTime(&xms, s->ev_xs[2 * j], s->ev_xs[2 * j + 1]) != hipSuccess) continue;
+            const double us = xms * 1e3;
+            x_us += us;
+            x_min = std::min(x_min, us);
+            x_max = std::max(x_max, us);
             x_n++;
         }
     }
     s->last_exchange_us = x_n ? x_us / x_n : 0.0;
+    s->last_exchange_stats[0] = s->last_exchange_us;
+    s->last_exchange_stats[1] = x_n ? x_min : 0.0;
+    s->last_exchange_stats[2] = x_max;
+    s->last_exchange_stats[3] = x_n;
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     const uint32_t p = h_state[1];
     const uint32_t nrec = std::min(count, p + (h_state[0] ? 1u : 0u));
@@ -6797,6 +6813,12 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
 }
 
 double pe_last_exchange_us(const pe_stack* s) { return s ? s->last_exchange_us : 0.0; }
+
+int pe_last_exchange_stats(const pe_stack* s, double* out4) {
+    if (!s || !out4) return PE_EINVAL;
+    for (int i = 0; i < 4; i++) out4[i] = s->last_exchange_stats[i];
+    return PE_OK;
+}
 
 int pe_speculation_stats(const pe_stack* s, uint64_t* out4) {
     if (!s || !out4) return PE_EINVAL;

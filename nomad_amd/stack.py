@@ -543,8 +543,14 @@ class GenericStack(_Stack):
         return [RankedNode.from_c(out[i], self.nodes) for i in range(n)]
 
     def last_exchange_us(self) -> float:
-        """Device time of one all-gather in the last PlaceSharded (us)."""
+        """Device time of the all-gather in the last PlaceSharded (us, mean over every placement)."""
         return self._lib.pe_last_exchange_us(self._h)
+
+    def last_exchange_stats(self):
+        """(mean, min, max) us of the last PlaceSharded's all-gathers and the placements timed."""
+        out = (C.c_double * 4)()
+        self._lib.pe_last_exchange_stats(C.c_void_p(self._h), out)
+        return float(out[0]), float(out[1]), float(out[2]), int(out[3])
 
     def SpeculationStats(self):
         """(runs, Selects answered from records, rollbacks, records computed) of

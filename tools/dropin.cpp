@@ -240,22 +240,38 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     pe_system_view* v = (g_use_view && api->system_view_get) ? api->system_view_get(h) : nullptr;
+    // The shim's fast path keeps the view's fields in locals while it answers
+    // from host memory, and writes its log count back before any C call (the
+    // engine reads it there) and at the end.
+    uint32_t n_rows = 0, log_cap = 0, n_log = 0, pre = 0;
+    uint64_t* outcome = nullptr;
+    uint32_t* log = nullptr;
+    auto load_view = [&]() {
+        if (!v) return;
+        n_rows = (v->tg_index == tg) ? v->n_rows : 0u;
+        log_cap = v->log_cap;
+        n_log = v->n_log;
+        pre = v->preempt;
+        outcome = v->outcome;
+        log = v->log;
+    };
+    load_view();
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t row = rows[i];
-        if (v && v->n_rows && v->tg_index == tg && row < v->n_rows && v->n_log < v->log_cap) {
-            uint64_t bits = v->outcome[row];
+        if (row < n_rows && n_log < log_cap) {
+            const uint64_t bits = outcome[row];
             const bool nan = (bits & 0x7FF8000000000000ull) == 0x7FF8000000000000ull;
             const uint32_t code = nan ? (uint32_t)(bits & 3u) : 0u;
-            if (code != 3u && !(code == 2u && v->preempt)) {
+            if (code != 3u && !(code == 2u && pre)) {
                 if (code) {   // nil: filtered or exhausted
-                    v->log[v->n_log++] = row | PE_SYS_NIL;
+                    log[n_log++] = row | PE_SYS_NIL;
                     status[i] = (uint8_t)code;
                     score[i] = __builtin_nan("");
                 } else {      // an option, appended to the plan
                     double sc;
                     std::memcpy(&sc, &bits, sizeof(sc));
-                    v->log[v->n_log++] = row | PE_SYS_COMMITTED;
-                    v->outcome[row] = PE_SYS_STALE;
+                    log[n_log++] = row | PE_SYS_COMMITTED;
+                    outcome[row] = PE_SYS_STALE;
                     status[i] = 0;
                     score[i] = sc;
                     p++;
@@ -264,22 +280,23 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
                 continue;
             }
         }
+        if (v) v->n_log = n_log;   // the engine takes the log over first
         uint32_t limit;
         rc = api->set_nodes(h, rows + i, 1, &limit);
-        if (rc) break;
-        rc = api->select(h, tg, &none, &opt);
+        if (!rc) rc = api->select(h, tg, &none, &opt);
+        if (!rc && opt.row >= 0) rc = commit_opt(api, h, tg, opt, 0);
+        load_view();   // the crossing may have replaced or withdrawn the view
         if (rc) break;
         if (opt.row < 0) {
             status[i] = opt.nodes_filtered > 0 ? 1 : 2;
             score[i] = __builtin_nan("");
             continue;
         }
-        rc = commit_opt(api, h, tg, opt, 0);
-        if (rc) break;
         status[i] = 0;
         score[i] = opt.final_score;
         p++;
     }
+    if (v) v->n_log = n_log;
     if (!rc && flush) rc = flush(h);
     *seconds = std::chrono::duration<double>(clk::now() - t0).count();
     *placed = p;
