@@ -200,13 +200,14 @@ def cpu_baseline(nodes, allocs, job, seconds):
 # score word (verdict, affinity index, spread values; 1 B verdict when the word
 # does not apply: 73 B) + 4 B (job,tg) collisions + 4 B visit rank = 76 B.
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04", "sweep_traffic.json")
-CHAIN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "chain_traffic.json")
-PLAN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "plan_traffic.json")
+CHAIN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "c2_batch_traffic.json")
+PLAN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "plan_traffic.json")
 
 
 def plan_traffic(bytes_per_launch):
     """HBM bytes per k_plan_eval launch from the committed FETCH_SIZE / WRITE_SIZE
-    passes (tools/plan_prof.sh), when they were taken on this same workload."""
+    passes (tools/plan_prof.sh), when they were taken on this same workload
+    (the same algorithmic bytes per launch)."""
     try:
         d = json.load(open(PLAN_TRAFFIC_FILE))
     except (OSError, ValueError):
@@ -215,8 +216,8 @@ def plan_traffic(bytes_per_launch):
 
 
 def chain_traffic(evals_per_launch):
-    """HBM bytes per k_chain launch from the committed PMC passes over this
-    same headline workload (tools/profile_round.sh), or None."""
+    """HBM bytes per batched k_base + k_chain launch from the committed PMC
+    passes over this same workload (tools/batch_pmc.sh), or None."""
     try:
         with open(CHAIN_TRAFFIC_FILE) as f:
             t = json.load(f)
@@ -453,12 +454,14 @@ def section_c4_drop_in(device, cpu_s):
     st.SetStateColumnar(cs)
     times, placed = [], 0
     dropin.view_served(reset=True)
+    dropin.system_phases(reset=True)
     for i in range(4):
         st.ResetPlan()
         st.SetJob(job)
         _, _, placed, secs = dropin.system_loop(st, 0, rows)
         times.append(secs)
     from_view = dropin.view_served(reset=True) / 4
+    phases = {k: v / 4 * 1e3 for k, v in dropin.system_phases(reset=True).items()}
     stats = (C.c_uint64 * 2)()
     st._lib.pe_system_spec_stats(C.c_void_p(st._h), stats)
     kms = st.last_kernel_ms()
@@ -480,6 +483,7 @@ def section_c4_drop_in(device, cpu_s):
                        "answered from it" % n,
            "placed": int(placed), "nodes_per_s": n / wall, "wall_ms": wall * 1e3, "cache_kernel_ms": kms,
            "cache_passes": int(stats[0]), "served_selects": int(stats[1]), "from_view_per_eval": from_view,
+           "ms_per_eval_by_phase": phases,
            "nodes_per_s_crossing": n / wall_x, "wall_ms_crossing": wall_x * 1e3}
     if cpu_s > 0:
         from oracle.oracle import OracleSystemStack

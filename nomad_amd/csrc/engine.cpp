@@ -2547,28 +2547,35 @@ static void sys_view_take(pe_stack* s) {
     if (!y.active || y.tgi >= s->tgs.size() || s->visit.size() != 1) { s->sys_taken = upto; return; }
     const auto name = s->tgs[y.tgi]->name;
     uint64_t* cache = s->h_sys_cache.as<uint64_t>();
-    if (s->elig_log.empty() && (s->elig_mute || s->tgs[y.tgi]->elig_complete)) {
+    auto take_fast = [&](uint32_t k0) {
         // nothing for EvalEligibility to log: the per-node SetNodes / Select
         // bookkeeping leaves the last entry's state, and only the commits
         // need one step each
         uint32_t last = PE_NONE;
         bool last_nil = true;
         uint32_t cnt = 0;
-        y.pending.reserve(y.pending.size() + (upto - s->sys_taken));
-        s->plan.reserve(s->plan.size() + (upto - s->sys_taken));
-        for (uint32_t k = s->sys_taken; k < upto; k++) {
+        // one branch-light pass: the committed rows compacted into the queue
+        // (the caller marked their outcome stale, nomad_pe.h), then the plan
+        // entries from them
+        const size_t p0 = y.pending.size();
+        y.pending.resize(p0 + (upto - k0));
+        uint32_t* q = y.pending.data() + p0;
+        size_t c = 0;
+        const uint32_t nn = (uint32_t)s->nodes.size();
+        for (uint32_t k = k0; k < upto; k++) {
             const uint32_t e = v.log[k];
             const uint32_t row = e & PE_SYS_ROW_MASK;
-            if (row >= s->nodes.size()) continue;
+            if (row >= nn) continue;
             cnt++;
             last = row;
             last_nil = (e & PE_SYS_NIL) != 0;
-            if (!last_nil && (e & PE_SYS_COMMITTED)) {
-                y.pending.push_back(row);
-                cache[row] = kSysStale;
-                s->plan.emplace_back(name, row);
-            }
+            q[c] = row;
+            c += (!last_nil && (e & PE_SYS_COMMITTED)) ? 1u : 0u;
         }
+        y.pending.resize(p0 + c);
+        const size_t l0 = s->plan.size();
+        s->plan.resize(l0 + c);
+        for (size_t i = 0; i < c; i++) s->plan[l0 + i] = std::make_pair(name, q[i]);
         if (cnt) {
             const uint32_t le = v.log[upto - 1];
             const bool committed = !last_nil && (le & PE_SYS_COMMITTED) && (le & PE_SYS_ROW_MASK) == last;
@@ -2585,10 +2592,12 @@ static void sys_view_take(pe_stack* s) {
             s->offers = 0xFFFFFFFFu;
             s->metrics_valid = false;
         }
-        s->sys_taken = upto;
-        return;
-    }
-    for (uint32_t k = s->sys_taken; k < upto; k++) {
+    };
+    // entry by entry while EvalEligibility still learns classes, then the
+    // rest at once
+    uint32_t k = s->sys_taken;
+    for (; k < upto; k++) {
+        if (s->elig_log.empty() && (s->elig_mute || s->tgs[y.tgi]->elig_complete)) break;
         const uint32_t e = v.log[k];
         const uint32_t row = e & PE_SYS_ROW_MASK;
         if (row >= s->nodes.size()) continue;
@@ -2618,6 +2627,7 @@ static void sys_view_take(pe_stack* s) {
             s->offer_row = -1;
         }
     }
+    if (k < upto) take_fast(k);
     s->sys_taken = upto;
 }
 
@@ -5357,12 +5367,14 @@ static bool sys_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, 
     if (s->visit.size() != 1 || s->metrics_on || !s->have_job || tgi >= s->tgs.size()) return false;
     if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
     if (!y.active || y.tgi != tgi) {
-        // start after the group's second single-node Select: one pass over the
-        // snapshot costs about as much as a handful of single Selects
+        // start at the group's first single-node Select: one pass over the
+        // snapshot (~90 us at 100k rows) costs less than one single Select
+        // after SetJob (~130 us with its launch and synchronisation)
         if (y.singles_tgi != tgi) { y.singles_tgi = tgi; y.singles = 0; }
-        if (++y.singles < 3) return false;
+        if (y.singles == PE_NONE) return false;   // not cacheable: the single Select path, until SetJob
+        y.singles++;
         const int r = sys_start(s, tgi);
-        if (r == PE_EUNSUPPORTED) { y.singles = 0; s->err.clear(); return false; }
+        if (r == PE_EUNSUPPORTED) { y.singles = PE_NONE; s->err.clear(); return false; }
         if (r) { *rc = r; return true; }
     }
     const uint32_t row = s->visit[0];

@@ -3,7 +3,7 @@
 SystemScheduler.computePlacements (scheduler_system.go:283-425) calls, for
 every node it places on, SetNodes([node]) then Select and appends a placed
 option to the plan. tools/dropin.cpp runs exactly that loop in C against the
-engine and against the oracle. From a task group's third single-node Select
+engine and against the oracle. From a task group's first single-node Select
 the engine answers from a per-row cache filled by one k_system pass (no
 commit) and queues the commits (pe_flush / any later device call applies
 them). Results must equal the oracle's Select by Select, and the pe_system_place
@@ -69,8 +69,8 @@ def test_system_caller_protocol_matches_oracle(n, view):
     ro = dropin.system_loop(o, 0, rows)
     _same(re_, ro)
     passes, served = _stats(e)
-    assert passes == 1 and served == n - 2
-    assert dropin.view_served(reset=True) == (n - 3 if view else 0)
+    assert passes == 1 and served == n   # the first Select starts the cache pass
+    assert dropin.view_served(reset=True) == (n - 1 if view else 0)   # the first triple starts the pass
     assert re_[2] > 0.8 * n
     # the batch path on a fresh evaluation gives the same outcomes
     e.ResetPlan()
@@ -141,7 +141,7 @@ def test_system_view_protocol_and_withdrawal():
     v = _sys_view(e)
     assert v.n_rows == 0
     out_e, out_o = [], []
-    for r in range(3):   # the first Selects cross; the third starts the cache pass
+    for r in range(3):   # through C: the first starts the cache pass, the next two are served
         for st, out in ((e, out_e), (o, out_o)):
             st.SetNodes([r])
             x = st.Select(0)

@@ -230,6 +230,16 @@ int dropin_evals(const dropin_api* api, void* h, const pe_strtab* strs, const pe
 // `flush` (may be null) is called once at the end, inside the timed region:
 // the entry point that forces queued device work (e.g. the next call that
 // reads the device state). Returns 0 or the first failing status.
+// Wall time of dropin_system's parts since the last reset: [0] the triples that
+// crossed into C, [1] the whole loop (crossings included), [2] the final flush.
+static double g_sys_phase[3];
+void dropin_system_phases(double* out3, int reset) {
+    for (int i = 0; i < 3; i++) {
+        out3[i] = g_sys_phase[i];
+        if (reset) g_sys_phase[i] = 0.0;
+    }
+}
+
 int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* rows, uint32_t n, uint8_t* status,
                   double* score, uint32_t* placed, int (*flush)(void*), double* seconds) {
     pe_select_options none;
@@ -281,11 +291,13 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
             }
         }
         if (v) v->n_log = n_log;   // the engine takes the log over first
+        const auto tc = clk::now();
         uint32_t limit;
         rc = api->set_nodes(h, rows + i, 1, &limit);
         if (!rc) rc = api->select(h, tg, &none, &opt);
         if (!rc && opt.row >= 0) rc = commit_opt(api, h, tg, opt, 0);
         load_view();   // the crossing may have replaced or withdrawn the view
+        g_sys_phase[0] += std::chrono::duration<double>(clk::now() - tc).count();
         if (rc) break;
         if (opt.row < 0) {
             status[i] = opt.nodes_filtered > 0 ? 1 : 2;
@@ -297,8 +309,12 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
         p++;
     }
     if (v) v->n_log = n_log;
+    const auto tf = clk::now();
     if (!rc && flush) rc = flush(h);
-    *seconds = std::chrono::duration<double>(clk::now() - t0).count();
+    const auto te = clk::now();
+    g_sys_phase[2] += std::chrono::duration<double>(te - tf).count();
+    *seconds = std::chrono::duration<double>(te - t0).count();
+    g_sys_phase[1] += *seconds - std::chrono::duration<double>(te - tf).count();
     *placed = p;
     return rc;
 }

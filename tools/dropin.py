@@ -40,6 +40,8 @@ def load():
         lib.dropin_use_view.argtypes = [C.c_int]
         lib.dropin_view_served.restype = C.c_uint64
         lib.dropin_view_served.argtypes = [C.c_int]
+        lib.dropin_system_phases.restype = None
+        lib.dropin_system_phases.argtypes = [C.POINTER(C.c_double), C.c_int]
         lib.dropin_use_metrics.restype = None
         lib.dropin_use_metrics.argtypes = [C.c_int]
         lib.dropin_metric_bytes.restype = C.c_uint64
@@ -121,6 +123,14 @@ def phase_seconds(reset=True):
     out = (C.c_double * 5)()
     load().dropin_phase_seconds(out, int(reset))
     return dict(zip(PHASES, list(out)))
+
+
+def system_phases(reset=True):
+    """Seconds of dropin_system's parts summed since the last reset: triples
+    that crossed into C, the whole loop, the final flush."""
+    out = (C.c_double * 3)()
+    load().dropin_system_phases(out, int(reset))
+    return {"crossing": out[0], "loop": out[1], "flush": out[2]}
 
 
 def system_loop(stack, tg, rows, flush=True):
