@@ -210,6 +210,57 @@ def _header_tables():
     return tabs, fold
 
 
+def test_unicode_scripts_and_folding_match_the_regex_module():
+    """The shared Unicode 13.0.0 tables (nomad_amd/csrc/unicode13.h, read by
+    the engine and by the oracle's restatement alike) against a third source
+    that neither side uses: the `regex` module's own Unicode database. Every
+    script's set of assigned code points and every simple-folding orbit must
+    agree; the only differences are later Unicode versions' changes (U+16FE2 /
+    U+16FE3 moved from Common to Han in 14.0) and the Turkic-only fold of
+    U+0131 (CaseFolding.txt status T, outside Go's C+S SimpleFold)."""
+    regex = pytest.importorskip("regex")
+    tabs, fold = _header_tables()
+    assigned = [c for c in range(0x110000)
+                if unicodedata.category(chr(c)) != "Cn" and not (0xD800 <= c <= 0xDFFF)]
+    text = "".join(chr(c) for c in assigned)
+    aset = set(assigned)
+    later = {0x16FE2: ("Common", "Han"), 0x16FE3: ("Common", "Han")}
+    for (kind, name), rs in tabs.items():
+        if kind != "scr":
+            continue
+        mine = set()
+        for a, b in rs:
+            mine.update(range(a, b + 1))
+        mine &= aset
+        theirs = {ord(x) for x in regex.findall(r"\p{Script=%s}" % name, text)}
+        for c in mine ^ theirs:
+            assert c in later and name in later[c], (name, hex(c))
+    parent = {}
+
+    def root(x):
+        while parent.get(x, x) != x:
+            x = parent[x]
+        return x
+    for c, f in fold.items():
+        a, b = root(c), root(f)
+        if a != b:
+            parent[a] = b
+    members = sorted(set(fold) | set(fold.values()))
+    orbit = {}
+    for c in members:
+        orbit.setdefault(root(c), set()).add(c)
+    ms = "".join(chr(c) for c in members)
+    for c in members:
+        got = {ord(x) for x in regex.findall(r"(?iV0)" + regex.escape(chr(c)), ms)}
+        assert got == orbit[root(c)], hex(c)
+    mset = set(members)
+    for c in assigned:
+        if c in mset or c == 0x131:
+            continue
+        for v in (chr(c).lower(), chr(c).upper(), chr(c).title()):
+            assert not (len(v) == 1 and v != chr(c) and regex.fullmatch(r"(?iV0)" + regex.escape(chr(c)), v)), hex(c)
+
+
 def test_unicode_tables_match_python_unicodedata():
     """The generated Unicode 13.0.0 data against Python's unicodedata (also 13.0.0)."""
     assert unicodedata.unidata_version == "13.0.0"

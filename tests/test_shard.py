@@ -219,3 +219,56 @@ def test_engine_rccl_sharded_loop_matches_place(n, count):
     # the plan is shared: the next Select on both handles agrees
     x, y = a.SelectRaw(0), b.SelectRaw(0)
     assert (x.row, x.final_score) == (y.row, y.final_score)
+
+
+def _engine_system_worker(rank, world, port, q):
+    # one engine process per rank, every rank on the box's GPU 0 at the same
+    # time (the one-GPU rehearsal of the per-GPU processes): its contiguous
+    # range of the SetNodes list, no data-path collective
+    from nomad_amd import synth_columnar
+    from nomad_amd.stack import SystemStack
+    _init(rank, world, port)
+    n = 100000
+    cs = synth_columnar.ColumnarState(n, seed=11, kind="c4", prefill=0.05)
+    job = synth.mock_system_job()
+    rows = np.random.Generator(np.random.PCG64(5)).permutation(n).astype(np.uint32)
+    st = SystemStack(device=0)
+    st.SetStateColumnar(cs)
+    st.SetJob(job)
+    dist.barrier()   # the ranks' placements run concurrently
+    b, e, score, status, placed = shard.system_place_sharded(st, rows, rank, world)
+    got = [None] * world
+    dist.all_gather_object(got, (b, e, score.tolist(), status.tolist(), placed))
+    st.close()
+    if rank == 0:
+        q.put(got)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_c4_concurrent_rank_processes_match_oracle(world):
+    """C4 at its full 100k nodes, `world` engine processes placing their
+    shards concurrently on one GPU: the union equals the oracle's unsharded
+    placement (tests/test_full_size.py runs the same shards one after another)."""
+    from nomad_amd import synth_columnar
+    from oracle.oracle import OracleSystemStack
+    got = _run(_engine_system_worker, world)
+    n = 100000
+    cs = synth_columnar.ColumnarState(n, seed=11, kind="c4", prefill=0.05)
+    job = synth.mock_system_job()
+    rows = np.random.Generator(np.random.PCG64(5)).permutation(n).astype(np.uint32)
+    o = OracleSystemStack()
+    o.SetStateColumnar(cs)
+    o.SetJob(job)
+    o.SetNodes(rows)
+    so, to, po = o.SystemPlace(0)
+    score = np.empty(n)
+    status = np.empty(n, dtype=np.uint8)
+    total = 0
+    for b, e, sc, st, p in got:
+        score[b:e], status[b:e] = sc, st
+        total += p
+    assert total == po and np.array_equal(status, to)
+    placed = to == 0
+    assert np.array_equal(score[placed], so[placed])
