@@ -146,12 +146,12 @@ hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, cons
                                     uint32_t* pcount, uint32_t* dev_free, hipStream_t st);
 hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st);
 hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* status, double* score,
-                            hipStream_t st);
+                            hipStream_t st, double* parts = nullptr, uint8_t* nparts = nullptr);
 hipError_t pe_launch_resolve(const pe::EvictResolveArgs* r, hipStream_t st);
 hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st);
 hipError_t pe_launch_static_gate(const uint8_t* blocked, const uint32_t* coll_tg, uint32_t* gate, uint32_t n,
                                  hipStream_t st);
-uint32_t pe_ploop_max_n();
+uint32_t pe_ploop_max_n(uint32_t words);
 hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted, uint32_t* pcount,
                                     uint32_t* dev_free, uint32_t* placed, hipStream_t st);
 size_t pe_fold_feas_max_classes();
@@ -729,6 +729,7 @@ struct pe_stack {
     DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)
     DevMem d_pset_g, d_pset_gb;              // FULL k_place per-value tables beyond the LDS budget (batch: gb)  // device-resident parallel count loop (k_ploop)
     DevMem d_ploop_parts, d_ploop_nparts;   // k_ploop: Preempt records per position (parts, count)
+    DevMem d_ploop_pparts, d_ploop_pnparts;   // k_ploop: plain records per position (parts, count)
 
     // Speculative count loop behind pe_select / pe_commit: the
     // first plain Select of a task group runs the device count loop for the
@@ -5668,7 +5669,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     *placed = 0;
     const uint32_t n = (uint32_t)s->visit.size();
     if (!count || (std::getenv("PE_PLOOP") && std::getenv("PE_PLOOP")[0] == '0')) return PE_OK;
-    if (!g.psets.empty() || g.psets_dynamic || !s->visit_unique || n == 0 || n > pe_ploop_max_n()) return PE_OK;
+    if (!g.psets.empty() || g.psets_dynamic || !s->visit_unique || n == 0) return PE_OK;
     if (g.ask.cores > 0) return PE_OK;   // k_ploop is compiled without reserved cores
     if (has_static(g)) return PE_OK;  // the static port gate is rebuilt on the host after evictions
     for (size_t k = 0; k < s->tgs.size(); k++)
@@ -5685,6 +5686,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, s->d_ev_out.ensure(16));
     HIP_TRY(s, s->d_ev_flags.ensure(16));
     if (!words) words = s->evict_words;
+    if (n > pe_ploop_max_n(words)) return PE_OK;   // the outcome codes outgrow the workgroup's LDS
     HIP_TRY(s, s->d_loop_out.ensure(sizeof(pe_ranked_node) * (size_t)count));
     HIP_TRY(s, s->d_ploop_mask.ensure(sizeof(uint32_t) * words * (size_t)count));
     HIP_TRY(s, s->d_loop_state.ensure(8 * sizeof(uint32_t)));
@@ -5692,8 +5694,11 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
     HIP_TRY(s, hipMemsetAsync(s->d_loop_state.p, 0, 8 * sizeof(uint32_t), s->stream));
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
+    HIP_TRY(s, s->d_ploop_pparts.ensure(sizeof(double) * PE_MAX_SCORES * (size_t)n));
+    HIP_TRY(s, s->d_ploop_pnparts.ensure(n));
     HIP_TRY_STATE(s, pe_launch_census(&A, s->d_ev_out.as<uint32_t>(), s->d_ev_status_p.as<uint8_t>(),
-                                s->d_ev_score_p.as<double>(), s->stream));
+                                      s->d_ev_score_p.as<double>(), s->stream, s->d_ploop_pparts.as<double>(),
+                                      s->d_ploop_pnparts.as<uint8_t>()));
     pe::PLoopArgs L;
     std::memset(&L, 0, sizeof(L));
     L.P = preempt_args(s, g);
@@ -5733,6 +5738,8 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     }
     L.st_plain = s->d_ev_status_p.as<uint8_t>();
     L.sc_plain = s->d_ev_score_p.as<double>();
+    L.parts_plain = s->d_ploop_pparts.as<double>();
+    L.nparts_plain = s->d_ploop_pnparts.as<uint8_t>();
     L.preempted = s->d_preempted.as<uint8_t>();
     L.pcount = s->d_pcount.as<uint32_t>();
     L.dev_free = s->d_dev_free.as<uint32_t>();
@@ -5754,8 +5761,8 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     }
     const bool prof = std::getenv("PE_PLACE_PROF") != nullptr;
     if (prof) {
-        HIP_TRY(s, s->d_prof.ensure(16 * sizeof(unsigned long long)));
-        HIP_TRY(s, hipMemsetAsync(s->d_prof.p, 0, 16 * sizeof(unsigned long long), s->stream));
+        HIP_TRY(s, s->d_prof.ensure(24 * sizeof(unsigned long long)));
+        HIP_TRY(s, hipMemsetAsync(s->d_prof.p, 0, 24 * sizeof(unsigned long long), s->stream));
         L.prof = s->d_prof.as<unsigned long long>();
     }
     HIP_TRY_STATE(s, pe_launch_ploop(&L, s->stream));
@@ -5782,7 +5789,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     s->last_ms = ms;
     s->last_ms_pending = false;
     if (prof) {
-        unsigned long long h[16];
+        unsigned long long h[24];
         HIP_TRY(s, hipMemcpy(h, L.prof, sizeof(h), hipMemcpyDeviceToHost));
         std::fprintf(stderr, "k_ploop: %u placements, %.3f ms total; us: plain resolve %.1f, refresh %.1f, preempt "
                              "resolve %.1f, winner %.1f (its evict_eval %.1f, commit %.1f); refreshed %llu dirty + %llu pcount "
@@ -5790,6 +5797,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
                              "%.1f (%llu calls)\n",
                      st[0], ms, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[6] / 100.0, h[7] / 100.0, h[4],
                      h[5], h[8] / 100.0, h[9], h[10] / 100.0, h[11]);
+        std::fprintf(stderr, "k_ploop resolves: %llu steps in %llu calls\n", h[12], h[13]);
     }
     *handled = true;
     const uint32_t p = std::min(st[0], count);

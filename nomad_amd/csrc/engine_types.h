@@ -375,6 +375,8 @@ struct PLoopArgs {
     const uint8_t* st_plain;          // [n] plain outcomes by position (k_census)
     const uint8_t* dep_init;          // [n] or null: Preempt outcomes that read the preemption counts (k_evict)
     double* sc_plain;                 // [n] plain scores by position (rewritten for committed rows)
+    double* parts_plain;              // [n * PE_MAX_SCORES] their score parts, [n] their count (options only):
+    uint8_t* nparts_plain;            // a plain winner's record is read, not re-evaluated
     uint8_t* preempted;               // Plan.NodePreemptions flags (apply_preempt)
     uint32_t* pcount;
     uint32_t* dev_free;

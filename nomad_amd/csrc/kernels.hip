@@ -2435,18 +2435,25 @@ __global__ void __launch_bounds__(256) k_rank_of(const uint32_t* list, uint32_t 
 // (no overlay): counts[0] options, [1] filtered, [2] exhausted. With no option
 // the Select is nil after pulling every node, which the count loop's
 // preemption retry uses instead of a windowed scan of the whole list.
-__global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts, uint8_t* status, double* score) {
+// kParts: also the score parts of each option (k_ploop's plain winner records).
+template <bool kParts>
+__global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts, uint8_t* status, double* score,
+                                                double* parts, uint8_t* nparts) {
     const uint32_t stride = gridDim.x * blockDim.x;
     uint32_t c[3] = {0, 0, 0};
     Overlay none;
     none.keys = nullptr;
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < A.n_visit; j += stride) {
         NodeEval ev;
-        eval_node<false>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, nullptr, A.perms[j], &ev);
+        eval_node<kParts>(A.soa, A.tg, A.tg.class_ok, A.ask, none, A.penalty_bits, A.log10, nullptr, A.perms[j], &ev);
         c[ev.status]++;
         if (status) {   // per-position outcomes for a parallel Select (k_evict_resolve)
             status[j] = (uint8_t)ev.status;
             score[j] = ev.status == kOption ? ev.score : 0.0;
+        }
+        if (kParts && ev.status == kOption) {
+            nparts[j] = (uint8_t)ev.nscores;
+            for (int k = 0; k < PE_MAX_SCORES; k++) parts[(size_t)j * PE_MAX_SCORES + k] = ev.parts[k];
         }
     }
     // one atomic per workgroup and counter (not per wave): fewer same-address
@@ -3561,11 +3568,17 @@ hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs*
 }
 
 hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* status, double* score,
-                            hipStream_t st) {
+                            hipStream_t st, double* parts, uint8_t* nparts) {
     uint32_t blocks = (a->n_visit + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(pe::k_census, dim3(blocks), dim3(256), 0, st, *a, counts, status, score);
+    if (parts) {
+        if (!nparts || !status) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(pe::k_census<true>, dim3(blocks), dim3(256), 0, st, *a, counts, status, score, parts, nparts);
+    } else {
+        hipLaunchKernelGGL(pe::k_census<false>, dim3(blocks), dim3(256), 0, st, *a, counts, status, score, parts,
+                           nparts);
+    }
     return hipGetLastError();
 }
 
@@ -3863,21 +3876,48 @@ hipError_t pe_launch_sweep_loop(const pe::SweepArgs* a, uint32_t blocks, uint32_
 }
 
 // Device-resident count loop over sparse options (one workgroup); dynamic LDS
-// = 2 bits per position for each of the two outcome passes.
-constexpr uint32_t kPLoopMaxN = 229376;   // 2 x 2 bits + 1 bit per position in 160 KB of LDS
-uint32_t pe_ploop_max_n() { return kPLoopMaxN; }
+// = 2 bits per position for each of the two outcome passes + 1 dependency bit,
+// in what the workgroup's 160 KB leave beside the kernel's static LDS (which
+// grows with the eviction width).
+constexpr uint32_t kPLoopMaxN = 229376;
+constexpr int kLdsPerWorkgroup = 160 * 1024;
 static size_t pe_ploop_lds_bytes(uint32_t n) { return (2u * ((n + 15u) / 16u) + (n + 31u) / 32u) * sizeof(uint32_t); }
+
+static const void* ploop_fn(int wi) {
+    return wi == 0 ? reinterpret_cast<const void*>(&pe::k_ploop<1>) : reinterpret_cast<const void*>(&pe::k_ploop<8>);
+}
+
+// dynamic LDS bytes the launch may use (0: none / no device)
+static int ploop_max_dyn(int wi) {
+    static int v[2] = {-1, -1};
+    if (v[wi] < 0) {
+        hipFuncAttributes fa;
+        if (hipFuncGetAttributes(&fa, ploop_fn(wi)) != hipSuccess) {
+            (void)hipGetLastError();
+            return 0;
+        }
+        const int d = kLdsPerWorkgroup - (int)fa.sharedSizeBytes;
+        v[wi] = d > 0 ? d : 0;
+    }
+    return v[wi];
+}
+
+uint32_t pe_ploop_max_n(uint32_t words) {
+    if (!evict_width_ok(words)) return 0;
+    const size_t d = (size_t)ploop_max_dyn(words == 1u ? 0 : 1);
+    uint32_t n = (uint32_t)std::min<size_t>(kPLoopMaxN, d * 8u / 5u) & ~31u;   // 5/8 byte per position
+    while (n && pe_ploop_lds_bytes(n) > d) n -= 32u;
+    return n;
+}
 
 hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st) {
     const uint32_t n = a->P.n_visit;
-    if (n == 0 || n > kPLoopMaxN || !evict_width_ok(a->P.mask_words)) return hipErrorInvalidValue;
+    if (n == 0 || n > pe_ploop_max_n(a->P.mask_words)) return hipErrorInvalidValue;
     static bool attr[2] = {false, false};
     const int wi = a->P.mask_words == 1u ? 0 : 1;
     if (!attr[wi]) {
-        const void* fn = wi == 0 ? reinterpret_cast<const void*>(&pe::k_ploop<1>)
-                                 : reinterpret_cast<const void*>(&pe::k_ploop<8>);
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)pe_ploop_lds_bytes(kPLoopMaxN));
+        const hipError_t e = hipFuncSetAttribute(ploop_fn(wi), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 ploop_max_dyn(wi));
         if (e != hipSuccess) return e;
         attr[wi] = true;
     }
