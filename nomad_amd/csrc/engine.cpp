@@ -2230,14 +2230,17 @@ bool task_port_reason(pe_stack* s, const TgPlan& g, uint32_t row, std::string* w
 // node (CSR-relative bits) that hold a needed port on the address the ask
 // takes, and whether anything that no preemption removes blocks one (a node
 // reservation, an invalid port, no address, an alloc of the job itself).
-static uint32_t port_blockers(pe_stack* s, const TgPlan& g, uint32_t row, bool* permanent) {
+// The blockers are returned as a list of up to 8 CSR-relative indices, one
+// byte each (0xFF ends it); *overflow when more allocs block.
+static uint64_t port_blockers(pe_stack* s, const TgPlan& g, uint32_t row, bool* permanent, bool* overflow) {
     *permanent = false;
+    *overflow = false;
     const bool task = g.rports.empty();
     uint32_t ip = PE_NONE;
     bool keyed = true;   // ReservedHostPorts apply (always for an address)
     if (task) {
         const HostNode& h = s->nodes[row];
-        if (h.n_device_nets == 0) return 0;
+        if (h.n_device_nets == 0) return ~0ull;
         ip = h.first_yield;
         keyed = ip == h.first_ipfield;
         if (row < s->node_addrs.size())
@@ -2245,11 +2248,11 @@ static uint32_t port_blockers(pe_stack* s, const TgPlan& g, uint32_t row, bool* 
     } else {
         if (row < s->node_addrs.size())
             for (const HostAddr& a : s->node_addrs[row]) if (a.alias == g.net_host) { ip = a.ip; break; }
-        if (ip == PE_NONE) { *permanent = true; return 0; }
+        if (ip == PE_NONE) { *permanent = true; return ~0ull; }
     }
     const auto& ports = task ? g.trports : g.rports;
     const uint32_t b = s->h_node_alloc_off[row], e = s->h_node_alloc_off[row + 1];
-    uint32_t mask = 0;
+    std::vector<uint32_t> blk;
     for (const auto& rp : ports) {
         if (rp.first < 0 || rp.first >= 65536) { *permanent = true; continue; }
         if (row < s->node_addrs.size())
@@ -2265,23 +2268,30 @@ static uint32_t port_blockers(pe_stack* s, const TgPlan& g, uint32_t row, bool* 
             for (uint32_t q = a.port_begin; q < a.port_end; q++)
                 holds = holds || (s->alloc_ports[q].first == ip && s->alloc_ports[q].second == rp.first);
             if (!holds) continue;
-            if ((a.job == s->job_id && a.ns == s->job_ns) || k - b >= 32) *permanent = true;
-            else mask |= 1u << (k - b);
+            if (a.job == s->job_id && a.ns == s->job_ns) *permanent = true;
+            else if (std::find(blk.begin(), blk.end(), k - b) == blk.end()) blk.push_back(k - b);
         }
     }
-    return mask;
+    if (blk.size() > 8) {
+        *overflow = true;
+        return ~0ull;
+    }
+    std::sort(blk.begin(), blk.end());
+    uint64_t list = ~0ull;
+    for (size_t i = 0; i < blk.size(); i++) list = (list & ~(0xFFull << (8 * i))) | ((uint64_t)blk[i] << (8 * i));
+    return list;
 }
 
 static void port_step(pe_stack* s, const TgPlan& g, uint32_t row, bool own_placed, uint64_t* list, uint8_t* info,
-                      uint32_t* blockers) {
+                      uint64_t* blockers) {
     *list = ~0ull;
     *info = 0;
-    *blockers = 0;
+    *blockers = ~0ull;
     const auto& ports = g.rports.empty() ? g.trports : g.rports;
     const uint32_t b = s->h_node_alloc_off[row], e = s->h_node_alloc_off[row + 1];
-    // the holder list and blocker bits index the node's first 32 allocs: a
-    // wider node's reserved-port preemption stays on the host path
-    if (e - b > (uint32_t)pe::kMaxNodeAllocs) { *info = pe::kPortUnsup; return; }
+    // the holder and blocker lists hold one-byte CSR-relative indices (the
+    // widest eviction width covers 256 allocs)
+    if (e - b > 255u) { *info = pe::kPortUnsup; return; }
     std::map<int32_t, uint32_t> holder;
     std::set<int32_t> filtered;
     for (uint32_t k = b; k < e; k++) {
@@ -2294,12 +2304,13 @@ static void port_step(pe_stack* s, const TgPlan& g, uint32_t row, bool own_place
             else filtered.insert(s->alloc_ports[q].second);
         }
     }
-    uint32_t n = 0, mask = 0;
+    uint32_t n = 0;
+    std::vector<bool> listed(e - b, false);
     for (const auto& rp : ports) {
         auto it = holder.find(rp.first);
         if (it != holder.end()) {
-            if (((mask >> it->second) & 1u) || n >= 8) { *info = pe::kPortUnsup; return; }
-            mask |= 1u << it->second;
+            if (listed[it->second] || n >= 8) { *info = pe::kPortUnsup; return; }
+            listed[it->second] = true;
             *list = (*list & ~(0xFFull << (8 * n))) | ((uint64_t)it->second << (8 * n));
             n++;
         } else if (filtered.count(rp.first)) {
@@ -2307,8 +2318,9 @@ static void port_step(pe_stack* s, const TgPlan& g, uint32_t row, bool own_place
             return;
         }
     }
-    bool permanent = false;
-    *blockers = port_blockers(s, g, row, &permanent);
+    bool permanent = false, overflow = false;
+    *blockers = port_blockers(s, g, row, &permanent, &overflow);
+    if (overflow) { *info = pe::kPortUnsup; return; }
     *info = (uint8_t)(n | ((own_placed || permanent) ? pe::kPortBlocked : 0u));
 }
 
@@ -2792,7 +2804,7 @@ int build_psets(pe_stack* s, TgPlan& g) {
     std::vector<const SpreadSpec*> specs;
     for (auto& sp : s->job_spreads) specs.push_back(&sp);
     for (auto& sp : g.spreads) specs.push_back(&sp);
-    if (specs.size() > (size_t)pe::kMaxPsets) { g.unsupported = "more than 8 spread stanzas"; return PE_OK; }
+    if (specs.size() > (size_t)pe::kMaxPsets) { g.unsupported = "more than 16 spread stanzas"; return PE_OK; }
     // computeSpreadInfo once per task group name; weights accumulate (spread.go:254)
     if (!s->spread_info_done.count(g.name)) {
         s->spread_info_done.insert(g.name);
@@ -2894,7 +2906,7 @@ int build_psets(pe_stack* s, TgPlan& g) {
     for (auto& c : s->job_constraints) if (c.op == "distinct_property") dps.emplace_back(&c, true);
     for (auto& c : g.distinct_props) dps.emplace_back(&c, false);
     if (g.psets.size() + dps.size() > (size_t)pe::kMaxPsets) {
-        g.unsupported = "more than 8 spread and distinct_property sets";
+        g.unsupported = "more than 16 spread and distinct_property sets";
         return PE_OK;
     }
     for (auto& dp : dps) {
@@ -3168,7 +3180,7 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         // PreemptForNetwork's reserved-port step per node, for Selects with Preempt
         std::vector<uint64_t> plist(n);
         std::vector<uint8_t> pinfo(n);
-        std::vector<uint32_t> pblock(n);
+        std::vector<uint64_t> pblock(n);
         for (uint32_t r = 0; r < (uint32_t)n; r++) port_step(s, g, r, own[r] != 0, &plist[r], &pinfo[r], &pblock[r]);
         HIP_TRY(s, upload_s(s, g.port_list, plist));
         HIP_TRY(s, upload_s(s, g.port_info, pinfo));
@@ -3191,7 +3203,7 @@ pe::TgTables tables_of(TgPlan& g) {
     t.task_gate = g.trports.empty() ? nullptr : g.task_gate.as<uint32_t>();
     t.port_list = has_static(g) ? g.port_list.as<uint64_t>() : nullptr;
     t.port_info = has_static(g) ? g.port_info.as<uint8_t>() : nullptr;
-    t.port_block = has_static(g) ? g.port_block.as<uint32_t>() : nullptr;
+    t.port_block = has_static(g) ? g.port_block.as<uint64_t>() : nullptr;
     t.coll_tg = g.coll_tg.as<uint32_t>();
     if (!g.dev_reqs.empty()) {
         t.dev_free = g.dev_free;

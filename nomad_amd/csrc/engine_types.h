@@ -7,7 +7,7 @@
 
 namespace pe {
 
-constexpr int kMaxPsets = 8;          // spread + distinct_property sets of a task group on the device
+constexpr int kMaxPsets = 16;         // spread + distinct_property sets of a task group on the device
 // Per-value tables (spread boosts, use counts) are laid out set after set
 // (TgTables::pset_tab_off / pset_cnt_off), so a set may hold any number of
 // values. Kernels stage them in LDS while they fit kLdsPsetValues entries in
@@ -94,7 +94,8 @@ struct TgTables {
     // indices, one byte each, ask order) and kPort* flags
     const uint64_t* port_list;
     const uint8_t* port_info;
-    const uint32_t* port_block;  // [n] or null: allocs (CSR-relative bits) holding a needed port on the ask's address
+    const uint64_t* port_block;  // [n] or null: allocs holding a needed port on the ask's address (up to 8
+                                 // CSR-relative indices, one byte each, 0xFF ends the list)
     int n_psets;                                 // spread property sets first, then distinct_property sets
     int n_spread;                                // psets [0, n_spread) score, [n_spread, n_psets) filter
     uint32_t pset_allowed[kMaxPsets];            // distinct_property: allowed use count per value

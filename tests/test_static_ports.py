@@ -279,3 +279,52 @@ def test_static_port_preemption_count_loop(task):
     assert_same_placements(re, ro)
     assert [sorted(x.preempted) for x in re] == [sorted(x.preempted) for x in ro]
     assert sum(1 for x in re if x.preempted) > 5
+
+
+def wide_port_cluster(n, seed):
+    """task_port_cluster's nodes with 36-70 small allocs each on the busy ones,
+    the static port's holder anywhere in the node's list (often past slot 32)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    ids = sorted(synth.uuids(n, seed))
+    nodes, allocs = [], []
+    for k, nid in enumerate(ids):
+        ip = "10.%d.%d.%d" % (k >> 16, (k >> 8) & 255, k & 255)
+        nd = _node(nid, [("default", ip, "")], reserved_host_ports=())
+        nd.networks = [NetworkResource(mode="host", device="eth0", cidr=ip + "/32", mbits=1000)]
+        nd.name = "node-%05d" % k
+        nd.compute_class()
+        nodes.append(nd)
+        m = int(rng.integers(36, 71)) if rng.random() < 0.85 else int(rng.integers(0, 4))
+        holder = int(rng.integers(0, m)) if m else -1
+        for q in range(m):
+            ports = []
+            if q == holder or rng.random() < 0.05:
+                ports = [(ip, int(rng.choice([8080, 8080, 443])))]
+            allocs.append(Allocation(node_id=nid, job_id="svc-%d" % (q % 9), task_group="web",
+                                     cpu_shares=3700 // max(m, 1), memory_mb=64, disk_mb=20,
+                                     priority=int(rng.choice([20, 30, 95], p=[0.45, 0.45, 0.1])),
+                                     net_mbits=int(rng.choice([5, 10, 20])), ports=ports))
+    return nodes, allocs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("task", [True, False])
+def test_static_port_preemption_on_wide_nodes(task):
+    """Static-port preemption on nodes of 36-70 allocs (the holder past slot 32
+    on most): the blocker list is indices, not the first 32 slots' bits.
+    Engine vs oracle, preempted sets included."""
+    from nomad_amd.structs import SchedulerConfig
+    nodes, allocs = wide_port_cluster(400, seed=91)
+    if task:
+        job = task_static_job([8080], mbits=30, count=150, priority=70, cpu=1500)
+    else:
+        job = static_job([8080], dyn=0, count=150)
+        job.priority = 70
+        job.task_groups[0].tasks[0].cpu = 1500
+    cfg = SchedulerConfig(preempt_service=True)
+    perm = synth.shuffle(len(nodes), 10)
+    _, _, ro = run_place(OracleGenericStack, nodes, allocs, job, perm, config=cfg)
+    _, _, re = run_place(_engine, nodes, allocs, job, perm, config=cfg)
+    assert_same_placements(re, ro)
+    assert [sorted(x.preempted) for x in re] == [sorted(x.preempted) for x in ro]
+    assert sum(1 for x in re if x.preempted and any(p >= 0 for p in x.preempted)) > 5

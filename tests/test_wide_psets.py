@@ -1,5 +1,5 @@
 """Property sets past the LDS tables: spread and
-distinct_property sets of any number of values and up to 8 sets per task
+distinct_property sets of any number of values and up to 16 sets per task
 group. propertySet (scheduler/propertyset.go:14-355) keeps an unbounded map
 of value -> count; SpreadIterator (spread.go:96-228) scores against it. The
 engine lays the per-value tables out set after set and keeps them in LDS while
@@ -121,3 +121,49 @@ def test_select_protocol_with_many_values():
             res.append((r.row, r.final_score, tuple(r.scores)))
         out.append(res)
     assert out[0] == out[1]
+
+
+def _many_meta(nodes, keys, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    for nd in nodes:
+        for k, card in keys:
+            nd.meta[k] = "v%d" % int(rng.integers(0, card))
+        nd.compute_class()
+
+
+def test_ten_sets_against_the_oracle():
+    """Five spreads and five distinct_property sets (10 > round 4's 8)."""
+    nodes, allocs = cluster(3000, seed=21, slots=400)
+    keys = [("p%d" % k, 3 + 2 * k) for k in range(8)]
+    _many_meta(nodes, keys, 22)
+    jb = job(80,
+             spreads=[Spread("${meta.p0}", 30), Spread("${meta.p1}", 20, [SpreadTarget("v1", 40)]),
+                      Spread("${meta.p2}", 20), Spread("${node.datacenter}", 15),
+                      Spread("${meta.unique.slot}", 15)],
+             constraints=[Constraint("${meta.p3}", "30", "distinct_property"),
+                          Constraint("${meta.p4}", "25", "distinct_property")],
+             tg_constraints=[Constraint("${meta.p5}", "20", "distinct_property"),
+                             Constraint("${meta.p6}", "15", "distinct_property"),
+                             Constraint("${meta.p7}", "12", "distinct_property")])
+    re = _both(nodes, allocs, jb, synth.shuffle(len(nodes), 7))
+    assert sum(1 for x in re if x.row >= 0) > 40
+
+
+def test_sixteen_sets_and_the_limit_past_them():
+    nodes, allocs = cluster(1500, seed=23)
+    keys = [("q%d" % k, 4 + k) for k in range(17)]
+    _many_meta(nodes, keys, 24)
+    spreads = [Spread("${meta.q%d}" % k, 5 + k) for k in range(8)]
+    dps = [Constraint("${meta.q%d}" % k, "40", "distinct_property") for k in range(8, 16)]
+    jb = job(40, spreads=spreads, constraints=dps)
+    re = _both(nodes, allocs, jb, synth.shuffle(len(nodes), 8))
+    assert sum(1 for x in re if x.row >= 0) > 20
+    # a 17th set is past the device tables: the engine says so
+    from nomad_amd.stack import Unsupported
+    jb17 = job(40, spreads=spreads, constraints=dps + [Constraint("${meta.q16}", "40", "distinct_property")])
+    st = _engine()
+    st.SetState(nodes, allocs)
+    st.SetJob(jb17)
+    st.SetNodes(list(synth.shuffle(len(nodes), 8)))
+    with pytest.raises(Unsupported):
+        st.Select(0)
