@@ -96,12 +96,17 @@ def dist_init():
         import torch.distributed as dist
         # CPU tensors (timing reductions) over gloo, GPU tensors (the shard
         # record all-gather) over RCCL / xGMI
+        import datetime
+        # a rank that fails inside a section (caught there) leaves the others in
+        # that section's next collective: they fail after 5 minutes instead of
+        # gloo's default 30
+        timeout = datetime.timedelta(minutes=5)
         if torch.cuda.is_available():
             local = local % max(1, torch.cuda.device_count())   # rehearsals with fewer GPUs than ranks
             torch.cuda.set_device(local)
-            dist.init_process_group("cpu:gloo,cuda:nccl")
+            dist.init_process_group("cpu:gloo,cuda:nccl", timeout=timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         pg = dist
     return rank, world, local, pg
 
