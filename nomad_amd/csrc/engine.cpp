@@ -5809,7 +5809,8 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
                              "%.1f (%llu calls)\n",
                      st[0], ms, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[6] / 100.0, h[7] / 100.0, h[4],
                      h[5], h[8] / 100.0, h[9], h[10] / 100.0, h[11]);
-        std::fprintf(stderr, "k_ploop resolves: %llu steps in %llu calls\n", h[12], h[13]);
+        std::fprintf(stderr, "k_ploop resolves: %llu steps in %llu calls; committed rows' plain re-evaluation %.1f us "
+                             "(%llu calls)\n", h[12], h[13], h[14] / 100.0, h[15]);
     }
     *handled = true;
     const uint32_t p = std::min(st[0], count);
