@@ -729,6 +729,7 @@ struct pe_stack {
     DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)
     DevMem d_pset_g, d_pset_gb;              // FULL k_place per-value tables beyond the LDS budget (batch: gb)  // device-resident parallel count loop (k_ploop)
     DevMem d_ploop_parts, d_ploop_nparts;   // k_ploop: Preempt records per position (parts, count)
+    DevMem d_fused_parts, d_fused_nparts;   // fused k_chain: first-phase score parts per position
     DevMem d_ploop_pparts, d_ploop_pnparts;   // k_ploop: plain records per position (parts, count)
 
     // Speculative count loop behind pe_select / pe_commit: the
@@ -3914,6 +3915,10 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         if (fused) {
             A.fused = 1;
             A.base1 = nullptr;   // later phases re-evaluate rows holding placements
+            HIP_TRY(s, s->d_fused_parts.ensure(sizeof(double) * PE_MAX_SCORES * std::max<size_t>(n, 1)));
+            HIP_TRY(s, s->d_fused_nparts.ensure(std::max<size_t>(n, 1)));
+            A.fused_parts = s->d_fused_parts.as<double>();
+            A.fused_nparts = s->d_fused_nparts.as<uint8_t>();
             if (s->counts_pending) {   // SetJob's counts ride in this launch
                 A.counts = s->pending_counts;
                 s->counts_pending = false;
@@ -4059,6 +4064,8 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
             }
             chain = false;
             A.fused = 0;
+            A.fused_parts = nullptr;
+            A.fused_nparts = nullptr;
             A.base = nullptr;
             A.base1 = nullptr;
             A.base_by_pos = 0;

@@ -138,6 +138,7 @@ struct ChainEmit {
     int32_t row;                  // winner, -1 = nil
     uint32_t dk;                  // placements of the launch on the row before this one
     uint32_t consumed, filtered, exhausted, new_offset;
+    uint32_t pos;                 // the winner's visit position, or PE_NONE (an exhausted stream's)
     double score;                 // FinalScore
 };
 
@@ -246,6 +247,12 @@ struct BatchArgs {
     uint32_t* done_flag;          // or null: k_emit's workgroup b stores done_seq to done_flag[b] (system scope)
     uint32_t done_seq;
     unsigned long long* prof;     // k_chain step clocks (PE_CHAIN_PROF), or null
+    // FUSED k_chain (or null): the score parts of every position's first-phase
+    // evaluation (PE_MAX_SCORES doubles and a count per visit position); a
+    // record whose row held no placement of the launch copies them instead of
+    // evaluating the row again
+    double* fused_parts;
+    uint8_t* fused_nparts;
     // k_chain scratch, kChainMaxN doubles per workgroup: the window's values
     // by relative position (one thread per Select walks its own positions)
     double* chain_vs;

@@ -1410,6 +1410,15 @@ __device__ __forceinline__ void build_emit_rec(const BatchArgs& A, const ChainEm
     for (int q = 0; q < PE_MAX_DEVICE_REQ; q++) o.device_offer_group[q] = 0;
     if (m.row < 0) return;
     const uint32_t row = (uint32_t)m.row;
+    if (A.fused_parts && m.dk == 0 && m.pos != PE_NONE && A.ask.n_dev == 0) {
+        // the row's first-phase evaluation (its state at the launch's start)
+        const uint32_t np = A.fused_nparts[m.pos];
+        o.final_score = m.score;
+        o.n_scores = np;
+        for (int q = 0; q < PE_MAX_SCORES; q++)
+            if (q < (int)np) o.scores[q] = A.fused_parts[(size_t)m.pos * PE_MAX_SCORES + q];
+        return;
+    }
     NodeIn in;
     load_node(A.soa, A.tg, row, in);
     NodeEval ev;
@@ -1563,6 +1572,22 @@ constexpr uint32_t kIdxBits = 14, kIdxMask = (1u << kIdxBits) - 1u;
 __device__ __noinline__ void chain_emit_full(const BatchArgs& A, Overlay ov, uint32_t e, uint32_t it, int win_row,
                                              double score, uint32_t consumed, uint32_t f, uint32_t x, uint32_t next_off) {
     emit_placement<false>(A, A.tg.class_ok, ov, nullptr, e, it, win_row, score, consumed, f, x, next_off);
+}
+
+// The FUSED first phase's evaluation of visit position p: its value, and its
+// score parts into A.fused_parts (the records of winners without an earlier
+// placement of the launch copy them)
+__device__ __noinline__ double chain_eval_parts(const BatchArgs& A, uint32_t row, uint32_t p) {
+    NodeIn in;
+    load_node(A.soa, A.tg, row, in);
+    NodeEval ev;
+    ev.score = 0.0;
+    eval_loaded<true, false>(A.soa, A.tg, A.tg.class_ok, A.ask, 0u, A.penalty_bits, A.log10, nullptr, row, in, &ev);
+    if (ev.status == kOption) {
+        A.fused_nparts[p] = (uint8_t)ev.nscores;
+        for (int q = 0; q < PE_MAX_SCORES; q++) A.fused_parts[(size_t)p * PE_MAX_SCORES + q] = ev.parts[q];
+    }
+    return encode_eval(ev);
 }
 
 // value of (row, placements) re-evaluated: the k_base pipeline with dk placements
@@ -1818,7 +1843,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                             } else {
                                 r = perm[p];
                             }
-                            v = chain_reeval(Ak, r, 0u);
+                            v = A.fused_parts ? chain_eval_parts(Ak, r, p) : chain_reeval(Ak, r, 0u);
                             A.base[p] = v;
                         } else {
                             const double* src = ((one_mask >> q) & 1u) ? A.base1 : A.base;
@@ -2149,6 +2174,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     if (A.emit) {
                         ChainEmit& m = A.emit[it];
                         m.row = win_row;
+                        m.pos = wrap_pos(cur + sh.sel_pos[s], n);
                         m.dk = ov_count(ov, (uint32_t)win_row);
                         m.consumed = consumed;
                         m.filtered = sh.sel_f[s];
@@ -2195,6 +2221,7 @@ __global__ void __launch_bounds__(kChainBlock) k_chain(BatchArgs A, uint32_t n_e
                     if (A.emit) {
                         ChainEmit& m = A.emit[placed];
                         m.row = win_row;
+                        m.pos = PE_NONE;
                         m.dk = win_row >= 0 ? ov_count(ov, (uint32_t)win_row) : 0u;
                         m.consumed = n;
                         m.filtered = sh.sel_f[0];
