@@ -204,7 +204,7 @@ def cpu_baseline(nodes, allocs, job, seconds):
 # Scoring sweep bytes per node (pe_last_sweep_bytes): 64 B NodeRec + 4 B folded
 # score word (verdict, affinity index, spread values; 1 B verdict when the word
 # does not apply: 73 B) + 4 B (job,tg) collisions + 4 B visit rank = 76 B.
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04", "sweep_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "sweep_traffic.json")
 CHAIN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "c2_batch_traffic.json")
 PLAN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "plan_traffic.json")
 
@@ -233,7 +233,7 @@ def chain_traffic(evals_per_launch):
     return t["bytes_per_launch"]
 
 
-HEADLINE_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04", "headline_traffic.json")
+HEADLINE_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "headline_traffic.json")
 
 
 def headline_traffic(node_evals):
@@ -1153,6 +1153,8 @@ def main():
     extra = {}
     for sec in sections:
         gc.collect()
+        if rank == 0:
+            print("bench: section %s" % sec, file=sys.stderr, flush=True)
         try:
             if sec in ("c3", "c5"):
                 if rank == 0:

@@ -2,7 +2,10 @@
 # HBM traffic of the headline evaluation's device work (k_base + k_chain, the
 # bench line's roofline kernel): FETCH_SIZE and WRITE_SIZE in separate
 # rocprofv3 passes over the default bench loop, combined per evaluation by
-# tools/pmc_traffic.py (gfx950 FETCH_SIZE x 2 correction). Writes
+# tools/pmc_traffic.py with the per-pattern FETCH_SIZE factors measured by
+# tools/fetch_calib.hip (profiles/r04/fetch_calib_10000.json: k_base gathers
+# 64-B records, counted 0.927 of their bytes -> x 1.079; k_chain reads 8-B
+# values by position, counted 0.628 -> x 1.592). Writes
 # gpurun_out/headline_pmc/headline_traffic.json.
 set -eo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -18,8 +21,8 @@ cd "$ROOT"
 F=$(find "$OUT/fetch" -name "*counter_collection.csv" -print -quit)
 W=$(find "$OUT/write" -name "*counter_collection.csv" -print -quit)
 EV=$(python3 -c "import json;print(int(json.load(open('$OUT/f.json'))['roofline']['node_evals_per_launch']))")
-python3 tools/pmc_traffic.py "$F" "$W" "k_chain" "$EV" 60 "$OUT/chain.json" > /dev/null
-python3 tools/pmc_traffic.py "$F" "$W" "k_base" 10000 60 "$OUT/base.json" > /dev/null
+python3 tools/pmc_traffic.py "$F" "$W" "k_chain" "$EV" 60 "$OUT/chain.json" 1.592 > /dev/null
+python3 tools/pmc_traffic.py "$F" "$W" "k_base" 10000 60 "$OUT/base.json" 1.079 > /dev/null
 python3 - "$OUT" "$EV" <<'PY'
 import json, sys
 out, ev = sys.argv[1], int(sys.argv[2])
@@ -29,7 +32,10 @@ t = {"kernel": "k_base + k_chain", "node_evals": ev, "bytes_per_node_eval": 60,
      "bytes_per_launch": c["bytes_per_launch"] + b["bytes_per_launch"],
      "k_chain_bytes": c["bytes_per_launch"], "k_base_bytes": b["bytes_per_launch"],
      "algorithmic_bytes_per_launch": ev * 60,
-     "dispatches": [c["dispatches"], b["dispatches"]], "correction": c["correction"]}
+     "dispatches": [c["dispatches"], b["dispatches"]],
+     "k_chain_fetch_factor": c["fetch_factor"], "k_base_fetch_factor": b["fetch_factor"],
+     "correction": "FETCH_SIZE x factor calibrated per access pattern (tools/fetch_calib.hip, "
+                   "profiles/r04/fetch_calib_10000.json), WRITE_SIZE as is"}
 t["traffic_over_algorithmic"] = t["bytes_per_launch"] / t["algorithmic_bytes_per_launch"]
 open(out + "/headline_traffic.json", "w").write(json.dumps(t, indent=1) + "\n")
 print(json.dumps(t, indent=1))
