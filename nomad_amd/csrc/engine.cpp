@@ -4880,6 +4880,7 @@ struct ScoreHeap {
         return i > i0;
     }
     void push(ScoreMeta m) {   // heap.Push → ScoreHeap.Push (+ heap.Fix) then up(len-1)
+        if (items.capacity() < cap) items.reserve(cap);
         if (items.size() < cap) {
             items.push_back(std::move(m));
         } else if (m.norm > items[0].norm) {
@@ -4902,19 +4903,34 @@ struct ScoreHeap {
     }
 };
 
+// One AllocMetric map (string -> count) as it fills: a Select's maps hold a
+// handful of keys, so a short vector searched in place (no allocation once a
+// key is in) and sorted by key when written out (Go's map keys in order)
+struct MetricCounts {
+    std::vector<std::pair<std::string, int>> kv;
+    void add(std::string_view k) {
+        for (auto& e : kv)
+            if (e.first == k) {
+                e.second++;
+                return;
+            }
+        kv.emplace_back(std::string(k), 1);
+    }
+};
+
 // The maps of one Select as they fill (FilterNode / ExhaustedNode, ScoreNode).
 struct MetricAcc {
-    std::map<std::string, int> cf, kf, ce, de;
+    MetricCounts cf, kf, ce, de;
     ScoreHeap heap;
-    void filter(pe_stack* s, uint32_t row, const std::string& why) {
+    void filter(pe_stack* s, uint32_t row, std::string_view why) {
         const uint32_t nc = s->nodes[row].node_class;
-        if (nc != PE_NONE && !s->S(nc).empty()) cf[s->S(nc)]++;
-        if (!why.empty()) kf[why]++;
+        if (nc != PE_NONE && !s->S(nc).empty()) cf.add(s->S(nc));
+        if (!why.empty()) kf.add(why);
     }
-    void exhaust(pe_stack* s, uint32_t row, const std::string& dim) {
+    void exhaust(pe_stack* s, uint32_t row, std::string_view dim) {
         const uint32_t nc = s->nodes[row].node_class;
-        if (nc != PE_NONE && !s->S(nc).empty()) ce[s->S(nc)]++;
-        if (!dim.empty()) de[dim]++;
+        if (nc != PE_NONE && !s->S(nc).empty()) ce.add(s->S(nc));
+        if (!dim.empty()) de.add(dim);
     }
 };
 
@@ -5046,17 +5062,25 @@ static int metrics_outcome(pe_stack* s, TgPlan& g, const pe::Ask& a, uint32_t ro
     return PE_OK;
 }
 
-// pe_last_metrics' text of one Select's maps.
-static std::string metrics_text(pe_stack* s, MetricAcc& acc) {
-    std::string out;
-    auto put = [&](const char* k, const std::map<std::string, int>& mm) {
-        for (auto& kv : mm) out += std::string(k) + "\t" + kv.first + "\t" + std::to_string(kv.second) + "\n";
+// pe_last_metrics' text of one Select's maps, appended to `out`.
+static void metrics_text_into(pe_stack* s, MetricAcc& acc, std::string& out) {
+    char num[64];
+    auto put = [&](const char* k, MetricCounts& mm) {
+        std::sort(mm.kv.begin(), mm.kv.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        for (auto& kv : mm.kv) {
+            out += k;
+            out += '\t';
+            out += kv.first;
+            out += '\t';
+            const auto r = std::to_chars(num, num + sizeof num, kv.second);
+            out.append(num, r.ptr);
+            out += '\n';
+        }
     };
     put("CF", acc.cf); put("KF", acc.kf); put("CE", acc.ce); put("DE", acc.de);
     // ScoreMetaData (PopulateScoreMetaData): "SM\trank\tnode id\tnorm\tname=value,..."
     // (shortest round-trip decimal: the same doubles when parsed back)
     auto items = acc.heap.reverse_items();
-    char num[64];
     auto put_num = [&](double x) {
         const auto r = std::to_chars(num, num + sizeof num, x);
         out.append(num, r.ptr);
@@ -5079,6 +5103,11 @@ static std::string metrics_text(pe_stack* s, MetricAcc& acc) {
         }
         out += '\n';
     }
+}
+
+static std::string metrics_text(pe_stack* s, MetricAcc& acc) {
+    std::string out;
+    metrics_text_into(s, acc, out);
     return out;
 }
 
@@ -5260,6 +5289,7 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     }
     const double t2 = prof ? now_us() : 0.0;
     sp.mtext.clear();
+    sp.mtext.reserve((size_t)sp.n_rec * 800u);
     sp.mtext_off.assign(1, 0u);
     std::map<int, std::vector<uint32_t>> counts;
     size_t i = 0;
@@ -5268,7 +5298,7 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
             const int rc = metrics_outcome(s, g, a, rows[i], codes[i], &sc[i * 6], acc[k], counts);
             if (rc) return rc;
         }
-        sp.mtext += metrics_text(s, acc[k]);
+        metrics_text_into(s, acc[k], sp.mtext);
         sp.mtext_off.push_back((uint32_t)sp.mtext.size());
     }
     sp.metrics = true;

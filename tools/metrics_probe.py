@@ -1,0 +1,31 @@
+"""AllocMetric-on drop-in probe (GPU box): the headline caller loop (C2, 10k
+nodes, count 1000) with pe_set_metrics on and the maps copied out by the
+caller; per evaluation wall time, and with PE_METRICS_PROF=1 the speculative
+run's metric phases (host walk, k_trace, maps + text)."""
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+from nomad_amd import synth  # noqa: E402
+from nomad_amd.stack import GenericStack  # noqa: E402
+from tools import dropin  # noqa: E402
+
+n, count = 10000, 1000
+nodes, allocs = synth.cluster_c2(n, seed=42)
+job = synth.job_c2(count)
+orders = np.stack([synth.shuffle(n, 1000 + e) for e in range(8)])
+st = GenericStack()
+st.SetState(nodes, allocs)
+st.EnableMetrics(True)
+dropin.use_metrics(True)
+caller = dropin.prepare(st, job)
+caller(orders, count, n_evals=1)
+for i in range(4):
+    dropin.phase_seconds(reset=True)
+    t0 = time.perf_counter()
+    placed, ne, _, _, _ = caller(orders, count, n_evals=2)
+    dt = time.perf_counter() - t0
+    ph = dropin.phase_seconds(reset=True)
+    print("%.3f ms per evaluation" % (dt / ne * 1e3), {k: round(v / ne * 1e3, 3) for k, v in ph.items()}, flush=True)
