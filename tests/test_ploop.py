@@ -142,3 +142,22 @@ def test_ploop_skipped_plain_resolves_fail(variant, monkeypatch):
     monkeypatch.setenv("PE_PLOOP_CHECK_DEAD", "1")
     re, _ = _run_both(nodes, allocs, job, perm, SchedulerConfig(preempt_service=True))
     assert sum(1 for x in re if x.preempted) > 20
+
+
+def test_ploop_near_the_lds_limit():
+    """A list near the largest k_ploop takes (its codes fill the LDS the kernel's
+    static use leaves, pe_ploop_max_n): the device loop against the host-driven
+    loop of the same engine."""
+    nodes, allocs = synth.cluster_c5(220000, seed=31, busy=1.0)
+    job = synth.job_c5(60)
+    perm = synth.shuffle(len(nodes), 6)
+    cfg = SchedulerConfig(preempt_service=True)
+    _, _, dev = run_place(_engine, nodes, allocs, job, perm, config=cfg)
+    os.environ["PE_PLOOP"] = "0"
+    try:
+        _, _, host = run_place(_engine, nodes, allocs, job, perm, config=cfg)
+    finally:
+        del os.environ["PE_PLOOP"]
+    assert_same_placements(dev, host)
+    assert [sorted(x.preempted) for x in dev] == [sorted(x.preempted) for x in host]
+    assert sum(1 for x in dev if x.preempted) > 10
