@@ -148,8 +148,8 @@ def test_ploop_near_the_lds_limit():
     """A list near the largest k_ploop takes (its codes fill the LDS the kernel's
     static use leaves, pe_ploop_max_n): the device loop against the host-driven
     loop of the same engine."""
-    nodes, allocs = synth.cluster_c5(220000, seed=31, busy=1.0)
-    job = synth.job_c5(60)
+    nodes, allocs = synth.cluster_c5(220000, seed=31, busy=0.999)
+    job = synth.job_c5(200)
     perm = synth.shuffle(len(nodes), 6)
     cfg = SchedulerConfig(preempt_service=True)
     _, _, dev = run_place(_engine, nodes, allocs, job, perm, config=cfg)
