@@ -81,7 +81,7 @@ def parse():
     p.add_argument("--sweep-nodes", type=int, default=1 << 24,
                    help="nodes of the scoring-sweep roofline measurement (0 = skip)")
     p.add_argument("--sections", default="c1,c2_100k,c2_batch,c2_workers,c3,c4,c4_drop_in,c5,c3_sharded,c3_sharded_1m,"
-                                         "plan_apply,ingest",
+                                         "plan_apply,ingest,multi_loopback",
                    help="comma list of extra config sections (empty = none)")
     return p.parse_args()
 
@@ -680,6 +680,41 @@ def section_c3_sharded(device, rank, world, pg, placements=256, host_placements=
     return out
 
 
+def section_multi_loopback(device, n=20000, count=200):
+    """One handle over N devices (pe_config.device_ids) in the
+    loopback mode where every id names this GPU: the full-pass count loop of a
+    C3 job split over N replicas, per placement N k_sweep launches, the slices
+    copied between the replicas and N k_sweep_step launches, all issued from
+    the caller's thread. The wall time per placement at N = 8 is the host
+    cost of that launch sequence (the device work per launch is small)."""
+    from nomad_amd import synth
+    from nomad_amd.stack import GenericStack
+    nodes, allocs = synth.cluster_c3(n, seed=7)
+    job = synth.job_c3(count)
+    perm = synth.shuffle(len(nodes), 23)
+    out = {"workload": "C3 job count=%d on %d nodes, full pass, one handle over N loopback devices" % (count, n)}
+    for nd in (1, 2, 8):
+        st = GenericStack(devices=[device] * nd) if nd > 1 else GenericStack(device=device)
+        st.SetState(nodes, allocs)
+        walls = []
+        for i in range(3):
+            st.ResetPlan()
+            st.SetJob(job)
+            st.SetNodes(perm)
+            t0 = time.perf_counter()
+            _, _, placed, _ = st.PlaceArrays(0, count)
+            walls.append(time.perf_counter() - t0)
+        x = st.last_exchange_us()
+        st.close()
+        wall = float(np.median(walls[1:]))
+        out["n%d" % nd] = {"placements": int(placed), "ms_per_placement": wall / max(1, placed) * 1e3,
+                           "exchange_us_per_placement": x}
+    out["note"] = ("loopback: the N replicas share one GPU, so N > 1 adds launches and copies but no devices; "
+                   "n8.ms_per_placement - n1.ms_per_placement is the per-placement host cost of driving 8 replicas "
+                   "from one thread")
+    return out
+
+
 def section_ingest(device, n=100000, reps=5):
     """Snapshot ingest: a full pe_set_state of an n-node
     cluster against pe_update_allocs of a state-store delta (10 % of the allocs
@@ -1189,6 +1224,9 @@ def main():
             elif sec == "ingest":
                 if rank == 0:
                     extra[sec] = section_ingest(local)
+            elif sec == "multi_loopback":
+                if rank == 0:
+                    extra[sec] = section_multi_loopback(local)
         except Exception as e:   # an extra section never takes the headline line down
             extra[sec] = {"error": "%s: %s" % (type(e).__name__, e)}
         barrier(pg)
