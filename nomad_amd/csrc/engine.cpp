@@ -5848,6 +5848,9 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
                      h[5], h[8] / 100.0, h[9], h[10] / 100.0, h[11]);
         std::fprintf(stderr, "k_ploop resolves: %llu steps in %llu calls; committed rows' plain re-evaluation %.1f us "
                              "(%llu calls)\n", h[12], h[13], h[14] / 100.0, h[15]);
+        std::fprintf(stderr, "k_ploop winner detail us: record staging %.1f, plain eval + bookkeeping %.1f, end "
+                             "barrier %.1f, plain winner records %.1f (%llu)\n",
+                     h[17] / 100.0, h[18] / 100.0, h[19] / 100.0, h[20] / 100.0, h[21]);
     }
     *handled = true;
     const uint32_t p = std::min(st[0], count);

@@ -400,8 +400,10 @@ struct PLoopArgs {
     uint32_t* nil_out;
     uint32_t* state;                  // [0] placements, [1] cursor, [2] error (1: node outside the device limits,
                                       // 2: winner not an option, 3: a skipped plain resolve had a winner), [3] records
-    unsigned long long* prof;         // [6] or null (PE_PLACE_PROF): wall-clock ticks of the plain resolve, refresh,
+    unsigned long long* prof;         // [24] or null (PE_PLACE_PROF): wall-clock ticks of the plain resolve, refresh,
                                       // Preempt resolve, winner; refreshed dirty rows, refreshed pcount readers
+                                      // ([6..15] winner record, commit, probes, resolve steps, plain re-evaluation;
+                                      // [17..21] the winner section's parts)
 };
 
 struct SystemArgs {

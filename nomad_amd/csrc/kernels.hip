@@ -2504,33 +2504,36 @@ __global__ void __launch_bounds__(256) k_census(BatchArgs A, uint32_t* counts, u
 template <bool kCores = true>
 __device__ __forceinline__ void commit_row(const NodeSoA& s, const TgTables& t, const Ask& a, uint32_t row,
                                            uint32_t offers) {
+    // Every load before the first store: the counters share types with the
+    // record's fields, so a load placed after a store is issued only once the
+    // store's own load has returned, one HBM round trip per field.
     NodeRec& r = s.rec[row];
-    if (kCores) {
-        r.used_cpu += ask_cpu(s, a, row);
-        core_take(s, a, row, 1);
-    } else {
-        r.used_cpu += a.cpu;
-    }
-    r.used_mem += a.mem;
-    r.used_disk += a.disk;
-    r.used_mbits += a.commit_mbits;
-    r.used_dyn += a.commit_dyn;
-    s.coll_job[row] += 1;
-    t.coll_tg[row] += 1;
-    const uint32_t c = r.cls;
+    const int64_t cpu = r.used_cpu, mem = r.used_mem, disk = r.used_disk;
+    const int32_t mbits = r.used_mbits, dyn = r.used_dyn;
+    const uint32_t c = r.cls, cj = s.coll_job[row], ct = t.coll_tg[row];
+    const uint32_t fr0 = a.n_dev > 0 ? t.dev_free[row] : 0u;
+    const int64_t ac = kCores ? ask_cpu(s, a, row) : a.cpu;
+    uint32_t fr = fr0;
     if (a.n_dev > 0) {
         if (offers == 0xFFFFFFFFu) {
-            t.dev_free[row] = dev_after(a, t.dev_cls[c], t.dev_free[row], 1);
+            fr = dev_after(a, t.dev_cls[c], fr0, 1);
         } else {
-            uint32_t fr = t.dev_free[row];
             for (int q = 0; q < kMaxDevReq && q < a.n_dev; q++) {
                 const uint32_t g = (offers >> (8 * q)) & 255u, f = (fr >> (8 * g)) & 255u;
                 const uint32_t cnt = (uint32_t)a.dev_cnt[q];
                 fr -= (cnt < f ? cnt : f) << (8 * g);
             }
-            t.dev_free[row] = fr;
         }
     }
+    r.used_cpu = cpu + ac;
+    r.used_mem = mem + a.mem;
+    r.used_disk = disk + a.disk;
+    r.used_mbits = mbits + a.commit_mbits;
+    r.used_dyn = dyn + a.commit_dyn;
+    s.coll_job[row] = cj + 1u;
+    t.coll_tg[row] = ct + 1u;
+    if (a.n_dev > 0) t.dev_free[row] = fr;
+    if (kCores) core_take(s, a, row, 1);
     for (int p = 0; p < t.n_psets; p++) {
         const uint32_t v = pset_value(t, p, row, c);
         if (v != kMissing) t.pset_counts[p][v] += 1;
