@@ -126,7 +126,8 @@ def rccl_libraries():
             path = ln.split()[-1] if len(ln.split()) >= 6 else ""
             if "librccl" in path:
                 mapped.add(os.path.realpath(path))
-    return {"engine": os.path.realpath(engine) if engine else "", "mapped": sorted(mapped)}
+    path, _, ver = engine.partition(" (RCCL ")   # "<path> (RCCL x.y.z)"
+    return {"engine": os.path.realpath(path) if path else "", "version": ver.rstrip(")"), "mapped": sorted(mapped)}
 
 
 def barrier(pg):
@@ -1015,6 +1016,42 @@ def section_c2_workers(device, nodes, allocs, job, count, workers, seconds=3.0):
             "workers": workers, "placements_per_s": placed / wall, "evals": sum(r[1] for r in res)}
 
 
+_RATE_KEYS = ("placements_per_s", "nodes_per_s", "plan_nodes_per_s", "value")
+
+
+def summary(line):
+    """One short entry per section (its rate, the CPU baseline's, the roofline
+    fraction, AllocMetric-on rate), so the figures survive a truncated tail."""
+    def g3(x):
+        return float("%.3g" % x) if isinstance(x, (int, float)) else x
+
+    def rate(d):
+        for k in _RATE_KEYS:
+            if isinstance(d.get(k), (int, float)):
+                return g3(d[k])
+        return None
+
+    out = {"c2": rate(line), "c2_cpu": rate(line.get("cpu_baseline", {})),
+           "c2_frac": g3(line.get("roofline", {}).get("frac")),
+           "c2_metrics_on": rate(line.get("metrics_on", {})),
+           "sweep_frac": g3(line.get("sweep_roofline", {}).get("frac"))}
+    for k, d in line.get("configs", {}).items():
+        if not isinstance(d, dict):
+            continue
+        if "error" in d:
+            out[k] = "error"
+            continue
+        e = [rate(d)]
+        if isinstance(d.get("cpu_baseline"), dict):
+            e.append(rate(d["cpu_baseline"]))
+        if isinstance(d.get("roofline"), dict) and "frac" in d["roofline"]:
+            e.append("f%.3g" % d["roofline"]["frac"])
+        if isinstance(d.get("metrics_on"), dict):
+            e.append("m%.3g" % (rate(d["metrics_on"]) or 0.0))
+        out[k] = e if len(e) > 1 else e[0]
+    return out
+
+
 def main():
     args = parse()
     # The harness holds millions of Python objects (clusters, oracle state) by
@@ -1189,7 +1226,7 @@ def main():
     for sec in sections:
         gc.collect()
         if rank == 0:
-            print("bench: section %s" % sec, file=sys.stderr, flush=True)
+            print("s:%s" % sec, file=sys.stderr, flush=True)   # progress, kept short (driver tail)
         try:
             if sec in ("c3", "c5"):
                 if rank == 0:
@@ -1233,6 +1270,7 @@ def main():
     if rank == 0:
         line["configs"] = extra
         line["rccl"] = rccl_libraries()
+        line["summary"] = summary(line)   # last: the driver's 2000-char tail shows it
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     if pg is not None:

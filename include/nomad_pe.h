@@ -368,7 +368,9 @@ uint32_t pe_device_count(const pe_stack* s);
 int pe_comm_unique_id(uint8_t* out, size_t cap);
 /* The RCCL library the collectives call, bound at first use: the one the
  * process already has mapped (soname librccl.so.1, e.g. torch's), else
- * /opt/rocm/lib/librccl.so.1; "" when none loads. */
+ * /opt/rocm/lib/librccl.so.1, followed by " (RCCL major.minor.patch)"; ""
+ * when none loads or its major version differs from the rccl.h the engine is
+ * built against (the communicator calls then fail with that reason). */
 const char* pe_comm_library(void);
 int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id);
 /* The full-pass count loop (task groups with affinities / spreads, limit >=

@@ -57,7 +57,9 @@ struct RcclApi {
     decltype(&ncclGroupStart) GroupStart = nullptr;
     decltype(&ncclGroupEnd) GroupEnd = nullptr;
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
-    std::string path;
+    decltype(&ncclGetVersion) GetVersion = nullptr;
+    std::string path;     // the library in use, with its version
+    std::string error;    // why it was refused
     bool ok = false;
 };
 
@@ -79,12 +81,30 @@ const RcclApi& rccl() {
         PE_RCCL_SYM(GroupStart);
         PE_RCCL_SYM(GroupEnd);
         PE_RCCL_SYM(GetErrorString);
+        PE_RCCL_SYM(GetVersion);
 #undef PE_RCCL_SYM
         api.ok = api.GetUniqueId && api.CommInitRank && api.CommInitAll && api.AllGather && api.CommDestroy &&
-                 api.GroupStart && api.GroupEnd && api.GetErrorString;
+                 api.GroupStart && api.GroupEnd && api.GetErrorString && api.GetVersion;
         Dl_info info;
         if (api.GetUniqueId && dladdr(reinterpret_cast<void*>(api.GetUniqueId), &info) && info.dli_fname)
             api.path = info.dli_fname;
+        // The engine is compiled against /opt/rocm's rccl.h: the enums, the
+        // 128-byte ncclUniqueId and the calls it uses are fixed within a major
+        // version (the torch-bundled copy is usually a minor version apart).
+        // Another major version is refused, and the version is reported.
+        int ver = 0;
+        if (api.ok && api.GetVersion(&ver) != ncclSuccess) ver = 0;
+        const int major = ver >= 10000 ? ver / 10000 : ver / 1000;
+        const int minor = ver >= 10000 ? (ver / 100) % 100 : (ver / 100) % 10;
+        if (api.ok && major != NCCL_MAJOR) {
+            api.ok = false;
+            api.error = "RCCL " + std::to_string(major) + "." + std::to_string(minor) + " at " + api.path +
+                        ": the engine is built against RCCL " + std::to_string(NCCL_MAJOR) + "." +
+                        std::to_string(NCCL_MINOR);
+        } else if (!api.ok) {
+            api.error = "RCCL library unavailable (dlopen librccl.so.1 failed or a symbol is missing)";
+        }
+        if (ver) api.path += " (RCCL " + std::to_string(major) + "." + std::to_string(minor) + "." + std::to_string(ver % 100) + ")";
     });
     return api;
 }
@@ -106,7 +126,7 @@ ncclResult_t rc_CommDestroy(ncclComm_t c) { return rccl().ok ? rccl().CommDestro
 ncclResult_t rc_GroupStart() { return rccl().ok ? rccl().GroupStart() : ncclSystemError; }
 ncclResult_t rc_GroupEnd() { return rccl().ok ? rccl().GroupEnd() : ncclSystemError; }
 const char* rc_GetErrorString(ncclResult_t r) {
-    return rccl().ok ? rccl().GetErrorString(r) : "RCCL library unavailable (dlopen librccl.so.1 failed)";
+    return rccl().ok ? rccl().GetErrorString(r) : rccl().error.c_str();
 }
 }  // namespace
 
@@ -767,6 +787,9 @@ struct pe_stack {
         std::vector<MemoDelta> memo_log;
         std::vector<uint32_t> memo_off;
         std::vector<int8_t> memo_job0, memo_tg0;
+        // an evicting run frees the evicted allocs' reserved cores (host mirror
+        // and d_core_used): the run's starting used sets, for the rollback
+        std::vector<uint64_t> core_used0;
     } spec;
     // place_impl with the Preempt retry: per placement, the plain nil Select
     // the retry followed (nodes evaluated / filtered / exhausted, cursor;
@@ -774,7 +797,7 @@ struct pe_stack {
     std::vector<std::array<uint32_t, 4>>* nil_sink = nullptr;
     DevMem d_ploop_nil;
     DevMem d_trace_dk;                 // spec_metrics: per traced row, the earlier records' placements
-    DevMem ck_preempted, ck_pcount;
+    DevMem ck_preempted, ck_pcount, ck_core_used;
     std::vector<pe::EmitRec>* emit_sink = nullptr;   // run_place: keep chain records compact here
     bool emit_sunk = false;                          // ... and it did
     pe_spec_view sview{};              // the run's records for caller-served Selects (pe_spec_view_get)
@@ -6286,6 +6309,12 @@ static int spec_copy(pe_stack* s, TgPlan& g, bool to_ckpt) {
     if (s->spec.evict) {   // Plan.NodePreemptions: the preempted flags and the per-(job, tg) counts
         HIP_TRY(s, cp(s->d_preempted, s->ck_preempted, s->h_preempted.size()));
         HIP_TRY(s, cp(s->d_pcount, s->ck_pcount, sizeof(uint32_t) * std::max<uint32_t>(s->n_jtg_keys, 1)));
+        // evictions free the evicted allocs' reserved cores (apply_preempt)
+        if (s->has_cores) {
+            HIP_TRY(s, cp(s->d_core_used, s->ck_core_used, sizeof(uint64_t) * 4 * n));
+            if (to_ckpt) s->spec.core_used0 = s->h_core_used;
+            else if (s->spec.core_used0.size() == s->h_core_used.size()) s->h_core_used = s->spec.core_used0;
+        }
     }
     return PE_OK;
 }
@@ -6328,6 +6357,7 @@ static int spec_rollback_evict(pe_stack* s, uint32_t conf) {
         const size_t at = masks.size();
         masks.resize(at + words, 0u);
         for (uint32_t j = 0; j < spec_rec_npre(sp, k); j++) {
+            core_hold(s, spec_rec_pre(sp, k)[j], false);   // the confirmed eviction's cores stay free
             const uint32_t q = s->alloc_slot[spec_rec_pre(sp, k)[j]] - b;
             if (q >= 32u * words) return s->fail(PE_EINTERNAL, "replayed preemption past the eviction width");
             masks[at + (q >> 5)] |= 1u << (q & 31u);
@@ -6466,7 +6496,8 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     // other loop pays per placement: start with one and double while the runs
     // get used up (spec_flush).
     count = spec_chain_path(s, g) ? std::max<uint32_t>(count, 1u) : std::max<uint32_t>(std::min(count, sp.grow), 1u);
-    count = std::min<uint32_t>(count, 1u << 16);
+    // (with AllocMetric on, spec_metrics counts a row's earlier placements in 16 bits)
+    count = std::min<uint32_t>(count, s->metrics_on ? 0xFFFFu : 1u << 16);
     // With preemption enabled the run is selectNextOption's loop (generic_sched.go:
     // 773-792): a nil plain Select retried with Preempt=true, whose placement
     // evicts (§25). Evictions are not undone by subtraction: checkpoint.
@@ -6568,6 +6599,7 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
         if (mrc) {   // nothing served yet: the device and the memo go back to the run's start
             sp.active = true;
             sp.served = sp.confirmed = 0;
+            sp.metrics = true;   // spec_metrics set memo_job0 / memo_tg0 / memo_off first: rewind to them
             spec_memo_rewind(s, 0);
             sp.metrics = false;
             (void)spec_flush(s);

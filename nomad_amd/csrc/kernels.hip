@@ -3910,26 +3910,44 @@ hipError_t pe_launch_sweep_loop(const pe::SweepArgs* a, uint32_t blocks, uint32_
 // in what the workgroup's 160 KB leave beside the kernel's static LDS (which
 // grows with the eviction width).
 constexpr uint32_t kPLoopMaxN = 229376;
-constexpr int kLdsPerWorkgroup = 160 * 1024;
 static size_t pe_ploop_lds_bytes(uint32_t n) { return (2u * ((n + 15u) / 16u) + (n + 31u) / 32u) * sizeof(uint32_t); }
 
 static const void* ploop_fn(int wi) {
     return wi == 0 ? reinterpret_cast<const void*>(&pe::k_ploop<1>) : reinterpret_cast<const void*>(&pe::k_ploop<8>);
 }
 
-// dynamic LDS bytes the launch may use (0: none / no device)
+// The current device's LDS per workgroup (the opt-in limit where it reports
+// one, else the default limit): 160 KB on gfx950.
+static int lds_per_workgroup(int dev) {
+    int optin = 0, dflt = 0;
+    if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess) optin = 0;
+    if (hipDeviceGetAttribute(&dflt, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) dflt = 0;
+    (void)hipGetLastError();
+    return std::max(optin, dflt);
+}
+
+// dynamic LDS bytes the launch may use on the current device (0: none / no
+// device), cached per device
 static int ploop_max_dyn(int wi) {
-    static int v[2] = {-1, -1};
-    if (v[wi] < 0) {
+    constexpr int kDevs = 64;
+    static int v[kDevs][2];
+    static bool init[kDevs][2];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDevs) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    if (!init[dev][wi]) {
         hipFuncAttributes fa;
         if (hipFuncGetAttributes(&fa, ploop_fn(wi)) != hipSuccess) {
             (void)hipGetLastError();
             return 0;
         }
-        const int d = kLdsPerWorkgroup - (int)fa.sharedSizeBytes;
-        v[wi] = d > 0 ? d : 0;
+        const int d = lds_per_workgroup(dev) - (int)fa.sharedSizeBytes;
+        v[dev][wi] = d > 0 ? d : 0;
+        init[dev][wi] = true;
     }
-    return v[wi];
+    return v[dev][wi];
 }
 
 uint32_t pe_ploop_max_n(uint32_t words) {
@@ -3943,13 +3961,17 @@ uint32_t pe_ploop_max_n(uint32_t words) {
 hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st) {
     const uint32_t n = a->P.n_visit;
     if (n == 0 || n > pe_ploop_max_n(a->P.mask_words)) return hipErrorInvalidValue;
-    static bool attr[2] = {false, false};
     const int wi = a->P.mask_words == 1u ? 0 : 1;
-    if (!attr[wi]) {
-        const hipError_t e = hipFuncSetAttribute(ploop_fn(wi), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 ploop_max_dyn(wi));
-        if (e != hipSuccess) return e;
-        attr[wi] = true;
+    {   // per device: the attribute is set on the current device's function
+        static bool attr[64][2];
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+        if (!attr[dev][wi]) {
+            const hipError_t e = hipFuncSetAttribute(ploop_fn(wi), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     ploop_max_dyn(wi));
+            if (e != hipSuccess) return e;
+            attr[dev][wi] = true;
+        }
     }
     const size_t lds = pe_ploop_lds_bytes(n);
     if (wi == 0) hipLaunchKernelGGL(pe::k_ploop<1>, dim3(1), dim3(pe::kPLoopBlock), lds, st, *a);

@@ -188,3 +188,56 @@ def test_cores_fallbacks_are_explicit():
     from nomad_amd.stack import SelectOptions
     with pytest.raises(Unsupported):
         st.SelectRaw(0, SelectOptions(preempt=True))
+
+
+def _evicting_cores_cluster(n, seed):
+    """Every node full: one priority-20 alloc holds 7000 MB and reserved cores
+    1-6 of 8, so a 4096 MB ask evicts it and a cores=4 ask fits only where it
+    is gone (cores 0 and 7 stay free otherwise)."""
+    ids = sorted(synth.uuids(n, seed))
+    nodes, allocs = [], []
+    for k, nid in enumerate(ids):
+        nd = synth.mock_node(nid)
+        nd.name = "node-%05d" % k
+        nd.total_cores = 8
+        nd.cpu_shares = 8000
+        nd.memory_mb = 8192
+        nd.reservable_cores = list(range(8))
+        nd.compute_class()
+        nodes.append(nd)
+        allocs.append(Allocation(node_id=nid, job_id="batch-%d" % (k % 7), task_group="train",
+                                 cpu_shares=6000, memory_mb=7000, disk_mb=100, priority=20,
+                                 reserved_cores=[1, 2, 3, 4, 5, 6]))
+    return nodes, allocs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("via_view", [True, False])
+def test_rolled_back_evictions_keep_their_cores(via_view):
+    """A speculative run whose placements evict allocs holding reserved cores,
+    rolled back by a deviating commit: the unconfirmed evictions'
+    cores are held again on the device and in the host mirror, so the cores
+    asks of the next task group see exactly the oracle's used sets."""
+    from nomad_amd.stack import GenericStack
+    from tests.test_spec_view import CCaller, ViewAnswers, protocol_answers
+    from tests.test_dropin import assert_equal_runs
+    nodes, allocs = _evicting_cores_cluster(300, seed=12)
+    job = Job(id="evictor", priority=80, task_groups=[
+        TaskGroup(name="big", count=40, ephemeral_disk_mb=100,
+                  tasks=[Task(name="m", driver="exec", cpu=500, memory_mb=4096)]),
+        TaskGroup(name="pinned", count=30, ephemeral_disk_mb=100,
+                  tasks=[Task(name="p", driver="exec", cpu=0, memory_mb=256, cores=4)])])
+    perm = synth.shuffle(len(nodes), 4)
+    cfg = SchedulerConfig(preempt_service=True)
+    eng, ora = GenericStack(config=cfg), OracleGenericStack(config=cfg)
+    for st in (eng, ora):
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(perm)
+    dev = lambda i, row: (int(perm[(i * 11) % len(perm)]) if i % 7 == 3 else None)
+    ce = ViewAnswers(eng) if via_view else CCaller(eng)
+    a = protocol_answers(ce, 40, deviate=dev, tg=0) + protocol_answers(ce, 30, tg=1)
+    b = protocol_answers(CCaller(ora), 40, deviate=dev, tg=0) + protocol_answers(CCaller(ora), 30, tg=1)
+    assert_equal_runs(a, b)
+    assert eng.SpeculationStats()[2] >= 3   # rollbacks happened
+    assert sum(1 for x in b if x[0] != "nil" and x[7]) >= 40, "too few evicting placements"
