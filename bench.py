@@ -363,22 +363,36 @@ def section_c3(device, cpu_s):
         st.SetJob(job)
         st.SetNodes(perm)
         t0 = time.perf_counter()
-        _, _, placed, _ = st.PlaceArrays(0, 1000)
+        rows, _, placed, _ = st.PlaceArrays(0, 1000)
         times.append(time.perf_counter() - t0)
+    rows = np.array(rows[:placed])   # outlives the handle
     kernel_ms = st.last_kernel_ms()
     # the unchanged caller: the same evaluation through Select / Commit from
     # the C loop, answered by the speculative runs and the served-Select view
     d_wall, d_placed, d_rows, d_info = _drop_in(st, job, perm, 1000)
     st.close()
+    if d_placed != placed or not np.array_equal(d_rows[:placed], rows):
+        raise RuntimeError("C3 drop-in placements differ from pe_place's")
     wall = float(np.median(times[1:]))
+    # roofline of the full-pass loop: every placement reads each row's 76 B
+    # (SURVEY.md §8(d)); kernel_ms is the device time of pe_place's whole loop
+    c3_bytes = 76.0 * len(nodes) * placed
+    achieved = c3_bytes / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
     out = {"workload": "C3 drop-in: job_c3 count=1000 (spread + affinity + semver/regexp) on 10000 nodes, 3 DCs, "
                        "one evaluation: ResetPlan + SetJob + SetNodes + 1000 x (Select, Commit) from a C caller "
                        "loop, predicted pairs from the served-Select view",
            "placements": int(d_placed), "placements_per_s": d_placed / d_wall, "wall_ms": d_wall * 1e3,
            "node_evals_per_s": d_placed * len(nodes) / d_wall, "drop_in": d_info,
+           "same_rows_as_pe_place": True,
            "pe_place": {"placements": int(placed), "placements_per_s": placed / wall, "wall_ms": wall * 1e3,
                         "kernel_ms": kernel_ms,
-                        "note": "the whole count loop in one pe_place call (not the caller's protocol)"}}
+                        "note": "the whole count loop in one pe_place call (not the caller's protocol)"},
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "note": "76 B per node per placement (10k nodes x placements) over pe_place's device time "
+                                "(HIP events around the whole loop on the engine stream); the 760 KB table is "
+                                "L2-resident and each placement is a dependent sweep + merge + commit, so the "
+                                "loop is latency-bound"}}
     if cpu_s > 0:
         from oracle.oracle import OracleGenericStack
         from tools import dropin

@@ -373,13 +373,22 @@ int pe_comm_unique_id(uint8_t* out, size_t cap);
  * built against (the communicator calls then fail with that reason). */
 const char* pe_comm_library(void);
 int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id);
+/* A caller-provided transport instead of RCCL (ranks on hosts without an
+ * RCCL path between them, or the CPU rehearsal of the per-GPU processes):
+ * exchange(ctx, send, recv, bytes) is an all-gather in rank order, `bytes`
+ * from this rank into recv[rank * bytes], returning 0 on success. It is called
+ * from the thread inside pe_place_sharded once per placement, on host buffers
+ * (the record crosses PCIe both ways). Replaces any RCCL communicator. */
+typedef int (*pe_exchange_fn)(void* ctx, const void* send, void* recv, size_t bytes);
+int pe_comm_init_host(pe_stack* s, int nranks, int rank, pe_exchange_fn exchange, void* ctx);
 /* The full-pass count loop (task groups with affinities / spreads, limit >=
  * list) sharded over the ranks: every rank holds the whole snapshot, job and
- * SetNodes list and sweeps its rows [row_begin, row_end); per placement one
- * ncclAllGather of the ranks' 80-byte records on the engine stream, then every
- * rank resolves and commits the same winner (the gather carries every
- * workgroup's record: blocks x 80 B per rank). Every rank receives the same
- * records. Windowed task groups return PE_EUNSUPPORTED (replicas only). */
+ * SetNodes list and sweeps its rows [row_begin, row_end) into one 80-byte
+ * record (the sweep's last workgroup merges the rank's workgroup records);
+ * per placement one ncclAllGather of the ranks' records on the engine stream
+ * (nranks x 80 B), then every rank resolves and commits the same winner.
+ * Every rank receives the same records. Windowed task groups return
+ * PE_EUNSUPPORTED (replicas only). */
 int pe_place_sharded(pe_stack* s, uint32_t tg_index, uint32_t count, uint32_t row_begin, uint32_t row_end,
                      pe_ranked_node* out, uint32_t* placed);
 /* Device time of the all-gather in the last pe_place_sharded (microseconds,

@@ -7,6 +7,8 @@ exported by nomad_amd/libnomadpe.so.
 import ctypes as C
 
 u8p = C.POINTER(C.c_uint8)
+# pe_exchange_fn (pe_comm_init_host): all-gather of one record per rank
+pe_exchange_fn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 u32p = C.POINTER(C.c_uint32)
 u16p = C.POINTER(C.c_uint16)
 i32p = C.POINTER(C.c_int32)
@@ -224,7 +226,7 @@ ENGINE_SYMBOLS = [
     "pe_last_kernel_ms", "pe_stage_orders", "pe_place_batch", "pe_batch_results", "pe_last_phase_ms",
     "pe_check_constraint", "pe_last_sweep_bytes", "pe_select_shard", "pe_select_merge",
     "pe_set_metrics", "pe_last_metrics", "pe_update_allocs", "pe_speculation_stats",
-    "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init",
+    "pe_plan_stop", "pe_plan_pop_update", "pe_update_nodes", "pe_comm_unique_id", "pe_comm_init", "pe_comm_init_host",
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
     "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
     "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get", "pe_system_view_get", "pe_comm_library", "pe_last_exchange_stats",

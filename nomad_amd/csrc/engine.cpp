@@ -143,6 +143,7 @@ hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint
                                   uint32_t count, pe_ranked_node* out, uint32_t* state, unsigned long long* prof,
                                   hipStream_t st);
 hipError_t pe_launch_sweep_only(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t pe_launch_sweep_local(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t pe_launch_step_only(const pe::SweepArgs* a, uint32_t nrecs, const uint32_t* visit, uint32_t n,
                                uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_commit_rows(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
@@ -829,6 +830,11 @@ struct pe_stack {
     // engines, one GPU each; the sharded count loop gathers per-rank records
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // pe_comm_init_host: the caller's all-gather over host buffers instead of RCCL
+    pe_exchange_fn xfn = nullptr;
+    void* xctx = nullptr;
+    void* h_xbuf = nullptr;   // pinned: this rank's record, then nranks records
+    DevMem d_sweep_done;      // k_sweep<..., MERGE> arrival counter
 
     // One handle over several devices (pe_config.device_count > 1): `kids`
     // hold replicas of the snapshot, job and plan on the other devices. The
@@ -4245,6 +4251,7 @@ void pe_stack_destroy(pe_stack* s) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->comm) (void)rc_CommDestroy(s->comm);
+    if (s->h_xbuf) (void)hipHostFree(s->h_xbuf);
     if (s->ev_x0) (void)hipEventDestroy(s->ev_x0);
     if (s->ev_x1) (void)hipEventDestroy(s->ev_x1);
     for (hipEvent_t ev : s->ev_xs)
@@ -6790,6 +6797,8 @@ int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id) {
         (void)rc_CommDestroy(s->comm);
         s->comm = nullptr;
     }
+    s->xfn = nullptr;
+    s->xctx = nullptr;
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
     const ncclResult_t r = rc_CommInitRank(&s->comm, nranks, uid, rank);
@@ -6804,19 +6813,41 @@ int pe_comm_init(pe_stack* s, int nranks, int rank, const uint8_t* id) {
     return PE_OK;
 }
 
+int pe_comm_init_host(pe_stack* s, int nranks, int rank, pe_exchange_fn exchange, void* ctx) {
+    PE_FLUSH_RESET(s);
+    if (!s || !exchange || nranks < 1 || rank < 0 || rank >= nranks) return PE_EINVAL;
+    HIP_TRY(s, hipSetDevice(s->device));
+    if (s->comm) {
+        (void)rc_CommDestroy(s->comm);
+        s->comm = nullptr;
+    }
+    if (s->h_xbuf) {
+        (void)hipHostFree(s->h_xbuf);
+        s->h_xbuf = nullptr;
+    }
+    HIP_TRY(s, hipHostMalloc(&s->h_xbuf, sizeof(pe::SweepRec) * ((size_t)nranks + 1), hipHostMallocDefault));
+    s->xfn = exchange;
+    s->xctx = ctx;
+    s->nranks = nranks;
+    s->rank = rank;
+    return PE_OK;
+}
+
 // The full-pass count loop (limit >= list, affinity / spread task groups)
 // sharded over the communicator's ranks: every rank holds the whole snapshot
-// and sweeps rows [row_begin, row_end); per placement k_sweep writes the
-// rank's per-workgroup 80-byte records, one in-place ncclAllGather of them
-// over xGMI runs on the engine stream (an identity at one rank, skipped), and
-// k_sweep_step merges every rank's records,
-// resolves the winner, writes its record and commits
-// it on every rank. Nothing returns to the host between placements; the stop
-// flag is read every 64 placements.
+// and sweeps rows [row_begin, row_end); per placement k_sweep's last
+// workgroup merges the rank's workgroup records into its one 80-byte record
+// (at its rank's slot of the gather buffer), one in-place ncclAllGather of the
+// nranks records runs over xGMI on the engine stream (an identity at one rank,
+// skipped), and k_sweep_step merges them, resolves the winner (SURVEY.md
+// Appendix A1), writes its record and commits it on every rank. Nothing
+// returns to the host between placements; the stop flag is read every 64
+// placements. With a host transport (pe_comm_init_host) the record goes
+// through the caller's all-gather instead, once per placement.
 static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_begin, uint32_t row_end,
                      pe_ranked_node* out, uint32_t* placed) {
     if (!s || (!out && count)) return PE_EINVAL;
-    if (!s->comm) return s->fail(PE_ESTATE, "pe_comm_init not called");
+    if (!s->comm && !s->xfn) return s->fail(PE_ESTATE, "pe_comm_init not called");
     if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "sharded placement needs a generic stack");
     int rc = spec_flush(s);
     if (rc) return rc;
@@ -6841,19 +6872,30 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
     uint32_t blocks = 0;
     rc = sweep_setup(s, g, nullptr, row_begin, row_end, &A, &blocks);
     if (rc) return rc;
-    // every rank launches the same number of workgroups (sized for the
-    // largest range) so that the all-gather moves equal slices: rank r's
-    // workgroup records land in d_gather[r * blocks ...] and the step merges
-    // all nranks * blocks of them (no separate merge launch)
+    // per placement: the rank's sweep merged to one record at its slot of the
+    // gather buffer, nranks x 80 B exchanged, the step merges the nranks records
     const uint32_t rows_max = (uint32_t)((s->nodes.size() + (size_t)s->nranks - 1) / (size_t)s->nranks);
     blocks = std::max<uint32_t>(1, std::min<uint32_t>((rows_max + 255) / 256,
                                                       (uint32_t)s->n_cu * (uint32_t)s->sweep_per_cu_aux));
-    const size_t slice = sizeof(pe::SweepRec) * blocks;
-    HIP_TRY(s, s->d_gather.ensure(slice * (size_t)s->nranks));
-    A.recs = reinterpret_cast<pe::SweepRec*>(static_cast<char*>(s->d_gather.p) + slice * (size_t)s->rank);
+    const size_t rec_bytes = sizeof(pe::SweepRec);
+    HIP_TRY(s, s->d_sweep_recs.ensure(rec_bytes * blocks));
+    HIP_TRY(s, s->d_gather.ensure(rec_bytes * (size_t)s->nranks));
+    HIP_TRY(s, s->d_sweep_done.ensure(sizeof(uint32_t)));
+    HIP_TRY(s, hipMemsetAsync(s->d_sweep_done.p, 0, sizeof(uint32_t), s->stream));
+    A.recs = s->d_sweep_recs.as<pe::SweepRec>();
+    A.merged = s->d_gather.as<pe::SweepRec>() + s->rank;
+    A.done = s->d_sweep_done.as<uint32_t>();
     pe::SweepArgs A2 = A;   // the step merges the gathered records
     A2.recs = s->d_gather.as<pe::SweepRec>();
-    const uint32_t nrecs = blocks * (uint32_t)s->nranks;
+    uint32_t nrecs = (uint32_t)s->nranks;
+    // one rank exchanges nothing: its step merges the workgroup records itself
+    // (PE_SHARD_MERGE_ONE=1 runs the per-rank merge anyway, for measurement)
+    static const bool merge_one = std::getenv("PE_SHARD_MERGE_ONE") != nullptr;
+    const bool local_merge = s->nranks > 1 || merge_one;
+    if (!local_merge) {
+        A2.recs = A.recs;
+        nrecs = blocks;
+    }
     HIP_TRY(s, upload_visit(s, s->visit));
     HIP_TRY(s, s->d_loop_out.ensure(sizeof(pe_ranked_node) * (size_t)(count + 1)));
     HIP_TRY(s, s->d_loop_state.ensure(8 * sizeof(uint32_t)));
@@ -6863,7 +6905,14 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
     const uint32_t chunk = 64;
     double x_us = 0, x_min = 1e300, x_max = 0;
     uint32_t x_n = 0;
-    if (s->nranks > 1 && s->ev_xs.empty()) {   // an event pair around every placement's all-gather
+    auto x_add = [&](double us) {
+        x_us += us;
+        x_min = std::min(x_min, us);
+        x_max = std::max(x_max, us);
+        x_n++;
+    };
+    const bool host_x = s->xfn != nullptr && s->nranks > 1;
+    if (s->nranks > 1 && !host_x && s->ev_xs.empty()) {   // an event pair around every placement's all-gather
         s->ev_xs.resize(2 * chunk, nullptr);
         for (auto& e : s->ev_xs) HIP_TRY(s, hipEventCreate(&e));
     }
@@ -6872,10 +6921,21 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
     for (uint32_t k = 0; k < count && !h_state[0]; k += chunk) {
         const uint32_t m = std::min(chunk, count - k);
         for (uint32_t j = 0; j < m; j++) {
-            HIP_TRY_STATE(s, pe_launch_sweep_only(&A, blocks, s->stream));
-            if (s->nranks > 1) {   // in place: this rank's slice already sits at its offset
+            if (local_merge) HIP_TRY_STATE(s, pe_launch_sweep_local(&A, blocks, s->stream));
+            else HIP_TRY_STATE(s, pe_launch_sweep_only(&A, blocks, s->stream));
+            if (host_x) {   // the caller's transport: record to host, all-gather, records back
+                char* hb = static_cast<char*>(s->h_xbuf);
+                HIP_TRY(s, hipMemcpyAsync(hb, A.merged, rec_bytes, hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(s, hipStreamSynchronize(s->stream));
+                const double t0 = now_us();
+                const int xr = s->xfn(s->xctx, hb, hb + rec_bytes, rec_bytes);
+                x_add(now_us() - t0);
+                if (xr != 0) return s->fail(PE_EHIP, "pe_comm_init_host exchange failed: " + std::to_string(xr));
+                HIP_TRY(s, hipMemcpyAsync(A2.recs, hb + rec_bytes, rec_bytes * (size_t)s->nranks,
+                                          hipMemcpyHostToDevice, s->stream));
+            } else if (s->nranks > 1) {   // in place: this rank's record already sits at its offset
                 HIP_TRY(s, hipEventRecord(s->ev_xs[2 * j], s->stream));
-                const ncclResult_t r = rc_AllGather(A.recs, s->d_gather.p, slice, ncclUint8, s->comm, s->stream);
+                const ncclResult_t r = rc_AllGather(A.merged, s->d_gather.p, rec_bytes, ncclUint8, s->comm, s->stream);
                 if (r != ncclSuccess) return s->fail(PE_EHIP, std::string("ncclAllGather: ") + rc_GetErrorString(r));
                 HIP_TRY(s, hipEventRecord(s->ev_xs[2 * j + 1], s->stream));
             }
@@ -6884,14 +6944,10 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
         }
         HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
-        for (uint32_t j = 0; s->nranks > 1 && j < m; j++) {   // every placement's all-gather
+        for (uint32_t j = 0; s->nranks > 1 && !host_x && j < m; j++) {   // every placement's all-gather
             float xms = 0;
             if (hipEventElapsedTime(&xms, s->ev_xs[2 * j], s->ev_xs[2 * j + 1]) != hipSuccess) continue;
-            const double us = xms * 1e3;
-            x_us += us;
-            x_min = std::min(x_min, us);
-            x_max = std::max(x_max, us);
-            x_n++;
+            x_add(xms * 1e3);
         }
     }
     s->last_exchange_us = x_n ? x_us / x_n : 0.0;
@@ -7670,10 +7726,12 @@ static void kids_fresh(pe_stack* s, bool all_ok) {
 }
 
 // The full-pass count loop split over the handle's devices: rows
-// [n k / N, n (k+1) / N) on replica k, per placement one k_sweep per replica,
-// the records exchanged (ncclAllGather over the group's communicators, or
-// device copies in loopback), then every replica's k_sweep_step merges all
-// N x blocks records and commits the same winner.
+// [n k / N, n (k+1) / N) on replica k, per placement one k_sweep per replica
+// whose last workgroup merges the replica's records into one (at slot k of
+// its gather buffer), the N records exchanged (ncclAllGather over the group's
+// communicators, or device copies in loopback), then every replica's
+// k_sweep_step merges the N records and commits the same winner. The
+// exchange is timed on every placement (events on the root's stream).
 static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node* out, uint32_t* placed) {
     std::vector<pe_stack*> st{s};
     st.insert(st.end(), s->kids.begin(), s->kids.end());
@@ -7683,7 +7741,7 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
     const uint32_t rows_max = (nn + N - 1) / N;
     const uint32_t blocks = std::max<uint32_t>(
         1, std::min<uint32_t>((rows_max + 255) / 256, (uint32_t)s->n_cu * (uint32_t)s->sweep_per_cu_aux));
-    const size_t slice = sizeof(pe::SweepRec) * blocks;
+    const size_t rec_bytes = sizeof(pe::SweepRec);
     auto strm = [&](uint32_t k) { return s->loopback ? s->stream : st[k]->stream; };
     for (uint32_t k = 0; k < N; k++) {
         pe_stack* x = st[k];
@@ -7698,8 +7756,12 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
         rc = sweep_setup(x, *x->tgs[tgi], nullptr, (uint32_t)((uint64_t)nn * k / N),
                          (uint32_t)((uint64_t)nn * (k + 1) / N), &A[k], &b_unused);
         if (rc) return k ? s->fail(rc, "replica: " + x->err) : rc;
-        HIP_TRY(s, x->d_gather.ensure(slice * N));
-        A[k].recs = reinterpret_cast<pe::SweepRec*>(static_cast<char*>(x->d_gather.p) + slice * k);
+        HIP_TRY(s, x->d_sweep_recs.ensure(rec_bytes * blocks));
+        HIP_TRY(s, x->d_gather.ensure(rec_bytes * N));
+        HIP_TRY(s, x->d_sweep_done.ensure(sizeof(uint32_t)));
+        A[k].recs = x->d_sweep_recs.as<pe::SweepRec>();
+        A[k].merged = x->d_gather.as<pe::SweepRec>() + k;
+        A[k].done = x->d_sweep_done.as<uint32_t>();
         A2[k] = A[k];
         A2[k].recs = x->d_gather.as<pe::SweepRec>();
         HIP_TRY(s, upload_visit(x, x->visit));
@@ -7707,45 +7769,49 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
         HIP_TRY(s, x->d_loop_state.ensure(8 * sizeof(uint32_t)));
         HIP_TRY(s, hipStreamSynchronize(x->stream));   // uploads on the replica's own stream
         HIP_TRY(s, hipMemsetAsync(x->d_loop_state.p, 0, 8 * sizeof(uint32_t), strm(k)));
+        HIP_TRY(s, hipMemsetAsync(x->d_sweep_done.p, 0, sizeof(uint32_t), strm(k)));
         if (A[k].spread_tab) HIP_TRY(s, pe_launch_spread_table(&A[k].tg, x->d_spread_tab.as<double>(), strm(k)));
     }
     uint32_t h_state[5] = {0, 0, 0, 0, 0};
     const uint32_t chunk = 64;
-    double x_us = 0;
+    double x_us = 0, x_min = 1e300, x_max = 0;
     uint32_t x_n = 0;
-    if (!s->ev_x0) HIP_TRY(s, hipEventCreate(&s->ev_x0));
-    if (!s->ev_x1) HIP_TRY(s, hipEventCreate(&s->ev_x1));
     HIP_TRY(s, hipSetDevice(s->device));
+    if (s->ev_xs.empty()) {   // an event pair around every placement's exchange
+        s->ev_xs.resize(2 * chunk, nullptr);
+        for (auto& e : s->ev_xs) HIP_TRY(s, hipEventCreate(&e));
+    }
     HIP_TRY(s, hipEventRecord(s->ev0, s->stream));
     for (uint32_t p0 = 0; p0 < count && !h_state[0]; p0 += chunk) {
         const uint32_t m = std::min(chunk, count - p0);
         for (uint32_t j = 0; j < m; j++) {
             for (uint32_t k = 0; k < N; k++) {
                 HIP_TRY(s, hipSetDevice(st[k]->device));
-                HIP_TRY_STATE(s, pe_launch_sweep_only(&A[k], blocks, strm(k)));
+                HIP_TRY_STATE(s, pe_launch_sweep_local(&A[k], blocks, strm(k)));
             }
             HIP_TRY(s, hipSetDevice(s->device));
-            if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x0, s->stream));
+            HIP_TRY(s, hipEventRecord(s->ev_xs[2 * j], s->stream));
             if (s->loopback) {
-                // every replica's slice into every other replica's gather buffer
+                // every replica's record into every other replica's gather buffer
                 for (uint32_t k = 0; k < N; k++)
                     for (uint32_t e = 0; e < N; e++)
                         if (e != k)
-                            HIP_TRY(s, hipMemcpyAsync(static_cast<char*>(st[k]->d_gather.p) + slice * e,
-                                                      static_cast<char*>(st[e]->d_gather.p) + slice * e, slice,
+                            HIP_TRY(s, hipMemcpyAsync(st[k]->d_gather.as<pe::SweepRec>() + e,
+                                                      st[e]->d_gather.as<pe::SweepRec>() + e, rec_bytes,
                                                       hipMemcpyDeviceToDevice, s->stream));
             } else {
                 ncclResult_t r = rc_GroupStart();
                 for (uint32_t k = 0; k < N && r == ncclSuccess; k++)
-                    r = rc_AllGather(A[k].recs, st[k]->d_gather.p, slice, ncclUint8, s->group_comms[k], st[k]->stream);
+                    r = rc_AllGather(A[k].merged, st[k]->d_gather.p, rec_bytes, ncclUint8, s->group_comms[k],
+                                     st[k]->stream);
                 const ncclResult_t r2 = rc_GroupEnd();
                 if (r != ncclSuccess || r2 != ncclSuccess)
                     return s->fail(PE_EHIP, std::string("ncclAllGather: ") + rc_GetErrorString(r != ncclSuccess ? r : r2));
             }
-            if (j == 0) HIP_TRY(s, hipEventRecord(s->ev_x1, s->stream));
+            HIP_TRY(s, hipEventRecord(s->ev_xs[2 * j + 1], s->stream));
             for (uint32_t k = 0; k < N; k++) {
                 HIP_TRY(s, hipSetDevice(st[k]->device));
-                HIP_TRY_STATE(s, pe_launch_step_only(&A2[k], blocks * N, st[k]->d_visit.as<uint32_t>(), n, st[k]->offset,
+                HIP_TRY_STATE(s, pe_launch_step_only(&A2[k], N, st[k]->d_visit.as<uint32_t>(), n, st[k]->offset,
                                                st[k]->d_loop_out.as<pe_ranked_node>(),
                                                st[k]->d_loop_state.as<uint32_t>(), strm(k)));
             }
@@ -7753,19 +7819,27 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
         HIP_TRY(s, hipSetDevice(s->device));
         HIP_TRY(s, hipMemcpyAsync(h_state, s->d_loop_state.p, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
-        float xms = 0;
-        if (m && hipEventElapsedTime(&xms, s->ev_x0, s->ev_x1) == hipSuccess) {
-            x_us += xms * 1e3;
+        for (uint32_t j = 0; j < m; j++) {   // every placement's exchange
+            float xms = 0;
+            if (hipEventElapsedTime(&xms, s->ev_xs[2 * j], s->ev_xs[2 * j + 1]) != hipSuccess) continue;
+            const double us = xms * 1e3;
+            x_us += us;
+            x_min = std::min(x_min, us);
+            x_max = std::max(x_max, us);
             x_n++;
         }
     }
+    s->last_exchange_stats[0] = x_n ? x_us / x_n : 0.0;
+    s->last_exchange_stats[1] = x_n ? x_min : 0.0;
+    s->last_exchange_stats[2] = x_max;
+    s->last_exchange_stats[3] = x_n;
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     for (uint32_t k = 1; k < N; k++) {
         HIP_TRY(s, hipSetDevice(st[k]->device));
         HIP_TRY(s, hipStreamSynchronize(strm(k)));
     }
     HIP_TRY(s, hipSetDevice(s->device));
-    s->last_exchange_us = x_n ? x_us / x_n : 0.0;
+    s->last_exchange_us = s->last_exchange_stats[0];
     const uint32_t p = h_state[1];
     const uint32_t nrec = std::min(count, p + (h_state[0] ? 1u : 0u));
     if (nrec)

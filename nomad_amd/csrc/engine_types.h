@@ -301,6 +301,11 @@ struct SweepArgs {
     const uint32_t* node_aux;     // [n rows]
     const double* aff_vals;       // [kAuxValues]
     SweepRec* recs;               // [gridDim.x]
+    // k_sweep<..., MERGE>: the last workgroup to finish merges the grid's
+    // records into *merged (one record per shard); done counts finished
+    // workgroups and is left at 0
+    SweepRec* merged;
+    uint32_t* done;
 };
 constexpr int kAuxPsets = 2;
 constexpr int kAuxValues = 256;

@@ -2617,7 +2617,29 @@ __global__ void __launch_bounds__(256) k_apply_commits(NodeSoA s, TgTables t, As
 // AUX: the node's verdict, affinity index and spread values come folded in one
 // u32 per node (k_fold_aux) and resolve against LDS copies of the affinity
 // values and the spread boosts, so an option costs no dependent table load.
-template <int BLOCK, bool PF, int PROBE = 0, bool AUX = false>
+// The grid's last workgroup to finish merges every workgroup's record into
+// *A.merged (a shard's one record: the all-gather then moves 80 bytes per
+// rank). Each workgroup's record store is released by its arrival count; the
+// last one acquires them all (the records cross XCDs: agent scope).
+template <int BLOCK>
+__device__ __forceinline__ void sweep_last_merge(const SweepArgs& A, SweepRec* red) {
+    __shared__ uint32_t last;
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(A.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;   // workgroup-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    SweepRec r;
+    rec_init(r);
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += BLOCK) rec_merge(r, A.recs[i]);
+    rec_block_reduce<BLOCK>(r, red);
+    if (threadIdx.x == 0) {
+        *A.merged = r;
+        __hip_atomic_store(A.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int BLOCK, bool PF, int PROBE = 0, bool AUX = false, bool MERGE = false>
 __device__ __forceinline__ void sweep_block(const SweepArgs& A) {
     constexpr int W = BLOCK / 64;
     constexpr uint32_t kQueue = 128;
@@ -2731,11 +2753,12 @@ __device__ __forceinline__ void sweep_block(const SweepArgs& A) {
     if ((uint32_t)lane < qn) score_from(head);
     rec_block_reduce<BLOCK>(r, red);
     if (threadIdx.x == 0) A.recs[blockIdx.x] = r;
+    if (MERGE) sweep_last_merge<BLOCK>(A, red);
 }
 
-template <int BLOCK, bool PF, int PROBE = 0, bool AUX = false>
+template <int BLOCK, bool PF, int PROBE = 0, bool AUX = false, bool MERGE = false>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AUX ? 4 : 5))) k_sweep(SweepArgs A) {
-    sweep_block<BLOCK, PF, PROBE, AUX>(A);
+    sweep_block<BLOCK, PF, PROBE, AUX, MERGE>(A);
 }
 
 // Bound probes for the sweep (PE_SWEEP_VARIANT 5 / 6): 5 streams exactly the
@@ -3796,6 +3819,28 @@ hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec
         default: hipLaunchKernelGGL((pe::k_sweep<256, false>), dim3(blocks), dim3(256), 0, st, *a); break;
     }
     hipLaunchKernelGGL(pe::k_sweep_merge, dim3(1), dim3(512), 0, st, (const pe::SweepRec*)a->recs, blocks, merged);
+    return hipGetLastError();
+}
+
+// A shard's sweep merged to one record in the same launch (a->merged,
+// a->done: the sharded count loop's exchange payload).
+// Default: k_sweep, then k_sweep_merge into *merged (a second launch queued
+// behind it); PE_SHARD_MERGE=fused: the sweep's last workgroup merges (one
+// launch, but every workgroup's release at agent scope writes back its L2).
+hipError_t pe_launch_sweep_local(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st) {
+    static const bool fused = [] {
+        const char* e = std::getenv("PE_SHARD_MERGE");
+        return e && std::strcmp(e, "fused") == 0;
+    }();
+    if (!a->merged || (fused && !a->done)) return hipErrorInvalidValue;
+    if (fused) {
+        if (a->node_aux) hipLaunchKernelGGL((pe::k_sweep<256, false, 0, true, true>), dim3(blocks), dim3(256), 0, st, *a);
+        else hipLaunchKernelGGL((pe::k_sweep<256, false, 0, false, true>), dim3(blocks), dim3(256), 0, st, *a);
+        return hipGetLastError();
+    }
+    if (a->node_aux) hipLaunchKernelGGL((pe::k_sweep<256, false, 0, true>), dim3(blocks), dim3(256), 0, st, *a);
+    else hipLaunchKernelGGL((pe::k_sweep<256, false>), dim3(blocks), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(pe::k_sweep_merge, dim3(1), dim3(512), 0, st, (const pe::SweepRec*)a->recs, blocks, a->merged);
     return hipGetLastError();
 }
 

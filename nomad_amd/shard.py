@@ -17,9 +17,11 @@ state, ~64 B per node in HBM); what is split is the work:
 The collective is torch.distributed's all_gather: RCCL over xGMI on GPU tensors
 (backend "nccl"), gloo on CPU tensors for the multi-process CPU tests. On GPUs
 the whole sharded count loop also runs inside the engine (`device_place`,
-pe_place_sharded): the engine's own RCCL communicator all-gathers the records
-on the engine stream between k_sweep and k_sweep_step, so no placement returns
-to the host.
+pe_place_sharded): each rank's sweep merges its workgroup records into one
+80-byte record in the same launch, the engine's own RCCL communicator
+all-gathers the N records on the engine stream between k_sweep and
+k_sweep_step, so no placement returns to the host. `host_comm_init` runs the
+same engine loop over a torch.distributed transport instead.
 """
 from __future__ import annotations
 
@@ -98,6 +100,17 @@ def comm_init(stack, dist=None):
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
     stack.CommInit(world, rank, uid)
+    return rank, world
+
+
+def host_comm_init(stack, dist):
+    """Join every rank's engine over torch.distributed instead of RCCL
+    (pe_comm_init_host): the engine hands each placement's 80-byte record to
+    an all-gather on CPU tensors (gloo), e.g. ranks without an RCCL path, or
+    the one-GPU rehearsal of the per-GPU processes."""
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    stack.CommInitHost(world, rank, lambda rec: all_gather_bytes(dist, rec))
     return rank, world
 
 

@@ -78,6 +78,8 @@ def load_engine():
         lib.pe_place_sharded.restype = C.c_int
         lib.pe_place_sharded.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.POINTER(abi.pe_ranked_node), abi.u32p]
+        lib.pe_comm_init_host.restype = C.c_int
+        lib.pe_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, abi.pe_exchange_fn, C.c_void_p]
         lib.pe_last_exchange_us.restype = C.c_double
         lib.pe_last_exchange_us.argtypes = [C.c_void_p]
         lib.pe_select_merge.restype = C.c_int
@@ -530,6 +532,22 @@ class GenericStack(_Stack):
         rank passes the same 128-byte id (comm_unique_id on one rank)."""
         buf = np.frombuffer(bytes(unique_id), dtype=np.uint8).copy()
         self._check(self._lib.pe_comm_init(self._h, nranks, rank, buf.ctypes.data_as(abi.u8p)))
+
+    def CommInitHost(self, nranks: int, rank: int, all_gather):
+        """Join `nranks` engines over a caller transport (pe_comm_init_host):
+        all_gather(record: bytes) -> list of nranks records in rank order, called
+        once per placement of PlaceSharded (e.g. torch.distributed over gloo)."""
+        def exchange(_ctx, send, recv, nbytes):
+            try:
+                recs = all_gather(C.string_at(send, nbytes))
+                if len(recs) != nranks or any(len(r) != nbytes for r in recs):
+                    return 2
+                C.memmove(recv, b"".join(recs), nbytes * nranks)
+                return 0
+            except Exception:   # noqa: BLE001 - reported to the engine as a failed exchange
+                return 1
+        self._xfn = abi.pe_exchange_fn(exchange)   # kept alive with the handle
+        self._check(self._lib.pe_comm_init_host(self._h, nranks, rank, self._xfn, None))
 
     def PlaceSharded(self, tg, count: int, row_begin: int, row_end: int) -> List[RankedNode]:
         """The full-pass count loop over the communicator's ranks, this rank

@@ -58,6 +58,28 @@ def test_c3_bench_size_select_commit(c3_oracle):
     assert_same_placements(got, ro)
 
 
+def test_c3_bench_size_served_from_the_view(c3_oracle):
+    """The caller's Select / Commit pairs answered from the served-Select view
+    (pe_spec_view), as the bench's C3 drop-in loop takes them: every answer
+    equals the oracle's placement, cursor included."""
+    from nomad_amd.stack import GenericStack
+    from tests.test_dropin import _key
+    from tests.test_spec_view import ViewAnswers, protocol_answers
+    nodes, allocs, job, perm, _, ro = c3_oracle
+    e = GenericStack()
+    e.SetState(nodes, allocs)
+    e.SetJob(job)
+    e.SetNodes(list(perm))
+    vc = ViewAnswers(e)
+    got = protocol_answers(vc, COUNT, preempt=False)
+    e.close()
+    want = [_key(r) for r in ro]
+    assert len(got) == len(want)
+    for i, (x, y) in enumerate(zip(got, want)):
+        assert x[:7] == y[:7], ("Select %d" % i, x, y)
+    assert vc.served >= COUNT - 8, vc.served
+
+
 def _with_constraints(job, cons):
     return dataclasses.replace(job, constraints=cons)
 

@@ -272,3 +272,61 @@ def test_c4_concurrent_rank_processes_match_oracle(world):
     assert total == po and np.array_equal(status, to)
     placed = to == 0
     assert np.array_equal(score[placed], so[placed])
+
+
+def _engine_fullscan_worker(rank, world, port, q):
+    # one engine per rank, every rank on the box's GPU 0, the per-placement
+    # record exchange over gloo (pe_comm_init_host): the sharded count loop of
+    # pe_place_sharded with two ranks, engine on both sides
+    from nomad_amd.stack import GenericStack
+    _init(rank, world, port)
+    n, count = 6000, 150
+    nodes, allocs = synth.cluster_c3(n, seed=24)
+    job = synth.job_c3(count)
+    perm = synth.shuffle(n, 10)
+    st = GenericStack(device=0)
+    st.SetState(nodes, allocs)
+    st.SetJob(job)
+    st.SetNodes(list(perm))
+    shard.host_comm_init(st, dist)
+    got = shard.device_place(st, 0, count, n, rank, world)
+    stats = st.last_exchange_stats()
+    nxt = st.SelectRaw(0)   # the plan is the same on every rank afterwards
+    st.close()
+    keys = [(r.row, r.final_score, tuple(r.scores), r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted)
+            for r in got]
+    allk = [None] * world
+    dist.all_gather_object(allk, (keys, (nxt.row, nxt.final_score), stats))
+    if rank == 0:
+        q.put(allk)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_engine_sharded_loop_two_ranks_over_gloo():
+    """pe_place_sharded at world size 2: two engine processes on one GPU, each
+    sweeping half the rows into one merged record per placement, the records
+    all-gathered through torch.distributed (gloo) by the engine's host
+    transport. Both ranks return pe_place's records and the oracle's rows."""
+    from nomad_amd.stack import GenericStack
+    from oracle.oracle import OracleGenericStack
+    got = _run(_engine_fullscan_worker, 2)
+    n, count = 6000, 150
+    nodes, allocs = synth.cluster_c3(n, seed=24)
+    job = synth.job_c3(count)
+    perm = synth.shuffle(n, 10)
+    b, o = GenericStack(), OracleGenericStack()
+    for st in (b, o):
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(list(perm))
+    ref = b.Place(0, count)
+    keys = [(r.row, r.final_score, tuple(r.scores), r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted)
+            for r in ref]
+    oref = [(r.row, r.final_score) for r in o.Place(0, count)]
+    nb, no = b.SelectRaw(0), o.SelectRaw(0)
+    for k, nxt, stats in got:
+        assert k == keys
+        assert [(x[0], x[1]) for x in k] == oref
+        assert nxt == (nb.row, nb.final_score) == (no.row, no.final_score)
+        assert stats[3] == count   # every placement exchanged once
