@@ -5946,7 +5946,7 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     if (lds_loop) {
         const bool fprof = std::getenv("PE_FULL_PROF") != nullptr;   // per-phase clocks of the loop
         DevMem d_prof;
-        if (fprof) HIP_TRY(s, d_prof.ensure(8 * sizeof(unsigned long long)));
+        if (fprof) HIP_TRY(s, d_prof.ensure(12 * sizeof(unsigned long long)));
         HIP_TRY(s, hipMemsetAsync(s->d_loop_out.p, 0, sizeof(pe_ranked_node) * (size_t)count, s->stream));
         s->h_full_args = A;
         HIP_TRY(s, s->d_full_args.ensure(sizeof(pe::SweepArgs)));
@@ -5958,13 +5958,15 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
         if (fprof) {
-            unsigned long long h[8];
+            unsigned long long h[12];
             HIP_TRY(s, hipMemcpy(h, d_prof.p, sizeof(h), hipMemcpyDeviceToHost));
             const double p = std::max<uint32_t>(1, h_state[1]);
             std::fprintf(stderr, "k_fullpass_lds us/placement (wave 0): approx %.2f amax-reduce %.2f exact %.2f "
-                         "best-reduce %.2f barrier %.2f resolve %.2f winner+commit %.2f table %.2f\n",
+                         "best-reduce %.2f barrier %.2f resolve %.2f winner+commit %.2f table %.2f; winner lane: "
+                         "load %.2f score %.2f record+commit %.2f\n",
                          h[4] / 100.0 / p, h[5] / 100.0 / p, h[6] / 100.0 / p, h[7] / 100.0 / p, h[0] / 100.0 / p,
-                         h[1] / 100.0 / p, h[2] / 100.0 / p, h[3] / 100.0 / p);
+                         h[1] / 100.0 / p, h[2] / 100.0 / p, h[3] / 100.0 / p, h[8] / 100.0 / p, h[9] / 100.0 / p,
+                         h[10] / 100.0 / p);
         }
         if (h_state[5]) lds_loop = false;
     }

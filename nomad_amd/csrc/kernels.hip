@@ -3081,6 +3081,8 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
     auto rank_of_pos = [&](uint32_t pos) __attribute__((always_inline)) -> uint32_t {
         return pos >= off ? pos - off : pos + n - off;
     };
+    __shared__ unsigned long long sh_wprof[4];   // PE_FULL_PROF: the winner lane's load / score / record+commit
+    if (prof && tid < 4) sh_wprof[tid] = 0;
     unsigned long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = prof ? wall_clock64() : 0;
     auto mark = [&](int i) __attribute__((always_inline)) {
         if (prof && tid == 0) {
@@ -3139,18 +3141,26 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
         }
         mark(7);
         if (lane == 0) { red_s[wid] = best; red_r[wid] = best_rank; }
+        // Each wave's lanes 0-1 look their wave's candidate row up now (the
+        // winner is one of the waves' candidates): the dependent visit load
+        // overlaps the barrier and the resolve, and the winning wave loads its
+        // candidate's node straight after. (Loading the whole node here keeps
+        // ~20 more VGPRs live across the barrier: they spill.)
+        const uint32_t my_rank = best_rank;   // wave-uniform
+        uint32_t c_row = 0;
+        if (lane < 2 && my_rank != 0xFFFFFFFFu) {
+            uint32_t pos = off + my_rank;
+            if (pos >= n) pos -= n;
+            c_row = visit[pos];
+        }
         __syncthreads();
         mark(0);
-        // every wave resolves the block's winner itself (no second barrier)
+        // every wave resolves the block's winner itself (no second barrier):
+        // the maximum score, then the earliest rank among the waves holding it
         best = lane < kFullWaves ? red_s[lane] : -__builtin_inff();
         best_rank = lane < kFullWaves ? red_r[lane] : 0xFFFFFFFFu;
-        for (int o = kFullWaves / 2; o > 0; o >>= 1) {
-            const double ob = __shfl_xor(best, o);
-            const uint32_t orank = (uint32_t)__shfl_xor((int)best_rank, o);
-            if (ob > best || (ob == best && orank < best_rank)) { best = ob; best_rank = orank; }
-        }
-        best = __shfl(best, 0);
-        uint32_t win = (uint32_t)__shfl((int)best_rank, 0);
+        best = __ockl_wfred_max_f64(best);
+        uint32_t win = __ockl_wfred_min_u32(lane < kFullWaves && red_s[lane] == best ? best_rank : 0xFFFFFFFFu);
         if (win != 0xFFFFFFFFu && !(best > 0.0)) {   // every option non-positive: the skip rule decides (rare)
             SweepRec r;
             rec_init(r);
@@ -3167,6 +3177,18 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
         }
         mark(1);
         pe_ranked_node* o = out + it;
+        // the wave whose candidate won evaluates it; when the skip rule picked
+        // a rank no wave held (every option non-positive), wave 0 loads it
+        bool mine = win != 0xFFFFFFFFu && my_rank == win;
+        if (win != 0xFFFFFFFFu && wid == 0 &&
+            __ballot(lane < kFullWaves && red_r[lane] == win) == 0) {   // wave-uniform
+            mine = true;
+            if (lane < 2) {
+                uint32_t pos = off + win;
+                if (pos >= n) pos -= n;
+                c_row = visit[pos];
+            }
+        }
         if (wid == 0 && win == 0xFFFFFFFFu) {
             if (lane == 0) {
                 o->row = -1;
@@ -3177,16 +3199,21 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
                 state[0] = 1;
                 sh_stop = 1;
             }
-        } else if (wid == 0 && lane < 2) {
-            uint32_t pos = off + win;
-            if (pos >= n) pos -= n;
-            const uint32_t row = visit[pos];
-            // the winner's entry (the options are few per lane: scan for it)
+        } else if (mine && lane < 2) {
+            const uint32_t row = c_row;
+            const unsigned long long w0 = prof ? wall_clock64() : 0;
             NodeIn in;
             const uint32_t aux = load(row, in);
+            if (prof) {   // the load's latency alone
+                __builtin_amdgcn_s_waitcnt(0);
+                if (lane == 0) sh_wprof[0] += wall_clock64() - w0;
+            }
+            const unsigned long long w1 = prof ? wall_clock64() : 0;
             double s;
             uint32_t kk;
             const int st = head(row, in, aux, (uint32_t)lane, lane == 0 ? o->scores : parts1, &s, &kk);
+            if (prof && lane == 0) sh_wprof[1] += wall_clock64() - w1;
+            const unsigned long long w2 = prof ? wall_clock64() : 0;
             const int st1 = __shfl(st, 1);
             const uint32_t meta0 = (aux & 0x00FFFF00u);   // spread values: the entry's
             if (lane == 1) {
@@ -3241,6 +3268,7 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
                 state[1] = it + 1;
                 sh_nf += st1 == kFiltered;
                 sh_ne += st1 == kExhausted;
+                if (prof) sh_wprof[2] += wall_clock64() - w2;
             }
         }
         mark(2);
@@ -3264,6 +3292,8 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
     }
     if (prof && tid == 0)
         for (int i = 0; i < 8; i++) prof[i] = tp[i];
+    if (prof && tid == 0)
+        for (int i = 0; i < 3; i++) prof[8 + i] = sh_wprof[i];
     // the HBM table the next Select starts from
     for (int p = 0; p < np; p++)
         for (int v = tid; v < t.pset_nvals[p]; v += kFullThreads)
