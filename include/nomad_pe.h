@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 8u
+#define PE_ABI_VERSION 9u
 #define PE_NONE 0xFFFFFFFFu
 #define PE_MAX_SCORES 8
 #define PE_MAX_PREEMPT 16   /* PreemptedAllocs carried inline per RankedNode (the
@@ -502,6 +502,47 @@ int pe_set_metrics(pe_stack* s, int on);
  * CF / KF / CE / DE, keys sorted. Writes at most cap bytes (NUL-terminated) and
  * returns the bytes needed, or PE_ESTATE when the last Select has none. */
 int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap);
+/* The same maps in binary form (what the Go shim turns into AllocMetric
+ * without parsing text): count entries {kind, key, count} and the
+ * ScoreMetaData items in GetItemsReverse order (NormScore descending, Go's
+ * heap order for equal scores). A key without PE_METRIC_ENGINE_KEY is a
+ * string id of the caller's table (the node classes of ClassFiltered /
+ * ClassExhausted); a key with it names an engine string (checker reasons,
+ * dimensions: pe_metric_string), stable for the handle's life. The arrays
+ * stay valid until the next Select or state call. PE_ESTATE when the last
+ * Select has no maps. */
+#define PE_METRIC_ENGINE_KEY 0x80000000u
+#define PE_METRIC_CLASS_FILTERED 1u       /* AllocMetric.ClassFiltered[key]       */
+#define PE_METRIC_CONSTRAINT_FILTERED 2u  /* AllocMetric.ConstraintFiltered[key]  */
+#define PE_METRIC_CLASS_EXHAUSTED 3u      /* AllocMetric.ClassExhausted[key]      */
+#define PE_METRIC_DIMENSION_EXHAUSTED 4u  /* AllocMetric.DimensionExhausted[key]  */
+typedef struct pe_metric_count {
+    uint32_t kind;    /* PE_METRIC_* */
+    uint32_t key;     /* string id (see above) */
+    uint32_t count;
+} pe_metric_count;
+/* NodeScoreMeta.Scores names (the ScoreNode scorers, in the order they ran) */
+#define PE_SCORER_BINPACK 0u
+#define PE_SCORER_DEVICES 1u
+#define PE_SCORER_JOB_ANTI_AFFINITY 2u
+#define PE_SCORER_RESCHEDULE_PENALTY 3u   /* "node-reschedule-penalty" */
+#define PE_SCORER_NODE_AFFINITY 4u
+#define PE_SCORER_ALLOCATION_SPREAD 5u
+#define PE_SCORER_PREEMPTION 6u
+typedef struct pe_metric_score {
+    int32_t row;                      /* NodeID: the node table row */
+    uint32_t n_scores;
+    double norm;                      /* NormScore */
+    uint8_t scorer[PE_MAX_SCORES];    /* PE_SCORER_* */
+    double score[PE_MAX_SCORES];
+} pe_metric_score;
+int pe_last_metrics_bin(const pe_stack* s, const pe_metric_count** counts, uint32_t* n_counts,
+                        const pe_metric_score** scores, uint32_t* n_scores);
+/* The text of metric key `key` (an engine string or a caller string id):
+ * writes at most cap bytes (NUL-terminated), returns the bytes needed or
+ * PE_EINVAL for an unknown key. Scorer names: pe_scorer_name. */
+int64_t pe_metric_string(const pe_stack* s, uint32_t key, char* buf, size_t cap);
+const char* pe_scorer_name(uint32_t scorer);
 /* EvalEligibility (scheduler/context.go:190-356) as the reference chain would
  * hold it after this evaluation's Selects: the job-level and per task group
  * ComputedClassFeasibility entries FeasibilityWrapper.Next writes for every
@@ -564,8 +605,8 @@ int pe_get_cursor(const pe_stack* s, uint32_t* offset, uint32_t* limit);
  *     would have produced; they may replace or withdraw the records (v->epoch
  *     changes; v->n_rec 0: nothing to serve).
  * A record the engine returned through pe_select may be confirmed through the
- * view as well. With pe_set_metrics on, windowed runs without property sets or
- * preemption still publish records, each with its AllocMetric maps. A served record is the leading part of pe_ranked_node (row ..
+ * view as well. With pe_set_metrics on, the runs still publish records, each
+ * with its AllocMetric maps. A served record is the leading part of pe_ranked_node (row ..
  * new_offset) plus the device offers; served Selects never reserve cores.
  * Replaces: the Select / Commit crossings of computePlacements' loop. */
 #define PE_SPEC_PREEMPT 1u   /* pe_spec_rec.flags: answers the Select with Preempt=true */
@@ -589,11 +630,15 @@ typedef struct pe_spec_view {
     uint32_t confirmed;           /* caller and engine: records settled (Commits, nils) */
     const uint32_t* pre_off;      /* [n_rec + 1] or NULL: record k's PreemptedAllocs ... */
     const uint32_t* pre_allocs;   /* ... are pre_allocs[pre_off[k] .. pre_off[k + 1]) (alloc-table rows) */
-    /* With pe_set_metrics on: record k's AllocMetric maps, the text pe_last_metrics
-     * would return after that Select, are metrics[metrics_off[k] .. metrics_off[k + 1])
-     * (not NUL-terminated); NULL when the records carry none. */
-    const char* metrics;
-    const uint32_t* metrics_off;
+    /* With pe_set_metrics on: record k's AllocMetric maps, what
+     * pe_last_metrics_bin returns after that Select, are
+     * mcounts[mcounts_off[k] .. mcounts_off[k + 1]) and
+     * mscores[mscores_off[k] .. mscores_off[k + 1]); NULL when the records
+     * carry none. */
+    const pe_metric_count* mcounts;
+    const uint32_t* mcounts_off;
+    const pe_metric_score* mscores;
+    const uint32_t* mscores_off;
 } pe_spec_view;
 pe_spec_view* pe_spec_view_get(pe_stack* s);
 /* SystemScheduler.computePlacements (scheduler_system.go:283-425) runs, for

@@ -230,6 +230,7 @@ ENGINE_SYMBOLS = [
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
     "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
     "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get", "pe_system_view_get", "pe_comm_library", "pe_last_exchange_stats",
+    "pe_last_metrics_bin", "pe_metric_string", "pe_scorer_name",
 ]
 
 
@@ -244,11 +245,27 @@ class pe_spec_rec(C.Structure):   # nomad_pe.h: a served-Select record
 PE_SPEC_PREEMPT = 1   # pe_spec_rec.flags: answers the Select with Preempt=true
 
 
+PE_METRIC_CLASS_FILTERED, PE_METRIC_CONSTRAINT_FILTERED, PE_METRIC_CLASS_EXHAUSTED, PE_METRIC_DIMENSION_EXHAUSTED = 1, 2, 3, 4
+PE_METRIC_ENGINE_KEY = 0x80000000
+SCORER_NAMES = ("binpack", "devices", "job-anti-affinity", "node-reschedule-penalty", "node-affinity",
+                "allocation-spread", "preemption")
+
+
+class pe_metric_count(C.Structure):   # nomad_pe.h: one AllocMetric map entry
+    _fields_ = [("kind", C.c_uint32), ("key", C.c_uint32), ("count", C.c_uint32)]
+
+
+class pe_metric_score(C.Structure):   # nomad_pe.h: one NodeScoreMeta
+    _fields_ = [("row", C.c_int32), ("n_scores", C.c_uint32), ("norm", C.c_double),
+                ("scorer", C.c_uint8 * PE_MAX_SCORES), ("score", C.c_double * PE_MAX_SCORES)]
+
+
 class pe_spec_view(C.Structure):
     _fields_ = [("epoch", C.c_uint32), ("tg_index", C.c_uint32), ("n_rec", C.c_uint32), ("pad0", C.c_uint32),
                 ("recs", C.POINTER(pe_spec_rec)), ("served", C.c_uint32), ("confirmed", C.c_uint32),
                 ("pre_off", C.POINTER(C.c_uint32)), ("pre_allocs", C.POINTER(C.c_uint32)),
-                ("metrics", C.c_void_p), ("metrics_off", C.POINTER(C.c_uint32))]
+                ("mcounts", C.POINTER(pe_metric_count)), ("mcounts_off", C.POINTER(C.c_uint32)),
+                ("mscores", C.POINTER(pe_metric_score)), ("mscores_off", C.POINTER(C.c_uint32))]
 
 
 PE_SYS_NIL = 1 << 31

@@ -705,7 +705,31 @@ struct pe_stack {
     bool metrics_on = false, metrics_valid = false;
     std::map<uint32_t, std::vector<int8_t>> ref_tg_memo;
     std::vector<int8_t> ref_job_memo;
-    std::string metrics_text;
+    std::string metrics_text;          // pe_last_metrics: built from the binary maps on demand
+    bool metrics_text_ok = false;
+    // the last Select's maps in binary form (pe_last_metrics_bin)
+    std::vector<pe_metric_count> m_counts;
+    std::vector<pe_metric_score> m_scores;
+    // engine strings of metric keys (PE_METRIC_ENGINE_KEY | index)
+    std::vector<std::string> mstrs;
+    std::unordered_map<std::string, uint32_t> mstr_ix;
+    const char* mk_last_p = nullptr;   // the last interned C string (a reason pointer repeats)
+    uint32_t mk_last_id = 0;
+    uint32_t mkey(std::string_view t) {
+        auto it = mstr_ix.find(std::string(t));
+        if (it != mstr_ix.end()) return it->second;
+        const uint32_t id = PE_METRIC_ENGINE_KEY | (uint32_t)mstrs.size();
+        mstrs.emplace_back(t);
+        mstr_ix.emplace(mstrs.back(), id);
+        return id;
+    }
+    uint32_t mkey_p(const char* p) {   // reasons that are stable C strings (checker texts, literals)
+        if (p != mk_last_p) {
+            mk_last_id = mkey(p);
+            mk_last_p = p;
+        }
+        return mk_last_id;
+    }
 
     // EvalEligibility as the reference chain holds it (pe_get_eligibility,
     // context.go:190-356): every Select logs the visit-list span its chain
@@ -783,8 +807,10 @@ struct pe_stack {
         // texts pe_last_metrics returns (CSR), the reference-memo changes each
         // record's walk made (CSR) and the memo the run started from
         bool metrics = false;
-        std::string mtext;
-        std::vector<uint32_t> mtext_off;
+        std::vector<pe_metric_count> mcounts;
+        std::vector<uint32_t> mcounts_off;
+        std::vector<pe_metric_score> mscores;
+        std::vector<uint32_t> mscores_off;
         std::vector<MemoDelta> memo_log;
         std::vector<uint32_t> memo_off;
         std::vector<int8_t> memo_job0, memo_tg0;
@@ -2499,8 +2525,10 @@ static void spec_confirm_rec(pe_stack* s, uint32_t k, bool kids) {
 // pe_last_metrics after record k was served.
 static void spec_metrics_served(pe_stack* s, uint32_t k) {
     const pe_stack::Spec& sp = s->spec;
-    if (!sp.metrics || k + 1 >= sp.mtext_off.size()) return;
-    s->metrics_text.assign(sp.mtext, sp.mtext_off[k], sp.mtext_off[k + 1] - sp.mtext_off[k]);
+    if (!sp.metrics || k + 1 >= sp.mcounts_off.size()) return;
+    s->m_counts.assign(sp.mcounts.begin() + sp.mcounts_off[k], sp.mcounts.begin() + sp.mcounts_off[k + 1]);
+    s->m_scores.assign(sp.mscores.begin() + sp.mscores_off[k], sp.mscores.begin() + sp.mscores_off[k + 1]);
+    s->metrics_text_ok = false;
     s->metrics_valid = true;
 }
 
@@ -2553,8 +2581,10 @@ static void view_publish(pe_stack* s) {
     v.recs = sp.compact ? sp.crecs.data() : sp.vrecs.data();
     v.pre_off = sp.evict ? sp.pre_off.data() : nullptr;
     v.pre_allocs = sp.evict ? sp.pre_list.data() : nullptr;
-    v.metrics = sp.metrics ? sp.mtext.data() : nullptr;
-    v.metrics_off = sp.metrics ? sp.mtext_off.data() : nullptr;
+    v.mcounts = sp.metrics ? sp.mcounts.data() : nullptr;
+    v.mcounts_off = sp.metrics ? sp.mcounts_off.data() : nullptr;
+    v.mscores = sp.metrics ? sp.mscores.data() : nullptr;
+    v.mscores_off = sp.metrics ? sp.mscores_off.data() : nullptr;
     v.served = sp.served;
     v.confirmed = sp.confirmed;
     v.n_rec = (s->metrics_on && !sp.metrics) ? 0u : sp.n_rec;
@@ -2567,8 +2597,10 @@ static void view_withdraw(pe_stack* s) {
     v.n_rec = 0;
     v.recs = nullptr;
     v.pre_off = v.pre_allocs = nullptr;
-    v.metrics = nullptr;
-    v.metrics_off = nullptr;
+    v.mcounts = nullptr;
+    v.mcounts_off = nullptr;
+    v.mscores = nullptr;
+    v.mscores_off = nullptr;
     v.served = v.confirmed = 0;
 }
 
@@ -4858,24 +4890,19 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
 // reference's order.
 // The named scores of one option (at most 7 scorers: binpack, devices,
 // job-anti-affinity, node-reschedule-penalty, node-affinity,
-// allocation-spread, preemption); names are literals, so the heap moves PODs.
+// allocation-spread, preemption) as PE_SCORER_* ids, so the heap moves PODs.
+const char* const kScorerNames[7] = {"binpack", "devices", "job-anti-affinity", "node-reschedule-penalty",
+                                     "node-affinity", "allocation-spread", "preemption"};
 struct ScoreList {
-    const char* name[8];
+    uint8_t name[8];
     double val[8];
     uint32_t n = 0;
-    void emplace_back(const char* k, double v) {
-        name[n] = k;
+    void emplace_back(uint32_t k, double v) {
+        name[n] = (uint8_t)k;
         val[n] = v;
         n++;
     }
     uint32_t size() const { return n; }
-    void sort_by_name() {   // NodeScoreMeta.Scores is a map: its keys in order
-        for (uint32_t i = 1; i < n; i++)
-            for (uint32_t j = i; j > 0 && std::strcmp(name[j], name[j - 1]) < 0; j--) {
-                std::swap(name[j], name[j - 1]);
-                std::swap(val[j], val[j - 1]);
-            }
-    }
 };
 
 struct ScoreMeta {
@@ -4933,35 +4960,38 @@ struct ScoreHeap {
     }
 };
 
-// One AllocMetric map (string -> count) as it fills: a Select's maps hold a
-// handful of keys, so a short vector searched in place (no allocation once a
-// key is in) and sorted by key when written out (Go's map keys in order)
+// One AllocMetric map (key -> count) as it fills: a Select's maps hold a
+// handful of keys, so a short vector searched in place
 struct MetricCounts {
-    std::vector<std::pair<std::string, int>> kv;
-    void add(std::string_view k) {
+    std::vector<std::pair<uint32_t, uint32_t>> kv;
+    void add(uint32_t k) {
         for (auto& e : kv)
             if (e.first == k) {
                 e.second++;
                 return;
             }
-        kv.emplace_back(std::string(k), 1);
+        kv.emplace_back(k, 1u);
     }
 };
 
-// The maps of one Select as they fill (FilterNode / ExhaustedNode, ScoreNode).
+// The maps of one Select as they fill (FilterNode / ExhaustedNode, ScoreNode);
+// keys are caller string ids (node classes) or engine strings (reasons).
 struct MetricAcc {
     MetricCounts cf, kf, ce, de;
     ScoreHeap heap;
-    void filter(pe_stack* s, uint32_t row, std::string_view why) {
+    void filter(pe_stack* s, uint32_t row, uint32_t why) {
         const uint32_t nc = s->nodes[row].node_class;
-        if (nc != PE_NONE && !s->S(nc).empty()) cf.add(s->S(nc));
-        if (!why.empty()) kf.add(why);
+        if (nc != PE_NONE && !s->S(nc).empty()) cf.add(nc);
+        if (why != PE_NONE) kf.add(why);
     }
-    void exhaust(pe_stack* s, uint32_t row, std::string_view dim) {
+    void filter(pe_stack* s, uint32_t row, const std::string& why) { filter(s, row, s->mkey(why)); }
+    void exhaust(pe_stack* s, uint32_t row, uint32_t dim) {
         const uint32_t nc = s->nodes[row].node_class;
-        if (nc != PE_NONE && !s->S(nc).empty()) ce.add(s->S(nc));
-        if (!dim.empty()) de.add(dim);
+        if (nc != PE_NONE && !s->S(nc).empty()) ce.add(nc);
+        if (dim != PE_NONE) de.add(dim);
     }
+    void exhaust(pe_stack* s, uint32_t row, const std::string& dim) { exhaust(s, row, s->mkey(dim)); }
+    void exhaust(pe_stack* s, uint32_t row, const char* dim) { exhaust(s, row, s->mkey_p(dim)); }
 };
 
 // FeasibilityWrapper half of one Select's maps: the window's rows in visit
@@ -4976,6 +5006,7 @@ static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& or
     if (rt.size() != s->ncls) rt.assign(s->ncls, -1);
     pe::ConstraintEvaluator ev;
     static const char* kIneligible = "computed class ineligible";
+    const uint32_t ineligible = s->mkey_p(kIneligible);
     auto set_job = [&](uint32_t c, int8_t v) {
         if (log) log->push_back({false, c, v});
         s->ref_job_memo[c] = v;
@@ -5008,7 +5039,7 @@ static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& or
                 set_tg(c, why ? 0 : 1);
             }
         }
-        if (why) acc.filter(s, row, why);
+        if (why) acc.filter(s, row, why == kIneligible ? ineligible : s->mkey_p(why));
         else rows.push_back(row);
     }
 }
@@ -5022,20 +5053,20 @@ static int metrics_outcome(pe_stack* s, TgPlan& g, const pe::Ask& a, uint32_t ro
         case pe::kTrOption: {   // ScoreNode calls in chain order, then the NormScore push
             ScoreMeta sm;
             sm.row = row;
-            sm.scores.emplace_back("binpack", o[0]);
-            if (a.dev_tw != 0.0) sm.scores.emplace_back("devices", o[1]);
+            sm.scores.emplace_back(PE_SCORER_BINPACK, o[0]);
+            if (a.dev_tw != 0.0) sm.scores.emplace_back(PE_SCORER_DEVICES, o[1]);
             if (generic) {   // the SystemStack ranks with BinPack alone (stack.go:277-281)
-                if (a.anti_aff) sm.scores.emplace_back("job-anti-affinity", o[2]);
-                sm.scores.emplace_back("node-reschedule-penalty", (code & pe::kTrPenalty) ? -1.0 : 0.0);
-                if (!has_aff) sm.scores.emplace_back("node-affinity", 0.0);
-                else if (o[3] != 0.0) sm.scores.emplace_back("node-affinity", o[3]);
-                if (o[4] != 0.0) sm.scores.emplace_back("allocation-spread", o[4]);
+                if (a.anti_aff) sm.scores.emplace_back(PE_SCORER_JOB_ANTI_AFFINITY, o[2]);
+                sm.scores.emplace_back(PE_SCORER_RESCHEDULE_PENALTY, (code & pe::kTrPenalty) ? -1.0 : 0.0);
+                if (!has_aff) sm.scores.emplace_back(PE_SCORER_NODE_AFFINITY, 0.0);
+                else if (o[3] != 0.0) sm.scores.emplace_back(PE_SCORER_NODE_AFFINITY, o[3]);
+                if (o[4] != 0.0) sm.scores.emplace_back(PE_SCORER_ALLOCATION_SPREAD, o[4]);
             }
             sm.norm = o[5];
             acc.heap.push(std::move(sm));
             break;
         }
-        case pe::kTrDistinctHosts: acc.filter(s, row, "distinct_hosts"); break;
+        case pe::kTrDistinctHosts: acc.filter(s, row, s->mkey_p("distinct_hosts")); break;
         case pe::kTrDistinctProp: {   // propertyset.go:213-244
             const int p = (int)(code >> 8);
             PsetDev& ps = *g.psets[p];
@@ -5092,53 +5123,98 @@ static int metrics_outcome(pe_stack* s, TgPlan& g, const pe::Ask& a, uint32_t ro
     return PE_OK;
 }
 
-// pe_last_metrics' text of one Select's maps, appended to `out`.
-static void metrics_text_into(pe_stack* s, MetricAcc& acc, std::string& out) {
+// One Select's maps in binary form (pe_last_metrics_bin), appended.
+static void metrics_bin_into(MetricAcc& acc, std::vector<pe_metric_count>& counts,
+                             std::vector<pe_metric_score>& scores) {
+    auto put = [&](uint32_t kind, const MetricCounts& mm) {
+        for (auto& kv : mm.kv) counts.push_back(pe_metric_count{kind, kv.first, kv.second});
+    };
+    put(PE_METRIC_CLASS_FILTERED, acc.cf);
+    put(PE_METRIC_CONSTRAINT_FILTERED, acc.kf);
+    put(PE_METRIC_CLASS_EXHAUSTED, acc.ce);
+    put(PE_METRIC_DIMENSION_EXHAUSTED, acc.de);
+    for (auto& it : acc.heap.reverse_items()) {   // PopulateScoreMetaData: GetItemsReverse
+        pe_metric_score m;
+        std::memset(&m, 0, sizeof(m));
+        m.row = (int32_t)it.row;
+        m.n_scores = it.scores.n;
+        m.norm = it.norm;
+        for (uint32_t k = 0; k < it.scores.n && k < PE_MAX_SCORES; k++) {
+            m.scorer[k] = it.scores.name[k];
+            m.score[k] = it.scores.val[k];
+        }
+        scores.push_back(m);
+    }
+}
+
+static const std::string& metric_string(const pe_stack* s, uint32_t key) {
+    static const std::string none;
+    if (key & PE_METRIC_ENGINE_KEY) {
+        const uint32_t i = key & ~PE_METRIC_ENGINE_KEY;
+        return i < s->mstrs.size() ? s->mstrs[i] : none;
+    }
+    return s->S(key);
+}
+
+// pe_last_metrics' text of binary maps: "KIND\tKEY\tCOUNT" lines per map,
+// keys sorted (Go's map keys in order), then ScoreMetaData lines
+// "SM\trank\tnode id\tnorm\tname=value,..." with the names sorted and the
+// values in the shortest round-trip decimal (the same doubles when parsed).
+static void metrics_text_into(const pe_stack* s, const pe_metric_count* c, size_t nc, const pe_metric_score* sc,
+                              size_t ns, std::string& out) {
     char num[64];
-    auto put = [&](const char* k, MetricCounts& mm) {
-        std::sort(mm.kv.begin(), mm.kv.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-        for (auto& kv : mm.kv) {
-            out += k;
+    static const char* kinds[5] = {"", "CF", "KF", "CE", "DE"};
+    for (uint32_t kind = PE_METRIC_CLASS_FILTERED; kind <= PE_METRIC_DIMENSION_EXHAUSTED; kind++) {
+        std::vector<std::pair<const std::string*, uint32_t>> kv;
+        for (size_t i = 0; i < nc; i++)
+            if (c[i].kind == kind) kv.emplace_back(&metric_string(s, c[i].key), c[i].count);
+        std::sort(kv.begin(), kv.end(), [](const auto& x, const auto& y) { return *x.first < *y.first; });
+        for (auto& e : kv) {
+            out += kinds[kind];
             out += '\t';
-            out += kv.first;
+            out += *e.first;
             out += '\t';
-            const auto r = std::to_chars(num, num + sizeof num, kv.second);
+            const auto r = std::to_chars(num, num + sizeof num, e.second);
             out.append(num, r.ptr);
             out += '\n';
         }
-    };
-    put("CF", acc.cf); put("KF", acc.kf); put("CE", acc.ce); put("DE", acc.de);
-    // ScoreMetaData (PopulateScoreMetaData): "SM\trank\tnode id\tnorm\tname=value,..."
-    // (shortest round-trip decimal: the same doubles when parsed back)
-    auto items = acc.heap.reverse_items();
+    }
     auto put_num = [&](double x) {
         const auto r = std::to_chars(num, num + sizeof num, x);
         out.append(num, r.ptr);
     };
-    for (size_t i = 0; i < items.size(); i++) {
-        auto& it = items[i];
-        it.scores.sort_by_name();
+    for (size_t i = 0; i < ns; i++) {
+        const pe_metric_score& it = sc[i];
+        uint32_t order[PE_MAX_SCORES];
+        const uint32_t n = std::min<uint32_t>(it.n_scores, PE_MAX_SCORES);
+        for (uint32_t k = 0; k < n; k++) order[k] = k;
+        std::sort(order, order + n, [&](uint32_t x, uint32_t y) {   // NodeScoreMeta.Scores is a map
+            return std::strcmp(kScorerNames[it.scorer[x]], kScorerNames[it.scorer[y]]) < 0;
+        });
         out += "SM\t";
         out += (char)('0' + i);
         out += '\t';
-        out += s->S(s->nodes[it.row].id);
+        out += s->S(s->nodes[(uint32_t)it.row].id);
         out += '\t';
         put_num(it.norm);
         out += '\t';
-        for (uint32_t k = 0; k < it.scores.size(); k++) {
+        for (uint32_t k = 0; k < n; k++) {
             if (k) out += ',';
-            out += it.scores.name[k];
+            out += kScorerNames[it.scorer[order[k]]];
             out += '=';
-            put_num(it.scores.val[k]);
+            put_num(it.score[order[k]]);
         }
         out += '\n';
     }
 }
 
-static std::string metrics_text(pe_stack* s, MetricAcc& acc) {
-    std::string out;
-    metrics_text_into(s, acc, out);
-    return out;
+// The last Select's maps (pe_last_metrics_bin) from an accumulator.
+static void metrics_set_last(pe_stack* s, MetricAcc& acc) {
+    s->m_counts.clear();
+    s->m_scores.clear();
+    metrics_bin_into(acc, s->m_counts, s->m_scores);
+    s->metrics_text_ok = false;
+    s->metrics_valid = true;
 }
 
 static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
@@ -5228,21 +5304,21 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                     const uint32_t fl = (ec >> 16) & 255u;
                     ScoreMeta sm;
                     sm.row = row;
-                    sm.scores.emplace_back("binpack", o[0]);
-                    if (a.dev_tw != 0.0) sm.scores.emplace_back("devices", o[1]);
+                    sm.scores.emplace_back(PE_SCORER_BINPACK, o[0]);
+                    if (a.dev_tw != 0.0) sm.scores.emplace_back(PE_SCORER_DEVICES, o[1]);
                     if (generic) {
-                        if (a.anti_aff) sm.scores.emplace_back("job-anti-affinity", o[2]);
-                        sm.scores.emplace_back("node-reschedule-penalty", (fl & 1u) ? -1.0 : 0.0);
-                        if (!has_aff) sm.scores.emplace_back("node-affinity", 0.0);
-                        else if (o[3] != 0.0) sm.scores.emplace_back("node-affinity", o[3]);
-                        if (o[4] != 0.0) sm.scores.emplace_back("allocation-spread", o[4]);
-                        if (fl & 2u) sm.scores.emplace_back("preemption", o[5]);
+                        if (a.anti_aff) sm.scores.emplace_back(PE_SCORER_JOB_ANTI_AFFINITY, o[2]);
+                        sm.scores.emplace_back(PE_SCORER_RESCHEDULE_PENALTY, (fl & 1u) ? -1.0 : 0.0);
+                        if (!has_aff) sm.scores.emplace_back(PE_SCORER_NODE_AFFINITY, 0.0);
+                        else if (o[3] != 0.0) sm.scores.emplace_back(PE_SCORER_NODE_AFFINITY, o[3]);
+                        if (o[4] != 0.0) sm.scores.emplace_back(PE_SCORER_ALLOCATION_SPREAD, o[4]);
+                        if (fl & 2u) sm.scores.emplace_back(PE_SCORER_PREEMPTION, o[5]);
                     }
                     sm.norm = o[6];
                     acc.heap.push(std::move(sm));
                 } else if (st == 2) {   // kExhausted: no preemption frees enough (ExhaustedNode(dim))
                     const uint32_t d = (ec >> 8) & 255u;
-                    acc.exhaust(s, row, d == pe::kTrCpu ? "cpu" : (d == pe::kTrMemory ? "memory" : "disk"));
+                    acc.exhaust(s, row, d == pe::kTrCpu ? "cpu" : (d == pe::kTrMemory ? "memory" : "disk"));   // literals
                 } else if (st != 3) {   // kSkipped (device preemption failed) records nothing
                     return s->fail(PE_EHIP, "k_evict_trace: outcome differs from the host walk");
                 }
@@ -5252,9 +5328,21 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             if (rc) return rc;
         }
     }
-    s->metrics_text = metrics_text(s, acc);
-    s->metrics_valid = true;
+    metrics_set_last(s, acc);
     return PE_OK;
+}
+
+static void spec_metrics_reset(pe_stack::Spec& sp) {
+    sp.mcounts.clear();
+    sp.mscores.clear();
+    sp.mcounts_off.assign(1, 0u);
+    sp.mscores_off.assign(1, 0u);
+}
+
+static void spec_metrics_push(pe_stack::Spec& sp, MetricAcc& acc) {
+    metrics_bin_into(acc, sp.mcounts, sp.mscores);
+    sp.mcounts_off.push_back((uint32_t)sp.mcounts.size());
+    sp.mscores_off.push_back((uint32_t)sp.mscores.size());
 }
 
 // AllocMetric maps of every record of a speculative run (§25): record k's
@@ -5318,9 +5406,7 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         HIP_TRY(s, hipStreamSynchronize(s->stream));
     }
     const double t2 = prof ? now_us() : 0.0;
-    sp.mtext.clear();
-    sp.mtext.reserve((size_t)sp.n_rec * 800u);
-    sp.mtext_off.assign(1, 0u);
+    spec_metrics_reset(sp);
     std::map<int, std::vector<uint32_t>> counts;
     size_t i = 0;
     for (uint32_t k = 0; k < sp.n_rec; k++) {
@@ -5328,13 +5414,13 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
             const int rc = metrics_outcome(s, g, a, rows[i], codes[i], &sc[i * 6], acc[k], counts);
             if (rc) return rc;
         }
-        metrics_text_into(s, acc[k], sp.mtext);
-        sp.mtext_off.push_back((uint32_t)sp.mtext.size());
+        spec_metrics_push(sp, acc[k]);
     }
     sp.metrics = true;
     if (prof)
-        std::fprintf(stderr, "spec_metrics: %u records, %zu traced rows: walk %.1f us, trace %.1f us, maps+text %.1f us "
-                             "(%zu B)\n", sp.n_rec, rows.size(), t1 - t0, t2 - t1, now_us() - t2, sp.mtext.size());
+        std::fprintf(stderr, "spec_metrics: %u records, %zu traced rows: walk %.1f us, trace %.1f us, maps %.1f us "
+                             "(%zu counts, %zu scores)\n", sp.n_rec, rows.size(), t1 - t0, t2 - t1, now_us() - t2,
+                     sp.mcounts.size(), sp.mscores.size());
     return PE_OK;
 }
 
@@ -7515,8 +7601,15 @@ extern "C" int pe_set_metrics(pe_stack* s, int on) {
 
 extern "C" int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap) {
     if (!s) return PE_EINVAL;
-    view_take(const_cast<pe_stack*>(s));   // Selects the caller served from the view: the last one's maps
+    pe_stack* m = const_cast<pe_stack*>(s);
+    view_take(m);   // Selects the caller served from the view: the last one's maps
     if (!s->metrics_valid) return PE_ESTATE;
+    if (!s->metrics_text_ok) {
+        m->metrics_text.clear();
+        metrics_text_into(s, s->m_counts.data(), s->m_counts.size(), s->m_scores.data(), s->m_scores.size(),
+                          m->metrics_text);
+        m->metrics_text_ok = true;
+    }
     if (buf && cap) {
         const size_t k = std::min(cap - 1, s->metrics_text.size());
         std::memcpy(buf, s->metrics_text.data(), k);
@@ -7524,6 +7617,33 @@ extern "C" int64_t pe_last_metrics(const pe_stack* s, char* buf, size_t cap) {
     }
     return (int64_t)s->metrics_text.size() + 1;
 }
+
+extern "C" int pe_last_metrics_bin(const pe_stack* s, const pe_metric_count** counts, uint32_t* n_counts,
+                                   const pe_metric_score** scores, uint32_t* n_scores) {
+    if (!s || !counts || !n_counts || !scores || !n_scores) return PE_EINVAL;
+    view_take(const_cast<pe_stack*>(s));
+    if (!s->metrics_valid) return PE_ESTATE;
+    *counts = s->m_counts.data();
+    *n_counts = (uint32_t)s->m_counts.size();
+    *scores = s->m_scores.data();
+    *n_scores = (uint32_t)s->m_scores.size();
+    return PE_OK;
+}
+
+extern "C" int64_t pe_metric_string(const pe_stack* s, uint32_t key, char* buf, size_t cap) {
+    if (!s) return PE_EINVAL;
+    if ((key & PE_METRIC_ENGINE_KEY) ? (key & ~PE_METRIC_ENGINE_KEY) >= s->mstrs.size() : key >= s->strs.size())
+        return PE_EINVAL;
+    const std::string& t = metric_string(s, key);
+    if (buf && cap) {
+        const size_t k = std::min(cap - 1, t.size());
+        std::memcpy(buf, t.data(), k);
+        buf[k] = 0;
+    }
+    return (int64_t)t.size() + 1;
+}
+
+extern "C" const char* pe_scorer_name(uint32_t scorer) { return scorer < 7 ? kScorerNames[scorer] : ""; }
 
 // ---- wrappers that log the chain's visits for EvalEligibility -----------------
 

@@ -111,6 +111,38 @@ def parse_metrics(text: str) -> Dict:
     return out
 
 
+_KIND_NAMES = {abi.PE_METRIC_CLASS_FILTERED: "ClassFiltered", abi.PE_METRIC_CONSTRAINT_FILTERED: "ConstraintFiltered",
+               abi.PE_METRIC_CLASS_EXHAUSTED: "ClassExhausted",
+               abi.PE_METRIC_DIMENSION_EXHAUSTED: "DimensionExhausted"}
+
+
+def decode_metrics(stack, counts, c0: int, c1: int, scores, s0: int, s1: int) -> Dict:
+    """Binary AllocMetric maps (pe_metric_count[c0:c1], pe_metric_score[s0:s1])
+    in parse_metrics' shape; keys resolved through pe_metric_string."""
+    out = {v: {} for v in _KIND_NAMES.values()}
+    out["ScoreMetaData"] = []
+    cache = getattr(stack, "_mkey_cache", None)
+    if cache is None:
+        cache = stack._mkey_cache = {}
+    for i in range(c0, c1):
+        e = counts[i]
+        k = cache.get(e.key)
+        if k is None:
+            k = cache[e.key] = stack.MetricString(e.key)
+        out[_KIND_NAMES[e.kind]][k] = int(e.count)
+    for i in range(s0, s1):
+        m = scores[i]
+        parts = {abi.SCORER_NAMES[m.scorer[j]]: float(m.score[j]) for j in range(m.n_scores)}
+        out["ScoreMetaData"].append((stack.nodes[m.row].id, float(m.norm), parts))
+    return out
+
+
+def view_metrics(stack, view, k: int) -> Dict:
+    """Record k's maps from the served-Select view (pe_spec_view.mcounts / mscores)."""
+    return decode_metrics(stack, view.mcounts, view.mcounts_off[k], view.mcounts_off[k + 1],
+                          view.mscores, view.mscores_off[k], view.mscores_off[k + 1])
+
+
 @dataclass
 class SelectOptions:
     """SelectOptions (stack.go:34-39); nodes are given as node IDs or rows."""
@@ -240,6 +272,30 @@ class _Stack:
         buf = C.create_string_buffer(int(need) + 1)
         fn(self._h, buf, len(buf))
         return parse_metrics(buf.value.decode())
+
+    def LastMetricsBin(self) -> Dict:
+        """The last Select's maps from their binary form (pe_last_metrics_bin),
+        in LastMetrics' shape: what the Go shim reads without parsing text."""
+        lib = self._lib
+        lib.pe_last_metrics_bin.restype = C.c_int
+        lib.pe_last_metrics_bin.argtypes = [C.c_void_p, C.POINTER(C.POINTER(abi.pe_metric_count)), abi.u32p,
+                                            C.POINTER(C.POINTER(abi.pe_metric_score)), abi.u32p]
+        c, sc = C.POINTER(abi.pe_metric_count)(), C.POINTER(abi.pe_metric_score)()
+        nc, ns = C.c_uint32(0), C.c_uint32(0)
+        self._check(lib.pe_last_metrics_bin(self._h, C.byref(c), C.byref(nc), C.byref(sc), C.byref(ns)))
+        return decode_metrics(self, c, 0, nc.value, sc, 0, ns.value)
+
+    def MetricString(self, key: int) -> str:
+        """pe_metric_string: the text of an AllocMetric key."""
+        fn = self._lib.pe_metric_string
+        fn.restype = C.c_int64
+        fn.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]
+        need = fn(self._h, key, None, 0)
+        if need < 0:
+            self._check(int(need))
+        buf = C.create_string_buffer(int(need) + 1)
+        fn(self._h, key, buf, len(buf))
+        return buf.value.decode()
 
     # -- EvalEligibility and iterator state (context.go:190-356) -------------
     def Eligibility(self, changed_only: bool = False) -> Dict:

@@ -34,7 +34,7 @@ def test_every_declared_symbol_is_exported():
 def test_abi_version():
     lib = C.CDLL(LIB)
     lib.pe_abi_version.restype = C.c_uint32
-    assert lib.pe_abi_version() == 8
+    assert lib.pe_abi_version() == 9
 
 
 STRUCTS = ["pe_strtab", "pe_attr", "pe_node_table", "pe_alloc_table", "pe_constraint", "pe_affinity",

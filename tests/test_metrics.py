@@ -294,11 +294,12 @@ def test_metrics_preempt_selects_cpu_memory():
 def _view_metrics_loop(nodes, allocs, job, perm, placements, tg=0, deviate=()):
     """The Go shim's zero-crossing path with metrics on: Selects and Commits
     from the served-Select view, each served record's maps read from the view
-    (pe_spec_view.metrics), the rest through C; every Select's result and
-    maps equal the oracle's (generic_sched.go:558, 587: Allocation.Metrics)."""
+    (pe_spec_view.mcounts / mscores, binary), the rest through C (both the
+    text and the binary maps); every Select's result and maps equal the
+    oracle's (generic_sched.go:558, 587: Allocation.Metrics)."""
     import ctypes as C
     from nomad_amd import abi
-    from nomad_amd.stack import GenericStack, parse_metrics
+    from nomad_amd.stack import GenericStack, view_metrics
     eng, ora = GenericStack(), OracleGenericStack()
     for st in (eng, ora):
         st.EnableMetrics()
@@ -314,11 +315,10 @@ def _view_metrics_loop(nodes, allocs, job, perm, placements, tg=0, deviate=()):
         ro = ora.SelectRaw(tg)
         mo = ora.LastMetrics()
         if v.n_rec and v.tg_index == tg and v.served == v.confirmed and v.served < v.n_rec:
-            assert v.metrics and v.metrics_off, "served records carry no maps"
+            assert v.mcounts_off and v.mscores_off, "served records carry no maps"
             i = v.served
             r = v.recs[i]
-            a, b = v.metrics_off[i], v.metrics_off[i + 1]
-            me = parse_metrics(C.string_at(v.metrics + a, b - a).decode())
+            me = view_metrics(eng, v, i)
             v.served += 1
             if r.row < 0:
                 v.confirmed += 1
@@ -327,6 +327,7 @@ def _view_metrics_loop(nodes, allocs, job, perm, placements, tg=0, deviate=()):
         else:
             re = eng.SelectRaw(tg)
             me = eng.LastMetrics()
+            assert eng.LastMetricsBin() == me, k
             got = (re.row, re.nodes_evaluated, re.nodes_filtered, re.nodes_exhausted)
         assert got == (ro.row, ro.nodes_evaluated, ro.nodes_filtered, ro.nodes_exhausted), k
         assert me == mo, (k, me, mo)

@@ -45,12 +45,15 @@ struct dropin_api {
     int (*preempted_of)(const void*, uint32_t, uint32_t*, uint32_t);
     pe_spec_view* (*spec_view_get)(void*);   // null: every Select and Commit crosses
     pe_system_view* (*system_view_get)(void*);   // null: every per-node triple crosses
-    int64_t (*last_metrics)(const void*, char*, size_t);   // AllocMetric text of the last Select
+    int64_t (*last_metrics)(const void*, char*, size_t);   // AllocMetric text of the last Select (oracle)
+    int (*last_metrics_bin)(const void*, const pe_metric_count**, uint32_t*, const pe_metric_score**,
+                            uint32_t*);   // the engine's binary maps (null: the text)
 };
 
 // With metrics on, every Select's AllocMetric maps are copied out as the shim
-// fills Allocation.Metrics (generic_sched.go:558, 587): from the served
-// record's text in the view, else through last_metrics.
+// fills Allocation.Metrics (generic_sched.go:558, 587): the served record's
+// binary maps from the view, else through last_metrics_bin (engine) or the
+// text of last_metrics (oracle).
 static int g_metrics = 0;
 void dropin_use_metrics(int on) { g_metrics = on; }
 static uint64_t g_metric_bytes = 0;
@@ -60,15 +63,31 @@ uint64_t dropin_metric_bytes(int reset) {
     return x;
 }
 static char g_mbuf[1 << 16];
+static void copy_bin(const pe_metric_count* c, uint32_t nc, const pe_metric_score* sc, uint32_t ns) {
+    size_t a = (size_t)nc * sizeof(*c), b = (size_t)ns * sizeof(*sc);
+    if (a > sizeof(g_mbuf)) a = sizeof(g_mbuf);
+    if (b > sizeof(g_mbuf) - a) b = sizeof(g_mbuf) - a;
+    std::memcpy(g_mbuf, c, a);
+    std::memcpy(g_mbuf + a, sc, b);
+    g_metric_bytes += (uint64_t)nc * sizeof(*c) + (uint64_t)ns * sizeof(*sc);
+}
 static void metrics_from_view(const pe_spec_view* v, uint32_t k) {
-    if (!g_metrics || !v->metrics) return;
-    const uint32_t a = v->metrics_off[k], n = v->metrics_off[k + 1] - a;
-    const uint32_t c = n < sizeof(g_mbuf) ? n : (uint32_t)sizeof(g_mbuf);
-    std::memcpy(g_mbuf, v->metrics + a, c);
-    g_metric_bytes += n;
+    if (!g_metrics || !v->mcounts) return;
+    const uint32_t a = v->mcounts_off[k], b = v->mscores_off[k];
+    copy_bin(v->mcounts + a, v->mcounts_off[k + 1] - a, v->mscores + b, v->mscores_off[k + 1] - b);
 }
 static int metrics_from_c(const dropin_api* api, void* h) {
-    if (!g_metrics || !api->last_metrics) return 0;
+    if (!g_metrics) return 0;
+    if (api->last_metrics_bin) {
+        const pe_metric_count* c;
+        const pe_metric_score* sc;
+        uint32_t nc, ns;
+        const int rc = api->last_metrics_bin(h, &c, &nc, &sc, &ns);
+        if (rc) return rc;
+        copy_bin(c, nc, sc, ns);
+        return 0;
+    }
+    if (!api->last_metrics) return 0;
     const int64_t n = api->last_metrics(h, g_mbuf, sizeof(g_mbuf));
     if (n < 0) return (int)n;
     g_metric_bytes += (uint64_t)n;

@@ -20,7 +20,7 @@ _lib = None
 class dropin_api(C.Structure):
     _fields_ = [(name, C.c_void_p) for name in
                 ("reset_plan", "set_job", "set_nodes", "select", "commit", "commit_preempt", "preempted_of",
-                 "spec_view_get", "system_view_get", "last_metrics")]
+                 "spec_view_get", "system_view_get", "last_metrics", "last_metrics_bin")]
 
 
 def load():
