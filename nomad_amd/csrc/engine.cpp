@@ -4936,6 +4936,10 @@ struct ScoreHeap {
         }
         return i > i0;
     }
+    // whether push(m) changes the heap: a full heap ignores an item not above
+    // its minimum (and the closing up(len-1) of heap.Push is then a no-op, the
+    // heap property holding)
+    bool enters(double norm) const { return items.size() < cap || norm > items[0].norm; }
     void push(ScoreMeta m) {   // heap.Push → ScoreHeap.Push (+ heap.Fix) then up(len-1)
         if (items.capacity() < cap) items.reserve(cap);
         if (items.size() < cap) {
@@ -4999,7 +5003,7 @@ struct MetricAcc {
 // pass go to `rows` for k_trace. `log` (or null) receives the memo changes.
 static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
                          uint32_t evaluated, MetricAcc& acc, std::vector<uint32_t>& rows,
-                         std::vector<MemoDelta>* log = nullptr) {
+                         std::vector<MemoDelta>* log = nullptr, std::vector<uint8_t>* pass = nullptr) {
     const size_t m = order.size();
     if (s->ref_job_memo.size() != s->ncls) s->ref_job_memo.assign(s->ncls, -1);
     auto& rt = s->ref_tg_memo[g.name];
@@ -5039,8 +5043,12 @@ static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& or
                 set_tg(c, why ? 0 : 1);
             }
         }
-        if (why) acc.filter(s, row, why == kIneligible ? ineligible : s->mkey_p(why));
-        else rows.push_back(row);
+        if (why) {
+            acc.filter(s, row, why == kIneligible ? ineligible : s->mkey_p(why));
+        } else {
+            rows.push_back(row);
+            if (pass) (*pass)[(start + k) % m] = 1;
+        }
     }
 }
 
@@ -5051,6 +5059,7 @@ static int metrics_outcome(pe_stack* s, TgPlan& g, const pe::Ask& a, uint32_t ro
     const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
     switch (code & 255u) {
         case pe::kTrOption: {   // ScoreNode calls in chain order, then the NormScore push
+            if (!acc.heap.enters(o[5])) break;
             ScoreMeta sm;
             sm.row = row;
             sm.scores.emplace_back(PE_SCORER_BINPACK, o[0]);
@@ -5217,12 +5226,44 @@ static void metrics_set_last(pe_stack* s, MetricAcc& acc) {
     s->metrics_valid = true;
 }
 
+// Whole-list windows of one replay (spec_metrics_replay): once a walk over
+// the whole list changes no memo entry, every node's verdict no longer depends
+// on the visit order, so later whole-list walks take its filter counts and its
+// passing positions (rotated to their start) instead of walking again.
+struct WalkCache {
+    bool valid = false;
+    MetricCounts cf, kf;
+    std::vector<uint8_t> pass;   // per visit position
+};
+
 static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
-                           uint32_t evaluated, const pe_select_options* opts, bool evict = false) {
+                           uint32_t evaluated, const pe_select_options* opts, bool evict = false,
+                           std::vector<MemoDelta>* log = nullptr, WalkCache* wc = nullptr) {
     s->metrics_valid = false;
     MetricAcc acc;
     std::vector<uint32_t> rows;
-    metrics_walk(s, g, order, start, evaluated, acc, rows);
+    const size_t m = order.size();
+    const bool whole = wc && m && evaluated == m;
+    if (whole && wc->valid) {
+        acc.cf = wc->cf;
+        acc.kf = wc->kf;
+        rows.reserve(m);
+        for (uint32_t k = 0; k < m; k++) {
+            const uint32_t p = (uint32_t)((start + k) % m);
+            if (wc->pass[p]) rows.push_back(order[p]);
+        }
+    } else {
+        const size_t l0 = log ? log->size() : 0;
+        if (whole) wc->pass.assign(m, 0);
+        metrics_walk(s, g, order, start, evaluated, acc, rows, log, whole ? &wc->pass : nullptr);
+        const bool changed = log && log->size() != l0;
+        if (wc && (changed || !whole)) wc->valid = wc->valid && !changed;
+        if (whole && !changed && log) {
+            wc->valid = true;
+            wc->cf = acc.cf;
+            wc->kf = acc.kf;
+        }
+    }
     if (!rows.empty()) {
         HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
         HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
@@ -5301,6 +5342,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                                                               "network devices, reserved cores)");
                 if (st == 0) {   // option (kOption), preempting or not
                     const double* o = &named[i * 7];
+                    if (!acc.heap.enters(o[6])) continue;
                     const uint32_t fl = (ec >> 16) & 255u;
                     ScoreMeta sm;
                     sm.row = row;
@@ -5421,6 +5463,86 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         std::fprintf(stderr, "spec_metrics: %u records, %zu traced rows: walk %.1f us, trace %.1f us, maps %.1f us "
                              "(%zu counts, %zu scores)\n", sp.n_rec, rows.size(), t1 - t0, t2 - t1, now_us() - t2,
                      sp.mcounts.size(), sp.mscores.size());
+    return PE_OK;
+}
+
+static int spec_copy(pe_stack* s, TgPlan& g, bool to_ckpt);
+
+// AllocMetric maps of the runs the batched trace cannot rebuild — evicting
+// runs (a record's state depends on earlier evictions and on the plan's
+// preemption counts), full passes and property sets (spread boosts and
+// distinct_property counts move with every commit): the records' Selects are
+// re-traced one by one (compute_metrics: the FeasibilityWrapper walk with the
+// reference memo, k_trace / k_evict_trace) against the state each saw — the
+// run's checkpoint plus the earlier records' evictions and commits, replayed
+// in order. The device ends where the run left it (checkpoint + every record).
+// Whole-list windows (full passes, the nil Selects of a saturated cluster)
+// reuse one walk once the memo has settled (WalkCache).
+static int spec_metrics_replay(pe_stack* s, TgPlan& g, uint32_t off0) {
+    static const bool prof = std::getenv("PE_METRICS_PROF") != nullptr;
+    const double t0 = prof ? now_us() : 0.0;
+    pe_stack::Spec& sp = s->spec;
+    auto& rt = s->ref_tg_memo[g.name];
+    if (s->ref_job_memo.size() != s->ncls) s->ref_job_memo.assign(s->ncls, -1);
+    if (rt.size() != s->ncls) rt.assign(s->ncls, -1);
+    sp.memo_job0 = s->ref_job_memo;
+    sp.memo_tg0 = rt;
+    sp.memo_log.clear();
+    sp.memo_off.assign(1, 0u);
+    spec_metrics_reset(sp);
+    int rc = spec_copy(s, g, false);   // the run's starting state (host core mirror included)
+    if (rc) return rc;
+    const pe::Ask a = ask_for(s, g);
+    const pe::NodeSoA soa = soa_of(s);
+    const pe::TgTables t = tables_of(g);
+    pe_select_options pre;
+    std::memset(&pre, 0, sizeof(pre));
+    pre.preempt = 1;
+    WalkCache wc;
+    const uint32_t words = s->evict_words;
+    std::vector<uint32_t> mask;
+    uint32_t off = off0;
+    for (uint32_t k = 0; k < sp.n_rec; k++) {
+        pe_ranked_node r;
+        if (sp.compact) widen_rec(sp.crecs[k], &r);
+        else r = sp.recs[k];
+        const bool preempt = sp.evict && (sp.rflags[k] & PE_SPEC_PREEMPT) != 0;
+        rc = compute_metrics(s, g, s->visit, off, r.nodes_evaluated, preempt ? &pre : nullptr, preempt, &sp.memo_log,
+                             &wc);
+        if (rc) return rc;
+        sp.memo_off.push_back((uint32_t)sp.memo_log.size());
+        sp.mcounts.insert(sp.mcounts.end(), s->m_counts.begin(), s->m_counts.end());
+        sp.mscores.insert(sp.mscores.end(), s->m_scores.begin(), s->m_scores.end());
+        sp.mcounts_off.push_back((uint32_t)sp.mcounts.size());
+        sp.mscores_off.push_back((uint32_t)sp.mscores.size());
+        off = r.new_offset;
+        const bool placement = sp.evict ? sp.rec_place[k] != PE_NONE : k < sp.placed;
+        if (!placement || r.row < 0) continue;
+        const uint32_t row = (uint32_t)r.row;
+        if (const uint32_t np = spec_rec_npre(sp, k)) {   // Plan.AppendPreemptedAlloc, then the placement
+            const uint32_t b = s->h_node_alloc_off[row];
+            mask.assign(words, 0u);
+            for (uint32_t j = 0; j < np; j++) {
+                const uint32_t ai = spec_rec_pre(sp, k)[j];
+                core_hold(s, ai, false);
+                const uint32_t q = s->alloc_slot[ai] - b;
+                if (q >= 32u * words) return s->fail(PE_EINTERNAL, "replayed preemption past the eviction width");
+                mask[q >> 5] |= 1u << (q & 31u);
+            }
+            pe::PreemptArgs P = preempt_args(s, g);
+            HIP_TRY(s, upload_s(s, s->d_pre_mask, mask));
+            HIP_TRY_STATE(s, pe_launch_commit_preempt(&P, row, s->d_pre_mask.as<uint32_t>(),
+                                                      s->d_preempted.as<uint8_t>(), s->d_pcount.as<uint32_t>(),
+                                                      s->d_dev_free.as<uint32_t>(), s->stream));
+        }
+        HIP_TRY_STATE(s, pe_launch_commit(&soa, &t, &a, row, pack_offers(&r), s->stream));
+    }
+    HIP_TRY(s, hipStreamSynchronize(s->stream));
+    s->metrics_valid = false;
+    sp.metrics = true;
+    if (prof)
+        std::fprintf(stderr, "spec_metrics_replay: %u records: %.1f us (%zu counts, %zu scores)\n", sp.n_rec,
+                     now_us() - t0, sp.mcounts.size(), sp.mscores.size());
     return PE_OK;
 }
 
@@ -6367,15 +6489,20 @@ static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* op
     if (s->tgs[tgi]->ask.cores > 0) return false;   // the rollback kernel does not return reserved cores
     for (size_t k = 0; k < s->tgs.size(); k++)   // commits would rebuild a sibling's collision counts
         if (k != tgi && s->tgs[k]->name == s->tgs[tgi]->name) return false;
-    if (s->metrics_on) {
-        // the records' maps are traced against the run's starting state plus
-        // earlier placements (spec_metrics): windowed runs, no property sets,
-        // no evictions
-        TgPlan& g = *s->tgs[tgi];
-        if (s->cfg.preempt || tg_full_scan(s, g) || !g.distinct_props.empty()) return false;   // (sets may be unbuilt)
-        for (auto& c : s->job_constraints)
-            if (c.op == "distinct_property") return false;
-    }
+    // with AllocMetric on, the records' maps come from the batched trace
+    // (spec_metrics) or the replay (spec_metrics_replay); static port asks
+    // read host port mirrors that hold the run's end state: per Select
+    if (s->metrics_on && has_static(*s->tgs[tgi])) return false;
+    return true;
+}
+
+// Whether a run's maps come from one batched trace against the checkpoint
+// (windowed, no evictions, no property sets: a record's state differs from
+// the run's start by earlier placements alone), else from the replay.
+static bool spec_metrics_batched(pe_stack* s, TgPlan& g) {
+    if (s->spec.evict || tg_full_scan(s, g) || !g.distinct_props.empty() || !g.psets.empty()) return false;
+    for (auto& c : s->job_constraints)
+        if (c.op == "distinct_property") return false;
     return true;
 }
 
@@ -6690,7 +6817,7 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
         s->pre_overflow.clear();
     }
     if (s->metrics_on) {
-        const int mrc = spec_metrics(s, g, off0);
+        const int mrc = spec_metrics_batched(s, g) ? spec_metrics(s, g, off0) : spec_metrics_replay(s, g, off0);
         if (mrc) {   // nothing served yet: the device and the memo go back to the run's start
             sp.active = true;
             sp.served = sp.confirmed = 0;

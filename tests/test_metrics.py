@@ -374,3 +374,145 @@ def test_metrics_served_from_the_view_devices():
     job = synth.job_c5(150)
     from_view, _ = _view_metrics_loop(nodes, allocs, job, synth.shuffle(len(nodes), 5), 150)
     assert from_view >= 100, from_view
+
+
+def _view_metrics_protocol(eng, ora, count, preempt=False, tg=0, deviate=None):
+    """computePlacements' loop (Select, the Preempt retry on nil when
+    preemption is on, Commit with the preempted set) with AllocMetric on:
+    every Select answered from the served-Select view when it can be (its
+    maps from the view's binary arrays), else through C; every answer and
+    its maps equal the oracle's. deviate(i, row) -> another row to commit."""
+    import ctypes as C
+    from nomad_amd import abi
+    from nomad_amd.stack import SelectOptions, view_metrics
+    from tests.test_dropin import _key
+    from tests.test_spec_view import _rec_key
+    fn = eng._lib.pe_spec_view_get
+    fn.restype = C.POINTER(abi.pe_spec_view)
+    fn.argtypes = [C.c_void_p]
+    v = fn(eng._h).contents
+    stats = {"view": 0, "c": 0, "evicting": 0}
+
+    def ora_sel(opts):
+        r = ora.SelectRaw(tg, opts)
+        return (_key(r) if r.row >= 0 else ("nil", r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted,
+                                            r.new_offset)), r.row, tuple(r.preempted), ora.LastMetrics()
+
+    def eng_sel(opts):
+        pre = bool(opts is not None and opts.preempt)
+        if (v.n_rec and v.tg_index == tg and v.served == v.confirmed and v.served < v.n_rec
+                and bool(v.recs[v.served].flags & abi.PE_SPEC_PREEMPT) == pre):
+            assert v.mcounts_off and v.mscores_off, "served records carry no maps"
+            k = v.served
+            r = v.recs[k]
+            m = view_metrics(eng, v, k)
+            v.served += 1
+            stats["view"] += 1
+            p = tuple(v.pre_allocs[i] for i in range(v.pre_off[k], v.pre_off[k + 1])) if v.pre_off else ()
+            if r.row < 0:
+                v.confirmed += 1
+                return ("nil", r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted, r.new_offset), -1, (), m
+            return _rec_key(r, p), r.row, p, m
+        stats["c"] += 1
+        r = eng.SelectRaw(tg, opts)
+        m = eng.LastMetricsBin()
+        assert m == eng.LastMetrics()
+        return (_key(r) if r.row >= 0 else ("nil", r.nodes_evaluated, r.nodes_filtered, r.nodes_exhausted,
+                                            r.new_offset)), r.row, tuple(r.preempted), m
+
+    def eng_commit(row, pre):
+        if (v.n_rec and v.tg_index == tg and v.served == v.confirmed + 1 and v.recs[v.served - 1].row == row
+                and tuple(pre) == (tuple(v.pre_allocs[i] for i in range(v.pre_off[v.served - 1],
+                                                                       v.pre_off[v.served]))
+                                   if v.pre_off else ())):
+            v.confirmed += 1
+        else:
+            eng.Commit(tg, row, pre)
+
+    answers = 0
+    for i in range(count):
+        for opts in ((None, SelectOptions(preempt=True)) if preempt else (None,)):
+            ke, re_, pe_, me = eng_sel(opts)
+            ko, ro, po, mo = ora_sel(opts)
+            answers += 1
+            assert ke[:7] == ko[:7] and pe_ == po, ("answer %d" % answers, ke, ko)
+            assert me == mo, ("answer %d maps" % answers, me, mo)
+            if ro >= 0:
+                break
+        if ro < 0:
+            break
+        stats["evicting"] += bool(po)
+        alt = deviate(i, ro) if deviate else None
+        if alt is not None and alt != ro:
+            eng_commit(alt, ())
+            ora.Commit(tg, alt)
+        else:
+            eng_commit(ro, po)
+            ora.Commit(tg, ro, po)
+    return stats
+
+
+def _metrics_pair(nodes, allocs, job, perm, config=None):
+    from nomad_amd.stack import GenericStack
+    eng, ora = GenericStack(config=config), OracleGenericStack(config=config)
+    for st in (eng, ora):
+        st.EnableMetrics()
+        st.SetState(nodes, allocs)
+        st.SetJob(job)
+        st.SetNodes(perm)
+    return eng, ora
+
+
+@pytest.mark.gpu
+def test_metrics_view_c3_full_scan():
+    """C3 at its bench shape (10k nodes, spread + affinity + semver/regexp):
+    full-pass runs with AllocMetric on, every record's maps from the view."""
+    nodes, allocs = synth.cluster_c3(10000, seed=7)
+    eng, ora = _metrics_pair(nodes, allocs, synth.job_c3(300), synth.shuffle(10000, 17))
+    st = _view_metrics_protocol(eng, ora, 300)
+    assert st["view"] >= 280, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dev", [False, True])
+def test_metrics_view_preempt_retry(dev):
+    """Evicting runs (preemption on, a saturated C5-shaped cluster): the plain
+    nils and the Preempt options with their maps (preemption scores
+    included) from the view, with and without deviating commits."""
+    from nomad_amd.structs import SchedulerConfig
+    nodes, allocs = synth.cluster_c5(3000, seed=5, busy=0.97)
+    perm = synth.shuffle(len(nodes), 77)
+    eng, ora = _metrics_pair(nodes, allocs, synth.job_c5(250), perm, SchedulerConfig(preempt_service=True))
+    deviate = (lambda i, row: int(perm[(i * 13) % len(perm)]) if i % 41 == 17 else None) if dev else None
+    st = _view_metrics_protocol(eng, ora, 250, preempt=True, deviate=deviate)
+    assert st["evicting"] >= 20 and st["view"] >= 200, st
+
+
+@pytest.mark.gpu
+def test_metrics_view_c5_bench_shape_prefix():
+    """C5 at its bench shape (50k nodes, 99 % of the GPU nodes busy): the
+    evaluation's first 400 placements (the free instances, then the first
+    evicting placements), every answer's maps equal to the oracle's."""
+    from nomad_amd.structs import SchedulerConfig
+    nodes, allocs = synth.cluster_c5(50000, seed=5, busy=0.99)
+    eng, ora = _metrics_pair(nodes, allocs, synth.job_c5(1000), synth.shuffle(50000, 77),
+                             SchedulerConfig(preempt_service=True))
+    st = _view_metrics_protocol(eng, ora, 400, preempt=True)
+    assert st["evicting"] >= 10, st
+
+
+@pytest.mark.gpu
+def test_metrics_view_distinct_property_and_spread():
+    """Property sets (a job-level distinct_property and a spread): replayed
+    runs, maps from the view."""
+    from nomad_amd.structs import Spread
+    nodes, allocs = synth.cluster_c2(2000, seed=12)
+    for i, nd in enumerate(nodes):
+        nd.meta["rack"] = "r%d" % (i % 90)
+        nd.compute_class()
+    job = synth.job_c2(120)
+    job.constraints.append(Constraint("${meta.rack}", "2", "distinct_property"))
+    job.task_groups[0].spreads = [Spread("${node.datacenter}", 50, [])]
+    eng, ora = _metrics_pair(nodes, allocs, job, synth.shuffle(len(nodes), 4))
+    st = _view_metrics_protocol(eng, ora, 120)
+    assert st["view"] >= 100, st
