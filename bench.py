@@ -346,6 +346,47 @@ def _drop_in(st, job, perm, count, preempt=False, reps=3):
     return float(np.median(secs[1:])), placed, np.array(rows), info
 
 
+def _metrics_leg(st, job, perm, count, preempt=False, reps=2):
+    """The same drop-in evaluation with AllocMetric on (pe_set_metrics): every
+    Select's maps copied out by the C loop (the served record's binary maps
+    from the view, else pe_last_metrics_bin), as the shim fills
+    Allocation.Metrics (generic_sched.go:558, 587)."""
+    from tools import dropin
+    st.EnableMetrics(True)
+    dropin.use_metrics(True)
+    dropin.metric_bytes(reset=True)
+    try:
+        wall, placed, _, info = _drop_in(st, job, perm, count, preempt=preempt, reps=reps + 1)
+    finally:
+        dropin.use_metrics(False)
+        st.EnableMetrics(False)
+    return {"placements_per_s": placed / wall, "wall_ms": wall * 1e3, "placements": int(placed),
+            "metric_bytes_per_eval": dropin.metric_bytes(reset=True) / (reps + 1),
+            "from_view_per_eval": info["from_view_per_eval"]}
+
+
+def _oracle_metrics_rate(make, job, perm, count, budget_s, preempt=False):
+    """The oracle with AllocMetric on through the same C caller loop (every
+    Select's maps copied out as text): the evaluation's first k placements, k
+    grown until the sample takes about budget_s / 4."""
+    from tools import dropin
+    o = make()
+    o.EnableMetrics(True)
+    dropin.use_metrics(True)
+    try:
+        k, dt, op = 8, 0.0, 0
+        while True:
+            op, _, _, dt, _ = dropin.run(o, job, np.asarray(perm, dtype=np.uint32)[None, :], k, preempt=preempt)
+            if dt >= budget_s / 4 or op < k or k >= count:
+                break
+            k = min(count, k * 4)
+    finally:
+        dropin.use_metrics(False)
+    return {"value": op / dt, "unit": "placements/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
+            "sample": "the first %d placements of the same evaluation with AllocMetric on, through the same C "
+                      "caller loop (maps copied out as text), %.2f s, 1 thread" % (op, dt)}
+
+
 def section_c3(device, cpu_s):
     """C3: spread (dc1 50 % / dc2 30 %) + node affinity + semver / regexp
     constraints, count=1000 on 10k nodes: limit MaxInt32, so every placement is
@@ -370,6 +411,7 @@ def section_c3(device, cpu_s):
     # the unchanged caller: the same evaluation through Select / Commit from
     # the C loop, answered by the speculative runs and the served-Select view
     d_wall, d_placed, d_rows, d_info = _drop_in(st, job, perm, 1000)
+    m_on = _metrics_leg(st, job, perm, 1000)
     st.close()
     if d_placed != placed or not np.array_equal(d_rows[:placed], rows):
         raise RuntimeError("C3 drop-in placements differ from pe_place's")
@@ -410,7 +452,17 @@ def section_c3(device, cpu_s):
                                "sample": "the first %d placements of the same evaluation through the same C caller "
                                          "loop (ResetPlan + SetJob + SetNodes + Select / Commit), %.2f s, 1 thread"
                                          % (op, dt)}
+        m_on["cpu_baseline"] = _oracle_metrics_rate(
+            lambda: _oracle_generic(nodes, allocs), job, perm, 1000, cpu_s)
+    out["metrics_on"] = m_on
     return out
+
+
+def _oracle_generic(nodes, allocs, config=None):
+    from oracle.oracle import OracleGenericStack
+    o = OracleGenericStack(config=config)
+    o.SetState(nodes, allocs)
+    return o
 
 
 def section_c4(device, rank, world, pg, cpu_s):
@@ -495,16 +547,40 @@ def section_c4_drop_in(device, cpu_s):
             crossing.append(dropin.system_loop(st, 0, rows)[3])
     finally:
         dropin.use_view(True)
+    # with AllocMetric on: every node's maps (scheduler_system.go:334-337),
+    # assembled from the view's per-row entries (or pe_last_metrics_bin after
+    # a crossing)
+    st.EnableMetrics(True)
+    dropin.use_metrics(True)
+    dropin.metric_bytes(reset=True)
+    m_times = []
+    dropin.view_served(reset=True)
+    try:
+        for i in range(3):
+            st.ResetPlan()
+            st.SetJob(job)
+            m_times.append(dropin.system_loop(st, 0, rows)[3])
+    finally:
+        dropin.use_metrics(False)
+        st.EnableMetrics(False)
+    m_bytes = dropin.metric_bytes(reset=True) / 3
+    m_from_view = dropin.view_served(reset=True) / 3
     st.close()
     wall = float(np.median(times[1:]))
     wall_x = float(np.median(crossing[1:]))
+    wall_m = float(np.median(m_times[1:]))
     out = {"workload": "C4 caller protocol: mock.SystemJob on %d nodes, SetNodes([node]) + Select + Commit per "
                        "node from a C loop (one evaluation), the triples the served system-Select view covers "
                        "answered from it" % n,
            "placed": int(placed), "nodes_per_s": n / wall, "wall_ms": wall * 1e3, "cache_kernel_ms": kms,
            "cache_passes": int(stats[0]), "served_selects": int(stats[1]), "from_view_per_eval": from_view,
            "ms_per_eval_by_phase": phases,
-           "nodes_per_s_crossing": n / wall_x, "wall_ms_crossing": wall_x * 1e3}
+           "nodes_per_s_crossing": n / wall_x, "wall_ms_crossing": wall_x * 1e3,
+           "metrics_on": {"nodes_per_s": n / wall_m, "wall_ms": wall_m * 1e3, "metric_bytes_per_eval": m_bytes,
+                          "from_view_per_eval": m_from_view,
+                          "note": "the served system-Select view with per-row metric entries (the caller "
+                                  "assembles each Select's maps, the memo of failed classes included); the cache "
+                                  "pass adds one k_trace over the snapshot and the entries' host build"}}
     if cpu_s > 0:
         from oracle.oracle import OracleSystemStack
         o = OracleSystemStack()
@@ -514,7 +590,73 @@ def section_c4_drop_in(device, cpu_s):
         out["cpu_baseline"] = {"value": n / dt, "unit": "nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
                                "sample": "the same C caller loop over the same %d-node cluster and list in %.3f s, "
                                          "1 thread" % (n, dt)}
+        o.ResetPlan()
+        o.SetJob(job)
+        o.EnableMetrics(True)
+        dropin.use_metrics(True)
+        try:
+            _, _, _, dtm = dropin.system_loop(o, 0, rows)
+        finally:
+            dropin.use_metrics(False)
+        out["metrics_on"]["cpu_baseline"] = {
+            "value": n / dtm, "unit": "nodes/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
+            "sample": "the same C caller loop with AllocMetric on (maps copied out as text), %d nodes in %.3f s, "
+                      "1 thread" % (n, dtm)}
     return out
+
+
+def _c5_oracle_window(nodes, allocs, job, perm, cfg, rows, recs, placed, budget_s, min_evict, min_n,
+                      metrics=False):
+    """The C5 evaluation on the oracle through the caller's protocol (Select,
+    the Preempt retry on nil, Commit with the preempted set), timed over one
+    contiguous window from the evaluation's middle. The oracle pays, for every
+    node BinPack visits, a walk over all of the plan's preemptions
+    (rank.go:240-245 collects Plan.NodePreemptions for SetPreemptions on every
+    option), so a placement's cost grows linearly with the placements before
+    it (17 ms at the start, 1.8 s at the end on the build container,
+    profiles/r05/c5_oracle_timing.json): the window's mean per placement is
+    the evaluation's mean under linear growth. The engine's records before
+    the window are replayed into the oracle's plan untimed (bit-identical to
+    the oracle's own: tests/test_full_size.py)."""
+    from oracle.oracle import OracleGenericStack
+    from nomad_amd.stack import SelectOptions
+    o = OracleGenericStack(config=cfg)
+    o.SetState(nodes, allocs)
+    o.SetJob(job)
+    lim = o.SetNodes(perm)
+    j0 = placed // 2 - 60
+    for i in range(j0):
+        o.Commit(0, int(rows[i]), [int(x) for x in recs["preempted"][i][:int(recs["n_preempted"][i])]])
+    o.SetCursor(int(recs["new_offset"][j0 - 1]), lim, tg=0)   # where those Selects left the iterator
+    if metrics:
+        o.EnableMetrics(True)
+    ts, kinds = [], []
+    m = None
+    t0 = time.perf_counter()
+    j = j0
+    while j < placed and (sum(kinds) < min_evict or len(ts) < min_n) and time.perf_counter() - t0 < budget_s:
+        t1 = time.perf_counter()
+        r = o.Select(0)
+        m = o.LastMetrics() if metrics else None   # Allocation.Metrics of the plain Select
+        if r is None:
+            r = o.Select(0, SelectOptions(preempt=True))
+            m = o.LastMetrics() if metrics else None
+        if r is None:
+            break
+        o.Commit(0, r.row, r.preempted)
+        ts.append(time.perf_counter() - t1)
+        kinds.append(bool(r.preempted))
+        j += 1
+    del m
+    mean = float(np.mean(ts)) if ts else 0.0
+    return {"value": 1.0 / mean if mean > 0 else 0.0, "unit": "placements/s", "cores": 1, "kind": "port",
+            "cpu": cpu_model(),
+            "sample": "placements %d-%d of this evaluation (%d evicting, %d plain) on the oracle through the "
+                      "caller's loop%s, 1 thread, after its first %d records were replayed untimed; %.1f s, "
+                      "%.0f ms per placement (the evaluation's mean: a placement's cost grows linearly with the "
+                      "plan's preemptions, rank.go:240-245)"
+                      % (j0, j - 1, sum(kinds), len(kinds) - sum(kinds), " with AllocMetric on" if metrics else "",
+                         j0, float(np.sum(ts)), mean * 1e3)}
 
 
 def section_c5(device, cpu_s):
@@ -545,6 +687,7 @@ def section_c5(device, cpu_s):
     # preempted set) from the C loop, answered by the speculative runs and the
     # served-Select view
     d_wall, d_placed, d_rows, d_info = _drop_in(st, job, perm, 1000, preempt=True)
+    m_on = _metrics_leg(st, job, perm, 1000, preempt=True, reps=1)
     st.close()
     if d_placed != placed or not np.array_equal(d_rows[:placed], rows[:placed]):
         raise RuntimeError("C5 drop-in placements differ from pe_place's")
@@ -571,39 +714,11 @@ def section_c5(device, cpu_s):
         # per placement is the evaluation's mean under linear growth), after
         # the engine's records before it are replayed into the oracle's plan
         # untimed (bit-identical to the oracle's own: tests/test_full_size.py).
-        from oracle.oracle import OracleGenericStack
-        from nomad_amd.stack import SelectOptions
-        o = OracleGenericStack(config=cfg)
-        o.SetState(nodes, allocs)
-        o.SetJob(job)
-        lim = o.SetNodes(perm)
-        j0 = placed // 2 - 60
-        for i in range(j0):
-            o.Commit(0, int(rows[i]), [int(x) for x in recs["preempted"][i][:int(recs["n_preempted"][i])]])
-        o.SetCursor(int(recs["new_offset"][j0 - 1]), lim, tg=0)   # where those Selects left the iterator
-        ts, kinds = [], []
-        t0 = time.perf_counter()
-        j = j0
-        while j < placed and (sum(kinds) < 100 or len(ts) < 120) and time.perf_counter() - t0 < cpu_s:
-            t1 = time.perf_counter()
-            r = o.Select(0)
-            if r is None:
-                r = o.Select(0, SelectOptions(preempt=True))
-            if r is None:
-                break
-            o.Commit(0, r.row, r.preempted)
-            ts.append(time.perf_counter() - t1)
-            kinds.append(bool(r.preempted))
-            j += 1
-        mean = float(np.mean(ts)) if ts else 0.0
-        out["cpu_baseline"] = {"value": 1.0 / mean if mean > 0 else 0.0, "unit": "placements/s", "cores": 1,
-                               "kind": "port", "cpu": cpu_model(),
-                               "sample": "placements %d-%d of this evaluation (%d evicting, %d plain) on the oracle "
-                                         "through the caller's loop, 1 thread, after its first %d records were "
-                                         "replayed untimed; %.1f s, %.0f ms per placement (the evaluation's mean: "
-                                         "a placement's cost grows linearly with the plan's preemptions, "
-                                         "rank.go:240-245)" % (j0, j - 1, sum(kinds), len(kinds) - sum(kinds), j0,
-                                                                 float(np.sum(ts)), mean * 1e3)}
+        out["cpu_baseline"] = _c5_oracle_window(nodes, allocs, job, perm, cfg, rows, recs, placed, cpu_s, 100, 120)
+        # with AllocMetric on: a shorter window of the same protocol
+        m_on["cpu_baseline"] = _c5_oracle_window(nodes, allocs, job, perm, cfg, rows, recs, placed,
+                                                 min(cpu_s, 40.0), 20, 24, metrics=True)
+    out["metrics_on"] = m_on
     return out
 
 
@@ -1142,7 +1257,8 @@ def main():
                   "metric_bytes_per_eval": m_bytes / max(1, m_done),
                   "note": "rank-local: the headline loop with pe_set_metrics on, every Select's AllocMetric maps "
                           "(ClassFiltered / ConstraintFiltered / ClassExhausted / DimensionExhausted / top-5 "
-                          "ScoreMetaData) copied out by the caller"}
+                          "ScoreMetaData) copied out by the caller in binary form (the served record's "
+                          "pe_metric_count / pe_metric_score arrays)"}
 
     # the dominant kernel of a step: the speculative count loop (k_base + k_chain),
     # timed with HIP events on the engine's stream by the same call path
@@ -1232,6 +1348,8 @@ def main():
                                               "chain; Go toolchain unavailable)"
                                               % (oe_all, args.count, len(nodes), secs_all)}
             line["speedup_vs_fastest_cpu_run"] = value / rates[-1]
+            metrics_on["cpu_baseline"] = _oracle_metrics_rate(lambda: _oracle_generic(nodes, allocs), job, orders[0],
+                                                              args.count, 8.0)
             _, multi = cpu_baseline(nodes, allocs, job, args.cpu_seconds)
             line["cpu_baseline_multicore"] = multi
     sections = [x for x in args.sections.split(",") if x]

@@ -677,6 +677,27 @@ typedef struct pe_system_view {
     uint32_t* log;                /* [log_cap] served Selects in order, written by the caller */
     uint32_t n_log;               /* caller and engine: entries written / taken over */
     uint32_t preempt;             /* nonzero: exhausted rows go to the engine */
+    /* With pe_set_metrics on (NULL otherwise): a served Select's AllocMetric
+     * maps (scheduler_system.go:334-337), which the caller assembles from
+     * per-row entries as FeasibilityWrapper and BinPack would have filled
+     * them (feasible.go:1061-1153):
+     *   option: ScoreMetaData = [{NodeID of row, NormScore = the outcome's
+     *     FinalScore, Scores = {"binpack": mscore[row]}}];
+     *   filtered: ConstraintFiltered[key]++ with key = mkey[row], except when
+     *     c = mclass[row] != PE_NONE and mfailed[c] is set: key =
+     *     mkey_ineligible ("computed class ineligible"); then mfailed[c] = 1
+     *     when c != PE_NONE (the EvalEligibility memo of the row's class);
+     *   exhausted: DimensionExhausted[mkey[row]]++;
+     *   filtered / exhausted: ClassFiltered / ClassExhausted[mnode_class[row]]++
+     *     unless it is PE_NONE (a node without NodeClass).
+     * Keys as pe_metric_count.key (pe_metric_string). */
+    const uint32_t* mkey;
+    const uint32_t* mclass;
+    uint8_t* mfailed;             /* caller and engine: per memo class */
+    const double* mscore;
+    const uint32_t* mnode_class;
+    uint32_t mkey_ineligible;
+    uint32_t pad1;
 } pe_system_view;
 pe_system_view* pe_system_view_get(pe_stack* s);
 int pe_set_cursor(pe_stack* s, uint32_t tg_index, uint32_t offset, uint32_t limit);

@@ -277,7 +277,9 @@ PE_SYS_STALE = 0x7FF8000000000003
 class pe_system_view(C.Structure):   # nomad_pe.h: the served system-Select view
     _fields_ = [("epoch", C.c_uint32), ("tg_index", C.c_uint32), ("n_rows", C.c_uint32), ("log_cap", C.c_uint32),
                 ("outcome", C.POINTER(C.c_uint64)), ("log", C.POINTER(C.c_uint32)), ("n_log", C.c_uint32),
-                ("preempt", C.c_uint32)]
+                ("preempt", C.c_uint32), ("mkey", C.POINTER(C.c_uint32)), ("mclass", C.POINTER(C.c_uint32)),
+                ("mfailed", C.POINTER(C.c_uint8)), ("mscore", C.POINTER(C.c_double)),
+                ("mnode_class", C.POINTER(C.c_uint32)), ("mkey_ineligible", C.c_uint32), ("pad1", C.c_uint32)]
 
 
 def bind(lib, prefix, create_name, destroy_name, error_name):

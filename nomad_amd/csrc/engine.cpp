@@ -683,6 +683,11 @@ struct pe_stack {
     int32_t job_priority = 0;
     std::vector<ParsedConstraint> job_constraints;
     bool job_escaped = false;
+    // per row for the metrics walk: the job checkers' FilterNode reason,
+    // kJfPass, or null (not yet run); and the row's dense class
+    std::vector<const char*> jf;
+    std::vector<uint32_t> jf_cls;
+    std::vector<uint32_t> trace_dk;   // spec_metrics: per row, the earlier records' placements (zero between uses)
     std::vector<ParsedAffinity> job_affinities;
     std::vector<SpreadSpec> job_spreads;
     std::vector<std::unique_ptr<TgPlan>> tgs;
@@ -723,8 +728,9 @@ struct pe_stack {
         mstr_ix.emplace(mstrs.back(), id);
         return id;
     }
-    uint32_t mkey_p(const char* p) {   // reasons that are stable C strings (checker texts, literals)
-        if (p != mk_last_p) {
+    uint32_t mkey_p(const char* p) {   // reasons that are C strings (checker texts, literals)
+        // the last pointer's key, when the text there is still the same
+        if (p != mk_last_p || std::strcmp(p, mstrs[mk_last_id & ~PE_METRIC_ENGINE_KEY].c_str()) != 0) {
             mk_last_id = mkey(p);
             mk_last_p = p;
         }
@@ -762,6 +768,18 @@ struct pe_stack {
         int32_t served_row = -1;          // the last served Select's pick, awaiting its commit
         std::vector<uint32_t> pending;    // committed rows not yet in HBM
         uint64_t passes = 0, served = 0;
+        // with AllocMetric on: every row's k_trace outcome and score values
+        // at the cache pass (the maps of a served Select on that row)
+        std::vector<uint32_t> tcode;
+        std::vector<double> tscore;
+        // ... and the served system-Select view's per-row entries
+        // (pe_system_view.mkey / mclass / mscore / mnode_class); mfailed is
+        // the caller's memo of failed classes, mfailed_eng the engine's copy
+        // as of the log entries taken over
+        std::vector<uint32_t> mkey, mclass, mnode_class;
+        std::vector<double> mscore;
+        std::vector<uint8_t> mfailed, mfailed_eng;
+        bool mready = false;
     } sys;
     PinnedMem h_sys_cache;                // per row: FinalScore, or a NaN carrying the outcome (kSysDirty: stale)
     DevMem d_identity;
@@ -769,6 +787,7 @@ struct pe_stack {
     DevMem d_sys_res;                     // k_system_rows outcomes by row
     uint64_t test_fallback_every = 0, test_select_calls = 0;   // PE_TEST_FALLBACK_EVERY
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
+    PinnedMem h_trace_codes, h_trace_sc;   // spec_metrics: the batched trace's outcomes
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
     DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;
     DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)
@@ -1308,6 +1327,26 @@ const char* job_fail(const pe_stack* s, pe::ConstraintEvaluator& ev, const NodeV
 
 bool job_feasible(const pe_stack* s, pe::ConstraintEvaluator& ev, const NodeView& n) {
     return job_fail(s, ev, n) == nullptr;
+}
+
+// job_fail of a row, cached per row for the job and snapshot (the checkers
+// are a pure function of the node's attributes and the job's constraints)
+const char kJfPass[] = "";
+static void jf_ready(pe_stack* s) {
+    if (s->jf.size() == s->nodes.size()) return;
+    s->jf.assign(s->nodes.size(), nullptr);
+    s->jf_cls.resize(s->nodes.size());
+    for (size_t r = 0; r < s->nodes.size(); r++) s->jf_cls[r] = s->nodes[r].cls;
+}
+
+const char* job_fail_cached(pe_stack* s, pe::ConstraintEvaluator& ev, uint32_t row) {
+    const char* w = s->jf[row];
+    if (!w) {
+        w = job_fail(s, ev, s->view(row));
+        if (!w) w = kJfPass;
+        s->jf[row] = w;
+    }
+    return w == kJfPass ? nullptr : w;
 }
 
 // tg checkers in GenericStack/SystemStack order: drivers, constraints, host
@@ -2613,6 +2652,42 @@ constexpr uint64_t kSysNaNBits = 0x7FF8000000000000ull;
 constexpr uint64_t kSysStale = kSysNaNBits | 3u;
 static_assert(kSysStale == PE_SYS_STALE, "the view's stale marker is the cache's");
 
+static void metrics_set_last_sys(pe_stack* s, uint32_t row, uint32_t code, bool failed_before);
+
+// The caller's log entries [k0, upto) with AllocMetric on: the memo of failing
+// classes as the sequential Selects left it (the engine's copy, then the
+// caller's array and the reference memo), and the last Select's maps.
+static void sys_view_take_metrics(pe_stack* s, uint32_t k0, uint32_t upto) {
+    pe_system_view& v = s->sysview;
+    pe_stack::SysSpec& y = s->sys;
+    const uint64_t* cache = s->h_sys_cache.as<uint64_t>();
+    const uint32_t nn = (uint32_t)s->nodes.size(), ncls = s->ncls;
+    for (uint32_t k = k0; k < upto; k++) {
+        const uint32_t e = v.log[k];
+        const uint32_t row = e & PE_SYS_ROW_MASK;
+        if (row >= nn) continue;
+        uint32_t code = 0;
+        bool before = false;
+        if (e & PE_SYS_NIL) {
+            code = (uint32_t)(cache[row] & 3u);
+            const uint32_t mc = y.mclass[row];
+            if (code == 1 && mc != PE_NONE) {
+                before = y.mfailed_eng[mc] != 0;
+                y.mfailed_eng[mc] = 1;
+            }
+        }
+        if (k + 1 == upto) metrics_set_last_sys(s, row, code, before);
+    }
+    std::memcpy(y.mfailed.data(), y.mfailed_eng.data(), y.mfailed.size());
+    auto& rt = s->ref_tg_memo[s->tgs[y.tgi]->name];
+    if (s->ref_job_memo.size() != ncls) s->ref_job_memo.assign(ncls, -1);
+    if (rt.size() != ncls) rt.assign(ncls, -1);
+    for (uint32_t c = 0; c < ncls; c++) {
+        if (y.mfailed_eng[c]) s->ref_job_memo[c] = 0;
+        if (y.mfailed_eng[ncls + c]) rt[c] = 0;
+    }
+}
+
 static void sys_view_take(pe_stack* s) {
     pe_system_view& v = s->sysview;
     if (!v.n_rows || v.n_log == s->sys_taken) return;
@@ -2703,6 +2778,7 @@ static void sys_view_take(pe_stack* s) {
         }
     }
     if (k < upto) take_fast(k);
+    if (s->metrics_on && y.mready && v.mfailed) sys_view_take_metrics(s, s->sys_taken, upto);
     s->sys_taken = upto;
 }
 
@@ -2718,7 +2794,14 @@ static void sys_view_publish(pe_stack* s) {
     s->sys_taken = 0;
     v.outcome = s->h_sys_cache.as<uint64_t>();
     v.preempt = s->cfg.preempt ? 1u : 0u;
-    v.n_rows = (s->metrics_on || !s->kids.empty()) ? 0u : n;
+    const bool m = s->metrics_on && s->sys.mready;
+    v.mkey = m ? s->sys.mkey.data() : nullptr;
+    v.mclass = m ? s->sys.mclass.data() : nullptr;
+    v.mfailed = m ? s->sys.mfailed.data() : nullptr;
+    v.mscore = m ? s->sys.mscore.data() : nullptr;
+    v.mnode_class = m ? s->sys.mnode_class.data() : nullptr;
+    v.mkey_ineligible = s->mkey_p("computed class ineligible");
+    v.n_rows = ((s->metrics_on && !m) || !s->kids.empty()) ? 0u : n;
 }
 
 static void sys_view_withdraw(pe_stack* s) {
@@ -4466,6 +4549,7 @@ static void elig_visit_list(pe_stack* s, uint32_t tgi, const std::vector<uint32_
 }
 
 static int set_state_one(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
+    if (s) s->jf.clear();   // node attributes change: the job checkers run again
     if (!s || !strs || !nodes) return PE_EINVAL;
     spec_drop(s);
     s->counts_pending = false;   // a new snapshot: its arrays are rebuilt (the job's counts by the next SetJob)
@@ -4539,6 +4623,7 @@ static int update_allocs_one(pe_stack* s, const pe_strtab* strs, const pe_alloc_
 }
 
 static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const uint32_t* index) {
+    if (s) s->jf.clear();   // node attributes change: the job checkers run again
     if (!s || !nodes) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
@@ -4651,6 +4736,7 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     s->job_ns = j->ns;
     s->job_priority = j->priority;
     s->job_constraints.clear();
+    s->jf.clear();
     s->job_escaped = false;
     for (uint32_t i = 0; i < j->constraint_count; i++) {
         s->job_constraints.push_back(parse_constraint(s, j->constraints[j->constraint_off + i]));
@@ -4912,23 +4998,24 @@ struct ScoreMeta {
 };
 
 struct ScoreHeap {
-    std::vector<ScoreMeta> items;
-    size_t cap = 5;   // MaxRetainedNodeScores (structs.go:178)
-    bool less(size_t i, size_t j) const { return items[i].norm < items[j].norm; }
-    void up(size_t j) {
+    static constexpr uint32_t cap = 5;   // MaxRetainedNodeScores (structs.go:178)
+    ScoreMeta items[cap];
+    uint32_t len = 0;
+    bool less(uint32_t i, uint32_t j) const { return items[i].norm < items[j].norm; }
+    void up(uint32_t j) {
         while (j > 0) {
-            const size_t i = (j - 1) / 2;
+            const uint32_t i = (j - 1) / 2;
             if (!less(j, i)) break;
             std::swap(items[i], items[j]);
             j = i;
         }
     }
-    bool down(size_t i0, size_t n) {
-        size_t i = i0;
+    bool down(uint32_t i0, uint32_t n) {
+        uint32_t i = i0;
         for (;;) {
-            const size_t j1 = 2 * i + 1;
+            const uint32_t j1 = 2 * i + 1;
             if (j1 >= n) break;
-            size_t j = j1;
+            uint32_t j = j1;
             if (j1 + 1 < n && less(j1 + 1, j1)) j = j1 + 1;
             if (!less(j, i)) break;
             std::swap(items[i], items[j]);
@@ -4939,42 +5026,55 @@ struct ScoreHeap {
     // whether push(m) changes the heap: a full heap ignores an item not above
     // its minimum (and the closing up(len-1) of heap.Push is then a no-op, the
     // heap property holding)
-    bool enters(double norm) const { return items.size() < cap || norm > items[0].norm; }
-    void push(ScoreMeta m) {   // heap.Push → ScoreHeap.Push (+ heap.Fix) then up(len-1)
-        if (items.capacity() < cap) items.reserve(cap);
-        if (items.size() < cap) {
-            items.push_back(std::move(m));
+    bool enters(double norm) const { return len < cap || norm > items[0].norm; }
+    void push(const ScoreMeta& m) {   // heap.Push → ScoreHeap.Push (+ heap.Fix) then up(len-1)
+        if (len < cap) {
+            items[len++] = m;
         } else if (m.norm > items[0].norm) {
-            items[0] = std::move(m);
-            if (!down(0, items.size())) up(0);
+            items[0] = m;
+            if (!down(0, len)) up(0);
         }
-        up(items.size() - 1);
+        up(len - 1);
     }
-    std::vector<ScoreMeta> reverse_items() {   // GetItemsReverse: heap.Pop until empty
-        std::vector<ScoreMeta> out(items.size());
-        size_t i = items.size();
-        while (!items.empty()) {
-            const size_t n = items.size() - 1;
+    // GetItemsReverse: heap.Pop until empty, into out[0 .. len) (descending)
+    uint32_t reverse_items(ScoreMeta* out) {
+        const uint32_t total = len;
+        uint32_t i = total;
+        while (len > 0) {
+            const uint32_t n = len - 1;
             std::swap(items[0], items[n]);
             down(0, n);
-            out[--i] = std::move(items.back());
-            items.pop_back();
+            out[--i] = items[n];
+            len--;
         }
-        return out;
+        return total;
     }
 };
 
 // One AllocMetric map (key -> count) as it fills: a Select's maps hold a
 // handful of keys, so a short vector searched in place
 struct MetricCounts {
-    std::vector<std::pair<uint32_t, uint32_t>> kv;
+    static constexpr uint32_t kInline = 6;   // most maps: a few keys, no allocation
+    std::pair<uint32_t, uint32_t> in[kInline];
+    uint32_t n = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> more;
     void add(uint32_t k) {
-        for (auto& e : kv)
+        for (uint32_t i = 0; i < n; i++)
+            if (in[i].first == k) {
+                in[i].second++;
+                return;
+            }
+        for (auto& e : more)
             if (e.first == k) {
                 e.second++;
                 return;
             }
-        kv.emplace_back(k, 1u);
+        if (n < kInline) in[n++] = {k, 1u};
+        else more.emplace_back(k, 1u);
+    }
+    void append(uint32_t kind, std::vector<pe_metric_count>& out) const {
+        for (uint32_t i = 0; i < n; i++) out.push_back(pe_metric_count{kind, in[i].first, in[i].second});
+        for (auto& e : more) out.push_back(pe_metric_count{kind, e.first, e.second});
     }
 };
 
@@ -4983,6 +5083,13 @@ struct MetricCounts {
 struct MetricAcc {
     MetricCounts cf, kf, ce, de;
     ScoreHeap heap;
+    void reset() {
+        for (MetricCounts* c : {&cf, &kf, &ce, &de}) {
+            c->n = 0;
+            c->more.clear();
+        }
+        heap.len = 0;
+    }
     void filter(pe_stack* s, uint32_t row, uint32_t why) {
         const uint32_t nc = s->nodes[row].node_class;
         if (nc != PE_NONE && !s->S(nc).empty()) cf.add(nc);
@@ -5019,27 +5126,31 @@ static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& or
         if (log) log->push_back({true, c, v});
         rt[c] = v;
     };
-    for (uint32_t k = 0; k < evaluated && m; k++) {
-        const uint32_t row = order[(start + k) % m];
-        const NodeView v = s->view(row);
-        const uint32_t c = s->nodes[row].cls;
+    jf_ready(s);
+    const uint32_t* cls_of = s->jf_cls.data();
+    uint32_t p = m ? start % (uint32_t)m : 0;
+    for (uint32_t k = 0; k < evaluated && m; k++, p = p + 1 == m ? 0 : p + 1) {
+        const uint32_t row = order[p];
+        const uint32_t c = cls_of[row];
         const char* why = nullptr;
+        // the node's attribute views only when a checker runs (a known class
+        // decides the common case from the memo alone)
         if (s->job_escaped) {
-            why = job_fail(s, ev, v);
+            why = job_fail_cached(s, ev, row);
         } else if (s->ref_job_memo[c] == 0) {
             why = kIneligible;
-        } else {
-            why = job_fail(s, ev, v);
+        } else if (s->ref_job_memo[c] == -1 || !s->job_constraints.empty()) {
+            why = job_fail_cached(s, ev, row);
             if (why) set_job(c, 0);
             else if (s->ref_job_memo[c] == -1) set_job(c, 1);
         }
         if (!why) {
             if (g.escaped) {
-                why = tg_fail(s, ev, g, v);
+                why = tg_fail(s, ev, g, s->view(row));
             } else if (rt[c] == 0) {
                 why = kIneligible;
             } else if (rt[c] == -1) {
-                why = tg_fail(s, ev, g, v);
+                why = tg_fail(s, ev, g, s->view(row));
                 set_tg(c, why ? 0 : 1);
             }
         }
@@ -5047,7 +5158,7 @@ static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& or
             acc.filter(s, row, why == kIneligible ? ineligible : s->mkey_p(why));
         } else {
             rows.push_back(row);
-            if (pass) (*pass)[(start + k) % m] = 1;
+            if (pass) (*pass)[p] = 1;
         }
     }
 }
@@ -5072,7 +5183,7 @@ static int metrics_outcome(pe_stack* s, TgPlan& g, const pe::Ask& a, uint32_t ro
                 if (o[4] != 0.0) sm.scores.emplace_back(PE_SCORER_ALLOCATION_SPREAD, o[4]);
             }
             sm.norm = o[5];
-            acc.heap.push(std::move(sm));
+            acc.heap.push(sm);
             break;
         }
         case pe::kTrDistinctHosts: acc.filter(s, row, s->mkey_p("distinct_hosts")); break;
@@ -5135,14 +5246,14 @@ static int metrics_outcome(pe_stack* s, TgPlan& g, const pe::Ask& a, uint32_t ro
 // One Select's maps in binary form (pe_last_metrics_bin), appended.
 static void metrics_bin_into(MetricAcc& acc, std::vector<pe_metric_count>& counts,
                              std::vector<pe_metric_score>& scores) {
-    auto put = [&](uint32_t kind, const MetricCounts& mm) {
-        for (auto& kv : mm.kv) counts.push_back(pe_metric_count{kind, kv.first, kv.second});
-    };
-    put(PE_METRIC_CLASS_FILTERED, acc.cf);
-    put(PE_METRIC_CONSTRAINT_FILTERED, acc.kf);
-    put(PE_METRIC_CLASS_EXHAUSTED, acc.ce);
-    put(PE_METRIC_DIMENSION_EXHAUSTED, acc.de);
-    for (auto& it : acc.heap.reverse_items()) {   // PopulateScoreMetaData: GetItemsReverse
+    acc.cf.append(PE_METRIC_CLASS_FILTERED, counts);
+    acc.kf.append(PE_METRIC_CONSTRAINT_FILTERED, counts);
+    acc.ce.append(PE_METRIC_CLASS_EXHAUSTED, counts);
+    acc.de.append(PE_METRIC_DIMENSION_EXHAUSTED, counts);
+    ScoreMeta items[ScoreHeap::cap];
+    const uint32_t ni = acc.heap.reverse_items(items);
+    for (uint32_t q = 0; q < ni; q++) {   // PopulateScoreMetaData: GetItemsReverse
+        const ScoreMeta& it = items[q];
         pe_metric_score m;
         std::memset(&m, 0, sizeof(m));
         m.row = (int32_t)it.row;
@@ -5163,6 +5274,33 @@ static const std::string& metric_string(const pe_stack* s, uint32_t key) {
         return i < s->mstrs.size() ? s->mstrs[i] : none;
     }
     return s->S(key);
+}
+
+// The map key a row's k_trace outcome records in a single-node Select:
+// *kind 0 an option (no key), PE_METRIC_CONSTRAINT_FILTERED (distinct_hosts)
+// or PE_METRIC_DIMENSION_EXHAUSTED; false for outcomes whose reason needs the
+// host's port mirrors or property counts (not on the system cache path).
+static bool trace_key(pe_stack* s, uint32_t code, uint32_t* kind, uint32_t* key) {
+    *kind = PE_METRIC_DIMENSION_EXHAUSTED;
+    const char* t = nullptr;
+    switch (code & 255u) {
+        case pe::kTrOption: *kind = 0; *key = PE_NONE; return true;
+        case pe::kTrDistinctHosts: *kind = PE_METRIC_CONSTRAINT_FILTERED; t = "distinct_hosts"; break;
+        case pe::kTrNoAddr: t = "network: no addresses available"; break;
+        case pe::kTrDynPorts: case pe::kTrTaskDyn: t = "network: dynamic port selection failed"; break;
+        case pe::kTrNoNetworks: t = "network: no networks available"; break;
+        case pe::kTrBandwidth: t = "network: bandwidth exceeded"; break;
+        case pe::kTrDevNone: t = "devices: no devices available"; break;
+        case pe::kTrDevZero: t = "devices: invalid request of zero devices"; break;
+        case pe::kTrDevNoMatch: t = "devices: no devices match request"; break;
+        case pe::kTrCpu: t = "cpu"; break;
+        case pe::kTrCores: t = "cores"; break;
+        case pe::kTrMemory: t = "memory"; break;
+        case pe::kTrDisk: t = "disk"; break;
+        default: return false;
+    }
+    *key = s->mkey_p(t);
+    return true;
 }
 
 // pe_last_metrics' text of binary maps: "KIND\tKEY\tCOUNT" lines per map,
@@ -5222,6 +5360,35 @@ static void metrics_set_last(pe_stack* s, MetricAcc& acc) {
     s->m_counts.clear();
     s->m_scores.clear();
     metrics_bin_into(acc, s->m_counts, s->m_scores);
+    s->metrics_text_ok = false;
+    s->metrics_valid = true;
+}
+
+// The maps of a single-node system Select on `row` served from the view
+// (code: the cache's outcome, 0 option / 1 filtered / 2 exhausted;
+// failed_before: the row's memo class had already failed).
+static void metrics_set_last_sys(pe_stack* s, uint32_t row, uint32_t code, bool failed_before) {
+    const pe_stack::SysSpec& y = s->sys;
+    s->m_counts.clear();
+    s->m_scores.clear();
+    const uint32_t nc = y.mnode_class[row];
+    if (code == 0) {
+        pe_metric_score m;
+        std::memset(&m, 0, sizeof(m));
+        m.row = (int32_t)row;
+        m.n_scores = 1;
+        m.norm = y.tscore[6 * (size_t)row + 5];
+        m.scorer[0] = PE_SCORER_BINPACK;
+        m.score[0] = y.mscore[row];
+        s->m_scores.push_back(m);
+    } else if (code == 1) {
+        if (nc != PE_NONE) s->m_counts.push_back(pe_metric_count{PE_METRIC_CLASS_FILTERED, nc, 1});
+        const uint32_t key = failed_before ? s->sysview.mkey_ineligible : y.mkey[row];
+        s->m_counts.push_back(pe_metric_count{PE_METRIC_CONSTRAINT_FILTERED, key, 1});
+    } else {
+        if (nc != PE_NONE) s->m_counts.push_back(pe_metric_count{PE_METRIC_CLASS_EXHAUSTED, nc, 1});
+        s->m_counts.push_back(pe_metric_count{PE_METRIC_DIMENSION_EXHAUSTED, y.mkey[row], 1});
+    }
     s->metrics_text_ok = false;
     s->metrics_valid = true;
 }
@@ -5357,7 +5524,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                         if (fl & 2u) sm.scores.emplace_back(PE_SCORER_PREEMPTION, o[5]);
                     }
                     sm.norm = o[6];
-                    acc.heap.push(std::move(sm));
+                    acc.heap.push(sm);
                 } else if (st == 2) {   // kExhausted: no preemption frees enough (ExhaustedNode(dim))
                     const uint32_t d = (ec >> 8) & 255u;
                     acc.exhaust(s, row, d == pe::kTrCpu ? "cpu" : (d == pe::kTrMemory ? "memory" : "disk"));   // literals
@@ -5406,28 +5573,38 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     sp.memo_tg0 = rt;
     sp.memo_log.clear();
     sp.memo_off.assign(1, 0u);
-    std::vector<MetricAcc> acc(sp.n_rec);
+    // one accumulator per record, kept across runs (no page faults per run)
+    static thread_local std::vector<MetricAcc> acc;
+    if (acc.size() < sp.n_rec) acc.resize(sp.n_rec);
+    for (uint32_t k = 0; k < sp.n_rec; k++) acc[k].reset();
     std::vector<uint32_t> rows, rec_end(sp.n_rec);
     std::vector<uint16_t> dks;
-    std::unordered_map<uint32_t, uint16_t> placed_on;   // row -> placements of earlier records
+    if (s->trace_dk.size() != s->nodes.size()) s->trace_dk.assign(s->nodes.size(), 0u);
+    uint32_t* placed_on = s->trace_dk.data();   // row -> placements of earlier records
+    rows.reserve(16 * (size_t)sp.n_rec);
+    dks.reserve(16 * (size_t)sp.n_rec);
     uint32_t off = off0;
     for (uint32_t k = 0; k < sp.n_rec; k++) {
         const uint32_t ev = sp.compact ? sp.crecs[k].nodes_evaluated : sp.recs[k].nodes_evaluated;
         const size_t r0 = rows.size();
         metrics_walk(s, g, order, off, ev, acc[k], rows, &sp.memo_log);
         sp.memo_off.push_back((uint32_t)sp.memo_log.size());
-        for (size_t i = r0; i < rows.size(); i++) {
-            auto it = placed_on.find(rows[i]);
-            dks.push_back(it == placed_on.end() ? 0 : it->second);
-        }
+        for (size_t i = r0; i < rows.size(); i++) dks.push_back((uint16_t)placed_on[rows[i]]);
         rec_end[k] = (uint32_t)rows.size();
         const int32_t row = spec_rec_row(sp, k);
         if (row >= 0) placed_on[(uint32_t)row]++;
         off = sp.compact ? sp.crecs[k].new_offset : sp.recs[k].new_offset;
     }
+    for (uint32_t k = 0; k < sp.n_rec; k++) {   // back to zero for the next run
+        const int32_t row = spec_rec_row(sp, k);
+        if (row >= 0) placed_on[(uint32_t)row] = 0;
+    }
     const double t1 = prof ? now_us() : 0.0;
-    std::vector<uint32_t> codes(rows.size());
-    std::vector<double> sc(rows.size() * 6);
+    // the outcomes land in pinned host buffers kept across runs
+    HIP_TRY(s, s->h_trace_codes.ensure(std::max<size_t>(rows.size(), 1) * sizeof(uint32_t)));
+    HIP_TRY(s, s->h_trace_sc.ensure(std::max<size_t>(rows.size(), 1) * 6 * sizeof(double)));
+    const uint32_t* codes = s->h_trace_codes.as<uint32_t>();
+    const double* sc = s->h_trace_sc.as<double>();
     pe::Ask a = ask_for(s, g);
     if (!rows.empty()) {
         HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
@@ -5443,8 +5620,10 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         HIP_TRY_STATE(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
                                          s->d_trace_out.as<uint32_t>(), nullptr, s->log10, nullptr,
                                          s->d_trace_scores.as<double>(), s->stream, s->d_trace_dk.as<uint16_t>()));
-        HIP_TRY(s, hipMemcpyAsync(codes.data(), s->d_trace_out.p, codes.size() * 4, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(s, hipMemcpyAsync(sc.data(), s->d_trace_scores.p, sc.size() * 8, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(s, hipMemcpyAsync(s->h_trace_codes.p, s->d_trace_out.p, rows.size() * 4, hipMemcpyDeviceToHost,
+                                  s->stream));
+        HIP_TRY(s, hipMemcpyAsync(s->h_trace_sc.p, s->d_trace_scores.p, rows.size() * 48, hipMemcpyDeviceToHost,
+                                  s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
     }
     const double t2 = prof ? now_us() : 0.0;
@@ -5600,6 +5779,70 @@ static bool sys_cacheable(pe_stack* s, TgPlan& g) {
            (g.escaped || g.nonuniform.empty()) && s->visit_unique;
 }
 
+// The served system-Select view's per-row AllocMetric entries (nomad_pe.h,
+// pe_system_view.mkey ...) from the cache pass's k_trace outcomes: the
+// FeasibilityWrapper reason of each row as if its class were unknown to the
+// memo (the job checkers per row, cached; the task-group checkers per node
+// signature, or per row when the group escapes), the memo class that turns
+// later nodes of a failing class into "computed class ineligible", and the
+// BinPack outcome. The caller's memo starts from the reference memo.
+static void sys_metrics_build(pe_stack* s, TgPlan& g) {
+    pe_stack::SysSpec& y = s->sys;
+    const uint32_t n = (uint32_t)s->nodes.size(), ncls = s->ncls;
+    y.mready = false;
+    if (y.tcode.size() != n) return;
+    jf_ready(s);
+    y.mkey.assign(n, PE_NONE);
+    y.mclass.assign(n, PE_NONE);
+    y.mscore.assign(n, 0.0);
+    y.mnode_class.resize(n);
+    for (uint32_t r = 0; r < n; r++) {
+        const uint32_t nc = s->nodes[r].node_class;
+        y.mnode_class[r] = (nc != PE_NONE && !s->S(nc).empty()) ? nc : PE_NONE;
+    }
+    if (s->ref_job_memo.size() != ncls) s->ref_job_memo.assign(ncls, -1);
+    auto& rt = s->ref_tg_memo[g.name];
+    if (rt.size() != ncls) rt.assign(ncls, -1);
+    y.mfailed.assign(2 * (size_t)ncls, 0);
+    for (uint32_t c = 0; c < ncls; c++) {
+        y.mfailed[c] = s->ref_job_memo[c] == 0;
+        y.mfailed[ncls + c] = rt[c] == 0;
+    }
+    y.mfailed_eng = y.mfailed;
+    pe::ConstraintEvaluator ev;
+    std::vector<const char*> by_sig(s->sig_rep.size(), nullptr);
+    std::vector<uint8_t> sig_done(s->sig_rep.size(), 0);
+    for (uint32_t r = 0; r < n; r++) {
+        const uint32_t c = s->jf_cls[r];
+        const char* why = job_fail_cached(s, ev, r);
+        uint32_t mc = PE_NONE;
+        if (why) {
+            if (!s->job_escaped) mc = c;
+        } else if (g.escaped) {
+            why = tg_fail(s, ev, g, s->view(r));
+        } else {
+            const uint32_t sg = s->nodes[r].sig;
+            if (sg < sig_done.size()) {
+                if (!sig_done[sg]) { by_sig[sg] = tg_fail(s, ev, g, s->view(r)); sig_done[sg] = 1; }
+                why = by_sig[sg];
+            } else {
+                why = tg_fail(s, ev, g, s->view(r));
+            }
+            if (why) mc = ncls + c;
+        }
+        if (why) {
+            y.mkey[r] = s->mkey_p(why);
+            y.mclass[r] = mc;
+            continue;
+        }
+        uint32_t kind, key;
+        if (!trace_key(s, y.tcode[r], &kind, &key)) return;   // the view carries no maps: Selects cross
+        y.mkey[r] = key;
+        if (kind == 0) y.mscore[r] = y.tscore[6 * (size_t)r];   // binpack
+    }
+    y.mready = true;
+}
+
 static int sys_start(pe_stack* s, uint32_t tgi) {
     ApiScope prof_(s, "sys_start");
     pe_stack::SysSpec& y = s->sys;
@@ -5635,7 +5878,27 @@ static int sys_start(pe_stack* s, uint32_t tgi) {
     HIP_TRY_STATE(s, pe_launch_system(&A, s->stream));
     HIP_TRY(s, hipEventRecord(s->ev1, s->stream));
     HIP_TRY(s, hipMemcpyAsync(s->h_sys_cache.p, s->d_sys_res.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s->stream));
+    y.tcode.clear();
+    y.tscore.clear();
+    if (s->metrics_on) {
+        // the AllocMetric outcome of every row in the same state (k_trace over
+        // all rows; the FeasibilityWrapper half is walked per Select, since its
+        // reasons depend on the order the caller visits the classes in)
+        HIP_TRY(s, s->d_trace_out.ensure(sizeof(uint32_t) * (size_t)std::max<uint32_t>(n, 1)));
+        HIP_TRY(s, s->d_trace_scores.ensure(6 * sizeof(double) * (size_t)std::max<uint32_t>(n, 1)));
+        y.tcode.resize(n);
+        y.tscore.resize(6 * (size_t)n);
+        HIP_TRY_STATE(s, pe_launch_trace(&A.soa, &A.tg, &A.ask, s->d_identity.as<uint32_t>(), n,
+                                         s->d_trace_out.as<uint32_t>(), nullptr, s->log10, nullptr,
+                                         s->d_trace_scores.as<double>(), s->stream));
+        HIP_TRY(s, hipMemcpyAsync(y.tcode.data(), s->d_trace_out.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost,
+                                  s->stream));
+        HIP_TRY(s, hipMemcpyAsync(y.tscore.data(), s->d_trace_scores.p, 6 * sizeof(double) * n,
+                                  hipMemcpyDeviceToHost, s->stream));
+    }
     HIP_TRY(s, hipStreamSynchronize(s->stream));
+    y.mready = false;
+    if (s->metrics_on) sys_metrics_build(s, g);
     float ms = 0;
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
@@ -5652,7 +5915,7 @@ static int sys_start(pe_stack* s, uint32_t tgi) {
 // per-row cache. Returns false when the caller must take the single Select path.
 static bool sys_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, pe_ranked_node* out, int* rc) {
     pe_stack::SysSpec& y = s->sys;
-    if (s->visit.size() != 1 || s->metrics_on || !s->have_job || tgi >= s->tgs.size()) return false;
+    if (s->visit.size() != 1 || !s->have_job || tgi >= s->tgs.size()) return false;
     if (opts && (opts->penalty_count || opts->preferred_count || opts->preempt)) return false;
     if (!y.active || y.tgi != tgi) {
         // start at the group's first single-node Select: one pass over the
@@ -5691,6 +5954,23 @@ static bool sys_serve(pe_stack* s, uint32_t tgi, const pe_select_options* opts, 
     s->metrics_valid = false;
     elig_log_span(s, tgi, 0, 1);
     *rc = PE_OK;
+    if (s->metrics_on && row < y.tcode.size()) {   // the one node's maps (compute_metrics' steps)
+        TgPlan& g = *s->tgs[tgi];
+        MetricAcc acc;
+        std::vector<uint32_t> rows;
+        std::vector<MemoDelta> d;
+        metrics_walk(s, g, s->visit, 0, 1, acc, rows, &d);   // advances the reference memo
+        for (const MemoDelta& m : d)   // ... and the view's memo of failed classes
+            if (m.v == 0 && y.mready && m.cls < s->ncls) {
+                const size_t i = (m.tg ? s->ncls : 0u) + m.cls;
+                if (i < y.mfailed.size()) y.mfailed[i] = y.mfailed_eng[i] = 1;
+            }
+        if (!rows.empty()) {
+            std::map<int, std::vector<uint32_t>> counts;
+            *rc = metrics_outcome(s, g, ask_for(s, g), row, y.tcode[row], &y.tscore[6 * (size_t)row], acc, counts);
+        }
+        if (*rc == PE_OK) metrics_set_last(s, acc);
+    }
     return true;
 }
 
@@ -7720,8 +8000,9 @@ extern "C" int pe_set_metrics(pe_stack* s, int on) {
         const int frc = spec_flush(s);
         if (frc) return frc;
     }
+    if ((on != 0) != s->metrics_on) sys_deactivate(s);   // the next cache pass traces rows (or stops)
     s->metrics_on = on != 0;
-    if (s->metrics_on) sys_view_withdraw(s);   // served Selects would carry no metrics
+    if (s->metrics_on) sys_view_withdraw(s);   // the view's outcomes carry no maps
     s->metrics_valid = false;
     return PE_OK;
 }

@@ -133,7 +133,8 @@ def decode_metrics(stack, counts, c0: int, c1: int, scores, s0: int, s1: int) ->
     for i in range(s0, s1):
         m = scores[i]
         parts = {abi.SCORER_NAMES[m.scorer[j]]: float(m.score[j]) for j in range(m.n_scores)}
-        out["ScoreMetaData"].append((stack.nodes[m.row].id, float(m.norm), parts))
+        nid = stack.nodes[m.row].id if stack.nodes is not None else stack.state.node_id(m.row)
+        out["ScoreMetaData"].append((nid, float(m.norm), parts))
     return out
 
 

@@ -67,6 +67,7 @@ class ColumnarState:
         uniq, inv = np.unique(combo, return_inverse=True)
         cc_ids = np.array([I("v1:cc%d" % int(c)) for c in uniq], dtype=np.uint32)
 
+        self.node_id = (lambda k: "node-%08d" % k) if n <= (1 << 20) else (lambda k: "node-shared-id")
         nt = abi.pe_node_table()
         nt.n = n
         if n <= (1 << 20):

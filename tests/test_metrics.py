@@ -516,3 +516,137 @@ def test_metrics_view_distinct_property_and_spread():
     eng, ora = _metrics_pair(nodes, allocs, job, synth.shuffle(len(nodes), 4))
     st = _view_metrics_protocol(eng, ora, 120)
     assert st["view"] >= 100, st
+
+
+@pytest.mark.gpu
+def test_metrics_system_c4_100k():
+    """C4 at its bench shape (100k nodes): SystemScheduler's per-node
+    SetNodes([node]) + Select + Commit with AllocMetric on, answered from the
+    engine's per-row cache (one k_system pass plus one k_trace pass); every
+    node's maps equal the oracle's, the memo's "computed class ineligible"
+    included."""
+    import numpy as np
+    from nomad_amd import synth_columnar
+    from nomad_amd.stack import SystemStack
+    from oracle.oracle import OracleSystemStack
+    n = 100000
+    cs = synth_columnar.ColumnarState(n, seed=11, kind="c4", prefill=0.05)
+    job = synth.mock_system_job()
+    rows = np.random.Generator(np.random.PCG64(5)).permutation(n).astype(np.uint32)
+    eng, ora = SystemStack(), OracleSystemStack()
+    for st in (eng, ora):
+        st.EnableMetrics()
+        st.SetStateColumnar(cs)
+        st.SetJob(job)
+    kinds = set()
+    for i, r in enumerate(rows):
+        eng.SetNodes([int(r)])
+        ora.SetNodes([int(r)])
+        re, ro = eng.SelectRaw(0), ora.SelectRaw(0)
+        assert (re.row, re.final_score, re.nodes_filtered, re.nodes_exhausted) == \
+               (ro.row, ro.final_score, ro.nodes_filtered, ro.nodes_exhausted), i
+        me, mo = eng.LastMetrics(), ora.LastMetrics()
+        assert me == mo, (i, me, mo)
+        if i % 997 == 0:
+            assert eng.LastMetricsBin() == me, i
+        kinds |= {k for k in ("ConstraintFiltered", "DimensionExhausted", "ScoreMetaData") if mo[k]}
+        if ro.row >= 0:
+            eng.Commit(0, re.row)
+            ora.Commit(0, ro.row)
+    assert kinds == {"ConstraintFiltered", "DimensionExhausted", "ScoreMetaData"}, kinds
+    import ctypes as C
+    out = (C.c_uint64 * 2)()
+    eng._check(eng._lib.pe_system_spec_stats(C.c_void_p(eng._h), out))
+    assert out[1] >= n - 2, tuple(out)   # every Select after the pass's first from the cache
+
+
+@pytest.mark.gpu
+def test_metrics_system_view_c4_100k():
+    """The served system-Select view with AllocMetric on, at the C4 bench
+    shape: the caller answers SetNodes([node]) + Select + Commit from the
+    view and assembles each Select's maps from its per-row entries
+    (pe_system_view.mkey / mclass / mfailed / mscore / mnode_class, as the Go
+    shim would); every node's maps equal the oracle's, and a crossing Select
+    afterwards (the log taken over: the memo and the last maps) too."""
+    import ctypes as C
+    import numpy as np
+    from nomad_amd import abi, synth_columnar
+    from nomad_amd.stack import SystemStack
+    from oracle.oracle import OracleSystemStack
+    n = 100000
+    cs = synth_columnar.ColumnarState(n, seed=11, kind="c4", prefill=0.05)
+    job = synth.mock_system_job()
+    rows = np.random.Generator(np.random.PCG64(5)).permutation(n).astype(np.uint32)
+    eng, ora = SystemStack(), OracleSystemStack()
+    for st in (eng, ora):
+        st.EnableMetrics()
+        st.SetStateColumnar(cs)
+        st.SetJob(job)
+    fn = eng._lib.pe_system_view_get
+    fn.restype = C.POINTER(abi.pe_system_view)
+    fn.argtypes = [C.c_void_p]
+    v = fn(eng._h).contents
+    keys = {}
+
+    def key(k):
+        if k not in keys:
+            keys[k] = eng.MetricString(k)
+        return keys[k]
+
+    def view_maps(r, code, score):
+        m = {"ClassFiltered": {}, "ConstraintFiltered": {}, "ClassExhausted": {}, "DimensionExhausted": {},
+             "ScoreMetaData": []}
+        nc = v.mnode_class[r]
+        if code == 0:
+            m["ScoreMetaData"] = [(cs.node_id(r), score, {"binpack": v.mscore[r]})]
+        elif code == 1:
+            k, mc = v.mkey[r], v.mclass[r]
+            if mc != abi.PE_NONE:
+                if v.mfailed[mc]:
+                    k = v.mkey_ineligible
+                v.mfailed[mc] = 1
+            if nc != abi.PE_NONE:
+                m["ClassFiltered"] = {key(nc): 1}
+            m["ConstraintFiltered"] = {key(k): 1}
+        else:
+            if nc != abi.PE_NONE:
+                m["ClassExhausted"] = {key(nc): 1}
+            m["DimensionExhausted"] = {key(v.mkey[r]): 1}
+        return m
+
+    served = 0
+    for i, r in enumerate(rows):
+        r = int(r)
+        ora.SetNodes([r])
+        ro = ora.SelectRaw(0)
+        mo = ora.LastMetrics()
+        bits = v.outcome[r] if v.n_rows else 0x7FF8000000000003
+        nan = (bits & 0x7FF8000000000000) == 0x7FF8000000000000
+        code = bits & 3 if nan else 0
+        if not v.n_rows or r >= v.n_rows or code == 3 or v.n_log >= v.log_cap:
+            eng.SetNodes([r])
+            re = eng.SelectRaw(0)
+            got = (re.row, re.final_score) if re.row >= 0 else None
+            me = eng.LastMetrics()
+            if re.row >= 0:
+                eng.Commit(0, re.row)
+        else:
+            assert v.mkey and v.mfailed, "the view carries no metric entries"
+            score = C.c_double.from_buffer_copy(C.c_uint64(bits)).value
+            me = view_maps(r, code, score)
+            if code:
+                v.log[v.n_log] = r | abi.PE_SYS_NIL
+                got = None
+            else:
+                v.log[v.n_log] = r | abi.PE_SYS_COMMITTED
+                v.outcome[r] = abi.PE_SYS_STALE
+                got = (r, score)
+            v.n_log += 1
+            served += 1
+        assert got == ((ro.row, ro.final_score) if ro.row >= 0 else None), i
+        assert me == mo, (i, me, mo)
+        if ro.row >= 0:
+            ora.Commit(0, ro.row)
+        if i == 50000:   # a crossing in the middle: the log is taken over, the last maps with it
+            assert eng.LastMetrics() == mo
+    assert served >= n - 10, served

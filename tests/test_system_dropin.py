@@ -197,6 +197,7 @@ def test_system_view_protocol_and_withdrawal():
     assert out_e[-1] == out_o[-1]
     ee, oe = e.Eligibility(), o.Eligibility()
     assert ee["job"] == oe["job"] and ee["tgs"] == oe["tgs"]
-    # metrics on: the served Selects would carry no metrics, the view goes
+    # metrics on: the outcomes carry no maps, the view goes until the next
+    # cache pass republishes it with its per-row metric entries
     e.EnableMetrics(True)
     assert v.n_rows == 0 and v.epoch != epoch

@@ -275,6 +275,10 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
     uint32_t n_rows = 0, log_cap = 0, n_log = 0, pre = 0;
     uint64_t* outcome = nullptr;
     uint32_t* log = nullptr;
+    const uint32_t *mkey = nullptr, *mclass = nullptr, *mnc = nullptr;
+    uint8_t* mfailed = nullptr;
+    const double* mscore = nullptr;
+    uint32_t m_inel = 0;
     auto load_view = [&]() {
         if (!v) return;
         n_rows = (v->tg_index == tg) ? v->n_rows : 0u;
@@ -283,6 +287,43 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
         pre = v->preempt;
         outcome = v->outcome;
         log = v->log;
+        mkey = v->mkey;
+        mclass = v->mclass;
+        mfailed = v->mfailed;
+        mscore = v->mscore;
+        mnc = v->mnode_class;
+        m_inel = v->mkey_ineligible;
+    };
+    // With metrics on, a served Select's maps as the shim assembles them from
+    // the view's per-row entries (nomad_pe.h pe_system_view)
+    auto view_maps = [&](uint32_t row, uint32_t code, double sc) {
+        if (!g_metrics || !mkey) return;
+        pe_metric_count c[2];
+        pe_metric_score m;
+        uint32_t nc = 0, ns = 0;
+        const uint32_t cls = mnc[row];
+        if (code == 0) {
+            std::memset(&m, 0, sizeof(m));
+            m.row = (int32_t)row;
+            m.n_scores = 1;
+            m.norm = sc;
+            m.scorer[0] = PE_SCORER_BINPACK;
+            m.score[0] = mscore[row];
+            ns = 1;
+        } else if (code == 1) {
+            uint32_t key = mkey[row];
+            const uint32_t mc = mclass[row];
+            if (mc != PE_NONE) {
+                if (mfailed[mc]) key = m_inel;
+                mfailed[mc] = 1;
+            }
+            if (cls != PE_NONE) c[nc++] = pe_metric_count{PE_METRIC_CLASS_FILTERED, cls, 1};
+            c[nc++] = pe_metric_count{PE_METRIC_CONSTRAINT_FILTERED, key, 1};
+        } else {
+            if (cls != PE_NONE) c[nc++] = pe_metric_count{PE_METRIC_CLASS_EXHAUSTED, cls, 1};
+            c[nc++] = pe_metric_count{PE_METRIC_DIMENSION_EXHAUSTED, mkey[row], 1};
+        }
+        copy_bin(c, nc, &m, ns);
     };
     load_view();
     for (uint32_t i = 0; i < n; i++) {
@@ -291,14 +332,16 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
             const uint64_t bits = outcome[row];
             const bool nan = (bits & 0x7FF8000000000000ull) == 0x7FF8000000000000ull;
             const uint32_t code = nan ? (uint32_t)(bits & 3u) : 0u;
-            if (code != 3u && !(code == 2u && pre)) {
+            if (code != 3u && !(code == 2u && pre) && (!g_metrics || mkey)) {
                 if (code) {   // nil: filtered or exhausted
+                    view_maps(row, code, 0.0);
                     log[n_log++] = row | PE_SYS_NIL;
                     status[i] = (uint8_t)code;
                     score[i] = __builtin_nan("");
                 } else {      // an option, appended to the plan
                     double sc;
                     std::memcpy(&sc, &bits, sizeof(sc));
+                    view_maps(row, 0u, sc);
                     log[n_log++] = row | PE_SYS_COMMITTED;
                     outcome[row] = PE_SYS_STALE;
                     status[i] = 0;
@@ -314,6 +357,7 @@ int dropin_system(const dropin_api* api, void* h, uint32_t tg, const uint32_t* r
         uint32_t limit;
         rc = api->set_nodes(h, rows + i, 1, &limit);
         if (!rc) rc = api->select(h, tg, &none, &opt);
+        if (!rc) rc = metrics_from_c(api, h);   // Allocation.Metrics (scheduler_system.go:334-337)
         if (!rc && opt.row >= 0) rc = commit_opt(api, h, tg, opt, 0);
         load_view();   // the crossing may have replaced or withdrawn the view
         g_sys_phase[0] += std::chrono::duration<double>(clk::now() - tc).count();
