@@ -945,6 +945,7 @@ struct pe_stack {
 
 extern "C" {
 static void elig_log_span(pe_stack* s, uint32_t tgi, uint32_t begin, uint32_t len);
+static void metrics_set_last_sys(pe_stack* s, uint32_t row, uint32_t code, bool failed_before);
 static void kid_log(pe_stack* s, uint8_t kind, uint32_t tgi, int32_t row, const uint32_t* a, uint32_t n);
 }
 
@@ -2651,8 +2652,6 @@ static void view_withdraw(pe_stack* s) {
 constexpr uint64_t kSysNaNBits = 0x7FF8000000000000ull;
 constexpr uint64_t kSysStale = kSysNaNBits | 3u;
 static_assert(kSysStale == PE_SYS_STALE, "the view's stale marker is the cache's");
-
-static void metrics_set_last_sys(pe_stack* s, uint32_t row, uint32_t code, bool failed_before);
 
 // The caller's log entries [k0, upto) with AllocMetric on: the memo of failing
 // classes as the sequential Selects left it (the engine's copy, then the
