@@ -482,7 +482,7 @@ def section_c4(device, rank, world, pg, cpu_s):
         st.SetJob(job)
         barrier(pg)
         t0 = time.perf_counter()
-        _, _, _, _, placed = shard.system_place_sharded(st, rows, rank, world)
+        _, _, _, _, placed = shard.system_place_sharded(st, rows, rank, world, view=True)
         dt = time.perf_counter() - t0
         barrier(pg)
         times.append(reduce(pg, dt, lambda d: d.ReduceOp.MAX))

@@ -460,9 +460,14 @@ void pe_last_phase_ms(const pe_stack* s, double* out4);
 /* SystemScheduler.computePlacements (scheduler_system.go:283-425) for one task
  * group over every row of the SetNodes list: one single-node Select per row.
  * out_row_score[n] = FinalScore or NaN when filtered/exhausted;
- * out_status[n] = 0 placed, 1 filtered, 2 exhausted. Commits placed allocs. */
+ * out_status[n] = 0 placed, 1 filtered, 2 exhausted. Commits placed allocs.
+ * Both arrays NULL: the results stay in the engine's page-locked staging,
+ * read through pe_system_results (no copy into caller memory). */
 int pe_system_place(pe_stack* s, uint32_t tg_index, double* out_score,
                     uint8_t* out_status, uint32_t* placed);
+/* The last pe_system_place's results in the engine's staging (score[n],
+ * status[n], as above), valid until the next pe_system_place on the handle. */
+int pe_system_results(const pe_stack* s, const double** score, const uint8_t** status, uint32_t* n);
 /* Full-scan Select sharded over GPUs (one process per GPU, each holding the
  * same snapshot, job, SetNodes list and plan). Each rank sweeps
  * the snapshot rows [row_begin, row_end) it owns into a pe_shard_rec: the

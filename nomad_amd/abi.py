@@ -230,7 +230,7 @@ ENGINE_SYMBOLS = [
     "pe_place_sharded", "pe_last_exchange_us", "pe_get_eligibility", "pe_put_eligibility", "pe_get_cursor",
     "pe_set_cursor", "pe_flush", "pe_system_spec_stats", "pe_device_count", "pe_set_kernel_split",
     "pe_last_kernel_split", "pe_preempted_of", "pe_spec_view_get", "pe_system_view_get", "pe_comm_library", "pe_last_exchange_stats",
-    "pe_last_metrics_bin", "pe_metric_string", "pe_scorer_name",
+    "pe_last_metrics_bin", "pe_metric_string", "pe_scorer_name", "pe_system_results",
 ]
 
 

@@ -782,6 +782,7 @@ struct pe_stack {
         bool mready = false;
     } sys;
     PinnedMem h_sys_cache;                // per row: FinalScore, or a NaN carrying the outcome (kSysDirty: stale)
+    uint32_t sys_res_n = 0;               // pe_system_results: entries of the last pe_system_place
     DevMem d_identity;
     uint32_t identity_n = 0;
     DevMem d_sys_res;                     // k_system_rows outcomes by row
@@ -4906,6 +4907,25 @@ int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_
     ApiScope prof_(s, "set_nodes");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     if (!rows && n) return s->fail(PE_EINVAL, "null rows");
+    if (n > 1 && n == s->visit.size() && std::memcmp(rows, s->visit.data(), sizeof(uint32_t) * n) == 0) {
+        // the same list again (a SystemScheduler evaluation over the same
+        // ready nodes, a replayed evaluation): already validated, and its
+        // device copy and visit ranks stay resident; the iterator restarts
+        const int frc = spec_flush(s);
+        if (frc) return frc;
+        s->gen++;
+        elig_resolve(s);
+        s->offset = 0;
+        uint32_t lim = 2;
+        if (s->cfg.stack_kind == PE_STACK_GENERIC && !s->cfg.batch) {
+            const uint32_t log_limit = (uint32_t)std::ceil(std::log2((double)n));
+            if (log_limit > lim) lim = log_limit;
+        }
+        s->limit = lim;
+        if (limit_out) *limit_out = lim;
+        invalidate_tables(s);
+        return PE_OK;
+    }
     // validate before touching any state: a rejected list leaves the previous one
     // in place. The same pass finds repeated rows (the chain and sweep loops and
     // the system placement need a list without them).
@@ -7773,7 +7793,9 @@ static int system_place_distinct(pe_stack* s, uint32_t tgi, TgPlan& g, double* o
 }
 
 static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
-    if (!s || !out_score || !out_status) return PE_EINVAL;
+    // out_score and out_status both null: the results stay in the engine's
+    // page-locked staging (pe_system_results), no copy into the caller's arrays
+    if (!s || (!out_score) != (!out_status)) return PE_EINVAL;
     {
         const int frc = spec_flush(s);
         if (frc) return frc;
@@ -7820,7 +7842,8 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
         const uint32_t nn = (uint32_t)s->nodes.size();
         HIP_TRY(s, s->d_rank_of.ensure(sizeof(uint32_t) * (size_t)std::max<uint32_t>(nn, 1)));
         HIP_TRY(s, s->d_sys_res.ensure(sizeof(uint64_t) * (size_t)std::max<uint32_t>(nn, 1)));
-        HIP_TRY(s, pe_launch_rank_of(s->d_visit.as<uint32_t>(), n, s->d_rank_of.as<uint32_t>(), nn, s->stream));
+        if (!s->rank_of_valid)   // (kept while the list is unchanged)
+            HIP_TRY(s, pe_launch_rank_of(s->d_visit.as<uint32_t>(), n, s->d_rank_of.as<uint32_t>(), nn, s->stream));
         s->rank_of_valid = true;   // the same table ensure_rank_of would build
         A.rank_of = s->d_rank_of.as<uint32_t>();
         A.res = s->d_sys_res.as<uint64_t>();
@@ -7853,8 +7876,14 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
             std::memcpy(&v, h + placed_off + 4 * k, 4);
             p += v;
         }
-        std::memcpy(out_score, h, sizeof(double) * n);
-        std::memcpy(out_status, h + st_off, n);
+        if (out_score) {
+            std::memcpy(out_score, h, sizeof(double) * n);
+            std::memcpy(out_status, h + st_off, n);
+        } else {   // the staging arrays are the results (and the inputs of the steps below)
+            out_score = reinterpret_cast<double*>(s->h_sys_out.as<uint8_t>());
+            out_status = s->h_sys_out.as<uint8_t>() + st_off;
+        }
+        s->sys_res_n = n;
     }
     ApiScope prof_p_(s, "system.plan");
     float ms = 0;
@@ -7886,6 +7915,7 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
         if (g.ask.cores > 0)   // the host mirror of the placements' reserved cores
             for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) core_record(s, g, (int32_t)s->visit[i], true, cores);
     }
+
     if (s->cfg.preempt) {
         // BinPack with evict (stack.go:267-278) on the nodes the plain fit exhausted
         std::vector<uint32_t> pos, rows;
@@ -8060,6 +8090,16 @@ static int system_place_one(pe_stack* s, uint32_t tgi, double* out_score, uint8_
     // one single-node Select per row of the list (scheduler_system.go:290-422)
     if (rc == PE_OK) elig_log_span(s, tgi, 0, (uint32_t)s->visit.size());
     return rc;
+}
+
+int pe_system_results(const pe_stack* s, const double** score, const uint8_t** status, uint32_t* n) {
+    if (!s || !score || !status || !n) return PE_EINVAL;
+    if (!s->h_sys_out.p || !s->sys_res_n) return PE_ESTATE;
+    const size_t st_off = sizeof(double) * (size_t)s->sys_res_n;
+    *score = reinterpret_cast<const double*>(s->h_sys_out.as<uint8_t>());
+    *status = s->h_sys_out.as<uint8_t>() + st_off;
+    *n = s->sys_res_n;
+    return PE_OK;
 }
 
 int pe_place_sharded(pe_stack* s, uint32_t tgi, uint32_t count, uint32_t row_begin, uint32_t row_end,
@@ -8622,9 +8662,9 @@ int pe_preempted_of(const pe_stack* s, uint32_t record, uint32_t* out, uint32_t 
 
 int pe_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint8_t* out_status, uint32_t* placed) {
     PE_FLUSH_RESET(s);
-    if (!s || !out_score || !out_status) return PE_EINVAL;
+    if (!s || (!out_score) != (!out_status)) return PE_EINVAL;
     s->pre_overflow.clear();
-    if (!s->kids.empty() && s->kids_valid) {
+    if (!s->kids.empty() && s->kids_valid && out_score) {   // (the staged-results form runs on the root)
         int rc = spec_flush(s);
         if (rc) return rc;
         if (multi_system_ok(s, tgi) && kids_sync(s) == PE_OK) {

@@ -120,13 +120,14 @@ def device_place(stack, tg, count: int, n_rows: int, rank: int, world: int):
     return stack.PlaceSharded(tg, count, b, e)
 
 
-def system_place_sharded(stack, rows: Sequence[int], rank: int, world: int, tg=0):
+def system_place_sharded(stack, rows: Sequence[int], rank: int, world: int, tg=0, view: bool = False):
     """SystemScheduler placements over this rank's range of the SetNodes list.
-    Returns (begin, end, scores, statuses, placed) for the range."""
+    Returns (begin, end, scores, statuses, placed) for the range; with `view`
+    the arrays are the engine's staging (valid until its next SystemPlace)."""
     rows = np.asarray(rows, dtype=np.uint32)
     b, e = shard_range(len(rows), rank, world)
     stack.SetNodes(rows[b:e])
-    score, status, placed = stack.SystemPlace(tg)
+    score, status, placed = stack.SystemPlaceView(tg) if view else stack.SystemPlace(tg)
     return b, e, score, status, placed
 
 

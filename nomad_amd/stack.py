@@ -514,6 +514,22 @@ class _Stack:
         self._check(self._fn("place")(self._h, self._tg_index(tg), count, out, C.byref(placed)))
         return arr["row"].copy(), arr["final_score"].copy(), placed.value, arr
 
+    def SystemPlaceView(self, tg):
+        """SystemPlace with the results left in the engine's page-locked
+        staging (pe_system_place with null arrays + pe_system_results): numpy
+        views valid until the next SystemPlace on this stack, no copy."""
+        placed = C.c_uint32(0)
+        self._check(self._fn("system_place")(self._h, self._tg_index(tg), None, None, C.byref(placed)))
+        lib = self._lib
+        lib.pe_system_results.restype = C.c_int
+        lib.pe_system_results.argtypes = [C.c_void_p, C.POINTER(abi.f64p), C.POINTER(abi.u8p), abi.u32p]
+        sc, st, n = abi.f64p(), abi.u8p(), C.c_uint32(0)
+        self._check(lib.pe_system_results(self._h, C.byref(sc), C.byref(st), C.byref(n)))
+        if n.value == 0:
+            return np.empty(0), np.empty(0, dtype=np.uint8), placed.value
+        return (np.ctypeslib.as_array(sc, shape=(n.value,)), np.ctypeslib.as_array(st, shape=(n.value,)),
+                placed.value)
+
     def SystemPlace(self, tg):
         n = len(self._visit)
         score = np.empty(max(1, n), dtype=np.float64)

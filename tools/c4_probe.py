@@ -16,14 +16,15 @@ job = synth.mock_system_job()
 rows = np.random.Generator(np.random.PCG64(5)).permutation(n).astype(np.uint32)
 st = SystemStack()
 st.SetStateColumnar(cs)
-for i in range(6):
+for i in range(12):
+    view = i >= 6   # the zero-copy results (SystemPlaceView) for the second half
     st.ResetPlan()
     st.SetJob(job)
     t0 = time.perf_counter()
     st.SetNodes(rows)
     t1 = time.perf_counter()
-    _, _, placed = st.SystemPlace(0)
+    _, _, placed = st.SystemPlaceView(0) if view else st.SystemPlace(0)
     t2 = time.perf_counter()
-    print("iter %d: SetNodes %.1f us, SystemPlace %.1f us (kernel %.1f us), placed %d"
-          % (i, (t1 - t0) * 1e6, (t2 - t1) * 1e6, st.last_kernel_ms() * 1e3, placed))
+    print("iter %d%s: SetNodes %.1f us, SystemPlace %.1f us (kernel %.1f us), placed %d"
+          % (i, " view" if view else "", (t1 - t0) * 1e6, (t2 - t1) * 1e6, st.last_kernel_ms() * 1e3, placed))
 st.close()
