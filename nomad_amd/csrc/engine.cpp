@@ -694,7 +694,15 @@ struct pe_stack {
     // retired task groups whose device tables the next SetJob reuses: freeing
     // them (hipFree) would synchronise the device on every evaluation
     std::vector<std::unique_ptr<TgPlan>> tg_pool;
-    std::vector<std::pair<uint32_t, uint32_t>> plan;   // committed (tg name id, row)
+    std::vector<std::pair<uint32_t, uint32_t>> plan;   // committed (tg name id, row); read through plan_of
+    // a system placement's plan entries not yet written out: the rows of
+    // `visit` whose staged outcome is 0 (written by plan_settle when the plan
+    // is next read, dropped by ResetPlan)
+    struct PlanDefer {
+        bool active = false;
+        uint32_t name = 0, n = 0;
+        const uint8_t* status = nullptr;
+    } plan_defer;
 
     // SpreadIterator bookkeeping (spread.go:99-102, 254)
     std::set<uint32_t> spread_info_done;
@@ -943,6 +951,30 @@ struct pe_stack {
         }
     }
 };
+
+// The deferred system placement's Plan.AppendAlloc entries (list order).
+static void plan_settle(pe_stack* s) {
+    pe_stack::PlanDefer& d = s->plan_defer;
+    if (!d.active) return;
+    d.active = false;
+    const uint32_t n = std::min<uint32_t>(d.n, (uint32_t)s->visit.size());
+    size_t p = 0;
+    for (uint32_t i = 0; i < n; i++) p += d.status[i] == 0;
+    const size_t base = s->plan.size();
+    s->plan.resize(base + p + 1);   // one slot of slack: the writes below are branch-free
+    std::pair<uint32_t, uint32_t>* w = s->plan.data() + base;
+    for (uint32_t i = 0; i < n; i++) {
+        w->first = d.name;
+        w->second = s->visit[i];
+        w += d.status[i] == 0;
+    }
+    s->plan.resize(base + p);
+}
+
+static inline std::vector<std::pair<uint32_t, uint32_t>>& plan_of(pe_stack* s) {
+    plan_settle(s);
+    return s->plan;
+}
 
 extern "C" {
 static void elig_log_span(pe_stack* s, uint32_t tgi, uint32_t begin, uint32_t len);
@@ -2555,7 +2587,7 @@ static void spec_confirm_rec(pe_stack* s, uint32_t k, bool kids) {
     const int32_t row = spec_rec_row(sp, k);
     if (row < 0) return;
     s->gen++;
-    s->plan.emplace_back(s->tgs[sp.tgi]->name, (uint32_t)row);
+    plan_of(s).emplace_back(s->tgs[sp.tgi]->name, (uint32_t)row);
     invalidate_job_distinct(s, sp.tgi);
     if (kids && !s->kids.empty()) {
         const uint32_t np = spec_rec_npre(sp, k);
@@ -2691,6 +2723,7 @@ static void sys_view_take_metrics(pe_stack* s, uint32_t k0, uint32_t upto) {
 static void sys_view_take(pe_stack* s) {
     pe_system_view& v = s->sysview;
     if (!v.n_rows || v.n_log == s->sys_taken) return;
+    plan_settle(s);   // the take-over moves the list
     ApiScope prof_(s, "sys_view_take");
     pe_stack::SysSpec& y = s->sys;
     const uint32_t upto = std::min(v.n_log, v.log_cap);
@@ -2723,9 +2756,9 @@ static void sys_view_take(pe_stack* s) {
             c += (!last_nil && (e & PE_SYS_COMMITTED)) ? 1u : 0u;
         }
         y.pending.resize(p0 + c);
-        const size_t l0 = s->plan.size();
-        s->plan.resize(l0 + c);
-        for (size_t i = 0; i < c; i++) s->plan[l0 + i] = std::make_pair(name, q[i]);
+        const size_t l0 = plan_of(s).size();
+        plan_of(s).resize(l0 + c);
+        for (size_t i = 0; i < c; i++) plan_of(s)[l0 + i] = std::make_pair(name, q[i]);
         if (cnt) {
             const uint32_t le = v.log[upto - 1];
             const bool committed = !last_nil && (le & PE_SYS_COMMITTED) && (le & PE_SYS_ROW_MASK) == last;
@@ -2773,7 +2806,7 @@ static void sys_view_take(pe_stack* s) {
             y.served_row = -1;
             y.pending.push_back(row);
             cache[row] = kSysStale;
-            s->plan.emplace_back(name, row);
+            plan_of(s).emplace_back(name, row);
             s->offer_row = -1;
         }
     }
@@ -2823,6 +2856,7 @@ static void sys_deactivate(pe_stack* s) {
 // from the views, then launches a deferred ResetPlan copy.
 #define PE_FLUSH_RESET(s)                             \
     do {                                              \
+        if (s) plan_settle(s);                        \
         if (s) view_take(s);                          \
         if ((s) && ((s)->reset_pending || (s)->fold_pending)) { \
             const int frc_ = flush_reset(s);          \
@@ -2849,7 +2883,7 @@ int build_collisions(pe_stack* s, bool own = false, bool defer = false) {
         };
         for (uint32_t i : s->own_allocs())
             if (!s->stopped(i)) { add(s->allocs[i].row, s->allocs[i].tg); if (own) mine[s->allocs[i].row]++; }
-        for (auto& p : s->plan) add(p.second, p.first);
+        for (auto& p : plan_of(s)) add(p.second, p.first);
         if (own) HIP_TRY(s, upload_s(s, s->d_own_existing, mine));
         HIP_TRY(s, upload_s(s, s->d_coll_job, job));
         for (uint32_t g = 0; g < ntg; g++) HIP_TRY(s, upload_s(s, s->tgs[g]->coll_tg, tg[g]));
@@ -2864,7 +2898,7 @@ int build_collisions(pe_stack* s, bool own = false, bool defer = false) {
     };
     for (uint32_t i : s->own_allocs())
         if (!s->stopped(i)) add(s->allocs[i].row, s->allocs[i].tg, own);   // ProposedAllocs drops plan stops
-    for (auto& p : s->plan) add(p.second, p.first, false);
+    for (auto& p : plan_of(s)) add(p.second, p.first, false);
     std::sort(keys.begin(), keys.end());
     std::vector<uint2> ents;
     for (size_t i = 0; i < keys.size();) {
@@ -2932,7 +2966,7 @@ std::vector<uint32_t> cleared_counts(pe_stack* s, size_t nvals, F node_val, bool
         }
     if (!any) return {};
     std::vector<uint8_t> prop(nvals, 0);
-    for (auto& p : s->plan)
+    for (auto& p : plan_of(s))
         if (job_level || p.first == tg_name) {
             const uint32_t v = node_val(p.second);
             if (v != pe::kMissing) prop[v] = 1;
@@ -3000,7 +3034,7 @@ int build_psets(pe_stack* s, TgPlan& g) {
                 uint32_t v = node_val(a.row);
                 if (v != pe::kMissing) ps->h_counts[v]++;
             }
-        for (auto& p : s->plan)
+        for (auto& p : plan_of(s))
             if (p.first == g.name) {
                 uint32_t v = node_val(p.second);
                 if (v != pe::kMissing) ps->h_counts[v]++;
@@ -3103,7 +3137,7 @@ int build_psets(pe_stack* s, TgPlan& g) {
                 const uint32_t v = node_val(a.row);
                 if (v != pe::kMissing) ps->h_counts[v]++;
             }
-        for (auto& p : s->plan)
+        for (auto& p : plan_of(s))
             if (job_level || p.first == g.name) {
                 const uint32_t v = node_val(p.second);
                 if (v != pe::kMissing) ps->h_counts[v]++;
@@ -3310,7 +3344,7 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         // proposed snapshot allocs, this group's placements). The device adds
         // the group's later placements (gate).
         std::vector<uint8_t> own(n, 0), blocked(n, 0);
-        for (auto& p : s->plan)
+        for (auto& p : plan_of(s))
             if (p.first == g.name && p.second < n) own[p.second] = 1;
         const bool task = g.rports.empty();
         for (uint32_t r = 0; r < (uint32_t)n; r++)
@@ -4186,7 +4220,7 @@ int run_place(pe_stack* s, uint32_t tgi, uint32_t count, int commit, const std::
         }
         if (commit)
             for (uint32_t i = 0; i < st[0]; i++)
-                s->plan.emplace_back(g.name, (uint32_t)(chain && sink ? (*sink)[done + i].row : out[done + i].row));
+                plan_of(s).emplace_back(g.name, (uint32_t)(chain && sink ? (*sink)[done + i].row : out[done + i].row));
         if (hprof) {
             const double t3 = now_us();
             h_launch += t1 - t0;
@@ -4549,6 +4583,7 @@ static void elig_visit_list(pe_stack* s, uint32_t tgi, const std::vector<uint32_
 }
 
 static int set_state_one(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const pe_alloc_table* allocs) {
+    if (s) plan_settle(s);   // the deferred entries index the current list
     if (s) s->jf.clear();   // node attributes change: the job checkers run again
     if (!s || !strs || !nodes) return PE_EINVAL;
     spec_drop(s);
@@ -4561,7 +4596,7 @@ static int set_state_one(pe_stack* s, const pe_strtab* strs, const pe_node_table
     s->sid.clear();
     s->add_strings(strs);
     s->have_state = false;
-    s->plan.clear();
+    plan_of(s).clear();
     s->tg_memo.clear();
     s->job_memo.clear();
     s->ref_tg_memo.clear();
@@ -4581,6 +4616,7 @@ static int set_state_one(pe_stack* s, const pe_strtab* strs, const pe_node_table
 }
 
 static int update_allocs_one(pe_stack* s, const pe_strtab* strs, const pe_alloc_table* allocs, const uint32_t* index) {
+    if (s) plan_settle(s);   // the deferred entries index the current list
     if (!s || !allocs) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
@@ -4605,7 +4641,7 @@ static int update_allocs_one(pe_stack* s, const pe_strtab* strs, const pe_alloc_
     // a new evaluation context, as after pe_set_state
     std::fill(s->h_preempted.begin(), s->h_preempted.end(), 0);
     s->offer_row = -1;
-    s->plan.clear();
+    plan_of(s).clear();
     s->tg_memo.clear();
     s->job_memo.clear();
     s->ref_tg_memo.clear();
@@ -4623,6 +4659,7 @@ static int update_allocs_one(pe_stack* s, const pe_strtab* strs, const pe_alloc_
 }
 
 static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_table* nodes, const uint32_t* index) {
+    if (s) plan_settle(s);   // the deferred entries index the current list
     if (s) s->jf.clear();   // node attributes change: the job checkers run again
     if (!s || !nodes) return PE_EINVAL;
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
@@ -4653,7 +4690,7 @@ static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_ta
     std::vector<uint32_t> rows;
     for (uint32_t r : target)
         if (r < n_old) rows.push_back(r);
-    s->plan.clear();
+    plan_of(s).clear();
     s->tg_memo.clear();
     s->job_memo.clear();
     s->ref_tg_memo.clear();
@@ -4675,6 +4712,7 @@ static int update_nodes_one(pe_stack* s, const pe_strtab* strs, const pe_node_ta
 // SetJob's k_counts launch (one launch less per evaluation)
 static int reset_plan_one(pe_stack* s, bool may_defer) {
     if (!s) return PE_EINVAL;
+    s->plan_defer.active = false;   // the plan is emptied below
     ApiScope prof_(s, "reset_plan");
     if (!s->have_state) return s->fail(PE_ESTATE, "pe_set_state not called");
     spec_drop(s);
@@ -4698,7 +4736,7 @@ static int reset_plan_one(pe_stack* s, bool may_defer) {
     s->node_update.clear();
     s->stop_count.assign(s->allocs.size(), 0);
     s->offer_row = -1;   // stream-ordered: later launches and uploads see the reset state
-    s->plan.clear();
+    plan_of(s).clear();
     s->tg_memo.clear();
     s->job_memo.clear();
     s->ref_tg_memo.clear();
@@ -4888,6 +4926,7 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
 
 int pe_set_nodes(pe_stack* s, const uint32_t* rows, uint32_t n, uint32_t* limit_out) {
     if (!s) return PE_EINVAL;
+    plan_settle(s);   // the deferred entries index the current list
     sys_view_take(s);   // the caller's served system Selects first
     if (n == 1 && rows && s->sys.active && s->visit.size() == 1 && rows[0] < s->nodes.size()) {
         // SystemScheduler's per-node SetNodes while the per-row cache answers:
@@ -6122,7 +6161,7 @@ static int commit_impl(pe_stack* s, uint32_t tgi, int32_t row) {
     s->offer_row = -1;
     HIP_TRY_STATE(s, pe_launch_commit(&soa, &t, &a, (uint32_t)row, offers, s->stream));
     HIP_TRY(s, hipStreamSynchronize(s->stream));
-    s->plan.emplace_back(g.name, (uint32_t)row);
+    plan_of(s).emplace_back(g.name, (uint32_t)row);
     invalidate_job_distinct(s, tgi);
     if (g.psets_dynamic) g.psets_built = false;   // cleared values: GetCombinedUseMap is not additive
     // the coll_tg of other task groups with the same name also see this alloc
@@ -6394,7 +6433,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     for (uint32_t k = 0; k < recs; k++) std::memset(out[k].preempted, 0, sizeof(out[k].preempted));
     for (uint32_t k = 0; k < p; k++) {
         const uint32_t row = (uint32_t)out[k].row;
-        s->plan.emplace_back(g.name, row);
+        plan_of(s).emplace_back(g.name, row);
         set_preempted(s, out[k], rec0 + k, row, masks.data() + (size_t)k * words, words, true);
     }
     *placed = p;
@@ -6513,7 +6552,7 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
     s->last_ms_pending = false;
-    for (uint32_t i = 0; i < p; i++) s->plan.emplace_back(g.name, (uint32_t)out[i].row);   // Plan.AppendAlloc
+    for (uint32_t i = 0; i < p; i++) plan_of(s).emplace_back(g.name, (uint32_t)out[i].row);   // Plan.AppendAlloc
     s->offer_row = -1;
     *placed = p;
     return PE_OK;
@@ -7010,7 +7049,7 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     // placements of the group still to come in this evaluation (tg.Count minus
     // the plan's), at least the run length grown from earlier used-up runs
     uint32_t done = 0;
-    for (auto& p : s->plan) done += p.first == g.name;
+    for (auto& p : plan_of(s)) done += p.first == g.name;
     uint32_t count = g.count > 0 && (uint32_t)g.count > done ? (uint32_t)g.count - done : 0u;
     // The phase-static chain (k_base + k_chain) costs about the same for one
     // placement as for the whole count: run the group's remaining count. Every
@@ -7031,7 +7070,7 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
         rc = spec_copy(s, g, true);
         if (rc) return rc;
     }
-    const size_t plan0 = s->plan.size();
+    const size_t plan0 = plan_of(s).size();
     if (sp.recs.size() < count) sp.recs.resize(count);
     uint32_t placed = 0;
     s->emit_sink = sp.evict ? nullptr : &sp.crecs;
@@ -7049,7 +7088,7 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     s->emit_sink = nullptr;
     s->nil_sink = nullptr;
     sp.compact = !sp.evict && s->emit_sunk;
-    s->plan.resize(plan0);   // the plan holds confirmed placements only
+    plan_of(s).resize(plan0);   // the plan holds confirmed placements only
     // A failed run leaves the device as the caller last saw it (and the host
     // mirror of the preempted allocs: the run's placements are dropped).
     auto undo_run = [&](int err) {
@@ -7174,7 +7213,7 @@ static int commit_one(pe_stack* s, uint32_t tgi, int32_t row) {
         s->sys.served_row = -1;
         s->sys.pending.push_back((uint32_t)row);
         s->h_sys_cache.as<uint64_t>()[(uint32_t)row] = kSysDirty;
-        s->plan.emplace_back(s->tgs[tgi]->name, (uint32_t)row);
+        plan_of(s).emplace_back(s->tgs[tgi]->name, (uint32_t)row);
         s->offer_row = -1;
         return PE_OK;
     }
@@ -7480,7 +7519,7 @@ static int place_sharded_impl(pe_stack* s, uint32_t tgi, uint32_t count, uint32_
     HIP_TRY(s, hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
     s->last_ms_pending = false;
-    for (uint32_t i = 0; i < p; i++) s->plan.emplace_back(g.name, (uint32_t)out[i].row);   // Plan.AppendAlloc
+    for (uint32_t i = 0; i < p; i++) plan_of(s).emplace_back(g.name, (uint32_t)out[i].row);   // Plan.AppendAlloc
     invalidate_job_distinct(s, tgi);
     s->offer_row = -1;
     if (placed) *placed = p;
@@ -7644,7 +7683,7 @@ int pe_place_batch(pe_stack* s, uint32_t tgi, uint32_t count, pe_placement* out,
         if (frc) return frc;
     }
     if (s->cfg.stack_kind != PE_STACK_GENERIC) return s->fail(PE_ESTATE, "pe_place_batch needs a generic stack");
-    if (!s->plan.empty()) return s->fail(PE_ESTATE, "batch evaluations start from a fresh plan (pe_reset_plan)");
+    if (!plan_of(s).empty()) return s->fail(PE_ESTATE, "batch evaluations start from a fresh plan (pe_reset_plan)");
     if (!s->have_job || tgi >= s->tgs.size()) return s->fail(PE_ESTATE, "pe_set_job not called / bad task group");
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(s, hipSetDevice(s->device));
@@ -7783,7 +7822,7 @@ static int system_place_distinct(pe_stack* s, uint32_t tgi, TgPlan& g, double* o
         HIP_TRY_STATE(s, pe_launch_commit_rows(&soa, &t, &a, s->d_commit_rows.as<uint32_t>(), (uint32_t)accepted.size(),
                                          s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
-        for (uint32_t r : accepted) s->plan.emplace_back(g.name, r);
+        for (uint32_t r : accepted) plan_of(s).emplace_back(g.name, r);
     }
     for (auto& q : g.psets) q->h_counts.clear();   // stale: the next Select rebuilds the sets
     g.psets_built = false;
@@ -7796,6 +7835,7 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
     // out_score and out_status both null: the results stay in the engine's
     // page-locked staging (pe_system_results), no copy into the caller's arrays
     if (!s || (!out_score) != (!out_status)) return PE_EINVAL;
+    plan_settle(s);   // the staging below is overwritten
     {
         const int frc = spec_flush(s);
         if (frc) return frc;
@@ -7900,17 +7940,14 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
         return PE_OK;
     }
     {
-        // Plan.AppendAlloc of every placed node, branch-free (one slot of slack)
-        const size_t base = s->plan.size();
-        s->plan.resize(base + p + 1);
-        std::pair<uint32_t, uint32_t>* w = s->plan.data() + base;
-        const uint32_t nm = g.name;
-        for (uint32_t i = 0; i < n; i++) {
-            w->first = nm;
-            w->second = s->visit[i];
-            w += out_status[i] == 0;
-        }
-        s->plan.resize(base + p);
+        // Plan.AppendAlloc of every placed node: written when the plan is next
+        // read (plan_settle; ResetPlan drops it), from the staged outcomes when
+        // the caller reads them there, else from its copy
+        s->plan_defer.active = true;
+        s->plan_defer.name = g.name;
+        s->plan_defer.n = n;
+        s->plan_defer.status = s->h_sys_out.as<uint8_t>() + st_off;
+        if (s->cfg.preempt || g.ask.cores > 0) plan_settle(s);   // the steps below append / read it
         uint64_t cores[4];
         if (g.ask.cores > 0)   // the host mirror of the placements' reserved cores
             for (uint32_t i = 0; i < n; i++) if (out_status[i] == 0) core_record(s, g, (int32_t)s->visit[i], true, cores);
@@ -8008,7 +8045,7 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
                     if (st[k] != 0) continue;   // exhausted / skipped nodes stay exhausted
                     out_status[pos[k]] = 0;
                     out_score[pos[k]] = sc[k];
-                    s->plan.emplace_back(g.name, rows[k]);
+                    plan_of(s).emplace_back(g.name, rows[k]);
                     pe_ranked_node r;   // the host mirrors of the evictions k_commit_evicted applied
                     set_preempted(s, r, k, rows[k], masks.data() + (size_t)k * W, W, true);
                     p++;
@@ -8420,7 +8457,7 @@ static int multi_place(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node
     s->last_ms = ms;
     s->last_ms_pending = false;
     for (pe_stack* x : st) {
-        for (uint32_t i = 0; i < p; i++) x->plan.emplace_back(x->tgs[tgi]->name, (uint32_t)out[i].row);
+        for (uint32_t i = 0; i < p; i++) plan_of(x).emplace_back(x->tgs[tgi]->name, (uint32_t)out[i].row);
         invalidate_job_distinct(x, tgi);
         x->offer_row = -1;
         x->gen++;
@@ -8525,7 +8562,7 @@ static int multi_system_place(pe_stack* s, uint32_t tgi, double* out_score, uint
         HIP_TRY(s, hipSetDevice(x->device));
         HIP_TRY(s, hipStreamSynchronize(x->stream));
         for (uint32_t e = 0; e < N; e++)
-            for (uint32_t r : rows[e]) x->plan.emplace_back(x->tgs[tgi]->name, r);   // list order
+            for (uint32_t r : rows[e]) plan_of(x).emplace_back(x->tgs[tgi]->name, r);   // list order
         sys_deactivate(x);
         x->gen++;
     }
