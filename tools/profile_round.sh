@@ -27,6 +27,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
   python3 "$ROOT/bench.py" --no-cpu --steps 10 --warmup 2 --sections "" > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5trace" -o c5 -- \
   python3 "$ROOT/tools/c5_prof.py" 4 > "$OUT/c5trace.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c3trace" -o c3 -- \
+  python3 "$ROOT/tools/c3_full_prof.py" > "$OUT/c3trace.log" 2>&1
 cd "$ROOT"
 bash tools/headline_pmc.sh > "$OUT/headline_pmc.log" 2>&1
 cp gpurun_out/headline_pmc/headline_traffic.json "$OUT/headline_traffic.json"
