@@ -205,7 +205,7 @@ def cpu_baseline(nodes, allocs, job, seconds):
 # Scoring sweep bytes per node (pe_last_sweep_bytes): 64 B NodeRec + 4 B folded
 # score word (verdict, affinity index, spread values; 1 B verdict when the word
 # does not apply: 73 B) + 4 B (job,tg) collisions + 4 B visit rank = 76 B.
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "sweep_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r06", "sweep_traffic.json")
 CHAIN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "c2_batch_traffic.json")
 PLAN_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "plan_traffic.json")
 
@@ -234,7 +234,7 @@ def chain_traffic(evals_per_launch):
     return t["bytes_per_launch"]
 
 
-HEADLINE_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "headline_traffic.json")
+HEADLINE_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r06", "headline_traffic.json")
 
 
 def headline_traffic(node_evals):
