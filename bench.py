@@ -875,7 +875,9 @@ def section_ingest(device, n=100000, reps=5):
     lib, h = st._lib, st._h
     lib.pe_update_allocs.restype = C.c_int
     lib.pe_update_allocs.argtypes = [C.c_void_p, C.POINTER(abi.pe_strtab), C.POINTER(abi.pe_alloc_table), abi.u32p]
+    t_enc = time.perf_counter()
     es = EncodedState(nodes, allocs, Interner())
+    enc_s = time.perf_counter() - t_enc
     t_full, t_upd = [], []
     idx = np.asarray(index, dtype=np.uint32)
     for _ in range(reps):
@@ -926,7 +928,10 @@ def section_ingest(device, n=100000, reps=5):
                         % (n, len(allocs), sum(1 for i in index if i != abi.PE_NONE),
                            sum(1 for i in index if i == abi.PE_NONE), n // 100, n // 1000),
             "set_state_ms": full * 1e3, "update_allocs_ms": upd * 1e3, "speedup": full / upd,
-            "update_nodes_ms": unodes * 1e3}
+            "update_nodes_ms": unodes * 1e3, "python_encode_ms": enc_s * 1e3,
+            "note": "set_state / update_* time the C calls alone on already flattened tables (the engine's host "
+                    "interning, class and signature building and uploads); python_encode_ms is the Python "
+                    "flattening of the same snapshot (the cgo shim's work), timed apart"}
 
 
 def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
@@ -968,6 +973,8 @@ def section_plan_apply(device, rank, world, pg, cpu_s, n=100000, reps=8):
            "call_ms": wall * 1e3, "plan_nodes_per_s_call": n / wall,
            "call_note": "call = host flattening of the plan's allocs + PCIe upload + kernel + reasons back",
            "snapshot_upload_s": upload_s,
+           "snapshot_split_s": dict(zip(("python_encode", "pe_planner_set_state"),
+                                        getattr(pl, "last_set_state_split", (None, None)))),
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": plan_traffic(bytes_launch) if world == 1 else None,
                         "kernel": "k_plan_eval",

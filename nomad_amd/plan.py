@@ -354,11 +354,16 @@ class Planner:
         self.alloc_index = {a.id: i for i, a in enumerate(self.allocs)}
         # one growing string table for the snapshot and every later plan: the
         # library then maps only the strings a call adds
+        import time
+        t0 = time.perf_counter()
         self.interner = it = Interner()
         nt, nk = encode_nodes(self.nodes, it)
         at, ak = encode_allocs(self.allocs, it, [self.row_of[a.node_id] for a in self.allocs])
         st, sk = it.table()
+        t1 = time.perf_counter()
         self._check(self.lib.pe_planner_set_state(self.h, C.byref(st), C.byref(nt), C.byref(at)))
+        # (the Python flattening, the pe_planner_set_state call on the flat arrays) in seconds
+        self.last_set_state_split = (t1 - t0, time.perf_counter() - t1)
 
     def snapshot_alloc(self, alloc_id: str) -> Optional[PlanAlloc]:
         j = self.alloc_index.get(alloc_id)
