@@ -144,6 +144,8 @@ hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint
                                   hipStream_t st);
 hipError_t pe_launch_sweep_only(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t pe_launch_sweep_local(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const uint32_t* rows, const uint32_t* rec_end,
+                               uint32_t n_rec, uint32_t flags, pe_metric_score* out, uint8_t* n_out, hipStream_t st);
 hipError_t pe_launch_step_only(const pe::SweepArgs* a, uint32_t nrecs, const uint32_t* visit, uint32_t n,
                                uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_commit_rows(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
@@ -796,7 +798,8 @@ struct pe_stack {
     DevMem d_sys_res;                     // k_system_rows outcomes by row
     uint64_t test_fallback_every = 0, test_select_calls = 0;   // PE_TEST_FALLBACK_EVERY
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
-    PinnedMem h_trace_codes, h_trace_sc;   // spec_metrics: the batched trace's outcomes
+    PinnedMem h_trace_codes, h_trace_top;   // spec_metrics: the batched trace's outcomes and ScoreMetaData
+    DevMem d_trace_rec_end, d_trace_top;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
     DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;
     DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)
@@ -5185,7 +5188,18 @@ static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& or
         rt[c] = v;
     };
     jf_ready(s);
+    // the loop's tables in locals (the row pushes would make the compiler
+    // reload every member); the vectors are not resized inside it
     const uint32_t* cls_of = s->jf_cls.data();
+    const char** jfp = s->jf.data();
+    int8_t* jm = s->ref_job_memo.data();
+    int8_t* tm = rt.data();
+    const bool job_esc = s->job_escaped, job_cons = !s->job_constraints.empty(), tg_esc = g.escaped;
+    auto job_why = [&](uint32_t row) -> const char* {   // job_fail_cached, its hit inlined
+        const char* w = jfp[row];
+        if (!w) return job_fail_cached(s, ev, row);   // fills jfp[row]
+        return w == kJfPass ? nullptr : w;
+    };
     uint32_t p = m ? start % (uint32_t)m : 0;
     for (uint32_t k = 0; k < evaluated && m; k++, p = p + 1 == m ? 0 : p + 1) {
         const uint32_t row = order[p];
@@ -5193,21 +5207,21 @@ static void metrics_walk(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& or
         const char* why = nullptr;
         // the node's attribute views only when a checker runs (a known class
         // decides the common case from the memo alone)
-        if (s->job_escaped) {
-            why = job_fail_cached(s, ev, row);
-        } else if (s->ref_job_memo[c] == 0) {
+        if (job_esc) {
+            why = job_why(row);
+        } else if (jm[c] == 0) {
             why = kIneligible;
-        } else if (s->ref_job_memo[c] == -1 || !s->job_constraints.empty()) {
-            why = job_fail_cached(s, ev, row);
+        } else if (jm[c] == -1 || job_cons) {
+            why = job_why(row);
             if (why) set_job(c, 0);
-            else if (s->ref_job_memo[c] == -1) set_job(c, 1);
+            else if (jm[c] == -1) set_job(c, 1);
         }
         if (!why) {
-            if (g.escaped) {
+            if (tg_esc) {
                 why = tg_fail(s, ev, g, s->view(row));
-            } else if (rt[c] == 0) {
+            } else if (tm[c] == 0) {
                 why = kIneligible;
-            } else if (rt[c] == -1) {
+            } else if (tm[c] == -1) {
                 why = tg_fail(s, ev, g, s->view(row));
                 set_tg(c, why ? 0 : 1);
             }
@@ -5642,10 +5656,13 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     rows.reserve(16 * (size_t)sp.n_rec);
     dks.reserve(16 * (size_t)sp.n_rec);
     uint32_t off = off0;
+    double t_walks = 0.0;
     for (uint32_t k = 0; k < sp.n_rec; k++) {
         const uint32_t ev = sp.compact ? sp.crecs[k].nodes_evaluated : sp.recs[k].nodes_evaluated;
         const size_t r0 = rows.size();
+        const double tw = prof ? now_us() : 0.0;
         metrics_walk(s, g, order, off, ev, acc[k], rows, &sp.memo_log);
+        if (prof) t_walks += now_us() - tw;
         sp.memo_off.push_back((uint32_t)sp.memo_log.size());
         for (size_t i = r0; i < rows.size(); i++) dks.push_back((uint16_t)placed_on[rows[i]]);
         rec_end[k] = (uint32_t)rows.size();
@@ -5658,11 +5675,13 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         if (row >= 0) placed_on[(uint32_t)row] = 0;
     }
     const double t1 = prof ? now_us() : 0.0;
-    // the outcomes land in pinned host buffers kept across runs
+    // the outcome codes and every record's ScoreMetaData (k_trace_top) land in
+    // pinned host buffers kept across runs; the score values stay on the device
     HIP_TRY(s, s->h_trace_codes.ensure(std::max<size_t>(rows.size(), 1) * sizeof(uint32_t)));
-    HIP_TRY(s, s->h_trace_sc.ensure(std::max<size_t>(rows.size(), 1) * 6 * sizeof(double)));
+    HIP_TRY(s, s->h_trace_top.ensure(std::max<size_t>(sp.n_rec, 1) * (5 * sizeof(pe_metric_score) + 1)));
     const uint32_t* codes = s->h_trace_codes.as<uint32_t>();
-    const double* sc = s->h_trace_sc.as<double>();
+    const pe_metric_score* top = s->h_trace_top.as<pe_metric_score>();
+    const uint8_t* n_top = reinterpret_cast<const uint8_t*>(top + 5 * (size_t)sp.n_rec);
     pe::Ask a = ask_for(s, g);
     if (!rows.empty()) {
         HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
@@ -5678,28 +5697,47 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         HIP_TRY_STATE(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
                                          s->d_trace_out.as<uint32_t>(), nullptr, s->log10, nullptr,
                                          s->d_trace_scores.as<double>(), s->stream, s->d_trace_dk.as<uint16_t>()));
+        const size_t top_bytes = 5 * sizeof(pe_metric_score) * (size_t)sp.n_rec;
+        HIP_TRY(s, upload_s(s, s->d_trace_rec_end, rec_end));
+        HIP_TRY(s, s->d_trace_top.ensure(top_bytes + sp.n_rec));
+        const uint32_t flags = (a.dev_tw != 0.0 ? 1u : 0u) | (a.anti_aff ? 2u : 0u) |
+                               (!g.affinities.empty() ? 4u : 0u) |
+                               (s->cfg.stack_kind == PE_STACK_GENERIC ? 8u : 0u);
+        HIP_TRY_STATE(s, pe_launch_trace_top(s->d_trace_out.as<uint32_t>(), s->d_trace_scores.as<double>(),
+                                             s->d_trace_rows.as<uint32_t>(), s->d_trace_rec_end.as<uint32_t>(),
+                                             sp.n_rec, flags, s->d_trace_top.as<pe_metric_score>(),
+                                             s->d_trace_top.as<uint8_t>() + top_bytes, s->stream));
         HIP_TRY(s, hipMemcpyAsync(s->h_trace_codes.p, s->d_trace_out.p, rows.size() * 4, hipMemcpyDeviceToHost,
                                   s->stream));
-        HIP_TRY(s, hipMemcpyAsync(s->h_trace_sc.p, s->d_trace_scores.p, rows.size() * 48, hipMemcpyDeviceToHost,
+        HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.p, s->d_trace_top.p, top_bytes + sp.n_rec, hipMemcpyDeviceToHost,
                                   s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
+    } else {
+        std::memset(s->h_trace_top.as<uint8_t>() + 5 * sizeof(pe_metric_score) * (size_t)sp.n_rec, 0, sp.n_rec);
     }
     const double t2 = prof ? now_us() : 0.0;
     spec_metrics_reset(sp);
     std::map<int, std::vector<uint32_t>> counts;
     size_t i = 0;
     for (uint32_t k = 0; k < sp.n_rec; k++) {
-        for (; i < rec_end[k]; i++) {
-            const int rc = metrics_outcome(s, g, a, rows[i], codes[i], &sc[i * 6], acc[k], counts);
+        for (; i < rec_end[k]; i++) {   // the options' ScoreMetaData came from k_trace_top
+            if ((codes[i] & 255u) == pe::kTrOption) continue;
+            const int rc = metrics_outcome(s, g, a, rows[i], codes[i], nullptr, acc[k], counts);
             if (rc) return rc;
         }
-        spec_metrics_push(sp, acc[k]);
+        acc[k].cf.append(PE_METRIC_CLASS_FILTERED, sp.mcounts);
+        acc[k].kf.append(PE_METRIC_CONSTRAINT_FILTERED, sp.mcounts);
+        acc[k].ce.append(PE_METRIC_CLASS_EXHAUSTED, sp.mcounts);
+        acc[k].de.append(PE_METRIC_DIMENSION_EXHAUSTED, sp.mcounts);
+        sp.mscores.insert(sp.mscores.end(), top + 5 * (size_t)k, top + 5 * (size_t)k + n_top[k]);
+        sp.mcounts_off.push_back((uint32_t)sp.mcounts.size());
+        sp.mscores_off.push_back((uint32_t)sp.mscores.size());
     }
     sp.metrics = true;
     if (prof)
-        std::fprintf(stderr, "spec_metrics: %u records, %zu traced rows: walk %.1f us, trace %.1f us, maps %.1f us "
-                             "(%zu counts, %zu scores)\n", sp.n_rec, rows.size(), t1 - t0, t2 - t1, now_us() - t2,
-                     sp.mcounts.size(), sp.mscores.size());
+        std::fprintf(stderr, "spec_metrics: %u records, %zu traced rows: walk %.1f us (in metrics_walk %.1f us), "
+                             "trace %.1f us, maps %.1f us (%zu counts, %zu scores)\n", sp.n_rec, rows.size(), t1 - t0,
+                     t_walks, t2 - t1, now_us() - t2, sp.mcounts.size(), sp.mscores.size());
     return PE_OK;
 }
 

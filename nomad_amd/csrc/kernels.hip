@@ -549,6 +549,99 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
     out[i] = code;
 }
 
+// ScoreMetaData of every record of a speculative run from k_trace's outcomes
+// (rows of record k: rec_end[k-1] .. rec_end[k]): one lane per record pushes
+// its options' NormScores in visit order into a 5-slot min-heap exactly as
+// kheap.ScoreHeap.Push does under container/heap (replace the minimum only
+// when strictly greater, heap.Fix, then up(len - 1); lib/kheap/score_heap.go),
+// pops them (GetItemsReverse) and writes the NodeScoreMeta items in their
+// binary form with the names metrics_outcome gives them
+// (structs.go:9976-10018). flags: 1 devices scored, 2 job anti-affinity
+// scored, 4 node affinities exist, 8 generic stack.
+__global__ void __launch_bounds__(64) k_trace_top(const uint32_t* codes, const double* sc, const uint32_t* rows,
+                                                  const uint32_t* rec_end, uint32_t n_rec, uint32_t flags,
+                                                  pe_metric_score* out, uint8_t* n_out) {
+    const uint32_t k = blockIdx.x * 64 + threadIdx.x;
+    if (k >= n_rec) return;
+    const uint32_t b = k ? rec_end[k - 1] : 0u, e = rec_end[k];
+    double hn[5];
+    uint32_t hi[5];
+    uint32_t len = 0;
+    auto less = [&](uint32_t x, uint32_t y) { return hn[x] < hn[y]; };
+    auto swap_ = [&](uint32_t x, uint32_t y) {
+        const double tn = hn[x]; hn[x] = hn[y]; hn[y] = tn;
+        const uint32_t ti = hi[x]; hi[x] = hi[y]; hi[y] = ti;
+    };
+    auto up = [&](uint32_t j) {
+        while (j > 0) {
+            const uint32_t i = (j - 1) / 2;
+            if (!less(j, i)) break;
+            swap_(i, j);
+            j = i;
+        }
+    };
+    auto down = [&](uint32_t i0, uint32_t n) {
+        uint32_t i = i0;
+        for (;;) {
+            const uint32_t j1 = 2 * i + 1;
+            if (j1 >= n) break;
+            uint32_t j = j1;
+            if (j1 + 1 < n && less(j1 + 1, j1)) j = j1 + 1;
+            if (!less(j, i)) break;
+            swap_(i, j);
+            i = j;
+        }
+        return i > i0;
+    };
+    for (uint32_t x = b; x < e; x++) {
+        if ((codes[x] & 255u) != kTrOption) continue;
+        const double norm = sc[(size_t)x * 6 + 5];
+        if (len < 5) {
+            hn[len] = norm;
+            hi[len] = x;
+            len++;
+        } else if (norm > hn[0]) {
+            hn[0] = norm;
+            hi[0] = x;
+            if (!down(0, len)) up(0);
+        }
+        up(len - 1);
+    }
+    // GetItemsReverse: heap.Pop until empty, the last popped first
+    uint32_t order[5];
+    const uint32_t total = len;
+    uint32_t at = total;
+    while (len > 0) {
+        const uint32_t n = len - 1;
+        swap_(0, n);
+        down(0, n);
+        order[--at] = hi[n];
+        len--;
+    }
+    n_out[k] = (uint8_t)total;
+    for (uint32_t q = 0; q < total; q++) {
+        const uint32_t x = order[q];
+        const double* o = sc + (size_t)x * 6;
+        pe_metric_score m;
+        for (int j = 0; j < PE_MAX_SCORES; j++) { m.scorer[j] = 0; m.score[j] = 0.0; }
+        uint32_t ns = 0;
+        m.scorer[ns] = PE_SCORER_BINPACK; m.score[ns++] = o[0];
+        if (flags & 1u) { m.scorer[ns] = PE_SCORER_DEVICES; m.score[ns++] = o[1]; }
+        if (flags & 8u) {   // the SystemStack ranks with BinPack alone (stack.go:277-281)
+            if (flags & 2u) { m.scorer[ns] = PE_SCORER_JOB_ANTI_AFFINITY; m.score[ns++] = o[2]; }
+            m.scorer[ns] = PE_SCORER_RESCHEDULE_PENALTY;
+            m.score[ns++] = (codes[x] & kTrPenalty) ? -1.0 : 0.0;
+            if (!(flags & 4u)) { m.scorer[ns] = PE_SCORER_NODE_AFFINITY; m.score[ns++] = 0.0; }
+            else if (o[3] != 0.0) { m.scorer[ns] = PE_SCORER_NODE_AFFINITY; m.score[ns++] = o[3]; }
+            if (o[4] != 0.0) { m.scorer[ns] = PE_SCORER_ALLOCATION_SPREAD; m.score[ns++] = o[4]; }
+        }
+        m.row = (int32_t)rows[x];
+        m.n_scores = ns;
+        m.norm = o[5];
+        out[(size_t)k * 5 + q] = m;
+    }
+}
+
 // evenSpreadScoreBoost (spread.go:178-228) / target boost (spread.go:143-164)
 // per value of each property set, from the eval's use counts: `counts` in the
 // pset_cnt_off layout (an LDS copy, or the loop's own counts), or null to read
@@ -3849,6 +3942,14 @@ hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec
         default: hipLaunchKernelGGL((pe::k_sweep<256, false>), dim3(blocks), dim3(256), 0, st, *a); break;
     }
     hipLaunchKernelGGL(pe::k_sweep_merge, dim3(1), dim3(512), 0, st, (const pe::SweepRec*)a->recs, blocks, merged);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const uint32_t* rows, const uint32_t* rec_end,
+                               uint32_t n_rec, uint32_t flags, pe_metric_score* out, uint8_t* n_out, hipStream_t st) {
+    if (!n_rec) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_trace_top, dim3((n_rec + 63) / 64), dim3(64), 0, st, codes, sc, rows, rec_end, n_rec,
+                       flags, out, n_out);
     return hipGetLastError();
 }
 
