@@ -39,6 +39,7 @@
 #include "constraint_eval.h"
 #include "engine_types.h"
 #include "gomath_dev.h"
+#include "gosort.h"
 
 // ---- RCCL, bound at run time ------------------------------------------------
 // The engine's collectives (pe_comm_init / pe_place_sharded, the one-handle
@@ -172,6 +173,7 @@ hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* s
                             hipStream_t st, double* parts = nullptr, uint8_t* nparts = nullptr);
 hipError_t pe_launch_resolve(const pe::EvictResolveArgs* r, hipStream_t st);
 hipError_t pe_launch_ploop(const pe::PLoopArgs* a, hipStream_t st);
+hipError_t pe_launch_md_gate(pe::MdNet* md, const uint32_t* coll_tg, uint32_t n, hipStream_t st);
 hipError_t pe_launch_static_gate(const uint8_t* blocked, const uint32_t* coll_tg, uint32_t* gate, uint32_t n,
                                  hipStream_t st);
 uint32_t pe_ploop_max_n(uint32_t words);
@@ -337,12 +339,21 @@ struct HostAlloc {
     bool terminal;
     int32_t priority = 0, max_parallel = 0;
     int64_t cpu = 0, mem = 0, disk = 0;
-    int32_t mbits = 0, dyn = 0;            // network use on the node's host device
+    int32_t mbits = 0, dyn = 0;            // network use: bandwidth on device net_dev, dynamic-range ports
     bool has_net = false;                  // Flattened.Networks non-empty (PreemptForNetwork candidates)
+    uint32_t net_dev = PE_NONE;            // Device of its networks (str id; PE_NONE: the node's first)
     uint32_t dev_begin = 0, dev_end = 0;   // into pe_stack::alloc_dev
     uint64_t cores[4] = {0, 0, 0, 0};      // Flattened.Cpu.ReservedCores (ids < 256)
     bool cores_beyond = false;             // a reserved core id >= 256
     uint32_t port_begin = 0, port_end = 0; // into pe_stack::alloc_ports: (HostIP str id, port) held
+};
+
+// One AvailNetworks entry of a node (NodeResources.Networks with a Device,
+// network.go:108-114): device, MBits, its IP field and the one address
+// yieldIP gives from its CIDR (PE_NONE: unknown).
+struct HostNet {
+    uint32_t dev, ipfield, yield;
+    int32_t mbits;
 };
 
 // One NodeNetworks address (NetworkIndex.SetNode, network.go:92-141).
@@ -493,6 +504,15 @@ struct TgPlan {
     // 309-342): the holders to preempt first (CSR-relative alloc indices, one
     // byte each, in ask order) and flags (kPort*)
     DevMem port_list, port_info, port_block;
+    // multi-device nodes (TgTables::md, build_md): the per-node records, the
+    // device network each plan placement of the group took on a node (index
+    // into the node's AvailNetworks, plan order), the last Preempt verdicts'
+    // choices, and the other groups' plan entries when the records were built
+    DevMem md_dev;
+    bool md_on = false;
+    std::unordered_map<uint32_t, std::vector<uint8_t>> md_hist;
+    std::unordered_map<uint32_t, uint8_t> md_vdev;
+    size_t md_other = 0;
     std::vector<std::unique_ptr<PsetDev>> psets;
     bool psets_built = false;
     bool elig_complete = false;   // every class's EvalEligibility entries are known (pe_get_eligibility)
@@ -560,6 +580,8 @@ struct pe_stack {
     std::vector<std::pair<uint32_t, uint32_t>> alloc_dev;   // (device group on the node, instances held)
     std::vector<std::pair<uint32_t, int32_t>> alloc_ports;  // (HostIP, port) held by allocs
     std::vector<std::vector<HostAddr>> node_addrs;          // per node, node order
+    std::vector<std::vector<HostNet>> node_dnets;           // nodes with several device networks: all of them
+    uint32_t n_multi_net = 0;                               // nodes with several device networks
     std::vector<std::vector<int>> node_rhp;                 // per node ReservedHostPorts, parsed
     // device groups per node and their attributes
     RowIndex dev_ix;
@@ -1666,6 +1688,7 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
     for (uint32_t j = 0; j < m; j++) {
         const uint32_t i = order[j], r = target[i];
         HostNode& h = s->nodes[r];
+        if (r < n_old && h.n_device_nets > 1) s->n_multi_net--;
         h = HostNode();
         h.id = nt->id[i]; h.name = nt->name[i]; h.dc = nt->datacenter[i];
         h.node_class = nt->node_class[i]; h.cclass = nt->computed_class[i];
@@ -1691,6 +1714,16 @@ int apply_nodes(pe_stack* s, const pe_node_table* nt, const std::vector<uint32_t
                 }
                 h.n_device_nets++;
             }
+        }
+        s->node_dnets.resize(n_new);
+        s->node_dnets[r].clear();
+        if (h.n_device_nets > 1) {   // AvailNetworks in node order (yieldIP walks them, network.go:294-315)
+            s->n_multi_net++;
+            for (uint32_t k = nt->net_off[i]; k < nt->net_off[i + 1]; k++)
+                if (!s->S(nt->net_device[k]).empty())
+                    s->node_dnets[r].push_back(HostNet{nt->net_device[k], nt->net_ip ? nt->net_ip[k] : PE_NONE,
+                                                       nt->net_cidr_ip ? nt->net_cidr_ip[k] : PE_NONE,
+                                                       nt->net_mbits[k]});
         }
         h.n_devices = (uint16_t)s->dev_ix.n(r);
         pe::NodeRec& rec = s->h_node_rec[r];
@@ -1875,6 +1908,8 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     s->max_dev_groups = 0;
     s->h_core_rsvable.clear(); s->h_core_avail.clear(); s->h_core_spc.clear(); s->h_core_bad.clear();
     s->n_core_bad = s->n_core_rows = 0;
+    s->node_dnets.clear();
+    s->n_multi_net = 0;
     std::vector<uint32_t> target(nt->n);
     for (uint32_t i = 0; i < nt->n; i++) target[i] = i;
     int rc = apply_nodes(s, nt, target, nt->n);
@@ -1886,6 +1921,13 @@ int build_state(pe_stack* s, const pe_node_table* nt, const pe_alloc_table* at) 
     rc = append_allocs(s, at, nullptr);
     if (rc) return rc;
     return build_alloc_state(s);
+}
+
+// Whether an alloc's bandwidth is on its node's first device network (the one
+// the NodeRec keeps, NetworkIndex.UsedBandwidth[device]).
+static inline bool on_first_dev(const pe_stack* s, const HostAlloc& a) {
+    const uint32_t f = s->nodes[a.row].first_dev;
+    return a.net_dev == PE_NONE || (f != PE_NONE && s->S(a.net_dev) == s->S(f));
 }
 
 // Allocations of a pe_alloc_table into the host mirror: appended, or, with
@@ -1911,9 +1953,11 @@ int append_allocs(pe_stack* s, const pe_alloc_table* at, const uint32_t* index) 
             s->alloc_ports.emplace_back(at->port_ip[k], at->port_value[k]);
         a.port_end = (uint32_t)s->alloc_ports.size();
         a.has_net = at->has_network ? at->has_network[i] != 0 : (a.mbits > 0 || a.dyn > 0 || a.port_end > a.port_begin);
-        if (at->net_device && at->net_device[i] != PE_NONE && a.has_net &&
-            (s->nodes[row].first_dev == PE_NONE || s->S(at->net_device[i]) != s->S(s->nodes[row].first_dev)))
-            s->net_other_dev++;   // its bandwidth is not on the device the engine keeps per node
+        if (at->net_device && at->net_device[i] != PE_NONE) {
+            a.net_dev = at->net_device[i];
+            if (a.has_net && (s->nodes[row].first_dev == PE_NONE || s->S(a.net_dev) != s->S(s->nodes[row].first_dev)))
+                s->net_other_dev++;   // its bandwidth is not on the device the NodeRec keeps: a multi-device node
+        }
         for (uint32_t k = at->core_off ? at->core_off[i] : 0; at->core_off && k < at->core_off[i + 1]; k++) {
             const uint16_t c = at->core_id[k];
             if (c >= 256) a.cores_beyond = true;
@@ -1965,7 +2009,9 @@ static uint8_t alloc_row(pe_stack* s, uint32_t r, std::vector<uint32_t>* slots_c
         rec.used_cpu += a.cpu;
         rec.used_mem += a.mem;
         rec.used_disk += a.disk;
-        rec.used_mbits += a.mbits;
+        // UsedBandwidth of the NodeRec's device (the node's first); allocs on
+        // another device make the node a multi-device one (build_md)
+        if (on_first_dev(s, a)) rec.used_mbits += a.mbits;
         rec.used_dyn += a.dyn;
         pe::PreemptAlloc& x = s->h_palloc[slot];
         x.dev_g = x.dev_c = 0;
@@ -2081,7 +2127,9 @@ int build_alloc_state(pe_stack* s) {
             x.priority = a.priority; x.max_parallel = a.max_parallel;
             x.job_key = s->job_keys.emplace(std::make_pair(a.job, a.ns), (uint32_t)s->job_keys.size()).first->second;
             x.jtg_key = jtg.emplace(std::make_tuple(a.job, a.ns, a.tg), (uint32_t)jtg.size()).first->second;
-            x.mbits = a.mbits;
+            // what a stop or eviction gives back to the NodeRec's device (the
+            // node's first); other devices' bandwidth is the host's (build_md)
+            x.mbits = on_first_dev(s, a) ? a.mbits : 0;
             x.dyn = a.dyn;
             x.state_index = i | (a.has_net ? pe::kAllocHasNet : 0u);
         }
@@ -2414,6 +2462,373 @@ static uint64_t port_blockers(pe_stack* s, const TgPlan& g, uint32_t row, bool* 
     return list;
 }
 
+// ---- multi-device nodes (TgTables::md) -------------------------------------
+// A task network ask on a snapshot where some node has several device
+// networks, or allocs on a device other than its first: those nodes' outcome
+// comes from the host (engine_types.h MdNet). The per-node dynamic-port count
+// stays node-wide, as on every other node.
+static inline bool tg_md(const pe_stack* s, const TgPlan& g) {
+    return g.ask.has_task_net > 0 && (s->n_multi_net > 0 || s->net_other_dev > 0);
+}
+
+// A node's AvailNetworks (the device networks) in node order.
+static void node_nets(const pe_stack* s, uint32_t r, std::vector<HostNet>& out) {
+    out.clear();
+    if (r < s->node_dnets.size() && !s->node_dnets[r].empty()) { out = s->node_dnets[r]; return; }
+    const HostNode& h = s->nodes[r];
+    if (h.n_device_nets) out.push_back(HostNet{h.first_dev, h.first_ipfield, h.first_yield, h.first_mbits});
+}
+
+static inline uint32_t canon(const pe_stack* s, uint32_t id) {
+    if (id == PE_NONE) return PE_NONE;
+    const uint32_t c = s->lookup(s->S(id));
+    return c == PE_NONE ? id : c;
+}
+
+// One node's NetworkIndex for the group's AssignNetwork (network.go:92-230,
+// 407-482): its AvailNetworks in node order, AvailBandwidth / UsedBandwidth
+// per device, the node-wide dynamic-range count, and the ports the plan's
+// placements hold; `removed` marks CSR-relative allocs PreemptForNetwork took
+// out of the proposed list.
+struct MdIndex {
+    pe_stack* s = nullptr;
+    const TgPlan* g = nullptr;
+    uint32_t row = 0, b = 0, e = 0;
+    std::vector<HostNet> nets;
+    std::vector<uint32_t> dev;                          // canonical device of each network
+    std::vector<std::pair<uint32_t, int32_t>> avail, used;
+    int32_t dyn = 0;
+    std::vector<std::pair<uint32_t, int32_t>> extra;    // (ip, port) held by plan placements
+    std::vector<uint8_t> removed;
+    uint32_t alias_ip = PE_NONE;                        // the group network's address (its static ports)
+
+    int32_t& used_of(uint32_t d) {
+        for (auto& u : used) if (u.first == d) return u.second;
+        used.emplace_back(d, 0);
+        return used.back().second;
+    }
+    int32_t avail_of(uint32_t d) const {
+        for (auto& u : avail) if (u.first == d) return u.second;
+        return 0;
+    }
+    uint32_t alloc_dev(const HostAlloc& a) const {
+        return a.net_dev == PE_NONE ? canon(s, s->nodes[row].first_dev) : canon(s, a.net_dev);
+    }
+    // UsedPorts[ip] (network.go:54-70, 92-141, 238-293): address reservations
+    // of that IP, ReservedHostPorts on the keys SetNode made (the networks' IP
+    // fields and the addresses), the proposed allocs' ports, the plan's.
+    bool port_used(uint32_t ip, int32_t v) const {
+        bool keyed = false;
+        for (const HostNet& nw : nets) keyed = keyed || nw.ipfield == ip;
+        if (row < s->node_addrs.size())
+            for (const HostAddr& a : s->node_addrs[row])
+                if (a.ip == ip) {
+                    keyed = true;
+                    if (std::binary_search(a.reserved.begin(), a.reserved.end(), v)) return true;
+                }
+        if (keyed && row < s->node_rhp.size() && std::binary_search(s->node_rhp[row].begin(), s->node_rhp[row].end(), v))
+            return true;
+        for (uint32_t k = b; k < e; k++) {
+            if (s->h_preempted[k] || removed[k - b]) continue;
+            const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+            for (uint32_t q = a.port_begin; q < a.port_end; q++)
+                if (s->alloc_ports[q].first == ip && s->alloc_ports[q].second == v) return true;
+        }
+        for (auto& x : extra) if (x.first == ip && x.second == v) return true;
+        return false;
+    }
+    // One AssignNetwork (yieldIP over the networks, one address each):
+    // bandwidth, the ask's ReservedPorts on the address, the dynamic ports.
+    // The refusal is the last network's (err is overwritten per address).
+    bool assign(int32_t idx_dyn, int* choice, uint32_t* code) const {
+        const pe::Ask& a = g->ask;
+        *code = pe::kTrNoNetworks;
+        for (size_t i = 0; i < nets.size(); i++) {
+            int32_t u = 0;
+            for (auto& x : used) if (x.first == dev[i]) u = x.second;
+            if (u + a.task_mbits > avail_of(dev[i])) { *code = pe::kTrBandwidth; continue; }
+            bool bad = false;
+            for (size_t q = 0; q < g->trports.size() && !bad; q++) {
+                const int32_t v = g->trports[q].first;
+                if (v < 0 || v >= 65536) {
+                    *code = pe::kTrTaskStatic | pe::kMdCoded | pe::kMdInvalidPort | ((uint32_t)q << 8);
+                    bad = true;
+                } else if (port_used(nets[i].yield, v)) {
+                    *code = pe::kTrTaskStatic | pe::kMdCoded | ((uint32_t)q << 8);
+                    bad = true;
+                }
+            }
+            if (bad) continue;
+            if (pe::kDynPortCapacity - idx_dyn < a.task_dyn) { *code = pe::kTrTaskDyn; continue; }
+            *choice = (int)i;
+            return true;
+        }
+        return false;
+    }
+    // What one placement of the group leaves in the index for the next
+    // (NetworkIndex.AddAllocs of the placed alloc, network.go:144-193): the
+    // group ports when the group network has ports, else the task network's
+    // bandwidth and ports on the device it took.
+    void apply(int choice) {
+        const pe::Ask& a = g->ask;
+        const bool shared = g->has_network && g->net_ports > 0;
+        if (a.commit_mbits) used_of(dev[(size_t)choice]) += a.commit_mbits;
+        dyn += a.commit_dyn;
+        if (!shared) {
+            for (auto& rp : g->trports) extra.emplace_back(nets[(size_t)choice].yield, rp.first);
+        } else {
+            for (auto& rp : g->rports) extra.emplace_back(alias_ip, rp.first);
+        }
+    }
+};
+
+// Whether `row` is a multi-device node: several device networks, or an alloc
+// with bandwidth held on a device other than the first.
+static bool md_node(const pe_stack* s, uint32_t row) {
+    if (s->nodes[row].n_device_nets > 1) return true;
+    if (!s->net_other_dev) return false;
+    const uint32_t first = canon(s, s->nodes[row].first_dev);
+    for (uint32_t k = s->h_node_alloc_off[row]; k < s->h_node_alloc_off[row + 1]; k++) {
+        if (s->h_preempted[k]) continue;
+        const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+        if (a.has_net && a.net_dev != PE_NONE && canon(s, a.net_dev) != first) return true;
+    }
+    return false;
+}
+
+// Go 1.16 sort.Slice over CSR-relative indices by a precomputed key.
+static void go_sort_by(std::vector<uint32_t>& v, const std::vector<double>& key) {
+    struct Less {
+        const double* k;
+        bool operator()(uint32_t x, uint32_t y) const { return k[x] < k[y]; }
+    };
+    if (!v.empty()) pe::go_sort(v.data(), (int)v.size(), Less{key.data()});
+}
+
+// PreemptForNetwork (preemption.go:270-455) for the task network's ask on a
+// multi-device node, then the retried AssignNetwork; the same steps as the
+// device's preempt_for_network (evict.inc), with the candidates grouped by
+// device. Fills the MdNet's ev / pre and *choice (kMdPre).
+static void md_preempt(const MdIndex& x0, const std::map<std::tuple<uint32_t, uint32_t, uint32_t>, int>& pcount,
+                       pe::MdNet* m, int* choice) {
+    pe_stack* s = x0.s;
+    const TgPlan& g = *x0.g;
+    const int32_t needed = g.ask.task_mbits;
+    std::vector<uint32_t> lst;
+    std::map<uint32_t, std::set<int32_t>> filtered;
+    std::set<uint32_t> devs;
+    for (uint32_t k = x0.b; k < x0.e; k++) {
+        if (s->h_preempted[k]) continue;
+        const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+        if ((a.job == s->job_id && a.ns == s->job_ns) || !a.has_net) continue;   // SetCandidates; Networks[0]
+        const uint32_t d = x0.alloc_dev(a);
+        if (s->job_priority - a.priority < 10) {
+            for (uint32_t q = a.port_begin; q < a.port_end; q++) filtered[d].insert(s->alloc_ports[q].second);
+            continue;
+        }
+        devs.insert(d);
+        lst.push_back(k - x0.b);
+    }
+    m->ev = pe::kMdSkip;
+    if (devs.empty()) return;
+    if (devs.size() > 1) { m->ev = pe::kMdUnsup; return; }   // deviceToAllocs in Go map order
+    const uint32_t D = *devs.begin();
+    const int32_t total = x0.avail_of(D);
+    if (total < needed) return;
+    int32_t used_d = 0;
+    for (auto& u : x0.used) if (u.first == D) used_d = u.second;
+    const int32_t free_bw = total - used_d;
+    auto al = [&](uint32_t rel) -> const HostAlloc& { return s->allocs[s->h_palloc_index[x0.b + rel]]; };
+    std::vector<uint32_t> pre;
+    int32_t pbw = 0;
+    if (!g.trports.empty()) {   // the reserved ports first (preemption.go:309-342)
+        std::map<int32_t, uint32_t> holder;
+        for (uint32_t rel : lst) {
+            const HostAlloc& a = al(rel);
+            for (uint32_t q = a.port_begin; q < a.port_end; q++) holder[s->alloc_ports[q].second] = rel;
+        }
+        for (auto& rp : g.trports) {
+            auto it = holder.find(rp.first);
+            if (it != holder.end()) {
+                if (std::find(pre.begin(), pre.end(), it->second) != pre.end()) { m->ev = pe::kMdUnsup; return; }
+                pbw += al(it->second).mbits;
+                pre.push_back(it->second);
+            } else if (filtered[D].count(rp.first)) {
+                return;   // a higher-priority alloc holds it: the next device, and there is none
+            }
+        }
+        size_t n = lst.size();   // RemoveAllocs: swap with the last
+        for (size_t i = 0; i < n; i++)
+            if (std::find(pre.begin(), pre.end(), lst[i]) != pre.end()) { lst[i] = lst[n - 1]; i--; n--; }
+        lst.resize(n);
+    }
+    std::vector<double> key(x0.e - x0.b, 0.0);
+    const double dn = (double)needed;
+    auto dist = [&](uint32_t rel) { return std::fabs((double)((int64_t)needed - al(rel).mbits) / dn); };
+    bool met = pbw + free_bw >= needed;
+    for (int64_t after = INT64_MIN; !met;) {   // filterAndGroupPreemptibleAllocs: priorities ascending
+        int64_t pr = INT64_MAX;
+        for (uint32_t rel : lst) if (al(rel).priority > after && al(rel).priority < pr) pr = al(rel).priority;
+        if (pr == INT64_MAX) break;
+        after = pr;
+        std::vector<uint32_t> v;
+        for (uint32_t rel : lst) if (al(rel).priority == pr) v.push_back(rel);
+        for (uint32_t rel : v) {   // scoreForNetwork (preemption.go:653-660)
+            const HostAlloc& a = al(rel);
+            auto it = pcount.find(std::make_tuple(a.job, a.ns, a.tg));
+            const int num = it == pcount.end() ? 0 : it->second;
+            double pen = 0.0;
+            if (a.max_parallel > 0 && num >= a.max_parallel) pen = (double)((num + 1) - a.max_parallel) * 50.0;
+            key[rel] = dist(rel) + pen;
+        }
+        go_sort_by(v, key);
+        for (uint32_t rel : v) {
+            pbw += al(rel).mbits;
+            pre.push_back(rel);
+            if (pbw + free_bw >= needed) { met = true; break; }
+        }
+    }
+    if (!met || pre.empty()) return;
+    for (uint32_t rel : pre) key[rel] = -dist(rel);   // filterSuperset: distance descending
+    go_sort_by(pre, key);
+    int32_t avail = free_bw;
+    std::vector<uint32_t> out;
+    for (uint32_t rel : pre) {
+        out.push_back(rel);
+        avail += al(rel).mbits;
+        if (avail != 0 && needed != 0 && avail >= needed) break;
+    }
+    if (out.size() > 8) { m->ev = pe::kMdUnsup; return; }
+    // the retried AssignNetwork on a fresh index of the remaining allocs: the
+    // group's port offer is not in it (rank.go:362-371)
+    MdIndex x1 = x0;
+    for (uint32_t rel : out) {
+        const HostAlloc& a = al(rel);
+        x1.removed[rel] = 1;
+        if (a.mbits) x1.used_of(x1.alloc_dev(a)) -= a.mbits;
+        x1.dyn -= a.dyn;
+    }
+    uint32_t code;
+    if (!x1.assign(x1.dyn, choice, &code)) return;
+    m->ev = pe::kMdPre;
+    m->n_pre = (uint8_t)out.size();
+    m->pre = ~0ull;
+    for (size_t i = 0; i < out.size(); i++) m->pre = (m->pre & ~(0xFFull << (8 * i))) | ((uint64_t)out[i] << (8 * i));
+}
+
+// The group's MdNet per node (TgTables::md) from the host mirror: the plan's
+// placements of the group replayed onto the devices they took (md_hist),
+// then first fit for the admitted count, the first refusal's reason, and the
+// Preempt Select's verdict.
+static int build_md(pe_stack* s, TgPlan& g) {
+    const uint32_t n = (uint32_t)s->nodes.size();
+    std::vector<pe::MdNet> md(n);
+    for (auto& m : md) { std::memset(&m, 0, sizeof(m)); m.lim = ~0u; }
+    std::unordered_map<uint32_t, uint32_t> own;                 // row -> the group's plan placements
+    std::unordered_map<uint32_t, int32_t> other_dyn;            // row -> other groups' placements' ports
+    g.md_other = 0;
+    for (auto& p : plan_of(s)) {
+        if (p.second >= n) continue;
+        if (p.first == g.name) { own[p.second]++; continue; }
+        g.md_other++;
+        for (auto& t : s->tgs)
+            if (t->name == p.first) { other_dyn[p.second] += t->ask.commit_dyn; break; }
+    }
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, int> pcount;   // Plan.NodePreemptions per job / group
+    for (size_t k = 0; k < s->h_preempted.size() && k < s->h_palloc_index.size(); k++)
+        if (s->h_preempted[k] == 1) {
+            const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+            pcount[std::make_tuple(a.job, a.ns, a.tg)]++;
+        }
+    std::unordered_map<uint32_t, uint8_t> vdev;
+    vdev.swap(g.md_vdev);
+    for (auto it = g.md_hist.begin(); it != g.md_hist.end();) {   // popped or reset plans
+        auto o = own.find(it->first);
+        const size_t keep = o == own.end() ? 0 : o->second;
+        if (it->second.size() > keep) it->second.resize(keep);
+        if (it->second.empty()) it = g.md_hist.erase(it);
+        else ++it;
+    }
+    const int32_t tg_part = g.ask.tg_dyn > 0 ? g.ask.tg_dyn + g.ask.static_dyn : 0;
+    const bool changes = g.ask.commit_mbits != 0 || g.ask.commit_dyn != 0 ||
+                         (g.has_network && g.net_ports > 0 ? !g.rports.empty() : !g.trports.empty());
+    for (uint32_t r = 0; r < n; r++) {
+        if (!md_node(s, r)) continue;
+        MdIndex x;
+        x.s = s;
+        x.g = &g;
+        x.row = r;
+        x.b = s->h_node_alloc_off[r];
+        x.e = s->h_node_alloc_off[r + 1];
+        x.removed.assign(x.e - x.b, 0);
+        node_nets(s, r, x.nets);
+        for (const HostNet& nw : x.nets) {
+            const uint32_t d = canon(s, nw.dev);
+            x.dev.push_back(d);
+            bool found = false;   // AvailBandwidth[device]: the last network naming it
+            for (auto& a : x.avail) if (a.first == d) { a.second = nw.mbits; found = true; }
+            if (!found) x.avail.emplace_back(d, nw.mbits);
+        }
+        if (r < s->node_addrs.size())
+            for (const HostAddr& a : s->node_addrs[r]) if (a.alias == g.net_host) { x.alias_ip = a.ip; break; }
+        x.dyn = s->h_base_rec[r].used_dyn;
+        for (uint32_t k = x.b; k < x.e; k++) {
+            const HostAlloc& a = s->allocs[s->h_palloc_index[k]];
+            if (s->h_preempted[k]) { x.dyn -= a.dyn; continue; }
+            if (a.mbits) x.used_of(x.alloc_dev(a)) += a.mbits;
+        }
+        {
+            auto od = other_dyn.find(r);
+            if (od != other_dyn.end()) x.dyn += od->second;
+        }
+        // the group's placements on the node, in plan order, on the devices they took
+        auto o = own.find(r);
+        const uint32_t placed = o == own.end() ? 0u : o->second;
+        std::vector<uint8_t>& hist = g.md_hist[r];
+        for (uint32_t j = 0; j < placed; j++) {
+            if (j == hist.size()) {
+                int ch = -1;
+                uint32_t code;
+                auto v = vdev.find(r);
+                if (v != vdev.end() && v->second < x.nets.size()) { ch = v->second; vdev.erase(v); }
+                else if (!x.assign(x.dyn + tg_part, &ch, &code)) ch = -1;
+                if (ch < 0) return s->fail(PE_EUNSUPPORTED, "a placement's network device on a multi-device node is unknown");
+                hist.push_back((uint8_t)ch);
+            }
+            x.apply(hist[j]);
+        }
+        if (hist.empty()) g.md_hist.erase(r);
+        pe::MdNet& m = md[r];
+        // the Preempt Select's verdict (built on this state; the Select rebuilds)
+        int ch0 = -1;
+        uint32_t code0 = 0;
+        if (x.assign(x.dyn + tg_part, &ch0, &code0)) {
+            m.ev = pe::kMdFit;
+            g.md_vdev[r] = (uint8_t)ch0;
+        } else {
+            int chp = -1;
+            md_preempt(x, pcount, &m, &chp);
+            if (m.ev == pe::kMdPre) g.md_vdev[r] = (uint8_t)chp;
+        }
+        // first fit for the plain Selects: placements admitted, the refusal after
+        uint32_t slots = 0, code = 0;
+        MdIndex y = x;
+        for (;;) {
+            int ch;
+            if (!y.assign(y.dyn + tg_part, &ch, &code)) break;
+            if (!changes || slots + 1 >= pe::kMdUnbounded - 1) { slots = pe::kMdUnbounded; break; }
+            slots++;
+            y.apply(ch);
+        }
+        m.lim = slots;
+        m.code = code;
+    }
+    HIP_TRY(s, upload_s(s, g.md_dev, md));
+    HIP_TRY_STATE(s, pe_launch_md_gate(g.md_dev.as<pe::MdNet>(), g.coll_tg.as<uint32_t>(), n, s->stream));
+    g.md_on = true;
+    return PE_OK;
+}
+
 static void port_step(pe_stack* s, const TgPlan& g, uint32_t row, bool own_placed, uint64_t* list, uint8_t* info,
                       uint64_t* blockers) {
     *list = ~0ull;
@@ -2458,7 +2873,7 @@ static void port_step(pe_stack* s, const TgPlan& g, uint32_t row, bool own_place
 
 // Static port gates follow ProposedAllocs: stops and evictions free ports.
 void invalidate_static(pe_stack* s) {
-    for (auto& g : s->tgs) if (has_static(*g)) g->tables_valid = false;
+    for (auto& g : s->tgs) if (has_static(*g) || g->md_on) g->tables_valid = false;
 }
 
 pe::NodeSoA soa_of(pe_stack* s) {
@@ -3368,6 +3783,11 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         HIP_TRY(s, upload_s(s, g.port_info, pinfo));
         HIP_TRY(s, upload_s(s, g.port_block, pblock));
     }
+    g.md_on = false;
+    if (tg_md(s, g)) {   // task network on multi-device nodes: the host's first fit and verdicts
+        const int rc = build_md(s, g);
+        if (rc) return rc;
+    }
     g.tables_valid = true;
     return PE_OK;
 }
@@ -3386,6 +3806,7 @@ pe::TgTables tables_of(TgPlan& g) {
     t.port_list = has_static(g) ? g.port_list.as<uint64_t>() : nullptr;
     t.port_info = has_static(g) ? g.port_info.as<uint8_t>() : nullptr;
     t.port_block = has_static(g) ? g.port_block.as<uint64_t>() : nullptr;
+    t.md = g.md_on ? g.md_dev.as<pe::MdNet>() : nullptr;
     t.coll_tg = g.coll_tg.as<uint32_t>();
     if (!g.dev_reqs.empty()) {
         t.dev_free = g.dev_free;
@@ -3436,12 +3857,15 @@ int prepare_tg(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& order, ui
     if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
     if (!s->cores_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, s->cores_unsupported);
     if (g.ask.cores > 0 && !s->cores_tg_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, s->cores_tg_unsupported);
-    if ((g.ask.tg_dyn > 0 || g.ask.has_task_net) && s->net_other_dev)
-        return s->fail(PE_EUNSUPPORTED, "network asks with allocs on a node's other network device");
     if (!g.psets_built) {
         int rc = build_psets(s, g);
         if (rc) return rc;
         if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
+    }
+    if (g.tables_valid && g.md_on) {   // another group's placements moved the nodes' dynamic ports
+        size_t other = 0;
+        for (auto& p : plan_of(s)) other += p.first != g.name;
+        if (other != g.md_other) g.tables_valid = false;
     }
     if (!g.tables_valid) {
         int rc = build_tables(s, g, order, start);
@@ -4903,18 +5327,25 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     }
     for (auto& g : s->tgs) {   // AssignNetwork's address: the network CIDR's one address on every node
         if (g->trports.empty()) continue;
-        for (auto& nd : s->nodes)
-            if (nd.n_device_nets > 0 && !nd.yield_known) {
-                g->unsupported = "task static ports on a network whose CIDR is not one known address";
-                break;
-            }
+        for (uint32_t r = 0; r < (uint32_t)s->nodes.size() && g->unsupported.empty(); r++) {
+            const HostNode& nd = s->nodes[r];
+            bool known = nd.n_device_nets == 0 || nd.yield_known;
+            if (nd.n_device_nets > 1)
+                for (const HostNet& nw : s->node_dnets[r]) known = known && nw.yield != PE_NONE;
+            if (!known) g->unsupported = "task static ports on a network whose CIDR is not one known address";
+        }
     }
     if (!generic) s->job_spreads.clear();
-    // task networks must resolve against a single host device network on every node
-    for (auto& g : s->tgs) {
-        if (g->ask.has_task_net)
-            for (auto& nd : s->nodes)
-                if (nd.n_device_nets > 1) { g->unsupported = "task network asks on multi-device nodes"; break; }
+    // multi-device nodes (build_md) model one task network of one group: the
+    // replay of the plan puts only that group's placements on the devices
+    if (s->n_multi_net > 0 || s->net_other_dev > 0) {
+        int with_net = 0;
+        for (auto& g : s->tgs) with_net += g->ask.has_task_net > 0;
+        for (auto& g : s->tgs) {
+            if (g->ask.has_task_net > 1) g->unsupported = "several task networks in a group, with multi-device nodes";
+            else if (g->ask.has_task_net && with_net > 1)
+                g->unsupported = "task networks in several groups of a job, with multi-device nodes";
+        }
     }
     s->have_job = true;
     for (auto& g : s->tgs) s->ex_tg_escaped[g->name] = g->escaped;   // EvalEligibility.SetJob (context.go:221-234)
@@ -5294,7 +5725,16 @@ static int metrics_outcome(pe_stack* s, TgPlan& g, const pe::Ask& a, uint32_t ro
         }
         case pe::kTrTaskStatic: {
             std::string why;
-            if (!task_port_reason(s, g, row, &why)) why = static_port_collision(s, g);
+            const uint32_t q = (code >> 8) & 255u;
+            if ((code & pe::kMdCoded) && q < g.trports.size()) {   // a multi-device node: the host's record
+                const auto& rp = g.trports[q];
+                why = (code & pe::kMdInvalidPort)
+                          ? "invalid port " + std::to_string(rp.first) + " (out of range)"
+                          : "reserved port collision " + (rp.second == PE_NONE ? std::string() : s->S(rp.second)) +
+                                "=" + std::to_string(rp.first);
+            } else if (!task_port_reason(s, g, row, &why)) {
+                why = static_port_collision(s, g);
+            }
             acc.exhaust(s, row, "network: " + why);
             break;
         }
@@ -6106,6 +6546,8 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
     if (s->cfg.stack_kind != PE_STACK_GENERIC) {
         // SystemStack.Select: single pass over the (single-node) list, no limit;
         // BinPack evicts when the scheduler configuration enables preemption
+        // (multi-device verdicts are built for the state the Select sees)
+        if (s->cfg.preempt && tgi < s->tgs.size() && tg_md(s, *s->tgs[tgi])) s->tgs[tgi]->tables_valid = false;
         int rc = prepare_tg(s, tgi, s->visit, 0);
         if (rc) return rc;
         uint32_t placed, no;
@@ -6148,6 +6590,8 @@ static int select_impl(pe_stack* s, uint32_t tgi, const pe_select_options* opts,
         if (out->row >= 0) return PE_OK;
         return select_impl(s, tgi, &o2, out, rec);
     }
+    if (opts && opts->preempt && tgi < s->tgs.size() && tg_md(s, *s->tgs[tgi]))
+        s->tgs[tgi]->tables_valid = false;   // the multi-device verdicts for the state this Select sees
     int rc = prepare_tg(s, tgi, s->visit, s->offset);
     if (rc) return rc;
     TgPlan& g = *s->tgs[tgi];
@@ -6637,6 +7081,8 @@ static int place_impl(pe_stack* s, uint32_t tgi, uint32_t count, pe_ranked_node*
     TgPlan& g = *s->tgs[tgi];
     if (tg_full_scan(s, g)) s->limit = 0x7FFFFFFF;
     const bool retry = retry_preempt && s->cfg.preempt;
+    if (retry && g.md_on)   // the Preempt verdicts hold for one state: per Select (pe_select)
+        return s->fail(PE_EUNSUPPORTED, "count loop with preemption on multi-device nodes");
     uint32_t p = 0, no = s->offset;
     if (g.psets_dynamic || retry || tg_full_scan(s, g)) {
         // no windowed chain launch first on these paths
@@ -6869,6 +7315,9 @@ static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* op
     // (spec_metrics) or the replay (spec_metrics_replay); static port asks
     // read host port mirrors that hold the run's end state: per Select
     if (s->metrics_on && has_static(*s->tgs[tgi])) return false;
+    // multi-device nodes: the Preempt verdicts are built per Select (and
+    // the maps' port texts from the host's records): no evicting or traced runs
+    if ((s->cfg.preempt || s->metrics_on) && tg_md(s, *s->tgs[tgi])) return false;
     return true;
 }
 
@@ -7999,6 +8448,9 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
         if (!rows.empty()) {
             if (!s->preempt_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, "preemption: " + s->preempt_unsupported);
             if (g.ask.cores > 0) return s->fail(PE_EUNSUPPORTED, "reserved cores with preemption");
+            if (g.md_on)
+                for (uint32_t r : rows)
+                    if (md_node(s, r)) return s->fail(PE_EUNSUPPORTED, "system preemption on multi-device nodes");
             // the max_parallel penalty reads the plan's preemption counts, which
             // earlier nodes grow: then the nodes go one at a time in list order
             bool serial = false;

@@ -71,6 +71,32 @@ struct NodeSoA {
     const int64_t* core_spc;        // [n] SharesPerCore = CpuShares / TotalCpuCores
 };
 
+// A node with several host network devices, or with allocs on a device other
+// than its first ("multi-device node"): NetworkIndex keeps bandwidth per device
+// (UsedBandwidth / AvailBandwidth, network.go:36-43, 108-114, 196-217) and
+// AssignNetwork walks the AvailNetworks in order (yieldIP, network.go:294-315,
+// 407-482), which the one device of the NodeRec does not hold. The host
+// (engine.cpp build_md) gives such a node's task-network outcome per task
+// group: placements of the group are admitted while coll_tg + dk < lim (first
+// fit over the devices, as consecutive AssignNetwork calls place them; lim is
+// ~0u on other nodes), `code` is the kTr* outcome of the first refused one
+// (kTrTaskStatic with the port's index in bits 8-15, kMdInvalidPort for a port
+// out of range, kMdCoded), and `ev` the Preempt Select's outcome at coll_tg ==
+// coll: the offer fits as is, PreemptForNetwork (preemption.go:270-455)
+// preempts the listed allocs (CSR-relative indices, one byte each) and the
+// retried offer fits, the node is skipped, or outside the modelled surface
+// (candidates on two devices: the reference ranges over a Go map).
+enum : uint8_t { kMdFit = 0, kMdPre = 1, kMdSkip = 2, kMdUnsup = 3 };
+constexpr uint32_t kMdCoded = 1u << 17;         // a kTrTaskStatic code whose port index is in bits 8-15
+constexpr uint32_t kMdInvalidPort = 1u << 16;   // ... and that port is out of range
+struct alignas(8) MdNet {
+    uint32_t lim, coll, code;
+    uint8_t ev, n_pre, _pad[2];
+    uint64_t pre;
+};
+static_assert(sizeof(MdNet) == 24, "MdNet is 24 bytes");
+constexpr uint32_t kMdUnbounded = 0xFFFFFFFEu;   // MdNet::lim as built: no placement limit
+
 // Per (job, task group) feasibility / affinity / spread tables for a Select.
 // kPort* flags of TgTables.port_info
 constexpr uint8_t kPortCount = 0x0F;     // holders listed
@@ -96,6 +122,7 @@ struct TgTables {
     const uint8_t* port_info;
     const uint64_t* port_block;  // [n] or null: allocs holding a needed port on the ask's address (up to 8
                                  // CSR-relative indices, one byte each, 0xFF ends the list)
+    const MdNet* md;             // [n] or null: the task network on multi-device nodes (host-built)
     int n_psets;                                 // spread property sets first, then distinct_property sets
     int n_spread;                                // psets [0, n_spread) score, [n_spread, n_psets) filter
     uint32_t pset_allowed[kMaxPsets];            // distinct_property: allowed use count per value

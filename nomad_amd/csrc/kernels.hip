@@ -26,6 +26,7 @@
 #include <cstring>
 #include "engine_types.h"
 #include "gomath_dev.h"
+#include "gosort.h"
 
 namespace pe {
 
@@ -295,12 +296,17 @@ __device__ __forceinline__ int status_loaded(const NodeSoA& s, const TgTables& t
             dyn += a.tg_dyn + a.static_dyn;
         }
         if (a.has_task_net) {
-            const int32_t avail = r.avail_mbits;
-            const int32_t mb = r.used_mbits + (int32_t)dk * a.commit_mbits;
-            if (avail < 0 || mb + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) return kExhausted;
-            if (t.task_gate) {   // AssignNetwork's static ports (network.go:419-431), host-built gate
-                const uint32_t gt = t.task_gate[row];
-                if (gt == 0u || in.coll_tg + dk + 1u != gt) return kExhausted;
+            const uint32_t md_lim = t.md ? t.md[row].lim : ~0u;
+            if (md_lim != ~0u) {   // a multi-device node: the host's first fit over its devices
+                if (in.coll_tg + dk >= md_lim) return kExhausted;
+            } else {
+                const int32_t avail = r.avail_mbits;
+                const int32_t mb = r.used_mbits + (int32_t)dk * a.commit_mbits;
+                if (avail < 0 || mb + a.task_mbits > avail || kDynPortCapacity - dyn < a.task_dyn) return kExhausted;
+                if (t.task_gate) {   // AssignNetwork's static ports (network.go:419-431), host-built gate
+                    const uint32_t gt = t.task_gate[row];
+                    if (gt == 0u || in.coll_tg + dk + 1u != gt) return kExhausted;
+                }
             }
         }
     }
@@ -480,7 +486,10 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
             else if (kDynPortCapacity - dyn - a.static_dyn < 1) code = kTrDynPorts;
             dyn += a.tg_dyn + a.static_dyn;
         }
-        if (code == kTrOption && a.has_task_net) {
+        const uint32_t md_lim = (code == kTrOption && a.has_task_net && t.md) ? t.md[row].lim : ~0u;
+        if (md_lim != ~0u) {   // a multi-device node: the host's outcome of the first refused placement
+            if (in.coll_tg + dk >= md_lim) code = t.md[row].code;
+        } else if (code == kTrOption && a.has_task_net) {
             if (r.avail_mbits < 0) code = kTrNoNetworks;
             else if (r.used_mbits + a.task_mbits > r.avail_mbits) code = kTrBandwidth;
             else if (t.task_gate && (t.task_gate[row] == 0u || in.coll_tg + dk + 1u != t.task_gate[row])) code = kTrTaskStatic;
@@ -3544,6 +3553,20 @@ __global__ void __launch_bounds__(256) k_static_gate(const uint8_t* blocked, con
     if (i < n) gate[i] = blocked[i] ? 0u : coll_tg[i] + 1u;
 }
 
+// Multi-device gates (TgTables::md): the host wrote the admitted placement
+// count in `lim` (kMdUnbounded: no limit); the rows get the group's collision
+// count at build time added (saturating below ~0u, which marks other rows).
+__global__ void __launch_bounds__(256) k_md_gate(MdNet* md, const uint32_t* coll_tg, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    MdNet& m = md[i];
+    if (m.lim == ~0u) return;
+    const uint32_t c = coll_tg[i];
+    m.coll = c;
+    const uint64_t lim = (uint64_t)c + m.lim;
+    m.lim = (m.lim == kMdUnbounded || lim >= (uint64_t)kMdUnbounded) ? kMdUnbounded : (uint32_t)lim;
+}
+
 #include "evict.inc"
 
 }  // namespace pe
@@ -4159,5 +4182,11 @@ hipError_t pe_launch_static_gate(const uint8_t* blocked, const uint32_t* coll_tg
                                  hipStream_t st) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(pe::k_static_gate, dim3((n + 255) / 256), dim3(256), 0, st, blocked, coll_tg, gate, n);
+    return hipGetLastError();
+}
+
+hipError_t pe_launch_md_gate(pe::MdNet* md, const uint32_t* coll_tg, uint32_t n, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_md_gate, dim3((n + 255) / 256), dim3(256), 0, st, md, coll_tg, n);
     return hipGetLastError();
 }

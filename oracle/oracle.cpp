@@ -94,8 +94,9 @@ struct OAlloc {
     int state_index = -1;                    // row of the state alloc table (-1: plan alloc)
     std::vector<uint16_t> cores;             // Flattened.Cpu.ReservedCores (a set)
     std::vector<std::pair<std::string, int>> ports;   // (HostIP, port) held (NetworkIndex.AddAllocs)
-    bool has_net = false;                    // Flattened.Networks non-empty (on the node's first device)
-    bool other_dev = false;                  // its networks are on another device than the node's first
+    bool has_net = false;                    // Flattened.Networks non-empty
+    std::string dev;                         // Device of its networks (Networks[0].Device): the key of its
+                                             // UsedBandwidth and of its PreemptForNetwork group
 };
 
 struct OConstraint { std::string l, r, op; };
@@ -918,6 +919,7 @@ struct RankedNode {
     std::vector<uint16_t> cores;             // Cpu.ReservedCores of the tasks, in task order
     int64_t cpu = 0;                         // the alloc's CpuShares (SharesPerCore x cores for core tasks)
     std::vector<std::pair<std::string, int>> ports;   // static ports of the offer (HostIP, value)
+    std::string net_dev;                     // Device of the task network's offer (AssignNetwork)
 };
 
 struct RankIterator { virtual ~RankIterator() {} virtual RankedNode* Next() = 0; virtual void Reset() = 0; };
@@ -1223,25 +1225,38 @@ struct Preemptor {
     }
 
     // PreemptForNetwork (preemption.go:270-455) for an ask of `needed` MBits and
-    // the ReservedPorts values `ports`, every candidate's network on the node's
-    // device (total: AvailBandwidth, used: the NetworkIndex's UsedBandwidth).
+    // the ReservedPorts values `ports`: candidates grouped by their network's
+    // device (deviceToAllocs), filteredReservedPorts per device, the device's
+    // AvailBandwidth and the NetworkIndex's UsedBandwidth of it. The reference
+    // ranges over the deviceToAllocs map: with candidates on two devices its
+    // answer depends on Go's map order, which is not modelled (Unsupported).
     // An alloc's ReservedPorts are the values of the ports it holds.
-    std::vector<const OAlloc*> ForNetwork(int32_t needed, int32_t total, int32_t used,
+    std::vector<const OAlloc*> ForNetwork(int32_t needed, const std::map<std::string, int32_t>& avail_bw,
+                                          const std::map<std::string, int32_t>& used_bw,
                                           const std::vector<int>& ports = {}) {
         if (current.empty()) return {};
-        std::vector<const OAlloc*> dev;
-        std::set<int> filtered;   // filteredReservedPorts: ports of allocs too close in priority
+        std::map<std::string, std::vector<const OAlloc*>> by_dev;
+        std::map<std::string, std::set<int>> filtered_by_dev;   // ports of allocs too close in priority
         for (const OAlloc* a : current) {
             if (!a->has_net) continue;
             if (job_priority - a->priority < 10) {
-                for (auto& pp : a->ports) filtered.insert(pp.second);
+                for (auto& pp : a->ports) filtered_by_dev[a->dev].insert(pp.second);
                 continue;
             }
-            dev.push_back(a);
+            by_dev[a->dev].push_back(a);
         }
-        if (dev.empty()) return {};
+        if (by_dev.empty()) return {};
+        if (by_dev.size() > 1) throw Unsupported("network preemption candidates on several network devices (map order)");
+        const std::string& device = by_dev.begin()->first;
+        std::vector<const OAlloc*> dev = by_dev.begin()->second;
+        const std::set<int>& filtered = filtered_by_dev[device];
+        auto at = [](const std::map<std::string, int32_t>& m, const std::string& k) {
+            auto it = m.find(k);
+            return it == m.end() ? 0 : it->second;
+        };
+        const int32_t total = at(avail_bw, device);
         if (total < needed) return {};
-        const int32_t free_bw = total - used;
+        const int32_t free_bw = total - at(used_bw, device);
         int32_t pbw = 0;
         std::vector<const OAlloc*> best;
         if (!ports.empty()) {
@@ -1378,17 +1393,24 @@ struct BinPackIterator : RankIterator {
     const OTaskGroup* tg = nullptr;
     bool spread_algo = false, oversub = false;
 
-    // NetworkIndex SetNode + AddAllocs: dynamic-range ports in use and the
-    // bandwidth used on the device (network.go:92-200)
-    static void index_usage(const ONode& n, const std::vector<const OAlloc*>& proposed, int32_t* dyn, int32_t* mbits) {
+    // NetworkIndex SetNode + AddAllocs: dynamic-range ports in use (counted
+    // per node) and UsedBandwidth per device (network.go:92-230)
+    static void index_usage(const ONode& n, const std::vector<const OAlloc*>& proposed, int32_t* dyn,
+                            std::map<std::string, int32_t>* used_bw) {
         *dyn = n.reserved_dyn;
-        *mbits = 0;
-        for (const OAlloc* a : proposed) { if (a->terminal) continue; *dyn += a->dyn_ports; *mbits += a->mbits; }
+        used_bw->clear();
+        for (const OAlloc* a : proposed) {
+            if (a->terminal) continue;
+            *dyn += a->dyn_ports;
+            if (a->mbits) (*used_bw)[a->dev] += a->mbits;
+        }
     }
-    // AvailBandwidth of the node's (first) host network device
-    static int32_t device_bandwidth(const ONode& n) {
-        for (auto& nw : n.nets) if (!nw.device.empty()) return nw.mbits;
-        return 0;
+    // AvailBandwidth: per device, the MBits of the last AvailNetworks entry
+    // naming it (SetNode, network.go:108-114)
+    static std::map<std::string, int32_t> avail_bandwidth(const ONode& n) {
+        std::map<std::string, int32_t> m;
+        for (auto& nw : n.nets) if (!nw.device.empty()) m[nw.device] = nw.mbits;
+        return m;
     }
 
     static double score_fit(bool spread, const ONode& n, int64_t ucpu, int64_t umem) {
@@ -1408,14 +1430,11 @@ struct BinPackIterator : RankIterator {
             if (!option) return nullptr;
             const ONode& n = *option->node;
             auto proposed = ctx->ProposedAllocs(n.row);
-            bool net_ask = tg->has_network;
-            for (auto& t : tg->tasks) net_ask = net_ask || t.has_network;
-            if (net_ask)   // UsedBandwidth is per device (network.go:196-230); kept for the first only
-                for (const OAlloc* a : proposed)
-                    if (a->other_dev && !a->terminal) throw Unsupported("allocs on another network device");
             // NetworkIndex: SetNode + AddAllocs
-            int32_t used_dyn = 0, used_mbits = 0;
-            index_usage(n, proposed, &used_dyn, &used_mbits);
+            int32_t used_dyn = 0;
+            std::map<std::string, int32_t> used_bw;
+            const std::map<std::string, int32_t> avail_bw = avail_bandwidth(n);
+            index_usage(n, proposed, &used_dyn, &used_bw);
             DevAlloc dev(&n);
             dev.AddAllocs(proposed);
             double total_dev_w = 0.0, sum_dev_match = 0.0;
@@ -1425,6 +1444,7 @@ struct BinPackIterator : RankIterator {
             pre.SetNode(n);
             pre.SetPreemptions(ctx->plan);
             option->ports.clear();
+            option->net_dev.clear();
             // UsedPorts[ip] of the NetworkIndex (network.go:92-293): SetNode keys the
             // AvailNetworks' IP fields and the addresses (their ReservedPorts), then
             // marks ReservedHostPorts on every key; AddAllocs marks the proposed
@@ -1485,11 +1505,11 @@ struct BinPackIterator : RankIterator {
                     // PreemptForNetwork on the group's ask (rank.go:273-300); nil skips
                     // the node without an ExhaustedNode, and so does a failed retry
                     pre.SetCandidates(proposed);
-                    auto np = pre.ForNetwork(0, device_bandwidth(n), used_mbits, rport_values);
+                    auto np = pre.ForNetwork(0, avail_bw, used_bw, rport_values);
                     if (np.empty()) continue;
                     to_preempt.insert(to_preempt.end(), np.begin(), np.end());
                     proposed = remove_allocs(proposed, np);
-                    index_usage(n, proposed, &used_dyn, &used_mbits);   // a new NetworkIndex
+                    index_usage(n, proposed, &used_dyn, &used_bw);   // a new NetworkIndex
                     if (!assign_ports(proposed).empty()) continue;
                 }
                 used_dyn += static_dyn + tg->net_dyn;   // AddReservedPorts(offer)
@@ -1507,11 +1527,14 @@ struct BinPackIterator : RankIterator {
                     std::vector<int> rport_values;
                     for (auto& rp : t.rports) rport_values.push_back(rp.first);
                     const std::string* yield_ip = nullptr;
+                    const std::string* yield_dev = nullptr;
                     auto assign_network = [&](const std::vector<const OAlloc*>& prop, std::string* err) {
                         *err = "no networks available";
-                        for (auto& nw : n.nets) {
+                        for (auto& nw : n.nets) {   // yieldIP: the AvailNetworks in node order
                             if (nw.device.empty()) continue;
-                            if (used_mbits + t.net_mbits > nw.mbits) { *err = "bandwidth exceeded"; continue; }
+                            auto ub = used_bw.find(nw.device);
+                            const int32_t used = ub == used_bw.end() ? 0 : ub->second;
+                            if (used + t.net_mbits > avail_bw.at(nw.device)) { *err = "bandwidth exceeded"; continue; }
                             if (!t.rports.empty()) {
                                 if (nw.cidr_ip.empty()) throw Unsupported("task static ports on a network that is not one address");
                                 bool bad = false;
@@ -1531,6 +1554,7 @@ struct BinPackIterator : RankIterator {
                             }
                             if (kDynPortCapacity - used_dyn < t.net_dyn) { *err = "dynamic port selection failed"; continue; }
                             yield_ip = &nw.cidr_ip;
+                            yield_dev = &nw.device;
                             return true;
                         }
                         return false;
@@ -1540,21 +1564,20 @@ struct BinPackIterator : RankIterator {
                     if (!ok && evict) {
                         // PreemptForNetwork on the task's ask (rank.go:343-379); the
                         // rebuilt index holds the remaining proposed allocs only
-                        int ndev = 0;
-                        for (auto& nw : n.nets) ndev += nw.device.empty() ? 0 : 1;
-                        if (ndev > 1) throw Unsupported("network preemption on a node with several network devices");
                         pre.SetCandidates(proposed);
-                        auto np = pre.ForNetwork(t.net_mbits, device_bandwidth(n), used_mbits, rport_values);
+                        auto np = pre.ForNetwork(t.net_mbits, avail_bw, used_bw, rport_values);
                         if (np.empty()) { skip = true; break; }
                         to_preempt.insert(to_preempt.end(), np.begin(), np.end());
                         proposed = remove_allocs(proposed, np);
-                        index_usage(n, proposed, &used_dyn, &used_mbits);
+                        index_usage(n, proposed, &used_dyn, &used_bw);
                         idx_offers.clear();   // the rebuilt index holds no earlier offers
                         std::string err2;
                         if (!assign_network(proposed, &err2)) { skip = true; break; }
                     }
                     if (!ok && !evict) { ctx->metrics.ExhaustedNode(&n, "network: " + err); skip = true; break; }
-                    used_mbits += t.net_mbits; used_dyn += t.net_dyn;   // AddReserved(offer)
+                    used_bw[*yield_dev] += t.net_mbits;   // AddReserved(offer)
+                    used_dyn += t.net_dyn;
+                    option->net_dev = *yield_dev;
                     for (auto& rp : t.rports) {
                         option->ports.push_back({*yield_ip, rp.first});
                         idx_offers.push_back({*yield_ip, rp.first});
@@ -1960,6 +1983,7 @@ struct oracle_stack {
     std::vector<uint16_t> offer_cores;                 // and its reserved cores / CpuShares / static ports
     int64_t offer_cpu = 0;
     std::vector<std::pair<std::string, int>> offer_ports;
+    std::string offer_net_dev;
 
     explicit oracle_stack(const pe_config& c) : cfg(c) {
         ctx.state = &state;
@@ -2084,11 +2108,11 @@ int oracle_set_state(oracle_stack* s, const pe_strtab* strs, const pe_node_table
         a.state_index = (int)i;
         const bool held_ports = at->port_off && at->port_off[i + 1] > at->port_off[i];
         a.has_net = at->has_network ? at->has_network[i] != 0 : (a.mbits > 0 || a.dyn_ports > 0 || held_ports);
-        if (at->net_device && at->net_device[i] != PE_NONE && a.has_net) {
-            std::string first;
+        if (at->net_device && at->net_device[i] != PE_NONE) {
+            a.dev = S(st, at->net_device[i]);
+        } else {   // the node's first host network device (pe_alloc_table.net_device)
             const ONode& nd = st.nodes[(size_t)a.node_row];
-            for (auto& nw : nd.nets) if (!nw.device.empty()) { first = nw.device; break; }
-            a.other_dev = S(st, at->net_device[i]) != first;
+            for (auto& nw : nd.nets) if (!nw.device.empty()) { a.dev = nw.device; break; }
         }
         a.max_parallel = at->max_parallel ? at->max_parallel[i] : 0;
         if (at->dev_off)
@@ -2353,7 +2377,10 @@ static int select_rec(oracle_stack* s, uint32_t tgi, const pe_select_options* op
         RankedNode* o = s->cfg.stack_kind == PE_STACK_GENERIC ? generic_select(s, tgi, opts) : system_select(s, tgi);
         fill_out(out, o, s);
         s->offer_row = o ? o->node->row : -1;
-        if (o) { s->offers = o->offers; s->offer_cores = o->cores; s->offer_cpu = o->cpu; s->offer_ports = o->ports; }
+        if (o) {
+            s->offers = o->offers; s->offer_cores = o->cores; s->offer_cpu = o->cpu; s->offer_ports = o->ports;
+            s->offer_net_dev = o->net_dev;
+        }
     } catch (const Unsupported& e) {
         s->err = std::string("unsupported: ") + e.what();
         return PE_EUNSUPPORTED;
@@ -2379,8 +2406,18 @@ int oracle_commit(oracle_stack* s, uint32_t tgi, int32_t row) {
         a.cores = s->offer_cores;
         a.cpu = s->offer_cpu;
         a.ports = s->offer_ports;
+        a.dev = s->offer_net_dev;
     } else {   // commit without a Select of this node: assign on the proposed state
         const ONode& n = s->state.nodes[(size_t)row];
+        {   // AssignNetwork's device: the first AvailNetworks entry with the bandwidth
+            std::map<std::string, int32_t> used, avail;
+            for (auto& nw : n.nets) if (!nw.device.empty()) avail[nw.device] = nw.mbits;
+            for (const OAlloc* p : s->ctx.ProposedAllocs(row)) if (!p->terminal && p->mbits) used[p->dev] += p->mbits;
+            int32_t ask_mbits = 0;
+            for (auto& t : tg.tasks) if (t.has_network) ask_mbits += t.net_mbits;
+            for (auto& nw : n.nets)
+                if (!nw.device.empty() && used[nw.device] + ask_mbits <= avail[nw.device]) { a.dev = nw.device; break; }
+        }
         DevAlloc dev(&n);
         dev.AddAllocs(s->ctx.ProposedAllocs(row));
         for (auto& t : tg.tasks)

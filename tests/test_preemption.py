@@ -12,8 +12,8 @@ static port ("No preemption because existing allocs are not low priority",
 static port ...", "one alloc meets static port need ...", "alloc that meets
 static port need ...") ask static ports in a task network (AssignNetwork's
 ReservedPorts and PreemptForNetwork's reserved-port step); "preempt only from
-device that has allocation with unused reserved port" needs a second network
-device and is refused (PE_EUNSUPPORTED, the reference chain answers).
+device that has allocation with unused reserved port" runs on a node with two
+network devices (test_preempt_only_from_device_with_unused_reserved_port).
 """
 import math
 
@@ -448,27 +448,94 @@ def test_preempt_skips_nodes_without_dynamic_ports(stack_cls):
     assert r.preempted == [1]
 
 
+def two_nic_node():
+    """preemption_test.go:408's node: preemption_node() with a second host
+    network device, eth0 192.168.0.100/32 and eth1 192.168.1.100/32 at 1000
+    MBits each."""
+    nd = preemption_node()
+    nd.networks = [NetworkResource(mode="host", device="eth0", cidr="192.168.0.100/32", mbits=1000),
+                   NetworkResource(mode="host", device="eth1", cidr="192.168.1.100/32", mbits=1000)]
+    nd.compute_class()
+    return nd
+
+
+def on(dev, a):
+    a.net_device = dev
+    return a
+
+
 @pytest.mark.parametrize("stack_cls", STACKS)
-def test_alloc_on_other_network_device_is_refused(stack_cls):
-    """NetworkIndex keeps bandwidth per device (UsedBandwidth[device],
-    network.go:196-230) and PreemptForNetwork groups candidates by their
-    network's device (preemption.go:302-331). Both sides keep it for the node's
-    first device only, so a network ask on a node holding an alloc on another
-    device is refused (PE_EUNSUPPORTED / oracle Unsupported) rather than
-    answered from the wrong device's figures; with the alloc on eth0 the same
-    case places and preempts."""
-    node = preemption_node()
-    job = ask_job(1100, 1000, mbits=840)
-    for dev, refused in (("eth1", True), ("eth0", False)):
-        allocs = [alloc(0, LOW, 2800, 2256), alloc(1, LOW, 200, 256, mbits=800)]
-        allocs[1].net_device = dev
+def test_preempt_only_from_device_with_unused_reserved_port(stack_cls):
+    """"preempt only from device that has allocation with unused reserved port"
+    (preemption_test.go:408-496): bandwidth is kept per device
+    (NetworkIndex.UsedBandwidth[device], network.go:196-230), AssignNetwork
+    walks the node's two devices (yieldIP, network.go:294-315, 407-482) and
+    finds neither with 700 MBits free; PreemptForNetwork groups the candidates
+    by device (preemption.go:292-331): only eth0 holds a low-priority one, the
+    high-priority holder of port 88 sits on eth1, so the low-priority eth0
+    alloc is preempted and the retried offer lands on eth0."""
+    node = two_nic_node()
+    allocs = [on("eth0", alloc(0, HIGH, 1200, 2256, mbits=150)),
+              on("eth1", alloc(1, HIGH, 200, 256, mbits=600, ports=[("192.168.0.200", 88)])),
+              on("eth0", alloc(2, LOW, 200, 256, mbits=600))]
+    job = ask_job(600, 1000, mbits=700, ports=[("db", 88)])
+    st = stack_cls()
+    st.SetState([node], allocs)
+    st.SetJob(job)
+    st.SetNodes([node])
+    plain = st.SelectRaw(0)
+    assert plain.row == -1 and plain.nodes_exhausted == 1
+    r = st.SelectRaw(0, SelectOptions(preempt=True))
+    assert r.row == 0 and set(r.preempted) == {2}
+    want = 1.0 / (1.0 + math.exp(0.0048 * (net_priority([LOW]) - 2048.0)))
+    assert abs(r.scores[-1] - want) <= 1e-12 * want
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_candidates_on_two_devices_are_refused(stack_cls):
+    """PreemptForNetwork ranges over its deviceToAllocs map
+    (preemption.go:335-408): with preemptible candidates on both devices the
+    reference's answer depends on Go's map order, so both sides refuse
+    (PE_EUNSUPPORTED / oracle Unsupported) and the caller's chain answers; with
+    the eth1 candidate raised to a close priority only eth0 has candidates and
+    the answer is the reference's."""
+    node = two_nic_node()
+    job = ask_job(600, 1000, mbits=700)
+    for prio1, refused in ((LOW, True), (HIGH, False)):
+        allocs = [on("eth0", alloc(0, HIGH, 1200, 2256, mbits=150)),
+                  on("eth1", alloc(1, prio1, 200, 256, mbits=600)),
+                  on("eth0", alloc(2, LOW, 200, 256, mbits=600))]
         st = stack_cls()
         st.SetState([node], allocs)
         st.SetJob(job)
         st.SetNodes([node])
+        assert st.SelectRaw(0).row == -1
         if refused:
             with pytest.raises(Exception, match="(?i)unsupported|network device"):
                 st.SelectRaw(0, SelectOptions(preempt=True))
         else:
+            r = st.SelectRaw(0, SelectOptions(preempt=True))
+            assert r.row == 0 and r.preempted == [2]
+
+
+@pytest.mark.parametrize("stack_cls", STACKS)
+def test_alloc_on_a_device_the_node_lacks(stack_cls):
+    """An alloc whose network names a device the node has no network for
+    holds bandwidth on that device only (UsedBandwidth[device]): the node's
+    eth0 keeps its 1000 MBits and the 840-MBit ask places without eviction.
+    With the alloc on eth0 the network is short and PreemptForNetwork picks it."""
+    node = preemption_node()
+    job = ask_job(1100, 1000, mbits=840)
+    for dev in ("eth1", "eth0"):
+        allocs = [alloc(0, LOW, 2000, 2256), on(dev, alloc(1, LOW, 200, 256, mbits=800))]
+        st = stack_cls()
+        st.SetState([node], allocs)
+        st.SetJob(job)
+        st.SetNodes([node])
+        plain = st.SelectRaw(0)
+        if dev == "eth1":
+            assert plain.row == 0 and plain.preempted == []
+        else:
+            assert plain.row == -1
             r = st.SelectRaw(0, SelectOptions(preempt=True))
             assert r.row == 0 and r.preempted == [1]
