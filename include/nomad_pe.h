@@ -157,9 +157,9 @@ typedef struct pe_alloc_table {
     const uint8_t* has_network;
     /* the Device of the alloc's networks (NetworkResource.Device; string id),
        or PE_NONE / NULL: the node's first host network device. Bandwidth is
-       kept per node on that device (NetworkIndex.UsedBandwidth[device],
-       network.go:196-230): a network ask on a node holding an alloc on another
-       device is refused (PE_EUNSUPPORTED) */
+       kept per device (NetworkIndex.UsedBandwidth[device], network.go:196-230);
+       a Select with Preempt whose PreemptForNetwork candidates sit on two
+       devices returns PE_EUNSUPPORTED (the reference ranges over a Go map) */
     const uint32_t* net_device;
 } pe_alloc_table;
 
