@@ -1984,7 +1984,7 @@ constexpr uint8_t kRowCoreOut = 4;    // allocs hold cores outside the node's av
 // full build assigns them (the last assignment wins there).
 static void alloc_state_reasons(pe_stack* s) {
     s->preempt_unsupported = s->n_row_devent ? "alloc device entries beyond 4 x 255"
-                             : s->evict_too_many ? "more than 256 allocs on a node"
+                             : s->evict_too_many ? "more than 1024 allocs on a node"
                              : s->n_row_overheld ? "device instances held beyond the healthy count"
                                                  : "";
     s->cores_unsupported = s->n_row_core_out ? "allocs holding reserved cores outside the node's available set"
@@ -2114,7 +2114,7 @@ int build_alloc_state(pe_stack* s) {
         std::vector<uint32_t> fill(s->h_node_alloc_off.begin(), s->h_node_alloc_off.end() - 1);
         uint32_t max_m = 0;
         for (uint32_t i = 0; i < n; i++) max_m = std::max(max_m, cnt[i + 1]);
-        s->evict_words = max_m <= 32u ? 1u : 8u;
+        s->evict_words = max_m <= 32u ? 1u : max_m <= 256u ? 8u : 32u;
         s->evict_too_many = max_m > pe::kEvictMaxAllocs;
         for (uint32_t i = 0; i < s->allocs.size(); i++) {
             const HostAlloc& a = s->allocs[i];
@@ -2698,7 +2698,7 @@ static void md_preempt(const MdIndex& x0, const std::map<std::tuple<uint32_t, ui
         avail += al(rel).mbits;
         if (avail != 0 && needed != 0 && avail >= needed) break;
     }
-    if (out.size() > 8) { m->ev = pe::kMdUnsup; return; }
+    if (out.size() > 8 || *std::max_element(out.begin(), out.end()) > 254u) { m->ev = pe::kMdUnsup; return; }
     // the retried AssignNetwork on a fresh index of the remaining allocs: the
     // group's port offer is not in it (rank.go:362-371)
     MdIndex x1 = x0;
@@ -4228,7 +4228,7 @@ int run_parallel_select(pe_stack* s, TgPlan& g, pe_ranked_node* out, uint32_t* n
     HIP_TRY(s, s->d_ev_status.ensure(n));
     HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * n));
     HIP_TRY(s, s->d_ev_out.ensure(16));
-    HIP_TRY(s, s->d_ev_mask.ensure(sizeof(uint32_t) * (pe::kEvictWidths[1] + 1)));
+    HIP_TRY(s, s->d_ev_mask.ensure(sizeof(uint32_t) * (pe::kEvictMaxWords + 1)));
     HIP_TRY(s, s->d_ev_flags.ensure(16));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_out.p, 0, 16, s->stream));
@@ -4319,7 +4319,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
     HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * n));
     HIP_TRY(s, s->d_ev_flags.ensure(16));
     HIP_TRY(s, s->d_ev_out.ensure(16));
-    HIP_TRY(s, s->d_ev_mask.ensure(sizeof(uint32_t) * (pe::kEvictWidths[1] + 1)));
+    HIP_TRY(s, s->d_ev_mask.ensure(sizeof(uint32_t) * (pe::kEvictMaxWords + 1)));
     HIP_TRY(s, s->d_record.ensure(sizeof(pe_ranked_node)));
     HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));
     P.status = s->d_ev_status.as<uint8_t>();
@@ -4363,7 +4363,7 @@ int run_evict_select(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order,
         HIP_TRY_STATE(s, pe_launch_evict_record(&P, row, s->d_record.as<pe_ranked_node>(), s->d_ev_mask.as<uint32_t>(),
                                           s->stream));
         pe_ranked_node rr;
-        uint32_t mask[pe::kEvictWidths[1] + 1];
+        uint32_t mask[pe::kEvictMaxWords + 1];
         HIP_TRY(s, hipMemcpyAsync(&rr, s->d_record.p, sizeof(rr), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipMemcpyAsync(mask, s->d_ev_mask.p, sizeof(uint32_t) * (P.mask_words + 1), hipMemcpyDeviceToHost,
                                   s->stream));
@@ -6793,6 +6793,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
     HIP_TRY(s, s->d_ev_out.ensure(16));
     HIP_TRY(s, s->d_ev_flags.ensure(16));
     if (!words) words = s->evict_words;
+    if (words > pe::kPLoopMaxWords) return PE_OK;   // nodes past k_ploop's width: the per-Select path (W = 32)
     if (n > pe_ploop_max_n(words)) return PE_OK;   // the outcome codes outgrow the workgroup's LDS
     HIP_TRY(s, s->d_loop_out.ensure(sizeof(pe_ranked_node) * (size_t)count));
     HIP_TRY(s, s->d_ploop_mask.ensure(sizeof(uint32_t) * words * (size_t)count));
@@ -8480,11 +8481,10 @@ static int system_place_impl(pe_stack* s, uint32_t tgi, double* out_score, uint8
             } else {
                 const uint32_t E = (uint32_t)rows.size();
                 pe::PreemptArgs P = preempt_args(s, g);
-                const uint32_t W8 = pe::kEvictWidths[1];
                 HIP_TRY(s, upload_s(s, s->d_ev_rows, rows));
                 HIP_TRY(s, s->d_ev_status.ensure(E));
                 HIP_TRY(s, s->d_ev_score.ensure(sizeof(double) * E));
-                HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * W8 * E));
+                HIP_TRY(s, s->d_ev_masks.ensure(sizeof(uint32_t) * pe::kEvictMaxWords * E));
                 HIP_TRY(s, s->d_ev_offers.ensure(sizeof(uint32_t) * E));
                 HIP_TRY(s, s->d_ev_flags.ensure(16));
                 HIP_TRY(s, hipMemsetAsync(s->d_ev_flags.p, 0, 16, s->stream));

@@ -394,10 +394,12 @@ struct PreemptArgs {
     // and ProposedAllocs lists of up to 64 x mask_words (kEvictWidths)
     uint32_t mask_words;
 };
-constexpr uint32_t kEvictWidths[2] = {1u, 8u};   // instantiated widths, narrowest first
+constexpr uint32_t kEvictWidths[3] = {1u, 8u, 32u};   // instantiated widths, narrowest first
+constexpr uint32_t kEvictMaxWords = 32u;
+constexpr uint32_t kPLoopMaxWords = 8u;               // k_ploop's widest (its lists live in LDS)
 constexpr uint32_t kEvictUnsup = 1u;   // PreemptArgs::flags: a node outside what the device path models
 constexpr uint32_t kEvictWider = 2u;   // a node's alloc list exceeds the launch's eviction width
-constexpr uint32_t kEvictMaxAllocs = 32u * 8u;    // node allocs the widest launch evaluates
+constexpr uint32_t kEvictMaxAllocs = 32u * kEvictMaxWords;   // node allocs the widest launch evaluates
 
 // LimitIterator + MaxScoreIterator over per-position results.
 struct EvictResolveArgs {

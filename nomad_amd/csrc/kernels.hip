@@ -3746,13 +3746,15 @@ hipError_t pe_launch_resolve(const pe::EvictResolveArgs* r, hipStream_t st) {
     return hipGetLastError();
 }
 
-// Eviction widths (evict.inc): W = 1 (<= 32 allocs per node) or 8 (<= 256).
-// A wide launch keeps its per-lane lists in scratch: the grid is capped lower
-// so that its scratch reservation stays small.
-static inline bool evict_width_ok(uint32_t w) { return w == 1u || w == 8u; }
+// Eviction widths (evict.inc): W = 1 (<= 32 allocs per node), 8 (<= 256) or
+// 32 (<= 1024 allocs, ProposedAllocs <= 2048). A wide launch keeps its
+// per-lane lists in scratch (lane-interleaved, so the lanes' accesses to one
+// list element coalesce; W = 32 is ~19 KB per lane): the grid is capped lower
+// so that the scratch reservation stays small (32 x 256 lanes: ~150 MB).
+static inline bool evict_width_ok(uint32_t w) { return w == 1u || w == 8u || w == 32u; }
 static inline uint32_t evict_blocks(uint32_t n, uint32_t w) {
     uint32_t blocks = (n + 255) / 256;
-    const uint32_t cap = w == 1u ? 2048u : 256u;
+    const uint32_t cap = w == 1u ? 2048u : w == 8u ? 256u : 32u;
     if (blocks > cap) blocks = cap;
     return blocks ? blocks : 1u;
 }
@@ -3761,7 +3763,8 @@ hipError_t pe_launch_evict(const pe::PreemptArgs* a, const pe::EvictResolveArgs*
     if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
     const uint32_t blocks = evict_blocks(a->n_visit, a->mask_words);
     if (a->mask_words == 1u) hipLaunchKernelGGL((pe::k_evict<false, 1>), dim3(blocks), dim3(256), 0, st, *a);
-    else hipLaunchKernelGGL((pe::k_evict<false, 8>), dim3(blocks), dim3(256), 0, st, *a);
+    else if (a->mask_words == 8u) hipLaunchKernelGGL((pe::k_evict<false, 8>), dim3(blocks), dim3(256), 0, st, *a);
+    else hipLaunchKernelGGL((pe::k_evict<false, 32>), dim3(blocks), dim3(256), 0, st, *a);
     hipLaunchKernelGGL(pe::k_evict_resolve, dim3(1), dim3(pe::kResolveBlock), 0, st, *r);
     return hipGetLastError();
 }
@@ -3784,14 +3787,16 @@ hipError_t pe_launch_census(const pe::BatchArgs* a, uint32_t* counts, uint8_t* s
 hipError_t pe_launch_evict_only(const pe::PreemptArgs* a, hipStream_t st) {
     if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
     const uint32_t blocks = evict_blocks(a->n_visit, a->mask_words);
-    const bool w1 = a->mask_words == 1u;
+    const uint32_t w = a->mask_words;
     if (a->parts_out) {
         if (!a->nparts_out || !a->mask_out || !a->offers_out) return hipErrorInvalidValue;
-        if (w1) hipLaunchKernelGGL((pe::k_evict<true, 1>), dim3(blocks), dim3(256), 0, st, *a);
-        else hipLaunchKernelGGL((pe::k_evict<true, 8>), dim3(blocks), dim3(256), 0, st, *a);
+        if (w == 1u) hipLaunchKernelGGL((pe::k_evict<true, 1>), dim3(blocks), dim3(256), 0, st, *a);
+        else if (w == 8u) hipLaunchKernelGGL((pe::k_evict<true, 8>), dim3(blocks), dim3(256), 0, st, *a);
+        else hipLaunchKernelGGL((pe::k_evict<true, 32>), dim3(blocks), dim3(256), 0, st, *a);
     } else {
-        if (w1) hipLaunchKernelGGL((pe::k_evict<false, 1>), dim3(blocks), dim3(256), 0, st, *a);
-        else hipLaunchKernelGGL((pe::k_evict<false, 8>), dim3(blocks), dim3(256), 0, st, *a);
+        if (w == 1u) hipLaunchKernelGGL((pe::k_evict<false, 1>), dim3(blocks), dim3(256), 0, st, *a);
+        else if (w == 8u) hipLaunchKernelGGL((pe::k_evict<false, 8>), dim3(blocks), dim3(256), 0, st, *a);
+        else hipLaunchKernelGGL((pe::k_evict<false, 32>), dim3(blocks), dim3(256), 0, st, *a);
     }
     return hipGetLastError();
 }
@@ -3801,7 +3806,8 @@ hipError_t pe_launch_evict_record(const pe::PreemptArgs* a, uint32_t row, pe_ran
                                   hipStream_t st) {
     if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
     if (a->mask_words == 1u) hipLaunchKernelGGL(pe::k_evict_record<1>, dim3(1), dim3(64), 0, st, *a, row, out, mask);
-    else hipLaunchKernelGGL(pe::k_evict_record<8>, dim3(1), dim3(64), 0, st, *a, row, out, mask);
+    else if (a->mask_words == 8u) hipLaunchKernelGGL(pe::k_evict_record<8>, dim3(1), dim3(64), 0, st, *a, row, out, mask);
+    else hipLaunchKernelGGL(pe::k_evict_record<32>, dim3(1), dim3(64), 0, st, *a, row, out, mask);
     return hipGetLastError();
 }
 
@@ -3814,8 +3820,11 @@ hipError_t pe_launch_commit_evicted(const pe::PreemptArgs* a, uint8_t* preempted
     if (a->mask_words == 1u)
         hipLaunchKernelGGL(pe::k_commit_evicted<1>, dim3(blocks), dim3(256), 0, st, *a, preempted, pcount, dev_free,
                            placed);
-    else
+    else if (a->mask_words == 8u)
         hipLaunchKernelGGL(pe::k_commit_evicted<8>, dim3(blocks), dim3(256), 0, st, *a, preempted, pcount, dev_free,
+                           placed);
+    else
+        hipLaunchKernelGGL(pe::k_commit_evicted<32>, dim3(blocks), dim3(256), 0, st, *a, preempted, pcount, dev_free,
                            placed);
     return hipGetLastError();
 }
@@ -3827,8 +3836,11 @@ hipError_t pe_launch_commit_preempt(const pe::PreemptArgs* a, uint32_t row, cons
     if (a->mask_words == 1u)
         hipLaunchKernelGGL(pe::k_commit_preempt<1>, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount,
                            dev_free);
-    else
+    else if (a->mask_words == 8u)
         hipLaunchKernelGGL(pe::k_commit_preempt<8>, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount,
+                           dev_free);
+    else
+        hipLaunchKernelGGL(pe::k_commit_preempt<32>, dim3(1), dim3(64), 0, st, *a, row, mask, preempted, pcount,
                            dev_free);
     return hipGetLastError();
 }
@@ -3887,8 +3899,10 @@ hipError_t pe_launch_evict_trace(const pe::PreemptArgs* a, const uint32_t* rows,
     if (!evict_width_ok(a->mask_words)) return hipErrorInvalidValue;
     if (a->mask_words == 1u)
         hipLaunchKernelGGL(pe::k_evict_trace<1>, dim3((n + 63) / 64), dim3(64), 0, st, *a, rows, n, code, named);
-    else
+    else if (a->mask_words == 8u)
         hipLaunchKernelGGL(pe::k_evict_trace<8>, dim3((n + 63) / 64), dim3(64), 0, st, *a, rows, n, code, named);
+    else
+        hipLaunchKernelGGL(pe::k_evict_trace<32>, dim3((n + 63) / 64), dim3(64), 0, st, *a, rows, n, code, named);
     return hipGetLastError();
 }
 
@@ -4150,7 +4164,7 @@ static int ploop_max_dyn(int wi) {
 }
 
 uint32_t pe_ploop_max_n(uint32_t words) {
-    if (!evict_width_ok(words)) return 0;
+    if (words != 1u && words != 8u) return 0;   // k_ploop<1> / <8> only (pe::kPLoopMaxWords)
     const size_t d = (size_t)ploop_max_dyn(words == 1u ? 0 : 1);
     uint32_t n = (uint32_t)std::min<size_t>(kPLoopMaxN, d * 8u / 5u) & ~31u;   // 5/8 byte per position
     while (n && pe_ploop_lds_bytes(n) > d) n -= 32u;

@@ -163,3 +163,52 @@ def test_select_commit_protocol_with_long_preempted_lists():
         out.append(res)
     assert out[0] == out[1]
     assert max(len(x[2]) for x in out[0]) > 16
+
+
+def dense_cluster(n_nodes, per_node, seed):
+    """Nodes of `per_node` (> 256) small low-priority allocs, sized so that the
+    node holds them all: the widest eviction width (W = 32, 1024 allocs)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes, allocs = [], []
+    for k in range(n_nodes):
+        nd = synth.mock_node("dense-%04d" % k)
+        nd.name = "dense-%04d" % k
+        nd.cpu_shares = per_node * 520 + 2000
+        nd.memory_mb = per_node * 1050 + 4096
+        nd.disk_mb = per_node * 110 + 8192
+        nd.compute_class()
+        nodes.append(nd)
+        for i in range(per_node):
+            allocs.append(Allocation(node_id=nd.id, job_id="bg-%d" % (i % 11), task_group="w%d" % (i % 3),
+                                     cpu_shares=int(rng.integers(100, 900)), memory_mb=int(rng.integers(200, 1800)),
+                                     disk_mb=100, priority=int(rng.choice([20, 30, 40])), max_parallel=(i % 4)))
+    return nodes, allocs
+
+
+@pytest.mark.parametrize("per_node", [300, 600])
+def test_preemption_past_256_allocs(per_node):
+    """Nodes of 300 and 600 allocs: PreemptForTaskGroup over the whole list
+    at W = 32 (masks of 32 words, index lists of 1024 / 2048 entries in the
+    lane's scratch); the count loop takes the per-Select path past k_ploop's
+    width. Placement by placement equal to the oracle."""
+    nodes, allocs = dense_cluster(6, per_node, seed=per_node)
+    job = big_ask_job(8, 30000, 8000)
+    re = _both(nodes, allocs, job, synth.shuffle(len(nodes), 7))
+    assert sum(1 for x in re if x.row >= 0) >= 4
+    assert max(len(x.preempted) for x in re) > 16
+
+
+def test_proposed_allocs_past_512():
+    """250 state allocs (a W = 8 snapshot) plus more than 262 plan placements
+    of the job on the node: ProposedAllocs passes 512 entries and the evicting
+    Selects rerun at W = 32."""
+    nd = synth.mock_node("solo")
+    nd.name = "solo"
+    nd.cpu_shares, nd.memory_mb, nd.disk_mb = 100000, 1 << 20, 1 << 20
+    nd.compute_class()
+    allocs = [Allocation(node_id=nd.id, job_id="low-%d" % (i % 3), task_group="w", cpu_shares=200, memory_mb=256,
+                         disk_mb=10, priority=20) for i in range(250)]
+    job = big_ask_job(420, 150, 64)
+    re = _both([nd], allocs, job, [0])
+    assert sum(1 for x in re if x.row >= 0) > 340
+    assert any(x.preempted for x in re)
