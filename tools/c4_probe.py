@@ -14,10 +14,12 @@ n = 100000
 cs = synth_columnar.ColumnarState(n, seed=11, kind="c4", prefill=0.05)
 job = synth.mock_system_job()
 rows = np.random.Generator(np.random.PCG64(5)).permutation(n).astype(np.uint32)
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 12
 st = SystemStack()
 st.SetStateColumnar(cs)
-for i in range(12):
-    view = i >= 6   # the zero-copy results (SystemPlaceView) for the second half
+walls = []
+for i in range(iters):
+    view = i >= min(6, iters // 2)   # the zero-copy results (SystemPlaceView) for the second half
     st.ResetPlan()
     st.SetJob(job)
     t0 = time.perf_counter()
@@ -25,6 +27,12 @@ for i in range(12):
     t1 = time.perf_counter()
     _, _, placed = st.SystemPlaceView(0) if view else st.SystemPlace(0)
     t2 = time.perf_counter()
-    print("iter %d%s: SetNodes %.1f us, SystemPlace %.1f us (kernel %.1f us), placed %d"
-          % (i, " view" if view else "", (t1 - t0) * 1e6, (t2 - t1) * 1e6, st.last_kernel_ms() * 1e3, placed))
+    if view:
+        walls.append((t2 - t0) * 1e6)
+    if iters <= 12:
+        print("iter %d%s: SetNodes %.1f us, SystemPlace %.1f us (kernel %.1f us), placed %d"
+              % (i, " view" if view else "", (t1 - t0) * 1e6, (t2 - t1) * 1e6, st.last_kernel_ms() * 1e3, placed))
+w = np.sort(np.array(walls[1:]))
+print("SetNodes + SystemPlaceView over %d calls: p10 %.1f  median %.1f  p90 %.1f us"
+      % (len(w), w[len(w) // 10], np.median(w), w[9 * len(w) // 10]))
 st.close()

@@ -1,3 +1,10 @@
+#!/bin/bash
+# C4 host-overhead breakdown: the engine's API profile and a runtime timeline
 mkdir -p gpurun_out/r6f
-timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_metrics.py -k "system" > gpurun_out/r6f/t.log 2>&1 ; \
-PE_METRICS_PROF=1 timeout -k 10 600 python bench.py --steps 4 --warmup 1 --sweep-nodes 0 --sections c3,c4_drop_in,c5 --c5-cpu-seconds 30 > gpurun_out/r6f/b.json 2> gpurun_out/r6f/b.err
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+PE_API_PROF=1 timeout -k 10 120 python tools/c4_probe.py > gpurun_out/r6f/probe.txt 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace --output-format csv \
+  -d gpurun_out/r6f/trace -o c4 -- python tools/c4_probe.py > gpurun_out/r6f/trace.txt 2>&1
+rc=$?
+tail -20 gpurun_out/r6f/probe.txt
+exit $rc

@@ -1,3 +1,7 @@
+#!/bin/bash
 mkdir -p gpurun_out/r6g
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_metrics.py tests/test_cores.py tests/test_static_ports.py > gpurun_out/r6g/t.log 2>&1 ; \
-PE_METRICS_PROF=1 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --sweep-nodes 0 --sections "" > gpurun_out/r6g/b.json 2> gpurun_out/r6g/b.err
+for k in 1 2 3; do
+timeout -k 10 120 python tools/c4_probe.py 400 > gpurun_out/r6g/new$k.txt 2>&1 && \
+PE_SYS_SPLIT_SYNC=1 timeout -k 10 120 python tools/c4_probe.py 400 > gpurun_out/r6g/old$k.txt 2>&1 || exit 1
+done
+for f in gpurun_out/r6g/new*.txt gpurun_out/r6g/old*.txt; do echo $f $(tail -1 $f); done
