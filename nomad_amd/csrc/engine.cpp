@@ -140,6 +140,8 @@ hipError_t pe_launch_scatter_rows(void* dst, uint32_t words, const void* payload
 hipError_t pe_launch_counts(const pe::CountDsts* d, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
                             const pe::ResetArgs* r, hipStream_t st);
 size_t pe_fullpass_lds_bytes(uint32_t n);
+hipError_t pe_launch_fullpass_svc(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
+                                  uint32_t count, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
                                   uint32_t count, pe_ranked_node* out, uint32_t* state, unsigned long long* prof,
                                   hipStream_t st);
@@ -6981,11 +6983,29 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         HIP_TRY(s, s->d_full_args.ensure(sizeof(pe::SweepArgs)));
         HIP_TRY(s, hipMemcpyAsync(s->d_full_args.p, &s->h_full_args, sizeof(pe::SweepArgs), hipMemcpyHostToDevice,
                                   s->stream));
-        HIP_TRY_STATE(s, pe_launch_fullpass_lds(s->d_full_args.as<pe::SweepArgs>(), A.spread_tab ? A.tg.n_psets : 0,
-                                          s->d_visit.as<uint32_t>(), n, count, s->d_loop_out.as<pe_ranked_node>(),
-                                          state, fprof ? d_prof.as<unsigned long long>() : nullptr, s->stream));
-        HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(s, hipStreamSynchronize(s->stream));
+        const int np = A.spread_tab ? A.tg.n_psets : 0;
+        // the service-wave loop (k_fullpass_svc, up to 3840 options): target
+        // spreads and asks without devices or reserved cores (its commit is
+        // the stores-only one), on runs long enough to repay building every
+        // option's next entry too
+        bool svc = !fprof && count >= 8 && A.ask.n_dev == 0 && A.ask.cores == 0 && np == A.tg.n_psets;
+        for (int p = 0; p < g.n_spread && svc; p++) svc = !g.psets[p]->even;
+        if (const char* e = std::getenv("PE_FULL_SVC")) svc = svc && std::atoi(e) != 0;
+        if (svc) {
+            HIP_TRY_STATE(s, pe_launch_fullpass_svc(s->d_full_args.as<pe::SweepArgs>(), np, s->d_visit.as<uint32_t>(), n,
+                                              count, s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
+            HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(s, hipStreamSynchronize(s->stream));
+            svc = h_state[5] == 0;   // more options than its entries: nothing committed, the loop below
+            if (!svc) HIP_TRY(s, hipMemsetAsync(state, 0, 8 * sizeof(uint32_t), s->stream));
+        }
+        if (!svc) {
+            HIP_TRY_STATE(s, pe_launch_fullpass_lds(s->d_full_args.as<pe::SweepArgs>(), np,
+                                              s->d_visit.as<uint32_t>(), n, count, s->d_loop_out.as<pe_ranked_node>(),
+                                              state, fprof ? d_prof.as<unsigned long long>() : nullptr, s->stream));
+            HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(s, hipStreamSynchronize(s->stream));
+        }
         if (fprof) {
             unsigned long long h[12];
             HIP_TRY(s, hipMemcpy(h, d_prof.p, sizeof(h), hipMemcpyDeviceToHost));

@@ -3402,6 +3402,324 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_lds(const SweepArgs* 
             const_cast<double*>(A.spread_tab)[t.pset_tab_off[p] + v] = tab[t.pset_tab_off[p] + v];
 }
 
+// The full-pass loop with a service wave (C3's shape: target spreads, no
+// device asks or reserved cores). Waves 0-14 hold the options (kSvcPer per
+// lane) and run each placement's approximate and exact passes as
+// k_fullpass_lds does; wave 15 serves the winners one placement behind. The
+// build gives every option its entry with one more placement of the loop as
+// well (next sum / meta), so at the resolve thread 0 swaps the winner's next
+// entry in and updates its spread boost, and the next placement's passes start
+// at once. Meanwhile the service wave loads the winner, writes its record
+// (lane 0, dk = 0), evaluates the entry two placements on (lane 1, dk = 2:
+// the next entry the winner swaps in) and commits it. The next placement's
+// barrier waits for the service, so a winner's next entry is in place before
+// it can win again. Results equal k_fullpass_lds. More options than kSvcCap:
+// state[5] = 1 before any commit (the host runs k_fullpass_lds instead).
+constexpr int kSvcEntryWaves = kFullWaves - 1;
+constexpr int kSvcEntryLanes = kSvcEntryWaves * 64;
+constexpr int kSvcPer = 4;
+constexpr uint32_t kSvcCap = (uint32_t)kSvcEntryLanes * kSvcPer;   // 3840 options, 32 B of LDS each
+
+template <int NP>
+__global__ void __launch_bounds__(kFullThreads) k_fullpass_svc(const SweepArgs* __restrict__ Ap, const uint32_t* visit,
+                                                               uint32_t n, uint32_t count, pe_ranked_node* out,
+                                                               uint32_t* state) {
+    const SweepArgs& A = *Ap;
+    extern __shared__ double svc_sum[];                                      // [kSvcCap] score_head sums
+    double* next_sum = svc_sum + kSvcCap;                                     // ... with one more placement
+    uint32_t* ent_meta = reinterpret_cast<uint32_t*>(next_sum + kSvcCap);     // status | k << 2 | spread values
+    uint32_t* next_meta = ent_meta + kSvcCap;
+    uint32_t* ent_rank = next_meta + kSvcCap;                                 // visit rank (LimitIterator order)
+    uint32_t* ent_row = ent_rank + kSvcCap;
+    __shared__ double tab[kAuxPsets * (kAuxValues + 1)];
+    __shared__ double desired[kAuxPsets * kAuxValues];
+    __shared__ uint32_t counts[kAuxPsets * kAuxValues];
+    __shared__ double aff_lds[kAuxValues];
+    __shared__ double red_s[kFullWaves];
+    __shared__ uint32_t red_r[kFullWaves], red_e[kFullWaves], red_f[kFullWaves], red_x[kFullWaves];
+    __shared__ SweepRec red[kFullWaves];
+    __shared__ uint32_t scratch[4];
+    __shared__ uint32_t sh_nf, sh_ne, sh_stop, sh_win, sh_win_e, sh_m;
+    __shared__ uint32_t pend_on, pend_e, pend_nf, pend_ne, pend_it;   // the winner the service wave serves next
+    __shared__ double pend_sp;                                        // its spread score at its placement
+    __shared__ double parts1[PE_MAX_SCORES];                          // lane 1's parts (unused)
+    __shared__ double rcp_k[8];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const TgTables& t = A.tg;
+    constexpr int np = NP;
+    const uint32_t off = A.offset;
+    for (int i = tid; i < kAuxValues; i += kFullThreads) aff_lds[i] = A.aff_vals[i];
+    if (tid < 8) rcp_k[tid] = tid ? 1.0 / (double)tid : 0.0;
+    if (tid == 0) { sh_m = 0; pend_on = 0; }
+    for (int p = 0; p < np; p++)
+        for (int v = tid; v < t.pset_nvals[p]; v += kFullThreads) {
+            counts[t.pset_cnt_off[p] + v] = t.pset_counts[p][v];
+            desired[t.pset_cnt_off[p] + v] = t.pset_desired[p][v];   // target spreads only (the host checks)
+        }
+    __syncthreads();
+    if (np) build_spread_table<kFullThreads>(t, counts, tab, scratch);
+    auto spread_of = [&](uint32_t meta) __attribute__((always_inline)) -> double {   // lookup_scores' total
+        double sp = 0.0;
+#pragma unroll
+        for (int p = 0; p < np; p++) {
+            const uint32_t v = (meta >> (8 + 8 * p)) & 255u;
+            sp += (v == kAuxMissing) ? -1.0 : tab[t.pset_tab_off[p] + v];
+        }
+        return sp;
+    };
+    auto load = [&](uint32_t row, NodeIn& in) __attribute__((always_inline)) -> uint32_t {   // the sweep's AUX fetch
+        in.r = A.soa.rec[row];
+        in.coll_tg = t.coll_tg[row];
+        in.dev_free = t.dev_free ? t.dev_free[row] : 0u;
+        const uint32_t aux = A.node_aux[row];
+        in.feas = aux >> 31;
+        return aux;
+    };
+    // status and score_head of a loaded node with dk placements of this loop
+    // added; with a `parts` pointer the parts are written there
+    auto head = [&](uint32_t row, const NodeIn& in, uint32_t aux, uint32_t dk, double* parts, double* sum,
+                    uint32_t* kk) __attribute__((always_inline)) -> int {
+        ScoreIn si;
+        const int st = status_loaded(A.soa, t, t.class_ok, A.ask, dk, row, in, &si);
+        *kk = 0;
+        *sum = 0.0;
+        if (st == kOption) {
+            si.penalty = A.penalty_bits ? (A.penalty_bits[row >> 5] >> (row & 31)) & 1u : 0u;
+            si.aff = aff_lds[aux & 255u];
+            si.spread = 0.0;
+            *sum = parts ? score_head<true>(A.ask, A.log10, si, parts, *kk)
+                         : score_head<false>(A.ask, A.log10, si, nullptr, *kk);
+        }
+        return st;
+    };
+    auto final_sum = [&](uint32_t e, uint32_t* kk_out) __attribute__((always_inline)) -> double {
+        const uint32_t meta = ent_meta[e];
+        double sum = svc_sum[e];
+        const double sp = spread_of(meta);
+        uint32_t kk = (meta >> 2) & 7u;
+        if (sp != 0.0) { sum += sp; kk++; }
+        *kk_out = kk;
+        return sum;
+    };
+    auto rank_of_pos = [&](uint32_t pos) __attribute__((always_inline)) -> uint32_t {
+        return pos >= off ? pos - off : pos + n - off;
+    };
+    // build: every option's entry now and with one more placement of the loop
+    uint32_t nf = 0, ne = 0;
+    for (uint32_t pos = tid; pos < n; pos += kFullThreads) {
+        const uint32_t row = visit[pos];
+        NodeIn in;
+        const uint32_t aux = load(row, in);
+        double s;
+        uint32_t kk;
+        const int st = head(row, in, aux, 0u, nullptr, &s, &kk);
+        nf += st == kFiltered;
+        ne += st == kExhausted;
+        if (st == kOption) {
+            const uint32_t e = atomicAdd(&sh_m, 1u);
+            if (e < kSvcCap) {
+                svc_sum[e] = s;
+                ent_meta[e] = (uint32_t)st | (kk << 2) | (aux & 0x00FFFF00u);
+                ent_rank[e] = rank_of_pos(pos);
+                ent_row[e] = row;
+                double s1;
+                uint32_t k1;
+                const int st1 = head(row, in, aux, 1u, nullptr, &s1, &k1);
+                next_sum[e] = s1;
+                next_meta[e] = (uint32_t)st1 | (k1 << 2) | (aux & 0x00FFFF00u);
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        nf += (uint32_t)__shfl_xor((int)nf, o);
+        ne += (uint32_t)__shfl_xor((int)ne, o);
+    }
+    if (lane == 0) { red_f[wid] = nf; red_x[wid] = ne; }
+    __syncthreads();
+    const uint32_t m = sh_m;
+    if (m > kSvcCap) {   // uniform: nothing committed yet, the host takes the other loop
+        if (tid == 0) state[5] = 1;
+        return;
+    }
+    if (tid == 0) {
+        uint32_t a = 0, b = 0;
+        for (int w = 0; w < kFullWaves; w++) { a += red_f[w]; b += red_x[w]; }
+        sh_nf = a;
+        sh_ne = b;
+        sh_stop = 0;
+    }
+    __syncthreads();
+    // the service of one winner (lanes 0 and 1 of wave 15): its record (lane
+    // 0: the placement's state, dk = 0), its entry two placements on (lane 1,
+    // dk = 2: what it swaps in when it wins again), the commit (lane 0)
+    auto serve = [&]() __attribute__((always_inline)) {
+        const uint32_t e = pend_e, row = ent_row[e];
+        pe_ranked_node* o = out + pend_it;
+        NodeIn in;
+        const uint32_t aux = load(row, in);
+        double s;
+        uint32_t kk;
+        // both lanes take the parts-keeping path (lockstep, no divergence)
+        const int st = head(row, in, aux, lane == 0 ? 0u : 2u, lane == 0 ? o->scores : parts1, &s, &kk);
+        if (lane == 1) {
+            next_sum[e] = s;
+            next_meta[e] = (uint32_t)st | (kk << 2) | (aux & 0x00FFFF00u);
+        } else {
+            const double sp = pend_sp;
+            if (sp != 0.0) {   // SpreadIterator (spread.go:110-174)
+                s += sp;
+                o->scores[kk] = sp;
+                kk++;
+            }
+            o->row = (int32_t)row;
+            o->final_score = s / (double)kk;   // ScoreNormalizationIterator (rank.go:762-767)
+            o->n_scores = kk;
+            o->nodes_evaluated = n;            // a full pass pulls every node
+            o->nodes_filtered = pend_nf;
+            o->nodes_exhausted = pend_ne;
+            o->new_offset = off;               // and leaves the cursor where it is
+            record_offers(A.soa, A.ask, t, row, 0u, o);
+            NodeRec& r = A.soa.rec[row];       // commit_row from the loaded values: stores only
+            r.used_cpu = in.r.used_cpu + A.ask.cpu;
+            r.used_mem = in.r.used_mem + A.ask.mem;
+            r.used_disk = in.r.used_disk + A.ask.disk;
+            r.used_mbits = in.r.used_mbits + A.ask.commit_mbits;
+            r.used_dyn = in.r.used_dyn + A.ask.commit_dyn;
+            A.soa.coll_job[row] += 1;
+            t.coll_tg[row] = in.coll_tg + 1;
+            pend_on = 0;   // thread 0 sets the next one after the barrier
+        }
+    };
+    for (uint32_t it = 0; it < count; it++) {
+        if (wid < kSvcEntryWaves) {
+            double ap[kSvcPer];
+            double amax = -__builtin_inff();
+#pragma unroll
+            for (int j = 0; j < kSvcPer; j++) {
+                const uint32_t e = (uint32_t)tid + (uint32_t)j * kSvcEntryLanes;
+                ap[j] = -__builtin_inff();
+                if (e < m) {
+                    uint32_t kk;
+                    const double sum = final_sum(e, &kk);
+                    if ((ent_meta[e] & 3u) == (uint32_t)kOption) ap[j] = sum * rcp_k[kk];
+                }
+                amax = ap[j] > amax ? ap[j] : amax;
+            }
+            amax = __ockl_wfred_max_f64(amax);
+            const double cut = amax - (__builtin_fabs(amax) * 0x1p-48 + 0x1p-1000);
+            double best = -__builtin_inff();
+            uint32_t best_rank = 0xFFFFFFFFu, best_e = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < kSvcPer; j++) {
+                const bool near = ap[j] >= cut && ap[j] != -__builtin_inff();   // options only
+                if (__ballot(near)) {
+                    if (near) {
+                        const uint32_t e = (uint32_t)tid + (uint32_t)j * kSvcEntryLanes;
+                        uint32_t kk;
+                        const double sc = final_sum(e, &kk) / (double)kk;
+                        const uint32_t rk = ent_rank[e];
+                        if (sc > best || (sc == best && rk < best_rank)) { best = sc; best_rank = rk; best_e = e; }
+                    }
+                }
+            }
+            {   // the wave's (max, earliest rank) over its few candidate lanes
+                uint64_t cand = __ballot(best_rank != 0xFFFFFFFFu);
+                double wb = -__builtin_inff();
+                uint32_t wr = 0xFFFFFFFFu, we = 0xFFFFFFFFu;
+                while (cand) {
+                    const int l = __builtin_ctzll(cand);
+                    cand &= cand - 1;
+                    const double b = readlane_f64(best, l);
+                    const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)best_rank, l);
+                    if (b > wb || (b == wb && r < wr)) {
+                        wb = b;
+                        wr = r;
+                        we = (uint32_t)__builtin_amdgcn_readlane((int)best_e, l);
+                    }
+                }
+                if (lane == 0) { red_s[wid] = wb; red_r[wid] = wr; red_e[wid] = we; }
+            }
+        } else {
+            if (pend_on && lane < 2) serve();
+            if (lane == 0) { red_s[wid] = -__builtin_inff(); red_r[wid] = 0xFFFFFFFFu; }
+        }
+        __syncthreads();
+        // every thread resolves the block's winner (max score, then the
+        // earliest rank among the waves holding it)
+        double best = lane < kFullWaves ? red_s[lane] : -__builtin_inff();
+        best = __ockl_wfred_max_f64(best);
+        uint32_t win = __ockl_wfred_min_u32(lane < kFullWaves && red_s[lane] == best ? red_r[lane] : 0xFFFFFFFFu);
+        bool skip_rule = false;
+        if (win != 0xFFFFFFFFu && !(best > 0.0)) {   // every option non-positive: the skip rule decides (rare)
+            skip_rule = true;
+            SweepRec r;
+            rec_init(r);
+            for (uint32_t e = tid; e < m; e += kFullThreads) {
+                if ((ent_meta[e] & 3u) != (uint32_t)kOption) continue;
+                uint32_t kk;
+                const double sum = final_sum(e, &kk);
+                rec_add(r, ent_rank[e], sum / (double)kk);
+            }
+            rec_block_reduce<kFullThreads>(r, red);
+            if (tid == 0) sh_win = rec_winner(r);
+            __syncthreads();
+            win = sh_win;
+            if (win != 0xFFFFFFFFu) {
+                for (uint32_t e = tid; e < m; e += kFullThreads)
+                    if (ent_rank[e] == win) sh_win_e = e;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            pe_ranked_node* o = out + it;
+            if (win == 0xFFFFFFFFu) {
+                o->row = -1;
+                o->nodes_evaluated = n;            // a full pass pulls every node
+                o->nodes_filtered = sh_nf;
+                o->nodes_exhausted = sh_ne;
+                o->new_offset = off;
+                state[0] = 1;
+                sh_stop = 1;
+            } else {
+                uint32_t e = sh_win_e;
+                if (!skip_rule)
+                    for (int w = 0; w < kFullWaves; w++)
+                        if (red_s[w] == best && red_r[w] == win) { e = red_e[w]; break; }
+                const uint32_t meta0 = ent_meta[e];
+                pend_e = e;
+                pend_it = it;
+                pend_nf = sh_nf;
+                pend_ne = sh_ne;
+                pend_sp = spread_of(meta0);   // the boost this placement saw
+                pend_on = 1;
+                // the winner's entry with this placement added
+                svc_sum[e] = next_sum[e];
+                ent_meta[e] = next_meta[e];
+                const uint32_t st1 = next_meta[e] & 3u;
+                sh_nf += st1 == (uint32_t)kFiltered;
+                sh_ne += st1 == (uint32_t)kExhausted;
+#pragma unroll
+                for (int p = 0; p < np; p++) {   // the target boost of the winner's value (build_spread_table)
+                    const uint32_t v = (meta0 >> (8 + 8 * p)) & 255u;
+                    if (v == kAuxMissing) continue;
+                    const uint32_t c = ++counts[t.pset_cnt_off[p] + v];
+                    t.pset_counts[p][v] = c;
+                    const double d = desired[t.pset_cnt_off[p] + v];
+                    tab[t.pset_tab_off[p] + v] = d != d ? -1.0 : ((d - (double)(c + 1u)) / d) * t.pset_weight_frac[p];
+                }
+                state[1] = it + 1;
+            }
+        }
+        __syncthreads();
+        if (sh_stop) break;
+    }
+    if (wid == kSvcEntryWaves && pend_on && lane < 2) serve();   // the last winner
+    // the HBM table the next Select starts from
+    for (int p = 0; p < np; p++)
+        for (int v = tid; v < t.pset_nvals[p]; v += kFullThreads)
+            const_cast<double*>(A.spread_tab)[t.pset_tab_off[p] + v] = tab[t.pset_tab_off[p] + v];
+}
+
 // Grid-wide barrier of the persistent count loop (every workgroup resident;
 // the host launches at most one per CU). Stores of the whole workgroup are
 // released at agent scope before the arrival and acquired after it, so rows
@@ -4087,6 +4405,39 @@ hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint
         default:
             hipLaunchKernelGGL(pe::k_fullpass_lds<2>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
                                out, state, prof);
+            break;
+    }
+    return hipGetLastError();
+}
+
+size_t pe_fullpass_svc_bytes() { return (size_t)pe::kSvcCap * (2 * sizeof(double) + 4 * sizeof(uint32_t)); }
+uint32_t pe_fullpass_svc_cap() { return pe::kSvcCap; }
+
+hipError_t pe_launch_fullpass_svc(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
+                                  uint32_t count, pe_ranked_node* out, uint32_t* state, hipStream_t st) {
+    const size_t lds = pe_fullpass_svc_bytes();
+    static bool attr = false;
+    if (!attr) {
+        for (const void* f : {reinterpret_cast<const void*>(&pe::k_fullpass_svc<0>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<1>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<2>)}) {
+            const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        attr = true;
+    }
+    switch (np) {
+        case 0:
+            hipLaunchKernelGGL(pe::k_fullpass_svc<0>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
+                               out, state);
+            break;
+        case 1:
+            hipLaunchKernelGGL(pe::k_fullpass_svc<1>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
+                               out, state);
+            break;
+        default:
+            hipLaunchKernelGGL(pe::k_fullpass_svc<2>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
+                               out, state);
             break;
     }
     return hipGetLastError();
