@@ -3657,9 +3657,18 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         } else {
             g.job_ok_node.clear();
         }
-        classify_classes(s, g, ev);
-        decide_classes(s, g, ev, memo, order.data(), order.size(), start);
-        class_ok = class_verdicts(s, g, memo);
+        {
+            ApiScope prof_c_(s, "tables.classify");
+            classify_classes(s, g, ev);
+        }
+        {
+            ApiScope prof_d_(s, "tables.decide");
+            decide_classes(s, g, ev, memo, order.data(), order.size(), start);
+        }
+        {
+            ApiScope prof_v_(s, "tables.verdicts");
+            class_ok = class_verdicts(s, g, memo);
+        }
         if (s->job_escaped) node_ok = g.job_ok_node;
     }
     g.node_ok_used = !node_ok.empty();
@@ -3703,6 +3712,7 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
         }
     }
 
+    ApiScope prof_aff_(s, "tables.affinity+rest");
     // NodeAffinityIterator score per class (rank.go:698-725)
     g.has_aff_table = !g.affinities.empty();
     g.node_aff_used = false;
@@ -3860,6 +3870,7 @@ int prepare_tg(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& order, ui
     if (!s->cores_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, s->cores_unsupported);
     if (g.ask.cores > 0 && !s->cores_tg_unsupported.empty()) return s->fail(PE_EUNSUPPORTED, s->cores_tg_unsupported);
     if (!g.psets_built) {
+        ApiScope prof_p_(s, "prepare_tg.psets");
         int rc = build_psets(s, g);
         if (rc) return rc;
         if (!g.unsupported.empty()) return s->fail(PE_EUNSUPPORTED, g.unsupported);
@@ -3870,6 +3881,7 @@ int prepare_tg(pe_stack* s, uint32_t tgi, const std::vector<uint32_t>& order, ui
         if (other != g.md_other) g.tables_valid = false;
     }
     if (!g.tables_valid) {
+        ApiScope prof_t_(s, "prepare_tg.tables");
         int rc = build_tables(s, g, order, start);
         if (rc) return rc;
     }
@@ -4042,6 +4054,7 @@ int sweep_setup(pe_stack* s, TgPlan& g, const pe_select_options* opts, uint32_t 
         A.spread_tab = s->d_spread_tab.as<double>();
     }
     if (!g.aux_valid) {
+        ApiScope prof_a_(s, "sweep.build_aux");
         int rc = build_aux(s, g, A.tg);
         if (rc) return rc;
     }
@@ -6947,6 +6960,7 @@ static int ploop_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
 // `count` x (run_sweep_select + pe_commit).
 static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count, pe_ranked_node* out,
                             uint32_t* placed) {
+    ApiScope prof_(s, "sweep_count_loop");
     const uint32_t n = (uint32_t)s->visit.size();
     pe::SweepArgs A;
     uint32_t blocks = 0;
@@ -6988,10 +7002,12 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         // spreads and asks without devices or reserved cores (its commit is
         // the stores-only one), on runs long enough to repay building every
         // option's next entry too
-        bool svc = !fprof && count >= 8 && A.ask.n_dev == 0 && A.ask.cores == 0 && np == A.tg.n_psets;
+        bool svc = !fprof && count >= 8 && A.ask.n_dev == 0 && A.ask.cores == 0 && np == A.tg.n_psets &&
+                   A.tg.n_psets == A.tg.n_spread;
         for (int p = 0; p < g.n_spread && svc; p++) svc = !g.psets[p]->even;
         if (const char* e = std::getenv("PE_FULL_SVC")) svc = svc && std::atoi(e) != 0;
         if (svc) {
+            ApiScope prof_k_(s, "sweep.svc_kernel+sync");
             HIP_TRY_STATE(s, pe_launch_fullpass_svc(s->d_full_args.as<pe::SweepArgs>(), np, s->d_visit.as<uint32_t>(), n,
                                               count, s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
             HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
@@ -7563,7 +7579,11 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     // placement as for the whole count: run the group's remaining count. Every
     // other loop pays per placement: start with one and double while the runs
     // get used up (spec_flush).
-    count = spec_chain_path(s, g) ? std::max<uint32_t>(count, 1u) : std::max<uint32_t>(std::min(count, sp.grow), 1u);
+    // A full-pass loop (k_fullpass_svc) pays ~50 us to build its entries
+    // whatever the run length and ~4 us per placement: its runs start at 16.
+    const uint32_t grow = tg_full_scan(s, g) && !s->cfg.preempt ? std::max<uint32_t>(sp.grow, 16u) : sp.grow;
+    sp.grow = grow;   // (x4 from here while the runs get used up)
+    count = spec_chain_path(s, g) ? std::max<uint32_t>(count, 1u) : std::max<uint32_t>(std::min(count, grow), 1u);
     // (with AllocMetric on, spec_metrics counts a row's earlier placements in 16 bits)
     count = std::min<uint32_t>(count, s->metrics_on ? 0xFFFFu : 1u << 16);
     // With preemption enabled the run is selectNextOption's loop (generic_sched.go:

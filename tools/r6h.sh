@@ -12,3 +12,4 @@ timeout -k 10 120 python tools/c3_full_prof.py > gpurun_out/r6h/svc$k.txt 2>&1 &
 PE_FULL_SVC=0 timeout -k 10 120 python tools/c3_full_prof.py > gpurun_out/r6h/lds$k.txt 2>&1 || exit 1
 done
 for f in gpurun_out/r6h/svc*.txt gpurun_out/r6h/lds*.txt; do echo $f; tail -2 $f; done
+timeout -k 10 300 python tools/c3_dropin_probe.py > gpurun_out/r6h/dropin.txt 2>&1; tail -5 gpurun_out/r6h/dropin.txt

@@ -1,3 +1,7 @@
+#!/bin/bash
 mkdir -p gpurun_out/r6i
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_metrics.py tests/test_system_dropin.py tests/test_abi.py > gpurun_out/r6i/t.log 2>&1 ; \
-PE_METRICS_PROF=1 timeout -k 10 400 python bench.py --steps 10 --warmup 2 --sweep-nodes 0 --sections c4_drop_in > gpurun_out/r6i/b.json 2> gpurun_out/r6i/b.err
+timeout -k 10 120 python tools/c3_full_prof.py > gpurun_out/r6i/svc.txt 2>&1 && \
+PE_API_PROF=1 timeout -k 10 300 python tools/c3_dropin_probe.py > gpurun_out/r6i/dropin.txt 2>&1
+rc=$?
+tail -2 gpurun_out/r6i/svc.txt; cat gpurun_out/r6i/dropin.txt | tail -45
+exit $rc
