@@ -1,3 +1,11 @@
+#!/bin/bash
+# same-box A/B of the C1 section: the session's start (9caa00e) vs now
 mkdir -p gpurun_out/r6l
-PE_API_PROF=1 timeout -k 10 120 python tools/c4_probe.py > gpurun_out/r6l/p.txt 2>&1 && \
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_system_dropin.py tests/test_shard.py tests/test_full_size.py tests/test_metrics.py -k "system or c4 or shard" > gpurun_out/r6l/t.log 2>&1
+for k in 1 2 3; do
+  PE_ENGINE_LIB=$PWD/abold/libnomadpe_9caa00e.so timeout -k 10 200 python bench.py --no-cpu --sections c1 > gpurun_out/r6l/old$k.json 2>/dev/null || exit 1
+  timeout -k 10 200 python bench.py --no-cpu --sections c1 > gpurun_out/r6l/new$k.json 2>/dev/null || exit 1
+done
+for f in gpurun_out/r6l/*.json; do python3 -c "
+import json,sys
+l=[x for x in open('$f') if x.startswith('{')][-1]; d=json.loads(l)
+print('$f', d['configs']['c1']['ms_per_eval'], d['ms_per_step'])"; done
