@@ -477,7 +477,7 @@ def section_c4(device, rank, world, pg, cpu_s):
     st = SystemStack(device=device)
     st.SetStateColumnar(cs)
     times, kms, placed = [], [], 0
-    for i in range(4):
+    for i in range(64):   # a ~0.1 ms call: enough repetitions for a stable median
         st.ResetPlan()
         st.SetJob(job)
         barrier(pg)
@@ -492,7 +492,8 @@ def section_c4(device, rank, world, pg, cpu_s):
     wall = float(np.median(times[1:]))
     out = {"workload": "C4: mock.SystemJob on %d nodes, %d contiguous shards (one per GPU)" % (n, world),
            "scaling": "strong", "placed": total, "nodes_per_s": n / wall, "wall_ms": wall * 1e3,
-           "kernel_ms_rank0": float(np.median(kms[1:]))}
+           "wall_ms_p10_p90": [float(np.percentile(times[1:], 10)) * 1e3, float(np.percentile(times[1:], 90)) * 1e3],
+           "calls": len(times) - 1, "kernel_ms_rank0": float(np.median(kms[1:]))}
     if cpu_s > 0 and rank == 0:
         from oracle.oracle import OracleSystemStack
         o = OracleSystemStack()
