@@ -737,6 +737,14 @@ struct pe_stack {
     // EvalEligibility memo, per task-group name: class -> -1 undecided / 0 / 1
     std::map<uint32_t, std::vector<int8_t>> tg_memo;
     std::vector<int8_t> job_memo;
+    // Per-class checker results of earlier SetJobs on this node table: the
+    // job's constraints, a task group's checkers (per signature) and its node
+    // affinities are pure functions of the node attributes, so a job set
+    // again (every evaluation of the same job) reuses them (cls_cache_*).
+    uint64_t cc_gen = 0;
+    std::unordered_map<std::string, std::vector<int8_t>> cc_job;
+    std::unordered_map<std::string, std::vector<uint8_t>> cc_sig;
+    std::unordered_map<std::string, std::vector<double>> cc_aff;
 
     // AllocMetric maps (pe_set_metrics): the memo as the reference chain has
     // seen it so far (classes become known only when one of their nodes is
@@ -3581,23 +3589,75 @@ int build_psets(pe_stack* s, TgPlan& g) {
     return PE_OK;
 }
 
+// The checker caches hold for one node table (nodes_gen); a handful of
+// distinct jobs at most.
+static void cls_cache_sync(pe_stack* s) {
+    if (s->cc_gen == s->nodes_gen && s->cc_job.size() + s->cc_sig.size() + s->cc_aff.size() < 96) return;
+    s->cc_gen = s->nodes_gen;
+    s->cc_job.clear();
+    s->cc_sig.clear();
+    s->cc_aff.clear();
+}
+
+// The inputs of job_fail: the job constraints (Constraint.String() holds all
+// three fields).
+static std::string job_checker_key(const pe_stack* s) {
+    std::string k;
+    for (auto& c : s->job_constraints) { k += c.text; k += '\x1f'; }
+    return k;
+}
+
+// The inputs of tg_fail (drivers, constraints, host volumes, network mode,
+// port host network), or "" when not cached (device requests).
+static std::string tg_checker_key(const pe_stack* s, const TgPlan& g) {
+    if (!g.dev_reqs.empty()) return std::string();
+    std::string k = "D";
+    for (uint32_t d : g.drivers) { k += s->S(d); k += '\x1f'; }
+    k += "C";
+    for (auto& c : g.constraints) { k += c.text; k += '\x1f'; }
+    k += "V";
+    for (auto& v : g.volumes) { k += s->S(v.first); k += v.second ? "+ro\x1f" : "+rw\x1f"; }
+    k += "N";
+    k += s->S(g.net_mode);
+    k += '\x1f';
+    k += g.net_ports > 0 ? "P" + s->S(g.net_host) : std::string("-");
+    return k;
+}
+
 // Task-group checker verdict per signature and, per class, whether every
 // signature of the class agrees ("uniform": the memo outcome does not depend
 // on which member is visited first).
 void classify_classes(pe_stack* s, TgPlan& g, pe::ConstraintEvaluator& ev) {
     if (!g.sig_tg.empty()) return;
-    g.sig_tg.assign(s->sig_rep.size(), 0);
-    for (size_t sg = 0; sg < s->sig_rep.size(); sg++)
-        g.sig_tg[sg] = tg_feasible(s, ev, g, s->view(s->sig_rep[sg])) ? 1 : 0;
+    cls_cache_sync(s);
+    const std::string tk = tg_checker_key(s, g);
+    auto ct = tk.empty() ? s->cc_sig.end() : s->cc_sig.find(tk);
+    if (ct != s->cc_sig.end() && ct->second.size() == s->sig_rep.size()) {
+        g.sig_tg = ct->second;
+    } else {
+        g.sig_tg.assign(s->sig_rep.size(), 0);
+        for (size_t sg = 0; sg < s->sig_rep.size(); sg++)
+            g.sig_tg[sg] = tg_feasible(s, ev, g, s->view(s->sig_rep[sg])) ? 1 : 0;
+        if (!tk.empty()) s->cc_sig[tk] = g.sig_tg;
+    }
     g.class_uniform.assign(s->ncls, 1);
     g.class_verdict.assign(s->ncls, 0);
     if (s->job_memo.size() != s->ncls) s->job_memo.assign(s->ncls, -1);
+    if (!s->job_escaped) {   // job_feasible per class, from the cache when the job was set before
+        const std::string jk = job_checker_key(s);
+        auto cj = s->cc_job.find(jk);
+        if (cj == s->cc_job.end() || cj->second.size() != s->ncls) {
+            std::vector<int8_t> v(s->ncls);
+            for (uint32_t c = 0; c < s->ncls; c++) v[c] = job_feasible(s, ev, s->view(s->class_rep[c])) ? 1 : 0;
+            cj = s->cc_job.insert_or_assign(jk, std::move(v)).first;
+        }
+        for (uint32_t c = 0; c < s->ncls; c++)
+            if (s->job_memo[c] == -1) s->job_memo[c] = cj->second[c];
+    }
     for (uint32_t c = 0; c < s->ncls; c++) {
         const auto& sigs = s->class_sigs[c];
         g.class_verdict[c] = sigs.empty() ? 0 : g.sig_tg[sigs[0]];   // a class left without members: no node reads it
         for (uint32_t sg : sigs) if (g.sig_tg[sg] != g.class_verdict[c]) g.class_uniform[c] = 0;
-        if (!s->job_escaped && s->job_memo[c] == -1)
-            s->job_memo[c] = job_feasible(s, ev, s->view(s->class_rep[c])) ? 1 : 0;
     }
     g.nonuniform.clear();
     for (uint32_t c = 0; c < s->ncls; c++) if (!g.class_uniform[c]) g.nonuniform.push_back(c);
@@ -3737,8 +3797,16 @@ int build_tables(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uin
             g.h_aff_node = std::move(na);
             g.h_aff_class.clear();
         } else {
-            std::vector<double> ca(s->ncls);
-            for (uint32_t c = 0; c < s->ncls; c++) ca[c] = score(s->view(s->class_rep[c]));
+            std::string ak;   // the affinities' texts and weights: the per-class scores' inputs
+            for (auto& a : g.affinities) { ak += a.c.text; ak += '\x1f'; ak += std::to_string(a.weight); ak += '\x1f'; }
+            cls_cache_sync(s);
+            auto ct = s->cc_aff.find(ak);
+            if (ct == s->cc_aff.end() || ct->second.size() != s->ncls) {
+                std::vector<double> v(s->ncls);
+                for (uint32_t c = 0; c < s->ncls; c++) v[c] = score(s->view(s->class_rep[c]));
+                ct = s->cc_aff.insert_or_assign(ak, std::move(v)).first;
+            }
+            std::vector<double> ca = ct->second;
             HIP_TRY(s, upload_s(s, g.class_aff, ca));
             g.h_aff_class = std::move(ca);
             g.h_aff_node.clear();
