@@ -745,6 +745,8 @@ struct pe_stack {
     std::unordered_map<std::string, std::vector<int8_t>> cc_job;
     std::unordered_map<std::string, std::vector<uint8_t>> cc_sig;
     std::unordered_map<std::string, std::vector<double>> cc_aff;
+    // a spread target's values: interned value ids in first-seen class order, and per class
+    std::unordered_map<std::string, std::pair<std::vector<uint32_t>, std::vector<uint32_t>>> cc_val;
 
     // AllocMetric maps (pe_set_metrics): the memo as the reference chain has
     // seen it so far (classes become known only when one of their nodes is
@@ -3405,6 +3407,8 @@ std::vector<uint32_t> cleared_counts(pe_stack* s, size_t nvals, F node_val, bool
 }
 
 // Spread property sets for a task group (spread.go:76-104, propertyset.go).
+static void cls_cache_sync(pe_stack* s);
+
 int build_psets(pe_stack* s, TgPlan& g) {
     g.psets.clear();
     g.psets_dynamic = false;
@@ -3450,7 +3454,18 @@ int build_psets(pe_stack* s, TgPlan& g) {
             by_node.resize(n);
             for (size_t i = 0; i < n; i++) by_node[i] = value_of(s->view((uint32_t)i));
         } else {
-            for (uint32_t c = 0; c < s->ncls; c++) by_class[c] = value_of(s->view(s->class_rep[c]));
+            // the values per class, from the cache when the target was spread on before
+            const std::string vk = s->S(sp->attribute);
+            cls_cache_sync(s);
+            auto cv = s->cc_val.find(vk);
+            if (cv != s->cc_val.end() && cv->second.second.size() == s->ncls) {
+                ps->value_str = cv->second.first;
+                for (uint32_t i = 0; i < (uint32_t)ps->value_str.size(); i++) ps->value_index.emplace(ps->value_str[i], i);
+                by_class = cv->second.second;
+            } else {
+                for (uint32_t c = 0; c < s->ncls; c++) by_class[c] = value_of(s->view(s->class_rep[c]));
+                s->cc_val[vk] = std::make_pair(ps->value_str, by_class);
+            }
         }
         // existing allocs of this job and task group (populateExisting) + plan allocs
         auto node_val = [&](uint32_t row) {
@@ -3592,11 +3607,13 @@ int build_psets(pe_stack* s, TgPlan& g) {
 // The checker caches hold for one node table (nodes_gen); a handful of
 // distinct jobs at most.
 static void cls_cache_sync(pe_stack* s) {
-    if (s->cc_gen == s->nodes_gen && s->cc_job.size() + s->cc_sig.size() + s->cc_aff.size() < 96) return;
+    if (s->cc_gen == s->nodes_gen && s->cc_job.size() + s->cc_sig.size() + s->cc_aff.size() + s->cc_val.size() < 96)
+        return;
     s->cc_gen = s->nodes_gen;
     s->cc_job.clear();
     s->cc_sig.clear();
     s->cc_aff.clear();
+    s->cc_val.clear();
 }
 
 // The inputs of job_fail: the job constraints (Constraint.String() holds all
