@@ -140,7 +140,7 @@ hipError_t pe_launch_scatter_rows(void* dst, uint32_t words, const void* payload
 hipError_t pe_launch_counts(const pe::CountDsts* d, uint32_t nd, uint32_t n, const uint2* ents, uint32_t m,
                             const pe::ResetArgs* r, hipStream_t st);
 size_t pe_fullpass_lds_bytes(uint32_t n);
-hipError_t pe_launch_fullpass_svc(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
+hipError_t pe_launch_fullpass_svc(const pe::SweepArgs* a_dev, int np, bool lean, const uint32_t* visit, uint32_t n,
                                   uint32_t count, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
                                   uint32_t count, pe_ranked_node* out, uint32_t* state, unsigned long long* prof,
@@ -7093,8 +7093,13 @@ static int sweep_count_loop(pe_stack* s, TgPlan& g, uint32_t tgi, uint32_t count
         if (const char* e = std::getenv("PE_FULL_SVC")) svc = svc && std::atoi(e) != 0;
         if (svc) {
             ApiScope prof_k_(s, "sweep.svc_kernel+sync");
-            HIP_TRY_STATE(s, pe_launch_fullpass_svc(s->d_full_args.as<pe::SweepArgs>(), np, s->d_visit.as<uint32_t>(), n,
-                                              count, s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
+            // the lean service evaluation: asks whose dk-dependent checks are AllocsFit's alone
+            bool lean = !A.ask.distinct_job && !A.ask.distinct_tg && A.ask.tg_dyn == 0 && !A.ask.has_task_net &&
+                        !A.tg.static_gate && !A.tg.task_gate && !A.tg.md;
+            if (const char* e = std::getenv("PE_SVC_LEAN")) lean = lean && std::atoi(e) != 0;
+            HIP_TRY_STATE(s, pe_launch_fullpass_svc(s->d_full_args.as<pe::SweepArgs>(), np, lean,
+                                              s->d_visit.as<uint32_t>(), n, count,
+                                              s->d_loop_out.as<pe_ranked_node>(), state, s->stream));
             HIP_TRY(s, hipMemcpyAsync(h_state, state, sizeof(h_state), hipMemcpyDeviceToHost, s->stream));
             HIP_TRY(s, hipStreamSynchronize(s->stream));
             svc = h_state[5] == 0;   // more options than its entries: nothing committed, the loop below

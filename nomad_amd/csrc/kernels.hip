@@ -3420,7 +3420,12 @@ constexpr int kSvcEntryLanes = kSvcEntryWaves * 64;
 constexpr int kSvcPer = 4;
 constexpr uint32_t kSvcCap = (uint32_t)kSvcEntryLanes * kSvcPer;   // 3840 options, 32 B of LDS each
 
-template <int NP>
+// LEAN (the host checks): no distinct_hosts, no network asks or static ports,
+// no devices, no reserved cores, no distinct_property, no multi-device record:
+// an option of the build stays feasible, and the service's evaluation with dk
+// placements added is AllocsFit's three comparisons and the scores
+// (status_loaded + score_head reduced to the branches such an ask takes).
+template <int NP, bool LEAN>
 __global__ void __launch_bounds__(kFullThreads) k_fullpass_svc(const SweepArgs* __restrict__ Ap, const uint32_t* visit,
                                                                uint32_t n, uint32_t count, pe_ranked_node* out,
                                                                uint32_t* state) {
@@ -3560,7 +3565,34 @@ __global__ void __launch_bounds__(kFullThreads) k_fullpass_svc(const SweepArgs* 
         double s;
         uint32_t kk;
         // both lanes take the parts-keeping path (lockstep, no divergence)
-        const int st = head(row, in, aux, lane == 0 ? 0u : 2u, lane == 0 ? o->scores : parts1, &s, &kk);
+        int st;
+        if (LEAN) {
+            const uint32_t dk = lane == 0 ? 0u : 2u;
+            const NodeRec& r = in.r;
+            const int64_t ucpu = r.used_cpu + (int64_t)(dk + 1) * A.ask.cpu;
+            const int64_t umem = r.used_mem + (int64_t)(dk + 1) * A.ask.mem;
+            const int64_t udisk = r.used_disk + (int64_t)(dk + 1) * A.ask.disk;
+            s = 0.0;
+            kk = 0;
+            if (r.cap_cpu < ucpu || r.cap_mem < umem || r.cap_disk < udisk) {   // AllocsFit
+                st = kExhausted;
+            } else {
+                ScoreIn si;
+                si.ccpu = r.cap_cpu;
+                si.cmem = r.cap_mem;
+                si.ucpu = ucpu;
+                si.umem = umem;
+                si.dev_aff = 0.0;
+                si.coll = in.coll_tg + dk;
+                si.penalty = A.penalty_bits ? (A.penalty_bits[row >> 5] >> (row & 31)) & 1u : 0u;
+                si.aff = aff_lds[aux & 255u];
+                si.spread = 0.0;
+                s = score_head<true>(A.ask, A.log10, si, lane == 0 ? o->scores : parts1, kk);
+                st = kOption;
+            }
+        } else {
+            st = head(row, in, aux, lane == 0 ? 0u : 2u, lane == 0 ? o->scores : parts1, &s, &kk);
+        }
         if (lane == 1) {
             next_sum[e] = s;
             next_meta[e] = (uint32_t)st | (kk << 2) | (aux & 0x00FFFF00u);
@@ -4413,33 +4445,35 @@ hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint
 size_t pe_fullpass_svc_bytes() { return (size_t)pe::kSvcCap * (2 * sizeof(double) + 4 * sizeof(uint32_t)); }
 uint32_t pe_fullpass_svc_cap() { return pe::kSvcCap; }
 
-hipError_t pe_launch_fullpass_svc(const pe::SweepArgs* a_dev, int np, const uint32_t* visit, uint32_t n,
+hipError_t pe_launch_fullpass_svc(const pe::SweepArgs* a_dev, int np, bool lean, const uint32_t* visit, uint32_t n,
                                   uint32_t count, pe_ranked_node* out, uint32_t* state, hipStream_t st) {
     const size_t lds = pe_fullpass_svc_bytes();
     static bool attr = false;
     if (!attr) {
-        for (const void* f : {reinterpret_cast<const void*>(&pe::k_fullpass_svc<0>),
-                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<1>),
-                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<2>)}) {
+        for (const void* f : {reinterpret_cast<const void*>(&pe::k_fullpass_svc<0, false>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<1, false>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<2, false>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<0, true>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<1, true>),
+                              reinterpret_cast<const void*>(&pe::k_fullpass_svc<2, true>)}) {
             const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
         attr = true;
     }
-    switch (np) {
-        case 0:
-            hipLaunchKernelGGL(pe::k_fullpass_svc<0>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
-                               out, state);
-            break;
-        case 1:
-            hipLaunchKernelGGL(pe::k_fullpass_svc<1>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
-                               out, state);
-            break;
-        default:
-            hipLaunchKernelGGL(pe::k_fullpass_svc<2>, dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count,
-                               out, state);
-            break;
+#define PE_SVC_LAUNCH(NPV, L)                                                                                         \
+    hipLaunchKernelGGL((pe::k_fullpass_svc<NPV, L>), dim3(1), dim3(pe::kFullThreads), lds, st, a_dev, visit, n, count, \
+                       out, state)
+    if (lean) {
+        if (np == 0) PE_SVC_LAUNCH(0, true);
+        else if (np == 1) PE_SVC_LAUNCH(1, true);
+        else PE_SVC_LAUNCH(2, true);
+    } else {
+        if (np == 0) PE_SVC_LAUNCH(0, false);
+        else if (np == 1) PE_SVC_LAUNCH(1, false);
+        else PE_SVC_LAUNCH(2, false);
     }
+#undef PE_SVC_LAUNCH
     return hipGetLastError();
 }
 
