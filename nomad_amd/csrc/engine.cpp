@@ -7670,8 +7670,9 @@ static int spec_start(pe_stack* s, uint32_t tgi, pe_ranked_node* out) {
     // other loop pays per placement: start with one and double while the runs
     // get used up (spec_flush).
     // A full-pass loop (k_fullpass_svc) pays ~50 us to build its entries
-    // whatever the run length and ~4 us per placement: its runs start at 16.
-    const uint32_t grow = tg_full_scan(s, g) && !s->cfg.preempt ? std::max<uint32_t>(sp.grow, 16u) : sp.grow;
+    // and ~0.1 ms of launch and host work per run whatever its length, and
+    // ~3.5 us per placement: its runs start at 64.
+    const uint32_t grow = tg_full_scan(s, g) && !s->cfg.preempt ? std::max<uint32_t>(sp.grow, 64u) : sp.grow;
     sp.grow = grow;   // (x4 from here while the runs get used up)
     count = spec_chain_path(s, g) ? std::max<uint32_t>(count, 1u) : std::max<uint32_t>(std::min(count, grow), 1u);
     // (with AllocMetric on, spec_metrics counts a row's earlier placements in 16 bits)

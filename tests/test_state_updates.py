@@ -247,3 +247,41 @@ def test_update_nodes_many_rounds_lists_move_and_compact():
         got = st.Place(0, 60)
         _, _, want = run_place(OracleGenericStack, cur, allocs, job, perm)
         assert_same_placements(got, want)
+
+
+@pytest.mark.gpu
+def test_checker_caches_across_jobs():
+    """The engine reuses per-class checker results of earlier SetJobs on the
+    same node table (job constraints, task-group checkers, node affinities,
+    spread values). Jobs that differ in one constraint, in an
+    affinity weight or in the spread target, set in turn on one stack, each
+    place exactly as a fresh oracle does; a node update in between drops the
+    caches."""
+    from nomad_amd.stack import GenericStack
+    from nomad_amd.structs import Affinity, Constraint, Spread, SpreadTarget
+    nodes, allocs = synth.cluster_c3(1500, seed=41)
+    a = synth.job_c3(60)
+    b = copy.deepcopy(a)
+    b.id = "svc-b"
+    b.constraints[2] = Constraint("${meta.rack}", "^r[5-9]", "regexp")
+    c = copy.deepcopy(a)
+    c.id = "svc-c"
+    c.affinities = [Affinity("${node.class}", "c3", "=", 80)]
+    d = copy.deepcopy(a)
+    d.id = "svc-d"
+    d.spreads = [Spread("${attr.os.version}", 100, [SpreadTarget("5.4.0", 40), SpreadTarget("5.10.12", 40)])]
+    st = GenericStack()
+    st.SetState(nodes, allocs)
+    state = nodes
+    for k, job in enumerate([a, b, a, c, d, a, "update", b, a]):
+        if job == "update":
+            changed, index, state = _node_delta(state, 9, n_changed=80, n_new=5)
+            st.UpdateNodes(changed, index)
+            continue
+        st.ResetPlan()
+        st.SetJob(job)
+        perm = synth.shuffle(len(state), 20 + k)
+        st.SetNodes(list(perm))
+        got = st.Place(0, job.task_groups[0].count)
+        _, _, want = run_place(OracleGenericStack, state, allocs, job, perm)
+        assert_same_placements(got, want)
