@@ -712,6 +712,10 @@ struct pe_stack {
     // per row for the metrics walk: the job checkers' FilterNode reason,
     // kJfPass, or null (not yet run); and the row's dense class
     std::vector<const char*> jf;
+    // the job constraints jf was filled for (job_checker_key) and their texts,
+    // which the jf entries point into: SetJob keeps jf while they are the same
+    std::string jf_key;
+    std::vector<std::string> jf_texts;
     std::vector<uint32_t> jf_cls;
     std::vector<uint32_t> trace_dk;   // spec_metrics: per row, the earlier records' placements (zero between uses)
     std::vector<ParsedAffinity> job_affinities;
@@ -832,8 +836,8 @@ struct pe_stack {
     DevMem d_sys_res;                     // k_system_rows outcomes by row
     uint64_t test_fallback_every = 0, test_select_calls = 0;   // PE_TEST_FALLBACK_EVERY
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
-    PinnedMem h_trace_codes, h_trace_top;   // spec_metrics: the batched trace's outcomes and ScoreMetaData
-    DevMem d_trace_rec_end, d_trace_top;
+    PinnedMem h_trace_top;   // spec_metrics: the batched trace's ScoreMetaData and outcome codes
+    DevMem d_trace_top;
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
     DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;
     DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)
@@ -888,7 +892,6 @@ struct pe_stack {
     // evaluated PE_NONE when the placement took no retry)
     std::vector<std::array<uint32_t, 4>>* nil_sink = nullptr;
     DevMem d_ploop_nil;
-    DevMem d_trace_dk;                 // spec_metrics: per traced row, the earlier records' placements
     DevMem ck_preempted, ck_pcount, ck_core_used;
     std::vector<pe::EmitRec>* emit_sink = nullptr;   // run_place: keep chain records compact here
     bool emit_sunk = false;                          // ... and it did
@@ -1413,8 +1416,13 @@ static void jf_ready(pe_stack* s) {
 const char* job_fail_cached(pe_stack* s, pe::ConstraintEvaluator& ev, uint32_t row) {
     const char* w = s->jf[row];
     if (!w) {
-        w = job_fail(s, ev, s->view(row));
-        if (!w) w = kJfPass;
+        w = kJfPass;
+        const NodeView n = s->view(row);
+        for (size_t k = 0; k < s->job_constraints.size(); k++)
+            if (!meets(s, ev, s->job_constraints[k], n)) {
+                w = s->jf_texts[k].c_str();   // the same text, kept across SetJob
+                break;
+            }
         s->jf[row] = w;
     }
     return w == kJfPass ? nullptr : w;
@@ -5301,11 +5309,20 @@ static int set_job_one(pe_stack* s, const pe_strtab* strs, const pe_job* j) {
     s->job_ns = j->ns;
     s->job_priority = j->priority;
     s->job_constraints.clear();
-    s->jf.clear();
     s->job_escaped = false;
     for (uint32_t i = 0; i < j->constraint_count; i++) {
         s->job_constraints.push_back(parse_constraint(s, j->constraints[j->constraint_off + i]));
         s->job_escaped = s->job_escaped || s->job_constraints.back().escapes;
+    }
+    {   // the per-row job checker outcomes hold for the same constraints (and
+        // node table: SetState / UpdateNodes clear them)
+        std::string key = job_checker_key(s);
+        if (key != s->jf_key) {
+            s->jf.clear();
+            s->jf_key = std::move(key);
+            s->jf_texts.clear();
+            for (auto& c : s->job_constraints) s->jf_texts.push_back(c.text);
+        }
     }
     bool job_distinct_hosts = false;
     for (auto& c : s->job_constraints) {
@@ -6196,13 +6213,12 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     rows.reserve(16 * (size_t)sp.n_rec);
     dks.reserve(16 * (size_t)sp.n_rec);
     uint32_t off = off0;
-    double t_walks = 0.0;
+    uint64_t walked = 0;
     for (uint32_t k = 0; k < sp.n_rec; k++) {
         const uint32_t ev = sp.compact ? sp.crecs[k].nodes_evaluated : sp.recs[k].nodes_evaluated;
+        walked += ev;
         const size_t r0 = rows.size();
-        const double tw = prof ? now_us() : 0.0;
         metrics_walk(s, g, order, off, ev, acc[k], rows, &sp.memo_log);
-        if (prof) t_walks += now_us() - tw;
         sp.memo_off.push_back((uint32_t)sp.memo_log.size());
         for (size_t i = r0; i < rows.size(); i++) dks.push_back((uint16_t)placed_on[rows[i]]);
         rec_end[k] = (uint32_t)rows.size();
@@ -6215,45 +6231,49 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         if (row >= 0) placed_on[(uint32_t)row] = 0;
     }
     const double t1 = prof ? now_us() : 0.0;
-    // the outcome codes and every record's ScoreMetaData (k_trace_top) land in
-    // pinned host buffers kept across runs; the score values stay on the device
-    HIP_TRY(s, s->h_trace_codes.ensure(std::max<size_t>(rows.size(), 1) * sizeof(uint32_t)));
-    HIP_TRY(s, s->h_trace_top.ensure(std::max<size_t>(sp.n_rec, 1) * (5 * sizeof(pe_metric_score) + 1)));
-    const uint32_t* codes = s->h_trace_codes.as<uint32_t>();
+    // one upload (the traced rows, the records' ends, the rows' dk) and one
+    // download (every record's ScoreMetaData from k_trace_top, its count, the
+    // outcome codes) through buffers kept across runs; the score values stay
+    // on the device
+    const size_t n_rows = rows.size();
+    const size_t top_bytes = 5 * sizeof(pe_metric_score) * (size_t)sp.n_rec;
+    const size_t codes_at = (top_bytes + sp.n_rec + 15) & ~size_t(15);
+    HIP_TRY(s, s->h_trace_top.ensure(codes_at + std::max<size_t>(n_rows, 1) * sizeof(uint32_t)));
     const pe_metric_score* top = s->h_trace_top.as<pe_metric_score>();
-    const uint8_t* n_top = reinterpret_cast<const uint8_t*>(top + 5 * (size_t)sp.n_rec);
+    const uint8_t* n_top = s->h_trace_top.as<uint8_t>() + top_bytes;
+    const uint32_t* codes = reinterpret_cast<const uint32_t*>(s->h_trace_top.as<uint8_t>() + codes_at);
     pe::Ask a = ask_for(s, g);
-    if (!rows.empty()) {
+    if (n_rows) {
+        rows.insert(rows.end(), rec_end.begin(), rec_end.end());
+        const size_t dk_at = rows.size();
+        rows.resize(dk_at + (n_rows + 1) / 2, 0u);
+        std::memcpy(rows.data() + dk_at, dks.data(), n_rows * sizeof(uint16_t));
         HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
-        HIP_TRY(s, upload_s(s, s->d_trace_dk, dks));
-        HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
-        HIP_TRY(s, s->d_trace_scores.ensure(rows.size() * 6 * sizeof(double)));
+        const uint32_t* d_rows = s->d_trace_rows.as<uint32_t>();
+        HIP_TRY(s, s->d_trace_scores.ensure(n_rows * 6 * sizeof(double)));
+        HIP_TRY(s, s->d_trace_top.ensure(codes_at + n_rows * sizeof(uint32_t)));
+        uint32_t* d_codes = reinterpret_cast<uint32_t*>(s->d_trace_top.as<uint8_t>() + codes_at);
         pe::NodeSoA soa = soa_of(s);   // the run's starting state: the checkpoint
         pe::TgTables t = tables_of(g);
         soa.rec = s->ck_rec.as<pe::NodeRec>();
         soa.coll_job = s->ck_coll_job.as<uint32_t>();
         t.coll_tg = s->ck_coll_tg.as<uint32_t>();
         if (t.dev_free) t.dev_free = s->ck_dev_free.as<uint32_t>();
-        HIP_TRY_STATE(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
-                                         s->d_trace_out.as<uint32_t>(), nullptr, s->log10, nullptr,
-                                         s->d_trace_scores.as<double>(), s->stream, s->d_trace_dk.as<uint16_t>()));
-        const size_t top_bytes = 5 * sizeof(pe_metric_score) * (size_t)sp.n_rec;
-        HIP_TRY(s, upload_s(s, s->d_trace_rec_end, rec_end));
-        HIP_TRY(s, s->d_trace_top.ensure(top_bytes + sp.n_rec));
+        HIP_TRY_STATE(s, pe_launch_trace(&soa, &t, &a, d_rows, (uint32_t)n_rows, d_codes, nullptr, s->log10, nullptr,
+                                         s->d_trace_scores.as<double>(), s->stream,
+                                         reinterpret_cast<const uint16_t*>(d_rows + dk_at)));
         const uint32_t flags = (a.dev_tw != 0.0 ? 1u : 0u) | (a.anti_aff ? 2u : 0u) |
                                (!g.affinities.empty() ? 4u : 0u) |
                                (s->cfg.stack_kind == PE_STACK_GENERIC ? 8u : 0u);
-        HIP_TRY_STATE(s, pe_launch_trace_top(s->d_trace_out.as<uint32_t>(), s->d_trace_scores.as<double>(),
-                                             s->d_trace_rows.as<uint32_t>(), s->d_trace_rec_end.as<uint32_t>(),
+        HIP_TRY_STATE(s, pe_launch_trace_top(d_codes, s->d_trace_scores.as<double>(), d_rows, d_rows + n_rows,
                                              sp.n_rec, flags, s->d_trace_top.as<pe_metric_score>(),
                                              s->d_trace_top.as<uint8_t>() + top_bytes, s->stream));
-        HIP_TRY(s, hipMemcpyAsync(s->h_trace_codes.p, s->d_trace_out.p, rows.size() * 4, hipMemcpyDeviceToHost,
-                                  s->stream));
-        HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.p, s->d_trace_top.p, top_bytes + sp.n_rec, hipMemcpyDeviceToHost,
-                                  s->stream));
+        HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.p, s->d_trace_top.p, codes_at + n_rows * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
+        rows.resize(n_rows);
     } else {
-        std::memset(s->h_trace_top.as<uint8_t>() + 5 * sizeof(pe_metric_score) * (size_t)sp.n_rec, 0, sp.n_rec);
+        std::memset(s->h_trace_top.as<uint8_t>() + top_bytes, 0, sp.n_rec);
     }
     const double t2 = prof ? now_us() : 0.0;
     spec_metrics_reset(sp);
@@ -6275,9 +6295,9 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     }
     sp.metrics = true;
     if (prof)
-        std::fprintf(stderr, "spec_metrics: %u records, %zu traced rows: walk %.1f us (in metrics_walk %.1f us), "
-                             "trace %.1f us, maps %.1f us (%zu counts, %zu scores)\n", sp.n_rec, rows.size(), t1 - t0,
-                     t_walks, t2 - t1, now_us() - t2, sp.mcounts.size(), sp.mscores.size());
+        std::fprintf(stderr, "spec_metrics: %u records, %llu walked, %zu traced rows: walk %.1f us, trace %.1f us, "
+                             "maps %.1f us (%zu counts, %zu scores)\n", sp.n_rec,
+                     (unsigned long long)walked, n_rows, t1 - t0, t2 - t1, now_us() - t2, sp.mcounts.size(), sp.mscores.size());
     return PE_OK;
 }
 

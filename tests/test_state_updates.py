@@ -285,3 +285,45 @@ def test_checker_caches_across_jobs():
         got = st.Place(0, job.task_groups[0].count)
         _, _, want = run_place(OracleGenericStack, state, allocs, job, perm)
         assert_same_placements(got, want)
+
+
+@pytest.mark.gpu
+def test_job_checker_rows_across_jobs_metrics():
+    """The per-row job checker outcomes (the FilterNode reasons of
+    FeasibilityWrapper's job checkers, feasible.go:1086-1097) are kept across
+    evaluations of jobs with the same constraints and dropped when a
+    constraint text or the node table changes: every Select's AllocMetric maps
+    equal a fresh oracle's, jobs set in turn on one stack."""
+    from nomad_amd.stack import GenericStack
+    from nomad_amd.structs import Constraint
+    nodes, allocs = synth.cluster_c3(1200, seed=43)
+    a = synth.job_c3(40)
+    b = copy.deepcopy(a)
+    b.id = "svc-b"
+    b.constraints[2] = Constraint("${meta.rack}", "^r[5-9]", "regexp")
+    st = GenericStack()
+    st.SetState(nodes, allocs)
+    st.EnableMetrics(True)
+    state = nodes
+    for k, job in enumerate([a, a, b, a, "update", a, b]):
+        if job == "update":
+            changed, index, state = _node_delta(state, 5, n_changed=120, n_new=4)
+            st.UpdateNodes(changed, index)
+            continue
+        st.ResetPlan()
+        st.SetJob(job)
+        perm = list(synth.shuffle(len(state), 60 + k))
+        st.SetNodes(perm)
+        o = OracleGenericStack()
+        o.SetState(state, allocs)
+        o.SetJob(job)
+        o.SetNodes(perm)
+        o.EnableMetrics(True)
+        for _ in range(25):
+            ro, re = o.SelectRaw(0), st.SelectRaw(0)
+            assert_same_placements([re], [ro])
+            assert st.LastMetrics() == o.LastMetrics()
+            if ro.row < 0:
+                break
+            o.Commit(0, ro.row)
+            st.Commit(0, ro.row)
