@@ -147,8 +147,8 @@ hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint
                                   hipStream_t st);
 hipError_t pe_launch_sweep_only(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t pe_launch_sweep_local(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
-hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const uint32_t* rows, const uint32_t* rec_end,
-                               uint32_t n_rec, uint32_t flags, pe_metric_score* out, uint8_t* n_out, hipStream_t st);
+hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const pe::TraceSrc* src, uint32_t flags,
+                               pe_metric_score* out, uint8_t* n_out, hipStream_t st);
 hipError_t pe_launch_step_only(const pe::SweepArgs* a, uint32_t nrecs, const uint32_t* visit, uint32_t n,
                                uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_commit_rows(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
@@ -213,6 +213,11 @@ hipError_t pe_launch_sweep_loop(const pe::SweepArgs* a, uint32_t blocks, uint32_
 hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
                            uint32_t n, uint32_t* out, const uint32_t* penalty_bits, double log10,
                            const double* spread_tab, double* scores, hipStream_t st, const uint16_t* dks = nullptr);
+hipError_t pe_launch_trace_batch(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a,
+                                 const pe::TraceSrc* src, uint32_t n, uint32_t* out, double log10,
+                                 const double* spread_tab, double* scores, hipStream_t st);
+hipError_t pe_launch_spread_tables(const pe::TgTables* t, uint32_t n_rec, uint32_t* delta, double* tab,
+                                   hipStream_t st);
 
 namespace {
 
@@ -717,7 +722,6 @@ struct pe_stack {
     std::string jf_key;
     std::vector<std::string> jf_texts;
     std::vector<uint32_t> jf_cls;
-    std::vector<uint32_t> trace_dk;   // spec_metrics: per row, the earlier records' placements (zero between uses)
     std::vector<ParsedAffinity> job_affinities;
     std::vector<SpreadSpec> job_spreads;
     std::vector<std::unique_ptr<TgPlan>> tgs;
@@ -838,6 +842,7 @@ struct pe_stack {
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     PinnedMem h_trace_top;   // spec_metrics: the batched trace's ScoreMetaData and outcome codes
     DevMem d_trace_top;
+    DevMem d_trace_delta, d_trace_tabs;   // spec_metrics: per record spread use counts and boost tables
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
     DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;
     DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)
@@ -3521,6 +3526,8 @@ int build_psets(pe_stack* s, TgPlan& g) {
         ps->weight_frac = (double)(int8_t)si->weight / (double)s->sum_spread_weights;
         HIP_TRY(s, upload_s(s, ps->val_class, by_class));
         if (ps->per_node) HIP_TRY(s, upload_s(s, ps->val_node, by_node));
+        ps->h_val_class = std::move(by_class);   // host copies (the batched metrics trace's counts)
+        ps->h_val_node = std::move(by_node);
         std::vector<uint32_t> cnt = ps->h_counts;
         if (cnt.empty()) cnt.push_back(0);
         HIP_TRY(s, upload_s(s, ps->counts, cnt));
@@ -6188,8 +6195,11 @@ static void spec_metrics_push(pe_stack::Spec& sp, MetricAcc& acc) {
 // its window is walked on the host in record order (the FeasibilityWrapper
 // half, with the reference memo), and every row that passes is traced in one
 // k_trace launch against the checkpoint of the starting state, with dk = the
-// earlier records' placements on the row. Windowed runs without property sets
-// and without evictions only (their state differs by placements alone).
+// earlier records' placements on the row and each record's spread boosts from
+// its own use counts (k_spread_tables). Whole-list windows (full passes) whose
+// walk no longer changes the memo are one cached list, rotated per record on
+// the device (TraceSrc). Runs without evictions and distinct_property sets only
+// (their state differs by placements alone; spec_metrics_batched).
 static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     static const bool prof = std::getenv("PE_METRICS_PROF") != nullptr;
     const double t0 = prof ? now_us() : 0.0;
@@ -6206,36 +6216,65 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     static thread_local std::vector<MetricAcc> acc;
     if (acc.size() < sp.n_rec) acc.resize(sp.n_rec);
     for (uint32_t k = 0; k < sp.n_rec; k++) acc[k].reset();
-    std::vector<uint32_t> rows, rec_end(sp.n_rec);
-    std::vector<uint16_t> dks;
-    if (s->trace_dk.size() != s->nodes.size()) s->trace_dk.assign(s->nodes.size(), 0u);
-    uint32_t* placed_on = s->trace_dk.data();   // row -> placements of earlier records
-    rows.reserve(16 * (size_t)sp.n_rec);
-    dks.reserve(16 * (size_t)sp.n_rec);
-    uint32_t off = off0;
+    // record k's rows: walked on the host into xrows (rsrc[k] = their offset),
+    // or, once a whole-list walk no longer changes the memo, the cached walk's
+    // passing rows `list` rotated to the record's start (kTraceRot | index)
+    std::vector<uint32_t> xrows, rec_end(sp.n_rec), rsrc(sp.n_rec), list, lpos;
+    xrows.reserve(16 * (size_t)sp.n_rec);
+    bool list_live = false, list_done = false;   // one cached list per batch
+    uint32_t off = off0, n_entries = 0;
     uint64_t walked = 0;
+    const size_t m = order.size();
+    WalkCache wc;
     for (uint32_t k = 0; k < sp.n_rec; k++) {
         const uint32_t ev = sp.compact ? sp.crecs[k].nodes_evaluated : sp.recs[k].nodes_evaluated;
         walked += ev;
-        const size_t r0 = rows.size();
-        metrics_walk(s, g, order, off, ev, acc[k], rows, &sp.memo_log);
+        const bool whole = m && ev == m;
+        if (whole && wc.valid && list_live) {
+            acc[k].cf = wc.cf;
+            acc[k].kf = wc.kf;
+            const uint32_t st = (uint32_t)(off % m);
+            size_t s0 = (size_t)(std::lower_bound(lpos.begin(), lpos.end(), st) - lpos.begin());
+            if (s0 == lpos.size()) s0 = 0;
+            rsrc[k] = pe::kTraceRot | (uint32_t)s0;
+            n_entries += (uint32_t)list.size();
+        } else {
+            const size_t x0 = xrows.size(), l0 = sp.memo_log.size();
+            if (whole) wc.pass.assign(m, 0);
+            metrics_walk(s, g, order, off, ev, acc[k], xrows, &sp.memo_log, whole ? &wc.pass : nullptr);
+            wc.valid = whole && sp.memo_log.size() == l0;
+            list_live = false;
+            if (wc.valid && !list_done) {
+                wc.cf = acc[k].cf;
+                wc.kf = acc[k].kf;
+                for (uint32_t p = 0; p < m; p++)
+                    if (wc.pass[p]) {
+                        list.push_back(order[p]);
+                        lpos.push_back(p);
+                    }
+                list_done = list_live = true;
+            }
+            rsrc[k] = (uint32_t)x0;
+            n_entries += (uint32_t)(xrows.size() - x0);
+        }
+        if (xrows.size() >= (size_t)pe::kTraceRot) return s->fail(PE_EINTERNAL, "spec_metrics: trace rows overflow");
         sp.memo_off.push_back((uint32_t)sp.memo_log.size());
-        for (size_t i = r0; i < rows.size(); i++) dks.push_back((uint16_t)placed_on[rows[i]]);
-        rec_end[k] = (uint32_t)rows.size();
-        const int32_t row = spec_rec_row(sp, k);
-        if (row >= 0) placed_on[(uint32_t)row]++;
+        rec_end[k] = n_entries;
         off = sp.compact ? sp.crecs[k].new_offset : sp.recs[k].new_offset;
     }
-    for (uint32_t k = 0; k < sp.n_rec; k++) {   // back to zero for the next run
-        const int32_t row = spec_rec_row(sp, k);
-        if (row >= 0) placed_on[(uint32_t)row] = 0;
-    }
+    auto row_of = [&](uint32_t k, uint32_t j) -> uint32_t {   // trace_row on the host
+        const uint32_t src = rsrc[k];
+        if (!(src & pe::kTraceRot)) return xrows[src + j];
+        size_t p = (size_t)(src - pe::kTraceRot) + j;
+        if (p >= list.size()) p -= list.size();
+        return list[p];
+    };
     const double t1 = prof ? now_us() : 0.0;
-    // one upload (the traced rows, the records' ends, the rows' dk) and one
-    // download (every record's ScoreMetaData from k_trace_top, its count, the
-    // outcome codes) through buffers kept across runs; the score values stay
-    // on the device
-    const size_t n_rows = rows.size();
+    // one upload (walked rows, records' ends and sources, the cached list, the
+    // placements) and one download (every record's ScoreMetaData from
+    // k_trace_top, its count, the outcome codes) through buffers kept across
+    // runs; the score values stay on the device
+    const size_t n_rows = n_entries;
     const size_t top_bytes = 5 * sizeof(pe_metric_score) * (size_t)sp.n_rec;
     const size_t codes_at = (top_bytes + sp.n_rec + 15) & ~size_t(15);
     HIP_TRY(s, s->h_trace_top.ensure(codes_at + std::max<size_t>(n_rows, 1) * sizeof(uint32_t)));
@@ -6244,12 +6283,36 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     const uint32_t* codes = reinterpret_cast<const uint32_t*>(s->h_trace_top.as<uint8_t>() + codes_at);
     pe::Ask a = ask_for(s, g);
     if (n_rows) {
-        rows.insert(rows.end(), rec_end.begin(), rec_end.end());
-        const size_t dk_at = rows.size();
-        rows.resize(dk_at + (n_rows + 1) / 2, 0u);
-        std::memcpy(rows.data() + dk_at, dks.data(), n_rows * sizeof(uint16_t));
-        HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
-        const uint32_t* d_rows = s->d_trace_rows.as<uint32_t>();
+        std::vector<uint64_t> pl;   // (row, record) of the run's placements
+        for (uint32_t k = 0; k < sp.n_rec; k++) {
+            const int32_t row = spec_rec_row(sp, k);
+            if (row >= 0) pl.push_back((uint64_t)(uint32_t)row << 32 | k);
+        }
+        std::sort(pl.begin(), pl.end());
+        std::vector<uint32_t> in;
+        in.reserve(xrows.size() + 2 * (size_t)sp.n_rec + list.size() + 2 * pl.size() + 1);
+        in.insert(in.end(), xrows.begin(), xrows.end());
+        const size_t at_end = in.size();
+        in.insert(in.end(), rec_end.begin(), rec_end.end());
+        const size_t at_src = in.size();
+        in.insert(in.end(), rsrc.begin(), rsrc.end());
+        const size_t at_list = in.size();
+        in.insert(in.end(), list.begin(), list.end());
+        if (in.size() & 1) in.push_back(0u);
+        const size_t at_pl = in.size();
+        in.resize(at_pl + 2 * pl.size());
+        if (!pl.empty()) std::memcpy(in.data() + at_pl, pl.data(), pl.size() * sizeof(uint64_t));
+        HIP_TRY(s, upload_s(s, s->d_trace_rows, in));
+        const uint32_t* d_in = s->d_trace_rows.as<uint32_t>();
+        pe::TraceSrc src{};
+        src.rows = d_in;
+        src.rec_end = d_in + at_end;
+        src.rsrc = d_in + at_src;
+        src.list = d_in + at_list;
+        src.pl = reinterpret_cast<const uint64_t*>(d_in + at_pl);
+        src.n_rec = sp.n_rec;
+        src.n_list = (uint32_t)list.size();
+        src.n_pl = (uint32_t)pl.size();
         HIP_TRY(s, s->d_trace_scores.ensure(n_rows * 6 * sizeof(double)));
         HIP_TRY(s, s->d_trace_top.ensure(codes_at + n_rows * sizeof(uint32_t)));
         uint32_t* d_codes = reinterpret_cast<uint32_t*>(s->d_trace_top.as<uint8_t>() + codes_at);
@@ -6259,19 +6322,41 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
         soa.coll_job = s->ck_coll_job.as<uint32_t>();
         t.coll_tg = s->ck_coll_tg.as<uint32_t>();
         if (t.dev_free) t.dev_free = s->ck_dev_free.as<uint32_t>();
-        HIP_TRY_STATE(s, pe_launch_trace(&soa, &t, &a, d_rows, (uint32_t)n_rows, d_codes, nullptr, s->log10, nullptr,
-                                         s->d_trace_scores.as<double>(), s->stream,
-                                         reinterpret_cast<const uint16_t*>(d_rows + dk_at)));
+        const double* stab = nullptr;
+        if (t.n_spread > 0) {   // every record's boosts from its own use counts (k_spread_tables)
+            for (int p = 0; p < t.n_psets; p++) t.pset_counts[p] = s->ck_pset[p].as<uint32_t>();
+            const size_t nc = t.pset_cnt_total;
+            std::vector<uint32_t> delta((size_t)sp.n_rec * nc, 0u), cur(nc, 0u);
+            for (uint32_t k = 0; k < sp.n_rec; k++) {
+                std::copy(cur.begin(), cur.end(), delta.begin() + (size_t)k * nc);
+                const int32_t row = spec_rec_row(sp, k);
+                if (row < 0) continue;
+                for (int p = 0; p < t.n_psets; p++) {
+                    const PsetDev& ps = *g.psets[p];
+                    const uint32_t c = s->nodes[(uint32_t)row].cls;
+                    if (ps.per_node ? ps.h_val_node.size() <= (size_t)row : ps.h_val_class.size() <= c)
+                        return s->fail(PE_EINTERNAL, "spec_metrics: a spread set's host values are missing");
+                    const uint32_t v = ps.per_node ? ps.h_val_node[(uint32_t)row] : ps.h_val_class[c];
+                    if (v != pe::kMissing) cur[t.pset_cnt_off[p] + v]++;
+                }
+            }
+            HIP_TRY(s, upload_s(s, s->d_trace_delta, delta));
+            HIP_TRY(s, s->d_trace_tabs.ensure(sizeof(double) * (size_t)sp.n_rec * t.pset_tab_total));
+            HIP_TRY_STATE(s, pe_launch_spread_tables(&t, sp.n_rec, s->d_trace_delta.as<uint32_t>(),
+                                                     s->d_trace_tabs.as<double>(), s->stream));
+            stab = s->d_trace_tabs.as<double>();
+        }
+        HIP_TRY_STATE(s, pe_launch_trace_batch(&soa, &t, &a, &src, (uint32_t)n_rows, d_codes, s->log10, stab,
+                                               s->d_trace_scores.as<double>(), s->stream));
         const uint32_t flags = (a.dev_tw != 0.0 ? 1u : 0u) | (a.anti_aff ? 2u : 0u) |
                                (!g.affinities.empty() ? 4u : 0u) |
                                (s->cfg.stack_kind == PE_STACK_GENERIC ? 8u : 0u);
-        HIP_TRY_STATE(s, pe_launch_trace_top(d_codes, s->d_trace_scores.as<double>(), d_rows, d_rows + n_rows,
-                                             sp.n_rec, flags, s->d_trace_top.as<pe_metric_score>(),
+        HIP_TRY_STATE(s, pe_launch_trace_top(d_codes, s->d_trace_scores.as<double>(), &src, flags,
+                                             s->d_trace_top.as<pe_metric_score>(),
                                              s->d_trace_top.as<uint8_t>() + top_bytes, s->stream));
         HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.p, s->d_trace_top.p, codes_at + n_rows * sizeof(uint32_t),
                                   hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));
-        rows.resize(n_rows);
     } else {
         std::memset(s->h_trace_top.as<uint8_t>() + top_bytes, 0, sp.n_rec);
     }
@@ -6280,9 +6365,10 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     std::map<int, std::vector<uint32_t>> counts;
     size_t i = 0;
     for (uint32_t k = 0; k < sp.n_rec; k++) {
+        const size_t b = i;
         for (; i < rec_end[k]; i++) {   // the options' ScoreMetaData came from k_trace_top
             if ((codes[i] & 255u) == pe::kTrOption) continue;
-            const int rc = metrics_outcome(s, g, a, rows[i], codes[i], nullptr, acc[k], counts);
+            const int rc = metrics_outcome(s, g, a, row_of(k, (uint32_t)(i - b)), codes[i], nullptr, acc[k], counts);
             if (rc) return rc;
         }
         acc[k].cf.append(PE_METRIC_CLASS_FILTERED, sp.mcounts);
@@ -7471,11 +7557,21 @@ static bool spec_eligible(pe_stack* s, uint32_t tgi, const pe_select_options* op
 // Whether a run's maps come from one batched trace against the checkpoint
 // (windowed, no evictions, no property sets: a record's state differs from
 // the run's start by earlier placements alone), else from the replay.
+// Whether spec_metrics traces the run's records in one batch: not for
+// evicting runs nor distinct_property sets (their state moves with more than
+// the placements), and within the batch's sizes (every record's passing rows
+// of a full pass, every record's spread counts).
+constexpr uint64_t kBatchedTraceRows = 12u << 20;
+constexpr uint64_t kBatchedSpreadCounts = 4u << 20;
 static bool spec_metrics_batched(pe_stack* s, TgPlan& g) {
-    if (s->spec.evict || tg_full_scan(s, g) || !g.distinct_props.empty() || !g.psets.empty()) return false;
+    if (s->spec.evict || !g.distinct_props.empty() || g.psets.size() != (size_t)g.n_spread) return false;
     for (auto& c : s->job_constraints)
         if (c.op == "distinct_property") return false;
-    return true;
+    const uint64_t n_rec = s->spec.n_rec;
+    if (tg_full_scan(s, g) && n_rec * s->visit.size() > kBatchedTraceRows) return false;
+    uint64_t nc = 0;
+    for (auto& ps : g.psets) nc += ps->value_str.size();
+    return n_rec * nc <= kBatchedSpreadCounts;
 }
 
 // Copies between the live dynamic columns and the checkpoint (to_ckpt: save).

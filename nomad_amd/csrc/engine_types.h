@@ -38,6 +38,25 @@ enum : uint32_t {
     kTrPenalty = 1u << 16,      // option: node in the rescheduling penalty set
 };
 
+// The entries of a k_trace launch. Plain: entry i is rows[i], with dks[i]
+// (or 0) placements the state lacks. Batched (rec_end set: every record of a
+// speculative run, spec_metrics): entry i belongs to record k, the first with
+// rec_end[k] > i, as its j-th row: rows[rsrc[k] + j] (a window walked on the
+// host), or with kTraceRot set list[(rsrc[k] - kTraceRot + j) mod n_list] (a
+// whole-list walk the memo no longer changes, rotated to the record's start);
+// its dk counts the run's placements (row << 32 | record, sorted) on the row
+// by records before k.
+constexpr uint32_t kTraceRot = 0x80000000u;
+struct TraceSrc {
+    const uint32_t* rows;
+    const uint16_t* dks;
+    const uint32_t* rec_end;
+    const uint32_t* rsrc;
+    const uint32_t* list;
+    const uint64_t* pl;
+    uint32_t n_rec, n_list, n_pl;
+};
+
 struct DevClass {
     uint8_t match[kMaxDevReq];            // bit g: group g matches request q
     uint32_t n_groups;

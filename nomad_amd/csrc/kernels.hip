@@ -449,16 +449,59 @@ __device__ __forceinline__ void eval_node(const NodeSoA& s, const TgTables& t, c
 // Options also get their named scores (ScoreNode calls, rank.go:516-522, 591-593,
 // 635-637, 704-722, spread.go:170, rank.go:769) as 6 doubles: binpack, devices,
 // job-anti-affinity, node-affinity, allocation-spread, normalized-score.
-// `dks` (or null): per entry, placements of this task group on the row that
-// the state lacks (a speculative run's earlier Selects, traced against the
-// run's starting state; no property sets then), applied as status_loaded does.
-__global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint32_t n, uint32_t* out,
-                        const uint32_t* penalty_bits, double log10, const double* spread_tab, double* sc,
-                        const uint16_t* dks) {
+// Row of entry j of record k of a batched trace (TraceSrc).
+__device__ __forceinline__ uint32_t trace_row(const TraceSrc& r, uint32_t k, uint32_t j) {
+    const uint32_t src = r.rsrc[k];
+    if (!(src & kTraceRot)) return r.rows[src + j];
+    uint32_t p = (src - kTraceRot) + j;
+    if (p >= r.n_list) p -= r.n_list;
+    return r.list[p];
+}
+
+// Placements of records before k on `row` (the sorted (row, record) pairs).
+__device__ __forceinline__ uint32_t trace_dk(const TraceSrc& r, uint32_t row, uint32_t k) {
+    const uint64_t key = (uint64_t)row << 32;
+    uint32_t lo = 0, hi = r.n_pl;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (r.pl[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    uint32_t d = 0;
+    for (; lo < r.n_pl && (uint32_t)(r.pl[lo] >> 32) == row && (uint32_t)r.pl[lo] < k; lo++) d++;
+    return d;
+}
+
+// Record of entry i of a batched trace: the first k with rec_end[k] > i.
+__device__ __forceinline__ uint32_t trace_rec(const TraceSrc& r, uint32_t i) {
+    uint32_t lo = 0, hi = r.n_rec;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (r.rec_end[mid] > i) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+// dk (TraceSrc): placements of this task group on the row that the state
+// lacks (a speculative run's earlier Selects, traced against the run's
+// starting state; no distinct_property sets then), applied as status_loaded
+// does. In a batched trace record k's spread boosts are spread_tab + k *
+// pset_tab_total (k_spread_tables: the record's own use counts).
+__global__ void k_trace(NodeSoA s, TgTables t, Ask a, TraceSrc src, uint32_t n, uint32_t* out,
+                        const uint32_t* penalty_bits, double log10, const double* spread_tab, double* sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t row = rows[i];
-    const uint32_t dk = dks ? (uint32_t)dks[i] : 0u;
+    uint32_t row, dk;
+    if (src.rec_end) {
+        const uint32_t k = trace_rec(src, i);
+        row = trace_row(src, k, i - (k ? src.rec_end[k - 1] : 0u));
+        dk = trace_dk(src, row, k);
+        if (spread_tab) spread_tab += (size_t)k * t.pset_tab_total;
+    } else {
+        row = src.rows[i];
+        dk = src.dks ? (uint32_t)src.dks[i] : 0u;
+    }
     NodeIn in;
     load_node(s, t, row, in);
     NodeRec& r = in.r;
@@ -559,7 +602,7 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
 }
 
 // ScoreMetaData of every record of a speculative run from k_trace's outcomes
-// (rows of record k: rec_end[k-1] .. rec_end[k]): one lane per record pushes
+// (rows of record k: rec_end[k-1] .. rec_end[k]): one wave per record pushes
 // its options' NormScores in visit order into a 5-slot min-heap exactly as
 // kheap.ScoreHeap.Push does under container/heap (replace the minimum only
 // when strictly greater, heap.Fix, then up(len - 1); lib/kheap/score_heap.go),
@@ -567,12 +610,15 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, const uint32_t* rows, uint
 // binary form with the names metrics_outcome gives them
 // (structs.go:9976-10018). flags: 1 devices scored, 2 job anti-affinity
 // scored, 4 node affinities exist, 8 generic stack.
-__global__ void __launch_bounds__(64) k_trace_top(const uint32_t* codes, const double* sc, const uint32_t* rows,
-                                                  const uint32_t* rec_end, uint32_t n_rec, uint32_t flags,
-                                                  pe_metric_score* out, uint8_t* n_out) {
-    const uint32_t k = blockIdx.x * 64 + threadIdx.x;
-    if (k >= n_rec) return;
-    const uint32_t b = k ? rec_end[k - 1] : 0u, e = rec_end[k];
+// A push that does not enter a full heap changes nothing, and the heap's
+// minimum only grows, so the wave reads 64 entries at a time and pushes, in
+// order and with the heap held alike in every lane, only those above the
+// minimum at the chunk's start (all of them while the heap fills).
+__global__ void __launch_bounds__(64) k_trace_top(const uint32_t* codes, const double* sc, TraceSrc src,
+                                                  uint32_t flags, pe_metric_score* out, uint8_t* n_out) {
+    const uint32_t k = blockIdx.x, lane = threadIdx.x;
+    if (k >= src.n_rec) return;
+    const uint32_t b = k ? src.rec_end[k - 1] : 0u, e = src.rec_end[k];
     double hn[5];
     uint32_t hi[5];
     uint32_t len = 0;
@@ -602,20 +648,32 @@ __global__ void __launch_bounds__(64) k_trace_top(const uint32_t* codes, const d
         }
         return i > i0;
     };
-    for (uint32_t x = b; x < e; x++) {
-        if ((codes[x] & 255u) != kTrOption) continue;
-        const double norm = sc[(size_t)x * 6 + 5];
-        if (len < 5) {
-            hn[len] = norm;
-            hi[len] = x;
-            len++;
-        } else if (norm > hn[0]) {
-            hn[0] = norm;
-            hi[0] = x;
-            if (!down(0, len)) up(0);
+    for (uint32_t c = b; c < e; c += 64) {
+        const uint32_t x = c + lane;
+        double mine = 0.0;
+        bool cand = false;
+        if (x < e && (codes[x] & 255u) == kTrOption) {
+            mine = sc[(size_t)x * 6 + 5];
+            cand = len < 5 || mine > hn[0];
         }
-        up(len - 1);
+        uint64_t mask = __ballot(cand);
+        while (mask) {
+            const uint32_t l = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+            mask &= mask - 1;
+            const double norm = __shfl(mine, (int)l);
+            if (len < 5) {
+                hn[len] = norm;
+                hi[len] = c + l;
+                len++;
+            } else if (norm > hn[0]) {
+                hn[0] = norm;
+                hi[0] = c + l;
+                if (!down(0, len)) up(0);
+            }
+            up(len - 1);
+        }
     }
+    if (lane != 0) return;
     // GetItemsReverse: heap.Pop until empty, the last popped first
     uint32_t order[5];
     const uint32_t total = len;
@@ -644,7 +702,7 @@ __global__ void __launch_bounds__(64) k_trace_top(const uint32_t* codes, const d
             else if (o[3] != 0.0) { m.scorer[ns] = PE_SCORER_NODE_AFFINITY; m.score[ns++] = o[3]; }
             if (o[4] != 0.0) { m.scorer[ns] = PE_SCORER_ALLOCATION_SPREAD; m.score[ns++] = o[4]; }
         }
-        m.row = (int32_t)rows[x];
+        m.row = (int32_t)trace_row(src, k, x - b);
         m.n_scores = ns;
         m.norm = o[5];
         out[(size_t)k * 5 + q] = m;
@@ -2920,6 +2978,21 @@ __global__ void __launch_bounds__(512) k_sweep_merge(const SweepRec* recs, uint3
 
 // Spread contribution table in HBM for the sweep path (same code as the
 // persistent loop's LDS table, so both paths are bit-identical).
+// The spread boost tables of every record of a speculative run (spec_metrics):
+// record k's use counts are the run's starting counts (t.pset_counts, the
+// checkpoint) plus the earlier records' placements (`delta`: n_rec x
+// pset_cnt_total, host-built, completed here in place); one block per record,
+// its table at tab + k * pset_tab_total. Spread sets only.
+__global__ void __launch_bounds__(256) k_spread_tables(TgTables t, uint32_t* delta, double* tab) {
+    __shared__ uint32_t scratch[4];
+    const uint32_t k = blockIdx.x;
+    uint32_t* cnt = delta + (size_t)k * t.pset_cnt_total;
+    for (int p = 0; p < t.n_psets; p++)
+        for (int v = threadIdx.x; v < t.pset_nvals[p]; v += 256) cnt[t.pset_cnt_off[p] + v] += t.pset_counts[p][v];
+    __syncthreads();
+    build_spread_table<256>(t, cnt, tab + (size_t)k * t.pset_tab_total, scratch);
+}
+
 __global__ void __launch_bounds__(256) k_spread_table(TgTables t, double* tab) {
     __shared__ uint32_t counts[kLdsPsetValues];
     __shared__ uint32_t scratch[4];
@@ -4332,11 +4405,10 @@ hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec
     return hipGetLastError();
 }
 
-hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const uint32_t* rows, const uint32_t* rec_end,
-                               uint32_t n_rec, uint32_t flags, pe_metric_score* out, uint8_t* n_out, hipStream_t st) {
-    if (!n_rec) return hipSuccess;
-    hipLaunchKernelGGL(pe::k_trace_top, dim3((n_rec + 63) / 64), dim3(64), 0, st, codes, sc, rows, rec_end, n_rec,
-                       flags, out, n_out);
+hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const pe::TraceSrc* src, uint32_t flags,
+                               pe_metric_score* out, uint8_t* n_out, hipStream_t st) {
+    if (!src->n_rec) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_trace_top, dim3(src->n_rec), dim3(64), 0, st, codes, sc, *src, flags, out, n_out);
     return hipGetLastError();
 }
 
@@ -4392,8 +4464,29 @@ hipError_t pe_launch_trace(const pe::NodeSoA* s, const pe::TgTables* t, const pe
                            uint32_t n, uint32_t* out, const uint32_t* penalty_bits, double log10,
                            const double* spread_tab, double* scores, hipStream_t st, const uint16_t* dks) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(pe::k_trace, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, rows, n, out,
-                       penalty_bits, log10, spread_tab, scores, dks);
+    pe::TraceSrc src{};
+    src.rows = rows;
+    src.dks = dks;
+    hipLaunchKernelGGL(pe::k_trace, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, src, n, out,
+                       penalty_bits, log10, spread_tab, scores);
+    return hipGetLastError();
+}
+
+// Every record of a speculative run in one launch (TraceSrc batched form).
+hipError_t pe_launch_trace_batch(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a,
+                                 const pe::TraceSrc* src, uint32_t n, uint32_t* out, double log10,
+                                 const double* spread_tab, double* scores, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_trace, dim3((n + 255) / 256), dim3(256), 0, st, *s, *t, *a, *src, n, out,
+                       nullptr, log10, spread_tab, scores);
+    return hipGetLastError();
+}
+
+// Spread boost tables of every record of a speculative run (k_spread_tables).
+hipError_t pe_launch_spread_tables(const pe::TgTables* t, uint32_t n_rec, uint32_t* delta, double* tab,
+                                   hipStream_t st) {
+    if (n_rec == 0) return hipSuccess;
+    hipLaunchKernelGGL(pe::k_spread_tables, dim3(n_rec), dim3(256), 0, st, *t, delta, tab);
     return hipGetLastError();
 }
 

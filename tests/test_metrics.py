@@ -650,3 +650,31 @@ def test_metrics_system_view_c4_100k():
         if i == 50000:   # a crossing in the middle: the log is taken over, the last maps with it
             assert eng.LastMetrics() == mo
     assert served >= n - 10, served
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["even_and_targets", "per_node_values", "affinity_only"])
+def test_metrics_view_batched_spreads(kind):
+    """Full-pass runs traced in one batch (spec_metrics): every record's spread
+    boosts from its own use counts (k_spread_tables), an even spread beside a
+    targeted one over 90 values, a spread over a per-node attribute, and an
+    affinity-only full pass; maps from the view equal the oracle's."""
+    from nomad_amd.structs import Affinity, Spread, SpreadTarget
+    nodes, allocs = synth.cluster_c2(2000, seed=13)
+    for i, nd in enumerate(nodes):
+        nd.meta["rack"] = "r%d" % (i % 90)
+        nd.datacenter = "dc%d" % (i % 3)
+        nd.compute_class()
+    job = synth.job_c2(150)
+    job.datacenters = ["dc0", "dc1", "dc2"]
+    tg = job.task_groups[0]
+    if kind == "even_and_targets":
+        tg.spreads = [Spread("${node.datacenter}", 50, []),
+                      Spread("${meta.rack}", 30, [SpreadTarget("r1", 20), SpreadTarget("r2", 30)])]
+    elif kind == "per_node_values":
+        tg.spreads = [Spread("${node.unique.name}", 40, [])]
+    else:
+        tg.affinities = [Affinity("${meta.rack}", "r1[0-9]", "regexp", 60)]
+    eng, ora = _metrics_pair(nodes, allocs, job, synth.shuffle(len(nodes), 9))
+    st = _view_metrics_protocol(eng, ora, 150)
+    assert st["view"] >= 120, st

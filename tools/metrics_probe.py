@@ -13,8 +13,13 @@ from nomad_amd.stack import GenericStack  # noqa: E402
 from tools import dropin  # noqa: E402
 
 n, count = 10000, 1000
-nodes, allocs = synth.cluster_c2(n, seed=42)
-job = synth.job_c2(count)
+kind = sys.argv[1] if len(sys.argv) > 1 else "c2"
+if kind == "c3":   # spread + affinity full passes (the batched spread trace)
+    nodes, allocs = synth.cluster_c3(n, seed=7)
+    job = synth.job_c3(count)
+else:
+    nodes, allocs = synth.cluster_c2(n, seed=42)
+    job = synth.job_c2(count)
 orders = np.stack([synth.shuffle(n, 1000 + e) for e in range(8)])
 st = GenericStack()
 st.SetState(nodes, allocs)
