@@ -6039,9 +6039,21 @@ struct WalkCache {
     std::vector<uint8_t> pass;   // per visit position
 };
 
+// PE_METRICS_PROF: compute_metrics' phases (walk, trace launches + syncs,
+// eviction trace, outcomes) summed over a replay
+static double g_cm_prof[4];
+
 static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& order, uint32_t start,
                            uint32_t evaluated, const pe_select_options* opts, bool evict = false,
                            std::vector<MemoDelta>* log = nullptr, WalkCache* wc = nullptr) {
+    static const bool prof = std::getenv("PE_METRICS_PROF") != nullptr;
+    double tp = prof ? now_us() : 0.0;
+    auto lap = [&](int k) {
+        if (!prof) return;
+        const double t = now_us();
+        g_cm_prof[k] += t - tp;
+        tp = t;
+    };
     s->metrics_valid = false;
     MetricAcc acc;
     std::vector<uint32_t> rows;
@@ -6067,6 +6079,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             wc->kf = acc.kf;
         }
     }
+    lap(0);
     if (!rows.empty()) {
         HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
         HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
@@ -6102,6 +6115,10 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         std::vector<uint32_t> ecodes;
         std::vector<double> named;
         if (evict) {
+            if (prof) {
+                HIP_TRY(s, hipStreamSynchronize(s->stream));
+                lap(1);
+            }
             pe::PreemptArgs P = preempt_args(s, g);
             P.penalty_bits = pbits;
             P.spread_tab = stab;
@@ -6133,6 +6150,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             }
         }
         HIP_TRY(s, hipStreamSynchronize(s->stream));
+        lap(evict ? 2 : 1);
         const bool has_aff = !g.affinities.empty();
         const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
         std::map<int, std::vector<uint32_t>> counts;   // distinct_property use counts, read on demand
@@ -6174,6 +6192,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         }
     }
     metrics_set_last(s, acc);
+    lap(3);
     return PE_OK;
 }
 
@@ -6461,9 +6480,12 @@ static int spec_metrics_replay(pe_stack* s, TgPlan& g, uint32_t off0) {
     HIP_TRY(s, hipStreamSynchronize(s->stream));
     s->metrics_valid = false;
     sp.metrics = true;
-    if (prof)
-        std::fprintf(stderr, "spec_metrics_replay: %u records: %.1f us (%zu counts, %zu scores)\n", sp.n_rec,
-                     now_us() - t0, sp.mcounts.size(), sp.mscores.size());
+    if (prof) {
+        std::fprintf(stderr, "spec_metrics_replay: %u records: %.1f us (%zu counts, %zu scores); walk %.1f, trace "
+                             "%.1f, evict trace %.1f, outcomes %.1f us\n", sp.n_rec, now_us() - t0, sp.mcounts.size(),
+                     sp.mscores.size(), g_cm_prof[0], g_cm_prof[1], g_cm_prof[2], g_cm_prof[3]);
+        for (double& x : g_cm_prof) x = 0.0;
+    }
     return PE_OK;
 }
 
