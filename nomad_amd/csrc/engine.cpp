@@ -841,8 +841,10 @@ struct pe_stack {
     uint64_t test_fallback_every = 0, test_select_calls = 0;   // PE_TEST_FALLBACK_EVERY
     DevMem d_trace_rows, d_trace_out, d_trace_scores;
     PinnedMem h_trace_top;   // spec_metrics: the batched trace's ScoreMetaData and outcome codes
+    DevMem d_cm_ends;        // compute_metrics: the one record's end and source (k_trace_top)
     DevMem d_trace_top;
     DevMem d_trace_delta, d_trace_tabs;   // spec_metrics: per record spread use counts and boost tables
+    DevMem d_wc_list;                     // compute_metrics: a settled whole-list walk's passing rows
     DevMem d_loop_out, d_loop_state;   // device-resident full-pass count loop
     DevMem d_ploop_mask, d_ev_score_p, d_ev_status_p, d_ev_dep;
     DevMem d_pre_mask;                       // a commit's preempted set (evict_words words)
@@ -6037,6 +6039,10 @@ struct WalkCache {
     bool valid = false;
     MetricCounts cf, kf;
     std::vector<uint8_t> pass;   // per visit position
+    // the passing rows in position order and their positions, built at the
+    // first reuse, and whether d_wc_list holds them
+    std::vector<uint32_t> list, lpos;
+    bool built = false, on_dev = false;
 };
 
 // PE_METRICS_PROF: compute_metrics' phases (walk, trace launches + syncs,
@@ -6059,13 +6065,43 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
     std::vector<uint32_t> rows;
     const size_t m = order.size();
     const bool whole = wc && m && evaluated == m;
+    bool rows_on_dev = false;
     if (whole && wc->valid) {
         acc.cf = wc->cf;
         acc.kf = wc->kf;
-        rows.reserve(m);
-        for (uint32_t k = 0; k < m; k++) {
-            const uint32_t p = (uint32_t)((start + k) % m);
-            if (wc->pass[p]) rows.push_back(order[p]);
+        if (!wc->built) {
+            wc->list.clear();
+            wc->lpos.clear();
+            for (uint32_t p = 0; p < m; p++)
+                if (wc->pass[p]) {
+                    wc->list.push_back(order[p]);
+                    wc->lpos.push_back(p);
+                }
+            wc->built = true;
+            wc->on_dev = false;
+        }
+        // the window's passing rows: the list rotated to its start, on the
+        // host and (two device copies of the list uploaded once) on the device
+        const size_t P = wc->list.size();
+        size_t s0 = (size_t)(std::lower_bound(wc->lpos.begin(), wc->lpos.end(), (uint32_t)(start % m)) -
+                             wc->lpos.begin());
+        if (s0 == P) s0 = 0;
+        rows.reserve(P);
+        rows.insert(rows.end(), wc->list.begin() + s0, wc->list.end());
+        rows.insert(rows.end(), wc->list.begin(), wc->list.begin() + s0);
+        if (P) {
+            if (!wc->on_dev) {
+                HIP_TRY(s, upload_s(s, s->d_wc_list, wc->list));
+                wc->on_dev = true;
+            }
+            HIP_TRY(s, s->d_trace_rows.ensure(P * sizeof(uint32_t)));
+            const uint32_t* l = s->d_wc_list.as<uint32_t>();
+            uint32_t* r = s->d_trace_rows.as<uint32_t>();
+            HIP_TRY(s, hipMemcpyAsync(r, l + s0, (P - s0) * sizeof(uint32_t), hipMemcpyDeviceToDevice, s->stream));
+            if (s0)
+                HIP_TRY(s, hipMemcpyAsync(r + (P - s0), l, s0 * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                          s->stream));
+            rows_on_dev = true;
         }
     } else {
         const size_t l0 = log ? log->size() : 0;
@@ -6075,13 +6111,17 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         if (wc && (changed || !whole)) wc->valid = wc->valid && !changed;
         if (whole && !changed && log) {
             wc->valid = true;
+            wc->built = false;
             wc->cf = acc.cf;
             wc->kf = acc.kf;
         }
     }
     lap(0);
+    const pe_metric_score* dtop = nullptr;   // plain Selects: k_trace_top's items
+    pe_metric_score dtop_items[5];
+    uint32_t dtop_n = 0;
     if (!rows.empty()) {
-        HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
+        if (!rows_on_dev) HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
         HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
         HIP_TRY(s, s->d_trace_scores.ensure(rows.size() * 6 * sizeof(double)));
         pe::NodeSoA soa = soa_of(s);
@@ -6106,14 +6146,43 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         HIP_TRY_STATE(s, pe_launch_trace(&soa, &t, &a, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
                                    s->d_trace_out.as<uint32_t>(), pbits, s->log10, stab,
                                    s->d_trace_scores.as<double>(), s->stream));
-        std::vector<uint32_t> codes(rows.size());
-        std::vector<double> sc(rows.size() * 6);
-        HIP_TRY(s, hipMemcpyAsync(codes.data(), s->d_trace_out.p, codes.size() * 4, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(s, hipMemcpyAsync(sc.data(), s->d_trace_scores.p, sc.size() * 8, hipMemcpyDeviceToHost, s->stream));
+        // the outcome codes and (plain Selects) the top-5 ScoreMetaData from
+        // k_trace_top come back; the score values stay on the device. (Host
+        // vectors: the staged copy leaves them in the CPU's caches, and the
+        // outcome loop read a pinned buffer the DMA wrote about twice as
+        // slowly, same-box A/B.)
+        const size_t n = rows.size();
+        const size_t top_bytes = 5 * sizeof(pe_metric_score);
+        static thread_local std::vector<uint32_t> codes_v, ecodes_v;
+        static thread_local std::vector<double> named_v;
+        codes_v.resize(n);
+        const uint32_t* codes = codes_v.data();
+        alignas(8) uint8_t top_buf[5 * sizeof(pe_metric_score) + 8];
+        if (!evict) {
+            HIP_TRY(s, upload_s(s, s->d_cm_ends, std::vector<uint32_t>{(uint32_t)n, 0u}));
+            pe::TraceSrc src{};
+            src.rows = s->d_trace_rows.as<uint32_t>();
+            src.rec_end = s->d_cm_ends.as<uint32_t>();
+            src.rsrc = src.rec_end + 1;
+            src.n_rec = 1;
+            HIP_TRY(s, s->d_trace_top.ensure(top_bytes + 1));
+            const uint32_t flags = (a.dev_tw != 0.0 ? 1u : 0u) | (a.anti_aff ? 2u : 0u) |
+                                   (!g.affinities.empty() ? 4u : 0u) |
+                                   (s->cfg.stack_kind == PE_STACK_GENERIC ? 8u : 0u);
+            HIP_TRY_STATE(s, pe_launch_trace_top(s->d_trace_out.as<uint32_t>(), s->d_trace_scores.as<double>(), &src,
+                                                 flags, s->d_trace_top.as<pe_metric_score>(),
+                                                 s->d_trace_top.as<uint8_t>() + top_bytes, s->stream));
+            HIP_TRY(s, hipMemcpyAsync(top_buf, s->d_trace_top.p, top_bytes + 1, hipMemcpyDeviceToHost, s->stream));
+        }
+        HIP_TRY(s, hipMemcpyAsync(codes_v.data(), s->d_trace_out.p, n * 4, hipMemcpyDeviceToHost, s->stream));
         // Select with Preempt: BinPack with evict per row (rank.go:480-503) and
         // the ScoreNode values of the options, preemption score included
-        std::vector<uint32_t> ecodes;
-        std::vector<double> named;
+        if (evict) {
+            ecodes_v.resize(n);
+            named_v.resize(n * 7);
+        }
+        uint32_t* ecodes = ecodes_v.data();
+        double* named = named_v.data();
         if (evict) {
             if (prof) {
                 HIP_TRY(s, hipStreamSynchronize(s->stream));
@@ -6129,19 +6198,17 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
             }
             HIP_TRY(s, s->d_ev_tcodes.ensure(rows.size() * sizeof(uint32_t)));
             HIP_TRY(s, s->d_ev_named.ensure(rows.size() * 7 * sizeof(double)));
-            ecodes.resize(rows.size());
-            named.resize(rows.size() * 7);
             for (;;) {   // a row wider than the launch: the trace again, wider
                 HIP_TRY_STATE(s, pe_launch_evict_trace(&P, s->d_trace_rows.as<uint32_t>(), (uint32_t)rows.size(),
                                                        s->d_ev_tcodes.as<uint32_t>(), s->d_ev_named.as<double>(),
                                                        s->stream));
-                HIP_TRY(s, hipMemcpyAsync(ecodes.data(), s->d_ev_tcodes.p, ecodes.size() * 4, hipMemcpyDeviceToHost,
+                HIP_TRY(s, hipMemcpyAsync(ecodes, s->d_ev_tcodes.p, n * 4, hipMemcpyDeviceToHost,
                                           s->stream));
-                HIP_TRY(s, hipMemcpyAsync(named.data(), s->d_ev_named.p, named.size() * 8, hipMemcpyDeviceToHost,
+                HIP_TRY(s, hipMemcpyAsync(named, s->d_ev_named.p, n * 7 * sizeof(double), hipMemcpyDeviceToHost,
                                           s->stream));
                 HIP_TRY(s, hipStreamSynchronize(s->stream));
                 bool wider = false;
-                for (uint32_t ec : ecodes) wider = wider || (((ec >> 24) & pe::kEvictWider) != 0u);
+                for (size_t i = 0; i < n; i++) wider = wider || (((ecodes[i] >> 24) & pe::kEvictWider) != 0u);
                 if (!wider) break;
                 P.mask_words = wider_words(P.mask_words);
                 if (!P.mask_words)
@@ -6151,6 +6218,11 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         }
         HIP_TRY(s, hipStreamSynchronize(s->stream));
         lap(evict ? 2 : 1);
+        if (!evict) {
+            std::memcpy(dtop_items, top_buf, top_bytes);
+            dtop = dtop_items;
+            dtop_n = std::min<uint32_t>(top_buf[top_bytes], 5u);
+        }
         const bool has_aff = !g.affinities.empty();
         const bool generic = s->cfg.stack_kind == PE_STACK_GENERIC;
         std::map<int, std::vector<uint32_t>> counts;   // distinct_property use counts, read on demand
@@ -6187,11 +6259,13 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
                 }
                 continue;
             }
-            const int rc = metrics_outcome(s, g, a, row, code, &sc[i * 6], acc, counts);
+            if (base == pe::kTrOption) continue;   // the options' ScoreMetaData came from k_trace_top
+            const int rc = metrics_outcome(s, g, a, row, code, nullptr, acc, counts);
             if (rc) return rc;
         }
     }
     metrics_set_last(s, acc);
+    if (dtop) s->m_scores.assign(dtop, dtop + dtop_n);
     lap(3);
     return PE_OK;
 }
