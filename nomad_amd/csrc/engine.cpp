@@ -148,7 +148,7 @@ hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint
 hipError_t pe_launch_sweep_only(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t pe_launch_sweep_local(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const pe::TraceSrc* src, uint32_t flags,
-                               pe_metric_score* out, uint8_t* n_out, hipStream_t st);
+                               pe_metric_score* out, uint8_t* n_out, hipStream_t st, uint32_t n_entries);
 hipError_t pe_launch_step_only(const pe::SweepArgs* a, uint32_t nrecs, const uint32_t* visit, uint32_t n,
                                uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_commit_rows(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
@@ -722,6 +722,7 @@ struct pe_stack {
     std::string jf_key;
     std::vector<std::string> jf_texts;
     std::vector<uint32_t> jf_cls;
+    std::vector<uint32_t> jf_mclass;   // the row's metric class key (node_class, PE_NONE when empty)
     std::vector<ParsedAffinity> job_affinities;
     std::vector<SpreadSpec> job_spreads;
     std::vector<std::unique_ptr<TgPlan>> tgs;
@@ -1417,7 +1418,12 @@ static void jf_ready(pe_stack* s) {
     if (s->jf.size() == s->nodes.size()) return;
     s->jf.assign(s->nodes.size(), nullptr);
     s->jf_cls.resize(s->nodes.size());
-    for (size_t r = 0; r < s->nodes.size(); r++) s->jf_cls[r] = s->nodes[r].cls;
+    s->jf_mclass.resize(s->nodes.size());
+    for (size_t r = 0; r < s->nodes.size(); r++) {
+        s->jf_cls[r] = s->nodes[r].cls;
+        const uint32_t nc = s->nodes[r].node_class;
+        s->jf_mclass[r] = (nc != PE_NONE && !s->S(nc).empty()) ? nc : PE_NONE;
+    }
 }
 
 const char* job_fail_cached(pe_stack* s, pe::ConstraintEvaluator& ev, uint32_t row) {
@@ -5708,15 +5714,21 @@ struct MetricAcc {
         }
         heap.len = 0;
     }
-    void filter(pe_stack* s, uint32_t row, uint32_t why) {
+    // the row's node class key: the flat per-row copy (jf_ready) when current
+    static uint32_t mclass(const pe_stack* s, uint32_t row) {
+        if (row < s->jf_mclass.size() && s->jf.size() == s->nodes.size()) return s->jf_mclass[row];
         const uint32_t nc = s->nodes[row].node_class;
-        if (nc != PE_NONE && !s->S(nc).empty()) cf.add(nc);
+        return (nc != PE_NONE && !s->S(nc).empty()) ? nc : PE_NONE;
+    }
+    void filter(pe_stack* s, uint32_t row, uint32_t why) {
+        const uint32_t nc = mclass(s, row);
+        if (nc != PE_NONE) cf.add(nc);
         if (why != PE_NONE) kf.add(why);
     }
     void filter(pe_stack* s, uint32_t row, const std::string& why) { filter(s, row, s->mkey(why)); }
     void exhaust(pe_stack* s, uint32_t row, uint32_t dim) {
-        const uint32_t nc = s->nodes[row].node_class;
-        if (nc != PE_NONE && !s->S(nc).empty()) ce.add(nc);
+        const uint32_t nc = mclass(s, row);
+        if (nc != PE_NONE) ce.add(nc);
         if (dim != PE_NONE) de.add(dim);
     }
     void exhaust(pe_stack* s, uint32_t row, const std::string& dim) { exhaust(s, row, s->mkey(dim)); }
@@ -6122,7 +6134,8 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
     uint32_t dtop_n = 0;
     if (!rows.empty()) {
         if (!rows_on_dev) HIP_TRY(s, upload_s(s, s->d_trace_rows, rows));
-        HIP_TRY(s, s->d_trace_out.ensure(rows.size() * sizeof(uint32_t)));
+        // the codes, then (plain Selects) k_trace_top's items and count
+        HIP_TRY(s, s->d_trace_out.ensure(((rows.size() * 4 + 15) & ~size_t(15)) + 5 * sizeof(pe_metric_score) + 8));
         HIP_TRY(s, s->d_trace_scores.ensure(rows.size() * 6 * sizeof(double)));
         pe::NodeSoA soa = soa_of(s);
         pe::TgTables t = tables_of(g);
@@ -6155,26 +6168,35 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         const size_t top_bytes = 5 * sizeof(pe_metric_score);
         static thread_local std::vector<uint32_t> codes_v, ecodes_v;
         static thread_local std::vector<double> named_v;
-        codes_v.resize(n);
-        const uint32_t* codes = codes_v.data();
-        alignas(8) uint8_t top_buf[5 * sizeof(pe_metric_score) + 8];
+        // plain Selects: the codes, then the top-5 and its count, in one buffer
+        // and one download
+        const size_t top_at = (n * 4 + 15) & ~size_t(15);
+        codes_v.resize(evict ? n : (top_at + top_bytes + 8) / 4);
         if (!evict) {
-            HIP_TRY(s, upload_s(s, s->d_cm_ends, std::vector<uint32_t>{(uint32_t)n, 0u}));
+            const std::vector<uint32_t> ends{(uint32_t)n, 0u};
+            const uint32_t* d_ends = reinterpret_cast<const uint32_t*>(stage_only(s, ends));
+            if (!d_ends) {
+                HIP_TRY(s, upload_s(s, s->d_cm_ends, ends));
+                d_ends = s->d_cm_ends.as<uint32_t>();
+            }
             pe::TraceSrc src{};
             src.rows = s->d_trace_rows.as<uint32_t>();
-            src.rec_end = s->d_cm_ends.as<uint32_t>();
-            src.rsrc = src.rec_end + 1;
+            src.rec_end = d_ends;
+            src.rsrc = d_ends + 1;
             src.n_rec = 1;
-            HIP_TRY(s, s->d_trace_top.ensure(top_bytes + 1));
+            uint8_t* d_top = s->d_trace_out.as<uint8_t>() + top_at;
             const uint32_t flags = (a.dev_tw != 0.0 ? 1u : 0u) | (a.anti_aff ? 2u : 0u) |
                                    (!g.affinities.empty() ? 4u : 0u) |
                                    (s->cfg.stack_kind == PE_STACK_GENERIC ? 8u : 0u);
             HIP_TRY_STATE(s, pe_launch_trace_top(s->d_trace_out.as<uint32_t>(), s->d_trace_scores.as<double>(), &src,
-                                                 flags, s->d_trace_top.as<pe_metric_score>(),
-                                                 s->d_trace_top.as<uint8_t>() + top_bytes, s->stream));
-            HIP_TRY(s, hipMemcpyAsync(top_buf, s->d_trace_top.p, top_bytes + 1, hipMemcpyDeviceToHost, s->stream));
+                                                 flags, reinterpret_cast<pe_metric_score*>(d_top),
+                                                 d_top + top_bytes, s->stream, (uint32_t)n));
+            HIP_TRY(s, hipMemcpyAsync(codes_v.data(), s->d_trace_out.p, top_at + top_bytes + 1,
+                                      hipMemcpyDeviceToHost, s->stream));
+        } else {
+            HIP_TRY(s, hipMemcpyAsync(codes_v.data(), s->d_trace_out.p, n * 4, hipMemcpyDeviceToHost, s->stream));
         }
-        HIP_TRY(s, hipMemcpyAsync(codes_v.data(), s->d_trace_out.p, n * 4, hipMemcpyDeviceToHost, s->stream));
+        const uint8_t* top_buf = reinterpret_cast<const uint8_t*>(codes_v.data()) + top_at;
         // Select with Preempt: BinPack with evict per row (rank.go:480-503) and
         // the ScoreNode values of the options, preemption score included
         if (evict) {
@@ -6218,6 +6240,7 @@ static int compute_metrics(pe_stack* s, TgPlan& g, const std::vector<uint32_t>& 
         }
         HIP_TRY(s, hipStreamSynchronize(s->stream));
         lap(evict ? 2 : 1);
+        const uint32_t* codes = codes_v.data();
         if (!evict) {
             std::memcpy(dtop_items, top_buf, top_bytes);
             dtop = dtop_items;
@@ -6446,7 +6469,7 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
                                (s->cfg.stack_kind == PE_STACK_GENERIC ? 8u : 0u);
         HIP_TRY_STATE(s, pe_launch_trace_top(d_codes, s->d_trace_scores.as<double>(), &src, flags,
                                              s->d_trace_top.as<pe_metric_score>(),
-                                             s->d_trace_top.as<uint8_t>() + top_bytes, s->stream));
+                                             s->d_trace_top.as<uint8_t>() + top_bytes, s->stream, (uint32_t)n_rows));
         HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.p, s->d_trace_top.p, codes_at + n_rows * sizeof(uint32_t),
                                   hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(s, hipStreamSynchronize(s->stream));

@@ -611,14 +611,85 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, TraceSrc src, uint32_t n, 
 // (structs.go:9976-10018). flags: 1 devices scored, 2 job anti-affinity
 // scored, 4 node affinities exist, 8 generic stack.
 // A push that does not enter a full heap changes nothing, and the heap's
-// minimum only grows, so the wave reads 64 entries at a time and pushes, in
-// order and with the heap held alike in every lane, only those above the
-// minimum at the chunk's start (all of them while the heap fills).
-__global__ void __launch_bounds__(64) k_trace_top(const uint32_t* codes, const double* sc, TraceSrc src,
-                                                  uint32_t flags, pe_metric_score* out, uint8_t* n_out) {
-    const uint32_t k = blockIdx.x, lane = threadIdx.x;
-    if (k >= src.n_rec) return;
+// minimum only grows. The record's entries are split among the block's waves;
+// each wave keeps the top-5 NormScores of its own segment so far and lists the
+// entries that enter it: an entry that does not enter its segment's top-5 is
+// at or below the minimum of a heap that has seen at least that prefix, so it
+// does not enter the record's heap either. Wave 0 then pushes the listed
+// entries in order into the heap (held alike in every lane). A segment with
+// more entering entries than its list holds sends the record to wave 0's
+// sequential pass over every entry.
+constexpr uint32_t kTopWaves = 16, kTopCand = 128;
+__global__ void __launch_bounds__(1024) k_trace_top(const uint32_t* codes, const double* sc, TraceSrc src,
+                                                    uint32_t flags, pe_metric_score* out, uint8_t* n_out) {
+    __shared__ uint32_t cand_x[kTopWaves][kTopCand];
+    __shared__ double cand_v[kTopWaves][kTopCand];
+    __shared__ uint32_t cand_n[kTopWaves];
+    __shared__ uint32_t overflow;
+    const uint32_t k = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t nw = blockDim.x >> 6;
+    if (k >= src.n_rec) return;   // uniform across the block
     const uint32_t b = k ? src.rec_end[k - 1] : 0u, e = src.rec_end[k];
+    if (tid == 0) overflow = 0;
+    {   // phase 1: the segment's entering entries
+        const uint32_t total = e - b, seg = (total + nw - 1) / nw;
+        const uint32_t sb = b + min(total, w * seg), se = b + min(total, (w + 1) * seg);
+        double t[5];   // the segment's top-5 so far (values), unsorted; tmin its minimum once full
+        uint32_t tl = 0, nc = 0;
+        double tmin = 0.0;
+        bool over = false;
+        constexpr uint32_t U = 4;
+        for (uint32_t c = sb; c < se; c += 64 * U) {
+            uint32_t cd[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t x = c + u * 64 + lane;
+                cd[u] = x < se ? codes[x] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t x = c + u * 64 + lane;
+                const bool opt = (cd[u] & 255u) == kTrOption;
+                const double v = opt ? sc[(size_t)x * 6 + 5] : 0.0;
+                uint64_t mask = __ballot(opt && (tl < 5 || v > tmin));
+                while (mask) {
+                    const uint32_t l = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+                    mask &= mask - 1;
+                    const double nv = __shfl(v, (int)l);
+                    if (tl < 5) {
+                        t[tl++] = nv;   // tl is wave-uniform: a static index after unrolling below
+                    } else if (nv > tmin) {
+                        bool done = false;   // replace one minimum
+#pragma unroll
+                        for (int q = 0; q < 5; q++)
+                            if (!done && t[q] == tmin) { t[q] = nv; done = true; }
+                    } else {
+                        continue;
+                    }
+                    if (tl == 5) {
+                        tmin = t[0];
+#pragma unroll
+                        for (int q = 1; q < 5; q++) tmin = t[q] < tmin ? t[q] : tmin;
+                    }
+                    if (nc < kTopCand) {
+                        if (lane == 0) {
+                            cand_x[w][nc] = c + u * 64 + l;
+                            cand_v[w][nc] = nv;
+                        }
+                        nc++;
+                    } else {
+                        over = true;
+                    }
+                }
+            }
+        }
+        if (lane == 0) {
+            cand_n[w] = nc;
+            if (over) atomicOr(&overflow, 1u);
+        }
+    }
+    __syncthreads();
+    if (w != 0) return;
     double hn[5];
     uint32_t hi[5];
     uint32_t len = 0;
@@ -648,29 +719,32 @@ __global__ void __launch_bounds__(64) k_trace_top(const uint32_t* codes, const d
         }
         return i > i0;
     };
-    for (uint32_t c = b; c < e; c += 64) {
-        const uint32_t x = c + lane;
-        double mine = 0.0;
-        bool cand = false;
-        if (x < e && (codes[x] & 255u) == kTrOption) {
-            mine = sc[(size_t)x * 6 + 5];
-            cand = len < 5 || mine > hn[0];
+    auto push = [&](double norm, uint32_t x) {   // ScoreHeap.Push under container/heap
+        if (len < 5) {
+            hn[len] = norm;
+            hi[len] = x;
+            len++;
+        } else if (norm > hn[0]) {
+            hn[0] = norm;
+            hi[0] = x;
+            if (!down(0, len)) up(0);
         }
-        uint64_t mask = __ballot(cand);
-        while (mask) {
-            const uint32_t l = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
-            mask &= mask - 1;
-            const double norm = __shfl(mine, (int)l);
-            if (len < 5) {
-                hn[len] = norm;
-                hi[len] = c + l;
-                len++;
-            } else if (norm > hn[0]) {
-                hn[0] = norm;
-                hi[0] = c + l;
-                if (!down(0, len)) up(0);
+        up(len - 1);
+    };
+    if (!overflow) {
+        for (uint32_t q = 0; q < nw; q++)
+            for (uint32_t i = 0; i < cand_n[q]; i++) push(cand_v[q][i], cand_x[q][i]);
+    } else {   // every entry in order, 64 at a time (a candidate pass over the whole record)
+        for (uint32_t c = b; c < e; c += 64) {
+            const uint32_t x = c + lane;
+            const bool opt = x < e && (codes[x] & 255u) == kTrOption;
+            const double v = opt ? sc[(size_t)x * 6 + 5] : 0.0;
+            uint64_t mask = __ballot(opt && (len < 5 || v > hn[0]));
+            while (mask) {
+                const uint32_t l = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+                mask &= mask - 1;
+                push(__shfl(v, (int)l), c + l);
             }
-            up(len - 1);
         }
     }
     if (lane != 0) return;
@@ -4406,9 +4480,13 @@ hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec
 }
 
 hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const pe::TraceSrc* src, uint32_t flags,
-                               pe_metric_score* out, uint8_t* n_out, hipStream_t st) {
+                               pe_metric_score* out, uint8_t* n_out, hipStream_t st, uint32_t n_entries) {
     if (!src->n_rec) return hipSuccess;
-    hipLaunchKernelGGL(pe::k_trace_top, dim3(src->n_rec), dim3(64), 0, st, codes, sc, *src, flags, out, n_out);
+    // waves per record: about 2048 entries each, 1 to kTopWaves
+    const uint32_t avg = n_entries / src->n_rec;
+    const uint32_t waves = std::max<uint32_t>(1u, std::min<uint32_t>(pe::kTopWaves, (avg + 2047u) / 2048u));
+    hipLaunchKernelGGL(pe::k_trace_top, dim3(src->n_rec), dim3(64 * waves), 0, st, codes, sc, *src, flags, out,
+                       n_out);
     return hipGetLastError();
 }
 
