@@ -237,11 +237,14 @@ struct DevMem {
         p = nullptr;
         bytes = 0;
     }
+    // at least b bytes (contents not kept); 1/8 headroom, so sizes that creep
+    // up call after call (a run's traced rows) do not reallocate each time
     hipError_t ensure(size_t b) {
         if (b <= bytes && p) return hipSuccess;
         release();
-        hipError_t e = hipMalloc(&p, b ? b : 16);
-        if (e == hipSuccess) bytes = b ? b : 16;
+        const size_t want = std::max<size_t>(b + b / 8, 16);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) bytes = want;
         return e;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }
@@ -280,11 +283,12 @@ struct PinnedMem {
         bytes = 0;
         dp_of = nullptr;
     }
-    hipError_t ensure(size_t b) {
+    hipError_t ensure(size_t b) {   // 1/8 headroom, as DevMem::ensure
         if (b <= bytes && p) return hipSuccess;
         release();
-        hipError_t e = hipHostMalloc(&p, b ? b : 16, hipHostMallocMapped);
-        if (e == hipSuccess) bytes = b ? b : 16;
+        const size_t want = std::max<size_t>(b + b / 8, 16);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocMapped);
+        if (e == hipSuccess) bytes = want;
         return e;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }

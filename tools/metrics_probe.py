@@ -2,6 +2,7 @@
 nodes, count 1000) with pe_set_metrics on and the maps copied out by the
 caller; per evaluation wall time, and with PE_METRICS_PROF=1 the speculative
 run's metric phases (host walk, k_trace, maps + text)."""
+import os
 import sys
 import time
 
@@ -38,7 +39,7 @@ caller(orders, count, preempt=preempt, n_evals=1)
 for i in range(2 if preempt else 4):
     dropin.phase_seconds(reset=True)
     t0 = time.perf_counter()
-    placed, ne, _, _, _ = caller(orders, count, preempt=preempt, n_evals=2)
+    placed, ne, _, _, _ = caller(orders, count, preempt=preempt, n_evals=int(os.environ.get("PROBE_EVALS", "2")))
     dt = time.perf_counter() - t0
     ph = dropin.phase_seconds(reset=True)
     print("%.3f ms per evaluation" % (dt / ne * 1e3), {k: round(v / ne * 1e3, 3) for k, v in ph.items()}, flush=True)
