@@ -148,7 +148,8 @@ hipError_t pe_launch_fullpass_lds(const pe::SweepArgs* a_dev, int np, const uint
 hipError_t pe_launch_sweep_only(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t pe_launch_sweep_local(const pe::SweepArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const pe::TraceSrc* src, uint32_t flags,
-                               pe_metric_score* out, uint8_t* n_out, hipStream_t st, uint32_t n_entries);
+                               pe_metric_score* out, uint8_t* n_out, hipStream_t st, uint32_t n_entries,
+                               uint32_t* n_other = nullptr, uint2* other_list = nullptr);
 hipError_t pe_launch_step_only(const pe::SweepArgs* a, uint32_t nrecs, const uint32_t* visit, uint32_t n,
                                uint32_t offset, pe_ranked_node* out, uint32_t* state, hipStream_t st);
 hipError_t pe_launch_commit_rows(const pe::NodeSoA* s, const pe::TgTables* t, const pe::Ask* a, const uint32_t* rows,
@@ -6396,8 +6397,18 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     // runs; the score values stay on the device
     const size_t n_rows = n_entries;
     const size_t top_bytes = 5 * sizeof(pe_metric_score) * (size_t)sp.n_rec;
-    const size_t codes_at = (top_bytes + sp.n_rec + 15) & ~size_t(15);
+    // per record: its entries that are not options, and the first kOther of
+    // them (entry, code) as k_trace_top lists them
+    constexpr uint32_t kOther = 128;   // = kTopOther (kernels.hip)
+    const size_t other_at = (top_bytes + sp.n_rec + 15) & ~size_t(15);
+    const size_t olist_at = (other_at + 4 * (size_t)sp.n_rec + 15) & ~size_t(15);
+    const size_t codes_at = (olist_at + 8 * (size_t)kOther * sp.n_rec + 15) & ~size_t(15);
+    // the lists pay off when the codes are many times their size (full passes)
+    const bool use_list = 4 * (size_t)n_rows > 4 * 8 * (size_t)kOther * sp.n_rec;
+    bool all_codes = !use_list;
     HIP_TRY(s, s->h_trace_top.ensure(codes_at + std::max<size_t>(n_rows, 1) * sizeof(uint32_t)));
+    const uint32_t* olist = reinterpret_cast<const uint32_t*>(s->h_trace_top.as<uint8_t>() + olist_at);
+    const uint32_t* n_other = reinterpret_cast<const uint32_t*>(s->h_trace_top.as<uint8_t>() + other_at);
     const pe_metric_score* top = s->h_trace_top.as<pe_metric_score>();
     const uint8_t* n_top = s->h_trace_top.as<uint8_t>() + top_bytes;
     const uint32_t* codes = reinterpret_cast<const uint32_t*>(s->h_trace_top.as<uint8_t>() + codes_at);
@@ -6473,12 +6484,30 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
                                (s->cfg.stack_kind == PE_STACK_GENERIC ? 8u : 0u);
         HIP_TRY_STATE(s, pe_launch_trace_top(d_codes, s->d_trace_scores.as<double>(), &src, flags,
                                              s->d_trace_top.as<pe_metric_score>(),
-                                             s->d_trace_top.as<uint8_t>() + top_bytes, s->stream, (uint32_t)n_rows));
-        HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.p, s->d_trace_top.p, codes_at + n_rows * sizeof(uint32_t),
-                                  hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(s, hipStreamSynchronize(s->stream));
+                                             s->d_trace_top.as<uint8_t>() + top_bytes, s->stream, (uint32_t)n_rows,
+                                             reinterpret_cast<uint32_t*>(s->d_trace_top.as<uint8_t>() + other_at),
+                                             use_list ? reinterpret_cast<uint2*>(s->d_trace_top.as<uint8_t>() +
+                                                                                 olist_at)
+                                                      : nullptr));
+        if (use_list) {
+            // the ScoreMetaData, the per-record counts and lists first; every
+            // code only when a record has more than its list holds
+            HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.p, s->d_trace_top.p, codes_at, hipMemcpyDeviceToHost,
+                                      s->stream));
+            HIP_TRY(s, hipStreamSynchronize(s->stream));
+            for (uint32_t k = 0; k < sp.n_rec && !all_codes; k++) all_codes = n_other[k] > kOther;
+            if (all_codes) {
+                HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.as<uint8_t>() + codes_at, d_codes,
+                                          n_rows * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(s, hipStreamSynchronize(s->stream));
+            }
+        } else {   // short runs: everything in one copy
+            HIP_TRY(s, hipMemcpyAsync(s->h_trace_top.p, s->d_trace_top.p, codes_at + n_rows * sizeof(uint32_t),
+                                      hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(s, hipStreamSynchronize(s->stream));
+        }
     } else {
-        std::memset(s->h_trace_top.as<uint8_t>() + top_bytes, 0, sp.n_rec);
+        std::memset(s->h_trace_top.as<uint8_t>() + top_bytes, 0, codes_at - top_bytes);
     }
     const double t2 = prof ? now_us() : 0.0;
     spec_metrics_reset(sp);
@@ -6486,6 +6515,16 @@ static int spec_metrics(pe_stack* s, TgPlan& g, uint32_t off0) {
     size_t i = 0;
     for (uint32_t k = 0; k < sp.n_rec; k++) {
         const size_t b = i;
+        if (!n_other[k]) {
+            i = rec_end[k];   // options only
+        } else if (use_list && n_other[k] <= kOther) {   // the listed entries (maps are counts: order is free)
+            for (uint32_t q = 0; q < n_other[k]; q++) {
+                const uint32_t j = olist[2 * ((size_t)k * kOther + q)], code = olist[2 * ((size_t)k * kOther + q) + 1];
+                const int rc = metrics_outcome(s, g, a, row_of(k, j), code, nullptr, acc[k], counts);
+                if (rc) return rc;
+            }
+            i = rec_end[k];
+        }
         for (; i < rec_end[k]; i++) {   // the options' ScoreMetaData came from k_trace_top
             if ((codes[i] & 255u) == pe::kTrOption) continue;
             const int rc = metrics_outcome(s, g, a, row_of(k, (uint32_t)(i - b)), codes[i], nullptr, acc[k], counts);

@@ -620,22 +620,28 @@ __global__ void k_trace(NodeSoA s, TgTables t, Ask a, TraceSrc src, uint32_t n, 
 // more entering entries than its list holds sends the record to wave 0's
 // sequential pass over every entry.
 constexpr uint32_t kTopWaves = 16, kTopCand = 128;
+// n_other (or null): per record, its entries that are not options, the first
+// kTopOther of them (entry index within the record, code; in no particular
+// order) at other_list + k * kTopOther.
+constexpr uint32_t kTopOther = 128;
 __global__ void __launch_bounds__(1024) k_trace_top(const uint32_t* codes, const double* sc, TraceSrc src,
-                                                    uint32_t flags, pe_metric_score* out, uint8_t* n_out) {
+                                                    uint32_t flags, pe_metric_score* out, uint8_t* n_out,
+                                                    uint32_t* n_other, uint2* other_list) {
     __shared__ uint32_t cand_x[kTopWaves][kTopCand];
     __shared__ double cand_v[kTopWaves][kTopCand];
     __shared__ uint32_t cand_n[kTopWaves];
-    __shared__ uint32_t overflow;
+    __shared__ uint32_t overflow, others;
     const uint32_t k = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint32_t nw = blockDim.x >> 6;
     if (k >= src.n_rec) return;   // uniform across the block
     const uint32_t b = k ? src.rec_end[k - 1] : 0u, e = src.rec_end[k];
-    if (tid == 0) overflow = 0;
-    {   // phase 1: the segment's entering entries
+    if (tid == 0) overflow = others = 0;
+    __syncthreads();
+    {   // phase 1: the segment's entering entries (and its entries that are not options)
         const uint32_t total = e - b, seg = (total + nw - 1) / nw;
         const uint32_t sb = b + min(total, w * seg), se = b + min(total, (w + 1) * seg);
         double t[5];   // the segment's top-5 so far (values), unsorted; tmin its minimum once full
-        uint32_t tl = 0, nc = 0;
+        uint32_t tl = 0, nc = 0, n_not = 0;
         double tmin = 0.0;
         bool over = false;
         constexpr uint32_t U = 4;
@@ -650,6 +656,12 @@ __global__ void __launch_bounds__(1024) k_trace_top(const uint32_t* codes, const
             for (uint32_t u = 0; u < U; u++) {
                 const uint32_t x = c + u * 64 + lane;
                 const bool opt = (cd[u] & 255u) == kTrOption;
+                const bool other = x < se && !opt;
+                n_not += (uint32_t)__popcll(__ballot(other));
+                if (other && other_list) {
+                    const uint32_t q = atomicAdd(&others, 1u);
+                    if (q < kTopOther) other_list[(size_t)k * kTopOther + q] = make_uint2(x - b, cd[u]);
+                }
                 const double v = opt ? sc[(size_t)x * 6 + 5] : 0.0;
                 uint64_t mask = __ballot(opt && (tl < 5 || v > tmin));
                 while (mask) {
@@ -686,9 +698,11 @@ __global__ void __launch_bounds__(1024) k_trace_top(const uint32_t* codes, const
         if (lane == 0) {
             cand_n[w] = nc;
             if (over) atomicOr(&overflow, 1u);
+            if (n_not && !other_list) atomicAdd(&others, n_not);
         }
     }
     __syncthreads();
+    if (tid == 0 && n_other) n_other[k] = others;
     if (w != 0) return;
     double hn[5];
     uint32_t hi[5];
@@ -4480,13 +4494,14 @@ hipError_t pe_launch_sweep(const pe::SweepArgs* a, uint32_t blocks, pe::SweepRec
 }
 
 hipError_t pe_launch_trace_top(const uint32_t* codes, const double* sc, const pe::TraceSrc* src, uint32_t flags,
-                               pe_metric_score* out, uint8_t* n_out, hipStream_t st, uint32_t n_entries) {
+                               pe_metric_score* out, uint8_t* n_out, hipStream_t st, uint32_t n_entries,
+                               uint32_t* n_other, uint2* other_list) {
     if (!src->n_rec) return hipSuccess;
     // waves per record: about 2048 entries each, 1 to kTopWaves
     const uint32_t avg = n_entries / src->n_rec;
     const uint32_t waves = std::max<uint32_t>(1u, std::min<uint32_t>(pe::kTopWaves, (avg + 2047u) / 2048u));
     hipLaunchKernelGGL(pe::k_trace_top, dim3(src->n_rec), dim3(64 * waves), 0, st, codes, sc, *src, flags, out,
-                       n_out);
+                       n_out, n_other, other_list);
     return hipGetLastError();
 }
 
