@@ -16,7 +16,7 @@ devices), windowed and full-pass.
 import pytest
 
 from nomad_amd import synth
-from nomad_amd.structs import Constraint, Job, NetworkResource, Task, TaskGroup
+from nomad_amd.structs import Allocation, Constraint, Job, NetworkResource, Task, TaskGroup
 from oracle.oracle import OracleGenericStack
 
 
@@ -678,3 +678,27 @@ def test_metrics_view_batched_spreads(kind):
     eng, ora = _metrics_pair(nodes, allocs, job, synth.shuffle(len(nodes), 9))
     st = _view_metrics_protocol(eng, ora, 150)
     assert st["view"] >= 120, st
+
+
+@pytest.mark.gpu
+def test_metrics_view_rising_scores():
+    """Scores that rise along the visit order (each node a little fuller than
+    the one before): every option of a full pass enters the record's top-5
+    heap for a moment, so k_trace_top's segment lists overflow and the
+    record's heap is built by the sequential pass; the ScoreMetaData, order
+    included, equal the oracle's."""
+    from nomad_amd.structs import Affinity
+    n = 3000
+    nodes, allocs = [], []
+    for i, nid in enumerate(sorted(synth.uuids(n, 21))):
+        nd = synth.mock_node(nid)
+        nd.name = "node-%05d" % i
+        nd.compute_class()
+        nodes.append(nd)
+        allocs.append(Allocation(node_id=nid, job_id="fill", task_group="web", cpu_shares=1 + i,
+                                 memory_mb=64, disk_mb=10, priority=50))
+    job = synth.job_c2(24)
+    job.task_groups[0].affinities = [Affinity("${node.class}", "no-such-class", "=", 50)]
+    eng, ora = _metrics_pair(nodes, allocs, job, list(range(n)))
+    st = _view_metrics_protocol(eng, ora, 24)
+    assert st["view"] >= 16, st
